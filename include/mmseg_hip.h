@@ -1,0 +1,142 @@
+/*
+ * mmseg_hip.h — C ABI of libmmseg_hip.so, the MI355X (gfx950) kernels of the
+ * multimodal organ segmentation training step.
+ *
+ * The reference (wittyseok/multimodal-organ-segmentation) has no FFI: its hot
+ * path is implicit ATen ops reached through torch.nn modules.  Each entry
+ * point below replaces the ATen op(s) named in its comment (reference
+ * file:line); the Python mirror of the reference API
+ * (multimodal-organ-segmentation_amd/models, /trainer) binds them with ctypes
+ * (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *   - Every function returns 0 on success, non-zero on failure; the message of
+ *     the last failure on the calling thread is mmseg_last_error().  No C++
+ *     exception crosses the ABI.
+ *   - All pointers are device pointers owned by the caller (torch caching
+ *     allocator); kernels never allocate or free.  Workspaces are sized by the
+ *     *_ws_floats() queries.
+ *   - `stream` is a hipStream_t; every call is enqueue-only (no host sync), so
+ *     call sequences can be captured into a hipGraph.
+ *   - Activations are NDHWC: element (n, v, c) at base[(n*V + v)*ld + c],
+ *     V = D*H*W, ld >= C (ld > C: a slot of a wider concat buffer).
+ *   - dtype: 0 = fp32 storage (parity mode), 1 = bf16 storage; all
+ *     accumulation is fp32.  Reductions are fixed-order (deterministic).
+ */
+#ifndef MMSEG_HIP_H
+#define MMSEG_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------- plumbing */
+const char* mmseg_last_error(void);
+int mmseg_abi_version(void);
+
+/* --------------------------------------------------------- GEMM family */
+/* Gather modes: 0 CONV3 (3x3x3, pad 1), 1 POINT (1x1x1), 2 CONVT_FWD (k2 s2,
+ * output scatter), 3 CONVT_DGRAD (k2 s2, child gather). */
+
+/* fp32 torch-layout weights -> MFMA B-operand layout [KGp][Cpad][8].
+ * mode 0/1: Conv3d W[Co][Ci][3][3][3] fwd / dgrad (flipped, transposed)
+ * mode 2/3: 1x1 Conv3d W[Co][Ci] fwd / dgrad
+ * mode 4/5: ConvTranspose3d W[Ci][Co][2][2][2] fwd / dgrad
+ * Replaces the weight reads of nn.Conv3d / nn.ConvTranspose3d (unet.py:26-27, 95, 163). */
+int mmseg_pack_weight(const float* w, void* dst, int mode, int Co, int Ci, int Cip, int KG, int KGp, int Cpad,
+                      int dtype, void* stream);
+
+/* Implicit-GEMM forward / data-gradient convolution on MFMA.
+ * Replaces aten::convolution (fwd) and convolution_backward (grad_input) of
+ * Conv3d(k3,p1) unet.py:26-27, ConvTranspose3d(k2,s2) unet.py:95, and the
+ * 1x1 projections unet.py:163 / dual_encoder.py:75.  splitk_ws holds
+ * ksplit*M*Ncols floats when ksplit > 1. */
+int mmseg_conv_gemm(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
+                    float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W,
+                    int ksplit, int dtype, void* stream);
+
+/* Weight-gradient partials part[ksplit][Ca][Ncols] (fp32), K = voxels.
+ * Replaces convolution_backward (grad_weight) of the same layers. */
+int mmseg_wgrad(const void* a, int lda, const void* b, int ldb, float* part, int mode, int Ca, int Ncols,
+                int cpg_shift, long long V, int D, int H, int W, int ksplit, int dtype, void* stream);
+int mmseg_wgrad_splits(long long V, int ksplit);
+/* Fixed-order sum of the partials into the torch-layout fp32 gradient. */
+int mmseg_wgrad_reduce(const float* part, float* grad, int Ca, int Ncols, int ksplit, int cpad, int creal, int ntap,
+                       int accumulate, void* stream);
+/* Bias gradient out[c] (+)= sum_v dy[v][c] (convolution_backward grad_bias). */
+int mmseg_colsum(const void* dy, int ld, int C, long long V, float* part, int nblk, float* out, int accumulate,
+                 int dtype, void* stream);
+
+/* ---------------------------------------- InstanceNorm3d + ReLU, MaxPool */
+long long mmseg_instnorm_ws_floats(int N, long long V, int C);
+/* Per-(n,c) mean / 1/sqrt(var+eps) (nn.InstanceNorm3d unet.py:34-35, biased var).
+ * mean[n*mean_ld + c]; rstd may be NULL (channel means only, e.g. AdaptiveAvgPool3d). */
+int mmseg_instnorm_stats(const void* x, int ldx, int N, long long V, int C, float eps, float* mean, int mean_ld,
+                         float* rstd, float* ws, int dtype, void* stream);
+/* y = relu((x - mean) * rstd)  (InstanceNorm3d + ReLU(inplace), unet.py:54-59). */
+int mmseg_instnorm_relu_fwd(const void* x, int ldx, void* y, int ldy, int N, long long V, int C, const float* mean,
+                            const float* rstd, int dtype, void* stream);
+/* Backward of InstanceNorm3d + ReLU with dy gathered as
+ *   dy = scale1*alpha1[n]*p1 + beta[n][c] + maxpool_bwd(pool_dy, pool_idx)
+ * (MaxPool3d backward unet.py:73 and the DualEncoder fusion backward
+ * dual_encoder.py:167-199 fused in; any source may be NULL). */
+int mmseg_instnorm_relu_bwd(const void* x, int ldx, const float* mean, const float* rstd, const void* p1, int ld1,
+                            float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
+                            const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N,
+                            int D, int H, int W, int C, float* ws, int dtype, void* stream);
+/* MaxPool3d(2) forward + argmax (0..7, z-major; first max wins) (unet.py:73). */
+int mmseg_maxpool2_fwd(const void* x, int ldx, void* y, int ldy, uint8_t* idx, int N, int D, int H, int W, int C,
+                       int dtype, void* stream);
+
+/* ---------------------------------------------------- modality fusion */
+/* out = wconst * sum_m src_m (mean / add fusion, dual_encoder.py:184-186,193-195)
+ * or sum_m wts[n][m] * src_m (CrossModalAttention weighting, dual_encoder.py:252-254). */
+int mmseg_fuse_fwd(const void* const* srcs, const int* lds, int M, float wconst, const float* wts, void* out, int ldo,
+                   int N, long long V, int C, int dtype, void* stream);
+/* CrossModalAttention gate: Linear -> ReLU -> Linear -> softmax (dual_encoder.py:226-233). */
+int mmseg_attn_gate_fwd(const float* pooled, const float* W1, const float* b1, const float* W2, const float* b2,
+                        float* hbuf, float* wts, int N, int MC, int Hd, int M, void* stream);
+int mmseg_attn_gate_bwd(const void* const* srcs, const int* lds, int M, const void* dfused, int ldd, int N, long long V,
+                        int C, const float* pooled, const float* W1, const float* W2, const float* hbuf,
+                        const float* wts, float* beta, float* gW1, float* gb1, float* gW2, float* gb2, int Hd,
+                        float* ws, int accumulate, int dtype, void* stream);
+
+/* ------------------------------------------------- head, loss, metric */
+/* NCDHW fp32 volume channels [c0, c0+cnt) -> NDHWC 8-channel engine layout
+ * (batch["image"] as consumed by the first Conv3d, unet.py:181 / dual_encoder.py:133). */
+int mmseg_pack_input(const float* x, int Ctot, int c0, int cnt, int N, long long V, void* out, int dtype,
+                     void* stream);
+/* Dropout3d scale + 1x1 out_conv -> NCDHW fp32 logits (unet.py:195-196). */
+int mmseg_head_fwd(const void* x, int ldx, int Cin, const float* W, const float* b, const float* dscale, int C, int N,
+                   long long V, float* logits, int dtype, void* stream);
+long long mmseg_head_ws_floats(int C, int Cin, int N, long long V);
+int mmseg_head_bwd(const void* x, int ldx, int Cin, const float* W, const float* dscale, int C, int N, long long V,
+                   const float* dlogits, void* dx, int lddx, float* gW, float* gb, float* ws, int accumulate, int dtype,
+                   void* stream);
+/* Fused softmax + Dice/Tversky + CE statistics and loss (losses.py:39-80, 160-185,
+ * 216-228).  type 0: dice_w*Dice + ce_w*CE ; type 1: dice_w*Tversky + ce_w*CE. */
+long long mmseg_loss_ws_floats(int N, int C, long long V);
+int mmseg_loss_fwd(const float* logits, const void* labels, int label_bytes, int N, int C, long long V, int type,
+                   float dice_w, float ce_w, float smooth, float alpha, float beta, int include_bg,
+                   const float* class_w, float* loss_out, float* ws, void* stream);
+int mmseg_loss_bwd(const float* logits, const void* labels, int label_bytes, int N, int C, long long V, int type,
+                   float dice_w, float ce_w, float smooth, float alpha, float beta, int include_bg,
+                   const float* class_w, const float* gout, float gconst, float* dlogits, const float* ws,
+                   void* stream);
+/* argmax + per-class intersection / pred / target counts (trainer.py:290-291, metrics.py:42-67). */
+int mmseg_dice_counts(const float* logits, const void* labels, int label_bytes, int N, int C, long long V,
+                      unsigned long long* counts, void* pred_out, void* stream);
+/* counts from class-index masks (DiceMetric.update(pred, target), metrics.py:42-67). */
+int mmseg_dice_counts_idx(const void* pred, int pred_bytes, const void* labels, int label_bytes, long long total, int C,
+                          unsigned long long* counts, void* stream);
+/* AdamW step over flat fp32 buffers (torch.optim.AdamW op order, trainer.py:115-117). */
+int mmseg_adamw(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
+                float eps, float wd, int step, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMSEG_HIP_H */

@@ -1,0 +1,610 @@
+// Segmentation head, losses, metric and optimizer kernels.
+//
+//   head:   Dropout3d (per-(n,c) scale) + 1x1 Conv3d out_conv
+//           (reference unet.py:162-163,195-196; dual_encoder.py:83-84,157-158)
+//           NDHWC features -> NCDHW fp32 logits (the reference's output layout)
+//   loss:   softmax over C + one-hot + per-(b,c) Dice / Tversky sums + CE in one
+//           pass; fixed-order finalize; a second pass writes dlogits.
+//           DiceLoss losses.py:39-80, DiceCELoss 216-228 (nn.CrossEntropyLoss
+//           with optional class weights), TverskyLoss 160-185.
+//   metric: argmax over C + per-class integer intersection / union counts
+//           (DiceMetric.update, metrics.py:42-67) — integer, exact.
+//   optim:  AdamW in torch's single-tensor op order (torch.optim.AdamW, as
+//           configured by trainer.py:115-117), over flat parameter buffers.
+//   input:  NCDHW fp32 volume -> NDHWC (8-channel padded) engine layout.
+#include "mmseg_common.h"
+
+namespace {
+
+constexpr int CMAX = 16;
+
+// -------------------------------------------------------------- input pack
+template <typename T>
+__global__ void pack_input_kernel(const float* __restrict__ x, int Ctot, int c0, int cnt, long long V, int N,
+                                  T* __restrict__ out) {
+  const long long total = (long long)N * V;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long n = i / V, v = i - n * V;
+    V8<T> o;
+    o.zero();
+    for (int c = 0; c < cnt; ++c) o.set(c, x[(n * Ctot + c0 + c) * V + v]);
+    o.store(out + i * 8);
+  }
+}
+
+// ----------------------------------------------------------------- head
+// logits[n][c][v] = b[c] + sum_ci W[c][ci] * s[n][ci] * x[n,v,ci]
+template <typename T>
+__global__ void head_fwd_kernel(const T* __restrict__ x, int ldx, int Cin, const float* __restrict__ Wt,
+                                const float* __restrict__ bias, const float* __restrict__ dscale, int C, long long V,
+                                int N, float* __restrict__ logits) {
+  extern __shared__ float sw[];  // C*Cin
+  for (int i = threadIdx.x; i < C * Cin; i += blockDim.x) sw[i] = Wt[i];
+  __syncthreads();
+  const long long total = (long long)N * V;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long n = i / V, v = i - n * V;
+    float acc[CMAX];
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) acc[c] = c < C ? bias[c] : 0.f;
+    for (int cg = 0; cg < Cin / 8; ++cg) {
+      V8<T> a;
+      a.load(x + i * ldx + cg * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float xv = a.get(j);
+        if (dscale) xv *= dscale[n * Cin + cg * 8 + j];
+#pragma unroll
+        for (int c = 0; c < CMAX; ++c)
+          if (c < C) acc[c] = fmaf(sw[c * Cin + cg * 8 + j], xv, acc[c]);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c < C) logits[(n * C + c) * V + v] = acc[c];
+  }
+}
+
+// dx[n,v,ci] = s[n][ci] * sum_c dlog[n][c][v] * W[c][ci]
+template <typename T>
+__global__ void head_dgrad_kernel(const float* __restrict__ dlog, const float* __restrict__ Wt,
+                                  const float* __restrict__ dscale, int C, int Cin, long long V, int N,
+                                  T* __restrict__ dx, int lddx) {
+  extern __shared__ float sw[];
+  for (int i = threadIdx.x; i < C * Cin; i += blockDim.x) sw[i] = Wt[i];
+  __syncthreads();
+  const long long total = (long long)N * V;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long n = i / V, v = i - n * V;
+    float d[CMAX];
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) d[c] = c < C ? dlog[(n * C + c) * V + v] : 0.f;
+    for (int cg = 0; cg < Cin / 8; ++cg) {
+      V8<T> o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int ci = cg * 8 + j;
+        float a = 0.f;
+#pragma unroll
+        for (int c = 0; c < CMAX; ++c)
+          if (c < C) a = fmaf(d[c], sw[c * Cin + ci], a);
+        if (dscale) a *= dscale[n * Cin + ci];
+        o.set(j, a);
+      }
+      o.store(dx + i * lddx + cg * 8);
+    }
+  }
+}
+
+// partial dW[c][ci] and db[c] per voxel chunk (block), fixed order.
+template <typename T>
+__global__ void head_wgrad_partial(const T* __restrict__ x, int ldx, const float* __restrict__ dlog,
+                                   const float* __restrict__ dscale, int C, int Cin, long long V, int N,
+                                   long long vpc, float* __restrict__ part) {
+  constexpr int KV = 64;
+  extern __shared__ float sh[];
+  float* xs = sh;              // KV * Cin
+  float* ds = sh + KV * Cin;   // C * KV
+  const long long total = (long long)N * V;
+  const long long e0 = (long long)blockIdx.x * vpc;
+  long long e1 = e0 + vpc;
+  if (e1 > total) e1 = total;
+  const int npairs = C * Cin + C;  // (c, ci) pairs then bias terms
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (long long eb = e0; eb < e1; eb += KV) {
+    __syncthreads();
+    for (int t = threadIdx.x; t < KV * Cin; t += blockDim.x) {
+      const int vv = t / Cin, ci = t - vv * Cin;
+      const long long e = eb + vv;
+      float val = 0.f;
+      if (e < e1) {
+        val = to_f<T>(x[e * ldx + ci]);
+        if (dscale) val *= dscale[(e / V) * Cin + ci];
+      }
+      xs[t] = val;
+    }
+    for (int t = threadIdx.x; t < C * KV; t += blockDim.x) {
+      const int c = t / KV, vv = t - c * KV;
+      const long long e = eb + vv;
+      float val = 0.f;
+      if (e < e1) {
+        const long long n = e / V, v = e - n * V;
+        val = dlog[(n * C + c) * V + v];
+      }
+      ds[t] = val;
+    }
+    __syncthreads();
+    for (int k = 0; k < 4; ++k) {
+      const int p = threadIdx.x + k * blockDim.x;
+      if (p >= npairs) break;
+      float a = acc[k];
+      if (p < C * Cin) {
+        const int c = p / Cin, ci = p - c * Cin;
+        for (int vv = 0; vv < KV; ++vv) a = fmaf(ds[c * KV + vv], xs[vv * Cin + ci], a);
+      } else {
+        const int c = p - C * Cin;
+        for (int vv = 0; vv < KV; ++vv) a += ds[c * KV + vv];
+      }
+      acc[k] = a;
+    }
+  }
+  for (int k = 0; k < 4; ++k) {
+    const int p = threadIdx.x + k * blockDim.x;
+    if (p < npairs) part[(long long)blockIdx.x * npairs + p] = acc[k];
+  }
+}
+
+__global__ void head_wgrad_reduce(const float* __restrict__ part, int nblk, int C, int Cin, float* __restrict__ gW,
+                                  float* __restrict__ gb, int accumulate) {
+  const int npairs = C * Cin + C;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npairs) return;
+  float a = 0.f;
+  for (int b = 0; b < nblk; ++b) a += part[(long long)b * npairs + p];
+  float* dst = p < C * Cin ? gW + p : gb + (p - C * Cin);
+  *dst = accumulate ? *dst + a : a;
+}
+
+// ----------------------------------------------------------------- losses
+struct LossCfg {
+  int type;             // 0 = dice/ce family, 1 = tversky
+  float dice_w, ce_w;   // weights of the region term and the CE term
+  float smooth, alpha, beta;
+  int include_bg;
+  const float* cw;      // CE class weights [C] or null
+};
+
+// per (n, chunk): [P_c][I_c][T_c] (3C) + ce_num + ce_den
+template <typename LT>
+__global__ void loss_stats_kernel(const float* __restrict__ logits, const LT* __restrict__ labels, int C,
+                                  long long V, long long vpc, LossCfg cfg, float* __restrict__ part) {
+  const int n = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
+  float P[CMAX], I[CMAX], Tc[CMAX];
+#pragma unroll
+  for (int c = 0; c < CMAX; ++c) P[c] = I[c] = Tc[c] = 0.f;
+  float ce = 0.f, cden = 0.f;
+  const long long v0 = (long long)chunk * vpc;
+  long long v1 = v0 + vpc;
+  if (v1 > V) v1 = V;
+  const float* L = logits + (long long)n * C * V;
+  for (long long v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
+    float z[CMAX];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c < C) {
+        z[c] = L[c * V + v];
+        mx = fmaxf(mx, z[c]);
+      }
+    float se = 0.f;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c < C) se += expf(z[c] - mx);
+    const float lse = mx + logf(se);
+    const int y = (int)labels[(long long)n * V + v];
+    const float inv = 1.f / se;
+    float zy = 0.f;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c < C) {
+        const float p = expf(z[c] - mx) * inv;
+        P[c] += p;
+        if (c == y) {
+          I[c] += p;
+          Tc[c] += 1.f;
+          zy = z[c];
+        }
+      }
+    const float wy = cfg.cw ? cfg.cw[y] : 1.f;
+    ce = fmaf(wy, lse - zy, ce);
+    cden += wy;
+  }
+  __shared__ float red[4][3 * CMAX + 2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int c = 0; c < C; ++c) {
+    float a = wave_sum(P[c]), b = wave_sum(I[c]), d = wave_sum(Tc[c]);
+    if (lane == 0) {
+      red[wave][c] = a;
+      red[wave][C + c] = b;
+      red[wave][2 * C + c] = d;
+    }
+  }
+  {
+    float a = wave_sum(ce), b = wave_sum(cden);
+    if (lane == 0) {
+      red[wave][3 * C] = a;
+      red[wave][3 * C + 1] = b;
+    }
+  }
+  __syncthreads();
+  const int nv = 3 * C + 2;
+  for (int k = threadIdx.x; k < nv; k += blockDim.x)
+    part[((long long)n * nchunk + chunk) * nv + k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+}
+
+// one block: loss scalar + per-(n,c) dp coefficients (dp = a*t + b) + ce scale
+__global__ void loss_finalize_kernel(const float* __restrict__ part, int N, int C, int nchunk, LossCfg cfg,
+                                     float* __restrict__ loss_out, float* __restrict__ coef) {
+  __shared__ double acc_loss[256];
+  const int nv = 3 * C + 2;
+  double region = 0.0;
+  const int c0 = (cfg.type == 0 && !cfg.include_bg) ? 1 : 0;
+  const double nterms = (double)N * (C - c0);
+  for (int e = threadIdx.x; e < N * C; e += blockDim.x) {
+    const int n = e / C, c = e - n * C;
+    double P = 0, I = 0, T = 0;
+    for (int k = 0; k < nchunk; ++k) {
+      const float* p = part + ((long long)n * nchunk + k) * nv;
+      P += p[c];
+      I += p[C + c];
+      T += p[2 * C + c];
+    }
+    double a = 0.0, b = 0.0;
+    const double s = cfg.smooth;
+    if (c >= c0) {
+      if (cfg.type == 0) {
+        const double U = P + T;
+        const double dice = (2.0 * I + s) / (U + s);
+        region += 1.0 - dice;
+        a = -(2.0 / (U + s)) / nterms;
+        b = ((2.0 * I + s) / ((U + s) * (U + s))) / nterms;
+      } else {
+        const double fp = P - I, fn = T - I;
+        const double num = I + s;
+        const double den = I + cfg.alpha * fp + cfg.beta * fn + s;
+        region += 1.0 - num / den;
+        a = -((den - num * (1.0 - cfg.alpha - cfg.beta)) / (den * den)) / nterms;
+        b = (num * cfg.alpha / (den * den)) / nterms;
+      }
+    }
+    coef[e * 2 + 0] = (float)(a * cfg.dice_w);
+    coef[e * 2 + 1] = (float)(b * cfg.dice_w);
+  }
+  acc_loss[threadIdx.x] = region;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double r = 0.0;
+    for (int t = 0; t < (int)blockDim.x; ++t) r += acc_loss[t];
+    double ce = 0.0, den = 0.0;
+    for (int n = 0; n < N; ++n)
+      for (int k = 0; k < nchunk; ++k) {
+        const float* p = part + ((long long)n * nchunk + k) * nv;
+        ce += p[3 * C];
+        den += p[3 * C + 1];
+      }
+    const double lv = cfg.dice_w * (r / nterms) + cfg.ce_w * (ce / den);
+    loss_out[0] = (float)lv;
+    coef[2 * N * C] = (float)(cfg.ce_w / den);   // CE gradient scale
+  }
+}
+
+// dlogits = gout * [ p*(dp - sum p dp) + ce_scale * w_y * (p - t) ]
+template <typename LT>
+__global__ void loss_bwd_kernel(const float* __restrict__ logits, const LT* __restrict__ labels, int C, long long V,
+                                int N, LossCfg cfg, const float* __restrict__ coef, const float* __restrict__ gout,
+                                float gconst, float* __restrict__ dlogits) {
+  const long long total = (long long)N * V;
+  const float g = gout ? gout[0] * gconst : gconst;
+  const float ces = coef[2 * N * C];
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long n = i / V, v = i - n * V;
+    const float* L = logits + n * C * V;
+    float z[CMAX], p[CMAX];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c < C) {
+        z[c] = L[c * V + v];
+        mx = fmaxf(mx, z[c]);
+      }
+    float se = 0.f;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c < C) {
+        p[c] = expf(z[c] - mx);
+        se += p[c];
+      }
+    const float inv = 1.f / se;
+    const int y = (int)labels[i];
+    const float wy = cfg.cw ? cfg.cw[y] : 1.f;
+    float dp[CMAX];
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c < C) {
+        p[c] *= inv;
+        const float t = c == y ? 1.f : 0.f;
+        const float* cf = coef + ((long long)n * C + c) * 2;
+        dp[c] = cf[0] * t + cf[1];
+        s = fmaf(p[c], dp[c], s);
+      }
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c < C) {
+        const float t = c == y ? 1.f : 0.f;
+        const float d = p[c] * (dp[c] - s) + ces * wy * (p[c] - t);
+        dlogits[(n * C + c) * V + v] = g * d;
+      }
+  }
+}
+
+// -------------------------------------------------------------- metric
+// counts[0..C) intersection, [C..2C) pred count, [2C..3C) target count
+template <typename LT>
+__global__ void dice_counts_kernel(const float* __restrict__ logits, const LT* __restrict__ labels, int C, long long V,
+                                   int N, unsigned long long* __restrict__ counts, LT* __restrict__ pred_out) {
+  __shared__ unsigned int sc[3 * CMAX];
+  for (int k = threadIdx.x; k < 3 * C; k += blockDim.x) sc[k] = 0;
+  __syncthreads();
+  const long long total = (long long)N * V;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long n = i / V, v = i - n * V;
+    const float* L = logits + n * C * V;
+    int best = 0;
+    float bv = L[v];
+    for (int c = 1; c < C; ++c) {
+      const float z = L[c * V + v];
+      if (z > bv || (z != z && bv == bv)) {  // first maximum; NaN counts as maximal (torch.argmax)
+        bv = z;
+        best = c;
+      }
+    }
+    const int y = (int)labels[i];
+    if (pred_out) pred_out[i] = (LT)best;
+    atomicAdd(&sc[C + best], 1u);
+    if (y >= 0 && y < C) {
+      atomicAdd(&sc[2 * C + y], 1u);
+      if (y == best) atomicAdd(&sc[y], 1u);
+    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 3 * C; k += blockDim.x)
+    if (sc[k]) atomicAdd(&counts[k], (unsigned long long)sc[k]);
+}
+
+template <typename PT, typename LT>
+__global__ void dice_counts_idx_kernel(const PT* __restrict__ pred, const LT* __restrict__ labels, int C,
+                                       long long total, unsigned long long* __restrict__ counts) {
+  __shared__ unsigned int sc[3 * CMAX];
+  for (int k = threadIdx.x; k < 3 * C; k += blockDim.x) sc[k] = 0;
+  __syncthreads();
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int p = (int)pred[i], y = (int)labels[i];
+    if (p >= 0 && p < C) atomicAdd(&sc[C + p], 1u);
+    if (y >= 0 && y < C) {
+      atomicAdd(&sc[2 * C + y], 1u);
+      if (y == p) atomicAdd(&sc[y], 1u);
+    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 3 * C; k += blockDim.x)
+    if (sc[k]) atomicAdd(&counts[k], (unsigned long long)sc[k]);
+}
+
+// ------------------------------------------------------------------ AdamW
+__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                             float* __restrict__ v, long long n, float decay, float beta1, float omb1, float beta2,
+                             float omb2, float eps, float step_size, float bc2_sqrt) {
+#pragma clang fp contract(off)
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    float pv = p[i];
+    const float gv = g[i];
+    pv = pv * decay;                          // param.mul_(1 - lr * wd)
+    float mv = m[i];
+    mv = omb1 < 0.5f ? mv + omb1 * (gv - mv)  // exp_avg.lerp_(grad, 1 - beta1)
+                     : gv - (gv - mv) * (1.f - omb1);
+    float vv = v[i];
+    vv = vv * beta2 + (omb2 * gv) * gv;       // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
+    const float denom = sqrtf(vv) / bc2_sqrt + eps;
+    pv = pv + (-step_size) * (mv / denom);
+    p[i] = pv;
+    m[i] = mv;
+    v[i] = vv;
+  }
+}
+
+int grid_for(long long total) {
+  long long b = (total + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+int loss_chunks(long long V, long long* vpc) {
+  long long nch = (V + 8191) / 8192;
+  if (nch > 512) nch = 512;
+  if (nch < 1) nch = 1;
+  *vpc = (V + nch - 1) / nch;
+  return (int)((V + *vpc - 1) / *vpc);
+}
+
+}  // namespace
+
+extern "C" {
+
+int mmseg_pack_input(const float* x, int Ctot, int c0, int cnt, int N, long long V, void* out, int dtype,
+                     void* stream) {
+  MMSEG_REQUIRE(cnt >= 1 && cnt <= 8, "pack_input: 1..8 channels per pack (got %d)", cnt);
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = grid_for((long long)N * V);
+  if (dtype == MMSEG_BF16)
+    hipLaunchKernelGGL(pack_input_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, x, Ctot, c0, cnt, V, N, (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(pack_input_kernel<float>, dim3(grid), dim3(256), 0, s, x, Ctot, c0, cnt, V, N, (float*)out);
+  return mmseg::check_launch("pack_input");
+}
+
+int mmseg_head_fwd(const void* x, int ldx, int Cin, const float* W, const float* b, const float* dscale, int C, int N,
+                   long long V, float* logits, int dtype, void* stream) {
+  MMSEG_REQUIRE(C >= 1 && C <= CMAX && Cin % 8 == 0, "head: 1 <= C <= %d, Cin%%8 == 0", CMAX);
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = grid_for((long long)N * V);
+  const size_t shm = (size_t)C * Cin * sizeof(float);
+  if (dtype == MMSEG_BF16)
+    hipLaunchKernelGGL(head_fwd_kernel<bf16_t>, dim3(grid), dim3(256), shm, s, (const bf16_t*)x, ldx, Cin, W, b, dscale,
+                       C, V, N, logits);
+  else
+    hipLaunchKernelGGL(head_fwd_kernel<float>, dim3(grid), dim3(256), shm, s, (const float*)x, ldx, Cin, W, b, dscale,
+                       C, V, N, logits);
+  return mmseg::check_launch("head_fwd");
+}
+
+long long mmseg_head_ws_floats(int C, int Cin, int N, long long V) {
+  const long long nblk = 512;
+  return nblk * (C * Cin + C);
+}
+
+int mmseg_head_bwd(const void* x, int ldx, int Cin, const float* W, const float* dscale, int C, int N, long long V,
+                   const float* dlogits, void* dx, int lddx, float* gW, float* gb, float* ws, int accumulate, int dtype,
+                   void* stream) {
+  MMSEG_REQUIRE(C >= 1 && C <= CMAX && Cin % 8 == 0 && C * Cin + C <= 1024, "head_bwd: shape");
+  hipStream_t s = (hipStream_t)stream;
+  const long long total = (long long)N * V;
+  const int grid = grid_for(total);
+  const size_t shm = (size_t)C * Cin * sizeof(float);
+  long long nblk = 512;
+  long long vpc = ((total + nblk - 1) / nblk + 63) / 64 * 64;
+  nblk = (total + vpc - 1) / vpc;
+  const size_t shm2 = (size_t)(64 * Cin + C * 64) * sizeof(float);
+  // weight-gradient partials first: dx may alias x (the engine reuses the feature buffer)
+  if (dtype == MMSEG_BF16) {
+    hipLaunchKernelGGL(head_wgrad_partial<bf16_t>, dim3((int)nblk), dim3(256), shm2, s, (const bf16_t*)x, ldx, dlogits,
+                       dscale, C, Cin, V, N, vpc, ws);
+    if (dx)
+      hipLaunchKernelGGL(head_dgrad_kernel<bf16_t>, dim3(grid), dim3(256), shm, s, dlogits, W, dscale, C, Cin, V, N,
+                         (bf16_t*)dx, lddx);
+  } else {
+    hipLaunchKernelGGL(head_wgrad_partial<float>, dim3((int)nblk), dim3(256), shm2, s, (const float*)x, ldx, dlogits,
+                       dscale, C, Cin, V, N, vpc, ws);
+    if (dx)
+      hipLaunchKernelGGL(head_dgrad_kernel<float>, dim3(grid), dim3(256), shm, s, dlogits, W, dscale, C, Cin, V, N,
+                         (float*)dx, lddx);
+  }
+  if (mmseg::check_launch("head_bwd")) return 1;
+  hipLaunchKernelGGL(head_wgrad_reduce, dim3(ceil_div(C * Cin + C, 256)), dim3(256), 0, s, ws, (int)nblk, C, Cin, gW,
+                     gb, accumulate);
+  return mmseg::check_launch("head_wgrad_reduce");
+}
+
+long long mmseg_loss_ws_floats(int N, int C, long long V) {
+  long long vpc;
+  int nch = loss_chunks(V, &vpc);
+  return (long long)N * nch * (3 * C + 2) + 2LL * N * C + 1;
+}
+
+// label_bytes: 8 (int64, the reference's dtype) or 1 (uint8)
+int mmseg_loss_fwd(const float* logits, const void* labels, int label_bytes, int N, int C, long long V, int type,
+                   float dice_w, float ce_w, float smooth, float alpha, float beta, int include_bg,
+                   const float* class_w, float* loss_out, float* ws, void* stream) {
+  MMSEG_REQUIRE(C >= 2 && C <= CMAX, "loss: 2 <= C <= %d", CMAX);
+  MMSEG_REQUIRE(label_bytes == 8 || label_bytes == 1, "loss: labels must be int64 or uint8");
+  LossCfg cfg{type, dice_w, ce_w, smooth, alpha, beta, include_bg, class_w};
+  long long vpc;
+  const int nch = loss_chunks(V, &vpc);
+  float* part = ws;
+  float* coef = ws + (long long)N * nch * (3 * C + 2);
+  hipStream_t s = (hipStream_t)stream;
+  if (label_bytes == 8)
+    hipLaunchKernelGGL(loss_stats_kernel<int64_t>, dim3(nch, N), dim3(256), 0, s, logits, (const int64_t*)labels, C, V,
+                       vpc, cfg, part);
+  else
+    hipLaunchKernelGGL(loss_stats_kernel<uint8_t>, dim3(nch, N), dim3(256), 0, s, logits, (const uint8_t*)labels, C, V,
+                       vpc, cfg, part);
+  if (mmseg::check_launch("loss_stats")) return 1;
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, part, N, C, nch, cfg, loss_out, coef);
+  return mmseg::check_launch("loss_finalize");
+}
+
+// Must follow mmseg_loss_fwd with the same ws.  gout (device scalar) may be null.
+int mmseg_loss_bwd(const float* logits, const void* labels, int label_bytes, int N, int C, long long V, int type,
+                   float dice_w, float ce_w, float smooth, float alpha, float beta, int include_bg,
+                   const float* class_w, const float* gout, float gconst, float* dlogits, const float* ws,
+                   void* stream) {
+  LossCfg cfg{type, dice_w, ce_w, smooth, alpha, beta, include_bg, class_w};
+  long long vpc;
+  const int nch = loss_chunks(V, &vpc);
+  const float* coef = ws + (long long)N * nch * (3 * C + 2);
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = grid_for((long long)N * V);
+  if (label_bytes == 8)
+    hipLaunchKernelGGL(loss_bwd_kernel<int64_t>, dim3(grid), dim3(256), 0, s, logits, (const int64_t*)labels, C, V, N,
+                       cfg, coef, gout, gconst, dlogits);
+  else
+    hipLaunchKernelGGL(loss_bwd_kernel<uint8_t>, dim3(grid), dim3(256), 0, s, logits, (const uint8_t*)labels, C, V, N,
+                       cfg, coef, gout, gconst, dlogits);
+  return mmseg::check_launch("loss_bwd");
+}
+
+// counts: 3*C uint64 (must be zeroed by the caller, accumulates); pred_out optional (same dtype as labels)
+int mmseg_dice_counts(const float* logits, const void* labels, int label_bytes, int N, int C, long long V,
+                      unsigned long long* counts, void* pred_out, void* stream) {
+  MMSEG_REQUIRE(C >= 1 && C <= CMAX, "dice_counts: C <= %d", CMAX);
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = grid_for((long long)N * V) > 2048 ? 2048 : grid_for((long long)N * V);
+  if (label_bytes == 8)
+    hipLaunchKernelGGL(dice_counts_kernel<int64_t>, dim3(grid), dim3(256), 0, s, logits, (const int64_t*)labels, C, V,
+                       N, counts, (int64_t*)pred_out);
+  else
+    hipLaunchKernelGGL(dice_counts_kernel<uint8_t>, dim3(grid), dim3(256), 0, s, logits, (const uint8_t*)labels, C, V,
+                       N, counts, (uint8_t*)pred_out);
+  return mmseg::check_launch("dice_counts");
+}
+
+// counts from class-index masks (DiceMetric.update(pred, target), metrics.py:42-67); int64 or uint8 masks
+int mmseg_dice_counts_idx(const void* pred, int pred_bytes, const void* labels, int label_bytes, long long total, int C,
+                          unsigned long long* counts, void* stream) {
+  MMSEG_REQUIRE(C >= 1 && C <= CMAX && (pred_bytes == 8 || pred_bytes == 1) && (label_bytes == 8 || label_bytes == 1),
+                "dice_counts_idx: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = grid_for(total) > 2048 ? 2048 : grid_for(total);
+#define DCI(PT, LT) \
+  hipLaunchKernelGGL((dice_counts_idx_kernel<PT, LT>), dim3(grid), dim3(256), 0, s, (const PT*)pred, (const LT*)labels, C, total, counts)
+  if (pred_bytes == 8 && label_bytes == 8) DCI(int64_t, int64_t);
+  else if (pred_bytes == 8) DCI(int64_t, uint8_t);
+  else if (label_bytes == 8) DCI(uint8_t, int64_t);
+  else DCI(uint8_t, uint8_t);
+#undef DCI
+  return mmseg::check_launch("dice_counts_idx");
+}
+
+int mmseg_adamw(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
+                float eps, float wd, int step, void* stream) {
+  const double bc1 = 1.0 - pow((double)beta1, step);
+  const double bc2 = 1.0 - pow((double)beta2, step);
+  const float step_size = (float)(lr / bc1);
+  const float bc2s = (float)sqrt(bc2);
+  const int grid = grid_for(n) > 4096 ? 4096 : grid_for(n);
+  const float decay = (float)(1.0 - (double)lr * (double)wd);
+  const float omb1 = (float)(1.0 - (double)beta1), omb2 = (float)(1.0 - (double)beta2);
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, decay, beta1, omb1,
+                     beta2, omb2, eps, step_size, bc2s);
+  return mmseg::check_launch("adamw");
+}
+
+}  // extern "C"

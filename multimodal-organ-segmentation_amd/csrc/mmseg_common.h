@@ -1,0 +1,109 @@
+// Common device/host helpers for the MI355X (gfx950) segmentation kernels.
+//
+// Activation layout inside the engine is NDHWC ("voxel-major, channels
+// contiguous"): element (n, v, c) of a tensor with C channels lives at
+// base[(n*V + v) * ld + c], where V = D*H*W and ld >= C is the voxel stride.
+// ld > C lets a tensor live inside a wider buffer (the decoder's
+// [upsampled | skip] concat buffer), so torch.cat never materialises.
+//
+// Storage type T is float (parity mode) or __bf16 (throughput mode); every
+// accumulation is fp32.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+typedef __bf16 bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+enum MmsegDtype { MMSEG_F32 = 0, MMSEG_BF16 = 1 };
+
+#define MMSEG_WAVE 64
+
+// ---------------------------------------------------------------- errors
+namespace mmseg {
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+}  // namespace mmseg
+
+#define MMSEG_REQUIRE(cond, ...)              \
+  do {                                        \
+    if (!(cond)) {                            \
+      mmseg::set_error(__VA_ARGS__);          \
+      return 1;                               \
+    }                                         \
+  } while (0)
+
+// --------------------------------------------------------- 8-wide vectors
+// A "v8" is 8 consecutive channels of one voxel: 16 B for bf16, 32 B for f32.
+template <typename T> struct V8;
+template <> struct V8<float> {
+  float v[8];
+  __device__ __forceinline__ void load(const float* p) {
+    float4 a = *reinterpret_cast<const float4*>(p);
+    float4 b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  __device__ __forceinline__ void store(float* p) const {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+  __device__ __forceinline__ float get(int i) const { return v[i]; }
+  __device__ __forceinline__ void set(int i, float x) { v[i] = x; }
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 0.f;
+  }
+};
+template <> struct V8<bf16_t> {
+  bf16x8 v;
+  __device__ __forceinline__ void load(const bf16_t* p) { v = *reinterpret_cast<const bf16x8*>(p); }
+  __device__ __forceinline__ void store(bf16_t* p) const { *reinterpret_cast<bf16x8*>(p) = v; }
+  __device__ __forceinline__ float get(int i) const { return (float)v[i]; }
+  __device__ __forceinline__ void set(int i, float x) { v[i] = (bf16_t)x; }
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (bf16_t)0.f;
+  }
+};
+
+template <typename T> __device__ __forceinline__ float to_f(T x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f(float x) { return (T)x; }
+
+// ------------------------------------------------------------ reductions
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+__device__ __forceinline__ double wave_sum_d(double x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+
+static inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// 3x3x3 tap t in [0,27): (kz, ky, kx) = (t/9, (t/3)%3, t%3), offsets -1..1.
+__device__ __forceinline__ void tap_delta(int t, int& dz, int& dy, int& dx) {
+  dz = t / 9 - 1;
+  dy = (t / 3) % 3 - 1;
+  dx = t % 3 - 1;
+}
+
+// Bitmask of the 27 taps whose neighbour of voxel (z,y,x) is inside the volume.
+__device__ __forceinline__ uint32_t tap_valid_mask(int z, int y, int x, int D, int H, int W) {
+  uint32_t mz = (z > 0 ? 1u : 0u) | 2u | (z < D - 1 ? 4u : 0u);
+  uint32_t my = (y > 0 ? 1u : 0u) | 2u | (y < H - 1 ? 4u : 0u);
+  uint32_t mx = (x > 0 ? 1u : 0u) | 2u | (x < W - 1 ? 4u : 0u);
+  uint32_t m = 0;
+#pragma unroll
+  for (int t = 0; t < 27; ++t) {
+    int kz = t / 9, ky = (t / 3) % 3, kx = t % 3;
+    if (((mz >> kz) & 1u) && ((my >> ky) & 1u) && ((mx >> kx) & 1u)) m |= (1u << t);
+  }
+  return m;
+}

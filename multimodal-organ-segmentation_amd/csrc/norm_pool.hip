@@ -1,0 +1,668 @@
+// HBM-bound kernels of the ConvBlock3D / DownBlock3D / DualEncoder fusion path.
+//
+//   InstanceNorm3d(affine=False, eps=1e-5, biased variance) + ReLU
+//       (reference unet.py:34-35,45,53-60)       -> instnorm_stats / _relu_fwd
+//   its backward (+ ReLU mask)                    -> instnorm_relu_bwd_{reduce,apply}
+//       with the MaxPool3d(2) backward (unet.py:73) and the fusion backward
+//       (dual_encoder.py:193-195 mean / 184-186 add / 188-191 attention) fused
+//       into the dy gather, so neither the pooled gradient nor the fused-level
+//       gradient is ever materialised per modality.
+//   MaxPool3d(2) forward with argmax (ties -> first in z,y,x scan order)
+//   modality fusion forward: weighted sum over M level tensors
+//   CrossModalAttention gate (dual_encoder.py:207-254): pooled mean -> Linear ->
+//       ReLU -> Linear -> softmax, and its backward.
+//
+// All reductions are two-level and fixed-order (per-block partials, then a
+// single-thread-per-output sweep), so results are bitwise reproducible.
+#include "mmseg_common.h"
+
+namespace {
+
+// ------------------------------------------------------------------ stats
+// partial sums of (x - K) and (x - K)^2 per (n, chunk, c); K = x[n, voxel 0, c]
+template <typename T>
+__global__ void in_stats_partial(const T* __restrict__ x, int ld, long long V, int C, long long vpc,
+                                 float* __restrict__ part) {
+  const int n = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
+  const int C8 = C >> 3;
+  const int lanes_v = 256 / C8;
+  const int tid = threadIdx.x;
+  const int cg = tid % C8, vl = tid / C8;
+  const T* xn = x + (long long)n * V * ld;
+  float s1[8], s2[8], K[8];
+  V8<T> k8;
+  k8.load(xn + cg * 8);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s1[j] = 0.f;
+    s2[j] = 0.f;
+    K[j] = k8.get(j);
+  }
+  const long long v0 = (long long)chunk * vpc;
+  long long v1 = v0 + vpc;
+  if (v1 > V) v1 = V;
+  if (vl < lanes_v) {
+    for (long long v = v0 + vl; v < v1; v += lanes_v) {
+      V8<T> a;
+      a.load(xn + v * ld + cg * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = a.get(j) - K[j];
+        s1[j] += d;
+        s2[j] = fmaf(d, d, s2[j]);
+      }
+    }
+  }
+  __shared__ float red[2][256 * 8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][tid * 8 + j] = s1[j];
+    red[1][tid * 8 + j] = s2[j];
+  }
+  __syncthreads();
+  // one thread per (c) sums the voxel lanes in fixed order
+  for (int c = tid; c < C; c += 256) {
+    const int g = c >> 3, j = c & 7;
+    float a = 0.f, b = 0.f;
+    for (int l = 0; l < lanes_v; ++l) {
+      a += red[0][(l * C8 + g) * 8 + j];
+      b += red[1][(l * C8 + g) * 8 + j];
+    }
+    float* p = part + (((long long)n * nchunk + chunk) * C + c) * 2;
+    p[0] = a;
+    p[1] = b;
+  }
+}
+
+template <typename T>
+__global__ void in_stats_finalize(const T* __restrict__ x, int ld, long long V, int N, int C, int nchunk,
+                                  const float* __restrict__ part, float eps, float* __restrict__ mean,
+                                  int mean_ld, float* __restrict__ rstd) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= N * C) return;
+  const int n = idx / C, c = idx - n * C;
+  double a = 0.0, b = 0.0;
+  for (int k = 0; k < nchunk; ++k) {
+    const float* p = part + (((long long)n * nchunk + k) * C + c) * 2;
+    a += p[0];
+    b += p[1];
+  }
+  const double K = to_f<T>(x[(long long)n * V * ld + c]);
+  const double m1 = a / (double)V;
+  double var = b / (double)V - m1 * m1;
+  if (var < 0) var = 0;
+  mean[(long long)n * mean_ld + c] = (float)(K + m1);
+  if (rstd) rstd[idx] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+// y = relu((x - mean) * rstd); 8 channels per thread
+template <typename T>
+__global__ void in_relu_apply(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, long long V, int N,
+                              int C, const float* __restrict__ mean, const float* __restrict__ rstd) {
+  const int C8 = C >> 3;
+  const long long total = (long long)N * V * C8;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % C8);
+    const long long nv = i / C8;
+    const int n = (int)(nv / V);
+    V8<T> a, o;
+    a.load(x + nv * ldx + cg * 8);
+    const float* mu = mean + n * C + cg * 8;
+    const float* rs = rstd + n * C + cg * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float h = (a.get(j) - mu[j]) * rs[j];
+      o.set(j, h > 0.f ? h : 0.f);
+    }
+    o.store(y + nv * ldy + cg * 8);
+  }
+}
+
+// --------------------------------------------------------------- maxpool
+// 2x2x2, stride 2.  idx = a*4 + b*2 + c (z,y,x), first maximum wins.
+template <typename T>
+__global__ void maxpool2_fwd(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy,
+                             uint8_t* __restrict__ idx, int N, int D, int H, int W, int C) {
+  const int C8 = C >> 3;
+  const int Do = D >> 1, Ho = H >> 1, Wo = W >> 1;
+  const long long Vo = (long long)Do * Ho * Wo;
+  const long long total = (long long)N * Vo * C8;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % C8);
+    long long q = i / C8;
+    const int xo = (int)(q % Wo);
+    q /= Wo;
+    const int yo = (int)(q % Ho);
+    q /= Ho;
+    const int zo = (int)(q % Do);
+    const long long n = q / Do;
+    const long long in0 = ((n * D + 2 * zo) * H + 2 * yo) * (long long)W + 2 * xo;
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const long long vin = in0 + ((long long)(t >> 2) * H + ((t >> 1) & 1)) * W + (t & 1);
+      V8<T> a;
+      a.load(x + vin * ldx + cg * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        // torch CPU max_pool3d: (val > maxval) || isnan(val) replaces
+        const float v = a.get(j);
+        if (t == 0 || v > best[j] || v != v) {
+          best[j] = v;
+          bi[j] = (uint8_t)t;
+        }
+      }
+    }
+    V8<T> o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o.set(j, best[j]);
+    const long long vo = ((n * Do + zo) * Ho + yo) * Wo + xo;
+    o.store(y + vo * ldy + cg * 8);
+    uint2 packed;
+    packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    *reinterpret_cast<uint2*>(idx + vo * C + cg * 8) = packed;
+  }
+}
+
+// ------------------------------------------------------------- dy gather
+// dy(n, v, c) = scale1 * alpha1[n] * p1[n,v,c] + beta[n,c]
+//             + (pool_idx[n, pool(v), c] == sub(v) ? pool_dy[n, pool(v), c] : 0)
+struct DySrc {
+  const void* p1;
+  int ld1;
+  float scale1;
+  const float* alpha1;   // [N] (stride alpha_stride) or null
+  int alpha_stride;
+  const float* beta;     // [N][C] (stride beta_stride per n) or null
+  int beta_stride;
+  const void* pool_dy;   // [N][Vo][C] with ld pool_ld, or null
+  int pool_ld;
+  const uint8_t* pool_idx;  // [N][Vo][C]
+};
+
+template <typename T>
+__device__ __forceinline__ void gather_dy(const DySrc& s, long long n, long long v, long long nv, int cg, int C, int D,
+                                          int H, int W, float* dy) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dy[j] = 0.f;
+  if (s.p1) {
+    V8<T> a;
+    a.load(reinterpret_cast<const T*>(s.p1) + nv * s.ld1 + cg * 8);
+    float sc = s.scale1;
+    if (s.alpha1) sc *= s.alpha1[n * s.alpha_stride];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dy[j] = a.get(j) * sc;
+  }
+  if (s.beta) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dy[j] += s.beta[n * s.beta_stride + cg * 8 + j];
+  }
+  if (s.pool_dy) {
+    const int x = (int)(v % W);
+    long long q = v / W;
+    const int y = (int)(q % H);
+    const int z = (int)(q / H);
+    const int Ho = H >> 1, Wo = W >> 1, Do = D >> 1;
+    const long long vo = (n * Do + (z >> 1)) * (long long)Ho * Wo + (long long)(y >> 1) * Wo + (x >> 1);
+    const uint8_t sub = (uint8_t)(((z & 1) << 2) | ((y & 1) << 1) | (x & 1));
+    V8<T> pd;
+    pd.load(reinterpret_cast<const T*>(s.pool_dy) + vo * s.pool_ld + cg * 8);
+    const uint2 packed = *reinterpret_cast<const uint2*>(s.pool_idx + vo * C + cg * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t w = j < 4 ? packed.x : packed.y;
+      const uint8_t id = (uint8_t)((w >> ((j & 3) * 8)) & 0xff);
+      if (id == sub) dy[j] += pd.get(j);
+    }
+  }
+}
+
+// partial sums of g and g*xhat, g = dy * [xhat > 0]
+template <typename T>
+__global__ void in_bwd_partial(const T* __restrict__ x, int ldx, const float* __restrict__ mean,
+                               const float* __restrict__ rstd, DySrc s, long long V, int C, int D, int H, int W,
+                               long long vpc, float* __restrict__ part) {
+  const int n = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
+  const int C8 = C >> 3;
+  const int lanes_v = 256 / C8;
+  const int tid = threadIdx.x;
+  const int cg = tid % C8, vl = tid / C8;
+  float sg[8], sgx[8], mu[8], rs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sg[j] = 0.f;
+    sgx[j] = 0.f;
+    mu[j] = mean[n * C + cg * 8 + j];
+    rs[j] = rstd[n * C + cg * 8 + j];
+  }
+  const long long v0 = (long long)chunk * vpc;
+  long long v1 = v0 + vpc;
+  if (v1 > V) v1 = V;
+  if (vl < lanes_v) {
+    for (long long v = v0 + vl; v < v1; v += lanes_v) {
+      const long long nv = (long long)n * V + v;
+      V8<T> a;
+      a.load(x + nv * ldx + cg * 8);
+      float dy[8];
+      gather_dy<T>(s, n, v, nv, cg, C, D, H, W, dy);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float h = (a.get(j) - mu[j]) * rs[j];
+        const float g = h > 0.f ? dy[j] : 0.f;
+        sg[j] += g;
+        sgx[j] = fmaf(g, h, sgx[j]);
+      }
+    }
+  }
+  __shared__ float red[2][256 * 8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][tid * 8 + j] = sg[j];
+    red[1][tid * 8 + j] = sgx[j];
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    const int g = c >> 3, j = c & 7;
+    float a = 0.f, b = 0.f;
+    for (int l = 0; l < lanes_v; ++l) {
+      a += red[0][(l * C8 + g) * 8 + j];
+      b += red[1][(l * C8 + g) * 8 + j];
+    }
+    float* p = part + (((long long)n * nchunk + chunk) * C + c) * 2;
+    p[0] = a;
+    p[1] = b;
+  }
+}
+
+__global__ void in_bwd_finalize(const float* __restrict__ part, int N, int C, int nchunk, long long V,
+                                float* __restrict__ coef) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= N * C) return;
+  const int n = idx / C, c = idx - n * C;
+  double a = 0.0, b = 0.0;
+  for (int k = 0; k < nchunk; ++k) {
+    const float* p = part + (((long long)n * nchunk + k) * C + c) * 2;
+    a += p[0];
+    b += p[1];
+  }
+  coef[idx * 2 + 0] = (float)(a / (double)V);
+  coef[idx * 2 + 1] = (float)(b / (double)V);
+}
+
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat))
+template <typename T>
+__global__ void in_bwd_apply(const T* __restrict__ x, int ldx, const float* __restrict__ mean,
+                             const float* __restrict__ rstd, DySrc s, const float* __restrict__ coef, T* __restrict__ dx,
+                             int lddx, long long V, int N, int C, int D, int H, int W) {
+  const int C8 = C >> 3;
+  const long long total = (long long)N * V * C8;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % C8);
+    const long long nv = i / C8;
+    const long long n = nv / V;
+    const long long v = nv - n * V;
+    V8<T> a, o;
+    a.load(x + nv * ldx + cg * 8);
+    float dy[8];
+    gather_dy<T>(s, n, v, nv, cg, C, D, H, W, dy);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int nc = (int)n * C + cg * 8 + j;
+      const float rs = rstd[nc];
+      const float h = (a.get(j) - mean[nc]) * rs;
+      const float g = h > 0.f ? dy[j] : 0.f;
+      o.set(j, rs * (g - coef[nc * 2] - h * coef[nc * 2 + 1]));
+    }
+    o.store(dx + nv * lddx + cg * 8);
+  }
+}
+
+// ---------------------------------------------------------------- fusion
+// out[n,v,c] = sum_m w_m * src_m[n,v,c],  w_m = wconst or wts[n*M + m]
+struct FuseSrc {
+  const void* p[4];
+  int ld[4];
+  int M;
+  float wconst;
+  const float* wts;   // [N][M] or null
+};
+
+template <typename T>
+__global__ void fuse_fwd(FuseSrc s, T* __restrict__ out, int ldo, long long V, int N, int C) {
+  const int C8 = C >> 3;
+  const long long total = (long long)N * V * C8;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % C8);
+    const long long nv = i / C8;
+    const int n = (int)(nv / V);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int m = 0; m < s.M; ++m) {
+      V8<T> a;
+      a.load(reinterpret_cast<const T*>(s.p[m]) + nv * s.ld[m] + cg * 8);
+      const float w = s.wts ? s.wts[n * s.M + m] : 1.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = s.wts ? fmaf(a.get(j), w, acc[j]) : acc[j] + a.get(j);
+    }
+    V8<T> o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o.set(j, s.wts ? acc[j] : acc[j] * s.wconst);
+    o.store(out + nv * ldo + cg * 8);
+  }
+}
+
+// dots[n][m] partial: sum_{v,c} dfused[n,v,c] * src_m[n,v,c]
+template <typename T>
+__global__ void fuse_dot_partial(FuseSrc s, const T* __restrict__ dfused, int ldd, long long V, int C, long long vpc,
+                                 float* __restrict__ part) {
+  const int n = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
+  const int C8 = C >> 3;
+  const int tid = threadIdx.x;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const long long v0 = (long long)chunk * vpc;
+  long long v1 = v0 + vpc;
+  if (v1 > V) v1 = V;
+  const long long e0 = v0 * C8, e1 = v1 * C8;
+  for (long long e = e0 + tid; e < e1; e += 256) {
+    const long long v = e / C8;
+    const int cg = (int)(e - v * C8);
+    const long long nv = (long long)n * V + v;
+    V8<T> d;
+    d.load(dfused + nv * ldd + cg * 8);
+    for (int m = 0; m < s.M; ++m) {
+      V8<T> a;
+      a.load(reinterpret_cast<const T*>(s.p[m]) + nv * s.ld[m] + cg * 8);
+      float t = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t = fmaf(a.get(j), d.get(j), t);
+      acc[m] += t;
+    }
+  }
+  __shared__ float red[4][4];
+  const int lane = tid & 63, wave = tid >> 6;
+  for (int m = 0; m < s.M; ++m) {
+    float w = wave_sum(acc[m]);
+    if (lane == 0) red[m][wave] = w;
+  }
+  __syncthreads();
+  if (tid < s.M) part[((long long)n * nchunk + chunk) * 4 + tid] = red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3];
+}
+
+// ---------------------------------------------------- attention gate (SE)
+// pooled [N][MC] -> h = relu(W1 pooled + b1) [N][Hd] -> logits = W2 h + b2 [N][M] -> w = softmax
+__global__ void attn_gate_fwd(const float* __restrict__ pooled, const float* __restrict__ W1,
+                              const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ b2,
+                              float* __restrict__ hbuf, float* __restrict__ wts, int MC, int Hd, int M) {
+  const int n = blockIdx.x;
+  extern __shared__ float sh[];
+  float* h = sh;  // Hd
+  for (int k = threadIdx.x; k < Hd; k += blockDim.x) {
+    float a = 0.f;
+    for (int i = 0; i < MC; ++i) a = fmaf(W1[(long long)k * MC + i], pooled[(long long)n * MC + i], a);
+    a += b1[k];
+    a = a > 0.f ? a : 0.f;
+    h[k] = a;
+    hbuf[(long long)n * Hd + k] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float lg[4];
+    float mx = -INFINITY;
+    for (int m = 0; m < M; ++m) {
+      float a = 0.f;
+      for (int k = 0; k < Hd; ++k) a = fmaf(W2[m * Hd + k], h[k], a);
+      lg[m] = a + b2[m];
+      mx = fmaxf(mx, lg[m]);
+    }
+    float se = 0.f;
+    for (int m = 0; m < M; ++m) {
+      lg[m] = expf(lg[m] - mx);
+      se += lg[m];
+    }
+    for (int m = 0; m < M; ++m) wts[n * M + m] = lg[m] / se;
+  }
+}
+
+// Backward of the gate for all N (one block): inputs dots part -> dw[n][m];
+// writes beta[n][MC] = dpooled / V and the Linear gradients (accumulated).
+__global__ void attn_gate_bwd(const float* __restrict__ dot_part, int nchunk, const float* __restrict__ pooled,
+                              const float* __restrict__ W1, const float* __restrict__ W2,
+                              const float* __restrict__ hbuf, const float* __restrict__ wts, float* __restrict__ beta,
+                              float* __restrict__ gW1, float* __restrict__ gb1, float* __restrict__ gW2,
+                              float* __restrict__ gb2, int N, int MC, int Hd, int M, long long V, int accumulate) {
+  extern __shared__ float sh[];
+  float* dlog = sh;              // N*M
+  float* dh = sh + N * M;        // N*Hd
+  const int tid = threadIdx.x;
+  if (tid < N * M) {
+    const int n = tid / M, m = tid % M;
+    // dw for (n, *) in fixed order
+    float dw[4];
+    float s = 0.f;
+    for (int mm = 0; mm < M; ++mm) {
+      float a = 0.f;
+      for (int k = 0; k < nchunk; ++k) a += dot_part[((long long)n * nchunk + k) * 4 + mm];
+      dw[mm] = a;
+      s += wts[n * M + mm] * a;
+    }
+    dlog[tid] = wts[n * M + m] * (dw[m] - s);
+  }
+  __syncthreads();
+  for (int e = tid; e < N * Hd; e += blockDim.x) {
+    const int n = e / Hd, k = e % Hd;
+    float a = 0.f;
+    for (int m = 0; m < M; ++m) a = fmaf(W2[m * Hd + k], dlog[n * M + m], a);
+    dh[e] = hbuf[e] > 0.f ? a : 0.f;
+  }
+  __syncthreads();
+  // Linear2 grads
+  for (int e = tid; e < M * Hd; e += blockDim.x) {
+    const int m = e / Hd, k = e % Hd;
+    float a = 0.f;
+    for (int n = 0; n < N; ++n) a = fmaf(dlog[n * M + m], hbuf[n * Hd + k], a);
+    gW2[e] = accumulate ? gW2[e] + a : a;
+  }
+  for (int m = tid; m < M; m += blockDim.x) {
+    float a = 0.f;
+    for (int n = 0; n < N; ++n) a += dlog[n * M + m];
+    gb2[m] = accumulate ? gb2[m] + a : a;
+  }
+  // Linear1 grads and dpooled
+  for (long long e = tid; e < (long long)Hd * MC; e += blockDim.x) {
+    const int k = (int)(e / MC), i = (int)(e % MC);
+    float a = 0.f;
+    for (int n = 0; n < N; ++n) a = fmaf(dh[n * Hd + k], pooled[(long long)n * MC + i], a);
+    gW1[e] = accumulate ? gW1[e] + a : a;
+  }
+  for (int k = tid; k < Hd; k += blockDim.x) {
+    float a = 0.f;
+    for (int n = 0; n < N; ++n) a += dh[n * Hd + k];
+    gb1[k] = accumulate ? gb1[k] + a : a;
+  }
+  const float invV = 1.f / (float)V;
+  for (long long e = tid; e < (long long)N * MC; e += blockDim.x) {
+    const int n = (int)(e / MC), i = (int)(e % MC);
+    float a = 0.f;
+    for (int k = 0; k < Hd; ++k) a = fmaf(W1[(long long)k * MC + i], dh[n * Hd + k], a);
+    beta[e] = a * invV;
+  }
+}
+
+int grid_for(long long total) {
+  long long b = (total + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+int chunks_for(long long V, int C, long long* vpc) {
+  // ~ (4096 x C8 lanes) voxels per chunk, at most 256 chunks
+  const int lanes_v = 256 / (C >> 3);
+  long long want = (long long)lanes_v * 32;
+  long long nch = (V + want - 1) / want;
+  if (nch > 256) nch = 256;
+  if (nch < 1) nch = 1;
+  *vpc = (V + nch - 1) / nch;
+  return (int)((V + *vpc - 1) / *vpc);
+}
+
+}  // namespace
+
+extern "C" {
+
+// Workspace (floats) the stats / bwd-reduce kernels need for N samples.
+long long mmseg_instnorm_ws_floats(int N, long long V, int C) {
+  long long vpc;
+  int nch = chunks_for(V, C, &vpc);
+  return (long long)N * nch * C * 2 + (long long)N * C * 2;
+}
+
+// mean[n*mean_ld + c], rstd[n*C + c] (rstd may be null: channel means only)
+int mmseg_instnorm_stats(const void* x, int ldx, int N, long long V, int C, float eps, float* mean, int mean_ld,
+                         float* rstd, float* ws, int dtype, void* stream) {
+  MMSEG_REQUIRE(C % 8 == 0 && C <= 2048, "instnorm: C=%d must be a multiple of 8", C);
+  long long vpc;
+  const int nch = chunks_for(V, C, &vpc);
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(nch, N);
+  if (dtype == MMSEG_BF16) {
+    hipLaunchKernelGGL(in_stats_partial<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, V, C, vpc, ws);
+    hipLaunchKernelGGL(in_stats_finalize<bf16_t>, dim3(ceil_div(N * C, 256)), dim3(256), 0, s, (const bf16_t*)x, ldx,
+                       V, N, C, nch, ws, eps, mean, mean_ld, rstd);
+  } else {
+    hipLaunchKernelGGL(in_stats_partial<float>, grid, dim3(256), 0, s, (const float*)x, ldx, V, C, vpc, ws);
+    hipLaunchKernelGGL(in_stats_finalize<float>, dim3(ceil_div(N * C, 256)), dim3(256), 0, s, (const float*)x, ldx, V,
+                       N, C, nch, ws, eps, mean, mean_ld, rstd);
+  }
+  return mmseg::check_launch("instnorm_stats");
+}
+
+int mmseg_instnorm_relu_fwd(const void* x, int ldx, void* y, int ldy, int N, long long V, int C, const float* mean,
+                            const float* rstd, int dtype, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = grid_for((long long)N * V * (C / 8));
+  if (dtype == MMSEG_BF16)
+    hipLaunchKernelGGL(in_relu_apply<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, ldx, (bf16_t*)y, ldy, V,
+                       N, C, mean, rstd);
+  else
+    hipLaunchKernelGGL(in_relu_apply<float>, dim3(grid), dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy, V, N,
+                       C, mean, rstd);
+  return mmseg::check_launch("instnorm_relu_fwd");
+}
+
+// dy sources: see DySrc.  Any of p1 / beta / pool_dy may be null.
+int mmseg_instnorm_relu_bwd(const void* x, int ldx, const float* mean, const float* rstd, const void* p1, int ld1,
+                            float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
+                            const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N,
+                            int D, int H, int W, int C, float* ws, int dtype, void* stream) {
+  MMSEG_REQUIRE(C % 8 == 0, "instnorm_bwd: C=%d must be a multiple of 8", C);
+  MMSEG_REQUIRE(!pool_dy || ((D | H | W) & 1) == 0, "instnorm_bwd: pooled gather needs even dims");
+  const long long V = (long long)D * H * W;
+  long long vpc;
+  const int nch = chunks_for(V, C, &vpc);
+  DySrc src{p1, ld1, scale1, alpha1, alpha_stride, beta, beta_stride, pool_dy, pool_ld, pool_idx};
+  hipStream_t s = (hipStream_t)stream;
+  float* part = ws;
+  float* coef = ws + (long long)N * nch * C * 2;
+  dim3 grid(nch, N);
+  const int ag = grid_for((long long)N * V * (C / 8));
+  if (dtype == MMSEG_BF16) {
+    hipLaunchKernelGGL(in_bwd_partial<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, mean, rstd, src, V, C, D,
+                       H, W, vpc, part);
+    hipLaunchKernelGGL(in_bwd_finalize, dim3(ceil_div(N * C, 256)), dim3(256), 0, s, part, N, C, nch, V, coef);
+    hipLaunchKernelGGL(in_bwd_apply<bf16_t>, dim3(ag), dim3(256), 0, s, (const bf16_t*)x, ldx, mean, rstd, src, coef,
+                       (bf16_t*)dx, lddx, V, N, C, D, H, W);
+  } else {
+    hipLaunchKernelGGL(in_bwd_partial<float>, grid, dim3(256), 0, s, (const float*)x, ldx, mean, rstd, src, V, C, D,
+                       H, W, vpc, part);
+    hipLaunchKernelGGL(in_bwd_finalize, dim3(ceil_div(N * C, 256)), dim3(256), 0, s, part, N, C, nch, V, coef);
+    hipLaunchKernelGGL(in_bwd_apply<float>, dim3(ag), dim3(256), 0, s, (const float*)x, ldx, mean, rstd, src, coef,
+                       (float*)dx, lddx, V, N, C, D, H, W);
+  }
+  return mmseg::check_launch("instnorm_relu_bwd");
+}
+
+int mmseg_maxpool2_fwd(const void* x, int ldx, void* y, int ldy, uint8_t* idx, int N, int D, int H, int W, int C,
+                       int dtype, void* stream) {
+  MMSEG_REQUIRE(C % 8 == 0 && ((D | H | W) & 1) == 0, "maxpool2: C%%8==0 and even dims required");
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = grid_for((long long)N * (D / 2) * (H / 2) * (W / 2) * (C / 8));
+  if (dtype == MMSEG_BF16)
+    hipLaunchKernelGGL(maxpool2_fwd<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, ldx, (bf16_t*)y, ldy, idx,
+                       N, D, H, W, C);
+  else
+    hipLaunchKernelGGL(maxpool2_fwd<float>, dim3(grid), dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy, idx, N,
+                       D, H, W, C);
+  return mmseg::check_launch("maxpool2_fwd");
+}
+
+// out = wconst * sum_m src_m   (wts == null)   or   sum_m wts[n][m] * src_m
+int mmseg_fuse_fwd(const void* const* srcs, const int* lds, int M, float wconst, const float* wts, void* out, int ldo,
+                   int N, long long V, int C, int dtype, void* stream) {
+  MMSEG_REQUIRE(M >= 1 && M <= 4 && C % 8 == 0, "fuse: 1 <= M <= 4 and C%%8==0");
+  FuseSrc s{};
+  for (int m = 0; m < M; ++m) {
+    s.p[m] = srcs[m];
+    s.ld[m] = lds[m];
+  }
+  s.M = M;
+  s.wconst = wconst;
+  s.wts = wts;
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = grid_for((long long)N * V * (C / 8));
+  if (dtype == MMSEG_BF16)
+    hipLaunchKernelGGL(fuse_fwd<bf16_t>, dim3(grid), dim3(256), 0, st, s, (bf16_t*)out, ldo, V, N, C);
+  else
+    hipLaunchKernelGGL(fuse_fwd<float>, dim3(grid), dim3(256), 0, st, s, (float*)out, ldo, V, N, C);
+  return mmseg::check_launch("fuse_fwd");
+}
+
+int mmseg_attn_gate_fwd(const float* pooled, const float* W1, const float* b1, const float* W2, const float* b2,
+                        float* hbuf, float* wts, int N, int MC, int Hd, int M, void* stream) {
+  MMSEG_REQUIRE(M <= 4, "attn gate: M <= 4");
+  hipLaunchKernelGGL(attn_gate_fwd, dim3(N), dim3(256), Hd * sizeof(float), (hipStream_t)stream, pooled, W1, b1, W2,
+                     b2, hbuf, wts, MC, Hd, M);
+  return mmseg::check_launch("attn_gate_fwd");
+}
+
+// Backward of the attention fusion gate.  Computes dw from (dfused . src_m),
+// then beta = dpooled / V (feed to instnorm_relu_bwd) and the Linear grads.
+int mmseg_attn_gate_bwd(const void* const* srcs, const int* lds, int M, const void* dfused, int ldd, int N, long long V,
+                        int C, const float* pooled, const float* W1, const float* W2, const float* hbuf,
+                        const float* wts, float* beta, float* gW1, float* gb1, float* gW2, float* gb2, int Hd,
+                        float* ws, int accumulate, int dtype, void* stream) {
+  MMSEG_REQUIRE(M <= 4 && C % 8 == 0, "attn gate bwd: M <= 4");
+  FuseSrc s{};
+  for (int m = 0; m < M; ++m) {
+    s.p[m] = srcs[m];
+    s.ld[m] = lds[m];
+  }
+  s.M = M;
+  long long want = 256 * 64;
+  long long nch = (V * (C / 8) + want - 1) / want;
+  if (nch > 256) nch = 256;
+  long long vpc = (V + nch - 1) / nch;
+  nch = (V + vpc - 1) / vpc;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == MMSEG_BF16)
+    hipLaunchKernelGGL(fuse_dot_partial<bf16_t>, dim3((int)nch, N), dim3(256), 0, st, s, (const bf16_t*)dfused, ldd, V,
+                       C, vpc, ws);
+  else
+    hipLaunchKernelGGL(fuse_dot_partial<float>, dim3((int)nch, N), dim3(256), 0, st, s, (const float*)dfused, ldd, V, C,
+                       vpc, ws);
+  if (mmseg::check_launch("fuse_dot_partial")) return 1;
+  const int MC = M * C;
+  const size_t shm = (size_t)(N * M + N * Hd) * sizeof(float);
+  hipLaunchKernelGGL(attn_gate_bwd, dim3(1), dim3(256), shm, st, ws, (int)nch, pooled, W1, W2, hbuf, wts, beta, gW1,
+                     gb1, gW2, gb2, N, MC, Hd, M, V, accumulate);
+  return mmseg::check_launch("attn_gate_bwd");
+}
+
+}  // extern "C"

@@ -1,0 +1,110 @@
+"""Data parallelism over RCCL (torch.distributed backend "nccl" == RCCL on
+ROCm), one process per GPU.  The reference is single-process;
+this is new work whose oracle is "N ranks x B == 1 rank x N*B".
+
+  * sharding: rank r takes samples r, r+W, ... of each global batch
+    (DistributedSampler semantics) — see `shard_indices`;
+  * gradients live in the engine's flat arena; `GradBuckets` splits it into
+    ~bucket_mb buckets (reverse registration order = backward order) and
+    all-reduces each bucket with ReduceOp.AVG as soon as the engine has
+    written every gradient in it, so RCCL traffic over xGMI overlaps the rest
+    of the backward; `finish()` joins them before the optimizer step;
+  * validation counts (Dice I/U) are summed with one all_reduce.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+def world() -> int:
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def rank() -> int:
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+def init_from_env(backend: Optional[str] = None) -> int:
+    """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/MASTER_*); returns local rank."""
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    return local
+
+
+def shard_indices(n_samples: int, r: int, w: int) -> List[int]:
+    return list(range(r, n_samples, w))
+
+
+class GradBuckets:
+    """Bucketed, backward-overlapped gradient averaging over a flat arena."""
+
+    def __init__(self, grad_flat: torch.Tensor, param_offsets: List[int], param_sizes: List[int],
+                 bucket_mb: float = 32.0, group=None):
+        self.grad = grad_flat
+        self.group = group
+        self.w = world()
+        nbytes = int(bucket_mb * 1024 * 1024)
+        # buckets over parameter index ranges, from the END of the arena (backward order)
+        self.buckets = []          # (lo_param, hi_param, lo_elem, hi_elem)
+        hi = len(param_offsets)
+        while hi > 0:
+            lo = hi - 1
+            size = param_sizes[lo]
+            while lo > 0 and (size + param_sizes[lo - 1]) * 4 <= nbytes:
+                lo -= 1
+                size += param_sizes[lo]
+            self.buckets.append((lo, hi, param_offsets[lo], param_offsets[hi - 1] + param_sizes[hi - 1]))
+            hi = lo
+        self.owner = [0] * len(param_offsets)
+        for b, (lo, hi, _, _) in enumerate(self.buckets):
+            for i in range(lo, hi):
+                self.owner[i] = b
+        self.reset()
+
+    def reset(self):
+        self.pending = [hi - lo for (lo, hi, _, _) in self.buckets]
+        self.works = []
+
+    def _reduce(self, b: int):
+        _, _, lo, hi = self.buckets[b]
+        t = self.grad[lo:hi]
+        if dist.get_backend(self.group) == "nccl":
+            self.works.append(dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group, async_op=True))
+        else:  # gloo has no AVG
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            t.div_(self.w)
+
+    def param_ready(self, idx: int):
+        if self.w == 1:
+            return
+        b = self.owner[idx]
+        self.pending[b] -= 1
+        if self.pending[b] == 0:
+            self._reduce(b)
+
+    def finish(self):
+        if self.w == 1:
+            return
+        for b, n in enumerate(self.pending):
+            if n > 0:          # a parameter the engine did not report: reduce anyway (correctness first)
+                self.pending[b] = 0
+                self._reduce(b)
+        for wk in self.works:
+            wk.wait()
+        self.reset()
+
+
+def allreduce_sum_(t: torch.Tensor) -> torch.Tensor:
+    if world() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t

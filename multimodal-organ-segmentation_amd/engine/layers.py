@@ -1,0 +1,297 @@
+"""Engine layers: each binds an nn.Module parameter container (so state-dict
+names, init and checkpoints stay the reference's) to the HIP kernels.
+
+  Conv3      nn.Conv3d(k=3, pad=1)          reference unet.py:26-27
+  ConvT2     nn.ConvTranspose3d(k=2, s=2)   reference unet.py:95
+  Point      nn.Conv3d(k=1) fusion proj     reference dual_encoder.py:75
+  Block      ConvBlock3D = (Conv3 + InstanceNorm3d + ReLU) x 2   unet.py:12-60
+  Head       Dropout3d + out_conv 1x1       unet.py:162-163 / dual_encoder.py:83-84
+
+Forward/backward are explicit kernel sequences.  Backward buffers alias
+forward buffers whose last reader has already run (weight-gradient GEMMs are
+always issued before the data-gradient GEMM that overwrites their input),
+so a training step needs no activation memory beyond the forward's.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from .._lib import ptr
+from .runtime import Act, FlatParams, Runtime, pow2_shift, round_up
+
+MODE_CONV3, MODE_POINT, MODE_CONVT_FWD, MODE_CONVT_DGRAD = 0, 1, 2, 3
+IN_EPS = 1e-5
+TARGET_BLOCKS = 1024
+
+
+def _col_tile(n: int) -> int:
+    return round_up(n, 64 if n >= 64 else 32)
+
+
+def _gemm_ksplit(M: int, ncols: int, KG: int) -> int:
+    tiles = -(-M // 128) * -(-ncols // (64 if ncols >= 64 else 32))
+    if tiles >= 512 or KG < 32:
+        return 1
+    return max(1, min(-(-512 // tiles), KG // 16))
+
+
+def _wgrad_ksplit(rows: int, ncols: int, V: int) -> int:
+    tiles = -(-ncols // 64) * -(-rows // (64 if rows % 64 == 0 else 32))
+    return max(1, min(-(-TARGET_BLOCKS // tiles), V // 512))
+
+
+@dataclass
+class DySpec:
+    """Gradient sources of an InstanceNorm+ReLU output (see mmseg_instnorm_relu_bwd)."""
+    p1: Optional[Act] = None
+    scale1: float = 1.0
+    alpha: Optional[torch.Tensor] = None   # [N][stride] fp32
+    alpha_off: int = 0
+    alpha_stride: int = 0
+    beta: Optional[torch.Tensor] = None    # [N][stride] fp32
+    beta_off: int = 0
+    beta_stride: int = 0
+    pool_dy: Optional[Act] = None
+    pool_idx: Optional[torch.Tensor] = None
+
+
+class Conv3:
+    def __init__(self, rt: Runtime, conv: nn.Conv3d, flat: FlatParams, cin_pad: Optional[int] = None,
+                 need_dgrad: bool = True):
+        self.rt, self.conv, self.flat = rt, conv, flat
+        self.Co, self.Ci = conv.weight.shape[:2]
+        self.Cip = cin_pad or self.Ci
+        if self.Co % 8 or self.Cip % 8:
+            raise ValueError("conv channels must be multiples of 8")
+        self.cpg_shift = pow2_shift(self.Cip // 8)
+        self.KG = 27 * self.Cip // 8
+        self.KGp = round_up(self.KG, 4)
+        self.Cpad = _col_tile(self.Co)
+        self.wf = torch.empty(self.KGp * self.Cpad * 8, dtype=rt.dtype, device=rt.device)
+        self.need_dgrad = need_dgrad
+        if need_dgrad:
+            self.dshift = pow2_shift(self.Co // 8)
+            self.KGd = 27 * self.Co // 8
+            self.KGdp = round_up(self.KGd, 4)
+            self.Cpad_d = _col_tile(self.Cip)
+            self.wd = torch.empty(self.KGdp * self.Cpad_d * 8, dtype=rt.dtype, device=rt.device)
+
+    def pack(self):
+        L, s, w = self.rt.lib, self.rt.stream, self.conv.weight
+        L.mmseg_pack_weight(ptr(w), ptr(self.wf), 0, self.Co, self.Ci, self.Cip, self.KG, self.KGp, self.Cpad,
+                            self.rt.code, s)
+        if self.need_dgrad:
+            L.mmseg_pack_weight(ptr(w), ptr(self.wd), 1, self.Co, self.Ci, self.Cip, self.KGd, self.KGdp,
+                                self.Cpad_d, self.rt.code, s)
+
+    def fwd(self, x: Act, y: Act):
+        M = x.N * x.V
+        ks = _gemm_ksplit(M, self.Co, self.KG)
+        ws = self.rt.ws(ks * M * self.Co) if ks > 1 else None
+        self.rt.lib.mmseg_conv_gemm(x.ptr, x.ld, ptr(self.wf), ptr(self.conv.bias), y.ptr, y.ld, ptr(ws), MODE_CONV3,
+                                    M, self.Co, self.Cpad, self.KG, self.cpg_shift, x.D, x.H, x.W, ks, self.rt.code,
+                                    self.rt.stream)
+
+    def bwd(self, x: Act, dy: Act, dx: Optional[Act], accumulate: bool):
+        L, s, code = self.rt.lib, self.rt.stream, self.rt.code
+        V = x.N * x.V
+        ncols = 27 * self.Cip
+        ks = L.mmseg_wgrad_splits(V, _wgrad_ksplit(self.Co, ncols, V))
+        part = self.rt.ws(max(ks * self.Co * ncols, 256 * self.Co))
+        L.mmseg_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, ptr(part), MODE_CONV3, self.Co, ncols, self.cpg_shift, V, x.D, x.H,
+                      x.W, ks, code, s)
+        L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.conv.weight)), self.Co, ncols, ks, self.Cip, self.Ci,
+                             27, int(accumulate), s)
+        nblk = 256
+        L.mmseg_colsum(dy.ptr, dy.ld, self.Co, V, ptr(part), nblk, ptr(self.flat.grad(self.conv.bias)),
+                       int(accumulate), code, s)
+        self.flat.mark(self.conv.weight, self.conv.bias)
+        if dx is not None:
+            M = V
+            ks = _gemm_ksplit(M, self.Ci, self.KGd)
+            ws = self.rt.ws(ks * M * self.Ci) if ks > 1 else None
+            L.mmseg_conv_gemm(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, ptr(ws), MODE_CONV3, M, self.Ci,
+                              self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, ks, code, s)
+
+
+class ConvT2:
+    def __init__(self, rt: Runtime, up: nn.ConvTranspose3d, flat: FlatParams):
+        self.rt, self.up, self.flat = rt, up, flat
+        self.Ci, self.Co = up.weight.shape[:2]
+        if self.Ci % 8 or self.Co % 8:
+            raise ValueError("transposed-conv channels must be multiples of 8")
+        self.KG = self.Ci // 8
+        self.KGp = round_up(self.KG, 4)
+        self.Cpad = _col_tile(8 * self.Co)
+        self.wf = torch.empty(self.KGp * self.Cpad * 8, dtype=rt.dtype, device=rt.device)
+        self.dshift = pow2_shift(self.Co // 8)
+        self.KGd = self.Co  # 8 taps x Co/8 groups
+        self.KGdp = round_up(self.KGd, 4)
+        self.Cpad_d = _col_tile(self.Ci)
+        self.wd = torch.empty(self.KGdp * self.Cpad_d * 8, dtype=rt.dtype, device=rt.device)
+
+    def pack(self):
+        L, s, w = self.rt.lib, self.rt.stream, self.up.weight
+        L.mmseg_pack_weight(ptr(w), ptr(self.wf), 4, self.Co, self.Ci, self.Ci, self.KG, self.KGp, self.Cpad,
+                            self.rt.code, s)
+        L.mmseg_pack_weight(ptr(w), ptr(self.wd), 5, self.Co, self.Ci, self.Ci, self.KGd, self.KGdp, self.Cpad_d,
+                            self.rt.code, s)
+
+    def fwd(self, x: Act, y: Act):
+        M = x.N * x.V
+        ncols = 8 * self.Co
+        ks = _gemm_ksplit(M, ncols, self.KG)
+        ws = self.rt.ws(ks * M * ncols) if ks > 1 else None
+        self.rt.lib.mmseg_conv_gemm(x.ptr, x.ld, ptr(self.wf), ptr(self.up.bias), y.ptr, y.ld, ptr(ws),
+                                    MODE_CONVT_FWD, M, ncols, self.Cpad, self.KG, 0, x.D, x.H, x.W, ks, self.rt.code,
+                                    self.rt.stream)
+
+    def bwd(self, x: Act, dy: Act, dx: Optional[Act], accumulate: bool):
+        """x: input grid (D,H,W); dy: output grid (2D,2H,2W)."""
+        L, s, code = self.rt.lib, self.rt.stream, self.rt.code
+        V = x.N * x.V
+        ncols = 8 * self.Co
+        ks = L.mmseg_wgrad_splits(V, _wgrad_ksplit(self.Ci, ncols, V))
+        part = self.rt.ws(max(ks * self.Ci * ncols, 256 * self.Co))
+        L.mmseg_wgrad(x.ptr, x.ld, dy.ptr, dy.ld, ptr(part), MODE_CONVT_DGRAD, self.Ci, ncols, self.dshift, V, x.D,
+                      x.H, x.W, ks, code, s)
+        L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.up.weight)), self.Ci, ncols, ks, self.Co, self.Co, 8,
+                             int(accumulate), s)
+        L.mmseg_colsum(dy.ptr, dy.ld, self.Co, dy.N * dy.V, ptr(part), 256, ptr(self.flat.grad(self.up.bias)),
+                       int(accumulate), code, s)
+        self.flat.mark(self.up.weight, self.up.bias)
+        if dx is not None:
+            ks = _gemm_ksplit(V, self.Ci, self.KGd)
+            ws = self.rt.ws(ks * V * self.Ci) if ks > 1 else None
+            L.mmseg_conv_gemm(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, ptr(ws), MODE_CONVT_DGRAD, V, self.Ci,
+                              self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, ks, code, s)
+
+
+class Point:
+    """1x1x1 Conv3d on NDHWC (the DualEncoder concat-fusion projection)."""
+
+    def __init__(self, rt: Runtime, conv: nn.Conv3d, flat: FlatParams):
+        self.rt, self.conv, self.flat = rt, conv, flat
+        self.Co, self.Ci = conv.weight.shape[:2]
+        self.KG, self.KGp, self.Cpad = self.Ci // 8, round_up(self.Ci // 8, 4), _col_tile(self.Co)
+        self.KGd, self.KGdp, self.Cpad_d = self.Co // 8, round_up(self.Co // 8, 4), _col_tile(self.Ci)
+        self.wf = torch.empty(self.KGp * self.Cpad * 8, dtype=rt.dtype, device=rt.device)
+        self.wd = torch.empty(self.KGdp * self.Cpad_d * 8, dtype=rt.dtype, device=rt.device)
+
+    def pack(self):
+        L, s, w = self.rt.lib, self.rt.stream, self.conv.weight
+        L.mmseg_pack_weight(ptr(w), ptr(self.wf), 2, self.Co, self.Ci, self.Ci, self.KG, self.KGp, self.Cpad,
+                            self.rt.code, s)
+        L.mmseg_pack_weight(ptr(w), ptr(self.wd), 3, self.Co, self.Ci, self.Ci, self.KGd, self.KGdp, self.Cpad_d,
+                            self.rt.code, s)
+
+    def fwd(self, x: Act, y: Act):
+        M = x.N * x.V
+        self.rt.lib.mmseg_conv_gemm(x.ptr, x.ld, ptr(self.wf), ptr(self.conv.bias), y.ptr, y.ld, None, MODE_POINT, M,
+                                    self.Co, self.Cpad, self.KG, 0, x.D, x.H, x.W, 1, self.rt.code, self.rt.stream)
+
+    def bwd(self, x: Act, dy: Act, dx: Optional[Act], accumulate: bool):
+        L, s, code = self.rt.lib, self.rt.stream, self.rt.code
+        V = x.N * x.V
+        ks = L.mmseg_wgrad_splits(V, _wgrad_ksplit(self.Co, self.Ci, V))
+        part = self.rt.ws(max(ks * self.Co * self.Ci, 256 * self.Co))
+        L.mmseg_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, ptr(part), MODE_POINT, self.Co, self.Ci, 0, V, x.D, x.H, x.W, ks,
+                      code, s)
+        L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.conv.weight)), self.Co, self.Ci, ks, self.Ci, self.Ci,
+                             1, int(accumulate), s)
+        L.mmseg_colsum(dy.ptr, dy.ld, self.Co, V, ptr(part), 256, ptr(self.flat.grad(self.conv.bias)),
+                       int(accumulate), code, s)
+        self.flat.mark(self.conv.weight, self.conv.bias)
+        if dx is not None:
+            L.mmseg_conv_gemm(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, None, MODE_POINT, V, self.Ci,
+                              self.Cpad_d, self.KGd, 0, x.D, x.H, x.W, 1, code, s)
+
+
+class Block:
+    """ConvBlock3D: conv1 -> IN -> ReLU -> conv2 -> IN -> ReLU (reference unet.py:53-60)."""
+
+    def __init__(self, rt: Runtime, module: nn.Module, flat: FlatParams, cin_pad: Optional[int] = None,
+                 need_dgrad: bool = True):
+        self.rt = rt
+        self.c1 = Conv3(rt, module.conv1, flat, cin_pad=cin_pad, need_dgrad=need_dgrad)
+        self.c2 = Conv3(rt, module.conv2, flat)
+        self.Co = self.c1.Co
+        self.shape = None
+
+    def pack(self):
+        self.c1.pack()
+        self.c2.pack()
+
+    def setup(self, N, D, H, W):
+        if self.shape == (N, D, H, W):
+            return
+        self.shape = (N, D, H, W)
+        rt, C = self.rt, self.Co
+        self.x1 = rt.act(N, D, H, W, C)
+        self.y1 = rt.act(N, D, H, W, C)
+        self.x2 = rt.act(N, D, H, W, C)
+        self.stats = torch.empty(4, N * C, dtype=torch.float32, device=rt.device)  # m1, r1, m2, r2
+
+    def _norm_fwd(self, x: Act, y: Act, m: torch.Tensor, r: torch.Tensor):
+        L, s, code = self.rt.lib, self.rt.stream, self.rt.code
+        ws = self.rt.ws(L.mmseg_instnorm_ws_floats(x.N, x.V, x.C))
+        L.mmseg_instnorm_stats(x.ptr, x.ld, x.N, x.V, x.C, IN_EPS, ptr(m), x.C, ptr(r), ptr(ws), code, s)
+        L.mmseg_instnorm_relu_fwd(x.ptr, x.ld, y.ptr, y.ld, x.N, x.V, x.C, ptr(m), ptr(r), code, s)
+
+    def _norm_bwd(self, x: Act, m: torch.Tensor, r: torch.Tensor, dy: DySpec, dx: Act):
+        L, s, code = self.rt.lib, self.rt.stream, self.rt.code
+        ws = self.rt.ws(L.mmseg_instnorm_ws_floats(x.N, x.V, x.C))
+        p1 = dy.p1
+        es = 4
+        alpha = None if dy.alpha is None else dy.alpha.data_ptr() + dy.alpha_off * es
+        beta = None if dy.beta is None else dy.beta.data_ptr() + dy.beta_off * es
+        L.mmseg_instnorm_relu_bwd(x.ptr, x.ld, ptr(m), ptr(r),
+                                  p1.ptr if p1 is not None else None, p1.ld if p1 is not None else 0, dy.scale1,
+                                  alpha, dy.alpha_stride, beta, dy.beta_stride,
+                                  dy.pool_dy.ptr if dy.pool_dy is not None else None,
+                                  dy.pool_dy.ld if dy.pool_dy is not None else 0, ptr(dy.pool_idx),
+                                  dx.ptr, dx.ld, x.N, x.D, x.H, x.W, x.C, ptr(ws), code, s)
+
+    def fwd(self, xin: Act, out: Act):
+        self.setup(xin.N, xin.D, xin.H, xin.W)
+        st = self.stats
+        self.c1.fwd(xin, self.x1)
+        self._norm_fwd(self.x1, self.y1, st[0], st[1])
+        self.c2.fwd(self.y1, self.x2)
+        self._norm_fwd(self.x2, out, st[2], st[3])
+
+    def bwd(self, xin: Act, dy: DySpec, dxin: Optional[Act], accumulate: bool):
+        st = self.stats
+        g2 = self.x2                      # in place over x2
+        self._norm_bwd(self.x2, st[2], st[3], dy, g2)
+        dy1 = self.y1                     # conv2 wgrad reads y1 before dgrad overwrites it
+        self.c2.bwd(self.y1, g2, dy1, accumulate)
+        g1 = self.x1
+        self._norm_bwd(self.x1, st[0], st[1], DySpec(p1=dy1), g1)
+        self.c1.bwd(xin, g1, dxin, accumulate)
+
+
+class Head:
+    """Dropout3d (per-(n,c) scale) + 1x1 out_conv -> NCDHW fp32 logits."""
+
+    def __init__(self, rt: Runtime, conv: nn.Conv3d, flat: FlatParams):
+        self.rt, self.conv, self.flat = rt, conv, flat
+        self.C, self.Cin = conv.weight.shape[:2]
+
+    def fwd(self, x: Act, logits: torch.Tensor, dscale: Optional[torch.Tensor]):
+        self.dscale = dscale
+        self.rt.lib.mmseg_head_fwd(x.ptr, x.ld, self.Cin, ptr(self.conv.weight), ptr(self.conv.bias), ptr(dscale),
+                                   self.C, x.N, x.V, ptr(logits), self.rt.code, self.rt.stream)
+
+    def bwd(self, x: Act, dlogits: torch.Tensor, dx: Optional[Act], accumulate: bool):
+        L = self.rt.lib
+        ws = self.rt.ws(L.mmseg_head_ws_floats(self.C, self.Cin, x.N, x.V))
+        L.mmseg_head_bwd(x.ptr, x.ld, self.Cin, ptr(self.conv.weight), ptr(self.dscale), self.C, x.N, x.V,
+                         ptr(dlogits), dx.ptr if dx is not None else None, dx.ld if dx is not None else 0,
+                         ptr(self.flat.grad(self.conv.weight)), ptr(self.flat.grad(self.conv.bias)), ptr(ws),
+                         int(accumulate), self.rt.code, self.rt.stream)
+        self.flat.mark(self.conv.weight, self.conv.bias)

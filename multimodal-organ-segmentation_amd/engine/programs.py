@@ -1,0 +1,307 @@
+"""Whole-network programs: UNet3D and DualEncoder forward / backward as fixed
+kernel sequences over buffers planned once per input shape.
+
+Memory plan (per level l, spatial S/2^l, F[l] channels, NDHWC):
+  cat[l]   [N, V_l, 2F[l]]  decoder input: [:F] = upsampled, [F:] = skip.
+           The encoder (UNet) or the fusion kernel (DualEncoder) writes the
+           skip straight into its slot and the transposed conv writes the
+           upsampled half, so torch.cat (reference unet.py:111) never runs.
+  pooled[l], idx[l]         MaxPool3d output + argmax (uint8) feeding level l.
+  dcat / dd / dp            backward tensors alias cat / decoder outputs /
+                            pooled (their last forward reader has run).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from .._lib import ptr
+from .layers import Block, ConvT2, DySpec, Head, Point
+from .runtime import Act, FlatParams, Runtime
+
+
+def _check_dims(D, H, W, levels):
+    f = 1 << (levels - 1)
+    if D % f or H % f or W % f:
+        raise ValueError(
+            f"spatial dims {D}x{H}x{W} must be divisible by {f} (the reference's size-mismatch "
+            "interpolate branch, unet.py:108-109, is not on the engine path)")
+
+
+class _Decoder:
+    """Shared decoder + head of UNet3D / DualEncoder (reference unet.py:189-196)."""
+
+    def __init__(self, rt: Runtime, up_blocks: nn.ModuleList, out_conv: nn.Conv3d, dropout: float,
+                 flat: FlatParams, features: List[int]):
+        self.rt, self.F = rt, features
+        self.ups = [ConvT2(rt, d.up, flat) for d in up_blocks]
+        self.blocks = [Block(rt, d.conv, flat) for d in up_blocks]
+        self.head = Head(rt, out_conv, flat)
+        self.p = dropout
+
+    def pack(self):
+        for u in self.ups:
+            u.pack()
+        for b in self.blocks:
+            b.pack()
+
+    def setup(self, N, dims):
+        rt, F = self.rt, self.F
+        self.cat = [rt.act(N, *dims[l], 2 * F[l]) for l in range(len(F) - 1)]
+        self.dout = [rt.act(N, *dims[l], F[l]) for l in range(len(F) - 1)]
+
+    def skip_slot(self, l: int) -> Act:
+        return self.cat[l].slot(self.F[l], self.F[l])
+
+    def fwd(self, bottom: Act, training: bool):
+        h = bottom
+        nl = len(self.F) - 1
+        for j in range(nl):
+            l = nl - 1 - j
+            self.ups[j].fwd(h, self.cat[l].slot(0, self.F[l]))
+            self.blocks[j].fwd(self.cat[l], self.dout[l])
+            h = self.dout[l]
+        dscale = None
+        if training and self.p > 0:
+            keep = torch.empty(h.N, h.C, device=self.rt.device).bernoulli_(1.0 - self.p)
+            dscale = keep / (1.0 - self.p)
+        # fresh logits every call (caching allocator, no copy): callers may keep them
+        logits = torch.empty(h.N, self.head.C, h.D, h.H, h.W, dtype=torch.float32, device=self.rt.device)
+        self.head.fwd(h, logits, dscale)
+        return logits
+
+    def bwd(self, bottom: Act, dlogits: torch.Tensor, accumulate: bool) -> Act:
+        """Returns the gradient of `bottom` (aliases `bottom`'s buffer)."""
+        nl = len(self.F) - 1
+        dh = self.dout[0]
+        self.head.bwd(self.dout[0], dlogits, dh, accumulate)
+        for j in reversed(range(nl)):
+            l = nl - 1 - j
+            self.blocks[j].bwd(self.cat[l], DySpec(p1=dh), self.cat[l], accumulate)   # dcat aliases cat
+            x_up = bottom if j == 0 else self.dout[l + 1]
+            self.ups[j].bwd(x_up, self.cat[l].slot(0, self.F[l]), x_up, accumulate)   # dd aliases x_up
+            dh = x_up
+        return bottom
+
+
+class UNetProgram:
+    """UNet3D (reference unet.py:116-200) on the HIP engine."""
+
+    def __init__(self, rt: Runtime, m: nn.Module, flat: FlatParams):
+        self.rt, self.m, self.flat = rt, m, flat
+        self.F = list(m.features)
+        self.L = len(self.F)
+        self.cin = m.in_channels
+        if self.cin > 8:
+            raise ValueError("UNet3D engine supports up to 8 input channels")
+        self.init = Block(rt, m.init_conv, flat, cin_pad=8, need_dgrad=False)
+        self.enc = [Block(rt, e.conv, flat) for e in m.encoders]
+        self.dec = _Decoder(rt, m.decoders, m.out_conv, m.dropout_p, flat, self.F)
+        self.shape = None
+
+    def pack(self):
+        self.init.pack()
+        for b in self.enc:
+            b.pack()
+        self.dec.pack()
+
+    def setup(self, N, D, H, W):
+        if self.shape == (N, D, H, W):
+            return
+        _check_dims(D, H, W, self.L)
+        self.shape = (N, D, H, W)
+        rt, F = self.rt, self.F
+        dims = [(D >> l, H >> l, W >> l) for l in range(self.L)]
+        self.dims = dims
+        self.xin = rt.act(N, *dims[0], 8)
+        self.dec.setup(N, dims)
+        self.pooled = [None] + [rt.act(N, *dims[l], F[l - 1]) for l in range(1, self.L)]
+        self.idx = [None] + [torch.empty(N * dims[l][0] * dims[l][1] * dims[l][2] * F[l - 1], dtype=torch.uint8,
+                                         device=rt.device) for l in range(1, self.L)]
+        self.bottom = rt.act(N, *dims[-1], F[-1])
+
+    def level_out(self, l: int) -> Act:
+        return self.dec.skip_slot(l) if l < self.L - 1 else self.bottom
+
+    def forward(self, x: torch.Tensor, training: bool) -> torch.Tensor:
+        N, Cx, D, H, W = x.shape
+        self.setup(N, D, H, W)
+        L, s, code = self.rt.lib, self.rt.stream, self.rt.code
+        self.pack()
+        L.mmseg_pack_input(ptr(x), Cx, 0, Cx, N, D * H * W, self.xin.ptr, code, s)
+        self.init.fwd(self.xin, self.level_out(0))
+        for l in range(1, self.L):
+            prev = self.level_out(l - 1)
+            d = self.dims[l - 1]
+            L.mmseg_maxpool2_fwd(prev.ptr, prev.ld, self.pooled[l].ptr, self.pooled[l].ld, ptr(self.idx[l]), N, *d,
+                                 prev.C, code, s)
+            self.enc[l - 1].fwd(self.pooled[l], self.level_out(l))
+        return self.dec.fwd(self.bottom, training)
+
+    def backward(self, dlogits: torch.Tensor, accumulate: bool):
+        dbottom = self.dec.bwd(self.bottom, dlogits, accumulate)
+        dy = DySpec(p1=dbottom)
+        for l in range(self.L - 1, 0, -1):
+            self.enc[l - 1].bwd(self.pooled[l], dy, self.pooled[l], accumulate)   # dp aliases pooled
+            dy = DySpec(p1=self.dec.skip_slot(l - 1), pool_dy=self.pooled[l], pool_idx=self.idx[l])
+        self.init.bwd(self.xin, dy, None, accumulate)
+
+
+class DualEncoderProgram:
+    """DualEncoder (reference dual_encoder.py:15-204): one encoder per
+    modality, per-level fusion (mean / add / concat+1x1 / CrossModalAttention),
+    shared decoder."""
+
+    def __init__(self, rt: Runtime, m: nn.Module, flat: FlatParams):
+        self.rt, self.m, self.flat = rt, m, flat
+        self.F = list(m.features)
+        self.L = len(self.F)
+        self.M = m.num_modalities
+        if self.M > 4:
+            raise ValueError("DualEncoder engine supports up to 4 modalities")
+        self.fusion = m.fusion_kind
+        self.encs = []
+        for e in m.encoders:
+            blocks = [Block(rt, e["init_conv"], flat, cin_pad=8, need_dgrad=False)]
+            blocks += [Block(rt, b.conv, flat) for b in e["blocks"]]
+            self.encs.append(blocks)
+        self.proj = [Point(rt, p, flat) for p in m.fusion_proj] if self.fusion == "concat" else None
+        self.gates = list(m.fusion_layers) if self.fusion == "attention" else None
+        self.dec = _Decoder(rt, m.decoder, m.out_conv, m.dropout_p, flat, self.F)
+        self.flat = flat
+        self.shape = None
+
+    def pack(self):
+        for blocks in self.encs:
+            for b in blocks:
+                b.pack()
+        if self.proj:
+            for p in self.proj:
+                p.pack()
+        self.dec.pack()
+
+    def setup(self, N, D, H, W):
+        if self.shape == (N, D, H, W):
+            return
+        _check_dims(D, H, W, self.L)
+        self.shape = (N, D, H, W)
+        rt, F, M = self.rt, self.F, self.M
+        dims = [(D >> l, H >> l, W >> l) for l in range(self.L)]
+        self.dims = dims
+        self.xin = [rt.act(N, *dims[0], 8) for _ in range(M)]
+        self.dec.setup(N, dims)
+        # per-modality level outputs
+        if self.fusion == "concat":
+            self.ycat = [rt.act(N, *dims[l], M * F[l]) for l in range(self.L)]
+            self.y = [[self.ycat[l].slot(m * F[l], F[l]) for l in range(self.L)] for m in range(M)]
+        else:
+            self.y = [[rt.act(N, *dims[l], F[l]) for l in range(self.L)] for _ in range(M)]
+        self.pooled = [[None] + [rt.act(N, *dims[l], F[l - 1]) for l in range(1, self.L)] for _ in range(M)]
+        self.idx = [[None] + [torch.empty(N * dims[l][0] * dims[l][1] * dims[l][2] * F[l - 1], dtype=torch.uint8,
+                                          device=rt.device) for l in range(1, self.L)] for _ in range(M)]
+        self.bottom = rt.act(N, *dims[-1], F[-1])
+        if self.fusion == "attention":
+            self.pooled_mean = [torch.empty(N, M * F[l], dtype=torch.float32, device=rt.device) for l in range(self.L)]
+            self.gate_h = [torch.empty(N, M * F[l] // 4, dtype=torch.float32, device=rt.device) for l in range(self.L)]
+            self.gate_w = [torch.empty(N, M, dtype=torch.float32, device=rt.device) for l in range(self.L)]
+            self.gate_beta = [torch.empty(N, M * F[l], dtype=torch.float32, device=rt.device) for l in range(self.L)]
+
+    def fused_out(self, l: int) -> Act:
+        return self.dec.skip_slot(l) if l < self.L - 1 else self.bottom
+
+    def _fuse_fwd(self, l: int):
+        L, s, code = self.rt.lib, self.rt.stream, self.rt.code
+        out = self.fused_out(l)
+        ys = [self.y[m][l] for m in range(self.M)]
+        N, V, C = out.N, out.V, out.C
+        if self.fusion == "concat":
+            self.proj[l].fwd(self.ycat[l], out)
+            return
+        srcs = _ptr_array([y.ptr for y in ys])
+        lds = _int_array([y.ld for y in ys])
+        if self.fusion == "attention":
+            g = self.gates[l]
+            for m, y in enumerate(ys):
+                ws = self.rt.ws(L.mmseg_instnorm_ws_floats(N, V, C))
+                L.mmseg_instnorm_stats(y.ptr, y.ld, N, V, C, 0.0, self.pooled_mean[l].data_ptr() + m * C * 4,
+                                       self.M * C, None, ptr(ws), code, s)
+            lin1, lin2 = g.attention[2], g.attention[4]
+            L.mmseg_attn_gate_fwd(ptr(self.pooled_mean[l]), ptr(lin1.weight), ptr(lin1.bias), ptr(lin2.weight),
+                                  ptr(lin2.bias), ptr(self.gate_h[l]), ptr(self.gate_w[l]), N, self.M * C,
+                                  lin1.weight.shape[0], self.M, s)
+            L.mmseg_fuse_fwd(srcs, lds, self.M, 1.0, ptr(self.gate_w[l]), out.ptr, out.ld, N, V, C, code, s)
+        else:
+            wconst = 1.0 if self.fusion == "add" else 1.0 / self.M
+            L.mmseg_fuse_fwd(srcs, lds, self.M, wconst, None, out.ptr, out.ld, N, V, C, code, s)
+
+    def forward(self, x: torch.Tensor, training: bool) -> torch.Tensor:
+        N, Cx, D, H, W = x.shape
+        if Cx != self.M:
+            raise ValueError(f"DualEncoder expects {self.M} modalities, got {Cx} channels")
+        self.setup(N, D, H, W)
+        L, s, code = self.rt.lib, self.rt.stream, self.rt.code
+        self.pack()
+        for m in range(self.M):
+            L.mmseg_pack_input(ptr(x), Cx, m, 1, N, D * H * W, self.xin[m].ptr, code, s)
+            blocks = self.encs[m]
+            blocks[0].fwd(self.xin[m], self.y[m][0])
+            for l in range(1, self.L):
+                prev = self.y[m][l - 1]
+                L.mmseg_maxpool2_fwd(prev.ptr, prev.ld, self.pooled[m][l].ptr, self.pooled[m][l].ld,
+                                     ptr(self.idx[m][l]), N, *self.dims[l - 1], prev.C, code, s)
+                blocks[l].fwd(self.pooled[m][l], self.y[m][l])
+        for l in range(self.L):
+            self._fuse_fwd(l)
+        return self.dec.fwd(self.bottom, training)
+
+    def backward(self, dlogits: torch.Tensor, accumulate: bool):
+        L, s, code = self.rt.lib, self.rt.stream, self.rt.code
+        self.dec.bwd(self.bottom, dlogits, accumulate)
+        M = self.M
+        for l in range(self.L - 1, -1, -1):
+            dfused = self.fused_out(l)          # holds d(fused_l) now
+            N, V, C = dfused.N, dfused.V, dfused.C
+            base: List[DySpec] = []
+            if self.fusion == "concat":
+                # 1x1 projection backward: d(ycat) aliases ycat (its wgrad ran first)
+                self.proj[l].bwd(self.ycat[l], dfused, self.ycat[l], accumulate)
+                base = [DySpec(p1=self.y[m][l]) for m in range(M)]
+            elif self.fusion == "attention":
+                g = self.gates[l]
+                lin1, lin2 = g.attention[2], g.attention[4]
+                ys = [self.y[m][l] for m in range(M)]
+                ws = self.rt.ws(256 * 4 * N)
+                fl = self.flat
+                L.mmseg_attn_gate_bwd(_ptr_array([y.ptr for y in ys]), _int_array([y.ld for y in ys]), M,
+                                      dfused.ptr, dfused.ld, N, V, C, ptr(self.pooled_mean[l]), ptr(lin1.weight),
+                                      ptr(lin2.weight), ptr(self.gate_h[l]), ptr(self.gate_w[l]),
+                                      ptr(self.gate_beta[l]), ptr(fl.grad(lin1.weight)), ptr(fl.grad(lin1.bias)),
+                                      ptr(fl.grad(lin2.weight)), ptr(fl.grad(lin2.bias)), lin1.weight.shape[0],
+                                      ptr(ws), int(accumulate), code, s)
+                fl.mark(lin1.weight, lin1.bias, lin2.weight, lin2.bias)
+                base = [DySpec(p1=dfused, alpha=self.gate_w[l], alpha_off=m, alpha_stride=M,
+                               beta=self.gate_beta[l], beta_off=m * C, beta_stride=M * C) for m in range(M)]
+            else:
+                sc = 1.0 if self.fusion == "add" else 1.0 / M
+                base = [DySpec(p1=dfused, scale1=sc) for _ in range(M)]
+            for m in range(M):
+                dy = base[m]
+                if l < self.L - 1:
+                    dy.pool_dy = self.pooled[m][l + 1]
+                    dy.pool_idx = self.idx[m][l + 1]
+                blk = self.encs[m][l]
+                if l > 0:
+                    blk.bwd(self.pooled[m][l], dy, self.pooled[m][l], accumulate)
+                else:
+                    blk.bwd(self.xin[m], dy, None, accumulate)
+
+
+def _ptr_array(ptrs):
+    return (ctypes.c_void_p * len(ptrs))(*ptrs)
+
+
+def _int_array(vals):
+    return (ctypes.c_int * len(vals))(*vals)

@@ -1,0 +1,153 @@
+"""Device runtime of the segmentation engine: activation views, workspace,
+flat parameter / gradient arenas.
+
+Design (MI355X-first, not a translation of the reference's module graph):
+  * activations are NDHWC views (`Act`) into device buffers planned once per
+    input shape and reused every step, so a whole step is a fixed sequence of
+    kernel launches on one HIP stream (hipGraph-capturable);
+  * all parameters of a model live in ONE flat fp32 buffer and all gradients
+    in another (p.data / p.grad are views), so data-parallel all-reduce moves a
+    few large buckets and AdamW is a single kernel over the arena;
+  * every kernel is called through the C ABI (`_lib.lib()`); there is no
+    eager-PyTorch fallback for any op on the path.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import torch
+
+from .._lib import DTYPE_CODE, lib, ptr, stream_handle
+
+
+@dataclass
+class Act:
+    """NDHWC activation view: element (n, v, c) at buf[(n*V + v)*ld + off + c]."""
+    buf: torch.Tensor
+    off: int
+    C: int
+    ld: int
+    N: int
+    D: int
+    H: int
+    W: int
+
+    @property
+    def V(self) -> int:
+        return self.D * self.H * self.W
+
+    @property
+    def ptr(self) -> int:
+        return self.buf.data_ptr() + self.off * self.buf.element_size()
+
+    def slot(self, off: int, C: int) -> "Act":
+        return Act(self.buf, self.off + off, C, self.ld, self.N, self.D, self.H, self.W)
+
+    def to_ncdhw(self) -> torch.Tensor:
+        """Debug/test helper: materialise as a float32 NCDHW tensor (a copy)."""
+        t = self.buf[: self.N * self.V * self.ld].view(self.N, self.D, self.H, self.W, self.ld)
+        return t[..., self.off:self.off + self.C].permute(0, 4, 1, 2, 3).float().contiguous()
+
+
+class Runtime:
+    """Per-model device context: dtype, workspace arena, flat param/grad arenas."""
+
+    def __init__(self, device: torch.device, dtype: torch.dtype):
+        if device.type != "cuda":
+            raise RuntimeError(
+                "the MI355X segmentation engine runs on a ROCm device only (got %s); "
+                "there is no CPU fallback" % device)
+        if dtype not in DTYPE_CODE:
+            raise ValueError(f"engine dtype must be float32 or bfloat16, got {dtype}")
+        self.device = device
+        self.dtype = dtype
+        self.code = DTYPE_CODE[dtype]
+        self.lib = lib()
+        self._ws = torch.empty(0, dtype=torch.float32, device=device)
+
+    # ---------------------------------------------------------------- alloc
+    def act(self, N: int, D: int, H: int, W: int, C: int, ld: Optional[int] = None) -> Act:
+        ld = C if ld is None else ld
+        buf = torch.empty(N * D * H * W * ld, dtype=self.dtype, device=self.device)
+        return Act(buf, 0, C, ld, N, D, H, W)
+
+    def ws(self, nfloats: int) -> torch.Tensor:
+        """Scratch fp32 workspace shared by consecutive ops on the stream."""
+        nfloats = int(max(nfloats, 1))
+        if self._ws.numel() < nfloats:
+            self._ws = torch.empty(int(nfloats * 1.25) + 1024, dtype=torch.float32, device=self.device)
+        return self._ws
+
+    @property
+    def stream(self) -> int:
+        return stream_handle()
+
+
+class FlatParams:
+    """Flattens a module's parameters (registration order) into one fp32
+    device buffer and their gradients into another; p.data / p.grad become
+    views.  Gradients are written by the engine (accumulate flag per step)."""
+
+    def __init__(self, params: List[torch.nn.Parameter]):
+        self.params = list(params)
+        self.offsets: List[int] = []
+        off = 0
+        for p in self.params:
+            self.offsets.append(off)
+            off += p.numel()
+        self.numel = off
+        dev = self.params[0].device
+        self.flat = torch.empty(off, dtype=torch.float32, device=dev)
+        self.grad_flat = torch.zeros(off, dtype=torch.float32, device=dev)
+        with torch.no_grad():
+            for p, o in zip(self.params, self.offsets):
+                self.flat[o:o + p.numel()].copy_(p.detach().reshape(-1))
+                p.data = self.flat[o:o + p.numel()].view_as(p)
+        self.grad_views = [self.grad_flat[o:o + p.numel()].view_as(p) for p, o in zip(self.params, self.offsets)]
+        self.index: Dict[int, int] = {id(p): i for i, p in enumerate(self.params)}
+        self.sizes = [p.numel() for p in self.params]
+        self.on_ready = None      # callback(param_index) once the param's gradient is final (DP buckets)
+
+    def mark(self, *params: torch.nn.Parameter) -> None:
+        if self.on_ready is not None:
+            for p in params:
+                self.on_ready(self.index[id(p)])
+
+    def intact(self) -> bool:
+        """True if every p.data is still a view of the arena (a .to()/load may rebind it)."""
+        base = self.flat.data_ptr()
+        es = 4
+        return all(p.data.data_ptr() == base + o * es and p.dtype == torch.float32
+                   for p, o in zip(self.params, self.offsets))
+
+    def grad(self, p: torch.nn.Parameter) -> torch.Tensor:
+        return self.grad_views[self.index[id(p)]]
+
+    def begin_backward(self) -> bool:
+        """Returns `accumulate`: False when grads were cleared (p.grad None),
+        True when the step accumulates into existing grads (accumulation_steps > 1)."""
+        accumulate = all(p.grad is not None for p in self.params)
+        if accumulate:
+            # re-attach if a user replaced p.grad by a fresh tensor
+            for p, g in zip(self.params, self.grad_views):
+                if p.grad.data_ptr() != g.data_ptr():
+                    g.copy_(p.grad)
+        return accumulate
+
+    def end_backward(self) -> None:
+        for p, g in zip(self.params, self.grad_views):
+            if p.grad is None or p.grad.data_ptr() != g.data_ptr():
+                p.grad = g
+
+
+def pow2_shift(c8: int) -> int:
+    s = int(round(math.log2(c8)))
+    if (1 << s) != c8:
+        raise ValueError(f"channel count {c8 * 8} must be 8 x a power of two")
+    return s
+
+
+def round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m

@@ -1,0 +1,113 @@
+"""UNet3D on the MI355X engine — mirror of the reference's
+src/models/backbones/unet.py API (class names, constructor arguments,
+state-dict names, RNG init order), executed by the HIP engine.
+
+The nn.Modules here are parameter containers: creating them consumes the CPU
+RNG in exactly the reference's order (reference unet.py:26-27, 95, 148-163),
+so `torch.manual_seed(s); build_model(cfg)` yields bit-identical initial
+weights, and reference checkpoints load unchanged.  `UNet3D.forward` runs the
+whole network as one HIP program (engine/programs.py); the block modules'
+own forward is only the container interface.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, List, Tuple, Union
+
+import torch
+import torch.nn as nn
+
+from ...engine import run_engine
+
+SUPPORTED_NORM = ("instance",)
+
+
+class ConvBlock3D(nn.Module):
+    """(Conv3d 3^3 pad 1 -> InstanceNorm3d -> ReLU) x 2   (reference unet.py:12-60)."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel_size: int = 3, padding: int = 1,
+                 norm: str = "instance", activation: str = "relu"):
+        super().__init__()
+        if kernel_size != 3 or padding != 1:
+            raise NotImplementedError("engine ConvBlock3D: kernel_size=3, padding=1 only")
+        if norm not in SUPPORTED_NORM or activation != "relu":
+            raise NotImplementedError(f"engine ConvBlock3D: norm={norm!r}/activation={activation!r} not on the "
+                                      "HIP path (reference default instance/relu is)")
+        # construction order = RNG order: conv1, conv2, then the parameter-free norms
+        self.conv1 = nn.Conv3d(in_channels, out_channels, 3, padding=1)
+        self.conv2 = nn.Conv3d(out_channels, out_channels, 3, padding=1)
+        self.norm1 = nn.InstanceNorm3d(out_channels)
+        self.norm2 = nn.InstanceNorm3d(out_channels)
+        self.act = nn.ReLU(inplace=True)
+
+    def forward(self, x):  # pragma: no cover - container only
+        raise RuntimeError("ConvBlock3D is executed as part of the whole-network HIP program")
+
+
+class DownBlock3D(nn.Module):
+    """MaxPool3d(2) -> ConvBlock3D   (reference unet.py:63-79)."""
+
+    def __init__(self, in_channels: int, out_channels: int, norm: str = "instance"):
+        super().__init__()
+        self.pool = nn.MaxPool3d(2)
+        self.conv = ConvBlock3D(in_channels, out_channels, norm=norm)
+
+    def forward(self, x):  # pragma: no cover
+        raise RuntimeError("DownBlock3D is executed as part of the whole-network HIP program")
+
+
+class UpBlock3D(nn.Module):
+    """ConvTranspose3d(k2,s2) -> cat([up, skip]) -> ConvBlock3D   (reference unet.py:82-113)."""
+
+    def __init__(self, in_channels: int, out_channels: int, norm: str = "instance", mode: str = "transpose"):
+        super().__init__()
+        if mode != "transpose":
+            raise NotImplementedError("engine UpBlock3D: mode='transpose' only (reference default)")
+        self.up = nn.ConvTranspose3d(in_channels, in_channels // 2, kernel_size=2, stride=2)
+        self.conv = ConvBlock3D(in_channels, out_channels, norm=norm)
+
+    def forward(self, x, skip):  # pragma: no cover
+        raise RuntimeError("UpBlock3D is executed as part of the whole-network HIP program")
+
+
+class UNet3D(nn.Module):
+    """3D UNet: init block, len(features)-1 down blocks, as many up blocks, 1x1 head
+    (reference unet.py:116-205)."""
+
+    def __init__(self, in_channels: int = 1, out_channels: int = 8, features: List[int] = (32, 64, 128, 256, 512),
+                 norm: str = "instance", dropout: float = 0.0, **kwargs):
+        super().__init__()
+        features = list(features)
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.features = features
+        self.dropout_p = float(dropout)
+        self.init_conv = ConvBlock3D(in_channels, features[0], norm=norm)
+        self.encoders = nn.ModuleList(
+            [DownBlock3D(a, b, norm=norm) for a, b in zip(features[:-1], features[1:])])
+        self.decoders = nn.ModuleList(
+            [UpBlock3D(features[i], features[i - 1], norm=norm) for i in range(len(features) - 1, 0, -1)])
+        self.dropout = nn.Dropout3d(dropout) if dropout > 0 else nn.Identity()
+        self.out_conv = nn.Conv3d(features[0], out_channels, kernel_size=1)
+        self.engine_dtype = torch.float32
+
+    def forward(self, x: torch.Tensor, return_features: bool = False
+                ) -> Union[torch.Tensor, Tuple[torch.Tensor, List[torch.Tensor]]]:
+        logits = run_engine(self, "unet", x)
+        if return_features:
+            prog = self.__dict__["_engine"].program
+            feats = [prog.level_out(l).to_ncdhw() for l in range(len(self.features) - 1)]
+            return logits, feats
+        return logits
+
+    @property
+    def encoder_channels(self) -> List[int]:
+        return self.features
+
+
+def build_unet3d(config: Dict[str, Any]) -> UNet3D:
+    """reference unet.py:208-226."""
+    mc = config["model"]
+    bb = mc.get("backbone", {})
+    return UNet3D(in_channels=mc["in_channels"], out_channels=mc["out_channels"],
+                  features=bb.get("features", [32, 64, 128, 256, 512]), norm=bb.get("norm", "instance"),
+                  dropout=mc.get("head", {}).get("dropout", 0.0))

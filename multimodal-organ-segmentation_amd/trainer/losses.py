@@ -1,0 +1,137 @@
+"""Segmentation losses on the MI355X engine — mirror of the reference's
+src/trainer/losses.py (DiceLoss 12-80, TverskyLoss 128-185, DiceCELoss
+188-228, get_loss 231-267).
+
+Every loss runs as two HIP passes (mmseg_loss_fwd / mmseg_loss_bwd): one pass
+computes softmax over C, the one-hot per-(b,c) sums Σp, Σp·t, Σt and the CE
+sum with wavefront-shuffle reductions and a fixed-order finalize; the backward
+pass writes dlogits directly (no autograd graph of ~10 elementwise ops).
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, Optional
+
+import torch
+import torch.nn as nn
+
+from .._lib import lib, ptr, stream_handle
+
+TYPE_DICE, TYPE_TVERSKY = 0, 1
+
+
+class _SegLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, spec, class_w):
+        if logits.device.type != "cuda":
+            raise RuntimeError("HIP loss kernels need ROCm tensors; there is no CPU path")
+        logits = logits.float().contiguous()
+        if target.dtype not in (torch.int64, torch.uint8):
+            target = target.long()
+        target = target.contiguous()
+        N, C = logits.shape[:2]
+        V = logits.numel() // (N * C)
+        if target.numel() != N * V:
+            raise ValueError(f"target shape {tuple(target.shape)} does not match logits {tuple(logits.shape)}")
+        L = lib()
+        ws = torch.empty(L.mmseg_loss_ws_floats(N, C, V), dtype=torch.float32, device=logits.device)
+        loss = torch.empty((), dtype=torch.float32, device=logits.device)
+        cw = None if class_w is None else class_w.to(logits.device, torch.float32).contiguous()
+        args = (N, C, V, spec["type"], spec["dice_w"], spec["ce_w"], spec["smooth"], spec["alpha"], spec["beta"],
+                int(spec["include_bg"]), ptr(cw))
+        L.mmseg_loss_fwd(ptr(logits), ptr(target), target.element_size(), *args, ptr(loss), ptr(ws), stream_handle())
+        ctx.save_for_backward(logits, target, ws, cw if cw is not None else torch.empty(0))
+        ctx.args = args
+        ctx.has_cw = cw is not None
+        return loss
+
+    @staticmethod
+    def backward(ctx, gout):
+        logits, target, ws, cw = ctx.saved_tensors
+        N, C, V = ctx.args[:3]
+        dlogits = torch.empty_like(logits)
+        g = gout.float().contiguous()
+        lib().mmseg_loss_bwd(ptr(logits), ptr(target), target.element_size(), *ctx.args, ptr(g), 1.0, ptr(dlogits),
+                             ptr(ws), stream_handle())
+        return dlogits, None, None, None
+
+
+class _HipLoss(nn.Module):
+    def _spec(self) -> Dict[str, Any]:
+        raise NotImplementedError
+
+    def forward(self, pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+        if getattr(self, "reduction", "mean") != "mean":
+            raise NotImplementedError("HIP losses implement reduction='mean' (the reference's default)")
+        return _SegLoss.apply(pred, target, self._spec(), getattr(self, "class_weights", None))
+
+
+class DiceLoss(_HipLoss):
+    """softmax -> one-hot -> per-(b,c) (2I+s)/(U+s) -> 1 - dice -> mean (reference losses.py:12-80)."""
+
+    def __init__(self, smooth: float = 1.0, reduction: str = "mean", softmax: bool = True,
+                 include_background: bool = True):
+        super().__init__()
+        if not softmax:
+            raise NotImplementedError("HIP DiceLoss applies softmax (reference default)")
+        self.smooth, self.reduction, self.softmax, self.include_background = smooth, reduction, softmax, include_background
+
+    def _spec(self):
+        return dict(type=TYPE_DICE, dice_w=1.0, ce_w=0.0, smooth=self.smooth, alpha=0.0, beta=0.0,
+                    include_bg=self.include_background)
+
+
+class CrossEntropyLoss(_HipLoss):
+    """nn.CrossEntropyLoss(weight) with mean reduction over B*H*W*D (reference losses.py:214)."""
+
+    def __init__(self, weight: Optional[torch.Tensor] = None):
+        super().__init__()
+        self.class_weights = weight
+
+    def _spec(self):
+        return dict(type=TYPE_DICE, dice_w=0.0, ce_w=1.0, smooth=1.0, alpha=0.0, beta=0.0, include_bg=True)
+
+
+class TverskyLoss(_HipLoss):
+    """(tp+s)/(tp + a*fp + b*fn + s) per (b,c), 1 - T, mean (reference losses.py:128-185)."""
+
+    def __init__(self, alpha: float = 0.5, beta: float = 0.5, smooth: float = 1.0, reduction: str = "mean"):
+        super().__init__()
+        self.alpha, self.beta, self.smooth, self.reduction = alpha, beta, smooth, reduction
+
+    def _spec(self):
+        return dict(type=TYPE_TVERSKY, dice_w=1.0, ce_w=0.0, smooth=self.smooth, alpha=self.alpha, beta=self.beta,
+                    include_bg=True)
+
+
+class DiceCELoss(_HipLoss):
+    """dice_weight * DiceLoss + ce_weight * CrossEntropy, fused (reference losses.py:188-228)."""
+
+    def __init__(self, dice_weight: float = 0.5, ce_weight: float = 0.5, class_weights: Optional[torch.Tensor] = None,
+                 include_background: bool = True):
+        super().__init__()
+        self.dice_weight, self.ce_weight = dice_weight, ce_weight
+        self.class_weights = class_weights
+        self.include_background = include_background
+
+    def _spec(self):
+        return dict(type=TYPE_DICE, dice_w=self.dice_weight, ce_w=self.ce_weight, smooth=1.0, alpha=0.0, beta=0.0,
+                    include_bg=self.include_background)
+
+
+def get_loss(config: Dict[str, Any]) -> nn.Module:
+    """reference losses.py:231-267."""
+    lc = config["training"]["loss"]
+    name = lc["name"].lower()
+    cw = lc.get("class_weights")
+    cw = torch.tensor(cw, dtype=torch.float32) if cw is not None else None
+    if name == "dice":
+        return DiceLoss()
+    if name in ("ce", "cross_entropy"):
+        return CrossEntropyLoss(weight=cw)
+    if name == "dice_ce":
+        return DiceCELoss(dice_weight=lc.get("dice_weight", 0.5), ce_weight=lc.get("ce_weight", 0.5), class_weights=cw)
+    if name == "focal":
+        raise NotImplementedError("FocalLoss is not on the HIP path (no BASELINE config uses it; SURVEY §2.1)")
+    if name == "tversky":
+        return TverskyLoss(alpha=lc.get("tversky_alpha", 0.5), beta=lc.get("tversky_beta", 0.5))
+    return DiceCELoss()

@@ -1,0 +1,78 @@
+"""AdamW over the engine's flat parameter arena: one HIP kernel per step
+(mmseg_adamw) instead of torch's per-parameter loop.  Subclasses
+torch.optim.AdamW so param_groups / state_dict() / load_state_dict() keep the
+torch format the reference's checkpoints use (trainer.py:115-117,
+build.py:170-180): per-parameter state 'step', 'exp_avg', 'exp_avg_sq', where
+exp_avg / exp_avg_sq are views of two flat fp32 moment buffers."""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+
+from .._lib import lib, ptr, stream_handle
+
+
+def _arena_of(params: List[torch.Tensor]):
+    """(base tensor, numel) if the params are consecutive views of one fp32 buffer, else None."""
+    p0 = params[0]
+    if p0.device.type != "cuda" or any(p.dtype != torch.float32 for p in params):
+        return None
+    base = p0.data.data_ptr()
+    off = 0
+    for p in params:
+        if p.data.data_ptr() != base + off * 4 or not p.data.is_contiguous():
+            return None
+        off += p.numel()
+    return base, off
+
+
+class FlatAdamW(torch.optim.AdamW):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, **kw):
+        super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, foreach=False, **kw)
+        self._flat = {}
+
+    def _moments(self, gi: int, group, numel: int, device):
+        params = group["params"]
+        m, v = self._flat.get(gi, (None, None))
+        if m is None or m.numel() != numel or m.device != device:
+            m = torch.zeros(numel, dtype=torch.float32, device=device)
+            v = torch.zeros(numel, dtype=torch.float32, device=device)
+            self._flat[gi] = (m, v)
+        off = 0
+        for p in params:
+            st = self.state[p]
+            n = p.numel()
+            mv, vv = m[off:off + n].view_as(p), v[off:off + n].view_as(p)
+            if "exp_avg" in st and st["exp_avg"].data_ptr() != mv.data_ptr():
+                mv.copy_(st["exp_avg"])      # state loaded from a checkpoint: move into the arena
+                vv.copy_(st["exp_avg_sq"])
+            if "step" not in st:
+                st["step"] = torch.tensor(0.0)
+            st["exp_avg"], st["exp_avg_sq"] = mv, vv
+            off += n
+        return m, v
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        for gi, group in enumerate(self.param_groups):
+            params = [p for p in group["params"]]
+            if any(p.grad is None for p in params):
+                raise RuntimeError("FlatAdamW: every parameter needs a gradient (engine writes all of them)")
+            arena = _arena_of(params)
+            garena = _arena_of([p.grad for p in params])
+            if arena is None or garena is None:
+                raise RuntimeError("FlatAdamW needs the engine's flat parameter/gradient arena on a ROCm device "
+                                   "(run one forward/backward through the model first); there is no CPU path")
+            if group.get("amsgrad") or group.get("maximize"):
+                raise NotImplementedError("FlatAdamW: amsgrad / maximize are not on the HIP path")
+            base, n = arena
+            m, v = self._moments(gi, group, n, params[0].device)
+            step = int(self.state[params[0]]["step"].item()) + 1
+            for p in params:
+                self.state[p]["step"] = torch.tensor(float(step))
+            b1, b2 = group["betas"]
+            lib().mmseg_adamw(base, garena[0], ptr(m), ptr(v), n, float(group["lr"]), float(b1), float(b2),
+                              float(group["eps"]), float(group["weight_decay"]), step, stream_handle())
+        return loss

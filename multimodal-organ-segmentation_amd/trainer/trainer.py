@@ -1,0 +1,241 @@
+"""Trainer — mirror of the reference's src/trainer/trainer.py (Trainer 21-433)
+with the per-batch body factored into `train_step(batch, batch_idx)`
+(the reference inlines it at trainer.py:231-261).
+
+Same constructor, config keys, history / checkpoint format and epoch loop.
+MI355X-specific behaviour:
+  * mixed precision = the engine's bf16 activation storage with fp32
+    parameters / gradients / optimizer state, so no GradScaler is needed
+    (bf16 has fp32's exponent range); the reference's fp16 autocast +
+    GradScaler (trainer.py:237-248) therefore maps to a no-op scaler;
+  * AdamW runs as one HIP kernel over the flat parameter arena (FlatAdamW);
+  * data parallelism (one process per GPU, torchrun env) averages gradients
+    with bucketed RCCL all-reduces overlapped with the backward; only the
+    accumulation boundary micro-step communicates; rank 0 logs/checkpoints;
+  * validation accumulates Dice counts on the device (fused argmax + counts),
+    one host sync per validation pass instead of one per batch.
+"""
+from __future__ import annotations
+
+import os
+from pathlib import Path
+from typing import Any, Dict, Optional, Tuple, Union
+
+import torch
+import torch.nn as nn
+
+from ..distributed import ddp
+from ..models.build import load_checkpoint, save_checkpoint
+from .losses import get_loss
+from .metrics import DiceMetric, get_metrics
+from .optim import FlatAdamW
+
+try:
+    from tqdm import tqdm
+except ImportError:  # pragma: no cover
+    def tqdm(it, **kw):
+        return it
+
+
+class Trainer:
+    def __init__(self, config: Dict[str, Any], model: nn.Module, train_loader=None, val_loader=None,
+                 logger: Optional[Any] = None, resume_from: Optional[str] = None):
+        self.config = config
+        self.model = model
+        self.train_loader = train_loader
+        self.val_loader = val_loader
+        self.logger = logger
+        self.epochs = config["training"]["epochs"]
+        self.device = self._get_device()
+        self.model = self.model.to(self.device)
+        self.optimizer = self._setup_optimizer()
+        self.scheduler = self._setup_scheduler()
+        self.criterion = get_loss(config)
+        self.metrics = get_metrics(config)
+        self.use_amp = config["hardware"].get("mixed_precision", False)
+        self.scaler = None  # bf16 engine: no loss scaling needed (see module docstring)
+        self.accumulation_steps = config["training"].get("accumulation_steps", 1)
+        self.rank, self.world = ddp.rank(), ddp.world()
+        self.output_dir = Path(config["experiment"]["output_dir"]) / config["experiment"]["name"]
+        if self.rank == 0:
+            self.output_dir.mkdir(parents=True, exist_ok=True)
+        self.current_epoch = 0
+        self.best_metric = 0.0
+        self.history = {"train_loss": [], "val_loss": [], "val_dice": []}
+        self._buckets = None
+        if resume_from:
+            self._resume(resume_from)
+
+    # ------------------------------------------------------------- setup
+    def _get_device(self) -> torch.device:
+        dev = self.config["hardware"]["device"]
+        if dev == "cuda" and torch.cuda.is_available():
+            return torch.device("cuda", torch.cuda.current_device())
+        raise RuntimeError("the MI355X trainer needs hardware.device == 'cuda' on a ROCm GPU (no CPU path)")
+
+    def _setup_optimizer(self) -> torch.optim.Optimizer:
+        oc = self.config["training"]["optimizer"]
+        name = oc["name"].lower()
+        lr, wd = oc["lr"], oc.get("weight_decay", 0)
+        params = list(self.model.parameters())
+        if name == "adamw":
+            return FlatAdamW(params, lr=lr, weight_decay=wd, betas=tuple(oc.get("betas", [0.9, 0.999])))
+        if name == "adam":
+            return torch.optim.Adam(params, lr=lr, weight_decay=wd)
+        if name == "sgd":
+            return torch.optim.SGD(params, lr=lr, momentum=oc.get("momentum", 0.9), weight_decay=wd)
+        return FlatAdamW(params, lr=lr, weight_decay=wd)
+
+    def _setup_scheduler(self):
+        sc = self.config["training"].get("scheduler", {})
+        name = sc.get("name", "cosine").lower()
+        if name == "cosine":
+            warm = sc.get("warmup_epochs", 0)
+            return torch.optim.lr_scheduler.CosineAnnealingLR(self.optimizer, T_max=self.epochs - warm,
+                                                              eta_min=sc.get("min_lr", 1e-6))
+        if name == "step":
+            return torch.optim.lr_scheduler.StepLR(self.optimizer, step_size=sc.get("step_size", 30),
+                                                   gamma=sc.get("gamma", 0.1))
+        if name == "plateau":
+            return torch.optim.lr_scheduler.ReduceLROnPlateau(self.optimizer, mode="max",
+                                                              patience=sc.get("patience", 10),
+                                                              factor=sc.get("factor", 0.1))
+        return None
+
+    def _resume(self, path: str) -> None:
+        """reference trainer.py:150-164 (scheduler / history not restored, as in the reference)."""
+        ckpt = load_checkpoint(self.model, path)
+        if "optimizer_state_dict" in ckpt:
+            self.optimizer.load_state_dict(ckpt["optimizer_state_dict"])
+        if "epoch" in ckpt:
+            self.current_epoch = ckpt["epoch"]
+        if "best_metric" in ckpt:
+            self.best_metric = ckpt["best_metric"]
+        if self.logger:
+            self.logger.info(f"Resumed from epoch {self.current_epoch}")
+
+    # ----------------------------------------------------------- DP hooks
+    def _engine_flat(self):
+        bb = getattr(self.model, "backbone", self.model)
+        eng = bb.__dict__.get("_engine")
+        return eng.flat if eng is not None else None
+
+    def _arm_buckets(self, communicate: bool):
+        if self.world == 1:
+            return
+        flat = self._engine_flat()
+        if flat is None:
+            return
+        if self._buckets is None or self._buckets.grad is not flat.grad_flat:
+            mb = float(self.config.get("distributed", {}).get("bucket_mb", 32))
+            self._buckets = ddp.GradBuckets(flat.grad_flat, flat.offsets, flat.sizes, bucket_mb=mb)
+        flat.on_ready = self._buckets.param_ready if communicate else None
+
+    # ----------------------------------------------------------- training
+    def train_step(self, batch: Dict[str, torch.Tensor], batch_idx: int, sync: bool = True) -> Union[float, torch.Tensor]:
+        """One per-batch body of the reference's _train_epoch (trainer.py:231-261):
+        H2D, forward, loss / accumulation_steps, backward, optimizer step + zero_grad
+        every accumulation_steps batches.  Returns the un-scaled loss (python float,
+        or a device scalar with sync=False)."""
+        images = batch["image"].to(self.device, non_blocking=True)
+        labels = batch["label"].to(self.device, non_blocking=True)
+        boundary = (batch_idx + 1) % self.accumulation_steps == 0
+        outputs = self.model(images)
+        loss = self.criterion(outputs, labels) / self.accumulation_steps
+        self._arm_buckets(boundary)
+        loss.backward()
+        if boundary:
+            if self._buckets is not None and self.world > 1:
+                self._buckets.finish()
+            self.optimizer.step()
+            self.optimizer.zero_grad()
+        out = loss.detach() * self.accumulation_steps
+        return out.item() if sync else out
+
+    def _train_epoch(self) -> float:
+        self.model.train()
+        total = 0.0
+        n = len(self.train_loader)
+        self.optimizer.zero_grad()
+        it = tqdm(self.train_loader, desc=f"Epoch {self.current_epoch + 1}") if self.rank == 0 else self.train_loader
+        for batch_idx, batch in enumerate(it):
+            lv = self.train_step(batch, batch_idx)
+            total += lv
+            if self.rank == 0 and hasattr(it, "set_postfix"):
+                it.set_postfix({"loss": f"{lv:.4f}"})
+        return total / n
+
+    def _validate(self) -> Tuple[float, Dict[str, float]]:
+        self.model.eval()
+        dm = DiceMetric(num_classes=self.config["model"]["out_channels"])
+        total = torch.zeros((), dtype=torch.float64, device=self.device)
+        n = len(self.val_loader)
+        with torch.no_grad():
+            for batch in self.val_loader:
+                images = batch["image"].to(self.device, non_blocking=True)
+                labels = batch["label"].to(self.device, non_blocking=True)
+                outputs = self.model(images)
+                total += self.criterion(outputs, labels).double()
+                dm.update_from_logits(outputs, labels)
+        if self.world > 1:
+            packed = torch.cat([total.view(1).float(), dm.intersection, dm.union])
+            ddp.allreduce_sum_(packed)
+            C = dm.num_classes
+            total = packed[0].double()
+            dm.intersection, dm.union = packed[1:1 + C], packed[1 + C:]
+            n *= self.world
+        return (total / n).item(), dm.compute()
+
+    def evaluate(self) -> Dict[str, float]:
+        _, metrics = self._validate()
+        return metrics
+
+    def train(self) -> Dict[str, Any]:
+        es = self.config["training"].get("early_stopping", {})
+        patience = es.get("patience", 30)
+        no_improve = 0
+        for epoch in range(self.current_epoch, self.epochs):
+            self.current_epoch = epoch
+            train_loss = self._train_epoch()
+            self.history["train_loss"].append(train_loss)
+            val_loss, val_metrics = self._validate()
+            self.history["val_loss"].append(val_loss)
+            self.history["val_dice"].append(val_metrics.get("dice", 0))
+            if self.logger and self.rank == 0:
+                self.logger.info(f"Epoch [{epoch + 1}/{self.epochs}] Train Loss: {train_loss:.4f} "
+                                 f"Val Loss: {val_loss:.4f} Val Dice: {val_metrics.get('dice', 0):.4f}")
+            if self.scheduler is not None:
+                if isinstance(self.scheduler, torch.optim.lr_scheduler.ReduceLROnPlateau):
+                    self.scheduler.step(val_metrics.get("dice", 0))
+                else:
+                    self.scheduler.step()
+            self._save_checkpoints(val_metrics)
+            if val_metrics.get("dice", 0) > self.best_metric:
+                self.best_metric = val_metrics.get("dice", 0)
+                no_improve = 0
+            else:
+                no_improve += 1
+            if es.get("enabled", False) and no_improve >= patience:
+                if self.logger and self.rank == 0:
+                    self.logger.info(f"Early stopping at epoch {epoch + 1}")
+                break
+        return self.history
+
+    def predict(self, input_path, output_path) -> None:  # pragma: no cover - NIfTI I/O is out of scope
+        raise NotImplementedError("inference over NIfTI folders is outside the engine's scope (SURVEY §8f rank 2)")
+
+    def _save_checkpoints(self, metrics: Dict[str, float]) -> None:
+        """reference trainer.py:397-433 (rank 0 only)."""
+        if self.rank != 0:
+            return
+        cc = self.config["training"].get("checkpoint", {})
+        if cc.get("save_last", True):
+            save_checkpoint(self.model, self.optimizer, self.current_epoch, str(self.output_dir / "last.pth"),
+                            best_metric=self.best_metric, history=self.history)
+        if cc.get("save_best", True) and metrics.get("dice", 0) >= self.best_metric:
+            save_checkpoint(self.model, self.optimizer, self.current_epoch, str(self.output_dir / "best.pth"),
+                            best_metric=metrics.get("dice", 0), history=self.history)
+        every = cc.get("save_every", 0)
+        if every > 0 and (self.current_epoch + 1) % every == 0:
+            save_checkpoint(self.model, self.optimizer, self.current_epoch,
+                            str(self.output_dir / f"epoch_{self.current_epoch + 1}.pth"), best_metric=self.best_metric)

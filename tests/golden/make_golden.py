@@ -1,0 +1,239 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE
+(wittyseok/multimodal-organ-segmentation, mounted read-only at /root/reference)
+on the CPU of the build container.
+
+Run once, here (the reference never travels to the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+Only data is written (inputs + expected outputs as .npz); no reference source
+is copied.  The reference is imported in place; `nibabel` is absent in this
+image, so a two-class stub is put in sys.modules before `src.utils` is touched
+(only the trainer imports need it; no NIfTI I/O happens).
+"""
+from __future__ import annotations
+
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+import torch
+
+REF = os.environ.get("MMSEG_REFERENCE", "/root/reference")
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _import_reference():
+    sys.dont_write_bytecode = True
+    if "nibabel" not in sys.modules:
+        nib = types.ModuleType("nibabel")
+        nib.Nifti1Header = type("Nifti1Header", (), {})
+        nib.Nifti1Image = type("Nifti1Image", (), {})
+        sys.modules["nibabel"] = nib
+    sys.path.insert(0, REF)
+    import src.models.build as build  # noqa: E402
+    import src.trainer.losses as losses  # noqa: E402
+    import src.trainer.metrics as metrics  # noqa: E402
+    import src.trainer.trainer as trainer  # noqa: E402
+    import src.models.fusion.attention_fusion as attn  # noqa: E402
+    return build, losses, metrics, trainer, attn
+
+
+build, losses, metrics, trainer_mod, attn_mod = _import_reference()
+
+
+def base_config(model: str, modalities, out_channels: int, features, fusion="cross_attention",
+                loss="dice_ce", lr=1e-3):
+    return {
+        "experiment": {"name": "golden", "output_dir": tempfile.mkdtemp(prefix="mmseg_golden_"), "seed": 0},
+        "data": {"modalities": list(modalities)},
+        "model": {"name": model, "in_channels": len(modalities), "out_channels": out_channels,
+                  "backbone": {"features": list(features), "norm": "instance"},
+                  "fusion": {"type": fusion}, "head": {"dropout": 0.0}},
+        "training": {"epochs": 1, "batch_size": 2, "accumulation_steps": 1,
+                     "optimizer": {"name": "adamw", "lr": lr, "weight_decay": 1e-5, "betas": [0.9, 0.999]},
+                     "scheduler": {"name": "none"},
+                     "loss": {"name": loss, "dice_weight": 0.5, "ce_weight": 0.5, "class_weights": None}},
+        "hardware": {"device": "cpu", "mixed_precision": False},
+    }
+
+
+def param_summary(named):
+    names, sums, abss, samp = [], [], [], []
+    for k, v in named:
+        v = v.detach().double().flatten()
+        names.append(k)
+        sums.append(v.sum().item())
+        abss.append(v.abs().sum().item())
+        idx = torch.linspace(0, v.numel() - 1, 16).long()
+        samp.append(v[idx].numpy())
+    return np.array(names), np.array(sums), np.array(abss), np.stack(samp)
+
+
+def model_case(tag, cfg, S, B, seed=0, steps=3, full_logits=False):
+    """Forward + loss + grads at init, then a `steps`-batch reference Trainer epoch."""
+    torch.manual_seed(seed)
+    model = build.build_model(cfg)
+    M = len(cfg["data"]["modalities"])
+    C = cfg["model"]["out_channels"]
+    g = torch.Generator().manual_seed(seed + 1)
+    xs = torch.randn(steps + 1, B, M, S, S, S, generator=g)
+    ys = torch.randint(0, C, (steps + 1, B, S, S, S), generator=g)
+    init_names, init_sum, init_abs, init_samp = param_summary(model.backbone.named_parameters())
+
+    crit = losses.get_loss(cfg)
+    model.train()
+    out = model(xs[0])
+    loss = crit(out, ys[0])
+    loss.backward()
+    g_names, g_sum, g_abs, g_samp = param_summary((k, p.grad) for k, p in model.backbone.named_parameters())
+    gnorm = np.array([p.grad.double().norm().item() for _, p in model.backbone.named_parameters()])
+    model.zero_grad(set_to_none=True)
+
+    # reference Trainer: per-batch body of _train_epoch (trainer.py:231-261) over `steps` batches
+    tr = trainer_mod.Trainer(config=cfg, model=model)
+    recorded = []
+    orig = tr.criterion
+
+    def rec(o, t):
+        l = orig(o, t)
+        recorded.append(l.item())
+        return l
+
+    tr.criterion = rec
+    tr.train_loader = [{"image": xs[1 + i], "label": ys[1 + i]} for i in range(steps)]
+    tr._train_epoch()
+    with torch.no_grad():
+        model.eval()
+        out_after = model(xs[0])
+    # inputs are NOT stored: tests regenerate them from the same seeded CPU generator
+    # (torch.Generator().manual_seed(seed + 1); randn then randint, shapes as above)
+    flat = out.detach().reshape(-1)
+    sidx = torch.randperm(flat.numel(), generator=torch.Generator().manual_seed(99))[:4096]
+    extra = {"logits": out.detach().numpy()} if full_logits else {}
+    np.savez_compressed(
+        os.path.join(OUT, f"{tag}.npz"), S=np.int64(S), B=np.int64(B), steps=np.int64(steps),
+        logits_sum=np.float64(out.detach().double().sum()), logits_abs=np.float64(out.detach().double().abs().sum()),
+        sample_idx=sidx.numpy(), sample_logits=flat[sidx].numpy(), loss=np.float64(loss.item()), **extra,
+        init_names=init_names, init_sum=init_sum, init_abs=init_abs, init_samp=init_samp,
+        grad_sum=g_sum, grad_abs=g_abs, grad_samp=g_samp, grad_norm=gnorm,
+        traj_losses=np.array(recorded), after_sample=out_after.reshape(-1)[sidx].numpy(),
+        after_sum=np.float64(out_after.double().sum()),
+        features=np.array(cfg["model"]["backbone"]["features"]), seed=np.int64(seed),
+    )
+    print(tag, "loss", loss.item(), "traj", recorded)
+
+
+def loss_case():
+    g = torch.Generator().manual_seed(7)
+    out = {}
+    for C in (3, 6, 7):
+        logits = (torch.randn(2, C, 8, 9, 10, generator=g) * 3).requires_grad_(True)
+        labels = torch.randint(0, C, (2, 8, 9, 10), generator=g)
+        out[f"logits_C{C}"] = logits.detach().numpy()
+        out[f"labels_C{C}"] = labels.numpy()
+        cw = torch.rand(C, generator=g) + 0.5
+        out[f"cw_C{C}"] = cw.numpy()
+        mods = {
+            "dicece": losses.DiceCELoss(),
+            "dicece_w": losses.DiceCELoss(dice_weight=0.3, ce_weight=0.7, class_weights=cw),
+            "dice": losses.DiceLoss(),
+            "dice_nobg": losses.DiceLoss(include_background=False),
+            "ce": torch.nn.CrossEntropyLoss(),
+            "tversky": losses.TverskyLoss(),
+            "tversky_37": losses.TverskyLoss(alpha=0.3, beta=0.7),
+        }
+        for name, mod in mods.items():
+            if logits.grad is not None:
+                logits.grad = None
+            l = mod(logits, labels)
+            l.backward()
+            out[f"{name}_C{C}"] = np.float64(l.item())
+            out[f"{name}_C{C}_grad"] = logits.grad.numpy().copy()
+    np.savez_compressed(os.path.join(OUT, "losses.npz"), **out)
+    print("losses done")
+
+
+def metric_case():
+    rng = np.random.default_rng(11)
+    out = {}
+    for C in (3, 6):
+        dm = metrics.DiceMetric(num_classes=C)
+        preds, tgts = [], []
+        for _ in range(3):
+            p = rng.integers(0, C, size=(2, 12, 12, 12))
+            t = rng.integers(0, C, size=(2, 12, 12, 12))
+            if C == 6:
+                p[p == 5] = 4  # class 5 absent from predictions
+                t[t == 5] = 4  # ... and from targets: absent class -> dice 1.0
+            preds.append(p)
+            tgts.append(t)
+            dm.update(torch.from_numpy(p), torch.from_numpy(t))
+        res = dm.compute()
+        out[f"pred_C{C}"] = np.stack(preds)
+        out[f"tgt_C{C}"] = np.stack(tgts)
+        out[f"inter_C{C}"] = dm.intersection.numpy()
+        out[f"union_C{C}"] = dm.union.numpy()
+        out[f"dice_C{C}"] = np.float64(res["dice"])
+        out[f"dpc_C{C}"] = np.array(res["dice_per_class"])
+    np.savez_compressed(os.path.join(OUT, "dice_metric.npz"), **out)
+    print("metric done")
+
+
+def cross_attention_case():
+    torch.manual_seed(3)
+    mod = attn_mod.CrossAttentionFusion(32, num_heads=4)
+    g = torch.Generator().manual_seed(4)
+    q = torch.randn(2, 32, 6, 6, 6, generator=g).requires_grad_(True)
+    kv = torch.randn(2, 32, 6, 6, 6, generator=g).requires_grad_(True)
+    o = mod(q, kv)
+    w = torch.randn(o.shape, generator=g)
+    (o * w).sum().backward()
+    sd = {k: v.detach().numpy() for k, v in mod.state_dict().items()}
+    np.savez_compressed(os.path.join(OUT, "cross_attention.npz"), q=q.detach().numpy(), kv=kv.detach().numpy(),
+                        out=o.detach().numpy(), cot=w.numpy(), dq=q.grad.numpy(), dkv=kv.grad.numpy(),
+                        **{"p_" + k: v for k, v in sd.items()},
+                        **{"g_" + k: p.grad.numpy() for k, p in mod.named_parameters()})
+    print("cross attention done")
+
+
+def full_case(tag, cfg, S, B, seed):
+    """Full-size configs: forward summary only (logits stats + seeded voxel samples)."""
+    torch.manual_seed(seed)
+    model = build.build_model(cfg)
+    M = len(cfg["data"]["modalities"])
+    C = cfg["model"]["out_channels"]
+    rng = np.random.Generator(np.random.PCG64(seed + 100))
+    x = torch.from_numpy(rng.standard_normal((B, M, S, S, S), dtype=np.float32))
+    y = torch.from_numpy(rng.integers(0, C, size=(B, S, S, S)).astype(np.int64))
+    with torch.no_grad():
+        out = model(x)
+        loss = losses.get_loss(cfg)(out, y)
+    flat = out.reshape(B, C, -1)
+    idx = rng.integers(0, S ** 3, size=1024)
+    names, psum, pabs, _ = param_summary(model.backbone.named_parameters())
+    np.savez_compressed(os.path.join(OUT, f"{tag}.npz"), S=np.int64(S), B=np.int64(B), seed=np.int64(seed),
+                        logits_sum=np.float64(out.double().sum()), logits_abs=np.float64(out.double().abs().sum()),
+                        logits_absmax=np.float64(out.abs().max()), sample_idx=idx,
+                        sample_logits=flat[:, :, idx].numpy(), loss=np.float64(loss.item()),
+                        argmax_hist=np.bincount(out.argmax(1).flatten().numpy(), minlength=C),
+                        param_names=names, param_sum=psum, param_abs=pabs)
+    print(tag, "loss", loss.item())
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(8)
+    feats = [8, 16, 32, 64, 128]
+    model_case("unet_tiny", base_config("unet", ["CT", "PET"], 3, feats), S=32, B=2, full_logits=True)
+    for fz in ("cross_attention", "concat", "add", "attention"):
+        model_case(f"dual_tiny_{fz}", base_config("dual_encoder", ["CT", "PET"], 3, feats, fusion=fz), S=32, B=2)
+    model_case("dual_tiny_m3_tversky", base_config("dual_encoder", ["CT", "PET", "MRI"], 6, feats,
+                                                   fusion="cross_attention", loss="tversky"), S=32, B=2)
+    loss_case()
+    metric_case()
+    cross_attention_case()
+    full_case("full_unet_c2", base_config("unet", ["CT", "PET"], 6, [32, 64, 128, 256, 512]), S=96, B=2, seed=1234)
+    full_case("full_dual_c3", base_config("dual_encoder", ["CT", "PET"], 6, [32, 64, 128, 256, 512]),
+              S=96, B=2, seed=1234)

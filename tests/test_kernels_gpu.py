@@ -1,0 +1,295 @@
+"""Kernel-level parity: every HIP kernel family against a torch CPU fp64
+restatement of the same op (the floating-point oracle for a single kernel),
+on small odd shapes.  fp32 storage must agree to ~1e-5 normwise; bf16 storage
+is compared against the op evaluated on the same bf16-rounded inputs."""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+import mmseg_amd  # noqa: F401
+from mmseg_amd.engine.layers import Conv3, ConvT2, DySpec, Head, Point, Block
+from mmseg_amd.engine.runtime import Act, FlatParams, Runtime
+from mmseg_amd._lib import lib, ptr, stream_handle
+from tests.helpers import from_ndhwc, golden, rel, to_ndhwc
+
+pytestmark = pytest.mark.gpu
+DTYPES = [torch.float32, torch.bfloat16]
+TOL = {torch.float32: 2e-5, torch.bfloat16: 1.2e-2}
+GTOL = {torch.float32: 2e-5, torch.bfloat16: 2e-3}   # fp32-accumulated gradient outputs
+
+
+def _q(t, dtype):
+    """round through the storage dtype, return fp64 CPU"""
+    return t.detach().to(dtype).double().cpu()
+
+
+def _act(x, dtype):
+    N, C, D, H, W = x.shape
+    return Act(to_ndhwc(x, dtype), 0, C, C, N, D, H, W)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("cin,cout,shape", [
+    (8, 32, (2, 5, 6, 7)), (32, 32, (1, 8, 8, 8)), (64, 32, (2, 6, 6, 6)), (32, 64, (1, 6, 7, 5)),
+    (128, 64, (2, 4, 4, 4)), (256, 128, (1, 3, 2, 2)), (16, 8, (2, 4, 5, 6))])
+def test_conv3_fwd_dgrad_wgrad(dev, dtype, cin, cout, shape):
+    torch.manual_seed(cin + cout)
+    conv = nn.Conv3d(cin, cout, 3, padding=1).to(dev)
+    rt = Runtime(dev, dtype)
+    flat = FlatParams(list(conv.parameters()))
+    layer = Conv3(rt, conv, flat)
+    N, D, H, W = shape
+    x = torch.randn(N, cin, D, H, W, device=dev)
+    xa = _act(x, dtype)
+    ya = rt.act(N, D, H, W, cout)
+    layer.pack()
+    layer.fwd(xa, ya)
+    xd = _q(x, dtype).requires_grad_(True)
+    wd = _q(conv.weight, dtype).requires_grad_(True)
+    bd = conv.bias.detach().double().cpu().requires_grad_(True)
+    ref = F.conv3d(xd, wd, bd, padding=1)
+    out = from_ndhwc(ya.buf, N, cout, D, H, W)
+    assert rel(out, ref) < TOL[dtype]
+    dy = torch.randn(ref.shape, device=dev)
+    dya = _act(dy, dtype)
+    dxa = rt.act(N, D, H, W, cin)
+    layer.bwd(xa, dya, dxa, accumulate=False)
+    (ref * _q(dy, dtype)).sum().backward()
+    assert rel(from_ndhwc(dxa.buf, N, cin, D, H, W), xd.grad) < TOL[dtype]
+    assert rel(flat.grad(conv.weight), wd.grad) < GTOL[dtype]
+    assert rel(flat.grad(conv.bias), bd.grad) < GTOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_conv3_stem_padded_input(dev, dtype):
+    """first conv: 1-2 real input channels packed into an 8-channel NDHWC tile"""
+    torch.manual_seed(5)
+    conv = nn.Conv3d(2, 32, 3, padding=1).to(dev)
+    rt = Runtime(dev, dtype)
+    flat = FlatParams(list(conv.parameters()))
+    layer = Conv3(rt, conv, flat, cin_pad=8, need_dgrad=False)
+    N, D, H, W = 2, 6, 8, 4
+    x = torch.randn(N, 2, D, H, W, device=dev)
+    xa = rt.act(N, D, H, W, 8)
+    lib().mmseg_pack_input(ptr(x), 2, 0, 2, N, D * H * W, xa.ptr, rt.code, stream_handle())
+    ya = rt.act(N, D, H, W, 32)
+    layer.pack()
+    layer.fwd(xa, ya)
+    xd = _q(x, dtype)
+    wd = _q(conv.weight, dtype).requires_grad_(True)
+    bd = conv.bias.detach().double().cpu().requires_grad_(True)
+    ref = F.conv3d(xd, wd, bd, padding=1)
+    assert rel(from_ndhwc(ya.buf, N, 32, D, H, W), ref) < TOL[dtype]
+    dy = torch.randn(ref.shape, device=dev)
+    layer.bwd(xa, _act(dy, dtype), None, accumulate=False)
+    (ref * _q(dy, dtype)).sum().backward()
+    assert rel(flat.grad(conv.weight), wd.grad) < GTOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("cin,cout,shape", [(64, 32, (2, 3, 4, 5)), (128, 64, (1, 4, 4, 4)), (16, 8, (2, 2, 3, 2)),
+                                            (512, 256, (2, 3, 3, 3))])
+def test_convT_fwd_dgrad_wgrad(dev, dtype, cin, cout, shape):
+    torch.manual_seed(cin)
+    up = nn.ConvTranspose3d(cin, cout, 2, stride=2).to(dev)
+    rt = Runtime(dev, dtype)
+    flat = FlatParams(list(up.parameters()))
+    layer = ConvT2(rt, up, flat)
+    N, D, H, W = shape
+    x = torch.randn(N, cin, D, H, W, device=dev)
+    xa = _act(x, dtype)
+    # write into the first half of a 2*cout concat buffer, like the decoder does
+    cat = rt.act(N, 2 * D, 2 * H, 2 * W, 2 * cout)
+    layer.pack()
+    layer.fwd(xa, cat.slot(0, cout))
+    xd = _q(x, dtype).requires_grad_(True)
+    wd = _q(up.weight, dtype).requires_grad_(True)
+    bd = up.bias.detach().double().cpu().requires_grad_(True)
+    ref = F.conv_transpose3d(xd, wd, bd, stride=2)
+    out = from_ndhwc(cat.buf, N, cout, 2 * D, 2 * H, 2 * W, ld=2 * cout)
+    assert rel(out, ref) < TOL[dtype]
+    dy = torch.randn(ref.shape, device=dev)
+    dyc = Act(to_ndhwc(dy, dtype, ld=2 * cout), 0, cout, 2 * cout, N, 2 * D, 2 * H, 2 * W)
+    dxa = rt.act(N, D, H, W, cin)
+    layer.bwd(xa, dyc, dxa, accumulate=False)
+    (ref * _q(dy, dtype)).sum().backward()
+    assert rel(from_ndhwc(dxa.buf, N, cin, D, H, W), xd.grad) < TOL[dtype]
+    assert rel(flat.grad(up.weight), wd.grad) < GTOL[dtype]
+    assert rel(flat.grad(up.bias), bd.grad) < GTOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_point_conv(dev, dtype):
+    torch.manual_seed(3)
+    conv = nn.Conv3d(96, 32, 1).to(dev)
+    rt = Runtime(dev, dtype)
+    flat = FlatParams(list(conv.parameters()))
+    layer = Point(rt, conv, flat)
+    N, D, H, W = 2, 3, 4, 5
+    x = torch.randn(N, 96, D, H, W, device=dev)
+    xa = _act(x, dtype)
+    ya = rt.act(N, D, H, W, 32)
+    layer.pack()
+    layer.fwd(xa, ya)
+    xd = _q(x, dtype).requires_grad_(True)
+    wd = _q(conv.weight, dtype).requires_grad_(True)
+    bd = conv.bias.detach().double().cpu().requires_grad_(True)
+    ref = F.conv3d(xd, wd, bd)
+    assert rel(from_ndhwc(ya.buf, N, 32, D, H, W), ref) < TOL[dtype]
+    dy = torch.randn(ref.shape, device=dev)
+    dxa = rt.act(N, D, H, W, 96)
+    layer.bwd(xa, _act(dy, dtype), dxa, accumulate=False)
+    (ref * _q(dy, dtype)).sum().backward()
+    assert rel(from_ndhwc(dxa.buf, N, 96, D, H, W), xd.grad) < TOL[dtype]
+    assert rel(flat.grad(conv.weight), wd.grad) < GTOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("C,shape", [(32, (2, 6, 8, 4)), (8, (1, 4, 4, 4)), (256, (2, 2, 4, 2))])
+def test_instnorm_relu_maxpool(dev, dtype, C, shape):
+    """IN+ReLU fwd, MaxPool3d fwd (argmax), IN+ReLU bwd with dy = skip + maxpool_bwd."""
+    torch.manual_seed(C)
+    N, D, H, W = shape
+    x = (torch.randn(N, C, D, H, W, device=dev) * 2 + 0.7)
+    L, s, code = lib(), stream_handle(), (0 if dtype == torch.float32 else 1)
+    xa = _act(x, dtype)
+    ya = Act(torch.empty_like(xa.buf), 0, C, C, N, D, H, W)
+    stats = torch.empty(2, N * C, device=dev)
+    ws = torch.empty(L.mmseg_instnorm_ws_floats(N, D * H * W, C), device=dev)
+    L.mmseg_instnorm_stats(xa.ptr, C, N, D * H * W, C, 1e-5, ptr(stats[0]), C, ptr(stats[1]), ptr(ws), code, s)
+    L.mmseg_instnorm_relu_fwd(xa.ptr, C, ya.ptr, C, N, D * H * W, C, ptr(stats[0]), ptr(stats[1]), code, s)
+    xd = _q(x, dtype).requires_grad_(True)
+    yref = torch.relu(F.instance_norm(xd, eps=1e-5))
+    y = from_ndhwc(ya.buf, N, C, D, H, W)
+    assert rel(y, yref) < TOL[dtype]
+    # maxpool on the engine's own y (ties among ReLU zeros -> first index, like torch)
+    pa = Act(torch.empty(N * D * H * W * C // 8, dtype=dtype, device=dev), 0, C, C, N, D // 2, H // 2, W // 2)
+    idx = torch.empty(N * D * H * W * C // 8, dtype=torch.uint8, device=dev)
+    L.mmseg_maxpool2_fwd(ya.ptr, C, pa.ptr, C, ptr(idx), N, D, H, W, C, code, s)
+    yq = y.double().cpu().requires_grad_(True)
+    pref, iref = F.max_pool3d(yq, 2, return_indices=True)
+    assert rel(from_ndhwc(pa.buf, N, C, D // 2, H // 2, W // 2), pref) == 0.0
+    # backward: dy = dskip + maxpool_bwd(dp)
+    dskip = torch.randn(N, C, D, H, W, device=dev)
+    dp = torch.randn(N, C, D // 2, H // 2, W // 2, device=dev)
+    dpa = _act(dp, dtype)
+    dxa = Act(torch.empty_like(xa.buf), 0, C, C, N, D, H, W)
+    ws2 = torch.empty(L.mmseg_instnorm_ws_floats(N, D * H * W, C), device=dev)
+    dska = _act(dskip, dtype)
+    L.mmseg_instnorm_relu_bwd(xa.ptr, C, ptr(stats[0]), ptr(stats[1]), dska.ptr, C, 1.0, None, 0, None, 0,
+                              dpa.ptr, C, ptr(idx), dxa.ptr, C, N, D, H, W, C, ptr(ws2), code, s)
+    # reference: grads through relu(IN(x)), the pooled gradient routed by the engine's own argmax
+    Do, Ho, Wo = D // 2, H // 2, W // 2
+    it = idx.view(N, Do, Ho, Wo, C).permute(0, 4, 1, 2, 3).long().cpu()
+    dpq = _q(dp, dtype)
+    routed = torch.zeros(N, C, D, H, W, dtype=torch.float64)
+    for t in range(8):
+        a, b, c = t >> 2, (t >> 1) & 1, t & 1
+        routed[:, :, a::2, b::2, c::2] += (it == t).double() * dpq
+    yr = torch.relu(F.instance_norm(xd, eps=1e-5))
+    (yr * (_q(dskip, dtype) + routed)).sum().backward()
+    tol = 2e-4 if dtype == torch.float32 else 3e-2
+    assert rel(from_ndhwc(dxa.buf, N, C, D, H, W), xd.grad) < tol
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_head(dev, dtype):
+    torch.manual_seed(1)
+    conv = nn.Conv3d(32, 6, 1).to(dev)
+    rt = Runtime(dev, dtype)
+    flat = FlatParams(list(conv.parameters()))
+    head = Head(rt, conv, flat)
+    N, D, H, W = 2, 4, 6, 8
+    x = torch.randn(N, 32, D, H, W, device=dev)
+    xa = _act(x, dtype)
+    logits = torch.empty(N, 6, D, H, W, device=dev)
+    head.fwd(xa, logits, None)
+    xd = _q(x, dtype).requires_grad_(True)
+    w = conv.weight.detach().double().cpu().requires_grad_(True)
+    b = conv.bias.detach().double().cpu().requires_grad_(True)
+    ref = F.conv3d(xd, w, b)
+    assert rel(logits, ref) < 2e-6
+    dl = torch.randn_like(logits)
+    dxa = rt.act(N, D, H, W, 32)
+    head.bwd(xa, dl, dxa, accumulate=False)
+    (ref * dl.double().cpu()).sum().backward()
+    assert rel(from_ndhwc(dxa.buf, N, 32, D, H, W), xd.grad) < TOL[dtype]
+    assert rel(flat.grad(conv.weight), w.grad) < 2e-5
+    assert rel(flat.grad(conv.bias), b.grad) < 2e-5
+
+
+@pytest.mark.parametrize("C", [3, 6, 7])
+def test_losses_vs_reference_golden(dev, C):
+    from mmseg_amd.trainer.losses import CrossEntropyLoss, DiceCELoss, DiceLoss, TverskyLoss
+    g = golden("losses")
+    logits = torch.from_numpy(g[f"logits_C{C}"]).to(dev)
+    labels = torch.from_numpy(g[f"labels_C{C}"]).to(dev)
+    cw = torch.from_numpy(g[f"cw_C{C}"])
+    mods = {"dicece": DiceCELoss(), "dicece_w": DiceCELoss(0.3, 0.7, class_weights=cw), "dice": DiceLoss(),
+            "dice_nobg": DiceLoss(include_background=False), "ce": CrossEntropyLoss(),
+            "tversky": TverskyLoss(), "tversky_37": TverskyLoss(alpha=0.3, beta=0.7)}
+    for name, mod in mods.items():
+        lg = logits.clone().requires_grad_(True)
+        loss = mod(lg, labels)
+        loss.backward()
+        assert abs(loss.item() - float(g[f"{name}_C{C}"])) < 2e-6 * max(1.0, abs(float(g[f"{name}_C{C}"]))), name
+        assert rel(lg.grad, torch.from_numpy(g[f"{name}_C{C}_grad"])) < 1e-5, name
+
+
+def test_loss_uint8_labels_and_scaled_grad(dev):
+    from mmseg_amd.trainer.losses import DiceCELoss
+    g = golden("losses")
+    logits = torch.from_numpy(g["logits_C6"]).to(dev).requires_grad_(True)
+    labels = torch.from_numpy(g["labels_C6"]).to(dev)
+    (DiceCELoss()(logits, labels.to(torch.uint8)) / 4).backward()
+    assert rel(logits.grad * 4, torch.from_numpy(g["dicece_C6_grad"])) < 1e-5
+
+
+@pytest.mark.parametrize("C", [3, 6])
+def test_dice_metric_bit_identical(dev, C):
+    from mmseg_amd.trainer.metrics import DiceMetric
+    g = golden("dice_metric")
+    dm = DiceMetric(num_classes=C)
+    for p, t in zip(g[f"pred_C{C}"], g[f"tgt_C{C}"]):
+        dm.update(torch.from_numpy(p).to(dev), torch.from_numpy(t).to(dev))
+    res = dm.compute()
+    assert np.array_equal(dm.intersection.cpu().numpy(), g[f"inter_C{C}"])
+    assert np.array_equal(dm.union.cpu().numpy(), g[f"union_C{C}"])
+    assert res["dice"] == float(g[f"dice_C{C}"])
+    assert res["dice_per_class"] == list(g[f"dpc_C{C}"])
+
+
+def test_dice_counts_from_logits_matches_argmax(dev):
+    from mmseg_amd.trainer.metrics import DiceMetric
+    torch.manual_seed(0)
+    logits = torch.randn(2, 6, 7, 8, 9, device=dev)
+    logits[:, 2, 0, 0, :] = logits[:, 4, 0, 0, :]  # exact ties -> first index
+    labels = torch.randint(0, 6, (2, 7, 8, 9), device=dev)
+    a, b = DiceMetric(6), DiceMetric(6)
+    a.update_from_logits(logits, labels)
+    b.update(logits.argmax(1), labels)
+    assert torch.equal(a.intersection, b.intersection) and torch.equal(a.union, b.union)
+
+
+def test_adamw_matches_torch(dev):
+    from mmseg_amd.trainer.optim import FlatAdamW
+    torch.manual_seed(0)
+    flat = torch.randn(1000, device=dev)
+    params = [torch.nn.Parameter(flat[:600].view(20, 30)), torch.nn.Parameter(flat[600:].view(400))]
+    gflat = torch.randn(1000, device=dev)
+    params[0].grad, params[1].grad = gflat[:600].view(20, 30), gflat[600:]
+    ref = [torch.nn.Parameter(p.detach().cpu().clone()) for p in params]
+    for r, p in zip(ref, params):
+        r.grad = p.grad.detach().cpu().clone()
+    opt = FlatAdamW(params, lr=1e-3, weight_decay=1e-5)
+    ropt = torch.optim.AdamW(ref, lr=1e-3, weight_decay=1e-5)
+    for _ in range(3):
+        opt.step()
+        ropt.step()
+    for r, p in zip(ref, params):
+        assert rel(p, r) < 1e-6
+    sd = opt.state_dict()
+    assert set(sd["state"][0]) == {"step", "exp_avg", "exp_avg_sq"}
+    assert rel(sd["state"][0]["exp_avg"], ropt.state_dict()["state"][0]["exp_avg"]) < 1e-6

@@ -1,0 +1,185 @@
+"""Model-level parity of the HIP engine against the reference, through the
+drop-in API (build_model / get_loss / Trainer.train_step):
+
+  * tiny configs: init weights (RNG order), logits, loss, per-parameter grad
+    norms and a 3-step AdamW trajectory vs golden fixtures captured from the
+    reference (tests/golden/make_golden.py);
+  * full BASELINE sizes (UNet3D c2, DualEncoder c3 at 96^3, B=2): logits vs
+    the reference's seeded voxel samples, loss, argmax histogram;
+  * bf16 storage mode against the same goldens at a bf16 tolerance;
+  * bitwise determinism of two identical steps.
+
+Tolerances: fp32 logits 1e-3 normwise relative (north_star), measured ~1e-6.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+import mmseg_amd  # noqa: F401
+from mmseg_amd.models.build import build_model
+from mmseg_amd.trainer.losses import get_loss
+from mmseg_amd.trainer.trainer import Trainer
+from tests.helpers import golden, rel
+
+pytestmark = pytest.mark.gpu
+
+
+def make_config(model, modalities, out_channels, features, fusion="cross_attention", loss="dice_ce", lr=1e-3,
+                dtype="float32", tmp="/tmp/mmseg_test_out"):
+    return {
+        "experiment": {"name": "t", "output_dir": tmp, "seed": 0},
+        "data": {"modalities": list(modalities)},
+        "model": {"name": model, "in_channels": len(modalities), "out_channels": out_channels,
+                  "backbone": {"features": list(features), "norm": "instance"},
+                  "fusion": {"type": fusion}, "head": {"dropout": 0.0}},
+        "training": {"epochs": 1, "batch_size": 2, "accumulation_steps": 1,
+                     "optimizer": {"name": "adamw", "lr": lr, "weight_decay": 1e-5, "betas": [0.9, 0.999]},
+                     "scheduler": {"name": "none"},
+                     "loss": {"name": loss, "dice_weight": 0.5, "ce_weight": 0.5, "class_weights": None},
+                     "checkpoint": {"save_last": False, "save_best": False}},
+        "hardware": {"device": "cuda", "mixed_precision": False, "engine_dtype": dtype},
+    }
+
+
+TINY = {
+    "unet_tiny": ("unet", ["CT", "PET"], 3, "cross_attention", "dice_ce"),
+    "dual_tiny_cross_attention": ("dual_encoder", ["CT", "PET"], 3, "cross_attention", "dice_ce"),
+    "dual_tiny_concat": ("dual_encoder", ["CT", "PET"], 3, "concat", "dice_ce"),
+    "dual_tiny_add": ("dual_encoder", ["CT", "PET"], 3, "add", "dice_ce"),
+    "dual_tiny_attention": ("dual_encoder", ["CT", "PET"], 3, "attention", "dice_ce"),
+    "dual_tiny_m3_tversky": ("dual_encoder", ["CT", "PET", "MRI"], 6, "cross_attention", "tversky"),
+}
+
+
+def _inputs(g, M, C):
+    S, B, steps = int(g["S"]), int(g["B"]), int(g["steps"])
+    gen = torch.Generator().manual_seed(int(g["seed"]) + 1)
+    xs = torch.randn(steps + 1, B, M, S, S, S, generator=gen)
+    ys = torch.randint(0, C, (steps + 1, B, S, S, S), generator=gen)
+    return xs, ys
+
+
+def _build(tag, dtype="float32"):
+    model, mods, C, fusion, loss = TINY[tag]
+    g = golden(tag)
+    cfg = make_config(model, mods, C, list(g["features"]), fusion=fusion, loss=loss, dtype=dtype)
+    torch.manual_seed(int(g["seed"]))
+    m = build_model(cfg)
+    return cfg, m, g, len(mods), C
+
+
+@pytest.mark.parametrize("tag", list(TINY))
+def test_tiny_model_matches_reference(dev, tag):
+    cfg, m, g, M, C = _build(tag)
+    names = list(g["init_names"])
+    bb = dict(m.backbone.named_parameters())
+    assert list(bb) == names, "parameter registration order differs from the reference"
+    init_sum = np.array([bb[n].detach().double().sum().item() for n in names])
+    assert np.array_equal(init_sum, g["init_sum"]), "initial weights differ from the reference (RNG order)"
+    xs, ys = _inputs(g, M, C)
+    crit = get_loss(cfg)
+    m.train()
+    out = m(xs[0].to(dev))
+    loss = crit(out, ys[0].to(dev))
+    loss.backward()
+    flat = out.detach().reshape(-1).cpu()
+    sidx = torch.from_numpy(g["sample_idx"])
+    assert rel(flat[sidx], torch.from_numpy(g["sample_logits"])) < 1e-4
+    if "logits" in g:
+        assert rel(out, torch.from_numpy(g["logits"])) < 1e-4
+    assert abs(loss.item() - float(g["loss"])) < 1e-5
+    gn = np.array([bb[n].grad.double().norm().item() for n in names])
+    relg = np.abs(gn - g["grad_norm"]) / np.maximum(g["grad_norm"], 1e-12)
+    # conv biases before InstanceNorm have mathematically-zero gradients (fp noise)
+    dead = np.array([n.endswith(("conv1.bias", "conv2.bias")) for n in names])
+    assert relg[~dead].max() < 1e-3, [n for n, r, d in zip(names, relg, dead) if r >= 1e-3 and not d]
+    assert (gn[dead] < 1e-2 * max(gn[~dead].max(), 1e-12)).all()
+
+
+@pytest.mark.parametrize("tag", ["unet_tiny", "dual_tiny_cross_attention", "dual_tiny_attention",
+                                 "dual_tiny_m3_tversky"])
+def test_tiny_trajectory_matches_reference_trainer(dev, tag):
+    cfg, m, g, M, C = _build(tag)
+    xs, ys = _inputs(g, M, C)
+    tr = Trainer(cfg, m)
+    losses = [tr.train_step({"image": xs[1 + i], "label": ys[1 + i]}, i) for i in range(int(g["steps"]))]
+    assert np.allclose(losses, g["traj_losses"], rtol=0, atol=2e-5), (losses, g["traj_losses"])
+    m.eval()
+    with torch.no_grad():
+        after = m(xs[0].to(dev)).reshape(-1).cpu()
+    assert rel(after[torch.from_numpy(g["sample_idx"])], torch.from_numpy(g["after_sample"])) < 1e-3
+
+
+@pytest.mark.parametrize("tag", ["unet_tiny", "dual_tiny_cross_attention"])
+def test_tiny_bf16_close_to_reference(dev, tag):
+    cfg, m, g, M, C = _build(tag, dtype="bfloat16")
+    xs, ys = _inputs(g, M, C)
+    out = m(xs[0].to(dev))
+    flat = out.detach().reshape(-1).cpu()
+    assert rel(flat[torch.from_numpy(g["sample_idx"])], torch.from_numpy(g["sample_logits"])) < 5e-2
+    assert abs(get_loss(cfg)(out, ys[0].to(dev)).item() - float(g["loss"])) < 5e-3
+
+
+def test_step_bitwise_deterministic(dev):
+    cfg, m, g, M, C = _build("dual_tiny_attention")
+    xs, ys = _inputs(g, M, C)
+    crit = get_loss(cfg)
+    grads = []
+    for _ in range(2):
+        m.zero_grad(set_to_none=True)
+        crit(m(xs[0].to(dev)), ys[0].to(dev)).backward()
+        grads.append(torch.cat([p.grad.reshape(-1).clone() for p in m.parameters()]))
+    assert torch.equal(grads[0], grads[1])
+
+
+def test_accumulation_matches_two_batch_sum(dev):
+    """accumulation_steps=2 must equal the average of the two micro-batch gradients."""
+    cfg, m, g, M, C = _build("unet_tiny")
+    xs, ys = _inputs(g, M, C)
+    crit = get_loss(cfg)
+    m2 = copy.deepcopy(m)
+    m.zero_grad(set_to_none=True)
+    (crit(m(xs[0].to(dev)), ys[0].to(dev)) / 2).backward()
+    (crit(m(xs[1].to(dev)), ys[1].to(dev)) / 2).backward()
+    acc = torch.cat([p.grad.reshape(-1) for p in m.parameters()]).clone()
+    parts = []
+    for i in range(2):
+        m2.zero_grad(set_to_none=True)
+        crit(m2(xs[i].to(dev)), ys[i].to(dev)).backward()
+        parts.append(torch.cat([p.grad.reshape(-1) for p in m2.parameters()]).clone())
+    assert rel(acc, (parts[0] + parts[1]) / 2) < 1e-5
+
+
+def test_validate_dice(dev):
+    cfg, m, g, M, C = _build("unet_tiny")
+    xs, ys = _inputs(g, M, C)
+    tr = Trainer(cfg, m, val_loader=[{"image": xs[i], "label": ys[i]} for i in range(2)])
+    vloss, met = tr._validate()
+    assert 0.0 <= met["dice"] <= 1.0 and len(met["dice_per_class"]) == C and np.isfinite(vloss)
+
+
+@pytest.mark.parametrize("tag,model", [("full_unet_c2", "unet"), ("full_dual_c3", "dual_encoder")])
+def test_full_size_forward_matches_reference(dev, tag, model):
+    g = golden(tag)
+    S, B, seed = int(g["S"]), int(g["B"]), int(g["seed"])
+    cfg = make_config(model, ["CT", "PET"], 6, [32, 64, 128, 256, 512])
+    torch.manual_seed(seed)
+    m = build_model(cfg)
+    psum = np.array([p.detach().double().sum().item() for p in m.backbone.parameters()])
+    assert np.array_equal(psum, g["param_sum"])
+    rng = np.random.Generator(np.random.PCG64(seed + 100))
+    x = torch.from_numpy(rng.standard_normal((B, 2, S, S, S), dtype=np.float32))
+    y = torch.from_numpy(rng.integers(0, 6, size=(B, S, S, S)).astype(np.int64))
+    idx = torch.from_numpy(rng.integers(0, S ** 3, size=1024))
+    assert torch.equal(idx, torch.from_numpy(g["sample_idx"]))
+    m.eval()
+    with torch.no_grad():
+        out = m(x.to(dev))
+        loss = get_loss(cfg)(out, y.to(dev))
+    samp = out.reshape(B, 6, -1)[:, :, idx.to(dev)].cpu()
+    assert rel(samp, torch.from_numpy(g["sample_logits"])) < 1e-3
+    assert abs(loss.item() - float(g["loss"])) < 1e-4 * abs(float(g["loss"]))
+    hist = torch.bincount(out.argmax(1).reshape(-1), minlength=6).cpu().numpy()
+    assert np.abs(hist - g["argmax_hist"]).sum() <= 1e-4 * hist.sum()
