@@ -1,0 +1,197 @@
+"""Throughput benchmark: 96^3 CT+PET training patches/s/node for the
+DualEncoder + "cross_attention" (= mean fusion in the reference) training
+step on the HIP engine, 1..8 MI355X (BASELINE.json metric / configs[2]).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step = Trainer.train_step on one pre-staged synthetic phantom batch
+(forward, DiceCE, backward, RCCL gradient all-reduce for N>1, AdamW),
+accumulation_steps=1, dropout 0, bf16 activations / fp32 params+grads.
+Per-GPU batch is fixed (weak scaling); value = N*B*K / max-over-ranks time.
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_BF16_TFLOPS = 2500.0    # dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+def make_config(model, batch, dtype, out_channels=6, modalities=("CT", "PET")):
+    return {
+        "experiment": {"name": "bench", "output_dir": "/tmp/mmseg_bench", "seed": 42},
+        "data": {"modalities": list(modalities)},
+        "model": {"name": model, "in_channels": len(modalities), "out_channels": out_channels,
+                  "backbone": {"features": [32, 64, 128, 256, 512], "norm": "instance"},
+                  "fusion": {"type": "cross_attention"}, "head": {"dropout": 0.0}},
+        "training": {"epochs": 1, "batch_size": batch, "accumulation_steps": 1,
+                     "optimizer": {"name": "adamw", "lr": 1e-4, "weight_decay": 1e-5, "betas": [0.9, 0.999]},
+                     "scheduler": {"name": "none"},
+                     "loss": {"name": "dice_ce", "dice_weight": 0.5, "ce_weight": 0.5, "class_weights": None},
+                     "checkpoint": {"save_last": False, "save_best": False}},
+        "hardware": {"device": "cuda", "mixed_precision": dtype == "bf16",
+                     "engine_dtype": "bfloat16" if dtype == "bf16" else "float32"},
+        "distributed": {"bucket_mb": 32},
+    }
+
+
+def cpu_baseline(model_name, batch, size, out_channels, modalities, threads):
+    """The oracle (torch-CPU fp32 restatement of the reference step) on the host cores:
+    1 warm-up step on a 32^3 patch, then ONE timed full-size step (bounded sample)."""
+    from oracle import mmseg_oracle as O
+    torch.set_num_threads(threads)
+    M = len(modalities)
+    feats = [32, 64, 128, 256, 512]
+    torch.manual_seed(0)
+    if model_name == "dual_encoder":
+        p = O.init_dual_encoder(M, out_channels, feats, "cross_attention")
+        fwd = lambda pp, x: O.dual_encoder_forward(pp, x, "cross_attention")  # noqa: E731
+    else:
+        p = O.init_unet3d(M, out_channels, feats)
+        fwd = O.unet3d_forward
+    st = O.OracleStep(p, fwd, O.dice_ce_loss)
+    g = torch.Generator().manual_seed(5)
+    xw = torch.randn(1, M, 32, 32, 32, generator=g)
+    st.step(xw, torch.randint(0, out_channels, (1, 32, 32, 32), generator=g))
+    x = torch.randn(batch, M, size, size, size, generator=g)
+    y = torch.randint(0, out_channels, (batch, size, size, size), generator=g)
+    t0 = time.perf_counter()
+    st.step(x, y)
+    dt = time.perf_counter() - t0
+    return {"value": batch / dt, "unit": "patches/s", "cores": threads, "kind": "port",
+            "sample": f"1 oracle train step (fwd+DiceCE+bwd+AdamW), {model_name} B={batch} {size}^3 fp32, "
+                      f"{dt:.1f} s on {threads} threads ({platform.processor() or platform.machine()})"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="dual_encoder", choices=["dual_encoder", "unet"])
+    ap.add_argument("--batch", type=int, default=2, help="per-GPU batch")
+    ap.add_argument("--size", type=int, default=96)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--timer-steps", type=int, default=3, help="extra steps timed per kernel family (roofline)")
+    args = ap.parse_args()
+
+    import mmseg_amd  # noqa: F401
+    from mmseg_amd.data import device_batches
+    from mmseg_amd.distributed import ddp
+    from mmseg_amd.engine.profiler import TIMER
+    from mmseg_amd.models.build import build_model
+    from mmseg_amd.trainer.trainer import Trainer
+
+    local = ddp.init_from_env("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    rank, world = ddp.rank(), ddp.world()
+    n_gpus = world
+
+    cfg = make_config(args.model, args.batch, args.dtype)
+    torch.manual_seed(42)
+    model = build_model(cfg)
+    trainer = Trainer(cfg, model)
+    batches = device_batches(4, args.batch, args.size, 6, ["CT", "PET"], dev, seed=1234 + 1000 * rank)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    step = 0
+    for _ in range(args.warmup):
+        trainer.train_step(batches[step % len(batches)], step, sync=False)
+        step += 1
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    last = None
+    for _ in range(args.steps):
+        last = trainer.train_step(batches[step % len(batches)], step, sync=False)
+        step += 1
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    loss_val = float(last.item()) if last is not None else float("nan")
+
+    # per-kernel-family timing over a separate live window (HIP events on the launching stream)
+    TIMER.start()
+    for _ in range(args.timer_steps):
+        trainer.train_step(batches[step % len(batches)], step, sync=False)
+        step += 1
+    TIMER.stop()
+    fam = TIMER.summary()
+    dom = max(fam.items(), key=lambda kv: kv[1]["ms"]) if fam else None
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    value = n_gpus * args.batch * args.steps / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    roofline = None
+    if dom is not None:
+        name, a = dom
+        avg_ms = a["ms"] / a["launches"]
+        flops_per_launch = a["flops"] / a["launches"]
+        achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
+        peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
+        roofline = {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": peak,
+                    "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                    "avg_launch_ms": round(avg_ms, 4), "launches_per_step": a["launches"] // max(args.timer_steps, 1),
+                    "algorithmic_gflop_per_launch": round(flops_per_launch / 1e9, 3)}
+    families = {k: {"ms_per_step": round(v["ms"] / args.timer_steps, 3),
+                    "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1) if v["ms"] > 0 else None}
+                for k, v in sorted(fam.items(), key=lambda kv: -kv[1]["ms"])}
+    cpu = None
+    if n_gpus == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.model, args.batch, args.size, 6, ["CT", "PET"], args.cpu_threads)
+    workload = ("DualEncoder fusion=cross_attention (mean, dual_encoder.py:193-195) CT+PET"
+                if args.model == "dual_encoder" else "UNet3D early_fusion 2-ch")
+    out = {
+        "metric": "96^3 2-modality patches/sec/node (train step)",
+        "value": round(value, 3), "unit": "patches/s", "n_gpus": n_gpus, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (seeded CT/PET phantoms, pre-staged in HBM)",
+        "config": {"workload": f"{workload} {args.size}^3, 6 classes, DiceCE, AdamW, per-GPU batch {args.batch}",
+                   "model": args.model, "global_batch": args.batch * n_gpus, "patch": [args.size] * 3,
+                   "parallelism": f"dp{n_gpus}"},
+        "loss": round(loss_val, 5),
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "kernel_families": families,
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -49,6 +49,11 @@ int mmseg_abi_version(void);
 int mmseg_pack_weight(const float* w, void* dst, int mode, int Co, int Ci, int Cip, int KG, int KGp, int Cpad,
                       int dtype, void* stream);
 
+/* Batched form: one launch packs every layer of a model from a device table of
+ * descriptors {w, dst, mode, Co, Ci, Cip, KG, KGp, Cpad, pad, begin} (mmseg_pack_desc_bytes() each). */
+int mmseg_pack_desc_bytes(void);
+int mmseg_pack_weights_batched(const void* descs, int n, long long total, int dtype, void* stream);
+
 /* Implicit-GEMM forward / data-gradient convolution on MFMA.
  * Replaces aten::convolution (fwd) and convolution_backward (grad_input) of
  * Conv3d(k3,p1) unet.py:26-27, ConvTranspose3d(k2,s2) unet.py:95, and the
@@ -59,13 +64,14 @@ int mmseg_conv_gemm(const void* a, int lda, const void* wpacked, const float* bi
                     int ksplit, int dtype, void* stream);
 
 /* Weight-gradient partials part[ksplit][Ca][Ncols] (fp32), K = voxels.
- * Replaces convolution_backward (grad_weight) of the same layers. */
-int mmseg_wgrad(const void* a, int lda, const void* b, int ldb, float* part, int mode, int Ca, int Ncols,
-                int cpg_shift, long long V, int D, int H, int W, int ksplit, int dtype, void* stream);
+ * Replaces convolution_backward (grad_weight) of the same layers; with
+ * bias_part != NULL (a = dy) also the grad_bias partials bias_part[ksplit][Ca]. */
+int mmseg_wgrad(const void* a, int lda, const void* b, int ldb, float* part, float* bias_part, int mode, int Ca,
+                int Ncols, int cpg_shift, long long V, int D, int H, int W, int ksplit, int dtype, void* stream);
 int mmseg_wgrad_splits(long long V, int ksplit);
 /* Fixed-order sum of the partials into the torch-layout fp32 gradient. */
-int mmseg_wgrad_reduce(const float* part, float* grad, int Ca, int Ncols, int ksplit, int cpad, int creal, int ntap,
-                       int accumulate, void* stream);
+int mmseg_wgrad_reduce(const float* part, float* grad, const float* bias_part, float* bias_grad, int Ca, int Ncols,
+                       int ksplit, int cpad, int creal, int ntap, int accumulate, void* stream);
 /* Bias gradient out[c] (+)= sum_v dy[v][c] (convolution_backward grad_bias). */
 int mmseg_colsum(const void* dy, int ld, int C, long long V, float* part, int nblk, float* out, int accumulate,
                  int dtype, void* stream);

@@ -55,6 +55,10 @@ class MmsegError(RuntimeError):
     pass
 
 
+# int-returning entry points that return a value, not a status
+_VALUE_FUNCS = ("mmseg_abi_version", "mmseg_wgrad_splits", "mmseg_pack_desc_bytes")
+
+
 class _Lib:
     def __init__(self, path: str = LIB_PATH):
         if not os.path.exists(path):
@@ -76,8 +80,11 @@ class _Lib:
         fn = getattr(self.dll, name)
 
         def call(*args):
+            # numpy scalars (e.g. channel counts read from configs / fixtures) are not ctypes-convertible
+            args = tuple(a.item() if hasattr(a, "item") and not hasattr(a, "data_ptr") and not isinstance(a, (int, float))
+                         else a for a in args)
             rc = fn(*args)
-            if self.protos[name][0] is ctypes.c_int and name not in ("mmseg_abi_version", "mmseg_wgrad_splits") and rc != 0:
+            if self.protos[name][0] is ctypes.c_int and name not in _VALUE_FUNCS and rc != 0:
                 raise MmsegError(f"{name} failed: {self.dll.mmseg_last_error().decode(errors='replace')}")
             return rc
 

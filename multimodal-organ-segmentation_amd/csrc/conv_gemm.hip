@@ -23,7 +23,15 @@
 // fixed-order split-K pass, so weight gradients are bitwise deterministic.
 #include "mmseg_common.h"
 
+#include <stdlib.h>
+
 namespace {
+
+// Tuning knobs for in-process A/B runs (tools/kbench.py); defaults are the shipped choice.
+int knob(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
 
 enum GatherMode { MODE_CONV3 = 0, MODE_POINT = 1, MODE_CONVT_FWD = 2, MODE_CONVT_DGRAD = 3 };
 
@@ -36,6 +44,7 @@ struct GemmArgs {
   int M, Ncols, Cpad, KG, cpg_shift;
   int D, H, W;               // row grid
   int ksplit, kg_per_split;  // k-groups per split (multiple of 4)
+  int swz;                   // XCD-aware block remap
 };
 
 template <typename T>
@@ -134,9 +143,11 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs g) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const long long m0 = (long long)blockIdx.x * BM + wm * RM * 16;
-  const int n0 = blockIdx.y * BN + wn * RN * 16;
-  const int ks = blockIdx.z;
+  const int mt_n = (g.M + BM - 1) / BM, nt_n = (g.Ncols + BN - 1) / BN;
+  const int tile = g.swz ? xcd_swizzle(blockIdx.x, mt_n * nt_n * g.ksplit) : (int)blockIdx.x;
+  const int mt = tile % mt_n, nt = (tile / mt_n) % nt_n, ks = tile / (mt_n * nt_n);
+  const long long m0 = (long long)mt * BM + wm * RM * 16;
+  const int n0 = nt * BN + wn * RN * 16;
   const int kg_begin = ks * g.kg_per_split;
   int kg_end = kg_begin + g.kg_per_split;
   const int KGp = (g.KG + 3) & ~3;
@@ -222,6 +233,169 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs g) {
   }
 }
 
+// ------------------------------------------------------ brick conv (3^3)
+// LDS-staged halo tiles for the 3x3x3 convolution (fwd, and dgrad with the
+// flipped / transposed weights): a block owns a 4x4x8 output brick (128
+// voxels, one sample) x BN output channels.  Per 32-channel input chunk the
+// 6x6x10 input halo is staged ONCE into LDS and reused by all 27 taps (the
+// per-lane gather kernel above re-reads it 27x through L1/L2), and the chunk's
+// weights are staged one kz-plane (9 taps) at a time.  Register prefetch of
+// the next stage overlaps its global loads with the current MFMAs.
+// Wave w computes brick z-slice w (32 voxels = 2 row tiles) x BN columns.
+constexpr int BRK_Z = 4, BRK_Y = 4, BRK_X = 8;
+constexpr int HLO_Z = BRK_Z + 2, HLO_Y = BRK_Y + 2, HLO_X = BRK_X + 2;
+constexpr int HLO_V = HLO_Z * HLO_Y * HLO_X;   // 360 halo voxels
+constexpr int CK = 32;                          // input channels per chunk
+
+template <typename T, int BN>
+__global__ __launch_bounds__(256) void conv3_brick_kernel(GemmArgs g) {
+  constexpr int EP = 16 / sizeof(T);
+  constexpr int XP = CK + EP;                   // halo row pitch (elements)
+  constexpr int WP = CK;                        // weight row pitch (elements)
+  constexpr int RN = BN / 16;
+  constexpr int XS = HLO_V * XP, WS = 9 * BN * WP;
+  __shared__ __attribute__((aligned(16))) T lds[XS + WS];
+  T* Xl = lds;
+  T* Wl = lds + XS;
+  constexpr int X_ITEMS = HLO_V * (CK / 8);     // V8 loads per halo stage
+  constexpr int X_PER = (X_ITEMS + 255) / 256;
+  constexpr int W_ITEMS = 9 * BN * (CK / 8);
+  constexpr int W_PER = (W_ITEMS + 255) / 256;
+
+  const T* A = reinterpret_cast<const T*>(g.a);
+  const T* Bw = reinterpret_cast<const T*>(g.b);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int bz_n = g.D / BRK_Z, by_n = g.H / BRK_Y, bx_n = g.W / BRK_X;
+  const int nbrick = (g.M / (g.D * g.H * g.W)) * bz_n * by_n * bx_n;
+  const int nt_n = (g.Ncols + BN - 1) / BN;
+  const int tile = g.swz ? xcd_swizzle(blockIdx.x, nbrick * nt_n) : (int)blockIdx.x;
+  int bidx = tile % nbrick;
+  const int nt = tile / nbrick;
+  const int bx = bidx % bx_n; bidx /= bx_n;
+  const int by = bidx % by_n; bidx /= by_n;
+  const int bz = bidx % bz_n;
+  const int n = bidx / bz_n;
+  const int z0 = bz * BRK_Z, y0 = by * BRK_Y, x0 = bx * BRK_X;
+  const long long HW = (long long)g.H * g.W;
+  const long long nbase = (long long)n * g.D * HW;
+  const int n0 = nt * BN;
+  const int cin = 8 << g.cpg_shift;             // channels of the A source
+  const int nchunk = cin / CK;
+  const int nstage = nchunk * 3;
+
+  V8<T> xr[X_PER], wr[W_PER];
+  auto load_x = [&](int c) {
+#pragma unroll
+    for (int k = 0; k < X_PER; ++k) {
+      const int e = tid + k * 256;
+      if (e < X_ITEMS) {
+        const int h = e >> 2, cg = e & 3;
+        const int hx = h % HLO_X, hy = (h / HLO_X) % HLO_Y, hz = h / (HLO_X * HLO_Y);
+        const int z = z0 - 1 + hz, y = y0 - 1 + hy, x = x0 - 1 + hx;
+        if ((unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W)
+          xr[k].load(A + (nbase + z * HW + (long long)y * g.W + x) * g.lda + c * CK + cg * 8);
+        else
+          xr[k].zero();
+      }
+    }
+  };
+  auto load_w = [&](int c, int kz) {
+#pragma unroll
+    for (int k = 0; k < W_PER; ++k) {
+      const int e = tid + k * 256;
+      if (e < W_ITEMS) {
+        const int cg = e & 3, q = e >> 2;
+        const int col = q % BN, t9 = q / BN;
+        const int tap = kz * 9 + t9;
+        const int kgi = tap * (cin / 8) + c * 4 + cg;
+        wr[k].load(Bw + ((long long)kgi * g.Cpad + n0 + col) * 8);
+      }
+    }
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int k = 0; k < X_PER; ++k) {
+      const int e = tid + k * 256;
+      if (e < X_ITEMS) xr[k].store(Xl + (e >> 2) * XP + (e & 3) * 8);
+    }
+  };
+  auto store_w = [&]() {
+#pragma unroll
+    for (int k = 0; k < W_PER; ++k) {
+      const int e = tid + k * 256;
+      if (e < W_ITEMS) {
+        const int cg = e & 3, q = e >> 2;   // q = t9*BN + col
+        wr[k].store(Wl + q * WP + cg * 8);
+      }
+    }
+  };
+
+  f32x4 acc[2][RN];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // lane's rows: row r = lane&15 of tile i -> brick voxel (wave, 2i + (r>>3), r&7)
+  const int r16 = lane & 15, kg = lane >> 4;
+  int hrow[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) hrow[i] = (wave * HLO_Y + (2 * i + (r16 >> 3))) * HLO_X + (r16 & 7);
+
+  load_x(0);
+  load_w(0, 0);
+  store_x();
+  store_w();
+  __syncthreads();
+  for (int st = 0; st < nstage; ++st) {
+    const int c = st / 3, kz = st - c * 3;
+    const int sn = st + 1;
+    const bool more = sn < nstage;
+    const int cn = sn / 3, kzn = sn - cn * 3;
+    if (more) {
+      load_w(cn, kzn);
+      if (kzn == 0) load_x(cn);
+    }
+#pragma unroll
+    for (int t9 = 0; t9 < 9; ++t9) {
+      const int ky = t9 / 3, kx = t9 - ky * 3;
+      const int hoff = (kz * HLO_Y + ky) * HLO_X + kx;
+      V8<T> af[2], bf[RN];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i].load(Xl + (hrow[i] + hoff) * XP + kg * 8);
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bf[j].load(Wl + (t9 * BN + j * 16 + r16) * WP + kg * 8);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) mfma_step<T>(acc[i][j], af[i], bf[j]);
+    }
+    __syncthreads();
+    if (more) {
+      store_w();
+      if (kzn == 0) store_x();
+      __syncthreads();
+    }
+  }
+
+  T* O = reinterpret_cast<T*>(g.out);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int col = n0 + j * 16 + r16;
+      if (col >= g.Ncols) continue;
+      const float bv = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = kg * 4 + r;            // 0..15 within the tile
+        const int y = y0 + 2 * i + (row >> 3), x = x0 + (row & 7), z = z0 + wave;
+        const long long vox = nbase + z * HW + (long long)y * g.W + x;
+        O[vox * g.ldo + col] = from_f<T>(acc[i][j][r] + bv);
+      }
+    }
+}
+
 // Fixed-order split-K reduction for the forward GEMM: out = sum_k part[k] (+bias).
 template <typename T, int MODE>
 __global__ void gemm_splitk_reduce(GemmArgs g) {
@@ -257,116 +431,198 @@ __global__ void gemm_splitk_reduce(GemmArgs g) {
 //   CONV3 : A = dy (rows = Cout), B = x at v + off(tap), col = tap*Cin + ci
 //   POINT : A = dy, B = x at v
 //   CONVT : A = x (rows = Cin), B = dy at child(v, tap), col = tap*Cout + co
+// Both operands are staged into LDS in their natural [voxel][channel] layout
+// with 16-byte vector writes (double-buffered, one barrier per stage); the
+// MFMA fragments (K = voxels) are read with the gfx950 transposed LDS read
+// ds_read_b64_tr_b16 (bf16) or as single f32 elements (f32 path).
+// bias_part (optional, A = dy): blocks of column tile 0 also emit per-row
+// sums of A, i.e. the bias gradient partials.
 struct WgradArgs {
   const void* a;  int lda;
   const void* b;  int ldb;
   float* part;
+  float* bias_part;
   int Ca, Ncols, cpg_shift;
   long long V;               // voxels in the a-grid
   int D, H, W;
   int ksplit;
   long long vox_per_split;   // multiple of KV
+  int swz;
 };
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef short v8i16 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+__device__ __forceinline__ bf16x8 tr_frag(const bf16_t* p_lo, const bf16_t* p_hi) {
+  v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(p_lo));
+  v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(p_hi));
+  v8i16 c = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, c);
+}
+
+template <int MODE>
+__device__ __forceinline__ bool gather_src(long long vox, int kgi, int cpg_shift, const WgradArgs& g, long long& src,
+                                           int& c8) {
+  if (MODE == MODE_CONV3) {
+    const int t = kgi >> cpg_shift;
+    c8 = kgi & ((1 << cpg_shift) - 1);
+    const int x = (int)(vox % g.W);
+    long long q = vox / g.W;
+    const int y = (int)(q % g.H);
+    q /= g.H;
+    const int z = (int)(q % g.D);
+    int dz, dy, dx;
+    tap_delta(t, dz, dy, dx);
+    src = vox + ((long long)dz * g.H + dy) * g.W + dx;
+    return (unsigned)(z + dz) < (unsigned)g.D && (unsigned)(y + dy) < (unsigned)g.H &&
+           (unsigned)(x + dx) < (unsigned)g.W;
+  } else if (MODE == MODE_CONVT_DGRAD) {
+    const int t = kgi >> cpg_shift;
+    c8 = kgi & ((1 << cpg_shift) - 1);
+    const int x = (int)(vox % g.W);
+    long long q = vox / g.W;
+    const int y = (int)(q % g.H);
+    q /= g.H;
+    const int z = (int)(q % g.D);
+    const long long n = q / g.D;
+    src = ((n * 2LL * g.D + 2 * z + (t >> 2)) * 2LL * g.H + 2 * y + ((t >> 1) & 1)) * 2LL * g.W + 2 * x + (t & 1);
+    return true;
+  }
+  c8 = kgi;
+  src = vox;
+  return true;
+}
 
 template <typename T, int MODE, int WM, int WN, int RM, int RN, int KV>
 __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs g) {
   constexpr int BM = WM * RM * 16;
   constexpr int BN = WN * RN * 16;
-  constexpr int PAD = 16 / sizeof(T);
-  constexpr int LDS_ROW = KV + PAD;   // elements
-  __shared__ __attribute__((aligned(16))) T As[BM * LDS_ROW];
-  __shared__ __attribute__((aligned(16))) T Bs[BN * LDS_ROW];
+  constexpr int EP = 16 / sizeof(T);
+  constexpr int PA = BM + EP, PB = BN + EP;      // LDS row pitch (elements), 16-B aligned rows
+  constexpr int AG = BM / 8, BG = BN / 8;
+  constexpr int A_PER = KV * AG / 256, B_PER = KV * BG / 256;
+  static_assert(A_PER >= 1 && B_PER >= 1 && (256 % AG) == 0 && (256 % BG) == 0, "tile/thread mismatch");
+  constexpr int SA = KV * PA, SB = KV * PB;
+  __shared__ __attribute__((aligned(16))) T lds[2 * (SA + SB)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int row0 = blockIdx.y * BM;
-  const int col0 = blockIdx.x * BN;
-  const int ks = blockIdx.z;
+  const int ct_n = (g.Ncols + BN - 1) / BN, rt_n = (g.Ca + BM - 1) / BM;
+  const int tile = g.swz ? xcd_swizzle(blockIdx.x, ct_n * rt_n * g.ksplit) : (int)blockIdx.x;
+  const int ctile = tile % ct_n, rtile = (tile / ct_n) % rt_n, ks = tile / (ct_n * rt_n);
+  const int row0 = rtile * BM;
+  const int col0 = ctile * BN;
   const long long v_begin = ks * g.vox_per_split;
   long long v_end = v_begin + g.vox_per_split;
   if (v_end > g.V) v_end = g.V;
-
   const T* A = reinterpret_cast<const T*>(g.a);
   const T* B = reinterpret_cast<const T*>(g.b);
+  const bool do_bias = g.bias_part != nullptr && ctile == 0;
+
+  // fixed per-thread column group (256 % BG == 0) -> fixed tap / channel group
+  const int cga = tid % AG, cgb = tid % BG;
+  const int kgi_b = (col0 >> 3) + cgb;
+  const bool col_ok = kgi_b * 8 < g.Ncols;
+  const bool row_ok = row0 + cga * 8 < g.Ca;
 
   f32x4 acc[RM][RN];
 #pragma unroll
   for (int i = 0; i < RM; ++i)
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float bsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
-  constexpr int AG = BM / 8;  // 8-channel groups per voxel (A tile)
-  constexpr int BG = BN / 8;
-  const int cpg_mask = (1 << g.cpg_shift) - 1;
-
-  for (long long vb = v_begin; vb < v_end; vb += KV) {
-    // ---- stage A: KV voxels x BM channels, stored As[ch][v]
-    for (int e = tid; e < KV * AG; e += 256) {
-      const int v = e / AG, cg = e - v * AG;
-      const long long vox = vb + v;
-      V8<T> val;
-      if (vox < v_end && row0 + cg * 8 < g.Ca) val.load(A + vox * g.lda + row0 + cg * 8);
-      else val.zero();
+  V8<T> ra[A_PER], rb[B_PER];
+  auto load_stage = [&](long long vb) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) As[(cg * 8 + j) * LDS_ROW + v] = from_f<T>(val.get(j));
-    }
-    // ---- stage B: KV voxels x BN gathered columns, stored Bs[col][v]
-    for (int e = tid; e < KV * BG; e += 256) {
-      const int v = e / BG, cg = e - v * BG;
+    for (int k = 0; k < A_PER; ++k) {
+      const int v = (tid + k * 256) / AG;
       const long long vox = vb + v;
-      const int kgi = (col0 >> 3) + cg;
-      V8<T> val;
-      bool ok = vox < v_end && kgi * 8 < g.Ncols;
-      long long src = vox;
-      int c8 = kgi;
-      if (ok && MODE == MODE_CONV3) {
-        const int t = kgi >> g.cpg_shift;
-        c8 = kgi & cpg_mask;
-        const int x = (int)(vox % g.W);
-        long long q = vox / g.W;
-        const int y = (int)(q % g.H);
-        q /= g.H;
-        const int z = (int)(q % g.D);
-        int dz, dy, dx;
-        tap_delta(t, dz, dy, dx);
-        ok = (unsigned)(z + dz) < (unsigned)g.D && (unsigned)(y + dy) < (unsigned)g.H &&
-             (unsigned)(x + dx) < (unsigned)g.W;
-        src = vox + ((long long)dz * g.H + dy) * g.W + dx;
-      } else if (ok && MODE == MODE_CONVT_DGRAD) {
-        const int t = kgi >> g.cpg_shift;
-        c8 = kgi & cpg_mask;
-        const int x = (int)(vox % g.W);
-        long long q = vox / g.W;
-        const int y = (int)(q % g.H);
-        q /= g.H;
-        const int z = (int)(q % g.D);
-        const long long n = q / g.D;
-        src = ((n * 2LL * g.D + 2 * z + (t >> 2)) * 2LL * g.H + 2 * y + ((t >> 1) & 1)) * 2LL * g.W + 2 * x + (t & 1);
+      if (vox < v_end && row_ok) ra[k].load(A + vox * g.lda + row0 + cga * 8);
+      else ra[k].zero();
+    }
+#pragma unroll
+    for (int k = 0; k < B_PER; ++k) {
+      const int v = (tid + k * 256) / BG;
+      const long long vox = vb + v;
+      long long src;
+      int c8;
+      const bool ok = vox < v_end && col_ok && gather_src<MODE>(vox, kgi_b, g.cpg_shift, g, src, c8);
+      if (ok) rb[k].load(B + src * g.ldb + c8 * 8);
+      else rb[k].zero();
+    }
+  };
+  auto write_stage = [&](int buf) {
+    T* As = lds + buf * (SA + SB);
+    T* Bs = As + SA;
+#pragma unroll
+    for (int k = 0; k < A_PER; ++k) {
+      const int v = (tid + k * 256) / AG;
+      ra[k].store(As + v * PA + cga * 8);
+      if (do_bias) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bsum[j] += ra[k].get(j);
       }
-      if (ok) val.load(B + src * g.ldb + c8 * 8);
-      else val.zero();
-#pragma unroll
-      for (int j = 0; j < 8; ++j) Bs[(cg * 8 + j) * LDS_ROW + v] = from_f<T>(val.get(j));
     }
-    __syncthreads();
-    // ---- MFMA over the staged KV voxels
 #pragma unroll
-    for (int kk = 0; kk < KV; kk += 32) {
-      V8<T> af[RM], bfr[RN];
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-        af[i].load(&As[(wm * RM * 16 + i * 16 + (lane & 15)) * LDS_ROW + kk + (lane >> 4) * 8]);
-#pragma unroll
-      for (int j = 0; j < RN; ++j)
-        bfr[j].load(&Bs[(wn * RN * 16 + j * 16 + (lane & 15)) * LDS_ROW + kk + (lane >> 4) * 8]);
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int j = 0; j < RN; ++j) mfma_step<T>(acc[i][j], af[i], bfr[j]);
+    for (int k = 0; k < B_PER; ++k) {
+      const int v = (tid + k * 256) / BG;
+      rb[k].store(Bs + v * PB + cgb * 8);
     }
+  };
+
+  const int g4 = lane >> 4, i16 = lane & 15, q = i16 >> 2, p4 = i16 & 3;
+  int buf = 0;
+  if (v_begin < v_end) {
+    load_stage(v_begin);
+    write_stage(0);
+  }
+  __syncthreads();
+  for (long long vb = v_begin; vb < v_end; vb += KV) {
+    const bool more = vb + KV < v_end;
+    if (more) load_stage(vb + KV);
+    const T* As = lds + buf * (SA + SB);
+    const T* Bs = As + SA;
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int kk = 0; kk < KV; kk += 32) {
+        bf16x8 af[RM], bfr[RN];
+#pragma unroll
+        for (int i = 0; i < RM; ++i) {
+          const bf16_t* base = (const bf16_t*)As + (kk + 8 * g4 + q) * PA + wm * RM * 16 + i * 16 + 4 * p4;
+          af[i] = tr_frag(base, base + 4 * PA);
+        }
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          const bf16_t* base = (const bf16_t*)Bs + (kk + 8 * g4 + q) * PB + wn * RN * 16 + j * 16 + 4 * p4;
+          bfr[j] = tr_frag(base, base + 4 * PB);
+        }
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+#pragma unroll 4
+      for (int kk = 0; kk < KV; kk += 4) {
+        float af[RM], bfr[RN];
+#pragma unroll
+        for (int i = 0; i < RM; ++i) af[i] = (float)As[(kk + g4) * PA + wm * RM * 16 + i * 16 + i16];
+#pragma unroll
+        for (int j = 0; j < RN; ++j) bfr[j] = (float)Bs[(kk + g4) * PB + wn * RN * 16 + j * 16 + i16];
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (more) write_stage(buf ^ 1);
     __syncthreads();
+    buf ^= 1;
   }
 
 #pragma unroll
@@ -382,6 +638,19 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs g) {
         g.part[((long long)ks * g.Ca + row) * g.Ncols + col] = acc[i][j][r];
       }
     }
+  if (do_bias) {
+    // fixed-order reduction of the per-thread row sums (threads with equal tid % AG share rows)
+    float* red = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[tid * 8 + j] = bsum[j];
+    __syncthreads();
+    if (tid < BM) {
+      const int cg = tid >> 3, j = tid & 7;
+      float sacc = 0.f;
+      for (int t = cg; t < 256; t += AG) sacc += red[t * 8 + j];
+      if (row0 + tid < g.Ca) g.bias_part[(long long)ks * g.Ca + row0 + tid] = sacc;
+    }
+  }
 }
 
 // part[ks][row][col] -> torch-layout gradient (fixed-order sum over ks).
@@ -391,6 +660,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs g) {
 struct WReduceArgs {
   const float* part;
   float* grad;
+  const float* bias_part;
+  float* bias_grad;
   int Ca, Ncols, ksplit;
   int cpad, creal;    // per-tap channel count in cols (padded) and real count
   int ntap;           // 27 (CONV3), 1 (POINT), 8 (CONVT)
@@ -399,20 +670,27 @@ struct WReduceArgs {
 
 __global__ void wgrad_reduce_kernel(WReduceArgs g, int mode) {
   long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long total = (long long)g.Ca * g.creal * g.ntap;
+  const long long total = (long long)g.Ca * g.Ncols;     // enumerate the partial layout: coalesced reads
+  if (g.bias_part && idx >= total && idx < total + g.Ca) {
+    const int row = (int)(idx - total);
+    float v = 0.f;
+    for (int k = 0; k < g.ksplit; ++k) v += g.bias_part[(long long)k * g.Ca + row];
+    g.bias_grad[row] = g.accumulate ? g.bias_grad[row] + v : v;
+    return;
+  }
   if (idx >= total) return;
-  // idx enumerates the torch layout [row][c_real][tap]
-  const int t = (int)(idx % g.ntap);
-  long long q = idx / g.ntap;
-  const int c = (int)(q % g.creal);
-  const int row = (int)(q / g.creal);
-  const int col = t * g.cpad + c;
-  const long long stride = (long long)g.Ca * g.Ncols;
+  const int row = (int)(idx / g.Ncols);
+  const int col = (int)(idx - (long long)row * g.Ncols);
+  const int t = col / g.cpad, c = col - t * g.cpad;
+  if (c >= g.creal || t >= g.ntap) return;
   float v = 0.f;
-  const float* p = g.part + (long long)row * g.Ncols + col;
+  const long long stride = total;
+  const float* p = g.part + idx;
   for (int k = 0; k < g.ksplit; ++k) v += p[k * stride];
-  if (g.accumulate) g.grad[idx] += v;
-  else g.grad[idx] = v;
+  // torch layout [row][c_real][tap]
+  const long long dst = ((long long)row * g.creal + c) * g.ntap + t;
+  if (g.accumulate) g.grad[dst] += v;
+  else g.grad[dst] = v;
 }
 
 // Column sums (bias gradient): db[c] = sum_v dy[v][c], split over voxels.
@@ -450,14 +728,16 @@ __global__ void colsum_partial_kernel(const T* __restrict__ dy, int ld, int C, l
   }
 }
 
+// one wave per channel: lanes stride over the block partials, fixed shuffle tree
 __global__ void colsum_reduce_kernel(const float* __restrict__ part, int nblk, int C, float* __restrict__ out,
                                      int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (c >= C) return;
   float v = 0.f;
-  for (int b = 0; b < nblk; ++b) v += part[(long long)b * C + c];
-  if (accumulate) out[c] += v;
-  else out[c] = v;
+  for (int b = lane; b < nblk; b += 64) v += part[(long long)b * C + c];
+  v = wave_sum(v);
+  if (lane == 0) out[c] = accumulate ? out[c] + v : v;
 }
 
 // ------------------------------------------------------------ weight pack
@@ -517,18 +797,87 @@ __global__ void pack_weight_kernel(PackArgs g, int mode) {
   reinterpret_cast<T*>(g.dst)[idx] = from_f<T>(v);
 }
 
+// Batched pack: one launch packs every layer of a model (descriptor table in device memory).
+struct PackDesc {
+  const float* w;
+  void* dst;
+  int mode, Co, Ci, Cip, KG, KGp, Cpad, pad0;
+  long long begin;   // first element (of the virtual concatenation) owned by this descriptor
+};
+
+template <typename T>
+__global__ void pack_weight_batched_kernel(const PackDesc* __restrict__ descs, int n, long long total) {
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {                    // last descriptor with begin <= idx
+      const int mid = (lo + hi + 1) >> 1;
+      if (descs[mid].begin <= idx) lo = mid;
+      else hi = mid - 1;
+    }
+    const PackDesc d = descs[lo];
+    const long long li = idx - d.begin;
+    const int j = (int)(li & 7);
+    const long long q = li >> 3;
+    const int col = (int)(q % d.Cpad);
+    const int kgi = (int)(q / d.Cpad);
+    float v = 0.f;
+    if (kgi < d.KG) {
+      switch (d.mode) {
+        case 0: {
+          const int cpg = d.Cip >> 3, t = kgi / cpg, ci = (kgi % cpg) * 8 + j, co = col;
+          if (co < d.Co && ci < d.Ci) v = d.w[((long long)co * d.Ci + ci) * 27 + t];
+        } break;
+        case 1: {
+          const int cpg = d.Co >> 3, t = kgi / cpg, co = (kgi % cpg) * 8 + j, ci = col;
+          if (ci < d.Ci) v = d.w[((long long)co * d.Ci + ci) * 27 + (26 - t)];
+        } break;
+        case 2: {
+          const int ci = kgi * 8 + j, co = col;
+          if (co < d.Co && ci < d.Ci) v = d.w[(long long)co * d.Ci + ci];
+        } break;
+        case 3: {
+          const int co = kgi * 8 + j, ci = col;
+          if (ci < d.Ci && co < d.Co) v = d.w[(long long)co * d.Ci + ci];
+        } break;
+        case 4: {
+          const int ci = kgi * 8 + j;
+          const int t = col / d.Co, co = col % d.Co;
+          if (t < 8 && ci < d.Ci) v = d.w[((long long)ci * d.Co + co) * 8 + t];
+        } break;
+        case 5: {
+          const int cpg = d.Co >> 3, t = kgi / cpg, co = (kgi % cpg) * 8 + j, ci = col;
+          if (ci < d.Ci) v = d.w[((long long)ci * d.Co + co) * 8 + t];
+        } break;
+      }
+    }
+    reinterpret_cast<T*>(d.dst)[li] = from_f<T>(v);
+  }
+}
+
 // ------------------------------------------------------------ host launch
 template <typename T, int MODE>
 int launch_gemm(GemmArgs g, hipStream_t s) {
   const int Cbig = g.Ncols >= 64;
   dim3 block(256);
+  if (MODE == MODE_CONV3 && g.ksplit == 1 && knob("MMSEG_BRICK", 1) && (8 << g.cpg_shift) % CK == 0 &&
+      g.D % BRK_Z == 0 && g.H % BRK_Y == 0 && g.W % BRK_X == 0 && g.lda % 8 == 0) {
+    const int nb = (g.M / (g.D * g.H * g.W)) * (g.D / BRK_Z) * (g.H / BRK_Y) * (g.W / BRK_X);
+    const int bn = (g.Ncols >= 64 && knob("MMSEG_BRICK_BN", 64) == 64) ? 64 : 32;
+    if (bn == 64) {
+      hipLaunchKernelGGL((conv3_brick_kernel<T, 64>), dim3(nb * ceil_div(g.Ncols, 64)), block, 0, s, g);
+    } else {
+      hipLaunchKernelGGL((conv3_brick_kernel<T, 32>), dim3(nb * ceil_div(g.Ncols, 32)), block, 0, s, g);
+    }
+    return mmseg::check_launch("conv3_brick");
+  }
   if (!Cbig) {
     // BM=128, BN=32
-    dim3 grid(ceil_div(g.M, 128), ceil_div(g.Ncols, 32), g.ksplit);
+    dim3 grid(ceil_div(g.M, 128) * ceil_div(g.Ncols, 32) * g.ksplit);
     hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, 4, 1, 2, 2>), grid, block, 0, s, g);
   } else {
     // BM=128, BN=64
-    dim3 grid(ceil_div(g.M, 128), ceil_div(g.Ncols, 64), g.ksplit);
+    dim3 grid(ceil_div(g.M, 128) * ceil_div(g.Ncols, 64) * g.ksplit);
     hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, 2, 2, 4, 2>), grid, block, 0, s, g);
   }
   if (mmseg::check_launch("conv_gemm")) return 1;
@@ -555,12 +904,23 @@ int launch_gemm_mode(GemmArgs g, int mode, hipStream_t s) {
 template <typename T, int MODE>
 int launch_wgrad(WgradArgs g, hipStream_t s) {
   dim3 block(256);
+  const int bn = knob("MMSEG_WGRAD_BN", 64);
   if (g.Ca % 64 == 0) {
-    dim3 grid(ceil_div(g.Ncols, 64), g.Ca / 64, g.ksplit);
-    hipLaunchKernelGGL((wgrad_kernel<T, MODE, 2, 2, 2, 2, 64>), grid, block, 0, s, g);
+    if (bn == 128) {
+      dim3 grid(ceil_div(g.Ncols, 128) * (g.Ca / 64) * g.ksplit);
+      hipLaunchKernelGGL((wgrad_kernel<T, MODE, 2, 2, 2, 4, 64>), grid, block, 0, s, g);
+    } else {
+      dim3 grid(ceil_div(g.Ncols, 64) * (g.Ca / 64) * g.ksplit);
+      hipLaunchKernelGGL((wgrad_kernel<T, MODE, 2, 2, 2, 2, 64>), grid, block, 0, s, g);
+    }
   } else {
-    dim3 grid(ceil_div(g.Ncols, 64), ceil_div(g.Ca, 32), g.ksplit);
-    hipLaunchKernelGGL((wgrad_kernel<T, MODE, 1, 4, 2, 1, 64>), grid, block, 0, s, g);
+    if (bn == 128) {
+      dim3 grid(ceil_div(g.Ncols, 128) * ceil_div(g.Ca, 32) * g.ksplit);
+      hipLaunchKernelGGL((wgrad_kernel<T, MODE, 1, 4, 2, 2, 64>), grid, block, 0, s, g);
+    } else {
+      dim3 grid(ceil_div(g.Ncols, 64) * ceil_div(g.Ca, 32) * g.ksplit);
+      hipLaunchKernelGGL((wgrad_kernel<T, MODE, 1, 4, 2, 1, 64>), grid, block, 0, s, g);
+    }
   }
   return mmseg::check_launch("wgrad");
 }
@@ -583,6 +943,23 @@ int mmseg_pack_weight(const float* w, void* dst, int mode, int Co, int Ci, int C
   return mmseg::check_launch("pack_weight");
 }
 
+// descs: device array of n PackDesc (64 B each, see mmseg_pack_desc_bytes); total = sum of KGp*Cpad*8.
+int mmseg_pack_desc_bytes(void) { return (int)sizeof(PackDesc); }
+
+int mmseg_pack_weights_batched(const void* descs, int n, long long total, int dtype, void* stream) {
+  MMSEG_REQUIRE(n >= 1, "pack_weights_batched: n >= 1");
+  hipStream_t s = (hipStream_t)stream;
+  long long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (dtype == MMSEG_BF16)
+    hipLaunchKernelGGL(pack_weight_batched_kernel<bf16_t>, dim3((int)blocks), dim3(256), 0, s, (const PackDesc*)descs,
+                       n, total);
+  else
+    hipLaunchKernelGGL(pack_weight_batched_kernel<float>, dim3((int)blocks), dim3(256), 0, s, (const PackDesc*)descs,
+                       n, total);
+  return mmseg::check_launch("pack_weights_batched");
+}
+
 // Generic implicit-GEMM: conv3 fwd / dgrad, 1x1, convT fwd / dgrad.
 int mmseg_conv_gemm(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
                     float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W,
@@ -595,20 +972,22 @@ int mmseg_conv_gemm(const void* a, int lda, const void* wpacked, const float* bi
   const int KGp = (KG + 3) & ~3;
   int kps = ((ceil_div(KGp, ksplit) + 3) / 4) * 4;
   ksplit = ceil_div(KGp, kps);
-  GemmArgs g{a, lda, wpacked, bias, out, ldo, splitk_ws, M, Ncols, Cpad, KG, cpg_shift, D, H, W, ksplit, kps};
+  GemmArgs g{a, lda, wpacked, bias, out, ldo, splitk_ws, M, Ncols, Cpad, KG, cpg_shift, D, H, W, ksplit, kps,
+             knob("MMSEG_SWIZZLE", 1)};
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16) return launch_gemm_mode<bf16_t>(g, mode, s);
   return launch_gemm_mode<float>(g, mode, s);
 }
 
 // Weight-gradient partials: part[ksplit][Ca][Ncols] (fp32).
-int mmseg_wgrad(const void* a, int lda, const void* b, int ldb, float* part, int mode, int Ca, int Ncols,
-                int cpg_shift, long long V, int D, int H, int W, int ksplit, int dtype, void* stream) {
+int mmseg_wgrad(const void* a, int lda, const void* b, int ldb, float* part, float* bias_part, int mode, int Ca,
+                int Ncols, int cpg_shift, long long V, int D, int H, int W, int ksplit, int dtype, void* stream) {
   MMSEG_REQUIRE(Ca % 8 == 0, "wgrad: rows (%d) must be a multiple of 8", Ca);
   MMSEG_REQUIRE(Ncols % 8 == 0, "wgrad: cols (%d) must be a multiple of 8", Ncols);
   long long vps = ((V + ksplit - 1) / ksplit + 63) / 64 * 64;
   ksplit = (int)((V + vps - 1) / vps);
-  WgradArgs g{a, lda, b, ldb, part, Ca, Ncols, cpg_shift, V, D, H, W, ksplit, vps};
+  WgradArgs g{a, lda, b, ldb, part, bias_part, Ca, Ncols, cpg_shift, V, D, H, W, ksplit, vps,
+              knob("MMSEG_WGRAD_SWIZZLE", 0)};
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16) {
     switch (mode) {
@@ -633,10 +1012,10 @@ int mmseg_wgrad_splits(long long V, int ksplit) {
   return (int)((V + vps - 1) / vps);
 }
 
-int mmseg_wgrad_reduce(const float* part, float* grad, int Ca, int Ncols, int ksplit, int cpad, int creal, int ntap,
-                       int accumulate, void* stream) {
-  WReduceArgs g{part, grad, Ca, Ncols, ksplit, cpad, creal, ntap, accumulate};
-  long long total = (long long)Ca * creal * ntap;
+int mmseg_wgrad_reduce(const float* part, float* grad, const float* bias_part, float* bias_grad, int Ca, int Ncols,
+                       int ksplit, int cpad, int creal, int ntap, int accumulate, void* stream) {
+  WReduceArgs g{part, grad, bias_part, bias_grad, Ca, Ncols, ksplit, cpad, creal, ntap, accumulate};
+  long long total = (long long)Ca * Ncols + (bias_part ? Ca : 0);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, g, 0);
   return mmseg::check_launch("wgrad_reduce");
 }
@@ -655,7 +1034,7 @@ int mmseg_colsum(const void* dy, int ld, int C, long long V, float* part, int nb
     hipLaunchKernelGGL(colsum_partial_kernel<float>, dim3(nblk), dim3(256), 0, s, (const float*)dy, ld, C, V, vps,
                        part);
   if (mmseg::check_launch("colsum_partial")) return 1;
-  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, s, part, nblk, C, out, accumulate);
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(ceil_div(C, 4)), dim3(256), 0, s, part, nblk, C, out, accumulate);
   return mmseg::check_launch("colsum_reduce");
 }
 

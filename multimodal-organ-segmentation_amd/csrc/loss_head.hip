@@ -100,60 +100,67 @@ __global__ void head_dgrad_kernel(const float* __restrict__ dlog, const float* _
 }
 
 // partial dW[c][ci] and db[c] per voxel chunk (block), fixed order.
+// thread = (voxel lane, 8-channel group): vectorised x loads, 8x8 register tile per class chunk.
 template <typename T>
 __global__ void head_wgrad_partial(const T* __restrict__ x, int ldx, const float* __restrict__ dlog,
                                    const float* __restrict__ dscale, int C, int Cin, long long V, int N,
                                    long long vpc, float* __restrict__ part) {
-  constexpr int KV = 64;
-  extern __shared__ float sh[];
-  float* xs = sh;              // KV * Cin
-  float* ds = sh + KV * Cin;   // C * KV
+  __shared__ float red[256 * 8];
+  const int C8 = Cin >> 3;
+  const int lanes_v = 256 / C8;
+  const int tid = threadIdx.x;
+  const int cg = tid % C8, vl = tid / C8;
   const long long total = (long long)N * V;
   const long long e0 = (long long)blockIdx.x * vpc;
   long long e1 = e0 + vpc;
   if (e1 > total) e1 = total;
-  const int npairs = C * Cin + C;  // (c, ci) pairs then bias terms
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (long long eb = e0; eb < e1; eb += KV) {
-    __syncthreads();
-    for (int t = threadIdx.x; t < KV * Cin; t += blockDim.x) {
-      const int vv = t / Cin, ci = t - vv * Cin;
-      const long long e = eb + vv;
-      float val = 0.f;
-      if (e < e1) {
-        val = to_f<T>(x[e * ldx + ci]);
-        if (dscale) val *= dscale[(e / V) * Cin + ci];
-      }
-      xs[t] = val;
+  const int npairs = C * Cin + C;
+  for (int c0 = 0; c0 < C; c0 += 8) {
+    float acc[8][8], bacc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      bacc[k] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
     }
-    for (int t = threadIdx.x; t < C * KV; t += blockDim.x) {
-      const int c = t / KV, vv = t - c * KV;
-      const long long e = eb + vv;
-      float val = 0.f;
-      if (e < e1) {
+    if (vl < lanes_v) {
+      for (long long e = e0 + vl; e < e1; e += lanes_v) {
         const long long n = e / V, v = e - n * V;
-        val = dlog[(n * C + c) * V + v];
+        V8<T> a;
+        a.load(x + e * ldx + cg * 8);
+        float xv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[j] = dscale ? a.get(j) * dscale[n * Cin + cg * 8 + j] : a.get(j);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (c0 + k >= C) break;
+          const float d = dlog[(n * C + c0 + k) * V + v];
+          bacc[k] += d;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[k][j] = fmaf(d, xv[j], acc[k][j]);
+        }
       }
-      ds[t] = val;
     }
-    __syncthreads();
-    for (int k = 0; k < 4; ++k) {
-      const int p = threadIdx.x + k * blockDim.x;
-      if (p >= npairs) break;
-      float a = acc[k];
-      if (p < C * Cin) {
-        const int c = p / Cin, ci = p - c * Cin;
-        for (int vv = 0; vv < KV; ++vv) a = fmaf(ds[c * KV + vv], xs[vv * Cin + ci], a);
-      } else {
-        const int c = p - C * Cin;
-        for (int vv = 0; vv < KV; ++vv) a += ds[c * KV + vv];
+    for (int k = 0; k < 8 && c0 + k < C; ++k) {
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[tid * 8 + j] = acc[k][j];
+      __syncthreads();
+      for (int ci = tid; ci < Cin; ci += 256) {
+        const int g = ci >> 3, j = ci & 7;
+        float sacc = 0.f;
+        for (int l = 0; l < lanes_v; ++l) sacc += red[(l * C8 + g) * 8 + j];
+        part[(long long)blockIdx.x * npairs + (c0 + k) * Cin + ci] = sacc;
       }
-      acc[k] = a;
+      __syncthreads();
+      red[tid] = (cg == 0 && vl < lanes_v) ? bacc[k] : 0.f;
+      __syncthreads();
+      if (tid == 0) {
+        float sacc = 0.f;
+        for (int l = 0; l < lanes_v; ++l) sacc += red[l * C8];
+        part[(long long)blockIdx.x * npairs + C * Cin + c0 + k] = sacc;
+      }
     }
-  }
-  for (int k = 0; k < 4; ++k) {
-    const int p = threadIdx.x + k * blockDim.x;
-    if (p < npairs) part[(long long)blockIdx.x * npairs + p] = acc[k];
   }
 }
 
@@ -437,8 +444,8 @@ int grid_for(long long total) {
 }
 
 int loss_chunks(long long V, long long* vpc) {
-  long long nch = (V + 8191) / 8192;
-  if (nch > 512) nch = 512;
+  long long nch = (V + 2047) / 2048;
+  if (nch > 1024) nch = 1024;
   if (nch < 1) nch = 1;
   *vpc = (V + nch - 1) / nch;
   return (int)((V + *vpc - 1) / *vpc);
@@ -483,7 +490,7 @@ long long mmseg_head_ws_floats(int C, int Cin, int N, long long V) {
 int mmseg_head_bwd(const void* x, int ldx, int Cin, const float* W, const float* dscale, int C, int N, long long V,
                    const float* dlogits, void* dx, int lddx, float* gW, float* gb, float* ws, int accumulate, int dtype,
                    void* stream) {
-  MMSEG_REQUIRE(C >= 1 && C <= CMAX && Cin % 8 == 0 && C * Cin + C <= 1024, "head_bwd: shape");
+  MMSEG_REQUIRE(C >= 1 && C <= CMAX && Cin % 8 == 0 && Cin <= 2048, "head_bwd: shape");
   hipStream_t s = (hipStream_t)stream;
   const long long total = (long long)N * V;
   const int grid = grid_for(total);
@@ -491,7 +498,7 @@ int mmseg_head_bwd(const void* x, int ldx, int Cin, const float* W, const float*
   long long nblk = 512;
   long long vpc = ((total + nblk - 1) / nblk + 63) / 64 * 64;
   nblk = (total + vpc - 1) / vpc;
-  const size_t shm2 = (size_t)(64 * Cin + C * 64) * sizeof(float);
+  const size_t shm2 = 0;
   // weight-gradient partials first: dx may alias x (the engine reuses the feature buffer)
   if (dtype == MMSEG_BF16) {
     hipLaunchKernelGGL(head_wgrad_partial<bf16_t>, dim3((int)nblk), dim3(256), shm2, s, (const bf16_t*)x, ldx, dlogits,

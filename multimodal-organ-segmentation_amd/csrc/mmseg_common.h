@@ -107,3 +107,12 @@ __device__ __forceinline__ uint32_t tap_valid_mask(int z, int y, int x, int D, i
   }
   return m;
 }
+
+// XCD-aware block remap (MI355X: 8 XCDs, blocks dealt round-robin b -> b % 8).
+// Returns a logical tile id such that each XCD walks a CONTIGUOUS range of
+// logical tiles (neighbouring tiles share operand panels in that XCD's L2).
+// Bijective for any T (speed only; correctness never depends on placement).
+__device__ __forceinline__ int xcd_swizzle(int b, int T) {
+  const int xcd = b & 7, j = b >> 3, q = T >> 3, r = T & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+}

@@ -74,19 +74,24 @@ __global__ void in_stats_partial(const T* __restrict__ x, int ld, long long V, i
   }
 }
 
+// one wave per (n, c): lanes stride over the chunk partials, double shuffle tree (fixed order)
 template <typename T>
 __global__ void in_stats_finalize(const T* __restrict__ x, int ld, long long V, int N, int C, int nchunk,
                                   const float* __restrict__ part, float eps, float* __restrict__ mean,
                                   int mean_ld, float* __restrict__ rstd) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (idx >= N * C) return;
   const int n = idx / C, c = idx - n * C;
   double a = 0.0, b = 0.0;
-  for (int k = 0; k < nchunk; ++k) {
+  for (int k = lane; k < nchunk; k += 64) {
     const float* p = part + (((long long)n * nchunk + k) * C + c) * 2;
     a += p[0];
     b += p[1];
   }
+  a = wave_sum_d(a);
+  b = wave_sum_d(b);
+  if (lane != 0) return;
   const double K = to_f<T>(x[(long long)n * V * ld + c]);
   const double m1 = a / (double)V;
   double var = b / (double)V - m1 * m1;
@@ -280,17 +285,22 @@ __global__ void in_bwd_partial(const T* __restrict__ x, int ldx, const float* __
 
 __global__ void in_bwd_finalize(const float* __restrict__ part, int N, int C, int nchunk, long long V,
                                 float* __restrict__ coef) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (idx >= N * C) return;
   const int n = idx / C, c = idx - n * C;
   double a = 0.0, b = 0.0;
-  for (int k = 0; k < nchunk; ++k) {
+  for (int k = lane; k < nchunk; k += 64) {
     const float* p = part + (((long long)n * nchunk + k) * C + c) * 2;
     a += p[0];
     b += p[1];
   }
-  coef[idx * 2 + 0] = (float)(a / (double)V);
-  coef[idx * 2 + 1] = (float)(b / (double)V);
+  a = wave_sum_d(a);
+  b = wave_sum_d(b);
+  if (lane == 0) {
+    coef[idx * 2 + 0] = (float)(a / (double)V);
+    coef[idx * 2 + 1] = (float)(b / (double)V);
+  }
 }
 
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat))
@@ -534,11 +544,11 @@ int mmseg_instnorm_stats(const void* x, int ldx, int N, long long V, int C, floa
   dim3 grid(nch, N);
   if (dtype == MMSEG_BF16) {
     hipLaunchKernelGGL(in_stats_partial<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, V, C, vpc, ws);
-    hipLaunchKernelGGL(in_stats_finalize<bf16_t>, dim3(ceil_div(N * C, 256)), dim3(256), 0, s, (const bf16_t*)x, ldx,
+    hipLaunchKernelGGL(in_stats_finalize<bf16_t>, dim3(ceil_div(N * C, 4)), dim3(256), 0, s, (const bf16_t*)x, ldx,
                        V, N, C, nch, ws, eps, mean, mean_ld, rstd);
   } else {
     hipLaunchKernelGGL(in_stats_partial<float>, grid, dim3(256), 0, s, (const float*)x, ldx, V, C, vpc, ws);
-    hipLaunchKernelGGL(in_stats_finalize<float>, dim3(ceil_div(N * C, 256)), dim3(256), 0, s, (const float*)x, ldx, V,
+    hipLaunchKernelGGL(in_stats_finalize<float>, dim3(ceil_div(N * C, 4)), dim3(256), 0, s, (const float*)x, ldx, V,
                        N, C, nch, ws, eps, mean, mean_ld, rstd);
   }
   return mmseg::check_launch("instnorm_stats");
@@ -576,13 +586,13 @@ int mmseg_instnorm_relu_bwd(const void* x, int ldx, const float* mean, const flo
   if (dtype == MMSEG_BF16) {
     hipLaunchKernelGGL(in_bwd_partial<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, mean, rstd, src, V, C, D,
                        H, W, vpc, part);
-    hipLaunchKernelGGL(in_bwd_finalize, dim3(ceil_div(N * C, 256)), dim3(256), 0, s, part, N, C, nch, V, coef);
+    hipLaunchKernelGGL(in_bwd_finalize, dim3(ceil_div(N * C, 4)), dim3(256), 0, s, part, N, C, nch, V, coef);
     hipLaunchKernelGGL(in_bwd_apply<bf16_t>, dim3(ag), dim3(256), 0, s, (const bf16_t*)x, ldx, mean, rstd, src, coef,
                        (bf16_t*)dx, lddx, V, N, C, D, H, W);
   } else {
     hipLaunchKernelGGL(in_bwd_partial<float>, grid, dim3(256), 0, s, (const float*)x, ldx, mean, rstd, src, V, C, D,
                        H, W, vpc, part);
-    hipLaunchKernelGGL(in_bwd_finalize, dim3(ceil_div(N * C, 256)), dim3(256), 0, s, part, N, C, nch, V, coef);
+    hipLaunchKernelGGL(in_bwd_finalize, dim3(ceil_div(N * C, 4)), dim3(256), 0, s, part, N, C, nch, V, coef);
     hipLaunchKernelGGL(in_bwd_apply<float>, dim3(ag), dim3(256), 0, s, (const float*)x, ldx, mean, rstd, src, coef,
                        (float*)dx, lddx, V, N, C, D, H, W);
   }

@@ -14,6 +14,7 @@ so a training step needs no activation memory beyond the forward's.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -21,11 +22,17 @@ import torch
 import torch.nn as nn
 
 from .._lib import ptr
+from .profiler import TIMER
 from .runtime import Act, FlatParams, Runtime, pow2_shift, round_up
 
 MODE_CONV3, MODE_POINT, MODE_CONVT_FWD, MODE_CONVT_DGRAD = 0, 1, 2, 3
 IN_EPS = 1e-5
 TARGET_BLOCKS = 1024
+
+
+def _gemm_name(rt: Runtime, ncols: int, mode: str) -> str:
+    tile = "128x64" if ncols >= 64 else "128x32"
+    return f"conv_gemm[{'bf16' if rt.code else 'f32'},{mode},{tile}]"
 
 
 def _col_tile(n: int) -> int:
@@ -39,8 +46,31 @@ def _gemm_ksplit(M: int, ncols: int, KG: int) -> int:
     return max(1, min(-(-512 // tiles), KG // 16))
 
 
+class BatchedPacker:
+    """All weight packs of a program in ONE launch (descriptor table uploaded once)."""
+
+    def __init__(self, rt: Runtime, descs):
+        import struct
+        self.rt = rt
+        nbytes = rt.lib.mmseg_pack_desc_bytes()
+        blob = bytearray()
+        begin = 0
+        for (w, dst, mode, Co, Ci, Cip, KG, KGp, Cpad) in descs:
+            rec = struct.pack("<QQ8iq", w, dst, mode, Co, Ci, Cip, KG, KGp, Cpad, 0, begin)
+            assert len(rec) == nbytes, (len(rec), nbytes)
+            blob += rec
+            begin += KGp * Cpad * 8
+        self.n = len(descs)
+        self.total = begin
+        self.table = torch.frombuffer(bytes(blob), dtype=torch.uint8).to(rt.device)
+
+    def run(self):
+        self.rt.lib.mmseg_pack_weights_batched(ptr(self.table), self.n, self.total, self.rt.code, self.rt.stream)
+
+
 def _wgrad_ksplit(rows: int, ncols: int, V: int) -> int:
-    tiles = -(-ncols // 64) * -(-rows // (64 if rows % 64 == 0 else 32))
+    bn = int(os.environ.get("MMSEG_WGRAD_BN", "64"))
+    tiles = -(-ncols // bn) * -(-rows // (64 if rows % 64 == 0 else 32))
     return max(1, min(-(-TARGET_BLOCKS // tiles), V // 512))
 
 
@@ -80,42 +110,47 @@ class Conv3:
             self.Cpad_d = _col_tile(self.Cip)
             self.wd = torch.empty(self.KGdp * self.Cpad_d * 8, dtype=rt.dtype, device=rt.device)
 
-    def pack(self):
-        L, s, w = self.rt.lib, self.rt.stream, self.conv.weight
-        L.mmseg_pack_weight(ptr(w), ptr(self.wf), 0, self.Co, self.Ci, self.Cip, self.KG, self.KGp, self.Cpad,
-                            self.rt.code, s)
+    def descs(self):
+        w = self.conv.weight
+        d = [(ptr(w), ptr(self.wf), 0, self.Co, self.Ci, self.Cip, self.KG, self.KGp, self.Cpad)]
         if self.need_dgrad:
-            L.mmseg_pack_weight(ptr(w), ptr(self.wd), 1, self.Co, self.Ci, self.Cip, self.KGd, self.KGdp,
-                                self.Cpad_d, self.rt.code, s)
+            d.append((ptr(w), ptr(self.wd), 1, self.Co, self.Ci, self.Cip, self.KGd, self.KGdp, self.Cpad_d))
+        return d
+
+    def pack(self):
+        for d in self.descs():
+            self.rt.lib.mmseg_pack_weight(*d, self.rt.code, self.rt.stream)
 
     def fwd(self, x: Act, y: Act):
         M = x.N * x.V
         ks = _gemm_ksplit(M, self.Co, self.KG)
         ws = self.rt.ws(ks * M * self.Co) if ks > 1 else None
-        self.rt.lib.mmseg_conv_gemm(x.ptr, x.ld, ptr(self.wf), ptr(self.conv.bias), y.ptr, y.ld, ptr(ws), MODE_CONV3,
-                                    M, self.Co, self.Cpad, self.KG, self.cpg_shift, x.D, x.H, x.W, ks, self.rt.code,
-                                    self.rt.stream)
+        with TIMER.region(_gemm_name(self.rt, self.Co, "conv3"), flops=2.0 * M * self.Co * 27 * self.Ci):
+            self.rt.lib.mmseg_conv_gemm(x.ptr, x.ld, ptr(self.wf), ptr(self.conv.bias), y.ptr, y.ld, ptr(ws),
+                                        MODE_CONV3, M, self.Co, self.Cpad, self.KG, self.cpg_shift, x.D, x.H, x.W, ks,
+                                        self.rt.code, self.rt.stream)
 
     def bwd(self, x: Act, dy: Act, dx: Optional[Act], accumulate: bool):
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
         V = x.N * x.V
         ncols = 27 * self.Cip
         ks = L.mmseg_wgrad_splits(V, _wgrad_ksplit(self.Co, ncols, V))
-        part = self.rt.ws(max(ks * self.Co * ncols, 256 * self.Co))
-        L.mmseg_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, ptr(part), MODE_CONV3, self.Co, ncols, self.cpg_shift, V, x.D, x.H,
-                      x.W, ks, code, s)
-        L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.conv.weight)), self.Co, ncols, ks, self.Cip, self.Ci,
-                             27, int(accumulate), s)
-        nblk = 256
-        L.mmseg_colsum(dy.ptr, dy.ld, self.Co, V, ptr(part), nblk, ptr(self.flat.grad(self.conv.bias)),
-                       int(accumulate), code, s)
+        part = self.rt.ws(ks * self.Co * ncols + ks * self.Co)
+        bpart = part.data_ptr() + ks * self.Co * ncols * 4
+        with TIMER.region(f"wgrad[{'bf16' if code else 'f32'},conv3]", flops=2.0 * V * self.Co * 27 * self.Ci):
+            L.mmseg_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, ptr(part), bpart, MODE_CONV3, self.Co, ncols, self.cpg_shift, V,
+                          x.D, x.H, x.W, ks, code, s)
+        L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.conv.weight)), bpart,
+                             ptr(self.flat.grad(self.conv.bias)), self.Co, ncols, ks, self.Cip, self.Ci, 27,
+                             int(accumulate), s)
         self.flat.mark(self.conv.weight, self.conv.bias)
         if dx is not None:
             M = V
             ks = _gemm_ksplit(M, self.Ci, self.KGd)
             ws = self.rt.ws(ks * M * self.Ci) if ks > 1 else None
-            L.mmseg_conv_gemm(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, ptr(ws), MODE_CONV3, M, self.Ci,
-                              self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, ks, code, s)
+            with TIMER.region(_gemm_name(self.rt, self.Ci, "conv3"), flops=2.0 * M * self.Co * 27 * self.Ci):
+                L.mmseg_conv_gemm(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, ptr(ws), MODE_CONV3, M, self.Ci,
+                                  self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, ks, code, s)
 
 
 class ConvT2:
@@ -134,12 +169,14 @@ class ConvT2:
         self.Cpad_d = _col_tile(self.Ci)
         self.wd = torch.empty(self.KGdp * self.Cpad_d * 8, dtype=rt.dtype, device=rt.device)
 
+    def descs(self):
+        w = self.up.weight
+        return [(ptr(w), ptr(self.wf), 4, self.Co, self.Ci, self.Ci, self.KG, self.KGp, self.Cpad),
+                (ptr(w), ptr(self.wd), 5, self.Co, self.Ci, self.Ci, self.KGd, self.KGdp, self.Cpad_d)]
+
     def pack(self):
-        L, s, w = self.rt.lib, self.rt.stream, self.up.weight
-        L.mmseg_pack_weight(ptr(w), ptr(self.wf), 4, self.Co, self.Ci, self.Ci, self.KG, self.KGp, self.Cpad,
-                            self.rt.code, s)
-        L.mmseg_pack_weight(ptr(w), ptr(self.wd), 5, self.Co, self.Ci, self.Ci, self.KGd, self.KGdp, self.Cpad_d,
-                            self.rt.code, s)
+        for d in self.descs():
+            self.rt.lib.mmseg_pack_weight(*d, self.rt.code, self.rt.stream)
 
     def fwd(self, x: Act, y: Act):
         M = x.N * x.V
@@ -157,10 +194,11 @@ class ConvT2:
         ncols = 8 * self.Co
         ks = L.mmseg_wgrad_splits(V, _wgrad_ksplit(self.Ci, ncols, V))
         part = self.rt.ws(max(ks * self.Ci * ncols, 256 * self.Co))
-        L.mmseg_wgrad(x.ptr, x.ld, dy.ptr, dy.ld, ptr(part), MODE_CONVT_DGRAD, self.Ci, ncols, self.dshift, V, x.D,
-                      x.H, x.W, ks, code, s)
-        L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.up.weight)), self.Ci, ncols, ks, self.Co, self.Co, 8,
-                             int(accumulate), s)
+        with TIMER.region(f"wgrad[{'bf16' if code else 'f32'},convT]", flops=2.0 * V * self.Ci * 8 * self.Co):
+            L.mmseg_wgrad(x.ptr, x.ld, dy.ptr, dy.ld, ptr(part), None, MODE_CONVT_DGRAD, self.Ci, ncols, self.dshift,
+                          V, x.D, x.H, x.W, ks, code, s)
+        L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.up.weight)), None, None, self.Ci, ncols, ks, self.Co,
+                             self.Co, 8, int(accumulate), s)
         L.mmseg_colsum(dy.ptr, dy.ld, self.Co, dy.N * dy.V, ptr(part), 256, ptr(self.flat.grad(self.up.bias)),
                        int(accumulate), code, s)
         self.flat.mark(self.up.weight, self.up.bias)
@@ -182,12 +220,14 @@ class Point:
         self.wf = torch.empty(self.KGp * self.Cpad * 8, dtype=rt.dtype, device=rt.device)
         self.wd = torch.empty(self.KGdp * self.Cpad_d * 8, dtype=rt.dtype, device=rt.device)
 
+    def descs(self):
+        w = self.conv.weight
+        return [(ptr(w), ptr(self.wf), 2, self.Co, self.Ci, self.Ci, self.KG, self.KGp, self.Cpad),
+                (ptr(w), ptr(self.wd), 3, self.Co, self.Ci, self.Ci, self.KGd, self.KGdp, self.Cpad_d)]
+
     def pack(self):
-        L, s, w = self.rt.lib, self.rt.stream, self.conv.weight
-        L.mmseg_pack_weight(ptr(w), ptr(self.wf), 2, self.Co, self.Ci, self.Ci, self.KG, self.KGp, self.Cpad,
-                            self.rt.code, s)
-        L.mmseg_pack_weight(ptr(w), ptr(self.wd), 3, self.Co, self.Ci, self.Ci, self.KGd, self.KGdp, self.Cpad_d,
-                            self.rt.code, s)
+        for d in self.descs():
+            self.rt.lib.mmseg_pack_weight(*d, self.rt.code, self.rt.stream)
 
     def fwd(self, x: Act, y: Act):
         M = x.N * x.V
@@ -198,13 +238,13 @@ class Point:
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
         V = x.N * x.V
         ks = L.mmseg_wgrad_splits(V, _wgrad_ksplit(self.Co, self.Ci, V))
-        part = self.rt.ws(max(ks * self.Co * self.Ci, 256 * self.Co))
-        L.mmseg_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, ptr(part), MODE_POINT, self.Co, self.Ci, 0, V, x.D, x.H, x.W, ks,
-                      code, s)
-        L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.conv.weight)), self.Co, self.Ci, ks, self.Ci, self.Ci,
-                             1, int(accumulate), s)
-        L.mmseg_colsum(dy.ptr, dy.ld, self.Co, V, ptr(part), 256, ptr(self.flat.grad(self.conv.bias)),
-                       int(accumulate), code, s)
+        part = self.rt.ws(ks * self.Co * self.Ci + ks * self.Co)
+        bpart = part.data_ptr() + ks * self.Co * self.Ci * 4
+        L.mmseg_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, ptr(part), bpart, MODE_POINT, self.Co, self.Ci, 0, V, x.D, x.H, x.W,
+                      ks, code, s)
+        L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.conv.weight)), bpart,
+                             ptr(self.flat.grad(self.conv.bias)), self.Co, self.Ci, ks, self.Ci, self.Ci, 1,
+                             int(accumulate), s)
         self.flat.mark(self.conv.weight, self.conv.bias)
         if dx is not None:
             L.mmseg_conv_gemm(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, None, MODE_POINT, V, self.Ci,
@@ -221,6 +261,9 @@ class Block:
         self.c2 = Conv3(rt, module.conv2, flat)
         self.Co = self.c1.Co
         self.shape = None
+
+    def descs(self):
+        return self.c1.descs() + self.c2.descs()
 
     def pack(self):
         self.c1.pack()

@@ -13,13 +13,14 @@ Memory plan (per level l, spatial S/2^l, F[l] channels, NDHWC):
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.nn as nn
 
 from .._lib import ptr
-from .layers import Block, ConvT2, DySpec, Head, Point
+from .layers import BatchedPacker, Block, ConvT2, DySpec, Head, Point
 from .runtime import Act, FlatParams, Runtime
 
 
@@ -42,11 +43,13 @@ class _Decoder:
         self.head = Head(rt, out_conv, flat)
         self.p = dropout
 
-    def pack(self):
+    def descs(self):
+        d = []
         for u in self.ups:
-            u.pack()
+            d += u.descs()
         for b in self.blocks:
-            b.pack()
+            d += b.descs()
+        return d
 
     def setup(self, N, dims):
         rt, F = self.rt, self.F
@@ -103,10 +106,16 @@ class UNetProgram:
         self.shape = None
 
     def pack(self):
-        self.init.pack()
-        for b in self.enc:
-            b.pack()
-        self.dec.pack()
+        if os.environ.get("MMSEG_BATCHED_PACK", "0") != "1":
+            for d in self._all_descs():
+                self.rt.lib.mmseg_pack_weight(*d, self.rt.code, self.rt.stream)
+            return
+        if getattr(self, "_packer", None) is None:
+            d = self.init.descs()
+            for b in self.enc:
+                d += b.descs()
+            self._packer = BatchedPacker(self.rt, d + self.dec.descs())
+        self._packer.run()
 
     def setup(self, N, D, H, W):
         if self.shape == (N, D, H, W):
@@ -122,6 +131,12 @@ class UNetProgram:
         self.idx = [None] + [torch.empty(N * dims[l][0] * dims[l][1] * dims[l][2] * F[l - 1], dtype=torch.uint8,
                                          device=rt.device) for l in range(1, self.L)]
         self.bottom = rt.act(N, *dims[-1], F[-1])
+
+    def _all_descs(self):
+        d = self.init.descs()
+        for b in self.enc:
+            d += b.descs()
+        return d + self.dec.descs()
 
     def level_out(self, l: int) -> Act:
         return self.dec.skip_slot(l) if l < self.L - 1 else self.bottom
@@ -174,14 +189,31 @@ class DualEncoderProgram:
         self.flat = flat
         self.shape = None
 
-    def pack(self):
+    def _all_descs(self):
+        d = []
         for blocks in self.encs:
             for b in blocks:
-                b.pack()
+                d += b.descs()
         if self.proj:
             for p in self.proj:
-                p.pack()
-        self.dec.pack()
+                d += p.descs()
+        return d + self.dec.descs()
+
+    def pack(self):
+        if os.environ.get("MMSEG_BATCHED_PACK", "0") != "1":
+            for d in self._all_descs():
+                self.rt.lib.mmseg_pack_weight(*d, self.rt.code, self.rt.stream)
+            return
+        if getattr(self, "_packer", None) is None:
+            d = []
+            for blocks in self.encs:
+                for b in blocks:
+                    d += b.descs()
+            if self.proj:
+                for p in self.proj:
+                    d += p.descs()
+            self._packer = BatchedPacker(self.rt, d + self.dec.descs())
+        self._packer.run()
 
     def setup(self, N, D, H, W):
         if self.shape == (N, D, H, W):

@@ -51,7 +51,7 @@ class DualEncoder(nn.Module):
         super().__init__()
         if in_channels_per_modality != 1:
             raise NotImplementedError("engine DualEncoder: one channel per modality (reference builder default)")
-        features = list(features)
+        features = [int(f) for f in features]
         self.in_channels_per_modality = in_channels_per_modality
         self.num_modalities = num_modalities
         self.out_channels = out_channels

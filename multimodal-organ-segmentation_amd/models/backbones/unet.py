@@ -76,7 +76,7 @@ class UNet3D(nn.Module):
     def __init__(self, in_channels: int = 1, out_channels: int = 8, features: List[int] = (32, 64, 128, 256, 512),
                  norm: str = "instance", dropout: float = 0.0, **kwargs):
         super().__init__()
-        features = list(features)
+        features = [int(f) for f in features]
         self.in_channels = in_channels
         self.out_channels = out_channels
         self.features = features
