@@ -448,6 +448,7 @@ struct WgradArgs {
   int ksplit;
   long long vox_per_split;   // multiple of KV
   int swz;
+  int brick;                 // CONV3 only: ksplit splits the brick list instead of voxels
 };
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
@@ -649,6 +650,210 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs g) {
       float sacc = 0.f;
       for (int t = cg; t < 256; t += AG) sacc += red[t * 8 + j];
       if (row0 + tid < g.Ca) g.bias_part[(long long)ks * g.Ca + row0 + tid] = sacc;
+    }
+  }
+}
+
+// ------------------------------------------------------- brick wgrad (3^3)
+// dW[co][tap][ci] partials with the input halo reused by all 27 taps: a block
+// owns 32 output channels x one 32-channel input chunk x ALL 27 taps, and walks
+// a contiguous range of 4x4x8 bricks.  Per brick it stages dy [128 vox][32 co]
+// and the x halo [6x6x10][32 ci] into LDS; K = the brick's 128 voxels.  The
+// MFMA operands are read with ds_read_b64_tr_b16 (K = voxels is the strided
+// dimension of NDHWC): the A rows come from the dy tile, the B rows from halo
+// rows shifted by the tap (4 arbitrary row addresses per 16-lane group).
+// Wave w accumulates taps [7w, 7w+7) -> 2 x 7 x 2 MFMA tiles in registers.
+template <typename T>
+__global__ __launch_bounds__(256) void wgrad_brick_kernel(WgradArgs g) {
+  constexpr int EP = 16 / sizeof(T);
+  constexpr int DP = 32 + EP;                    // dy tile pitch
+  constexpr int XP = CK + EP;                    // halo pitch
+  constexpr int DS = 128 * DP, XS = HLO_V * XP;
+  __shared__ __attribute__((aligned(16))) T lds[DS + XS];
+  T* Dl = lds;
+  T* Xl = lds + DS;
+  constexpr int D_ITEMS = 128 * 4, X_ITEMS = HLO_V * 4;
+  constexpr int D_PER = D_ITEMS / 256, X_PER = (X_ITEMS + 255) / 256;
+
+  const T* Dy = reinterpret_cast<const T*>(g.a);
+  const T* X = reinterpret_cast<const T*>(g.b);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cin = 8 << g.cpg_shift;
+  const int nchunk = cin / CK, rt_n = g.Ca / 32;
+  const int tile = blockIdx.x;
+  const int ct = tile % nchunk, rt = (tile / nchunk) % rt_n, ks = tile / (nchunk * rt_n);
+  const int bz_n = g.D / BRK_Z, by_n = g.H / BRK_Y, bx_n = g.W / BRK_X;
+  const long long nbrick = (g.V / ((long long)g.D * g.H * g.W)) * bz_n * by_n * bx_n;
+  const long long bpk = (nbrick + g.ksplit - 1) / g.ksplit;
+  const long long b_begin = ks * bpk;
+  const long long b_end = b_begin + bpk < nbrick ? b_begin + bpk : nbrick;
+  const long long HW = (long long)g.H * g.W;
+  const int row0 = rt * 32, c0 = ct * CK;
+  const bool do_bias = g.bias_part != nullptr && ct == 0;
+  const int t_begin = wave * 7, t_cnt = wave == 3 ? 6 : 7;
+
+  f32x4 acc[2][7][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < 7; ++t)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][t][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float bsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  V8<T> dr[D_PER], xr[X_PER];
+  auto brick_origin = [&](long long b, long long& nbase, int& z0, int& y0, int& x0) {
+    const int bx = (int)(b % bx_n);
+    long long q = b / bx_n;
+    const int by = (int)(q % by_n);
+    q /= by_n;
+    const int bz = (int)(q % bz_n);
+    const long long n = q / bz_n;
+    nbase = n * g.D * HW;
+    z0 = bz * BRK_Z;
+    y0 = by * BRK_Y;
+    x0 = bx * BRK_X;
+  };
+  auto load = [&](long long b) {
+    long long nbase;
+    int z0, y0, x0;
+    brick_origin(b, nbase, z0, y0, x0);
+#pragma unroll
+    for (int k = 0; k < D_PER; ++k) {
+      const int e = tid + k * 256, v = e >> 2, cg = e & 3;
+      const int z = z0 + (v >> 5), y = y0 + ((v >> 3) & 3), x = x0 + (v & 7);
+      dr[k].load(Dy + (nbase + z * HW + (long long)y * g.W + x) * g.lda + row0 + cg * 8);
+    }
+#pragma unroll
+    for (int k = 0; k < X_PER; ++k) {
+      const int e = tid + k * 256;
+      if (e < X_ITEMS) {
+        const int h = e >> 2, cg = e & 3;
+        const int hx = h % HLO_X, hy = (h / HLO_X) % HLO_Y, hz = h / (HLO_X * HLO_Y);
+        const int z = z0 - 1 + hz, y = y0 - 1 + hy, x = x0 - 1 + hx;
+        if ((unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W)
+          xr[k].load(X + (nbase + z * HW + (long long)y * g.W + x) * g.ldb + c0 + cg * 8);
+        else
+          xr[k].zero();
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int k = 0; k < D_PER; ++k) {
+      const int e = tid + k * 256;
+      dr[k].store(Dl + (e >> 2) * DP + (e & 3) * 8);
+      if (do_bias) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bsum[j] += dr[k].get(j);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < X_PER; ++k) {
+      const int e = tid + k * 256;
+      if (e < X_ITEMS) xr[k].store(Xl + (e >> 2) * XP + (e & 3) * 8);
+    }
+  };
+
+  const int g4 = lane >> 4, i16 = lane & 15, q = i16 >> 2, p4 = i16 & 3;
+  if (b_begin < b_end) {
+    load(b_begin);
+    store();
+  }
+  __syncthreads();
+  for (long long b = b_begin; b < b_end; ++b) {
+    const bool more = b + 1 < b_end;
+    if (more) load(b + 1);
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int kk = 0; kk < 128; kk += 32) {
+        bf16x8 af[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const bf16_t* base = (const bf16_t*)Dl + (kk + 8 * g4 + q) * DP + i * 16 + 4 * p4;
+          af[i] = tr_frag(base, base + 4 * DP);
+        }
+        // B rows: voxels v = kk + 8*g4 + q (+4) -> halo row of (v) shifted by the tap
+        const int v_lo = kk + 8 * g4 + q, v_hi = v_lo + 4;
+        const int hlo = ((v_lo >> 5) * HLO_Y + ((v_lo >> 3) & 3)) * HLO_X + (v_lo & 7);
+        const int hhi = ((v_hi >> 5) * HLO_Y + ((v_hi >> 3) & 3)) * HLO_X + (v_hi & 7);
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+          if (t < t_cnt) {
+            const int tap = t_begin + t;
+            const int kz = tap / 9, ky = (tap / 3) % 3, kx = tap % 3;
+            const int hoff = (kz * HLO_Y + ky) * HLO_X + kx;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const bf16_t* pl = (const bf16_t*)Xl + (hlo + hoff) * XP + j * 16 + 4 * p4;
+              const bf16_t* ph = (const bf16_t*)Xl + (hhi + hoff) * XP + j * 16 + 4 * p4;
+              const bf16x8 bfr = tr_frag(pl, ph);
+#pragma unroll
+              for (int i = 0; i < 2; ++i)
+                acc[i][t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][t][j], 0, 0, 0);
+            }
+          }
+        }
+      }
+    } else {
+      for (int kk = 0; kk < 128; kk += 4) {
+        const int v = kk + g4;
+        const int hv = ((v >> 5) * HLO_Y + ((v >> 3) & 3)) * HLO_X + (v & 7);
+        float af[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = (float)Dl[v * DP + i * 16 + i16];
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+          if (t < t_cnt) {
+            const int tap = t_begin + t;
+            const int kz = tap / 9, ky = (tap / 3) % 3, kx = tap % 3;
+            const int hoff = (kz * HLO_Y + ky) * HLO_X + kx;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const float bv = (float)Xl[(hv + hoff) * XP + j * 16 + i16];
+#pragma unroll
+              for (int i = 0; i < 2; ++i)
+                acc[i][t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bv, acc[i][t][j], 0, 0, 0);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (more) {
+      store();
+      __syncthreads();
+    }
+  }
+
+  // partial layout [ks][Ca][Ncols], col = tap*cin + ci
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < 7; ++t) {
+      if (t >= t_cnt) continue;
+      const int tap = t_begin + t;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = tap * cin + c0 + j * 16 + i16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = row0 + i * 16 + g4 * 4 + r;
+          g.part[((long long)ks * g.Ca + row) * g.Ncols + col] = acc[i][t][j][r];
+        }
+      }
+    }
+  if (do_bias) {
+    float* red = reinterpret_cast<float*>(lds);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[tid * 8 + j] = bsum[j];
+    __syncthreads();
+    if (tid < 32) {
+      const int cg = tid >> 3, j = tid & 7;
+      float sacc = 0.f;
+      for (int t = cg; t < 256; t += 4) sacc += red[t * 8 + j];
+      g.bias_part[(long long)ks * g.Ca + row0 + tid] = sacc;
     }
   }
 }
@@ -904,6 +1109,12 @@ int launch_gemm_mode(GemmArgs g, int mode, hipStream_t s) {
 template <typename T, int MODE>
 int launch_wgrad(WgradArgs g, hipStream_t s) {
   dim3 block(256);
+  if (MODE == MODE_CONV3 && g.brick) {
+    const int cin = 8 << g.cpg_shift;
+    dim3 grid((cin / CK) * (g.Ca / 32) * g.ksplit);
+    hipLaunchKernelGGL((wgrad_brick_kernel<T>), grid, block, 0, s, g);
+    return mmseg::check_launch("wgrad_brick");
+  }
   const int bn = knob("MMSEG_WGRAD_BN", 64);
   if (g.Ca % 64 == 0) {
     if (bn == 128) {
@@ -923,6 +1134,11 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
     }
   }
   return mmseg::check_launch("wgrad");
+}
+
+int wgrad_brick_ok(int Ca, int cpg_shift, int D, int H, int W, int lda, int ldb) {
+  return knob("MMSEG_WGRAD_BRICK", 1) && Ca % 32 == 0 && (8 << cpg_shift) % CK == 0 && D % BRK_Z == 0 &&
+         H % BRK_Y == 0 && W % BRK_X == 0 && lda % 8 == 0 && ldb % 8 == 0;
 }
 
 }  // namespace
@@ -984,10 +1200,18 @@ int mmseg_wgrad(const void* a, int lda, const void* b, int ldb, float* part, flo
                 int Ncols, int cpg_shift, long long V, int D, int H, int W, int ksplit, int dtype, void* stream) {
   MMSEG_REQUIRE(Ca % 8 == 0, "wgrad: rows (%d) must be a multiple of 8", Ca);
   MMSEG_REQUIRE(Ncols % 8 == 0, "wgrad: cols (%d) must be a multiple of 8", Ncols);
+  const int brick = mode == MODE_CONV3 && wgrad_brick_ok(Ca, cpg_shift, D, H, W, lda, ldb);
   long long vps = ((V + ksplit - 1) / ksplit + 63) / 64 * 64;
-  ksplit = (int)((V + vps - 1) / vps);
+  if (brick) {
+    const long long nbrick = V / 128;
+    if (ksplit > nbrick) ksplit = (int)nbrick;
+    const long long bpk = (nbrick + ksplit - 1) / ksplit;
+    ksplit = (int)((nbrick + bpk - 1) / bpk);
+  } else {
+    ksplit = (int)((V + vps - 1) / vps);
+  }
   WgradArgs g{a, lda, b, ldb, part, bias_part, Ca, Ncols, cpg_shift, V, D, H, W, ksplit, vps,
-              knob("MMSEG_WGRAD_SWIZZLE", 0)};
+              knob("MMSEG_WGRAD_SWIZZLE", 0), brick};
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16) {
     switch (mode) {
@@ -1010,6 +1234,15 @@ int mmseg_wgrad(const void* a, int lda, const void* b, int ldb, float* part, flo
 int mmseg_wgrad_splits(long long V, int ksplit) {
   long long vps = ((V + ksplit - 1) / ksplit + 63) / 64 * 64;
   return (int)((V + vps - 1) / vps);
+}
+
+// Same for the CONV3 brick path (splits the list of 4x4x8 bricks).
+int mmseg_wgrad_splits_conv3(long long V, int ksplit, int Ca, int cpg_shift, int D, int H, int W, int lda, int ldb) {
+  if (!wgrad_brick_ok(Ca, cpg_shift, D, H, W, lda, ldb)) return mmseg_wgrad_splits(V, ksplit);
+  const long long nbrick = V / 128;
+  if (ksplit > nbrick) ksplit = (int)nbrick;
+  const long long bpk = (nbrick + ksplit - 1) / ksplit;
+  return (int)((nbrick + bpk - 1) / bpk);
 }
 
 int mmseg_wgrad_reduce(const float* part, float* grad, const float* bias_part, float* bias_grad, int Ca, int Ncols,

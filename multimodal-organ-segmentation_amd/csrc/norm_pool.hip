@@ -19,7 +19,12 @@
 namespace {
 
 // ------------------------------------------------------------------ stats
-// partial sums of (x - K) and (x - K)^2 per (n, chunk, c); K = x[n, voxel 0, c]
+// Welford / Chan statistics: each thread keeps (n, mean, M2) for its 8
+// channels; lanes are merged in a fixed order inside the block and chunks in a
+// fixed order in the finalize (double).  A shifted-sums formulation is NOT
+// used: convolution outputs are far from stationary near the volume border, so
+// any single shift value can sit many sigmas from the channel mean and the
+// E[x^2]-E[x]^2 cancellation then costs the gradients ~1e-2 accuracy.
 template <typename T>
 __global__ void in_stats_partial(const T* __restrict__ x, int ld, long long V, int C, long long vpc,
                                  float* __restrict__ part) {
@@ -29,15 +34,13 @@ __global__ void in_stats_partial(const T* __restrict__ x, int ld, long long V, i
   const int tid = threadIdx.x;
   const int cg = tid % C8, vl = tid / C8;
   const T* xn = x + (long long)n * V * ld;
-  float s1[8], s2[8], K[8];
-  V8<T> k8;
-  k8.load(xn + cg * 8);
+  float mu[8], m2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    s1[j] = 0.f;
-    s2[j] = 0.f;
-    K[j] = k8.get(j);
+    mu[j] = 0.f;
+    m2[j] = 0.f;
   }
+  float cnt = 0.f;
   const long long v0 = (long long)chunk * vpc;
   long long v1 = v0 + vpc;
   if (v1 > V) v1 = V;
@@ -45,58 +48,86 @@ __global__ void in_stats_partial(const T* __restrict__ x, int ld, long long V, i
     for (long long v = v0 + vl; v < v1; v += lanes_v) {
       V8<T> a;
       a.load(xn + v * ld + cg * 8);
+      cnt += 1.f;
+      const float inv = 1.f / cnt;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float d = a.get(j) - K[j];
-        s1[j] += d;
-        s2[j] = fmaf(d, d, s2[j]);
+        const float xv = a.get(j);
+        const float d = xv - mu[j];
+        mu[j] = fmaf(d, inv, mu[j]);
+        m2[j] = fmaf(d, xv - mu[j], m2[j]);
       }
     }
   }
   __shared__ float red[2][256 * 8];
+  __shared__ float rcnt[256];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    red[0][tid * 8 + j] = s1[j];
-    red[1][tid * 8 + j] = s2[j];
+    red[0][tid * 8 + j] = mu[j];
+    red[1][tid * 8 + j] = m2[j];
   }
+  rcnt[tid] = (vl < lanes_v) ? cnt : 0.f;
   __syncthreads();
-  // one thread per (c) sums the voxel lanes in fixed order
+  // one thread per channel merges the voxel lanes in fixed order (Chan)
   for (int c = tid; c < C; c += 256) {
     const int g = c >> 3, j = c & 7;
-    float a = 0.f, b = 0.f;
+    float na = 0.f, ma = 0.f, sa = 0.f;
     for (int l = 0; l < lanes_v; ++l) {
-      a += red[0][(l * C8 + g) * 8 + j];
-      b += red[1][(l * C8 + g) * 8 + j];
+      const int t = l * C8 + g;
+      const float nb = rcnt[t];
+      if (nb == 0.f) continue;
+      const float mb = red[0][t * 8 + j], sb = red[1][t * 8 + j];
+      const float nn = na + nb;
+      const float delta = mb - ma;
+      ma = ma + delta * (nb / nn);
+      sa = sa + sb + delta * delta * (na * nb / nn);
+      na = nn;
     }
     float* p = part + (((long long)n * nchunk + chunk) * C + c) * 2;
-    p[0] = a;
-    p[1] = b;
+    p[0] = ma;
+    p[1] = sa;
   }
 }
 
-// one wave per (n, c): lanes stride over the chunk partials, double shuffle tree (fixed order)
+// one wave per (n, c): fixed-order Chan merge of the chunk partials in double
 template <typename T>
 __global__ void in_stats_finalize(const T* __restrict__ x, int ld, long long V, int N, int C, int nchunk,
-                                  const float* __restrict__ part, float eps, float* __restrict__ mean,
+                                  long long vpc, const float* __restrict__ part, float eps, float* __restrict__ mean,
                                   int mean_ld, float* __restrict__ rstd) {
   const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (idx >= N * C) return;
   const int n = idx / C, c = idx - n * C;
-  double a = 0.0, b = 0.0;
-  for (int k = lane; k < nchunk; k += 64) {
+  double na = 0.0, ma = 0.0, sa = 0.0;
+  for (int k = lane; k < nchunk; k += 64) {   // each lane: its chunks in order
     const float* p = part + (((long long)n * nchunk + k) * C + c) * 2;
-    a += p[0];
-    b += p[1];
+    const long long v0 = (long long)k * vpc;
+    const long long v1 = v0 + vpc < V ? v0 + vpc : V;
+    const double nb = (double)(v1 - v0);
+    if (nb <= 0) continue;
+    const double nn = na + nb, delta = (double)p[0] - ma;
+    ma += delta * (nb / nn);
+    sa += (double)p[1] + delta * delta * (na * nb / nn);
+    na = nn;
   }
-  a = wave_sum_d(a);
-  b = wave_sum_d(b);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {          // fixed butterfly: deterministic Chan merge across lanes
+    const double nb = __shfl_xor(na, o, 64), mb = __shfl_xor(ma, o, 64), sb = __shfl_xor(sa, o, 64);
+    const double nn = na + nb;
+    if (nn > 0) {
+      // order the pair by lane id so both partners compute the bitwise-same result
+      const bool lo = (lane & o) == 0;
+      const double n1 = lo ? na : nb, m1 = lo ? ma : mb, s1 = lo ? sa : sb;
+      const double n2 = lo ? nb : na, m2 = lo ? mb : ma, s2 = lo ? sb : sa;
+      const double delta = m2 - m1;
+      ma = m1 + delta * (n2 / nn);
+      sa = s1 + s2 + delta * delta * (n1 * n2 / nn);
+      na = nn;
+    }
+  }
   if (lane != 0) return;
-  const double K = to_f<T>(x[(long long)n * V * ld + c]);
-  const double m1 = a / (double)V;
-  double var = b / (double)V - m1 * m1;
-  if (var < 0) var = 0;
-  mean[(long long)n * mean_ld + c] = (float)(K + m1);
+  const double var = sa / (double)V;
+  mean[(long long)n * mean_ld + c] = (float)ma;
   if (rstd) rstd[idx] = (float)(1.0 / sqrt(var + (double)eps));
 }
 
@@ -545,11 +576,11 @@ int mmseg_instnorm_stats(const void* x, int ldx, int N, long long V, int C, floa
   if (dtype == MMSEG_BF16) {
     hipLaunchKernelGGL(in_stats_partial<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, V, C, vpc, ws);
     hipLaunchKernelGGL(in_stats_finalize<bf16_t>, dim3(ceil_div(N * C, 4)), dim3(256), 0, s, (const bf16_t*)x, ldx,
-                       V, N, C, nch, ws, eps, mean, mean_ld, rstd);
+                       V, N, C, nch, vpc, ws, eps, mean, mean_ld, rstd);
   } else {
     hipLaunchKernelGGL(in_stats_partial<float>, grid, dim3(256), 0, s, (const float*)x, ldx, V, C, vpc, ws);
     hipLaunchKernelGGL(in_stats_finalize<float>, dim3(ceil_div(N * C, 4)), dim3(256), 0, s, (const float*)x, ldx, V,
-                       N, C, nch, ws, eps, mean, mean_ld, rstd);
+                       N, C, nch, vpc, ws, eps, mean, mean_ld, rstd);
   }
   return mmseg::check_launch("instnorm_stats");
 }

@@ -1,1 +1,2 @@
 from .synthetic import SyntheticSegDataset, device_batches, phantom  # noqa: F401
+from .dataloader import get_dataloader, get_dataset  # noqa: F401

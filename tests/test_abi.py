@@ -44,3 +44,10 @@ def test_no_cpu_fallback():
     from mmseg_amd.engine.runtime import Runtime
     with pytest.raises(RuntimeError):
         Runtime(torch.device("cpu"), torch.float32)
+
+
+def test_value_returning_entry_points_do_not_raise():
+    L = _lib.lib()
+    assert L.mmseg_wgrad_splits(1 << 20, 64) >= 1
+    assert L.mmseg_wgrad_splits_conv3(2 * 96 ** 3, 512, 32, 2, 96, 96, 96, 32, 32) >= 1
+    assert L.mmseg_pack_desc_bytes() == 56

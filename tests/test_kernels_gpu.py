@@ -35,7 +35,7 @@ def _act(x, dtype):
     (8, 32, (2, 5, 6, 7)), (32, 32, (1, 8, 8, 8)), (64, 32, (2, 6, 6, 6)), (32, 64, (1, 6, 7, 5)),
     (128, 64, (2, 4, 4, 4)), (256, 128, (1, 3, 2, 2)), (16, 8, (2, 4, 5, 6)),
     # shapes taken by the LDS-halo brick kernel (D%4, H%4, W%8, Cin%32): BN=32 / BN=64 / ragged Ncols
-    (32, 32, (2, 4, 4, 8)), (64, 32, (1, 8, 4, 16)), (32, 64, (1, 4, 8, 8)), (64, 96, (2, 4, 4, 8)),
+    (32, 32, (2, 4, 4, 8)), (64, 32, (1, 8, 4, 16)), (32, 64, (1, 4, 8, 8)), (256, 64, (2, 4, 4, 8)),
     (128, 128, (1, 8, 8, 8))])
 def test_conv3_fwd_dgrad_wgrad(dev, dtype, cin, cout, shape):
     torch.manual_seed(cin + cout)
