@@ -51,6 +51,20 @@ def make_config(model, batch, dtype, out_channels=6, modalities=("CT", "PET")):
     }
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*pmc_traffic*.json,
+    made by tools/rocprof_families.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    if kernel not in d:
+        return None, os.path.relpath(files[-1], ROOT)
+    return d[kernel]["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(model_name, batch, size, out_channels, modalities, threads):
     """The oracle (torch-CPU fp32 restatement of the reference step) on the host cores:
     1 warm-up step on a 32^3 patch, then ONE timed full-size step (bounded sample)."""
@@ -162,8 +176,11 @@ def main():
         flops_per_launch = a["flops"] / a["launches"]
         achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
         peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
+        traffic, tsrc = pmc_traffic(name)
         roofline = {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": peak,
-                    "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                    "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                    "traffic": round(traffic) if traffic is not None else None, "traffic_unit": "B/launch",
+                    "traffic_source": tsrc,
                     "avg_launch_ms": round(avg_ms, 4), "launches_per_step": a["launches"] // max(args.timer_steps, 1),
                     "algorithmic_gflop_per_launch": round(flops_per_launch / 1e9, 3)}
     families = {k: {"ms_per_step": round(v["ms"] / args.timer_steps, 3),

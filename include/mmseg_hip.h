@@ -35,6 +35,8 @@ extern "C" {
 
 /* ------------------------------------------------------------- plumbing */
 const char* mmseg_last_error(void);
+/* Name of the main kernel the last conv/wgrad entry point launched on this thread (for the per-kernel timer). */
+const char* mmseg_last_kernel(void);
 int mmseg_abi_version(void);
 
 /* --------------------------------------------------------- GEMM family */

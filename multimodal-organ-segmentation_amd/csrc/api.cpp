@@ -7,6 +7,9 @@
 
 namespace mmseg {
 static thread_local char g_err[1024] = {0};
+static thread_local const char* g_kernel = "";
+
+void note_kernel(const char* name) { g_kernel = name; }
 
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -27,5 +30,6 @@ int check_launch(const char* what) {
 
 extern "C" {
 const char* mmseg_last_error(void) { return mmseg::g_err; }
+const char* mmseg_last_kernel(void) { return mmseg::g_kernel; }
 int mmseg_abi_version(void) { return 1; }
 }

@@ -1069,6 +1069,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
       g.D % BRK_Z == 0 && g.H % BRK_Y == 0 && g.W % BRK_X == 0 && g.lda % 8 == 0) {
     const int nb = (g.M / (g.D * g.H * g.W)) * (g.D / BRK_Z) * (g.H / BRK_Y) * (g.W / BRK_X);
     const int bn = (g.Ncols >= 64 && knob("MMSEG_BRICK_BN", 64) == 64) ? 64 : 32;
+    mmseg::note_kernel(bn == 64 ? "conv3_brick_kernel<BN64>" : "conv3_brick_kernel<BN32>");
     if (bn == 64) {
       hipLaunchKernelGGL((conv3_brick_kernel<T, 64>), dim3(nb * ceil_div(g.Ncols, 64)), block, 0, s, g);
     } else {
@@ -1078,10 +1079,16 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
   }
   if (!Cbig) {
     // BM=128, BN=32
+    static const char* nm[4] = {"conv_gemm_kernel<conv3,128x32>", "conv_gemm_kernel<point,128x32>",
+                                "conv_gemm_kernel<convT_fwd,128x32>", "conv_gemm_kernel<convT_dgrad,128x32>"};
+    mmseg::note_kernel(nm[MODE]);
     dim3 grid(ceil_div(g.M, 128) * ceil_div(g.Ncols, 32) * g.ksplit);
     hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, 4, 1, 2, 2>), grid, block, 0, s, g);
   } else {
     // BM=128, BN=64
+    static const char* nm[4] = {"conv_gemm_kernel<conv3,128x64>", "conv_gemm_kernel<point,128x64>",
+                                "conv_gemm_kernel<convT_fwd,128x64>", "conv_gemm_kernel<convT_dgrad,128x64>"};
+    mmseg::note_kernel(nm[MODE]);
     dim3 grid(ceil_div(g.M, 128) * ceil_div(g.Ncols, 64) * g.ksplit);
     hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, 2, 2, 4, 2>), grid, block, 0, s, g);
   }
@@ -1112,10 +1119,14 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
   if (MODE == MODE_CONV3 && g.brick) {
     const int cin = 8 << g.cpg_shift;
     dim3 grid((cin / CK) * (g.Ca / 32) * g.ksplit);
+    mmseg::note_kernel("wgrad_brick_kernel");
     hipLaunchKernelGGL((wgrad_brick_kernel<T>), grid, block, 0, s, g);
     return mmseg::check_launch("wgrad_brick");
   }
   const int bn = knob("MMSEG_WGRAD_BN", 64);
+  static const char* nm[4] = {"wgrad_kernel<conv3>", "wgrad_kernel<point>", "wgrad_kernel<convT_fwd>",
+                              "wgrad_kernel<convT_dgrad>"};
+  mmseg::note_kernel(nm[MODE]);
   if (g.Ca % 64 == 0) {
     if (bn == 128) {
       dim3 grid(ceil_div(g.Ncols, 128) * (g.Ca / 64) * g.ksplit);

@@ -26,6 +26,9 @@ enum MmsegDtype { MMSEG_F32 = 0, MMSEG_BF16 = 1 };
 namespace mmseg {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+// Record the main kernel an entry point launched (mmseg_last_kernel(); the
+// per-kernel timer names its regions with it, matching rocprofv3's names).
+void note_kernel(const char* name);
 }  // namespace mmseg
 
 #define MMSEG_REQUIRE(cond, ...)              \

@@ -30,9 +30,9 @@ IN_EPS = 1e-5
 TARGET_BLOCKS = 1024
 
 
-def _gemm_name(rt: Runtime, ncols: int, mode: str) -> str:
-    tile = "128x64" if ncols >= 64 else "128x32"
-    return f"conv_gemm[{'bf16' if rt.code else 'f32'},{mode},{tile}]"
+def _gemm_name(rt: Runtime, ncols: int, mode: str):
+    """Timer family = the kernel the library actually launched (same name as in rocprofv3 traces)."""
+    return lambda: f"{rt.lib.mmseg_last_kernel().decode()}[{'bf16' if rt.code else 'f32'}]"
 
 
 def _col_tile(n: int) -> int:
@@ -143,7 +143,7 @@ class Conv3:
         ks = L.mmseg_wgrad_splits_conv3(V, want, self.Co, self.cpg_shift, x.D, x.H, x.W, dy.ld, x.ld)
         part = self.rt.ws(ks * self.Co * ncols + ks * self.Co)
         bpart = part.data_ptr() + ks * self.Co * ncols * 4
-        with TIMER.region(f"wgrad[{'bf16' if code else 'f32'},conv3]", flops=2.0 * V * self.Co * 27 * self.Ci):
+        with TIMER.region(_gemm_name(self.rt, 0, "conv3"), flops=2.0 * V * self.Co * 27 * self.Ci):
             L.mmseg_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, ptr(part), bpart, MODE_CONV3, self.Co, ncols, self.cpg_shift, V,
                           x.D, x.H, x.W, ks, code, s)
         L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.conv.weight)), bpart,
@@ -200,7 +200,7 @@ class ConvT2:
         ncols = 8 * self.Co
         ks = L.mmseg_wgrad_splits(V, _wgrad_ksplit(self.Ci, ncols, V))
         part = self.rt.ws(max(ks * self.Ci * ncols, 256 * self.Co))
-        with TIMER.region(f"wgrad[{'bf16' if code else 'f32'},convT]", flops=2.0 * V * self.Ci * 8 * self.Co):
+        with TIMER.region(_gemm_name(self.rt, 0, "convT"), flops=2.0 * V * self.Ci * 8 * self.Co):
             L.mmseg_wgrad(x.ptr, x.ld, dy.ptr, dy.ld, ptr(part), None, MODE_CONVT_DGRAD, self.Ci, ncols, self.dshift,
                           V, x.D, x.H, x.W, ks, code, s)
         L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.up.weight)), None, None, self.Ci, ncols, ks, self.Co,

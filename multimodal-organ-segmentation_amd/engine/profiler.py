@@ -24,7 +24,8 @@ class KernelTimer:
         self.enabled = False
 
     @contextmanager
-    def region(self, name: str, flops: float = 0.0, nbytes: float = 0.0):
+    def region(self, name, flops: float = 0.0, nbytes: float = 0.0):
+        """`name` may be a callable evaluated after the launch (e.g. the kernel the library chose)."""
         if not self.enabled:
             yield
             return
@@ -33,7 +34,7 @@ class KernelTimer:
         s.record()
         yield
         e.record()
-        self.records.append((name, flops, nbytes, s, e))
+        self.records.append((name() if callable(name) else name, flops, nbytes, s, e))
 
     def summary(self):
         torch.cuda.synchronize()

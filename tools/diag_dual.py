@@ -37,7 +37,10 @@ def oracle_fwd(p, x, keep):
         f = block(p, f"encoders.{m}.init_conv.", x[:, m:m + 1], keep)
         fl = [f]
         for i in range(4):
-            f = block(p, f"encoders.{m}.blocks.{i}.conv.", F.max_pool3d(f, 2), keep)
+            pl = F.max_pool3d(f, 2)
+            pl.retain_grad()
+            keep[("pooled", m, i + 1)] = pl
+            f = block(p, f"encoders.{m}.blocks.{i}.conv.", pl, keep)
             fl.append(f)
         per.append(fl)
     fused = []
@@ -64,6 +67,25 @@ def oracle_fwd(p, x, keep):
     for j, skip in enumerate(reversed(fused[:-1])):
         y = O.up_block(p, f"decoder.{j}.", y, skip)
     return F.conv3d(y, p["out_conv.weight"], p["out_conv.bias"])
+
+
+def _gpu_dy(prog, m, l):
+    """reconstruct the engine's effective dy of level output (m, l) from its buffers (mean fusion)"""
+    dfused = prog.fused_out(l).to_ncdhw().double().cpu()
+    dy = dfused / prog.M if FUSION != "attention" else torch.zeros_like(dfused)
+    if FUSION == "attention":
+        w = prog.gate_w[l].double().cpu()
+        beta = prog.gate_beta[l].double().cpu()
+        C = dfused.shape[1]
+        dy = dfused * w[:, m].view(-1, 1, 1, 1, 1) + beta[:, m * C:(m + 1) * C].view(-1, C, 1, 1, 1)
+    if l < prog.L - 1:
+        dp = prog.pooled[m][l + 1].to_ncdhw().double().cpu()
+        N, C, Do, Ho, Wo = dp.shape
+        it = prog.idx[m][l + 1].view(N, Do, Ho, Wo, C).permute(0, 4, 1, 2, 3).long().cpu()
+        for t in range(8):
+            a, b, c = t >> 2, (t >> 1) & 1, t & 1
+            dy[:, :, a::2, b::2, c::2] += (it == t).double() * dp
+    return dy
 
 
 def main():
@@ -95,7 +117,14 @@ def main():
                 blk = prog.encs[mm][l]
                 x1, x2, y2 = keep[pre]
                 # after backward the engine holds g2 in x2's buffer and g1 in x1's buffer
-                print(f"  m{mm} L{l}: g2 {rel(blk.x2.to_ncdhw(), x2.grad):.2e}  g1 {rel(blk.x1.to_ncdhw(), x1.grad):.2e}"
+                extra = ""
+                if l >= 1:
+                    extra = f"  dp {rel(prog.pooled[mm][l].to_ncdhw(), keep[('pooled', mm, l)].grad):.2e}"
+                gdy = _gpu_dy(prog, mm, l)
+                diff = (gdy - y2.grad).abs()
+                nbad = int((diff > 1e-3 * y2.grad.abs().max()).sum())
+                extra += f"  dy {rel(gdy, y2.grad):.2e} (bad elems {nbad}/{diff.numel()})"
+                print(f"  m{mm} L{l}: g2 {rel(blk.x2.to_ncdhw(), x2.grad):.2e}  g1 {rel(blk.x1.to_ncdhw(), x1.grad):.2e}" + extra +
                       f"  dW2 {rel(m.backbone.get_parameter(pre + 'conv2.weight').grad, p[pre + 'conv2.weight'].grad):.2e}"
                       f"  dW1 {rel(m.backbone.get_parameter(pre + 'conv1.weight').grad, p[pre + 'conv1.weight'].grad):.2e}")
         tr.optimizer.step()

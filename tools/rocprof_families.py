@@ -1,0 +1,103 @@
+"""Summarise rocprofv3 CSV output by the engine's kernel families.
+
+    python tools/rocprof_families.py stats  <prof_kernel_stats.csv>  [steps]
+    python tools/rocprof_families.py traffic <fetch_counter_collection.csv> <write_counter_collection.csv> [out.json]
+
+`stats` prints per-family calls / average duration (the same family names the
+in-process timer reports through mmseg_last_kernel(), so bench.py's
+`roofline.avg_launch_ms` can be checked against the trace).
+
+`traffic` turns two separate PMC passes (FETCH_SIZE, WRITE_SIZE; one counter
+group per pass) into HBM bytes per launch per family, with the gfx950
+correction of MI355X_MICROARCH.md: FETCH_SIZE counts 128-B streaming requests
+at 64 B, so it is doubled; WRITE_SIZE is taken as is.  Both counters are in KB.
+"""
+from __future__ import annotations
+
+import csv
+import json
+import re
+import sys
+from collections import defaultdict
+
+_MODES = {"0": "conv3", "1": "point", "2": "convT_fwd", "3": "convT_dgrad"}
+
+
+def family(name: str) -> str:
+    """Map a (mangled or demangled) kernel name to the engine's family name."""
+    dt = "bf16" if ("DF16b" in name or "__bf16" in name) else "f32"
+    m = re.search(r"conv3_brick_kernelI(?:DF16b|f)Li(\d+)E", name)
+    if m:
+        return f"conv3_brick_kernel<BN{m.group(1)}>[{dt}]"
+    m = re.search(r"conv_gemm_kernelI(?:DF16b|f)Li(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d)E", name)
+    if m:
+        tile = "128x32" if (m.group(2), m.group(3)) == ("4", "1") else "128x64"
+        return f"conv_gemm_kernel<{_MODES[m.group(1)]},{tile}>[{dt}]"
+    if "wgrad_brick_kernel" in name:
+        return f"wgrad_brick_kernel[{dt}]"
+    m = re.search(r"wgrad_kernelI(?:DF16b|f)Li(\d)E", name)
+    if m:
+        return f"wgrad_kernel<{_MODES[m.group(1)]}>[{dt}]"
+    m = re.search(r"(?:_GLOBAL__N_1\d+|::)([A-Za-z_][A-Za-z0-9_]*?)(?:I|\(|E|$)", name)
+    return m.group(1) if m else name
+
+
+def stats(path: str, steps: int = 1):
+    agg = defaultdict(lambda: [0, 0.0])
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            a = agg[family(r["Name"])]
+            a[0] += int(r["Calls"])
+            a[1] += float(r["TotalDurationNs"])
+    tot = sum(v[1] for v in agg.values())
+    print(f"{'family':48s} {'calls':>7s} {'avg_us':>9s} {'ms/step':>8s} {'%':>6s}")
+    for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        print(f"{k:48s} {c:7d} {t / c / 1e3:9.1f} {t / steps / 1e6:8.3f} {100 * t / tot:6.2f}")
+
+
+def _counter_rows(path: str, counter: str):
+    """{dispatch_id: (family, value_bytes)} summed over the counter's instances."""
+    out = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r.get("Counter_Name") != counter:
+                continue
+            did = r.get("Dispatch_Id") or r.get("Correlation_Id")
+            fam = family(r["Kernel_Name"])
+            v = float(r["Counter_Value"]) * 1024.0  # KB -> bytes
+            if did in out:
+                out[did] = (fam, out[did][1] + v)
+            else:
+                out[did] = (fam, v)
+    return out
+
+
+def traffic(fetch_csv: str, write_csv: str):
+    fetch = _counter_rows(fetch_csv, "FETCH_SIZE")
+    write = _counter_rows(write_csv, "WRITE_SIZE")
+    fam_f, fam_w = defaultdict(list), defaultdict(list)
+    for fam, v in fetch.values():
+        fam_f[fam].append(2.0 * v)  # gfx950: FETCH_SIZE reports half of a wide streaming read
+    for fam, v in write.values():
+        fam_w[fam].append(v)
+    res = {}
+    for fam in sorted(set(fam_f) | set(fam_w)):
+        f = fam_f.get(fam, [])
+        w = fam_w.get(fam, [])
+        fb = sum(f) / len(f) if f else 0.0
+        wb = sum(w) / len(w) if w else 0.0
+        res[fam] = {"launches": max(len(f), len(w)), "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
+                    "hbm_bytes_per_launch": fb + wb}
+    return res
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "stats":
+        stats(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 1)
+    elif sys.argv[1] == "traffic":
+        r = traffic(sys.argv[2], sys.argv[3])
+        js = json.dumps(r, indent=1)
+        if len(sys.argv) > 4:
+            with open(sys.argv[4], "w") as f:
+                f.write(js + "\n")
+        print(js)
