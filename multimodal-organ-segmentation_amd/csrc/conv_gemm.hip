@@ -396,6 +396,212 @@ __global__ __launch_bounds__(256) void conv3_brick_kernel(GemmArgs g) {
     }
 }
 
+// ------------------------------------------------- brick conv v2 (3^3)
+// Same algorithm as conv3_brick_kernel with a 2x larger per-wave tile and
+// bank-conflict-free LDS images:
+//   * block = (4*ZW) x 8 x 8 output voxels x BN columns; wave w owns z-slices
+//     [w*ZW, (w+1)*ZW) = 4*ZW row tiles of 16 voxels (two 8-voxel x-rows each),
+//     so one B fragment feeds 4*ZW MFMAs and one A fragment feeds BN/16;
+//   * halo image: 32 channels of a voxel = 4 consecutive 16-B quads, y-rows
+//     padded to 42 quads.  A ds_read_b128 lane group then touches 16 distinct
+//     bank quads for every tap shift (checked exhaustively on the host for
+//     the lane groups of MI355X_MICROARCH.md §LDS);
+//   * weight image: rows of 4 quads, quad index XOR-swizzled by bit 3 of the
+//     column, which makes the 16-lane groups conflict-free as well;
+//   * epilogue staged through LDS so every lane stores 16-B vectors.
+constexpr int B2_Y = 8, B2_X = 8;
+constexpr int H2_Y = B2_Y + 2, H2_X = B2_X + 2;
+
+template <typename T>
+struct Brick2Layout {
+  static constexpr int QV = 2 * (int)sizeof(T);      // 16-B quads per voxel (32 channels): 4 bf16, 8 f32
+  static constexpr int QG = QV / 4;                    // quads per 8-channel group
+  static constexpr int RY = H2_X * QV + 2;             // quads per halo y-row (padded)
+  static constexpr int RZ = H2_Y * RY;                 // quads per halo z-plane
+};
+
+__device__ __forceinline__ int w2_swz(int col) { return ((col >> 3) & 1) << 1; }
+
+template <typename T, int BN, int ZW>
+__global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kernel(GemmArgs g) {
+  using L = Brick2Layout<T>;
+  constexpr int BZ = 4 * ZW, HZ = BZ + 2;
+  constexpr int RM = 4 * ZW, RN = BN / 16;
+  constexpr int XQ = HZ * L::RZ;                      // halo quads
+  constexpr int WQ = 9 * BN * L::QV;                  // weight quads (one kz plane)
+  constexpr int EQ = (BZ * 64 * BN * (int)sizeof(T) + 15) / 16;   // epilogue tile quads
+  constexpr int LQ = (XQ + WQ) > EQ ? (XQ + WQ) : EQ;
+  __shared__ __attribute__((aligned(16))) float4 lds4[LQ];
+  T* Xl = reinterpret_cast<T*>(lds4);
+  T* Wl = reinterpret_cast<T*>(lds4 + XQ);
+  constexpr int EPQ = 16 / sizeof(T);                 // elements per quad
+  constexpr int HV = HZ * H2_Y * H2_X;
+  constexpr int X_ITEMS = HV * 4;                     // 8-channel groups per halo stage
+  constexpr int X_PER = (X_ITEMS + 255) / 256;
+  constexpr int W_ITEMS = 9 * BN * 4;
+  constexpr int W_PER = (W_ITEMS + 255) / 256;
+
+  const T* A = reinterpret_cast<const T*>(g.a);
+  const T* Bw = reinterpret_cast<const T*>(g.b);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int bz_n = g.D / BZ, by_n = g.H / B2_Y, bx_n = g.W / B2_X;
+  const int nbrick = (g.M / (g.D * g.H * g.W)) * bz_n * by_n * bx_n;
+  const int nt_n = (g.Ncols + BN - 1) / BN;
+  const int tile = g.swz ? xcd_swizzle(blockIdx.x, nbrick * nt_n) : (int)blockIdx.x;
+  int bidx = tile % nbrick;
+  const int nt = tile / nbrick;
+  const int bx = bidx % bx_n; bidx /= bx_n;
+  const int by = bidx % by_n; bidx /= by_n;
+  const int bz = bidx % bz_n;
+  const int n = bidx / bz_n;
+  const int z0 = bz * BZ, y0 = by * B2_Y, x0 = bx * B2_X;
+  const long long HW = (long long)g.H * g.W;
+  const long long nbase = (long long)n * g.D * HW;
+  const int n0 = nt * BN;
+  const int cin = 8 << g.cpg_shift;
+  const int nchunk = cin / CK;
+  const int nstage = nchunk * 3;
+
+  V8<T> xr[X_PER], wr[W_PER];
+  auto load_x = [&](int c) {
+#pragma unroll
+    for (int k = 0; k < X_PER; ++k) {
+      const int e = tid + k * 256;
+      if (e < X_ITEMS) {
+        const int h = e >> 2, cg = e & 3;
+        const int hx = h % H2_X, hy = (h / H2_X) % H2_Y, hz = h / (H2_X * H2_Y);
+        const int z = z0 - 1 + hz, y = y0 - 1 + hy, x = x0 - 1 + hx;
+        if ((unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W)
+          xr[k].load(A + (nbase + z * HW + (long long)y * g.W + x) * g.lda + c * CK + cg * 8);
+        else
+          xr[k].zero();
+      }
+    }
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int k = 0; k < X_PER; ++k) {
+      const int e = tid + k * 256;
+      if (e < X_ITEMS) {
+        const int h = e >> 2, cg = e & 3;
+        const int hx = h % H2_X, hy = (h / H2_X) % H2_Y, hz = h / (H2_X * H2_Y);
+        xr[k].store(Xl + (hz * L::RZ + hy * L::RY + hx * L::QV + cg * L::QG) * EPQ);
+      }
+    }
+  };
+  auto load_w = [&](int c, int kz) {
+#pragma unroll
+    for (int k = 0; k < W_PER; ++k) {
+      const int e = tid + k * 256;
+      if (e < W_ITEMS) {
+        const int cg = e & 3, q = e >> 2;
+        const int col = q % BN, t9 = q / BN;
+        const int kgi = (kz * 9 + t9) * (cin / 8) + c * 4 + cg;
+        wr[k].load(Bw + ((long long)kgi * g.Cpad + n0 + col) * 8);
+      }
+    }
+  };
+  auto store_w = [&]() {
+#pragma unroll
+    for (int k = 0; k < W_PER; ++k) {
+      const int e = tid + k * 256;
+      if (e < W_ITEMS) {
+        const int cg = e & 3, q = e >> 2;     // q = t9*BN + col
+        wr[k].store(Wl + (q * L::QV + (cg ^ w2_swz(q)) * L::QG) * EPQ);
+      }
+    }
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int r16 = lane & 15, kg = lane >> 4;
+  int aq[RM];   // halo quad of the lane's row for tap (0,0,0), group kg
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    const int zs = wave * ZW + (i >> 2), yr = 2 * (i & 3) + (r16 >> 3), xr_ = r16 & 7;
+    aq[i] = zs * L::RZ + yr * L::RY + xr_ * L::QV + kg * L::QG;
+  }
+  int bq[RN];
+#pragma unroll
+  for (int j = 0; j < RN; ++j) {
+    const int col = j * 16 + r16;
+    bq[j] = col * L::QV + (kg ^ w2_swz(col)) * L::QG;
+  }
+
+  load_x(0);
+  load_w(0, 0);
+  store_x();
+  store_w();
+  __syncthreads();
+  for (int st = 0; st < nstage; ++st) {
+    const int c = st / 3, kz = st - c * 3;
+    const int sn = st + 1;
+    const bool more = sn < nstage;
+    const int cn = sn / 3, kzn = sn - cn * 3;
+    if (more) {
+      load_w(cn, kzn);
+      if (kzn == 0) load_x(cn);
+    }
+#pragma unroll
+    for (int t9 = 0; t9 < 9; ++t9) {
+      const int ky = t9 / 3, kx = t9 - ky * 3;
+      const int hoff = kz * L::RZ + ky * L::RY + kx * L::QV;
+      V8<T> af[RM], bf[RN];
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bf[j].load(Wl + (t9 * BN * L::QV + bq[j]) * EPQ);
+#pragma unroll
+      for (int i = 0; i < RM; ++i) af[i].load(Xl + (aq[i] + hoff) * EPQ);
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) mfma_step<T>(acc[i][j], af[i], bf[j]);
+    }
+    __syncthreads();
+    if (more) {
+      store_w();
+      if (kzn == 0) store_x();
+      __syncthreads();
+    }
+  }
+
+  // epilogue: acc (+bias) -> LDS tile [BZ*64 voxels][BN] -> 16-B vector stores
+  T* El = reinterpret_cast<T*>(lds4);
+  constexpr int EP = BN + 8;   // padded pitch (elements)
+  static_assert(BZ * 64 * (BN + 8) * sizeof(T) <= LQ * 16, "epilogue tile must fit");
+#pragma unroll
+  for (int j = 0; j < RN; ++j) {
+    const int col = j * 16 + r16;
+    const float bv = (g.bias && n0 + col < g.Ncols) ? g.bias[n0 + col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int v = (wave * ZW + (i >> 2)) * 64 + (2 * (i & 3)) * 8 + kg * 4 + r;   // voxel in brick (z,y,x)
+        El[v * EP + col] = from_f<T>(acc[i][j][r] + bv);
+      }
+  }
+  __syncthreads();
+  T* O = reinterpret_cast<T*>(g.out);
+  constexpr int CG = BN / 8;                  // 8-column groups per voxel
+  constexpr int O_ITEMS = BZ * 64 * CG;
+#pragma unroll
+  for (int k = 0; k < O_ITEMS / 256; ++k) {
+    const int e = tid + k * 256;
+    const int v = e / CG, cg = e % CG;
+    const int col = n0 + cg * 8;
+    if (col < g.Ncols) {
+      const int z = z0 + (v >> 6), y = y0 + ((v >> 3) & 7), x = x0 + (v & 7);
+      V8<T> o;
+      o.load(El + v * EP + cg * 8);
+      o.store(O + (nbase + z * HW + (long long)y * g.W + x) * g.ldo + col);
+    }
+  }
+}
+
 // Fixed-order split-K reduction for the forward GEMM: out = sum_k part[k] (+bias).
 template <typename T, int MODE>
 __global__ void gemm_splitk_reduce(GemmArgs g) {
@@ -1065,7 +1271,26 @@ template <typename T, int MODE>
 int launch_gemm(GemmArgs g, hipStream_t s) {
   const int Cbig = g.Ncols >= 64;
   dim3 block(256);
-  if (MODE == MODE_CONV3 && g.ksplit == 1 && knob("MMSEG_BRICK", 1) && (8 << g.cpg_shift) % CK == 0 &&
+  const int brick = knob("MMSEG_BRICK", 2);
+  if (MODE == MODE_CONV3 && g.ksplit == 1 && brick == 2 && (8 << g.cpg_shift) % CK == 0 && g.D % 4 == 0 &&
+      g.H % B2_Y == 0 && g.W % B2_X == 0 && g.lda % 8 == 0 && g.ldo % 8 == 0 && g.Ncols % 32 == 0) {
+    const int nb1 = (g.M / (g.D * g.H * g.W)) * (g.D / 4) * (g.H / B2_Y) * (g.W / B2_X);
+    const int min_blocks = knob("MMSEG_BRICK2_MINBLK", 512);
+    if (g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
+      mmseg::note_kernel("conv3_brick2_kernel<BN64,ZW1>");
+      hipLaunchKernelGGL((conv3_brick2_kernel<T, 64, 1>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
+    } else if (sizeof(T) == 2 && g.D % 8 == 0 && knob("MMSEG_BRICK2_ZW", 1) == 2) {
+      if constexpr (sizeof(T) == 2) {
+        mmseg::note_kernel("conv3_brick2_kernel<BN32,ZW2>");
+        hipLaunchKernelGGL((conv3_brick2_kernel<T, 32, 2>), dim3(nb1 / 2 * (g.Ncols / 32)), block, 0, s, g);
+      }
+    } else {
+      mmseg::note_kernel("conv3_brick2_kernel<BN32,ZW1>");
+      hipLaunchKernelGGL((conv3_brick2_kernel<T, 32, 1>), dim3(nb1 * (g.Ncols / 32)), block, 0, s, g);
+    }
+    return mmseg::check_launch("conv3_brick2");
+  }
+  if (MODE == MODE_CONV3 && g.ksplit == 1 && brick == 1 && (8 << g.cpg_shift) % CK == 0 &&
       g.D % BRK_Z == 0 && g.H % BRK_Y == 0 && g.W % BRK_X == 0 && g.lda % 8 == 0) {
     const int nb = (g.M / (g.D * g.H * g.W)) * (g.D / BRK_Z) * (g.H / BRK_Y) * (g.W / BRK_X);
     const int bn = (g.Ncols >= 64 && knob("MMSEG_BRICK_BN", 64) == 64) ? 64 : 32;
