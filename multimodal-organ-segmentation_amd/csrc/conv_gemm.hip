@@ -1079,25 +1079,37 @@ struct WReduceArgs {
   int accumulate;
 };
 
+// 256 threads = 64 consecutive partial-layout elements x 4 split slices: slice
+// s sums splits k = s, s+4, ... (coalesced 256-B loads, 4x the loads in
+// flight of one thread per element), then the 4 slice sums are added in order.
 __global__ void wgrad_reduce_kernel(WReduceArgs g, int mode) {
-  long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const long long idx = (long long)blockIdx.x * 64 + lane;
   const long long total = (long long)g.Ca * g.Ncols;     // enumerate the partial layout: coalesced reads
-  if (g.bias_part && idx >= total && idx < total + g.Ca) {
+  const long long nout = total + (g.bias_part ? g.Ca : 0);
+  float v = 0.f;
+  if (idx < total) {
+    const float* p = g.part + idx;
+#pragma unroll 4
+    for (int k = sl; k < g.ksplit; k += 4) v += p[(long long)k * total];
+  } else if (idx < nout) {
     const int row = (int)(idx - total);
-    float v = 0.f;
-    for (int k = 0; k < g.ksplit; ++k) v += g.bias_part[(long long)k * g.Ca + row];
+    for (int k = sl; k < g.ksplit; k += 4) v += g.bias_part[(long long)k * g.Ca + row];
+  }
+  red[sl][lane] = v;
+  __syncthreads();
+  if (sl != 0 || idx >= nout) return;
+  v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+  if (idx >= total) {
+    const int row = (int)(idx - total);
     g.bias_grad[row] = g.accumulate ? g.bias_grad[row] + v : v;
     return;
   }
-  if (idx >= total) return;
   const int row = (int)(idx / g.Ncols);
   const int col = (int)(idx - (long long)row * g.Ncols);
   const int t = col / g.cpad, c = col - t * g.cpad;
   if (c >= g.creal || t >= g.ntap) return;
-  float v = 0.f;
-  const long long stride = total;
-  const float* p = g.part + idx;
-  for (int k = 0; k < g.ksplit; ++k) v += p[k * stride];
   // torch layout [row][c_real][tap]
   const long long dst = ((long long)row * g.creal + c) * g.ntap + t;
   if (g.accumulate) g.grad[dst] += v;
@@ -1485,7 +1497,7 @@ int mmseg_wgrad_reduce(const float* part, float* grad, const float* bias_part, f
                        int ksplit, int cpad, int creal, int ntap, int accumulate, void* stream) {
   WReduceArgs g{part, grad, bias_part, bias_grad, Ca, Ncols, ksplit, cpad, creal, ntap, accumulate};
   long long total = (long long)Ca * Ncols + (bias_part ? Ca : 0);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, g, 0);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(total, 64)), dim3(256), 0, (hipStream_t)stream, g, 0);
   return mmseg::check_launch("wgrad_reduce");
 }
 

@@ -164,15 +164,21 @@ __global__ void head_wgrad_partial(const T* __restrict__ x, int ldx, const float
   }
 }
 
+// one wave per output (C*Cin weights + C biases): lanes stride over the block
+// partials, fixed shuffle tree -> deterministic, 64 loads in flight per output
 __global__ void head_wgrad_reduce(const float* __restrict__ part, int nblk, int C, int Cin, float* __restrict__ gW,
                                   float* __restrict__ gb, int accumulate) {
   const int npairs = C * Cin + C;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (p >= npairs) return;
   float a = 0.f;
-  for (int b = 0; b < nblk; ++b) a += part[(long long)b * npairs + p];
-  float* dst = p < C * Cin ? gW + p : gb + (p - C * Cin);
-  *dst = accumulate ? *dst + a : a;
+  for (int b = lane; b < nblk; b += 64) a += part[(long long)b * npairs + p];
+  a = wave_sum(a);
+  if (lane == 0) {
+    float* dst = p < C * Cin ? gW + p : gb + (p - C * Cin);
+    *dst = accumulate ? *dst + a : a;
+  }
 }
 
 // ----------------------------------------------------------------- losses
@@ -253,55 +259,59 @@ __global__ void loss_stats_kernel(const float* __restrict__ logits, const LT* __
 }
 
 // one block: loss scalar + per-(n,c) dp coefficients (dp = a*t + b) + ce scale
+// 256 threads.  Phase 1: wave w sums quantity (n, q) over the chunks (lanes
+// stride the chunks, fixed fp64 shuffle tree).  Phase 2: thread e = (n, c)
+// forms the region term and its gradient coefficients.  Phase 3: thread 0
+// adds the N*C region terms and the CE sums in index order.
 __global__ void loss_finalize_kernel(const float* __restrict__ part, int N, int C, int nchunk, LossCfg cfg,
                                      float* __restrict__ loss_out, float* __restrict__ coef) {
-  __shared__ double acc_loss[256];
+  extern __shared__ double S[];           // [N*nv] sums, then [N*C] region terms
   const int nv = 3 * C + 2;
-  double region = 0.0;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int pr = wave; pr < N * nv; pr += 4) {
+    const int n = pr / nv, q = pr - n * nv;
+    double a = 0.0;
+    for (int k = lane; k < nchunk; k += 64) a += part[((long long)n * nchunk + k) * nv + q];
+    a = wave_sum_d(a);
+    if (lane == 0) S[pr] = a;
+  }
+  __syncthreads();
+  double* R = S + N * nv;
   const int c0 = (cfg.type == 0 && !cfg.include_bg) ? 1 : 0;
   const double nterms = (double)N * (C - c0);
   for (int e = threadIdx.x; e < N * C; e += blockDim.x) {
     const int n = e / C, c = e - n * C;
-    double P = 0, I = 0, T = 0;
-    for (int k = 0; k < nchunk; ++k) {
-      const float* p = part + ((long long)n * nchunk + k) * nv;
-      P += p[c];
-      I += p[C + c];
-      T += p[2 * C + c];
-    }
-    double a = 0.0, b = 0.0;
+    const double P = S[n * nv + c], I = S[n * nv + C + c], T = S[n * nv + 2 * C + c];
+    double a = 0.0, b = 0.0, region = 0.0;
     const double s = cfg.smooth;
     if (c >= c0) {
       if (cfg.type == 0) {
         const double U = P + T;
         const double dice = (2.0 * I + s) / (U + s);
-        region += 1.0 - dice;
+        region = 1.0 - dice;
         a = -(2.0 / (U + s)) / nterms;
         b = ((2.0 * I + s) / ((U + s) * (U + s))) / nterms;
       } else {
         const double fp = P - I, fn = T - I;
         const double num = I + s;
         const double den = I + cfg.alpha * fp + cfg.beta * fn + s;
-        region += 1.0 - num / den;
+        region = 1.0 - num / den;
         a = -((den - num * (1.0 - cfg.alpha - cfg.beta)) / (den * den)) / nterms;
         b = (num * cfg.alpha / (den * den)) / nterms;
       }
     }
+    R[e] = region;
     coef[e * 2 + 0] = (float)(a * cfg.dice_w);
     coef[e * 2 + 1] = (float)(b * cfg.dice_w);
   }
-  acc_loss[threadIdx.x] = region;
   __syncthreads();
   if (threadIdx.x == 0) {
-    double r = 0.0;
-    for (int t = 0; t < (int)blockDim.x; ++t) r += acc_loss[t];
-    double ce = 0.0, den = 0.0;
-    for (int n = 0; n < N; ++n)
-      for (int k = 0; k < nchunk; ++k) {
-        const float* p = part + ((long long)n * nchunk + k) * nv;
-        ce += p[3 * C];
-        den += p[3 * C + 1];
-      }
+    double r = 0.0, ce = 0.0, den = 0.0;
+    for (int e = 0; e < N * C; ++e) r += R[e];
+    for (int n = 0; n < N; ++n) {
+      ce += S[n * nv + 3 * C];
+      den += S[n * nv + 3 * C + 1];
+    }
     const double lv = cfg.dice_w * (r / nterms) + cfg.ce_w * (ce / den);
     loss_out[0] = (float)lv;
     coef[2 * N * C] = (float)(cfg.ce_w / den);   // CE gradient scale
@@ -514,7 +524,7 @@ int mmseg_head_bwd(const void* x, int ldx, int Cin, const float* W, const float*
                          (float*)dx, lddx);
   }
   if (mmseg::check_launch("head_bwd")) return 1;
-  hipLaunchKernelGGL(head_wgrad_reduce, dim3(ceil_div(C * Cin + C, 256)), dim3(256), 0, s, ws, (int)nblk, C, Cin, gW,
+  hipLaunchKernelGGL(head_wgrad_reduce, dim3(ceil_div(C * Cin + C, 4)), dim3(256), 0, s, ws, (int)nblk, C, Cin, gW,
                      gb, accumulate);
   return mmseg::check_launch("head_wgrad_reduce");
 }
@@ -544,7 +554,9 @@ int mmseg_loss_fwd(const float* logits, const void* labels, int label_bytes, int
     hipLaunchKernelGGL(loss_stats_kernel<uint8_t>, dim3(nch, N), dim3(256), 0, s, logits, (const uint8_t*)labels, C, V,
                        vpc, cfg, part);
   if (mmseg::check_launch("loss_stats")) return 1;
-  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, part, N, C, nch, cfg, loss_out, coef);
+  const size_t shm = sizeof(double) * ((size_t)N * (3 * C + 2) + (size_t)N * C);
+  MMSEG_REQUIRE(shm <= 64 * 1024, "loss: batch too large for the finalize pass (N=%d, C=%d)", N, C);
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), shm, s, part, N, C, nch, cfg, loss_out, coef);
   return mmseg::check_launch("loss_finalize");
 }
 

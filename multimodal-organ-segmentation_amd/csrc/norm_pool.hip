@@ -25,15 +25,20 @@ namespace {
 // used: convolution outputs are far from stationary near the volume border, so
 // any single shift value can sit many sigmas from the channel mean and the
 // E[x^2]-E[x]^2 cancellation then costs the gradients ~1e-2 accuracy.
+// Block = (256 / C8) voxel lanes x C8 channel groups; a thread owns 8 channels
+// of one sample and walks voxels v0+vl, v0+vl+lanes_v, ... of its chunk,
+// issuing UNR independent 16-B loads before consuming them (the HBM latency is
+// hidden by loads in flight, not by occupancy alone).
+constexpr int UNR = 4;
+
 template <typename T>
-__global__ void in_stats_partial(const T* __restrict__ x, int ld, long long V, int C, long long vpc,
-                                 float* __restrict__ part) {
+__global__ void in_stats_partial(const T* __restrict__ x, int ld, int V, int C, int vpc, float* __restrict__ part) {
   const int n = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
   const int C8 = C >> 3;
   const int lanes_v = 256 / C8;
   const int tid = threadIdx.x;
   const int cg = tid % C8, vl = tid / C8;
-  const T* xn = x + (long long)n * V * ld;
+  const T* xn = x + (long long)n * V * ld + cg * 8;
   float mu[8], m2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -41,22 +46,32 @@ __global__ void in_stats_partial(const T* __restrict__ x, int ld, long long V, i
     m2[j] = 0.f;
   }
   float cnt = 0.f;
-  const long long v0 = (long long)chunk * vpc;
-  long long v1 = v0 + vpc;
-  if (v1 > V) v1 = V;
-  if (vl < lanes_v) {
-    for (long long v = v0 + vl; v < v1; v += lanes_v) {
-      V8<T> a;
-      a.load(xn + v * ld + cg * 8);
-      cnt += 1.f;
-      const float inv = 1.f / cnt;
+  const int v0 = chunk * vpc;
+  const int v1 = v0 + vpc < V ? v0 + vpc : V;
+  auto upd = [&](const V8<T>& a) {
+    cnt += 1.f;
+    const float inv = 1.f / cnt;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float xv = a.get(j);
-        const float d = xv - mu[j];
-        mu[j] = fmaf(d, inv, mu[j]);
-        m2[j] = fmaf(d, xv - mu[j], m2[j]);
-      }
+    for (int j = 0; j < 8; ++j) {
+      const float xv = a.get(j);
+      const float d = xv - mu[j];
+      mu[j] = fmaf(d, inv, mu[j]);
+      m2[j] = fmaf(d, xv - mu[j], m2[j]);
+    }
+  };
+  if (vl < lanes_v) {
+    int v = v0 + vl;
+    for (; v + (UNR - 1) * lanes_v < v1; v += UNR * lanes_v) {
+      V8<T> a[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) a[u].load(xn + (long long)(v + u * lanes_v) * ld);
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) upd(a[u]);
+    }
+    for (; v < v1; v += lanes_v) {
+      V8<T> a;
+      a.load(xn + (long long)v * ld);
+      upd(a);
     }
   }
   __shared__ float red[2][256 * 8];
@@ -87,6 +102,13 @@ __global__ void in_stats_partial(const T* __restrict__ x, int ld, long long V, i
     p[0] = ma;
     p[1] = sa;
   }
+}
+
+__device__ __forceinline__ void load8f(const float* p, float* d) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w;
+  d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
 }
 
 // one wave per (n, c): fixed-order Chan merge of the chunk partials in double
@@ -131,27 +153,38 @@ __global__ void in_stats_finalize(const T* __restrict__ x, int ld, long long V, 
   if (rstd) rstd[idx] = (float)(1.0 / sqrt(var + (double)eps));
 }
 
-// y = relu((x - mean) * rstd); 8 channels per thread
+// y = relu((x - mean) * rstd); a thread owns 8 channels of one sample (their
+// mean / rstd stay in registers) and UNR voxels per step; grid (chunks, N).
 template <typename T>
-__global__ void in_relu_apply(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, long long V, int N,
-                              int C, const float* __restrict__ mean, const float* __restrict__ rstd) {
-  const int C8 = C >> 3;
-  const long long total = (long long)N * V * C8;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int cg = (int)(i % C8);
-    const long long nv = i / C8;
-    const int n = (int)(nv / V);
-    V8<T> a, o;
-    a.load(x + nv * ldx + cg * 8);
-    const float* mu = mean + n * C + cg * 8;
-    const float* rs = rstd + n * C + cg * 8;
+__global__ void in_relu_apply(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, int V, int C, int vpc,
+                              const float* __restrict__ mean, const float* __restrict__ rstd) {
+  const int n = blockIdx.y;
+  const int C8 = C >> 3, lanes_v = 256 / C8;
+  const int cg = threadIdx.x % C8, vl = threadIdx.x / C8;
+  if (vl >= lanes_v) return;
+  float mu[8], rs[8];
+  load8f(mean + n * C + cg * 8, mu);
+  load8f(rstd + n * C + cg * 8, rs);
+  const T* xn = x + (long long)n * V * ldx + cg * 8;
+  T* yn = y + (long long)n * V * ldy + cg * 8;
+  const int v0 = blockIdx.x * vpc;
+  const int v1 = v0 + vpc < V ? v0 + vpc : V;
+  for (int vb = v0 + vl; vb < v1; vb += UNR * lanes_v) {
+    V8<T> a[UNR];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float h = (a.get(j) - mu[j]) * rs[j];
-      o.set(j, h > 0.f ? h : 0.f);
+    for (int u = 0; u < UNR; ++u)
+      if (vb + u * lanes_v < v1) a[u].load(xn + (long long)(vb + u * lanes_v) * ldx);
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      if (vb + u * lanes_v >= v1) break;
+      V8<T> o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float h = (a[u].get(j) - mu[j]) * rs[j];
+        o.set(j, h > 0.f ? h : 0.f);
+      }
+      o.store(yn + (long long)(vb + u * lanes_v) * ldy);
     }
-    o.store(y + nv * ldy + cg * 8);
   }
 }
 
@@ -220,48 +253,77 @@ struct DySrc {
   const uint8_t* pool_idx;  // [N][Vo][C]
 };
 
+// Per-thread view of a DySrc for one sample and one 8-channel group: the
+// scale, beta and base pointers are resolved once, the per-voxel work is the
+// loads and the pool-window test.
 template <typename T>
-__device__ __forceinline__ void gather_dy(const DySrc& s, long long n, long long v, long long nv, int cg, int C, int D,
-                                          int H, int W, float* dy) {
+struct DyCtx {
+  const T* p1;
+  int ld1;
+  float sc;
+  float beta[8];
+  bool has_beta;
+  const T* pdy;
+  int pool_ld;
+  const uint8_t* pidx;
+  int C, H, W, Ho, Wo, HWo;
+
+  __device__ __forceinline__ DyCtx(const DySrc& s, int n, int V, int cg, int C_, int D, int H_, int W_) {
+    C = C_;
+    H = H_;
+    W = W_;
+    p1 = s.p1 ? reinterpret_cast<const T*>(s.p1) + (long long)n * V * s.ld1 + cg * 8 : nullptr;
+    ld1 = s.ld1;
+    sc = s.scale1 * (s.alpha1 ? s.alpha1[n * s.alpha_stride] : 1.f);
+    has_beta = s.beta != nullptr;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) dy[j] = 0.f;
-  if (s.p1) {
-    V8<T> a;
-    a.load(reinterpret_cast<const T*>(s.p1) + nv * s.ld1 + cg * 8);
-    float sc = s.scale1;
-    if (s.alpha1) sc *= s.alpha1[n * s.alpha_stride];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dy[j] = a.get(j) * sc;
+    for (int j = 0; j < 8; ++j) beta[j] = has_beta ? s.beta[n * s.beta_stride + cg * 8 + j] : 0.f;
+    Ho = H >> 1;
+    Wo = W >> 1;
+    HWo = Ho * Wo;
+    const long long Vo = (long long)(D >> 1) * HWo;
+    pdy = s.pool_dy ? reinterpret_cast<const T*>(s.pool_dy) + (long long)n * Vo * s.pool_ld + cg * 8 : nullptr;
+    pool_ld = s.pool_ld;
+    pidx = s.pool_dy ? s.pool_idx + (long long)n * Vo * C + cg * 8 : nullptr;
   }
-  if (s.beta) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dy[j] += s.beta[n * s.beta_stride + cg * 8 + j];
-  }
-  if (s.pool_dy) {
-    const int x = (int)(v % W);
-    long long q = v / W;
-    const int y = (int)(q % H);
-    const int z = (int)(q / H);
-    const int Ho = H >> 1, Wo = W >> 1, Do = D >> 1;
-    const long long vo = (n * Do + (z >> 1)) * (long long)Ho * Wo + (long long)(y >> 1) * Wo + (x >> 1);
-    const uint8_t sub = (uint8_t)(((z & 1) << 2) | ((y & 1) << 1) | (x & 1));
-    V8<T> pd;
-    pd.load(reinterpret_cast<const T*>(s.pool_dy) + vo * s.pool_ld + cg * 8);
-    const uint2 packed = *reinterpret_cast<const uint2*>(s.pool_idx + vo * C + cg * 8);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t w = j < 4 ? packed.x : packed.y;
-      const uint8_t id = (uint8_t)((w >> ((j & 3) * 8)) & 0xff);
-      if (id == sub) dy[j] += pd.get(j);
+
+  // raw loads for voxel v (issued early), then combine
+  struct Raw {
+    V8<T> a, pd;
+    uint2 id;
+    uint8_t sub;
+  };
+  __device__ __forceinline__ void load(int v, Raw& r) const {
+    if (p1) r.a.load(p1 + (long long)v * ld1);
+    if (pdy) {
+      const int x = v % W;
+      const int q = v / W;
+      const int y = q % H, z = q / H;
+      const int vo = (z >> 1) * HWo + (y >> 1) * Wo + (x >> 1);
+      r.sub = (uint8_t)(((z & 1) << 2) | ((y & 1) << 1) | (x & 1));
+      r.pd.load(pdy + (long long)vo * pool_ld);
+      r.id = *reinterpret_cast<const uint2*>(pidx + (long long)vo * C);
     }
   }
-}
+  __device__ __forceinline__ void combine(const Raw& r, float* dy) const {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dy[j] = (p1 ? r.a.get(j) * sc : 0.f) + beta[j];
+    if (pdy) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t w = j < 4 ? r.id.x : r.id.y;
+        const uint8_t id = (uint8_t)((w >> ((j & 3) * 8)) & 0xff);
+        if (id == r.sub) dy[j] += r.pd.get(j);
+      }
+    }
+  }
+};
 
 // partial sums of g and g*xhat, g = dy * [xhat > 0]
 template <typename T>
 __global__ void in_bwd_partial(const T* __restrict__ x, int ldx, const float* __restrict__ mean,
-                               const float* __restrict__ rstd, DySrc s, long long V, int C, int D, int H, int W,
-                               long long vpc, float* __restrict__ part) {
+                               const float* __restrict__ rstd, DySrc s, int V, int C, int D, int H, int W, int vpc,
+                               float* __restrict__ part) {
   const int n = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
   const int C8 = C >> 3;
   const int lanes_v = 256 / C8;
@@ -272,25 +334,35 @@ __global__ void in_bwd_partial(const T* __restrict__ x, int ldx, const float* __
   for (int j = 0; j < 8; ++j) {
     sg[j] = 0.f;
     sgx[j] = 0.f;
-    mu[j] = mean[n * C + cg * 8 + j];
-    rs[j] = rstd[n * C + cg * 8 + j];
   }
-  const long long v0 = (long long)chunk * vpc;
-  long long v1 = v0 + vpc;
-  if (v1 > V) v1 = V;
+  load8f(mean + n * C + cg * 8, mu);
+  load8f(rstd + n * C + cg * 8, rs);
+  const DyCtx<T> dc(s, n, V, cg, C, D, H, W);
+  const T* xn = x + (long long)n * V * ldx + cg * 8;
+  const int v0 = chunk * vpc;
+  const int v1 = v0 + vpc < V ? v0 + vpc : V;
   if (vl < lanes_v) {
-    for (long long v = v0 + vl; v < v1; v += lanes_v) {
-      const long long nv = (long long)n * V + v;
-      V8<T> a;
-      a.load(x + nv * ldx + cg * 8);
-      float dy[8];
-      gather_dy<T>(s, n, v, nv, cg, C, D, H, W, dy);
+    for (int vb = v0 + vl; vb < v1; vb += UNR * lanes_v) {
+      V8<T> a[UNR];
+      typename DyCtx<T>::Raw r[UNR];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float h = (a.get(j) - mu[j]) * rs[j];
-        const float g = h > 0.f ? dy[j] : 0.f;
-        sg[j] += g;
-        sgx[j] = fmaf(g, h, sgx[j]);
+      for (int u = 0; u < UNR; ++u)
+        if (vb + u * lanes_v < v1) {
+          a[u].load(xn + (long long)(vb + u * lanes_v) * ldx);
+          dc.load(vb + u * lanes_v, r[u]);
+        }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        if (vb + u * lanes_v >= v1) break;
+        float dy[8];
+        dc.combine(r[u], dy);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float h = (a[u].get(j) - mu[j]) * rs[j];
+          const float g = h > 0.f ? dy[j] : 0.f;
+          sg[j] += g;
+          sgx[j] = fmaf(g, h, sgx[j]);
+        }
       }
     }
   }
@@ -334,32 +406,56 @@ __global__ void in_bwd_finalize(const float* __restrict__ part, int N, int C, in
   }
 }
 
-// dx = rstd * (g - mean(g) - xhat * mean(g * xhat))
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)); same thread layout as the apply kernels
 template <typename T>
 __global__ void in_bwd_apply(const T* __restrict__ x, int ldx, const float* __restrict__ mean,
                              const float* __restrict__ rstd, DySrc s, const float* __restrict__ coef, T* __restrict__ dx,
-                             int lddx, long long V, int N, int C, int D, int H, int W) {
-  const int C8 = C >> 3;
-  const long long total = (long long)N * V * C8;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int cg = (int)(i % C8);
-    const long long nv = i / C8;
-    const long long n = nv / V;
-    const long long v = nv - n * V;
-    V8<T> a, o;
-    a.load(x + nv * ldx + cg * 8);
-    float dy[8];
-    gather_dy<T>(s, n, v, nv, cg, C, D, H, W, dy);
+                             int lddx, int V, int C, int D, int H, int W, int vpc) {
+  const int n = blockIdx.y;
+  const int C8 = C >> 3, lanes_v = 256 / C8;
+  const int cg = threadIdx.x % C8, vl = threadIdx.x / C8;
+  if (vl >= lanes_v) return;
+  float mu[8], rs[8], ca[8], cb[8];
+  load8f(mean + n * C + cg * 8, mu);
+  load8f(rstd + n * C + cg * 8, rs);
+  {
+    float t[16];
+    load8f(coef + (n * C + cg * 8) * 2, t);
+    load8f(coef + (n * C + cg * 8) * 2 + 8, t + 8);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int nc = (int)n * C + cg * 8 + j;
-      const float rs = rstd[nc];
-      const float h = (a.get(j) - mean[nc]) * rs;
-      const float g = h > 0.f ? dy[j] : 0.f;
-      o.set(j, rs * (g - coef[nc * 2] - h * coef[nc * 2 + 1]));
+      ca[j] = t[2 * j];
+      cb[j] = t[2 * j + 1];
     }
-    o.store(dx + nv * lddx + cg * 8);
+  }
+  const DyCtx<T> dc(s, n, V, cg, C, D, H, W);
+  const T* xn = x + (long long)n * V * ldx + cg * 8;
+  T* dxn = dx + (long long)n * V * lddx + cg * 8;
+  const int v0 = blockIdx.x * vpc;
+  const int v1 = v0 + vpc < V ? v0 + vpc : V;
+  for (int vb = v0 + vl; vb < v1; vb += UNR * lanes_v) {
+    V8<T> a[UNR];
+    typename DyCtx<T>::Raw r[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+      if (vb + u * lanes_v < v1) {
+        a[u].load(xn + (long long)(vb + u * lanes_v) * ldx);
+        dc.load(vb + u * lanes_v, r[u]);
+      }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      if (vb + u * lanes_v >= v1) break;
+      float dy[8];
+      dc.combine(r[u], dy);
+      V8<T> o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float h = (a[u].get(j) - mu[j]) * rs[j];
+        const float g = h > 0.f ? dy[j] : 0.f;
+        o.set(j, rs[j] * (g - ca[j] - h * cb[j]));
+      }
+      o.store(dxn + (long long)(vb + u * lanes_v) * lddx);
+    }
   }
 }
 
@@ -544,13 +640,23 @@ int grid_for(long long total) {
 }
 
 int chunks_for(long long V, int C, long long* vpc) {
-  // ~ (4096 x C8 lanes) voxels per chunk, at most 256 chunks
+  // reduction passes: ~16 voxels per thread (lanes_v = 256 / C8 voxel lanes), at most 1024 chunks
   const int lanes_v = 256 / (C >> 3);
-  long long want = (long long)lanes_v * 32;
+  long long want = (long long)lanes_v * 16;
   long long nch = (V + want - 1) / want;
-  if (nch > 256) nch = 256;
+  if (nch > 1024) nch = 1024;
   if (nch < 1) nch = 1;
   *vpc = (V + nch - 1) / nch;
+  return (int)((V + *vpc - 1) / *vpc);
+}
+
+int apply_chunks(long long V, int C, int* vpc) {
+  // elementwise passes: 2 x UNR voxels per thread
+  const int lanes_v = 256 / (C >> 3);
+  long long want = (long long)lanes_v * 2 * UNR;
+  long long nch = (V + want - 1) / want;
+  if (nch < 1) nch = 1;
+  *vpc = (int)((V + nch - 1) / nch);
   return (int)((V + *vpc - 1) / *vpc);
 }
 
@@ -569,16 +675,18 @@ long long mmseg_instnorm_ws_floats(int N, long long V, int C) {
 int mmseg_instnorm_stats(const void* x, int ldx, int N, long long V, int C, float eps, float* mean, int mean_ld,
                          float* rstd, float* ws, int dtype, void* stream) {
   MMSEG_REQUIRE(C % 8 == 0 && C <= 2048, "instnorm: C=%d must be a multiple of 8", C);
+  MMSEG_REQUIRE(V * ldx < (1LL << 31), "instnorm: per-sample extent must fit int32");
   long long vpc;
   const int nch = chunks_for(V, C, &vpc);
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(nch, N);
   if (dtype == MMSEG_BF16) {
-    hipLaunchKernelGGL(in_stats_partial<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, V, C, vpc, ws);
+    hipLaunchKernelGGL(in_stats_partial<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, (int)V, C, (int)vpc,
+                       ws);
     hipLaunchKernelGGL(in_stats_finalize<bf16_t>, dim3(ceil_div(N * C, 4)), dim3(256), 0, s, (const bf16_t*)x, ldx,
                        V, N, C, nch, vpc, ws, eps, mean, mean_ld, rstd);
   } else {
-    hipLaunchKernelGGL(in_stats_partial<float>, grid, dim3(256), 0, s, (const float*)x, ldx, V, C, vpc, ws);
+    hipLaunchKernelGGL(in_stats_partial<float>, grid, dim3(256), 0, s, (const float*)x, ldx, (int)V, C, (int)vpc, ws);
     hipLaunchKernelGGL(in_stats_finalize<float>, dim3(ceil_div(N * C, 4)), dim3(256), 0, s, (const float*)x, ldx, V,
                        N, C, nch, vpc, ws, eps, mean, mean_ld, rstd);
   }
@@ -587,14 +695,17 @@ int mmseg_instnorm_stats(const void* x, int ldx, int N, long long V, int C, floa
 
 int mmseg_instnorm_relu_fwd(const void* x, int ldx, void* y, int ldy, int N, long long V, int C, const float* mean,
                             const float* rstd, int dtype, void* stream) {
+  MMSEG_REQUIRE(C % 8 == 0 && C <= 2048, "instnorm_relu_fwd: C=%d must be a multiple of 8", C);
+  MMSEG_REQUIRE(V * (ldx > ldy ? ldx : ldy) < (1LL << 31), "instnorm_relu_fwd: per-sample extent must fit int32");
   hipStream_t s = (hipStream_t)stream;
-  const int grid = grid_for((long long)N * V * (C / 8));
+  int vpc;
+  const dim3 grid(apply_chunks(V, C, &vpc), N);
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(in_relu_apply<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, ldx, (bf16_t*)y, ldy, V,
-                       N, C, mean, rstd);
+    hipLaunchKernelGGL(in_relu_apply<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, (bf16_t*)y, ldy, (int)V,
+                       C, vpc, mean, rstd);
   else
-    hipLaunchKernelGGL(in_relu_apply<float>, dim3(grid), dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy, V, N,
-                       C, mean, rstd);
+    hipLaunchKernelGGL(in_relu_apply<float>, grid, dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy, (int)V, C,
+                       vpc, mean, rstd);
   return mmseg::check_launch("instnorm_relu_fwd");
 }
 
@@ -603,29 +714,32 @@ int mmseg_instnorm_relu_bwd(const void* x, int ldx, const float* mean, const flo
                             float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
                             const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N,
                             int D, int H, int W, int C, float* ws, int dtype, void* stream) {
-  MMSEG_REQUIRE(C % 8 == 0, "instnorm_bwd: C=%d must be a multiple of 8", C);
+  MMSEG_REQUIRE(C % 8 == 0 && C <= 2048, "instnorm_bwd: C=%d must be a multiple of 8 and <= 2048", C);
   MMSEG_REQUIRE(!pool_dy || ((D | H | W) & 1) == 0, "instnorm_bwd: pooled gather needs even dims");
   const long long V = (long long)D * H * W;
+  MMSEG_REQUIRE(V * (ldx > lddx ? ldx : lddx) < (1LL << 31) && V * (ld1 > pool_ld ? ld1 : pool_ld) < (1LL << 31),
+                "instnorm_bwd: per-sample extent must fit int32");
   long long vpc;
   const int nch = chunks_for(V, C, &vpc);
+  int avpc;
+  const int anch = apply_chunks(V, C, &avpc);
   DySrc src{p1, ld1, scale1, alpha1, alpha_stride, beta, beta_stride, pool_dy, pool_ld, pool_idx};
   hipStream_t s = (hipStream_t)stream;
   float* part = ws;
   float* coef = ws + (long long)N * nch * C * 2;
-  dim3 grid(nch, N);
-  const int ag = grid_for((long long)N * V * (C / 8));
+  dim3 grid(nch, N), agrid(anch, N);
   if (dtype == MMSEG_BF16) {
-    hipLaunchKernelGGL(in_bwd_partial<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, mean, rstd, src, V, C, D,
-                       H, W, vpc, part);
+    hipLaunchKernelGGL(in_bwd_partial<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, mean, rstd, src, (int)V,
+                       C, D, H, W, (int)vpc, part);
     hipLaunchKernelGGL(in_bwd_finalize, dim3(ceil_div(N * C, 4)), dim3(256), 0, s, part, N, C, nch, V, coef);
-    hipLaunchKernelGGL(in_bwd_apply<bf16_t>, dim3(ag), dim3(256), 0, s, (const bf16_t*)x, ldx, mean, rstd, src, coef,
-                       (bf16_t*)dx, lddx, V, N, C, D, H, W);
+    hipLaunchKernelGGL(in_bwd_apply<bf16_t>, agrid, dim3(256), 0, s, (const bf16_t*)x, ldx, mean, rstd, src, coef,
+                       (bf16_t*)dx, lddx, (int)V, C, D, H, W, avpc);
   } else {
-    hipLaunchKernelGGL(in_bwd_partial<float>, grid, dim3(256), 0, s, (const float*)x, ldx, mean, rstd, src, V, C, D,
-                       H, W, vpc, part);
+    hipLaunchKernelGGL(in_bwd_partial<float>, grid, dim3(256), 0, s, (const float*)x, ldx, mean, rstd, src, (int)V, C,
+                       D, H, W, (int)vpc, part);
     hipLaunchKernelGGL(in_bwd_finalize, dim3(ceil_div(N * C, 4)), dim3(256), 0, s, part, N, C, nch, V, coef);
-    hipLaunchKernelGGL(in_bwd_apply<float>, dim3(ag), dim3(256), 0, s, (const float*)x, ldx, mean, rstd, src, coef,
-                       (float*)dx, lddx, V, N, C, D, H, W);
+    hipLaunchKernelGGL(in_bwd_apply<float>, agrid, dim3(256), 0, s, (const float*)x, ldx, mean, rstd, src, coef,
+                       (float*)dx, lddx, (int)V, C, D, H, W, avpc);
   }
   return mmseg::check_launch("instnorm_relu_bwd");
 }

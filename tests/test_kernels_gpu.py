@@ -38,6 +38,27 @@ def _act(x, dtype):
     (32, 32, (2, 4, 4, 8)), (64, 32, (1, 8, 4, 16)), (32, 64, (1, 4, 8, 8)), (256, 64, (2, 4, 4, 8)),
     (128, 128, (1, 8, 8, 8))])
 def test_conv3_fwd_dgrad_wgrad(dev, dtype, cin, cout, shape):
+    _check_conv3(dev, dtype, cin, cout, shape)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("knobs,cin,cout,shape", [
+    # brick v2 variants (kernel choice is by grid size; the knobs force each one on a small grid)
+    ({"MMSEG_BRICK2_MINBLK": "0"}, 64, 64, (2, 8, 16, 8)),          # BN64 ZW1
+    ({"MMSEG_BRICK2_MINBLK": "0"}, 32, 128, (1, 4, 8, 16)),         # BN64 ZW1, 2 column tiles
+    ({"MMSEG_BRICK2_ZW": "2"}, 32, 32, (1, 8, 8, 16)),              # BN32 ZW2 (bf16 only; f32 takes ZW1)
+    ({"MMSEG_BRICK2_ZW": "2"}, 64, 32, (2, 8, 8, 8)),               # BN32 ZW2, dgrad with 2 input chunks
+    ({}, 128, 32, (1, 4, 16, 8)),                                   # BN32 ZW1, 4 input chunks
+    ({"MMSEG_BRICK": "1"}, 64, 64, (2, 8, 8, 8)),                   # v1 brick
+    ({"MMSEG_BRICK": "0"}, 64, 64, (2, 8, 8, 8)),                   # per-lane gather GEMM
+])
+def test_conv3_kernel_variants(dev, dtype, knobs, cin, cout, shape, monkeypatch):
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    _check_conv3(dev, dtype, cin, cout, shape)
+
+
+def _check_conv3(dev, dtype, cin, cout, shape):
     torch.manual_seed(cin + cout)
     conv = nn.Conv3d(cin, cout, 3, padding=1).to(dev)
     rt = Runtime(dev, dtype)
