@@ -56,6 +56,10 @@ int mmseg_pack_weight(const float* w, void* dst, int mode, int Co, int Ci, int C
 int mmseg_pack_desc_bytes(void);
 int mmseg_pack_weights_batched(const void* descs, int n, long long total, int dtype, void* stream);
 
+/* Split count the CONV3 kernel choice wants for this shape (value-returning, not a status): the caller
+ * allocates ksplit*M*Ncols fp32 of split-K workspace and passes ksplit to mmseg_conv_gemm. */
+int mmseg_conv3_splits(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,
+                       int dtype);
 /* Implicit-GEMM forward / data-gradient convolution on MFMA.
  * Replaces aten::convolution (fwd) and convolution_backward (grad_input) of
  * Conv3d(k3,p1) unet.py:26-27, ConvTranspose3d(k2,s2) unet.py:95, and the

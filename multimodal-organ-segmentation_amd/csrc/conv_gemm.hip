@@ -602,6 +602,286 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kern
   }
 }
 
+// ------------------------------------- runtime-brick conv (small volumes)
+// conv3_brick2_kernel for volumes whose sides are not multiples of 8 (the
+// 12^3 and 6^3 levels): the brick (bz, by, bx), <= 256 voxels, is chosen on the
+// host among divisors of (D, H, W), and the 27*Cin reduction can be split over
+// 32-channel chunks (fp32 partials [ks][M][Ncols] + gemm_splitk_reduce) so that
+// a handful of bricks still fills the chip.  Row r of the block (wave*64 + i*16
+// + lane%16) is brick voxel r; rows >= bz*by*bx compute garbage and are never
+// stored.
+constexpr int BR_MAXHV = 640;   // halo voxels staged per block (host guarantees)
+// halo image quads available (host guarantees (bz+2)(by+2)((bx+2)*QV+2) <= this): 40 KB bf16 / 80 KB f32
+__host__ __device__ constexpr int br_xq(int tsize) { return tsize == 2 ? 2560 : 5120; }
+
+template <typename T, int BN>
+__global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kernel(GemmArgs g, int bz, int by,
+                                                                                   int bx) {
+  using L = Brick2Layout<T>;
+  constexpr int RM = 4, RN = BN / 16;
+  constexpr int XQ = br_xq(sizeof(T));
+  constexpr int WQ = 9 * BN * L::QV;
+  constexpr int EQ = (256 * (BN + 4) * 4 + 15) / 16;   // fp32 epilogue tile
+  constexpr int LQ = (XQ + WQ) > EQ ? (XQ + WQ) : EQ;
+  __shared__ __attribute__((aligned(16))) float4 lds4[LQ];
+  T* Xl = reinterpret_cast<T*>(lds4);
+  T* Wl = reinterpret_cast<T*>(lds4 + XQ);
+  constexpr int EPQ = 16 / sizeof(T);
+  constexpr int X_PER = (BR_MAXHV * 4 + 255) / 256;
+  constexpr int W_ITEMS = 9 * BN * 4;
+  constexpr int W_PER = (W_ITEMS + 255) / 256;
+
+  const int HX = bx + 2, HY = by + 2, HZ = bz + 2;
+  const int RY = HX * L::QV + 2, RZ = HY * RY;
+  const int HV = HZ * HY * HX;
+  const int X_ITEMS = HV * 4;
+  const int rows = bz * by * bx;
+
+  const T* A = reinterpret_cast<const T*>(g.a);
+  const T* Bw = reinterpret_cast<const T*>(g.b);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int bz_n = g.D / bz, by_n = g.H / by, bx_n = g.W / bx;
+  const int nbrick = (g.M / (g.D * g.H * g.W)) * bz_n * by_n * bx_n;
+  const int nt_n = (g.Ncols + BN - 1) / BN;
+  const int tile = g.swz ? xcd_swizzle(blockIdx.x, nbrick * nt_n * g.ksplit) : (int)blockIdx.x;
+  int bidx = tile % nbrick;
+  const int nt = (tile / nbrick) % nt_n;
+  const int ks = tile / (nbrick * nt_n);
+  const int bxi = bidx % bx_n; bidx /= bx_n;
+  const int byi = bidx % by_n; bidx /= by_n;
+  const int bzi = bidx % bz_n;
+  const int n = bidx / bz_n;
+  const int z0 = bzi * bz, y0 = byi * by, x0 = bxi * bx;
+  const long long HW = (long long)g.H * g.W;
+  const long long nbase = (long long)n * g.D * HW;
+  const int n0 = nt * BN;
+  const int cin = 8 << g.cpg_shift;
+  const int nchunk = cin / CK;
+  const int cps = (nchunk + g.ksplit - 1) / g.ksplit;
+  const int c_begin = ks * cps;
+  const int c_end = c_begin + cps < nchunk ? c_begin + cps : nchunk;
+
+  V8<T> xr[X_PER], wr[W_PER];
+  auto load_x = [&](int c) {
+#pragma unroll
+    for (int k = 0; k < X_PER; ++k) {
+      const int e = tid + k * 256;
+      if (e < X_ITEMS) {
+        const int h = e >> 2, cg = e & 3;
+        const int hx = h % HX, t = h / HX;
+        const int hy = t % HY, hz = t / HY;
+        const int z = z0 - 1 + hz, y = y0 - 1 + hy, x = x0 - 1 + hx;
+        if ((unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W)
+          xr[k].load(A + (nbase + z * HW + (long long)y * g.W + x) * g.lda + c * CK + cg * 8);
+        else
+          xr[k].zero();
+      }
+    }
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int k = 0; k < X_PER; ++k) {
+      const int e = tid + k * 256;
+      if (e < X_ITEMS) {
+        const int h = e >> 2, cg = e & 3;
+        const int hx = h % HX, t = h / HX;
+        const int hy = t % HY, hz = t / HY;
+        xr[k].store(Xl + (hz * RZ + hy * RY + hx * L::QV + cg * L::QG) * EPQ);
+      }
+    }
+  };
+  auto load_w = [&](int c, int kz) {
+#pragma unroll
+    for (int k = 0; k < W_PER; ++k) {
+      const int e = tid + k * 256;
+      if (e < W_ITEMS) {
+        const int cg = e & 3, q = e >> 2;
+        const int col = q % BN, t9 = q / BN;
+        const int kgi = (kz * 9 + t9) * (cin / 8) + c * 4 + cg;
+        wr[k].load(Bw + ((long long)kgi * g.Cpad + n0 + col) * 8);
+      }
+    }
+  };
+  auto store_w = [&]() {
+#pragma unroll
+    for (int k = 0; k < W_PER; ++k) {
+      const int e = tid + k * 256;
+      if (e < W_ITEMS) {
+        const int cg = e & 3, q = e >> 2;
+        wr[k].store(Wl + (q * L::QV + (cg ^ w2_swz(q)) * L::QG) * EPQ);
+      }
+    }
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int r16 = lane & 15, kg = lane >> 4;
+  int aq[RM];
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    int rr = wave * 64 + i * 16 + r16;
+    if (rr >= rows) rr = 0;   // padding rows read voxel 0's halo (never stored)
+    const int rx = rr % bx, t = rr / bx;
+    const int ry = t % by, rz = t / by;
+    aq[i] = rz * RZ + ry * RY + rx * L::QV + kg * L::QG;
+  }
+  int bq[RN];
+#pragma unroll
+  for (int j = 0; j < RN; ++j) {
+    const int col = j * 16 + r16;
+    bq[j] = col * L::QV + (kg ^ w2_swz(col)) * L::QG;
+  }
+
+  const int st_begin = c_begin * 3, st_end = c_end * 3;
+  if (st_begin < st_end) {
+    load_x(c_begin);
+    load_w(c_begin, 0);
+    store_x();
+    store_w();
+  }
+  __syncthreads();
+  for (int st = st_begin; st < st_end; ++st) {
+    const int kz = st % 3;
+    const int sn = st + 1;
+    const bool more = sn < st_end;
+    const int cn = sn / 3, kzn = sn - cn * 3;
+    if (more) {
+      load_w(cn, kzn);
+      if (kzn == 0) load_x(cn);
+    }
+#pragma unroll
+    for (int t9 = 0; t9 < 9; ++t9) {
+      const int ky = t9 / 3, kx = t9 - ky * 3;
+      const int hoff = kz * RZ + ky * RY + kx * L::QV;
+      V8<T> af[RM], bf[RN];
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bf[j].load(Wl + (t9 * BN * L::QV + bq[j]) * EPQ);
+#pragma unroll
+      for (int i = 0; i < RM; ++i) af[i].load(Xl + (aq[i] + hoff) * EPQ);
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) mfma_step<T>(acc[i][j], af[i], bf[j]);
+    }
+    __syncthreads();
+    if (more) {
+      store_w();
+      if (kzn == 0) store_x();
+      __syncthreads();
+    }
+  }
+
+  // epilogue through LDS: rows < bz*by*bx only
+  auto row_vox = [&](int rr) {
+    const int rx = rr % bx, t = rr / bx;
+    const int ry = t % by, rz = t / by;
+    return nbase + (z0 + rz) * HW + (long long)(y0 + ry) * g.W + (x0 + rx);
+  };
+  if (g.ksplit == 1) {
+    T* El = reinterpret_cast<T*>(lds4);
+    constexpr int EP = BN + 8;
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int col = j * 16 + r16;
+      const float bv = (g.bias && n0 + col < g.Ncols) ? g.bias[n0 + col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) El[(wave * 64 + i * 16 + kg * 4 + r) * EP + col] = from_f<T>(acc[i][j][r] + bv);
+    }
+    __syncthreads();
+    T* O = reinterpret_cast<T*>(g.out);
+    constexpr int CG = BN / 8;
+    for (int e = tid; e < rows * CG; e += 256) {
+      const int rr = e / CG, cg = e % CG;
+      const int col = n0 + cg * 8;
+      if (col < g.Ncols) {
+        V8<T> o;
+        o.load(El + rr * EP + cg * 8);
+        o.store(O + row_vox(rr) * g.ldo + col);
+      }
+    }
+  } else {
+    float* El = reinterpret_cast<float*>(lds4);
+    constexpr int EP = BN + 4;
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int col = j * 16 + r16;
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) El[(wave * 64 + i * 16 + kg * 4 + r) * EP + col] = acc[i][j][r];
+    }
+    __syncthreads();
+    constexpr int CG = BN / 4;
+    for (int e = tid; e < rows * CG; e += 256) {
+      const int rr = e / CG, cg = e % CG;
+      const int col = n0 + cg * 4;
+      if (col < g.Ncols) {
+        const float4 v = *reinterpret_cast<const float4*>(El + rr * EP + cg * 4);
+        *reinterpret_cast<float4*>(g.part + ((long long)ks * g.M + row_vox(rr)) * g.Ncols + col) = v;
+      }
+    }
+  }
+}
+
+// Host-side choice of the CONV3 kernel (shared by the launcher and mmseg_conv3_splits).
+struct Conv3Plan {
+  int kind;          // 0 per-lane gather GEMM, 1 brick2, 2 runtime brick
+  int bz, by, bx;    // kind 2
+  int ks;            // splits the plan wants (kind 2: over 32-channel chunks)
+  int bn;            // kind 2 column tile
+};
+
+Conv3Plan plan_conv3(int M, int Ncols, int cin, int D, int H, int W, int lda, int ldo, int tsize) {
+  Conv3Plan p{0, 0, 0, 0, 1, 32};
+  const int brick = knob("MMSEG_BRICK", 2);
+  const bool base_ok = cin % CK == 0 && lda % 8 == 0 && ldo % 8 == 0 && Ncols % 32 == 0;
+  if (brick == 2 && base_ok && D % 4 == 0 && H % B2_Y == 0 && W % B2_X == 0) {
+    p.kind = 1;
+    return p;
+  }
+  if (brick >= 2 && base_ok && knob("MMSEG_BRICKR", 1)) {
+    int best = 0;
+    for (int bz = 1; bz <= D && bz <= 8; ++bz) {
+      if (D % bz) continue;
+      for (int by = 1; by <= H && by <= 16; ++by) {
+        if (H % by) continue;
+        for (int bx = 1; bx <= W && bx <= 16; ++bx) {
+          if (W % bx) continue;
+          const int rows = bz * by * bx;
+          const int halo = (bz + 2) * (by + 2) * (bx + 2);
+          const int hq = (bz + 2) * (by + 2) * ((bx + 2) * 2 * tsize + 2);
+          if (rows > 256 || halo > BR_MAXHV || hq > br_xq(tsize)) continue;
+          const int score = rows * 4 + (bx % 8 == 0 ? 2 : 0) + (by % 8 == 0 ? 1 : 0);
+          if (score > best) {
+            best = score;
+            p.bz = bz; p.by = by; p.bx = bx;
+          }
+        }
+      }
+    }
+    if (best >= 64 * 4) {   // at least a quarter of the 256-row tile in use
+      p.kind = 2;
+      p.bn = (tsize == 2 && Ncols % 64 == 0) ? 64 : 32;
+      const int nb = (M / (D * H * W)) * (D / p.bz) * (H / p.by) * (W / p.bx);
+      const int nt = (Ncols + p.bn - 1) / p.bn;
+      const int nchunk = cin / CK;
+      int ks = (512 + nb * nt - 1) / (nb * nt);
+      if (ks > nchunk) ks = nchunk;
+      if (ks < 1) ks = 1;
+      const int cps = (nchunk + ks - 1) / ks;
+      p.ks = (nchunk + cps - 1) / cps;
+      return p;
+    }
+  }
+  return p;
+}
+
 // Fixed-order split-K reduction for the forward GEMM: out = sum_k part[k] (+bias).
 template <typename T, int MODE>
 __global__ void gemm_splitk_reduce(GemmArgs g) {
@@ -1284,8 +1564,34 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
   const int Cbig = g.Ncols >= 64;
   dim3 block(256);
   const int brick = knob("MMSEG_BRICK", 2);
-  if (MODE == MODE_CONV3 && g.ksplit == 1 && brick == 2 && (8 << g.cpg_shift) % CK == 0 && g.D % 4 == 0 &&
-      g.H % B2_Y == 0 && g.W % B2_X == 0 && g.lda % 8 == 0 && g.ldo % 8 == 0 && g.Ncols % 32 == 0) {
+  const Conv3Plan plan = MODE == MODE_CONV3 ? plan_conv3(g.M, g.Ncols, 8 << g.cpg_shift, g.D, g.H, g.W, g.lda, g.ldo,
+                                                         (int)sizeof(T))
+                                            : Conv3Plan{0, 0, 0, 0, 1, 32};
+  if (plan.kind == 2) {
+    const int nb = (g.M / (g.D * g.H * g.W)) * (g.D / plan.bz) * (g.H / plan.by) * (g.W / plan.bx);
+    const int nchunk = (8 << g.cpg_shift) / CK;
+    if (g.ksplit > nchunk) g.ksplit = nchunk;
+    const int cps = (nchunk + g.ksplit - 1) / g.ksplit;
+    g.ksplit = (nchunk + cps - 1) / cps;
+    const dim3 grid(nb * ((g.Ncols + plan.bn - 1) / plan.bn) * g.ksplit);
+    if (plan.bn == 64) {
+      if constexpr (sizeof(T) == 2) {
+        mmseg::note_kernel("conv3_brickr_kernel<BN64>");
+        hipLaunchKernelGGL((conv3_brickr_kernel<T, 64>), grid, block, 0, s, g, plan.bz, plan.by, plan.bx);
+      }
+    } else {
+      mmseg::note_kernel("conv3_brickr_kernel<BN32>");
+      hipLaunchKernelGGL((conv3_brickr_kernel<T, 32>), grid, block, 0, s, g, plan.bz, plan.by, plan.bx);
+    }
+    if (mmseg::check_launch("conv3_brickr")) return 1;
+    if (g.ksplit > 1) {
+      const long long total = (long long)g.M * g.Ncols;
+      hipLaunchKernelGGL((gemm_splitk_reduce<T, MODE>), dim3(ceil_div(total, 256)), dim3(256), 0, s, g);
+      return mmseg::check_launch("gemm_splitk_reduce");
+    }
+    return 0;
+  }
+  if (plan.kind == 1 && g.ksplit == 1) {
     const int nb1 = (g.M / (g.D * g.H * g.W)) * (g.D / 4) * (g.H / B2_Y) * (g.W / B2_X);
     const int min_blocks = knob("MMSEG_BRICK2_MINBLK", 512);
     if (g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
@@ -1441,6 +1747,22 @@ int mmseg_conv_gemm(const void* a, int lda, const void* wpacked, const float* bi
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16) return launch_gemm_mode<bf16_t>(g, mode, s);
   return launch_gemm_mode<float>(g, mode, s);
+}
+
+// Number of K splits the CONV3 path wants for this shape (callers size the
+// split-K workspace, ksplit*M*Ncols floats, with it and pass it as ksplit).
+int mmseg_conv3_splits(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,
+                       int dtype) {
+  const int tsize = dtype == MMSEG_BF16 ? 2 : 4;
+  const Conv3Plan p = plan_conv3(M, Ncols, 8 << cpg_shift, D, H, W, lda, ldo, tsize);
+  if (p.kind == 2) return p.ks;
+  if (p.kind == 1) return 1;
+  // per-lane gather GEMM: enough (128 x 64|32) tiles to fill the chip
+  const int tiles = ceil_div(M, 128) * ceil_div(Ncols, Ncols >= 64 ? 64 : 32);
+  if (tiles >= 512 || KG < 32) return 1;
+  int ks = ceil_div(512, tiles);
+  if (ks > KG / 16) ks = KG / 16;
+  return ks < 1 ? 1 : ks;
 }
 
 // Weight-gradient partials: part[ksplit][Ca][Ncols] (fp32).

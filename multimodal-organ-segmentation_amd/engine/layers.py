@@ -123,7 +123,8 @@ class Conv3:
 
     def fwd(self, x: Act, y: Act):
         M = x.N * x.V
-        ks = _gemm_ksplit(M, self.Co, self.KG)
+        ks = self.rt.lib.mmseg_conv3_splits(M, self.Co, self.Cpad, self.KG, self.cpg_shift, x.D, x.H, x.W, x.ld, y.ld,
+                                            self.rt.code)
         ws = self.rt.ws(ks * M * self.Co) if ks > 1 else None
         with TIMER.region(_gemm_name(self.rt, self.Co, "conv3"), flops=2.0 * M * self.Co * 27 * self.Ci):
             self.rt.lib.mmseg_conv_gemm(x.ptr, x.ld, ptr(self.wf), ptr(self.conv.bias), y.ptr, y.ld, ptr(ws),
@@ -152,7 +153,7 @@ class Conv3:
         self.flat.mark(self.conv.weight, self.conv.bias)
         if dx is not None:
             M = V
-            ks = _gemm_ksplit(M, self.Ci, self.KGd)
+            ks = L.mmseg_conv3_splits(M, self.Ci, self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, dy.ld, dx.ld, code)
             ws = self.rt.ws(ks * M * self.Ci) if ks > 1 else None
             with TIMER.region(_gemm_name(self.rt, self.Ci, "conv3"), flops=2.0 * M * self.Co * 27 * self.Ci):
                 L.mmseg_conv_gemm(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, ptr(ws), MODE_CONV3, M, self.Ci,

@@ -49,6 +49,9 @@ def test_conv3_fwd_dgrad_wgrad(dev, dtype, cin, cout, shape):
     ({"MMSEG_BRICK2_ZW": "2"}, 32, 32, (1, 8, 8, 16)),              # BN32 ZW2 (bf16 only; f32 takes ZW1)
     ({"MMSEG_BRICK2_ZW": "2"}, 64, 32, (2, 8, 8, 8)),               # BN32 ZW2, dgrad with 2 input chunks
     ({}, 128, 32, (1, 4, 16, 8)),                                   # BN32 ZW1, 4 input chunks
+    ({}, 256, 128, (2, 12, 12, 12)),                                 # runtime brick (3,6,12) + chunk split-K
+    ({}, 512, 256, (1, 6, 6, 6)),                                    # runtime brick (6,6,6), 16 chunks
+    ({"MMSEG_BRICKR": "0"}, 256, 128, (2, 12, 12, 12)),              # same through the gather GEMM
     ({"MMSEG_BRICK": "1"}, 64, 64, (2, 8, 8, 8)),                   # v1 brick
     ({"MMSEG_BRICK": "0"}, 64, 64, (2, 8, 8, 8)),                   # per-lane gather GEMM
 ])

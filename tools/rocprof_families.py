@@ -26,6 +26,12 @@ _MODES = {"0": "conv3", "1": "point", "2": "convT_fwd", "3": "convT_dgrad"}
 def family(name: str) -> str:
     """Map a (mangled or demangled) kernel name to the engine's family name."""
     dt = "bf16" if ("DF16b" in name or "__bf16" in name) else "f32"
+    m = re.search(r"conv3_brick2_kernelI(?:DF16b|f)Li(\d+)ELi(\d+)E", name)
+    if m:
+        return f"conv3_brick2_kernel<BN{m.group(1)},ZW{m.group(2)}>[{dt}]"
+    m = re.search(r"conv3_brickr_kernelI(?:DF16b|f)Li(\d+)E", name)
+    if m:
+        return f"conv3_brickr_kernel<BN{m.group(1)}>[{dt}]"
     m = re.search(r"conv3_brick_kernelI(?:DF16b|f)Li(\d+)E", name)
     if m:
         return f"conv3_brick_kernel<BN{m.group(1)}>[{dt}]"
