@@ -74,8 +74,11 @@ int mmseg_conv_gemm(const void* a, int lda, const void* wpacked, const float* bi
  * bias_part != NULL (a = dy) also the grad_bias partials bias_part[ksplit][Ca]. */
 int mmseg_wgrad(const void* a, int lda, const void* b, int ldb, float* part, float* bias_part, int mode, int Ca,
                 int Ncols, int cpg_shift, long long V, int D, int H, int W, int ksplit, int dtype, void* stream);
+/* Split counts mmseg_wgrad will use (value-returning): callers size part[] with them.  For CONV3 the
+ * library picks the split of its brick kernels itself; ksplit is then only the caller's workspace cap. */
 int mmseg_wgrad_splits(long long V, int ksplit);
-int mmseg_wgrad_splits_conv3(long long V, int ksplit, int Ca, int cpg_shift, int D, int H, int W, int lda, int ldb);
+int mmseg_wgrad_splits_conv3(long long V, int ksplit, int Ca, int cpg_shift, int D, int H, int W, int lda, int ldb,
+                             int dtype);
 /* Fixed-order sum of the partials into the torch-layout fp32 gradient. */
 int mmseg_wgrad_reduce(const float* part, float* grad, const float* bias_part, float* bias_grad, int Ca, int Ncols,
                        int ksplit, int cpad, int creal, int ntap, int accumulate, void* stream);

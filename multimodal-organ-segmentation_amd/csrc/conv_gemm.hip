@@ -1344,6 +1344,200 @@ __global__ __launch_bounds__(256) void wgrad_brick_kernel(WgradArgs g) {
   }
 }
 
+// ------------------------------------------------ brick wgrad v2 (3^3)
+// 8 waves, 64 output channels x one 32-channel input chunk x all 27 taps per
+// block (wgrad_brick_kernel has 32 x 32): each tap-shifted halo fragment now
+// feeds 4 MFMAs instead of 2 and one staged halo serves twice the output
+// channels, so LDS reads and L2 traffic per MAC drop by a third.  Taps are
+// dealt 4,4,4,3,3,3,3,3 over the waves (acc: 4 taps x 4 x 2 tiles = 128
+// VGPRs).  The two LDS stage buffers alternate, one barrier per brick.
+template <typename T, int MT>
+__global__ __launch_bounds__(512, MT == 2 ? 2 : 1) void wgrad_brick2_kernel(WgradArgs g) {
+  constexpr int EP = 16 / sizeof(T);
+  constexpr int CO = MT * 16, CG = CO / 8;       // output channels per block, 8-channel groups
+  constexpr int DP = CO + EP;                    // dy tile pitch (elements)
+  constexpr int XP = CK + EP;                    // halo pitch
+  constexpr int DS = 128 * DP, XS = HLO_V * XP;
+  __shared__ __attribute__((aligned(16))) T lds[2 * (DS + XS)];
+  constexpr int D_ITEMS = 128 * CG, X_ITEMS = HLO_V * 4;
+  constexpr int D_PER = D_ITEMS / 512, X_PER = (X_ITEMS + 511) / 512;
+
+  const T* Dy = reinterpret_cast<const T*>(g.a);
+  const T* X = reinterpret_cast<const T*>(g.b);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cin = 8 << g.cpg_shift;
+  const int nchunk = cin / CK, rt_n = g.Ca / CO;
+  const int tile = blockIdx.x;
+  const int ct = tile % nchunk, rt = (tile / nchunk) % rt_n, ks = tile / (nchunk * rt_n);
+  const int bz_n = g.D / BRK_Z, by_n = g.H / BRK_Y, bx_n = g.W / BRK_X;
+  const long long nbrick = (g.V / ((long long)g.D * g.H * g.W)) * bz_n * by_n * bx_n;
+  const long long bpk = (nbrick + g.ksplit - 1) / g.ksplit;
+  const long long b_begin = ks * bpk;
+  const long long b_end = b_begin + bpk < nbrick ? b_begin + bpk : nbrick;
+  const long long HW = (long long)g.H * g.W;
+  const int row0 = rt * CO, c0 = ct * CK;
+  const bool do_bias = g.bias_part != nullptr && ct == 0;
+  const int t_begin = wave < 3 ? 4 * wave : 12 + 3 * (wave - 3);
+  const int t_cnt = wave < 3 ? 4 : 3;
+
+  f32x4 acc[4][MT][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[t][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float bsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  V8<T> dr[D_PER], xr[X_PER];
+  auto load = [&](long long b) {
+    const int bx = (int)(b % bx_n);
+    long long q = b / bx_n;
+    const int by = (int)(q % by_n);
+    q /= by_n;
+    const int bz = (int)(q % bz_n);
+    const long long nbase = (q / bz_n) * g.D * HW;
+    const int z0 = bz * BRK_Z, y0 = by * BRK_Y, x0 = bx * BRK_X;
+#pragma unroll
+    for (int k = 0; k < D_PER; ++k) {
+      const int e = tid + k * 512, v = e / CG, cg = e % CG;
+      const int z = z0 + (v >> 5), y = y0 + ((v >> 3) & 3), x = x0 + (v & 7);
+      dr[k].load(Dy + (nbase + z * HW + (long long)y * g.W + x) * g.lda + row0 + cg * 8);
+    }
+#pragma unroll
+    for (int k = 0; k < X_PER; ++k) {
+      const int e = tid + k * 512;
+      if (e < X_ITEMS) {
+        const int h = e >> 2, cg = e & 3;
+        const int hx = h % HLO_X, hy = (h / HLO_X) % HLO_Y, hz = h / (HLO_X * HLO_Y);
+        const int z = z0 - 1 + hz, y = y0 - 1 + hy, x = x0 - 1 + hx;
+        if ((unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W)
+          xr[k].load(X + (nbase + z * HW + (long long)y * g.W + x) * g.ldb + c0 + cg * 8);
+        else
+          xr[k].zero();
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    T* Dl = lds + buf * (DS + XS);
+    T* Xl = Dl + DS;
+#pragma unroll
+    for (int k = 0; k < D_PER; ++k) {
+      const int e = tid + k * 512;
+      dr[k].store(Dl + (e / CG) * DP + (e % CG) * 8);
+      if (do_bias) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bsum[j] += dr[k].get(j);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < X_PER; ++k) {
+      const int e = tid + k * 512;
+      if (e < X_ITEMS) xr[k].store(Xl + (e >> 2) * XP + (e & 3) * 8);
+    }
+  };
+
+  const int g4 = lane >> 4, i16 = lane & 15, q = i16 >> 2, p4 = i16 & 3;
+  int buf = 0;
+  if (b_begin < b_end) {
+    load(b_begin);
+    store(0);
+  }
+  __syncthreads();
+  for (long long b = b_begin; b < b_end; ++b) {
+    const bool more = b + 1 < b_end;
+    if (more) load(b + 1);
+    const T* Dl = lds + buf * (DS + XS);
+    const T* Xl = Dl + DS;
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int kk = 0; kk < 128; kk += 32) {
+        bf16x8 af[MT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          const bf16_t* base = (const bf16_t*)Dl + (kk + 8 * g4 + q) * DP + i * 16 + 4 * p4;
+          af[i] = tr_frag(base, base + 4 * DP);
+        }
+        const int v_lo = kk + 8 * g4 + q, v_hi = v_lo + 4;
+        const int hlo = ((v_lo >> 5) * HLO_Y + ((v_lo >> 3) & 3)) * HLO_X + (v_lo & 7);
+        const int hhi = ((v_hi >> 5) * HLO_Y + ((v_hi >> 3) & 3)) * HLO_X + (v_hi & 7);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (t < t_cnt) {
+            const int tap = t_begin + t;
+            const int kz = tap / 9, ky = (tap / 3) % 3, kx = tap % 3;
+            const int hoff = (kz * HLO_Y + ky) * HLO_X + kx;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const bf16_t* pl = (const bf16_t*)Xl + (hlo + hoff) * XP + j * 16 + 4 * p4;
+              const bf16_t* ph = (const bf16_t*)Xl + (hhi + hoff) * XP + j * 16 + 4 * p4;
+              const bf16x8 bfr = tr_frag(pl, ph);
+#pragma unroll
+              for (int i = 0; i < MT; ++i)
+                acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[t][i][j], 0, 0, 0);
+            }
+          }
+        }
+      }
+    } else {
+      for (int kk = 0; kk < 128; kk += 4) {
+        const int v = kk + g4;
+        const int hv = ((v >> 5) * HLO_Y + ((v >> 3) & 3)) * HLO_X + (v & 7);
+        float af[MT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) af[i] = (float)Dl[v * DP + i * 16 + i16];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (t < t_cnt) {
+            const int tap = t_begin + t;
+            const int kz = tap / 9, ky = (tap / 3) % 3, kx = tap % 3;
+            const int hoff = (kz * HLO_Y + ky) * HLO_X + kx;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const float bv = (float)Xl[(hv + hoff) * XP + j * 16 + i16];
+#pragma unroll
+              for (int i = 0; i < MT; ++i)
+                acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bv, acc[t][i][j], 0, 0, 0);
+            }
+          }
+        }
+      }
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (t >= t_cnt) continue;
+    const int tap = t_begin + t;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = tap * cin + c0 + j * 16 + i16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = row0 + i * 16 + g4 * 4 + r;
+          g.part[((long long)ks * g.Ca + row) * g.Ncols + col] = acc[t][i][j][r];
+        }
+      }
+  }
+  if (do_bias) {
+    float* red = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[tid * 8 + j] = bsum[j];
+    __syncthreads();
+    if (tid < CO) {
+      const int cg = tid >> 3, j = tid & 7;
+      float sacc = 0.f;
+      for (int t = cg; t < 512; t += CG) sacc += red[t * 8 + j];
+      g.bias_part[(long long)ks * g.Ca + row0 + tid] = sacc;
+    }
+  }
+}
+
 // part[ks][row][col] -> torch-layout gradient (fixed-order sum over ks).
 //   CONV3 : grad[co][ci][tap]    row=co, col = tap*Cin_pad + ci, ci < Cin_real
 //   POINT : grad[co][ci]         row=co, col = ci
@@ -1659,6 +1853,21 @@ int launch_gemm_mode(GemmArgs g, int mode, hipStream_t s) {
 template <typename T, int MODE>
 int launch_wgrad(WgradArgs g, hipStream_t s) {
   dim3 block(256);
+  if constexpr (sizeof(T) == 2) {
+    if (MODE == MODE_CONV3 && g.brick == 2) {
+      const int cin = 8 << g.cpg_shift;
+      if (g.Ca % 64 == 0) {
+        dim3 grid((cin / CK) * (g.Ca / 64) * g.ksplit);
+        mmseg::note_kernel("wgrad_brick2_kernel<CO64>");
+        hipLaunchKernelGGL((wgrad_brick2_kernel<T, 4>), grid, dim3(512), 0, s, g);
+      } else {
+        dim3 grid((cin / CK) * (g.Ca / 32) * g.ksplit);
+        mmseg::note_kernel("wgrad_brick2_kernel<CO32>");
+        hipLaunchKernelGGL((wgrad_brick2_kernel<T, 2>), grid, dim3(512), 0, s, g);
+      }
+      return mmseg::check_launch("wgrad_brick2");
+    }
+  }
   if (MODE == MODE_CONV3 && g.brick) {
     const int cin = 8 << g.cpg_shift;
     dim3 grid((cin / CK) * (g.Ca / 32) * g.ksplit);
@@ -1690,9 +1899,29 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
   return mmseg::check_launch("wgrad");
 }
 
-int wgrad_brick_ok(int Ca, int cpg_shift, int D, int H, int W, int lda, int ldb) {
-  return knob("MMSEG_WGRAD_BRICK", 1) && Ca % 32 == 0 && (8 << cpg_shift) % CK == 0 && D % BRK_Z == 0 &&
-         H % BRK_Y == 0 && W % BRK_X == 0 && lda % 8 == 0 && ldb % 8 == 0;
+// 0: generic wgrad_kernel, 1: wgrad_brick_kernel (32 co), 2: wgrad_brick2_kernel (64 co)
+// (v2 is bf16 only: its two fp32 stage buffers would not fit in LDS)
+int wgrad_brick_ok(int Ca, int cpg_shift, int D, int H, int W, int lda, int ldb, int dtype) {
+  const int k = knob("MMSEG_WGRAD_BRICK", 2);
+  if (!(k && Ca % 32 == 0 && (8 << cpg_shift) % CK == 0 && D % BRK_Z == 0 && H % BRK_Y == 0 && W % BRK_X == 0 &&
+        lda % 8 == 0 && ldb % 8 == 0))
+    return 0;
+  return (k >= 2 && dtype == MMSEG_BF16 && (Ca % 64 == 0 || knob("MMSEG_WGRAD_BRICK2_CO32", 1))) ? 2 : 1;
+}
+
+// Split count of the CONV3 brick wgrad: enough blocks to fill the chip, capped by
+// the caller's workspace (cap) and by one brick per split.
+int brick_wgrad_splits(long long V, int cap, int Ca, int cpg_shift, int kind) {
+  const int nchunk = (8 << cpg_shift) / CK;
+  const int tiles = nchunk * (Ca / ((kind == 2 && Ca % 64 == 0) ? 64 : 32));
+  const int target = kind == 2 ? 512 : 1024;
+  long long ks = (target + tiles - 1) / tiles;
+  if (ks > cap) ks = cap;
+  const long long nbrick = V / 128;
+  if (ks > nbrick) ks = nbrick;
+  if (ks < 1) ks = 1;
+  const long long bpk = (nbrick + ks - 1) / ks;
+  return (int)((nbrick + bpk - 1) / bpk);
 }
 
 }  // namespace
@@ -1770,13 +1999,10 @@ int mmseg_wgrad(const void* a, int lda, const void* b, int ldb, float* part, flo
                 int Ncols, int cpg_shift, long long V, int D, int H, int W, int ksplit, int dtype, void* stream) {
   MMSEG_REQUIRE(Ca % 8 == 0, "wgrad: rows (%d) must be a multiple of 8", Ca);
   MMSEG_REQUIRE(Ncols % 8 == 0, "wgrad: cols (%d) must be a multiple of 8", Ncols);
-  const int brick = mode == MODE_CONV3 && wgrad_brick_ok(Ca, cpg_shift, D, H, W, lda, ldb);
+  const int brick = mode == MODE_CONV3 ? wgrad_brick_ok(Ca, cpg_shift, D, H, W, lda, ldb, dtype) : 0;
   long long vps = ((V + ksplit - 1) / ksplit + 63) / 64 * 64;
   if (brick) {
-    const long long nbrick = V / 128;
-    if (ksplit > nbrick) ksplit = (int)nbrick;
-    const long long bpk = (nbrick + ksplit - 1) / ksplit;
-    ksplit = (int)((nbrick + bpk - 1) / bpk);
+    ksplit = brick_wgrad_splits(V, ksplit, Ca, cpg_shift, brick);
   } else {
     ksplit = (int)((V + vps - 1) / vps);
   }
@@ -1807,12 +2033,11 @@ int mmseg_wgrad_splits(long long V, int ksplit) {
 }
 
 // Same for the CONV3 brick path (splits the list of 4x4x8 bricks).
-int mmseg_wgrad_splits_conv3(long long V, int ksplit, int Ca, int cpg_shift, int D, int H, int W, int lda, int ldb) {
-  if (!wgrad_brick_ok(Ca, cpg_shift, D, H, W, lda, ldb)) return mmseg_wgrad_splits(V, ksplit);
-  const long long nbrick = V / 128;
-  if (ksplit > nbrick) ksplit = (int)nbrick;
-  const long long bpk = (nbrick + ksplit - 1) / ksplit;
-  return (int)((nbrick + bpk - 1) / bpk);
+int mmseg_wgrad_splits_conv3(long long V, int ksplit, int Ca, int cpg_shift, int D, int H, int W, int lda, int ldb,
+                             int dtype) {
+  const int kind = wgrad_brick_ok(Ca, cpg_shift, D, H, W, lda, ldb, dtype);
+  if (!kind) return mmseg_wgrad_splits(V, ksplit);
+  return brick_wgrad_splits(V, ksplit, Ca, cpg_shift, kind);
 }
 
 int mmseg_wgrad_reduce(const float* part, float* grad, const float* bias_part, float* bias_grad, int Ca, int Ncols,

@@ -136,12 +136,11 @@ class Conv3:
         V = x.N * x.V
         ncols = 27 * self.Cip
         if self.Cip % 32 == 0 and self.Co % 32 == 0:
-            # brick path: blocks = (Cin/32)(Co/32) x splits; partials capped at ~32 MB
-            tiles = (self.Cip // 32) * (self.Co // 32)
-            want = max(1, min(-(-1024 // tiles), (8 << 20) // (self.Co * ncols)))
+            # brick path: the library picks the split; we only cap the partials at ~32 MB
+            want = max(1, (8 << 20) // (self.Co * ncols))
         else:
             want = _wgrad_ksplit(self.Co, ncols, V)
-        ks = L.mmseg_wgrad_splits_conv3(V, want, self.Co, self.cpg_shift, x.D, x.H, x.W, dy.ld, x.ld)
+        ks = L.mmseg_wgrad_splits_conv3(V, want, self.Co, self.cpg_shift, x.D, x.H, x.W, dy.ld, x.ld, code)
         part = self.rt.ws(ks * self.Co * ncols + ks * self.Co)
         bpart = part.data_ptr() + ks * self.Co * ncols * 4
         with TIMER.region(_gemm_name(self.rt, 0, "conv3"), flops=2.0 * V * self.Co * 27 * self.Ci):

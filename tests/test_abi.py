@@ -49,5 +49,6 @@ def test_no_cpu_fallback():
 def test_value_returning_entry_points_do_not_raise():
     L = _lib.lib()
     assert L.mmseg_wgrad_splits(1 << 20, 64) >= 1
-    assert L.mmseg_wgrad_splits_conv3(2 * 96 ** 3, 512, 32, 2, 96, 96, 96, 32, 32) >= 1
+    assert L.mmseg_wgrad_splits_conv3(2 * 96 ** 3, 512, 32, 2, 96, 96, 96, 32, 32, 1) >= 1
+    assert L.mmseg_conv3_splits(2 * 12 ** 3, 256, 256, 27 * 32, 5, 12, 12, 12, 256, 256, 1) >= 1
     assert L.mmseg_pack_desc_bytes() == 56

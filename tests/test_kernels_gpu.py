@@ -52,6 +52,11 @@ def test_conv3_fwd_dgrad_wgrad(dev, dtype, cin, cout, shape):
     ({}, 256, 128, (2, 12, 12, 12)),                                 # runtime brick (3,6,12) + chunk split-K
     ({}, 512, 256, (1, 6, 6, 6)),                                    # runtime brick (6,6,6), 16 chunks
     ({"MMSEG_BRICKR": "0"}, 256, 128, (2, 12, 12, 12)),              # same through the gather GEMM
+    ({"MMSEG_WGRAD_BRICK": "1"}, 64, 128, (2, 4, 8, 8)),             # v1 brick wgrad (32 co per block)
+    ({"MMSEG_WGRAD_BRICK": "0"}, 64, 64, (1, 4, 8, 8)),              # generic wgrad
+    ({}, 32, 128, (1, 8, 4, 16)),                                    # v2 brick wgrad, 2 row tiles of 64 co
+    ({}, 64, 32, (2, 4, 4, 16)),                                     # v2 brick wgrad, 32 co per block
+    ({"MMSEG_WGRAD_BRICK2_CO32": "0"}, 64, 32, (2, 4, 4, 16)),       # v1 for 32 co
     ({"MMSEG_BRICK": "1"}, 64, 64, (2, 8, 8, 8)),                   # v1 brick
     ({"MMSEG_BRICK": "0"}, 64, 64, (2, 8, 8, 8)),                   # per-lane gather GEMM
 ])
