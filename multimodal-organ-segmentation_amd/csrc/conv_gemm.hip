@@ -1694,6 +1694,73 @@ __global__ void pack_weight_kernel(PackArgs g, int mode) {
   reinterpret_cast<T*>(g.dst)[idx] = from_f<T>(v);
 }
 
+// Batched 3^3 pack: one launch writes BOTH operand images of every 3^3 conv of
+// a model (forward [27*Cip/8][Cpad][8] and flipped/transposed data-gradient
+// [27*Co/8][Cpad_d][8]) from ONE coalesced read of the fp32 master weights.
+// Block = (8 output channels, 32 input channels) of one layer: the 8 x 32 x 27
+// source floats are contiguous runs per output channel, staged in LDS, then
+// written as 16-B vectors (8 input channels for the forward image, 8 output
+// channels for the data-gradient image).  Entries the block does not own
+// (K padding, Cin padding of the stem) are zero from allocation.
+struct Pack3Desc {
+  const float* w;       // [Co][Ci][27]
+  void* wf;             // forward image
+  void* wd;             // data-gradient image or null
+  int Co, Ci, Cip, Cpad, Cpad_d;
+  int block_begin;      // first block of this layer in the launch
+  int pad0, pad1;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void pack_conv3_batched_kernel(const Pack3Desc* __restrict__ descs, int n) {
+  __shared__ float sw[8][32][28];
+  int lo = 0, hi = n - 1;
+  const int b = blockIdx.x;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (descs[mid].block_begin <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const Pack3Desc d = descs[lo];
+  const int nci = (d.Ci + 31) / 32;
+  const int lb = b - d.block_begin;
+  const int co0 = (lb / nci) * 8, ci0 = (lb % nci) * 32;
+  const int cis = d.Ci - ci0 < 32 ? d.Ci - ci0 : 32;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < 8 * 32 * 27; e += 256) {
+    const int co = e / (32 * 27), r = e - co * (32 * 27);
+    const int ci = r / 27, t = r - ci * 27;
+    sw[co][ci][t] = (ci < cis && co0 + co < d.Co) ? d.w[((long long)(co0 + co) * d.Ci + ci0) * 27 + r] : 0.f;
+  }
+  __syncthreads();
+  // forward image: (t, 8-ci group, co) -> 16 B
+  const int cpg = d.Cip >> 3;
+  const int ngrp = ((d.Cip - ci0) < 32 ? (d.Cip - ci0) : 32) >> 3;
+  T* wf = reinterpret_cast<T*>(d.wf);
+  for (int e = tid; e < 27 * 4 * 8; e += 256) {
+    const int co = e & 7, cg = (e >> 3) & 3, t = e >> 5;
+    if (cg >= ngrp || co0 + co >= d.Co) continue;
+    V8<T> v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v.set(j, sw[co][cg * 8 + j][t]);
+    const long long kgi = (long long)t * cpg + (ci0 >> 3) + cg;
+    v.store(wf + (kgi * d.Cpad + co0 + co) * 8);
+  }
+  if (d.wd == nullptr) return;
+  // data-gradient image: tap s -> kgi = (26 - s) * Co/8 + co0/8, column ci, 8 co per vector
+  const int cpgd = d.Co >> 3;
+  T* wd = reinterpret_cast<T*>(d.wd);
+  for (int e = tid; e < 27 * 32; e += 256) {
+    const int ci = e & 31, t = e >> 5;
+    if (ci >= cis) continue;
+    V8<T> v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v.set(j, sw[j][ci][t]);
+    const long long kgi = (long long)(26 - t) * cpgd + (co0 >> 3);
+    v.store(wd + (kgi * d.Cpad_d + ci0 + ci) * 8);
+  }
+}
+
 // Batched pack: one launch packs every layer of a model (descriptor table in device memory).
 struct PackDesc {
   const float* w;
@@ -1940,6 +2007,20 @@ int mmseg_pack_weight(const float* w, void* dst, int mode, int Co, int Ci, int C
   else
     hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(ceil_div(total, 256)), dim3(256), 0, s, g, mode);
   return mmseg::check_launch("pack_weight");
+}
+
+int mmseg_pack3_desc_bytes(void) { return (int)sizeof(Pack3Desc); }
+
+// descs: device array of n Pack3Desc sorted by block_begin; nblocks = total blocks
+// (sum over layers of Co/8 * ceil(Ci/32)).  The images must be zero-initialised once.
+int mmseg_pack_conv3_batched(const void* descs, int n, int nblocks, int dtype, void* stream) {
+  MMSEG_REQUIRE(n >= 1 && nblocks >= 1, "pack_conv3_batched: empty table");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MMSEG_BF16)
+    hipLaunchKernelGGL(pack_conv3_batched_kernel<bf16_t>, dim3(nblocks), dim3(256), 0, s, (const Pack3Desc*)descs, n);
+  else
+    hipLaunchKernelGGL(pack_conv3_batched_kernel<float>, dim3(nblocks), dim3(256), 0, s, (const Pack3Desc*)descs, n);
+  return mmseg::check_launch("pack_conv3_batched");
 }
 
 // descs: device array of n PackDesc (64 B each, see mmseg_pack_desc_bytes); total = sum of KGp*Cpad*8.

@@ -46,26 +46,42 @@ def _gemm_ksplit(M: int, ncols: int, KG: int) -> int:
     return max(1, min(-(-512 // tiles), KG // 16))
 
 
-class BatchedPacker:
-    """All weight packs of a program in ONE launch (descriptor table uploaded once)."""
+class Packer:
+    """Weight packing of a whole program per step: every 3^3 conv's two operand images in ONE launch
+    (mmseg_pack_conv3_batched: one coalesced read of the fp32 weights), the few transposed / 1x1 layers
+    per layer.  MMSEG_PACK=0 selects the per-layer element-wise pack (A/B only)."""
 
     def __init__(self, rt: Runtime, descs):
         import struct
         self.rt = rt
-        nbytes = rt.lib.mmseg_pack_desc_bytes()
-        blob = bytearray()
-        begin = 0
-        for (w, dst, mode, Co, Ci, Cip, KG, KGp, Cpad) in descs:
-            rec = struct.pack("<QQ8iq", w, dst, mode, Co, Ci, Cip, KG, KGp, Cpad, 0, begin)
+        self.per_layer = list(descs) if os.environ.get("MMSEG_PACK", "1") == "0" else []
+        if self.per_layer:
+            return
+        nbytes = rt.lib.mmseg_pack3_desc_bytes()
+        blob, begin, n = bytearray(), 0, 0
+        dgrad = {d[0]: d for d in descs if d[2] == 1}
+        for d in descs:
+            w, dst, mode, Co, Ci, Cip, KG, KGp, Cpad = d
+            if mode == 1:
+                continue
+            if mode != 0:
+                self.per_layer.append(d)
+                continue
+            dd = dgrad.get(w)
+            rec = struct.pack("<QQQ8i", w, dst, dd[1] if dd else 0, Co, Ci, Cip, Cpad, dd[8] if dd else 0, begin, 0, 0)
             assert len(rec) == nbytes, (len(rec), nbytes)
             blob += rec
-            begin += KGp * Cpad * 8
-        self.n = len(descs)
-        self.total = begin
-        self.table = torch.frombuffer(bytes(blob), dtype=torch.uint8).to(rt.device)
+            begin += (Co // 8) * (-(-Ci // 32))
+            n += 1
+        self.n, self.nblocks = n, begin
+        self.table = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(rt.device) if n else None
 
     def run(self):
-        self.rt.lib.mmseg_pack_weights_batched(ptr(self.table), self.n, self.total, self.rt.code, self.rt.stream)
+        L, s, code = self.rt.lib, self.rt.stream, self.rt.code
+        if self.table is not None and not os.environ.get("MMSEG_PACK", "1") == "0":
+            L.mmseg_pack_conv3_batched(ptr(self.table), self.n, self.nblocks, code, s)
+        for d in self.per_layer:
+            L.mmseg_pack_weight(*d, code, s)
 
 
 def _wgrad_ksplit(rows: int, ncols: int, V: int) -> int:
@@ -101,14 +117,15 @@ class Conv3:
         self.KG = 27 * self.Cip // 8
         self.KGp = round_up(self.KG, 4)
         self.Cpad = _col_tile(self.Co)
-        self.wf = torch.empty(self.KGp * self.Cpad * 8, dtype=rt.dtype, device=rt.device)
+        # zeros: the batched pack never writes the K / Cin padding entries
+        self.wf = torch.zeros(self.KGp * self.Cpad * 8, dtype=rt.dtype, device=rt.device)
         self.need_dgrad = need_dgrad
         if need_dgrad:
             self.dshift = pow2_shift(self.Co // 8)
             self.KGd = 27 * self.Co // 8
             self.KGdp = round_up(self.KGd, 4)
             self.Cpad_d = _col_tile(self.Cip)
-            self.wd = torch.empty(self.KGdp * self.Cpad_d * 8, dtype=rt.dtype, device=rt.device)
+            self.wd = torch.zeros(self.KGdp * self.Cpad_d * 8, dtype=rt.dtype, device=rt.device)
 
     def descs(self):
         w = self.conv.weight

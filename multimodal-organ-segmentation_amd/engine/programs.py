@@ -20,7 +20,7 @@ import torch
 import torch.nn as nn
 
 from .._lib import ptr
-from .layers import BatchedPacker, Block, ConvT2, DySpec, Head, Point
+from .layers import Block, ConvT2, DySpec, Head, Packer, Point
 from .runtime import Act, FlatParams, Runtime
 
 
@@ -106,15 +106,8 @@ class UNetProgram:
         self.shape = None
 
     def pack(self):
-        if os.environ.get("MMSEG_BATCHED_PACK", "0") != "1":
-            for d in self._all_descs():
-                self.rt.lib.mmseg_pack_weight(*d, self.rt.code, self.rt.stream)
-            return
         if getattr(self, "_packer", None) is None:
-            d = self.init.descs()
-            for b in self.enc:
-                d += b.descs()
-            self._packer = BatchedPacker(self.rt, d + self.dec.descs())
+            self._packer = Packer(self.rt, self._all_descs())
         self._packer.run()
 
     def setup(self, N, D, H, W):
@@ -200,19 +193,8 @@ class DualEncoderProgram:
         return d + self.dec.descs()
 
     def pack(self):
-        if os.environ.get("MMSEG_BATCHED_PACK", "0") != "1":
-            for d in self._all_descs():
-                self.rt.lib.mmseg_pack_weight(*d, self.rt.code, self.rt.stream)
-            return
         if getattr(self, "_packer", None) is None:
-            d = []
-            for blocks in self.encs:
-                for b in blocks:
-                    d += b.descs()
-            if self.proj:
-                for p in self.proj:
-                    d += p.descs()
-            self._packer = BatchedPacker(self.rt, d + self.dec.descs())
+            self._packer = Packer(self.rt, self._all_descs())
         self._packer.run()
 
     def setup(self, N, D, H, W):

@@ -325,3 +325,33 @@ def test_adamw_matches_torch(dev):
     sd = opt.state_dict()
     assert set(sd["state"][0]) == {"step", "exp_avg", "exp_avg_sq"}
     assert rel(sd["state"][0]["exp_avg"], ropt.state_dict()["state"][0]["exp_avg"]) < 1e-6
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_batched_conv3_pack_matches_per_layer_pack(dev, dtype):
+    """mmseg_pack_conv3_batched (one launch, both operand images) == the per-layer element-wise pack, bitwise,
+    for a stem (1 real channel padded to 8, no data-gradient image) and ragged / multi-chunk layers."""
+    from mmseg_amd.engine.layers import Packer
+    torch.manual_seed(3)
+    rt = Runtime(dev, dtype)
+    shapes = [(32, 1, 8, False), (64, 32, None, True), (32, 64, None, True), (256, 128, None, True),
+              (16, 8, None, True)]
+    convs = [nn.Conv3d(ci, co, 3, padding=1).to(dev) for co, ci, _, _ in shapes]
+    flat = FlatParams([p for c in convs for p in c.parameters()])
+    layers = [Conv3(rt, c, flat, cin_pad=cp, need_dgrad=nd) for c, (_, _, cp, nd) in zip(convs, shapes)]
+    descs = [d for l in layers for d in l.descs()]
+    Packer(rt, descs).run()
+    got = [(l.wf.clone(), l.wd.clone() if l.need_dgrad else None) for l in layers]
+    for l in layers:
+        l.wf.fill_(7)
+        if l.need_dgrad:
+            l.wd.fill_(7)
+        for d in l.descs():
+            lib().mmseg_pack_weight(*d, rt.code, rt.stream)
+    torch.cuda.synchronize()
+    for l, (wf, wd) in zip(layers, got):
+        ref_f = l.wf.clone()
+        # the per-layer pack writes every entry (zeros in the padding): compare everything
+        assert torch.equal(wf.view(torch.int16) if dtype == torch.bfloat16 else wf, ref_f.view(torch.int16) if dtype == torch.bfloat16 else ref_f)
+        if wd is not None:
+            assert torch.equal(wd, l.wd)

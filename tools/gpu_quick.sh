@@ -12,7 +12,7 @@ timeout -k 10 300 python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline > 
 tail -1 $O/bench.log
 if [ -n "$PROF" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o prof -- python3 $R/bench.py --steps 10 --warmup 3 --timer-steps 0 --no-cpu-baseline > $O/prof.log 2>&1 || exit 1
-  python3 $R/tools/rocprof_families.py stats $O/trace/prof_kernel_stats.csv 13 | head -30
+  python3 $R/tools/rocprof_families.py stats $O/trace/prof_kernel_stats.csv 13 > $O/families.txt; head -32 $O/families.txt
 fi
 if [ $# -gt 0 ]; then
   timeout -k 10 600 python3 $R/tools/kbench.py --variants "$@" > $O/kbench.log 2>&1 || exit 1
