@@ -75,6 +75,19 @@ int mmseg_conv_gemm(const void* a, int lda, const void* wpacked, const float* bi
                     float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W,
                     int ksplit, int dtype, void* stream);
 
+/* First conv of an encoder with Cr <= 8 real input channels (unet.py:26 via unet.py:154-157 / dual_encoder.py:66-70)
+ * on the 8-channel packed input (ldx == 8), K = 27*Cr exactly instead of 27*8.  Replaces aten::convolution and
+ * convolution_backward (grad_weight, grad_bias) of that layer.  mmseg_stem_ok / _kp / _wgrad_splits return values.
+ * Weight gradient: part[ks][Co][KP] + bias_part[ks][Co], summed by mmseg_wgrad_reduce(Ca=Co, Ncols=KP, cpad=creal=Cr,
+ * ntap=27). */
+int mmseg_stem_ok(int cr, int Co, int D, int H, int W, int ldx, int ldy);
+int mmseg_stem_kp(int cr);
+int mmseg_stem_wgrad_splits(int N, int D, int H, int W, int want);
+int mmseg_stem_fwd(const void* x, int ldx, int cr, const float* w, const float* bias, void* y, int ldy, int N, int D,
+                   int H, int W, int Co, int dtype, void* stream);
+int mmseg_stem_wgrad(const void* dy, int lddy, const void* x, int ldx, int cr, float* part, float* bias_part, int N,
+                     int D, int H, int W, int Co, int ksplit, int dtype, void* stream);
+
 /* Weight-gradient partials part[ksplit][Ca][Ncols] (fp32), K = voxels.
  * Replaces convolution_backward (grad_weight) of the same layers; with
  * bias_part != NULL (a = dy) also the grad_bias partials bias_part[ksplit][Ca]. */

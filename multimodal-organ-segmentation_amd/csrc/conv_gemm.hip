@@ -196,39 +196,87 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs g) {
   // epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + r
   T* O = reinterpret_cast<T*>(g.out);
   const int Cout = (MODE == MODE_CONVT_FWD) ? (g.Ncols >> 3) : g.Ncols;
+  if (g.ksplit > 1) {
 #pragma unroll
-  for (int i = 0; i < RM; ++i) {
+    for (int i = 0; i < RM; ++i)
 #pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      const int col = n0 + j * 16 + (lane & 15);
-      if (col >= g.Ncols) continue;
+      for (int j = 0; j < RN; ++j) {
+        const int col = n0 + j * 16 + (lane & 15);
+        if (col >= g.Ncols) continue;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const long long row = m0 + i * 16 + (lane >> 4) * 4 + r;
-        if (row >= g.M) continue;
-        float v = acc[i][j][r];
-        if (g.ksplit > 1) {
-          g.part[((long long)ks * g.M + row) * g.Ncols + col] = v;
-          continue;
-        }
-        if (MODE == MODE_CONVT_FWD) {
-          const int t = col / Cout, co = col - t * Cout;
-          if (g.bias) v += g.bias[co];
-          // child voxel of input voxel `row` for tap t
-          const int x = (int)(row % g.W);
-          long long q = row / g.W;
-          const int y = (int)(q % g.H);
-          q /= g.H;
-          const int z = (int)(q % g.D);
-          const long long n = q / g.D;
-          const long long child = ((n * 2LL * g.D + 2 * z + (t >> 2)) * 2LL * g.H + 2 * y + ((t >> 1) & 1)) * 2LL * g.W +
-                                  2 * x + (t & 1);
-          O[child * g.ldo + co] = from_f<T>(v);
-        } else {
-          if (g.bias) v += g.bias[col];
-          O[row * g.ldo + col] = from_f<T>(v);
+        for (int r = 0; r < 4; ++r) {
+          const long long row = m0 + i * 16 + (lane >> 4) * 4 + r;
+          if (row < g.M) g.part[((long long)ks * g.M + row) * g.Ncols + col] = acc[i][j][r];
         }
       }
+    return;
+  }
+  // stage the (BM x BN) tile through LDS so every lane stores 8 channels (16 B bf16) at once;
+  // for the transposed conv an 8-column group is 8 channels of ONE child voxel (Cout % 8 == 0)
+  constexpr int EPT = BN + 8;
+  __shared__ __attribute__((aligned(16))) T El[BM * EPT];
+  const long long mt0 = (long long)mt * BM;
+  const int nt0 = nt * BN;
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int lc = wn * RN * 16 + j * 16 + (lane & 15);
+      const int col = nt0 + lc;
+      float bv = 0.f;
+      if (g.bias && col < g.Ncols) bv = g.bias[MODE == MODE_CONVT_FWD ? col % Cout : col];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int lr = wm * RM * 16 + i * 16 + (lane >> 4) * 4 + r;
+        El[lr * EPT + lc] = from_f<T>(acc[i][j][r] + bv);
+      }
+    }
+  __syncthreads();
+  constexpr int CG = BN / 8;
+  const bool vec = g.ldo % 8 == 0 && g.Ncols % 8 == 0 && (reinterpret_cast<uintptr_t>(g.out) & 15) == 0;
+  if (!vec) {   // odd strides: element-wise stores from the staged tile
+    for (int e = threadIdx.x; e < BM * BN; e += 256) {
+      const int lr = e / BN, lc = e % BN;
+      const long long row = mt0 + lr;
+      const int col = nt0 + lc;
+      if (row >= g.M || col >= g.Ncols) continue;
+      if (MODE == MODE_CONVT_FWD) {
+        const int t = col / Cout, co = col - t * Cout;
+        const int x = (int)(row % g.W);
+        long long q = row / g.W;
+        const int y = (int)(q % g.H);
+        q /= g.H;
+        const int z = (int)(q % g.D);
+        const long long n = q / g.D;
+        const long long child = ((n * 2LL * g.D + 2 * z + (t >> 2)) * 2LL * g.H + 2 * y + ((t >> 1) & 1)) *
+                                    2LL * g.W + 2 * x + (t & 1);
+        O[child * g.ldo + co] = El[lr * EPT + lc];
+      } else {
+        O[row * g.ldo + col] = El[lr * EPT + lc];
+      }
+    }
+    return;
+  }
+  for (int e = threadIdx.x; e < BM * CG; e += 256) {
+    const int lr = e / CG, cg = e % CG;
+    const long long row = mt0 + lr;
+    const int col = nt0 + cg * 8;
+    if (row >= g.M || col >= g.Ncols) continue;
+    V8<T> o;
+    o.load(El + lr * EPT + cg * 8);
+    if (MODE == MODE_CONVT_FWD) {
+      const int t = col / Cout, co = col - t * Cout;
+      const int x = (int)(row % g.W);
+      long long q = row / g.W;
+      const int y = (int)(q % g.H);
+      q /= g.H;
+      const int z = (int)(q % g.D);
+      const long long n = q / g.D;
+      const long long child = ((n * 2LL * g.D + 2 * z + (t >> 2)) * 2LL * g.H + 2 * y + ((t >> 1) & 1)) * 2LL * g.W +
+                              2 * x + (t & 1);
+      o.store(O + child * g.ldo + co);
+    } else {
+      o.store(O + row * g.ldo + col);
     }
   }
 }

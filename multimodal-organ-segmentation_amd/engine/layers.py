@@ -138,7 +138,17 @@ class Conv3:
         for d in self.descs():
             self.rt.lib.mmseg_pack_weight(*d, self.rt.code, self.rt.stream)
 
+    def _stem(self, x: Act, y_ld: int) -> bool:
+        """First conv on the packed input: K = 27*Ci real taps*channels (stem.hip)."""
+        return (not self.need_dgrad and self.Cip == 8 and os.environ.get("MMSEG_STEM", "1") != "0"
+                and bool(self.rt.lib.mmseg_stem_ok(self.Ci, self.Co, x.D, x.H, x.W, x.ld, y_ld)))
+
     def fwd(self, x: Act, y: Act):
+        if self._stem(x, y.ld):
+            with TIMER.region("stem_fwd_kernel", flops=2.0 * x.N * x.V * self.Co * 27 * self.Ci):
+                self.rt.lib.mmseg_stem_fwd(x.ptr, x.ld, self.Ci, ptr(self.conv.weight), ptr(self.conv.bias), y.ptr,
+                                           y.ld, x.N, x.D, x.H, x.W, self.Co, self.rt.code, self.rt.stream)
+            return
         M = x.N * x.V
         ks = self.rt.lib.mmseg_conv3_splits(M, self.Co, self.Cpad, self.KG, self.cpg_shift, x.D, x.H, x.W, x.ld, y.ld,
                                             self.rt.code)
@@ -151,6 +161,19 @@ class Conv3:
     def bwd(self, x: Act, dy: Act, dx: Optional[Act], accumulate: bool):
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
         V = x.N * x.V
+        if dx is None and self._stem(x, dy.ld):
+            ks = L.mmseg_stem_wgrad_splits(x.N, x.D, x.H, x.W, 2048)
+            kp = L.mmseg_stem_kp(self.Ci)
+            part = self.rt.ws(ks * self.Co * kp + ks * self.Co)
+            bpart = part.data_ptr() + ks * self.Co * kp * 4
+            with TIMER.region("stem_wgrad_kernel", flops=2.0 * V * self.Co * 27 * self.Ci):
+                L.mmseg_stem_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, self.Ci, ptr(part), bpart, x.N, x.D, x.H, x.W, self.Co,
+                                   ks, code, s)
+            L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.conv.weight)), bpart,
+                                 ptr(self.flat.grad(self.conv.bias)), self.Co, kp, ks, self.Ci, self.Ci, 27,
+                                 int(accumulate), s)
+            self.flat.mark(self.conv.weight, self.conv.bias)
+            return
         ncols = 27 * self.Cip
         if self.Cip % 32 == 0 and self.Co % 32 == 0:
             # brick path: the library picks the split; we only cap the partials at ~32 MB

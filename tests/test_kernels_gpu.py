@@ -95,29 +95,34 @@ def _check_conv3(dev, dtype, cin, cout, shape):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
-def test_conv3_stem_padded_input(dev, dtype):
-    """first conv: 1-2 real input channels packed into an 8-channel NDHWC tile"""
+@pytest.mark.parametrize("cr,co,shape", [
+    (2, 32, (2, 6, 8, 4)),                      # generic path (shape not brick-aligned)
+    (1, 32, (2, 4, 8, 16)), (2, 32, (1, 8, 8, 8)), (3, 16, (1, 4, 16, 8)), (4, 32, (1, 4, 8, 8)),  # stem.hip
+])
+def test_conv3_stem_padded_input(dev, dtype, cr, co, shape):
+    """first conv: 1-4 real input channels packed into an 8-channel NDHWC tile"""
     torch.manual_seed(5)
-    conv = nn.Conv3d(2, 32, 3, padding=1).to(dev)
+    conv = nn.Conv3d(cr, co, 3, padding=1).to(dev)
     rt = Runtime(dev, dtype)
     flat = FlatParams(list(conv.parameters()))
     layer = Conv3(rt, conv, flat, cin_pad=8, need_dgrad=False)
-    N, D, H, W = 2, 6, 8, 4
-    x = torch.randn(N, 2, D, H, W, device=dev)
+    N, D, H, W = shape
+    x = torch.randn(N, cr, D, H, W, device=dev)
     xa = rt.act(N, D, H, W, 8)
-    lib().mmseg_pack_input(ptr(x), 2, 0, 2, N, D * H * W, xa.ptr, rt.code, stream_handle())
-    ya = rt.act(N, D, H, W, 32)
+    lib().mmseg_pack_input(ptr(x), cr, 0, cr, N, D * H * W, xa.ptr, rt.code, stream_handle())
+    ya = rt.act(N, D, H, W, co)
     layer.pack()
     layer.fwd(xa, ya)
     xd = _q(x, dtype)
     wd = _q(conv.weight, dtype).requires_grad_(True)
     bd = conv.bias.detach().double().cpu().requires_grad_(True)
     ref = F.conv3d(xd, wd, bd, padding=1)
-    assert rel(from_ndhwc(ya.buf, N, 32, D, H, W), ref) < TOL[dtype]
+    assert rel(from_ndhwc(ya.buf, N, co, D, H, W), ref) < TOL[dtype]
     dy = torch.randn(ref.shape, device=dev)
     layer.bwd(xa, _act(dy, dtype), None, accumulate=False)
     (ref * _q(dy, dtype)).sum().backward()
     assert rel(flat.grad(conv.weight), wd.grad) < GTOL[dtype]
+    assert rel(flat.grad(conv.bias), bd.grad) < GTOL[dtype]
 
 
 @pytest.mark.parametrize("dtype", DTYPES)

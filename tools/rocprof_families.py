@@ -41,7 +41,7 @@ def family(name: str) -> str:
         return f"conv_gemm_kernel<{_MODES[m.group(1)]},{tile}>[{dt}]"
     if "wgrad_brick_kernel" in name:
         return f"wgrad_brick_kernel[{dt}]"
-    m = re.search(r"wgrad_kernelI(?:DF16b|f)Li(\d)E", name)
+    m = re.search(r"(?<![a-z_])wgrad_kernelI(?:DF16b|f)Li(\d)E", name)
     if m:
         return f"wgrad_kernel<{_MODES[m.group(1)]}>[{dt}]"
     m = re.search(r"(?:_GLOBAL__N_1\d+|::)([A-Za-z_][A-Za-z0-9_]*?)(?:I|\(|E|$)", name)
