@@ -88,6 +88,18 @@ int mmseg_stem_fwd(const void* x, int ldx, int cr, const float* w, const float* 
 int mmseg_stem_wgrad(const void* dy, int lddy, const void* x, int ldx, int cr, float* part, float* bias_part, int N,
                      int D, int H, int W, int Co, int ksplit, int dtype, void* stream);
 
+/* Fused InstanceNorm statistics (unet.py:34 InstanceNorm3d following each Conv3d): when the CONV3 brick kernel
+ * for a shape can emit them, mmseg_conv3_stats_bricks returns the bricks per sample (value-returning, 0 = not
+ * available) and mmseg_conv_gemm_stats writes stats_part[N][bricks][Ncols][2] = per-brick (mean, M2) of the stored
+ * outputs; mmseg_instnorm_stats_bricks turns them into mean / rstd, replacing the statistics pass over the output. */
+int mmseg_conv3_stats_bricks(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,
+                             int dtype);
+int mmseg_conv_gemm_stats(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
+                          float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H,
+                          int W, int ksplit, float* stats_part, int dtype, void* stream);
+int mmseg_instnorm_stats_bricks(const float* part, int N, int C, int nb, int cnt, float eps, float* mean, int mean_ld,
+                                float* rstd, void* stream);
+
 /* Weight-gradient partials part[ksplit][Ca][Ncols] (fp32), K = voxels.
  * Replaces convolution_backward (grad_weight) of the same layers; with
  * bias_part != NULL (a = dy) also the grad_bias partials bias_part[ksplit][Ca]. */

@@ -45,7 +45,47 @@ struct GemmArgs {
   int D, H, W;               // row grid
   int ksplit, kg_per_split;  // k-groups per split (multiple of 4)
   int swz;                   // XCD-aware block remap
+  float* stats;              // brick kernels, ksplit == 1: per-brick InstanceNorm partials (mean, M2), or null
 };
+
+// Per-brick InstanceNorm statistics of a staged output tile (fused into the
+// brick conv epilogue, so the IN stats pass never re-reads the conv output).
+// El: [rows][EP] staged outputs (already rounded to the storage type, i.e. the
+// exact values InstanceNorm will read); channel c = tid % BN, voxel slices
+// tid / BN.  Two passes over LDS (mean, then sum of squared deviations), fixed
+// order -> deterministic.  out[(brick * C + col) * 2 + {0, 1}] = (mean, M2).
+template <typename T, int BN>
+__device__ __forceinline__ void brick_in_stats(const T* El, int EP, int rows, float* red, float* out, long long brick,
+                                               int n0, int C) {
+  constexpr int S = 256 / BN;
+  const int tid = threadIdx.x, c = tid % BN, sl = tid / BN;
+  float a = 0.f;
+  for (int v = sl; v < rows; v += S) a += (float)El[v * EP + c];
+  red[tid] = a;
+  __syncthreads();
+  if (tid < BN) {
+    float t = 0.f;
+    for (int k = 0; k < S; ++k) t += red[k * BN + tid];
+    red[256 + tid] = t / (float)rows;
+  }
+  __syncthreads();
+  const float mu = red[256 + c];
+  float q = 0.f;
+  for (int v = sl; v < rows; v += S) {
+    const float d = (float)El[v * EP + c] - mu;
+    q = fmaf(d, d, q);
+  }
+  __syncthreads();
+  red[tid] = q;
+  __syncthreads();
+  if (tid < BN && n0 + tid < C) {
+    float t = 0.f;
+    for (int k = 0; k < S; ++k) t += red[k * BN + tid];
+    float* o = out + (brick * C + n0 + tid) * 2;
+    o[0] = red[256 + tid];
+    o[1] = t;
+  }
+}
 
 template <typename T>
 __device__ __forceinline__ void mfma_step(f32x4& acc, const V8<T>& a, const V8<T>& b);
@@ -619,7 +659,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kern
   // epilogue: acc (+bias) -> LDS tile [BZ*64 voxels][BN] -> 16-B vector stores
   T* El = reinterpret_cast<T*>(lds4);
   constexpr int EP = BN + 8;   // padded pitch (elements)
-  static_assert(BZ * 64 * (BN + 8) * sizeof(T) <= LQ * 16, "epilogue tile must fit");
+  static_assert(BZ * 64 * (BN + 8) * sizeof(T) + 2048 <= LQ * 16, "epilogue tile (+ stats scratch) must fit");
 #pragma unroll
   for (int j = 0; j < RN; ++j) {
     const int col = j * 16 + r16;
@@ -633,6 +673,11 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kern
       }
   }
   __syncthreads();
+  if (g.stats) {
+    float* red = reinterpret_cast<float*>(El + BZ * 64 * EP);
+    const long long brick = (long long)n * (bz_n * by_n * bx_n) + ((long long)bz * by_n + by) * bx_n + bx;
+    brick_in_stats<T, BN>(El, EP, BZ * 64, red, g.stats, brick, n0, g.Ncols);
+  }
   T* O = reinterpret_cast<T*>(g.out);
   constexpr int CG = BN / 8;                  // 8-column groups per voxel
   constexpr int O_ITEMS = BZ * 64 * CG;
@@ -842,6 +887,11 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kern
         for (int r = 0; r < 4; ++r) El[(wave * 64 + i * 16 + kg * 4 + r) * EP + col] = from_f<T>(acc[i][j][r] + bv);
     }
     __syncthreads();
+    if (g.stats) {
+      float* red = reinterpret_cast<float*>(El + 256 * EP);
+      const long long brick = (long long)n * (bz_n * by_n * bx_n) + ((long long)bzi * by_n + byi) * bx_n + bxi;
+      brick_in_stats<T, BN>(El, EP, rows, red, g.stats, brick, n0, g.Ncols);
+    }
     T* O = reinterpret_cast<T*>(g.out);
     constexpr int CG = BN / 8;
     for (int e = tid; e < rows * CG; e += 256) {
@@ -2089,9 +2139,43 @@ int mmseg_pack_weights_batched(const void* descs, int n, long long total, int dt
 }
 
 // Generic implicit-GEMM: conv3 fwd / dgrad, 1x1, convT fwd / dgrad.
+// Bricks per sample whose InstanceNorm partials the CONV3 kernel for this shape
+// can emit from its epilogue (mmseg_conv_gemm_stats), or 0 when it cannot
+// (gather GEMM, split-K).  Every brick holds V / (bricks per sample) voxels.
+int mmseg_conv3_stats_bricks(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,
+                             int dtype) {
+  if (!knob("MMSEG_FUSED_STATS", 0)) return 0;   // off by default: no net gain measured (bench r01 q11)
+  const int tsize = dtype == MMSEG_BF16 ? 2 : 4;
+  const Conv3Plan p = plan_conv3(M, Ncols, 8 << cpg_shift, D, H, W, lda, ldo, tsize);
+  if (p.kind == 2) return p.ks == 1 ? (D / p.bz) * (H / p.by) * (W / p.bx) : 0;
+  if (p.kind == 1) {
+    const int nb1 = (M / (D * H * W)) * (D / 4) * (H / B2_Y) * (W / B2_X);
+    const bool bn64 = Ncols % 64 == 0 && nb1 * (Ncols / 64) >= knob("MMSEG_BRICK2_MINBLK", 512);
+    const int zw = (!bn64 && tsize == 2 && D % 8 == 0 && knob("MMSEG_BRICK2_ZW", 1) == 2) ? 2 : 1;
+    return (D / (4 * zw)) * (H / B2_Y) * (W / B2_X);
+  }
+  return 0;
+}
+
+int mmseg_conv_gemm_stats(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
+                          float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H,
+                          int W, int ksplit, float* stats_part, int dtype, void* stream);
+
 int mmseg_conv_gemm(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
                     float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W,
                     int ksplit, int dtype, void* stream) {
+  return mmseg_conv_gemm_stats(a, lda, wpacked, bias, out, ldo, splitk_ws, mode, M, Ncols, Cpad, KG, cpg_shift, D, H,
+                               W, ksplit, nullptr, dtype, stream);
+}
+
+// mmseg_conv_gemm + per-brick InstanceNorm partials of the output (stats_part:
+// [N][bricks per sample][Ncols][2] floats, see mmseg_conv3_stats_bricks).
+int mmseg_conv_gemm_stats(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
+                          float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H,
+                          int W, int ksplit, float* stats_part, int dtype, void* stream) {
+  MMSEG_REQUIRE(!stats_part || (mode == MODE_CONV3 && ksplit == 1 &&
+                                mmseg_conv3_stats_bricks(M, Ncols, Cpad, KG, cpg_shift, D, H, W, lda, ldo, dtype) > 0),
+                "conv_gemm_stats: fused statistics need a brick kernel without split-K for this shape");
   MMSEG_REQUIRE(lda % 8 == 0 && ldo >= 1, "conv_gemm: lda must be a multiple of 8 (got %d)", lda);
   MMSEG_REQUIRE(Cpad >= ((Ncols + (Ncols >= 64 ? 63 : 31)) / (Ncols >= 64 ? 64 : 32)) * (Ncols >= 64 ? 64 : 32),
                 "conv_gemm: packed weights must be padded to the column tile (Cpad=%d, Ncols=%d)", Cpad, Ncols);
@@ -2101,7 +2185,7 @@ int mmseg_conv_gemm(const void* a, int lda, const void* wpacked, const float* bi
   int kps = ((ceil_div(KGp, ksplit) + 3) / 4) * 4;
   ksplit = ceil_div(KGp, kps);
   GemmArgs g{a, lda, wpacked, bias, out, ldo, splitk_ws, M, Ncols, Cpad, KG, cpg_shift, D, H, W, ksplit, kps,
-             knob("MMSEG_SWIZZLE", 1)};
+             knob("MMSEG_SWIZZLE", 1), stats_part};
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16) return launch_gemm_mode<bf16_t>(g, mode, s);
   return launch_gemm_mode<float>(g, mode, s);

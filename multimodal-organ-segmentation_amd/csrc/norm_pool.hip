@@ -153,6 +153,31 @@ __global__ void in_stats_finalize(const T* __restrict__ x, int ld, long long V, 
   if (rstd) rstd[idx] = (float)(1.0 / sqrt(var + (double)eps));
 }
 
+// Statistics from equal-count per-brick partials (mean_b, M2_b) written by the
+// brick conv epilogue: one wave per (n, c); mean = avg(mean_b), M2 = sum M2_b +
+// cnt * sum (mean_b - mean)^2 (Chan for equal counts), fp64, fixed lane order.
+__global__ void in_stats_from_bricks(const float* __restrict__ part, int N, int C, int nb, int cnt, float eps,
+                                     float* __restrict__ mean, int mean_ld, float* __restrict__ rstd) {
+  const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (idx >= N * C) return;
+  const int n = idx / C, c = idx - n * C;
+  const float* p = part + ((long long)n * nb * C + c) * 2;
+  double sm = 0.0;
+  for (int b = lane; b < nb; b += 64) sm += (double)p[(long long)b * C * 2];
+  sm = wave_sum_d(sm);
+  const double mu = sm / (double)nb;
+  double m2 = 0.0;
+  for (int b = lane; b < nb; b += 64) {
+    const double d = (double)p[(long long)b * C * 2] - mu;
+    m2 += (double)p[(long long)b * C * 2 + 1] + (double)cnt * d * d;
+  }
+  m2 = wave_sum_d(m2);
+  if (lane != 0) return;
+  mean[(long long)n * mean_ld + c] = (float)mu;
+  if (rstd) rstd[idx] = (float)(1.0 / sqrt(m2 / ((double)nb * cnt) + (double)eps));
+}
+
 // y = relu((x - mean) * rstd); a thread owns 8 channels of one sample (their
 // mean / rstd stay in registers) and UNR voxels per step; grid (chunks, N).
 template <typename T>
@@ -691,6 +716,15 @@ int mmseg_instnorm_stats(const void* x, int ldx, int N, long long V, int C, floa
                        N, C, nch, vpc, ws, eps, mean, mean_ld, rstd);
   }
   return mmseg::check_launch("instnorm_stats");
+}
+
+// mean / rstd from the per-brick partials of mmseg_conv_gemm_stats (nb bricks of cnt voxels per sample).
+int mmseg_instnorm_stats_bricks(const float* part, int N, int C, int nb, int cnt, float eps, float* mean, int mean_ld,
+                                float* rstd, void* stream) {
+  MMSEG_REQUIRE(nb >= 1 && cnt >= 1, "instnorm_stats_bricks: nb, cnt >= 1");
+  hipLaunchKernelGGL(in_stats_from_bricks, dim3(ceil_div(N * C, 4)), dim3(256), 0, (hipStream_t)stream, part, N, C,
+                     nb, cnt, eps, mean, mean_ld, rstd);
+  return mmseg::check_launch("instnorm_stats_bricks");
 }
 
 int mmseg_instnorm_relu_fwd(const void* x, int ldx, void* y, int ldy, int N, long long V, int C, const float* mean,

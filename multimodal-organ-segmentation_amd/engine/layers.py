@@ -143,7 +143,20 @@ class Conv3:
         return (not self.need_dgrad and self.Cip == 8 and os.environ.get("MMSEG_STEM", "1") != "0"
                 and bool(self.rt.lib.mmseg_stem_ok(self.Ci, self.Co, x.D, x.H, x.W, x.ld, y_ld)))
 
-    def fwd(self, x: Act, y: Act):
+    def stats_bricks(self, x: Act, y: Act) -> int:
+        """Bricks per sample for which fwd() can emit fused InstanceNorm partials (0 = not available)."""
+        if self._stem(x, y.ld):
+            return 0
+        return self.rt.lib.mmseg_conv3_stats_bricks(x.N * x.V, self.Co, self.Cpad, self.KG, self.cpg_shift, x.D, x.H,
+                                                    x.W, x.ld, y.ld, self.rt.code)
+
+    def fwd(self, x: Act, y: Act, stats_part: Optional[torch.Tensor] = None):
+        if stats_part is not None:
+            with TIMER.region(_gemm_name(self.rt, self.Co, "conv3"), flops=2.0 * x.N * x.V * self.Co * 27 * self.Ci):
+                self.rt.lib.mmseg_conv_gemm_stats(x.ptr, x.ld, ptr(self.wf), ptr(self.conv.bias), y.ptr, y.ld, None,
+                                                  MODE_CONV3, x.N * x.V, self.Co, self.Cpad, self.KG, self.cpg_shift,
+                                                  x.D, x.H, x.W, 1, ptr(stats_part), self.rt.code, self.rt.stream)
+            return
         if self._stem(x, y.ld):
             with TIMER.region("stem_fwd_kernel", flops=2.0 * x.N * x.V * self.Co * 27 * self.Ci):
                 self.rt.lib.mmseg_stem_fwd(x.ptr, x.ld, self.Ci, ptr(self.conv.weight), ptr(self.conv.bias), y.ptr,
@@ -324,11 +337,15 @@ class Block:
         self.y1 = rt.act(N, D, H, W, C)
         self.x2 = rt.act(N, D, H, W, C)
         self.stats = torch.empty(4, N * C, dtype=torch.float32, device=rt.device)  # m1, r1, m2, r2
+        self.nb = None   # fused-statistics bricks per sample of (conv1, conv2), set on the first forward
 
-    def _norm_fwd(self, x: Act, y: Act, m: torch.Tensor, r: torch.Tensor):
+    def _norm_fwd(self, x: Act, y: Act, m: torch.Tensor, r: torch.Tensor, part=None, nb: int = 0):
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
-        ws = self.rt.ws(L.mmseg_instnorm_ws_floats(x.N, x.V, x.C))
-        L.mmseg_instnorm_stats(x.ptr, x.ld, x.N, x.V, x.C, IN_EPS, ptr(m), x.C, ptr(r), ptr(ws), code, s)
+        if part is not None:
+            L.mmseg_instnorm_stats_bricks(ptr(part), x.N, x.C, nb, x.V // nb, IN_EPS, ptr(m), x.C, ptr(r), s)
+        else:
+            ws = self.rt.ws(L.mmseg_instnorm_ws_floats(x.N, x.V, x.C))
+            L.mmseg_instnorm_stats(x.ptr, x.ld, x.N, x.V, x.C, IN_EPS, ptr(m), x.C, ptr(r), ptr(ws), code, s)
         L.mmseg_instnorm_relu_fwd(x.ptr, x.ld, y.ptr, y.ld, x.N, x.V, x.C, ptr(m), ptr(r), code, s)
 
     def _norm_bwd(self, x: Act, m: torch.Tensor, r: torch.Tensor, dy: DySpec, dx: Act):
@@ -348,10 +365,16 @@ class Block:
     def fwd(self, xin: Act, out: Act):
         self.setup(xin.N, xin.D, xin.H, xin.W)
         st = self.stats
-        self.c1.fwd(xin, self.x1)
-        self._norm_fwd(self.x1, self.y1, st[0], st[1])
-        self.c2.fwd(self.y1, self.x2)
-        self._norm_fwd(self.x2, out, st[2], st[3])
+        if self.nb is None:
+            self.nb = (self.c1.stats_bricks(xin, self.x1), self.c2.stats_bricks(self.y1, self.x2))
+            n = max(self.nb)
+            self.part = torch.empty(xin.N * n * self.Co * 2, dtype=torch.float32, device=self.rt.device) if n else None
+        p1 = self.part if self.nb[0] else None
+        p2 = self.part if self.nb[1] else None
+        self.c1.fwd(xin, self.x1, stats_part=p1)
+        self._norm_fwd(self.x1, self.y1, st[0], st[1], p1, self.nb[0])
+        self.c2.fwd(self.y1, self.x2, stats_part=p2)
+        self._norm_fwd(self.x2, out, st[2], st[3], p2, self.nb[1])
 
     def bwd(self, xin: Act, dy: DySpec, dxin: Optional[Act], accumulate: bool):
         st = self.stats

@@ -360,3 +360,41 @@ def test_batched_conv3_pack_matches_per_layer_pack(dev, dtype):
         assert torch.equal(wf.view(torch.int16) if dtype == torch.bfloat16 else wf, ref_f.view(torch.int16) if dtype == torch.bfloat16 else ref_f)
         if wd is not None:
             assert torch.equal(wd, l.wd)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("knobs,cin,cout,shape", [
+    ({"MMSEG_FUSED_STATS": "1"}, 32, 32, (2, 8, 8, 16)),                              # brick2 BN32
+    ({"MMSEG_FUSED_STATS": "1", "MMSEG_BRICK2_MINBLK": "0"}, 32, 64, (1, 4, 8, 8)),   # brick2 BN64
+    ({"MMSEG_FUSED_STATS": "1", "MMSEG_BRICK2_ZW": "2"}, 32, 32, (1, 8, 8, 8)),      # brick2 ZW2 (bf16 only)
+    ({"MMSEG_FUSED_STATS": "1"}, 64, 64, (2, 6, 6, 6)),                               # runtime brick, no split
+])
+def test_conv3_fused_instnorm_stats(dev, dtype, knobs, cin, cout, shape, monkeypatch):
+    """per-brick (mean, M2) from the conv epilogue + mmseg_instnorm_stats_bricks == InstanceNorm statistics of the
+    stored output (fp64 reference on the same stored values)."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    torch.manual_seed(cin * 7 + cout)
+    conv = nn.Conv3d(cin, cout, 3, padding=1).to(dev)
+    rt = Runtime(dev, dtype)
+    flat = FlatParams(list(conv.parameters()))
+    layer = Conv3(rt, conv, flat)
+    N, D, H, W = shape
+    x = torch.randn(N, cin, D, H, W, device=dev)
+    xa = _act(x, dtype)
+    ya = rt.act(N, D, H, W, cout)
+    layer.pack()
+    nb = layer.stats_bricks(xa, ya)
+    if nb == 0:
+        pytest.skip("no fused-statistics kernel for this shape/dtype")
+    part = torch.empty(N * nb * cout * 2, device=dev)
+    layer.fwd(xa, ya, stats_part=part)
+    mean = torch.empty(N * cout, device=dev)
+    rstd = torch.empty(N * cout, device=dev)
+    lib().mmseg_instnorm_stats_bricks(ptr(part), N, cout, nb, D * H * W // nb, 1e-5, ptr(mean), cout, ptr(rstd),
+                                      stream_handle())
+    y = from_ndhwc(ya.buf, N, cout, D, H, W).double().cpu().reshape(N, cout, -1)
+    m_ref = y.mean(-1)
+    r_ref = 1.0 / torch.sqrt(y.var(-1, unbiased=False) + 1e-5)
+    assert rel(mean.cpu().reshape(N, cout), m_ref) < 1e-5
+    assert rel(rstd.cpu().reshape(N, cout), r_ref) < 1e-5
