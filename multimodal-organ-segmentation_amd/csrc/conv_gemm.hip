@@ -1636,6 +1636,248 @@ __global__ __launch_bounds__(512, MT == 2 ? 2 : 1) void wgrad_brick2_kernel(Wgra
   }
 }
 
+// ------------------------------------- runtime-brick wgrad (small volumes)
+// wgrad_brick2_kernel for volumes whose sides are not multiples of (4, 4, 8)
+// (the 12^3 and 6^3 levels): brick (bz, by, bx) chosen on the host, <= 128
+// voxels (K of one brick, zero-padded to 128) and a halo of <= 384 voxels.
+// The voxel -> halo-row map of a lane does not depend on the brick, so it is
+// computed once (4 k-steps x 2 rows).
+constexpr int WR_MAXHV = 384;
+
+template <typename T, int MT>
+__global__ __launch_bounds__(512) void wgrad_brickr_kernel(WgradArgs g, int bz, int by, int bx) {
+  constexpr int EP = 16 / sizeof(T);
+  constexpr int CO = MT * 16, CG = CO / 8;
+  constexpr int DP = CO + EP;
+  constexpr int XP = CK + EP;
+  constexpr int DS = 128 * DP, XS = WR_MAXHV * XP;
+  __shared__ __attribute__((aligned(16))) T lds[2 * (DS + XS)];
+  constexpr int D_ITEMS = 128 * CG, X_MAX = WR_MAXHV * 4;
+  constexpr int D_PER = (D_ITEMS + 511) / 512, X_PER = (X_MAX + 511) / 512;
+
+  const T* Dy = reinterpret_cast<const T*>(g.a);
+  const T* X = reinterpret_cast<const T*>(g.b);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cin = 8 << g.cpg_shift;
+  const int nchunk = cin / CK, rt_n = g.Ca / CO;
+  const int tile = blockIdx.x;
+  const int ct = tile % nchunk, rt = (tile / nchunk) % rt_n, ks = tile / (nchunk * rt_n);
+  const int HX = bx + 2, HY = by + 2, HZ = bz + 2;
+  const int HV = HZ * HY * HX, rows = bz * by * bx;
+  const int bz_n = g.D / bz, by_n = g.H / by, bx_n = g.W / bx;
+  const long long nbrick = (g.V / ((long long)g.D * g.H * g.W)) * bz_n * by_n * bx_n;
+  const long long bpk = (nbrick + g.ksplit - 1) / g.ksplit;
+  const long long b_begin = ks * bpk;
+  const long long b_end = b_begin + bpk < nbrick ? b_begin + bpk : nbrick;
+  const long long HW = (long long)g.H * g.W;
+  const int row0 = rt * CO, c0 = ct * CK;
+  const bool do_bias = g.bias_part != nullptr && ct == 0;
+  const int t_begin = wave < 3 ? 4 * wave : 12 + 3 * (wave - 3);
+  const int t_cnt = wave < 3 ? 4 : 3;
+
+  f32x4 acc[4][MT][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[t][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float bsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  auto vox_halo = [&](int v) {   // brick voxel -> halo row (tap 0); padding voxels map to row 0 (dy is 0 there)
+    if (v >= rows) return 0;
+    const int rx = v % bx, q = v / bx;
+    return ((q / by) * HY + q % by) * HX + rx;
+  };
+
+  V8<T> dr[D_PER], xr[X_PER];
+  auto load = [&](long long b) {
+    const int bxi = (int)(b % bx_n);
+    long long q = b / bx_n;
+    const int byi = (int)(q % by_n);
+    q /= by_n;
+    const int bzi = (int)(q % bz_n);
+    const long long nbase = (q / bz_n) * g.D * HW;
+    const int z0 = bzi * bz, y0 = byi * by, x0 = bxi * bx;
+#pragma unroll
+    for (int k = 0; k < D_PER; ++k) {
+      const int e = tid + k * 512, v = e / CG, cg = e % CG;
+      if (e < D_ITEMS) {
+        if (v < rows) {
+          const int rx = v % bx, qq = v / bx;
+          const int ry = qq % by, rz = qq / by;
+          dr[k].load(Dy + (nbase + (z0 + rz) * HW + (long long)(y0 + ry) * g.W + x0 + rx) * g.lda + row0 + cg * 8);
+        } else {
+          dr[k].zero();
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < X_PER; ++k) {
+      const int e = tid + k * 512;
+      if (e < HV * 4) {
+        const int h = e >> 2, cg = e & 3;
+        const int hx = h % HX, qq = h / HX;
+        const int hy = qq % HY, hz = qq / HY;
+        const int z = z0 - 1 + hz, y = y0 - 1 + hy, x = x0 - 1 + hx;
+        if ((unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W)
+          xr[k].load(X + (nbase + z * HW + (long long)y * g.W + x) * g.ldb + c0 + cg * 8);
+        else
+          xr[k].zero();
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    T* Dl = lds + buf * (DS + XS);
+    T* Xl = Dl + DS;
+#pragma unroll
+    for (int k = 0; k < D_PER; ++k) {
+      const int e = tid + k * 512;
+      if (e < D_ITEMS) {
+        dr[k].store(Dl + (e / CG) * DP + (e % CG) * 8);
+        if (do_bias) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bsum[j] += dr[k].get(j);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < X_PER; ++k) {
+      const int e = tid + k * 512;
+      if (e < HV * 4) xr[k].store(Xl + (e >> 2) * XP + (e & 3) * 8);
+    }
+  };
+
+  const int g4 = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
+  int hlo[4], hhi[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    hlo[s] = vox_halo(s * 32 + 8 * g4 + q4);
+    hhi[s] = vox_halo(s * 32 + 8 * g4 + q4 + 4);
+  }
+  int toff[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int tap = t_begin + (t < t_cnt ? t : 0);
+    toff[t] = ((tap / 9) * HY + (tap / 3) % 3) * HX + tap % 3;
+  }
+  int buf = 0;
+  if (b_begin < b_end) {
+    load(b_begin);
+    store(0);
+  }
+  __syncthreads();
+  for (long long b = b_begin; b < b_end; ++b) {
+    const bool more = b + 1 < b_end;
+    if (more) load(b + 1);
+    const T* Dl = lds + buf * (DS + XS);
+    const T* Xl = Dl + DS;
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        if (s * 32 >= rows) break;
+        bf16x8 af[MT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          const bf16_t* base = (const bf16_t*)Dl + (s * 32 + 8 * g4 + q4) * DP + i * 16 + 4 * p4;
+          af[i] = tr_frag(base, base + 4 * DP);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (t < t_cnt) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const bf16_t* pl = (const bf16_t*)Xl + (hlo[s] + toff[t]) * XP + j * 16 + 4 * p4;
+              const bf16_t* ph = (const bf16_t*)Xl + (hhi[s] + toff[t]) * XP + j * 16 + 4 * p4;
+              const bf16x8 bfr = tr_frag(pl, ph);
+#pragma unroll
+              for (int i = 0; i < MT; ++i)
+                acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[t][i][j], 0, 0, 0);
+            }
+          }
+        }
+      }
+    } else {
+      for (int kk = 0; kk < rows; kk += 4) {
+        const int v = kk + g4;
+        const int hv = vox_halo(v);
+        float af[MT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) af[i] = (float)Dl[v * DP + i * 16 + i16];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (t < t_cnt) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const float bv = (float)Xl[(hv + toff[t]) * XP + j * 16 + i16];
+#pragma unroll
+              for (int i = 0; i < MT; ++i)
+                acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bv, acc[t][i][j], 0, 0, 0);
+            }
+          }
+        }
+      }
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (t >= t_cnt) continue;
+    const int tap = t_begin + t;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = tap * cin + c0 + j * 16 + i16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = row0 + i * 16 + g4 * 4 + r;
+          g.part[((long long)ks * g.Ca + row) * g.Ncols + col] = acc[t][i][j][r];
+        }
+      }
+  }
+  if (do_bias) {
+    float* red = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[tid * 8 + j] = bsum[j];
+    __syncthreads();
+    if (tid < CO) {
+      const int cg = tid >> 3, j = tid & 7;
+      float sacc = 0.f;
+      for (int t = cg; t < 512; t += CG) sacc += red[t * 8 + j];
+      g.bias_part[(long long)ks * g.Ca + row0 + tid] = sacc;
+    }
+  }
+}
+
+struct WBrick { int bz, by, bx; };
+
+// Runtime brick for the small-volume wgrad: divisors of (D, H, W), <= 128 voxels,
+// halo <= WR_MAXHV; the most voxels wins.  {0,0,0} = none.
+WBrick plan_wgrad_brickr(int D, int H, int W) {
+  WBrick best{0, 0, 0};
+  int brows = 0;
+  for (int bz = 1; bz <= D && bz <= 16; ++bz) {
+    if (D % bz) continue;
+    for (int by = 1; by <= H && by <= 16; ++by) {
+      if (H % by) continue;
+      for (int bx = 1; bx <= W && bx <= 16; ++bx) {
+        if (W % bx) continue;
+        const int rows = bz * by * bx;
+        if (rows > 128 || (bz + 2) * (by + 2) * (bx + 2) > WR_MAXHV) continue;
+        if (rows > brows) {
+          brows = rows;
+          best = {bz, by, bx};
+        }
+      }
+    }
+  }
+  return brows >= 32 ? best : WBrick{0, 0, 0};
+}
+
 // part[ks][row][col] -> torch-layout gradient (fixed-order sum over ks).
 //   CONV3 : grad[co][ci][tap]    row=co, col = tap*Cin_pad + ci, ci < Cin_real
 //   POINT : grad[co][ci]         row=co, col = ci
@@ -1651,41 +1893,66 @@ struct WReduceArgs {
   int accumulate;
 };
 
-// 256 threads = 64 consecutive partial-layout elements x 4 split slices: slice
-// s sums splits k = s, s+4, ... (coalesced 256-B loads, 4x the loads in
-// flight of one thread per element), then the 4 slice sums are added in order.
-__global__ void wgrad_reduce_kernel(WReduceArgs g, int mode) {
-  __shared__ float red[4][64];
-  const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const long long idx = (long long)blockIdx.x * 64 + lane;
-  const long long total = (long long)g.Ca * g.Ncols;     // enumerate the partial layout: coalesced reads
-  const long long nout = total + (g.bias_part ? g.Ca : 0);
-  float v = 0.f;
-  if (idx < total) {
-    const float* p = g.part + idx;
+// 256 threads = (256/S) float4 columns x S split slices: slice s sums splits
+// k = s, s+S, ... with 16-B loads, then the S slice sums are added in slice
+// order -> deterministic.  S follows ksplit (1 for a few splits, up to 64 for
+// thousands), so every thread has a few independent loads in flight.  Bias
+// partials ([ks][Ca], after the weight columns) are summed by the blocks past
+// the weight range.
+template <int S>
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(WReduceArgs g) {
+  constexpr int NC = 256 / S;                 // float4 columns per block
+  __shared__ float4 red[S][NC];
+  const int col4 = threadIdx.x % NC, sl = threadIdx.x / NC;
+  const long long total = (long long)g.Ca * g.Ncols;   // multiple of 4
+  const long long e0 = ((long long)blockIdx.x * NC + col4) * 4;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e0 < total) {
+    const float4* p = reinterpret_cast<const float4*>(g.part + e0);
+    const long long stride4 = total / 4;
 #pragma unroll 4
-    for (int k = sl; k < g.ksplit; k += 4) v += p[(long long)k * total];
-  } else if (idx < nout) {
-    const int row = (int)(idx - total);
-    for (int k = sl; k < g.ksplit; k += 4) v += g.bias_part[(long long)k * g.Ca + row];
+    for (int k = sl; k < g.ksplit; k += S) {
+      const float4 a = p[(long long)k * stride4];
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+  } else if (g.bias_part) {
+    const long long r0 = e0 - total;   // bias rows r0 .. r0+3
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (r0 + q >= g.Ca) break;
+      float a = 0.f;
+      for (int k = sl; k < g.ksplit; k += S) a += g.bias_part[(long long)k * g.Ca + r0 + q];
+      (&v.x)[q] = a;
+    }
   }
-  red[sl][lane] = v;
-  __syncthreads();
-  if (sl != 0 || idx >= nout) return;
-  v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
-  if (idx >= total) {
-    const int row = (int)(idx - total);
-    g.bias_grad[row] = g.accumulate ? g.bias_grad[row] + v : v;
-    return;
+  if (S > 1) {
+    red[sl][col4] = v;
+    __syncthreads();
+    if (sl != 0) return;
+#pragma unroll
+    for (int k = 1; k < S; ++k) {
+      const float4 a = red[k][col4];
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
   }
-  const int row = (int)(idx / g.Ncols);
-  const int col = (int)(idx - (long long)row * g.Ncols);
-  const int t = col / g.cpad, c = col - t * g.cpad;
-  if (c >= g.creal || t >= g.ntap) return;
-  // torch layout [row][c_real][tap]
-  const long long dst = ((long long)row * g.creal + c) * g.ntap + t;
-  if (g.accumulate) g.grad[dst] += v;
-  else g.grad[dst] = v;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const long long idx = e0 + q;
+    const float val = (&v.x)[q];
+    if (idx >= total) {
+      const long long row = idx - total;
+      if (!g.bias_part || row >= g.Ca) continue;
+      g.bias_grad[row] = g.accumulate ? g.bias_grad[row] + val : val;
+      continue;
+    }
+    const int row = (int)(idx / g.Ncols);
+    const int col = (int)(idx - (long long)row * g.Ncols);
+    const int tt = col / g.cpad, c = col - tt * g.cpad;
+    if (c >= g.creal || tt >= g.ntap) continue;
+    const long long dst = ((long long)row * g.creal + c) * g.ntap + tt;   // torch layout [row][c_real][tap]
+    if (g.accumulate) g.grad[dst] += val;
+    else g.grad[dst] = val;
+  }
 }
 
 // Column sums (bias gradient): db[c] = sum_v dy[v][c], split over voxels.
@@ -2019,6 +2286,20 @@ template <typename T, int MODE>
 int launch_wgrad(WgradArgs g, hipStream_t s) {
   dim3 block(256);
   if constexpr (sizeof(T) == 2) {
+    if (MODE == MODE_CONV3 && g.brick == 3) {
+      const int cin = 8 << g.cpg_shift;
+      const WBrick wb = plan_wgrad_brickr(g.D, g.H, g.W);
+      if (g.Ca % 64 == 0) {
+        dim3 grid((cin / CK) * (g.Ca / 64) * g.ksplit);
+        mmseg::note_kernel("wgrad_brickr_kernel<CO64>");
+        hipLaunchKernelGGL((wgrad_brickr_kernel<T, 4>), grid, dim3(512), 0, s, g, wb.bz, wb.by, wb.bx);
+      } else {
+        dim3 grid((cin / CK) * (g.Ca / 32) * g.ksplit);
+        mmseg::note_kernel("wgrad_brickr_kernel<CO32>");
+        hipLaunchKernelGGL((wgrad_brickr_kernel<T, 2>), grid, dim3(512), 0, s, g, wb.bz, wb.by, wb.bx);
+      }
+      return mmseg::check_launch("wgrad_brickr");
+    }
     if (MODE == MODE_CONV3 && g.brick == 2) {
       const int cin = 8 << g.cpg_shift;
       if (g.Ca % 64 == 0) {
@@ -2064,25 +2345,31 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
   return mmseg::check_launch("wgrad");
 }
 
-// 0: generic wgrad_kernel, 1: wgrad_brick_kernel (32 co), 2: wgrad_brick2_kernel (64 co)
-// (v2 is bf16 only: its two fp32 stage buffers would not fit in LDS)
+// 0: generic wgrad_kernel, 1: wgrad_brick_kernel (32 co), 2: wgrad_brick2_kernel (64 / 32 co),
+// 3: wgrad_brickr_kernel (runtime brick, small volumes).
+// (v2 / runtime brick are bf16 only: their two fp32 stage buffers would not fit in LDS)
 int wgrad_brick_ok(int Ca, int cpg_shift, int D, int H, int W, int lda, int ldb, int dtype) {
   const int k = knob("MMSEG_WGRAD_BRICK", 2);
-  if (!(k && Ca % 32 == 0 && (8 << cpg_shift) % CK == 0 && D % BRK_Z == 0 && H % BRK_Y == 0 && W % BRK_X == 0 &&
-        lda % 8 == 0 && ldb % 8 == 0))
-    return 0;
-  return (k >= 2 && dtype == MMSEG_BF16 && (Ca % 64 == 0 || knob("MMSEG_WGRAD_BRICK2_CO32", 1))) ? 2 : 1;
+  if (!(k && Ca % 32 == 0 && (8 << cpg_shift) % CK == 0 && lda % 8 == 0 && ldb % 8 == 0)) return 0;
+  if (D % BRK_Z == 0 && H % BRK_Y == 0 && W % BRK_X == 0)
+    return (k >= 2 && dtype == MMSEG_BF16 && (Ca % 64 == 0 || knob("MMSEG_WGRAD_BRICK2_CO32", 1))) ? 2 : 1;
+  if (k >= 2 && dtype == MMSEG_BF16 && knob("MMSEG_WGRAD_BRICKR", 1) && plan_wgrad_brickr(D, H, W).bz) return 3;
+  return 0;
 }
 
 // Split count of the CONV3 brick wgrad: enough blocks to fill the chip, capped by
 // the caller's workspace (cap) and by one brick per split.
-int brick_wgrad_splits(long long V, int cap, int Ca, int cpg_shift, int kind) {
+int brick_wgrad_splits(long long V, int cap, int Ca, int cpg_shift, int kind, int D, int H, int W) {
   const int nchunk = (8 << cpg_shift) / CK;
-  const int tiles = nchunk * (Ca / ((kind == 2 && Ca % 64 == 0) ? 64 : 32));
-  const int target = kind == 2 ? 512 : 1024;
+  const int tiles = nchunk * (Ca / ((kind >= 2 && Ca % 64 == 0) ? 64 : 32));
+  const int target = kind >= 2 ? 512 : 1024;
   long long ks = (target + tiles - 1) / tiles;
   if (ks > cap) ks = cap;
-  const long long nbrick = V / 128;
+  long long nbrick = V / 128;
+  if (kind == 3) {
+    const WBrick wb = plan_wgrad_brickr(D, H, W);
+    nbrick = V / (wb.bz * wb.by * wb.bx);
+  }
   if (ks > nbrick) ks = nbrick;
   if (ks < 1) ks = 1;
   const long long bpk = (nbrick + ks - 1) / ks;
@@ -2215,7 +2502,7 @@ int mmseg_wgrad(const void* a, int lda, const void* b, int ldb, float* part, flo
   const int brick = mode == MODE_CONV3 ? wgrad_brick_ok(Ca, cpg_shift, D, H, W, lda, ldb, dtype) : 0;
   long long vps = ((V + ksplit - 1) / ksplit + 63) / 64 * 64;
   if (brick) {
-    ksplit = brick_wgrad_splits(V, ksplit, Ca, cpg_shift, brick);
+    ksplit = brick_wgrad_splits(V, ksplit, Ca, cpg_shift, brick, D, H, W);
   } else {
     ksplit = (int)((V + vps - 1) / vps);
   }
@@ -2250,14 +2537,25 @@ int mmseg_wgrad_splits_conv3(long long V, int ksplit, int Ca, int cpg_shift, int
                              int dtype) {
   const int kind = wgrad_brick_ok(Ca, cpg_shift, D, H, W, lda, ldb, dtype);
   if (!kind) return mmseg_wgrad_splits(V, ksplit);
-  return brick_wgrad_splits(V, ksplit, Ca, cpg_shift, kind);
+  return brick_wgrad_splits(V, ksplit, Ca, cpg_shift, kind, D, H, W);
 }
 
 int mmseg_wgrad_reduce(const float* part, float* grad, const float* bias_part, float* bias_grad, int Ca, int Ncols,
                        int ksplit, int cpad, int creal, int ntap, int accumulate, void* stream) {
+  MMSEG_REQUIRE(((long long)Ca * Ncols) % 4 == 0 && (reinterpret_cast<uintptr_t>(part) & 15) == 0,
+                "wgrad_reduce: Ca*Ncols %% 4 == 0 and a 16-B aligned partial buffer");
   WReduceArgs g{part, grad, bias_part, bias_grad, Ca, Ncols, ksplit, cpad, creal, ntap, accumulate};
-  long long total = (long long)Ca * Ncols + (bias_part ? Ca : 0);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(total, 64)), dim3(256), 0, (hipStream_t)stream, g, 0);
+  const long long total = (long long)Ca * Ncols + (bias_part ? Ca : 0);
+  hipStream_t s = (hipStream_t)stream;
+  // slices: ~8+ loads per thread when the splits allow, 1 slice for a handful of splits
+  if (ksplit >= 512)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<64>, dim3(ceil_div(total, 16)), dim3(256), 0, s, g);
+  else if (ksplit >= 64)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<8>, dim3(ceil_div(total, 128)), dim3(256), 0, s, g);
+  else if (ksplit >= 8)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<2>, dim3(ceil_div(total, 512)), dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(ceil_div(total, 1024)), dim3(256), 0, s, g);
   return mmseg::check_launch("wgrad_reduce");
 }
 
