@@ -174,6 +174,7 @@ def main():
         name, a = dom
         avg_ms = a["ms"] / a["launches"]
         flops_per_launch = a["flops"] / a["launches"]
+        bytes_per_launch = a["bytes"] / a["launches"]
         achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
         peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
         traffic, tsrc = pmc_traffic(name)
@@ -182,7 +183,8 @@ def main():
                     "traffic": round(traffic) if traffic is not None else None, "traffic_unit": "B/launch",
                     "traffic_source": tsrc,
                     "avg_launch_ms": round(avg_ms, 4), "launches_per_step": a["launches"] // max(args.timer_steps, 1),
-                    "algorithmic_gflop_per_launch": round(flops_per_launch / 1e9, 3)}
+                    "algorithmic_gflop_per_launch": round(flops_per_launch / 1e9, 3),
+                    "algorithmic_bytes_per_launch": round(bytes_per_launch)}
     families = {k: {"ms_per_step": round(v["ms"] / args.timer_steps, 3),
                     "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1) if v["ms"] > 0 else None}
                 for k, v in sorted(fam.items(), key=lambda kv: -kv[1]["ms"])}

@@ -35,6 +35,13 @@ def _gemm_name(rt: Runtime, ncols: int, mode: str):
     return lambda: f"{rt.lib.mmseg_last_kernel().decode()}[{'bf16' if rt.code else 'f32'}]"
 
 
+def _io_bytes(rt: Runtime, vox: int, cin: int, cout: int, wcount: int, wbytes: int = 2) -> float:
+    """Compulsory HBM bytes of one conv launch: read `cin` channels and write `cout` channels of `vox`
+    voxels at the storage width, plus the weights (`wcount` values of `wbytes`)."""
+    es = rt.dtype.itemsize
+    return float(vox * (cin + cout) * es + wcount * wbytes)
+
+
 def _col_tile(n: int) -> int:
     return round_up(n, 64 if n >= 64 else 32)
 
@@ -152,13 +159,15 @@ class Conv3:
 
     def fwd(self, x: Act, y: Act, stats_part: Optional[torch.Tensor] = None):
         if stats_part is not None:
-            with TIMER.region(_gemm_name(self.rt, self.Co, "conv3"), flops=2.0 * x.N * x.V * self.Co * 27 * self.Ci):
+            with TIMER.region(_gemm_name(self.rt, self.Co, "conv3"), flops=2.0 * x.N * x.V * self.Co * 27 * self.Ci,
+                              nbytes=_io_bytes(self.rt, x.N * x.V, self.Ci, self.Co, 27 * self.Ci * self.Co)):
                 self.rt.lib.mmseg_conv_gemm_stats(x.ptr, x.ld, ptr(self.wf), ptr(self.conv.bias), y.ptr, y.ld, None,
                                                   MODE_CONV3, x.N * x.V, self.Co, self.Cpad, self.KG, self.cpg_shift,
                                                   x.D, x.H, x.W, 1, ptr(stats_part), self.rt.code, self.rt.stream)
             return
         if self._stem(x, y.ld):
-            with TIMER.region("stem_fwd_kernel", flops=2.0 * x.N * x.V * self.Co * 27 * self.Ci):
+            with TIMER.region("stem_fwd_kernel", flops=2.0 * x.N * x.V * self.Co * 27 * self.Ci,
+                              nbytes=_io_bytes(self.rt, x.N * x.V, 8, self.Co, 27 * self.Ci * self.Co, 4)):
                 self.rt.lib.mmseg_stem_fwd(x.ptr, x.ld, self.Ci, ptr(self.conv.weight), ptr(self.conv.bias), y.ptr,
                                            y.ld, x.N, x.D, x.H, x.W, self.Co, self.rt.code, self.rt.stream)
             return
@@ -166,7 +175,8 @@ class Conv3:
         ks = self.rt.lib.mmseg_conv3_splits(M, self.Co, self.Cpad, self.KG, self.cpg_shift, x.D, x.H, x.W, x.ld, y.ld,
                                             self.rt.code)
         ws = self.rt.ws(ks * M * self.Co) if ks > 1 else None
-        with TIMER.region(_gemm_name(self.rt, self.Co, "conv3"), flops=2.0 * M * self.Co * 27 * self.Ci):
+        with TIMER.region(_gemm_name(self.rt, self.Co, "conv3"), flops=2.0 * M * self.Co * 27 * self.Ci,
+                          nbytes=_io_bytes(self.rt, M, self.Cip, self.Co, 27 * self.Cip * self.Co)):
             self.rt.lib.mmseg_conv_gemm(x.ptr, x.ld, ptr(self.wf), ptr(self.conv.bias), y.ptr, y.ld, ptr(ws),
                                         MODE_CONV3, M, self.Co, self.Cpad, self.KG, self.cpg_shift, x.D, x.H, x.W, ks,
                                         self.rt.code, self.rt.stream)
@@ -179,7 +189,8 @@ class Conv3:
             kp = L.mmseg_stem_kp(self.Ci)
             part = self.rt.ws(ks * self.Co * kp + ks * self.Co)
             bpart = part.data_ptr() + ks * self.Co * kp * 4
-            with TIMER.region("stem_wgrad_kernel", flops=2.0 * V * self.Co * 27 * self.Ci):
+            with TIMER.region("stem_wgrad_kernel", flops=2.0 * V * self.Co * 27 * self.Ci,
+                              nbytes=_io_bytes(self.rt, V, 8, self.Co, 27 * self.Ci * self.Co, 4)):
                 L.mmseg_stem_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, self.Ci, ptr(part), bpart, x.N, x.D, x.H, x.W, self.Co,
                                    ks, code, s)
             L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.conv.weight)), bpart,
@@ -196,7 +207,8 @@ class Conv3:
         ks = L.mmseg_wgrad_splits_conv3(V, want, self.Co, self.cpg_shift, x.D, x.H, x.W, dy.ld, x.ld, code)
         part = self.rt.ws(ks * self.Co * ncols + ks * self.Co)
         bpart = part.data_ptr() + ks * self.Co * ncols * 4
-        with TIMER.region(_gemm_name(self.rt, 0, "conv3"), flops=2.0 * V * self.Co * 27 * self.Ci):
+        with TIMER.region(_gemm_name(self.rt, 0, "conv3"), flops=2.0 * V * self.Co * 27 * self.Ci,
+                          nbytes=_io_bytes(self.rt, V, self.Cip, self.Co, 27 * self.Cip * self.Co, 4)):
             L.mmseg_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, ptr(part), bpart, MODE_CONV3, self.Co, ncols, self.cpg_shift, V,
                           x.D, x.H, x.W, ks, code, s)
         L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.conv.weight)), bpart,
@@ -207,7 +219,8 @@ class Conv3:
             M = V
             ks = L.mmseg_conv3_splits(M, self.Ci, self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, dy.ld, dx.ld, code)
             ws = self.rt.ws(ks * M * self.Ci) if ks > 1 else None
-            with TIMER.region(_gemm_name(self.rt, self.Ci, "conv3"), flops=2.0 * M * self.Co * 27 * self.Ci):
+            with TIMER.region(_gemm_name(self.rt, self.Ci, "conv3"), flops=2.0 * M * self.Co * 27 * self.Ci,
+                              nbytes=_io_bytes(self.rt, M, self.Co, self.Cip, 27 * self.Cip * self.Co)):
                 L.mmseg_conv_gemm(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, ptr(ws), MODE_CONV3, M, self.Ci,
                                   self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, ks, code, s)
 
@@ -253,7 +266,8 @@ class ConvT2:
         ncols = 8 * self.Co
         ks = L.mmseg_wgrad_splits(V, _wgrad_ksplit(self.Ci, ncols, V))
         part = self.rt.ws(max(ks * self.Ci * ncols, 256 * self.Co))
-        with TIMER.region(_gemm_name(self.rt, 0, "convT"), flops=2.0 * V * self.Ci * 8 * self.Co):
+        with TIMER.region(_gemm_name(self.rt, 0, "convT"), flops=2.0 * V * self.Ci * 8 * self.Co,
+                          nbytes=_io_bytes(self.rt, V, self.Ci, 8 * self.Co, 8 * self.Ci * self.Co, 4)):
             L.mmseg_wgrad(x.ptr, x.ld, dy.ptr, dy.ld, ptr(part), None, MODE_CONVT_DGRAD, self.Ci, ncols, self.dshift,
                           V, x.D, x.H, x.W, ks, code, s)
         L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.up.weight)), None, None, self.Ci, ncols, ks, self.Co,

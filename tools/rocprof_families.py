@@ -39,6 +39,12 @@ def family(name: str) -> str:
     if m:
         tile = "128x32" if (m.group(2), m.group(3)) == ("4", "1") else "128x64"
         return f"conv_gemm_kernel<{_MODES[m.group(1)]},{tile}>[{dt}]"
+    m = re.search(r"wgrad_brick([2r])_kernelI(?:DF16b|f)Li(\d+)E", name)
+    if m:
+        return f"wgrad_brick{m.group(1)}_kernel<CO{int(m.group(2)) * 16}>[{dt}]"
+    m = re.search(r"wgrad_reduce_kernelILi(\d+)E|wgrad_reduce_kernel<(\d+)>", name)
+    if m:
+        return f"wgrad_reduce_kernel<{m.group(1) or m.group(2)}>"
     if "wgrad_brick_kernel" in name:
         return f"wgrad_brick_kernel[{dt}]"
     m = re.search(r"(?<![a-z_])wgrad_kernelI(?:DF16b|f)Li(\d)E", name)
