@@ -113,6 +113,16 @@ int mmseg_wgrad_splits_conv3(long long V, int ksplit, int Ca, int cpg_shift, int
 /* Fixed-order sum of the partials into the torch-layout fp32 gradient. */
 int mmseg_wgrad_reduce(const float* part, float* grad, const float* bias_part, float* bias_grad, int Ca, int Ncols,
                        int ksplit, int cpad, int creal, int ntap, int accumulate, void* stream);
+/* Weight + bias gradient of a 3^3 Conv3d (convolution_backward grad_weight / grad_bias of unet.py:26-27)
+ * straight into the torch-layout fp32 grad[Co][Ci][3][3][3] and bias_grad[Co] (NULL: no bias), = or +=
+ * (accumulate).  dy: [V][Co] (ld lddy), x: [V][Cip] (ld ldx), Cip = 8 << cpg_shift >= Ci real channels.
+ * The library picks kernel and voxel split; ws holds mmseg_conv3_wgrad_ws_floats() floats (a smaller
+ * ws_floats clamps the split; 0 is enough whenever the query returned 0). */
+long long mmseg_conv3_wgrad_ws_floats(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W,
+                                      int lddy, int ldx, int dtype);
+int mmseg_conv3_wgrad(const void* dy, int lddy, const void* x, int ldx, float* grad, float* bias_grad, int Co, int Cip,
+                      int Ci, int cpg_shift, long long V, int D, int H, int W, float* ws, long long ws_floats,
+                      int accumulate, int dtype, void* stream);
 /* Bias gradient out[c] (+)= sum_v dy[v][c] (convolution_backward grad_bias). */
 int mmseg_colsum(const void* dy, int ld, int C, long long V, float* part, int nblk, float* out, int accumulate,
                  int dtype, void* stream);

@@ -1033,6 +1033,11 @@ struct WgradArgs {
   long long vox_per_split;   // multiple of KV
   int swz;
   int brick;                 // CONV3 only: ksplit splits the brick list instead of voxels
+  // brick2 / brickr kernels (CONV3, bf16) write channel-major tiles (col = ci*27 + tap, the torch
+  // order of grad[co][ci][3][3][3]); with ksplit == 1 and grad != null straight into the gradient.
+  float* grad;
+  float* bias_grad;
+  int accumulate;
 };
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
@@ -1442,6 +1447,69 @@ __global__ __launch_bounds__(256) void wgrad_brick_kernel(WgradArgs g) {
   }
 }
 
+
+// Epilogue of the brick wgrad kernels (8 waves, acc[t][i][j] = rows i*16.., input channels j*16.., tap
+// t_begin + t): the block's [MT*16 co][32 ci][27 taps] fp32 tile goes through LDS 16 co-rows at a time and
+// leaves as contiguous float4 rows in channel-major order (torch grad[co][ci][tap] order), either into the
+// split partial part[ks][Ca][Ncols] or, for a single split, straight into the gradient (= or +=).
+// LDS pitch 868 floats: a ds_write_b32 lane group (two co-rows x 16 ci, ci stride 27) hits 32 distinct banks.
+constexpr int WEP_P = 868;
+template <int MT>
+__device__ __forceinline__ void wgrad_store_chmajor(const f32x4 (&acc)[4][MT][2], int t_begin, int t_cnt, float* L,
+                                                    const WgradArgs& g, int ks, int row0, int c0) {
+  const int tid = threadIdx.x, lane = tid & 63, g4 = lane >> 4, i16 = lane & 15;
+  const bool direct = g.grad != nullptr && g.ksplit == 1;
+  float* base = direct ? g.grad : g.part + (long long)ks * g.Ca * g.Ncols;
+  const bool accum = direct && g.accumulate;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (t >= t_cnt) continue;
+      const int tap = t_begin + t;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) L[(g4 * 4 + r) * WEP_P + (j * 16 + i16) * 27 + tap] = acc[t][i][j][r];
+    }
+    __syncthreads();
+    for (int e = tid; e < 16 * 216; e += 512) {
+      const int rr = e / 216, q = e - rr * 216;
+      const float4 v = *reinterpret_cast<const float4*>(L + rr * WEP_P + q * 4);
+      float4* d = reinterpret_cast<float4*>(base + (long long)(row0 + i * 16 + rr) * g.Ncols + c0 * 27 + q * 4);
+      if (accum) {
+        const float4 o = *d;
+        *d = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+      } else {
+        *d = v;
+      }
+    }
+  }
+}
+
+// Bias-gradient epilogue of the brick wgrad kernels: per-thread column sums of the staged dy rows
+// (8 channels of group tid % CG), reduced over the 512 threads in fixed order.
+template <int CG>
+__device__ __forceinline__ void wgrad_store_bias(const float (&bsum)[8], float* red, const WgradArgs& g, int ks,
+                                                 int row0) {
+  constexpr int CO = CG * 8;
+  const int tid = threadIdx.x;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[tid * 8 + j] = bsum[j];
+  __syncthreads();
+  if (tid < CO) {
+    const int cg = tid >> 3, j = tid & 7;
+    float sacc = 0.f;
+    for (int t = cg; t < 512; t += CG) sacc += red[t * 8 + j];
+    if (g.bias_grad != nullptr && g.ksplit == 1)
+      g.bias_grad[row0 + tid] = g.accumulate ? g.bias_grad[row0 + tid] + sacc : sacc;
+    else
+      g.bias_part[(long long)ks * g.Ca + row0 + tid] = sacc;
+  }
+}
+
 // ------------------------------------------------ brick wgrad v2 (3^3)
 // 8 waves, 64 output channels x one 32-channel input chunk x all 27 taps per
 // block (wgrad_brick_kernel has 32 x 32): each tap-shifted halo fragment now
@@ -1606,34 +1674,10 @@ __global__ __launch_bounds__(512, MT == 2 ? 2 : 1) void wgrad_brick2_kernel(Wgra
     buf ^= 1;
   }
 
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    if (t >= t_cnt) continue;
-    const int tap = t_begin + t;
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int col = tap * cin + c0 + j * 16 + i16;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = row0 + i * 16 + g4 * 4 + r;
-          g.part[((long long)ks * g.Ca + row) * g.Ncols + col] = acc[t][i][j][r];
-        }
-      }
-  }
-  if (do_bias) {
-    float* red = reinterpret_cast<float*>(lds);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) red[tid * 8 + j] = bsum[j];
-    __syncthreads();
-    if (tid < CO) {
-      const int cg = tid >> 3, j = tid & 7;
-      float sacc = 0.f;
-      for (int t = cg; t < 512; t += CG) sacc += red[t * 8 + j];
-      g.bias_part[(long long)ks * g.Ca + row0 + tid] = sacc;
-    }
-  }
+  static_assert(sizeof(lds) >= 16 * WEP_P * sizeof(float) && sizeof(lds) >= 512 * 8 * sizeof(float),
+                "epilogue staging must fit the stage buffers");
+  wgrad_store_chmajor<MT>(acc, t_begin, t_cnt, reinterpret_cast<float*>(lds), g, ks, row0, c0);
+  if (do_bias) wgrad_store_bias<CG>(bsum, reinterpret_cast<float*>(lds), g, ks, row0);
 }
 
 // ------------------------------------- runtime-brick wgrad (small volumes)
@@ -1823,34 +1867,10 @@ __global__ __launch_bounds__(512) void wgrad_brickr_kernel(WgradArgs g, int bz, 
     buf ^= 1;
   }
 
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    if (t >= t_cnt) continue;
-    const int tap = t_begin + t;
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int col = tap * cin + c0 + j * 16 + i16;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = row0 + i * 16 + g4 * 4 + r;
-          g.part[((long long)ks * g.Ca + row) * g.Ncols + col] = acc[t][i][j][r];
-        }
-      }
-  }
-  if (do_bias) {
-    float* red = reinterpret_cast<float*>(lds);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) red[tid * 8 + j] = bsum[j];
-    __syncthreads();
-    if (tid < CO) {
-      const int cg = tid >> 3, j = tid & 7;
-      float sacc = 0.f;
-      for (int t = cg; t < 512; t += CG) sacc += red[t * 8 + j];
-      g.bias_part[(long long)ks * g.Ca + row0 + tid] = sacc;
-    }
-  }
+  static_assert(sizeof(lds) >= 16 * WEP_P * sizeof(float) && sizeof(lds) >= 512 * 8 * sizeof(float),
+                "epilogue staging must fit the stage buffers");
+  wgrad_store_chmajor<MT>(acc, t_begin, t_cnt, reinterpret_cast<float*>(lds), g, ks, row0, c0);
+  if (do_bias) wgrad_store_bias<CG>(bsum, reinterpret_cast<float*>(lds), g, ks, row0);
 }
 
 struct WBrick { int bz, by, bx; };
@@ -1891,6 +1911,7 @@ struct WReduceArgs {
   int cpad, creal;    // per-tap channel count in cols (padded) and real count
   int ntap;           // 27 (CONV3), 1 (POINT), 8 (CONVT)
   int accumulate;
+  int chmajor;        // cols are channel-major (col = c*ntap + tap, brick2/brickr partials) instead of tap-major
 };
 
 // 256 threads = (256/S) float4 columns x S split slices: slice s sums splits
@@ -1947,7 +1968,14 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(WReduceArgs g) {
     }
     const int row = (int)(idx / g.Ncols);
     const int col = (int)(idx - (long long)row * g.Ncols);
-    const int tt = col / g.cpad, c = col - tt * g.cpad;
+    int tt, c;
+    if (g.chmajor) {
+      c = col / g.ntap;
+      tt = col - c * g.ntap;
+    } else {
+      tt = col / g.cpad;
+      c = col - tt * g.cpad;
+    }
     if (c >= g.creal || tt >= g.ntap) continue;
     const long long dst = ((long long)row * g.creal + c) * g.ntap + tt;   // torch layout [row][c_real][tap]
     if (g.accumulate) g.grad[dst] += val;
@@ -2362,8 +2390,16 @@ int wgrad_brick_ok(int Ca, int cpg_shift, int D, int H, int W, int lda, int ldb,
 int brick_wgrad_splits(long long V, int cap, int Ca, int cpg_shift, int kind, int D, int H, int W) {
   const int nchunk = (8 << cpg_shift) / CK;
   const int tiles = nchunk * (Ca / ((kind >= 2 && Ca % 64 == 0) ? 64 : 32));
-  const int target = kind >= 2 ? 512 : 1024;
-  long long ks = (target + tiles - 1) / tiles;
+  // v2 / runtime-brick kernels: one wave of resident blocks (256 CUs x blocks per CU: 2 for the 32-co brick2
+  // kernel, 1 for the 64-co and runtime-brick kernels, whose stage buffers take > 80 KB of LDS), never more:
+  // a partial second wave of 512-thread blocks costs a whole block time.
+  long long ks;
+  if (kind >= 2) {
+    const int slots = (kind == 2 && Ca % 64 != 0) ? 512 : 256;
+    ks = (long long)slots * knob("MMSEG_WGRAD_WAVES", 1) / tiles;
+  } else {
+    ks = (1024 + tiles - 1) / tiles;
+  }
   if (ks > cap) ks = cap;
   long long nbrick = V / 128;
   if (kind == 3) {
@@ -2374,6 +2410,60 @@ int brick_wgrad_splits(long long V, int cap, int Ca, int cpg_shift, int kind, in
   if (ks < 1) ks = 1;
   const long long bpk = (nbrick + ks - 1) / ks;
   return (int)((nbrick + bpk - 1) / bpk);
+}
+
+
+int mmseg_wgrad_splits_impl(long long V, int ksplit) {
+  long long vps = ((V + ksplit - 1) / ksplit + 63) / 64 * 64;
+  return (int)((V + vps - 1) / vps);
+}
+
+// CONV3 weight-gradient plan (mmseg_conv3_wgrad): kernel kind (wgrad_brick_ok), split count, whether the
+// kernel writes the torch-layout gradient itself (brick2 / brickr, one split, unpadded input channels),
+// and the workspace (floats) of the split partials + bias partials otherwise.
+struct Conv3WgradPlan {
+  int kind, ksplit, direct;
+  long long ws;
+};
+
+Conv3WgradPlan plan_conv3_wgrad(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W, int lda,
+                                int ldb, int dtype, long long ws_cap) {
+  Conv3WgradPlan p{0, 1, 0, 0};
+  const long long ncols = 27LL * Cip;
+  const long long per_split = (long long)Co * ncols + Co;
+  int cap = (int)(ws_cap / per_split);
+  if (cap < 1) cap = 1;
+  p.kind = wgrad_brick_ok(Co, cpg_shift, D, H, W, lda, ldb, dtype);
+  if (p.kind) {
+    p.ksplit = brick_wgrad_splits(V, cap, Co, cpg_shift, p.kind, D, H, W);
+  } else {
+    const int bn = knob("MMSEG_WGRAD_BN", 64);
+    const long long tiles = ((ncols + bn - 1) / bn) * ((Co + (Co % 64 == 0 ? 63 : 31)) / (Co % 64 == 0 ? 64 : 32));
+    long long want = (1024 + tiles - 1) / tiles;
+    if (want > V / 512) want = V / 512;
+    if (want > cap) want = cap;
+    if (want < 1) want = 1;
+    p.ksplit = mmseg_wgrad_splits_impl(V, (int)want);
+  }
+  p.direct = p.kind >= 2 && p.ksplit == 1 && Ci == Cip;
+  p.ws = p.direct ? 0 : p.ksplit * per_split;
+  return p;
+}
+
+int launch_wgrad_reduce(WReduceArgs g, void* stream) {
+  const int ksplit = g.ksplit;
+  const long long total = (long long)g.Ca * g.Ncols + (g.bias_part ? g.Ca : 0);
+  hipStream_t s = (hipStream_t)stream;
+  // slices: ~8+ loads per thread when the splits allow, 1 slice for a handful of splits
+  if (ksplit >= 512)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<64>, dim3(ceil_div(total, 16)), dim3(256), 0, s, g);
+  else if (ksplit >= 64)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<8>, dim3(ceil_div(total, 128)), dim3(256), 0, s, g);
+  else if (ksplit >= 8)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<2>, dim3(ceil_div(total, 512)), dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(ceil_div(total, 1024)), dim3(256), 0, s, g);
+  return mmseg::check_launch("wgrad_reduce");
 }
 
 }  // namespace
@@ -2499,7 +2589,10 @@ int mmseg_wgrad(const void* a, int lda, const void* b, int ldb, float* part, flo
                 int Ncols, int cpg_shift, long long V, int D, int H, int W, int ksplit, int dtype, void* stream) {
   MMSEG_REQUIRE(Ca % 8 == 0, "wgrad: rows (%d) must be a multiple of 8", Ca);
   MMSEG_REQUIRE(Ncols % 8 == 0, "wgrad: cols (%d) must be a multiple of 8", Ncols);
-  const int brick = mode == MODE_CONV3 ? wgrad_brick_ok(Ca, cpg_shift, D, H, W, lda, ldb, dtype) : 0;
+  // legacy entry (tap-major partials + mmseg_wgrad_reduce): brick kinds 2/3 write channel-major tiles and
+  // are reached through mmseg_conv3_wgrad only
+  int brick = mode == MODE_CONV3 ? wgrad_brick_ok(Ca, cpg_shift, D, H, W, lda, ldb, dtype) : 0;
+  if (brick > 1) brick = 1;
   long long vps = ((V + ksplit - 1) / ksplit + 63) / 64 * 64;
   if (brick) {
     ksplit = brick_wgrad_splits(V, ksplit, Ca, cpg_shift, brick, D, H, W);
@@ -2507,7 +2600,7 @@ int mmseg_wgrad(const void* a, int lda, const void* b, int ldb, float* part, flo
     ksplit = (int)((V + vps - 1) / vps);
   }
   WgradArgs g{a, lda, b, ldb, part, bias_part, Ca, Ncols, cpg_shift, V, D, H, W, ksplit, vps,
-              knob("MMSEG_WGRAD_SWIZZLE", 0), brick};
+              knob("MMSEG_WGRAD_SWIZZLE", 0), brick, nullptr, nullptr, 0};
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16) {
     switch (mode) {
@@ -2527,15 +2620,13 @@ int mmseg_wgrad(const void* a, int lda, const void* b, int ldb, float* part, flo
 }
 
 // Effective split count the wgrad launcher will use (callers size `part` with it).
-int mmseg_wgrad_splits(long long V, int ksplit) {
-  long long vps = ((V + ksplit - 1) / ksplit + 63) / 64 * 64;
-  return (int)((V + vps - 1) / vps);
-}
+int mmseg_wgrad_splits(long long V, int ksplit) { return mmseg_wgrad_splits_impl(V, ksplit); }
 
 // Same for the CONV3 brick path (splits the list of 4x4x8 bricks).
 int mmseg_wgrad_splits_conv3(long long V, int ksplit, int Ca, int cpg_shift, int D, int H, int W, int lda, int ldb,
                              int dtype) {
-  const int kind = wgrad_brick_ok(Ca, cpg_shift, D, H, W, lda, ldb, dtype);
+  int kind = wgrad_brick_ok(Ca, cpg_shift, D, H, W, lda, ldb, dtype);
+  if (kind > 1) kind = 1;   // the legacy entry's kernels (see mmseg_wgrad)
   if (!kind) return mmseg_wgrad_splits(V, ksplit);
   return brick_wgrad_splits(V, ksplit, Ca, cpg_shift, kind, D, H, W);
 }
@@ -2544,19 +2635,39 @@ int mmseg_wgrad_reduce(const float* part, float* grad, const float* bias_part, f
                        int ksplit, int cpad, int creal, int ntap, int accumulate, void* stream) {
   MMSEG_REQUIRE(((long long)Ca * Ncols) % 4 == 0 && (reinterpret_cast<uintptr_t>(part) & 15) == 0,
                 "wgrad_reduce: Ca*Ncols %% 4 == 0 and a 16-B aligned partial buffer");
-  WReduceArgs g{part, grad, bias_part, bias_grad, Ca, Ncols, ksplit, cpad, creal, ntap, accumulate};
-  const long long total = (long long)Ca * Ncols + (bias_part ? Ca : 0);
+  WReduceArgs g{part, grad, bias_part, bias_grad, Ca, Ncols, ksplit, cpad, creal, ntap, accumulate, 0};
+  return launch_wgrad_reduce(g, stream);
+}
+
+// Weight (+ bias) gradient of a 3^3 conv straight into the torch-layout fp32 gradient
+// grad[Co][Ci][27] (+ bias_grad[Co]), = or += (accumulate).  The library picks kernel and split;
+// ws holds mmseg_conv3_wgrad_ws_floats() floats (more lets it split further, fewer is clamped).
+long long mmseg_conv3_wgrad_ws_floats(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W,
+                                      int lddy, int ldx, int dtype) {
+  const long long cap = (long long)knob("MMSEG_WGRAD_CAP_MF", 16) << 20;
+  return plan_conv3_wgrad(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype, cap).ws;
+}
+
+int mmseg_conv3_wgrad(const void* dy, int lddy, const void* x, int ldx, float* grad, float* bias_grad, int Co, int Cip,
+                      int Ci, int cpg_shift, long long V, int D, int H, int W, float* ws, long long ws_floats,
+                      int accumulate, int dtype, void* stream) {
+  MMSEG_REQUIRE(Co % 8 == 0 && Cip % 8 == 0 && Ci <= Cip && (8 << cpg_shift) == Cip,
+                "conv3_wgrad: Co=%d, Cip=%d must be multiples of 8, Ci=%d <= Cip, Cip = 8 << cpg_shift", Co, Cip, Ci);
+  const Conv3WgradPlan p = plan_conv3_wgrad(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype, ws_floats);
+  MMSEG_REQUIRE(p.ws <= ws_floats && (p.ws == 0 || ws != nullptr), "conv3_wgrad: workspace of %lld floats < %lld",
+                ws_floats, p.ws);
+  const int ncols = 27 * Cip;
+  float* part = p.direct ? nullptr : ws;
+  float* bpart = (p.direct || bias_grad == nullptr) ? nullptr : ws + (long long)p.ksplit * Co * ncols;
+  const long long vps = ((V + p.ksplit - 1) / p.ksplit + 63) / 64 * 64;
+  WgradArgs g{dy, lddy, x, ldx, part, p.direct ? bias_grad : bpart, Co, ncols, cpg_shift, V, D, H, W, p.ksplit, vps,
+              knob("MMSEG_WGRAD_SWIZZLE", 0), p.kind, p.direct ? grad : nullptr, p.direct ? bias_grad : nullptr,
+              accumulate};
   hipStream_t s = (hipStream_t)stream;
-  // slices: ~8+ loads per thread when the splits allow, 1 slice for a handful of splits
-  if (ksplit >= 512)
-    hipLaunchKernelGGL(wgrad_reduce_kernel<64>, dim3(ceil_div(total, 16)), dim3(256), 0, s, g);
-  else if (ksplit >= 64)
-    hipLaunchKernelGGL(wgrad_reduce_kernel<8>, dim3(ceil_div(total, 128)), dim3(256), 0, s, g);
-  else if (ksplit >= 8)
-    hipLaunchKernelGGL(wgrad_reduce_kernel<2>, dim3(ceil_div(total, 512)), dim3(256), 0, s, g);
-  else
-    hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(ceil_div(total, 1024)), dim3(256), 0, s, g);
-  return mmseg::check_launch("wgrad_reduce");
+  const int rc = dtype == MMSEG_BF16 ? launch_wgrad<bf16_t, MODE_CONV3>(g, s) : launch_wgrad<float, MODE_CONV3>(g, s);
+  if (rc || p.direct) return rc;
+  WReduceArgs r{part, grad, bpart, bias_grad, Co, ncols, p.ksplit, Cip, Ci, 27, accumulate, p.kind >= 2 ? 1 : 0};
+  return launch_wgrad_reduce(r, stream);
 }
 
 // Bias gradient: out[c] (+)= sum_v dy[v][c]; part must hold nblk*C floats.

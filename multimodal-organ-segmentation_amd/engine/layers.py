@@ -198,22 +198,14 @@ class Conv3:
                                  int(accumulate), s)
             self.flat.mark(self.conv.weight, self.conv.bias)
             return
-        ncols = 27 * self.Cip
-        if self.Cip % 32 == 0 and self.Co % 32 == 0:
-            # brick path: the library picks the split; we only cap the partials at ~32 MB
-            want = max(1, (8 << 20) // (self.Co * ncols))
-        else:
-            want = _wgrad_ksplit(self.Co, ncols, V)
-        ks = L.mmseg_wgrad_splits_conv3(V, want, self.Co, self.cpg_shift, x.D, x.H, x.W, dy.ld, x.ld, code)
-        part = self.rt.ws(ks * self.Co * ncols + ks * self.Co)
-        bpart = part.data_ptr() + ks * self.Co * ncols * 4
+        wsf = L.mmseg_conv3_wgrad_ws_floats(V, self.Co, self.Cip, self.Ci, self.cpg_shift, x.D, x.H, x.W, dy.ld,
+                                            x.ld, code)
+        ws = self.rt.ws(wsf) if wsf > 0 else None
         with TIMER.region(_gemm_name(self.rt, 0, "conv3"), flops=2.0 * V * self.Co * 27 * self.Ci,
                           nbytes=_io_bytes(self.rt, V, self.Cip, self.Co, 27 * self.Cip * self.Co, 4)):
-            L.mmseg_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, ptr(part), bpart, MODE_CONV3, self.Co, ncols, self.cpg_shift, V,
-                          x.D, x.H, x.W, ks, code, s)
-        L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.conv.weight)), bpart,
-                             ptr(self.flat.grad(self.conv.bias)), self.Co, ncols, ks, self.Cip, self.Ci, 27,
-                             int(accumulate), s)
+            L.mmseg_conv3_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, ptr(self.flat.grad(self.conv.weight)),
+                                ptr(self.flat.grad(self.conv.bias)), self.Co, self.Cip, self.Ci, self.cpg_shift, V,
+                                x.D, x.H, x.W, ptr(ws), wsf, int(accumulate), code, s)
         self.flat.mark(self.conv.weight, self.conv.bias)
         if dx is not None:
             M = V
