@@ -695,6 +695,245 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kern
   }
 }
 
+
+// ------------------------------------------------- brick conv v3 (3^3)
+// conv3_brick2_kernel (same 4x8x8-voxel brick, halo / weight LDS images and
+// 9-tap stages) with the per-block fixed costs cut, which at Cin = 32 (one
+// chunk, three stages per block) were ~5 VALU per MFMA (rocprofv3
+// SQ_INSTS_VALU / SQ_INSTS_MFMA on the 96^3 layers):
+//   * halo staging: thread t < 240 owns one (x, 8-channel group) column of the
+//     halo and walks its 60 (z, y) rows 6 apart, so the voxel offset, the LDS
+//     slot and the z / y bounds advance by block-uniform steps; the loads are
+//     buffer loads whose out-of-volume lanes carry an offset past the buffer
+//     end and read zeros (no branch, no zero fill);
+//   * the MFMA computes the transposed tile W^T X (A and B swapped), so a lane
+//     holds 4 consecutive output channels of one voxel: bias, bf16 packing and
+//     an 8-B global store straight from the accumulators, no LDS epilogue.
+template <typename T>
+__device__ __forceinline__ void buf_load_v8(V8<T>& v, __amdgpu_buffer_rsrc_t r, uint32_t off);
+template <>
+__device__ __forceinline__ void buf_load_v8<bf16_t>(V8<bf16_t>& v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const i32x4 t = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  v.v = __builtin_bit_cast(bf16x8, t);
+}
+template <>
+__device__ __forceinline__ void buf_load_v8<float>(V8<float>& v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const i32x4 a = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  const i32x4 b = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16, 0, 0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v.v[j] = __builtin_bit_cast(float, a[j]);
+    v.v[4 + j] = __builtin_bit_cast(float, b[j]);
+  }
+}
+
+template <typename T, int BN>
+__global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kernel(GemmArgs g, int upb) {
+  using L = Brick2Layout<T>;
+  constexpr int BZ = 4, HZ = BZ + 2;
+  constexpr int RM = 4, RN = BN / 16;
+  constexpr int XQ = HZ * L::RZ;
+  constexpr int WQ = 9 * BN * L::QV;
+  __shared__ __attribute__((aligned(16))) float4 lds4[XQ + WQ];
+  T* Xl = reinterpret_cast<T*>(lds4);
+  T* Wl = reinterpret_cast<T*>(lds4 + XQ);
+  constexpr int EPQ = 16 / sizeof(T);
+  constexpr int XROWS = HZ * H2_Y;                    // 60 (z, y) halo rows
+  constexpr int XK = XROWS / 6;                       // rows per thread (6 rows per pass of 240 threads)
+  constexpr int W_ITEMS = 9 * BN * 4;
+  constexpr int W_PER = (W_ITEMS + 255) / 256;
+  static_assert(XROWS % 6 == 0, "halo rows per pass");
+
+  const T* Bw = reinterpret_cast<const T*>(g.b);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int bz_n = g.D / BZ, by_n = g.H / B2_Y, bx_n = g.W / B2_X;
+  const int nbrick = (g.M / (g.D * g.H * g.W)) * bz_n * by_n * bx_n;
+  const int nt_n = (g.Ncols + BN - 1) / BN;
+  const int units = nbrick * nt_n;
+  // this block's units: a contiguous range (consecutive units share halo columns in L2); unit = brick * nt_n + nt
+  const int blk = g.swz ? xcd_swizzle(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int u_begin = blk * upb;
+  const int u_end = u_begin + upb < units ? u_begin + upb : units;
+  if (u_begin >= u_end) return;
+  const int HW = g.H * g.W;
+  const int cin = 8 << g.cpg_shift;
+  const int nchunk = cin / CK;
+  const int nstage = nchunk * 3;
+  const int ldb = g.lda * (int)sizeof(T);            // bytes per voxel
+  const int vox_per_n = g.D * HW;
+
+  // ---- halo column of this thread: (hx, cg) fixed, rows r0, r0+6, ... (hz = r / 10, hy = r % 10)
+  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(g.a), 0, (int)((long long)(g.M / vox_per_n) * vox_per_n * ldb), 0x00020000);
+  const bool xact = tid < 240;
+  const int xq = tid % 40, r0 = tid / 40;
+  const int hx = xq >> 2, cg = xq & 3;
+  // row r0 + 6k -> (hz, hy) = divmod by 10 ((row * 205) >> 11 is exact for row < 1029); recomputed where
+  // used rather than kept in 2 x XK registers (the BN64 instantiation is at the 256-VGPR cap)
+  auto row_hz = [&](int k) { return ((r0 + 6 * k) * 205) >> 11; };
+  const int xlds0 = (hx * L::QV + cg * L::QG) * EPQ;
+  struct Unit { int n, z0, y0, x0, n0; };
+  auto unit_of = [&](int u) {
+    Unit r;
+    const int nt = u % nt_n;
+    int b = u / nt_n;
+    const int bx = b % bx_n; b /= bx_n;
+    const int by = b % by_n; b /= by_n;
+    r.z0 = (b % bz_n) * BZ;
+    r.n = b / bz_n;
+    r.y0 = by * B2_Y;
+    r.x0 = bx * B2_X;
+    r.n0 = nt * BN;
+    return r;
+  };
+  uint32_t xoff[XK];
+  auto set_x = [&](const Unit& q) {    // per-unit halo offsets; out-of-volume lanes point past the buffer end
+    const int xx = q.x0 - 1 + hx;
+    const bool xok = xact && (unsigned)xx < (unsigned)g.W;
+    const int vb = q.n * vox_per_n + xx;
+#pragma unroll
+    for (int k = 0; k < XK; ++k) {
+      const int hz = row_hz(k), hy = r0 + 6 * k - 10 * hz;
+      const int zz = q.z0 - 1 + hz, yy = q.y0 - 1 + hy;
+      const bool ok = xok && (unsigned)zz < (unsigned)g.D && (unsigned)yy < (unsigned)g.H;
+      xoff[k] = ok ? (uint32_t)((vb + zz * HW + yy * g.W) * ldb + cg * 8 * (int)sizeof(T)) : 0x80000000u;
+    }
+  };
+  V8<T> xr[XK], wr[W_PER];
+  auto load_x = [&](int c) {
+    const uint32_t coff = (uint32_t)(c * CK * (int)sizeof(T));
+#pragma unroll
+    for (int k = 0; k < XK; ++k) buf_load_v8<T>(xr[k], arsrc, xoff[k] + coff);   // OOB lanes read 0
+  };
+  auto store_x = [&]() {
+    if (xact) {
+#pragma unroll
+      for (int k = 0; k < XK; ++k) {
+        const int hz = row_hz(k), hy = r0 + 6 * k - 10 * hz;
+        xr[k].store(Xl + xlds0 + (hz * L::RZ + hy * L::RY) * EPQ);
+      }
+    }
+  };
+  auto load_w = [&](int n0, int c, int kz) {
+#pragma unroll
+    for (int k = 0; k < W_PER; ++k) {
+      const int e = tid + k * 256;
+      if (e < W_ITEMS) {
+        const int cgw = e & 3, q = e >> 2;
+        const int col = q % BN, t9 = q / BN;
+        const int kgi = (kz * 9 + t9) * (cin / 8) + c * 4 + cgw;
+        wr[k].load(Bw + ((long long)kgi * g.Cpad + n0 + col) * 8);
+      }
+    }
+  };
+  auto store_w = [&]() {
+#pragma unroll
+    for (int k = 0; k < W_PER; ++k) {
+      const int e = tid + k * 256;
+      if (e < W_ITEMS) {
+        const int cgw = e & 3, q = e >> 2;
+        wr[k].store(Wl + (q * L::QV + (cgw ^ w2_swz(q)) * L::QG) * EPQ);
+      }
+    }
+  };
+
+  const int r16 = lane & 15, kg = lane >> 4;
+  int aq[RM];
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    const int yr = 2 * (i & 3) + (r16 >> 3), xr_ = r16 & 7;
+    aq[i] = wave * L::RZ + yr * L::RY + xr_ * L::QV + kg * L::QG;
+  }
+  int bq[RN];
+#pragma unroll
+  for (int j = 0; j < RN; ++j) {
+    const int col = j * 16 + r16;
+    bq[j] = col * L::QV + (kg ^ w2_swz(col)) * L::QG;
+  }
+  T* O = reinterpret_cast<T*>(g.out);
+
+  Unit cur = unit_of(u_begin);
+  set_x(cur);
+  load_x(0);
+  load_w(cur.n0, 0, 0);
+  store_x();
+  store_w();
+  __syncthreads();
+  for (int u = u_begin; u < u_end; ++u) {
+    f32x4 acc[RM][RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const bool unext = u + 1 < u_end;
+    Unit nxt = cur;
+    if (unext) nxt = unit_of(u + 1);
+    for (int st = 0; st < nstage; ++st) {
+      const int c = st / 3, kz = st - c * 3;
+      // next stage: (cn, kzn) of this unit, or stage 0 of the next unit
+      const bool last = st + 1 == nstage;
+      const bool more = !last || unext;
+      const int sn = last ? 0 : st + 1;
+      const int cn = sn / 3, kzn = sn - cn * 3;
+      if (more) {
+        if (last) set_x(nxt);
+        load_w(last ? nxt.n0 : cur.n0, cn, kzn);
+        if (kzn == 0) load_x(cn);
+      }
+#pragma unroll
+      for (int t9 = 0; t9 < 9; ++t9) {
+        const int ky = t9 / 3, kx = t9 - ky * 3;
+        const int hoff = kz * L::RZ + ky * L::RY + kx * L::QV;
+        V8<T> af[RM], bf[RN];
+#pragma unroll
+        for (int j = 0; j < RN; ++j) bf[j].load(Wl + (t9 * BN * L::QV + bq[j]) * EPQ);
+#pragma unroll
+        for (int i = 0; i < RM; ++i) af[i].load(Xl + (aq[i] + hoff) * EPQ);
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j) mfma_step<T>(acc[i][j], bf[j], af[i]);   // transposed: rows = channels
+      }
+      __syncthreads();
+      if (more) {
+        store_w();
+        if (kzn == 0) store_x();
+        __syncthreads();
+      }
+    }
+    // epilogue: lane holds channels n0 + j*16 + 4*kg + (0..3) of voxel r16 of row tile i
+    const long long obase = (long long)cur.n * vox_per_n;
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int col = cur.n0 + j * 16 + 4 * kg;
+      if (col >= g.Ncols) continue;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (g.bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = g.bias[col + r];   // the bias view is only 4-B aligned
+      }
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int z = cur.z0 + wave, y = cur.y0 + 2 * (i & 3) + (r16 >> 3), x = cur.x0 + (r16 & 7);
+        T* dst = O + (obase + (long long)(z * g.H + y) * g.W + x) * g.ldo + col;
+        if constexpr (sizeof(T) == 2) {
+          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (bf16_t)(acc[i][j][r] + bv[r]);
+          *reinterpret_cast<bf16x4*>(dst) = o;
+        } else {
+          *reinterpret_cast<float4*>(dst) = make_float4(acc[i][j][0] + bv[0], acc[i][j][1] + bv[1],
+                                                        acc[i][j][2] + bv[2], acc[i][j][3] + bv[3]);
+        }
+      }
+    }
+    cur = nxt;
+  }
+}
+
 // ------------------------------------- runtime-brick conv (small volumes)
 // conv3_brick2_kernel for volumes whose sides are not multiples of 8 (the
 // 12^3 and 6^3 levels): the brick (bz, by, bx), <= 256 voxels, is chosen on the
@@ -2248,7 +2487,26 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
   if (plan.kind == 1 && g.ksplit == 1) {
     const int nb1 = (g.M / (g.D * g.H * g.W)) * (g.D / 4) * (g.H / B2_Y) * (g.W / B2_X);
     const int min_blocks = knob("MMSEG_BRICK2_MINBLK", 512);
-    if (g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
+    // v3 is bf16 only: its fp32 instantiation (f32 16x16x4 MFMA with swapped operands) returned the first
+    // row of each 4-row accumulator group in all four registers (tools/diag_b3.py); the fp32 parity path
+    // keeps the v2 kernel.
+    const bool v3 = sizeof(T) == 2 && g.stats == nullptr && knob("MMSEG_BRICK3", 1) != 0 &&
+                    knob("MMSEG_BRICK2_ZW", 1) != 2 &&
+                    (long long)g.M * g.lda * (long long)sizeof(T) < (1LL << 31);
+    // persistent: at most one wave of resident blocks (2 per CU), each over a contiguous range of units
+    const int maxblk = knob("MMSEG_BRICK3_BLOCKS", 512);
+    // (BN64 stays on v2 unless asked for: at 256 VGPRs the v3 instantiation spills and measured no faster)
+    if (v3 && knob("MMSEG_BRICK3_BN64", 0) && g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
+      const int units = nb1 * (g.Ncols / 64);
+      const int upb = maxblk > 0 ? ceil_div(units, maxblk) : 1;
+      mmseg::note_kernel("conv3_brick3_kernel<BN64>");
+      hipLaunchKernelGGL((conv3_brick3_kernel<T, 64>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
+    } else if (v3 && !(g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks)) {
+      const int units = nb1 * (g.Ncols / 32);
+      const int upb = maxblk > 0 ? ceil_div(units, maxblk) : 1;
+      mmseg::note_kernel("conv3_brick3_kernel<BN32>");
+      hipLaunchKernelGGL((conv3_brick3_kernel<T, 32>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
+    } else if (g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
       mmseg::note_kernel("conv3_brick2_kernel<BN64,ZW1>");
       hipLaunchKernelGGL((conv3_brick2_kernel<T, 64, 1>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
     } else if (sizeof(T) == 2 && g.D % 8 == 0 && knob("MMSEG_BRICK2_ZW", 1) == 2) {
