@@ -1756,12 +1756,18 @@ __device__ __forceinline__ void wgrad_store_bias(const float (&bsum)[8], float* 
 // channels, so LDS reads and L2 traffic per MAC drop by a third.  Taps are
 // dealt 4,4,4,3,3,3,3,3 over the waves (acc: 4 taps x 4 x 2 tiles = 128
 // VGPRs).  The two LDS stage buffers alternate, one barrier per brick.
-template <typename T, int MT>
-__global__ __launch_bounds__(512, MT == 2 ? 2 : 1) void wgrad_brick2_kernel(WgradArgs g) {
+// V = 3 (default): bank-conflict-free transposed reads.  A ds_read_b64_tr_b16 half-wave reads 8 tile rows
+// x 16 columns; with the K order below those 8 rows are 8 consecutive voxels (one x-row of the brick: lane
+// group g4, element j -> x = 4*(g4&1) + (j&3), y = 2*(g4>>1) + (j>>2)) in BOTH the dy tile and the halo, and
+// with row pitches of 24 or 40 dwords (== 8 mod 16) 8 consecutive rows cover the 64 banks exactly once.
+// V = 2: the previous K order (x = j&3 + 4*(j>>2), y = g4) with 20-dword pitches, 2-way conflicted
+// (SQ_LDS_BANK_CONFLICT = half the LDS-active cycles at 96^3).
+template <typename T, int MT, int V>
+__global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2_kernel(WgradArgs g) {
   constexpr int EP = 16 / sizeof(T);
   constexpr int CO = MT * 16, CG = CO / 8;       // output channels per block, 8-channel groups
-  constexpr int DP = CO + EP;                    // dy tile pitch (elements)
-  constexpr int XP = CK + EP;                    // halo pitch
+  constexpr int DP = V == 3 ? (MT == 2 ? 48 : 80) : CO + EP;   // dy tile pitch (elements)
+  constexpr int XP = V == 3 ? 48 : CK + EP;                    // halo pitch
   constexpr int DS = 128 * DP, XS = HLO_V * XP;
   __shared__ __attribute__((aligned(16))) T lds[2 * (DS + XS)];
   constexpr int D_ITEMS = 128 * CG, X_ITEMS = HLO_V * 4;
@@ -1858,12 +1864,13 @@ __global__ __launch_bounds__(512, MT == 2 ? 2 : 1) void wgrad_brick2_kernel(Wgra
 #pragma unroll
       for (int kk = 0; kk < 128; kk += 32) {
         bf16x8 af[MT];
+        const int v_lo = V == 3 ? kk + 16 * (g4 >> 1) + 4 * (g4 & 1) + q : kk + 8 * g4 + q;
+        const int v_hi = V == 3 ? v_lo + 8 : v_lo + 4;
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
-          const bf16_t* base = (const bf16_t*)Dl + (kk + 8 * g4 + q) * DP + i * 16 + 4 * p4;
-          af[i] = tr_frag(base, base + 4 * DP);
+          const bf16_t* base = (const bf16_t*)Dl + v_lo * DP + i * 16 + 4 * p4;
+          af[i] = tr_frag(base, base + (v_hi - v_lo) * DP);
         }
-        const int v_lo = kk + 8 * g4 + q, v_hi = v_lo + 4;
         const int hlo = ((v_lo >> 5) * HLO_Y + ((v_lo >> 3) & 3)) * HLO_X + (v_lo & 7);
         const int hhi = ((v_hi >> 5) * HLO_Y + ((v_hi >> 3) & 3)) * HLO_X + (v_hi & 7);
 #pragma unroll
@@ -2588,14 +2595,21 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
     }
     if (MODE == MODE_CONV3 && g.brick == 2) {
       const int cin = 8 << g.cpg_shift;
+      const bool v3 = knob("MMSEG_WGRAD_V3", 1) != 0;
       if (g.Ca % 64 == 0) {
         dim3 grid((cin / CK) * (g.Ca / 64) * g.ksplit);
-        mmseg::note_kernel("wgrad_brick2_kernel<CO64>");
-        hipLaunchKernelGGL((wgrad_brick2_kernel<T, 4>), grid, dim3(512), 0, s, g);
+        mmseg::note_kernel(v3 ? "wgrad_brick2_kernel<CO64,V3>" : "wgrad_brick2_kernel<CO64>");
+        if (v3)
+          hipLaunchKernelGGL((wgrad_brick2_kernel<T, 4, 3>), grid, dim3(512), 0, s, g);
+        else
+          hipLaunchKernelGGL((wgrad_brick2_kernel<T, 4, 2>), grid, dim3(512), 0, s, g);
       } else {
         dim3 grid((cin / CK) * (g.Ca / 32) * g.ksplit);
-        mmseg::note_kernel("wgrad_brick2_kernel<CO32>");
-        hipLaunchKernelGGL((wgrad_brick2_kernel<T, 2>), grid, dim3(512), 0, s, g);
+        mmseg::note_kernel(v3 ? "wgrad_brick2_kernel<CO32,V3>" : "wgrad_brick2_kernel<CO32>");
+        if (v3)
+          hipLaunchKernelGGL((wgrad_brick2_kernel<T, 2, 3>), grid, dim3(512), 0, s, g);
+        else
+          hipLaunchKernelGGL((wgrad_brick2_kernel<T, 2, 2>), grid, dim3(512), 0, s, g);
       }
       return mmseg::check_launch("wgrad_brick2");
     }
@@ -2653,7 +2667,7 @@ int brick_wgrad_splits(long long V, int cap, int Ca, int cpg_shift, int kind, in
   // a partial second wave of 512-thread blocks costs a whole block time.
   long long ks;
   if (kind >= 2) {
-    const int slots = (kind == 2 && Ca % 64 != 0) ? 512 : 256;
+    const int slots = (kind == 2 && Ca % 64 != 0 && knob("MMSEG_WGRAD_V3", 1) == 0) ? 512 : 256;
     ks = (long long)slots * knob("MMSEG_WGRAD_WAVES", 1) / tiles;
   } else {
     ks = (1024 + tiles - 1) / tiles;
