@@ -144,6 +144,14 @@ int mmseg_instnorm_relu_bwd(const void* x, int ldx, const float* mean, const flo
                             float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
                             const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N,
                             int D, int H, int W, int C, float* ws, int dtype, void* stream);
+/* The same two without the ReLU (relu = 0): InstanceNorm3d alone, as in the residual
+ * norm(query + out) of CrossAttentionFusion (attention_fusion.py:161-162). */
+int mmseg_instnorm_apply(const void* x, int ldx, void* y, int ldy, int N, long long V, int C, const float* mean,
+                         const float* rstd, int relu, int dtype, void* stream);
+int mmseg_instnorm_bwd(const void* x, int ldx, const float* mean, const float* rstd, const void* p1, int ld1,
+                       float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
+                       const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N, int D,
+                       int H, int W, int C, int relu, float* ws, int dtype, void* stream);
 /* MaxPool3d(2) forward + argmax (0..7, z-major; first max wins) (unet.py:73). */
 int mmseg_maxpool2_fwd(const void* x, int ldx, void* y, int ldy, uint8_t* idx, int N, int D, int H, int W, int C,
                        int dtype, void* stream);
@@ -160,6 +168,28 @@ int mmseg_attn_gate_bwd(const void* const* srcs, const int* lds, int M, const vo
                         int C, const float* pooled, const float* W1, const float* W2, const float* hbuf,
                         const float* wts, float* beta, float* gW1, float* gb1, float* gW2, float* gb2, int Hd,
                         float* ws, int accumulate, int dtype, void* stream);
+
+/* ------------------------------------------- multi-head cross-attention */
+/* CrossAttentionFusion (attention_fusion.py:77-164, unwired in the reference's model factory).
+ * Batched NT GEMM on MFMA: C[b][i][j] (+)= alpha * sum_k A[b][i][k] * B[b][j][k] (+ bias[j]), batch index
+ * b = outer * inner + in, operand X at X + outer*sX_outer + in*sX_inner, row stride ldX (elements).
+ * A/B in the storage dtype (K, lda, ldb, A/B strides multiples of 8, 16-B aligned); C fp32 (c_dtype 0) or
+ * the storage dtype.  Replaces the 1x1 Conv3d projections (:117-120, :159), einsum("bhdn,bhdm->bhnm")
+ * (:147-148), einsum("bhnm,bhdm->bhdn") (:153) and their gradients. */
+int mmseg_bgemm_nt(const void* a, long long sa_outer, long long sa_inner, int lda, const void* b, long long sb_outer,
+                   long long sb_inner, int ldb, void* c, long long sc_outer, long long sc_inner, int ldc,
+                   const float* bias, int batch, int inner, int M, int N, int K, float alpha, int accumulate,
+                   int c_dtype, int dtype, void* stream);
+/* dst[b][c][r] = src[b][r][c] with dtype conversion (0 fp32, 1 bf16): operand re-layout and the
+ * NCDHW fp32 <-> NDHWC module boundary. */
+int mmseg_transpose(const void* src, long long s_outer, long long s_inner, int lds, int src_dtype, void* dst,
+                    long long d_outer, long long d_inner, int ldd, int dst_dtype, int batch, int inner, int rows,
+                    int cols, void* stream);
+/* Row softmax of fp32 scores into P (storage dtype), F.softmax(attn, dim=-1) (:149), and its backward
+ * dS = P * (dP - rowsum(dP * P)). */
+int mmseg_softmax_rows(const float* S, int lds, void* P, int ldp, long long rows, int N, int dtype, void* stream);
+int mmseg_softmax_bwd_rows(const void* P, int ldp, const float* dP, int lddp, void* dS, int ldds, long long rows,
+                           int N, int dtype, void* stream);
 
 /* ------------------------------------------------- head, loss, metric */
 /* NCDHW fp32 volume channels [c0, c0+cnt) -> NDHWC 8-channel engine layout

@@ -16,6 +16,8 @@
 // single-thread-per-output sweep), so results are bitwise reproducible.
 #include "mmseg_common.h"
 
+#include <type_traits>
+
 namespace {
 
 // ------------------------------------------------------------------ stats
@@ -180,7 +182,7 @@ __global__ void in_stats_from_bricks(const float* __restrict__ part, int N, int 
 
 // y = relu((x - mean) * rstd); a thread owns 8 channels of one sample (their
 // mean / rstd stay in registers) and UNR voxels per step; grid (chunks, N).
-template <typename T>
+template <typename T, bool RELU = true>
 __global__ void in_relu_apply(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, int V, int C, int vpc,
                               const float* __restrict__ mean, const float* __restrict__ rstd) {
   const int n = blockIdx.y;
@@ -206,7 +208,7 @@ __global__ void in_relu_apply(const T* __restrict__ x, int ldx, T* __restrict__ 
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float h = (a[u].get(j) - mu[j]) * rs[j];
-        o.set(j, h > 0.f ? h : 0.f);
+        o.set(j, (!RELU || h > 0.f) ? h : 0.f);
       }
       o.store(yn + (long long)(vb + u * lanes_v) * ldy);
     }
@@ -345,7 +347,7 @@ struct DyCtx {
 };
 
 // partial sums of g and g*xhat, g = dy * [xhat > 0]
-template <typename T>
+template <typename T, bool RELU = true>
 __global__ void in_bwd_partial(const T* __restrict__ x, int ldx, const float* __restrict__ mean,
                                const float* __restrict__ rstd, DySrc s, int V, int C, int D, int H, int W, int vpc,
                                float* __restrict__ part) {
@@ -384,7 +386,7 @@ __global__ void in_bwd_partial(const T* __restrict__ x, int ldx, const float* __
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float h = (a[u].get(j) - mu[j]) * rs[j];
-          const float g = h > 0.f ? dy[j] : 0.f;
+          const float g = (!RELU || h > 0.f) ? dy[j] : 0.f;
           sg[j] += g;
           sgx[j] = fmaf(g, h, sgx[j]);
         }
@@ -432,7 +434,7 @@ __global__ void in_bwd_finalize(const float* __restrict__ part, int N, int C, in
 }
 
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)); same thread layout as the apply kernels
-template <typename T>
+template <typename T, bool RELU = true>
 __global__ void in_bwd_apply(const T* __restrict__ x, int ldx, const float* __restrict__ mean,
                              const float* __restrict__ rstd, DySrc s, const float* __restrict__ coef, T* __restrict__ dx,
                              int lddx, int V, int C, int D, int H, int W, int vpc) {
@@ -476,7 +478,7 @@ __global__ void in_bwd_apply(const T* __restrict__ x, int ldx, const float* __re
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float h = (a[u].get(j) - mu[j]) * rs[j];
-        const float g = h > 0.f ? dy[j] : 0.f;
+        const float g = (!RELU || h > 0.f) ? dy[j] : 0.f;
         o.set(j, rs[j] * (g - ca[j] - h * cb[j]));
       }
       o.store(dxn + (long long)(vb + u * lanes_v) * lddx);
@@ -727,20 +729,41 @@ int mmseg_instnorm_stats_bricks(const float* part, int N, int C, int nb, int cnt
   return mmseg::check_launch("instnorm_stats_bricks");
 }
 
+int mmseg_instnorm_apply(const void* x, int ldx, void* y, int ldy, int N, long long V, int C, const float* mean,
+                         const float* rstd, int relu, int dtype, void* stream);
+int mmseg_instnorm_bwd(const void* x, int ldx, const float* mean, const float* rstd, const void* p1, int ld1,
+                       float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
+                       const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N, int D,
+                       int H, int W, int C, int relu, float* ws, int dtype, void* stream);
+
 int mmseg_instnorm_relu_fwd(const void* x, int ldx, void* y, int ldy, int N, long long V, int C, const float* mean,
                             const float* rstd, int dtype, void* stream) {
-  MMSEG_REQUIRE(C % 8 == 0 && C <= 2048, "instnorm_relu_fwd: C=%d must be a multiple of 8", C);
-  MMSEG_REQUIRE(V * (ldx > ldy ? ldx : ldy) < (1LL << 31), "instnorm_relu_fwd: per-sample extent must fit int32");
+  return mmseg_instnorm_apply(x, ldx, y, ldy, N, V, C, mean, rstd, 1, dtype, stream);
+}
+
+int mmseg_instnorm_apply(const void* x, int ldx, void* y, int ldy, int N, long long V, int C, const float* mean,
+                         const float* rstd, int relu, int dtype, void* stream) {
+  MMSEG_REQUIRE(C % 8 == 0 && C <= 2048, "instnorm_apply: C=%d must be a multiple of 8", C);
+  MMSEG_REQUIRE(V * (ldx > ldy ? ldx : ldy) < (1LL << 31), "instnorm_apply: per-sample extent must fit int32");
   hipStream_t s = (hipStream_t)stream;
   int vpc;
   const dim3 grid(apply_chunks(V, C, &vpc), N);
-  if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(in_relu_apply<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, (bf16_t*)y, ldy, (int)V,
-                       C, vpc, mean, rstd);
-  else
-    hipLaunchKernelGGL(in_relu_apply<float>, grid, dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy, (int)V, C,
-                       vpc, mean, rstd);
-  return mmseg::check_launch("instnorm_relu_fwd");
+  if (dtype == MMSEG_BF16) {
+    if (relu)
+      hipLaunchKernelGGL((in_relu_apply<bf16_t, true>), grid, dim3(256), 0, s, (const bf16_t*)x, ldx, (bf16_t*)y, ldy,
+                         (int)V, C, vpc, mean, rstd);
+    else
+      hipLaunchKernelGGL((in_relu_apply<bf16_t, false>), grid, dim3(256), 0, s, (const bf16_t*)x, ldx, (bf16_t*)y,
+                         ldy, (int)V, C, vpc, mean, rstd);
+  } else {
+    if (relu)
+      hipLaunchKernelGGL((in_relu_apply<float, true>), grid, dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy,
+                         (int)V, C, vpc, mean, rstd);
+    else
+      hipLaunchKernelGGL((in_relu_apply<float, false>), grid, dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy,
+                         (int)V, C, vpc, mean, rstd);
+  }
+  return mmseg::check_launch("instnorm_apply");
 }
 
 // dy sources: see DySrc.  Any of p1 / beta / pool_dy may be null.
@@ -748,6 +771,14 @@ int mmseg_instnorm_relu_bwd(const void* x, int ldx, const float* mean, const flo
                             float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
                             const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N,
                             int D, int H, int W, int C, float* ws, int dtype, void* stream) {
+  return mmseg_instnorm_bwd(x, ldx, mean, rstd, p1, ld1, scale1, alpha1, alpha_stride, beta, beta_stride, pool_dy,
+                            pool_ld, pool_idx, dx, lddx, N, D, H, W, C, 1, ws, dtype, stream);
+}
+
+int mmseg_instnorm_bwd(const void* x, int ldx, const float* mean, const float* rstd, const void* p1, int ld1,
+                            float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
+                            const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N,
+                            int D, int H, int W, int C, int relu, float* ws, int dtype, void* stream) {
   MMSEG_REQUIRE(C % 8 == 0 && C <= 2048, "instnorm_bwd: C=%d must be a multiple of 8 and <= 2048", C);
   MMSEG_REQUIRE(!pool_dy || ((D | H | W) & 1) == 0, "instnorm_bwd: pooled gather needs even dims");
   const long long V = (long long)D * H * W;
@@ -762,18 +793,21 @@ int mmseg_instnorm_relu_bwd(const void* x, int ldx, const float* mean, const flo
   float* part = ws;
   float* coef = ws + (long long)N * nch * C * 2;
   dim3 grid(nch, N), agrid(anch, N);
+  auto run = [&](auto tag, auto relu_c) {
+    using T = decltype(tag);
+    constexpr bool R = decltype(relu_c)::value;
+    hipLaunchKernelGGL((in_bwd_partial<T, R>), grid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, (int)V, C, D,
+                       H, W, (int)vpc, part);
+    hipLaunchKernelGGL(in_bwd_finalize, dim3(ceil_div(N * C, 4)), dim3(256), 0, s, part, N, C, nch, V, coef);
+    hipLaunchKernelGGL((in_bwd_apply<T, R>), agrid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, coef, (T*)dx,
+                       lddx, (int)V, C, D, H, W, avpc);
+  };
   if (dtype == MMSEG_BF16) {
-    hipLaunchKernelGGL(in_bwd_partial<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, mean, rstd, src, (int)V,
-                       C, D, H, W, (int)vpc, part);
-    hipLaunchKernelGGL(in_bwd_finalize, dim3(ceil_div(N * C, 4)), dim3(256), 0, s, part, N, C, nch, V, coef);
-    hipLaunchKernelGGL(in_bwd_apply<bf16_t>, agrid, dim3(256), 0, s, (const bf16_t*)x, ldx, mean, rstd, src, coef,
-                       (bf16_t*)dx, lddx, (int)V, C, D, H, W, avpc);
+    if (relu) run(bf16_t{}, std::true_type{});
+    else run(bf16_t{}, std::false_type{});
   } else {
-    hipLaunchKernelGGL(in_bwd_partial<float>, grid, dim3(256), 0, s, (const float*)x, ldx, mean, rstd, src, (int)V, C,
-                       D, H, W, (int)vpc, part);
-    hipLaunchKernelGGL(in_bwd_finalize, dim3(ceil_div(N * C, 4)), dim3(256), 0, s, part, N, C, nch, V, coef);
-    hipLaunchKernelGGL(in_bwd_apply<float>, agrid, dim3(256), 0, s, (const float*)x, ldx, mean, rstd, src, coef,
-                       (float*)dx, lddx, (int)V, C, D, H, W, avpc);
+    if (relu) run(float{}, std::true_type{});
+    else run(float{}, std::false_type{});
   }
   return mmseg::check_launch("instnorm_relu_bwd");
 }

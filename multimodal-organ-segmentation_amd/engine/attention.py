@@ -1,0 +1,258 @@
+"""Multi-head cross-attention of CrossAttentionFusion (reference
+src/models/fusion/attention_fusion.py:77-164) as a fixed sequence of HIP
+launches (csrc/attention.hip + the InstanceNorm kernels of norm_pool.hip).
+
+Layout: features are NDHWC [B][V][C] in the engine storage dtype; head h is
+the channel slice [h*hd, (h+1)*hd) (the reference's view(B, heads, hd, V),
+:141-143), addressed through the batched GEMM's (sample, head) strides.
+Every product is `mmseg_bgemm_nt` (C = alpha * A B^T, both operands
+K-contiguous); operands that are not are re-laid out by `mmseg_transpose`.
+
+Forward (:129-164)                         Backward
+  Qp = q Wq^T + bq  (and Kp, Vp from kv)     dR = IN_bwd(R, dy)            (no ReLU)
+  S  = scale * Qp_h Kp_h^T   [B,h,V,V] f32   dO = dR Wo ; gWo = dR^T O ; gbo = colsum dR
+  P  = softmax_rows(S)                       dP = dO_h Vp_h^T ; dS = P (dP - rowsum(dP P))
+  O_h = P Vp_h                               dVp_h = P^T dO_h ; dQp_h = scale dS Kp_h
+  R  = q + O Wo^T + bo                       dKp_h = scale dS^T Qp_h
+  y  = InstanceNorm3d(R)                     projections: gW = dY^T X, gb = colsum dY,
+                                             dq = dR + dQp Wq, dkv = dKp Wk + dVp Wv
+Dropout on attn (:150) is the identity (p = 0, or eval mode).
+"""
+from __future__ import annotations
+
+from typing import Dict
+
+import torch
+
+from .._lib import ptr
+from .runtime import Runtime
+
+F32 = 0
+IN_EPS = 1e-5
+
+
+class CrossAttentionEngine:
+    def __init__(self, rt: Runtime, channels: int, heads: int):
+        if channels % heads:
+            raise ValueError("in_channels must be divisible by num_heads")
+        self.rt, self.C, self.h = rt, channels, heads
+        self.hd = channels // heads
+        if self.hd % 8 or channels % 8:
+            raise ValueError("the engine needs head_dim and channels to be multiples of 8")
+        self.scale = self.hd ** -0.5
+
+    # -------------------------------------------------------------- helpers
+    def _empty(self, *shape, f32=False):
+        return torch.empty(*shape, dtype=torch.float32 if f32 else self.rt.dtype, device=self.rt.device)
+
+    def _tr(self, src, s_o, s_i, lds, sdt, dst, d_o, d_i, ldd, ddt, batch, inner, rows, cols):
+        self.rt.lib.mmseg_transpose(ptr(src), s_o, s_i, lds, sdt, ptr(dst), d_o, d_i, ldd, ddt, batch, inner, rows,
+                                    cols, self.rt.stream)
+
+    def _gemm(self, a, sa, lda, b, sb, ldb, c, sc, ldc, batch, inner, M, N, K, alpha=1.0, bias=None, acc=False,
+              c_f32=False):
+        self.rt.lib.mmseg_bgemm_nt(ptr(a), sa[0], sa[1], lda, ptr(b), sb[0], sb[1], ldb, ptr(c), sc[0], sc[1], ldc,
+                                   ptr(bias), batch, inner, M, N, K, float(alpha), int(acc),
+                                   F32 if c_f32 else self.rt.code, self.rt.code, self.rt.stream)
+
+    def _cast(self, w: torch.Tensor) -> torch.Tensor:
+        """fp32 weight [Co][Ci] -> storage dtype, same layout (a 1 x n transpose)."""
+        out = self._empty(w.numel())
+        self._tr(w, 0, 0, w.numel(), F32, out, 0, 0, 1, self.rt.code, 1, 1, 1, w.numel())
+        return out
+
+    def _castT(self, w: torch.Tensor) -> torch.Tensor:
+        """fp32 weight [Co][Ci] -> storage dtype [Ci][Co]."""
+        C = self.C
+        out = self._empty(C * C)
+        self._tr(w, 0, 0, C, F32, out, 0, 0, C, self.rt.code, 1, 1, C, C)
+        return out
+
+    def _from_ncdhw(self, x: torch.Tensor) -> torch.Tensor:
+        B, C = x.shape[:2]
+        V = x[0, 0].numel()
+        out = self._empty(B * V * C)
+        self._tr(x, C * V, 0, V, F32, out, V * C, 0, C, self.rt.code, B, 1, C, V)
+        return out
+
+    def _to_ncdhw(self, t: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
+        B, C = like.shape[:2]
+        V = like[0, 0].numel()
+        out = torch.empty(like.shape, dtype=torch.float32, device=self.rt.device)
+        self._tr(t, V * C, 0, C, self.rt.code, out, C * V, 0, V, F32, B, 1, V, C)
+        return out
+
+    def _proj(self, x, w_c, bias, out, M, acc=False):
+        C = self.C
+        self._gemm(x, (0, 0), C, w_c, (0, 0), C, out, (0, 0), C, 1, 1, M, C, C, bias=bias, acc=acc)
+
+    def _wgrad(self, dy, x, gw: torch.Tensor, gb: torch.Tensor, M: int, ws: Dict):
+        """gW[co][ci] (+)= sum_v dY[v][co] X[v][ci]; gb[co] (+)= sum_v dY[v][co]."""
+        C, L = self.C, self.rt.lib
+        dyt, xt = ws["t1"], ws["t2"]
+        self._tr(dy, 0, 0, C, self.rt.code, dyt, 0, 0, M, self.rt.code, 1, 1, M, C)
+        self._tr(x, 0, 0, C, self.rt.code, xt, 0, 0, M, self.rt.code, 1, 1, M, C)
+        self._gemm(dyt, (0, 0), M, xt, (0, 0), M, gw, (0, 0), C, 1, 1, C, C, M, acc=ws["acc"], c_f32=True)
+        part = self.rt.ws(256 * C)
+        L.mmseg_colsum(ptr(dy), C, C, M, ptr(part), 256, ptr(gb), int(ws["acc"]), self.rt.code, self.rt.stream)
+
+    # -------------------------------------------------------------- forward
+    def forward(self, q: torch.Tensor, kv: torch.Tensor, p: Dict[str, torch.Tensor]):
+        """q, kv: NCDHW fp32 [B, C, *spatial]; p: {q_w, q_b, k_w, k_b, v_w, v_b, o_w, o_b} fp32.
+        Returns (y NCDHW fp32, saved state for backward)."""
+        B, C = q.shape[:2]
+        V = q[0, 0].numel()
+        h, hd = self.h, self.hd
+        if V % 8:
+            raise ValueError("the engine needs the voxel count to be a multiple of 8")
+        M = B * V
+        L, s, code = self.rt.lib, self.rt.stream, self.rt.code
+        st = {"shape": (B, V)}
+        qf, kvf = self._from_ncdhw(q), self._from_ncdhw(kv)
+        R = self._from_ncdhw(q)
+        wc = {k: self._cast(p[k + "_w"]) for k in ("q", "k", "v", "o")}
+        Qp, Kp, Vp = self._empty(M * C), self._empty(M * C), self._empty(M * C)
+        self._proj(qf, wc["q"], p["q_b"], Qp, M)
+        self._proj(kvf, wc["k"], p["k_b"], Kp, M)
+        self._proj(kvf, wc["v"], p["v_b"], Vp, M)
+        S = self._empty(B * h * V * V, f32=True)
+        hs = (V * C, hd)                                   # (sample, head) strides of a head slice
+        ss = (h * V * V, V * V)
+        self._gemm(Qp, hs, C, Kp, hs, C, S, ss, V, B * h, h, V, V, hd, alpha=self.scale, c_f32=True)
+        P = self._empty(B * h * V * V)
+        L.mmseg_softmax_rows(ptr(S), V, ptr(P), V, B * h * V, V, code, s)
+        Vt = self._empty(B * h * hd * V)
+        ts = (h * hd * V, hd * V)
+        self._tr(Vp, V * C, hd, C, code, Vt, ts[0], ts[1], V, code, B * h, h, V, hd)
+        O = self._empty(M * C)
+        self._gemm(P, ss, V, Vt, ts, V, O, hs, C, B * h, h, V, hd, V)
+        self._proj(O, wc["o"], p["o_b"], R, M, acc=True)   # R = q + out_proj(O)
+        mean = torch.empty(B * C, dtype=torch.float32, device=self.rt.device)
+        rstd = torch.empty(B * C, dtype=torch.float32, device=self.rt.device)
+        ws = self.rt.ws(L.mmseg_instnorm_ws_floats(B, V, C))
+        L.mmseg_instnorm_stats(ptr(R), C, B, V, C, IN_EPS, ptr(mean), C, ptr(rstd), ptr(ws), code, s)
+        y = self._empty(M * C)
+        L.mmseg_instnorm_apply(ptr(R), C, ptr(y), C, B, V, C, ptr(mean), ptr(rstd), 0, code, s)
+        st.update(qf=qf, kvf=kvf, Qp=Qp, Kp=Kp, Vp=Vp, P=P, O=O, R=R, mean=mean, rstd=rstd)
+        return self._to_ncdhw(y, q), st
+
+    # ------------------------------------------------------------- backward
+    def backward(self, dy: torch.Tensor, st: Dict, p: Dict[str, torch.Tensor], grads: Dict[str, torch.Tensor],
+                 accumulate: bool):
+        """dy: NCDHW fp32.  Writes (accumulate: adds) the parameter gradients into grads[...];
+        returns (dq, dkv) NCDHW fp32."""
+        B, V = st["shape"]
+        C, h, hd = self.C, self.h, self.hd
+        M = B * V
+        L, s, code = self.rt.lib, self.rt.stream, self.rt.code
+        dyf = self._from_ncdhw(dy)
+        dR = self._empty(M * C)
+        ws = self.rt.ws(L.mmseg_instnorm_ws_floats(B, V, C))
+        # InstanceNorm3d backward without ReLU (p1 = dy); spatial dims only matter for the pooled gather
+        L.mmseg_instnorm_bwd(ptr(st["R"]), C, ptr(st["mean"]), ptr(st["rstd"]), ptr(dyf), C, 1.0, None, 0, None, 0,
+                             None, 0, None, ptr(dR), C, B, 1, 1, V, C, 0, ptr(ws), code, s)
+        tws = {"t1": self._empty(M * C), "t2": self._empty(M * C), "acc": accumulate}
+        wT = {k: self._castT(p[k + "_w"]) for k in ("q", "k", "v", "o")}
+        # out_proj
+        self._wgrad(dR, st["O"], grads["o_w"], grads["o_b"], M, tws)
+        dO = self._empty(M * C)
+        self._proj(dR, wT["o"], None, dO, M)
+        # attention
+        hs, ss = (V * C, hd), (h * V * V, V * V)
+        ts = (h * hd * V, hd * V)
+        dP = self._empty(B * h * V * V, f32=True)
+        self._gemm(dO, hs, C, st["Vp"], hs, C, dP, ss, V, B * h, h, V, V, hd, c_f32=True)
+        dS = self._empty(B * h * V * V)
+        L.mmseg_softmax_bwd_rows(ptr(st["P"]), V, ptr(dP), V, ptr(dS), V, B * h * V, V, code, s)
+        XT = self._empty(B * h * V * V)                    # P^T, then dS^T
+        HT = self._empty(B * h * hd * V)                   # per-head [hd][V] operand
+        dQp, dKp, dVp = self._empty(M * C), self._empty(M * C), self._empty(M * C)
+        # dV_h = P^T dO_h
+        self._tr(st["P"], ss[0], ss[1], V, code, XT, ss[0], ss[1], V, code, B * h, h, V, V)
+        self._tr(dO, V * C, hd, C, code, HT, ts[0], ts[1], V, code, B * h, h, V, hd)
+        self._gemm(XT, ss, V, HT, ts, V, dVp, hs, C, B * h, h, V, hd, V)
+        # dQ_h = scale dS K_h
+        self._tr(st["Kp"], V * C, hd, C, code, HT, ts[0], ts[1], V, code, B * h, h, V, hd)
+        self._gemm(dS, ss, V, HT, ts, V, dQp, hs, C, B * h, h, V, hd, V, alpha=self.scale)
+        # dK_h = scale dS^T Q_h
+        self._tr(dS, ss[0], ss[1], V, code, XT, ss[0], ss[1], V, code, B * h, h, V, V)
+        self._tr(st["Qp"], V * C, hd, C, code, HT, ts[0], ts[1], V, code, B * h, h, V, hd)
+        self._gemm(XT, ss, V, HT, ts, V, dKp, hs, C, B * h, h, V, hd, V, alpha=self.scale)
+        # projections
+        self._wgrad(dQp, st["qf"], grads["q_w"], grads["q_b"], M, tws)
+        self._wgrad(dKp, st["kvf"], grads["k_w"], grads["k_b"], M, tws)
+        self._wgrad(dVp, st["kvf"], grads["v_w"], grads["v_b"], M, tws)
+        self._proj(dQp, wT["q"], None, dR, M, acc=True)     # dq = dR (residual) + dQp Wq
+        dkv = self._empty(M * C)
+        self._proj(dKp, wT["k"], None, dkv, M)
+        self._proj(dVp, wT["v"], None, dkv, M, acc=True)
+        return self._to_ncdhw(dR, dy), self._to_ncdhw(dkv, dy)
+
+
+class FusionHeadEngine:
+    """BidirectionalCrossAttention's head (reference attention_fusion.py:196-200, 214):
+    y = ReLU(InstanceNorm3d(Conv3d(2C -> C, k=1)(cat([a, b], dim=1)))).  The concatenation is one NDHWC
+    [V][2C] buffer both inputs are transposed into (torch.cat never runs); the 1x1 conv and its gradients are
+    mmseg_bgemm_nt products, the norm the ReLU-fused InstanceNorm kernels."""
+
+    def __init__(self, rt: Runtime, channels: int):
+        self.rt, self.C = rt, channels
+
+    def _empty(self, n, f32=False):
+        return torch.empty(n, dtype=torch.float32 if f32 else self.rt.dtype, device=self.rt.device)
+
+    def _tr(self, *a):
+        self.rt.lib.mmseg_transpose(*a, self.rt.stream)
+
+    def _gemm(self, a, lda, b, ldb, c, ldc, M, N, K, bias=None, acc=False, c_f32=False):
+        self.rt.lib.mmseg_bgemm_nt(ptr(a), 0, 0, lda, ptr(b), 0, 0, ldb, ptr(c), 0, 0, ldc, ptr(bias), 1, 1, M, N, K,
+                                   1.0, int(acc), F32 if c_f32 else self.rt.code, self.rt.code, self.rt.stream)
+
+    def forward(self, a: torch.Tensor, b: torch.Tensor, w: torch.Tensor, bias: torch.Tensor):
+        B, C = a.shape[:2]
+        V = a[0, 0].numel()
+        M, L, s, code = B * V, self.rt.lib, self.rt.stream, self.rt.code
+        X = self._empty(M * 2 * C)
+        for i, t in enumerate((a, b)):     # NCDHW fp32 -> channel slot i of the [V][2C] concat buffer
+            self._tr(ptr(t), C * V, 0, V, F32, ptr(X) + i * C * X.element_size(), V * 2 * C, 0, 2 * C, code, B, 1, C,
+                     V)
+        wc = self._empty(C * 2 * C)
+        self._tr(ptr(w), 0, 0, w.numel(), F32, ptr(wc), 0, 0, 1, code, 1, 1, 1, w.numel())
+        Z = self._empty(M * C)
+        self._gemm(X, 2 * C, wc, 2 * C, Z, C, M, C, 2 * C, bias=bias)
+        mean = torch.empty(B * C, dtype=torch.float32, device=self.rt.device)
+        rstd = torch.empty(B * C, dtype=torch.float32, device=self.rt.device)
+        ws = self.rt.ws(L.mmseg_instnorm_ws_floats(B, V, C))
+        L.mmseg_instnorm_stats(ptr(Z), C, B, V, C, IN_EPS, ptr(mean), C, ptr(rstd), ptr(ws), code, s)
+        y = self._empty(M * C)
+        L.mmseg_instnorm_apply(ptr(Z), C, ptr(y), C, B, V, C, ptr(mean), ptr(rstd), 1, code, s)
+        out = torch.empty(a.shape, dtype=torch.float32, device=self.rt.device)
+        self._tr(ptr(y), V * C, 0, C, code, ptr(out), C * V, 0, V, F32, B, 1, V, C)
+        return out, {"shape": (B, V), "X": X, "Z": Z, "mean": mean, "rstd": rstd}
+
+    def backward(self, dy: torch.Tensor, st, w: torch.Tensor, gw: torch.Tensor, gb: torch.Tensor):
+        B, V = st["shape"]
+        C, M, L, s, code = self.C, B * V, self.rt.lib, self.rt.stream, self.rt.code
+        dyf = self._empty(M * C)
+        self._tr(ptr(dy), C * V, 0, V, F32, ptr(dyf), V * C, 0, C, code, B, 1, C, V)
+        dZ = self._empty(M * C)
+        ws = self.rt.ws(L.mmseg_instnorm_ws_floats(B, V, C))
+        L.mmseg_instnorm_bwd(ptr(st["Z"]), C, ptr(st["mean"]), ptr(st["rstd"]), ptr(dyf), C, 1.0, None, 0, None, 0,
+                             None, 0, None, ptr(dZ), C, B, 1, 1, V, C, 1, ptr(ws), code, s)
+        dZt, Xt = self._empty(C * M), self._empty(2 * C * M)
+        self._tr(ptr(dZ), 0, 0, C, code, ptr(dZt), 0, 0, M, code, 1, 1, M, C)
+        self._tr(ptr(st["X"]), 0, 0, 2 * C, code, ptr(Xt), 0, 0, M, code, 1, 1, M, 2 * C)
+        self._gemm(dZt, M, Xt, M, gw, 2 * C, C, 2 * C, M, c_f32=True)          # gW[co][ci] = sum_v dZ X
+        part = self.rt.ws(256 * C)
+        L.mmseg_colsum(ptr(dZ), C, C, M, ptr(part), 256, ptr(gb), 0, code, s)
+        wt = self._empty(2 * C * C)
+        self._tr(ptr(w), 0, 0, 2 * C, F32, ptr(wt), 0, 0, C, code, 1, 1, C, 2 * C)   # W^T [2C][C]
+        dX = self._empty(M * 2 * C)
+        self._gemm(dZ, C, wt, C, dX, 2 * C, M, 2 * C, C)
+        outs = []
+        for i in range(2):
+            o = torch.empty(B, C, *dy.shape[2:], dtype=torch.float32, device=self.rt.device)
+            self._tr(ptr(dX) + i * C * dX.element_size(), V * 2 * C, 0, 2 * C, code, ptr(o), C * V, 0, V, F32, B, 1,
+                     V, C)
+            outs.append(o)
+        return outs

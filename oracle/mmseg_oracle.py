@@ -188,6 +188,15 @@ def cross_attention_fusion(p: Params, prefix: str, q_feat: Tensor, kv_feat: Tens
     return F.instance_norm(q_feat + conv("out_proj", out), eps=IN_EPS)
 
 
+def bidirectional_cross_attention(p: Params, prefix: str, f1: Tensor, f2: Tensor, num_heads: int) -> Tensor:
+    """BidirectionalCrossAttention.forward (reference attention_fusion.py:202-216): both directions, then
+    Conv3d(2C -> C, 1) + InstanceNorm3d + ReLU (:196-200)."""
+    a = cross_attention_fusion(p, prefix + "cross_attn_1to2.", f1, f2, num_heads)
+    b = cross_attention_fusion(p, prefix + "cross_attn_2to1.", f2, f1, num_heads)
+    z = F.conv3d(torch.cat([a, b], dim=1), p[prefix + "fusion.0.weight"], p[prefix + "fusion.0.bias"])
+    return F.relu(F.instance_norm(z, eps=IN_EPS))
+
+
 # --------------------------------------------------------------------------
 # losses / metric
 # --------------------------------------------------------------------------

@@ -199,6 +199,24 @@ def cross_attention_case():
     print("cross attention done")
 
 
+def bidirectional_case():
+    """BidirectionalCrossAttention (attention_fusion.py:167-216): two CrossAttentionFusion + 2C->C 1x1 conv,
+    InstanceNorm3d, ReLU; forward, input and parameter gradients at 6^3, C=32, 4 heads."""
+    torch.manual_seed(5)
+    mod = attn_mod.BidirectionalCrossAttention(32, num_heads=4)
+    g = torch.Generator().manual_seed(6)
+    f1 = torch.randn(2, 32, 6, 6, 6, generator=g).requires_grad_(True)
+    f2 = torch.randn(2, 32, 6, 6, 6, generator=g).requires_grad_(True)
+    o = mod(f1, f2)
+    w = torch.randn(o.shape, generator=g)
+    (o * w).sum().backward()
+    np.savez_compressed(os.path.join(OUT, "bidirectional_attention.npz"), f1=f1.detach().numpy(),
+                        f2=f2.detach().numpy(), out=o.detach().numpy(), cot=w.numpy(), d1=f1.grad.numpy(),
+                        d2=f2.grad.numpy(), **{"p_" + k: v.detach().numpy() for k, v in mod.state_dict().items()},
+                        **{"g_" + k: p.grad.numpy() for k, p in mod.named_parameters()})
+    print("bidirectional attention done")
+
+
 def full_case(tag, cfg, S, B, seed):
     """Full-size configs: forward summary only (logits stats + seeded voxel samples)."""
     torch.manual_seed(seed)
@@ -225,6 +243,10 @@ def full_case(tag, cfg, S, B, seed):
 
 if __name__ == "__main__":
     torch.set_num_threads(8)
+    if len(sys.argv) > 1:          # regenerate only the named cases, e.g. `make_golden.py bidirectional_case`
+        for name in sys.argv[1:]:
+            globals()[name]()
+        sys.exit(0)
     feats = [8, 16, 32, 64, 128]
     model_case("unet_tiny", base_config("unet", ["CT", "PET"], 3, feats), S=32, B=2, full_logits=True)
     for fz in ("cross_attention", "concat", "add", "attention"):

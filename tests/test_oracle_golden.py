@@ -108,6 +108,18 @@ def test_oracle_cross_attention_fusion():
     assert O.normwise_rel(kv.grad, torch.from_numpy(g["dkv"])) < 1e-5
 
 
+def test_oracle_bidirectional_cross_attention():
+    g = golden("bidirectional_attention")
+    p = {k[2:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("p_")}
+    f1 = torch.from_numpy(g["f1"]).requires_grad_(True)
+    f2 = torch.from_numpy(g["f2"]).requires_grad_(True)
+    out = O.bidirectional_cross_attention(p, "", f1, f2, num_heads=4)
+    assert O.normwise_rel(out, torch.from_numpy(g["out"])) < 1e-6
+    (out * torch.from_numpy(g["cot"])).sum().backward()
+    assert O.normwise_rel(f1.grad, torch.from_numpy(g["d1"])) < 1e-5
+    assert O.normwise_rel(f2.grad, torch.from_numpy(g["d2"])) < 1e-5
+
+
 def test_full_config_param_init_pinned():
     """full-size init checksums: the oracle's RNG order reproduces the reference's 22.6M / 36.7M params"""
     for tag, kind in (("full_unet_c2", "unet"), ("full_dual_c3", "dual")):
