@@ -191,6 +191,19 @@ int mmseg_softmax_rows(const float* S, int lds, void* P, int ldp, long long rows
 int mmseg_softmax_bwd_rows(const void* P, int ldp, const float* dP, int lddp, void* dS, int ldds, long long rows,
                            int N, int dtype, void* stream);
 
+/* ------------------------------------------------ sliding-window inference */
+/* MONAI sliding_window_inference (constant blending) as called by Trainer._sliding_window_inference
+ * (trainer.py:370-395).  win: device int[4*nw] = (n, z0, y0, x0) per window in the volume's frame
+ * (starts may be negative / past the end: zero padding).  gather: windows [nw][C][r0][r1][r2] of the
+ * NCDHW fp32 volume; accum: out[n] += one window's logits [C][r0][r1][r2] (call per window, in order);
+ * norm: out /= cz[z] * cy[y] * cx[x] (the per-axis window coverage). */
+int mmseg_window_gather(const float* vol, int N, int C, int D, int H, int W, const int* win, int nw, int r0, int r1,
+                        int r2, float* out, void* stream);
+int mmseg_window_accum(const float* logits, int N, int C, int D, int H, int W, int n, int z0, int y0, int x0, int r0,
+                       int r1, int r2, float* out, void* stream);
+int mmseg_window_norm(float* out, int N, int C, int D, int H, int W, const float* cz, const float* cy, const float* cx,
+                      void* stream);
+
 /* ------------------------------------------------- head, loss, metric */
 /* NCDHW fp32 volume channels [c0, c0+cnt) -> NDHWC 8-channel engine layout
  * (batch["image"] as consumed by the first Conv3d, unet.py:181 / dual_encoder.py:133). */

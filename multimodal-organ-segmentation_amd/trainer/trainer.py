@@ -222,7 +222,19 @@ class Trainer:
         return self.history
 
     def predict(self, input_path, output_path) -> None:  # pragma: no cover - NIfTI I/O is out of scope
-        raise NotImplementedError("inference over NIfTI folders is outside the engine's scope (SURVEY §8f rank 2)")
+        raise NotImplementedError("inference over NIfTI folders is outside the engine's scope (SURVEY §8f rank 2); "
+                                  "volumes already in memory go through _sliding_window_inference")
+
+    def _sliding_window_inference(self, image: torch.Tensor) -> torch.Tensor:
+        """reference trainer.py:370-395: MONAI sliding_window_inference(image, roi_size, sw_batch_size=
+        inference.batch_size, predictor=model, overlap) on device (inference/sliding_window.py).  The
+        reference's ImportError fallback (one full-volume forward) is not taken: the device restatement
+        always exists."""
+        from ..inference import sliding_window_inference
+        inf = self.config.get("inference", {})
+        sw = inf.get("sliding_window", {})
+        return sliding_window_inference(image.to(self.device), tuple(sw.get("roi_size", (96, 96, 96))),
+                                        int(inf.get("batch_size", 4)), self.model, float(sw.get("overlap", 0.5)))
 
     def _save_checkpoints(self, metrics: Dict[str, float]) -> None:
         """reference trainer.py:397-433 (rank 0 only)."""

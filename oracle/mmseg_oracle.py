@@ -198,6 +198,55 @@ def bidirectional_cross_attention(p: Params, prefix: str, f1: Tensor, f2: Tensor
 
 
 # --------------------------------------------------------------------------
+# sliding-window inference (reference trainer.py:370-395 -> MONAI 1.3
+# monai.inferers.sliding_window_inference, constant blending; MONAI is absent
+# here, so this restates its published algorithm: parity vs MONAI unpinned)
+# --------------------------------------------------------------------------
+def sliding_window_inference(inputs: Tensor, roi_size, sw_batch_size: int, predictor, overlap: float = 0.25) -> Tensor:
+    """CPU restatement: pad to the roi (zeros, symmetric), scan interval int(roi * (1 - overlap)) (roi when the
+    padded size equals the roi), dense_patch_slices starts (last window clamped to the end), windows image-major
+    in meshgrid 'ij' order, batched sw_batch_size at a time, output += pred, count_map += 1, output / count_map,
+    crop.  `predictor` receives each window batch on its own device; results are accumulated on the CPU."""
+    import math
+    N, M = inputs.shape[:2]
+    size = list(inputs.shape[2:])
+    roi = [r if r > 0 else s for r, s in zip(roi_size, size)]
+    pad = []
+    for k in range(len(size) - 1, -1, -1):          # F.pad order: last dim first
+        diff = max(roi[k] - size[k], 0)
+        pad += [diff // 2, diff - diff // 2]
+    x = F.pad(inputs.float().cpu(), pad, mode="constant", value=0.0)
+    psize = list(x.shape[2:])
+    interval = []
+    for r, s in zip(roi, psize):
+        interval.append(r if r == s else max(int(r * (1 - overlap)), 1))
+    starts = []
+    for d in range(3):
+        num = int(math.ceil(float(psize[d]) / interval[d]))
+        scan = next((i for i in range(num) if i * interval[d] + roi[d] >= psize[d]), None)
+        cnt = scan + 1 if scan is not None else 1
+        starts.append([i * interval[d] - max(i * interval[d] + roi[d] - psize[d], 0) for i in range(cnt)])
+    slices = [(a, b, c) for a in starts[0] for b in starts[1] for c in starts[2]]
+    wins = [(n, s_) for n in range(N) for s_ in slices]
+    out, count = None, None
+    dev = inputs.device
+    for b0 in range(0, len(wins), sw_batch_size):
+        chunk = wins[b0:b0 + sw_batch_size]
+        batch = torch.stack([x[n, :, a:a + roi[0], b:b + roi[1], c:c + roi[2]] for n, (a, b, c) in chunk])
+        pred = predictor(batch.to(dev))
+        pred = (pred[0] if isinstance(pred, (tuple, list)) else pred).float().cpu()
+        if out is None:
+            out = torch.zeros(N, pred.shape[1], *psize)
+            count = torch.zeros(N, 1, *psize)
+        for k, (n, (a, b, c)) in enumerate(chunk):
+            out[n, :, a:a + roi[0], b:b + roi[1], c:c + roi[2]] += pred[k]
+            count[n, :, a:a + roi[0], b:b + roi[1], c:c + roi[2]] += 1.0
+    out = out / count
+    lo = [pad[2 * (2 - d)] for d in range(3)]
+    return out[:, :, lo[0]:lo[0] + size[0], lo[1]:lo[1] + size[1], lo[2]:lo[2] + size[2]]
+
+
+# --------------------------------------------------------------------------
 # losses / metric
 # --------------------------------------------------------------------------
 def _softmax_onehot(pred: Tensor, target: Tensor):

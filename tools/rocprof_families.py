@@ -39,9 +39,13 @@ def family(name: str) -> str:
     if m:
         tile = "128x32" if (m.group(2), m.group(3)) == ("4", "1") else "128x64"
         return f"conv_gemm_kernel<{_MODES[m.group(1)]},{tile}>[{dt}]"
-    m = re.search(r"wgrad_brick([2r])_kernelI(?:DF16b|f)Li(\d+)E", name)
+    m = re.search(r"conv3_brick3_kernelI(?:DF16b|f)Li(\d+)E", name)
     if m:
-        return f"wgrad_brick{m.group(1)}_kernel<CO{int(m.group(2)) * 16}>[{dt}]"
+        return f"conv3_brick3_kernel<BN{m.group(1)}>[{dt}]"
+    m = re.search(r"wgrad_brick([2r])_kernelI(?:DF16b|f)Li(\d+)E(?:Li(\d)E)?", name)
+    if m:
+        v3 = ",V3" if m.group(3) == "3" else ""
+        return f"wgrad_brick{m.group(1)}_kernel<CO{int(m.group(2)) * 16}{v3}>[{dt}]"
     m = re.search(r"wgrad_reduce_kernelILi(\d+)E|wgrad_reduce_kernel<(\d+)>", name)
     if m:
         return f"wgrad_reduce_kernel<{m.group(1) or m.group(2)}>"
@@ -50,6 +54,9 @@ def family(name: str) -> str:
     m = re.search(r"(?<![a-z_])wgrad_kernelI(?:DF16b|f)Li(\d)E", name)
     if m:
         return f"wgrad_kernel<{_MODES[m.group(1)]}>[{dt}]"
+    m = re.search(r"\(anonymous namespace\)::([A-Za-z_][A-Za-z0-9_]*)[<(]", name)
+    if m:
+        return m.group(1)
     m = re.search(r"(?:_GLOBAL__N_1\d+|::)([A-Za-z_][A-Za-z0-9_]*?)(?:I|\(|E|$)", name)
     return m.group(1) if m else name
 
