@@ -144,6 +144,11 @@ int mmseg_instnorm_relu_bwd(const void* x, int ldx, const float* mean, const flo
                             float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
                             const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N,
                             int D, int H, int W, int C, float* ws, int dtype, void* stream);
+/* Statistics + normalisation (+ ReLU if relu) in one call: y = [relu]((x - mean) * rstd), mean / rstd written as
+ * by mmseg_instnorm_stats (mean_ld == C).  Volumes of <= 4096 voxels per sample take one fused launch (one block
+ * per 8-channel group and sample, the 12^3 / 6^3 levels); larger ones the stats + apply passes. */
+int mmseg_instnorm_fwd(const void* x, int ldx, void* y, int ldy, int N, long long V, int C, float eps, float* mean,
+                       int mean_ld, float* rstd, int relu, float* ws, int dtype, void* stream);
 /* The same two without the ReLU (relu = 0): InstanceNorm3d alone, as in the residual
  * norm(query + out) of CrossAttentionFusion (attention_fusion.py:161-162). */
 int mmseg_instnorm_apply(const void* x, int ldx, void* y, int ldy, int N, long long V, int C, const float* mean,

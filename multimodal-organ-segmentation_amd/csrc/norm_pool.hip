@@ -16,6 +16,7 @@
 // single-thread-per-output sweep), so results are bitwise reproducible.
 #include "mmseg_common.h"
 
+#include <stdlib.h>
 #include <type_traits>
 
 namespace {
@@ -486,6 +487,163 @@ __global__ void in_bwd_apply(const T* __restrict__ x, int ldx, const float* __re
   }
 }
 
+
+// ------------------------------------------------- small-volume fused IN
+// The 24^3 / 12^3 / 6^3 levels (V <= 16384 voxels per sample): one block of
+// 1024 threads per (8-channel group, sample) holds the whole reduction, so
+// InstanceNorm forward is ONE launch (statistics, then the normalised output
+// from a second, L2-resident read) instead of partial + finalize + apply, and
+// the backward likewise.  Per-thread Welford / sums in fp32, then a fixed
+// pairwise tree over the 1024 threads in LDS (deterministic).
+constexpr int SMALL_T = 1024;
+
+template <typename T, bool RELU>
+__global__ __launch_bounds__(SMALL_T) void in_small_fwd(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy,
+                                                       int V, int C, float eps, float* __restrict__ mean,
+                                                       int mean_ld, float* __restrict__ rstd) {
+  __shared__ float smu[SMALL_T * 8], sm2[SMALL_T * 8], scnt[SMALL_T];
+  const int cg = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
+  const T* xn = x + (long long)n * V * ldx + cg * 8;
+  float mu[8], m2[8], cnt = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) mu[j] = m2[j] = 0.f;
+  auto upd = [&](const V8<T>& a) {
+    cnt += 1.f;
+    const float inv = 1.f / cnt;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xv = a.get(j), d = xv - mu[j];
+      mu[j] = fmaf(d, inv, mu[j]);
+      m2[j] = fmaf(d, xv - mu[j], m2[j]);
+    }
+  };
+  int v = tid;
+  for (; v + 3 * SMALL_T < V; v += 4 * SMALL_T) {   // 4 loads in flight
+    V8<T> a[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u].load(xn + (long long)(v + u * SMALL_T) * ldx);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) upd(a[u]);
+  }
+  for (; v < V; v += SMALL_T) {
+    V8<T> a;
+    a.load(xn + (long long)v * ldx);
+    upd(a);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    smu[tid * 8 + j] = mu[j];
+    sm2[tid * 8 + j] = m2[j];
+  }
+  scnt[tid] = cnt;
+  __syncthreads();
+  for (int st = SMALL_T / 2; st > 0; st >>= 1) {   // Chan merge of thread t and t + st, fixed pairs
+    if (tid < st) {
+      const float na = scnt[tid], nb = scnt[tid + st], nn = na + nb;
+      if (nb > 0.f) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float ma = smu[tid * 8 + j], mb = smu[(tid + st) * 8 + j], dl = mb - ma;
+          smu[tid * 8 + j] = ma + dl * (nb / nn);
+          sm2[tid * 8 + j] = sm2[tid * 8 + j] + sm2[(tid + st) * 8 + j] + dl * dl * (na * nb / nn);
+        }
+        scnt[tid] = nn;
+      }
+    }
+    __syncthreads();
+  }
+  float m[8], rs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    m[j] = smu[j];
+    rs[j] = 1.f / sqrtf(sm2[j] / (float)V + eps);
+  }
+  if (tid < 8) {
+    mean[(long long)n * mean_ld + cg * 8 + tid] = smu[tid];
+    rstd[n * C + cg * 8 + tid] = 1.f / sqrtf(sm2[tid] / (float)V + eps);
+  }
+  T* yn = y + (long long)n * V * ldy + cg * 8;
+  for (int v = tid; v < V; v += SMALL_T) {
+    V8<T> a, o;
+    a.load(xn + (long long)v * ldx);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float h = (a.get(j) - m[j]) * rs[j];
+      o.set(j, (!RELU || h > 0.f) ? h : 0.f);
+    }
+    o.store(yn + (long long)v * ldy);
+  }
+}
+
+template <typename T, bool RELU>
+__global__ __launch_bounds__(SMALL_T) void in_small_bwd(const T* __restrict__ x, int ldx, const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd, DySrc s, T* __restrict__ dx,
+                                                       int lddx, int V, int C, int D, int H, int W) {
+  __shared__ float sa[SMALL_T * 8], sb[SMALL_T * 8];
+  const int cg = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
+  float mu[8], rs[8], ga[8], gb[8];
+  load8f(mean + n * C + cg * 8, mu);
+  load8f(rstd + n * C + cg * 8, rs);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ga[j] = gb[j] = 0.f;
+  const DyCtx<T> dc(s, n, V, cg, C, D, H, W);
+  const T* xn = x + (long long)n * V * ldx + cg * 8;
+  for (int v = tid; v < V; v += SMALL_T) {
+    V8<T> a;
+    typename DyCtx<T>::Raw r;
+    a.load(xn + (long long)v * ldx);
+    dc.load(v, r);
+    float dy[8];
+    dc.combine(r, dy);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float h = (a.get(j) - mu[j]) * rs[j];
+      const float g = (!RELU || h > 0.f) ? dy[j] : 0.f;
+      ga[j] += g;
+      gb[j] = fmaf(g, h, gb[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sa[tid * 8 + j] = ga[j];
+    sb[tid * 8 + j] = gb[j];
+  }
+  __syncthreads();
+  for (int st = SMALL_T / 2; st > 0; st >>= 1) {
+    if (tid < st) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sa[tid * 8 + j] += sa[(tid + st) * 8 + j];
+        sb[tid * 8 + j] += sb[(tid + st) * 8 + j];
+      }
+    }
+    __syncthreads();
+  }
+  float ca[8], cb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ca[j] = sa[j] / (float)V;
+    cb[j] = sb[j] / (float)V;
+  }
+  T* dxn = dx + (long long)n * V * lddx + cg * 8;
+  for (int v = tid; v < V; v += SMALL_T) {
+    V8<T> a;
+    typename DyCtx<T>::Raw r;
+    a.load(xn + (long long)v * ldx);
+    dc.load(v, r);
+    float dy[8];
+    dc.combine(r, dy);
+    V8<T> o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float h = (a.get(j) - mu[j]) * rs[j];
+      const float g = (!RELU || h > 0.f) ? dy[j] : 0.f;
+      o.set(j, rs[j] * (g - ca[j] - h * cb[j]));
+    }
+    o.store(dxn + (long long)v * lddx);
+  }
+}
+
 // ---------------------------------------------------------------- fusion
 // out[n,v,c] = sum_m w_m * src_m[n,v,c],  w_m = wconst or wts[n*M + m]
 struct FuseSrc {
@@ -666,6 +824,11 @@ int grid_for(long long total) {
   return (int)b;
 }
 
+int knob_small_v() {   // read per call (A/B runs and tests flip it in-process)
+  const char* e = getenv("MMSEG_IN_SMALL_V");
+  return e ? atoi(e) : 4096;
+}
+
 int chunks_for(long long V, int C, long long* vpc) {
   // reduction passes: ~16 voxels per thread (lanes_v = 256 / C8 voxel lanes), at most 1024 chunks
   const int lanes_v = 256 / (C >> 3);
@@ -731,10 +894,39 @@ int mmseg_instnorm_stats_bricks(const float* part, int N, int C, int nb, int cnt
 
 int mmseg_instnorm_apply(const void* x, int ldx, void* y, int ldy, int N, long long V, int C, const float* mean,
                          const float* rstd, int relu, int dtype, void* stream);
+int mmseg_instnorm_stats(const void* x, int ldx, int N, long long V, int C, float eps, float* mean, int mean_ld,
+                         float* rstd, float* ws, int dtype, void* stream);
 int mmseg_instnorm_bwd(const void* x, int ldx, const float* mean, const float* rstd, const void* p1, int ld1,
                        float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
                        const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N, int D,
                        int H, int W, int C, int relu, float* ws, int dtype, void* stream);
+
+int mmseg_instnorm_fwd(const void* x, int ldx, void* y, int ldy, int N, long long V, int C, float eps, float* mean,
+                       int mean_ld, float* rstd, int relu, float* ws, int dtype, void* stream) {
+  MMSEG_REQUIRE(C % 8 == 0 && C <= 2048, "instnorm_fwd: C=%d must be a multiple of 8", C);
+  if (V > knob_small_v()) {
+    if (mmseg_instnorm_stats(x, ldx, N, V, C, eps, mean, mean_ld, rstd, ws, dtype, stream)) return 1;
+    MMSEG_REQUIRE(mean_ld == C, "instnorm_fwd: the apply pass reads mean with ld = C");
+    return mmseg_instnorm_apply(x, ldx, y, ldy, N, V, C, mean, rstd, relu, dtype, stream);
+  }
+  MMSEG_REQUIRE(V * (ldx > ldy ? ldx : ldy) < (1LL << 31), "instnorm_fwd: per-sample extent must fit int32");
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid(C / 8, N);
+  auto run = [&](auto tag, auto relu_c) {
+    using T = decltype(tag);
+    constexpr bool R = decltype(relu_c)::value;
+    hipLaunchKernelGGL((in_small_fwd<T, R>), grid, dim3(SMALL_T), 0, s, (const T*)x, ldx, (T*)y, ldy, (int)V, C, eps,
+                       mean, mean_ld, rstd);
+  };
+  if (dtype == MMSEG_BF16) {
+    if (relu) run(bf16_t{}, std::true_type{});
+    else run(bf16_t{}, std::false_type{});
+  } else {
+    if (relu) run(float{}, std::true_type{});
+    else run(float{}, std::false_type{});
+  }
+  return mmseg::check_launch("instnorm_fwd");
+}
 
 int mmseg_instnorm_relu_fwd(const void* x, int ldx, void* y, int ldy, int N, long long V, int C, const float* mean,
                             const float* rstd, int dtype, void* stream) {
@@ -793,9 +985,15 @@ int mmseg_instnorm_bwd(const void* x, int ldx, const float* mean, const float* r
   float* part = ws;
   float* coef = ws + (long long)N * nch * C * 2;
   dim3 grid(nch, N), agrid(anch, N);
+  const bool small = V <= knob_small_v();
   auto run = [&](auto tag, auto relu_c) {
     using T = decltype(tag);
     constexpr bool R = decltype(relu_c)::value;
+    if (small) {
+      hipLaunchKernelGGL((in_small_bwd<T, R>), dim3(C / 8, N), dim3(SMALL_T), 0, s, (const T*)x, ldx, mean, rstd, src,
+                         (T*)dx, lddx, (int)V, C, D, H, W);
+      return;
+    }
     hipLaunchKernelGGL((in_bwd_partial<T, R>), grid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, (int)V, C, D,
                        H, W, (int)vpc, part);
     hipLaunchKernelGGL(in_bwd_finalize, dim3(ceil_div(N * C, 4)), dim3(256), 0, s, part, N, C, nch, V, coef);

@@ -349,10 +349,11 @@ class Block:
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
         if part is not None:
             L.mmseg_instnorm_stats_bricks(ptr(part), x.N, x.C, nb, x.V // nb, IN_EPS, ptr(m), x.C, ptr(r), s)
+            L.mmseg_instnorm_relu_fwd(x.ptr, x.ld, y.ptr, y.ld, x.N, x.V, x.C, ptr(m), ptr(r), code, s)
         else:
             ws = self.rt.ws(L.mmseg_instnorm_ws_floats(x.N, x.V, x.C))
-            L.mmseg_instnorm_stats(x.ptr, x.ld, x.N, x.V, x.C, IN_EPS, ptr(m), x.C, ptr(r), ptr(ws), code, s)
-        L.mmseg_instnorm_relu_fwd(x.ptr, x.ld, y.ptr, y.ld, x.N, x.V, x.C, ptr(m), ptr(r), code, s)
+            L.mmseg_instnorm_fwd(x.ptr, x.ld, y.ptr, y.ld, x.N, x.V, x.C, IN_EPS, ptr(m), x.C, ptr(r), 1, ptr(ws),
+                                 code, s)
 
     def _norm_bwd(self, x: Act, m: torch.Tensor, r: torch.Tensor, dy: DySpec, dx: Act):
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code

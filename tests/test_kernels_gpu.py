@@ -189,9 +189,11 @@ def test_point_conv(dev, dtype):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
-@pytest.mark.parametrize("C,shape", [(32, (2, 6, 8, 4)), (8, (1, 4, 4, 4)), (256, (2, 2, 4, 2))])
-def test_instnorm_relu_maxpool(dev, dtype, C, shape):
+@pytest.mark.parametrize("C,shape", [(32, (2, 6, 8, 4)), (8, (1, 4, 4, 4)), (256, (2, 2, 4, 2)), (64, (2, 24, 24, 24))])
+@pytest.mark.parametrize("small_v", ["16384", "0"])     # fused one-block-per-channel-group path / multi-pass path
+def test_instnorm_relu_maxpool(dev, dtype, C, shape, small_v, monkeypatch):
     """IN+ReLU fwd, MaxPool3d fwd (argmax), IN+ReLU bwd with dy = skip + maxpool_bwd."""
+    monkeypatch.setenv("MMSEG_IN_SMALL_V", small_v)
     torch.manual_seed(C)
     N, D, H, W = shape
     x = (torch.randn(N, C, D, H, W, device=dev) * 2 + 0.7)
@@ -200,8 +202,8 @@ def test_instnorm_relu_maxpool(dev, dtype, C, shape):
     ya = Act(torch.empty_like(xa.buf), 0, C, C, N, D, H, W)
     stats = torch.empty(2, N * C, device=dev)
     ws = torch.empty(L.mmseg_instnorm_ws_floats(N, D * H * W, C), device=dev)
-    L.mmseg_instnorm_stats(xa.ptr, C, N, D * H * W, C, 1e-5, ptr(stats[0]), C, ptr(stats[1]), ptr(ws), code, s)
-    L.mmseg_instnorm_relu_fwd(xa.ptr, C, ya.ptr, C, N, D * H * W, C, ptr(stats[0]), ptr(stats[1]), code, s)
+    L.mmseg_instnorm_fwd(xa.ptr, C, ya.ptr, C, N, D * H * W, C, 1e-5, ptr(stats[0]), C, ptr(stats[1]), 1, ptr(ws),
+                         code, s)
     xd = _q(x, dtype).requires_grad_(True)
     yref = torch.relu(F.instance_norm(xd, eps=1e-5))
     y = from_ndhwc(ya.buf, N, C, D, H, W)
