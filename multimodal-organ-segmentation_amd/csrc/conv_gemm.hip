@@ -729,7 +729,7 @@ __device__ __forceinline__ void buf_load_v8<float>(V8<float>& v, __amdgpu_buffer
   }
 }
 
-template <typename T, int BN>
+template <typename T, int BN, bool WU = false>
 __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kernel(GemmArgs g, int upb) {
   using L = Brick2Layout<T>;
   constexpr int BZ = 4, HZ = BZ + 2;
@@ -816,11 +816,15 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kern
       }
     }
   };
+  // Every thread issues W_PER loads / stores unconditionally (items past the stage are clamped onto the
+  // last item: a duplicate load and an identical store), so the compiler cannot sink a predicated load
+  // past the tap loop, where its latency would be exposed right before store_w.
   auto load_w = [&](int n0, int c, int kz) {
 #pragma unroll
     for (int k = 0; k < W_PER; ++k) {
-      const int e = tid + k * 256;
-      if (e < W_ITEMS) {
+      const int e0 = tid + k * 256;
+      if (WU || e0 < W_ITEMS) {
+        const int e = WU ? min(e0, W_ITEMS - 1) : e0;
         const int cgw = e & 3, q = e >> 2;
         const int col = q % BN, t9 = q / BN;
         const int kgi = (kz * 9 + t9) * (cin / 8) + c * 4 + cgw;
@@ -831,8 +835,9 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kern
   auto store_w = [&]() {
 #pragma unroll
     for (int k = 0; k < W_PER; ++k) {
-      const int e = tid + k * 256;
-      if (e < W_ITEMS) {
+      const int e0 = tid + k * 256;
+      if (WU || e0 < W_ITEMS) {
+        const int e = WU ? min(e0, W_ITEMS - 1) : e0;
         const int cgw = e & 3, q = e >> 2;
         wr[k].store(Wl + (q * L::QV + (cgw ^ w2_swz(q)) * L::QG) * EPQ);
       }
@@ -2512,7 +2517,10 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
       const int units = nb1 * (g.Ncols / 32);
       const int upb = maxblk > 0 ? ceil_div(units, maxblk) : 1;
       mmseg::note_kernel("conv3_brick3_kernel<BN32>");
-      hipLaunchKernelGGL((conv3_brick3_kernel<T, 32>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
+      if (knob("MMSEG_BRICK3_WU", 0))
+        hipLaunchKernelGGL((conv3_brick3_kernel<T, 32, true>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
+      else
+        hipLaunchKernelGGL((conv3_brick3_kernel<T, 32, false>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
     } else if (g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
       mmseg::note_kernel("conv3_brick2_kernel<BN64,ZW1>");
       hipLaunchKernelGGL((conv3_brick2_kernel<T, 64, 1>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
