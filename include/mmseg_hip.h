@@ -178,7 +178,8 @@ int mmseg_attn_gate_bwd(const void* const* srcs, const int* lds, int M, const vo
 /* CrossAttentionFusion (attention_fusion.py:77-164, unwired in the reference's model factory).
  * Batched NT GEMM on MFMA: C[b][i][j] (+)= alpha * sum_k A[b][i][k] * B[b][j][k] (+ bias[j]), batch index
  * b = outer * inner + in, operand X at X + outer*sX_outer + in*sX_inner, row stride ldX (elements).
- * A/B in the storage dtype (K, lda, ldb, A/B strides multiples of 8, 16-B aligned); C fp32 (c_dtype 0) or
+ * A/B in the storage dtype (lda, ldb, A/B strides multiples of 8, 16-B aligned; K not a multiple of 8 reads the
+ * last 8-group whole, so the row padding up to round_up(K, 8) of A or B must be zero); C fp32 (c_dtype 0) or
  * the storage dtype.  Replaces the 1x1 Conv3d projections (:117-120, :159), einsum("bhdn,bhdm->bhnm")
  * (:147-148), einsum("bhnm,bhdm->bhdn") (:153) and their gradients. */
 int mmseg_bgemm_nt(const void* a, long long sa_outer, long long sa_inner, int lda, const void* b, long long sb_outer,
@@ -195,6 +196,19 @@ int mmseg_transpose(const void* src, long long s_outer, long long s_inner, int l
 int mmseg_softmax_rows(const float* S, int lds, void* P, int ldp, long long rows, int N, int dtype, void* stream);
 int mmseg_softmax_bwd_rows(const void* P, int ldp, const float* dP, int lddp, void* dS, int ldds, long long rows,
                            int N, int dtype, void* stream);
+
+/* Swin window attention (MONAI SwinUNETR WindowAttention, reached from swin_unetr.py:80-96; MONAI absent ->
+ * parity unpinned).  relpos_bias: bias[h][n][m] = table[index[n*N+m]][h] (table [T][heads]).
+ * softmax_bias_rows: rows = windows*heads*N of fp32 scores S, P = softmax(S + bias[h] + mask[w]) (row
+ * padding [N, ldp) of P written as zeros, as by mmseg_softmax_rows / _bwd_rows) with
+ * h = (row / N) % heads, w = (row / (N*heads)) % nw (bias / mask may be NULL).
+ * relpos_table_grad: dB[h][n][m] = sum_b dS[b][h][n][m] (B window batches, fixed order), then
+ * gtable[t][h] (+)= sum over the CSR list offs[t]..offs[t+1] of (n*N+m) entries of dB[h]. */
+int mmseg_relpos_bias(const float* table, const int* index, int heads, int N, float* bias, void* stream);
+int mmseg_softmax_bias_rows(const float* S, int lds, const float* bias, const float* mask, int nw, int heads, void* P,
+                            int ldp, long long rows, int N, int dtype, void* stream);
+int mmseg_relpos_table_grad(const void* dS, int ldn, int B, int heads, int N, float* dB, const int* offs,
+                            const int* pairs, int T, float* gtable, int accumulate, int dtype, void* stream);
 
 /* ------------------------------------------------ sliding-window inference */
 /* MONAI sliding_window_inference (constant blending) as called by Trainer._sliding_window_inference

@@ -146,6 +146,7 @@ __global__ __launch_bounds__(256) void softmax_rows_kernel(const float* __restri
   const float inv = 1.f / sum;
   T* p = P + row * ldp;
   for (int m = lane; m < N; m += 64) p[m] = (T)(__expf(s[m] - mx) * inv);
+  for (int m = N + lane; m < ldp; m += 64) p[m] = (T)0.f;   // zero row padding (a K pad of the next GEMM)
 }
 
 // dS = P * (dP - sum_m dP * P), softmax backward per row.
@@ -163,8 +164,88 @@ __global__ __launch_bounds__(256) void softmax_bwd_rows_kernel(const T* __restri
   dot = wave_sum(dot);
   T* o = dS + row * ldds;
   for (int m = lane; m < N; m += 64) o[m] = (T)((float)p[m] * (d[m] - dot));
+  for (int m = N + lane; m < ldds; m += 64) o[m] = (T)0.f;
 }
 
+
+// ---------------------------------------------------- Swin window attention
+// MONAI SwinUNETR WindowAttention (monai/networks/nets/swin_unetr.py, v1.3;
+// reference swin_unetr.py:80-96 constructs it): scores + relative-position
+// bias B[h][n][m] = table[index[n][m]][h] (+ the shifted-window mask
+// M[w][n][m] of window w = b % nw), softmax over m.
+__global__ void relpos_bias_kernel(const float* __restrict__ table, const int* __restrict__ index, int heads, int N,
+                                   float* __restrict__ bias) {
+  const long long total = (long long)heads * N * N;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int h = (int)(e / ((long long)N * N));
+    const long long nm = e - (long long)h * N * N;
+    bias[e] = table[(long long)index[nm] * heads + h];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void softmax_bias_rows_kernel(const float* __restrict__ S, int lds_,
+                                                                const float* __restrict__ bias,
+                                                                const float* __restrict__ mask, int nw, int heads,
+                                                                T* __restrict__ P, int ldp, long long rows, int N) {
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int n = (int)(row % N);
+  const long long bh = row / N;
+  const int h = (int)(bh % heads);
+  const long long b = bh / heads;
+  const float* s = S + row * lds_;
+  const float* br = bias ? bias + ((long long)h * N + n) * N : nullptr;
+  const float* mr = mask ? mask + ((long long)(b % nw) * N + n) * N : nullptr;
+  auto val = [&](int m) {
+    float v = s[m];
+    if (br) v += br[m];
+    if (mr) v += mr[m];
+    return v;
+  };
+  float mx = -INFINITY;
+  for (int m = lane; m < N; m += 64) mx = fmaxf(mx, val(m));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  float sum = 0.f;
+  for (int m = lane; m < N; m += 64) sum += __expf(val(m) - mx);
+  sum = wave_sum(sum);
+  const float inv = 1.f / sum;
+  T* p = P + row * ldp;
+  for (int m = lane; m < N; m += 64) p[m] = (T)(__expf(val(m) - mx) * inv);
+  for (int m = N + lane; m < ldp; m += 64) p[m] = (T)0.f;
+}
+
+// dB[h][n][m] = sum over window-batches b (fixed order) of dS[b][h][n][m]
+template <typename T>
+__global__ void bias_grad_sum_kernel(const T* __restrict__ dS, int ldn, int B, int heads, int N,
+                                     float* __restrict__ dB) {
+  const long long hnm = (long long)heads * N * N;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < hnm;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long hn = e / N;
+    const int m = (int)(e - hn * N);
+    float a = 0.f;
+    for (int b = 0; b < B; ++b) a += (float)dS[((long long)b * heads * N + hn) * ldn + m];
+    dB[e] = a;
+  }
+}
+
+// gtable[t][h] (+)= sum over the (n, m) pairs with index[n][m] == t (CSR lists, fixed order)
+__global__ void relpos_table_grad_kernel(const float* __restrict__ dB, const int* __restrict__ offs,
+                                         const int* __restrict__ pairs, int T, int heads, int N,
+                                         float* __restrict__ gtable, int accumulate) {
+  const long long total = (long long)T * heads;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int t = (int)(e / heads), h = (int)(e % heads);
+    float a = 0.f;
+    for (int k = offs[t]; k < offs[t + 1]; ++k) a += dB[(long long)h * N * N + pairs[k]];
+    gtable[e] = accumulate ? gtable[e] + a : a;
+  }
+}
 }  // namespace
 
 extern "C" {
@@ -175,9 +256,11 @@ int mmseg_bgemm_nt(const void* a, long long sa_outer, long long sa_inner, int ld
                    int c_dtype, int dtype, void* stream) {
   MMSEG_REQUIRE(batch >= 1 && inner >= 1 && batch % inner == 0, "bgemm_nt: batch=%d must be a multiple of inner=%d",
                 batch, inner);
-  MMSEG_REQUIRE(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && sa_outer % 8 == 0 && sa_inner % 8 == 0 &&
-                    sb_outer % 8 == 0 && sb_inner % 8 == 0,
-                "bgemm_nt: K, lda, ldb and the A/B batch strides must be multiples of 8 (16-B fragments)");
+  // K need not be a multiple of 8: the last 8-element group is read whole, so the caller keeps the row
+  // padding [K, round_up(K, 8)) of A or B zero (and the other finite) -- the attention buffers do
+  MMSEG_REQUIRE(lda % 8 == 0 && ldb % 8 == 0 && lda >= ((K + 7) & ~7) && ldb >= ((K + 7) & ~7) &&
+                    sa_outer % 8 == 0 && sa_inner % 8 == 0 && sb_outer % 8 == 0 && sb_inner % 8 == 0,
+                "bgemm_nt: lda, ldb (>= K rounded up to 8) and the A/B batch strides must be multiples of 8");
   MMSEG_REQUIRE(((uintptr_t)a & 15) == 0 && ((uintptr_t)b & 15) == 0, "bgemm_nt: A and B must be 16-B aligned");
   if (M <= 0 || N <= 0) return 0;
   BgemmArgs g{a, sa_outer, sa_inner, lda, b, sb_outer, sb_inner, ldb, c, sc_outer, sc_inner, ldc, bias,
@@ -234,6 +317,46 @@ int mmseg_softmax_bwd_rows(const void* P, int ldp, const float* dP, int lddp, vo
     hipLaunchKernelGGL(softmax_bwd_rows_kernel<float>, grid, dim3(256), 0, s, (const float*)P, ldp, dP, lddp,
                        (float*)dS, ldds, rows, N);
   return mmseg::check_launch("softmax_bwd_rows");
+}
+
+int mmseg_relpos_bias(const float* table, const int* index, int heads, int N, float* bias, void* stream) {
+  const long long total = (long long)heads * N * N;
+  hipLaunchKernelGGL(relpos_bias_kernel, dim3((unsigned)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192)),
+                     dim3(256), 0, (hipStream_t)stream, table, index, heads, N, bias);
+  return mmseg::check_launch("relpos_bias");
+}
+
+int mmseg_softmax_bias_rows(const float* S, int lds, const float* bias, const float* mask, int nw, int heads, void* P,
+                            int ldp, long long rows, int N, int dtype, void* stream) {
+  MMSEG_REQUIRE(!mask || nw >= 1, "softmax_bias_rows: mask needs nw >= 1");
+  MMSEG_REQUIRE(rows % ((long long)N * heads) == 0, "softmax_bias_rows: rows must be windows x heads x N");
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  if (dtype == MMSEG_BF16)
+    hipLaunchKernelGGL(softmax_bias_rows_kernel<bf16_t>, grid, dim3(256), 0, s, S, lds, bias, mask, nw, heads,
+                       (bf16_t*)P, ldp, rows, N);
+  else
+    hipLaunchKernelGGL(softmax_bias_rows_kernel<float>, grid, dim3(256), 0, s, S, lds, bias, mask, nw, heads,
+                       (float*)P, ldp, rows, N);
+  return mmseg::check_launch("softmax_bias_rows");
+}
+
+int mmseg_relpos_table_grad(const void* dS, int ldn, int B, int heads, int N, float* dB, const int* offs,
+                            const int* pairs, int T, float* gtable, int accumulate, int dtype, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const long long hnm = (long long)heads * N * N;
+  const unsigned g1 = (unsigned)((hnm + 255) / 256 < 8192 ? (hnm + 255) / 256 : 8192);
+  if (dtype == MMSEG_BF16)
+    hipLaunchKernelGGL(bias_grad_sum_kernel<bf16_t>, dim3(g1), dim3(256), 0, s, (const bf16_t*)dS, ldn, B, heads, N,
+                       dB);
+  else
+    hipLaunchKernelGGL(bias_grad_sum_kernel<float>, dim3(g1), dim3(256), 0, s, (const float*)dS, ldn, B, heads, N,
+                       dB);
+  if (mmseg::check_launch("bias_grad_sum")) return 1;
+  const long long th = (long long)T * heads;
+  hipLaunchKernelGGL(relpos_table_grad_kernel, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, dB, offs, pairs, T,
+                     heads, N, gtable, accumulate);
+  return mmseg::check_launch("relpos_table_grad");
 }
 
 }  // extern "C"

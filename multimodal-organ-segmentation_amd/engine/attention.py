@@ -256,3 +256,143 @@ class FusionHeadEngine:
                      V, C)
             outs.append(o)
         return outs
+
+
+class WindowAttentionEngine:
+    """MONAI SwinUNETR WindowAttention (window multi-head self-attention with relative-position bias and the
+    shifted-window mask) on the engine: x [B windows, N tokens, C] -> [B, N, C].  The qkv / proj linears, QK^T,
+    P.V and every gradient product are mmseg_bgemm_nt (MFMA); the bias gather, the biased softmax and the
+    bias-table gradient are csrc/attention.hip kernels.  head_dim = C / heads must be a multiple of 8 (16 in
+    SwinUNETR at every stage).  N (343 for a 7^3 window) need not be a multiple of 8: every [*][N] operand
+    is stored with its rows padded to ldn = round_up(N, 8) and the padding zeroed, which is what the GEMM's
+    K-tail contract asks for (the same for the B*N token dimension of the weight-gradient products)."""
+
+    def __init__(self, rt: Runtime, dim: int, heads: int):
+        if dim % heads or (dim // heads) % 8:
+            raise ValueError("WindowAttention engine: dim / num_heads must be a multiple of 8")
+        self.rt, self.C, self.h, self.hd = rt, dim, heads, dim // heads
+        self.scale = self.hd ** -0.5
+
+    def _empty(self, n, f32=False, zero=False):
+        f = torch.zeros if zero else torch.empty
+        return f(int(n), dtype=torch.float32 if f32 else self.rt.dtype, device=self.rt.device)
+
+    def _tr(self, src, s_o, s_i, lds, sdt, dst, d_o, d_i, ldd, ddt, batch, inner, rows, cols):
+        self.rt.lib.mmseg_transpose(ptr(src), s_o, s_i, lds, sdt, ptr(dst), d_o, d_i, ldd, ddt, batch, inner, rows,
+                                    cols, self.rt.stream)
+
+    def _gemm(self, a, sa, lda, b, sb, ldb, c, sc, ldc, batch, inner, M, N, K, alpha=1.0, bias=None, acc=False,
+              c_f32=False):
+        self.rt.lib.mmseg_bgemm_nt(ptr(a), sa[0], sa[1], lda, ptr(b), sb[0], sb[1], ldb, ptr(c), sc[0], sc[1], ldc,
+                                   ptr(bias), batch, inner, M, N, K, float(alpha), int(acc),
+                                   F32 if c_f32 else self.rt.code, self.rt.code, self.rt.stream)
+
+    def _cast(self, t: torch.Tensor) -> torch.Tensor:
+        if self.rt.code == F32:
+            return t.contiguous().reshape(-1)
+        out = self._empty(t.numel())
+        self._tr(t, 0, 0, t.numel(), F32, out, 0, 0, 1, self.rt.code, 1, 1, 1, t.numel())
+        return out
+
+    def _castT(self, w: torch.Tensor) -> torch.Tensor:
+        """fp32 [R][Cc] -> storage dtype [Cc][R]."""
+        R, Cc = w.shape
+        out = self._empty(R * Cc)
+        self._tr(w, 0, 0, Cc, F32, out, 0, 0, R, self.rt.code, 1, 1, R, Cc)
+        return out
+
+    def _to_f32(self, t: torch.Tensor, shape) -> torch.Tensor:
+        if self.rt.code == F32:
+            return t.view(shape)
+        out = torch.empty(shape, dtype=torch.float32, device=self.rt.device)
+        self._tr(t, 0, 0, t.numel(), self.rt.code, out, 0, 0, 1, F32, 1, 1, 1, t.numel())
+        return out
+
+    def _colsum(self, y, ch, M, out, acc):
+        part = self.rt.ws(256 * ch)
+        self.rt.lib.mmseg_colsum(ptr(y), ch, ch, M, ptr(part), 256, ptr(out), int(acc), self.rt.code, self.rt.stream)
+
+    def _wgrad(self, dy, ch_out, x, ch_in, M, gw, acc):
+        """gW[co][ci] (+)= sum_t dY[t][co] X[t][ci] over the M tokens (token rows padded to ldm, zeroed)."""
+        code = self.rt.code
+        ldm = (M + 7) // 8 * 8
+        t1, t2 = self._empty(ch_out * ldm, zero=True), self._empty(ch_in * ldm, zero=True)
+        self._tr(dy, 0, 0, ch_out, code, t1, 0, 0, ldm, code, 1, 1, M, ch_out)
+        self._tr(x, 0, 0, ch_in, code, t2, 0, 0, ldm, code, 1, 1, M, ch_in)
+        self._gemm(t1, (0, 0), ldm, t2, (0, 0), ldm, gw, (0, 0), ch_in, 1, 1, ch_out, ch_in, M, acc=acc, c_f32=True)
+
+    def forward(self, x: torch.Tensor, mask, p, index: torch.Tensor):
+        """x [B, N, C] fp32; mask [nw, N, N] fp32 or None; p: qkv_w [3C][C], qkv_b [3C] | None, proj_w [C][C],
+        proj_b [C], table [T][heads]; index int32 [N*N] (device)."""
+        B, N, C = x.shape
+        h, hd, M = self.h, self.hd, B * N
+        ldn = (N + 7) // 8 * 8
+        L, s, code = self.rt.lib, self.rt.stream, self.rt.code
+        xf = self._cast(x)
+        qkv = self._empty(M * 3 * C)
+        self._gemm(xf, (0, 0), C, self._cast(p["qkv_w"]), (0, 0), C, qkv, (0, 0), 3 * C, 1, 1, M, 3 * C, C,
+                   bias=p.get("qkv_b"))
+        qs = (N * 3 * C, hd)                        # head-slice strides inside qkv
+        ss = (h * N * ldn, N * ldn)                 # [B][h][N][ldn] score-shaped buffers
+        S = self._empty(B * h * N * ldn, f32=True)
+        self._gemm(qkv, qs, 3 * C, qkv[C:], qs, 3 * C, S, ss, ldn, B * h, h, N, N, hd, alpha=self.scale, c_f32=True)
+        bias = self._empty(h * N * N, f32=True)
+        L.mmseg_relpos_bias(ptr(p["table"]), ptr(index), h, N, ptr(bias), s)
+        P = self._empty(B * h * N * ldn)
+        nw = mask.shape[0] if mask is not None else 0
+        L.mmseg_softmax_bias_rows(ptr(S), ldn, ptr(bias), ptr(mask), nw, h, ptr(P), ldn, B * h * N, N, code, s)
+        ts = (h * hd * ldn, hd * ldn)               # [B][h][hd][ldn] per-head transposed operands
+        Vt = self._empty(B * h * hd * ldn, zero=True)
+        self._tr(qkv[2 * C:], qs[0], qs[1], 3 * C, code, Vt, ts[0], ts[1], ldn, code, B * h, h, N, hd)
+        O = self._empty(M * C)
+        hs = (N * C, hd)
+        self._gemm(P, ss, ldn, Vt, ts, ldn, O, hs, C, B * h, h, N, hd, N)
+        y = self._empty(M * C)
+        self._gemm(O, (0, 0), C, self._cast(p["proj_w"]), (0, 0), C, y, (0, 0), C, 1, 1, M, C, C, bias=p["proj_b"])
+        return self._to_f32(y, (B, N, C)), {"shape": (B, N), "xf": xf, "qkv": qkv, "P": P, "O": O}
+
+    def backward(self, dy: torch.Tensor, st, p, grads, csr, accumulate: bool = False):
+        B, N = st["shape"]
+        C, h, hd = self.C, self.h, self.hd
+        M = B * N
+        ldn = (N + 7) // 8 * 8
+        L, s, code = self.rt.lib, self.rt.stream, self.rt.code
+        qkv, P, O = st["qkv"], st["P"], st["O"]
+        dyf = self._cast(dy)
+        # proj
+        self._wgrad(dyf, C, O, C, M, grads["proj_w"], accumulate)
+        self._colsum(dyf, C, M, grads["proj_b"], accumulate)
+        dO = self._empty(M * C)
+        self._gemm(dyf, (0, 0), C, self._castT(p["proj_w"]), (0, 0), C, dO, (0, 0), C, 1, 1, M, C, C)
+        # attention core
+        qs, ss, hs = (N * 3 * C, hd), (h * N * ldn, N * ldn), (N * C, hd)
+        ts = (h * hd * ldn, hd * ldn)
+        dP = self._empty(B * h * N * ldn, f32=True)
+        self._gemm(dO, hs, C, qkv[2 * C:], qs, 3 * C, dP, ss, ldn, B * h, h, N, N, hd, c_f32=True)
+        dS = self._empty(B * h * N * ldn)
+        L.mmseg_softmax_bwd_rows(ptr(P), ldn, ptr(dP), ldn, ptr(dS), ldn, B * h * N, N, code, s)
+        dB = self._empty(h * N * N, f32=True)
+        offs, pairs, T = csr
+        L.mmseg_relpos_table_grad(ptr(dS), ldn, B, h, N, ptr(dB), ptr(offs), ptr(pairs), T, ptr(grads["table"]),
+                                  int(accumulate), code, s)
+        dqkv = self._empty(M * 3 * C)
+        XT = self._empty(B * h * N * ldn, zero=True)
+        HT = self._empty(B * h * hd * ldn, zero=True)
+        # dQ_h = scale dS K_h
+        self._tr(qkv[C:], qs[0], qs[1], 3 * C, code, HT, ts[0], ts[1], ldn, code, B * h, h, N, hd)
+        self._gemm(dS, ss, ldn, HT, ts, ldn, dqkv, qs, 3 * C, B * h, h, N, hd, N, alpha=self.scale)
+        # dK_h = scale dS^T Q_h
+        self._tr(dS, ss[0], ss[1], ldn, code, XT, ss[0], ss[1], ldn, code, B * h, h, N, N)
+        self._tr(qkv, qs[0], qs[1], 3 * C, code, HT, ts[0], ts[1], ldn, code, B * h, h, N, hd)
+        self._gemm(XT, ss, ldn, HT, ts, ldn, dqkv[C:], qs, 3 * C, B * h, h, N, hd, N, alpha=self.scale)
+        # dV_h = P^T dO_h
+        self._tr(P, ss[0], ss[1], ldn, code, XT, ss[0], ss[1], ldn, code, B * h, h, N, N)
+        self._tr(dO, hs[0], hs[1], C, code, HT, ts[0], ts[1], ldn, code, B * h, h, N, hd)
+        self._gemm(XT, ss, ldn, HT, ts, ldn, dqkv[2 * C:], qs, 3 * C, B * h, h, N, hd, N)
+        # qkv linear
+        self._wgrad(dqkv, 3 * C, st["xf"], C, M, grads["qkv_w"], accumulate)
+        if "qkv_b" in grads:
+            self._colsum(dqkv, 3 * C, M, grads["qkv_b"], accumulate)
+        dx = self._empty(M * C)
+        self._gemm(dqkv, (0, 0), 3 * C, self._castT(p["qkv_w"]), (0, 0), 3 * C, dx, (0, 0), C, 1, 1, M, C, 3 * C)
+        return self._to_f32(dx, (B, N, C))

@@ -197,6 +197,28 @@ def bidirectional_cross_attention(p: Params, prefix: str, f1: Tensor, f2: Tensor
     return F.relu(F.instance_norm(z, eps=IN_EPS))
 
 
+def window_attention(p: Params, prefix: str, x: Tensor, mask, num_heads: int, index: Tensor) -> Tensor:
+    """MONAI 1.3 SwinUNETR WindowAttention.forward (monai/networks/nets/swin_unetr.py; the reference builds it
+    through swin_unetr.py:80-96) restated: qkv linear, q * scale, q @ k^T, + relative-position bias, (+ mask of
+    window b % nW), softmax, @ v, proj.  MONAI is absent: parity vs MONAI itself is unpinned."""
+    b, n, c = x.shape
+    hd = c // num_heads
+    qkv = F.linear(x, p[prefix + "qkv.weight"], p.get(prefix + "qkv.bias"))
+    qkv = qkv.reshape(b, n, 3, num_heads, hd).permute(2, 0, 3, 1, 4)
+    q, k, v = qkv[0] * hd ** -0.5, qkv[1], qkv[2]
+    attn = q @ k.transpose(-2, -1)
+    table = p[prefix + "relative_position_bias_table"]
+    bias = table[index[:n, :n].reshape(-1)].reshape(n, n, -1).permute(2, 0, 1)
+    attn = attn + bias.unsqueeze(0)
+    if mask is not None:
+        nw = mask.shape[0]
+        attn = attn.view(b // nw, nw, num_heads, n, n) + mask.unsqueeze(1).unsqueeze(0)
+        attn = attn.view(-1, num_heads, n, n)
+    attn = torch.softmax(attn, dim=-1)
+    out = (attn @ v).transpose(1, 2).reshape(b, n, c)
+    return F.linear(out, p[prefix + "proj.weight"], p[prefix + "proj.bias"])
+
+
 # --------------------------------------------------------------------------
 # sliding-window inference (reference trainer.py:370-395 -> MONAI 1.3
 # monai.inferers.sliding_window_inference, constant blending; MONAI is absent
