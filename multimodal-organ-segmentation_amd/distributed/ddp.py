@@ -65,6 +65,7 @@ class GradBuckets:
                 size += param_sizes[lo]
             self.buckets.append((lo, hi, param_offsets[lo], param_offsets[hi - 1] + param_sizes[hi - 1]))
             hi = lo
+        self.comm = None
         self.owner = [0] * len(param_offsets)
         for b, (lo, hi, _, _) in enumerate(self.buckets):
             for i in range(lo, hi):
@@ -74,12 +75,21 @@ class GradBuckets:
     def reset(self):
         self.pending = [hi - lo for (lo, hi, _, _) in self.buckets]
         self.works = []
+        self.events = [dict() for _ in self.buckets]   # bucket -> {stream handle: event after its last write}
 
     def _reduce(self, b: int):
         _, _, lo, hi = self.buckets[b]
         t = self.grad[lo:hi]
         if dist.get_backend(self.group) == "nccl":
-            self.works.append(dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group, async_op=True))
+            # The engine may write a bucket's gradients from several HIP streams (one per modality encoder):
+            # the collective is issued from a dedicated stream that first waits for every contributing
+            # stream's last write, so no compute stream is blocked and no write is missed.
+            if self.comm is None:
+                self.comm = torch.cuda.Stream(self.grad.device)
+            for ev in self.events[b].values():
+                self.comm.wait_event(ev)
+            with torch.cuda.stream(self.comm):
+                self.works.append(dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group, async_op=True))
         else:  # gloo has no AVG
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
             t.div_(self.w)
@@ -88,6 +98,11 @@ class GradBuckets:
         if self.w == 1:
             return
         b = self.owner[idx]
+        if self.grad.is_cuda:
+            cur = torch.cuda.current_stream(self.grad.device)
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            self.events[b][cur.cuda_stream] = ev
         self.pending[b] -= 1
         if self.pending[b] == 0:
             self._reduce(b)
@@ -100,7 +115,7 @@ class GradBuckets:
                 self.pending[b] = 0
                 self._reduce(b)
         for wk in self.works:
-            wk.wait()
+            wk.wait()      # makes the current (optimizer) stream wait for the collective
         self.reset()
 
 

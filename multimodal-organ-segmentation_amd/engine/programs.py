@@ -12,6 +12,7 @@ Memory plan (per level l, spatial S/2^l, F[l] channels, NDHWC):
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 from typing import Dict, List, Optional, Tuple
@@ -251,22 +252,67 @@ class DualEncoderProgram:
             wconst = 1.0 if self.fusion == "add" else 1.0 / self.M
             L.mmseg_fuse_fwd(srcs, lds, self.M, wconst, None, out.ptr, out.ld, N, V, C, code, s)
 
+    # ------------------------------------------------------- modality streams
+    # The M encoders are independent until the per-level fusion (forward) and after the decoder backward
+    # (backward, mean / add fusion): encoder m runs on HIP stream m (stream 0 = the caller's), so the small
+    # 12^3 / 6^3 kernels of one modality fill the CUs the other one leaves idle.  Each stream has its own
+    # scratch arena (Runtime.ws); the streams join before the fusion / at the end of the backward.
+    def _streams(self):
+        main = torch.cuda.current_stream(self.rt.device)
+        if not self.multistream:
+            return [main] * self.M
+        if getattr(self, "_side", None) is None:
+            self._side = [torch.cuda.Stream(self.rt.device) for _ in range(self.M - 1)]
+        return [main] + self._side
+
+    @property
+    def multistream(self) -> bool:
+        # off by default: measured 8.61 vs 8.35 ms per 96^3 DualEncoder step (streams from level 1, 2 or 3
+        # alike) -- the small levels' kernels did not overlap enough to pay for the cross-stream joins
+        return self.M > 1 and os.environ.get("MMSEG_MODALITY_STREAMS", "0") != "0"
+
+    def _on(self, streams, m):
+        if streams[m] is streams[0]:
+            return contextlib.nullcontext()
+        streams[m].wait_stream(streams[0])
+        return torch.cuda.stream(streams[m])
+
+    @property
+    def stream_level(self) -> int:
+        """First level whose encoder work runs on the modality streams: the 96^3 / 48^3 levels fill the chip
+        on their own (run concurrently they only contend for L2 / Infinity Cache), the smaller ones do not."""
+        return int(os.environ.get("MMSEG_STREAM_FROM_LEVEL", "2"))
+
+    def _enc_fwd_levels(self, m: int, x: torch.Tensor, lo: int, hi: int):
+        L, code, s = self.rt.lib, self.rt.code, self.rt.stream
+        N, Cx, D, H, W = x.shape
+        blocks = self.encs[m]
+        for l in range(lo, hi):
+            if l == 0:
+                L.mmseg_pack_input(ptr(x), Cx, m, 1, N, D * H * W, self.xin[m].ptr, code, s)
+                blocks[0].fwd(self.xin[m], self.y[m][0])
+                continue
+            prev = self.y[m][l - 1]
+            L.mmseg_maxpool2_fwd(prev.ptr, prev.ld, self.pooled[m][l].ptr, self.pooled[m][l].ld,
+                                 ptr(self.idx[m][l]), N, *self.dims[l - 1], prev.C, code, s)
+            blocks[l].fwd(self.pooled[m][l], self.y[m][l])
+
     def forward(self, x: torch.Tensor, training: bool) -> torch.Tensor:
         N, Cx, D, H, W = x.shape
         if Cx != self.M:
             raise ValueError(f"DualEncoder expects {self.M} modalities, got {Cx} channels")
         self.setup(N, D, H, W)
-        L, s, code = self.rt.lib, self.rt.stream, self.rt.code
         self.pack()
-        for m in range(self.M):
-            L.mmseg_pack_input(ptr(x), Cx, m, 1, N, D * H * W, self.xin[m].ptr, code, s)
-            blocks = self.encs[m]
-            blocks[0].fwd(self.xin[m], self.y[m][0])
-            for l in range(1, self.L):
-                prev = self.y[m][l - 1]
-                L.mmseg_maxpool2_fwd(prev.ptr, prev.ld, self.pooled[m][l].ptr, self.pooled[m][l].ld,
-                                     ptr(self.idx[m][l]), N, *self.dims[l - 1], prev.C, code, s)
-                blocks[l].fwd(self.pooled[m][l], self.y[m][l])
+        streams = self._streams()
+        split = min(max(self.stream_level, 0), self.L)
+        for m in range(self.M):                      # big levels: one stream, modality after modality
+            self._enc_fwd_levels(m, x, 0, split)
+        for m in range(self.M):                      # small levels: modality m on stream m
+            with self._on(streams, m):
+                self._enc_fwd_levels(m, x, split, self.L)
+        for m in range(1, self.M):
+            if streams[m] is not streams[0]:
+                streams[0].wait_stream(streams[m])
         for l in range(self.L):
             self._fuse_fwd(l)
         return self.dec.fwd(self.bottom, training)
@@ -275,6 +321,9 @@ class DualEncoderProgram:
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
         self.dec.bwd(self.bottom, dlogits, accumulate)
         M = self.M
+        if self.fusion in ("mean", "add"):
+            self._encoders_bwd_streams(accumulate)
+            return
         for l in range(self.L - 1, -1, -1):
             dfused = self.fused_out(l)          # holds d(fused_l) now
             N, V, C = dfused.N, dfused.V, dfused.C
@@ -311,6 +360,36 @@ class DualEncoderProgram:
                     blk.bwd(self.pooled[m][l], dy, self.pooled[m][l], accumulate)
                 else:
                     blk.bwd(self.xin[m], dy, None, accumulate)
+
+
+    def _encoders_bwd_streams(self, accumulate: bool):
+        """Mean / add fusion: every d(fused_l) is final once the decoder backward ran, so modality m's whole
+        encoder backward (all levels) is independent of the other modalities' and runs on its own stream."""
+        M = self.M
+        sc = 1.0 if self.fusion == "add" else 1.0 / M
+        streams = self._streams()
+        split = min(max(self.stream_level, 0), self.L)
+
+        def levels(m, hi, lo):
+            for l in range(hi - 1, lo - 1, -1):
+                dy = DySpec(p1=self.fused_out(l), scale1=sc)
+                if l < self.L - 1:
+                    dy.pool_dy = self.pooled[m][l + 1]
+                    dy.pool_idx = self.idx[m][l + 1]
+                blk = self.encs[m][l]
+                if l > 0:
+                    blk.bwd(self.pooled[m][l], dy, self.pooled[m][l], accumulate)
+                else:
+                    blk.bwd(self.xin[m], dy, None, accumulate)
+
+        for m in range(M):                           # small levels: modality m on stream m
+            with self._on(streams, m):
+                levels(m, self.L, split)
+        for m in range(1, M):
+            if streams[m] is not streams[0]:
+                streams[0].wait_stream(streams[m])
+        for m in range(M):                           # big levels: one stream
+            levels(m, split, 0)
 
 
 def _ptr_array(ptrs):

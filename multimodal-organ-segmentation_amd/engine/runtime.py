@@ -65,7 +65,7 @@ class Runtime:
         self.dtype = dtype
         self.code = DTYPE_CODE[dtype]
         self.lib = lib()
-        self._ws = torch.empty(0, dtype=torch.float32, device=device)
+        self._ws: Dict[int, torch.Tensor] = {}      # one scratch arena per HIP stream
 
     # ---------------------------------------------------------------- alloc
     def act(self, N: int, D: int, H: int, W: int, C: int, ld: Optional[int] = None) -> Act:
@@ -74,11 +74,15 @@ class Runtime:
         return Act(buf, 0, C, ld, N, D, H, W)
 
     def ws(self, nfloats: int) -> torch.Tensor:
-        """Scratch fp32 workspace shared by consecutive ops on the stream."""
+        """Scratch fp32 workspace shared by consecutive ops on the CURRENT stream (each stream has its own,
+        so programs that run independent work on side streams never share scratch)."""
         nfloats = int(max(nfloats, 1))
-        if self._ws.numel() < nfloats:
-            self._ws = torch.empty(int(nfloats * 1.25) + 1024, dtype=torch.float32, device=self.device)
-        return self._ws
+        key = self.stream
+        cur = self._ws.get(key)
+        if cur is None or cur.numel() < nfloats:
+            cur = torch.empty(int(nfloats * 1.25) + 1024, dtype=torch.float32, device=self.device)
+            self._ws[key] = cur
+        return cur
 
     @property
     def stream(self) -> int:
