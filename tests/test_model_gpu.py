@@ -194,6 +194,25 @@ def test_step_bitwise_deterministic(dev):
     assert torch.equal(grads[0], grads[1])
 
 
+@pytest.mark.parametrize("tag", ["dual_tiny_cross_attention", "dual_tiny_m3_tversky"])
+def test_modality_streams_bitwise_equal(dev, tag, monkeypatch):
+    """The optional per-modality HIP streams (MMSEG_MODALITY_STREAMS=1) run the same kernels in the same
+    per-modality order: logits and every gradient must be bitwise those of the single-stream step."""
+    cfg, m, g, M, C = _build(tag)
+    xs, ys = _inputs(g, M, C)
+    crit = get_loss(cfg)
+    res = []
+    for streams in ("0", "1"):
+        monkeypatch.setenv("MMSEG_MODALITY_STREAMS", streams)
+        m.zero_grad(set_to_none=True)
+        out = m(xs[0].to(dev))
+        crit(out, ys[0].to(dev)).backward()
+        torch.cuda.synchronize()
+        res.append((out.detach().clone(), torch.cat([p.grad.reshape(-1).clone() for p in m.parameters()])))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+
+
 def test_accumulation_matches_two_batch_sum(dev):
     """accumulation_steps=2 must equal the average of the two micro-batch gradients."""
     cfg, m, g, M, C = _build("unet_tiny")
