@@ -47,6 +47,8 @@ int mmseg_abi_version(void);
  * mode 0/1: Conv3d W[Co][Ci][3][3][3] fwd / dgrad (flipped, transposed)
  * mode 2/3: 1x1 Conv3d W[Co][Ci] fwd / dgrad
  * mode 4/5: ConvTranspose3d W[Ci][Co][2][2][2] fwd / dgrad
+ * mode 6/7: the mode 1 / mode 5 data-gradient images over Cip >= Co zero-padded output channels (the
+ *           reduction of a layer whose Co is not 8 x a power of two, e.g. SwinUNETR's 48 / 96 / 384)
  * Replaces the weight reads of nn.Conv3d / nn.ConvTranspose3d (unet.py:26-27, 95, 163). */
 int mmseg_pack_weight(const float* w, void* dst, int mode, int Co, int Ci, int Cip, int KG, int KGp, int Cpad,
                       int dtype, void* stream);
@@ -209,6 +211,48 @@ int mmseg_softmax_bias_rows(const float* S, int lds, const float* bias, const fl
                             int ldp, long long rows, int N, int dtype, void* stream);
 int mmseg_relpos_table_grad(const void* dS, int ldn, int B, int heads, int N, float* dB, const int* offs,
                             const int* pairs, int T, float* gtable, int accumulate, int dtype, void* stream);
+
+/* ---------------------------------------------------- SwinUNETR tokens */
+/* The SwinTransformer stages and UNETR residual blocks of MONAI SwinUNETR (built by the reference's
+ * swin_unetr.py:80-96; MONAI absent -> parity unpinned, restated in oracle/swin_oracle.py).  Token
+ * tensors are channels-last rows [rows][ld].
+ * layernorm_fwd: nn.LayerNorm(C) / F.layer_norm (gamma = beta = NULL: no affine, proj_out); mean / rstd
+ *   per row (may be NULL).  layernorm_bwd: dx (+)= (add_dx) the input gradient; dgamma / dbeta (+)=
+ *   (accumulate) from per-block partials in ws (mmseg_layernorm_bwd_ws_floats() floats). */
+int mmseg_layernorm_fwd(const void* x, int ldx, void* y, int ldy, long long rows, int C, const float* gamma,
+                        const float* beta, float eps, float* mean, float* rstd, int dtype, void* stream);
+long long mmseg_layernorm_bwd_ws_floats(long long rows, int C);
+int mmseg_layernorm_bwd(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, long long rows, int C,
+                        const float* gamma, const float* mean, const float* rstd, int add_dx, float* dgamma,
+                        float* dbeta, int accumulate, float* ws, int dtype, void* stream);
+/* nn.GELU() (exact erf) of MLPBlock, and its backward dh = dy * gelu'(h); n % 8 == 0, contiguous. */
+int mmseg_gelu_fwd(const void* h, void* y, long long n, int dtype, void* stream);
+int mmseg_gelu_bwd(const void* h, const void* dy, void* dh, long long n, int dtype, void* stream);
+/* out = a + b (contiguous, n % 8 == 0): the MLP residual of SwinTransformerBlock. */
+int mmseg_add(const void* a, const void* b, void* out, long long n, int dtype, void* stream);
+/* F.pad to the padded grid (Dp, Hp, Wp) + torch.roll(-s) + window_partition -> dst [B*nW][w0*w1*w2][C].
+ * window_reverse: the inverse (window_reverse + roll(+s) + crop) onto the real grid, plus add_src
+ * (the block's shortcut; NULL: none).  Also the backward of each other. */
+int mmseg_window_partition(const void* src, int ldx, int B, int D, int H, int W, int C, int w0, int w1, int w2,
+                           int s0, int s1, int s2, int Dp, int Hp, int Wp, void* dst, int dtype, void* stream);
+int mmseg_window_reverse(const void* win, int B, int D, int H, int W, int C, int w0, int w1, int w2, int s0, int s1,
+                         int s2, int Dp, int Hp, int Wp, const void* add_src, int ld_add, void* dst, int ld_dst,
+                         int dtype, void* stream);
+/* Legacy PatchMerging sub-grid concat [B, ceil(D/2).., 8C] (odd sides zero padded) and its backward
+ * (sum over the slots that read each voxel; voxels no slot reads get 0). */
+int mmseg_merge_gather(const void* x, int ldx, int B, int D, int H, int W, int C, void* out, int dtype, void* stream);
+int mmseg_merge_scatter(const void* dout, int B, int D, int H, int W, int C, void* dx, int lddx, int dtype,
+                        void* stream);
+/* PatchEmbed Conv3d(k2, s2) operand: NCDHW fp32 [B][Cin][D][H][W] -> [B*(D/2)(H/2)(W/2)][Kp],
+ * column ci*8 + kz*4 + ky*2 + kx (the weight's own flattening), columns >= 8*Cin zero. */
+int mmseg_patchify(const float* x, int B, int Cin, int D, int H, int W, int Kp, void* out, int dtype, void* stream);
+/* UnetResBlock tail: y = lrelu((a - ma) * ra + R), R = (b - mb) * rb (b normalised), b (identity
+ * residual, mb = rb = NULL) or 0 (b = NULL); stats [N][C].  lrelu_bwd: g = dy * (y > 0 ? 1 : slope). */
+int mmseg_res_apply(const void* a, int lda, const float* ma, const float* ra, const void* b, int ldb, const float* mb,
+                    const float* rb, void* y, int ldy, int N, long long V, int C, float slope, int dtype,
+                    void* stream);
+int mmseg_lrelu_bwd(const void* y, int ldy, const void* dy, int lddy, void* g, int ldg, long long rows, int C,
+                    float slope, int dtype, void* stream);
 
 /* ------------------------------------------------ sliding-window inference */
 /* MONAI sliding_window_inference (constant blending) as called by Trainer._sliding_window_inference

@@ -729,14 +729,17 @@ __device__ __forceinline__ void buf_load_v8<float>(V8<float>& v, __amdgpu_buffer
   }
 }
 
-template <typename T, int BN, bool WU = false>
+// WDB: the weight stage is double-buffered in LDS (2 x 18 KB for BN32 bf16; 2 blocks/CU still fit), so a
+// stage that only swaps weights needs one barrier (after its stores) instead of two; a stage that also
+// replaces the halo keeps the barrier before its stores.
+template <typename T, int BN, bool WU = false, bool WDB = false>
 __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kernel(GemmArgs g, int upb) {
   using L = Brick2Layout<T>;
   constexpr int BZ = 4, HZ = BZ + 2;
   constexpr int RM = 4, RN = BN / 16;
   constexpr int XQ = HZ * L::RZ;
   constexpr int WQ = 9 * BN * L::QV;
-  __shared__ __attribute__((aligned(16))) float4 lds4[XQ + WQ];
+  __shared__ __attribute__((aligned(16))) float4 lds4[XQ + (WDB ? 2 : 1) * WQ];
   T* Xl = reinterpret_cast<T*>(lds4);
   T* Wl = reinterpret_cast<T*>(lds4 + XQ);
   constexpr int EPQ = 16 / sizeof(T);
@@ -832,14 +835,15 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kern
       }
     }
   };
-  auto store_w = [&]() {
+  auto store_w = [&](int wbuf) {
+    T* Wd = Wl + wbuf * WQ * EPQ;
 #pragma unroll
     for (int k = 0; k < W_PER; ++k) {
       const int e0 = tid + k * 256;
       if (WU || e0 < W_ITEMS) {
         const int e = WU ? min(e0, W_ITEMS - 1) : e0;
         const int cgw = e & 3, q = e >> 2;
-        wr[k].store(Wl + (q * L::QV + (cgw ^ w2_swz(q)) * L::QG) * EPQ);
+        wr[k].store(Wd + (q * L::QV + (cgw ^ w2_swz(q)) * L::QG) * EPQ);
       }
     }
   };
@@ -864,8 +868,9 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kern
   load_x(0);
   load_w(cur.n0, 0, 0);
   store_x();
-  store_w();
+  store_w(0);
   __syncthreads();
+  int wb = 0;    // weight buffer of the current stage (WDB)
   for (int u = u_begin; u < u_end; ++u) {
     f32x4 acc[RM][RN];
 #pragma unroll
@@ -893,7 +898,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kern
         const int hoff = kz * L::RZ + ky * L::RY + kx * L::QV;
         V8<T> af[RM], bf[RN];
 #pragma unroll
-        for (int j = 0; j < RN; ++j) bf[j].load(Wl + (t9 * BN * L::QV + bq[j]) * EPQ);
+        for (int j = 0; j < RN; ++j) bf[j].load(Wl + (wb * WQ + t9 * BN * L::QV + bq[j]) * EPQ);
 #pragma unroll
         for (int i = 0; i < RM; ++i) af[i].load(Xl + (aq[i] + hoff) * EPQ);
 #pragma unroll
@@ -901,11 +906,25 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kern
 #pragma unroll
           for (int j = 0; j < RN; ++j) mfma_step<T>(acc[i][j], bf[j], af[i]);   // transposed: rows = channels
       }
-      __syncthreads();
-      if (more) {
-        store_w();
-        if (kzn == 0) store_x();
+      if constexpr (WDB) {
+        // the other weight buffer was last read in the previous stage, which every wave finished before
+        // that stage's closing barrier; only a halo swap must wait for this stage's readers
+        if (more) {
+          if (kzn == 0) {
+            __syncthreads();
+            store_x();
+          }
+          store_w(wb ^ 1);
+          __syncthreads();
+        }
+        wb ^= 1;
+      } else {
         __syncthreads();
+        if (more) {
+          store_w(0);
+          if (kzn == 0) store_x();
+          __syncthreads();
+        }
       }
     }
     // epilogue: lane holds channels n0 + j*16 + 4*kg + (0..3) of voxel r16 of row tile i
@@ -2333,6 +2352,14 @@ __global__ void pack_weight_kernel(PackArgs g, int mode) {
         const int cpg = g.Co >> 3, t = kgi / cpg, co = (kgi % cpg) * 8 + j, ci = col;
         if (ci < g.Ci) v = g.w[((long long)ci * g.Co + co) * 8 + t];
       } break;
+      case 6: {   // CONV3_DGRAD over Cop = Cip padded output channels (zero rows co >= Co)
+        const int cpg = g.Cip >> 3, t = kgi / cpg, co = (kgi % cpg) * 8 + j, ci = col;
+        if (ci < g.Ci && co < g.Co) v = g.w[((long long)co * g.Ci + ci) * 27 + (26 - t)];
+      } break;
+      case 7: {   // CONVT_DGRAD over Cop = Cip padded output channels
+        const int cpg = g.Cip >> 3, t = kgi / cpg, co = (kgi % cpg) * 8 + j, ci = col;
+        if (ci < g.Ci && co < g.Co) v = g.w[((long long)ci * g.Co + co) * 8 + t];
+      } break;
     }
   }
   reinterpret_cast<T*>(g.dst)[idx] = from_f<T>(v);
@@ -2519,6 +2546,9 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
       mmseg::note_kernel("conv3_brick3_kernel<BN32>");
       if (knob("MMSEG_BRICK3_WU", 0))
         hipLaunchKernelGGL((conv3_brick3_kernel<T, 32, true>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
+      else if (knob("MMSEG_BRICK3_WDB", 1))
+        hipLaunchKernelGGL((conv3_brick3_kernel<T, 32, false, true>), dim3(ceil_div(units, upb)), block, 0, s, g,
+                           upb);
       else
         hipLaunchKernelGGL((conv3_brick3_kernel<T, 32, false>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
     } else if (g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {

@@ -321,59 +321,48 @@ class WindowAttentionEngine:
         self._tr(x, 0, 0, ch_in, code, t2, 0, 0, ldm, code, 1, 1, M, ch_in)
         self._gemm(t1, (0, 0), ldm, t2, (0, 0), ldm, gw, (0, 0), ch_in, 1, 1, ch_out, ch_in, M, acc=acc, c_f32=True)
 
-    def forward(self, x: torch.Tensor, mask, p, index: torch.Tensor):
-        """x [B, N, C] fp32; mask [nw, N, N] fp32 or None; p: qkv_w [3C][C], qkv_b [3C] | None, proj_w [C][C],
-        proj_b [C], table [T][heads]; index int32 [N*N] (device)."""
-        B, N, C = x.shape
-        h, hd, M = self.h, self.hd, B * N
+    def core_fwd(self, qkv: torch.Tensor, B: int, N: int, mask, table: torch.Tensor, index: torch.Tensor):
+        """Attention core on a qkv buffer [B*N][3C] (storage dtype): softmax(scale q k^T + bias (+ mask)) v
+        -> (O [B*N][C], P [B][h][N][ldn]).  table [T][heads] fp32, index int32 [N*N] (device)."""
+        C, h, hd = self.C, self.h, self.hd
+        M = B * N
         ldn = (N + 7) // 8 * 8
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
-        xf = self._cast(x)
-        qkv = self._empty(M * 3 * C)
-        self._gemm(xf, (0, 0), C, self._cast(p["qkv_w"]), (0, 0), C, qkv, (0, 0), 3 * C, 1, 1, M, 3 * C, C,
-                   bias=p.get("qkv_b"))
         qs = (N * 3 * C, hd)                        # head-slice strides inside qkv
         ss = (h * N * ldn, N * ldn)                 # [B][h][N][ldn] score-shaped buffers
         S = self._empty(B * h * N * ldn, f32=True)
         self._gemm(qkv, qs, 3 * C, qkv[C:], qs, 3 * C, S, ss, ldn, B * h, h, N, N, hd, alpha=self.scale, c_f32=True)
         bias = self._empty(h * N * N, f32=True)
-        L.mmseg_relpos_bias(ptr(p["table"]), ptr(index), h, N, ptr(bias), s)
+        L.mmseg_relpos_bias(ptr(table), ptr(index), h, N, ptr(bias), s)
         P = self._empty(B * h * N * ldn)
         nw = mask.shape[0] if mask is not None else 0
         L.mmseg_softmax_bias_rows(ptr(S), ldn, ptr(bias), ptr(mask), nw, h, ptr(P), ldn, B * h * N, N, code, s)
+        del S
         ts = (h * hd * ldn, hd * ldn)               # [B][h][hd][ldn] per-head transposed operands
         Vt = self._empty(B * h * hd * ldn, zero=True)
         self._tr(qkv[2 * C:], qs[0], qs[1], 3 * C, code, Vt, ts[0], ts[1], ldn, code, B * h, h, N, hd)
         O = self._empty(M * C)
         hs = (N * C, hd)
         self._gemm(P, ss, ldn, Vt, ts, ldn, O, hs, C, B * h, h, N, hd, N)
-        y = self._empty(M * C)
-        self._gemm(O, (0, 0), C, self._cast(p["proj_w"]), (0, 0), C, y, (0, 0), C, 1, 1, M, C, C, bias=p["proj_b"])
-        return self._to_f32(y, (B, N, C)), {"shape": (B, N), "xf": xf, "qkv": qkv, "P": P, "O": O}
+        return O, P
 
-    def backward(self, dy: torch.Tensor, st, p, grads, csr, accumulate: bool = False):
-        B, N = st["shape"]
+    def core_bwd(self, dO: torch.Tensor, qkv: torch.Tensor, P: torch.Tensor, B: int, N: int, gtable: torch.Tensor,
+                 csr, accumulate: bool) -> torch.Tensor:
+        """Backward of core_fwd: dqkv [B*N][3C] (storage dtype); the bias-table gradient (+)= into gtable."""
         C, h, hd = self.C, self.h, self.hd
         M = B * N
         ldn = (N + 7) // 8 * 8
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
-        qkv, P, O = st["qkv"], st["P"], st["O"]
-        dyf = self._cast(dy)
-        # proj
-        self._wgrad(dyf, C, O, C, M, grads["proj_w"], accumulate)
-        self._colsum(dyf, C, M, grads["proj_b"], accumulate)
-        dO = self._empty(M * C)
-        self._gemm(dyf, (0, 0), C, self._castT(p["proj_w"]), (0, 0), C, dO, (0, 0), C, 1, 1, M, C, C)
-        # attention core
         qs, ss, hs = (N * 3 * C, hd), (h * N * ldn, N * ldn), (N * C, hd)
         ts = (h * hd * ldn, hd * ldn)
         dP = self._empty(B * h * N * ldn, f32=True)
         self._gemm(dO, hs, C, qkv[2 * C:], qs, 3 * C, dP, ss, ldn, B * h, h, N, N, hd, c_f32=True)
         dS = self._empty(B * h * N * ldn)
         L.mmseg_softmax_bwd_rows(ptr(P), ldn, ptr(dP), ldn, ptr(dS), ldn, B * h * N, N, code, s)
+        del dP
         dB = self._empty(h * N * N, f32=True)
         offs, pairs, T = csr
-        L.mmseg_relpos_table_grad(ptr(dS), ldn, B, h, N, ptr(dB), ptr(offs), ptr(pairs), T, ptr(grads["table"]),
+        L.mmseg_relpos_table_grad(ptr(dS), ldn, B, h, N, ptr(dB), ptr(offs), ptr(pairs), T, ptr(gtable),
                                   int(accumulate), code, s)
         dqkv = self._empty(M * 3 * C)
         XT = self._empty(B * h * N * ldn, zero=True)
@@ -389,6 +378,34 @@ class WindowAttentionEngine:
         self._tr(P, ss[0], ss[1], ldn, code, XT, ss[0], ss[1], ldn, code, B * h, h, N, N)
         self._tr(dO, hs[0], hs[1], C, code, HT, ts[0], ts[1], ldn, code, B * h, h, N, hd)
         self._gemm(XT, ss, ldn, HT, ts, ldn, dqkv[2 * C:], qs, 3 * C, B * h, h, N, hd, N)
+        return dqkv
+
+    def forward(self, x: torch.Tensor, mask, p, index: torch.Tensor):
+        """x [B, N, C] fp32; mask [nw, N, N] fp32 or None; p: qkv_w [3C][C], qkv_b [3C] | None, proj_w [C][C],
+        proj_b [C], table [T][heads]; index int32 [N*N] (device)."""
+        B, N, C = x.shape
+        M = B * N
+        xf = self._cast(x)
+        qkv = self._empty(M * 3 * C)
+        self._gemm(xf, (0, 0), C, self._cast(p["qkv_w"]), (0, 0), C, qkv, (0, 0), 3 * C, 1, 1, M, 3 * C, C,
+                   bias=p.get("qkv_b"))
+        O, P = self.core_fwd(qkv, B, N, mask, p["table"], index)
+        y = self._empty(M * C)
+        self._gemm(O, (0, 0), C, self._cast(p["proj_w"]), (0, 0), C, y, (0, 0), C, 1, 1, M, C, C, bias=p["proj_b"])
+        return self._to_f32(y, (B, N, C)), {"shape": (B, N), "xf": xf, "qkv": qkv, "P": P, "O": O}
+
+    def backward(self, dy: torch.Tensor, st, p, grads, csr, accumulate: bool = False):
+        B, N = st["shape"]
+        C = self.C
+        M = B * N
+        qkv, P, O = st["qkv"], st["P"], st["O"]
+        dyf = self._cast(dy)
+        # proj
+        self._wgrad(dyf, C, O, C, M, grads["proj_w"], accumulate)
+        self._colsum(dyf, C, M, grads["proj_b"], accumulate)
+        dO = self._empty(M * C)
+        self._gemm(dyf, (0, 0), C, self._castT(p["proj_w"]), (0, 0), C, dO, (0, 0), C, 1, 1, M, C, C)
+        dqkv = self.core_bwd(dO, qkv, P, B, N, grads["table"], csr, accumulate)
         # qkv linear
         self._wgrad(dqkv, 3 * C, st["xf"], C, M, grads["qkv_w"], accumulate)
         if "qkv_b" in grads:

@@ -37,7 +37,11 @@ class SegEngine:
                 or self.flat is None or not self.flat.intact()):
             self.rt = Runtime(device, self.dtype)
             self.flat = FlatParams(params)
-            cls = UNetProgram if self.kind == "unet" else DualEncoderProgram
+            if self.kind == "swin_unetr":
+                from .swin import SwinUNETRProgram
+                cls = SwinUNETRProgram
+            else:
+                cls = UNetProgram if self.kind == "unet" else DualEncoderProgram
             self.program = cls(self.rt, self.module, self.flat)
         return self
 

@@ -114,11 +114,15 @@ class DySpec:
 
 class Conv3:
     def __init__(self, rt: Runtime, conv: nn.Conv3d, flat: FlatParams, cin_pad: Optional[int] = None,
-                 need_dgrad: bool = True):
+                 need_dgrad: bool = True, cout_pad: Optional[int] = None):
+        """cin_pad: the input tensor's channel count seen by the GEMM (8 x a power of two >= Ci; the extra
+        channels meet zero weights).  cout_pad: the same for the data-gradient reduction over Co (its dy
+        tensor must hold cout_pad readable channels; pack mode 6 zeroes their weights)."""
         self.rt, self.conv, self.flat = rt, conv, flat
         self.Co, self.Ci = conv.weight.shape[:2]
         self.Cip = cin_pad or self.Ci
-        if self.Co % 8 or self.Cip % 8:
+        self.Cop = cout_pad or self.Co
+        if self.Co % 8 or self.Cip % 8 or self.Cop % 8 or self.Cop < self.Co:
             raise ValueError("conv channels must be multiples of 8")
         self.cpg_shift = pow2_shift(self.Cip // 8)
         self.KG = 27 * self.Cip // 8
@@ -128,8 +132,8 @@ class Conv3:
         self.wf = torch.zeros(self.KGp * self.Cpad * 8, dtype=rt.dtype, device=rt.device)
         self.need_dgrad = need_dgrad
         if need_dgrad:
-            self.dshift = pow2_shift(self.Co // 8)
-            self.KGd = 27 * self.Co // 8
+            self.dshift = pow2_shift(self.Cop // 8)
+            self.KGd = 27 * self.Cop // 8
             self.KGdp = round_up(self.KGd, 4)
             self.Cpad_d = _col_tile(self.Cip)
             self.wd = torch.zeros(self.KGdp * self.Cpad_d * 8, dtype=rt.dtype, device=rt.device)
@@ -138,7 +142,10 @@ class Conv3:
         w = self.conv.weight
         d = [(ptr(w), ptr(self.wf), 0, self.Co, self.Ci, self.Cip, self.KG, self.KGp, self.Cpad)]
         if self.need_dgrad:
-            d.append((ptr(w), ptr(self.wd), 1, self.Co, self.Ci, self.Cip, self.KGd, self.KGdp, self.Cpad_d))
+            if self.Cop != self.Co:
+                d.append((ptr(w), ptr(self.wd), 6, self.Co, self.Ci, self.Cop, self.KGd, self.KGdp, self.Cpad_d))
+            else:
+                d.append((ptr(w), ptr(self.wd), 1, self.Co, self.Ci, self.Cip, self.KGd, self.KGdp, self.Cpad_d))
         return d
 
     def pack(self):
@@ -204,9 +211,10 @@ class Conv3:
         with TIMER.region(_gemm_name(self.rt, 0, "conv3"), flops=2.0 * V * self.Co * 27 * self.Ci,
                           nbytes=_io_bytes(self.rt, V, self.Cip, self.Co, 27 * self.Cip * self.Co, 4)):
             L.mmseg_conv3_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, ptr(self.flat.grad(self.conv.weight)),
-                                ptr(self.flat.grad(self.conv.bias)), self.Co, self.Cip, self.Ci, self.cpg_shift, V,
-                                x.D, x.H, x.W, ptr(ws), wsf, int(accumulate), code, s)
-        self.flat.mark(self.conv.weight, self.conv.bias)
+                                ptr(self.flat.grad(self.conv.bias)) if self.conv.bias is not None else None, self.Co,
+                                self.Cip, self.Ci, self.cpg_shift, V, x.D, x.H, x.W, ptr(ws), wsf, int(accumulate),
+                                code, s)
+        self.flat.mark(*[p for p in (self.conv.weight, self.conv.bias) if p is not None])
         if dx is not None:
             M = V
             ks = L.mmseg_conv3_splits(M, self.Ci, self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, dy.ld, dx.ld, code)
@@ -218,25 +226,31 @@ class Conv3:
 
 
 class ConvT2:
-    def __init__(self, rt: Runtime, up: nn.ConvTranspose3d, flat: FlatParams):
+    def __init__(self, rt: Runtime, up: nn.ConvTranspose3d, flat: FlatParams, cout_pad: Optional[int] = None):
+        """cout_pad: channels of dy read by the data-gradient / weight-gradient gathers (8 x a power of two
+        >= Co; pack mode 7 zeroes their weights, the reduce drops their weight-gradient columns)."""
         self.rt, self.up, self.flat = rt, up, flat
         self.Ci, self.Co = up.weight.shape[:2]
-        if self.Ci % 8 or self.Co % 8:
+        self.Cop = cout_pad or self.Co
+        if self.Ci % 8 or self.Co % 8 or self.Cop % 8 or self.Cop < self.Co:
             raise ValueError("transposed-conv channels must be multiples of 8")
         self.KG = self.Ci // 8
         self.KGp = round_up(self.KG, 4)
         self.Cpad = _col_tile(8 * self.Co)
         self.wf = torch.empty(self.KGp * self.Cpad * 8, dtype=rt.dtype, device=rt.device)
-        self.dshift = pow2_shift(self.Co // 8)
-        self.KGd = self.Co  # 8 taps x Co/8 groups
+        self.dshift = pow2_shift(self.Cop // 8)
+        self.KGd = self.Cop  # 8 taps x Cop/8 groups
         self.KGdp = round_up(self.KGd, 4)
         self.Cpad_d = _col_tile(self.Ci)
         self.wd = torch.empty(self.KGdp * self.Cpad_d * 8, dtype=rt.dtype, device=rt.device)
 
     def descs(self):
         w = self.up.weight
-        return [(ptr(w), ptr(self.wf), 4, self.Co, self.Ci, self.Ci, self.KG, self.KGp, self.Cpad),
-                (ptr(w), ptr(self.wd), 5, self.Co, self.Ci, self.Ci, self.KGd, self.KGdp, self.Cpad_d)]
+        if self.Cop != self.Co:
+            dd = (ptr(w), ptr(self.wd), 7, self.Co, self.Ci, self.Cop, self.KGd, self.KGdp, self.Cpad_d)
+        else:
+            dd = (ptr(w), ptr(self.wd), 5, self.Co, self.Ci, self.Ci, self.KGd, self.KGdp, self.Cpad_d)
+        return [(ptr(w), ptr(self.wf), 4, self.Co, self.Ci, self.Ci, self.KG, self.KGp, self.Cpad), dd]
 
     def pack(self):
         for d in self.descs():
@@ -255,18 +269,19 @@ class ConvT2:
         """x: input grid (D,H,W); dy: output grid (2D,2H,2W)."""
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
         V = x.N * x.V
-        ncols = 8 * self.Co
+        ncols = 8 * self.Cop
         ks = L.mmseg_wgrad_splits(V, _wgrad_ksplit(self.Ci, ncols, V))
         part = self.rt.ws(max(ks * self.Ci * ncols, 256 * self.Co))
         with TIMER.region(_gemm_name(self.rt, 0, "convT"), flops=2.0 * V * self.Ci * 8 * self.Co,
                           nbytes=_io_bytes(self.rt, V, self.Ci, 8 * self.Co, 8 * self.Ci * self.Co, 4)):
             L.mmseg_wgrad(x.ptr, x.ld, dy.ptr, dy.ld, ptr(part), None, MODE_CONVT_DGRAD, self.Ci, ncols, self.dshift,
                           V, x.D, x.H, x.W, ks, code, s)
-        L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.up.weight)), None, None, self.Ci, ncols, ks, self.Co,
+        L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.up.weight)), None, None, self.Ci, ncols, ks, self.Cop,
                              self.Co, 8, int(accumulate), s)
-        L.mmseg_colsum(dy.ptr, dy.ld, self.Co, dy.N * dy.V, ptr(part), 256, ptr(self.flat.grad(self.up.bias)),
-                       int(accumulate), code, s)
-        self.flat.mark(self.up.weight, self.up.bias)
+        if self.up.bias is not None:
+            L.mmseg_colsum(dy.ptr, dy.ld, self.Co, dy.N * dy.V, ptr(part), 256, ptr(self.flat.grad(self.up.bias)),
+                           int(accumulate), code, s)
+        self.flat.mark(*[p for p in (self.up.weight, self.up.bias) if p is not None])
         if dx is not None:
             ks = _gemm_ksplit(V, self.Ci, self.KGd)
             ws = self.rt.ws(ks * V * self.Ci) if ks > 1 else None
