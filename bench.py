@@ -33,12 +33,15 @@ PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
 
 
-def make_config(model, batch, dtype, out_channels=6, modalities=("CT", "PET")):
+def make_config(model, batch, dtype, out_channels=6, modalities=("CT", "PET"), size=96):
+    backbone = {"features": [32, 64, 128, 256, 512], "norm": "instance"}
+    if model == "swin_unetr":     # config c4: SwinUNETR feature_size 48 (swin_unetr.py:180-200 defaults otherwise)
+        backbone = {"img_size": [size] * 3, "feature_size": 48}
     return {
         "experiment": {"name": "bench", "output_dir": "/tmp/mmseg_bench", "seed": 42},
         "data": {"modalities": list(modalities)},
         "model": {"name": model, "in_channels": len(modalities), "out_channels": out_channels,
-                  "backbone": {"features": [32, 64, 128, 256, 512], "norm": "instance"},
+                  "backbone": backbone,
                   "fusion": {"type": "cross_attention"}, "head": {"dropout": 0.0}},
         "training": {"epochs": 1, "batch_size": batch, "accumulation_steps": 1,
                      "optimizer": {"name": "adamw", "lr": 1e-4, "weight_decay": 1e-5, "betas": [0.9, 0.999]},
@@ -98,7 +101,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--model", default="dual_encoder", choices=["dual_encoder", "unet"])
+    ap.add_argument("--model", default="dual_encoder", choices=["dual_encoder", "unet", "swin_unetr"],
+                    help="swin_unetr = config c4 (use --size 128 --batch 1)")
     ap.add_argument("--batch", type=int, default=2, help="per-GPU batch")
     ap.add_argument("--size", type=int, default=96)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
@@ -120,7 +124,7 @@ def main():
     rank, world = ddp.rank(), ddp.world()
     n_gpus = world
 
-    cfg = make_config(args.model, args.batch, args.dtype)
+    cfg = make_config(args.model, args.batch, args.dtype, size=args.size)
     torch.manual_seed(42)
     model = build_model(cfg)
     trainer = Trainer(cfg, model)
@@ -189,12 +193,14 @@ def main():
                     "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1) if v["ms"] > 0 else None}
                 for k, v in sorted(fam.items(), key=lambda kv: -kv[1]["ms"])}
     cpu = None
-    if n_gpus == 1 and not args.no_cpu_baseline:
+    if n_gpus == 1 and not args.no_cpu_baseline and args.model != "swin_unetr":
         cpu = cpu_baseline(args.model, args.batch, args.size, 6, ["CT", "PET"], args.cpu_threads)
-    workload = ("DualEncoder fusion=cross_attention (mean, dual_encoder.py:193-195) CT+PET"
-                if args.model == "dual_encoder" else "UNet3D early_fusion 2-ch")
+    workload = {"dual_encoder": "DualEncoder fusion=cross_attention (mean, dual_encoder.py:193-195) CT+PET",
+                "unet": "UNet3D early_fusion 2-ch",
+                "swin_unetr": "SwinUNETR feature_size 48 (MONAI architecture; parity vs MONAI unpinned) CT+PET"}[
+        args.model]
     out = {
-        "metric": "96^3 2-modality patches/sec/node (train step)",
+        "metric": f"{args.size}^3 2-modality patches/sec/node (train step)",
         "value": round(value, 3), "unit": "patches/s", "n_gpus": n_gpus, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (seeded CT/PET phantoms, pre-staged in HBM)",

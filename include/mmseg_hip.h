@@ -56,7 +56,8 @@ int mmseg_pack_weight(const float* w, void* dst, int mode, int Co, int Ci, int C
 /* Batched form: one launch packs every layer of a model from a device table of
  * descriptors {w, dst, mode, Co, Ci, Cip, KG, KGp, Cpad, pad, begin} (mmseg_pack_desc_bytes() each). */
 /* Batched pack of every 3^3 conv of a model, both images (forward + data-gradient) from one read.
- * descs: device array of n records {w, wf, wd|NULL, Co, Ci, Cip, Cpad, Cpad_d, block_begin, pad, pad}
+ * descs: device array of n records {w, wf, wd|NULL, Co, Ci, Cip, Cpad, Cpad_d, block_begin, Cop, pad}
+ * (Cop: the data-gradient image's padded output-channel count, pack mode 6; 0 = Co)
  * (mmseg_pack3_desc_bytes() each), layer l owning blocks [block_begin, +Co/8*ceil(Ci/32)).
  * The images must be zero-initialised once (padding entries are never written). */
 int mmseg_pack3_desc_bytes(void);

@@ -2308,12 +2308,54 @@ __global__ void colsum_reduce_kernel(const float* __restrict__ part, int nblk, i
 //   3 POINT_DGRAD: kgi = c8, col = ci, co = c8*8+j
 //   4 CONVT_FWD  : W[Ci][Co][8]; kgi = c8 (ci), col = tap*Co + co
 //   5 CONVT_DGRAD: kgi = tap*(Co/8)+c8, col = ci, co = c8*8+j
+//   6 / 7        : modes 1 / 5 with Cip = the padded output-channel count (rows co >= Co zero)
 struct PackArgs {
   const float* w;
   void* dst;
   int Co, Ci, Cip;  // Cip: padded input channels (multiple of 8) for CONV3_FWD
   int KG, KGp, Cpad;
 };
+
+// Value of packed element (kgi, col, j) of a mode-`mode` image (0 outside the weight).
+__device__ __forceinline__ float pack_value(const float* __restrict__ w, int mode, int Co, int Ci, int Cip, int kgi,
+                                            int col, int j) {
+  switch (mode) {
+    case 0: {
+      const int cpg = Cip >> 3, t = kgi / cpg, ci = (kgi % cpg) * 8 + j, co = col;
+      if (co < Co && ci < Ci) return w[((long long)co * Ci + ci) * 27 + t];
+    } break;
+    case 1: {
+      const int cpg = Co >> 3, t = kgi / cpg, co = (kgi % cpg) * 8 + j, ci = col;
+      if (ci < Ci) return w[((long long)co * Ci + ci) * 27 + (26 - t)];
+    } break;
+    case 2: {
+      const int ci = kgi * 8 + j, co = col;
+      if (co < Co && ci < Ci) return w[(long long)co * Ci + ci];
+    } break;
+    case 3: {
+      const int co = kgi * 8 + j, ci = col;
+      if (ci < Ci && co < Co) return w[(long long)co * Ci + ci];
+    } break;
+    case 4: {
+      const int ci = kgi * 8 + j;
+      const int t = col / Co, co = col % Co;
+      if (t < 8 && ci < Ci) return w[((long long)ci * Co + co) * 8 + t];
+    } break;
+    case 5: {
+      const int cpg = Co >> 3, t = kgi / cpg, co = (kgi % cpg) * 8 + j, ci = col;
+      if (ci < Ci) return w[((long long)ci * Co + co) * 8 + t];
+    } break;
+    case 6: {   // CONV3_DGRAD over Cop = Cip padded output channels (zero rows co >= Co)
+      const int cpg = Cip >> 3, t = kgi / cpg, co = (kgi % cpg) * 8 + j, ci = col;
+      if (ci < Ci && co < Co) return w[((long long)co * Ci + ci) * 27 + (26 - t)];
+    } break;
+    case 7: {   // CONVT_DGRAD over Cop = Cip padded output channels
+      const int cpg = Cip >> 3, t = kgi / cpg, co = (kgi % cpg) * 8 + j, ci = col;
+      if (ci < Ci && co < Co) return w[((long long)ci * Co + co) * 8 + t];
+    } break;
+  }
+  return 0.f;
+}
 
 template <typename T>
 __global__ void pack_weight_kernel(PackArgs g, int mode) {
@@ -2324,44 +2366,7 @@ __global__ void pack_weight_kernel(PackArgs g, int mode) {
   const long long q = idx >> 3;
   const int col = (int)(q % g.Cpad);
   const int kgi = (int)(q / g.Cpad);
-  float v = 0.f;
-  if (kgi < g.KG) {
-    switch (mode) {
-      case 0: {
-        const int cpg = g.Cip >> 3, t = kgi / cpg, ci = (kgi % cpg) * 8 + j, co = col;
-        if (co < g.Co && ci < g.Ci) v = g.w[((long long)co * g.Ci + ci) * 27 + t];
-      } break;
-      case 1: {
-        const int cpg = g.Co >> 3, t = kgi / cpg, co = (kgi % cpg) * 8 + j, ci = col;
-        if (ci < g.Ci) v = g.w[((long long)co * g.Ci + ci) * 27 + (26 - t)];
-      } break;
-      case 2: {
-        const int ci = kgi * 8 + j, co = col;
-        if (co < g.Co && ci < g.Ci) v = g.w[(long long)co * g.Ci + ci];
-      } break;
-      case 3: {
-        const int co = kgi * 8 + j, ci = col;
-        if (ci < g.Ci && co < g.Co) v = g.w[(long long)co * g.Ci + ci];
-      } break;
-      case 4: {
-        const int ci = kgi * 8 + j;
-        const int t = col / g.Co, co = col % g.Co;
-        if (t < 8 && ci < g.Ci) v = g.w[((long long)ci * g.Co + co) * 8 + t];
-      } break;
-      case 5: {
-        const int cpg = g.Co >> 3, t = kgi / cpg, co = (kgi % cpg) * 8 + j, ci = col;
-        if (ci < g.Ci) v = g.w[((long long)ci * g.Co + co) * 8 + t];
-      } break;
-      case 6: {   // CONV3_DGRAD over Cop = Cip padded output channels (zero rows co >= Co)
-        const int cpg = g.Cip >> 3, t = kgi / cpg, co = (kgi % cpg) * 8 + j, ci = col;
-        if (ci < g.Ci && co < g.Co) v = g.w[((long long)co * g.Ci + ci) * 27 + (26 - t)];
-      } break;
-      case 7: {   // CONVT_DGRAD over Cop = Cip padded output channels
-        const int cpg = g.Cip >> 3, t = kgi / cpg, co = (kgi % cpg) * 8 + j, ci = col;
-        if (ci < g.Ci && co < g.Co) v = g.w[((long long)ci * g.Co + co) * 8 + t];
-      } break;
-    }
-  }
+  const float v = kgi < g.KG ? pack_value(g.w, mode, g.Co, g.Ci, g.Cip, kgi, col, j) : 0.f;
   reinterpret_cast<T*>(g.dst)[idx] = from_f<T>(v);
 }
 
@@ -2379,7 +2384,8 @@ struct Pack3Desc {
   void* wd;             // data-gradient image or null
   int Co, Ci, Cip, Cpad, Cpad_d;
   int block_begin;      // first block of this layer in the launch
-  int pad0, pad1;
+  int Cop;              // data-gradient reduction channels (pack mode 6: padded Co; 0 = Co)
+  int pad1;
 };
 
 template <typename T>
@@ -2418,8 +2424,9 @@ __global__ __launch_bounds__(256) void pack_conv3_batched_kernel(const Pack3Desc
     v.store(wf + (kgi * d.Cpad + co0 + co) * 8);
   }
   if (d.wd == nullptr) return;
-  // data-gradient image: tap s -> kgi = (26 - s) * Co/8 + co0/8, column ci, 8 co per vector
-  const int cpgd = d.Co >> 3;
+  // data-gradient image: tap s -> kgi = (26 - s) * Cop/8 + co0/8, column ci, 8 co per vector (rows co >= Co of a
+  // padded image are zero from allocation)
+  const int cpgd = (d.Cop > 0 ? d.Cop : d.Co) >> 3;
   T* wd = reinterpret_cast<T*>(d.wd);
   for (int e = tid; e < 27 * 32; e += 256) {
     const int ci = e & 31, t = e >> 5;
@@ -2456,36 +2463,7 @@ __global__ void pack_weight_batched_kernel(const PackDesc* __restrict__ descs, i
     const long long q = li >> 3;
     const int col = (int)(q % d.Cpad);
     const int kgi = (int)(q / d.Cpad);
-    float v = 0.f;
-    if (kgi < d.KG) {
-      switch (d.mode) {
-        case 0: {
-          const int cpg = d.Cip >> 3, t = kgi / cpg, ci = (kgi % cpg) * 8 + j, co = col;
-          if (co < d.Co && ci < d.Ci) v = d.w[((long long)co * d.Ci + ci) * 27 + t];
-        } break;
-        case 1: {
-          const int cpg = d.Co >> 3, t = kgi / cpg, co = (kgi % cpg) * 8 + j, ci = col;
-          if (ci < d.Ci) v = d.w[((long long)co * d.Ci + ci) * 27 + (26 - t)];
-        } break;
-        case 2: {
-          const int ci = kgi * 8 + j, co = col;
-          if (co < d.Co && ci < d.Ci) v = d.w[(long long)co * d.Ci + ci];
-        } break;
-        case 3: {
-          const int co = kgi * 8 + j, ci = col;
-          if (ci < d.Ci && co < d.Co) v = d.w[(long long)co * d.Ci + ci];
-        } break;
-        case 4: {
-          const int ci = kgi * 8 + j;
-          const int t = col / d.Co, co = col % d.Co;
-          if (t < 8 && ci < d.Ci) v = d.w[((long long)ci * d.Co + co) * 8 + t];
-        } break;
-        case 5: {
-          const int cpg = d.Co >> 3, t = kgi / cpg, co = (kgi % cpg) * 8 + j, ci = col;
-          if (ci < d.Ci) v = d.w[((long long)ci * d.Co + co) * 8 + t];
-        } break;
-      }
-    }
+    const float v = kgi < d.KG ? pack_value(d.w, d.mode, d.Co, d.Ci, d.Cip, kgi, col, j) : 0.f;
     reinterpret_cast<T*>(d.dst)[li] = from_f<T>(v);
   }
 }

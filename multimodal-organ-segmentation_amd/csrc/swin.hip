@@ -153,16 +153,39 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const T* __restrict_
   }
 }
 
-// out[c] (+)= sum_b part[b][k][C] over b (fixed order), k = 0 (dgamma) / 1 (dbeta)
-__global__ void ln_param_reduce_kernel(const float* __restrict__ part, int nb, int C, float* __restrict__ dgamma,
-                                       float* __restrict__ dbeta, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 2 * C) return;
-  const int k = c / C, cc = c - k * C;
+// out[c] (+)= sum_b part[b][k][C] over b, k = 0 (dgamma) / 1 (dbeta).  Block = 64 columns x 16 waves: wave w
+// sums partial rows w, w+16, ... (8 loads in flight), then the 16 wave sums are added in wave order (fixed).
+constexpr int LNR_WAVES = 16;
+__global__ __launch_bounds__(1024) void ln_param_reduce_kernel(const float* __restrict__ part, int nb, int C,
+                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                               int accumulate) {
+  __shared__ float red[LNR_WAVES][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;           // column of [2][C]
+  const bool ok = c < 2 * C;
+  const int k = ok ? c / C : 0, cc = ok ? c - k * C : 0;
   float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += part[((long long)b * 2 + k) * C + cc];
+  if (ok) {
+    const float* p = part + (long long)k * C + cc;
+    const long long stride = 2LL * C;
+    int b = wave;
+    for (; b + 7 * LNR_WAVES < nb; b += 8 * LNR_WAVES) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = p[(long long)(b + j * LNR_WAVES) * stride];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; b < nb; b += LNR_WAVES) s += p[(long long)b * stride];
+  }
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave != 0 || !ok) return;
+  float t = 0.f;
+#pragma unroll
+  for (int w = 0; w < LNR_WAVES; ++w) t += red[w][lane];
   float* out = k == 0 ? dgamma : dbeta;
-  if (out) out[cc] = accumulate ? out[cc] + s : s;
+  if (out) out[cc] = accumulate ? out[cc] + t : t;
 }
 
 // ------------------------------------------------------------------ GELU
@@ -441,7 +464,7 @@ int ln_nl(int C) {
 
 int ln_blocks(long long rows) {
   long long b = (rows + LN_WAVES - 1) / LN_WAVES;
-  return (int)(b < 2048 ? (b < 1 ? 1 : b) : 2048);
+  return (int)(b < 1024 ? (b < 1 ? 1 : b) : 1024);
 }
 
 template <typename T>
@@ -518,8 +541,8 @@ int mmseg_layernorm_bwd(const void* x, int ldx, const void* dy, int lddy, void* 
                     : ln_bwd_t<float>(x, ldx, dy, lddy, dx, lddx, rows, C, gamma, mean, rstd, add_dx, part, s);
   if (r || !part) return r;
   const int nb = ln_blocks(rows) * (64 * ln_nl(C) <= 1024 ? 1 : LN_WAVES);
-  hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(ceil_div(2LL * C, 256)), dim3(256), 0, s, part, nb, C, dgamma,
-                     dbeta, accumulate);
+  hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(ceil_div(2LL * C, 64)), dim3(64 * LNR_WAVES), 0, s, part, nb, C,
+                     dgamma, dbeta, accumulate);
   return mmseg::check_launch("ln_param_reduce");
 }
 

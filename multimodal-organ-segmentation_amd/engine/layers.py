@@ -55,38 +55,54 @@ def _gemm_ksplit(M: int, ncols: int, KG: int) -> int:
 
 class Packer:
     """Weight packing of a whole program per step: every 3^3 conv's two operand images in ONE launch
-    (mmseg_pack_conv3_batched: one coalesced read of the fp32 weights), the few transposed / 1x1 layers
-    per layer.  MMSEG_PACK=0 selects the per-layer element-wise pack (A/B only)."""
+    (mmseg_pack_conv3_batched: one coalesced read of the fp32 weights), the transposed / 1x1 / token-linear
+    images in one more (mmseg_pack_weights_batched).  MMSEG_PACK=0 selects the per-layer element-wise pack
+    (A/B only)."""
 
     def __init__(self, rt: Runtime, descs):
         import struct
         self.rt = rt
         self.per_layer = list(descs) if os.environ.get("MMSEG_PACK", "1") == "0" else []
+        self.table = self.gtable = None
         if self.per_layer:
             return
         nbytes = rt.lib.mmseg_pack3_desc_bytes()
         blob, begin, n = bytearray(), 0, 0
-        dgrad = {d[0]: d for d in descs if d[2] == 1}
+        dgrad = {d[0]: d for d in descs if d[2] in (1, 6)}
+        rest = []
         for d in descs:
             w, dst, mode, Co, Ci, Cip, KG, KGp, Cpad = d
-            if mode == 1:
+            if mode in (1, 6):
                 continue
             if mode != 0:
-                self.per_layer.append(d)
+                rest.append(d)
                 continue
             dd = dgrad.get(w)
-            rec = struct.pack("<QQQ8i", w, dst, dd[1] if dd else 0, Co, Ci, Cip, Cpad, dd[8] if dd else 0, begin, 0, 0)
+            cop = dd[5] if dd is not None and dd[2] == 6 else 0
+            rec = struct.pack("<QQQ8i", w, dst, dd[1] if dd else 0, Co, Ci, Cip, Cpad, dd[8] if dd else 0, begin, cop,
+                              0)
             assert len(rec) == nbytes, (len(rec), nbytes)
             blob += rec
             begin += (Co // 8) * (-(-Ci // 32))
             n += 1
         self.n, self.nblocks = n, begin
-        self.table = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(rt.device) if n else None
+        if n:
+            self.table = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(rt.device)
+        if rest:
+            gblob, total = bytearray(), 0
+            for (w, dst, mode, Co, Ci, Cip, KG, KGp, Cpad) in rest:
+                gblob += struct.pack("<QQ8iq", w, dst, mode, Co, Ci, Cip, KG, KGp, Cpad, 0, total)
+                total += KGp * Cpad * 8
+            assert len(gblob) == len(rest) * rt.lib.mmseg_pack_desc_bytes()
+            self.gtable = torch.frombuffer(gblob, dtype=torch.uint8).to(rt.device)
+            self.gn, self.gtotal = len(rest), total
 
     def run(self):
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
-        if self.table is not None and not os.environ.get("MMSEG_PACK", "1") == "0":
+        if self.table is not None:
             L.mmseg_pack_conv3_batched(ptr(self.table), self.n, self.nblocks, code, s)
+        if self.gtable is not None:
+            L.mmseg_pack_weights_batched(ptr(self.gtable), self.gn, self.gtotal, code, s)
         for d in self.per_layer:
             L.mmseg_pack_weight(*d, code, s)
 
@@ -114,20 +130,28 @@ class DySpec:
 
 class Conv3:
     def __init__(self, rt: Runtime, conv: nn.Conv3d, flat: FlatParams, cin_pad: Optional[int] = None,
-                 need_dgrad: bool = True, cout_pad: Optional[int] = None):
+                 need_dgrad: bool = True, cout_pad: Optional[int] = None, pad_cols: bool = False):
         """cin_pad: the input tensor's channel count seen by the GEMM (8 x a power of two >= Ci; the extra
         channels meet zero weights).  cout_pad: the same for the data-gradient reduction over Co (its dy
-        tensor must hold cout_pad readable channels; pack mode 6 zeroes their weights)."""
+        tensor must hold cout_pad readable channels; pack mode 6 zeroes their weights).
+        pad_cols (bias-free convs whose output / input-gradient tensors own cout_pad / cin_pad channels):
+        the GEMMs produce the padded column counts (zeros in the padding) and the weight gradient is taken
+        over cout_pad rows into a staging buffer, so channel counts like 48 run on the brick kernels."""
         self.rt, self.conv, self.flat = rt, conv, flat
         self.Co, self.Ci = conv.weight.shape[:2]
         self.Cip = cin_pad or self.Ci
         self.Cop = cout_pad or self.Co
         if self.Co % 8 or self.Cip % 8 or self.Cop % 8 or self.Cop < self.Co:
             raise ValueError("conv channels must be multiples of 8")
+        if pad_cols and conv.bias is not None:
+            raise ValueError("pad_cols: bias-free convs only")
+        self.pad_cols = pad_cols
+        self.ncols_f = self.Cop if pad_cols else self.Co
+        self.ncols_d = self.Cip if pad_cols else self.Ci
         self.cpg_shift = pow2_shift(self.Cip // 8)
         self.KG = 27 * self.Cip // 8
         self.KGp = round_up(self.KG, 4)
-        self.Cpad = _col_tile(self.Co)
+        self.Cpad = _col_tile(self.ncols_f)
         # zeros: the batched pack never writes the K / Cin padding entries
         self.wf = torch.zeros(self.KGp * self.Cpad * 8, dtype=rt.dtype, device=rt.device)
         self.need_dgrad = need_dgrad
@@ -135,8 +159,11 @@ class Conv3:
             self.dshift = pow2_shift(self.Cop // 8)
             self.KGd = 27 * self.Cop // 8
             self.KGdp = round_up(self.KGd, 4)
-            self.Cpad_d = _col_tile(self.Cip)
+            self.Cpad_d = _col_tile(self.ncols_d)
             self.wd = torch.zeros(self.KGdp * self.Cpad_d * 8, dtype=rt.dtype, device=rt.device)
+        # weight gradient over Cop rows (brick kernels need Co % 32 == 0) into a staging [Cop][Ci][27]
+        self.wg_stage = (torch.empty(self.Cop * self.Ci * 27, dtype=torch.float32, device=rt.device)
+                         if pad_cols and self.Co % 32 and self.Cop % 32 == 0 else None)
 
     def descs(self):
         w = self.conv.weight
@@ -179,13 +206,14 @@ class Conv3:
                                            y.ld, x.N, x.D, x.H, x.W, self.Co, self.rt.code, self.rt.stream)
             return
         M = x.N * x.V
-        ks = self.rt.lib.mmseg_conv3_splits(M, self.Co, self.Cpad, self.KG, self.cpg_shift, x.D, x.H, x.W, x.ld, y.ld,
+        nc = self.ncols_f
+        ks = self.rt.lib.mmseg_conv3_splits(M, nc, self.Cpad, self.KG, self.cpg_shift, x.D, x.H, x.W, x.ld, y.ld,
                                             self.rt.code)
-        ws = self.rt.ws(ks * M * self.Co) if ks > 1 else None
-        with TIMER.region(_gemm_name(self.rt, self.Co, "conv3"), flops=2.0 * M * self.Co * 27 * self.Ci,
+        ws = self.rt.ws(ks * M * nc) if ks > 1 else None
+        with TIMER.region(_gemm_name(self.rt, nc, "conv3"), flops=2.0 * M * self.Co * 27 * self.Ci,
                           nbytes=_io_bytes(self.rt, M, self.Cip, self.Co, 27 * self.Cip * self.Co)):
             self.rt.lib.mmseg_conv_gemm(x.ptr, x.ld, ptr(self.wf), ptr(self.conv.bias), y.ptr, y.ld, ptr(ws),
-                                        MODE_CONV3, M, self.Co, self.Cpad, self.KG, self.cpg_shift, x.D, x.H, x.W, ks,
+                                        MODE_CONV3, M, nc, self.Cpad, self.KG, self.cpg_shift, x.D, x.H, x.W, ks,
                                         self.rt.code, self.rt.stream)
 
     def bwd(self, x: Act, dy: Act, dx: Optional[Act], accumulate: bool):
@@ -205,23 +233,33 @@ class Conv3:
                                  int(accumulate), s)
             self.flat.mark(self.conv.weight, self.conv.bias)
             return
-        wsf = L.mmseg_conv3_wgrad_ws_floats(V, self.Co, self.Cip, self.Ci, self.cpg_shift, x.D, x.H, x.W, dy.ld,
+        rows = self.Cop if self.wg_stage is not None else self.Co
+        wsf = L.mmseg_conv3_wgrad_ws_floats(V, rows, self.Cip, self.Ci, self.cpg_shift, x.D, x.H, x.W, dy.ld,
                                             x.ld, code)
         ws = self.rt.ws(wsf) if wsf > 0 else None
+        wgrad = self.flat.grad(self.conv.weight)
         with TIMER.region(_gemm_name(self.rt, 0, "conv3"), flops=2.0 * V * self.Co * 27 * self.Ci,
                           nbytes=_io_bytes(self.rt, V, self.Cip, self.Co, 27 * self.Cip * self.Co, 4)):
-            L.mmseg_conv3_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, ptr(self.flat.grad(self.conv.weight)),
-                                ptr(self.flat.grad(self.conv.bias)) if self.conv.bias is not None else None, self.Co,
-                                self.Cip, self.Ci, self.cpg_shift, V, x.D, x.H, x.W, ptr(ws), wsf, int(accumulate),
-                                code, s)
+            L.mmseg_conv3_wgrad(dy.ptr, dy.ld, x.ptr, x.ld,
+                                ptr(self.wg_stage) if self.wg_stage is not None else ptr(wgrad),
+                                ptr(self.flat.grad(self.conv.bias)) if self.conv.bias is not None else None, rows,
+                                self.Cip, self.Ci, self.cpg_shift, V, x.D, x.H, x.W, ptr(ws), wsf,
+                                int(accumulate) if self.wg_stage is None else 0, code, s)
+        if self.wg_stage is not None:     # rows [0, Co) of the staging are the gradient's storage order
+            n = wgrad.numel()
+            if accumulate:
+                L.mmseg_add(ptr(wgrad), ptr(self.wg_stage), ptr(wgrad), n, 0, s)
+            else:
+                wgrad.view(-1).copy_(self.wg_stage[:n])
         self.flat.mark(*[p for p in (self.conv.weight, self.conv.bias) if p is not None])
         if dx is not None:
             M = V
-            ks = L.mmseg_conv3_splits(M, self.Ci, self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, dy.ld, dx.ld, code)
-            ws = self.rt.ws(ks * M * self.Ci) if ks > 1 else None
-            with TIMER.region(_gemm_name(self.rt, self.Ci, "conv3"), flops=2.0 * M * self.Co * 27 * self.Ci,
+            nc = self.ncols_d
+            ks = L.mmseg_conv3_splits(M, nc, self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, dy.ld, dx.ld, code)
+            ws = self.rt.ws(ks * M * nc) if ks > 1 else None
+            with TIMER.region(_gemm_name(self.rt, nc, "conv3"), flops=2.0 * M * self.Co * 27 * self.Ci,
                               nbytes=_io_bytes(self.rt, M, self.Co, self.Cip, 27 * self.Cip * self.Co)):
-                L.mmseg_conv_gemm(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, ptr(ws), MODE_CONV3, M, self.Ci,
+                L.mmseg_conv_gemm(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, ptr(ws), MODE_CONV3, M, nc,
                                   self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, ks, code, s)
 
 

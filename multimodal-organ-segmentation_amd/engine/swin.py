@@ -32,7 +32,7 @@ import torch.nn as nn
 
 from .._lib import ptr
 from .attention import WindowAttentionEngine
-from .layers import MODE_POINT, Conv3, ConvT2, Head, _col_tile, _gemm_ksplit, _wgrad_ksplit
+from .layers import MODE_POINT, Conv3, ConvT2, Head, Packer, _col_tile, _gemm_ksplit, _wgrad_ksplit
 from .runtime import Act, FlatParams, Runtime, round_up
 
 LN_EPS = 1e-5
@@ -326,8 +326,11 @@ class ResBlockProg:
         self.rt, self.cin, self.cout = rt, cin, cout
         self.cip = cin_ld if first else cpad(cin)
         self.cop = cpad(cout)
-        self.c1 = Conv3(rt, blk.conv1.conv, flat, cin_pad=self.cip, need_dgrad=not first, cout_pad=self.cop)
-        self.c2 = Conv3(rt, blk.conv2.conv, flat, cin_pad=self.cop, cout_pad=self.cop)
+        # pad_cols: the a1 / a2 / dh / da buffers own their padded channels (zero-filled by the GEMMs); the
+        # input gradient dx of conv1 is a whole buffer too (dcat, or the block's own dx)
+        self.c1 = Conv3(rt, blk.conv1.conv, flat, cin_pad=self.cip, need_dgrad=not first, cout_pad=self.cop,
+                        pad_cols=True)
+        self.c2 = Conv3(rt, blk.conv2.conv, flat, cin_pad=self.cop, cout_pad=self.cop, pad_cols=True)
         self.has3 = hasattr(blk, "conv3")
         self.c3 = Lin(rt, blk.conv3.conv.weight, None, flat, cin_pad=self.cip if first else None,
                       need_dgrad=not first) if self.has3 else None
@@ -481,10 +484,10 @@ class SwinUNETRProgram:
         return d
 
     def pack(self):
+        """Every packed weight image of the network in two launches (layers.Packer)."""
         if self._packed is None:
-            self._packed = self._descs()
-        for d in self._packed:
-            self.rt.lib.mmseg_pack_weight(*d, self.rt.code, self.rt.stream)
+            self._packed = Packer(self.rt, self._descs())
+        self._packed.run()
 
     def setup(self, N, D, H, W):
         if self.shape == (N, D, H, W):
