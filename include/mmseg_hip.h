@@ -255,6 +255,26 @@ int mmseg_res_apply(const void* a, int lda, const float* ma, const float* ra, co
 int mmseg_lrelu_bwd(const void* y, int ldy, const void* dy, int lddy, void* g, int ldg, long long rows, int C,
                     float slope, int dtype, void* stream);
 
+/* ------------------------------------------------------- device data path */
+/* ModalitySpecificNormalize (src/data/transforms.py:362-404) on one channel [V] fp32 in place:
+ * kind 0 CT window (lo = center - width/2, hi = center + width/2): clip + (x - lo) / (hi - lo);
+ * kind 1 PET: x / max(x) when max > 0; kind 2 MRI/US: (x - mean) / (std + 1e-8), fp64 statistics.
+ * ws: mmseg_normalize_ws_bytes() bytes (kinds 1, 2). */
+long long mmseg_normalize_ws_bytes(void);
+int mmseg_modality_normalize(float* x, long long V, int kind, double lo, double hi, void* ws, void* stream);
+/* Resize (transforms.py:215-250): scipy.ndimage.zoom order 1 per channel of src [C][D][H][W] -> dst
+ * [C][d][h][w] (corner-aligned, fp64 math), and order 0 for labels (int64 or uint8). */
+int mmseg_resize_linear(const float* src, int C, int D, int H, int W, float* dst, int d, int h, int w, void* stream);
+int mmseg_resize_nearest(const void* src, int label_bytes, int C, int D, int H, int W, void* dst, int d, int h, int w,
+                         void* stream);
+/* Synthetic phantom of one sample on the device (replaces the NIfTI load of dataset.py:74-117 for synthetic
+ * runs): label [S^3] (class c+1 inside ellipsoid c = geo[c*6 .. +6) = centre z,y,x, radius z,y,x, first
+ * class wins), image [M][S^3] = class_mean[m*(ncls+1) + label] + noise_sd[m] * N (|N| if abs_noise[m]),
+ * N standard normal from the SplitMix64 counter stream keys[m] (host array arguments). */
+int mmseg_phantom(int S, int ncls, const double* geo, int M, const float* class_mean, const float* noise_sd,
+                  const int* abs_noise, const unsigned long long* keys, void* label, int label_bytes, float* image,
+                  void* stream);
+
 /* ------------------------------------------------ sliding-window inference */
 /* MONAI sliding_window_inference (constant blending) as called by Trainer._sliding_window_inference
  * (trainer.py:370-395).  win: device int[4*nw] = (n, z0, y0, x0) per window in the volume's frame

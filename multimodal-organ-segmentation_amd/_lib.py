@@ -23,6 +23,7 @@ _CTYPE = {
     "int": ctypes.c_int,
     "long long": ctypes.c_longlong,
     "float": ctypes.c_float,
+    "double": ctypes.c_double,
     "size_t": ctypes.c_size_t,
     "void": None,
     "const char*": ctypes.c_char_p,

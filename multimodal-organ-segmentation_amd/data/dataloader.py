@@ -3,7 +3,8 @@
 The reference reads a CSV of NIfTI files (nibabel, absent here); the engine's
 loader serves the seeded synthetic phantoms of data/synthetic.py in the same
 batch format.  Under data parallelism each rank takes samples r, r+W, ...
-(DistributedSampler semantics)."""
+(DistributedSampler semantics).  With data.synthetic.device: true
+the phantoms are generated and normalised on the GPU instead (data/device.py)."""
 from typing import Any, Dict
 
 import torch
@@ -24,7 +25,19 @@ def get_dataset(config: Dict[str, Any], split: str = "train"):
                                seed=seed)
 
 
-def get_dataloader(config: Dict[str, Any], split: str = "train", shuffle=None, drop_last=None) -> DataLoader:
+def get_dataloader(config: Dict[str, Any], split: str = "train", shuffle=None, drop_last=None):
+    syn = config["data"].get("synthetic") or {}
+    if syn.get("device", False):
+        # data.synthetic.device: true -> phantoms generated and normalised on the GPU (data/device.py)
+        from .device import DeviceLoader, DevicePhantomDataset
+        n = syn["n_train"] if split == "train" else syn.get("n_val", 2)
+        seed = syn.get("seed", 1234) + (0 if split == "train" else 100000)
+        ds = DevicePhantomDataset(n, syn.get("size", 96), config["model"]["out_channels"],
+                                  config["data"]["modalities"], torch.device("cuda", torch.cuda.current_device()),
+                                  seed=seed, preprocessing=config["data"].get("preprocessing"))
+        return DeviceLoader(ds, config["training"]["batch_size"],
+                            shuffle=split == "train" if shuffle is None else shuffle,
+                            drop_last=split == "train" if drop_last is None else drop_last, seed=seed)
     ds = get_dataset(config, split)
     w, r = ddp.world(), ddp.rank()
     if w > 1:

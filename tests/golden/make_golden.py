@@ -217,6 +217,31 @@ def bidirectional_case():
     print("bidirectional attention done")
 
 
+def transforms_case():
+    """ModalitySpecificNormalize (transforms.py:362-404) + Resize (transforms.py:215-250, scipy zoom order 1 /
+    labels order 0) on a small raw CT (HU) / PET (SUV) / MRI sample, non-cubic and resized up and down."""
+    import src.data.transforms as T
+    rng = np.random.Generator(np.random.PCG64(77))
+    shape = (20, 24, 28)
+    ct = rng.uniform(-1200, 1500, shape).astype(np.float32)
+    pet = np.abs(rng.normal(2.0, 3.0, shape)).astype(np.float32)
+    mri = rng.normal(300.0, 80.0, shape).astype(np.float32)
+    image = np.stack([ct, pet, mri])
+    label = rng.integers(0, 5, size=shape).astype(np.int64)
+    cfg = {"data": {"modalities": ["CT", "PET", "MRI"],
+                    "preprocessing": {"ct": {"window_center": -100, "window_width": 700},
+                                      "pet": {"normalize": True}, "mri": {"normalize": True}}}}
+    norm = T.ModalitySpecificNormalize(cfg)({"image": image.copy()})["image"]
+    out = {"image_in": image, "label_in": label, "normalized": norm}
+    for name, size in (("up", (32, 30, 36)), ("down", (12, 16, 9))):
+        r = T.Resize(size, order=1)({"image": norm.copy(), "label": label.copy()})
+        out[f"resized_{name}"] = r["image"]
+        out[f"label_{name}"] = r["label"]
+        out[f"size_{name}"] = np.array(size, dtype=np.int64)
+    np.savez_compressed(os.path.join(OUT, "transforms.npz"), **out)
+    print("transforms done", norm.dtype, out["resized_up"].dtype, out["label_up"].dtype)
+
+
 def full_case(tag, cfg, S, B, seed):
     """Full-size configs: forward summary only (logits stats + seeded voxel samples)."""
     torch.manual_seed(seed)
@@ -256,6 +281,7 @@ if __name__ == "__main__":
     loss_case()
     metric_case()
     cross_attention_case()
+    transforms_case()
     full_case("full_unet_c2", base_config("unet", ["CT", "PET"], 6, [32, 64, 128, 256, 512]), S=96, B=2, seed=1234)
     full_case("full_dual_c3", base_config("dual_encoder", ["CT", "PET"], 6, [32, 64, 128, 256, 512]),
               S=96, B=2, seed=1234)
