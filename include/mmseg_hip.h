@@ -213,6 +213,22 @@ int mmseg_softmax_bias_rows(const float* S, int lds, const float* bias, const fl
 int mmseg_relpos_table_grad(const void* dS, int ldn, int B, int heads, int N, float* dB, const int* offs,
                             const int* pairs, int T, float* gtable, int accumulate, int dtype, void* stream);
 
+/* Fused window attention core (bf16, head_dim 8 or 16, <= 352 tokens per window): per (window, head),
+ * O = softmax(scale q k^T + table[rel(n, m)] (+ -100 across regions)) v with the scores kept on chip.
+ * qkv [B*N][3C] (q | k | v, head h at channels h*hd), O [B*N][C], lse [B*heads][352] (row log-sum-exp,
+ * mmseg_winattn_lse_floats()), table [heads][T] (the module's [T][heads] bias table transposed) with
+ * T = (2w0-1)(2w1-1)(2w2-1) of the module's full window
+ * (w0, w1, w2): rel() numbers the tokens in that window, as MONAI's relative_position_index[:N, :N];
+ * region [nw][N] uint8 labels of the shifted-window regions of window b % nw, or NULL (no mask).
+ * bwd: dqkv [B*N][3C] (every element written) and dS [B][heads][N][ldn] (bf16, keys >= N zero) for
+ * mmseg_relpos_table_grad. */
+long long mmseg_winattn_lse_floats(int B, int heads);
+int mmseg_winattn_fwd(const void* qkv, int B, int N, int C, int heads, const float* table, int T, int w0, int w1,
+                      int w2, const uint8_t* region, int nw, float scale, void* O, float* lse, void* stream);
+int mmseg_winattn_bwd(const void* qkv, const void* O, const void* dO, const float* lse, int B, int N, int C, int heads,
+                      const float* table, int T, int w0, int w1, int w2, const uint8_t* region, int nw, float scale,
+                      void* dqkv, void* dS, int ldn, void* stream);
+
 /* ---------------------------------------------------- SwinUNETR tokens */
 /* The SwinTransformer stages and UNETR residual blocks of MONAI SwinUNETR (built by the reference's
  * swin_unetr.py:80-96; MONAI absent -> parity unpinned, restated in oracle/swin_oracle.py).  Token

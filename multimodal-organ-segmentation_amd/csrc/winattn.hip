@@ -1,0 +1,412 @@
+// Fused Swin window attention (MONAI WindowAttention core, SwinUNETR via the
+// reference's swin_unetr.py:80-96): per (window, head) block, scores, the
+// relative-position bias, the shifted-window mask, softmax and P.V stay in
+// registers / LDS — no materialised N x N score or probability tensors.  bf16
+// storage, head_dim <= 16 (padded to the 16-deep MFMA K), N <= 352 tokens.
+//
+//   fwd   : S^T = K Q^T (v_mfma_f32_16x16x16_bf16: each lane then holds four
+//           consecutive keys of ONE query, which is exactly the A-operand
+//           layout P needs for O = P V), bias + mask; pass 1 over the key
+//           tiles takes the row max / sum, pass 2 recomputes the scores and
+//           accumulates O = P V; the row log-sum-exp is kept for the backward.
+//   bwd_kv: per key tile, over all query tiles: S and dP = dO V^T recomputed
+//           in the [query][key] layout, whose transposed A operand gives
+//           dV += P^T dO and dK += scale dS^T Q without shuffles.
+//   bwd_q : per query tile, over all key tiles: S^T / dP^T in the forward
+//           layout, dQ += scale dS K, and dS written [B][h][N][ldn] for the
+//           bias-table gradient (mmseg_relpos_table_grad).
+// Two backward passes keep every sum inside one wave (fixed order): no atomics.
+// The relative-position index is computed from the token coordinates in the
+// module's full window (MONAI indexes relative_position_index[:n, :n] for a
+// smaller window, i.e. keeps the full window's numbering), the mask from
+// per-window region labels (MONAI compute_mask: -100 across regions).
+#include "mmseg_common.h"
+
+namespace {
+
+constexpr int NPMAX = 352;            // tokens per window, padded to 16
+constexpr int TP = NPMAX + 8;         // pitch of the [16][tokens] transposed images (720 B: conflict-free)
+constexpr int TMAX = 2197;            // (2*7-1)^3 bias-table rows
+constexpr int NTMAX = NPMAX / 16;
+constexpr int WAVES = 8;               // waves per block (one (window, head) each)
+typedef short s4 __attribute__((ext_vector_type(4)));
+
+struct WinAttnArgs {
+  const bf16_t* qkv;     // [B*N][3C]
+  const bf16_t* O;       // [B*N][C] forward output (bwd)
+  const bf16_t* dO;      // [B*N][C] (bwd)
+  bf16_t* out;           // fwd: O [B*N][C]; bwd: dqkv [B*N][3C]
+  float* lse;            // [B*heads][NPMAX]
+  bf16_t* dS;            // bwd_q: [B][heads][N][ldn]
+  const float* table;    // [heads][T] (the module's [T][heads] table transposed: one contiguous row per head)
+  const uint8_t* region; // [nw][N] or null (no mask)
+  int B, N, C, heads, hd, nw, T, ldn;
+  int w0, w1, w2;        // the module's full window
+  float scale;
+};
+
+__device__ __forceinline__ s4 ld4(const bf16_t* p) { return *reinterpret_cast<const s4*>(p); }
+
+__device__ __forceinline__ s4 pack4(float a, float b, float c, float d) {
+  typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+  b4 v = {(bf16_t)a, (bf16_t)b, (bf16_t)c, (bf16_t)d};
+  return __builtin_bit_cast(s4, v);
+}
+
+__device__ __forceinline__ f32x4 mma(s4 a, s4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+
+// relative-position table row of tokens (n, m) in the full window's numbering:
+// ((dz + w0-1)(2w1-1) + dy + w1-1)(2w2-1) + dx + w2-1 = code(n) - code(m) + code_off with
+// code(n) = (z (2w1-1) + y)(2w2-1) + x, so a per-token code staged in LDS gives the row with one subtraction
+__device__ __forceinline__ void stage_codes(int* code, const WinAttnArgs& a, int np) {
+  for (int n = threadIdx.x; n < np; n += blockDim.x) {
+    const int z = n / (a.w1 * a.w2), y = (n / a.w2) % a.w1, x = n % a.w2;
+    code[n] = (z * (2 * a.w1 - 1) + y) * (2 * a.w2 - 1) + x;
+  }
+}
+__device__ __forceinline__ int code_off(const WinAttnArgs& a) {
+  return ((a.w0 - 1) * (2 * a.w1 - 1) + (a.w1 - 1)) * (2 * a.w2 - 1) + (a.w2 - 1);
+}
+
+// shared operand staging of one (window, head): rows [NPMAX][16] and/or transposed [16][TP]
+struct Stage {
+  int b, h, N, np;
+};
+
+__device__ __forceinline__ void stage_rows(bf16_t (*dst)[16], const bf16_t* src, int ld, int col0, const Stage& s,
+                                           int hd, bf16_t (*dstT)[TP]) {
+  // thread per (token, 8-channel half); zeros past N and past hd
+  for (int e = threadIdx.x; e < s.np * 2; e += blockDim.x) {
+    const int n = e >> 1, half = e & 1;
+    V8<bf16_t> v;
+    if (n < s.N && half * 8 < hd) {
+      if (hd >= half * 8 + 8) {
+        v.load(src + (long long)(s.b * s.N + n) * ld + col0 + half * 8);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v.set(j, half * 8 + j < hd ? (float)src[(long long)(s.b * s.N + n) * ld + col0 + half * 8 + j] : 0.f);
+      }
+    } else {
+      v.zero();
+    }
+    if (dst) v.store(&dst[n][half * 8]);
+    if (dstT) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dstT[half * 8 + j][n] = v.v[j];
+    }
+  }
+}
+
+__device__ __forceinline__ void stage_table(float* tab, const WinAttnArgs& a, int h) {
+  const float* row = a.table + (long long)h * a.T;
+  for (int t = threadIdx.x; t < a.T; t += blockDim.x) tab[t] = row[t];
+}
+
+__device__ __forceinline__ void stage_region(uint8_t* reg, const WinAttnArgs& a, int b) {
+  if (!a.region) return;
+  const uint8_t* r = a.region + (long long)(b % a.nw) * a.N;
+  for (int n = threadIdx.x; n < NPMAX; n += blockDim.x) reg[n] = n < a.N ? r[n] : 0;
+}
+
+// bias + mask of one query against 4 consecutive keys k0..k0+3 (the S^T lane layout), -inf past N
+__device__ __forceinline__ void scores_q(const f32x4& acc, bool qv, const float* tq, uint32_t rq, int k0,
+                                         const WinAttnArgs& a, const int* code, const uint8_t* reg, float v[4]) {
+  const int4 ck = *reinterpret_cast<const int4*>(code + k0);
+  const uint32_t rk = a.region ? *reinterpret_cast<const uint32_t*>(reg + k0) : 0u;
+  const int c[4] = {ck.x, ck.y, ck.z, ck.w};
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float t = acc[r] * a.scale + tq[-c[r]];
+    if (a.region && ((rk >> (8 * r)) & 255u) != rq) t -= 100.0f;
+    v[r] = (qv && k0 + r < a.N) ? t : -INFINITY;
+  }
+}
+
+// bias + mask of one key against 4 consecutive queries q0..q0+3 (the S lane layout)
+__device__ __forceinline__ void scores_k(const f32x4& acc, bool kv, const float* tk, uint32_t rk, int q0,
+                                         const WinAttnArgs& a, const int* code, const uint8_t* reg, float v[4]) {
+  const int4 cq = *reinterpret_cast<const int4*>(code + q0);
+  const uint32_t rq = a.region ? *reinterpret_cast<const uint32_t*>(reg + q0) : 0u;
+  const int c[4] = {cq.x, cq.y, cq.z, cq.w};
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float t = acc[r] * a.scale + tk[c[r]];
+    if (a.region && ((rq >> (8 * r)) & 255u) != rk) t -= 100.0f;
+    v[r] = (kv && q0 + r < a.N) ? t : -INFINITY;
+  }
+}
+
+// ------------------------------------------------------------------ forward
+// Two passes over the key tiles per query tile: (1) running max / sum of the row (each lane holds one query,
+// merged over the 4 lanes sharing it), (2) scores recomputed (one MFMA each), P = exp(s - lse), O += P V.
+__global__ __launch_bounds__(512) void winattn_fwd_kernel(WinAttnArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Vt[16][TP];
+  __shared__ float tab[TMAX];
+  __shared__ __attribute__((aligned(16))) int code[NPMAX];
+  __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
+  const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads;
+  const int np = (a.N + 15) & ~15, nt = np / 16;
+  const Stage st{b, h, a.N, np};
+  const int C3 = 3 * a.C, hoff = h * a.hd;
+  stage_rows(Qs, a.qkv, C3, hoff, st, a.hd, nullptr);
+  stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, nullptr);
+  stage_rows(nullptr, a.qkv, C3, 2 * a.C + hoff, st, a.hd, Vt);
+  stage_table(tab, a, h);
+  stage_codes(code, a, np);
+  stage_region(reg, a, b);
+  __syncthreads();
+  const float* ctab = tab + code_off(a);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  for (int qt = wave; qt < nt; qt += WAVES) {
+    const int q = qt * 16 + r16;
+    const s4 bq = ld4(&Qs[q][4 * g4]);
+    const bool qv = q < a.N;
+    const float* tq = ctab + code[q];
+    const uint32_t rq = reg[q];
+    float mx = -INFINITY, sum = 0.f;
+    for (int k0 = 0; k0 < nt; k0 += 4) {     // 4 key tiles per step: independent MFMAs / LDS lookups in flight
+      float v[4][4];
+      float tm = -INFINITY;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int kt = k0 + u < nt ? k0 + u : nt - 1;
+        const f32x4 acc = mma(ld4(&Ks[kt * 16 + r16][4 * g4]), bq, (f32x4){0.f, 0.f, 0.f, 0.f});
+        scores_q(acc, qv && k0 + u < nt, tq, rq, kt * 16 + 4 * g4, a, code, reg, v[u]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) tm = fmaxf(tm, v[u][r]);
+      }
+      if (tm > mx) {
+        sum *= __expf(mx - tm);
+        mx = tm;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sum += v[u][r] == -INFINITY ? 0.f : __expf(v[u][r] - mx);
+    }
+    // merge (max, sum) over the 4 lanes holding this query (xor 16, 32)
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) {
+      const float om = __shfl_xor(mx, o, 64), os = __shfl_xor(sum, o, 64);
+      const float m2 = fmaxf(mx, om);
+      sum = (mx == -INFINITY ? 0.f : sum * __expf(mx - m2)) + (om == -INFINITY ? 0.f : os * __expf(om - m2));
+      mx = m2;
+    }
+    const float lse = mx == -INFINITY ? 0.f : mx + __logf(sum);
+    if (g4 == 0 && q < a.N) a.lse[(long long)bh * NPMAX + q] = lse;
+    f32x4 o = {0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nt; ++kt) {
+      const f32x4 acc = mma(ld4(&Ks[kt * 16 + r16][4 * g4]), bq, (f32x4){0.f, 0.f, 0.f, 0.f});
+      float p[4];
+      scores_q(acc, qv, tq, rq, kt * 16 + 4 * g4, a, code, reg, p);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) p[r] = p[r] == -INFINITY ? 0.f : __expf(p[r] - lse);
+      o = mma(pack4(p[0], p[1], p[2], p[3]), ld4(&Vt[r16][kt * 16 + 4 * g4]), o);
+    }
+    if (r16 < a.hd) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = qt * 16 + 4 * g4 + r;
+        if (qq < a.N) a.out[(long long)(b * a.N + qq) * a.C + hoff + r16] = (bf16_t)o[r];
+      }
+    }
+  }
+}
+
+// D[q] = sum_d dO[q][d] O[q][d] of this head (fp32), staged into LDS
+__device__ __forceinline__ void stage_D(float* Dq, const WinAttnArgs& a, const Stage& s) {
+  for (int n = threadIdx.x; n < s.np; n += blockDim.x) {
+    float d = 0.f;
+    if (n < s.N) {
+      const long long base = (long long)(s.b * s.N + n) * a.C + s.h * a.hd;
+      for (int j = 0; j < a.hd; ++j) d += (float)a.dO[base + j] * (float)a.O[base + j];
+    }
+    Dq[n] = d;
+  }
+}
+
+// ------------------------------------------------------- backward: dK, dV
+__global__ __launch_bounds__(512) void winattn_bwd_kv_kernel(WinAttnArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t dOs[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Qt[16][TP];
+  __shared__ __attribute__((aligned(16))) bf16_t dOt[16][TP];
+  __shared__ float tab[TMAX];
+  __shared__ __attribute__((aligned(16))) float lse[NPMAX];
+  __shared__ __attribute__((aligned(16))) float Dq[NPMAX];
+  __shared__ __attribute__((aligned(16))) int code[NPMAX];
+  __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
+  const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads;
+  const int np = (a.N + 15) & ~15, nt = np / 16;
+  const Stage st{b, h, a.N, np};
+  const int C3 = 3 * a.C, hoff = h * a.hd;
+  stage_rows(Qs, a.qkv, C3, hoff, st, a.hd, Qt);
+  stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, nullptr);
+  stage_rows(Vs, a.qkv, C3, 2 * a.C + hoff, st, a.hd, nullptr);
+  stage_rows(dOs, a.dO, a.C, hoff, st, a.hd, dOt);
+  stage_table(tab, a, h);
+  stage_codes(code, a, np);
+  stage_region(reg, a, b);
+  stage_D(Dq, a, st);
+  for (int n = threadIdx.x; n < np; n += blockDim.x) lse[n] = n < a.N ? a.lse[(long long)bh * NPMAX + n] : 0.f;
+  __syncthreads();
+  const float* ctab = tab + code_off(a);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  for (int kt = wave; kt < nt; kt += WAVES) {
+    const int key = kt * 16 + r16;
+    const s4 bk = ld4(&Ks[key][4 * g4]);
+    const s4 bv = ld4(&Vs[key][4 * g4]);
+    const bool kv = key < a.N;
+    const float* tk = ctab - code[key];
+    const uint32_t rk = reg[key];
+    f32x4 dk = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
+    for (int qt = 0; qt < nt; ++qt) {
+      const f32x4 sc = mma(ld4(&Qs[qt * 16 + r16][4 * g4]), bk, (f32x4){0.f, 0.f, 0.f, 0.f});   // S[q][key]
+      const f32x4 dp = mma(ld4(&dOs[qt * 16 + r16][4 * g4]), bv, (f32x4){0.f, 0.f, 0.f, 0.f}); // dP[q][key]
+      float p[4], ds[4];
+      const int q0 = qt * 16 + 4 * g4;
+      scores_k(sc, kv, tk, rk, q0, a, code, reg, p);
+      const float4 l4 = *reinterpret_cast<const float4*>(lse + q0);
+      const float4 d4 = *reinterpret_cast<const float4*>(Dq + q0);
+      const float lq[4] = {l4.x, l4.y, l4.z, l4.w}, dq4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        p[r] = p[r] == -INFINITY ? 0.f : __expf(p[r] - lq[r]);
+        ds[r] = p[r] * (dp[r] - dq4[r]);
+      }
+      dv = mma(pack4(p[0], p[1], p[2], p[3]), ld4(&dOt[r16][qt * 16 + 4 * g4]), dv);
+      dk = mma(pack4(ds[0], ds[1], ds[2], ds[3]), ld4(&Qt[r16][qt * 16 + 4 * g4]), dk);
+    }
+    if (r16 < a.hd) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kk = kt * 16 + 4 * g4 + r;
+        if (kk < a.N) {
+          bf16_t* row = a.out + (long long)(b * a.N + kk) * C3;
+          row[a.C + hoff + r16] = (bf16_t)(dk[r] * a.scale);
+          row[2 * a.C + hoff + r16] = (bf16_t)dv[r];
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------- backward: dQ and dS
+__global__ __launch_bounds__(512) void winattn_bwd_q_kernel(WinAttnArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t dOs[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Kt[16][TP];
+  __shared__ float tab[TMAX];
+  __shared__ __attribute__((aligned(16))) float lse[NPMAX];
+  __shared__ __attribute__((aligned(16))) float Dq[NPMAX];
+  __shared__ __attribute__((aligned(16))) int code[NPMAX];
+  __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
+  const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads;
+  const int np = (a.N + 15) & ~15, nt = np / 16;
+  const Stage st{b, h, a.N, np};
+  const int C3 = 3 * a.C, hoff = h * a.hd;
+  stage_rows(Qs, a.qkv, C3, hoff, st, a.hd, nullptr);
+  stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, Kt);
+  stage_rows(Vs, a.qkv, C3, 2 * a.C + hoff, st, a.hd, nullptr);
+  stage_rows(dOs, a.dO, a.C, hoff, st, a.hd, nullptr);
+  stage_table(tab, a, h);
+  stage_codes(code, a, np);
+  stage_region(reg, a, b);
+  stage_D(Dq, a, st);
+  for (int n = threadIdx.x; n < np; n += blockDim.x) lse[n] = n < a.N ? a.lse[(long long)bh * NPMAX + n] : 0.f;
+  __syncthreads();
+  const float* ctab = tab + code_off(a);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  for (int qt = wave; qt < nt; qt += WAVES) {
+    const int q = qt * 16 + r16;
+    const s4 bq = ld4(&Qs[q][4 * g4]);
+    const s4 bdo = ld4(&dOs[q][4 * g4]);
+    const float lq = lse[q], dq_ = Dq[q];
+    const bool qv = q < a.N;
+    const float* tq = ctab + code[q];
+    const uint32_t rq = reg[q];
+    f32x4 dq = {0.f, 0.f, 0.f, 0.f};
+    bf16_t* dsrow = a.dS + ((long long)bh * a.N + q) * a.ldn;
+    for (int kt = 0; kt < nt; ++kt) {
+      const f32x4 sc = mma(ld4(&Ks[kt * 16 + r16][4 * g4]), bq, (f32x4){0.f, 0.f, 0.f, 0.f});   // S^T[key][q]
+      const f32x4 dp = mma(ld4(&Vs[kt * 16 + r16][4 * g4]), bdo, (f32x4){0.f, 0.f, 0.f, 0.f}); // dP^T[key][q]
+      float ds[4];
+      scores_q(sc, qv, tq, rq, kt * 16 + 4 * g4, a, code, reg, ds);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = ds[r] == -INFINITY ? 0.f : __expf(ds[r] - lq);
+        ds[r] = p * (dp[r] - dq_);
+      }
+      const s4 dsa = pack4(ds[0], ds[1], ds[2], ds[3]);
+      dq = mma(dsa, ld4(&Kt[r16][kt * 16 + 4 * g4]), dq);
+      if (q < a.N) {
+        const int k0 = kt * 16 + 4 * g4;
+        if (k0 + 3 < a.ldn) {
+          *reinterpret_cast<s4*>(dsrow + k0) = dsa;     // keys >= N carry ds = 0
+        } else {
+          typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+          const b4 v = __builtin_bit_cast(b4, dsa);
+          for (int r = 0; r < 4 && k0 + r < a.ldn; ++r) dsrow[k0 + r] = v[r];
+        }
+      }
+    }
+    if (r16 < a.hd) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = qt * 16 + 4 * g4 + r;
+        if (qq < a.N) a.out[(long long)(b * a.N + qq) * C3 + hoff + r16] = (bf16_t)(dq[r] * a.scale);
+      }
+    }
+  }
+}
+
+int check_args(const WinAttnArgs& a) {
+  MMSEG_REQUIRE(a.N >= 1 && a.N <= NPMAX && a.hd >= 1 && a.hd <= 16 && a.hd % 8 == 0 && a.C == a.heads * a.hd &&
+                    a.T <= TMAX && a.T == (2 * a.w0 - 1) * (2 * a.w1 - 1) * (2 * a.w2 - 1) &&
+                    (a.region == nullptr || a.nw >= 1),
+                "winattn: N <= %d, head_dim 8 or 16, table rows <= %d", NPMAX, TMAX);
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+long long mmseg_winattn_lse_floats(int B, int heads) { return (long long)B * heads * NPMAX; }
+
+int mmseg_winattn_fwd(const void* qkv, int B, int N, int C, int heads, const float* table, int T, int w0, int w1,
+                      int w2, const uint8_t* region, int nw, float scale, void* O, float* lse, void* stream) {
+  WinAttnArgs a{(const bf16_t*)qkv, nullptr, nullptr, (bf16_t*)O, lse, nullptr, table, region,
+                B, N, C, heads, C / heads, nw, T, 0, w0, w1, w2, scale};
+  if (check_args(a)) return 1;
+  hipLaunchKernelGGL(winattn_fwd_kernel, dim3(B * heads), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+  return mmseg::check_launch("winattn_fwd");
+}
+
+int mmseg_winattn_bwd(const void* qkv, const void* O, const void* dO, const float* lse, int B, int N, int C, int heads,
+                      const float* table, int T, int w0, int w1, int w2, const uint8_t* region, int nw, float scale,
+                      void* dqkv, void* dS, int ldn, void* stream) {
+  WinAttnArgs a{(const bf16_t*)qkv, (const bf16_t*)O, (const bf16_t*)dO, (bf16_t*)dqkv, const_cast<float*>(lse),
+                (bf16_t*)dS, table, region, B, N, C, heads, C / heads, nw, T, ldn, w0, w1, w2, scale};
+  if (check_args(a)) return 1;
+  MMSEG_REQUIRE(ldn >= N && ldn % 8 == 0, "winattn_bwd: ldn >= N, multiple of 8");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(winattn_bwd_kv_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  if (mmseg::check_launch("winattn_bwd_kv")) return 1;
+  hipLaunchKernelGGL(winattn_bwd_q_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  return mmseg::check_launch("winattn_bwd_q");
+}
+
+}  // extern "C"

@@ -54,6 +54,20 @@ def window_size_for(dims, window, shift):
     return tuple(ws), tuple(ss)
 
 
+def shift_regions(dims_p, ws, ss) -> np.ndarray:
+    """Region label of every token of every window [nW, N] (MONAI compute_mask's img_mask, partitioned)."""
+    img = np.zeros(dims_p, dtype=np.float32)
+    cnt = 0
+    for a in (slice(-ws[0]), slice(-ws[0], -ss[0]), slice(-ss[0], None)):
+        for b in (slice(-ws[1]), slice(-ws[1], -ss[1]), slice(-ss[1], None)):
+            for c in (slice(-ws[2]), slice(-ws[2], -ss[2]), slice(-ss[2], None)):
+                img[a, b, c] = cnt
+                cnt += 1
+    d, h, w = dims_p
+    t = img.reshape(d // ws[0], ws[0], h // ws[1], ws[1], w // ws[2], ws[2]).transpose(0, 2, 4, 1, 3, 5)
+    return t.reshape(-1, ws[0] * ws[1] * ws[2])
+
+
 def shift_mask(dims_p, ws, ss) -> np.ndarray:
     """MONAI compute_mask (3-D) on the padded grid: [nW, N, N] with -100 between tokens of different shifted
     regions (host-side plan, once per shape)."""
@@ -172,6 +186,20 @@ class SwinBlockProg:
     def descs(self):
         return self.qkv.descs() + self.proj.descs() + self.fc1.descs() + self.fc2.descs()
 
+    def _table_t(self) -> torch.Tensor:
+        """The bias table [T][heads] transposed to [heads][T] (one contiguous row per head for the kernels)."""
+        T, h = self.table.shape
+        out = torch.empty(h * T, dtype=torch.float32, device=self.rt.device)
+        self.rt.lib.mmseg_transpose(ptr(self.table), 0, 0, h, 0, ptr(out), 0, 0, T, 0, 1, 1, T, h, self.rt.stream)
+        return out
+
+    def _fused(self, Nw: int) -> bool:
+        """The fused window-attention kernels (csrc/winattn.hip): bf16 storage, head_dim 8 / 16, <= 352
+        tokens per window (MMSEG_WINATTN=0: the batched-GEMM path)."""
+        import os
+        return (self.rt.code == 1 and self.core.hd in (8, 16) and Nw <= 352
+                and os.environ.get("MMSEG_WINATTN", "1") != "0")
+
     def _empty(self, n):
         return torch.empty(int(n), dtype=self.rt.dtype, device=self.rt.device)
 
@@ -193,7 +221,18 @@ class SwinBlockProg:
         qkv = self._empty(Mw * 3 * C)
         self.qkv.fwd(xw, C, Mw, qkv, 3 * C)
         mask = geo["mask"] if any(sh) else None
-        O, P = self.core.core_fwd(qkv, B, Nw, mask, self.table, geo["index"])
+        fused = self._fused(Nw)
+        if fused:
+            O = self._empty(Mw * C)
+            P = torch.empty(L.mmseg_winattn_lse_floats(B, self.heads), dtype=torch.float32, device=rt.device)
+            region = geo["region"] if any(sh) else None
+            nw = region.shape[0] if region is not None else 0
+            w0, w1, w2 = geo["window"]
+            tabT = self._table_t()
+            L.mmseg_winattn_fwd(ptr(qkv), B, Nw, C, self.heads, ptr(tabT), self.table.shape[0], w0, w1, w2,
+                                ptr(region), nw, self.core.scale, ptr(O), ptr(P), s)
+        else:
+            O, P = self.core.core_fwd(qkv, B, Nw, mask, self.table, geo["index"])
         aw = self._empty(Mw * C)
         self.proj.fwd(O, C, Mw, aw, C)
         xm = self._empty(M * C)
@@ -211,7 +250,7 @@ class SwinBlockProg:
         out = self._empty(M * C)
         L.mmseg_add(ptr(xm), ptr(z), ptr(out), M * C, code, s)
         st = dict(x=x, st1=st1, xw=xw, qkv=qkv, O=O, P=P, xm=xm, st2=st2, ln2=ln2, h=hbuf, g=g, B=B, Nw=Nw, Mw=Mw,
-                  M=M, sh=sh)
+                  M=M, sh=sh, fused=fused)
         return out, st
 
     def bwd(self, dout: torch.Tensor, st: dict, geo, accumulate: bool) -> torch.Tensor:
@@ -233,7 +272,24 @@ class SwinBlockProg:
         dO = self._empty(Mw * C)
         self.proj.bwd(st["O"], C, daw, C, Mw, dO, C, accumulate)
         del daw
-        dqkv = self.core.core_bwd(dO, st["qkv"], st["P"], B, Nw, self.flat.grad(self.table), geo["csr"], accumulate)
+        if st["fused"]:
+            dqkv = self._empty(Mw * 3 * C)
+            ldn = (Nw + 7) // 8 * 8
+            dS = self._empty(B * self.heads * Nw * ldn)
+            region = geo["region"] if any(sh) else None
+            nw = region.shape[0] if region is not None else 0
+            w0, w1, w2 = geo["window"]
+            L.mmseg_winattn_bwd(ptr(st["qkv"]), ptr(st["O"]), ptr(dO), ptr(st["P"]), B, Nw, C, self.heads,
+                                ptr(self._table_t()), self.table.shape[0], w0, w1, w2, ptr(region), nw,
+                                self.core.scale, ptr(dqkv), ptr(dS), ldn, s)
+            dB = torch.empty(self.heads * Nw * Nw, dtype=torch.float32, device=rt.device)
+            offs, pairs, T = geo["csr"]
+            L.mmseg_relpos_table_grad(ptr(dS), ldn, B, self.heads, Nw, ptr(dB), ptr(offs), ptr(pairs), T,
+                                      ptr(self.flat.grad(self.table)), int(accumulate), code, s)
+            del dS
+        else:
+            dqkv = self.core.core_bwd(dO, st["qkv"], st["P"], B, Nw, self.flat.grad(self.table), geo["csr"],
+                                      accumulate)
         self.flat.mark(self.table)
         del dO
         dxw = self._empty(Mw * C)
@@ -275,7 +331,9 @@ class SwinStageProg:
         offs = torch.zeros(self.table_rows + 1, dtype=torch.int64)
         offs[1:] = torch.cumsum(counts, 0)
         mask = torch.from_numpy(shift_mask(padded, ws, ss)).to(dev) if any(ss) else None
-        self.geo = dict(grid=(N, d, h, w), ws=ws, ss=ss, padded=padded, mask=mask,
+        region = (torch.from_numpy(shift_regions(padded, ws, ss).astype(np.uint8)).to(dev) if any(ss) else None)
+        self.geo = dict(grid=(N, d, h, w), ws=ws, ss=ss, padded=padded, mask=mask, region=region,
+                        window=self.window,
                         index=idx.to(torch.int32).to(dev),
                         csr=(offs.to(torch.int32).to(dev), order.to(torch.int32).to(dev), self.table_rows))
         self.out_dims = tuple((s + 1) // 2 for s in (d, h, w))

@@ -295,3 +295,69 @@ def test_swin_unetr_train_step(dev):
         opt.step()
         losses.append(loss.item())
     assert all(np.isfinite(losses)) and losses[-1] < losses[0]
+
+
+# ------------------------------------------------------------ fused window attention
+@pytest.mark.parametrize("N,hd,heads,nwin,masked", [(343, 16, 3, 3, True), (343, 8, 2, 2, False), (64, 16, 2, 2, True),
+                                                    (8, 16, 1, 3, False)])
+def test_fused_window_attention_vs_torch(dev, N, hd, heads, nwin, masked):
+    """csrc/winattn.hip against a torch fp64 evaluation on the same bf16 operands: O, dq/dk/dv and the dS
+    the bias-table gradient is summed from.  Windows smaller than 7^3 use the 7^3 numbering
+    (relative_position_index[:N, :N])."""
+    C = heads * hd
+    B = 2 * nwin
+    g = torch.Generator().manual_seed(N + hd)
+    qkv = (torch.randn(B * N, 3 * C, generator=g)).to(torch.bfloat16)
+    table = torch.randn(13 ** 3, heads, generator=g) * 0.5
+    region = torch.randint(0, 4, (nwin, N), generator=g).to(torch.uint8) if masked else None
+    dO = torch.randn(B * N, C, generator=g).to(torch.bfloat16)
+    scale = hd ** -0.5
+    L, s = lib(), stream_handle()
+    qkvd, tabd, dOd = qkv.to(dev), table.t().contiguous().to(dev), dO.to(dev)
+    regd = region.to(dev) if masked else None
+    O = torch.empty(B * N, C, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(L.mmseg_winattn_lse_floats(B, heads), device=dev)
+    L.mmseg_winattn_fwd(ptr(qkvd), B, N, C, heads, ptr(tabd), 13 ** 3, 7, 7, 7, ptr(regd), nwin if masked else 0,
+                        scale, ptr(O), ptr(lse), s)
+    ldn = (N + 7) // 8 * 8
+    dqkv = torch.empty(B * N, 3 * C, dtype=torch.bfloat16, device=dev)
+    dS = torch.empty(B * heads * N * ldn, dtype=torch.bfloat16, device=dev)
+    L.mmseg_winattn_bwd(ptr(qkvd), ptr(O), ptr(dOd), ptr(lse), B, N, C, heads, ptr(tabd), 13 ** 3, 7, 7, 7,
+                        ptr(regd), nwin if masked else 0, scale, ptr(dqkv), ptr(dS), ldn, s)
+    # torch fp64 reference
+    x = qkv.double().view(B, N, 3, heads, hd).permute(2, 0, 3, 1, 4)
+    q, k, v = [t.clone().requires_grad_(True) for t in x]
+    idx = SO.relative_position_index((7, 7, 7))[:N, :N]
+    bias = table.double()[idx.reshape(-1)].view(N, N, heads).permute(2, 0, 1)
+    S = (q * scale) @ k.transpose(-1, -2) + bias
+    if masked:
+        m = torch.where(region[:, :, None] == region[:, None, :], 0.0, -100.0).double()
+        S = (S.view(B // nwin, nwin, heads, N, N) + m[None, :, None]).view(B, heads, N, N)
+    S.retain_grad()
+    P = torch.softmax(S, -1)
+    out = (P @ v).transpose(1, 2).reshape(B * N, C)
+    out.backward(dO.double())
+    assert rel2(O, out) < 1e-2
+    ref_dqkv = torch.stack([q.grad, k.grad, v.grad]).permute(1, 3, 0, 2, 4).reshape(B * N, 3 * C)
+    assert rel2(dqkv, ref_dqkv) < 3e-2
+    got_dS = dS.view(B, heads, N, ldn)[..., :N]
+    assert rel2(got_dS, S.grad) < 3e-2
+    assert torch.equal(dS.view(B, heads, N, ldn)[..., N:].cpu(), torch.zeros(B, heads, N, ldn - N, dtype=torch.bfloat16))
+
+
+def test_fused_attention_network_matches_unfused(dev, swin_case, monkeypatch):
+    """Whole bf16 SwinUNETR: the fused window attention vs the batched-GEMM path (MMSEG_WINATTN=0)."""
+    x, cot = swin_case
+    res = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("MMSEG_WINATTN", flag)
+        m = _model(dev, torch.bfloat16)
+        out = m(x[:1].to(dev))
+        (out * cot[:1].to(dev)).sum().backward()
+        res.append((out.float(), {n: p.grad.clone() for n, p in m.model.named_parameters()}))
+    assert rel2(res[0][0], res[1][0]) < 2e-2
+    # gradients: two bf16 roundings of the same step, so the LeakyReLU kink flips of
+    # test_swin_unetr_bf16_close_to_oracle separate them the same way (tens of %); the kernel-level parity is
+    # test_fused_window_attention_vs_torch
+    tab = [n for n in res[0][1] if "relative_position_bias_table" in n]
+    assert max(rel2(res[0][1][n], res[1][1][n]) for n in tab) < 0.5
