@@ -729,9 +729,10 @@ __device__ __forceinline__ void buf_load_v8<float>(V8<float>& v, __amdgpu_buffer
   }
 }
 
-// WDB: the weight stage is double-buffered in LDS (2 x 18 KB for BN32 bf16; 2 blocks/CU still fit), so a
-// stage that only swaps weights needs one barrier (after its stores) instead of two; a stage that also
-// replaces the halo keeps the barrier before its stores.
+// WDB (MMSEG_BRICK3_WDB=1; measured 1 % slower, off): the weight stage is double-buffered in LDS (2 x 18 KB
+// for BN32 bf16; 2 blocks/CU still fit), so a stage that only swaps weights needs one barrier (after its
+// stores) instead of two; a stage that also replaces the halo keeps the barrier before its stores.
+// (sched_group_barrier interleaving of the fragment reads with the MFMAs measured 8-13 % slower.)
 template <typename T, int BN, bool WU = false, bool WDB = false>
 __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kernel(GemmArgs g, int upb) {
   using L = Brick2Layout<T>;
@@ -2524,7 +2525,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
       mmseg::note_kernel("conv3_brick3_kernel<BN32>");
       if (knob("MMSEG_BRICK3_WU", 0))
         hipLaunchKernelGGL((conv3_brick3_kernel<T, 32, true>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
-      else if (knob("MMSEG_BRICK3_WDB", 1))
+      else if (knob("MMSEG_BRICK3_WDB", 0))
         hipLaunchKernelGGL((conv3_brick3_kernel<T, 32, false, true>), dim3(ceil_div(units, upb)), block, 0, s, g,
                            upb);
       else
