@@ -33,7 +33,7 @@ PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
 
 
-def make_config(model, batch, dtype, out_channels=6, modalities=("CT", "PET"), size=96):
+def make_config(model, batch, dtype, out_channels=6, modalities=("CT", "PET"), size=96, loss="dice_ce"):
     backbone = {"features": [32, 64, 128, 256, 512], "norm": "instance"}
     if model == "swin_unetr":     # config c4: SwinUNETR feature_size 48 (swin_unetr.py:180-200 defaults otherwise)
         backbone = {"img_size": [size] * 3, "feature_size": 48}
@@ -46,7 +46,8 @@ def make_config(model, batch, dtype, out_channels=6, modalities=("CT", "PET"), s
         "training": {"epochs": 1, "batch_size": batch, "accumulation_steps": 1,
                      "optimizer": {"name": "adamw", "lr": 1e-4, "weight_decay": 1e-5, "betas": [0.9, 0.999]},
                      "scheduler": {"name": "none"},
-                     "loss": {"name": "dice_ce", "dice_weight": 0.5, "ce_weight": 0.5, "class_weights": None},
+                     "loss": {"name": loss, "dice_weight": 0.5, "ce_weight": 0.5, "class_weights": None,
+                              "tversky_alpha": 0.5, "tversky_beta": 0.5},
                      "checkpoint": {"save_last": False, "save_best": False}},
         "hardware": {"device": "cuda", "mixed_precision": dtype == "bf16",
                      "engine_dtype": "bfloat16" if dtype == "bf16" else "float32"},
@@ -106,6 +107,8 @@ def main():
     ap.add_argument("--batch", type=int, default=2, help="per-GPU batch")
     ap.add_argument("--size", type=int, default=96)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--modalities", default="CT,PET", help="c5: CT,PET,MRI")
+    ap.add_argument("--loss", default="dice_ce", choices=["dice_ce", "tversky"], help="c5: tversky")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--timer-steps", type=int, default=3, help="extra steps timed per kernel family (roofline)")
@@ -124,11 +127,12 @@ def main():
     rank, world = ddp.rank(), ddp.world()
     n_gpus = world
 
-    cfg = make_config(args.model, args.batch, args.dtype, size=args.size)
+    mods = args.modalities.split(",")
+    cfg = make_config(args.model, args.batch, args.dtype, size=args.size, modalities=mods, loss=args.loss)
     torch.manual_seed(42)
     model = build_model(cfg)
     trainer = Trainer(cfg, model)
-    batches = device_batches(4, args.batch, args.size, 6, ["CT", "PET"], dev, seed=1234 + 1000 * rank)
+    batches = device_batches(4, args.batch, args.size, 6, mods, dev, seed=1234 + 1000 * rank)
 
     def barrier():
         if world > 1:
@@ -193,18 +197,20 @@ def main():
                     "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1) if v["ms"] > 0 else None}
                 for k, v in sorted(fam.items(), key=lambda kv: -kv[1]["ms"])}
     cpu = None
-    if n_gpus == 1 and not args.no_cpu_baseline and args.model != "swin_unetr":
-        cpu = cpu_baseline(args.model, args.batch, args.size, 6, ["CT", "PET"], args.cpu_threads)
-    workload = {"dual_encoder": "DualEncoder fusion=cross_attention (mean, dual_encoder.py:193-195) CT+PET",
-                "unet": "UNet3D early_fusion 2-ch",
-                "swin_unetr": "SwinUNETR feature_size 48 (MONAI architecture; parity vs MONAI unpinned) CT+PET"}[
+    if (n_gpus == 1 and not args.no_cpu_baseline and args.model != "swin_unetr" and len(mods) == 2
+            and args.loss == "dice_ce"):
+        cpu = cpu_baseline(args.model, args.batch, args.size, 6, mods, args.cpu_threads)
+    workload = {"dual_encoder": "DualEncoder fusion=cross_attention (mean, dual_encoder.py:193-195)",
+                "unet": "UNet3D early_fusion",
+                "swin_unetr": "SwinUNETR feature_size 48 (MONAI architecture; parity vs MONAI unpinned)"}[
         args.model]
     out = {
-        "metric": f"{args.size}^3 2-modality patches/sec/node (train step)",
+        "metric": f"{args.size}^3 {len(mods)}-modality patches/sec/node (train step)",
         "value": round(value, 3), "unit": "patches/s", "n_gpus": n_gpus, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (seeded CT/PET phantoms, pre-staged in HBM)",
-        "config": {"workload": f"{workload} {args.size}^3, 6 classes, DiceCE, AdamW, per-GPU batch {args.batch}",
+        "vs_baseline": None, "dtype": args.dtype, "data": f"synthetic (seeded {'/'.join(mods)} phantoms, pre-staged in HBM)",
+        "config": {"workload": f"{workload} {args.size}^3, modalities {'+'.join(mods)}, 6 classes, "
+                               f"{'DiceCE' if args.loss == 'dice_ce' else 'Tversky'}, AdamW, per-GPU batch {args.batch}",
                    "model": args.model, "global_batch": args.batch * n_gpus, "patch": [args.size] * 3,
                    "parallelism": f"dp{n_gpus}"},
         "loss": round(loss_val, 5),
