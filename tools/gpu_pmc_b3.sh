@@ -1,0 +1,13 @@
+#!/bin/bash
+# SQ counter passes on the brick3 forward (96^3, 32 -> 32): where the non-MFMA cycles go.
+cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/${1:-pb}
+mkdir -p $O
+CB="python3 $R/tools/convbench.py --shape 2,96,32,32 --only fwd --iters 5"
+timeout -k 10 120 $CB > $O/conv.log 2>&1 || exit 1
+tail -1 $O/conv.log
+timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU --output-format csv -d $O/p1 -o pmc -- $CB > $O/p1.log 2>&1 || { tail -5 $O/p1.log; exit 1; }
+timeout -s KILL 90 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM --output-format csv -d $O/p2 -o pmc -- $CB > $O/p2.log 2>&1 || { tail -5 $O/p2.log; exit 1; }
+timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d $O/p3 -o pmc -- $CB > $O/p3.log 2>&1 || { tail -5 $O/p3.log; exit 1; }
+echo done
