@@ -21,7 +21,6 @@ import platform
 import sys
 import time
 
-import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -208,7 +207,8 @@ def main():
         "metric": f"{args.size}^3 {len(mods)}-modality patches/sec/node (train step)",
         "value": round(value, 3), "unit": "patches/s", "n_gpus": n_gpus, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": args.dtype, "data": f"synthetic (seeded {'/'.join(mods)} phantoms, pre-staged in HBM)",
+        "vs_baseline": None, "dtype": args.dtype,
+        "data": f"synthetic (seeded {'/'.join(mods)} phantoms, pre-staged in HBM)",
         "config": {"workload": f"{workload} {args.size}^3, modalities {'+'.join(mods)}, 6 classes, "
                                f"{'DiceCE' if args.loss == 'dice_ce' else 'Tversky'}, AdamW, per-GPU batch {args.batch}",
                    "model": args.model, "global_batch": args.batch * n_gpus, "patch": [args.size] * 3,

@@ -24,7 +24,7 @@ norm_pool.hip, the LeakyReLU residual tail (mmseg_res_apply / _lrelu_bwd).
 from __future__ import annotations
 
 import math
-from typing import Dict, List, Optional, Tuple
+from typing import Optional, Tuple
 
 import numpy as np
 import torch

@@ -24,7 +24,7 @@ MONAI quirks kept on purpose (both are what MONAI 1.3 computes):
 """
 from __future__ import annotations
 
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List
 
 import torch
 import torch.nn.functional as F
