@@ -733,7 +733,11 @@ __device__ __forceinline__ void buf_load_v8<float>(V8<float>& v, __amdgpu_buffer
 // for BN32 bf16; 2 blocks/CU still fit), so a stage that only swaps weights needs one barrier (after its
 // stores) instead of two; a stage that also replaces the halo keeps the barrier before its stores.
 // (sched_group_barrier interleaving of the fragment reads with the MFMAs measured 8-13 % slower.)
-template <typename T, int BN, bool WU = false, bool WDB = false>
+// XP: the next halo chunk (or the next unit's first chunk) is loaded into registers at the FIRST stage of
+// the current chunk instead of its last, so its HBM latency is hidden behind three stages of MFMAs instead
+// of one (the registers are free from the current chunk's LDS store on; no extra VGPRs).  MMSEG_BRICK3_XP=1;
+// measured 4 % slower on the bench (q13), so off.
+template <typename T, int BN, bool WU = false, bool WDB = false, bool XP = false>
 __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kernel(GemmArgs g, int upb) {
   using L = Brick2Layout<T>;
   constexpr int BZ = 4, HZ = BZ + 2;
@@ -888,7 +892,17 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kern
       const bool more = !last || unext;
       const int sn = last ? 0 : st + 1;
       const int cn = sn / 3, kzn = sn - cn * 3;
-      if (more) {
+      if constexpr (XP) {
+        if (kz == 0) {
+          if (c + 1 < nchunk) {
+            load_x(c + 1);
+          } else if (unext) {
+            set_x(nxt);
+            load_x(0);
+          }
+        }
+        if (more) load_w(last ? nxt.n0 : cur.n0, cn, kzn);
+      } else if (more) {
         if (last) set_x(nxt);
         load_w(last ? nxt.n0 : cur.n0, cn, kzn);
         if (kzn == 0) load_x(cn);
@@ -2525,6 +2539,9 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
       mmseg::note_kernel("conv3_brick3_kernel<BN32>");
       if (knob("MMSEG_BRICK3_WU", 0))
         hipLaunchKernelGGL((conv3_brick3_kernel<T, 32, true>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
+      else if (knob("MMSEG_BRICK3_XP", 0))
+        hipLaunchKernelGGL((conv3_brick3_kernel<T, 32, false, false, true>), dim3(ceil_div(units, upb)), block, 0, s,
+                           g, upb);
       else if (knob("MMSEG_BRICK3_WDB", 0))
         hipLaunchKernelGGL((conv3_brick3_kernel<T, 32, false, true>), dim3(ceil_div(units, upb)), block, 0, s, g,
                            upb);
