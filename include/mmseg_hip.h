@@ -317,7 +317,9 @@ int mmseg_head_bwd(const void* x, int ldx, int Cin, const float* W, const float*
                    const float* dlogits, void* dx, int lddx, float* gW, float* gb, float* ws, int accumulate, int dtype,
                    void* stream);
 /* Fused softmax + Dice/Tversky + CE statistics and loss (losses.py:39-80, 160-185,
- * 216-228).  type 0: dice_w*Dice + ce_w*CE ; type 1: dice_w*Tversky + ce_w*CE. */
+ * 216-228).  type 0: dice_w*Dice + ce_w*CE ; type 1: dice_w*Tversky + ce_w*CE ; type 2: FocalLoss
+ * (losses.py:83-125: mean of (1 - exp(-ce_i))^gamma * ce_i with ce_i the class-weighted voxel CE; gamma is
+ * passed as alpha, dice_w = 0, ce_w = 1). */
 long long mmseg_loss_ws_floats(int N, int C, long long V);
 int mmseg_loss_fwd(const float* logits, const void* labels, int label_bytes, int N, int C, long long V, int type,
                    float dice_w, float ce_w, float smooth, float alpha, float beta, int include_bg,

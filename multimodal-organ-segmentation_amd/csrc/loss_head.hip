@@ -220,7 +220,7 @@ __global__ void head_wgrad_reduce(const float* __restrict__ part, int nblk, int 
 
 // ----------------------------------------------------------------- losses
 struct LossCfg {
-  int type;             // 0 = dice/ce family, 1 = tversky
+  int type;             // 0 = dice/ce family, 1 = tversky, 2 = focal (alpha = gamma; region weight 0)
   float dice_w, ce_w;   // weights of the region term and the CE term
   float smooth, alpha, beta;
   int include_bg;
@@ -269,8 +269,15 @@ __global__ void loss_stats_kernel(const float* __restrict__ logits, const LT* __
         }
       }
     const float wy = cfg.cw ? cfg.cw[y] : 1.f;
-    ce = fmaf(wy, lse - zy, ce);
-    cden += wy;
+    if (cfg.type == 2) {   // focal (losses.py:116-121): (1 - exp(-ce_i))^gamma * ce_i, plain mean over voxels
+      const float cei = wy * (lse - zy);
+      const float pt = expf(-cei);
+      ce += powf(1.f - pt, cfg.alpha) * cei;
+      cden += 1.f;
+    } else {
+      ce = fmaf(wy, lse - zy, ce);
+      cden += wy;
+    }
   }
   __shared__ float red[4][3 * CMAX + 2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -384,7 +391,17 @@ __global__ void loss_bwd_kernel(const float* __restrict__ logits, const LT* __re
       }
     const float inv = 1.f / se;
     const int y = (int)labels[i];
-    const float wy = cfg.cw ? cfg.cw[y] : 1.f;
+    float wy = cfg.cw ? cfg.cw[y] : 1.f;
+    if (cfg.type == 2) {   // focal: d f_i / d ce_i = gamma (1-pt)^(gamma-1) pt ce_i + (1-pt)^gamma, ce_i = w_y (lse - z_y)
+      float zy = 0.f;
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c)
+        if (c < C && c == y) zy = z[c];
+      const float cei = wy * (mx + logf(se) - zy);
+      const float pt = expf(-cei), q = 1.f - pt, gm = cfg.alpha;
+      const float dfd = (q > 0.f ? gm * powf(q, gm - 1.f) * pt * cei : 0.f) + powf(q, gm);
+      wy *= dfd;
+    }
     float dp[CMAX];
     float s = 0.f;
 #pragma unroll

@@ -16,7 +16,7 @@ import torch.nn as nn
 
 from .._lib import lib, ptr, stream_handle
 
-TYPE_DICE, TYPE_TVERSKY = 0, 1
+TYPE_DICE, TYPE_TVERSKY, TYPE_FOCAL = 0, 1, 2
 
 
 class _SegLoss(torch.autograd.Function):
@@ -103,6 +103,20 @@ class TverskyLoss(_HipLoss):
                     include_bg=True)
 
 
+class FocalLoss(_HipLoss):
+    """ce_i = CE(pred, target, weight=alpha, reduction='none'), (1 - exp(-ce_i))^gamma * ce_i, mean over voxels
+    (reference losses.py:83-125); gamma rides in the kernel's alpha slot (loss type 2)."""
+
+    def __init__(self, alpha: Optional[torch.Tensor] = None, gamma: float = 2.0, reduction: str = "mean"):
+        super().__init__()
+        self.alpha, self.gamma, self.reduction = alpha, gamma, reduction
+        self.class_weights = alpha
+
+    def _spec(self):
+        return dict(type=TYPE_FOCAL, dice_w=0.0, ce_w=1.0, smooth=1.0, alpha=float(self.gamma), beta=0.0,
+                    include_bg=True)
+
+
 class DiceCELoss(_HipLoss):
     """dice_weight * DiceLoss + ce_weight * CrossEntropy, fused (reference losses.py:188-228)."""
 
@@ -131,7 +145,7 @@ def get_loss(config: Dict[str, Any]) -> nn.Module:
     if name == "dice_ce":
         return DiceCELoss(dice_weight=lc.get("dice_weight", 0.5), ce_weight=lc.get("ce_weight", 0.5), class_weights=cw)
     if name == "focal":
-        raise NotImplementedError("FocalLoss is not on the HIP path (no BASELINE config uses it; SURVEY §2.1)")
+        return FocalLoss(alpha=cw)
     if name == "tversky":
         return TverskyLoss(alpha=lc.get("tversky_alpha", 0.5), beta=lc.get("tversky_beta", 0.5))
     return DiceCELoss()

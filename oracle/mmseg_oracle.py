@@ -308,6 +308,13 @@ def tversky_loss(pred: Tensor, target: Tensor, alpha: float = 0.5, beta: float =
     return (1.0 - (tp + smooth) / (tp + alpha * fp + beta * fn + smooth)).mean()
 
 
+def focal_loss(pred: Tensor, target: Tensor, alpha: Optional[Tensor] = None, gamma: float = 2.0) -> Tensor:
+    """FocalLoss.forward (reference losses.py:107-125): class-weighted voxel CE, (1 - exp(-ce))^gamma * ce, mean."""
+    ce = F.cross_entropy(pred, target, weight=alpha, reduction="none")
+    pt = torch.exp(-ce)
+    return ((1 - pt) ** gamma * ce).mean()
+
+
 def dice_counts(pred_idx: np.ndarray, target_idx: np.ndarray, num_classes: int):
     """Per-class integer intersection/union counts of DiceMetric.update (reference metrics.py:42-67)."""
     p = np.asarray(pred_idx).reshape(-1)

@@ -144,6 +144,8 @@ def loss_case():
             "ce": torch.nn.CrossEntropyLoss(),
             "tversky": losses.TverskyLoss(),
             "tversky_37": losses.TverskyLoss(alpha=0.3, beta=0.7),
+            "focal": losses.FocalLoss(),
+            "focal_w": losses.FocalLoss(alpha=cw),
         }
         for name, mod in mods.items():
             if logits.grad is not None:

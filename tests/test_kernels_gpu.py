@@ -266,14 +266,15 @@ def test_head(dev, dtype):
 
 @pytest.mark.parametrize("C", [3, 6, 7])
 def test_losses_vs_reference_golden(dev, C):
-    from mmseg_amd.trainer.losses import CrossEntropyLoss, DiceCELoss, DiceLoss, TverskyLoss
+    from mmseg_amd.trainer.losses import CrossEntropyLoss, DiceCELoss, DiceLoss, FocalLoss, TverskyLoss
     g = golden("losses")
     logits = torch.from_numpy(g[f"logits_C{C}"]).to(dev)
     labels = torch.from_numpy(g[f"labels_C{C}"]).to(dev)
     cw = torch.from_numpy(g[f"cw_C{C}"])
     mods = {"dicece": DiceCELoss(), "dicece_w": DiceCELoss(0.3, 0.7, class_weights=cw), "dice": DiceLoss(),
             "dice_nobg": DiceLoss(include_background=False), "ce": CrossEntropyLoss(),
-            "tversky": TverskyLoss(), "tversky_37": TverskyLoss(alpha=0.3, beta=0.7)}
+            "tversky": TverskyLoss(), "tversky_37": TverskyLoss(alpha=0.3, beta=0.7), "focal": FocalLoss(),
+            "focal_w": FocalLoss(alpha=cw)}
     for name, mod in mods.items():
         lg = logits.clone().requires_grad_(True)
         loss = mod(lg, labels)

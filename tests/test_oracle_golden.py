@@ -72,7 +72,8 @@ def test_oracle_losses(C):
     cw = torch.from_numpy(g[f"cw_C{C}"])
     fns = {"dicece": O.dice_ce_loss, "dicece_w": lambda a, b: O.dice_ce_loss(a, b, 0.3, 0.7, cw),
            "dice": O.dice_loss, "dice_nobg": lambda a, b: O.dice_loss(a, b, include_background=False),
-           "ce": O.ce_loss, "tversky": O.tversky_loss, "tversky_37": lambda a, b: O.tversky_loss(a, b, 0.3, 0.7)}
+           "ce": O.ce_loss, "tversky": O.tversky_loss, "tversky_37": lambda a, b: O.tversky_loss(a, b, 0.3, 0.7),
+           "focal": O.focal_loss, "focal_w": lambda a, b: O.focal_loss(a, b, cw)}
     for name, fn in fns.items():
         lg = logits.clone().requires_grad_(True)
         l = fn(lg, labels)
