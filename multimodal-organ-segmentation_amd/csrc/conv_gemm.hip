@@ -1217,7 +1217,9 @@ Conv3Plan plan_conv3(int M, int Ncols, int cin, int D, int H, int W, int lda, in
   Conv3Plan p{0, 0, 0, 0, 1, 32};
   const int brick = knob("MMSEG_BRICK", 2);
   const bool base_ok = cin % CK == 0 && lda % 8 == 0 && ldo % 8 == 0 && Ncols % 32 == 0;
-  if (brick == 2 && base_ok && D % 4 == 0 && H % B2_Y == 0 && W % B2_X == 0) {
+  // 48-column multiples (SwinUNETR's feature_size 48) run the brick2 kernel with 48-column tiles
+  const bool ok48 = cin % CK == 0 && lda % 8 == 0 && ldo % 8 == 0 && Ncols % 48 == 0 && knob("MMSEG_BRICK2_BN48", 1);
+  if (brick == 2 && (base_ok || ok48) && D % 4 == 0 && H % B2_Y == 0 && W % B2_X == 0) {
     p.kind = 1;
     return p;
   }
@@ -2528,7 +2530,10 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     // persistent: at most one wave of resident blocks (2 per CU), each over a contiguous range of units
     const int maxblk = knob("MMSEG_BRICK3_BLOCKS", 512);
     // (BN64 stays on v2 unless asked for: at 256 VGPRs the v3 instantiation spills and measured no faster)
-    if (v3 && knob("MMSEG_BRICK3_BN64", 0) && g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
+    if (g.Ncols % 32 != 0) {    // a multiple of 48 (plan_conv3)
+      mmseg::note_kernel("conv3_brick2_kernel<BN48,ZW1>");
+      hipLaunchKernelGGL((conv3_brick2_kernel<T, 48, 1>), dim3(nb1 * (g.Ncols / 48)), block, 0, s, g);
+    } else if (v3 && knob("MMSEG_BRICK3_BN64", 0) && g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
       const int units = nb1 * (g.Ncols / 64);
       const int upb = maxblk > 0 ? ceil_div(units, maxblk) : 1;
       mmseg::note_kernel("conv3_brick3_kernel<BN64>");

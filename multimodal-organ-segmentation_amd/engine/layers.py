@@ -146,8 +146,10 @@ class Conv3:
         if pad_cols and conv.bias is not None:
             raise ValueError("pad_cols: bias-free convs only")
         self.pad_cols = pad_cols
-        self.ncols_f = self.Cop if pad_cols else self.Co
-        self.ncols_d = self.Cip if pad_cols else self.Ci
+        # column counts the brick kernels take as they are (32- or 48-column tiles) stay unpadded
+        tile_ok = lambda c: c % 32 == 0 or c % 48 == 0   # noqa: E731
+        self.ncols_f = self.Cop if pad_cols and not tile_ok(self.Co) else self.Co
+        self.ncols_d = self.Cip if pad_cols and not tile_ok(self.Ci) else self.Ci
         self.cpg_shift = pow2_shift(self.Cip // 8)
         self.KG = 27 * self.Cip // 8
         self.KGp = round_up(self.KG, 4)

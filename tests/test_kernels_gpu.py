@@ -406,3 +406,36 @@ def test_conv3_fused_instnorm_stats(dev, dtype, knobs, cin, cout, shape, monkeyp
     r_ref = 1.0 / torch.sqrt(y.var(-1, unbiased=False) + 1e-5)
     assert rel(mean.cpu().reshape(N, cout), m_ref) < 1e-5
     assert rel(rstd.cpu().reshape(N, cout), r_ref) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("cin,cout,shape", [(48, 48, (1, 8, 8, 16)), (96, 48, (2, 4, 8, 8)), (48, 96, (1, 4, 8, 8)),
+                                            (24, 24, (1, 4, 8, 8)), (48, 48, (1, 6, 6, 6))])
+def test_conv3_channel_padded(dev, dtype, cin, cout, shape):
+    """SwinUNETR's bias-free convs over channel-padded buffers (Conv3 cin_pad / cout_pad / pad_cols): 48-column
+    brick tiles, padded K groups with zero weights (pack modes 0 / 6), staged Co-padded weight gradient."""
+    from mmseg_amd.engine.swin import cpad
+    torch.manual_seed(cin * 3 + cout)
+    conv = nn.Conv3d(cin, cout, 3, padding=1, bias=False).to(dev)
+    rt = Runtime(dev, dtype)
+    flat = FlatParams(list(conv.parameters()))
+    cip, cop = cpad(cin), cpad(cout)
+    layer = Conv3(rt, conv, flat, cin_pad=cip, cout_pad=cop, pad_cols=True)
+    N, D, H, W = shape
+    x = torch.randn(N, cin, D, H, W, device=dev)
+    xa = Act(to_ndhwc(x, dtype, ld=cip), 0, cin, cip, N, D, H, W)
+    ya = Act(torch.zeros(N * D * H * W * cop, dtype=dtype, device=dev), 0, cout, cop, N, D, H, W)
+    layer.pack()
+    layer.fwd(xa, ya)
+    xd = _q(x, dtype).requires_grad_(True)
+    wd = _q(conv.weight, dtype).requires_grad_(True)
+    ref = F.conv3d(xd, wd, padding=1)
+    assert rel(from_ndhwc(ya.buf, N, cout, D, H, W, ld=cop), ref) < TOL[dtype]
+    assert from_ndhwc(ya.buf, N, cop, D, H, W, ld=cop)[:, cout:].abs().max().item() == 0.0   # padding stays zero
+    dy = torch.randn(ref.shape, device=dev)
+    dya = Act(to_ndhwc(dy, dtype, ld=cop), 0, cout, cop, N, D, H, W)
+    dxa = Act(torch.zeros(N * D * H * W * cip, dtype=dtype, device=dev), 0, cin, cip, N, D, H, W)
+    layer.bwd(xa, dya, dxa, accumulate=False)
+    (ref * _q(dy, dtype)).sum().backward()
+    assert rel(from_ndhwc(dxa.buf, N, cin, D, H, W, ld=cip), xd.grad) < TOL[dtype]
+    assert rel(flat.grad(conv.weight), wd.grad) < GTOL[dtype]
