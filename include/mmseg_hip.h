@@ -100,6 +100,13 @@ int mmseg_conv3_stats_bricks(int M, int Ncols, int Cpad, int KG, int cpg_shift, 
 int mmseg_conv_gemm_stats(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
                           float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H,
                           int W, int ksplit, float* stats_part, int dtype, void* stream);
+/* mmseg_conv_gemm_stats whose A source holds only cin_real real channels (the rest are channel padding with zero
+ * packed weights, e.g. SwinUNETR's 96 / 192 / 384 / 768-channel tensors stored as 128 / 256 / 512 / 1024): the CONV3
+ * brick kernels skip the 32-channel K chunks wholly past cin_real.  cin_real = 0: all channels are real.  Replaces
+ * the same Conv3d call sites as mmseg_conv_gemm (monai SwinUNETR's UnetResBlock convs). */
+int mmseg_conv_gemm_ex(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
+                       float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H,
+                       int W, int ksplit, float* stats_part, int cin_real, int dtype, void* stream);
 int mmseg_instnorm_stats_bricks(const float* part, int N, int C, int nb, int cnt, float eps, float* mean, int mean_ld,
                                 float* rstd, void* stream);
 

@@ -46,7 +46,16 @@ struct GemmArgs {
   int ksplit, kg_per_split;  // k-groups per split (multiple of 4)
   int swz;                   // XCD-aware block remap
   float* stats;              // brick kernels, ksplit == 1: per-brick InstanceNorm partials (mean, M2), or null
+  int kchunks;               // CONV3 brick kernels: 32-channel input chunks holding real channels (0 = all);
+                             // the packed weights of the rest are zero (channel-padded K side), so they are skipped
 };
+
+// 32-channel K chunks a CONV3 brick kernel iterates: all of the (power-of-two) A source's, or only the
+// leading ones that hold real channels.
+__host__ __device__ __forceinline__ int gemm_nchunk(const GemmArgs& g) {
+  const int n = (8 << g.cpg_shift) / 32;
+  return (g.kchunks > 0 && g.kchunks < n) ? g.kchunks : n;
+}
 
 // Per-brick InstanceNorm statistics of a staged output tile (fused into the
 // brick conv epilogue, so the IN stats pass never re-reads the conv output).
@@ -368,7 +377,7 @@ __global__ __launch_bounds__(256) void conv3_brick_kernel(GemmArgs g) {
   const long long nbase = (long long)n * g.D * HW;
   const int n0 = nt * BN;
   const int cin = 8 << g.cpg_shift;             // channels of the A source
-  const int nchunk = cin / CK;
+  const int nchunk = gemm_nchunk(g);
   const int nstage = nchunk * 3;
 
   V8<T> xr[X_PER], wr[W_PER];
@@ -547,7 +556,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kern
   const long long nbase = (long long)n * g.D * HW;
   const int n0 = nt * BN;
   const int cin = 8 << g.cpg_shift;
-  const int nchunk = cin / CK;
+  const int nchunk = gemm_nchunk(g);
   const int nstage = nchunk * 3;
 
   V8<T> xr[X_PER], wr[W_PER];
@@ -767,7 +776,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kern
   if (u_begin >= u_end) return;
   const int HW = g.H * g.W;
   const int cin = 8 << g.cpg_shift;
-  const int nchunk = cin / CK;
+  const int nchunk = gemm_nchunk(g);
   const int nstage = nchunk * 3;
   const int ldb = g.lda * (int)sizeof(T);            // bytes per voxel
   const int vox_per_n = g.D * HW;
@@ -1027,7 +1036,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kern
   const long long nbase = (long long)n * g.D * HW;
   const int n0 = nt * BN;
   const int cin = 8 << g.cpg_shift;
-  const int nchunk = cin / CK;
+  const int nchunk = gemm_nchunk(g);
   const int cps = (nchunk + g.ksplit - 1) / g.ksplit;
   const int c_begin = ks * cps;
   const int c_end = c_begin + cps < nchunk ? c_begin + cps : nchunk;
@@ -1318,7 +1327,13 @@ struct WgradArgs {
   float* grad;
   float* bias_grad;
   int accumulate;
+  int kchunks;               // CONV3 brick kernels: 32-channel chunks of x holding real channels (0 = all)
 };
+
+__host__ __device__ __forceinline__ int wgrad_nchunk(int cpg_shift, int kchunks) {
+  const int n = (8 << cpg_shift) / 32;
+  return (kchunks > 0 && kchunks < n) ? kchunks : n;
+}
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef short v8i16 __attribute__((ext_vector_type(8)));
@@ -1548,7 +1563,7 @@ __global__ __launch_bounds__(256) void wgrad_brick_kernel(WgradArgs g) {
   const T* X = reinterpret_cast<const T*>(g.b);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cin = 8 << g.cpg_shift;
-  const int nchunk = cin / CK, rt_n = g.Ca / 32;
+  const int nchunk = wgrad_nchunk(g.cpg_shift, g.kchunks), rt_n = g.Ca / 32;
   const int tile = blockIdx.x;
   const int ct = tile % nchunk, rt = (tile / nchunk) % rt_n, ks = tile / (nchunk * rt_n);
   const int bz_n = g.D / BRK_Z, by_n = g.H / BRK_Y, bx_n = g.W / BRK_X;
@@ -1818,7 +1833,7 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
   const T* X = reinterpret_cast<const T*>(g.b);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cin = 8 << g.cpg_shift;
-  const int nchunk = cin / CK, rt_n = g.Ca / CO;
+  const int nchunk = wgrad_nchunk(g.cpg_shift, g.kchunks), rt_n = g.Ca / CO;
   const int tile = blockIdx.x;
   const int ct = tile % nchunk, rt = (tile / nchunk) % rt_n, ks = tile / (nchunk * rt_n);
   const int bz_n = g.D / BRK_Z, by_n = g.H / BRK_Y, bx_n = g.W / BRK_X;
@@ -1990,7 +2005,7 @@ __global__ __launch_bounds__(512) void wgrad_brickr_kernel(WgradArgs g, int bz, 
   const T* X = reinterpret_cast<const T*>(g.b);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cin = 8 << g.cpg_shift;
-  const int nchunk = cin / CK, rt_n = g.Ca / CO;
+  const int nchunk = wgrad_nchunk(g.cpg_shift, g.kchunks), rt_n = g.Ca / CO;
   const int tile = blockIdx.x;
   const int ct = tile % nchunk, rt = (tile / nchunk) % rt_n, ks = tile / (nchunk * rt_n);
   const int HX = bx + 2, HY = by + 2, HZ = bz + 2;
@@ -2496,7 +2511,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
                                             : Conv3Plan{0, 0, 0, 0, 1, 32};
   if (plan.kind == 2) {
     const int nb = (g.M / (g.D * g.H * g.W)) * (g.D / plan.bz) * (g.H / plan.by) * (g.W / plan.bx);
-    const int nchunk = (8 << g.cpg_shift) / CK;
+    const int nchunk = gemm_nchunk(g);
     if (g.ksplit > nchunk) g.ksplit = nchunk;
     const int cps = (nchunk + g.ksplit - 1) / g.ksplit;
     g.ksplit = (nchunk + cps - 1) / cps;
@@ -2619,31 +2634,29 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
   dim3 block(256);
   if constexpr (sizeof(T) == 2) {
     if (MODE == MODE_CONV3 && g.brick == 3) {
-      const int cin = 8 << g.cpg_shift;
       const WBrick wb = plan_wgrad_brickr(g.D, g.H, g.W);
       if (g.Ca % 64 == 0) {
-        dim3 grid((cin / CK) * (g.Ca / 64) * g.ksplit);
+        dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 64) * g.ksplit);
         mmseg::note_kernel("wgrad_brickr_kernel<CO64>");
         hipLaunchKernelGGL((wgrad_brickr_kernel<T, 4>), grid, dim3(512), 0, s, g, wb.bz, wb.by, wb.bx);
       } else {
-        dim3 grid((cin / CK) * (g.Ca / 32) * g.ksplit);
+        dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 32) * g.ksplit);
         mmseg::note_kernel("wgrad_brickr_kernel<CO32>");
         hipLaunchKernelGGL((wgrad_brickr_kernel<T, 2>), grid, dim3(512), 0, s, g, wb.bz, wb.by, wb.bx);
       }
       return mmseg::check_launch("wgrad_brickr");
     }
     if (MODE == MODE_CONV3 && g.brick == 2) {
-      const int cin = 8 << g.cpg_shift;
       const bool v3 = knob("MMSEG_WGRAD_V3", 1) != 0;
       if (g.Ca % 64 == 0) {
-        dim3 grid((cin / CK) * (g.Ca / 64) * g.ksplit);
+        dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 64) * g.ksplit);
         mmseg::note_kernel(v3 ? "wgrad_brick2_kernel<CO64,V3>" : "wgrad_brick2_kernel<CO64>");
         if (v3)
           hipLaunchKernelGGL((wgrad_brick2_kernel<T, 4, 3>), grid, dim3(512), 0, s, g);
         else
           hipLaunchKernelGGL((wgrad_brick2_kernel<T, 4, 2>), grid, dim3(512), 0, s, g);
       } else {
-        dim3 grid((cin / CK) * (g.Ca / 32) * g.ksplit);
+        dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 32) * g.ksplit);
         mmseg::note_kernel(v3 ? "wgrad_brick2_kernel<CO32,V3>" : "wgrad_brick2_kernel<CO32>");
         if (v3)
           hipLaunchKernelGGL((wgrad_brick2_kernel<T, 2, 3>), grid, dim3(512), 0, s, g);
@@ -2654,8 +2667,7 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
     }
   }
   if (MODE == MODE_CONV3 && g.brick) {
-    const int cin = 8 << g.cpg_shift;
-    dim3 grid((cin / CK) * (g.Ca / 32) * g.ksplit);
+    dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 32) * g.ksplit);
     mmseg::note_kernel("wgrad_brick_kernel");
     hipLaunchKernelGGL((wgrad_brick_kernel<T>), grid, block, 0, s, g);
     return mmseg::check_launch("wgrad_brick");
@@ -2698,8 +2710,9 @@ int wgrad_brick_ok(int Ca, int cpg_shift, int D, int H, int W, int lda, int ldb,
 
 // Split count of the CONV3 brick wgrad: enough blocks to fill the chip, capped by
 // the caller's workspace (cap) and by one brick per split.
-int brick_wgrad_splits(long long V, int cap, int Ca, int cpg_shift, int kind, int D, int H, int W) {
-  const int nchunk = (8 << cpg_shift) / CK;
+int brick_wgrad_splits(long long V, int cap, int Ca, int cpg_shift, int kind, int D, int H, int W,
+                       int kchunks = 0) {
+  const int nchunk = wgrad_nchunk(cpg_shift, kchunks);
   const int tiles = nchunk * (Ca / ((kind >= 2 && Ca % 64 == 0) ? 64 : 32));
   // v2 / runtime-brick kernels: one wave of resident blocks (256 CUs x blocks per CU: 2 for the 32-co brick2
   // kernel, 1 for the 64-co and runtime-brick kernels, whose stage buffers take > 80 KB of LDS), never more:
@@ -2729,6 +2742,10 @@ int mmseg_wgrad_splits_impl(long long V, int ksplit) {
   return (int)((V + vps - 1) / vps);
 }
 
+// Real 32-channel chunks of a channel-padded x (Ci < Cip), 0 = all (the brick wgrad kernels skip the rest; the
+// split reduction never reads the skipped columns' partials into the gradient).
+int wgrad_kchunks(int Cip, int Ci) { return (Ci < Cip && knob("MMSEG_KCHUNKS", 1)) ? (Ci + 31) / 32 : 0; }
+
 // CONV3 weight-gradient plan (mmseg_conv3_wgrad): kernel kind (wgrad_brick_ok), split count, whether the
 // kernel writes the torch-layout gradient itself (brick2 / brickr, one split, unpadded input channels),
 // and the workspace (floats) of the split partials + bias partials otherwise.
@@ -2746,7 +2763,7 @@ Conv3WgradPlan plan_conv3_wgrad(long long V, int Co, int Cip, int Ci, int cpg_sh
   if (cap < 1) cap = 1;
   p.kind = wgrad_brick_ok(Co, cpg_shift, D, H, W, lda, ldb, dtype);
   if (p.kind) {
-    p.ksplit = brick_wgrad_splits(V, cap, Co, cpg_shift, p.kind, D, H, W);
+    p.ksplit = brick_wgrad_splits(V, cap, Co, cpg_shift, p.kind, D, H, W, wgrad_kchunks(Cip, Ci));
   } else {
     const int bn = knob("MMSEG_WGRAD_BN", 64);
     const long long tiles = ((ncols + bn - 1) / bn) * ((Co + (Co % 64 == 0 ? 63 : 31)) / (Co % 64 == 0 ? 64 : 32));
@@ -2856,11 +2873,26 @@ int mmseg_conv_gemm(const void* a, int lda, const void* wpacked, const float* bi
                                W, ksplit, nullptr, dtype, stream);
 }
 
+int mmseg_conv_gemm_ex(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
+                       float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H,
+                       int W, int ksplit, float* stats_part, int cin_real, int dtype, void* stream);
+
 // mmseg_conv_gemm + per-brick InstanceNorm partials of the output (stats_part:
 // [N][bricks per sample][Ncols][2] floats, see mmseg_conv3_stats_bricks).
 int mmseg_conv_gemm_stats(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
                           float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H,
                           int W, int ksplit, float* stats_part, int dtype, void* stream) {
+  return mmseg_conv_gemm_ex(a, lda, wpacked, bias, out, ldo, splitk_ws, mode, M, Ncols, Cpad, KG, cpg_shift, D, H, W,
+                            ksplit, stats_part, 0, dtype, stream);
+}
+
+// mmseg_conv_gemm_stats for an A source whose channels past cin_real are padding (zero weights): the CONV3
+// brick kernels skip the 32-channel chunks wholly past cin_real.  cin_real = 0: every channel is real.
+int mmseg_conv_gemm_ex(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
+                       float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H,
+                       int W, int ksplit, float* stats_part, int cin_real, int dtype, void* stream) {
+  MMSEG_REQUIRE(cin_real >= 0 && cin_real <= (8 << cpg_shift), "conv_gemm: cin_real %d outside [0, %d]", cin_real,
+                8 << cpg_shift);
   MMSEG_REQUIRE(!stats_part || (mode == MODE_CONV3 && ksplit == 1 &&
                                 mmseg_conv3_stats_bricks(M, Ncols, Cpad, KG, cpg_shift, D, H, W, lda, ldo, dtype) > 0),
                 "conv_gemm_stats: fused statistics need a brick kernel without split-K for this shape");
@@ -2873,7 +2905,8 @@ int mmseg_conv_gemm_stats(const void* a, int lda, const void* wpacked, const flo
   int kps = ((ceil_div(KGp, ksplit) + 3) / 4) * 4;
   ksplit = ceil_div(KGp, kps);
   GemmArgs g{a, lda, wpacked, bias, out, ldo, splitk_ws, M, Ncols, Cpad, KG, cpg_shift, D, H, W, ksplit, kps,
-             knob("MMSEG_SWIZZLE", 1), stats_part};
+             knob("MMSEG_SWIZZLE", 1), stats_part,
+             (mode == MODE_CONV3 && knob("MMSEG_KCHUNKS", 1)) ? (cin_real + 31) / 32 : 0};
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16) return launch_gemm_mode<bf16_t>(g, mode, s);
   return launch_gemm_mode<float>(g, mode, s);
@@ -2973,7 +3006,7 @@ int mmseg_conv3_wgrad(const void* dy, int lddy, const void* x, int ldx, float* g
   const long long vps = ((V + p.ksplit - 1) / p.ksplit + 63) / 64 * 64;
   WgradArgs g{dy, lddy, x, ldx, part, p.direct ? bias_grad : bpart, Co, ncols, cpg_shift, V, D, H, W, p.ksplit, vps,
               knob("MMSEG_WGRAD_SWIZZLE", 0), p.kind, p.direct ? grad : nullptr, p.direct ? bias_grad : nullptr,
-              accumulate};
+              accumulate, wgrad_kchunks(Cip, Ci)};
   hipStream_t s = (hipStream_t)stream;
   const int rc = dtype == MMSEG_BF16 ? launch_wgrad<bf16_t, MODE_CONV3>(g, s) : launch_wgrad<float, MODE_CONV3>(g, s);
   if (rc || p.direct) return rc;

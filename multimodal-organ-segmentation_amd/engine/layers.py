@@ -166,6 +166,10 @@ class Conv3:
         # weight gradient over Cop rows (brick kernels need Co % 32 == 0) into a staging [Cop][Ci][27]
         self.wg_stage = (torch.empty(self.Cop * self.Ci * 27, dtype=torch.float32, device=rt.device)
                          if pad_cols and self.Co % 32 and self.Cop % 32 == 0 else None)
+        # real channels of the channel-padded K sides (0 = none padded): the brick kernels skip the
+        # 32-channel chunks past them
+        self.kreal_f = self.Ci if self.Cip > self.Ci else 0
+        self.kreal_d = self.Co if self.Cop > self.Co else 0
 
     def descs(self):
         w = self.conv.weight
@@ -197,9 +201,10 @@ class Conv3:
         if stats_part is not None:
             with TIMER.region(_gemm_name(self.rt, self.Co, "conv3"), flops=2.0 * x.N * x.V * self.Co * 27 * self.Ci,
                               nbytes=_io_bytes(self.rt, x.N * x.V, self.Ci, self.Co, 27 * self.Ci * self.Co)):
-                self.rt.lib.mmseg_conv_gemm_stats(x.ptr, x.ld, ptr(self.wf), ptr(self.conv.bias), y.ptr, y.ld, None,
-                                                  MODE_CONV3, x.N * x.V, self.Co, self.Cpad, self.KG, self.cpg_shift,
-                                                  x.D, x.H, x.W, 1, ptr(stats_part), self.rt.code, self.rt.stream)
+                self.rt.lib.mmseg_conv_gemm_ex(x.ptr, x.ld, ptr(self.wf), ptr(self.conv.bias), y.ptr, y.ld, None,
+                                               MODE_CONV3, x.N * x.V, self.Co, self.Cpad, self.KG, self.cpg_shift,
+                                               x.D, x.H, x.W, 1, ptr(stats_part), self.kreal_f, self.rt.code,
+                                               self.rt.stream)
             return
         if self._stem(x, y.ld):
             with TIMER.region("stem_fwd_kernel", flops=2.0 * x.N * x.V * self.Co * 27 * self.Ci,
@@ -214,9 +219,9 @@ class Conv3:
         ws = self.rt.ws(ks * M * nc) if ks > 1 else None
         with TIMER.region(_gemm_name(self.rt, nc, "conv3"), flops=2.0 * M * self.Co * 27 * self.Ci,
                           nbytes=_io_bytes(self.rt, M, self.Cip, self.Co, 27 * self.Cip * self.Co)):
-            self.rt.lib.mmseg_conv_gemm(x.ptr, x.ld, ptr(self.wf), ptr(self.conv.bias), y.ptr, y.ld, ptr(ws),
-                                        MODE_CONV3, M, nc, self.Cpad, self.KG, self.cpg_shift, x.D, x.H, x.W, ks,
-                                        self.rt.code, self.rt.stream)
+            self.rt.lib.mmseg_conv_gemm_ex(x.ptr, x.ld, ptr(self.wf), ptr(self.conv.bias), y.ptr, y.ld, ptr(ws),
+                                           MODE_CONV3, M, nc, self.Cpad, self.KG, self.cpg_shift, x.D, x.H, x.W, ks,
+                                           None, self.kreal_f, self.rt.code, self.rt.stream)
 
     def bwd(self, x: Act, dy: Act, dx: Optional[Act], accumulate: bool):
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
@@ -261,8 +266,9 @@ class Conv3:
             ws = self.rt.ws(ks * M * nc) if ks > 1 else None
             with TIMER.region(_gemm_name(self.rt, nc, "conv3"), flops=2.0 * M * self.Co * 27 * self.Ci,
                               nbytes=_io_bytes(self.rt, M, self.Co, self.Cip, 27 * self.Cip * self.Co)):
-                L.mmseg_conv_gemm(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, ptr(ws), MODE_CONV3, M, nc,
-                                  self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, ks, code, s)
+                L.mmseg_conv_gemm_ex(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, ptr(ws), MODE_CONV3, M, nc,
+                                     self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, ks, None, self.kreal_d, code,
+                                     s)
 
 
 class ConvT2:

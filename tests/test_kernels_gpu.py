@@ -410,7 +410,11 @@ def test_conv3_fused_instnorm_stats(dev, dtype, knobs, cin, cout, shape, monkeyp
 
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("cin,cout,shape", [(48, 48, (1, 8, 8, 16)), (96, 48, (2, 4, 8, 8)), (48, 96, (1, 4, 8, 8)),
-                                            (24, 24, (1, 4, 8, 8)), (48, 48, (1, 6, 6, 6))])
+                                            (24, 24, (1, 4, 8, 8)), (48, 48, (1, 6, 6, 6)),
+                                            # K-side padding skipped chunk-wise (96 of 128, 192 of 256 channels):
+                                            # brick / runtime-brick forward, dgrad and weight-gradient kernels
+                                            (96, 96, (1, 8, 8, 16)), (192, 96, (1, 4, 4, 4)),
+                                            (384, 192, (2, 4, 4, 4))])
 def test_conv3_channel_padded(dev, dtype, cin, cout, shape):
     """SwinUNETR's bias-free convs over channel-padded buffers (Conv3 cin_pad / cout_pad / pad_cols): 48-column
     brick tiles, padded K groups with zero weights (pack modes 0 / 6), staged Co-padded weight gradient."""
