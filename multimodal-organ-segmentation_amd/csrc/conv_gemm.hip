@@ -982,6 +982,194 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kern
   }
 }
 
+// ------------------------------------------------- brick conv v4 (3^3, bf16, Cin = 32, Co tile 32)
+// The 96^3 32 -> 32 layers.  v3 restages the 9-tap weight slab of every (brick, kz) stage through LDS and
+// every wave re-reads the same B fragments: per tap and wave 4 A + 2 B ds_read_b128 for 8 MFMAs, plus
+// 54 KB of weight and 38 KB of halo LDS writes per brick, and two barriers per stage.  v4:
+//   * the whole 27-tap x 32-ci x 32-co weight tile of the block's column tile lives in the accumulator
+//     register file (27 x 2 fragments = 216 AGPRs, loaded once per block straight from the packed
+//     [KG][Cpad][8] image, which is already fragment-ordered; mfma_aw); LDS holds only halos;
+//   * one block of 4 waves per CU (1 wave / SIMD), persistent over a contiguous brick range; the halo is
+//     double-buffered: the next brick's halo is loaded into registers when a brick starts and written to the
+//     other LDS buffer after 15 taps, so one barrier per brick;
+//   * each tap's 4 A reads are issued two taps ahead of their MFMAs (sched_barrier; left alone, hipcc
+//     issues them just before their MFMAs).
+// Measured (s_memtime stamps, 96^3 B=2 forward): ~200 cycles per tap against 128 of MFMA issue, and the
+// tap loop speeds up in proportion when the per-tap A reads are cut (half the reads: 146 cycles per tap):
+// the LDS read stream, not latency, barriers or the halo loads, is what bounds this kernel.
+// Requirements (host): bf16, one 32-channel K chunk, Ncols % 32 == 0, D % 4, H % 8, W % 8, no fused stats.
+
+// MFMA with the weight fragment pinned to the accumulator file: hipcc otherwise keeps the 216 weight
+// registers in VGPRs and, short of VGPRs, issues each tap's LDS reads just before their MFMAs.  The asm is one
+// opaque instruction to hipcc: it inserts the lgkmcnt waits for x, but no MFMA hazard padding, which
+// brick4_fence / brick4_wfence supply where the accumulators are read and after the weights are written.
+__device__ __forceinline__ void mfma_aw(f32x4& acc, const bf16x8& w, const bf16x8& x) {
+  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "a"(w), "v"(x));
+}
+__device__ __forceinline__ void brick4_fence(f32x4& a, f32x4& b) {
+  asm volatile("s_nop 7\n\ts_nop 7" : "+a"(a), "+a"(b));
+}
+__device__ __forceinline__ void brick4_wfence(bf16x8& a, bf16x8& b) {
+  asm volatile("s_nop 2" : "+a"(a), "+a"(b));
+}
+
+__global__ __launch_bounds__(256, 1) void conv3_brick4_kernel(GemmArgs g, int upb, int blocks_per_nt) {
+  using T = bf16_t;
+  using L = Brick2Layout<T>;
+  constexpr int BZ = 4, HZ = BZ + 2;
+  constexpr int RM = 4, RN = 2;
+  constexpr int PF = 2;                               // A-fragment prefetch distance (taps)
+  constexpr int XQ = HZ * L::RZ;
+  __shared__ __attribute__((aligned(16))) float4 lds4[2 * XQ];
+  T* Xl = reinterpret_cast<T*>(lds4);
+  constexpr int EPQ = 8;
+  constexpr int XROWS = HZ * H2_Y;                    // 60 (z, y) halo rows
+  constexpr int XK = XROWS / 6;                       // rows per thread (6 rows per pass of 240 threads)
+
+  const T* Bw = reinterpret_cast<const T*>(g.b);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int bz_n = g.D / BZ, by_n = g.H / B2_Y, bx_n = g.W / B2_X;
+  const int nbrick = (g.M / (g.D * g.H * g.W)) * bz_n * by_n * bx_n;
+  const int blk_all = g.swz ? xcd_swizzle(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int nt = blk_all / blocks_per_nt, blk = blk_all - nt * blocks_per_nt;
+  const int n0 = nt * 32;
+  const int u_begin = blk * upb;
+  const int u_end = u_begin + upb < nbrick ? u_begin + upb : nbrick;
+  if (u_begin >= u_end || n0 >= g.Ncols) return;
+  const int HW = g.H * g.W;
+  const int cin = 8 << g.cpg_shift;
+  const int ldb = g.lda * (int)sizeof(T);
+  const int vox_per_n = g.D * HW;
+  const int r16 = lane & 15, kg = lane >> 4;
+
+  // ---- weights: fragment (tap, j) = 8 input channels kg*8.. of output column n0 + j*16 + r16
+  V8<T> wf[27][RN];
+#pragma unroll
+  for (int t = 0; t < 27; ++t)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+      wf[t][j].load(Bw + ((long long)(t * (cin / 8) + kg) * g.Cpad + n0 + j * 16 + r16) * 8);
+#pragma unroll
+  for (int t = 0; t < 27; ++t) brick4_wfence(wf[t][0].v, wf[t][1].v);
+
+  // ---- halo column of this thread: (hx, cg) fixed, rows r0, r0+6, ... (hz = r / 10, hy = r % 10)
+  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(g.a), 0, (int)((long long)(g.M / vox_per_n) * vox_per_n * ldb), 0x00020000);
+  const bool xact = tid < 240;
+  const int xq = tid % 40, r0 = tid / 40;
+  const int hx = xq >> 2, cg = xq & 3;
+  auto row_hz = [&](int k) { return ((r0 + 6 * k) * 205) >> 11; };
+  const int xlds0 = (hx * L::QV + cg * L::QG) * EPQ;
+  struct Unit { int n, z0, y0, x0; };
+  auto unit_of = [&](int b) {
+    Unit r;
+    const int bx = b % bx_n; b /= bx_n;
+    const int by = b % by_n; b /= by_n;
+    r.z0 = (b % bz_n) * BZ;
+    r.n = b / bz_n;
+    r.y0 = by * B2_Y;
+    r.x0 = bx * B2_X;
+    return r;
+  };
+  V8<T> xr[XK];
+  auto load_x = [&](const Unit& q) {    // out-of-volume lanes point past the buffer end and read zeros
+    const int xx = q.x0 - 1 + hx;
+    const bool xok = xact && (unsigned)xx < (unsigned)g.W;
+    const int vb = q.n * vox_per_n + xx;
+#pragma unroll
+    for (int k = 0; k < XK; ++k) {
+      const int hz = row_hz(k), hy = r0 + 6 * k - 10 * hz;
+      const int zz = q.z0 - 1 + hz, yy = q.y0 - 1 + hy;
+      const bool ok = xok && (unsigned)zz < (unsigned)g.D && (unsigned)yy < (unsigned)g.H;
+      const uint32_t off = ok ? (uint32_t)((vb + zz * HW + yy * g.W) * ldb + cg * 16) : 0x80000000u;
+      buf_load_v8<T>(xr[k], arsrc, off);
+    }
+  };
+  auto store_x = [&](int buf) {
+    if (xact) {
+#pragma unroll
+      for (int k = 0; k < XK; ++k) {
+        const int hz = row_hz(k), hy = r0 + 6 * k - 10 * hz;
+        xr[k].store(Xl + buf * XQ * EPQ + xlds0 + (hz * L::RZ + hy * L::RY) * EPQ);
+      }
+    }
+  };
+  int aq[RM];
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    const int yr = 2 * i + (r16 >> 3), xr_ = r16 & 7;
+    aq[i] = wave * L::RZ + yr * L::RY + xr_ * L::QV + kg * L::QG;
+  }
+  float bv[RN][4];
+#pragma unroll
+  for (int j = 0; j < RN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[j][r] = g.bias ? g.bias[n0 + j * 16 + 4 * kg + r] : 0.f;
+  T* O = reinterpret_cast<T*>(g.out);
+
+  Unit cur = unit_of(u_begin);
+  load_x(cur);
+  store_x(0);
+  __syncthreads();
+  int b = 0;
+  // (Storing each brick's outputs a few taps into the next brick, from a second accumulator set, measured
+  // 25 % slower; loading the next halo in two halves, or storing it later, measured no faster.)
+  for (int u = u_begin; u < u_end; ++u) {
+    f32x4 acc[RM][RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const bool unext = u + 1 < u_end;
+    Unit nxt = cur;
+    if (unext) {
+      nxt = unit_of(u + 1);
+      load_x(nxt);
+    }
+    const T* Xb = Xl + b * XQ * EPQ;
+    auto hoff = [](int t) { return (t / 9) * L::RZ + ((t / 3) % 3) * L::RY + (t % 3) * L::QV; };
+    V8<T> af[PF + 1][RM];
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+#pragma unroll
+      for (int i = 0; i < RM; ++i) af[p][i].load(Xb + (aq[i] + hoff(p)) * EPQ);
+#pragma unroll
+    for (int t = 0; t < 27; ++t) {
+      if (t == 15 && unext) store_x(b ^ 1);
+      if (t + PF < 27) {
+#pragma unroll
+        for (int i = 0; i < RM; ++i) af[(t + PF) % (PF + 1)][i].load(Xb + (aq[i] + hoff(t + PF)) * EPQ);
+      }
+      __builtin_amdgcn_sched_barrier(0);   // keep the reads PF taps ahead of their MFMAs
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) mfma_aw(acc[i][j], wf[t][j].v, af[t % (PF + 1)][i].v);   // rows = channels
+    }
+#pragma unroll
+    for (int i = 0; i < RM; ++i) brick4_fence(acc[i][0], acc[i][1]);
+    // epilogue: lane holds channels n0 + j*16 + 4*kg + (0..3) of voxel r16 of row tile i
+    const long long obase = (long long)cur.n * vox_per_n;
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int col = n0 + j * 16 + 4 * kg;
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int z = cur.z0 + wave, y = cur.y0 + 2 * i + (r16 >> 3), x = cur.x0 + (r16 & 7);
+        T* dst = O + (obase + (long long)(z * g.H + y) * g.W + x) * g.ldo + col;
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (bf16_t)(acc[i][j][r] + bv[j][r]);
+        *reinterpret_cast<bf16x4*>(dst) = o;
+      }
+    }
+    __syncthreads();   // buffer b^1 is complete; buffer b is free for the brick after next
+    b ^= 1;
+    cur = nxt;
+  }
+}
+
 // ------------------------------------- runtime-brick conv (small volumes)
 // conv3_brick2_kernel for volumes whose sides are not multiples of 8 (the
 // 12^3 and 6^3 levels): the brick (bz, by, bx), <= 256 voxels, is chosen on the
@@ -2553,6 +2741,17 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
       const int upb = maxblk > 0 ? ceil_div(units, maxblk) : 1;
       mmseg::note_kernel("conv3_brick3_kernel<BN64>");
       hipLaunchKernelGGL((conv3_brick3_kernel<T, 64>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
+    } else if (v3 && gemm_nchunk(g) == 1 && g.Ncols % 32 == 0 && knob("MMSEG_BRICK4", 1) &&
+               !(g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks)) {
+      if constexpr (sizeof(T) == 2) {
+        // one persistent block per CU, each over a contiguous brick range of one 32-column tile
+        const int nt_n = g.Ncols / 32;
+        const int per_nt = std::max(1, knob("MMSEG_BRICK4_BLOCKS", 256) / nt_n);
+        const int upb = ceil_div(nb1, std::min(per_nt, nb1));
+        const int bpn = ceil_div(nb1, upb);
+        mmseg::note_kernel("conv3_brick4_kernel<BN32>");
+        hipLaunchKernelGGL(conv3_brick4_kernel, dim3(bpn * nt_n), block, 0, s, g, upb, bpn);
+      }
     } else if (v3 && !(g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks)) {
       const int units = nb1 * (g.Ncols / 32);
       const int upb = maxblk > 0 ? ceil_div(units, maxblk) : 1;

@@ -47,9 +47,14 @@ def test_conv3_fwd_dgrad_wgrad(dev, dtype, cin, cout, shape):
     ({"MMSEG_BRICK2_MINBLK": "0"}, 64, 64, (2, 8, 16, 8)),          # BN64 ZW1
     ({"MMSEG_BRICK2_MINBLK": "0"}, 32, 128, (1, 4, 8, 16)),         # BN64 ZW1, 2 column tiles
     # brick v3 (bf16 BN32 default; f32 takes v2): persistent blocks over several bricks / column tiles
-    ({"MMSEG_BRICK3_BLOCKS": "2"}, 32, 32, (2, 8, 16, 8)),           # 8 bricks over 2 blocks
+    ({"MMSEG_BRICK4": "0", "MMSEG_BRICK3_BLOCKS": "2"}, 32, 32, (2, 8, 16, 8)),   # 8 bricks over 2 blocks
     ({"MMSEG_BRICK3_BLOCKS": "3"}, 64, 128, (1, 4, 16, 16)),         # 4 col tiles x 4 bricks, ragged ranges
-    ({"MMSEG_BRICK3_BLOCKS": "0"}, 32, 32, (1, 12, 8, 24)),          # one unit per block, border bricks
+    ({"MMSEG_BRICK4": "0", "MMSEG_BRICK3_BLOCKS": "0"}, 32, 32, (1, 12, 8, 24)),  # one unit per block, border
+    # brick v4 (bf16, Cin 32, register-resident weights, double-buffered halo; f32 takes v2)
+    ({"MMSEG_BRICK4_BLOCKS": "3"}, 32, 32, (2, 8, 16, 8)),           # 8 bricks over 3 blocks, ragged ranges
+    ({"MMSEG_BRICK4_BLOCKS": "4"}, 32, 64, (1, 4, 8, 16)),           # 2 column tiles x 2 blocks each
+    ({}, 32, 32, (1, 12, 8, 24)),                                    # one brick per block, border bricks
+    ({"MMSEG_BRICK4_BLOCKS": "1"}, 32, 32, (2, 8, 16, 16)),          # one block over all 16 bricks of 2 samples
     ({"MMSEG_BRICK3_BN64": "1", "MMSEG_BRICK2_MINBLK": "0", "MMSEG_BRICK3_BLOCKS": "2"}, 64, 64, (2, 8, 8, 8)),
     ({"MMSEG_BRICK2_ZW": "2"}, 32, 32, (1, 8, 8, 16)),              # BN32 ZW2 (bf16 only; f32 takes ZW1)
     ({"MMSEG_BRICK2_ZW": "2"}, 64, 32, (2, 8, 8, 8)),               # BN32 ZW2, dgrad with 2 input chunks

@@ -39,6 +39,8 @@ def family(name: str) -> str:
     if m:
         tile = "128x32" if (m.group(2), m.group(3)) == ("4", "1") else "128x64"
         return f"conv_gemm_kernel<{_MODES[m.group(1)]},{tile}>[{dt}]"
+    if "conv3_brick4_kernel" in name:
+        return "conv3_brick4_kernel<BN32>[bf16]"
     m = re.search(r"conv3_brick3_kernelI(?:DF16b|f)Li(\d+)E", name)
     if m:
         return f"conv3_brick3_kernel<BN{m.group(1)}>[{dt}]"
