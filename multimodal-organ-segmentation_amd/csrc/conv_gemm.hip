@@ -1170,6 +1170,213 @@ __global__ __launch_bounds__(256, 1) void conv3_brick4_kernel(GemmArgs g, int up
   }
 }
 
+// ------------------------------------------------- brick conv v5 (3^3, bf16, Cin = 32, Co tile 32)
+// brick4 with the A-read stream halved.  A row tile is 16 consecutive x voxels of ONE y row (brick 4 z x
+// 4 y x 16 x, one z plane per wave), so the fragment of row tile i at tap ky is the fragment of halo row
+// i + ky: per (kz, kx) the 12 (ky, i) fragments are 6 distinct halo rows, read once and used by 24 MFMAs
+// (0.25 ds_read_b128 per MFMA instead of 0.5).  Halo image: voxel = 4 quads of 8 channels, the quad of
+// channel group kg at slot kg ^ (((hx >> 2) & 1) << 1), which makes the 16-lane groups of ds_read_b128
+// conflict-free for all three kx shifts; rows of 18 voxels, no padding.
+// Requirements (host): bf16, one 32-channel K chunk, Ncols % 32 == 0, D % 4, H % 4, W % 16, no fused stats.
+template <bool DBG = false>
+__global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int upb, int blocks_per_nt,
+                                                              long long* dbg = nullptr) {
+  using T = bf16_t;
+  constexpr int BZ = 4, BY = 4, BX = 16;
+  constexpr int HZ = BZ + 2, HY = BY + 2, HX = BX + 2;
+  constexpr int RY = HX * 4, RZ = HY * RY;             // quads per halo row / plane
+  constexpr int XQ = HZ * RZ;                          // 2592 quads = 41.5 KB
+  constexpr int RN = 2;
+  constexpr int XROWS = HZ * HY;                       // 36 (z, y) halo rows
+  constexpr int XK = XROWS / 3;                        // rows per thread (3 rows per pass of 216 threads)
+  __shared__ __attribute__((aligned(16))) float4 lds4[2 * XQ];
+  T* Xl = reinterpret_cast<T*>(lds4);
+  constexpr int EPQ = 8;
+
+  const T* Bw = reinterpret_cast<const T*>(g.b);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int bz_n = g.D / BZ, by_n = g.H / BY, bx_n = g.W / BX;
+  const int nbrick = (g.M / (g.D * g.H * g.W)) * bz_n * by_n * bx_n;
+  const int blk_all = g.swz ? xcd_swizzle(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int nt = blk_all / blocks_per_nt, blk = blk_all - nt * blocks_per_nt;
+  const int n0 = nt * 32;
+  const int u_begin = blk * upb;
+  const int u_end = u_begin + upb < nbrick ? u_begin + upb : nbrick;
+  if (u_begin >= u_end || n0 >= g.Ncols) return;
+  const int HW = g.H * g.W;
+  const int cin = 8 << g.cpg_shift;
+  const int ldb = g.lda * (int)sizeof(T);
+  const int vox_per_n = g.D * HW;
+  const int r16 = lane & 15, kg = lane >> 4;
+  // timing probe (DBG): lane 0 of waves 0 / 3 of blocks 0 and 100 record (s_memtime, s_memrealtime) pairs
+  long long* dp = nullptr;
+  int dn = 0;
+  if constexpr (DBG) {
+    const int sl = (blockIdx.x == 0 ? 0 : blockIdx.x == 100 ? 2 : -9) + (tid == 0 ? 0 : tid == 192 ? 1 : -9);
+    if (sl >= 0) dp = dbg + sl * 128;
+  }
+  auto stamp = [&]() {
+    if constexpr (DBG) {
+      if (dp && dn < 64) {
+        dp[64 + dn] = (long long)__builtin_amdgcn_s_memrealtime();
+        dp[dn++] = (long long)__builtin_amdgcn_s_memtime();
+      }
+    }
+  };
+  stamp();
+
+  V8<T> wf[27][RN];
+#pragma unroll
+  for (int t = 0; t < 27; ++t)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+      wf[t][j].load(Bw + ((long long)(t * (cin / 8) + kg) * g.Cpad + n0 + 8 * (r16 >> 2) + 4 * j + (r16 & 3)) * 8);
+#pragma unroll
+  for (int t = 0; t < 27; ++t) brick4_wfence(wf[t][0].v, wf[t][1].v);
+
+  // ---- halo staging: thread t < 216 owns quad column (hx, cg) = divmod(t % 72, 4) of rows t / 72 + 3k
+  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(g.a), 0, (int)((long long)(g.M / vox_per_n) * vox_per_n * ldb), 0x00020000);
+  const bool xact = tid < 216;
+  const int xq = tid % 72, r0 = tid / 72;
+  const int hx = xq >> 2, cg = xq & 3;
+  const int xlds0 = (hx * 4 + (cg ^ (((hx >> 2) & 1) << 1))) * EPQ;
+  struct Unit { int n, z0, y0, x0; };
+  auto unit_of = [&](int b) {
+    Unit r;
+    const int bx = b % bx_n; b /= bx_n;
+    const int by = b % by_n; b /= by_n;
+    r.z0 = (b % bz_n) * BZ;
+    r.n = b / bz_n;
+    r.y0 = by * BY;
+    r.x0 = bx * BX;
+    return r;
+  };
+  V8<T> xr[XK];
+  // byte offset of row k's element relative to the halo origin (z0 - 1, y0 - 1, x0 - 1), fixed per thread
+  uint32_t rel[XK];
+#pragma unroll
+  for (int k = 0; k < XK; ++k) {
+    const int row = r0 + 3 * k, hz = row / HY, hy = row - hz * HY;
+    rel[k] = (uint32_t)((hz * HW + hy * g.W + hx) * ldb + cg * 16);
+  }
+  // halo offsets of a brick: z / y interior bricks need one x test per lane (the unit base is uniform);
+  // border bricks test every row.  Out-of-volume lanes point past the buffer end and read zeros.
+  uint32_t xo[XK];
+  auto set_x = [&](const Unit& q) {
+    const int xx = q.x0 - 1 + hx;
+    const bool xok = xact && (unsigned)xx < (unsigned)g.W;
+    const int ob = ((q.n * g.D + q.z0 - 1) * g.H + q.y0 - 1) * g.W + q.x0 - 1;   // origin voxel (may be -1)
+    const uint32_t base = (uint32_t)(ob * ldb);
+    if (q.z0 >= 1 && q.z0 + BZ < g.D && q.y0 >= 1 && q.y0 + BY < g.H) {
+#pragma unroll
+      for (int k = 0; k < XK; ++k) xo[k] = xok ? base + rel[k] : 0x80000000u;
+    } else {
+#pragma unroll
+      for (int k = 0; k < XK; ++k) {
+        const int row = r0 + 3 * k, hz = row / HY, hy = row - hz * HY;
+        const int zz = q.z0 - 1 + hz, yy = q.y0 - 1 + hy;
+        const bool ok = xok && (unsigned)zz < (unsigned)g.D && (unsigned)yy < (unsigned)g.H;
+        xo[k] = ok ? base + rel[k] : 0x80000000u;
+      }
+    }
+  };
+  auto load_x = [&](int k0, int k1) {
+#pragma unroll
+    for (int k = k0; k < k1; ++k) buf_load_v8<T>(xr[k], arsrc, xo[k]);
+  };
+  auto store_x = [&](int buf, int k0, int k1) {
+    if (xact) {
+#pragma unroll
+      for (int k = k0; k < k1; ++k) xr[k].store(Xl + (buf * XQ + (r0 + 3 * k) * RY) * EPQ + xlds0);
+    }
+  };
+  // per-lane A offsets (quads) of the three kx shifts: voxel hx = r16 + kx, channel group kg
+  int ao[3];
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) {
+    const int h = r16 + kx;
+    ao[kx] = wave * RZ + h * 4 + (kg ^ (((h >> 2) & 1) << 1));
+  }
+  float bv[RN][4];
+#pragma unroll
+  for (int j = 0; j < RN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[j][r] = g.bias ? g.bias[n0 + 8 * kg + 4 * j + r] : 0.f;
+  T* O = reinterpret_cast<T*>(g.out);
+
+  Unit cur = unit_of(u_begin);
+  set_x(cur);
+  load_x(0, XK);
+  store_x(0, 0, XK);
+  __syncthreads();
+  stamp();
+  int b = 0;
+  for (int u = u_begin; u < u_end; ++u) {
+    f32x4 acc[BY][RN];
+#pragma unroll
+    for (int i = 0; i < BY; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const bool unext = u + 1 < u_end;
+    Unit nxt = cur;
+    if (unext) {
+      nxt = unit_of(u + 1);
+      set_x(nxt);
+    }
+    const T* Xb = Xl + b * XQ * EPQ;
+    // group q = (kz, kx) = divmod(q, 3): the 6 halo rows of plane wave + kz at shift kx
+    V8<T> af[2][HY];
+    auto load_group = [&](V8<T> (&f)[HY], int q) {
+      const int kz = q / 3, kx = q - kz * 3;
+#pragma unroll
+      for (int h = 0; h < HY; ++h) f[h].load(Xb + (ao[kx] + kz * RZ + h * RY) * EPQ);
+    };
+    stamp();
+    load_group(af[0], 0);
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      if (q + 1 < 9) load_group(af[(q + 1) & 1], q + 1);
+      // the next brick's halo: 4 rows loaded in each of groups 0..2, 2 rows stored in each of groups 3..8,
+      // so the loads' issue and the LDS writes overlap MFMAs
+      if (unext) {
+        if (q < 3) load_x(4 * q, 4 * q + 4);
+        else store_x(b ^ 1, 2 * (q - 3), 2 * (q - 3) + 2);
+      }
+      if (q == 5) stamp();
+      __builtin_amdgcn_sched_barrier(0);   // keep the next group's reads ahead of this group's MFMAs
+      const int kz = q / 3, kx = q - kz * 3;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int i = 0; i < BY; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j) mfma_aw(acc[i][j], wf[kz * 9 + ky * 3 + kx][j].v, af[q & 1][i + ky].v);
+    }
+#pragma unroll
+    for (int i = 0; i < BY; ++i) brick4_fence(acc[i][0], acc[i][1]);
+    stamp();
+    // epilogue: lane holds channels n0 + 8*kg + 4*j + (0..3) of voxel (z0 + wave, y0 + i, x0 + r16): one
+    // 16-B store per row tile
+    const long long obase = (long long)cur.n * vox_per_n;
+#pragma unroll
+    for (int i = 0; i < BY; ++i) {
+      const int z = cur.z0 + wave, y = cur.y0 + i, x = cur.x0 + r16;
+      T* dst = O + (obase + (long long)(z * g.H + y) * g.W + x) * g.ldo + n0 + 8 * kg;
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[4 * j + r] = (bf16_t)(acc[i][j][r] + bv[j][r]);
+      *reinterpret_cast<bf16x8*>(dst) = o;
+    }
+    stamp();
+    __syncthreads();   // buffer b^1 is complete; buffer b is free for the brick after next
+    b ^= 1;
+    cur = nxt;
+  }
+}
+
 // ------------------------------------- runtime-brick conv (small volumes)
 // conv3_brick2_kernel for volumes whose sides are not multiples of 8 (the
 // 12^3 and 6^3 levels): the brick (bz, by, bx), <= 256 voxels, is chosen on the
@@ -2749,8 +2956,36 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
         const int per_nt = std::max(1, knob("MMSEG_BRICK4_BLOCKS", 256) / nt_n);
         const int upb = ceil_div(nb1, std::min(per_nt, nb1));
         const int bpn = ceil_div(nb1, upb);
-        mmseg::note_kernel("conv3_brick4_kernel<BN32>");
-        hipLaunchKernelGGL(conv3_brick4_kernel, dim3(bpn * nt_n), block, 0, s, g, upb, bpn);
+        if (g.H % 4 == 0 && g.W % 16 == 0 && g.ldo % 8 == 0 && (reinterpret_cast<uintptr_t>(g.out) & 15) == 0 &&
+            knob("MMSEG_BRICK5", 1)) {   // (16-B output stores)
+          const int nb5 = (g.M / (g.D * g.H * g.W)) * (g.D / 4) * (g.H / 4) * (g.W / 16);
+          const int upb5 = ceil_div(nb5, std::min(per_nt, nb5));
+          const int bpn5 = ceil_div(nb5, upb5);
+          mmseg::note_kernel("conv3_brick5_kernel<BN32>");
+          if (knob("MMSEG_BRICK5_DBG", 0)) {   // phase timing probe (diagnostics only)
+            static long long* dbg = nullptr;
+            if (!dbg) hipMalloc(&dbg, 4 * 128 * sizeof(long long));
+            hipMemsetAsync(dbg, 0, 4 * 128 * sizeof(long long), s);
+            hipLaunchKernelGGL(conv3_brick5_kernel<true>, dim3(bpn5 * nt_n), block, 0, s, g, upb5, bpn5, dbg);
+            long long h[4 * 128];
+            hipStreamSynchronize(s);
+            hipMemcpy(h, dbg, sizeof(h), hipMemcpyDeviceToHost);
+            for (int w = 0; w < 4; ++w) {
+              const long long* q = h + w * 128;
+              int n = 1;
+              while (n < 64 && q[n]) ++n;
+              fprintf(stderr, "brick5 dbg slot %d upb %d: clock %.3f GHz:", w, upb5,
+                      (double)(q[n - 1] - q[0]) / (double)(q[64 + n - 1] - q[64] + 1) * 0.1);
+              for (int i = 1; i < n; ++i) fprintf(stderr, " %lld", q[i] - q[i - 1]);
+              fprintf(stderr, "\n");
+            }
+          } else {
+            hipLaunchKernelGGL(conv3_brick5_kernel<false>, dim3(bpn5 * nt_n), block, 0, s, g, upb5, bpn5, nullptr);
+          }
+        } else {
+          mmseg::note_kernel("conv3_brick4_kernel<BN32>");
+          hipLaunchKernelGGL(conv3_brick4_kernel, dim3(bpn * nt_n), block, 0, s, g, upb, bpn);
+        }
       }
     } else if (v3 && !(g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks)) {
       const int units = nb1 * (g.Ncols / 32);

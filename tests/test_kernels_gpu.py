@@ -54,7 +54,12 @@ def test_conv3_fwd_dgrad_wgrad(dev, dtype, cin, cout, shape):
     ({"MMSEG_BRICK4_BLOCKS": "3"}, 32, 32, (2, 8, 16, 8)),           # 8 bricks over 3 blocks, ragged ranges
     ({"MMSEG_BRICK4_BLOCKS": "4"}, 32, 64, (1, 4, 8, 16)),           # 2 column tiles x 2 blocks each
     ({}, 32, 32, (1, 12, 8, 24)),                                    # one brick per block, border bricks
+    ({"MMSEG_BRICK4_BLOCKS": "1", "MMSEG_BRICK5": "0"}, 32, 32, (2, 8, 16, 16)),   # v4, one block, 16 bricks
+    # brick v5 (W % 16: 4x4x16 bricks, ky-shared A fragments)
     ({"MMSEG_BRICK4_BLOCKS": "1"}, 32, 32, (2, 8, 16, 16)),          # one block over all 16 bricks of 2 samples
+    ({"MMSEG_BRICK4_BLOCKS": "3"}, 32, 32, (2, 8, 8, 32)),           # 16 bricks over 3 blocks, ragged ranges
+    ({}, 32, 32, (1, 12, 12, 16)),                                   # border bricks on every side
+    ({"MMSEG_BRICK4_BLOCKS": "4"}, 32, 64, (1, 4, 4, 32)),           # 2 column tiles
     ({"MMSEG_BRICK3_BN64": "1", "MMSEG_BRICK2_MINBLK": "0", "MMSEG_BRICK3_BLOCKS": "2"}, 64, 64, (2, 8, 8, 8)),
     ({"MMSEG_BRICK2_ZW": "2"}, 32, 32, (1, 8, 8, 16)),              # BN32 ZW2 (bf16 only; f32 takes ZW1)
     ({"MMSEG_BRICK2_ZW": "2"}, 64, 32, (2, 8, 8, 8)),               # BN32 ZW2, dgrad with 2 input chunks
