@@ -120,8 +120,9 @@ def main():
     from mmseg_amd.models.build import build_model
     from mmseg_amd.trainer.trainer import Trainer
 
-    local = ddp.init_from_env("nccl")
-    dev = torch.device("cuda", local)
+    # MMSEG_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices round-robin)
+    local = ddp.init_from_env(os.environ.get("MMSEG_DIST_BACKEND", "nccl"))
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     rank, world = ddp.rank(), ddp.world()
     n_gpus = world

@@ -33,8 +33,8 @@ def init_from_env(backend: Optional[str] = None) -> int:
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if ws > 1 and not dist.is_initialized():
-        if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend is None:   # MMSEG_DIST_BACKEND=gloo rehearses N ranks on one GPU (RCCL needs one GPU per rank)
+            backend = os.environ.get("MMSEG_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
