@@ -1178,7 +1178,7 @@ __global__ __launch_bounds__(256, 1) void conv3_brick4_kernel(GemmArgs g, int up
 // channel group kg at slot kg ^ (((hx >> 2) & 1) << 1), which makes the 16-lane groups of ds_read_b128
 // conflict-free for all three kx shifts; rows of 18 voxels, no padding.
 // Requirements (host): bf16, one 32-channel K chunk, Ncols % 32 == 0, D % 4, H % 4, W % 16, no fused stats.
-template <bool DBG = false>
+template <bool DBG = false, bool DMA = false>
 __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int upb, int blocks_per_nt,
                                                               long long* dbg = nullptr) {
   using T = bf16_t;
@@ -1285,6 +1285,48 @@ __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int up
 #pragma unroll
     for (int k = k0; k < k1; ++k) buf_load_v8<T>(xr[k], arsrc, xo[k]);
   };
+  // DMA: the halo goes straight from HBM into the LDS image (buffer_load ... lds; no staging registers, no
+  // ds_write).  Wave-instruction m covers image quads [64 m, 64 m + 64); wave w issues m = w, w + 4, ...
+  constexpr int DM = (XQ + 63) / 64;                  // 41 wave-instructions per halo
+  constexpr int DK = (DM + 3) / 4;                    // per wave (the last ones partly or wholly empty)
+  uint32_t drel[DK];                                  // lane's byte offset from the halo origin, or ~0u (no quad)
+  uint32_t dlm = 0, drm = 0;                          // bit k: lane's quad k is in halo column hx = 0 / hx = 17
+#pragma unroll
+  for (int kk = 0; kk < DK; ++kk) {
+    const int p = (wave + 4 * kk) * 64 + lane;
+    const int row = p / RY, qi = p - row * RY, h = qi >> 2, sl = qi & 3;
+    const int c = sl ^ (((h >> 2) & 1) << 1);
+    const int hz = row / HY, hy = row - hz * HY;
+    drel[kk] = p < XQ ? (uint32_t)((hz * HW + hy * g.W + h) * ldb + c * 16) : ~0u;
+    if (h == 0) dlm |= 1u << kk;
+    if (h == HX - 1) drm |= 1u << kk;
+  }
+  uint32_t dof[DK];
+  auto set_xd = [&](const Unit& q) {
+    const int ob = ((q.n * g.D + q.z0 - 1) * g.H + q.y0 - 1) * g.W + q.x0 - 1;
+    const uint32_t base = (uint32_t)(ob * ldb);
+    const uint32_t xbad = (q.x0 == 0 ? dlm : 0u) | (q.x0 + BX == g.W ? drm : 0u);
+    const bool inner = q.z0 >= 1 && q.z0 + BZ < g.D && q.y0 >= 1 && q.y0 + BY < g.H;
+#pragma unroll
+    for (int kk = 0; kk < DK; ++kk) {
+      bool ok = drel[kk] != ~0u && !((xbad >> kk) & 1u);
+      if (!inner) {
+        const int p = (wave + 4 * kk) * 64 + lane;
+        const int row = p / RY, hz = row / HY, hy = row - hz * HY;
+        ok = ok && (unsigned)(q.z0 - 1 + hz) < (unsigned)g.D && (unsigned)(q.y0 - 1 + hy) < (unsigned)g.H;
+      }
+      dof[kk] = ok ? base + drel[kk] : 0x80000000u;
+    }
+  };
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  auto issue_xd = [&](int buf, int k0, int k1) {
+#pragma unroll
+    for (int kk = k0; kk < k1; ++kk) {
+      if (wave + 4 * kk < DM)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            arsrc, (lds_ptr_t)(lds4 + buf * XQ + (wave + 4 * kk) * 64), 16, dof[kk], 0, 0, 0);
+    }
+  };
   auto store_x = [&](int buf, int k0, int k1) {
     if (xact) {
 #pragma unroll
@@ -1305,10 +1347,33 @@ __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int up
     for (int r = 0; r < 4; ++r) bv[j][r] = g.bias ? g.bias[n0 + 8 * kg + 4 * j + r] : 0.f;
   T* O = reinterpret_cast<T*>(g.out);
 
-  Unit cur = unit_of(u_begin);
-  set_x(cur);
-  load_x(0, XK);
-  store_x(0, 0, XK);
+  // epilogue of a finished brick (ev = its accumulators, copied out of the AGPRs): lane holds channels
+  // n0 + 8*kg + 4*j + (0..3) of voxel (z0 + wave, y0 + i, x0 + r16): one 16-B store per row tile
+  f32x4 ev[BY][RN];
+  auto epilogue = [&](const Unit& q) {
+    const long long obase = (long long)q.n * vox_per_n;
+#pragma unroll
+    for (int i = 0; i < BY; ++i) {
+      const int z = q.z0 + wave, y = q.y0 + i, x = q.x0 + r16;
+      T* dst = O + (obase + (long long)(z * g.H + y) * g.W + x) * g.ldo + n0 + 8 * kg;
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[4 * j + r] = (bf16_t)(ev[i][j][r] + bv[j][r]);
+      *reinterpret_cast<bf16x8*>(dst) = o;
+    }
+  };
+  Unit cur = unit_of(u_begin), prev = cur;
+  if constexpr (DMA) {
+    set_xd(cur);
+    issue_xd(0, 0, DK);
+    __builtin_amdgcn_s_waitcnt(0x0f70);    // vmcnt(0): this wave's halo pieces have landed
+  } else {
+    set_x(cur);
+    load_x(0, XK);
+    store_x(0, 0, XK);
+  }
   __syncthreads();
   stamp();
   int b = 0;
@@ -1321,8 +1386,22 @@ __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int up
     const bool unext = u + 1 < u_end;
     Unit nxt = cur;
     if (unext) {
-      nxt = unit_of(u + 1);
-      set_x(nxt);
+      // next brick of the contiguous range (x fastest), stepped with uniform adds instead of divisions
+      nxt.x0 += BX;
+      if (nxt.x0 == g.W) {
+        nxt.x0 = 0;
+        nxt.y0 += BY;
+        if (nxt.y0 == g.H) {
+          nxt.y0 = 0;
+          nxt.z0 += BZ;
+          if (nxt.z0 == g.D) {
+            nxt.z0 = 0;
+            ++nxt.n;
+          }
+        }
+      }
+      if constexpr (DMA) set_xd(nxt);
+      else set_x(nxt);
     }
     const T* Xb = Xl + b * XQ * EPQ;
     // group q = (kz, kx) = divmod(q, 3): the 6 halo rows of plane wave + kz at shift kx
@@ -1340,11 +1419,17 @@ __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int up
       // the next brick's halo: 4 rows loaded in each of groups 0..2, 2 rows stored in each of groups 3..8,
       // so the loads' issue and the LDS writes overlap MFMAs
       if (unext) {
-        if (q < 3) load_x(4 * q, 4 * q + 4);
-        else store_x(b ^ 1, 2 * (q - 3), 2 * (q - 3) + 2);
+        if constexpr (DMA) {
+          if (q < 3) issue_xd(b ^ 1, 4 * q, 4 * q + 4 < DK ? 4 * q + 4 : DK);
+        } else {
+          if (q < 3) load_x(4 * q, 4 * q + 4);
+          else store_x(b ^ 1, 2 * (q - 3), 2 * (q - 3) + 2);
+        }
       }
       if (q == 5) stamp();
       __builtin_amdgcn_sched_barrier(0);   // keep the next group's reads ahead of this group's MFMAs
+      // the previous brick's outputs: their VALU work and stores fill the first group's MFMA shadow
+      if (q == 0 && u > u_begin) epilogue(prev);
       const int kz = q / 3, kx = q - kz * 3;
 #pragma unroll
       for (int ky = 0; ky < 3; ++ky)
@@ -1356,25 +1441,18 @@ __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int up
 #pragma unroll
     for (int i = 0; i < BY; ++i) brick4_fence(acc[i][0], acc[i][1]);
     stamp();
-    // epilogue: lane holds channels n0 + 8*kg + 4*j + (0..3) of voxel (z0 + wave, y0 + i, x0 + r16): one
-    // 16-B store per row tile
-    const long long obase = (long long)cur.n * vox_per_n;
 #pragma unroll
-    for (int i = 0; i < BY; ++i) {
-      const int z = cur.z0 + wave, y = cur.y0 + i, x = cur.x0 + r16;
-      T* dst = O + (obase + (long long)(z * g.H + y) * g.W + x) * g.ldo + n0 + 8 * kg;
-      bf16x8 o;
+    for (int i = 0; i < BY; ++i)
 #pragma unroll
-      for (int j = 0; j < RN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[4 * j + r] = (bf16_t)(acc[i][j][r] + bv[j][r]);
-      *reinterpret_cast<bf16x8*>(dst) = o;
-    }
+      for (int j = 0; j < RN; ++j) ev[i][j] = acc[i][j];
+    prev = cur;
     stamp();
+    if constexpr (DMA) __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): the next halo has landed
     __syncthreads();   // buffer b^1 is complete; buffer b is free for the brick after next
     b ^= 1;
     cur = nxt;
   }
+  epilogue(prev);
 }
 
 // ------------------------------------- runtime-brick conv (small volumes)
@@ -2966,7 +3044,10 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
             static long long* dbg = nullptr;
             if (!dbg) hipMalloc(&dbg, 4 * 128 * sizeof(long long));
             hipMemsetAsync(dbg, 0, 4 * 128 * sizeof(long long), s);
-            hipLaunchKernelGGL(conv3_brick5_kernel<true>, dim3(bpn5 * nt_n), block, 0, s, g, upb5, bpn5, dbg);
+            if (knob("MMSEG_BRICK5_DMA", 0))
+              hipLaunchKernelGGL((conv3_brick5_kernel<true, true>), dim3(bpn5 * nt_n), block, 0, s, g, upb5, bpn5, dbg);
+            else
+              hipLaunchKernelGGL((conv3_brick5_kernel<true, false>), dim3(bpn5 * nt_n), block, 0, s, g, upb5, bpn5, dbg);
             long long h[4 * 128];
             hipStreamSynchronize(s);
             hipMemcpy(h, dbg, sizeof(h), hipMemcpyDeviceToHost);
@@ -2980,7 +3061,10 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
               fprintf(stderr, "\n");
             }
           } else {
-            hipLaunchKernelGGL(conv3_brick5_kernel<false>, dim3(bpn5 * nt_n), block, 0, s, g, upb5, bpn5, nullptr);
+            if (knob("MMSEG_BRICK5_DMA", 0))
+              hipLaunchKernelGGL((conv3_brick5_kernel<false, true>), dim3(bpn5 * nt_n), block, 0, s, g, upb5, bpn5, nullptr);
+            else
+              hipLaunchKernelGGL((conv3_brick5_kernel<false, false>), dim3(bpn5 * nt_n), block, 0, s, g, upb5, bpn5, nullptr);
           }
         } else {
           mmseg::note_kernel("conv3_brick4_kernel<BN32>");
