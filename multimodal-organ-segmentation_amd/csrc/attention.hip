@@ -233,17 +233,23 @@ __global__ void bias_grad_sum_kernel(const T* __restrict__ dS, int ldn, int B, i
   }
 }
 
-// gtable[t][h] (+)= sum over the (n, m) pairs with index[n][m] == t (CSR lists, fixed order)
-__global__ void relpos_table_grad_kernel(const float* __restrict__ dB, const int* __restrict__ offs,
-                                         const int* __restrict__ pairs, int T, int heads, int N,
-                                         float* __restrict__ gtable, int accumulate) {
+// gtable[t][h] (+)= sum over the (n, m) pairs with index[n][m] == t (CSR lists).  One wave per (t, h): lanes
+// stride over the pair list, then a fixed shuffle tree -> deterministic.  (One thread per entry walked its
+// list serially with T*heads = 6.6k threads: 129 us per SwinUNETR stage-0 block at 128^3.)
+__global__ __launch_bounds__(256) void relpos_table_grad_kernel(const float* __restrict__ dB,
+                                                                const int* __restrict__ offs,
+                                                                const int* __restrict__ pairs, int T, int heads,
+                                                                int N, float* __restrict__ gtable, int accumulate) {
   const long long total = (long long)T * heads;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
+  const int lane = threadIdx.x & 63;
+  for (long long e = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; e < total;
+       e += ((long long)gridDim.x * blockDim.x) >> 6) {
     const int t = (int)(e / heads), h = (int)(e % heads);
+    const float* dh = dB + (long long)h * N * N;
     float a = 0.f;
-    for (int k = offs[t]; k < offs[t + 1]; ++k) a += dB[(long long)h * N * N + pairs[k]];
-    gtable[e] = accumulate ? gtable[e] + a : a;
+    for (int k = offs[t] + lane; k < offs[t + 1]; k += 64) a += dh[pairs[k]];
+    a = wave_sum(a);
+    if (lane == 0) gtable[e] = accumulate ? gtable[e] + a : a;
   }
 }
 }  // namespace
@@ -354,7 +360,8 @@ int mmseg_relpos_table_grad(const void* dS, int ldn, int B, int heads, int N, fl
                        dB);
   if (mmseg::check_launch("bias_grad_sum")) return 1;
   const long long th = (long long)T * heads;
-  hipLaunchKernelGGL(relpos_table_grad_kernel, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, dB, offs, pairs, T,
+  hipLaunchKernelGGL(relpos_table_grad_kernel, dim3((unsigned)std::min<long long>((th + 3) / 4, 8192)), dim3(256), 0, s,
+                     dB, offs, pairs, T,
                      heads, N, gtable, accumulate);
   return mmseg::check_launch("relpos_table_grad");
 }
