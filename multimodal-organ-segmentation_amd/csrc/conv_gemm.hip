@@ -2895,7 +2895,7 @@ struct Pack3Desc {
 
 template <typename T>
 __global__ __launch_bounds__(256) void pack_conv3_batched_kernel(const Pack3Desc* __restrict__ descs, int n) {
-  __shared__ float sw[8][32][28];
+  __shared__ float sw[8][33][29];   // padded: conflict-free image reads (the [8][32][28] form was 32-way on the forward image)
   int lo = 0, hi = n - 1;
   const int b = blockIdx.x;
   while (lo < hi) {
@@ -2909,10 +2909,24 @@ __global__ __launch_bounds__(256) void pack_conv3_batched_kernel(const Pack3Desc
   const int co0 = (lb / nci) * 8, ci0 = (lb % nci) * 32;
   const int cis = d.Ci - ci0 < 32 ? d.Ci - ci0 : 32;
   const int tid = threadIdx.x;
-  for (int e = tid; e < 8 * 32 * 27; e += 256) {
-    const int co = e / (32 * 27), r = e - co * (32 * 27);
-    const int ci = r / 27, t = r - ci * 27;
-    sw[co][ci][t] = (ci < cis && co0 + co < d.Co) ? d.w[((long long)(co0 + co) * d.Ci + ci0) * 27 + r] : 0.f;
+  if (cis == 32 && co0 + 8 <= d.Co && (d.Ci & 3) == 0) {
+    // full tile: each co row of the tile is 864 contiguous floats, 16-B aligned -> float4 loads
+    for (int e = tid; e < 8 * 216; e += 256) {
+      const int co = e / 216, r4 = (e - co * 216) * 4;
+      const float4 v = *reinterpret_cast<const float4*>(d.w + ((long long)(co0 + co) * d.Ci + ci0) * 27 + r4);
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int r = r4 + k, ci = r / 27, t = r - ci * 27;
+        sw[co][ci][t] = vv[k];
+      }
+    }
+  } else {
+    for (int e = tid; e < 8 * 32 * 27; e += 256) {
+      const int co = e / (32 * 27), r = e - co * (32 * 27);
+      const int ci = r / 27, t = r - ci * 27;
+      sw[co][ci][t] = (ci < cis && co0 + co < d.Co) ? d.w[((long long)(co0 + co) * d.Ci + ci0) * 27 + r] : 0.f;
+    }
   }
   __syncthreads();
   // forward image: (t, 8-ci group, co) -> 16 B
