@@ -79,6 +79,57 @@ __global__ void in_stats_partial(const T* __restrict__ x, int ld, int V, int C, 
   }
   __shared__ float red[2][256 * 8];
   __shared__ float rcnt[256];
+  if ((C8 & (C8 - 1)) == 0 && C8 <= 32) {
+    // power-of-two channel groups: the voxel lanes of a wave are merged by a
+    // shuffle tree (lane l absorbs lane l+o, o = 32 .. C8: lower voxel lanes
+    // stay first, fixed order), then lanes < C8 of the 4 waves go through LDS
+    // and one thread per channel merges the 4 waves in order.  The serial
+    // 64-lane merge below cost ~2 us per block at C = 32.
+    for (int o = 32; o >= C8; o >>= 1) {
+      const float nb = __shfl_down(cnt, o, 64);
+      const float nn = cnt + nb;
+      const float fb = nn > 0.f ? nb / nn : 0.f;
+      const float fab = nn > 0.f ? cnt * fb : 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float mb = __shfl_down(mu[j], o, 64), sb = __shfl_down(m2[j], o, 64);
+        const float delta = mb - mu[j];
+        mu[j] = fmaf(delta, fb, mu[j]);
+        m2[j] = m2[j] + sb + delta * delta * fab;
+      }
+      cnt = nn;
+    }
+    const int lane = tid & 63, wave = tid >> 6;
+    if (lane < C8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[0][(wave * C8 + lane) * 8 + j] = mu[j];
+        red[1][(wave * C8 + lane) * 8 + j] = m2[j];
+      }
+      rcnt[wave * C8 + lane] = cnt;
+    }
+    __syncthreads();
+    if (tid < C) {
+      const int g = tid >> 3, j = tid & 7;
+      float na = 0.f, ma = 0.f, sa = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const int t = w * C8 + g;
+        const float nb = rcnt[t];
+        if (nb == 0.f) continue;
+        const float mb = red[0][t * 8 + j], sb = red[1][t * 8 + j];
+        const float nn = na + nb;
+        const float delta = mb - ma;
+        ma = ma + delta * (nb / nn);
+        sa = sa + sb + delta * delta * (na * nb / nn);
+        na = nn;
+      }
+      float* p = part + (((long long)n * nchunk + chunk) * C + tid) * 2;
+      p[0] = ma;
+      p[1] = sa;
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     red[0][tid * 8 + j] = mu[j];
@@ -114,17 +165,18 @@ __device__ __forceinline__ void load8f(const float* p, float* d) {
   d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
 }
 
-// one wave per (n, c): fixed-order Chan merge of the chunk partials in double
+// one 256-thread block per (n, c): fixed-order Chan merge of the chunk partials in double
+// (each thread its chunks in order, a fixed butterfly per wave, then the 4 waves in order;
+// one wave per (n, c) walked ~14 dependent chunk loads per lane at 96^3)
 template <typename T>
 __global__ void in_stats_finalize(const T* __restrict__ x, int ld, long long V, int N, int C, int nchunk,
                                   long long vpc, const float* __restrict__ part, float eps, float* __restrict__ mean,
                                   int mean_ld, float* __restrict__ rstd) {
-  const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (idx >= N * C) return;
+  const int idx = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = idx / C, c = idx - n * C;
   double na = 0.0, ma = 0.0, sa = 0.0;
-  for (int k = lane; k < nchunk; k += 64) {   // each lane: its chunks in order
+  for (int k = threadIdx.x; k < nchunk; k += 256) {   // each thread: its chunks in order
     const float* p = part + (((long long)n * nchunk + k) * C + c) * 2;
     const long long v0 = (long long)k * vpc;
     const long long v1 = v0 + vpc < V ? v0 + vpc : V;
@@ -150,7 +202,23 @@ __global__ void in_stats_finalize(const T* __restrict__ x, int ld, long long V, 
       na = nn;
     }
   }
-  if (lane != 0) return;
+  __shared__ double wred[4][3];
+  if (lane == 0) {
+    wred[wave][0] = na;
+    wred[wave][1] = ma;
+    wred[wave][2] = sa;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  na = 0.0; ma = 0.0; sa = 0.0;
+  for (int w = 0; w < 4; ++w) {
+    const double nb = wred[w][0];
+    if (nb <= 0) continue;
+    const double nn = na + nb, delta = wred[w][1] - ma;
+    ma += delta * (nb / nn);
+    sa += wred[w][2] + delta * delta * (na * nb / nn);
+    na = nn;
+  }
   const double var = sa / (double)V;
   mean[(long long)n * mean_ld + c] = (float)ma;
   if (rstd) rstd[idx] = (float)(1.0 / sqrt(var + (double)eps));
@@ -395,6 +463,38 @@ __global__ void in_bwd_partial(const T* __restrict__ x, int ldx, const float* __
     }
   }
   __shared__ float red[2][256 * 8];
+  if ((C8 & (C8 - 1)) == 0 && C8 <= 32) {
+    // shuffle tree over the voxel lanes of each wave (fixed order), then the 4 waves in order
+    for (int o = 32; o >= C8; o >>= 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sg[j] += __shfl_down(sg[j], o, 64);
+        sgx[j] += __shfl_down(sgx[j], o, 64);
+      }
+    }
+    const int lane = tid & 63, wave = tid >> 6;
+    if (lane < C8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[0][(wave * C8 + lane) * 8 + j] = sg[j];
+        red[1][(wave * C8 + lane) * 8 + j] = sgx[j];
+      }
+    }
+    __syncthreads();
+    if (tid < C) {
+      const int g = tid >> 3, j = tid & 7;
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        a += red[0][(w * C8 + g) * 8 + j];
+        b += red[1][(w * C8 + g) * 8 + j];
+      }
+      float* p = part + (((long long)n * nchunk + chunk) * C + tid) * 2;
+      p[0] = a;
+      p[1] = b;
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     red[0][tid * 8 + j] = sg[j];
@@ -414,21 +514,29 @@ __global__ void in_bwd_partial(const T* __restrict__ x, int ldx, const float* __
   }
 }
 
+// one 256-thread block per (n, c): fixed-order double sums of the chunk partials
 __global__ void in_bwd_finalize(const float* __restrict__ part, int N, int C, int nchunk, long long V,
                                 float* __restrict__ coef) {
-  const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (idx >= N * C) return;
+  const int idx = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = idx / C, c = idx - n * C;
   double a = 0.0, b = 0.0;
-  for (int k = lane; k < nchunk; k += 64) {
+  for (int k = threadIdx.x; k < nchunk; k += 256) {
     const float* p = part + (((long long)n * nchunk + k) * C + c) * 2;
     a += p[0];
     b += p[1];
   }
   a = wave_sum_d(a);
   b = wave_sum_d(b);
+  __shared__ double wred[4][2];
   if (lane == 0) {
+    wred[wave][0] = a;
+    wred[wave][1] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    a = (wred[0][0] + wred[1][0]) + (wred[2][0] + wred[3][0]);
+    b = (wred[0][1] + wred[1][1]) + (wred[2][1] + wred[3][1]);
     coef[idx * 2 + 0] = (float)(a / (double)V);
     coef[idx * 2 + 1] = (float)(b / (double)V);
   }
@@ -873,11 +981,11 @@ int mmseg_instnorm_stats(const void* x, int ldx, int N, long long V, int C, floa
   if (dtype == MMSEG_BF16) {
     hipLaunchKernelGGL(in_stats_partial<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, (int)V, C, (int)vpc,
                        ws);
-    hipLaunchKernelGGL(in_stats_finalize<bf16_t>, dim3(ceil_div(N * C, 4)), dim3(256), 0, s, (const bf16_t*)x, ldx,
+    hipLaunchKernelGGL(in_stats_finalize<bf16_t>, dim3(N * C), dim3(256), 0, s, (const bf16_t*)x, ldx,
                        V, N, C, nch, vpc, ws, eps, mean, mean_ld, rstd);
   } else {
     hipLaunchKernelGGL(in_stats_partial<float>, grid, dim3(256), 0, s, (const float*)x, ldx, (int)V, C, (int)vpc, ws);
-    hipLaunchKernelGGL(in_stats_finalize<float>, dim3(ceil_div(N * C, 4)), dim3(256), 0, s, (const float*)x, ldx, V,
+    hipLaunchKernelGGL(in_stats_finalize<float>, dim3(N * C), dim3(256), 0, s, (const float*)x, ldx, V,
                        N, C, nch, vpc, ws, eps, mean, mean_ld, rstd);
   }
   return mmseg::check_launch("instnorm_stats");
@@ -996,7 +1104,7 @@ int mmseg_instnorm_bwd(const void* x, int ldx, const float* mean, const float* r
     }
     hipLaunchKernelGGL((in_bwd_partial<T, R>), grid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, (int)V, C, D,
                        H, W, (int)vpc, part);
-    hipLaunchKernelGGL(in_bwd_finalize, dim3(ceil_div(N * C, 4)), dim3(256), 0, s, part, N, C, nch, V, coef);
+    hipLaunchKernelGGL(in_bwd_finalize, dim3(N * C), dim3(256), 0, s, part, N, C, nch, V, coef);
     hipLaunchKernelGGL((in_bwd_apply<T, R>), agrid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, coef, (T*)dx,
                        lddx, (int)V, C, D, H, W, avpc);
   };
