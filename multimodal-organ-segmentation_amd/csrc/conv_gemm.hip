@@ -1742,11 +1742,41 @@ Conv3Plan plan_conv3(int M, int Ncols, int cin, int D, int H, int W, int lda, in
   return p;
 }
 
+template <int MODE>
+int splitk_reduce_blocks(const GemmArgs& g) {
+  const long long total = (long long)g.M * g.Ncols;
+  const bool vec = MODE != MODE_CONVT_FWD && (g.Ncols & 3) == 0 && (g.ldo & 3) == 0 &&
+      (reinterpret_cast<uintptr_t>(g.part) & 15) == 0;
+  return ceil_div(vec ? (total + 3) / 4 : total, 256);
+}
+
 // Fixed-order split-K reduction for the forward GEMM: out = sum_k part[k] (+bias).
 template <typename T, int MODE>
 __global__ void gemm_splitk_reduce(GemmArgs g) {
-  long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   long long total = (long long)g.M * g.Ncols;
+  if (MODE != MODE_CONVT_FWD && (g.Ncols & 3) == 0 && (g.ldo & 3) == 0 &&
+      (reinterpret_cast<uintptr_t>(g.part) & 15) == 0) {
+    // 4 consecutive columns per thread: 16-B partial loads, 4 splits' loads in flight, fixed split order
+    const long long idx4 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (idx4 >= total) return;
+    const long long row = idx4 / g.Ncols;
+    const int col = (int)(idx4 - row * g.Ncols);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4* p = reinterpret_cast<const float4*>(g.part + idx4);
+    const long long st = total / 4;
+#pragma unroll 4
+    for (int k = 0; k < g.ksplit; ++k) {
+      const float4 a = p[(long long)k * st];
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+    if (g.bias) {
+      v.x += g.bias[col]; v.y += g.bias[col + 1]; v.z += g.bias[col + 2]; v.w += g.bias[col + 3];
+    }
+    T* O = reinterpret_cast<T*>(g.out) + row * g.ldo + col;
+    O[0] = from_f<T>(v.x); O[1] = from_f<T>(v.y); O[2] = from_f<T>(v.z); O[3] = from_f<T>(v.w);
+    return;
+  }
+  long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
   const long long row = idx / g.Ncols;
   const int col = (int)(idx - row * g.Ncols);
@@ -3015,7 +3045,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     if (mmseg::check_launch("conv3_brickr")) return 1;
     if (g.ksplit > 1) {
       const long long total = (long long)g.M * g.Ncols;
-      hipLaunchKernelGGL((gemm_splitk_reduce<T, MODE>), dim3(ceil_div(total, 256)), dim3(256), 0, s, g);
+      hipLaunchKernelGGL((gemm_splitk_reduce<T, MODE>), dim3(splitk_reduce_blocks<MODE>(g)), dim3(256), 0, s, g);
       return mmseg::check_launch("gemm_splitk_reduce");
     }
     return 0;
@@ -3143,7 +3173,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
   if (mmseg::check_launch("conv_gemm")) return 1;
   if (g.ksplit > 1) {
     long long total = (long long)g.M * g.Ncols;
-    hipLaunchKernelGGL((gemm_splitk_reduce<T, MODE>), dim3(ceil_div(total, 256)), dim3(256), 0, s, g);
+    hipLaunchKernelGGL((gemm_splitk_reduce<T, MODE>), dim3(splitk_reduce_blocks<MODE>(g)), dim3(256), 0, s, g);
     if (mmseg::check_launch("gemm_splitk_reduce")) return 1;
   }
   return 0;
@@ -3251,7 +3281,9 @@ int brick_wgrad_splits(long long V, int cap, int Ca, int cpg_shift, int kind, in
   // a partial second wave of 512-thread blocks costs a whole block time.
   long long ks;
   if (kind >= 2) {
-    const int slots = (kind == 2 && Ca % 64 != 0 && knob("MMSEG_WGRAD_V3", 1) == 0) ? 512 : 256;
+    const int slots = (kind == 2 && Ca % 64 != 0 && knob("MMSEG_WGRAD_V3", 1) == 0) ? 512
+                      : kind == 3 ? knob("MMSEG_WGRAD_RSLOTS", 256)   // runtime-brick kernel (24^3 .. 6^3 levels)
+                                  : 256;
     ks = (long long)slots * knob("MMSEG_WGRAD_WAVES", 1) / tiles;
   } else {
     ks = (1024 + tiles - 1) / tiles;
@@ -3314,7 +3346,8 @@ int launch_wgrad_reduce(WReduceArgs g, void* stream) {
   const int ksplit = g.ksplit;
   const long long total = (long long)g.Ca * g.Ncols + (g.bias_part ? g.Ca : 0);
   hipStream_t s = (hipStream_t)stream;
-  // slices: ~8+ loads per thread when the splits allow, 1 slice for a handful of splits
+  // slices: ~8+ loads per thread when the splits allow, 1 slice for a handful of splits.  (Choosing S for
+  // >= 2048 blocks instead measured far slower: the S-slice LDS epilogue is serial in one thread per column.)
   if (ksplit >= 512)
     hipLaunchKernelGGL(wgrad_reduce_kernel<64>, dim3(ceil_div(total, 16)), dim3(256), 0, s, g);
   else if (ksplit >= 64)

@@ -14,6 +14,8 @@
 //   input:  NCDHW fp32 volume -> NDHWC (8-channel padded) engine layout.
 #include "mmseg_common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int CMAX = 16;
@@ -64,6 +66,65 @@ __global__ void head_fwd_kernel(const T* __restrict__ x, int ldx, int Cin, const
 #pragma unroll
     for (int c = 0; c < CMAX; ++c)
       if (c < C) logits[(n * C + c) * V + v] = acc[c];
+  }
+}
+
+// Same head with the channel-group count CG = Cin / 8 known at compile time and
+// U = 4 voxels per thread (i, i + S, i + 2S, i + 3S with S the grid's thread
+// count): all U * CG 16-B feature loads are issued before any FMA, and one
+// grid of total / (256 U) blocks covers the volume once.  The one-voxel form
+// (one block per 256 voxels, each waiting on its weight preload and then on
+// 64 B of loads per thread) ran at ~2.2 TB/s.
+template <typename T, int CG, int CC>
+__global__ __launch_bounds__(256) void head_fwd_u_kernel(const T* __restrict__ x, int ldx,
+                                                         const float* __restrict__ Wt, const float* __restrict__ bias,
+                                                         const float* __restrict__ dscale, long long V, int N,
+                                                         float* __restrict__ logits) {
+  constexpr int Cin = CG * 8, U = 4;
+  __shared__ float sw[CC * Cin];
+  for (int i = threadIdx.x; i < CC * Cin; i += blockDim.x) sw[i] = Wt[i];
+  const long long total = (long long)N * V;
+  const long long S = (long long)gridDim.x * blockDim.x;
+  const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  V8<T> a[U][CG];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (i0 + u * S < total)
+#pragma unroll
+      for (int cg = 0; cg < CG; ++cg) a[u][cg].load(x + (i0 + u * S) * ldx + cg * 8);
+  __syncthreads();
+  float acc[U][CC];
+#pragma unroll
+  for (int c = 0; c < CC; ++c) {
+    const float b = bias[c];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u][c] = b;
+  }
+  // weights outer (read once from LDS per (ci, c)), the U voxels inner
+#pragma unroll
+  for (int cg = 0; cg < CG; ++cg)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float xv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        xv[u] = a[u][cg].get(j);
+        if (dscale && i0 + u * S < total) xv[u] *= dscale[((i0 + u * S) / V) * Cin + cg * 8 + j];
+      }
+#pragma unroll
+      for (int c = 0; c < CC; ++c) {
+        const float w = sw[c * Cin + cg * 8 + j];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u][c] = fmaf(w, xv[u], acc[u][c]);
+      }
+    }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long i = i0 + u * S;
+    if (i >= total) break;
+    const long long n = i / V, v = i - n * V;
+#pragma unroll
+    for (int c = 0; c < CC; ++c) logits[(n * CC + c) * V + v] = acc[u][c];
   }
 }
 
@@ -139,10 +200,10 @@ __global__ __launch_bounds__(256) void head_dgrad_q_kernel(const float* __restri
 // partial dW[c][ci] and db[c] per voxel chunk (block), fixed order.
 // thread = (voxel lane, 8-channel group): vectorised x loads, 8x8 register tile per class chunk.
 template <typename T>
-__global__ void head_wgrad_partial(const T* __restrict__ x, int ldx, const float* __restrict__ dlog,
+__global__ __launch_bounds__(256) void head_wgrad_partial(const T* __restrict__ x, int ldx, const float* __restrict__ dlog,
                                    const float* __restrict__ dscale, int C, int Cin, long long V, int N,
                                    long long vpc, float* __restrict__ part) {
-  __shared__ float red[256 * 8];
+  __shared__ float red[256 * 8 + 4];
   const int C8 = Cin >> 3;
   const int lanes_v = 256 / C8;
   const int tid = threadIdx.x;
@@ -161,22 +222,74 @@ __global__ void head_wgrad_partial(const T* __restrict__ x, int ldx, const float
       for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
     }
     if (vl < lanes_v) {
-      for (long long e = e0 + vl; e < e1; e += lanes_v) {
-        const long long n = e / V, v = e - n * V;
-        V8<T> a;
-        a.load(x + e * ldx + cg * 8);
-        float xv[8];
+      // U voxels per step: their feature and dlogits loads are issued before any FMA
+      constexpr int U = 2;
+      for (long long eb = e0 + vl; eb < e1; eb += U * lanes_v) {
+        V8<T> a[U];
+        float dd[U][8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) xv[j] = dscale ? a.get(j) * dscale[n * Cin + cg * 8 + j] : a.get(j);
+        for (int u = 0; u < U; ++u) {
+          const long long e = eb + u * lanes_v;
+          if (e < e1) {
+            const long long n = e / V, v = e - n * V;
+            a[u].load(x + e * ldx + cg * 8);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          if (c0 + k >= C) break;
-          const float d = dlog[(n * C + c0 + k) * V + v];
-          bacc[k] += d;
+            for (int k = 0; k < 8; ++k) dd[u][k] = c0 + k < C ? dlog[(n * C + c0 + k) * V + v] : 0.f;
+          }
+        }
 #pragma unroll
-          for (int j = 0; j < 8; ++j) acc[k][j] = fmaf(d, xv[j], acc[k][j]);
+        for (int u = 0; u < U; ++u) {
+          const long long e = eb + u * lanes_v;
+          if (e >= e1) break;
+          const long long n = e / V;
+          float xv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) xv[j] = dscale ? a[u].get(j) * dscale[n * Cin + cg * 8 + j] : a[u].get(j);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float d = dd[u][k];
+            bacc[k] += d;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[k][j] = fmaf(d, xv[j], acc[k][j]);
+          }
         }
       }
+    }
+    if ((C8 & (C8 - 1)) == 0 && C8 <= 32) {
+      // power-of-two channel groups: shuffle tree over the voxel lanes of each wave (fixed order), then
+      // the 4 waves in order through LDS (the serial 64-lane LDS sweep per class cost ~2 us per block)
+      for (int o = 32; o >= C8; o >>= 1) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          bacc[k] += __shfl_down(bacc[k], o, 64);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[k][j] += __shfl_down(acc[k][j], o, 64);
+        }
+      }
+      const int lane = tid & 63, wave = tid >> 6;
+      for (int k = 0; k < 8 && c0 + k < C; ++k) {
+        __syncthreads();
+        if (lane < C8) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) red[(wave * C8 + lane) * 8 + j] = acc[k][j];
+          if (lane == 0) red[4 * 32 * 8 + wave] = bacc[k];
+        }
+        __syncthreads();
+        for (int ci = tid; ci < Cin; ci += 256) {
+          const int g = ci >> 3, j = ci & 7;
+          float sacc = 0.f;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) sacc += red[(w * C8 + g) * 8 + j];
+          part[(long long)blockIdx.x * npairs + (c0 + k) * Cin + ci] = sacc;
+        }
+        if (tid == 0) {
+          float sacc = 0.f;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) sacc += red[4 * 32 * 8 + w];
+          part[(long long)blockIdx.x * npairs + C * Cin + c0 + k] = sacc;
+        }
+      }
+      continue;
     }
     for (int k = 0; k < 8 && c0 + k < C; ++k) {
       __syncthreads();
@@ -228,37 +341,57 @@ struct LossCfg {
 };
 
 // per (n, chunk): [P_c][I_c][T_c] (3C) + ce_num + ce_den
-template <typename LT>
-__global__ void loss_stats_kernel(const float* __restrict__ logits, const LT* __restrict__ labels, int C,
+template <typename LT, int CC>
+__global__ __launch_bounds__(256) void loss_stats_kernel(const float* __restrict__ logits, const LT* __restrict__ labels, int Crt,
                                   long long V, long long vpc, LossCfg cfg, float* __restrict__ part) {
+  // CC > 0: class count known at compile time (U voxels in flight); CC = 0: runtime C, one voxel at a time
+  const int C = CC > 0 ? CC : Crt;
+  constexpr int NC = CC > 0 ? CC : CMAX;
   const int n = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
-  float P[CMAX], I[CMAX], Tc[CMAX];
+  float P[NC], I[NC], Tc[NC];
 #pragma unroll
-  for (int c = 0; c < CMAX; ++c) P[c] = I[c] = Tc[c] = 0.f;
+  for (int c = 0; c < NC; ++c) P[c] = I[c] = Tc[c] = 0.f;
   float ce = 0.f, cden = 0.f;
   const long long v0 = (long long)chunk * vpc;
   long long v1 = v0 + vpc;
   if (v1 > V) v1 = V;
   const float* L = logits + (long long)n * C * V;
-  for (long long v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
-    float z[CMAX];
+  // U voxels per thread per step: their C logits and labels are loaded before any is consumed
+  constexpr int U = CC > 0 ? 4 : 1;
+  for (long long vb = v0 + threadIdx.x; vb < v1; vb += U * blockDim.x) {
+  float zu[U][NC];
+  int yu[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long v = vb + u * blockDim.x;
+    if (v < v1) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (c < C) zu[u][c] = L[c * V + v];
+      yu[u] = (int)labels[(long long)n * V + v];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (vb + u * blockDim.x >= v1) break;
+    float z[NC];
     float mx = -INFINITY;
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c)
+    for (int c = 0; c < NC; ++c)
       if (c < C) {
-        z[c] = L[c * V + v];
+        z[c] = zu[u][c];
         mx = fmaxf(mx, z[c]);
       }
     float se = 0.f;
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c)
+    for (int c = 0; c < NC; ++c)
       if (c < C) se += expf(z[c] - mx);
     const float lse = mx + logf(se);
-    const int y = (int)labels[(long long)n * V + v];
+    const int y = yu[u];
     const float inv = 1.f / se;
     float zy = 0.f;
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c)
+    for (int c = 0; c < NC; ++c)
       if (c < C) {
         const float p = expf(z[c] - mx) * inv;
         P[c] += p;
@@ -278,6 +411,7 @@ __global__ void loss_stats_kernel(const float* __restrict__ logits, const LT* __
       ce = fmaf(wy, lse - zy, ce);
       cden += wy;
     }
+  }
   }
   __shared__ float red[4][3 * CMAX + 2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -303,7 +437,7 @@ __global__ void loss_stats_kernel(const float* __restrict__ logits, const LT* __
 }
 
 // one block: loss scalar + per-(n,c) dp coefficients (dp = a*t + b) + ce scale
-// 256 threads.  Phase 1: wave w sums quantity (n, q) over the chunks (lanes
+// 1024 threads.  Phase 1: wave w sums quantity (n, q) over the chunks (lanes
 // stride the chunks, fixed fp64 shuffle tree).  Phase 2: thread e = (n, c)
 // forms the region term and its gradient coefficients.  Phase 3: thread 0
 // adds the N*C region terms and the CE sums in index order.
@@ -311,8 +445,8 @@ __global__ void loss_finalize_kernel(const float* __restrict__ part, int N, int 
                                      float* __restrict__ loss_out, float* __restrict__ coef) {
   extern __shared__ double S[];           // [N*nv] sums, then [N*C] region terms
   const int nv = 3 * C + 2;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int pr = wave; pr < N * nv; pr += 4) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
+  for (int pr = wave; pr < N * nv; pr += nwave) {
     const int n = pr / nv, q = pr - n * nv;
     double a = 0.0;
     for (int k = lane; k < nchunk; k += 64) a += part[((long long)n * nchunk + k) * nv + q];
@@ -363,49 +497,70 @@ __global__ void loss_finalize_kernel(const float* __restrict__ part, int N, int 
 }
 
 // dlogits = gout * [ p*(dp - sum p dp) + ce_scale * w_y * (p - t) ]
-template <typename LT>
-__global__ void loss_bwd_kernel(const float* __restrict__ logits, const LT* __restrict__ labels, int C, long long V,
+template <typename LT, int CC>
+__global__ __launch_bounds__(256) void loss_bwd_kernel(const float* __restrict__ logits, const LT* __restrict__ labels, int Crt, long long V,
                                 int N, LossCfg cfg, const float* __restrict__ coef, const float* __restrict__ gout,
                                 float gconst, float* __restrict__ dlogits) {
+  // CC > 0: class count known at compile time (U voxels in flight); CC = 0: runtime C, one voxel at a time
+  const int C = CC > 0 ? CC : Crt;
+  constexpr int NC = CC > 0 ? CC : CMAX;
   const long long total = (long long)N * V;
   const float g = gout ? gout[0] * gconst : gconst;
   const float ces = coef[2 * N * C];
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
+  // U voxels per thread (i, i + S, ...): logits and labels of all U loaded before any is consumed
+  constexpr int U = CC > 0 ? 4 : 1;
+  const long long S = (long long)gridDim.x * blockDim.x;
+  for (long long ib = (long long)blockIdx.x * blockDim.x + threadIdx.x; ib < total; ib += U * S) {
+  float zu[U][NC];
+  int yu[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long i = ib + u * S;
+    if (i < total) {
+      const long long n = i / V, v = i - n * V;
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (c < C) zu[u][c] = logits[(n * C + c) * V + v];
+      yu[u] = (int)labels[i];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long i = ib + u * S;
+    if (i >= total) break;
     const long long n = i / V, v = i - n * V;
-    const float* L = logits + n * C * V;
-    float z[CMAX], p[CMAX];
+    float z[NC], p[NC];
     float mx = -INFINITY;
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c)
+    for (int c = 0; c < NC; ++c)
       if (c < C) {
-        z[c] = L[c * V + v];
+        z[c] = zu[u][c];
         mx = fmaxf(mx, z[c]);
       }
     float se = 0.f;
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c)
+    for (int c = 0; c < NC; ++c)
       if (c < C) {
         p[c] = expf(z[c] - mx);
         se += p[c];
       }
     const float inv = 1.f / se;
-    const int y = (int)labels[i];
+    const int y = yu[u];
     float wy = cfg.cw ? cfg.cw[y] : 1.f;
     if (cfg.type == 2) {   // focal: d f_i / d ce_i = gamma (1-pt)^(gamma-1) pt ce_i + (1-pt)^gamma, ce_i = w_y (lse - z_y)
       float zy = 0.f;
 #pragma unroll
-      for (int c = 0; c < CMAX; ++c)
+      for (int c = 0; c < NC; ++c)
         if (c < C && c == y) zy = z[c];
       const float cei = wy * (mx + logf(se) - zy);
       const float pt = expf(-cei), q = 1.f - pt, gm = cfg.alpha;
       const float dfd = (q > 0.f ? gm * powf(q, gm - 1.f) * pt * cei : 0.f) + powf(q, gm);
       wy *= dfd;
     }
-    float dp[CMAX];
+    float dp[NC];
     float s = 0.f;
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c)
+    for (int c = 0; c < NC; ++c)
       if (c < C) {
         p[c] *= inv;
         const float t = c == y ? 1.f : 0.f;
@@ -414,12 +569,13 @@ __global__ void loss_bwd_kernel(const float* __restrict__ logits, const LT* __re
         s = fmaf(p[c], dp[c], s);
       }
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c)
+    for (int c = 0; c < NC; ++c)
       if (c < C) {
         const float t = c == y ? 1.f : 0.f;
         const float d = p[c] * (dp[c] - s) + ces * wy * (p[c] - t);
         dlogits[(n * C + c) * V + v] = g * d;
       }
+  }
   }
 }
 
@@ -535,6 +691,25 @@ int mmseg_head_fwd(const void* x, int ldx, int Cin, const float* W, const float*
                    long long V, float* logits, int dtype, void* stream) {
   MMSEG_REQUIRE(C >= 1 && C <= CMAX && Cin % 8 == 0, "head: 1 <= C <= %d, Cin%%8 == 0", CMAX);
   hipStream_t s = (hipStream_t)stream;
+  const int ugrid = (int)ceil_div((long long)N * V, 256LL * 4);
+  auto run_u = [&](auto tag, auto cg_c, auto cc_c) -> bool {
+    using T = decltype(tag);
+    constexpr int CG = decltype(cg_c)::value, CC = decltype(cc_c)::value;
+    if (Cin != CG * 8 || C != CC) return false;
+    hipLaunchKernelGGL((head_fwd_u_kernel<T, CG, CC>), dim3(ugrid), dim3(256), 0, s, (const T*)x, ldx, W, b, dscale,
+                       V, N, logits);
+    return true;
+  };
+  // the configs' heads: 32 (UNet / DualEncoder) or 48 (SwinUNETR fs=48) input channels, 3 / 6 / 7 classes
+  auto try_cc = [&](auto tag, auto cg_c) {
+    return run_u(tag, cg_c, std::integral_constant<int, 3>{}) || run_u(tag, cg_c, std::integral_constant<int, 6>{}) ||
+           run_u(tag, cg_c, std::integral_constant<int, 7>{});
+  };
+  auto try_u = [&](auto tag) {
+    return try_cc(tag, std::integral_constant<int, 4>{}) || try_cc(tag, std::integral_constant<int, 6>{});
+  };
+  if (ldx % 8 == 0 && (dtype == MMSEG_BF16 ? try_u(bf16_t{}) : try_u(float{})))
+    return mmseg::check_launch("head_fwd");
   const int grid = grid_for((long long)N * V);
   const size_t shm = (size_t)C * Cin * sizeof(float);
   if (dtype == MMSEG_BF16)
@@ -601,16 +776,23 @@ int mmseg_loss_fwd(const float* logits, const void* labels, int label_bytes, int
   float* part = ws;
   float* coef = ws + (long long)N * nch * (3 * C + 2);
   hipStream_t s = (hipStream_t)stream;
-  if (label_bytes == 8)
-    hipLaunchKernelGGL(loss_stats_kernel<int64_t>, dim3(nch, N), dim3(256), 0, s, logits, (const int64_t*)labels, C, V,
-                       vpc, cfg, part);
-  else
-    hipLaunchKernelGGL(loss_stats_kernel<uint8_t>, dim3(nch, N), dim3(256), 0, s, logits, (const uint8_t*)labels, C, V,
-                       vpc, cfg, part);
+  auto stats = [&](auto lt, auto cc) {
+    using LT = decltype(lt);
+    hipLaunchKernelGGL((loss_stats_kernel<LT, decltype(cc)::value>), dim3(nch, N), dim3(256), 0, s, logits,
+                       (const LT*)labels, C, V, vpc, cfg, part);
+  };
+  auto stats_c = [&](auto lt) {
+    if (C == 3) stats(lt, std::integral_constant<int, 3>{});
+    else if (C == 6) stats(lt, std::integral_constant<int, 6>{});
+    else if (C == 7) stats(lt, std::integral_constant<int, 7>{});
+    else stats(lt, std::integral_constant<int, 0>{});
+  };
+  if (label_bytes == 8) stats_c(int64_t{});
+  else stats_c(uint8_t{});
   if (mmseg::check_launch("loss_stats")) return 1;
   const size_t shm = sizeof(double) * ((size_t)N * (3 * C + 2) + (size_t)N * C);
   MMSEG_REQUIRE(shm <= 64 * 1024, "loss: batch too large for the finalize pass (N=%d, C=%d)", N, C);
-  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), shm, s, part, N, C, nch, cfg, loss_out, coef);
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), shm, s, part, N, C, nch, cfg, loss_out, coef);
   return mmseg::check_launch("loss_finalize");
 }
 
@@ -624,13 +806,21 @@ int mmseg_loss_bwd(const float* logits, const void* labels, int label_bytes, int
   const int nch = loss_chunks(V, &vpc);
   const float* coef = ws + (long long)N * nch * (3 * C + 2);
   hipStream_t s = (hipStream_t)stream;
-  const int grid = grid_for((long long)N * V);
-  if (label_bytes == 8)
-    hipLaunchKernelGGL(loss_bwd_kernel<int64_t>, dim3(grid), dim3(256), 0, s, logits, (const int64_t*)labels, C, V, N,
-                       cfg, coef, gout, gconst, dlogits);
-  else
-    hipLaunchKernelGGL(loss_bwd_kernel<uint8_t>, dim3(grid), dim3(256), 0, s, logits, (const uint8_t*)labels, C, V, N,
-                       cfg, coef, gout, gconst, dlogits);
+  auto bwd = [&](auto lt, auto cc) {
+    using LT = decltype(lt);
+    constexpr int CC = decltype(cc)::value;
+    const int grid = grid_for(CC > 0 ? ceil_div((long long)N * V, 4) : (long long)N * V);
+    hipLaunchKernelGGL((loss_bwd_kernel<LT, CC>), dim3(grid), dim3(256), 0, s, logits, (const LT*)labels, C, V, N, cfg,
+                       coef, gout, gconst, dlogits);
+  };
+  auto bwd_c = [&](auto lt) {
+    if (C == 3) bwd(lt, std::integral_constant<int, 3>{});
+    else if (C == 6) bwd(lt, std::integral_constant<int, 6>{});
+    else if (C == 7) bwd(lt, std::integral_constant<int, 7>{});
+    else bwd(lt, std::integral_constant<int, 0>{});
+  };
+  if (label_bytes == 8) bwd_c(int64_t{});
+  else bwd_c(uint8_t{});
   return mmseg::check_launch("loss_bwd");
 }
 

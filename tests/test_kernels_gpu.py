@@ -248,14 +248,17 @@ def test_instnorm_relu_maxpool(dev, dtype, C, shape, small_v, monkeypatch):
     assert rel(from_ndhwc(dxa.buf, N, C, D, H, W), xd.grad) < tol
 
 
+@pytest.mark.parametrize("shape", [(2, 4, 6, 8), (2, 16, 24, 20), (1, 9, 11, 13)])
 @pytest.mark.parametrize("dtype", DTYPES)
-def test_head(dev, dtype):
+def test_head(dev, dtype, shape):
+    """Head fwd/bwd vs fp64 conv3d; the larger shapes span several blocks of the 4-voxel-per-thread kernels
+    (and a ragged tail: 1287 voxels)."""
     torch.manual_seed(1)
     conv = nn.Conv3d(32, 6, 1).to(dev)
     rt = Runtime(dev, dtype)
     flat = FlatParams(list(conv.parameters()))
     head = Head(rt, conv, flat)
-    N, D, H, W = 2, 4, 6, 8
+    N, D, H, W = shape
     x = torch.randn(N, 32, D, H, W, device=dev)
     xa = _act(x, dtype)
     logits = torch.empty(N, 6, D, H, W, device=dev)
