@@ -316,6 +316,10 @@ int mmseg_window_norm(float* out, int N, int C, int D, int H, int W, const float
  * (batch["image"] as consumed by the first Conv3d, unet.py:181 / dual_encoder.py:133). */
 int mmseg_pack_input(const float* x, int Ctot, int c0, int cnt, int N, long long V, void* out, int dtype,
                      void* stream);
+/* Same channels packed without padding, (n*V + v)*cnt + c: the stem's input (mmseg_stem_* with ldx = cnt)
+ * reads 2*cnt bytes per voxel instead of 16. */
+int mmseg_pack_input_compact(const float* x, int Ctot, int c0, int cnt, int N, long long V, void* out, int dtype,
+                             void* stream);
 /* Dropout3d scale + 1x1 out_conv -> NCDHW fp32 logits (unet.py:195-196). */
 int mmseg_head_fwd(const void* x, int ldx, int Cin, const float* W, const float* b, const float* dscale, int C, int N,
                    long long V, float* logits, int dtype, void* stream);

@@ -35,6 +35,18 @@ __global__ void pack_input_kernel(const float* __restrict__ x, int Ctot, int c0,
   }
 }
 
+// compact variant for the stem: out[(n*V + v)*cnt + c], no channel padding
+template <typename T>
+__global__ void pack_input_compact_kernel(const float* __restrict__ x, int Ctot, int c0, int cnt, long long V, int N,
+                                          T* __restrict__ out) {
+  const long long total = (long long)N * V;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long n = i / V, v = i - n * V;
+    for (int c = 0; c < cnt; ++c) out[i * cnt + c] = from_f<T>(x[(n * Ctot + c0 + c) * V + v]);
+  }
+}
+
 // ----------------------------------------------------------------- head
 // logits[n][c][v] = b[c] + sum_ci W[c][ci] * s[n][ci] * x[n,v,ci]
 template <typename T>
@@ -685,6 +697,20 @@ int mmseg_pack_input(const float* x, int Ctot, int c0, int cnt, int N, long long
   else
     hipLaunchKernelGGL(pack_input_kernel<float>, dim3(grid), dim3(256), 0, s, x, Ctot, c0, cnt, V, N, (float*)out);
   return mmseg::check_launch("pack_input");
+}
+
+int mmseg_pack_input_compact(const float* x, int Ctot, int c0, int cnt, int N, long long V, void* out, int dtype,
+                             void* stream) {
+  MMSEG_REQUIRE(cnt >= 1 && cnt <= 4, "pack_input_compact: 1..4 channels (got %d)", cnt);
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = grid_for((long long)N * V);
+  if (dtype == MMSEG_BF16)
+    hipLaunchKernelGGL(pack_input_compact_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, x, Ctot, c0, cnt, V, N,
+                       (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(pack_input_compact_kernel<float>, dim3(grid), dim3(256), 0, s, x, Ctot, c0, cnt, V, N,
+                       (float*)out);
+  return mmseg::check_launch("pack_input_compact");
 }
 
 int mmseg_head_fwd(const void* x, int ldx, int Cin, const float* W, const float* b, const float* dscale, int C, int N,

@@ -55,10 +55,17 @@ __device__ __forceinline__ void stem_stage_halo(const StemArgs& g, T* Hl, long l
     const int hx = h % SHX, hy = (h / SHX) % SHY, hz = h / (SHX * SHY);
     const int z = z0 - 1 + hz, y = y0 - 1 + hy, x = x0 - 1 + hx;
     V8<T> v;
-    if ((unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W)
-      v.load(X + (nbase + z * HW + (long long)y * g.W + x) * g.ldx);
-    else
+    if ((unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W) {
+      const T* src = X + (nbase + z * HW + (long long)y * g.W + x) * g.ldx;
+      if (g.ldx == SCR) {
+        v.load(src);
+      } else {   // compact input (ldx = cr): only the real channels cross HBM
+        v.zero();
+        for (int c = 0; c < g.cr; ++c) v.set(c, (float)src[c]);
+      }
+    } else {
       v.zero();
+    }
     v.store(Hl + h * SCR);
   }
 }
@@ -264,7 +271,7 @@ int stem_kp(int cr) { return ((27 * cr + 31) / 32) * 32; }
 extern "C" {
 
 int mmseg_stem_ok(int cr, int Co, int D, int H, int W, int ldx, int ldy) {
-  return cr >= 1 && cr <= 4 && ldx == SCR && (Co == 16 || Co == 32) && ldy % 8 == 0 && D % SZ == 0 &&
+  return cr >= 1 && cr <= 4 && (ldx == SCR || ldx == cr) && (Co == 16 || Co == 32) && ldy % 8 == 0 && D % SZ == 0 &&
          H % SY == 0 && W % SX == 0;
 }
 

@@ -140,8 +140,8 @@ class UNetProgram:
         self.setup(N, D, H, W)
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
         self.pack()
-        L.mmseg_pack_input(ptr(x), Cx, 0, Cx, N, D * H * W, self.xin.ptr, code, s)
-        self.init.fwd(self.xin, self.level_out(0))
+        self.xin_v = _pack_input(self.rt, self.init, x, 0, Cx, self.xin)
+        self.init.fwd(self.xin_v, self.level_out(0))
         for l in range(1, self.L):
             prev = self.level_out(l - 1)
             d = self.dims[l - 1]
@@ -156,7 +156,7 @@ class UNetProgram:
         for l in range(self.L - 1, 0, -1):
             self.enc[l - 1].bwd(self.pooled[l], dy, self.pooled[l], accumulate)   # dp aliases pooled
             dy = DySpec(p1=self.dec.skip_slot(l - 1), pool_dy=self.pooled[l], pool_idx=self.idx[l])
-        self.init.bwd(self.xin, dy, None, accumulate)
+        self.init.bwd(self.xin_v, dy, None, accumulate)
 
 
 class DualEncoderProgram:
@@ -207,6 +207,7 @@ class DualEncoderProgram:
         dims = [(D >> l, H >> l, W >> l) for l in range(self.L)]
         self.dims = dims
         self.xin = [rt.act(N, *dims[0], 8) for _ in range(M)]
+        self.xin_v = list(self.xin)
         self.dec.setup(N, dims)
         # per-modality level outputs
         if self.fusion == "concat":
@@ -289,8 +290,8 @@ class DualEncoderProgram:
         blocks = self.encs[m]
         for l in range(lo, hi):
             if l == 0:
-                L.mmseg_pack_input(ptr(x), Cx, m, 1, N, D * H * W, self.xin[m].ptr, code, s)
-                blocks[0].fwd(self.xin[m], self.y[m][0])
+                self.xin_v[m] = _pack_input(self.rt, blocks[0], x, m, 1, self.xin[m])
+                blocks[0].fwd(self.xin_v[m], self.y[m][0])
                 continue
             prev = self.y[m][l - 1]
             L.mmseg_maxpool2_fwd(prev.ptr, prev.ld, self.pooled[m][l].ptr, self.pooled[m][l].ld,
@@ -359,7 +360,7 @@ class DualEncoderProgram:
                 if l > 0:
                     blk.bwd(self.pooled[m][l], dy, self.pooled[m][l], accumulate)
                 else:
-                    blk.bwd(self.xin[m], dy, None, accumulate)
+                    blk.bwd(self.xin_v[m], dy, None, accumulate)
 
 
     def _encoders_bwd_streams(self, accumulate: bool):
@@ -380,7 +381,7 @@ class DualEncoderProgram:
                 if l > 0:
                     blk.bwd(self.pooled[m][l], dy, self.pooled[m][l], accumulate)
                 else:
-                    blk.bwd(self.xin[m], dy, None, accumulate)
+                    blk.bwd(self.xin_v[m], dy, None, accumulate)
 
         for m in range(M):                           # small levels: modality m on stream m
             with self._on(streams, m):
@@ -398,3 +399,16 @@ def _ptr_array(ptrs):
 
 def _int_array(vals):
     return (ctypes.c_int * len(vals))(*vals)
+
+
+def _pack_input(rt, block, x: torch.Tensor, c0: int, cnt: int, xin: Act) -> Act:
+    """Pack channels [c0, c0+cnt) of the NCDHW input for `block`'s first conv.  When that conv takes the stem
+    path (stem.hip) the channels are packed without padding into the same buffer (ld = cnt), so the stem's
+    halo reads move 2*cnt bytes per voxel instead of 16; otherwise the 8-channel engine layout."""
+    N, Ctot, D, H, W = x.shape
+    xc = Act(xin.buf, 0, cnt, cnt, xin.N, xin.D, xin.H, xin.W)
+    if os.environ.get("MMSEG_STEM_COMPACT", "1") != "0" and block.c1._stem(xc, block.Co):
+        rt.lib.mmseg_pack_input_compact(ptr(x), Ctot, c0, cnt, N, D * H * W, xc.ptr, rt.code, rt.stream)
+        return xc
+    rt.lib.mmseg_pack_input(ptr(x), Ctot, c0, cnt, N, D * H * W, xin.ptr, rt.code, rt.stream)
+    return xin
