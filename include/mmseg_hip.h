@@ -254,6 +254,12 @@ int mmseg_gelu_fwd(const void* h, void* y, long long n, int dtype, void* stream)
 int mmseg_gelu_bwd(const void* h, const void* dy, void* dh, long long n, int dtype, void* stream);
 /* out = a + b (contiguous, n % 8 == 0): the MLP residual of SwinTransformerBlock. */
 int mmseg_add(const void* a, const void* b, void* out, long long n, int dtype, void* stream);
+/* nn.Dropout(p) at MONAI SwinUNETR's drop_rate sites (swin_unetr.py:87 drop_rate -> pos_drop,
+ * WindowAttention proj_drop, MLPBlock drop1/drop2).  y = keep ? x / (1 - p) : 0 over a [rows][C] buffer
+ * (in place allowed), keep from a counter hash of (seed, element index) — flat, or NCDHW order when ncdhw
+ * (rows = N * V).  The backward is the same call on the gradient with the same seed. */
+int mmseg_dropout(const void* x, void* y, long long rows, int C, long long V, int ncdhw, float p, long long seed,
+                  int dtype, void* stream);
 /* F.pad to the padded grid (Dp, Hp, Wp) + torch.roll(-s) + window_partition -> dst [B*nW][w0*w1*w2][C].
  * window_reverse: the inverse (window_reverse + roll(+s) + crop) onto the real grid, plus add_src
  * (the block's shortcut; NULL: none).  Also the backward of each other. */

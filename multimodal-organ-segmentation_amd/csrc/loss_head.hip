@@ -352,7 +352,16 @@ struct LossCfg {
   const float* cw;      // CE class weights [C] or null
 };
 
-// per (n, chunk): [P_c][I_c][T_c] (3C) + ce_num + ce_den
+// Label validity (the reference raises in F.one_hot / cross_entropy on a label outside [0, C)): such a
+// voxel contributes nothing and is counted; the finalize pass then makes the loss NaN and publishes the
+// count at coef[2NC+1] for the host to raise on.  Pure CE (region weight 0) skips torch's default
+// ignore_index -100 without counting it, as nn.CrossEntropyLoss does.
+__device__ __forceinline__ int label_state(int y, int C, const LossCfg& cfg) {
+  if ((unsigned)y < (unsigned)C) return 0;                 // valid
+  return (y == -100 && cfg.type == 0 && cfg.dice_w == 0.f) ? 1 : 2;   // 1 = ignored, 2 = invalid
+}
+
+// per (n, chunk): [P_c][I_c][T_c] (3C) + ce_num + ce_den + invalid-label count
 template <typename LT, int CC>
 __global__ __launch_bounds__(256) void loss_stats_kernel(const float* __restrict__ logits, const LT* __restrict__ labels, int Crt,
                                   long long V, long long vpc, LossCfg cfg, float* __restrict__ part) {
@@ -363,7 +372,7 @@ __global__ __launch_bounds__(256) void loss_stats_kernel(const float* __restrict
   float P[NC], I[NC], Tc[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) P[c] = I[c] = Tc[c] = 0.f;
-  float ce = 0.f, cden = 0.f;
+  float ce = 0.f, cden = 0.f, bad = 0.f;
   const long long v0 = (long long)chunk * vpc;
   long long v1 = v0 + vpc;
   if (v1 > V) v1 = V;
@@ -386,6 +395,12 @@ __global__ __launch_bounds__(256) void loss_stats_kernel(const float* __restrict
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (vb + u * blockDim.x >= v1) break;
+    const int y = yu[u];
+    const int ls = label_state(y, C, cfg);
+    if (ls) {
+      bad += ls == 2 ? 1.f : 0.f;
+      continue;
+    }
     float z[NC];
     float mx = -INFINITY;
 #pragma unroll
@@ -399,7 +414,6 @@ __global__ __launch_bounds__(256) void loss_stats_kernel(const float* __restrict
     for (int c = 0; c < NC; ++c)
       if (c < C) se += expf(z[c] - mx);
     const float lse = mx + logf(se);
-    const int y = yu[u];
     const float inv = 1.f / se;
     float zy = 0.f;
 #pragma unroll
@@ -425,7 +439,7 @@ __global__ __launch_bounds__(256) void loss_stats_kernel(const float* __restrict
     }
   }
   }
-  __shared__ float red[4][3 * CMAX + 2];
+  __shared__ float red[4][3 * CMAX + 3];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int c = 0; c < C; ++c) {
     float a = wave_sum(P[c]), b = wave_sum(I[c]), d = wave_sum(Tc[c]);
@@ -436,14 +450,15 @@ __global__ __launch_bounds__(256) void loss_stats_kernel(const float* __restrict
     }
   }
   {
-    float a = wave_sum(ce), b = wave_sum(cden);
+    float a = wave_sum(ce), b = wave_sum(cden), d = wave_sum(bad);
     if (lane == 0) {
       red[wave][3 * C] = a;
       red[wave][3 * C + 1] = b;
+      red[wave][3 * C + 2] = d;
     }
   }
   __syncthreads();
-  const int nv = 3 * C + 2;
+  const int nv = 3 * C + 3;
   for (int k = threadIdx.x; k < nv; k += blockDim.x)
     part[((long long)n * nchunk + chunk) * nv + k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
 }
@@ -456,7 +471,7 @@ __global__ __launch_bounds__(256) void loss_stats_kernel(const float* __restrict
 __global__ void loss_finalize_kernel(const float* __restrict__ part, int N, int C, int nchunk, LossCfg cfg,
                                      float* __restrict__ loss_out, float* __restrict__ coef) {
   extern __shared__ double S[];           // [N*nv] sums, then [N*C] region terms
-  const int nv = 3 * C + 2;
+  const int nv = 3 * C + 3;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
   for (int pr = wave; pr < N * nv; pr += nwave) {
     const int n = pr / nv, q = pr - n * nv;
@@ -496,15 +511,17 @@ __global__ void loss_finalize_kernel(const float* __restrict__ part, int N, int 
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    double r = 0.0, ce = 0.0, den = 0.0;
+    double r = 0.0, ce = 0.0, den = 0.0, bad = 0.0;
     for (int e = 0; e < N * C; ++e) r += R[e];
     for (int n = 0; n < N; ++n) {
       ce += S[n * nv + 3 * C];
       den += S[n * nv + 3 * C + 1];
+      bad += S[n * nv + 3 * C + 2];
     }
     const double lv = cfg.dice_w * (r / nterms) + cfg.ce_w * (ce / den);
-    loss_out[0] = (float)lv;
+    loss_out[0] = bad > 0.0 ? __builtin_nanf("") : (float)lv;
     coef[2 * N * C] = (float)(cfg.ce_w / den);   // CE gradient scale
+    coef[2 * N * C + 1] = (float)bad;            // labels outside [0, C): the host raises on a non-zero count
   }
 }
 
@@ -541,6 +558,13 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(const float* __restrict__
     const long long i = ib + u * S;
     if (i >= total) break;
     const long long n = i / V, v = i - n * V;
+    const int y = yu[u];
+    if (label_state(y, C, cfg)) {     // ignored / invalid label: no gradient through this voxel
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (c < C) dlogits[(n * C + c) * V + v] = 0.f;
+      continue;
+    }
     float z[NC], p[NC];
     float mx = -INFINITY;
 #pragma unroll
@@ -557,7 +581,6 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(const float* __restrict__
         se += p[c];
       }
     const float inv = 1.f / se;
-    const int y = yu[u];
     float wy = cfg.cw ? cfg.cw[y] : 1.f;
     if (cfg.type == 2) {   // focal: d f_i / d ce_i = gamma (1-pt)^(gamma-1) pt ce_i + (1-pt)^gamma, ce_i = w_y (lse - z_y)
       float zy = 0.f;
@@ -787,7 +810,7 @@ int mmseg_head_bwd(const void* x, int ldx, int Cin, const float* W, const float*
 long long mmseg_loss_ws_floats(int N, int C, long long V) {
   long long vpc;
   int nch = loss_chunks(V, &vpc);
-  return (long long)N * nch * (3 * C + 2) + 2LL * N * C + 1;
+  return (long long)N * nch * (3 * C + 3) + 2LL * N * C + 2;
 }
 
 // label_bytes: 8 (int64, the reference's dtype) or 1 (uint8)
@@ -800,7 +823,7 @@ int mmseg_loss_fwd(const float* logits, const void* labels, int label_bytes, int
   long long vpc;
   const int nch = loss_chunks(V, &vpc);
   float* part = ws;
-  float* coef = ws + (long long)N * nch * (3 * C + 2);
+  float* coef = ws + (long long)N * nch * (3 * C + 3);
   hipStream_t s = (hipStream_t)stream;
   auto stats = [&](auto lt, auto cc) {
     using LT = decltype(lt);
@@ -816,7 +839,7 @@ int mmseg_loss_fwd(const float* logits, const void* labels, int label_bytes, int
   if (label_bytes == 8) stats_c(int64_t{});
   else stats_c(uint8_t{});
   if (mmseg::check_launch("loss_stats")) return 1;
-  const size_t shm = sizeof(double) * ((size_t)N * (3 * C + 2) + (size_t)N * C);
+  const size_t shm = sizeof(double) * ((size_t)N * (3 * C + 3) + (size_t)N * C);
   MMSEG_REQUIRE(shm <= 64 * 1024, "loss: batch too large for the finalize pass (N=%d, C=%d)", N, C);
   hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), shm, s, part, N, C, nch, cfg, loss_out, coef);
   return mmseg::check_launch("loss_finalize");
@@ -830,7 +853,7 @@ int mmseg_loss_bwd(const float* logits, const void* labels, int label_bytes, int
   LossCfg cfg{type, dice_w, ce_w, smooth, alpha, beta, include_bg, class_w};
   long long vpc;
   const int nch = loss_chunks(V, &vpc);
-  const float* coef = ws + (long long)N * nch * (3 * C + 2);
+  const float* coef = ws + (long long)N * nch * (3 * C + 3);
   hipStream_t s = (hipStream_t)stream;
   auto bwd = [&](auto lt, auto cc) {
     using LT = decltype(lt);

@@ -229,6 +229,41 @@ __global__ void add_kernel(const T* __restrict__ a, const T* __restrict__ b, T* 
   }
 }
 
+// ------------------------------------------------------------ dropout
+// nn.Dropout(p) of MONAI SwinUNETR's drop_rate sites (pos_drop, WindowAttention.proj_drop, MLPBlock
+// drop1 / drop2).  Counter-based: the element with hash index h is kept iff the top 32 bits of
+// splitmix64(seed + h * 0x9E3779B97F4A7C15) are >= thr = p * 2^32, and a kept element is scaled by
+// 1 / (1 - p).  The backward applies the same call (same seed) to the gradient, so no mask is stored.
+// h is the flat index of a [rows][C] channels-last buffer, or (ncdhw) the element's index in NCDHW order
+// with rows = N * V (pos_drop acts on patch_embed's NCDHW output).
+__device__ __forceinline__ unsigned int drop_hash(unsigned long long seed, unsigned long long h) {
+  unsigned long long z = seed + h * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (unsigned int)(z >> 32);
+}
+
+template <typename T>
+__global__ void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, long long n8, int C, long long V,
+                               int ncdhw, unsigned long long seed, unsigned int thr, float scale) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    V8<T> a;
+    a.load(x + i * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const long long e = i * 8 + j;
+      long long h = e;
+      if (ncdhw) {
+        const long long r = e / C, c = e - r * C, n = r / V, v = r - n * V;
+        h = (n * C + c) * V + v;
+      }
+      a.set(j, drop_hash(seed, (unsigned long long)h) >= thr ? a.get(j) * scale : 0.f);
+    }
+    a.store(y + i * 8);
+  }
+}
+
 // ------------------------------------------------------------ windows
 struct WinArgs {
   int B, D, H, W, C;        // real grid and channels
@@ -568,6 +603,24 @@ int mmseg_gelu_bwd(const void* h, const void* dy, void* dh, long long n, int dty
     hipLaunchKernelGGL(gelu_bwd_kernel<float>, dim3(grid_of(n / 8)), dim3(256), 0, s, (const float*)h,
                        (const float*)dy, (float*)dh, n / 8);
   return mmseg::check_launch("gelu_bwd");
+}
+
+int mmseg_dropout(const void* x, void* y, long long rows, int C, long long V, int ncdhw, float p, long long seed,
+                  int dtype, void* stream) {
+  MMSEG_REQUIRE(rows * C % 8 == 0 && C > 0 && p >= 0.f && p < 1.f && (!ncdhw || (V > 0 && rows % V == 0)),
+                "dropout: rows*C %% 8 == 0, 0 <= p < 1, rows a multiple of V");
+  hipStream_t s = (hipStream_t)stream;
+  const long long n8 = rows * C / 8;
+  const double t = (double)p * 4294967296.0;
+  const unsigned int thr = t >= 4294967295.0 ? 0xffffffffu : (unsigned int)t;
+  const float scale = (float)(1.0 / (1.0 - (double)p));
+  if (dtype == MMSEG_BF16)
+    hipLaunchKernelGGL(dropout_kernel<bf16_t>, dim3(grid_of(n8)), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, n8,
+                       C, V, ncdhw, (unsigned long long)seed, thr, scale);
+  else
+    hipLaunchKernelGGL(dropout_kernel<float>, dim3(grid_of(n8)), dim3(256), 0, s, (const float*)x, (float*)y, n8, C,
+                       V, ncdhw, (unsigned long long)seed, thr, scale);
+  return mmseg::check_launch("dropout");
 }
 
 int mmseg_add(const void* a, const void* b, void* out, long long n, int dtype, void* stream) {

@@ -2,8 +2,9 @@
 ROCm), one process per GPU.  The reference is single-process (SURVEY §0.2);
 this is new work whose oracle is "N ranks x B == 1 rank x N*B".
 
-  * sharding: rank r takes samples r, r+W, ... of each global batch
-    (DistributedSampler semantics) — see `shard_indices`;
+  * sharding: rank r takes samples r, r+W, ... of the index list padded by
+    wrap-around to a multiple of W (DistributedSampler semantics), so every
+    rank runs the same number of batches — see `shard_indices`;
   * gradients live in the engine's flat arena; `GradBuckets` splits it into
     ~bucket_mb buckets (reverse registration order = backward order) and
     all-reduces each bucket with ReduceOp.AVG as soon as the engine has
@@ -42,7 +43,16 @@ def init_from_env(backend: Optional[str] = None) -> int:
 
 
 def shard_indices(n_samples: int, r: int, w: int) -> List[int]:
-    return list(range(r, n_samples, w))
+    """torch DistributedSampler(shuffle=False) order: pad the index list by wrapping around to
+    ceil(n/W)*W, then rank r takes r, r+W, ...  Every rank gets the same count, so no rank runs
+    an extra train_step (which would wait forever in a gradient all-reduce)."""
+    if n_samples <= 0:
+        return []
+    total = -(-n_samples // w) * w
+    idx = list(range(n_samples))
+    while len(idx) < total:
+        idx += idx[:total - len(idx)]
+    return idx[r:total:w]
 
 
 class GradBuckets:
@@ -80,17 +90,23 @@ class GradBuckets:
     def _reduce(self, b: int):
         _, _, lo, hi = self.buckets[b]
         t = self.grad[lo:hi]
-        if dist.get_backend(self.group) == "nccl":
+        if self.grad.is_cuda:
             # The engine may write a bucket's gradients from several HIP streams (one per modality encoder):
             # the collective is issued from a dedicated stream that first waits for every contributing
-            # stream's last write, so no compute stream is blocked and no write is missed.
+            # stream's last write, so no compute stream is blocked and no write is missed.  The same path
+            # runs for RCCL and for gloo over device tensors (ranks sharing one GPU in the tests).
             if self.comm is None:
                 self.comm = torch.cuda.Stream(self.grad.device)
             for ev in self.events[b].values():
                 self.comm.wait_event(ev)
             with torch.cuda.stream(self.comm):
-                self.works.append(dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group, async_op=True))
-        else:  # gloo has no AVG
+                if dist.get_backend(self.group) == "nccl":
+                    op = dist.ReduceOp.AVG
+                else:                       # gloo has no AVG: pre-scale on the comm stream, then SUM
+                    t.div_(self.w)
+                    op = dist.ReduceOp.SUM
+                self.works.append(dist.all_reduce(t, op=op, group=self.group, async_op=True))
+        else:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
             t.div_(self.w)
 
@@ -110,10 +126,18 @@ class GradBuckets:
     def finish(self):
         if self.w == 1:
             return
-        for b, n in enumerate(self.pending):
-            if n > 0:          # a parameter the engine did not report: reduce anyway (correctness first)
-                self.pending[b] = 0
-                self._reduce(b)
+        late = [b for b, n in enumerate(self.pending) if n > 0]
+        if late and self.grad.is_cuda:
+            # writes to unreported parameters may still be queued on the current stream: the late
+            # collectives wait for everything issued on it so far
+            cur = torch.cuda.current_stream(self.grad.device)
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            for b in late:
+                self.events[b][cur.cuda_stream] = ev
+        for b in late:         # a parameter the engine did not report: reduce anyway (correctness first)
+            self.pending[b] = 0
+            self._reduce(b)
         for wk in self.works:
             wk.wait()      # makes the current (optimizer) stream wait for the collective
         self.reset()

@@ -168,6 +168,24 @@ class LN:
                                   int(add_dx), None, None, 0, None, self.rt.code, self.rt.stream)
 
 
+class Drop:
+    """nn.Dropout(drop_rate) at MONAI SwinUNETR's sites (pos_drop, proj_drop, MLP drop1 / drop2) on the
+    counter-hash kernel mmseg_dropout: each forward draws one seed per site from torch's CPU generator
+    (so torch.manual_seed fixes the masks) and the backward re-applies the same call to the gradient."""
+
+    def __init__(self, rt: Runtime, p: float):
+        self.rt, self.p = rt, float(p)
+
+    @staticmethod
+    def seed() -> int:
+        return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+    def __call__(self, src: torch.Tensor, dst: torch.Tensor, rows: int, C: int, seed: int, V: int = 1,
+                 ncdhw: bool = False):
+        self.rt.lib.mmseg_dropout(ptr(src), ptr(dst), rows, C, V, int(ncdhw), self.p, seed, self.rt.code,
+                                  self.rt.stream)
+
+
 class SwinBlockProg:
     """SwinTransformerBlock: x + attn(windows(LN1(x))), then + MLP(LN2(.))."""
 
@@ -203,9 +221,11 @@ class SwinBlockProg:
     def _empty(self, n):
         return torch.empty(int(n), dtype=self.rt.dtype, device=self.rt.device)
 
-    def fwd(self, x: torch.Tensor, geo) -> Tuple[torch.Tensor, dict]:
-        """x [N*d*h*w][C] (storage dtype) -> (out, saved state)."""
+    def fwd(self, x: torch.Tensor, geo, drop: Optional[Drop] = None) -> Tuple[torch.Tensor, dict]:
+        """x [N*d*h*w][C] (storage dtype) -> (out, saved state).  drop: the block's three dropout sites
+        (training with drop_rate > 0), else None."""
         rt, L, s, code, C = self.rt, self.rt.lib, self.rt.stream, self.rt.code, self.C
+        seeds = (Drop.seed(), Drop.seed(), Drop.seed()) if drop is not None else None
         N, d, h, w = geo["grid"]
         ws, (dp, hp, wp) = geo["ws"], geo["padded"]
         sh = geo["ss"] if self.shifted else (0, 0, 0)
@@ -235,6 +255,8 @@ class SwinBlockProg:
             O, P = self.core.core_fwd(qkv, B, Nw, mask, self.table, geo["index"])
         aw = self._empty(Mw * C)
         self.proj.fwd(O, C, Mw, aw, C)
+        if seeds:                         # WindowAttention.proj_drop over the [B*nW, N, C] windows
+            drop(aw, aw, Mw, C, seeds[0])
         xm = self._empty(M * C)
         L.mmseg_window_reverse(ptr(aw), N, d, h, w, C, *ws, *sh, dp, hp, wp, ptr(x), C, ptr(xm), C, code, s)
         del aw
@@ -245,12 +267,16 @@ class SwinBlockProg:
         self.fc1.fwd(ln2, C, M, hbuf, hdim)
         g = self._empty(M * hdim)
         L.mmseg_gelu_fwd(ptr(hbuf), ptr(g), M * hdim, code, s)
+        if seeds:                         # MLPBlock drop1 (after the activation)
+            drop(g, g, M, hdim, seeds[1])
         z = self._empty(M * C)
         self.fc2.fwd(g, hdim, M, z, C)
+        if seeds:                         # MLPBlock drop2 (after linear2)
+            drop(z, z, M, C, seeds[2])
         out = self._empty(M * C)
         L.mmseg_add(ptr(xm), ptr(z), ptr(out), M * C, code, s)
         st = dict(x=x, st1=st1, xw=xw, qkv=qkv, O=O, P=P, xm=xm, st2=st2, ln2=ln2, h=hbuf, g=g, B=B, Nw=Nw, Mw=Mw,
-                  M=M, sh=sh, fused=fused)
+                  M=M, sh=sh, fused=fused, drop=drop, seeds=seeds)
         return out, st
 
     def bwd(self, dout: torch.Tensor, st: dict, geo, accumulate: bool) -> torch.Tensor:
@@ -260,8 +286,16 @@ class SwinBlockProg:
         ws, (dp, hp, wp) = geo["ws"], geo["padded"]
         M, Mw, B, Nw, sh = st["M"], st["Mw"], st["B"], st["Nw"], st["sh"]
         hdim = self.fc1.Co
+        drop, seeds = st["drop"], st["seeds"]
+        dz = dout
+        if seeds:
+            dz = self._empty(M * C)
+            drop(dout, dz, M, C, seeds[2])
         dg = self._empty(M * hdim)
-        self.fc2.bwd(st["g"], hdim, dout, C, M, dg, hdim, accumulate)
+        self.fc2.bwd(st["g"], hdim, dz, C, M, dg, hdim, accumulate)
+        del dz
+        if seeds:
+            drop(dg, dg, M, hdim, seeds[1])
         L.mmseg_gelu_bwd(ptr(st["h"]), ptr(dg), ptr(dg), M * hdim, code, s)
         dln2 = self._empty(M * C)
         self.fc1.bwd(st["ln2"], C, dg, hdim, M, dln2, C, accumulate)
@@ -269,6 +303,8 @@ class SwinBlockProg:
         self.ln2.bwd(st["xm"], C, st["st2"], dln2, C, dout, C, M, True, accumulate)   # dout := d xm
         daw = self._empty(Mw * C)
         L.mmseg_window_partition(ptr(dout), C, N, d, h, w, C, *ws, *sh, dp, hp, wp, ptr(daw), code, s)
+        if seeds:
+            drop(daw, daw, Mw, C, seeds[0])
         dO = self._empty(Mw * C)
         self.proj.bwd(st["O"], C, daw, C, Mw, dO, C, accumulate)
         del daw
@@ -338,12 +374,12 @@ class SwinStageProg:
                         csr=(offs.to(torch.int32).to(dev), order.to(torch.int32).to(dev), self.table_rows))
         self.out_dims = tuple((s + 1) // 2 for s in (d, h, w))
 
-    def fwd(self, x: torch.Tensor):
+    def fwd(self, x: torch.Tensor, drop: Optional[Drop] = None):
         rt, L, C = self.rt, self.rt.lib, self.dim
         N, d, h, w = self.geo["grid"]
         self.saved = []
         for b in self.blocks:
-            x, st = b.fwd(x, self.geo)
+            x, st = b.fwd(x, self.geo, drop)
             self.saved.append(st)
         d2, h2, w2 = self.out_dims
         M2 = N * d2 * h2 * w2
@@ -528,6 +564,9 @@ class SwinUNETRProgram:
                     for k, c_in, c_out in ((5, 16 * fs, 8 * fs), (4, 8 * fs, 4 * fs), (3, 4 * fs, 2 * fs),
                                            (2, 2 * fs, fs), (1, fs, fs))]
         self.head = Head(rt, net.out.conv.conv, flat)
+        self.drop_rate = float(getattr(m, "drop_rate", 0.0))
+        self.drop = Drop(rt, self.drop_rate) if self.drop_rate > 0 else None
+        self.pos_seed = None
         self.shape = None
         self._packed = None
 
@@ -593,11 +632,22 @@ class SwinUNETRProgram:
         M0 = N * g[0][0] * g[0][1] * g[0][2]
         x0 = torch.empty(M0 * fs, dtype=rt.dtype, device=rt.device)
         self.embed.fwd(self.patches, self.kp, M0, x0, fs)
+        drop = self.drop if training else None
+        self.pos_seed = Drop.seed() if drop is not None else None
+        if drop is not None:              # SwinTransformer.pos_drop on patch_embed's NCDHW output
+            V0 = g[0][0] * g[0][1] * g[0][2]
+            drop(x0, x0, M0, fs, self.pos_seed, V=V0, ncdhw=True)
         xs = [x0]
         h = x0
         for st in self.stages:
-            h = st.fwd(h)
+            h = st.fwd(h, drop)
             xs.append(h)
+        # dropout seeds of this forward by site (the tests regenerate the masks from them)
+        self.drop_seeds = {"pos": self.pos_seed} if drop is not None else {}
+        if drop is not None:
+            for i, st in enumerate(self.stages):
+                for j, sv in enumerate(st.saved):
+                    self.drop_seeds[f"swinViT.layers{i + 1}.0.blocks.{j}."] = sv["seeds"]
         self.xs = xs
         self.pst = []
         for i in range(5):
@@ -651,5 +701,7 @@ class SwinUNETRProgram:
             if i > 0:
                 dx = self.stages[i - 1].bwd(dx, accumulate)
         M0 = N * g[0][0] * g[0][1] * g[0][2]
+        if self.pos_seed is not None:
+            self.drop(dx, dx, M0, fs, self.pos_seed, V=g[0][0] * g[0][1] * g[0][2], ncdhw=True)
         self.embed.bwd(self.patches, self.kp, dx, fs, M0, None, 0, accumulate)
         self.xs = None

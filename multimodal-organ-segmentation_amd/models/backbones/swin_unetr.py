@@ -204,10 +204,11 @@ class PatchEmbed(nn.Module):
 
 class SwinTransformer(nn.Module):
     def __init__(self, in_chans: int, embed_dim: int, window_size: Sequence[int], depths: Sequence[int],
-                 num_heads: Sequence[int]):
+                 num_heads: Sequence[int], drop_rate: float = 0.0):
         super().__init__()
         self.patch_embed = PatchEmbed(2, in_chans, embed_dim)
-        self.pos_drop = nn.Dropout(p=0.0)
+        self.pos_drop = nn.Dropout(p=drop_rate)   # applied by the engine (engine/swin.py Drop), as are the
+        # blocks' proj_drop / MLP drop1 / drop2 of the same rate
         for i in range(4):
             layers = nn.ModuleList([BasicLayer(embed_dim * 2 ** i, depths[i], num_heads[i], window_size)])
             setattr(self, f"layers{i + 1}", layers)
@@ -217,11 +218,12 @@ class SwinUNETRNet(nn.Module):
     """monai.networks.nets.SwinUNETR module tree (v1.3, use_v2=False, downsample="merging")."""
 
     def __init__(self, in_channels: int, out_channels: int, feature_size: int, depths: Sequence[int],
-                 num_heads: Sequence[int], window_size: Sequence[int] = (7, 7, 7), normalize: bool = True):
+                 num_heads: Sequence[int], window_size: Sequence[int] = (7, 7, 7), normalize: bool = True,
+                 drop_rate: float = 0.0):
         super().__init__()
         fs = feature_size
         self.normalize = normalize
-        self.swinViT = SwinTransformer(in_channels, fs, window_size, depths, num_heads)
+        self.swinViT = SwinTransformer(in_channels, fs, window_size, depths, num_heads, drop_rate)
         self.encoder1 = UnetrBasicBlock(in_channels, fs)
         self.encoder2 = UnetrBasicBlock(fs, fs)
         self.encoder3 = UnetrBasicBlock(2 * fs, 2 * fs)
@@ -239,7 +241,8 @@ class SwinUNETR(nn.Module):
     """Reference SwinUNETR wrapper (swin_unetr.py:20-176): same constructor, `self.model`, forward(x,
     return_features), load_pretrained, get_encoder / get_decoder, encoder_channels.  The network runs as ONE
     HIP program (engine/swin.py).  Engine limits (raise otherwise): patch 2, 3-D, normalize=True,
-    downsample="merging", use_v2=False, dropout / attention dropout / drop-path 0, feature_size / 3 heads
+    downsample="merging", use_v2=False, attention dropout / drop-path 0 (drop_rate, the reference's head.dropout,
+    is supported: pos_drop, proj_drop and the MLP dropouts on the engine), feature_size / 3 heads
     -> head_dim a multiple of 8 (feature_size 24, 48, ...)."""
 
     def __init__(self, img_size: Tuple[int, int, int] = (96, 96, 96), in_channels: int = 1, out_channels: int = 8,
@@ -249,11 +252,14 @@ class SwinUNETR(nn.Module):
                  spatial_dims: int = 3, downsample: str = "merging", use_v2: bool = False,
                  pretrained: str = None, **kwargs):
         super().__init__()
-        if (norm_name != "instance" or drop_rate or attn_drop_rate or dropout_path_rate or not normalize
+        if (norm_name != "instance" or attn_drop_rate or dropout_path_rate or not normalize
                 or spatial_dims != 3 or downsample != "merging" or use_v2):
-            raise NotImplementedError("SwinUNETR engine: norm 'instance', no dropout / drop-path, normalize=True, "
-                                      "3-D, downsample='merging', use_v2=False (the reference's build_swin_unetr "
-                                      "defaults)")
+            raise NotImplementedError("SwinUNETR engine: norm 'instance', no attention dropout / drop-path, "
+                                      "normalize=True, 3-D, downsample='merging', use_v2=False (the reference's "
+                                      "build_swin_unetr defaults; drop_rate is supported)")
+        if not 0.0 <= drop_rate < 1.0:
+            raise ValueError(f"drop_rate must be in [0, 1), got {drop_rate}")
+        self.drop_rate = float(drop_rate)
         if feature_size % 12:
             raise ValueError("feature_size should be divisible by 12 (MONAI SwinUNETR)")
         if any(s % 32 for s in img_size):
@@ -270,7 +276,8 @@ class SwinUNETR(nn.Module):
         self.num_heads = tuple(num_heads)
         self.depths = tuple(depths)
         self.window_size = (7, 7, 7)
-        self.model = SwinUNETRNet(in_channels, out_channels, feature_size, depths, num_heads, self.window_size)
+        self.model = SwinUNETRNet(in_channels, out_channels, feature_size, depths, num_heads, self.window_size,
+                                  drop_rate=self.drop_rate)
         self.engine_dtype = torch.float32
         if pretrained is not None:
             self.load_pretrained(pretrained)

@@ -21,7 +21,7 @@ TYPE_DICE, TYPE_TVERSKY, TYPE_FOCAL = 0, 1, 2
 
 class _SegLoss(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, logits, target, spec, class_w):
+    def forward(ctx, logits, target, spec, class_w, owner):
         if logits.device.type != "cuda":
             raise RuntimeError("HIP loss kernels need ROCm tensors; there is no CPU path")
         logits = logits.float().contiguous()
@@ -39,6 +39,7 @@ class _SegLoss(torch.autograd.Function):
         args = (N, C, V, spec["type"], spec["dice_w"], spec["ce_w"], spec["smooth"], spec["alpha"], spec["beta"],
                 int(spec["include_bg"]), ptr(cw))
         L.mmseg_loss_fwd(ptr(logits), ptr(target), target.element_size(), *args, ptr(loss), ptr(ws), stream_handle())
+        owner.__dict__["_last_ws"] = ws       # its last float = count of labels outside [0, C)
         ctx.save_for_backward(logits, target, ws, cw if cw is not None else torch.empty(0))
         ctx.args = args
         ctx.has_cw = cw is not None
@@ -52,17 +53,31 @@ class _SegLoss(torch.autograd.Function):
         g = gout.float().contiguous()
         lib().mmseg_loss_bwd(ptr(logits), ptr(target), target.element_size(), *ctx.args, ptr(g), 1.0, ptr(dlogits),
                              ptr(ws), stream_handle())
-        return dlogits, None, None, None
+        return dlogits, None, None, None, None
 
 
 class _HipLoss(nn.Module):
+    """Labels outside [0, C) make the reference raise inside F.one_hot / cross_entropy.  The kernels cannot
+    raise without a host sync, so such voxels are skipped, counted on the device and turn the loss into NaN;
+    `invalid_labels()` (one sync) reads the count of the last call and `check_labels()` raises on it."""
+
     def _spec(self) -> Dict[str, Any]:
         raise NotImplementedError
+
+    def invalid_labels(self) -> int:
+        ws = self.__dict__.get("_last_ws")
+        return 0 if ws is None else int(ws[-1].item())   # coef[2NC+1], the workspace's last float
+
+    def check_labels(self) -> None:
+        n = self.invalid_labels()
+        if n:
+            raise RuntimeError(f"{n} target voxels hold a class index outside [0, num_classes) "
+                               "(the reference raises in F.one_hot / cross_entropy on such labels)")
 
     def forward(self, pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
         if getattr(self, "reduction", "mean") != "mean":
             raise NotImplementedError("HIP losses implement reduction='mean' (the reference's default)")
-        return _SegLoss.apply(pred, target, self._spec(), getattr(self, "class_weights", None))
+        return _SegLoss.apply(pred, target, self._spec(), getattr(self, "class_weights", None), self)
 
 
 class DiceLoss(_HipLoss):

@@ -16,15 +16,17 @@ from .._lib import lib, ptr, stream_handle
 
 
 class DiceMetric:
-    def __init__(self, num_classes: int, include_background: bool = False, reduction: str = "mean"):
+    def __init__(self, num_classes: int, include_background: bool = False, reduction: str = "mean",
+                 device: Optional[torch.device] = None):
         self.num_classes = num_classes
         self.include_background = include_background
         self.reduction = reduction
+        self.device = device       # accumulators live here from the start (a rank with no batches still packs them)
         self.reset()
 
     def reset(self) -> None:
-        self.intersection = torch.zeros(self.num_classes)
-        self.union = torch.zeros(self.num_classes)
+        self.intersection = torch.zeros(self.num_classes, device=self.device)
+        self.union = torch.zeros(self.num_classes, device=self.device)
         self.count = 0
         self._counts: Optional[torch.Tensor] = None
 

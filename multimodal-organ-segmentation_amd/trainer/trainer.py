@@ -150,7 +150,12 @@ class Trainer:
             self.optimizer.step()
             self.optimizer.zero_grad()
         out = loss.detach() * self.accumulation_steps
-        return out.item() if sync else out
+        if not sync:
+            return out
+        lv = out.item()
+        if lv != lv and hasattr(self.criterion, "check_labels"):
+            self.criterion.check_labels()      # NaN loss: raise if it came from out-of-range labels
+        return lv
 
     def _train_epoch(self) -> float:
         self.model.train()
@@ -167,9 +172,9 @@ class Trainer:
 
     def _validate(self) -> Tuple[float, Dict[str, float]]:
         self.model.eval()
-        dm = DiceMetric(num_classes=self.config["model"]["out_channels"])
+        dm = DiceMetric(num_classes=self.config["model"]["out_channels"], device=self.device)
         total = torch.zeros((), dtype=torch.float64, device=self.device)
-        n = len(self.val_loader)
+        n = 0
         with torch.no_grad():
             for batch in self.val_loader:
                 images = batch["image"].to(self.device, non_blocking=True)
@@ -177,14 +182,18 @@ class Trainer:
                 outputs = self.model(images)
                 total += self.criterion(outputs, labels).double()
                 dm.update_from_logits(outputs, labels)
+                n += 1
         if self.world > 1:
-            packed = torch.cat([total.view(1).float(), dm.intersection, dm.union])
+            # one all-reduce of [loss sum, batch count, I, U]: the real per-rank batch counts are summed,
+            # and a rank with no validation batches contributes zeros (its accumulators are on the device)
+            nb = torch.tensor([float(n)], device=self.device)
+            packed = torch.cat([total.view(1).float(), nb, dm.intersection, dm.union])
             ddp.allreduce_sum_(packed)
             C = dm.num_classes
             total = packed[0].double()
-            dm.intersection, dm.union = packed[1:1 + C], packed[1 + C:]
-            n *= self.world
-        return (total / n).item(), dm.compute()
+            n = int(round(packed[1].item()))
+            dm.intersection, dm.union = packed[2:2 + C], packed[2 + C:]
+        return (total / n).item() if n else float("nan"), dm.compute()
 
     def evaluate(self) -> Dict[str, float]:
         _, metrics = self._validate()

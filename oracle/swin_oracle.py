@@ -24,8 +24,9 @@ MONAI quirks kept on purpose (both are what MONAI 1.3 computes):
 """
 from __future__ import annotations
 
-from typing import Dict, List
+from typing import Callable, Dict, List, Optional
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -38,6 +39,39 @@ LN_EPS = 1e-5
 IN_EPS = 1e-5
 LRELU_SLOPE = 0.01
 MERGE_ORDER = ((0, 0, 0), (1, 0, 0), (0, 1, 0), (0, 0, 1), (1, 0, 1), (0, 1, 0), (0, 0, 1), (1, 1, 1))
+
+
+def dropout_keep(seed: int, n: int, p: float) -> np.ndarray:
+    """Keep mask of the engine's counter-hash dropout (csrc/swin.hip dropout_kernel) for hash indices 0..n-1:
+    splitmix64(seed + h * 0x9E3779B97F4A7C15) >> 32 >= p * 2^32.  MONAI draws its masks from torch's RNG, so
+    mask-level parity with the reference is undefined; this restates the engine's generator so the tests can
+    check that every site applies it (and its backward) where MONAI applies nn.Dropout."""
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + np.arange(n, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    t = float(np.float32(p)) * 4294967296.0      # p reaches the kernel as a C float
+    thr = 0xFFFFFFFF if t >= 4294967295.0 else int(t)
+    return (z >> np.uint64(32)) >= np.uint64(thr)
+
+
+def make_drop(p: float, seeds: Dict[str, object]) -> Callable[[Tensor, str], Tensor]:
+    """drop(t, site) for the oracle: t * keep / (1 - p) with the engine's mask of that site, where t is the
+    tensor in MONAI's layout at the site (pos_drop: NCDHW patch embedding; proj: [B*nW, N, C] windows; drop1 /
+    drop2: [b, d, h, w, c] token grids) and the hash index is t's flat index."""
+    scale = torch.tensor(1.0 / (1.0 - float(np.float32(p))), dtype=torch.float32)
+
+    def drop(t: Tensor, site: str) -> Tensor:
+        if site == "pos":
+            seed = seeds["pos"]
+        else:
+            pre, which = site.rsplit(".", 1)
+            seed = seeds[pre + "."][{"proj": 0, "drop1": 1, "drop2": 2}[which]]
+        keep = torch.from_numpy(dropout_keep(int(seed), t.numel(), p)).view(t.shape)
+        return torch.where(keep, t * scale.to(t.dtype), torch.zeros((), dtype=t.dtype))
+
+    return drop
 
 
 def relative_position_index(window) -> Tensor:
@@ -92,9 +126,10 @@ def compute_mask(dims, ws, ss) -> Tensor:
     return m.masked_fill(m != 0, float(-100.0)).masked_fill(m == 0, float(0.0))
 
 
-def swin_block(p: Params, pre: str, x: Tensor, mask: Tensor, window, shift, heads: int, index: Tensor) -> Tensor:
-    """SwinTransformerBlock.forward (part1: LN, pad, roll, window attention, reverse, unroll, crop; residual;
-    part2: LN, MLP(linear1, GELU, linear2); residual).  x [b, d, h, w, c]."""
+def swin_block(p: Params, pre: str, x: Tensor, mask: Tensor, window, shift, heads: int, index: Tensor,
+               drop: Optional[Callable] = None) -> Tensor:
+    """SwinTransformerBlock.forward (part1: LN, pad, roll, window attention (+ proj_drop), reverse, unroll, crop;
+    residual; part2: LN, MLP(linear1, GELU, drop1, linear2, drop2); residual).  x [b, d, h, w, c]."""
     b, d, h, w, c = x.shape
     ws, ss = get_window_size((d, h, w), window, shift)
     shortcut = x
@@ -109,6 +144,8 @@ def swin_block(p: Params, pre: str, x: Tensor, mask: Tensor, window, shift, head
         m = None
     xw = window_partition(y, ws)
     aw = window_attention(p, pre + "attn.", xw, m, heads, index)
+    if drop is not None:
+        aw = drop(aw.reshape(-1, ws[0] * ws[1] * ws[2], c), pre + "proj")
     y = window_reverse(aw.view(-1, ws[0] * ws[1] * ws[2], c), ws, (b, dp, hp, wp))
     if any(i > 0 for i in ss):
         y = torch.roll(y, shifts=ss, dims=(1, 2, 3))
@@ -117,7 +154,11 @@ def swin_block(p: Params, pre: str, x: Tensor, mask: Tensor, window, shift, head
     z = F.layer_norm(x, (c,), p[pre + "norm2.weight"], p[pre + "norm2.bias"], LN_EPS)
     z = F.linear(z, p[pre + "mlp.linear1.weight"], p[pre + "mlp.linear1.bias"])
     z = F.gelu(z)
+    if drop is not None:
+        z = drop(z, pre + "drop1")
     z = F.linear(z, p[pre + "mlp.linear2.weight"], p[pre + "mlp.linear2.bias"])
+    if drop is not None:
+        z = drop(z, pre + "drop2")
     return x + z
 
 
@@ -132,7 +173,8 @@ def patch_merging(p: Params, pre: str, x: Tensor) -> Tensor:
     return F.linear(x, p[pre + "reduction.weight"])
 
 
-def basic_layer(p: Params, pre: str, x: Tensor, depth: int, heads: int, window, index: Tensor) -> Tensor:
+def basic_layer(p: Params, pre: str, x: Tensor, depth: int, heads: int, window, index: Tensor,
+                drop: Optional[Callable] = None) -> Tensor:
     """BasicLayer.forward: x [b, c, d, h, w] -> blocks (even: no shift, odd: shift window//2) -> PatchMerging."""
     b, c, d, h, w = x.shape
     shift_full = tuple(i // 2 for i in window)
@@ -142,7 +184,7 @@ def basic_layer(p: Params, pre: str, x: Tensor, depth: int, heads: int, window, 
     mask = compute_mask((dp, hp, wp), ws, ss)
     for i in range(depth):
         x = swin_block(p, f"{pre}blocks.{i}.", x, mask, window, (0, 0, 0) if i % 2 == 0 else shift_full, heads,
-                       index)
+                       index, drop)
     x = patch_merging(p, pre + "downsample.", x)
     return x.permute(0, 4, 1, 2, 3)
 
@@ -156,13 +198,15 @@ def proj_out(x: Tensor, normalize: bool = True) -> Tensor:
 
 
 def swin_transformer(p: Params, pre: str, x: Tensor, depths, heads, window, index: Tensor,
-                     normalize: bool = True) -> List[Tensor]:
-    """SwinTransformer.forward: patch_embed (Conv3d k2 s2), proj_out of every stage's output."""
+                     normalize: bool = True, drop: Optional[Callable] = None) -> List[Tensor]:
+    """SwinTransformer.forward: patch_embed (Conv3d k2 s2), pos_drop, proj_out of every stage's output."""
     x0 = F.conv3d(x, p[pre + "patch_embed.proj.weight"], p[pre + "patch_embed.proj.bias"], stride=2)
+    if drop is not None:
+        x0 = drop(x0, "pos")
     outs = [proj_out(x0, normalize)]
     h = x0
     for i in range(4):
-        h = basic_layer(p, f"{pre}layers{i + 1}.0.", h, depths[i], heads[i], window, index)
+        h = basic_layer(p, f"{pre}layers{i + 1}.0.", h, depths[i], heads[i], window, index, drop)
         outs.append(proj_out(h, normalize))
     return outs
 
@@ -191,10 +235,11 @@ def unetr_up_block(p: Params, pre: str, x: Tensor, skip: Tensor) -> Tensor:
 
 
 def swin_unetr_forward(p: Params, x: Tensor, depths=(2, 2, 2, 2), heads=(3, 6, 12, 24), window=(7, 7, 7),
-                       normalize: bool = True, prefix: str = "") -> Tensor:
-    """MONAI SwinUNETR.forward: x [b, M, S^3] -> logits [b, C, S^3]."""
+                       normalize: bool = True, prefix: str = "", drop: Optional[Callable] = None) -> Tensor:
+    """MONAI SwinUNETR.forward: x [b, M, S^3] -> logits [b, C, S^3].  drop: the drop_rate sites in training
+    mode (make_drop), None = eval / drop_rate 0."""
     index = relative_position_index(window)
-    hs = swin_transformer(p, prefix + "swinViT.", x, depths, heads, window, index, normalize)
+    hs = swin_transformer(p, prefix + "swinViT.", x, depths, heads, window, index, normalize, drop)
     enc0 = unet_res_block(p, prefix + "encoder1.layer.", x)
     enc1 = unet_res_block(p, prefix + "encoder2.layer.", hs[0])
     enc2 = unet_res_block(p, prefix + "encoder3.layer.", hs[1])

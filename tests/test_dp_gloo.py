@@ -108,3 +108,16 @@ def test_bucket_layout_covers_arena_once():
     assert cover[0][0] == 0 and cover[-1][1] == sum(sizes)
     assert all(a[1] == b[0] for a, b in zip(cover, cover[1:]))
     assert sorted(i for b in gb.buckets for i in range(b[0], b[1])) == list(range(len(sizes)))
+
+
+@pytest.mark.parametrize("n,w", [(4, 2), (5, 2), (32, 6), (2, 4), (7, 8), (1, 3)])
+def test_shard_indices_match_distributed_sampler(n, w):
+    """Every rank gets ceil(n/W) samples (wrap-around padding), exactly DistributedSampler(shuffle=False)'s
+    order, so no rank runs an extra train_step and hangs the others in the gradient all-reduce."""
+    import mmseg_amd  # noqa: F401
+    from mmseg_amd.distributed.ddp import shard_indices
+    from torch.utils.data.distributed import DistributedSampler
+    shards = [shard_indices(n, r, w) for r in range(w)]
+    assert len({len(s) for s in shards}) == 1 and len(shards[0]) == -(-n // w)
+    for r in range(w):
+        assert shards[r] == list(DistributedSampler(range(n), num_replicas=w, rank=r, shuffle=False))

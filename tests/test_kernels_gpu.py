@@ -305,6 +305,43 @@ def test_loss_uint8_labels_and_scaled_grad(dev):
     assert rel(logits.grad * 4, torch.from_numpy(g["dicece_C6_grad"])) < 1e-5
 
 
+@pytest.mark.parametrize("C", [3, 6, 5])
+def test_loss_out_of_range_labels(dev, C):
+    """A label outside [0, C) makes the reference raise (F.one_hot / cross_entropy).  The kernels skip the
+    voxel (no out-of-bounds class-weight read), count it and return a NaN loss; check_labels() and
+    Trainer.train_step raise.  Pure CE ignores -100 like nn.CrossEntropyLoss (ignore_index default)."""
+    import torch.nn.functional as F
+    from mmseg_amd.trainer.losses import CrossEntropyLoss, DiceCELoss
+    g = torch.Generator().manual_seed(5)
+    logits = torch.randn(2, C, 6, 7, 5, generator=g)
+    labels = torch.randint(0, C, (2, 6, 7, 5), generator=g)
+    cw = torch.rand(C, generator=g) + 0.5
+    bad = labels.clone()
+    bad[0, 1, 2, 3], bad[1, 0, 0, 0], bad[1, 5, 6, 4] = 255, C, -3
+    for mod in (DiceCELoss(class_weights=cw), DiceCELoss(), CrossEntropyLoss(weight=cw)):
+        lg = logits.to(dev).requires_grad_(True)
+        loss = mod(lg, bad.to(dev))
+        loss.backward()
+        assert torch.isnan(loss).item() and mod.invalid_labels() == 3
+        assert torch.isfinite(lg.grad).all()
+        with pytest.raises(RuntimeError, match="outside"):
+            mod.check_labels()
+        assert mod(lg, labels.to(dev)).isfinite().item() and mod.invalid_labels() == 0
+        mod.check_labels()
+    # ignore_index -100 in pure CE: same value and gradient as torch's cross_entropy
+    ign = labels.clone()
+    ign[0, :2] = -100
+    lg = logits.to(dev).requires_grad_(True)
+    mod = CrossEntropyLoss(weight=cw)
+    loss = mod(lg, ign.to(dev))
+    loss.backward()
+    ref_lg = logits.double().requires_grad_(True)
+    ref = F.cross_entropy(ref_lg, ign, weight=cw.double())
+    ref.backward()
+    assert mod.invalid_labels() == 0 and abs(loss.item() - ref.item()) < 1e-5
+    assert rel(lg.grad.cpu(), ref_lg.grad.float()) < 1e-5
+
+
 @pytest.mark.parametrize("C", [3, 6])
 def test_dice_metric_bit_identical(dev, C):
     from mmseg_amd.trainer.metrics import DiceMetric

@@ -267,3 +267,15 @@ def test_full_size_forward_matches_reference(dev, tag, model):
     assert abs(loss.item() - float(g["loss"])) < 1e-4 * abs(float(g["loss"]))
     hist = torch.bincount(out.argmax(1).reshape(-1), minlength=6).cpu().numpy()
     assert np.abs(hist - g["argmax_hist"]).sum() <= 1e-4 * hist.sum()
+
+
+def test_train_step_raises_on_out_of_range_labels(dev):
+    """reference: F.one_hot raises on a class index >= num_classes; Trainer.train_step raises too
+    (the loss kernels count such voxels on the device; the step's loss.item() sees the NaN)."""
+    cfg, m, g, M, C = _build("unet_tiny")
+    xs, ys = _inputs(g, M, C)
+    tr = Trainer(cfg, m)
+    bad = ys[0].clone()
+    bad[0, 0, 0, 0] = C
+    with pytest.raises(RuntimeError, match="outside"):
+        tr.train_step({"image": xs[0], "label": bad}, 0)

@@ -193,9 +193,9 @@ def test_res_apply_and_lrelu_bwd(dev, dtype):
 
 
 # --------------------------------------------------------------------- whole network
-def _model(dev, dtype, fs=24, cin=2, cout=3, size=64):
+def _model(dev, dtype, fs=24, cin=2, cout=3, size=64, drop_rate=0.0):
     torch.manual_seed(1)
-    m = SwinUNETR(img_size=(size,) * 3, in_channels=cin, out_channels=cout, feature_size=fs)
+    m = SwinUNETR(img_size=(size,) * 3, in_channels=cin, out_channels=cout, feature_size=fs, drop_rate=drop_rate)
     with torch.no_grad():      # non-trivial LayerNorm affines and bias tables
         for name, p in m.named_parameters():
             if "norm" in name or "relative_position_bias_table" in name:
@@ -204,10 +204,10 @@ def _model(dev, dtype, fs=24, cin=2, cout=3, size=64):
     return m.to(dev)
 
 
-def _oracle(m, x, cot, dtype=torch.float64):
+def _oracle(m, x, cot, dtype=torch.float64, drop=None):
     p = {k: v.detach().cpu().to(dtype).requires_grad_(True) for k, v in m.model.named_parameters()}
     xr = x.to(dtype)
-    out = SO.swin_unetr_forward(p, xr, m.depths, m.num_heads)
+    out = SO.swin_unetr_forward(p, xr, m.depths, m.num_heads, drop=drop)
     (out * cot.to(dtype)).sum().backward()
     return out, {k: v.grad for k, v in p.items()}
 
@@ -361,3 +361,50 @@ def test_fused_attention_network_matches_unfused(dev, swin_case, monkeypatch):
     # test_fused_window_attention_vs_torch
     tab = [n for n in res[0][1] if "relative_position_bias_table" in n]
     assert max(rel2(res[0][1][n], res[1][1][n]) for n in tab) < 0.5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("ncdhw", [0, 1])
+def test_dropout_kernel_matches_mask(dev, dtype, ncdhw):
+    """mmseg_dropout: keep / scale exactly as the restated generator (oracle dropout_keep), the keep rate
+    ~1-p, and the same call on a gradient applies the same mask (the backward)."""
+    L = lib()
+    N, V, C, p, seed = 2, 1000, 24, 0.3, 123456789012345
+    x = torch.randn(N * V, C, device=dev).to(dtype)
+    y = torch.empty_like(x)
+    L.mmseg_dropout(ptr(x), ptr(y), N * V, C, V, ncdhw, p, seed, CODE[dtype], stream_handle())
+    keep = torch.from_numpy(SO.dropout_keep(seed, N * V * C, p))
+    if ncdhw:   # hash index of element (n, v, c) is its NCDHW position
+        keep = keep.view(N, C, V).permute(0, 2, 1).reshape(N * V, C)
+    else:
+        keep = keep.view(N * V, C)
+    scale = torch.tensor(1.0 / (1.0 - float(np.float32(p))), dtype=torch.float32)
+    ref = torch.where(keep, x.float().cpu() * scale, torch.zeros(())).to(dtype)
+    assert torch.equal(y.cpu(), ref)
+    assert abs(keep.float().mean().item() - (1 - p)) < 0.01
+    g = torch.ones_like(x)
+    L.mmseg_dropout(ptr(g), ptr(g), N * V, C, V, ncdhw, p, seed, CODE[dtype], stream_handle())
+    assert torch.equal(g.cpu() != 0, keep)
+
+
+def test_swin_unetr_dropout_matches_oracle(dev, swin_case):
+    """drop_rate > 0 (the reference's default config: head.dropout 0.1 -> SwinUNETR drop_rate): pos_drop,
+    proj_drop and the MLP drop1 / drop2 in training mode, forward and every gradient, against the oracle fed
+    the engine's masks; eval mode is the identity (equal to a drop_rate 0 model)."""
+    x, cot = swin_case
+    m = _model(dev, torch.float32, drop_rate=0.2)
+    out = m(x.to(dev))
+    seeds = dict(m.__dict__["_engine"].program.drop_seeds)
+    assert len(seeds) == 1 + 8
+    (out * cot.to(dev)).sum().backward()
+    ref, grads = _oracle(m, x, cot, drop=SO.make_drop(0.2, seeds))
+    assert rel(out, ref) < 1e-4
+    got = torch.cat([p.grad.reshape(-1).double().cpu() for _, p in m.model.named_parameters()])
+    want = torch.cat([grads[n].reshape(-1) for n, _ in m.model.named_parameters()])
+    assert ((got - want).norm() / want.norm()).item() < 1e-2
+    nodrop = _oracle(m, x, cot)[0]
+    assert rel(out, nodrop) > 1e-3          # the masks did change the output
+    m.eval()
+    m0 = _model(dev, torch.float32).eval()
+    with torch.no_grad():
+        assert torch.equal(m(x[:1].to(dev)), m0(x[:1].to(dev)))
