@@ -345,6 +345,23 @@ int mmseg_loss_bwd(const float* logits, const void* labels, int label_bytes, int
                    float dice_w, float ce_w, float smooth, float alpha, float beta, int include_bg,
                    const float* class_w, const float* gout, float gconst, float* dlogits, const float* ws,
                    void* stream);
+/* Fused training head + loss (the Trainer's fast path, trainer.py:238-243 in one pass each way):
+ * forward = head 1x1 conv (+ Dropout3d scale) + mmseg_loss_fwd's statistics without writing the logits;
+ * backward = dlogits + the head's data and weight gradient without writing dlogits (logits recomputed with
+ * the forward's operation order).  ws: mmseg_loss_ws_floats(N, C, V) floats, same layout (the count of
+ * out-of-range labels is its last float); wpart: mmseg_head_loss_wpart_floats() floats.
+ * mmseg_head_loss_ok: 1 when (C, Cin, ldx, dtype) has a kernel (2 <= C <= 8, Cin 8, 16 or 32). */
+int mmseg_head_loss_ok(int C, int Cin, int ldx, int dtype);
+long long mmseg_head_loss_wpart_floats(int C, int Cin, int N, long long V);
+int mmseg_head_loss_fwd(const void* x, int ldx, int Cin, const float* W, const float* b, const float* dscale, int C,
+                        int N, long long V, const void* labels, int label_bytes, int type, float dice_w, float ce_w,
+                        float smooth, float alpha, float beta, int include_bg, const float* class_w, float* loss_out,
+                        float* ws, int dtype, void* stream);
+int mmseg_head_loss_bwd(const void* x, int ldx, int Cin, const float* W, const float* b, const float* dscale, int C,
+                        int N, long long V, const void* labels, int label_bytes, int type, float dice_w, float ce_w,
+                        float smooth, float alpha, float beta, int include_bg, const float* class_w, const float* gout,
+                        float gconst, const float* ws, void* dx, int lddx, float* gW, float* gb, float* wpart,
+                        int accumulate, int dtype, void* stream);
 /* argmax + per-class intersection / pred / target counts (trainer.py:290-291, metrics.py:42-67). */
 int mmseg_dice_counts(const float* logits, const void* labels, int label_bytes, int N, int C, long long V,
                       unsigned long long* counts, void* pred_out, void* stream);

@@ -1467,9 +1467,13 @@ constexpr int BR_MAXHV = 640;   // halo voxels staged per block (host guarantees
 // halo image quads available (host guarantees (bz+2)(by+2)((bx+2)*QV+2) <= this): 40 KB bf16 / 80 KB f32
 __host__ __device__ constexpr int br_xq(int tsize) { return tsize == 2 ? 2560 : 5120; }
 
-template <typename T, int BN>
-__global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kernel(GemmArgs g, int bz, int by,
-                                                                                   int bx) {
+// CB* > 0: the brick is known at compile time (6x6x6 at the 12^3 / 6^3 levels), so the halo / epilogue index
+// arithmetic divides by constants (mul-shift) instead of runtime integer divisions, which at one 32-channel
+// chunk per block were most of the kernel's VALU work (8.6 VALU instructions per MFMA, rocprofv3 r02).
+template <typename T, int BN, int CBZ = 0, int CBY = 0, int CBX = 0>
+__global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kernel(GemmArgs g, int bz_rt, int by_rt,
+                                                                                   int bx_rt) {
+  const int bz = CBZ > 0 ? CBZ : bz_rt, by = CBY > 0 ? CBY : by_rt, bx = CBX > 0 ? CBX : bx_rt;
   using L = Brick2Layout<T>;
   constexpr int RM = 4, RN = BN / 16;
   constexpr int XQ = br_xq(sizeof(T));
@@ -1731,7 +1735,8 @@ Conv3Plan plan_conv3(int M, int Ncols, int cin, int D, int H, int W, int lda, in
       const int nb = (M / (D * H * W)) * (D / p.bz) * (H / p.by) * (W / p.bx);
       const int nt = (Ncols + p.bn - 1) / p.bn;
       const int nchunk = cin / CK;
-      int ks = (512 + nb * nt - 1) / (nb * nt);
+      const int slots = knob("MMSEG_BRICKR_SLOTS", 256);   // 512 measured 2-10 % slower at 12^3 / 6^3 (r02)
+      int ks = (slots + nb * nt - 1) / (nb * nt);
       if (ks > nchunk) ks = nchunk;
       if (ks < 1) ks = 1;
       const int cps = (nchunk + ks - 1) / ks;
@@ -2493,8 +2498,10 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
 // computed once (4 k-steps x 2 rows).
 constexpr int WR_MAXHV = 384;
 
-template <typename T, int MT>
-__global__ __launch_bounds__(512) void wgrad_brickr_kernel(WgradArgs g, int bz, int by, int bx) {
+// CB* > 0: compile-time brick (3x6x6 at the 12^3 / 6^3 levels), see conv3_brickr_kernel.
+template <typename T, int MT, int CBZ = 0, int CBY = 0, int CBX = 0>
+__global__ __launch_bounds__(512) void wgrad_brickr_kernel(WgradArgs g, int bz_rt, int by_rt, int bx_rt) {
+  const int bz = CBZ > 0 ? CBZ : bz_rt, by = CBY > 0 ? CBY : by_rt, bx = CBX > 0 ? CBX : bx_rt;
   constexpr int EP = 16 / sizeof(T);
   constexpr int CO = MT * 16, CG = CO / 8;
   constexpr int DP = CO + EP;
@@ -3033,11 +3040,18 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     const int cps = (nchunk + g.ksplit - 1) / g.ksplit;
     g.ksplit = (nchunk + cps - 1) / cps;
     const dim3 grid(nb * ((g.Ncols + plan.bn - 1) / plan.bn) * g.ksplit);
+    const bool b666 = plan.bz == 6 && plan.by == 6 && plan.bx == 6 && knob("MMSEG_BRICKR_CT", 1);
     if (plan.bn == 64) {
       if constexpr (sizeof(T) == 2) {
         mmseg::note_kernel("conv3_brickr_kernel<BN64>");
-        hipLaunchKernelGGL((conv3_brickr_kernel<T, 64>), grid, block, 0, s, g, plan.bz, plan.by, plan.bx);
+        if (b666)
+          hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6>), grid, block, 0, s, g, 6, 6, 6);
+        else
+          hipLaunchKernelGGL((conv3_brickr_kernel<T, 64>), grid, block, 0, s, g, plan.bz, plan.by, plan.bx);
       }
+    } else if (b666) {
+      mmseg::note_kernel("conv3_brickr_kernel<BN32>");
+      hipLaunchKernelGGL((conv3_brickr_kernel<T, 32, 6, 6, 6>), grid, block, 0, s, g, 6, 6, 6);
     } else {
       mmseg::note_kernel("conv3_brickr_kernel<BN32>");
       hipLaunchKernelGGL((conv3_brickr_kernel<T, 32>), grid, block, 0, s, g, plan.bz, plan.by, plan.bx);
@@ -3197,14 +3211,21 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
     if (MODE == MODE_CONV3 && g.brick == 3) {
       const WBrick wb = plan_wgrad_brickr(g.D, g.H, g.W);
+      const bool b366 = wb.bz == 3 && wb.by == 6 && wb.bx == 6 && knob("MMSEG_BRICKR_CT", 1);
       if (g.Ca % 64 == 0) {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 64) * g.ksplit);
         mmseg::note_kernel("wgrad_brickr_kernel<CO64>");
-        hipLaunchKernelGGL((wgrad_brickr_kernel<T, 4>), grid, dim3(512), 0, s, g, wb.bz, wb.by, wb.bx);
+        if (b366)
+          hipLaunchKernelGGL((wgrad_brickr_kernel<T, 4, 3, 6, 6>), grid, dim3(512), 0, s, g, 3, 6, 6);
+        else
+          hipLaunchKernelGGL((wgrad_brickr_kernel<T, 4>), grid, dim3(512), 0, s, g, wb.bz, wb.by, wb.bx);
       } else {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 32) * g.ksplit);
         mmseg::note_kernel("wgrad_brickr_kernel<CO32>");
-        hipLaunchKernelGGL((wgrad_brickr_kernel<T, 2>), grid, dim3(512), 0, s, g, wb.bz, wb.by, wb.bx);
+        if (b366)
+          hipLaunchKernelGGL((wgrad_brickr_kernel<T, 2, 3, 6, 6>), grid, dim3(512), 0, s, g, 3, 6, 6);
+        else
+          hipLaunchKernelGGL((wgrad_brickr_kernel<T, 2>), grid, dim3(512), 0, s, g, wb.bz, wb.by, wb.bx);
       }
       return mmseg::check_launch("wgrad_brickr");
     }
@@ -3293,6 +3314,11 @@ int brick_wgrad_splits(long long V, int cap, int Ca, int cpg_shift, int kind, in
   if (kind == 3) {
     const WBrick wb = plan_wgrad_brickr(D, H, W);
     nbrick = V / (wb.bz * wb.by * wb.bx);
+    // at least MMSEG_WGRAD_RMINB bricks per split: at 6^3 (4 bricks) one split writes the gradient directly;
+    // two splits moved 2x the 28 MB fp32 gradient of a 512->512 layer through partials and a reduce
+    // (41 -> 24 us, r02 convbench)
+    const long long minb = knob("MMSEG_WGRAD_RMINB", 4);
+    if (ks > nbrick / minb) ks = nbrick / minb;
   }
   if (ks > nbrick) ks = nbrick;
   if (ks < 1) ks = 1;

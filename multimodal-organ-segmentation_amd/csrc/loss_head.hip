@@ -361,6 +361,93 @@ __device__ __forceinline__ int label_state(int y, int C, const LossCfg& cfg) {
   return (y == -100 && cfg.type == 0 && cfg.dice_w == 0.f) ? 1 : 2;   // 1 = ignored, 2 = invalid
 }
 
+// One voxel's contribution to the loss statistics: softmax p over its C logits z, Sum p / Sum p*t / Sum t per
+// class and the (class-weighted / focal) CE term.  Shared by loss_stats_kernel and the fused head + loss
+// forward so both give the same bits.  y must be a valid label.
+template <int NC>
+__device__ __forceinline__ void loss_voxel_stats(const float* z, int C, int y, const LossCfg& cfg, float* P, float* I,
+                                                 float* Tc, float& ce, float& cden) {
+  float mx = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    if (c < C) mx = fmaxf(mx, z[c]);
+  float se = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    if (c < C) se += expf(z[c] - mx);
+  const float lse = mx + logf(se);
+  const float inv = 1.f / se;
+  float zy = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    if (c < C) {
+      const float p = expf(z[c] - mx) * inv;
+      P[c] += p;
+      if (c == y) {
+        I[c] += p;
+        Tc[c] += 1.f;
+        zy = z[c];
+      }
+    }
+  const float wy = cfg.cw ? cfg.cw[y] : 1.f;
+  if (cfg.type == 2) {   // focal (losses.py:116-121): (1 - exp(-ce_i))^gamma * ce_i, plain mean over voxels
+    const float cei = wy * (lse - zy);
+    const float pt = expf(-cei);
+    ce += powf(1.f - pt, cfg.alpha) * cei;
+    cden += 1.f;
+  } else {
+    ce = fmaf(wy, lse - zy, ce);
+    cden += wy;
+  }
+}
+
+// One voxel's dloss/dlogits (before the output-gradient scale): d = p (dp - Sum p dp) + ce_scale w_y (p - t),
+// dp = a t + b from the finalize pass's per-(n,c) coefficients cf = coef + 2 n C.  y must be valid.
+template <int NC>
+__device__ __forceinline__ void loss_voxel_grad(const float* z, int C, int y, const LossCfg& cfg,
+                                                const float* __restrict__ cf, float ces, float* d) {
+  float p[NC];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    if (c < C) mx = fmaxf(mx, z[c]);
+  float se = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    if (c < C) {
+      p[c] = expf(z[c] - mx);
+      se += p[c];
+    }
+  const float inv = 1.f / se;
+  float wy = cfg.cw ? cfg.cw[y] : 1.f;
+  if (cfg.type == 2) {   // focal: d f_i / d ce_i = gamma (1-pt)^(gamma-1) pt ce_i + (1-pt)^gamma, ce_i = w_y (lse - z_y)
+    float zy = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      if (c < C && c == y) zy = z[c];
+    const float cei = wy * (mx + logf(se) - zy);
+    const float pt = expf(-cei), q = 1.f - pt, gm = cfg.alpha;
+    const float dfd = (q > 0.f ? gm * powf(q, gm - 1.f) * pt * cei : 0.f) + powf(q, gm);
+    wy *= dfd;
+  }
+  float dp[NC];
+  float sacc = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    if (c < C) {
+      p[c] *= inv;
+      const float t = c == y ? 1.f : 0.f;
+      dp[c] = cf[2 * c] * t + cf[2 * c + 1];
+      sacc = fmaf(p[c], dp[c], sacc);
+    }
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    if (c < C) {
+      const float t = c == y ? 1.f : 0.f;
+      d[c] = p[c] * (dp[c] - sacc) + ces * wy * (p[c] - t);
+    }
+}
+
 // per (n, chunk): [P_c][I_c][T_c] (3C) + ce_num + ce_den + invalid-label count
 template <typename LT, int CC>
 __global__ __launch_bounds__(256) void loss_stats_kernel(const float* __restrict__ logits, const LT* __restrict__ labels, int Crt,
@@ -401,42 +488,7 @@ __global__ __launch_bounds__(256) void loss_stats_kernel(const float* __restrict
       bad += ls == 2 ? 1.f : 0.f;
       continue;
     }
-    float z[NC];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-      if (c < C) {
-        z[c] = zu[u][c];
-        mx = fmaxf(mx, z[c]);
-      }
-    float se = 0.f;
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-      if (c < C) se += expf(z[c] - mx);
-    const float lse = mx + logf(se);
-    const float inv = 1.f / se;
-    float zy = 0.f;
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-      if (c < C) {
-        const float p = expf(z[c] - mx) * inv;
-        P[c] += p;
-        if (c == y) {
-          I[c] += p;
-          Tc[c] += 1.f;
-          zy = z[c];
-        }
-      }
-    const float wy = cfg.cw ? cfg.cw[y] : 1.f;
-    if (cfg.type == 2) {   // focal (losses.py:116-121): (1 - exp(-ce_i))^gamma * ce_i, plain mean over voxels
-      const float cei = wy * (lse - zy);
-      const float pt = expf(-cei);
-      ce += powf(1.f - pt, cfg.alpha) * cei;
-      cden += 1.f;
-    } else {
-      ce = fmaf(wy, lse - zy, ce);
-      cden += wy;
-    }
+    loss_voxel_stats<NC>(zu[u], C, y, cfg, P, I, Tc, ce, cden);
   }
   }
   __shared__ float red[4][3 * CMAX + 3];
@@ -565,52 +617,361 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(const float* __restrict__
         if (c < C) dlogits[(n * C + c) * V + v] = 0.f;
       continue;
     }
-    float z[NC], p[NC];
+    float d[NC];
+    loss_voxel_grad<NC>(zu[u], C, y, cfg, coef + (long long)n * C * 2, ces, d);
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      if (c < C) dlogits[(n * C + c) * V + v] = g * d[c];
+  }
+  }
+}
+
+// ------------------------------------------------ fused head + loss (training)
+// The Trainer's fast path (Trainer.train_step with an engine model and a HIP loss): the 1x1 head, the loss
+// statistics and, in the backward, dlogits + the head's data and weight gradients, without materialising
+// logits or dlogits.  Unfused, the same work is head_fwd (x -> 42 MB fp32 logits at 96^3 B=2), loss_stats
+// (logits), loss_bwd (logits -> dlogits), head_dgrad (dlogits -> dx), head_wgrad_partial (x, dlogits): five
+// passes at ~2.3 TB/s, 260 us.  Fused: the forward reads x + labels; the backward reads x + labels and
+// writes dx, recomputing the logits.
+//
+// The head's two small GEMMs run on the matrix cores in exact fp32 (v_mfma_f32_16x16x4_f32, an fp32 fma
+// chain): a wave takes 16 voxels per step; lane l holds channels 8g..8g+7 (g = l >> 4) of voxel l & 15 from
+// one coalesced 16-B load (a wave's load = 16 voxels x 64 B, contiguous).
+//   logits^T = W . x^T   (A = W, B = x^T; MFMA kb sums channels 8g + kb over the lane groups g)
+//       -> lane l holds classes 4g..4g+3 of voxel l & 15: softmax = 4 registers + two cross-group shuffles;
+//   dx^T = W^T . dlogits^T   (B = the lane's own dlogits registers: MFMA kb sums class 4g + kb)
+//       -> lane l holds dx channels 16t + 4g .. +3 of voxel l & 15 (one 8-B store per 16-channel tile t);
+//   dW += dlogits x (fp32 FMAs in the load layout, the voxel's dlogits gathered with 8 shuffles).
+// Channel / class orders inside the sums differ from the unfused kernels', so values agree to fp32 rounding.
+template <typename T, int G>
+struct HeadLoad {   // the lane's 8 channels 8g..8g+7 of one voxel (zero for groups g >= G or invalid voxels)
+  V8<T> a;
+  __device__ __forceinline__ void load(const T* __restrict__ x, int ldx, long long row, bool ok, int g) {
+    if (ok && g < G) a.load(x + row * ldx + 8 * g);
+    else a.zero();
+  }
+};
+
+constexpr int HU = 4;   // 16-voxel tiles per wave step in the fused head + loss kernels
+
+template <int G>
+__device__ __forceinline__ f32x4 head_logits_t(const float* wA, const float* xs, const float* bz) {
+  f32x4 acc = {bz[0], bz[1], bz[2], bz[3]};
+#pragma unroll
+  for (int kb = 0; kb < 8; ++kb) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[kb], xs[kb], acc, 0, 0, 0);
+  return acc;
+}
+
+template <typename T, int G, typename LT>
+__global__ __launch_bounds__(256) void head_loss_stats_kernel(const T* __restrict__ x, int ldx,
+                                                              const float* __restrict__ Wt,
+                                                              const float* __restrict__ bias,
+                                                              const float* __restrict__ dscale, int C,
+                                                              const LT* __restrict__ labels, long long V,
+                                                              long long vpc, LossCfg cfg, float* __restrict__ part) {
+  constexpr int Cin = 8 * G;
+  __shared__ float red[4][52];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, v16 = lane & 15, g = lane >> 4;
+  const int n = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
+  float wA[8], sc[8], bz[4];
+#pragma unroll
+  for (int kb = 0; kb < 8; ++kb) {
+    wA[kb] = (v16 < C && g < G) ? Wt[v16 * Cin + 8 * g + kb] : 0.f;
+    sc[kb] = (dscale && g < G) ? dscale[n * Cin + 8 * g + kb] : 1.f;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bz[r] = 4 * g + r < C ? bias[4 * g + r] : 0.f;
+  float P[4], I[4], Tc[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) P[r] = I[r] = Tc[r] = 0.f;
+  float ce = 0.f, cden = 0.f, bad = 0.f;
+  const long long v0 = (long long)chunk * vpc;
+  const long long v1 = v0 + vpc < V ? v0 + vpc : V;
+  const long long base = (long long)n * V;
+  // HU tiles of 16 voxels per wave step, all their loads in flight before the first is used (one 16-B load
+  // per lane and tile is too little memory parallelism on its own)
+  for (long long vb = v0 + wave * 16 * HU; vb < v1; vb += 64 * HU) {
+  HeadLoad<T, G> lds_[HU];
+  int ys_[HU];
+#pragma unroll
+  for (int u = 0; u < HU; ++u) {
+    const long long v = vb + 16 * u + v16;
+    lds_[u].load(x, ldx, base + v, v < v1, g);
+    ys_[u] = v < v1 ? (int)labels[base + v] : 0;
+  }
+#pragma unroll
+  for (int u = 0; u < HU; ++u) {
+    const long long v = vb + 16 * u + v16;
+    const bool ok = v < v1;
+    const HeadLoad<T, G>& ld = lds_[u];
+    const int y = ys_[u];
+    float xs[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xs[j] = dscale ? ld.a.get(j) * sc[j] : ld.a.get(j);
+    const f32x4 acc = head_logits_t<G>(wA, xs, bz);
+    float z[4], e[4];
     float mx = -INFINITY;
 #pragma unroll
-    for (int c = 0; c < NC; ++c)
-      if (c < C) {
-        z[c] = zu[u][c];
-        mx = fmaxf(mx, z[c]);
-      }
+    for (int r = 0; r < 4; ++r) {
+      z[r] = 4 * g + r < C ? acc[r] : -INFINITY;
+      mx = fmaxf(mx, z[r]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     float se = 0.f;
 #pragma unroll
-    for (int c = 0; c < NC; ++c)
-      if (c < C) {
-        p[c] = expf(z[c] - mx);
-        se += p[c];
-      }
-    const float inv = 1.f / se;
-    float wy = cfg.cw ? cfg.cw[y] : 1.f;
-    if (cfg.type == 2) {   // focal: d f_i / d ce_i = gamma (1-pt)^(gamma-1) pt ce_i + (1-pt)^gamma, ce_i = w_y (lse - z_y)
-      float zy = 0.f;
+    for (int r = 0; r < 4; ++r) {
+      e[r] = 4 * g + r < C ? expf(z[r] - mx) : 0.f;
+      se += e[r];
+    }
+    se += __shfl_xor(se, 16, 64);
+    se += __shfl_xor(se, 32, 64);
+    const float lse = mx + logf(se), inv = 1.f / se;
+    const int ls = ok ? label_state(y, C, cfg) : 1;
+    if (ls == 0) {
 #pragma unroll
-      for (int c = 0; c < NC; ++c)
-        if (c < C && c == y) zy = z[c];
+      for (int r = 0; r < 4; ++r) {
+        const int c = 4 * g + r;
+        if (c < C) {
+          const float p = e[r] * inv;
+          P[r] += p;
+          if (c == y) {
+            I[r] += p;
+            Tc[r] += 1.f;
+          }
+        }
+      }
+      if ((y >> 2) == g) {   // the lane holding class y adds the voxel's CE term
+        float zy = z[0];
+#pragma unroll
+        for (int r = 1; r < 4; ++r)
+          if ((y & 3) == r) zy = z[r];
+        const float wy = cfg.cw ? cfg.cw[y] : 1.f;
+        if (cfg.type == 2) {
+          const float cei = wy * (lse - zy);
+          const float pt = expf(-cei);
+          ce += powf(1.f - pt, cfg.alpha) * cei;
+          cden += 1.f;
+        } else {
+          ce = fmaf(wy, lse - zy, ce);
+          cden += wy;
+        }
+      }
+    } else if (ls == 2 && g == 0) {
+      bad += 1.f;
+    }
+  }
+  }
+  // sums over the 16 voxel lanes of each group (fixed tree); lane 16g then holds classes 4g..4g+3
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      P[r] += __shfl_xor(P[r], o, 64);
+      I[r] += __shfl_xor(I[r], o, 64);
+      Tc[r] += __shfl_xor(Tc[r], o, 64);
+    }
+  ce = wave_sum(ce);
+  cden = wave_sum(cden);
+  bad = wave_sum(bad);
+  if (v16 == 0)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      red[wave][4 * g + r] = P[r];
+      red[wave][16 + 4 * g + r] = I[r];
+      red[wave][32 + 4 * g + r] = Tc[r];
+    }
+  if (lane == 0) {
+    red[wave][48] = ce;
+    red[wave][49] = cden;
+    red[wave][50] = bad;
+  }
+  __syncthreads();
+  const int nv = 3 * C + 3;
+  for (int k = threadIdx.x; k < nv; k += blockDim.x) {
+    const int src = k < 3 * C ? (k / C) * 16 + k % C : 48 + (k - 3 * C);
+    part[((long long)n * nchunk + chunk) * nv + k] = red[0][src] + red[1][src] + red[2][src] + red[3][src];
+  }
+}
+
+// wpart: per block [C*Cin + C] weight / bias gradient partials (head_wgrad_reduce sums them over the blocks)
+template <typename T, int G, int NC, typename LT>
+__global__ __launch_bounds__(256) void head_loss_bwd_kernel(const T* __restrict__ x, int ldx,
+                                                            const float* __restrict__ Wt,
+                                                            const float* __restrict__ bias,
+                                                            const float* __restrict__ dscale, int C,
+                                                            const LT* __restrict__ labels, long long V, long long vpc,
+                                                            LossCfg cfg, const float* __restrict__ coef,
+                                                            const float* __restrict__ gout, float gconst,
+                                                            T* __restrict__ dx, int lddx, float* __restrict__ wpart) {
+  constexpr int Cin = 8 * G, TN = (Cin + 15) / 16;
+  static_assert(NC <= 8, "dlogits gather covers 8 classes");
+  __shared__ float red[4][NC * Cin + NC];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, v16 = lane & 15, g = lane >> 4;
+  const int n = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
+  float wA[8], sc[8], bz[4], ca[4], cb[4];
+#pragma unroll
+  for (int kb = 0; kb < 8; ++kb) {
+    wA[kb] = (v16 < C && g < G) ? Wt[v16 * Cin + 8 * g + kb] : 0.f;
+    sc[kb] = (dscale && g < G) ? dscale[n * Cin + 8 * g + kb] : 1.f;
+  }
+  const float* cf = coef + (long long)n * C * 2;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int c = 4 * g + r;
+    bz[r] = c < C ? bias[c] : 0.f;
+    ca[r] = c < C ? cf[2 * c] : 0.f;
+    cb[r] = c < C ? cf[2 * c + 1] : 0.f;
+  }
+  // dx^T A operand: row ci = 16t + v16, k-slot g <-> class 4g + kb
+  float wD[TN][4], sd[TN][4];
+#pragma unroll
+  for (int t = 0; t < TN; ++t)
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const int ci = 16 * t + v16, c = 4 * g + kb;
+      wD[t][kb] = (ci < Cin && c < C) ? Wt[c * Cin + ci] : 0.f;
+      const int co = 16 * t + 4 * g + kb;     // the output channel of register kb
+      sd[t][kb] = (dscale && co < Cin) ? dscale[n * Cin + co] : 1.f;
+    }
+  const float gsc = gout ? gout[0] * gconst : gconst;
+  const float ces = coef[2 * gridDim.y * C];
+  float acc[NC][8], bacc[4];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[c][j] = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bacc[r] = 0.f;
+  const long long v0 = (long long)chunk * vpc;
+  const long long v1 = v0 + vpc < V ? v0 + vpc : V;
+  const long long base = (long long)n * V;
+  for (long long vb = v0 + wave * 16 * HU; vb < v1; vb += 64 * HU) {
+  HeadLoad<T, G> lds_[HU];
+  int ys_[HU];
+#pragma unroll
+  for (int u = 0; u < HU; ++u) {
+    const long long v = vb + 16 * u + v16;
+    lds_[u].load(x, ldx, base + v, v < v1, g);
+    ys_[u] = v < v1 ? (int)labels[base + v] : 0;
+  }
+#pragma unroll
+  for (int u = 0; u < HU; ++u) {
+    const long long v = vb + 16 * u + v16;
+    const bool ok = v < v1;
+    const HeadLoad<T, G>& ld = lds_[u];
+    const int y = ys_[u];
+    float xs[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xs[j] = dscale ? ld.a.get(j) * sc[j] : ld.a.get(j);
+    const f32x4 acc_l = head_logits_t<G>(wA, xs, bz);
+    float z[4], p[4];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      z[r] = 4 * g + r < C ? acc_l[r] : -INFINITY;
+      mx = fmaxf(mx, z[r]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float se = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      p[r] = 4 * g + r < C ? expf(z[r] - mx) : 0.f;
+      se += p[r];
+    }
+    se += __shfl_xor(se, 16, 64);
+    se += __shfl_xor(se, 32, 64);
+    const float inv = 1.f / se;
+    const int ls = ok ? label_state(y, C, cfg) : 1;
+    float wy = (ls == 0 && cfg.cw) ? cfg.cw[y] : 1.f;
+    if (cfg.type == 2) {   // focal: the lane group holding class y has z_y; every lane needs it
+      float zc = z[0];
+#pragma unroll
+      for (int r = 1; r < 4; ++r)
+        if ((y & 3) == r) zc = z[r];
+      const float zy = __shfl(zc, ((y >> 2) & 3) * 16 + v16, 64);
       const float cei = wy * (mx + logf(se) - zy);
       const float pt = expf(-cei), q = 1.f - pt, gm = cfg.alpha;
       const float dfd = (q > 0.f ? gm * powf(q, gm - 1.f) * pt * cei : 0.f) + powf(q, gm);
       wy *= dfd;
     }
-    float dp[NC];
-    float s = 0.f;
+    float dp[4], sp = 0.f;
 #pragma unroll
-    for (int c = 0; c < NC; ++c)
-      if (c < C) {
-        p[c] *= inv;
-        const float t = c == y ? 1.f : 0.f;
-        const float* cf = coef + ((long long)n * C + c) * 2;
-        dp[c] = cf[0] * t + cf[1];
-        s = fmaf(p[c], dp[c], s);
-      }
+    for (int r = 0; r < 4; ++r) {
+      p[r] *= inv;
+      const float t = 4 * g + r == y ? 1.f : 0.f;
+      dp[r] = ca[r] * t + cb[r];
+      sp = fmaf(p[r], dp[r], sp);
+    }
+    sp += __shfl_xor(sp, 16, 64);
+    sp += __shfl_xor(sp, 32, 64);
+    float d[4];
 #pragma unroll
-    for (int c = 0; c < NC; ++c)
-      if (c < C) {
-        const float t = c == y ? 1.f : 0.f;
-        const float d = p[c] * (dp[c] - s) + ces * wy * (p[c] - t);
-        dlogits[(n * C + c) * V + v] = g * d;
+    for (int r = 0; r < 4; ++r) {
+      const float t = 4 * g + r == y ? 1.f : 0.f;
+      d[r] = (ls == 0 && 4 * g + r < C) ? gsc * (p[r] * (dp[r] - sp) + ces * wy * (p[r] - t)) : 0.f;
+      bacc[r] += d[r];
+    }
+    // dx^T = W^T dlogits^T (exact fp32 MFMA), 4 channels of voxel v per lane and 16-channel tile
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) o = __builtin_amdgcn_mfma_f32_16x16x4f32(wD[t][kb], d[kb], o, 0, 0, 0);
+      const int co = 16 * t + 4 * g;
+      if (dx && ok && co < Cin) {
+        T* dst = dx + (base + v) * lddx + co;
+        if constexpr (sizeof(T) == 2) {
+          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          bf16x4 w4;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) w4[r] = (bf16_t)(dscale ? o[r] * sd[t][r] : o[r]);
+          *reinterpret_cast<bf16x4*>(dst) = w4;
+        } else {
+          float4 w4;
+          w4.x = dscale ? o[0] * sd[t][0] : o[0];
+          w4.y = dscale ? o[1] * sd[t][1] : o[1];
+          w4.z = dscale ? o[2] * sd[t][2] : o[2];
+          w4.w = dscale ? o[3] * sd[t][3] : o[3];
+          *reinterpret_cast<float4*>(dst) = w4;
+        }
       }
+    }
+    // dW[c][8g + j] += d[v][c] x[v][8g + j]: the voxel's dlogits of classes 0..NC-1 from lanes (c >> 2, v16)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const float dc = __shfl(d[c & 3], (c >> 2) * 16 + v16, 64);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[c][j] = fmaf(dc, xs[j], acc[c][j]);
+    }
   }
+  }
+  // fixed-order sums over the 16 voxel lanes of each group, then the 4 waves in order
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[c][j] += __shfl_xor(acc[c][j], o, 64);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bacc[r] += __shfl_xor(bacc[r], o, 64);
+  }
+  if (v16 == 0 && g < G)
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[wave][c * Cin + 8 * g + j] = acc[c][j];
+  if (v16 == 0)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (4 * g + r < NC) red[wave][NC * Cin + 4 * g + r] = bacc[r];
+  __syncthreads();
+  const long long blk = (long long)n * nchunk + chunk;
+  const int npairs = C * Cin + C;
+  for (int k = threadIdx.x; k < npairs; k += blockDim.x) {
+    const int src = k < C * Cin ? k : NC * Cin + (k - C * Cin);
+    wpart[blk * npairs + k] = red[0][src] + red[1][src] + red[2][src] + red[3][src];
   }
 }
 
@@ -704,6 +1065,30 @@ int loss_chunks(long long V, long long* vpc) {
   if (nch < 1) nch = 1;
   *vpc = (V + nch - 1) / nch;
   return (int)((V + *vpc - 1) / *vpc);
+}
+
+// Dispatch over the compile-time variants: storage type, 8-channel groups G (Cin = 8 G: 8 for the tiny test
+// networks, 16, 32 for the configs' heads), class slots NC >= C (<= 8), label type.
+template <typename F>
+bool head_loss_dispatch(int C, int Cin, int dtype, int label_bytes, F&& f) {
+  auto with_lt = [&](auto tag, auto g_c, auto nc_c) {
+    if (label_bytes == 8) f(tag, g_c, nc_c, int64_t{});
+    else f(tag, g_c, nc_c, uint8_t{});
+    return true;
+  };
+  auto with_nc = [&](auto tag, auto g_c) {
+    if (C <= 3) return with_lt(tag, g_c, std::integral_constant<int, 3>{});
+    if (C <= 6) return with_lt(tag, g_c, std::integral_constant<int, 6>{});
+    if (C <= 8) return with_lt(tag, g_c, std::integral_constant<int, 8>{});
+    return false;
+  };
+  auto with_g = [&](auto tag) {
+    if (Cin == 8) return with_nc(tag, std::integral_constant<int, 1>{});
+    if (Cin == 16) return with_nc(tag, std::integral_constant<int, 2>{});
+    if (Cin == 32) return with_nc(tag, std::integral_constant<int, 4>{});
+    return false;
+  };
+  return dtype == MMSEG_BF16 ? with_g(bf16_t{}) : with_g(float{});
 }
 
 }  // namespace
@@ -843,6 +1228,75 @@ int mmseg_loss_fwd(const float* logits, const void* labels, int label_bytes, int
   MMSEG_REQUIRE(shm <= 64 * 1024, "loss: batch too large for the finalize pass (N=%d, C=%d)", N, C);
   hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), shm, s, part, N, C, nch, cfg, loss_out, coef);
   return mmseg::check_launch("loss_finalize");
+}
+
+// ------------------------------------------------ fused head + loss entries
+int mmseg_head_loss_ok(int C, int Cin, int ldx, int dtype) {
+  if (C < 2 || C > 8 || ldx % 8 != 0 || !(Cin == 8 || Cin == 16 || Cin == 32)) return 0;
+  return (dtype == MMSEG_BF16 || dtype == MMSEG_F32) ? 1 : 0;
+}
+
+long long mmseg_head_loss_wpart_floats(int C, int Cin, int N, long long V) {
+  long long vpc;
+  const int nch = loss_chunks(V, &vpc);
+  return (long long)N * nch * (C * Cin + C);
+}
+
+int mmseg_head_loss_fwd(const void* x, int ldx, int Cin, const float* W, const float* b, const float* dscale, int C,
+                        int N, long long V, const void* labels, int label_bytes, int type, float dice_w, float ce_w,
+                        float smooth, float alpha, float beta, int include_bg, const float* class_w, float* loss_out,
+                        float* ws, int dtype, void* stream) {
+  MMSEG_REQUIRE(mmseg_head_loss_ok(C, Cin, ldx, dtype), "head_loss: unsupported shape (C=%d, Cin=%d, ldx=%d)", C,
+                Cin, ldx);
+  MMSEG_REQUIRE(label_bytes == 8 || label_bytes == 1, "head_loss: labels must be int64 or uint8");
+  LossCfg cfg{type, dice_w, ce_w, smooth, alpha, beta, include_bg, class_w};
+  long long vpc;
+  const int nch = loss_chunks(V, &vpc);
+  float* part = ws;
+  float* coef = ws + (long long)N * nch * (3 * C + 3);
+  hipStream_t s = (hipStream_t)stream;
+  head_loss_dispatch(C, Cin, dtype, label_bytes, [&](auto tag, auto g_c, auto nc_c, auto lt) {
+    using T = decltype(tag);
+    using LT = decltype(lt);
+    constexpr int G = decltype(g_c)::value, NC = decltype(nc_c)::value;
+    (void)NC;                 // the statistics kernel does not depend on NC: one instance per (T, G, LT)
+    mmseg::note_kernel("head_loss_stats_kernel");
+    hipLaunchKernelGGL((head_loss_stats_kernel<T, G, LT>), dim3(nch, N), dim3(256), 0, s, (const T*)x, ldx, W, b,
+                       dscale, C, (const LT*)labels, V, vpc, cfg, part);
+  });
+  if (mmseg::check_launch("head_loss_stats")) return 1;
+  const size_t shm = sizeof(double) * ((size_t)N * (3 * C + 3) + (size_t)N * C);
+  MMSEG_REQUIRE(shm <= 64 * 1024, "head_loss: batch too large for the finalize pass (N=%d, C=%d)", N, C);
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), shm, s, part, N, C, nch, cfg, loss_out, coef);
+  return mmseg::check_launch("loss_finalize");
+}
+
+// After mmseg_head_loss_fwd with the same ws.  dx may alias x (each voxel's features are read before its
+// gradient is written); dx null skips the data gradient.  gW [C][Cin] / gb [C] (=, or += with accumulate).
+int mmseg_head_loss_bwd(const void* x, int ldx, int Cin, const float* W, const float* b, const float* dscale, int C,
+                        int N, long long V, const void* labels, int label_bytes, int type, float dice_w, float ce_w,
+                        float smooth, float alpha, float beta, int include_bg, const float* class_w, const float* gout,
+                        float gconst, const float* ws, void* dx, int lddx, float* gW, float* gb, float* wpart,
+                        int accumulate, int dtype, void* stream) {
+  MMSEG_REQUIRE(mmseg_head_loss_ok(C, Cin, ldx, dtype) && (dx == nullptr || lddx % 8 == 0),
+                "head_loss_bwd: unsupported shape (C=%d, Cin=%d, ldx=%d, lddx=%d)", C, Cin, ldx, lddx);
+  LossCfg cfg{type, dice_w, ce_w, smooth, alpha, beta, include_bg, class_w};
+  long long vpc;
+  const int nch = loss_chunks(V, &vpc);
+  const float* coef = ws + (long long)N * nch * (3 * C + 3);
+  hipStream_t s = (hipStream_t)stream;
+  head_loss_dispatch(C, Cin, dtype, label_bytes, [&](auto tag, auto g_c, auto nc_c, auto lt) {
+    using T = decltype(tag);
+    using LT = decltype(lt);
+    constexpr int G = decltype(g_c)::value, NC = decltype(nc_c)::value;
+    mmseg::note_kernel("head_loss_bwd_kernel");
+    hipLaunchKernelGGL((head_loss_bwd_kernel<T, G, NC, LT>), dim3(nch, N), dim3(256), 0, s, (const T*)x, ldx, W, b,
+                       dscale, C, (const LT*)labels, V, vpc, cfg, coef, gout, gconst, (T*)dx, lddx, wpart);
+  });
+  if (mmseg::check_launch("head_loss_bwd")) return 1;
+  hipLaunchKernelGGL(head_wgrad_reduce, dim3(ceil_div(C * Cin + C, 4)), dim3(256), 0, s, wpart, N * nch, C, Cin, gW,
+                     gb, accumulate);
+  return mmseg::check_launch("head_wgrad_reduce");
 }
 
 // Must follow mmseg_loss_fwd with the same ws.  gout (device scalar) may be null.

@@ -57,6 +57,22 @@ class SegEngine:
         self.program.backward(dlogits.float().contiguous(), accumulate)
         self.flat.end_backward()
 
+    # ---- fused head + loss (Trainer fast path)
+    def forward_loss(self, x: torch.Tensor, training: bool, labels: torch.Tensor, spec: dict,
+                     cw: Optional[torch.Tensor]) -> torch.Tensor:
+        if x.dtype != torch.float32:
+            x = x.float()
+        x = x.contiguous()
+        self.ensure(x.device)
+        loss, ws = self.program.forward(x, training, loss=(labels, spec, cw))
+        self.loss_ws = ws
+        return loss
+
+    def backward_loss(self, gout: torch.Tensor) -> None:
+        accumulate = self.flat.begin_backward()
+        self.program.backward(None, accumulate, gout=gout.float().contiguous())
+        self.flat.end_backward()
+
 
 class _EngineFunction(torch.autograd.Function):
     @staticmethod
@@ -69,6 +85,44 @@ class _EngineFunction(torch.autograd.Function):
         ctx.engine.backward(dlogits)
         # parameter gradients were written by the engine into the flat arena
         return None, None, None, None
+
+
+class _EngineLossFunction(torch.autograd.Function):
+    """Network forward + head + loss as one autograd node (its input is the image, its output the loss)."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, engine, training, labels, spec, cw):
+        ctx.engine = engine
+        return engine.forward_loss(x, training, labels, spec, cw)
+
+    @staticmethod
+    def backward(ctx, gout):
+        ctx.engine.backward_loss(gout)
+        return None, None, None, None, None, None, None
+
+
+def fused_loss_supported(module: nn.Module, kind: str, x: torch.Tensor) -> bool:
+    """True when the network ends in the engine's 1x1 head and the fused head + loss kernels cover its shape
+    (UNet3D / DualEncoder, Cin 8 or 32, 2..8 classes)."""
+    if kind not in ("unet", "dual_encoder") or x.device.type != "cuda":
+        return False
+    eng = module.__dict__.get("_engine")
+    if eng is None:
+        eng = SegEngine(module, kind)
+        module.__dict__["_engine"] = eng
+    eng.ensure(x.device)
+    N, _, D, H, W = x.shape
+    eng.program.setup(N, D, H, W)
+    return eng.program.loss_ok()
+
+
+def run_engine_loss(module: nn.Module, kind: str, x: torch.Tensor, labels: torch.Tensor, spec: dict,
+                    cw: Optional[torch.Tensor]) -> torch.Tensor:
+    """forward + loss in one node (requires fused_loss_supported); backward runs the fused head + loss kernels
+    and then the network's backward, writing every parameter gradient into the flat arena."""
+    eng = module.__dict__["_engine"]
+    anchor = next(module.parameters())
+    return _EngineLossFunction.apply(x, anchor, eng, module.training, labels, spec, cw)
 
 
 def run_engine(module: nn.Module, kind: str, x: torch.Tensor) -> torch.Tensor:

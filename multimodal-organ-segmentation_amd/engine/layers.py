@@ -467,6 +467,37 @@ class Head:
         self.rt.lib.mmseg_head_fwd(x.ptr, x.ld, self.Cin, ptr(self.conv.weight), ptr(self.conv.bias), ptr(dscale),
                                    self.C, x.N, x.V, ptr(logits), self.rt.code, self.rt.stream)
 
+    # ---- fused head + loss (the Trainer's training step; csrc/loss_head.hip head_loss_*)
+    def loss_ok(self, x: Act) -> bool:
+        return x.off == 0 and bool(self.rt.lib.mmseg_head_loss_ok(self.C, self.Cin, x.ld, self.rt.code))
+
+    def fwd_loss(self, x: Act, labels: torch.Tensor, spec: dict, cw: Optional[torch.Tensor],
+                 dscale: Optional[torch.Tensor]) -> torch.Tensor:
+        """Head + loss statistics + finalize: the loss scalar, no logits written."""
+        L = self.rt.lib
+        ws = torch.empty(L.mmseg_loss_ws_floats(x.N, self.C, x.V), dtype=torch.float32, device=self.rt.device)
+        loss = torch.empty((), dtype=torch.float32, device=self.rt.device)
+        args = (spec["type"], spec["dice_w"], spec["ce_w"], spec["smooth"], spec["alpha"], spec["beta"],
+                int(spec["include_bg"]), ptr(cw))
+        L.mmseg_head_loss_fwd(x.ptr, x.ld, self.Cin, ptr(self.conv.weight), ptr(self.conv.bias), ptr(dscale), self.C,
+                              x.N, x.V, ptr(labels), labels.element_size(), *args, ptr(loss), ptr(ws), self.rt.code,
+                              self.rt.stream)
+        self.loss_state = (labels, args, ws, cw, dscale)
+        return loss, ws
+
+    def bwd_loss(self, x: Act, gout: torch.Tensor, dx: Optional[Act], accumulate: bool):
+        """dlogits (recomputed) -> head data + weight gradient, after fwd_loss."""
+        L = self.rt.lib
+        labels, args, ws, cw, dscale = self.loss_state
+        wpart = self.rt.ws(L.mmseg_head_loss_wpart_floats(self.C, self.Cin, x.N, x.V))
+        L.mmseg_head_loss_bwd(x.ptr, x.ld, self.Cin, ptr(self.conv.weight), ptr(self.conv.bias), ptr(dscale), self.C,
+                              x.N, x.V, ptr(labels), labels.element_size(), *args, ptr(gout), 1.0, ptr(ws),
+                              dx.ptr if dx is not None else None, dx.ld if dx is not None else 0,
+                              ptr(self.flat.grad(self.conv.weight)), ptr(self.flat.grad(self.conv.bias)), ptr(wpart),
+                              int(accumulate), self.rt.code, self.rt.stream)
+        self.flat.mark(self.conv.weight, self.conv.bias)
+        self.loss_state = None
+
     def bwd(self, x: Act, dlogits: torch.Tensor, dx: Optional[Act], accumulate: bool):
         L = self.rt.lib
         ws = self.rt.ws(L.mmseg_head_ws_floats(self.C, self.Cin, x.N, x.V))

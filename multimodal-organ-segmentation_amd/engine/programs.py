@@ -60,7 +60,8 @@ class _Decoder:
     def skip_slot(self, l: int) -> Act:
         return self.cat[l].slot(self.F[l], self.F[l])
 
-    def fwd(self, bottom: Act, training: bool):
+    def fwd(self, bottom: Act, training: bool, loss=None):
+        """-> logits; with loss = (labels, spec, class_w): the loss scalar (fused head + loss, no logits)."""
         h = bottom
         nl = len(self.F) - 1
         for j in range(nl):
@@ -72,16 +73,24 @@ class _Decoder:
         if training and self.p > 0:
             keep = torch.empty(h.N, h.C, device=self.rt.device).bernoulli_(1.0 - self.p)
             dscale = keep / (1.0 - self.p)
+        if loss is not None:
+            labels, spec, cw = loss
+            return self.head.fwd_loss(h, labels, spec, cw, dscale)
         # fresh logits every call (caching allocator, no copy): callers may keep them
         logits = torch.empty(h.N, self.head.C, h.D, h.H, h.W, dtype=torch.float32, device=self.rt.device)
         self.head.fwd(h, logits, dscale)
         return logits
 
-    def bwd(self, bottom: Act, dlogits: torch.Tensor, accumulate: bool) -> Act:
-        """Returns the gradient of `bottom` (aliases `bottom`'s buffer)."""
+    def bwd(self, bottom: Act, dlogits: Optional[torch.Tensor], accumulate: bool,
+            gout: Optional[torch.Tensor] = None) -> Act:
+        """Returns the gradient of `bottom` (aliases `bottom`'s buffer).  gout (a device scalar) instead of
+        dlogits: the fused head + loss backward of a forward that ran with `loss`."""
         nl = len(self.F) - 1
         dh = self.dout[0]
-        self.head.bwd(self.dout[0], dlogits, dh, accumulate)
+        if gout is not None:
+            self.head.bwd_loss(self.dout[0], gout, dh, accumulate)
+        else:
+            self.head.bwd(self.dout[0], dlogits, dh, accumulate)
         for j in reversed(range(nl)):
             l = nl - 1 - j
             self.blocks[j].bwd(self.cat[l], DySpec(p1=dh), self.cat[l], accumulate)   # dcat aliases cat
@@ -135,7 +144,7 @@ class UNetProgram:
     def level_out(self, l: int) -> Act:
         return self.dec.skip_slot(l) if l < self.L - 1 else self.bottom
 
-    def forward(self, x: torch.Tensor, training: bool) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, training: bool, loss=None) -> torch.Tensor:
         N, Cx, D, H, W = x.shape
         self.setup(N, D, H, W)
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
@@ -148,10 +157,13 @@ class UNetProgram:
             L.mmseg_maxpool2_fwd(prev.ptr, prev.ld, self.pooled[l].ptr, self.pooled[l].ld, ptr(self.idx[l]), N, *d,
                                  prev.C, code, s)
             self.enc[l - 1].fwd(self.pooled[l], self.level_out(l))
-        return self.dec.fwd(self.bottom, training)
+        return self.dec.fwd(self.bottom, training, loss)
 
-    def backward(self, dlogits: torch.Tensor, accumulate: bool):
-        dbottom = self.dec.bwd(self.bottom, dlogits, accumulate)
+    def loss_ok(self) -> bool:
+        return self.dec.head.loss_ok(self.dec.dout[0])
+
+    def backward(self, dlogits: Optional[torch.Tensor], accumulate: bool, gout: Optional[torch.Tensor] = None):
+        dbottom = self.dec.bwd(self.bottom, dlogits, accumulate, gout)
         dy = DySpec(p1=dbottom)
         for l in range(self.L - 1, 0, -1):
             self.enc[l - 1].bwd(self.pooled[l], dy, self.pooled[l], accumulate)   # dp aliases pooled
@@ -298,7 +310,7 @@ class DualEncoderProgram:
                                  ptr(self.idx[m][l]), N, *self.dims[l - 1], prev.C, code, s)
             blocks[l].fwd(self.pooled[m][l], self.y[m][l])
 
-    def forward(self, x: torch.Tensor, training: bool) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, training: bool, loss=None) -> torch.Tensor:
         N, Cx, D, H, W = x.shape
         if Cx != self.M:
             raise ValueError(f"DualEncoder expects {self.M} modalities, got {Cx} channels")
@@ -316,11 +328,14 @@ class DualEncoderProgram:
                 streams[0].wait_stream(streams[m])
         for l in range(self.L):
             self._fuse_fwd(l)
-        return self.dec.fwd(self.bottom, training)
+        return self.dec.fwd(self.bottom, training, loss)
 
-    def backward(self, dlogits: torch.Tensor, accumulate: bool):
+    def loss_ok(self) -> bool:
+        return self.dec.head.loss_ok(self.dec.dout[0])
+
+    def backward(self, dlogits: Optional[torch.Tensor], accumulate: bool, gout: Optional[torch.Tensor] = None):
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
-        self.dec.bwd(self.bottom, dlogits, accumulate)
+        self.dec.bwd(self.bottom, dlogits, accumulate, gout)
         M = self.M
         if self.fusion in ("mean", "add"):
             self._encoders_bwd_streams(accumulate)

@@ -63,6 +63,9 @@ class Trainer:
         self.best_metric = 0.0
         self.history = {"train_loss": [], "val_loss": [], "val_dice": []}
         self._buckets = None
+        # fused head + loss training step (engine.run_engine_loss): hardware.fused_head_loss (the
+        # MMSEG_FUSED_HEAD_LOSS env var overrides it per step, for A/B runs)
+        self.fused_head_loss = bool(config["hardware"].get("fused_head_loss", True))
         if resume_from:
             self._resume(resume_from)
 
@@ -131,6 +134,36 @@ class Trainer:
             self._buckets = ddp.GradBuckets(flat.grad_flat, flat.offsets, flat.sizes, bucket_mb=mb)
         flat.on_ready = self._buckets.param_ready if communicate else None
 
+    def _fused_loss(self, images: torch.Tensor, labels: torch.Tensor) -> Optional[torch.Tensor]:
+        """The step's loss through the fused head + loss node when the model / loss / shape allow it, else None.
+        Same values as criterion(model(images), labels): the logits are recomputed in the backward with the
+        forward's operation order, so no logits / dlogits tensors are written (five passes become two)."""
+        env = os.environ.get("MMSEG_FUSED_HEAD_LOSS")
+        if not ((env != "0") if env is not None else self.fused_head_loss):
+            return None
+        from ..engine.engine import fused_loss_supported, run_engine_loss
+        from ..models.backbones.dual_encoder import DualEncoder
+        from ..models.backbones.unet import UNet3D
+        from .losses import _HipLoss
+        crit = self.criterion
+        if not isinstance(crit, _HipLoss) or getattr(crit, "reduction", "mean") != "mean":
+            return None
+        bb = getattr(self.model, "backbone", self.model)
+        kind = "unet" if isinstance(bb, UNet3D) else "dual_encoder" if isinstance(bb, DualEncoder) else None
+        if kind is None or not fused_loss_supported(bb, kind, images):
+            return None
+        N = images.shape[0]
+        if labels.dtype not in (torch.int64, torch.uint8):
+            labels = labels.long()
+        labels = labels.contiguous()
+        if labels.numel() != N * images[0, 0].numel():
+            raise ValueError(f"target shape {tuple(labels.shape)} does not match images {tuple(images.shape)}")
+        cw = getattr(crit, "class_weights", None)
+        cw = None if cw is None else cw.to(images.device, torch.float32).contiguous()
+        loss = run_engine_loss(bb, kind, images, labels, crit._spec(), cw)
+        crit.__dict__["_last_ws"] = bb.__dict__["_engine"].loss_ws     # for check_labels()
+        return loss
+
     # ----------------------------------------------------------- training
     def train_step(self, batch: Dict[str, torch.Tensor], batch_idx: int, sync: bool = True) -> Union[float, torch.Tensor]:
         """One per-batch body of the reference's _train_epoch (trainer.py:231-261):
@@ -140,8 +173,10 @@ class Trainer:
         images = batch["image"].to(self.device, non_blocking=True)
         labels = batch["label"].to(self.device, non_blocking=True)
         boundary = (batch_idx + 1) % self.accumulation_steps == 0
-        outputs = self.model(images)
-        loss = self.criterion(outputs, labels) / self.accumulation_steps
+        loss = self._fused_loss(images, labels)
+        if loss is None:
+            loss = self.criterion(self.model(images), labels)
+        loss = loss / self.accumulation_steps
         self._arm_buckets(boundary)
         loss.backward()
         if boundary:

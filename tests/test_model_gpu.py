@@ -279,3 +279,47 @@ def test_train_step_raises_on_out_of_range_labels(dev):
     bad[0, 0, 0, 0] = C
     with pytest.raises(RuntimeError, match="outside"):
         tr.train_step({"image": xs[0], "label": bad}, 0)
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("tag", ["unet_tiny", "dual_tiny_cross_attention"])
+def test_fused_head_loss_matches_unfused(dev, tag, dtype):
+    """Trainer's fused head + loss node (engine.run_engine_loss: no logits / dlogits tensors, logits recomputed
+    in the backward) against model(x) -> criterion -> backward, for every HIP loss, class weights, uint8 labels
+    and an active Dropout3d (same device RNG state for both runs)."""
+    from mmseg_amd.engine.engine import fused_loss_supported, run_engine_loss
+    from mmseg_amd.trainer.losses import CrossEntropyLoss, DiceCELoss, DiceLoss, FocalLoss, TverskyLoss
+    cfg, m, g, M, C = _build(tag, dtype)
+    m.backbone.dropout_p = 0.3
+    m.train()
+    xs, ys = _inputs(g, M, C)
+    x, y = xs[0].to(dev), ys[0].to(dev)
+    bb = m.backbone
+    kind = "unet" if tag == "unet_tiny" else "dual_encoder"
+    assert fused_loss_supported(bb, kind, x)
+    cw = torch.rand(C, generator=torch.Generator().manual_seed(3)) + 0.5
+    losses = {"dicece": DiceCELoss(), "dicece_w": DiceCELoss(0.3, 0.7, class_weights=cw), "dice": DiceLoss(),
+              "ce_w": CrossEntropyLoss(weight=cw), "tversky": TverskyLoss(0.3, 0.7), "focal": FocalLoss()}
+    tol = 1e-5 if dtype == "float32" else 2e-2
+    for name, crit in losses.items():
+        for lab in (y, y.to(torch.uint8)):
+            res = []
+            for fused in (False, True):
+                m.zero_grad(set_to_none=True)
+                torch.cuda.manual_seed(7)
+                if fused:
+                    c = getattr(crit, "class_weights", None)
+                    c = None if c is None else c.to(dev, torch.float32)
+                    loss = run_engine_loss(bb, kind, x, lab, crit._spec(), c)
+                else:
+                    loss = crit(m(x), lab)
+                (loss * 0.5).backward()
+                torch.cuda.synchronize()
+                # conv biases in front of an InstanceNorm have a gradient of pure rounding noise (DESIGN (a)):
+                # compared are the weights and the head's bias
+                res.append((loss.item(), [p.grad.detach().double().cpu().clone() for n, p in m.named_parameters()
+                                          if not n.endswith("bias") or "out_conv" in n]))
+            (lu, gu), (lf, gf) = res
+            assert abs(lu - lf) <= 1e-5 * max(1.0, abs(lu)), (name, lu, lf)
+            for a, b in zip(gf, gu):
+                assert ((a - b).norm() / b.norm()).item() < tol, (name, dtype)
