@@ -170,12 +170,21 @@ int mmseg_instnorm_bwd(const void* x, int ldx, const float* mean, const float* r
 /* MaxPool3d(2) forward + argmax (0..7, z-major; first max wins) (unet.py:73). */
 int mmseg_maxpool2_fwd(const void* x, int ldx, void* y, int ldy, uint8_t* idx, int N, int D, int H, int W, int C,
                        int dtype, void* stream);
+/* The same over relu((x - mean) * rstd) of a PRE-norm x (mean / rstd [N][C]): values and argmax equal pooling
+ * the materialised InstanceNorm + ReLU output (rounded to the storage type first), which is never written. */
+int mmseg_maxpool2_norm_fwd(const void* x, int ldx, const float* mean, const float* rstd, void* y, int ldy,
+                            uint8_t* idx, int N, int D, int H, int W, int C, int dtype, void* stream);
 
 /* ---------------------------------------------------- modality fusion */
 /* out = wconst * sum_m src_m (mean / add fusion, dual_encoder.py:184-186,193-195)
  * or sum_m wts[n][m] * src_m (CrossModalAttention weighting, dual_encoder.py:252-254). */
 int mmseg_fuse_fwd(const void* const* srcs, const int* lds, int M, float wconst, const float* wts, void* out, int ldo,
                    int N, long long V, int C, int dtype, void* stream);
+/* mmseg_fuse_fwd over relu((src_m - mean_m) * rstd_m) of PRE-norm sources (the encoders' last InstanceNorm +
+ * ReLU applied on load; means / rstds: M pointers to [N][C] statistics). */
+int mmseg_fuse_norm_fwd(const void* const* srcs, const int* lds, const float* const* means, const float* const* rstds,
+                        int M, float wconst, const float* wts, void* out, int ldo, int N, long long V, int C,
+                        int dtype, void* stream);
 /* CrossModalAttention gate: Linear -> ReLU -> Linear -> softmax (dual_encoder.py:226-233). */
 int mmseg_attn_gate_fwd(const float* pooled, const float* W1, const float* b1, const float* W2, const float* b2,
                         float* hbuf, float* wts, int N, int MC, int Hd, int M, void* stream);

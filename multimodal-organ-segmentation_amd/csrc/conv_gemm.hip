@@ -3304,7 +3304,7 @@ int brick_wgrad_splits(long long V, int cap, int Ca, int cpg_shift, int kind, in
   if (kind >= 2) {
     const int slots = (kind == 2 && Ca % 64 != 0 && knob("MMSEG_WGRAD_V3", 1) == 0) ? 512
                       : kind == 3 ? knob("MMSEG_WGRAD_RSLOTS", 256)   // runtime-brick kernel (24^3 .. 6^3 levels)
-                                  : 256;
+                                  : knob("MMSEG_WGRAD_SLOTS", 256);
     ks = (long long)slots * knob("MMSEG_WGRAD_WAVES", 1) / tiles;
   } else {
     ks = (1024 + tiles - 1) / tiles;

@@ -286,9 +286,13 @@ __global__ void in_relu_apply(const T* __restrict__ x, int ldx, T* __restrict__ 
 
 // --------------------------------------------------------------- maxpool
 // 2x2x2, stride 2.  idx = a*4 + b*2 + c (z,y,x), first maximum wins.
-template <typename T>
+// NORM: x is the PRE-norm activation and the pooled values are relu((x - mean) * rstd) rounded to T, i.e.
+// exactly in_relu_apply's output, so values and argmax (ties included) equal pooling the materialised
+// InstanceNorm + ReLU output, which then never has to be written (DualEncoder mean / add fusion).
+template <typename T, bool NORM = false>
 __global__ void maxpool2_fwd(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy,
-                             uint8_t* __restrict__ idx, int N, int D, int H, int W, int C) {
+                             uint8_t* __restrict__ idx, int N, int D, int H, int W, int C,
+                             const float* __restrict__ mean = nullptr, const float* __restrict__ rstd = nullptr) {
   const int C8 = C >> 3;
   const int Do = D >> 1, Ho = H >> 1, Wo = W >> 1;
   const long long Vo = (long long)Do * Ho * Wo;
@@ -306,11 +310,23 @@ __global__ void maxpool2_fwd(const T* __restrict__ x, int ldx, T* __restrict__ y
     const long long in0 = ((n * D + 2 * zo) * H + 2 * yo) * (long long)W + 2 * xo;
     float best[8];
     uint8_t bi[8];
+    float mu[8], rs[8];
+    if constexpr (NORM) {
+      load8f(mean + n * C + cg * 8, mu);
+      load8f(rstd + n * C + cg * 8, rs);
+    }
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       const long long vin = in0 + ((long long)(t >> 2) * H + ((t >> 1) & 1)) * W + (t & 1);
       V8<T> a;
       a.load(x + vin * ldx + cg * 8);
+      if constexpr (NORM) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float h = (a.get(j) - mu[j]) * rs[j];
+          a.set(j, h > 0.f ? h : 0.f);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         // torch CPU max_pool3d: (val > maxval) || isnan(val) replaces
@@ -597,20 +613,34 @@ __global__ void in_bwd_apply(const T* __restrict__ x, int ldx, const float* __re
 
 
 // ------------------------------------------------- small-volume fused IN
-// The 24^3 / 12^3 / 6^3 levels (V <= 16384 voxels per sample): one block of
-// 1024 threads per (8-channel group, sample) holds the whole reduction, so
-// InstanceNorm forward is ONE launch (statistics, then the normalised output
-// from a second, L2-resident read) instead of partial + finalize + apply, and
-// the backward likewise.  Per-thread Welford / sums in fp32, then a fixed
-// pairwise tree over the 1024 threads in LDS (deterministic).
-constexpr int SMALL_T = 1024;
+// The 12^3 / 6^3 levels (V <= 4096 voxels per sample): one 256-thread block per (8-channel group, sample)
+// holds the whole reduction, so InstanceNorm forward is ONE launch (statistics, then the normalised output
+// from a second, L2-resident read) instead of partial + finalize + apply, and the backward likewise.
+// Per-thread Welford / sums in fp32; lanes merge with a fixed xor-shuffle tree (Chan's formula for the
+// Welford pairs), then the 4 waves in order through LDS: deterministic.  (The previous 1024-thread form
+// with a 10-level LDS tree and 68 KB of LDS spent most of its time in the tree: ~1.7 voxels per thread.)
+constexpr int SMALL_T = 256;
+
+__device__ __forceinline__ void chan_merge(float& cnt, float* mu, float* m2, float nb, const float* mb,
+                                           const float* m2b) {
+  const float na = cnt, nn = na + nb;
+  if (nb > 0.f) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float dl = mb[j] - mu[j];
+      mu[j] = mu[j] + dl * (nb / nn);
+      m2[j] = m2[j] + m2b[j] + dl * dl * (na * nb / nn);
+    }
+    cnt = nn;
+  }
+}
 
 template <typename T, bool RELU>
 __global__ __launch_bounds__(SMALL_T) void in_small_fwd(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy,
                                                        int V, int C, float eps, float* __restrict__ mean,
                                                        int mean_ld, float* __restrict__ rstd) {
-  __shared__ float smu[SMALL_T * 8], sm2[SMALL_T * 8], scnt[SMALL_T];
-  const int cg = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
+  __shared__ float smu[4][8], sm2[4][8], scnt[4], sfin[16];
+  const int cg = blockIdx.x, n = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const T* xn = x + (long long)n * V * ldx + cg * 8;
   float mu[8], m2[8], cnt = 0.f;
 #pragma unroll
@@ -639,13 +669,176 @@ __global__ __launch_bounds__(SMALL_T) void in_small_fwd(const T* __restrict__ x,
     upd(a);
   }
 #pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float mb[8], m2b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mb[j] = __shfl_xor(mu[j], o, 64);
+      m2b[j] = __shfl_xor(m2[j], o, 64);
+    }
+    chan_merge(cnt, mu, m2, __shfl_xor(cnt, o, 64), mb, m2b);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      smu[wave][j] = mu[j];
+      sm2[wave][j] = m2[j];
+    }
+    scnt[wave] = cnt;
+  }
+  __syncthreads();
+  if (tid < 8) {   // channel tid: the 4 waves in order
+    float c0 = scnt[0], m0 = smu[0][tid], q0 = sm2[0][tid];
+    for (int w = 1; w < 4; ++w) {
+      const float nb = scnt[w], nn = c0 + nb;
+      if (nb > 0.f) {
+        const float dl = smu[w][tid] - m0;
+        m0 = m0 + dl * (nb / nn);
+        q0 = q0 + sm2[w][tid] + dl * dl * (c0 * nb / nn);
+        c0 = nn;
+      }
+    }
+    const float rs = 1.f / sqrtf(q0 / (float)V + eps);
+    sfin[tid] = m0;
+    sfin[8 + tid] = rs;
+    mean[(long long)n * mean_ld + cg * 8 + tid] = m0;
+    rstd[n * C + cg * 8 + tid] = rs;
+  }
+  __syncthreads();
+  float m[8], rs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    m[j] = sfin[j];
+    rs[j] = sfin[8 + j];
+  }
+  T* yn = y + (long long)n * V * ldy + cg * 8;
+  for (int v = tid; v < V; v += SMALL_T) {
+    V8<T> a, o;
+    a.load(xn + (long long)v * ldx);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float h = (a.get(j) - m[j]) * rs[j];
+      o.set(j, (!RELU || h > 0.f) ? h : 0.f);
+    }
+    o.store(yn + (long long)v * ldy);
+  }
+}
+
+template <typename T, bool RELU>
+__global__ __launch_bounds__(SMALL_T) void in_small_bwd(const T* __restrict__ x, int ldx, const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd, DySrc s, T* __restrict__ dx,
+                                                       int lddx, int V, int C, int D, int H, int W) {
+  __shared__ float sa[4][8], sb[4][8], sfin[16];
+  const int cg = blockIdx.x, n = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float mu[8], rs[8], ga[8], gb[8];
+  load8f(mean + n * C + cg * 8, mu);
+  load8f(rstd + n * C + cg * 8, rs);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ga[j] = gb[j] = 0.f;
+  const DyCtx<T> dc(s, n, V, cg, C, D, H, W);
+  const T* xn = x + (long long)n * V * ldx + cg * 8;
+  for (int v = tid; v < V; v += SMALL_T) {
+    V8<T> a;
+    typename DyCtx<T>::Raw r;
+    a.load(xn + (long long)v * ldx);
+    dc.load(v, r);
+    float dy[8];
+    dc.combine(r, dy);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float h = (a.get(j) - mu[j]) * rs[j];
+      const float g = (!RELU || h > 0.f) ? dy[j] : 0.f;
+      ga[j] += g;
+      gb[j] = fmaf(g, h, gb[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ga[j] = wave_sum(ga[j]);
+    gb[j] = wave_sum(gb[j]);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sa[wave][j] = ga[j];
+      sb[wave][j] = gb[j];
+    }
+  }
+  __syncthreads();
+  if (tid < 8) {
+    sfin[tid] = (((sa[0][tid] + sa[1][tid]) + sa[2][tid]) + sa[3][tid]) / (float)V;
+    sfin[8 + tid] = (((sb[0][tid] + sb[1][tid]) + sb[2][tid]) + sb[3][tid]) / (float)V;
+  }
+  __syncthreads();
+  float ca[8], cb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ca[j] = sfin[j];
+    cb[j] = sfin[8 + j];
+  }
+  T* dxn = dx + (long long)n * V * lddx + cg * 8;
+  for (int v = tid; v < V; v += SMALL_T) {
+    V8<T> a;
+    typename DyCtx<T>::Raw r;
+    a.load(xn + (long long)v * ldx);
+    dc.load(v, r);
+    float dy[8];
+    dc.combine(r, dy);
+    V8<T> o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float h = (a.get(j) - mu[j]) * rs[j];
+      const float g = (!RELU || h > 0.f) ? dy[j] : 0.f;
+      o.set(j, rs[j] * (g - ca[j] - h * cb[j]));
+    }
+    o.store(dxn + (long long)v * lddx);
+  }
+}
+
+// The previous form (MMSEG_IN_SMALL_T=1024): 1024 threads, 10-level LDS tree.
+constexpr int SMALL_T1K = 1024;
+
+template <typename T, bool RELU>
+__global__ __launch_bounds__(SMALL_T1K) void in_small_fwd_1k(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy,
+                                                       int V, int C, float eps, float* __restrict__ mean,
+                                                       int mean_ld, float* __restrict__ rstd) {
+  __shared__ float smu[SMALL_T1K * 8], sm2[SMALL_T1K * 8], scnt[SMALL_T1K];
+  const int cg = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
+  const T* xn = x + (long long)n * V * ldx + cg * 8;
+  float mu[8], m2[8], cnt = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) mu[j] = m2[j] = 0.f;
+  auto upd = [&](const V8<T>& a) {
+    cnt += 1.f;
+    const float inv = 1.f / cnt;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xv = a.get(j), d = xv - mu[j];
+      mu[j] = fmaf(d, inv, mu[j]);
+      m2[j] = fmaf(d, xv - mu[j], m2[j]);
+    }
+  };
+  int v = tid;
+  for (; v + 3 * SMALL_T1K < V; v += 4 * SMALL_T1K) {   // 4 loads in flight
+    V8<T> a[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u].load(xn + (long long)(v + u * SMALL_T1K) * ldx);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) upd(a[u]);
+  }
+  for (; v < V; v += SMALL_T1K) {
+    V8<T> a;
+    a.load(xn + (long long)v * ldx);
+    upd(a);
+  }
+#pragma unroll
   for (int j = 0; j < 8; ++j) {
     smu[tid * 8 + j] = mu[j];
     sm2[tid * 8 + j] = m2[j];
   }
   scnt[tid] = cnt;
   __syncthreads();
-  for (int st = SMALL_T / 2; st > 0; st >>= 1) {   // Chan merge of thread t and t + st, fixed pairs
+  for (int st = SMALL_T1K / 2; st > 0; st >>= 1) {   // Chan merge of thread t and t + st, fixed pairs
     if (tid < st) {
       const float na = scnt[tid], nb = scnt[tid + st], nn = na + nb;
       if (nb > 0.f) {
@@ -671,7 +864,7 @@ __global__ __launch_bounds__(SMALL_T) void in_small_fwd(const T* __restrict__ x,
     rstd[n * C + cg * 8 + tid] = 1.f / sqrtf(sm2[tid] / (float)V + eps);
   }
   T* yn = y + (long long)n * V * ldy + cg * 8;
-  for (int v = tid; v < V; v += SMALL_T) {
+  for (int v = tid; v < V; v += SMALL_T1K) {
     V8<T> a, o;
     a.load(xn + (long long)v * ldx);
 #pragma unroll
@@ -684,10 +877,10 @@ __global__ __launch_bounds__(SMALL_T) void in_small_fwd(const T* __restrict__ x,
 }
 
 template <typename T, bool RELU>
-__global__ __launch_bounds__(SMALL_T) void in_small_bwd(const T* __restrict__ x, int ldx, const float* __restrict__ mean,
+__global__ __launch_bounds__(SMALL_T1K) void in_small_bwd_1k(const T* __restrict__ x, int ldx, const float* __restrict__ mean,
                                                        const float* __restrict__ rstd, DySrc s, T* __restrict__ dx,
                                                        int lddx, int V, int C, int D, int H, int W) {
-  __shared__ float sa[SMALL_T * 8], sb[SMALL_T * 8];
+  __shared__ float sa[SMALL_T1K * 8], sb[SMALL_T1K * 8];
   const int cg = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
   float mu[8], rs[8], ga[8], gb[8];
   load8f(mean + n * C + cg * 8, mu);
@@ -696,7 +889,7 @@ __global__ __launch_bounds__(SMALL_T) void in_small_bwd(const T* __restrict__ x,
   for (int j = 0; j < 8; ++j) ga[j] = gb[j] = 0.f;
   const DyCtx<T> dc(s, n, V, cg, C, D, H, W);
   const T* xn = x + (long long)n * V * ldx + cg * 8;
-  for (int v = tid; v < V; v += SMALL_T) {
+  for (int v = tid; v < V; v += SMALL_T1K) {
     V8<T> a;
     typename DyCtx<T>::Raw r;
     a.load(xn + (long long)v * ldx);
@@ -717,7 +910,7 @@ __global__ __launch_bounds__(SMALL_T) void in_small_bwd(const T* __restrict__ x,
     sb[tid * 8 + j] = gb[j];
   }
   __syncthreads();
-  for (int st = SMALL_T / 2; st > 0; st >>= 1) {
+  for (int st = SMALL_T1K / 2; st > 0; st >>= 1) {
     if (tid < st) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -734,7 +927,7 @@ __global__ __launch_bounds__(SMALL_T) void in_small_bwd(const T* __restrict__ x,
     cb[j] = sb[j] / (float)V;
   }
   T* dxn = dx + (long long)n * V * lddx + cg * 8;
-  for (int v = tid; v < V; v += SMALL_T) {
+  for (int v = tid; v < V; v += SMALL_T1K) {
     V8<T> a;
     typename DyCtx<T>::Raw r;
     a.load(xn + (long long)v * ldx);
@@ -760,9 +953,11 @@ struct FuseSrc {
   int M;
   float wconst;
   const float* wts;   // [N][M] or null
+  const float* mean[4];   // NORM: per-source InstanceNorm statistics [N][C] (sources are pre-norm, + ReLU)
+  const float* rstd[4];
 };
 
-template <typename T>
+template <typename T, bool NORM = false>
 __global__ void fuse_fwd(FuseSrc s, T* __restrict__ out, int ldo, long long V, int N, int C) {
   const int C8 = C >> 3;
   const long long total = (long long)N * V * C8;
@@ -777,6 +972,16 @@ __global__ void fuse_fwd(FuseSrc s, T* __restrict__ out, int ldo, long long V, i
     for (int m = 0; m < s.M; ++m) {
       V8<T> a;
       a.load(reinterpret_cast<const T*>(s.p[m]) + nv * s.ld[m] + cg * 8);
+      if constexpr (NORM) {   // in_relu_apply's value, rounded to T as the materialised output would be
+        float mu[8], rs[8];
+        load8f(s.mean[m] + n * C + cg * 8, mu);
+        load8f(s.rstd[m] + n * C + cg * 8, rs);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float h = (a.get(j) - mu[j]) * rs[j];
+          a.set(j, h > 0.f ? h : 0.f);
+        }
+      }
       const float w = s.wts ? s.wts[n * s.M + m] : 1.f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] = s.wts ? fmaf(a.get(j), w, acc[j]) : acc[j] + a.get(j);
@@ -937,6 +1142,11 @@ int knob_small_v() {   // read per call (A/B runs and tests flip it in-process)
   return e ? atoi(e) : 4096;
 }
 
+int knob_small_t() {
+  const char* e = getenv("MMSEG_IN_SMALL_T");
+  return e ? atoi(e) : 256;
+}
+
 int chunks_for(long long V, int C, long long* vpc) {
   // reduction passes: ~16 voxels per thread (lanes_v = 256 / C8 voxel lanes), at most 1024 chunks
   const int lanes_v = 256 / (C >> 3);
@@ -1023,8 +1233,12 @@ int mmseg_instnorm_fwd(const void* x, int ldx, void* y, int ldy, int N, long lon
   auto run = [&](auto tag, auto relu_c) {
     using T = decltype(tag);
     constexpr bool R = decltype(relu_c)::value;
-    hipLaunchKernelGGL((in_small_fwd<T, R>), grid, dim3(SMALL_T), 0, s, (const T*)x, ldx, (T*)y, ldy, (int)V, C, eps,
-                       mean, mean_ld, rstd);
+    if (knob_small_t() == 1024)
+      hipLaunchKernelGGL((in_small_fwd_1k<T, R>), grid, dim3(SMALL_T1K), 0, s, (const T*)x, ldx, (T*)y, ldy, (int)V, C,
+                         eps, mean, mean_ld, rstd);
+    else
+      hipLaunchKernelGGL((in_small_fwd<T, R>), grid, dim3(SMALL_T), 0, s, (const T*)x, ldx, (T*)y, ldy, (int)V, C, eps,
+                         mean, mean_ld, rstd);
   };
   if (dtype == MMSEG_BF16) {
     if (relu) run(bf16_t{}, std::true_type{});
@@ -1098,8 +1312,12 @@ int mmseg_instnorm_bwd(const void* x, int ldx, const float* mean, const float* r
     using T = decltype(tag);
     constexpr bool R = decltype(relu_c)::value;
     if (small) {
-      hipLaunchKernelGGL((in_small_bwd<T, R>), dim3(C / 8, N), dim3(SMALL_T), 0, s, (const T*)x, ldx, mean, rstd, src,
-                         (T*)dx, lddx, (int)V, C, D, H, W);
+      if (knob_small_t() == 1024)
+        hipLaunchKernelGGL((in_small_bwd_1k<T, R>), dim3(C / 8, N), dim3(SMALL_T1K), 0, s, (const T*)x, ldx, mean, rstd,
+                           src, (T*)dx, lddx, (int)V, C, D, H, W);
+      else
+        hipLaunchKernelGGL((in_small_bwd<T, R>), dim3(C / 8, N), dim3(SMALL_T), 0, s, (const T*)x, ldx, mean, rstd, src,
+                           (T*)dx, lddx, (int)V, C, D, H, W);
       return;
     }
     hipLaunchKernelGGL((in_bwd_partial<T, R>), grid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, (int)V, C, D,
@@ -1130,6 +1348,46 @@ int mmseg_maxpool2_fwd(const void* x, int ldx, void* y, int ldy, uint8_t* idx, i
     hipLaunchKernelGGL(maxpool2_fwd<float>, dim3(grid), dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy, idx, N,
                        D, H, W, C);
   return mmseg::check_launch("maxpool2_fwd");
+}
+
+// mmseg_maxpool2_fwd over relu((x - mean) * rstd) (x pre-norm, mean / rstd [N][C]): equal to pooling the
+// materialised InstanceNorm + ReLU output.
+int mmseg_maxpool2_norm_fwd(const void* x, int ldx, const float* mean, const float* rstd, void* y, int ldy,
+                            uint8_t* idx, int N, int D, int H, int W, int C, int dtype, void* stream) {
+  MMSEG_REQUIRE(C % 8 == 0 && ((D | H | W) & 1) == 0, "maxpool2: C%%8==0 and even dims required");
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = grid_for((long long)N * (D / 2) * (H / 2) * (W / 2) * (C / 8));
+  if (dtype == MMSEG_BF16)
+    hipLaunchKernelGGL((maxpool2_fwd<bf16_t, true>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x, ldx, (bf16_t*)y,
+                       ldy, idx, N, D, H, W, C, mean, rstd);
+  else
+    hipLaunchKernelGGL((maxpool2_fwd<float, true>), dim3(grid), dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy,
+                       idx, N, D, H, W, C, mean, rstd);
+  return mmseg::check_launch("maxpool2_norm_fwd");
+}
+
+// mmseg_fuse_fwd over relu((src_m - mean_m) * rstd_m) (pre-norm sources, statistics [N][C] per source)
+int mmseg_fuse_norm_fwd(const void* const* srcs, const int* lds, const float* const* means, const float* const* rstds,
+                        int M, float wconst, const float* wts, void* out, int ldo, int N, long long V, int C,
+                        int dtype, void* stream) {
+  MMSEG_REQUIRE(M >= 1 && M <= 4 && C % 8 == 0, "fuse: 1 <= M <= 4 and C%%8==0");
+  FuseSrc s{};
+  for (int m = 0; m < M; ++m) {
+    s.p[m] = srcs[m];
+    s.ld[m] = lds[m];
+    s.mean[m] = means[m];
+    s.rstd[m] = rstds[m];
+  }
+  s.M = M;
+  s.wconst = wconst;
+  s.wts = wts;
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = grid_for((long long)N * V * (C / 8));
+  if (dtype == MMSEG_BF16)
+    hipLaunchKernelGGL((fuse_fwd<bf16_t, true>), dim3(grid), dim3(256), 0, st, s, (bf16_t*)out, ldo, V, N, C);
+  else
+    hipLaunchKernelGGL((fuse_fwd<float, true>), dim3(grid), dim3(256), 0, st, s, (float*)out, ldo, V, N, C);
+  return mmseg::check_launch("fuse_norm_fwd");
 }
 
 // out = wconst * sum_m src_m   (wts == null)   or   sum_m wts[n][m] * src_m

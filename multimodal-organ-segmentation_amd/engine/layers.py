@@ -387,6 +387,10 @@ class Block:
         self.c2 = Conv3(rt, module.conv2, flat)
         self.Co = self.c1.Co
         self.shape = None
+        # defer_out: the block's last InstanceNorm + ReLU is applied by its consumers on load (DualEncoder mean /
+        # add fusion: maxpool + fusion read x2 and the statistics), so `out` is not written by fwd();
+        # materialize_out() writes it when someone needs it (return_features)
+        self.defer_out = False
 
     def descs(self):
         return self.c1.descs() + self.c2.descs()
@@ -442,7 +446,27 @@ class Block:
         self.c1.fwd(xin, self.x1, stats_part=p1)
         self._norm_fwd(self.x1, self.y1, st[0], st[1], p1, self.nb[0])
         self.c2.fwd(self.y1, self.x2, stats_part=p2)
-        self._norm_fwd(self.x2, out, st[2], st[3], p2, self.nb[1])
+        if self.defer_out:
+            self._norm_stats(self.x2, st[2], st[3], p2, self.nb[1])
+        else:
+            self._norm_fwd(self.x2, out, st[2], st[3], p2, self.nb[1])
+
+    def _norm_stats(self, x: Act, m: torch.Tensor, r: torch.Tensor, part=None, nb: int = 0):
+        L, s, code = self.rt.lib, self.rt.stream, self.rt.code
+        if part is not None:
+            L.mmseg_instnorm_stats_bricks(ptr(part), x.N, x.C, nb, x.V // nb, IN_EPS, ptr(m), x.C, ptr(r), s)
+        else:
+            ws = self.rt.ws(L.mmseg_instnorm_ws_floats(x.N, x.V, x.C))
+            L.mmseg_instnorm_stats(x.ptr, x.ld, x.N, x.V, x.C, IN_EPS, ptr(m), x.C, ptr(r), ptr(ws), code, s)
+
+    def out_stats(self):
+        """(pre-norm x2, mean, rstd) of the block's output InstanceNorm (for consumers of a deferred output)."""
+        return self.x2, self.stats[2], self.stats[3]
+
+    def materialize_out(self, out: Act):
+        L = self.rt.lib
+        L.mmseg_instnorm_relu_fwd(self.x2.ptr, self.x2.ld, out.ptr, out.ld, self.x2.N, self.x2.V, self.x2.C,
+                                  ptr(self.stats[2]), ptr(self.stats[3]), self.rt.code, self.rt.stream)
 
     def bwd(self, xin: Act, dy: DySpec, dxin: Optional[Act], accumulate: bool):
         st = self.stats

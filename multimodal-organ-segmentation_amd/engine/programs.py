@@ -25,6 +25,9 @@ from .layers import Block, ConvT2, DySpec, Head, Packer, Point
 from .runtime import Act, FlatParams, Runtime
 
 
+SMALL_IN_V = 4096   # norm_pool.hip knob_small_v(): at or below it InstanceNorm is one launch (stats + apply)
+
+
 def _check_dims(D, H, W, levels):
     f = 1 << (levels - 1)
     if D % f or H % f or W % f:
@@ -228,6 +231,7 @@ class DualEncoderProgram:
         else:
             self.y = [[rt.act(N, *dims[l], F[l]) for l in range(self.L)] for _ in range(M)]
         self.pooled = [[None] + [rt.act(N, *dims[l], F[l - 1]) for l in range(1, self.L)] for _ in range(M)]
+
         self.idx = [[None] + [torch.empty(N * dims[l][0] * dims[l][1] * dims[l][2] * F[l - 1], dtype=torch.uint8,
                                           device=rt.device) for l in range(1, self.L)] for _ in range(M)]
         self.bottom = rt.act(N, *dims[-1], F[-1])
@@ -263,7 +267,21 @@ class DualEncoderProgram:
             L.mmseg_fuse_fwd(srcs, lds, self.M, 1.0, ptr(self.gate_w[l]), out.ptr, out.ld, N, V, C, code, s)
         else:
             wconst = 1.0 if self.fusion == "add" else 1.0 / self.M
-            L.mmseg_fuse_fwd(srcs, lds, self.M, wconst, None, out.ptr, out.ld, N, V, C, code, s)
+            blks = [self.encs[m][l] for m in range(self.M)]
+            if blks[0].defer_out:
+                st = [b.out_stats() for b in blks]
+                L.mmseg_fuse_norm_fwd(_ptr_array([t[0].ptr for t in st]), _int_array([t[0].ld for t in st]),
+                                      _ptr_array([t[1].data_ptr() for t in st]), _ptr_array([t[2].data_ptr() for t in st]),
+                                      self.M, wconst, None, out.ptr, out.ld, N, V, C, code, s)
+            else:
+                L.mmseg_fuse_fwd(srcs, lds, self.M, wconst, None, out.ptr, out.ld, N, V, C, code, s)
+
+    def materialize_features(self):
+        """Write the encoder outputs the forward left deferred (return_features reads them)."""
+        for m in range(self.M):
+            for l in range(self.L):
+                if self.encs[m][l].defer_out:
+                    self.encs[m][l].materialize_out(self.y[m][l])
 
     # ------------------------------------------------------- modality streams
     # The M encoders are independent until the per-level fusion (forward) and after the decoder backward
@@ -306,8 +324,14 @@ class DualEncoderProgram:
                 blocks[0].fwd(self.xin_v[m], self.y[m][0])
                 continue
             prev = self.y[m][l - 1]
-            L.mmseg_maxpool2_fwd(prev.ptr, prev.ld, self.pooled[m][l].ptr, self.pooled[m][l].ld,
-                                 ptr(self.idx[m][l]), N, *self.dims[l - 1], prev.C, code, s)
+            pb = blocks[l - 1]
+            if pb.defer_out:
+                x2, mu, rs = pb.out_stats()
+                L.mmseg_maxpool2_norm_fwd(x2.ptr, x2.ld, ptr(mu), ptr(rs), self.pooled[m][l].ptr, self.pooled[m][l].ld,
+                                          ptr(self.idx[m][l]), N, *self.dims[l - 1], prev.C, code, s)
+            else:
+                L.mmseg_maxpool2_fwd(prev.ptr, prev.ld, self.pooled[m][l].ptr, self.pooled[m][l].ld,
+                                     ptr(self.idx[m][l]), N, *self.dims[l - 1], prev.C, code, s)
             blocks[l].fwd(self.pooled[m][l], self.y[m][l])
 
     def forward(self, x: torch.Tensor, training: bool, loss=None) -> torch.Tensor:
@@ -316,6 +340,13 @@ class DualEncoderProgram:
             raise ValueError(f"DualEncoder expects {self.M} modalities, got {Cx} channels")
         self.setup(N, D, H, W)
         self.pack()
+        # mean / add fusion: an encoder level's output IN + ReLU is applied on load by its maxpool and the fusion
+        # kernel (its only readers), so the apply pass never writes y (levels above the one-launch small-IN size)
+        defer = self.fusion in ("mean", "add") and os.environ.get("MMSEG_DEFER_ENC_NORM", "1") != "0"
+        for m in range(self.M):
+            for l in range(self.L):
+                d = self.dims[l]
+                self.encs[m][l].defer_out = defer and d[0] * d[1] * d[2] > SMALL_IN_V
         streams = self._streams()
         split = min(max(self.stream_level, 0), self.L)
         for m in range(self.M):                      # big levels: one stream, modality after modality

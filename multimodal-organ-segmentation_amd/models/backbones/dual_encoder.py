@@ -84,6 +84,7 @@ class DualEncoder(nn.Module):
         logits = run_engine(self, "dual_encoder", x)
         if return_features:
             prog = self.__dict__["_engine"].program
+            prog.materialize_features()
             enc = [[prog.y[m][l].to_ncdhw() for l in range(len(self.features))] for m in range(self.num_modalities)]
             fused = [prog.fused_out(l).to_ncdhw() for l in range(len(self.features))]
             return logits, {"encoder_features": enc, "fused_features": fused}

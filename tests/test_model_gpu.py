@@ -323,3 +323,26 @@ def test_fused_head_loss_matches_unfused(dev, tag, dtype):
             assert abs(lu - lf) <= 1e-5 * max(1.0, abs(lu)), (name, lu, lf)
             for a, b in zip(gf, gu):
                 assert ((a - b).norm() / b.norm()).item() < tol, (name, dtype)
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_deferred_encoder_norm_bitwise(dev, dtype, monkeypatch):
+    """DualEncoder mean fusion: the encoders' output InstanceNorm + ReLU applied on load by the maxpool and the
+    fusion kernel (never written) gives bit-identical logits, gradients and return_features to the
+    materialised path (MMSEG_DEFER_ENC_NORM=0)."""
+    g = golden("dual_tiny_cross_attention")
+    res = []
+    for defer in ("1", "0"):
+        monkeypatch.setenv("MMSEG_DEFER_ENC_NORM", defer)
+        cfg, m, g, M, C = _build("dual_tiny_cross_attention", dtype)
+        xs, ys = _inputs(g, M, C)
+        crit = get_loss(cfg)
+        out = m(xs[0].to(dev))
+        crit(out, ys[0].to(dev)).backward()
+        _, feats = m(xs[0].to(dev), return_features=True)
+        assert m.backbone.__dict__["_engine"].program.encs[0][0].defer_out == (defer == "1")
+        res.append((out.detach().clone(), torch.cat([p.grad.reshape(-1) for p in m.parameters()]).clone(),
+                    [f.clone() for lvl in feats["encoder_features"] for f in lvl]))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+    assert all(torch.equal(a, b) for a, b in zip(res[0][2], res[1][2]))
