@@ -1807,6 +1807,47 @@ __global__ void gemm_splitk_reduce(GemmArgs g) {
   }
 }
 
+// Vectorised split-K reduce with the splits dealt over S slices of the block (256 / S float4 columns per
+// block, ~4 splits per thread), slice sums a fixed pairwise LDS tree: at the small levels one thread per column
+// walking 8..16 splits left the reduce latency-bound.  Same summation tree for every run (deterministic).
+template <typename T, int S>
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_s(GemmArgs g) {
+  constexpr int NC = 256 / S;
+  __shared__ float4 red[S][NC];
+  const long long total = (long long)g.M * g.Ncols;
+  const int col4 = threadIdx.x % NC, sl = threadIdx.x / NC;
+  const long long idx4 = ((long long)blockIdx.x * NC + col4) * 4;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (idx4 < total) {
+    const float4* p = reinterpret_cast<const float4*>(g.part + idx4);
+    const long long st = total / 4;
+#pragma unroll 4
+    for (int k = sl; k < g.ksplit; k += S) {
+      const float4 a = p[(long long)k * st];
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+  }
+  red[sl][col4] = v;
+  __syncthreads();
+#pragma unroll
+  for (int h = S / 2; h > 0; h >>= 1) {
+    if (sl < h) {
+      const float4 a = red[sl + h][col4];
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+      red[sl][col4] = v;
+    }
+    __syncthreads();
+  }
+  if (sl != 0 || idx4 >= total) return;
+  const long long row = idx4 / g.Ncols;
+  const int col = (int)(idx4 - row * g.Ncols);
+  if (g.bias) {
+    v.x += g.bias[col]; v.y += g.bias[col + 1]; v.z += g.bias[col + 2]; v.w += g.bias[col + 3];
+  }
+  T* O = reinterpret_cast<T*>(g.out) + row * g.ldo + col;
+  O[0] = from_f<T>(v.x); O[1] = from_f<T>(v.y); O[2] = from_f<T>(v.z); O[3] = from_f<T>(v.w);
+}
+
 // ------------------------------------------------------------------ wgrad
 // part[ks][row][col] = sum_{v in split ks} A[v][row] * Bgather[v][col]
 //   CONV3 : A = dy (rows = Cout), B = x at v + off(tap), col = tap*Cin + ci
@@ -2759,14 +2800,20 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(WReduceArgs g) {
     }
   }
   if (S > 1) {
+    // slice sums: a fixed pairwise tree (S = 16..64 made the former serial sweep of one thread per column the
+    // kernel's critical path)
     red[sl][col4] = v;
     __syncthreads();
-    if (sl != 0) return;
 #pragma unroll
-    for (int k = 1; k < S; ++k) {
-      const float4 a = red[k][col4];
-      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    for (int h = S / 2; h > 0; h >>= 1) {
+      if (sl < h) {
+        const float4 a = red[sl + h][col4];
+        v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+        red[sl][col4] = v;
+      }
+      __syncthreads();
     }
+    if (sl != 0) return;
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -3026,6 +3073,26 @@ __global__ void pack_weight_batched_kernel(const PackDesc* __restrict__ descs, i
 
 // ------------------------------------------------------------ host launch
 template <typename T, int MODE>
+int launch_splitk_reduce(const GemmArgs& g, hipStream_t s) {
+  const long long total = (long long)g.M * g.Ncols;
+  const bool vec = MODE != MODE_CONVT_FWD && (g.Ncols & 3) == 0 && (g.ldo & 3) == 0 &&
+                   (reinterpret_cast<uintptr_t>(g.part) & 15) == 0;
+  int S = 1;
+  const int rpt = knob("MMSEG_SPLITK_RPT", 4);
+  while (S < 16 && g.ksplit / (2 * S) >= rpt) S *= 2;
+  if (vec && S > 1) {
+    const int nb = ceil_div(total / 4, 256 / S);
+    if (S == 16) hipLaunchKernelGGL((gemm_splitk_reduce_s<T, 16>), dim3(nb), dim3(256), 0, s, g);
+    else if (S == 8) hipLaunchKernelGGL((gemm_splitk_reduce_s<T, 8>), dim3(nb), dim3(256), 0, s, g);
+    else if (S == 4) hipLaunchKernelGGL((gemm_splitk_reduce_s<T, 4>), dim3(nb), dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((gemm_splitk_reduce_s<T, 2>), dim3(nb), dim3(256), 0, s, g);
+  } else {
+    hipLaunchKernelGGL((gemm_splitk_reduce<T, MODE>), dim3(splitk_reduce_blocks<MODE>(g)), dim3(256), 0, s, g);
+  }
+  return mmseg::check_launch("gemm_splitk_reduce");
+}
+
+template <typename T, int MODE>
 int launch_gemm(GemmArgs g, hipStream_t s) {
   const int Cbig = g.Ncols >= 64;
   dim3 block(256);
@@ -3057,11 +3124,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
       hipLaunchKernelGGL((conv3_brickr_kernel<T, 32>), grid, block, 0, s, g, plan.bz, plan.by, plan.bx);
     }
     if (mmseg::check_launch("conv3_brickr")) return 1;
-    if (g.ksplit > 1) {
-      const long long total = (long long)g.M * g.Ncols;
-      hipLaunchKernelGGL((gemm_splitk_reduce<T, MODE>), dim3(splitk_reduce_blocks<MODE>(g)), dim3(256), 0, s, g);
-      return mmseg::check_launch("gemm_splitk_reduce");
-    }
+    if (g.ksplit > 1) return launch_splitk_reduce<T, MODE>(g, s);
     return 0;
   }
   if (plan.kind == 1 && g.ksplit == 1) {
@@ -3185,11 +3248,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, 2, 2, 4, 2>), grid, block, 0, s, g);
   }
   if (mmseg::check_launch("conv_gemm")) return 1;
-  if (g.ksplit > 1) {
-    long long total = (long long)g.M * g.Ncols;
-    hipLaunchKernelGGL((gemm_splitk_reduce<T, MODE>), dim3(splitk_reduce_blocks<MODE>(g)), dim3(256), 0, s, g);
-    if (mmseg::check_launch("gemm_splitk_reduce")) return 1;
-  }
+  if (g.ksplit > 1) return launch_splitk_reduce<T, MODE>(g, s);
   return 0;
 }
 
@@ -3372,16 +3431,19 @@ int launch_wgrad_reduce(WReduceArgs g, void* stream) {
   const int ksplit = g.ksplit;
   const long long total = (long long)g.Ca * g.Ncols + (g.bias_part ? g.Ca : 0);
   hipStream_t s = (hipStream_t)stream;
-  // slices: ~8+ loads per thread when the splits allow, 1 slice for a handful of splits.  (Choosing S for
-  // >= 2048 blocks instead measured far slower: the S-slice LDS epilogue is serial in one thread per column.)
-  if (ksplit >= 512)
-    hipLaunchKernelGGL(wgrad_reduce_kernel<64>, dim3(ceil_div(total, 16)), dim3(256), 0, s, g);
-  else if (ksplit >= 64)
-    hipLaunchKernelGGL(wgrad_reduce_kernel<8>, dim3(ceil_div(total, 128)), dim3(256), 0, s, g);
-  else if (ksplit >= 8)
-    hipLaunchKernelGGL(wgrad_reduce_kernel<2>, dim3(ceil_div(total, 512)), dim3(256), 0, s, g);
-  else
-    hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(ceil_div(total, 1024)), dim3(256), 0, s, g);
+  // slices S: about MMSEG_WGRAD_RPT (default 8) split loads per thread, the slice sums a pairwise LDS tree
+  const int rpt = knob("MMSEG_WGRAD_RPT", 8);
+  int S = 1;
+  while (S < 64 && ksplit / (2 * S) >= rpt) S *= 2;
+  switch (S) {
+    case 64: hipLaunchKernelGGL(wgrad_reduce_kernel<64>, dim3(ceil_div(total, 16)), dim3(256), 0, s, g); break;
+    case 32: hipLaunchKernelGGL(wgrad_reduce_kernel<32>, dim3(ceil_div(total, 32)), dim3(256), 0, s, g); break;
+    case 16: hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(ceil_div(total, 64)), dim3(256), 0, s, g); break;
+    case 8: hipLaunchKernelGGL(wgrad_reduce_kernel<8>, dim3(ceil_div(total, 128)), dim3(256), 0, s, g); break;
+    case 4: hipLaunchKernelGGL(wgrad_reduce_kernel<4>, dim3(ceil_div(total, 256)), dim3(256), 0, s, g); break;
+    case 2: hipLaunchKernelGGL(wgrad_reduce_kernel<2>, dim3(ceil_div(total, 512)), dim3(256), 0, s, g); break;
+    default: hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(ceil_div(total, 1024)), dim3(256), 0, s, g); break;
+  }
   return mmseg::check_launch("wgrad_reduce");
 }
 
