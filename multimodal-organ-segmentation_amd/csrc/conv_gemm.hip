@@ -25,6 +25,10 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
 namespace {
 
 // Tuning knobs for in-process A/B runs (tools/kbench.py); defaults are the shipped choice.
@@ -519,7 +523,7 @@ struct Brick2Layout {
 
 __device__ __forceinline__ int w2_swz(int col) { return ((col >> 3) & 1) << 1; }
 
-template <typename T, int BN, int ZW>
+template <typename T, int BN, int ZW, bool PF = false>
 __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kernel(GemmArgs g) {
   using L = Brick2Layout<T>;
   constexpr int BZ = 4 * ZW, HZ = BZ + 2;
@@ -643,19 +647,43 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kern
       load_w(cn, kzn);
       if (kzn == 0) load_x(cn);
     }
+    if constexpr (PF) {
+      // fragments of tap t+1 are read while tap t's MFMAs run (one wave per SIMD cannot hide the LDS latency
+      // behind another wave's MFMAs)
+      V8<T> af[2][RM], bf[2][RN];
+      auto rd = [&](int t9, int b) {
+        const int ky = t9 / 3, kx = t9 - ky * 3;
+        const int hoff = kz * L::RZ + ky * L::RY + kx * L::QV;
 #pragma unroll
-    for (int t9 = 0; t9 < 9; ++t9) {
-      const int ky = t9 / 3, kx = t9 - ky * 3;
-      const int hoff = kz * L::RZ + ky * L::RY + kx * L::QV;
-      V8<T> af[RM], bf[RN];
+        for (int j = 0; j < RN; ++j) bf[b][j].load(Wl + (t9 * BN * L::QV + bq[j]) * EPQ);
 #pragma unroll
-      for (int j = 0; j < RN; ++j) bf[j].load(Wl + (t9 * BN * L::QV + bq[j]) * EPQ);
+        for (int i = 0; i < RM; ++i) af[b][i].load(Xl + (aq[i] + hoff) * EPQ);
+      };
+      rd(0, 0);
 #pragma unroll
-      for (int i = 0; i < RM; ++i) af[i].load(Xl + (aq[i] + hoff) * EPQ);
+      for (int t9 = 0; t9 < 9; ++t9) {
+        if (t9 < 8) rd(t9 + 1, (t9 + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < RM; ++i)
+        for (int i = 0; i < RM; ++i)
 #pragma unroll
-        for (int j = 0; j < RN; ++j) mfma_step<T>(acc[i][j], af[i], bf[j]);
+          for (int j = 0; j < RN; ++j) mfma_step<T>(acc[i][j], af[t9 & 1][i], bf[t9 & 1][j]);
+      }
+    } else {
+#pragma unroll
+      for (int t9 = 0; t9 < 9; ++t9) {
+        const int ky = t9 / 3, kx = t9 - ky * 3;
+        const int hoff = kz * L::RZ + ky * L::RY + kx * L::QV;
+        V8<T> af[RM], bf[RN];
+#pragma unroll
+        for (int j = 0; j < RN; ++j) bf[j].load(Wl + (t9 * BN * L::QV + bq[j]) * EPQ);
+#pragma unroll
+        for (int i = 0; i < RM; ++i) af[i].load(Xl + (aq[i] + hoff) * EPQ);
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j) mfma_step<T>(acc[i][j], af[i], bf[j]);
+      }
     }
     __syncthreads();
     if (more) {
@@ -1470,10 +1498,24 @@ __host__ __device__ constexpr int br_xq(int tsize) { return tsize == 2 ? 2560 : 
 // CB* > 0: the brick is known at compile time (6x6x6 at the 12^3 / 6^3 levels), so the halo / epilogue index
 // arithmetic divides by constants (mul-shift) instead of runtime integer divisions, which at one 32-channel
 // chunk per block were most of the kernel's VALU work (8.6 VALU instructions per MFMA, rocprofv3 r02).
-template <typename T, int BN, int CBZ = 0, int CBY = 0, int CBX = 0>
+template <typename T, int BN, int CBZ = 0, int CBY = 0, int CBX = 0, int DBG = 0, bool PF = false>
 __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kernel(GemmArgs g, int bz_rt, int by_rt,
-                                                                                   int bx_rt) {
+                                                                                   int bx_rt, long long* dbg = nullptr) {
   const int bz = CBZ > 0 ? CBZ : bz_rt, by = CBY > 0 ? CBY : by_rt, bx = CBX > 0 ? CBX : bx_rt;
+  // DBG 4: every block's (realtime, memtime) at start / end, block 0 wave 0's per-phase memtime stamps
+  int dn = 0;
+  auto stamp = [&]() {
+    if constexpr (DBG == 4) {
+      if (blockIdx.x == 0 && threadIdx.x == 0 && dn < 64) dbg[4 * 4096 + dn++] = (long long)__builtin_amdgcn_s_memtime();
+    }
+  };
+  if constexpr (DBG == 4) {
+    if (threadIdx.x == 0) {
+      dbg[4 * blockIdx.x + 0] = (long long)__builtin_amdgcn_s_memrealtime();
+      dbg[4 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memtime();
+    }
+  }
+  stamp();
   using L = Brick2Layout<T>;
   constexpr int RM = 4, RN = BN / 16;
   constexpr int XQ = br_xq(sizeof(T));
@@ -1601,15 +1643,39 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kern
     store_w();
   }
   __syncthreads();
+  stamp();
   for (int st = st_begin; st < st_end; ++st) {
     const int kz = st % 3;
     const int sn = st + 1;
     const bool more = sn < st_end;
     const int cn = sn / 3, kzn = sn - cn * 3;
-    if (more) {
+    if (more && DBG != 1) {
       load_w(cn, kzn);
       if (kzn == 0) load_x(cn);
     }
+    if constexpr (PF) {
+      // fragments of tap t+1 are read while tap t's MFMAs run: at one block per CU (one wave per SIMD) nothing
+      // else hides the LDS latency (s_memtime: ~4,200 cycles per 9-tap stage against 2,304 of MFMA)
+      V8<T> af[2][RM], bf[2][RN];
+      auto rd = [&](int t9, int b) {
+        const int ky = t9 / 3, kx = t9 - ky * 3;
+        const int hoff = kz * RZ + ky * RY + kx * L::QV;
+#pragma unroll
+        for (int j = 0; j < RN; ++j) bf[b][j].load(Wl + (t9 * BN * L::QV + bq[j]) * EPQ);
+#pragma unroll
+        for (int i = 0; i < RM; ++i) af[b][i].load(Xl + (aq[i] + hoff) * EPQ);
+      };
+      rd(0, 0);
+#pragma unroll
+      for (int t9 = 0; t9 < 9; ++t9) {
+        if (t9 < 8) rd(t9 + 1, (t9 + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j) mfma_step<T>(acc[i][j], af[t9 & 1][i], bf[t9 & 1][j]);
+      }
+    } else
 #pragma unroll
     for (int t9 = 0; t9 < 9; ++t9) {
       const int ky = t9 / 3, kx = t9 - ky * 3;
@@ -1619,17 +1685,27 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kern
       for (int j = 0; j < RN; ++j) bf[j].load(Wl + (t9 * BN * L::QV + bq[j]) * EPQ);
 #pragma unroll
       for (int i = 0; i < RM; ++i) af[i].load(Xl + (aq[i] + hoff) * EPQ);
+      if (DBG == 2) {
 #pragma unroll
-      for (int i = 0; i < RM; ++i)
+        for (int i = 0; i < RM; ++i)
 #pragma unroll
-        for (int j = 0; j < RN; ++j) mfma_step<T>(acc[i][j], af[i], bf[j]);
+          for (int j = 0; j < RN; ++j) acc[i][j][0] += (float)af[i].get(0) * (float)bf[j].get(1);
+      } else {
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j) mfma_step<T>(acc[i][j], af[i], bf[j]);
+      }
     }
+    stamp();
     __syncthreads();
-    if (more) {
+    stamp();
+    if (more && DBG != 3) {
       store_w();
       if (kzn == 0) store_x();
       __syncthreads();
     }
+    stamp();
   }
 
   // epilogue through LDS: rows < bz*by*bx only
@@ -1689,6 +1765,14 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kern
       }
     }
   }
+  if constexpr (DBG == 4) {
+    stamp();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      dbg[4 * blockIdx.x + 2] = (long long)__builtin_amdgcn_s_memrealtime();
+      dbg[4 * blockIdx.x + 3] = (long long)__builtin_amdgcn_s_memtime();
+    }
+  }
 }
 
 // Host-side choice of the CONV3 kernel (shared by the launcher and mmseg_conv3_splits).
@@ -1722,7 +1806,10 @@ Conv3Plan plan_conv3(int M, int Ncols, int cin, int D, int H, int W, int lda, in
           const int hq = (bz + 2) * (by + 2) * ((bx + 2) * 2 * tsize + 2);
           if (rows > 256 || halo > BR_MAXHV || hq > br_xq(tsize)) continue;
           const int score = rows * 4 + (bx % 8 == 0 ? 2 : 0) + (by % 8 == 0 ? 1 : 0);
-          if (score > best) {
+          // ties go to the smaller halo (12^3: 6x6x6, 512 halo voxels and the compile-time kernel, over 3x6x12)
+          const bool tie_better = score == best && knob("MMSEG_BRICKR_CUBE", 1) &&
+                                  halo < (p.bz + 2) * (p.by + 2) * (p.bx + 2);
+          if (score > best || tie_better) {
             best = score;
             p.bz = bz; p.by = by; p.bx = bx;
           }
@@ -2740,8 +2827,12 @@ WBrick plan_wgrad_brickr(int D, int H, int W) {
       for (int bx = 1; bx <= W && bx <= 16; ++bx) {
         if (W % bx) continue;
         const int rows = bz * by * bx;
-        if (rows > 128 || (bz + 2) * (by + 2) * (bx + 2) > WR_MAXHV) continue;
-        if (rows > brows) {
+        const int halo = (bz + 2) * (by + 2) * (bx + 2);
+        if (rows > 128 || halo > WR_MAXHV) continue;
+        // ties go to the smaller halo (12^3: 3x6x6, the compile-time kernel, over 3x3x12)
+        const bool tie_better = rows == brows && knob("MMSEG_BRICKR_CUBE", 1) &&
+                                halo < (best.bz + 2) * (best.by + 2) * (best.bx + 2);
+        if (rows > brows || tie_better) {
           brows = rows;
           best = {bz, by, bx};
         }
@@ -3111,8 +3202,55 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     if (plan.bn == 64) {
       if constexpr (sizeof(T) == 2) {
         mmseg::note_kernel("conv3_brickr_kernel<BN64>");
-        if (b666)
+        const int dbg = knob("MMSEG_BRICKR_DBG", 0);   // timing probes (diagnostics only, wrong results)
+        if (b666 && dbg == 1)
+          hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6, 1>), grid, block, 0, s, g, 6, 6, 6);
+        else if (b666 && dbg == 2)
+          hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6, 2>), grid, block, 0, s, g, 6, 6, 6);
+        else if (b666 && dbg == 3)
+          hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6, 3>), grid, block, 0, s, g, 6, 6, 6);
+        else if (dbg == 4) {
+          static long long* dp = nullptr;
+          const int nlong = 4 * 4096 + 64;
+          if (!dp) hipMalloc(&dp, nlong * sizeof(long long));
+          hipMemsetAsync(dp, 0, nlong * sizeof(long long), s);
+          const bool pf = knob("MMSEG_BRICKR_PF", 0);
+          if (b666 && pf)
+            hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6, 4, true>), grid, block, 0, s, g, 6, 6, 6, dp);
+          else if (b666)
+            hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6, 4>), grid, block, 0, s, g, 6, 6, 6, dp);
+          else if (pf)
+            hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 0, 0, 0, 4, true>), grid, block, 0, s, g, plan.bz, plan.by,
+                               plan.bx, dp);
+          else
+            hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 0, 0, 0, 4>), grid, block, 0, s, g, plan.bz, plan.by,
+                               plan.bx, dp);
+          std::vector<long long> h(nlong);
+          hipStreamSynchronize(s);
+          hipMemcpy(h.data(), dp, nlong * sizeof(long long), hipMemcpyDeviceToHost);
+          const int nbk = std::min((int)grid.x, 4096);
+          long long t0 = h[0], t1 = h[2], sumdur = 0;
+          for (int b = 0; b < nbk; ++b) {
+            t0 = std::min(t0, h[4 * b]);
+            t1 = std::max(t1, h[4 * b + 2]);
+            sumdur += h[4 * b + 2] - h[4 * b];
+          }
+          long long lastst = 0;
+          for (int b = 0; b < nbk; ++b) lastst = std::max(lastst, h[4 * b] - t0);
+          fprintf(stderr, "brickr dbg grid %d brick %dx%dx%d ks %d: span %.2f us, mean block %.2f us, last start %.2f us, "
+                  "block0 %.0f cycles / %.2f us:", (int)grid.x, plan.bz, plan.by, plan.bx, g.ksplit, (t1 - t0) * 0.01,
+                  sumdur * 0.01 / nbk, lastst * 0.01, (double)(h[3] - h[1]), (h[2] - h[0]) * 0.01);
+          const long long* q = h.data() + 4 * 4096;
+          for (int i = 1; i < 64 && q[i]; ++i) fprintf(stderr, " %lld", q[i] - q[i - 1]);
+          fprintf(stderr, "\n");
+        }
+        else if (b666 && knob("MMSEG_BRICKR_PF", 0))
+          hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6, 0, true>), grid, block, 0, s, g, 6, 6, 6);
+        else if (b666)
           hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6>), grid, block, 0, s, g, 6, 6, 6);
+        else if (knob("MMSEG_BRICKR_PF", 0))
+          hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 0, 0, 0, 0, true>), grid, block, 0, s, g, plan.bz, plan.by,
+                             plan.bx);
         else
           hipLaunchKernelGGL((conv3_brickr_kernel<T, 64>), grid, block, 0, s, g, plan.bz, plan.by, plan.bx);
       }
@@ -3208,7 +3346,10 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
         hipLaunchKernelGGL((conv3_brick3_kernel<T, 32, false>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
     } else if (g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
       mmseg::note_kernel("conv3_brick2_kernel<BN64,ZW1>");
-      hipLaunchKernelGGL((conv3_brick2_kernel<T, 64, 1>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
+      if (knob("MMSEG_TAP_PF", 1))   // 2 % on the 48^3 64-channel layers (r02)
+        hipLaunchKernelGGL((conv3_brick2_kernel<T, 64, 1, true>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
+      else
+        hipLaunchKernelGGL((conv3_brick2_kernel<T, 64, 1>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
     } else if (sizeof(T) == 2 && g.D % 8 == 0 && knob("MMSEG_BRICK2_ZW", 1) == 2) {
       if constexpr (sizeof(T) == 2) {
         mmseg::note_kernel("conv3_brick2_kernel<BN32,ZW2>");

@@ -149,7 +149,13 @@ def test_two_gloo_ranks_on_one_gpu_equal_one_rank_full_batch(dev):
         assert abs((res[0]["losses"][s] + res[1]["losses"][s]) / 2 - single["losses"][s]) < (1e-5 if s == 0
                                                                                                else 1e-4)
     assert np.array_equal(res[0]["weights"], res[1]["weights"])
-    assert _l2rel(res[0]["weights"], single["weights"]) < 1e-4
+    # the weights inherit step 1's gradient differences through AdamW, whose early updates are ~lr * sign(g)
+    # wherever |g| is near eps: a rounding-level gradient difference there moves a weight by up to ~lr, so the
+    # bound is lr-scaled per element and loose in L2 (< 1e-4 measured, then 3.6e-4 after the weight-gradient
+    # reduce changed its fixed summation order)
+    lr = 1e-3
+    assert np.abs(res[0]["weights"] - single["weights"]).max() <= 2 * lr * STEPS
+    assert _l2rel(res[0]["weights"], single["weights"]) < 1e-3
     # validation: the one batch lives on rank 0; both ranks report the same result, which is the
     # single-rank one up to the trained weights' rounding differences
     assert res[0]["vloss"] == res[1]["vloss"] and res[0]["dice"] == res[1]["dice"]

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--model", default="dual_encoder")
     ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--layers", action="store_true", help="also print every timed launch of the last step")
     args = ap.parse_args()
     import mmseg_amd  # noqa: F401
     from bench import make_config
@@ -70,6 +71,11 @@ def main():
                 step += 1
                 TIMER.stop()
                 fams[c] = {k: round(v["ms"], 3) for k, v in sorted(TIMER.summary().items(), key=lambda kv: -kv[1]["ms"])}
+                if args.layers:
+                    for i, (name, fl, nb, s0, s1) in enumerate(TIMER.records):
+                        us = s0.elapsed_time(s1) * 1e3
+                        print(f"layer {i:3d} {name:45s} {fl / 1e9:8.2f} GF {nb / 1e6:8.1f} MB {us:8.1f} us "
+                              f"{fl / us / 1e6 if us else 0:7.1f} TF/s")
     for c in combos:
         print(json.dumps({"variant": dict(c), "median_ms": round(statistics.median(res[c]), 3),
                           "min_ms": round(min(res[c]), 3), "families": fams[c]}))
