@@ -12,6 +12,8 @@
 // Weights are read straight from the fp32 master copy (no packed image).
 #include "mmseg_common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int SZ = 4, SY = 8, SX = 8;                 // output brick (256 voxels)
@@ -47,40 +49,47 @@ struct StemArgs {
   int ksplit;
 };
 
-template <typename T>
+// Halo of a brick in LDS, compact: [600 halo voxels][CR channels] (the padded 8-channel input layout would
+// put 16 B between the 2-B values one lane gathers, a 4-way bank conflict on every gather, r02 PMC).
+template <typename T, int CR>
 __device__ __forceinline__ void stem_stage_halo(const StemArgs& g, T* Hl, long long nbase, int z0, int y0, int x0) {
   const T* X = reinterpret_cast<const T*>(g.x);
   const long long HW = (long long)g.H * g.W;
   for (int h = threadIdx.x; h < SHV; h += blockDim.x) {
     const int hx = h % SHX, hy = (h / SHX) % SHY, hz = h / (SHX * SHY);
     const int z = z0 - 1 + hz, y = y0 - 1 + hy, x = x0 - 1 + hx;
-    V8<T> v;
-    if ((unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W) {
-      const T* src = X + (nbase + z * HW + (long long)y * g.W + x) * g.ldx;
-      if (g.ldx == SCR) {
-        v.load(src);
-      } else {   // compact input (ldx = cr): only the real channels cross HBM
-        v.zero();
-        for (int c = 0; c < g.cr; ++c) v.set(c, (float)src[c]);
-      }
-    } else {
-      v.zero();
-    }
-    v.store(Hl + h * SCR);
+    const bool in = (unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
+    const T* src = X + (nbase + z * HW + (long long)y * g.W + x) * g.ldx;
+#pragma unroll
+    for (int c = 0; c < CR; ++c) Hl[h * CR + c] = in ? src[c] : (T)0.f;
   }
 }
 
+// im2col column k of the stem (k = tap * CR + channel, 27 CR real columns padded to KP): its offset in the
+// compact halo relative to the row's tap-0 voxel, -1 for padding.  Built once per block into LDS.
+template <int CR>
+__device__ __forceinline__ int stem_koff(int k) {
+  const int t = k / CR, c = k - t * CR;
+  return k < 27 * CR ? stem_hv(0, t) * CR + c : -1;
+}
+
 // ---------------------------------------------------------------- forward
-// block = one 4x8x8 brick x all Co (<= 64) columns; wave w owns brick z-slice w
-// (4 row tiles of 16 voxels)
-template <typename T, int RN>
+// block = one 4x8x8 brick x all CO (16 / 32) columns; wave w owns brick z-slice w (4 row tiles of 16 voxels).
+// CR and CO are compile-time: the runtime divisions by cr / KP in the column bookkeeping were most of the
+// kernel's VALU instructions (1,056 per wave for 8 MFMAs, r02 PMC).
+template <typename T, int RN, int CR>
 __global__ __launch_bounds__(256) void stem_fwd_kernel(StemArgs g) {
-  // dynamic LDS: halo [600][8] | weights [Co][KP+8]; the epilogue tile [256][Co+8] reuses it after the MFMAs
-  extern __shared__ __attribute__((aligned(16))) unsigned char stem_lds[];
-  T* Hl = reinterpret_cast<T*>(stem_lds);
-  T* Wl = Hl + SHV * SCR;
-  T* El = Hl;
-  const int WP = g.KP + 8;
+  constexpr int K = 27 * CR, KP = ((K + 31) / 32) * 32, WP = KP + 8, CO = RN * 16, EP = CO + 8;
+  constexpr int HB = ((SHV * CR * (int)sizeof(T) + 15) / 16) * 16;
+  constexpr int WB = CO * WP * (int)sizeof(T);
+  constexpr int KB = KP * 4;
+  constexpr int EB = 256 * EP * (int)sizeof(T);
+  constexpr int LB = (HB + WB + KB) > EB ? (HB + WB + KB) : EB;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[LB];
+  T* Hl = reinterpret_cast<T*>(lds);
+  T* Wl = reinterpret_cast<T*>(lds + HB);
+  int* Kl = reinterpret_cast<int*>(lds + HB + WB);
+  T* El = reinterpret_cast<T*>(lds);   // epilogue tile, after the MFMAs
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bz_n = g.D / SZ, by_n = g.H / SY, bx_n = g.W / SX;
   int b = blockIdx.x;
@@ -91,17 +100,13 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(StemArgs g) {
   const long long HW = (long long)g.H * g.W;
   const long long nbase = (long long)n * g.D * HW;
   const int z0 = bz * SZ, y0 = by * SY, x0 = bx * SX;
-  const int K = 27 * g.cr;
-  stem_stage_halo<T>(g, Hl, nbase, z0, y0, x0);
-  for (int e = tid; e < g.Co * g.KP; e += 256) {
-    const int co = e / g.KP, k = e - co * g.KP;
-    float v = 0.f;
-    if (k < K) {
-      const int t = k / g.cr, c = k - t * g.cr;
-      v = g.w[((long long)co * g.cr + c) * 27 + t];
-    }
-    Wl[co * WP + k] = from_f<T>(v);
+  stem_stage_halo<T, CR>(g, Hl, nbase, z0, y0, x0);
+  for (int e = tid; e < CO * KP; e += 256) {
+    const int co = e / KP, k = e - co * KP;
+    const int t = k / CR, c = k - t * CR;
+    Wl[co * WP + k] = from_f<T>(k < K ? g.w[(co * CR + c) * 27 + t] : 0.f);
   }
+  if (tid < KP) Kl[tid] = stem_koff<CR>(tid);
   __syncthreads();
   const int r16 = lane & 15, kg = lane >> 4;
   f32x4 acc[4][RN];
@@ -109,23 +114,19 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(StemArgs g) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  int rbase[4];   // halo index (tap 0) of the lane's row in each row tile
+  int rbase[4];   // compact-halo offset (tap 0) of the lane's row in each row tile
 #pragma unroll
-  for (int i = 0; i < 4; ++i) rbase[i] = stem_hv(wave * 64 + i * 16 + r16, 0);
-  for (int kb = 0; kb < g.KP; kb += 32) {
-    // this lane's 8 im2col columns: LDS element offset (tap shift * 8 + channel), -1 = padding
+  for (int i = 0; i < 4; ++i) rbase[i] = stem_hv(wave * 64 + i * 16 + r16, 0) * CR;
+#pragma unroll
+  for (int kb = 0; kb < KP; kb += 32) {
     int koff[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = kb + kg * 8 + j;
-      const int t = k / g.cr, c = k - t * g.cr;
-      koff[j] = k < K ? stem_hv(0, t) * SCR + c : -1;
-    }
+    for (int j = 0; j < 8; ++j) koff[j] = Kl[kb + kg * 8 + j];
     V8<T> af[4], bf[RN];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) af[i].set(j, koff[j] >= 0 ? (float)Hl[rbase[i] * SCR + koff[j]] : 0.f);
+      for (int j = 0; j < 8; ++j) af[i].v[j] = koff[j] >= 0 ? Hl[rbase[i] + koff[j]] : (T)0.f;
 #pragma unroll
     for (int j = 0; j < RN; ++j) bf[j].load(Wl + (j * 16 + r16) * WP + kb + kg * 8);
 #pragma unroll
@@ -133,7 +134,6 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(StemArgs g) {
 #pragma unroll
       for (int j = 0; j < RN; ++j) stem_mfma<T>(acc[i][j], af[i], bf[j]);
   }
-  constexpr int EP = RN * 16 + 8;
   __syncthreads();   // El aliases the halo / weights
 #pragma unroll
   for (int j = 0; j < RN; ++j) {
@@ -147,7 +147,9 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(StemArgs g) {
   __syncthreads();
   T* Y = reinterpret_cast<T*>(g.y);
   constexpr int CG = RN * 2;
-  for (int e = tid; e < 256 * CG; e += 256) {
+#pragma unroll
+  for (int q = 0; q < CG; ++q) {
+    const int e = tid + q * 256;
     const int v = e / CG, cg = e % CG;
     const int z = z0 + (v >> 6), y = y0 + ((v >> 3) & 7), x = x0 + (v & 7);
     V8<T> o;
@@ -158,51 +160,54 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(StemArgs g) {
 
 // ------------------------------------------------------------ weight grad
 // block = a contiguous range of bricks; wave w accumulates the brick's voxel
-// steps w, w+4 (2 x 32 voxels) into the full [Co][KP] tile; the 4 wave tiles
+// steps w, w+4 (2 x 32 voxels) into the full [CO][KP] tile; the 4 wave tiles
 // are added in order at the end (deterministic).
-template <typename T, int RM, int RNK>
+template <typename T, int RM, int RNK, int CR>
 __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemArgs g) {
-  constexpr int DP = RM * 16 + 8;
-  constexpr int HB = SHV * SCR * sizeof(T), DB = 256 * DP * sizeof(T);
-  constexpr int RB = 4 * RM * 16 * (RNK * 16 + 1) * 4;
-  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[(HB + DB) > RB ? (HB + DB) : RB];
+  constexpr int K = 27 * CR, KP = RNK * 16, CO = RM * 16, CGd = CO / 8;
+  static_assert(KP == ((K + 31) / 32) * 32, "KP = 27 CR padded to 32");
+  constexpr int DP = CO + 8;
+  constexpr int HB = ((SHV * CR * (int)sizeof(T) + 15) / 16) * 16, DB = 256 * DP * (int)sizeof(T);
+  constexpr int RB = 4 * CO * (KP + 1) * 4;
+  constexpr int LB = (HB + DB + KP * 4) > RB ? (HB + DB + KP * 4) : RB;
+  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[LB];
   T* Hl = reinterpret_cast<T*>(lds_raw);
   T* Dl = reinterpret_cast<T*>(lds_raw + HB);
-  float (*red)[RM * 16][RNK * 16 + 1] = reinterpret_cast<float (*)[RM * 16][RNK * 16 + 1]>(lds_raw);
+  int* Kl = reinterpret_cast<int*>(lds_raw + HB + DB);
+  float (*red)[CO][KP + 1] = reinterpret_cast<float (*)[CO][KP + 1]>(lds_raw);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bz_n = g.D / SZ, by_n = g.H / SY, bx_n = g.W / SX;
-  const long long nbrick = (long long)g.N * bz_n * by_n * bx_n;
-  const long long bpk = (nbrick + g.ksplit - 1) / g.ksplit;
-  const long long b0 = blockIdx.x * bpk;
-  const long long b1 = b0 + bpk < nbrick ? b0 + bpk : nbrick;
+  const int nbrick = g.N * bz_n * by_n * bx_n;
+  const int bpk = (nbrick + g.ksplit - 1) / g.ksplit;
+  const int b0 = blockIdx.x * bpk;
+  const int b1 = b0 + bpk < nbrick ? b0 + bpk : nbrick;
   const long long HW = (long long)g.H * g.W;
-  const int K = 27 * g.cr;
   const T* Dy = reinterpret_cast<const T*>(g.dy);
   const int r16 = lane & 15, kg = lane >> 4;
+  if (tid < KP) Kl[tid] = stem_koff<CR>(tid);
   f32x4 acc[RM][RNK];
 #pragma unroll
   for (int i = 0; i < RM; ++i)
 #pragma unroll
     for (int j = 0; j < RNK; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float bsum = 0.f;   // bias partial of channel tid % Co over voxel slice tid / Co
-  int bko[RNK];       // this lane's im2col column per k tile: LDS offset (tap shift * 8 + channel), -1 = padding
-#pragma unroll
-  for (int jt = 0; jt < RNK; ++jt) {
-    const int k = jt * 16 + r16;
-    const int t = k / g.cr, c = k - t * g.cr;
-    bko[jt] = k < K ? stem_hv(0, t) * SCR + c : -1;
-  }
-  for (long long b = b0; b < b1; ++b) {
-    long long q = b;
-    const int bx = (int)(q % bx_n); q /= bx_n;
-    const int by = (int)(q % by_n); q /= by_n;
-    const int bz = (int)(q % bz_n);
-    const long long nbase = (q / bz_n) * g.D * HW;
+  float bsum = 0.f;   // bias partial of channel tid % CO over voxel slice tid / CO
+  int bko[RNK];       // this lane's im2col column per k tile (compact-halo offset), -1 = padding
+  for (int b = b0; b < b1; ++b) {
+    int q = b;
+    const int bx = q % bx_n; q /= bx_n;
+    const int by = q % by_n; q /= by_n;
+    const int bz = q % bz_n;
+    const long long nbase = (long long)(q / bz_n) * g.D * HW;
     const int z0 = bz * SZ, y0 = by * SY, x0 = bx * SX;
-    __syncthreads();   // previous brick fully consumed
-    stem_stage_halo<T>(g, Hl, nbase, z0, y0, x0);
-    const int CGd = g.Co / 8;
-    for (int e = tid; e < 256 * CGd; e += 256) {
+    __syncthreads();   // previous brick fully consumed (and, first time round, Kl written)
+    if (b == b0) {
+#pragma unroll
+      for (int jt = 0; jt < RNK; ++jt) bko[jt] = Kl[jt * 16 + r16];
+    }
+    stem_stage_halo<T, CR>(g, Hl, nbase, z0, y0, x0);
+#pragma unroll
+    for (int qq = 0; qq < CGd; ++qq) {
+      const int e = tid + qq * 256;
       const int v = e / CGd, cg = e % CGd;
       const int z = z0 + (v >> 6), y = y0 + ((v >> 3) & 7), x = x0 + (v & 7);
       V8<T> d;
@@ -210,9 +215,9 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemArgs g) {
       d.store(Dl + v * DP + cg * 8);
     }
     __syncthreads();
-    if (g.bias_part) {   // thread = (channel tid % Co, voxel slice tid / Co)
-      const int c = tid % g.Co, nsl = 256 / g.Co;
-      for (int v = tid / g.Co; v < 256; v += nsl) bsum += (float)Dl[v * DP + c];
+    if (g.bias_part) {   // thread = (channel tid % CO, voxel slice tid / CO)
+      const int c = tid % CO;
+      for (int v = tid / CO; v < 256; v += 256 / CO) bsum += (float)Dl[v * DP + c];
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -222,14 +227,13 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemArgs g) {
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) af[i].set(j, (float)Dl[(vb + kg * 8 + j) * DP + i * 16 + r16]);
+        for (int j = 0; j < 8; ++j) af[i].v[j] = Dl[(vb + kg * 8 + j) * DP + i * 16 + r16];
       // B = im2col: column k = jt*16 + r16, k-dim = the same 8 voxels (one x-row: halo j + const)
-      const int hb = stem_hv(vb + kg * 8, 0) * SCR;
+      const int hb = stem_hv(vb + kg * 8, 0) * CR;
 #pragma unroll
       for (int jt = 0; jt < RNK; ++jt) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          bf[jt].set(j, bko[jt] >= 0 ? (float)Hl[hb + j * SCR + bko[jt]] : 0.f);
+        for (int j = 0; j < 8; ++j) bf[jt].v[j] = bko[jt] >= 0 ? Hl[hb + j * CR + bko[jt]] : (T)0.f;
       }
 #pragma unroll
       for (int i = 0; i < RM; ++i)
@@ -237,7 +241,7 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemArgs g) {
         for (int jt = 0; jt < RNK; ++jt) stem_mfma<T>(acc[i][jt], af[i], bf[jt]);
     }
   }
-  // fixed-order combine of the 4 wave tiles -> part[ks][Co][KP] (red aliases the stage buffers)
+  // fixed-order combine of the 4 wave tiles -> part[ks][CO][KP] (red aliases the stage buffers)
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < RM; ++i)
@@ -246,20 +250,20 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemArgs g) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) red[wave][i * 16 + kg * 4 + r][jt * 16 + r16] = acc[i][jt][r];
   __syncthreads();
-  for (int e = tid; e < g.Co * g.KP; e += 256) {
-    const int co = e / g.KP, k = e - co * g.KP;
+  for (int e = tid; e < CO * KP; e += 256) {
+    const int co = e / KP, k = e - co * KP;
     const float v = ((red[0][co][k] + red[1][co][k]) + red[2][co][k]) + red[3][co][k];
-    g.part[((long long)blockIdx.x * g.Co + co) * g.KP + k] = v;
+    g.part[((long long)blockIdx.x * CO + co) * KP + k] = v;
   }
   if (g.bias_part) {
     __syncthreads();
     float* rb = reinterpret_cast<float*>(lds_raw);
     rb[tid] = bsum;
     __syncthreads();
-    if (tid < g.Co) {
+    if (tid < CO) {
       float a = 0.f;
-      for (int sl = 0; sl < 256 / g.Co; ++sl) a += rb[sl * g.Co + tid];
-      g.bias_part[(long long)blockIdx.x * g.Co + tid] = a;
+      for (int sl = 0; sl < 256 / CO; ++sl) a += rb[sl * CO + tid];
+      g.bias_part[(long long)blockIdx.x * CO + tid] = a;
     }
   }
 }
@@ -283,15 +287,22 @@ int mmseg_stem_fwd(const void* x, int ldx, int cr, const float* w, const float* 
   const dim3 grid(N * (D / SZ) * (H / SY) * (W / SX));
   hipStream_t s = (hipStream_t)stream;
   mmseg::note_kernel("stem_fwd_kernel");
-  const size_t ts = dtype == MMSEG_BF16 ? 2 : 4;
-  const size_t stage = (size_t)(SHV * SCR + Co * (stem_kp(cr) + 8)) * ts, epi = (size_t)256 * (Co + 8) * ts;
-  const size_t shm = stage > epi ? stage : epi;
+  auto run = [&](auto tag, auto rn) {
+    using T = decltype(tag);
+    constexpr int RN = decltype(rn)::value;
+    switch (cr) {
+      case 1: hipLaunchKernelGGL((stem_fwd_kernel<T, RN, 1>), grid, dim3(256), 0, s, g); break;
+      case 2: hipLaunchKernelGGL((stem_fwd_kernel<T, RN, 2>), grid, dim3(256), 0, s, g); break;
+      case 3: hipLaunchKernelGGL((stem_fwd_kernel<T, RN, 3>), grid, dim3(256), 0, s, g); break;
+      default: hipLaunchKernelGGL((stem_fwd_kernel<T, RN, 4>), grid, dim3(256), 0, s, g); break;
+    }
+  };
   if (dtype == MMSEG_BF16) {
-    if (Co == 16) hipLaunchKernelGGL((stem_fwd_kernel<bf16_t, 1>), grid, dim3(256), shm, s, g);
-    else hipLaunchKernelGGL((stem_fwd_kernel<bf16_t, 2>), grid, dim3(256), shm, s, g);
+    if (Co == 16) run(bf16_t{}, std::integral_constant<int, 1>{});
+    else run(bf16_t{}, std::integral_constant<int, 2>{});
   } else {
-    if (Co == 16) hipLaunchKernelGGL((stem_fwd_kernel<float, 1>), grid, dim3(256), shm, s, g);
-    else hipLaunchKernelGGL((stem_fwd_kernel<float, 2>), grid, dim3(256), shm, s, g);
+    if (Co == 16) run(float{}, std::integral_constant<int, 1>{});
+    else run(float{}, std::integral_constant<int, 2>{});
   }
   return mmseg::check_launch("stem_fwd");
 }
@@ -316,20 +327,23 @@ int mmseg_stem_wgrad(const void* dy, int lddy, const void* x, int ldx, int cr, f
   hipStream_t s = (hipStream_t)stream;
   mmseg::note_kernel("stem_wgrad_kernel");
   const dim3 grid(ksplit), blk(256);
-  const int rnk = stem_kp(cr) / 16;   // 2, 4, 6, 8
-#define STEM_WG(TT, RM_)                                                                   \
-  switch (rnk) {                                                                           \
-    case 2: hipLaunchKernelGGL((stem_wgrad_kernel<TT, RM_, 2>), grid, blk, 0, s, g); break; \
-    case 4: hipLaunchKernelGGL((stem_wgrad_kernel<TT, RM_, 4>), grid, blk, 0, s, g); break; \
-    case 6: hipLaunchKernelGGL((stem_wgrad_kernel<TT, RM_, 6>), grid, blk, 0, s, g); break; \
-    default: hipLaunchKernelGGL((stem_wgrad_kernel<TT, RM_, 8>), grid, blk, 0, s, g); break; \
-  }
+  auto run = [&](auto tag, auto rm) {
+    using T = decltype(tag);
+    constexpr int RM = decltype(rm)::value;
+    switch (cr) {
+      case 1: hipLaunchKernelGGL((stem_wgrad_kernel<T, RM, 2, 1>), grid, blk, 0, s, g); break;
+      case 2: hipLaunchKernelGGL((stem_wgrad_kernel<T, RM, 4, 2>), grid, blk, 0, s, g); break;
+      case 3: hipLaunchKernelGGL((stem_wgrad_kernel<T, RM, 6, 3>), grid, blk, 0, s, g); break;
+      default: hipLaunchKernelGGL((stem_wgrad_kernel<T, RM, 8, 4>), grid, blk, 0, s, g); break;
+    }
+  };
   if (dtype == MMSEG_BF16) {
-    if (Co == 16) { STEM_WG(bf16_t, 1) } else { STEM_WG(bf16_t, 2) }
+    if (Co == 16) run(bf16_t{}, std::integral_constant<int, 1>{});
+    else run(bf16_t{}, std::integral_constant<int, 2>{});
   } else {
-    if (Co == 16) { STEM_WG(float, 1) } else { STEM_WG(float, 2) }
+    if (Co == 16) run(float{}, std::integral_constant<int, 1>{});
+    else run(float{}, std::integral_constant<int, 2>{});
   }
-#undef STEM_WG
   return mmseg::check_launch("stem_wgrad");
 }
 
