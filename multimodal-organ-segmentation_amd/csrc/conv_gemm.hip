@@ -3576,7 +3576,12 @@ int launch_wgrad_reduce(WReduceArgs g, void* stream) {
   const int rpt = knob("MMSEG_WGRAD_RPT", 8);
   int S = 1;
   while (S < 64 && ksplit / (2 * S) >= rpt) S *= 2;
+  // small gradients over many splits (the stem: 1,056 values x 1,024 splits): more slices until the grid
+  // fills the chip, down to 2 loads per thread (S = 64 left it at 66 blocks, 12.8 us for 4 MB)
+  while (S < 256 && (total * S + 1023) / 1024 < knob("MMSEG_WGRAD_RBLK", 512) && ksplit / (2 * S) >= 2) S *= 2;
   switch (S) {
+    case 256: hipLaunchKernelGGL(wgrad_reduce_kernel<256>, dim3(ceil_div(total, 4)), dim3(256), 0, s, g); break;
+    case 128: hipLaunchKernelGGL(wgrad_reduce_kernel<128>, dim3(ceil_div(total, 8)), dim3(256), 0, s, g); break;
     case 64: hipLaunchKernelGGL(wgrad_reduce_kernel<64>, dim3(ceil_div(total, 16)), dim3(256), 0, s, g); break;
     case 32: hipLaunchKernelGGL(wgrad_reduce_kernel<32>, dim3(ceil_div(total, 32)), dim3(256), 0, s, g); break;
     case 16: hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(ceil_div(total, 64)), dim3(256), 0, s, g); break;

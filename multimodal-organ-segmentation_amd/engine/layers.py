@@ -227,7 +227,9 @@ class Conv3:
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
         V = x.N * x.V
         if dx is None and self._stem(x, dy.ld):
-            ks = L.mmseg_stem_wgrad_splits(x.N, x.D, x.H, x.W, 2048)
+            # 1,024 splits: one round of resident blocks at 96^3 B=2 and half the partials of 2,048 (r02 stembench:
+            # 42 + 12.8 us against 44 + 19.7 us with the reduce)
+            ks = L.mmseg_stem_wgrad_splits(x.N, x.D, x.H, x.W, int(os.environ.get("MMSEG_STEM_SPLITS", "1024")))
             kp = L.mmseg_stem_kp(self.Ci)
             part = self.rt.ws(ks * self.Co * kp + ks * self.Co)
             bpart = part.data_ptr() + ks * self.Co * kp * 4
