@@ -136,6 +136,9 @@ int mmseg_conv3_wgrad(const void* dy, int lddy, const void* x, int ldx, float* g
 /* Bias gradient out[c] (+)= sum_v dy[v][c] (convolution_backward grad_bias). */
 int mmseg_colsum(const void* dy, int ld, int C, long long V, float* part, int nblk, float* out, int accumulate,
                  int dtype, void* stream);
+/* out[c] (+)= sum_{b < nblk} part[b][c] in fixed order: the transposed conv's bias gradient from the column-sum
+ * partials mmseg_wgrad(MODE_CONVT_DGRAD, bias_part = [ksplit][8 Cout]) emits, with nblk = 8 ksplit. */
+int mmseg_colsum_reduce(const float* part, int nblk, int C, float* out, int accumulate, void* stream);
 
 /* ---------------------------------------- InstanceNorm3d + ReLU, MaxPool */
 long long mmseg_instnorm_ws_floats(int N, long long V, int C);

@@ -127,22 +127,20 @@ __device__ __forceinline__ RowInfo make_row(long long m, const GemmArgs& g) {
   r.base = m;
   r.tmask = 0;
   if (r.m < 0) return r;
+  // 32-bit index arithmetic: M < 2^31 (the host checks M * lda), and 64-bit divisions cost ~100 VALU each
   if (MODE == MODE_CONV3) {
-    int x = (int)(m % g.W);
-    long long t = m / g.W;
-    int y = (int)(t % g.H);
-    t /= g.H;
-    int z = (int)(t % g.D);
-    r.tmask = tap_valid_mask(z, y, x, g.D, g.H, g.W);
+    const unsigned mu = (unsigned)m;
+    const unsigned t = mu / (unsigned)g.W, x = mu - t * (unsigned)g.W;
+    const unsigned t2 = t / (unsigned)g.H, y = t - t2 * (unsigned)g.H;
+    const unsigned z = t2 % (unsigned)g.D;
+    r.tmask = tap_valid_mask((int)z, (int)y, (int)x, g.D, g.H, g.W);
   } else if (MODE == MODE_CONVT_DGRAD) {
-    int x = (int)(m % g.W);
-    long long t = m / g.W;
-    int y = (int)(t % g.H);
-    t /= g.H;
-    int z = (int)(t % g.D);
-    long long n = t / g.D;
-    long long H2 = 2LL * g.H, W2 = 2LL * g.W, D2 = 2LL * g.D;
-    r.base = ((n * D2 + 2 * z) * H2 + 2 * y) * W2 + 2 * x;
+    const unsigned mu = (unsigned)m;
+    const unsigned t = mu / (unsigned)g.W, x = mu - t * (unsigned)g.W;
+    const unsigned t2 = t / (unsigned)g.H, y = t - t2 * (unsigned)g.H;
+    const unsigned n = t2 / (unsigned)g.D, z = t2 - n * (unsigned)g.D;
+    const long long H2 = 2LL * g.H, W2 = 2LL * g.W, D2 = 2LL * g.D;
+    r.base = (((long long)n * D2 + 2 * z) * H2 + 2 * y) * W2 + 2 * x;
   }
   return r;
 }
@@ -186,6 +184,16 @@ template <typename T>
 __device__ __forceinline__ void load_b(V8<T>& v, int kgi, int col, const GemmArgs& g) {
   const T* B = reinterpret_cast<const T*>(g.b);
   v.load(B + ((long long)kgi * g.Cpad + col) * 8);
+}
+
+// Child voxel (2x grid) of input voxel `row` for transposed-conv tap t (32-bit divisions, see make_row).
+__device__ __forceinline__ long long convt_child(long long row, int t, const GemmArgs& g) {
+  const unsigned mu = (unsigned)row;
+  const unsigned q = mu / (unsigned)g.W, x = mu - q * (unsigned)g.W;
+  const unsigned q2 = q / (unsigned)g.H, y = q - q2 * (unsigned)g.H;
+  const unsigned n = q2 / (unsigned)g.D, z = q2 - n * (unsigned)g.D;
+  return (((long long)n * 2 * g.D + 2 * z + (t >> 2)) * 2LL * g.H + 2 * y + ((t >> 1) & 1)) * 2LL * g.W + 2 * x +
+         (t & 1);
 }
 
 // Block = WM x WN waves; wave tile = (RM*16) x (RN*16).
@@ -295,15 +303,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs g) {
       if (row >= g.M || col >= g.Ncols) continue;
       if (MODE == MODE_CONVT_FWD) {
         const int t = col / Cout, co = col - t * Cout;
-        const int x = (int)(row % g.W);
-        long long q = row / g.W;
-        const int y = (int)(q % g.H);
-        q /= g.H;
-        const int z = (int)(q % g.D);
-        const long long n = q / g.D;
-        const long long child = ((n * 2LL * g.D + 2 * z + (t >> 2)) * 2LL * g.H + 2 * y + ((t >> 1) & 1)) *
-                                    2LL * g.W + 2 * x + (t & 1);
-        O[child * g.ldo + co] = El[lr * EPT + lc];
+        O[convt_child(row, t, g) * g.ldo + co] = El[lr * EPT + lc];
       } else {
         O[row * g.ldo + col] = El[lr * EPT + lc];
       }
@@ -319,15 +319,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs g) {
     o.load(El + lr * EPT + cg * 8);
     if (MODE == MODE_CONVT_FWD) {
       const int t = col / Cout, co = col - t * Cout;
-      const int x = (int)(row % g.W);
-      long long q = row / g.W;
-      const int y = (int)(q % g.H);
-      q /= g.H;
-      const int z = (int)(q % g.D);
-      const long long n = q / g.D;
-      const long long child = ((n * 2LL * g.D + 2 * z + (t >> 2)) * 2LL * g.H + 2 * y + ((t >> 1) & 1)) * 2LL * g.W +
-                              2 * x + (t & 1);
-      o.store(O + child * g.ldo + co);
+      o.store(O + convt_child(row, t, g) * g.ldo + co);
     } else {
       o.store(O + row * g.ldo + col);
     }
@@ -1879,15 +1871,7 @@ __global__ void gemm_splitk_reduce(GemmArgs g) {
     const int Cout = g.Ncols >> 3;
     const int t = col / Cout, co = col - t * Cout;
     if (g.bias) v += g.bias[co];
-    const int x = (int)(row % g.W);
-    long long q = row / g.W;
-    const int y = (int)(q % g.H);
-    q /= g.H;
-    const int z = (int)(q % g.D);
-    const long long n = q / g.D;
-    const long long child = ((n * 2LL * g.D + 2 * z + (t >> 2)) * 2LL * g.H + 2 * y + ((t >> 1) & 1)) * 2LL * g.W +
-                            2 * x + (t & 1);
-    O[child * g.ldo + co] = from_f<T>(v);
+    O[convt_child(row, t, g) * g.ldo + co] = from_f<T>(v);
   } else {
     if (g.bias) v += g.bias[col];
     O[row * g.ldo + col] = from_f<T>(v);
@@ -1944,8 +1928,10 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_s(GemmArgs g) {
 // with 16-byte vector writes (double-buffered, one barrier per stage); the
 // MFMA fragments (K = voxels) are read with the gfx950 transposed LDS read
 // ds_read_b64_tr_b16 (bf16) or as single f32 elements (f32 path).
-// bias_part (optional, A = dy): blocks of column tile 0 also emit per-row
-// sums of A, i.e. the bias gradient partials.
+// bias_part (optional): the bias gradient partials.  A = dy (CONV3 / POINT): blocks of column tile 0 emit
+// per-row sums of A, bias_part[ks][Ca].  CONVT: blocks of row tile 0 emit per-column sums of the gathered dy
+// tile B, bias_part[ks][8 Cout] (col = tap*Cout + co), which mmseg_colsum_reduce folds over (ks, tap): the
+// separate colsum pass over dy (113 MB at the 96^3 upconv) is not needed.
 struct WgradArgs {
   const void* a;  int lda;
   const void* b;  int ldb;
@@ -1988,11 +1974,10 @@ __device__ __forceinline__ bool gather_src(long long vox, int kgi, int cpg_shift
   if (MODE == MODE_CONV3) {
     const int t = kgi >> cpg_shift;
     c8 = kgi & ((1 << cpg_shift) - 1);
-    const int x = (int)(vox % g.W);
-    long long q = vox / g.W;
-    const int y = (int)(q % g.H);
-    q /= g.H;
-    const int z = (int)(q % g.D);
+    // 32-bit divisions (V < 2^31, checked by the host)
+    const unsigned vu = (unsigned)vox;
+    const unsigned q = vu / (unsigned)g.W, q2 = q / (unsigned)g.H;
+    const int x = (int)(vu - q * (unsigned)g.W), y = (int)(q - q2 * (unsigned)g.H), z = (int)(q2 % (unsigned)g.D);
     int dz, dy, dx;
     tap_delta(t, dz, dy, dx);
     src = vox + ((long long)dz * g.H + dy) * g.W + dx;
@@ -2001,13 +1986,11 @@ __device__ __forceinline__ bool gather_src(long long vox, int kgi, int cpg_shift
   } else if (MODE == MODE_CONVT_DGRAD) {
     const int t = kgi >> cpg_shift;
     c8 = kgi & ((1 << cpg_shift) - 1);
-    const int x = (int)(vox % g.W);
-    long long q = vox / g.W;
-    const int y = (int)(q % g.H);
-    q /= g.H;
-    const int z = (int)(q % g.D);
-    const long long n = q / g.D;
-    src = ((n * 2LL * g.D + 2 * z + (t >> 2)) * 2LL * g.H + 2 * y + ((t >> 1) & 1)) * 2LL * g.W + 2 * x + (t & 1);
+    const unsigned vu = (unsigned)vox;
+    const unsigned q = vu / (unsigned)g.W, q2 = q / (unsigned)g.H, n = q2 / (unsigned)g.D;
+    const unsigned x = vu - q * (unsigned)g.W, y = q - q2 * (unsigned)g.H, z = q2 - n * (unsigned)g.D;
+    src = (((long long)n * 2LL * g.D + 2 * z + (t >> 2)) * 2LL * g.H + 2 * y + ((t >> 1) & 1)) * 2LL * g.W + 2 * x +
+          (t & 1);
     return true;
   }
   c8 = kgi;
@@ -2041,7 +2024,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs g) {
   if (v_end > g.V) v_end = g.V;
   const T* A = reinterpret_cast<const T*>(g.a);
   const T* B = reinterpret_cast<const T*>(g.b);
-  const bool do_bias = g.bias_part != nullptr && ctile == 0;
+  constexpr bool BCOL = MODE == MODE_CONVT_DGRAD;   // bias = column sums of B (see above)
+  const bool do_bias = g.bias_part != nullptr && (BCOL ? rtile == 0 : ctile == 0);
 
   // fixed per-thread column group (256 % BG == 0) -> fixed tap / channel group
   const int cga = tid % AG, cgb = tid % BG;
@@ -2083,7 +2067,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs g) {
     for (int k = 0; k < A_PER; ++k) {
       const int v = (tid + k * 256) / AG;
       ra[k].store(As + v * PA + cga * 8);
-      if (do_bias) {
+      if (!BCOL && do_bias) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) bsum[j] += ra[k].get(j);
       }
@@ -2092,6 +2076,10 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs g) {
     for (int k = 0; k < B_PER; ++k) {
       const int v = (tid + k * 256) / BG;
       rb[k].store(Bs + v * PB + cgb * 8);
+      if (BCOL && do_bias) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bsum[j] += rb[k].get(j);
+      }
     }
   };
 
@@ -2160,12 +2148,20 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs g) {
       }
     }
   if (do_bias) {
-    // fixed-order reduction of the per-thread row sums (threads with equal tid % AG share rows)
+    // fixed-order reduction of the per-thread row (column) sums: threads with equal tid % AG (tid % BG) share
+    // rows (columns)
     float* red = reinterpret_cast<float*>(lds);
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[tid * 8 + j] = bsum[j];
     __syncthreads();
-    if (tid < BM) {
+    if (BCOL) {
+      if (tid < BN) {
+        const int cg = tid >> 3, j = tid & 7;
+        float sacc = 0.f;
+        for (int t = cg; t < 256; t += BG) sacc += red[t * 8 + j];
+        if (col0 + tid < g.Ncols) g.bias_part[(long long)ks * g.Ncols + col0 + tid] = sacc;
+      }
+    } else if (tid < BM) {
       const int cg = tid >> 3, j = tid & 7;
       float sacc = 0.f;
       for (int t = cg; t < 256; t += AG) sacc += red[t * 8 + j];
@@ -2968,16 +2964,24 @@ __global__ void colsum_partial_kernel(const T* __restrict__ dy, int ld, int C, l
   }
 }
 
-// one wave per channel: lanes stride over the block partials, fixed shuffle tree
-__global__ void colsum_reduce_kernel(const float* __restrict__ part, int nblk, int C, float* __restrict__ out,
-                                     int accumulate) {
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (c >= C) return;
+// one 256-thread block per channel: threads stride over the block partials (4 loads in flight), a fixed
+// shuffle tree per wave, then the 4 waves in order (one wave per channel walked ~30 dependent loads per lane
+// for the transposed conv's 8 x ksplit column-sum partials)
+__global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restrict__ part, int nblk, int C,
+                                                            float* __restrict__ out, int accumulate) {
+  const int c = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float v = 0.f;
-  for (int b = lane; b < nblk; b += 64) v += part[(long long)b * C + c];
+#pragma unroll 4
+  for (int b = threadIdx.x; b < nblk; b += 256) v += part[(long long)b * C + c];
   v = wave_sum(v);
-  if (lane == 0) out[c] = accumulate ? out[c] + v : v;
+  __shared__ float wred[4];
+  if (lane == 0) wred[wave] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float t = ((wred[0] + wred[1]) + wred[2]) + wred[3];
+    out[c] = accumulate ? out[c] + t : t;
+  }
 }
 
 // ------------------------------------------------------------ weight pack
@@ -3373,6 +3377,32 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     }
     return mmseg::check_launch("conv3_brick");
   }
+  if (MODE == MODE_CONVT_FWD && g.Ncols % 256 == 0 && knob("MMSEG_CONVT_FWD_WIDE", 1)) {
+    // BM=64, BN=256: a block writes all 8 taps x 32 (or a quarter of 8 x 128 ...) output channels of its 64 input
+    // voxels, so each input row is read by one block instead of by Ncols / 64 column tiles
+    mmseg::note_kernel("conv_gemm_kernel<convT_fwd,64x256>");
+    dim3 grid(ceil_div(g.M, 64) * (g.Ncols / 256) * g.ksplit);
+    hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, 1, 4, 4, 4>), grid, block, 0, s, g);
+    if (mmseg::check_launch("conv_gemm")) return 1;
+    if (g.ksplit > 1) return launch_splitk_reduce<T, MODE>(g, s);
+    return 0;
+  }
+  if (MODE == MODE_CONVT_DGRAD && g.Ncols % 64 == 0 && knob("MMSEG_CONVT_DGRAD_TILE", 0) == 1) {
+    mmseg::note_kernel("conv_gemm_kernel<convT_dgrad,64x64>");
+    dim3 grid(ceil_div(g.M, 64) * (g.Ncols / 64) * g.ksplit);
+    hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, 2, 2, 2, 2>), grid, block, 0, s, g);
+    if (mmseg::check_launch("conv_gemm")) return 1;
+    if (g.ksplit > 1) return launch_splitk_reduce<T, MODE>(g, s);
+    return 0;
+  }
+  if (MODE == MODE_CONVT_DGRAD && g.Ncols % 128 == 0 && knob("MMSEG_CONVT_DGRAD_TILE", 0) == 2) {
+    mmseg::note_kernel("conv_gemm_kernel<convT_dgrad,64x128>");
+    dim3 grid(ceil_div(g.M, 64) * (g.Ncols / 128) * g.ksplit);
+    hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, 1, 4, 4, 2>), grid, block, 0, s, g);
+    if (mmseg::check_launch("conv_gemm")) return 1;
+    if (g.ksplit > 1) return launch_splitk_reduce<T, MODE>(g, s);
+    return 0;
+  }
   if (!Cbig) {
     // BM=128, BN=32
     static const char* nm[4] = {"conv_gemm_kernel<conv3,128x32>", "conv_gemm_kernel<point,128x32>",
@@ -3732,6 +3762,7 @@ int mmseg_wgrad(const void* a, int lda, const void* b, int ldb, float* part, flo
                 int Ncols, int cpg_shift, long long V, int D, int H, int W, int ksplit, int dtype, void* stream) {
   MMSEG_REQUIRE(Ca % 8 == 0, "wgrad: rows (%d) must be a multiple of 8", Ca);
   MMSEG_REQUIRE(Ncols % 8 == 0, "wgrad: cols (%d) must be a multiple of 8", Ncols);
+  MMSEG_REQUIRE(V < (1LL << 31), "wgrad: voxel count %lld must fit 31 bits", V);
   // legacy entry (tap-major partials + mmseg_wgrad_reduce): brick kinds 2/3 write channel-major tiles and
   // are reached through mmseg_conv3_wgrad only
   int brick = mode == MODE_CONV3 ? wgrad_brick_ok(Ca, cpg_shift, D, H, W, lda, ldb, dtype) : 0;
@@ -3827,7 +3858,16 @@ int mmseg_colsum(const void* dy, int ld, int C, long long V, float* part, int nb
     hipLaunchKernelGGL(colsum_partial_kernel<float>, dim3(nblk), dim3(256), 0, s, (const float*)dy, ld, C, V, vps,
                        part);
   if (mmseg::check_launch("colsum_partial")) return 1;
-  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(ceil_div(C, 4)), dim3(256), 0, s, part, nblk, C, out, accumulate);
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(C), dim3(256), 0, s, part, nblk, C, out, accumulate);
+  return mmseg::check_launch("colsum_reduce");
+}
+
+// out[c] (=, or += with accumulate) = sum over b < nblk of part[b][c], fixed order; the transposed conv's bias
+// gradient from mmseg_wgrad's CONVT column-sum partials is mmseg_colsum_reduce(bias_part, 8 * ksplit, Cout, ...).
+int mmseg_colsum_reduce(const float* part, int nblk, int C, float* out, int accumulate, void* stream) {
+  MMSEG_REQUIRE(nblk >= 1 && C >= 1, "colsum_reduce: nblk, C >= 1");
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part, nblk, C, out,
+                     accumulate);
   return mmseg::check_launch("colsum_reduce");
 }
 

@@ -319,14 +319,20 @@ class ConvT2:
         V = x.N * x.V
         ncols = 8 * self.Cop
         ks = L.mmseg_wgrad_splits(V, _wgrad_ksplit(self.Ci, ncols, V))
-        part = self.rt.ws(max(ks * self.Ci * ncols, 256 * self.Co))
+        # bias gradient: column sums of the gathered dy tile emitted by the weight-gradient kernel itself
+        # ([ks][8 Cop] after the weight partials, folded over (split, tap)), so dy is read once
+        fused_bias = self.up.bias is not None and self.Cop == self.Co
+        part = self.rt.ws(max(ks * self.Ci * ncols + (ks * ncols if fused_bias else 0), 256 * self.Co))
+        bpart = part.data_ptr() + ks * self.Ci * ncols * 4 if fused_bias else None
         with TIMER.region(_gemm_name(self.rt, 0, "convT"), flops=2.0 * V * self.Ci * 8 * self.Co,
                           nbytes=_io_bytes(self.rt, V, self.Ci, 8 * self.Co, 8 * self.Ci * self.Co, 4)):
-            L.mmseg_wgrad(x.ptr, x.ld, dy.ptr, dy.ld, ptr(part), None, MODE_CONVT_DGRAD, self.Ci, ncols, self.dshift,
-                          V, x.D, x.H, x.W, ks, code, s)
+            L.mmseg_wgrad(x.ptr, x.ld, dy.ptr, dy.ld, ptr(part), bpart, MODE_CONVT_DGRAD, self.Ci, ncols,
+                          self.dshift, V, x.D, x.H, x.W, ks, code, s)
         L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.up.weight)), None, None, self.Ci, ncols, ks, self.Cop,
                              self.Co, 8, int(accumulate), s)
-        if self.up.bias is not None:
+        if fused_bias:
+            L.mmseg_colsum_reduce(bpart, 8 * ks, self.Co, ptr(self.flat.grad(self.up.bias)), int(accumulate), s)
+        elif self.up.bias is not None:
             L.mmseg_colsum(dy.ptr, dy.ld, self.Co, dy.N * dy.V, ptr(part), 256, ptr(self.flat.grad(self.up.bias)),
                            int(accumulate), code, s)
         self.flat.mark(*[p for p in (self.up.weight, self.up.bias) if p is not None])

@@ -142,8 +142,10 @@ def test_conv3_stem_padded_input(dev, dtype, cr, co, shape):
 
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("cin,cout,shape", [(64, 32, (2, 3, 4, 5)), (128, 64, (1, 4, 4, 4)), (16, 8, (2, 2, 3, 2)),
-                                            (512, 256, (2, 3, 3, 3))])
+                                            (512, 256, (2, 3, 3, 3)), (64, 32, (2, 16, 12, 12))])
 def test_convT_fwd_dgrad_wgrad(dev, dtype, cin, cout, shape):
+    """(the last shape runs the weight gradient over many voxel splits: the bias gradient then comes from the
+    per-split, per-tap column sums folded by mmseg_colsum_reduce)"""
     torch.manual_seed(cin)
     up = nn.ConvTranspose3d(cin, cout, 2, stride=2).to(dev)
     rt = Runtime(dev, dtype)
