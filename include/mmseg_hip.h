@@ -362,14 +362,19 @@ int mmseg_loss_bwd(const float* logits, const void* labels, int label_bytes, int
  * backward = dlogits + the head's data and weight gradient without writing dlogits (logits recomputed with
  * the forward's operation order).  ws: mmseg_loss_ws_floats(N, C, V) floats, same layout (the count of
  * out-of-range labels is its last float); wpart: mmseg_head_loss_wpart_floats() floats.
- * mmseg_head_loss_ok: 1 when (C, Cin, ldx, dtype) has a kernel (2 <= C <= 8, Cin 8, 16 or 32). */
+ * mmseg_head_loss_ok: 1 when (C, Cin, ldx, dtype) has a kernel (2 <= C <= 8, Cin 8, 16 or 32).
+ * nmean / nrstd (optional, [N][Cin]): x is the PRE-norm input of the last decoder block's InstanceNorm + ReLU,
+ * applied on load exactly as mmseg_instnorm_relu_fwd would (relu((x - mean) * rstd) rounded to the storage
+ * type), so that block's output is never written. */
 int mmseg_head_loss_ok(int C, int Cin, int ldx, int dtype);
 long long mmseg_head_loss_wpart_floats(int C, int Cin, int N, long long V);
-int mmseg_head_loss_fwd(const void* x, int ldx, int Cin, const float* W, const float* b, const float* dscale, int C,
+int mmseg_head_loss_fwd(const void* x, int ldx, int Cin, const float* nmean, const float* nrstd, const float* W,
+                        const float* b, const float* dscale, int C,
                         int N, long long V, const void* labels, int label_bytes, int type, float dice_w, float ce_w,
                         float smooth, float alpha, float beta, int include_bg, const float* class_w, float* loss_out,
                         float* ws, int dtype, void* stream);
-int mmseg_head_loss_bwd(const void* x, int ldx, int Cin, const float* W, const float* b, const float* dscale, int C,
+int mmseg_head_loss_bwd(const void* x, int ldx, int Cin, const float* nmean, const float* nrstd, const float* W,
+                        const float* b, const float* dscale, int C,
                         int N, long long V, const void* labels, int label_bytes, int type, float dice_w, float ce_w,
                         float smooth, float alpha, float beta, int include_bg, const float* class_w, const float* gout,
                         float gconst, const float* ws, void* dx, int lddx, float* gW, float* gb, float* wpart,

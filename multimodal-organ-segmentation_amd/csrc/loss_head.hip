@@ -646,11 +646,36 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(const float* __restrict__
 template <typename T, int G>
 struct HeadLoad {   // the lane's 8 channels 8g..8g+7 of one voxel (zero for groups g >= G or invalid voxels)
   V8<T> a;
+  bool in;
   __device__ __forceinline__ void load(const T* __restrict__ x, int ldx, long long row, bool ok, int g) {
-    if (ok && g < G) a.load(x + row * ldx + 8 * g);
+    in = ok && g < G;
+    if (in) a.load(x + row * ldx + 8 * g);
     else a.zero();
   }
+  // the deferred InstanceNorm + ReLU of the last decoder block: relu((x - mean) * rstd) rounded to T, the
+  // same operations as in_relu_apply, so the values equal the materialised output bit for bit
+  __device__ __forceinline__ void norm(const float* mu, const float* rs) {
+    if (!in) return;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float h = (a.get(j) - mu[j]) * rs[j];
+      a.set(j, h > 0.f ? h : 0.f);
+    }
+  }
 };
+
+// the lane's 8 channels' InstanceNorm statistics (sample n), or none
+template <int G>
+__device__ __forceinline__ bool head_norm_stats(const float* nmean, const float* nrstd, int n, int g, float* mu,
+                                                float* rs) {
+  constexpr int Cin = 8 * G;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    mu[j] = (nmean && g < G) ? nmean[n * Cin + 8 * g + j] : 0.f;
+    rs[j] = (nmean && g < G) ? nrstd[n * Cin + 8 * g + j] : 1.f;
+  }
+  return nmean != nullptr;
+}
 
 constexpr int HU = 4;   // 16-voxel tiles per wave step in the fused head + loss kernels
 
@@ -664,6 +689,8 @@ __device__ __forceinline__ f32x4 head_logits_t(const float* wA, const float* xs,
 
 template <typename T, int G, typename LT>
 __global__ __launch_bounds__(256) void head_loss_stats_kernel(const T* __restrict__ x, int ldx,
+                                                              const float* __restrict__ nmean,
+                                                              const float* __restrict__ nrstd,
                                                               const float* __restrict__ Wt,
                                                               const float* __restrict__ bias,
                                                               const float* __restrict__ dscale, int C,
@@ -673,6 +700,8 @@ __global__ __launch_bounds__(256) void head_loss_stats_kernel(const T* __restric
   __shared__ float red[4][52];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, v16 = lane & 15, g = lane >> 4;
   const int n = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
+  float nmu[8], nrs[8];
+  const bool donorm = head_norm_stats<G>(nmean, nrstd, n, g, nmu, nrs);
   float wA[8], sc[8], bz[4];
 #pragma unroll
   for (int kb = 0; kb < 8; ++kb) {
@@ -698,6 +727,10 @@ __global__ __launch_bounds__(256) void head_loss_stats_kernel(const T* __restric
     const long long v = vb + 16 * u + v16;
     lds_[u].load(x, ldx, base + v, v < v1, g);
     ys_[u] = v < v1 ? (int)labels[base + v] : 0;
+  }
+  if (donorm) {
+#pragma unroll
+    for (int u = 0; u < HU; ++u) lds_[u].norm(nmu, nrs);
   }
 #pragma unroll
   for (int u = 0; u < HU; ++u) {
@@ -797,6 +830,8 @@ __global__ __launch_bounds__(256) void head_loss_stats_kernel(const T* __restric
 // wpart: per block [C*Cin + C] weight / bias gradient partials (head_wgrad_reduce sums them over the blocks)
 template <typename T, int G, int NC, typename LT>
 __global__ __launch_bounds__(256) void head_loss_bwd_kernel(const T* __restrict__ x, int ldx,
+                                                            const float* __restrict__ nmean,
+                                                            const float* __restrict__ nrstd,
                                                             const float* __restrict__ Wt,
                                                             const float* __restrict__ bias,
                                                             const float* __restrict__ dscale, int C,
@@ -809,6 +844,8 @@ __global__ __launch_bounds__(256) void head_loss_bwd_kernel(const T* __restrict_
   __shared__ float red[4][NC * Cin + NC];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, v16 = lane & 15, g = lane >> 4;
   const int n = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
+  float nmu[8], nrs[8];
+  const bool donorm = head_norm_stats<G>(nmean, nrstd, n, g, nmu, nrs);
   float wA[8], sc[8], bz[4], ca[4], cb[4];
 #pragma unroll
   for (int kb = 0; kb < 8; ++kb) {
@@ -854,6 +891,10 @@ __global__ __launch_bounds__(256) void head_loss_bwd_kernel(const T* __restrict_
     const long long v = vb + 16 * u + v16;
     lds_[u].load(x, ldx, base + v, v < v1, g);
     ys_[u] = v < v1 ? (int)labels[base + v] : 0;
+  }
+  if (donorm) {
+#pragma unroll
+    for (int u = 0; u < HU; ++u) lds_[u].norm(nmu, nrs);
   }
 #pragma unroll
   for (int u = 0; u < HU; ++u) {
@@ -1242,7 +1283,8 @@ long long mmseg_head_loss_wpart_floats(int C, int Cin, int N, long long V) {
   return (long long)N * nch * (C * Cin + C);
 }
 
-int mmseg_head_loss_fwd(const void* x, int ldx, int Cin, const float* W, const float* b, const float* dscale, int C,
+int mmseg_head_loss_fwd(const void* x, int ldx, int Cin, const float* nmean, const float* nrstd, const float* W,
+                        const float* b, const float* dscale, int C,
                         int N, long long V, const void* labels, int label_bytes, int type, float dice_w, float ce_w,
                         float smooth, float alpha, float beta, int include_bg, const float* class_w, float* loss_out,
                         float* ws, int dtype, void* stream) {
@@ -1261,8 +1303,8 @@ int mmseg_head_loss_fwd(const void* x, int ldx, int Cin, const float* W, const f
     constexpr int G = decltype(g_c)::value, NC = decltype(nc_c)::value;
     (void)NC;                 // the statistics kernel does not depend on NC: one instance per (T, G, LT)
     mmseg::note_kernel("head_loss_stats_kernel");
-    hipLaunchKernelGGL((head_loss_stats_kernel<T, G, LT>), dim3(nch, N), dim3(256), 0, s, (const T*)x, ldx, W, b,
-                       dscale, C, (const LT*)labels, V, vpc, cfg, part);
+    hipLaunchKernelGGL((head_loss_stats_kernel<T, G, LT>), dim3(nch, N), dim3(256), 0, s, (const T*)x, ldx, nmean,
+                       nrstd, W, b, dscale, C, (const LT*)labels, V, vpc, cfg, part);
   });
   if (mmseg::check_launch("head_loss_stats")) return 1;
   const size_t shm = sizeof(double) * ((size_t)N * (3 * C + 3) + (size_t)N * C);
@@ -1273,13 +1315,16 @@ int mmseg_head_loss_fwd(const void* x, int ldx, int Cin, const float* W, const f
 
 // After mmseg_head_loss_fwd with the same ws.  dx may alias x (each voxel's features are read before its
 // gradient is written); dx null skips the data gradient.  gW [C][Cin] / gb [C] (=, or += with accumulate).
-int mmseg_head_loss_bwd(const void* x, int ldx, int Cin, const float* W, const float* b, const float* dscale, int C,
+int mmseg_head_loss_bwd(const void* x, int ldx, int Cin, const float* nmean, const float* nrstd, const float* W,
+                        const float* b, const float* dscale, int C,
                         int N, long long V, const void* labels, int label_bytes, int type, float dice_w, float ce_w,
                         float smooth, float alpha, float beta, int include_bg, const float* class_w, const float* gout,
                         float gconst, const float* ws, void* dx, int lddx, float* gW, float* gb, float* wpart,
                         int accumulate, int dtype, void* stream) {
   MMSEG_REQUIRE(mmseg_head_loss_ok(C, Cin, ldx, dtype) && (dx == nullptr || lddx % 8 == 0),
                 "head_loss_bwd: unsupported shape (C=%d, Cin=%d, ldx=%d, lddx=%d)", C, Cin, ldx, lddx);
+  MMSEG_REQUIRE(!nmean || dx != x, "head_loss_bwd: with the deferred norm x is the pre-norm input the "
+                "InstanceNorm backward still reads; dx must not alias it");
   LossCfg cfg{type, dice_w, ce_w, smooth, alpha, beta, include_bg, class_w};
   long long vpc;
   const int nch = loss_chunks(V, &vpc);
@@ -1290,8 +1335,9 @@ int mmseg_head_loss_bwd(const void* x, int ldx, int Cin, const float* W, const f
     using LT = decltype(lt);
     constexpr int G = decltype(g_c)::value, NC = decltype(nc_c)::value;
     mmseg::note_kernel("head_loss_bwd_kernel");
-    hipLaunchKernelGGL((head_loss_bwd_kernel<T, G, NC, LT>), dim3(nch, N), dim3(256), 0, s, (const T*)x, ldx, W, b,
-                       dscale, C, (const LT*)labels, V, vpc, cfg, coef, gout, gconst, (T*)dx, lddx, wpart);
+    hipLaunchKernelGGL((head_loss_bwd_kernel<T, G, NC, LT>), dim3(nch, N), dim3(256), 0, s, (const T*)x, ldx, nmean,
+                       nrstd, W, b, dscale, C, (const LT*)labels, V, vpc, cfg, coef, gout, gconst, (T*)dx, lddx,
+                       wpart);
   });
   if (mmseg::check_launch("head_loss_bwd")) return 1;
   hipLaunchKernelGGL(head_wgrad_reduce, dim3(ceil_div(C * Cin + C, 4)), dim3(256), 0, s, wpart, N * nch, C, Cin, gW,

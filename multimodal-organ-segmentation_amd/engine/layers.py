@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import os
 from dataclasses import dataclass
-from typing import Optional
+from typing import Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -504,26 +504,29 @@ class Head:
         return x.off == 0 and bool(self.rt.lib.mmseg_head_loss_ok(self.C, self.Cin, x.ld, self.rt.code))
 
     def fwd_loss(self, x: Act, labels: torch.Tensor, spec: dict, cw: Optional[torch.Tensor],
-                 dscale: Optional[torch.Tensor]) -> torch.Tensor:
-        """Head + loss statistics + finalize: the loss scalar, no logits written."""
+                 dscale: Optional[torch.Tensor], norm: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+                 ) -> torch.Tensor:
+        """Head + loss statistics + finalize: the loss scalar, no logits written.  norm = (mean, rstd): x is the
+        last decoder block's pre-norm x2 and its InstanceNorm + ReLU is applied on load (Block.defer_out)."""
         L = self.rt.lib
         ws = torch.empty(L.mmseg_loss_ws_floats(x.N, self.C, x.V), dtype=torch.float32, device=self.rt.device)
         loss = torch.empty((), dtype=torch.float32, device=self.rt.device)
         args = (spec["type"], spec["dice_w"], spec["ce_w"], spec["smooth"], spec["alpha"], spec["beta"],
                 int(spec["include_bg"]), ptr(cw))
-        L.mmseg_head_loss_fwd(x.ptr, x.ld, self.Cin, ptr(self.conv.weight), ptr(self.conv.bias), ptr(dscale), self.C,
-                              x.N, x.V, ptr(labels), labels.element_size(), *args, ptr(loss), ptr(ws), self.rt.code,
-                              self.rt.stream)
-        self.loss_state = (labels, args, ws, cw, dscale)
+        nm, nr = (ptr(norm[0]), ptr(norm[1])) if norm is not None else (None, None)
+        L.mmseg_head_loss_fwd(x.ptr, x.ld, self.Cin, nm, nr, ptr(self.conv.weight), ptr(self.conv.bias), ptr(dscale),
+                              self.C, x.N, x.V, ptr(labels), labels.element_size(), *args, ptr(loss), ptr(ws),
+                              self.rt.code, self.rt.stream)
+        self.loss_state = (labels, args, ws, cw, dscale, (nm, nr))
         return loss, ws
 
     def bwd_loss(self, x: Act, gout: torch.Tensor, dx: Optional[Act], accumulate: bool):
         """dlogits (recomputed) -> head data + weight gradient, after fwd_loss."""
         L = self.rt.lib
-        labels, args, ws, cw, dscale = self.loss_state
+        labels, args, ws, cw, dscale, (nm, nr) = self.loss_state
         wpart = self.rt.ws(L.mmseg_head_loss_wpart_floats(self.C, self.Cin, x.N, x.V))
-        L.mmseg_head_loss_bwd(x.ptr, x.ld, self.Cin, ptr(self.conv.weight), ptr(self.conv.bias), ptr(dscale), self.C,
-                              x.N, x.V, ptr(labels), labels.element_size(), *args, ptr(gout), 1.0, ptr(ws),
+        L.mmseg_head_loss_bwd(x.ptr, x.ld, self.Cin, nm, nr, ptr(self.conv.weight), ptr(self.conv.bias), ptr(dscale),
+                              self.C, x.N, x.V, ptr(labels), labels.element_size(), *args, ptr(gout), 1.0, ptr(ws),
                               dx.ptr if dx is not None else None, dx.ld if dx is not None else 0,
                               ptr(self.flat.grad(self.conv.weight)), ptr(self.flat.grad(self.conv.bias)), ptr(wpart),
                               int(accumulate), self.rt.code, self.rt.stream)

@@ -67,9 +67,13 @@ class _Decoder:
         """-> logits; with loss = (labels, spec, class_w): the loss scalar (fused head + loss, no logits)."""
         h = bottom
         nl = len(self.F) - 1
+        # the fused head + loss applies the last block's InstanceNorm + ReLU on load, so the training forward
+        # never writes that block's output (113 MB at 96^3 B=2)
+        self.defer_head = loss is not None and os.environ.get("MMSEG_DEFER_HEAD_NORM", "1") != "0"
         for j in range(nl):
             l = nl - 1 - j
             self.ups[j].fwd(h, self.cat[l].slot(0, self.F[l]))
+            self.blocks[j].defer_out = self.defer_head and j == nl - 1
             self.blocks[j].fwd(self.cat[l], self.dout[l])
             h = self.dout[l]
         dscale = None
@@ -78,6 +82,9 @@ class _Decoder:
             dscale = keep / (1.0 - self.p)
         if loss is not None:
             labels, spec, cw = loss
+            if self.defer_head:
+                x2, mu, rs = self.blocks[nl - 1].out_stats()
+                return self.head.fwd_loss(x2, labels, spec, cw, dscale, norm=(mu, rs))
             return self.head.fwd_loss(h, labels, spec, cw, dscale)
         # fresh logits every call (caching allocator, no copy): callers may keep them
         logits = torch.empty(h.N, self.head.C, h.D, h.H, h.W, dtype=torch.float32, device=self.rt.device)
@@ -91,7 +98,8 @@ class _Decoder:
         nl = len(self.F) - 1
         dh = self.dout[0]
         if gout is not None:
-            self.head.bwd_loss(self.dout[0], gout, dh, accumulate)
+            hx = self.blocks[nl - 1].out_stats()[0] if self.defer_head else self.dout[0]
+            self.head.bwd_loss(hx, gout, dh, accumulate)
         else:
             self.head.bwd(self.dout[0], dlogits, dh, accumulate)
         for j in reversed(range(nl)):

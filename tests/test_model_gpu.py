@@ -326,6 +326,33 @@ def test_fused_head_loss_matches_unfused(dev, tag, dtype):
 
 
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("tag", ["unet_tiny", "dual_tiny_cross_attention"])
+def test_deferred_head_norm_bitwise(dev, tag, dtype, monkeypatch):
+    """Fused head + loss: the last decoder block's InstanceNorm + ReLU applied on load by the head kernels (its
+    output never written) gives a bit-identical loss and gradients to the materialised path
+    (MMSEG_DEFER_HEAD_NORM=0), with an active Dropout3d."""
+    from mmseg_amd.engine.engine import fused_loss_supported, run_engine_loss
+    from mmseg_amd.trainer.losses import DiceCELoss
+    kind = "unet" if tag == "unet_tiny" else "dual_encoder"
+    res = []
+    for defer in ("1", "0"):
+        monkeypatch.setenv("MMSEG_DEFER_HEAD_NORM", defer)
+        cfg, m, g, M, C = _build(tag, dtype)
+        m.backbone.dropout_p = 0.3
+        m.train()
+        xs, ys = _inputs(g, M, C)
+        assert fused_loss_supported(m.backbone, kind, xs[0].to(dev))
+        torch.cuda.manual_seed(7)
+        loss = run_engine_loss(m.backbone, kind, xs[0].to(dev), ys[0].to(dev), DiceCELoss()._spec(), None)
+        loss.backward()
+        torch.cuda.synchronize()
+        assert m.backbone.__dict__["_engine"].program.dec.blocks[-1].defer_out == (defer == "1")
+        res.append((loss.detach().clone(), torch.cat([p.grad.reshape(-1) for p in m.parameters()]).clone()))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
 def test_deferred_encoder_norm_bitwise(dev, dtype, monkeypatch):
     """DualEncoder mean fusion: the encoders' output InstanceNorm + ReLU applied on load by the maxpool and the
     fusion kernel (never written) gives bit-identical logits, gradients and return_features to the

@@ -52,11 +52,11 @@ def main():
                          ptr(hws), 0, 1, s)
 
     def fused_fwd():
-        L.mmseg_head_loss_fwd(ptr(x), Cin, Cin, ptr(W), ptr(b), None, C, N, V, ptr(y), 8, *args8, ptr(loss), ptr(ws),
+        L.mmseg_head_loss_fwd(ptr(x), Cin, Cin, None, None, ptr(W), ptr(b), None, C, N, V, ptr(y), 8, *args8, ptr(loss), ptr(ws),
                               1, s)
 
     def fused_bwd():
-        L.mmseg_head_loss_bwd(ptr(x), Cin, Cin, ptr(W), ptr(b), None, C, N, V, ptr(y), 8, *args8, ptr(g), 1.0,
+        L.mmseg_head_loss_bwd(ptr(x), Cin, Cin, None, None, ptr(W), ptr(b), None, C, N, V, ptr(y), 8, *args8, ptr(g), 1.0,
                               ptr(ws), ptr(dx), Cin, ptr(gW), ptr(gb), ptr(wpart), 0, 1, s)
 
     def timeit(fn):
