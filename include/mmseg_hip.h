@@ -133,6 +133,20 @@ long long mmseg_conv3_wgrad_ws_floats(long long V, int Co, int Cip, int Ci, int 
 int mmseg_conv3_wgrad(const void* dy, int lddy, const void* x, int ldx, float* grad, float* bias_grad, int Co, int Cip,
                       int Ci, int cpg_shift, long long V, int D, int H, int W, float* ws, long long ws_floats,
                       int accumulate, int dtype, void* stream);
+/* Deferred InstanceNorm + ReLU of a 3^3 conv's input (the block's conv1 output is never written by its
+ * normalisation pass): the input holds the PRE-norm activation and the kernels stage
+ * relu((x - mean[n][c]) * rstd[n][c]) rounded to bf16, the values mmseg_instnorm_relu_fwd would write.
+ * *_ok return 1 when the shape runs the kernels that support it (brick5 forward, brick2 weight gradient). */
+int mmseg_conv3_norm_ok(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,
+                        int dtype);
+int mmseg_conv3_fwd_norm(const void* a, int lda, const float* nmean, const float* nrstd, const void* wpacked,
+                         const float* bias, void* out, int ldo, int M, int Ncols, int Cpad, int KG, int cpg_shift,
+                         int D, int H, int W, int dtype, void* stream);
+int mmseg_conv3_wgrad_norm_ok(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W, int lddy,
+                              int ldx, int dtype);
+int mmseg_conv3_wgrad_norm(const void* dy, int lddy, const void* x, int ldx, const float* nmean, const float* nrstd,
+                           float* grad, float* bias_grad, int Co, int Cip, int Ci, int cpg_shift, long long V, int D,
+                           int H, int W, float* ws, long long ws_floats, int accumulate, int dtype, void* stream);
 /* Bias gradient out[c] (+)= sum_v dy[v][c] (convolution_backward grad_bias). */
 int mmseg_colsum(const void* dy, int ld, int C, long long V, float* part, int nblk, float* out, int accumulate,
                  int dtype, void* stream);

@@ -52,7 +52,21 @@ struct GemmArgs {
   float* stats;              // brick kernels, ksplit == 1: per-brick InstanceNorm partials (mean, M2), or null
   int kchunks;               // CONV3 brick kernels: 32-channel input chunks holding real channels (0 = all);
                              // the packed weights of the rest are zero (channel-padded K side), so they are skipped
+  // deferred InstanceNorm + ReLU of the A source (brick5 only, mmseg_conv3_fwd_norm): A holds the PRE-norm
+  // activation, the kernel stages relu((a - nmean[n][c]) * nrstd[n][c]) rounded to T (in_relu_apply's values)
+  const float* nmean;
+  const float* nrstd;
 };
+
+// The deferred norm of 8 staged channels: relu((v - mu) * rs) rounded to T, in_relu_apply's operations.
+template <typename T>
+__device__ __forceinline__ void norm_relu8(V8<T>& v, const float* mu, const float* rs) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float h = (v.get(j) - mu[j]) * rs[j];
+    v.set(j, h > 0.f ? h : 0.f);
+  }
+}
 
 // 32-channel K chunks a CONV3 brick kernel iterates: all of the (power-of-two) A source's, or only the
 // leading ones that hold real channels.
@@ -1283,7 +1297,20 @@ __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int up
   // halo offsets of a brick: z / y interior bricks need one x test per lane (the unit base is uniform);
   // border bricks test every row.  Out-of-volume lanes point past the buffer end and read zeros.
   uint32_t xo[XK];
+  // deferred norm of the A source: the statistics of the sample of the brick being staged (set_x runs once per
+  // staged brick, before its store_x)
+  float nmu[8], nrs[8];
+  int norm_n = -1;
   auto set_x = [&](const Unit& q) {
+    if (g.nmean && q.n != norm_n) {
+      norm_n = q.n;
+      const int cb = q.n * cin + cg * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        nmu[j] = g.nmean[cb + j];
+        nrs[j] = g.nrstd[cb + j];
+      }
+    }
     const int xx = q.x0 - 1 + hx;
     const bool xok = xact && (unsigned)xx < (unsigned)g.W;
     const int ob = ((q.n * g.D + q.z0 - 1) * g.H + q.y0 - 1) * g.W + q.x0 - 1;   // origin voxel (may be -1)
@@ -1350,7 +1377,10 @@ __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int up
   auto store_x = [&](int buf, int k0, int k1) {
     if (xact) {
 #pragma unroll
-      for (int k = k0; k < k1; ++k) xr[k].store(Xl + (buf * XQ + (r0 + 3 * k) * RY) * EPQ + xlds0);
+      for (int k = k0; k < k1; ++k) {
+        if (g.nmean && xo[k] != 0x80000000u) norm_relu8<T>(xr[k], nmu, nrs);   // padding stays 0
+        xr[k].store(Xl + (buf * XQ + (r0 + 3 * k) * RY) * EPQ + xlds0);
+      }
     }
   };
   // per-lane A offsets (quads) of the three kx shifts: voxel hx = r16 + kx, channel group kg
@@ -1826,6 +1856,39 @@ Conv3Plan plan_conv3(int M, int Ncols, int cin, int D, int H, int W, int lda, in
   return p;
 }
 
+// True when launch_gemm<bf16, CONV3> runs conv3_brick5_kernel for this shape (the only conv kernel that
+// applies a deferred InstanceNorm + ReLU to its A source): the conditions of its branch in launch_gemm and of
+// every branch taken before it.
+bool brick5_selected(const GemmArgs& g, int tsize) {
+  if (tsize != 2 || g.ksplit != 1 || g.stats != nullptr) return false;
+  const Conv3Plan plan = plan_conv3(g.M, g.Ncols, 8 << g.cpg_shift, g.D, g.H, g.W, g.lda, g.ldo, tsize);
+  if (plan.kind != 1) return false;
+  const int nb1 = (g.M / (g.D * g.H * g.W)) * (g.D / 4) * (g.H / B2_Y) * (g.W / B2_X);
+  const int min_blocks = knob("MMSEG_BRICK2_MINBLK", 512);
+  const bool v3 = knob("MMSEG_BRICK3", 1) != 0 && knob("MMSEG_BRICK2_ZW", 1) != 2 &&
+                  (long long)g.M * g.lda * 2LL < (1LL << 31);
+  const bool wide = g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks;
+  if (!v3 || g.Ncols % 32 != 0 || (knob("MMSEG_BRICK3_BN64", 0) && wide)) return false;
+  if (gemm_nchunk(g) != 1 || !knob("MMSEG_BRICK4", 1) || wide) return false;
+  return g.H % 4 == 0 && g.W % 16 == 0 && g.ldo % 8 == 0 && (reinterpret_cast<uintptr_t>(g.out) & 15) == 0 &&
+         knob("MMSEG_BRICK5", 1);
+}
+
+int launch_brick5(const GemmArgs& g, hipStream_t s, long long* dbg, bool dma) {
+  const int nt_n = g.Ncols / 32;
+  const int per_nt = std::max(1, knob("MMSEG_BRICK4_BLOCKS", 256) / nt_n);
+  const int nb5 = (g.M / (g.D * g.H * g.W)) * (g.D / 4) * (g.H / 4) * (g.W / 16);
+  const int upb5 = ceil_div(nb5, std::min(per_nt, nb5));
+  const int bpn5 = ceil_div(nb5, upb5);
+  mmseg::note_kernel("conv3_brick5_kernel<BN32>");
+  const dim3 grid(bpn5 * nt_n), block(256);
+  if (dbg && dma) hipLaunchKernelGGL((conv3_brick5_kernel<true, true>), grid, block, 0, s, g, upb5, bpn5, dbg);
+  else if (dbg) hipLaunchKernelGGL((conv3_brick5_kernel<true, false>), grid, block, 0, s, g, upb5, bpn5, dbg);
+  else if (dma) hipLaunchKernelGGL((conv3_brick5_kernel<false, true>), grid, block, 0, s, g, upb5, bpn5, nullptr);
+  else hipLaunchKernelGGL((conv3_brick5_kernel<false, false>), grid, block, 0, s, g, upb5, bpn5, nullptr);
+  return upb5;
+}
+
 template <int MODE>
 int splitk_reduce_blocks(const GemmArgs& g) {
   const long long total = (long long)g.M * g.Ncols;
@@ -1950,6 +2013,10 @@ struct WgradArgs {
   float* bias_grad;
   int accumulate;
   int kchunks;               // CONV3 brick kernels: 32-channel chunks of x holding real channels (0 = all)
+  // deferred InstanceNorm + ReLU of x (wgrad_brick2 only, mmseg_conv3_wgrad_norm): x holds the PRE-norm
+  // activation, staged as relu((x - nmean[n][c]) * nrstd[n][c]) rounded to T
+  const float* nmean;
+  const float* nrstd;
 };
 
 __host__ __device__ __forceinline__ int wgrad_nchunk(int cpg_shift, int kchunks) {
@@ -2489,14 +2556,20 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
   float bsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
   V8<T> dr[D_PER], xr[X_PER];
+  uint32_t xin = 0;    // bit k: xr[k] is an in-volume voxel (padding stays 0 under the deferred norm)
+  int xn = 0;          // sample of the staged brick
+  int norm_n = -1;     // sample whose deferred-norm statistics nmu / nrs hold
+  float nmu[8], nrs[8];
   auto load = [&](long long b) {
     const int bx = (int)(b % bx_n);
     long long q = b / bx_n;
     const int by = (int)(q % by_n);
     q /= by_n;
     const int bz = (int)(q % bz_n);
-    const long long nbase = (q / bz_n) * g.D * HW;
+    xn = (int)(q / bz_n);
+    const long long nbase = (long long)xn * g.D * HW;
     const int z0 = bz * BRK_Z, y0 = by * BRK_Y, x0 = bx * BRK_X;
+    xin = 0;
 #pragma unroll
     for (int k = 0; k < D_PER; ++k) {
       const int e = tid + k * 512, v = e / CG, cg = e % CG;
@@ -2510,10 +2583,12 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
         const int h = e >> 2, cg = e & 3;
         const int hx = h % HLO_X, hy = (h / HLO_X) % HLO_Y, hz = h / (HLO_X * HLO_Y);
         const int z = z0 - 1 + hz, y = y0 - 1 + hy, x = x0 - 1 + hx;
-        if ((unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W)
+        if ((unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W) {
           xr[k].load(X + (nbase + z * HW + (long long)y * g.W + x) * g.ldb + c0 + cg * 8);
-        else
+          xin |= 1u << k;
+        } else {
           xr[k].zero();
+        }
       }
     }
   };
@@ -2528,6 +2603,20 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
 #pragma unroll
         for (int j = 0; j < 8; ++j) bsum[j] += dr[k].get(j);
       }
+    }
+    if (g.nmean) {   // deferred InstanceNorm + ReLU of x: channels c0 + 8 (tid & 3) .. of sample xn
+      if (xn != norm_n) {   // (the statistics change only when the brick range crosses into the next sample)
+        norm_n = xn;
+        const int cb = xn * cin + c0 + (tid & 3) * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          nmu[j] = g.nmean[cb + j];
+          nrs[j] = g.nrstd[cb + j];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < X_PER; ++k)
+        if ((xin >> k) & 1u) norm_relu8<T>(xr[k], nmu, nrs);
     }
 #pragma unroll
     for (int k = 0; k < X_PER; ++k) {
@@ -3189,6 +3278,12 @@ int launch_splitk_reduce(const GemmArgs& g, hipStream_t s) {
 
 template <typename T, int MODE>
 int launch_gemm(GemmArgs g, hipStream_t s) {
+  if (g.nmean) {   // deferred InstanceNorm + ReLU of A: brick5 only (mmseg_conv3_norm_ok)
+    MMSEG_REQUIRE(MODE == MODE_CONV3 && brick5_selected(g, (int)sizeof(T)),
+                  "conv3 with a deferred norm needs the brick5 kernel for this shape (mmseg_conv3_norm_ok)");
+    launch_brick5(g, s, nullptr, false);
+    return mmseg::check_launch("conv3_brick5_norm");
+  }
   const int Cbig = g.Ncols >= 64;
   dim3 block(256);
   const int brick = knob("MMSEG_BRICK", 2);
@@ -3299,18 +3394,12 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
         const int bpn = ceil_div(nb1, upb);
         if (g.H % 4 == 0 && g.W % 16 == 0 && g.ldo % 8 == 0 && (reinterpret_cast<uintptr_t>(g.out) & 15) == 0 &&
             knob("MMSEG_BRICK5", 1)) {   // (16-B output stores)
-          const int nb5 = (g.M / (g.D * g.H * g.W)) * (g.D / 4) * (g.H / 4) * (g.W / 16);
-          const int upb5 = ceil_div(nb5, std::min(per_nt, nb5));
-          const int bpn5 = ceil_div(nb5, upb5);
-          mmseg::note_kernel("conv3_brick5_kernel<BN32>");
+          const bool dma = knob("MMSEG_BRICK5_DMA", 0) != 0;
           if (knob("MMSEG_BRICK5_DBG", 0)) {   // phase timing probe (diagnostics only)
             static long long* dbg = nullptr;
             if (!dbg) hipMalloc(&dbg, 4 * 128 * sizeof(long long));
             hipMemsetAsync(dbg, 0, 4 * 128 * sizeof(long long), s);
-            if (knob("MMSEG_BRICK5_DMA", 0))
-              hipLaunchKernelGGL((conv3_brick5_kernel<true, true>), dim3(bpn5 * nt_n), block, 0, s, g, upb5, bpn5, dbg);
-            else
-              hipLaunchKernelGGL((conv3_brick5_kernel<true, false>), dim3(bpn5 * nt_n), block, 0, s, g, upb5, bpn5, dbg);
+            const int upb5 = launch_brick5(g, s, dbg, dma);
             long long h[4 * 128];
             hipStreamSynchronize(s);
             hipMemcpy(h, dbg, sizeof(h), hipMemcpyDeviceToHost);
@@ -3324,10 +3413,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
               fprintf(stderr, "\n");
             }
           } else {
-            if (knob("MMSEG_BRICK5_DMA", 0))
-              hipLaunchKernelGGL((conv3_brick5_kernel<false, true>), dim3(bpn5 * nt_n), block, 0, s, g, upb5, bpn5, nullptr);
-            else
-              hipLaunchKernelGGL((conv3_brick5_kernel<false, false>), dim3(bpn5 * nt_n), block, 0, s, g, upb5, bpn5, nullptr);
+            launch_brick5(g, s, nullptr, dma);
           }
         } else {
           mmseg::note_kernel("conv3_brick4_kernel<BN32>");
@@ -3741,6 +3827,33 @@ int mmseg_conv_gemm_ex(const void* a, int lda, const void* wpacked, const float*
   return launch_gemm_mode<float>(g, mode, s);
 }
 
+// 1 when mmseg_conv3_fwd_norm can run this shape (the brick5 kernel, the only conv forward that applies a
+// deferred InstanceNorm + ReLU to its input): bf16, one 32-channel input chunk, 32 output columns, W % 16.
+int mmseg_conv3_norm_ok(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,
+                        int dtype) {
+  if (dtype != MMSEG_BF16 || !knob("MMSEG_DEFER_CONV_NORM", 1)) return 0;
+  GemmArgs g{};
+  g.lda = lda; g.ldo = ldo; g.M = M; g.Ncols = Ncols; g.Cpad = Cpad; g.KG = KG; g.cpg_shift = cpg_shift;
+  g.D = D; g.H = H; g.W = W; g.ksplit = 1;
+  g.out = reinterpret_cast<void*>(static_cast<uintptr_t>(256));   // the caller's output is 16-B aligned (checked)
+  return brick5_selected(g, 2) ? 1 : 0;
+}
+
+// 3^3 conv forward of an A source holding the PRE-norm activation of an InstanceNorm + ReLU: the kernel stages
+// relu((a - nmean[n][c]) * nrstd[n][c]) rounded to bf16, exactly the values mmseg_instnorm_relu_fwd would
+// write, so that output never has to be materialised (requires mmseg_conv3_norm_ok).
+int mmseg_conv3_fwd_norm(const void* a, int lda, const float* nmean, const float* nrstd, const void* wpacked,
+                         const float* bias, void* out, int ldo, int M, int Ncols, int Cpad, int KG, int cpg_shift,
+                         int D, int H, int W, int dtype, void* stream) {
+  MMSEG_REQUIRE(nmean && nrstd && (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
+                    mmseg_conv3_norm_ok(M, Ncols, Cpad, KG, cpg_shift, D, H, W, lda, ldo, dtype),
+                "conv3_fwd_norm: unsupported shape (mmseg_conv3_norm_ok)");
+  const int KGp = (KG + 3) & ~3;
+  GemmArgs g{a, lda, wpacked, bias, out, ldo, nullptr, M, Ncols, Cpad, KG, cpg_shift, D, H, W, 1, KGp,
+             knob("MMSEG_SWIZZLE", 1), nullptr, 0, nmean, nrstd};
+  return launch_gemm<bf16_t, MODE_CONV3>(g, (hipStream_t)stream);
+}
+
 // Number of K splits the CONV3 path wants for this shape (callers size the
 // split-K workspace, ksplit*M*Ncols floats, with it and pass it as ksplit).
 int mmseg_conv3_splits(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,
@@ -3822,12 +3935,43 @@ long long mmseg_conv3_wgrad_ws_floats(long long V, int Co, int Cip, int Ci, int 
   return plan_conv3_wgrad(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype, cap).ws;
 }
 
+int conv3_wgrad_impl(const void* dy, int lddy, const void* x, int ldx, const float* nmean, const float* nrstd,
+                     float* grad, float* bias_grad, int Co, int Cip, int Ci, int cpg_shift, long long V, int D, int H,
+                     int W, float* ws, long long ws_floats, int accumulate, int dtype, void* stream);
+
 int mmseg_conv3_wgrad(const void* dy, int lddy, const void* x, int ldx, float* grad, float* bias_grad, int Co, int Cip,
                       int Ci, int cpg_shift, long long V, int D, int H, int W, float* ws, long long ws_floats,
                       int accumulate, int dtype, void* stream) {
+  return conv3_wgrad_impl(dy, lddy, x, ldx, nullptr, nullptr, grad, bias_grad, Co, Cip, Ci, cpg_shift, V, D, H, W, ws,
+                          ws_floats, accumulate, dtype, stream);
+}
+
+// 1 when mmseg_conv3_wgrad_norm can run this shape: the brick2 weight-gradient kernel (the only one that applies
+// a deferred InstanceNorm + ReLU to x), no channel padding, bf16.
+int mmseg_conv3_wgrad_norm_ok(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W, int lddy,
+                              int ldx, int dtype) {
+  if (dtype != MMSEG_BF16 || Ci != Cip || !knob("MMSEG_WGRAD_V3", 1) || !knob("MMSEG_DEFER_CONV_NORM", 1)) return 0;
+  return plan_conv3_wgrad(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype, 1LL << 40).kind == 2 ? 1 : 0;
+}
+
+// mmseg_conv3_wgrad with x the PRE-norm activation of an InstanceNorm + ReLU ([N][Cip] mean / rstd), applied on
+// staging exactly as mmseg_instnorm_relu_fwd would write it (requires mmseg_conv3_wgrad_norm_ok).
+int mmseg_conv3_wgrad_norm(const void* dy, int lddy, const void* x, int ldx, const float* nmean, const float* nrstd,
+                           float* grad, float* bias_grad, int Co, int Cip, int Ci, int cpg_shift, long long V, int D,
+                           int H, int W, float* ws, long long ws_floats, int accumulate, int dtype, void* stream) {
+  MMSEG_REQUIRE(nmean && nrstd && mmseg_conv3_wgrad_norm_ok(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype),
+                "conv3_wgrad_norm: unsupported shape (mmseg_conv3_wgrad_norm_ok)");
+  return conv3_wgrad_impl(dy, lddy, x, ldx, nmean, nrstd, grad, bias_grad, Co, Cip, Ci, cpg_shift, V, D, H, W, ws,
+                          ws_floats, accumulate, dtype, stream);
+}
+
+int conv3_wgrad_impl(const void* dy, int lddy, const void* x, int ldx, const float* nmean, const float* nrstd,
+                     float* grad, float* bias_grad, int Co, int Cip, int Ci, int cpg_shift, long long V, int D, int H,
+                     int W, float* ws, long long ws_floats, int accumulate, int dtype, void* stream) {
   MMSEG_REQUIRE(Co % 8 == 0 && Cip % 8 == 0 && Ci <= Cip && (8 << cpg_shift) == Cip,
                 "conv3_wgrad: Co=%d, Cip=%d must be multiples of 8, Ci=%d <= Cip, Cip = 8 << cpg_shift", Co, Cip, Ci);
   const Conv3WgradPlan p = plan_conv3_wgrad(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype, ws_floats);
+  MMSEG_REQUIRE(!nmean || p.kind == 2, "conv3_wgrad: a deferred norm needs the brick2 weight-gradient kernel");
   MMSEG_REQUIRE(p.ws <= ws_floats && (p.ws == 0 || ws != nullptr), "conv3_wgrad: workspace of %lld floats < %lld",
                 ws_floats, p.ws);
   const int ncols = 27 * Cip;
@@ -3836,7 +3980,7 @@ int mmseg_conv3_wgrad(const void* dy, int lddy, const void* x, int ldx, float* g
   const long long vps = ((V + p.ksplit - 1) / p.ksplit + 63) / 64 * 64;
   WgradArgs g{dy, lddy, x, ldx, part, p.direct ? bias_grad : bpart, Co, ncols, cpg_shift, V, D, H, W, p.ksplit, vps,
               knob("MMSEG_WGRAD_SWIZZLE", 0), p.kind, p.direct ? grad : nullptr, p.direct ? bias_grad : nullptr,
-              accumulate, wgrad_kchunks(Cip, Ci)};
+              accumulate, wgrad_kchunks(Cip, Ci), nmean, nrstd};
   hipStream_t s = (hipStream_t)stream;
   const int rc = dtype == MMSEG_BF16 ? launch_wgrad<bf16_t, MODE_CONV3>(g, s) : launch_wgrad<float, MODE_CONV3>(g, s);
   if (rc || p.direct) return rc;

@@ -223,10 +223,32 @@ class Conv3:
                                            MODE_CONV3, M, nc, self.Cpad, self.KG, self.cpg_shift, x.D, x.H, x.W, ks,
                                            None, self.kreal_f, self.rt.code, self.rt.stream)
 
-    def bwd(self, x: Act, dy: Act, dx: Optional[Act], accumulate: bool):
+    def norm_ok(self, x: Act, y: Act) -> bool:
+        """True when this conv can take its input as the PRE-norm activation of an InstanceNorm + ReLU and apply
+        it on staging, forward and weight gradient (fwd_norm / bwd(norm=...)): the brick5 / brick2 kernels."""
+        L, code = self.rt.lib, self.rt.code
+        return (self.need_dgrad and self.wg_stage is None and self.Cip == self.Ci and self.ncols_f == self.Co
+                and not self._stem(x, y.ld)
+                and bool(L.mmseg_conv3_norm_ok(x.N * x.V, self.ncols_f, self.Cpad, self.KG, self.cpg_shift, x.D,
+                                               x.H, x.W, x.ld, y.ld, code))
+                and bool(L.mmseg_conv3_wgrad_norm_ok(x.N * x.V, self.Co, self.Cip, self.Ci, self.cpg_shift, x.D,
+                                                     x.H, x.W, y.ld, x.ld, code)))
+
+    def fwd_norm(self, x: Act, mean: torch.Tensor, rstd: torch.Tensor, y: Act):
+        """fwd() of relu(InstanceNorm(x)) with x the pre-norm activation (requires norm_ok)."""
+        with TIMER.region(_gemm_name(self.rt, self.ncols_f, "conv3"), flops=2.0 * x.N * x.V * self.Co * 27 * self.Ci,
+                          nbytes=_io_bytes(self.rt, x.N * x.V, self.Cip, self.Co, 27 * self.Cip * self.Co)):
+            self.rt.lib.mmseg_conv3_fwd_norm(x.ptr, x.ld, ptr(mean), ptr(rstd), ptr(self.wf), ptr(self.conv.bias),
+                                             y.ptr, y.ld, x.N * x.V, self.ncols_f, self.Cpad, self.KG,
+                                             self.cpg_shift, x.D, x.H, x.W, self.rt.code, self.rt.stream)
+
+    def bwd(self, x: Act, dy: Act, dx: Optional[Act], accumulate: bool,
+            norm: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
+        """norm = (mean, rstd): x is the pre-norm activation of an InstanceNorm + ReLU applied on staging by the
+        weight-gradient kernel (see fwd_norm)."""
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
         V = x.N * x.V
-        if dx is None and self._stem(x, dy.ld):
+        if dx is None and norm is None and self._stem(x, dy.ld):
             # 1,024 splits: one round of resident blocks at 96^3 B=2 and half the partials of 2,048 (r02 stembench:
             # 42 + 12.8 us against 44 + 19.7 us with the reduce)
             ks = L.mmseg_stem_wgrad_splits(x.N, x.D, x.H, x.W, int(os.environ.get("MMSEG_STEM_SPLITS", "1024")))
@@ -249,11 +271,17 @@ class Conv3:
         wgrad = self.flat.grad(self.conv.weight)
         with TIMER.region(_gemm_name(self.rt, 0, "conv3"), flops=2.0 * V * self.Co * 27 * self.Ci,
                           nbytes=_io_bytes(self.rt, V, self.Cip, self.Co, 27 * self.Cip * self.Co, 4)):
-            L.mmseg_conv3_wgrad(dy.ptr, dy.ld, x.ptr, x.ld,
-                                ptr(self.wg_stage) if self.wg_stage is not None else ptr(wgrad),
-                                ptr(self.flat.grad(self.conv.bias)) if self.conv.bias is not None else None, rows,
-                                self.Cip, self.Ci, self.cpg_shift, V, x.D, x.H, x.W, ptr(ws), wsf,
-                                int(accumulate) if self.wg_stage is None else 0, code, s)
+            if norm is not None:
+                L.mmseg_conv3_wgrad_norm(dy.ptr, dy.ld, x.ptr, x.ld, ptr(norm[0]), ptr(norm[1]), ptr(wgrad),
+                                         ptr(self.flat.grad(self.conv.bias)) if self.conv.bias is not None else None,
+                                         rows, self.Cip, self.Ci, self.cpg_shift, V, x.D, x.H, x.W, ptr(ws), wsf,
+                                         int(accumulate), code, s)
+            else:
+                L.mmseg_conv3_wgrad(dy.ptr, dy.ld, x.ptr, x.ld,
+                                    ptr(self.wg_stage) if self.wg_stage is not None else ptr(wgrad),
+                                    ptr(self.flat.grad(self.conv.bias)) if self.conv.bias is not None else None, rows,
+                                    self.Cip, self.Ci, self.cpg_shift, V, x.D, x.H, x.W, ptr(ws), wsf,
+                                    int(accumulate) if self.wg_stage is None else 0, code, s)
         if self.wg_stage is not None:     # rows [0, Co) of the staging are the gradient's storage order
             n = wgrad.numel()
             if accumulate:
@@ -417,6 +445,10 @@ class Block:
         self.x2 = rt.act(N, D, H, W, C)
         self.stats = torch.empty(4, N * C, dtype=torch.float32, device=rt.device)  # m1, r1, m2, r2
         self.nb = None   # fused-statistics bricks per sample of (conv1, conv2), set on the first forward
+        # conv1's InstanceNorm + ReLU applied by conv2's kernels on staging (y1 never written): the 96^3 32 -> 32
+        # layers (brick5 forward, brick2 weight gradient)
+        self.norm1_ok = None
+        self.defer1 = False
 
     def _norm_fwd(self, x: Act, y: Act, m: torch.Tensor, r: torch.Tensor, part=None, nb: int = 0):
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
@@ -451,9 +483,16 @@ class Block:
             self.part = torch.empty(xin.N * n * self.Co * 2, dtype=torch.float32, device=self.rt.device) if n else None
         p1 = self.part if self.nb[0] else None
         p2 = self.part if self.nb[1] else None
+        if self.norm1_ok is None:
+            self.norm1_ok = not self.nb[1] and self.c2.norm_ok(self.x1, self.x2)
+        self.defer1 = self.norm1_ok and os.environ.get("MMSEG_DEFER_CONV_NORM", "1") != "0"   # per forward (A/B)
         self.c1.fwd(xin, self.x1, stats_part=p1)
-        self._norm_fwd(self.x1, self.y1, st[0], st[1], p1, self.nb[0])
-        self.c2.fwd(self.y1, self.x2, stats_part=p2)
+        if self.defer1:
+            self._norm_stats(self.x1, st[0], st[1], p1, self.nb[0])
+            self.c2.fwd_norm(self.x1, st[0], st[1], self.x2)
+        else:
+            self._norm_fwd(self.x1, self.y1, st[0], st[1], p1, self.nb[0])
+            self.c2.fwd(self.y1, self.x2, stats_part=p2)
         if self.defer_out:
             self._norm_stats(self.x2, st[2], st[3], p2, self.nb[1])
         else:
@@ -481,7 +520,10 @@ class Block:
         g2 = self.x2                      # in place over x2
         self._norm_bwd(self.x2, st[2], st[3], dy, g2)
         dy1 = self.y1                     # conv2 wgrad reads y1 before dgrad overwrites it
-        self.c2.bwd(self.y1, g2, dy1, accumulate)
+        if self.defer1:                   # (y1 was never written: the weight gradient normalises x1 itself)
+            self.c2.bwd(self.x1, g2, dy1, accumulate, norm=(st[0], st[1]))
+        else:
+            self.c2.bwd(self.y1, g2, dy1, accumulate)
         g1 = self.x1
         self._norm_bwd(self.x1, st[0], st[1], DySpec(p1=dy1), g1)
         self.c1.bwd(xin, g1, dxin, accumulate)

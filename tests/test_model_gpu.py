@@ -352,6 +352,35 @@ def test_deferred_head_norm_bitwise(dev, tag, dtype, monkeypatch):
     assert torch.equal(res[0][1], res[1][1])
 
 
+@pytest.mark.parametrize("model", ["unet", "dual_encoder"])
+def test_deferred_conv_norm_bitwise(dev, model, monkeypatch):
+    """bf16, 32-channel top level (the brick5 / brick2 kernels): conv1's InstanceNorm + ReLU applied by conv2's
+    forward and weight-gradient kernels on staging (y1 never written) gives a bit-identical loss and gradients
+    to the materialised path (MMSEG_DEFER_CONV_NORM=0)."""
+    from mmseg_amd.engine.engine import fused_loss_supported, run_engine_loss
+    from mmseg_amd.trainer.losses import DiceCELoss
+    gen = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 2, 32, 32, 32, generator=gen).to(dev)
+    y = torch.randint(0, 3, (2, 32, 32, 32), generator=gen).to(dev)
+    res = []
+    for defer in ("1", "0"):
+        monkeypatch.setenv("MMSEG_DEFER_CONV_NORM", defer)
+        cfg = make_config(model, ["CT", "PET"], 3, [32, 64, 128], dtype="bfloat16")
+        torch.manual_seed(0)
+        m = build_model(cfg).to(dev)
+        m.train()
+        assert fused_loss_supported(m.backbone, model, x)
+        loss = run_engine_loss(m.backbone, model, x, y, DiceCELoss()._spec(), None)
+        loss.backward()
+        torch.cuda.synchronize()
+        prog = m.backbone.__dict__["_engine"].program
+        top = prog.init if model == "unet" else prog.encs[0][0]
+        assert top.defer1 == (defer == "1") and prog.dec.blocks[-1].defer1 == (defer == "1")
+        res.append((loss.detach().clone(), torch.cat([p.grad.reshape(-1) for p in m.parameters()]).clone()))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+
+
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
 def test_deferred_encoder_norm_bitwise(dev, dtype, monkeypatch):
     """DualEncoder mean fusion: the encoders' output InstanceNorm + ReLU applied on load by the maxpool and the
