@@ -133,6 +133,14 @@ long long mmseg_conv3_wgrad_ws_floats(long long V, int Co, int Cip, int Ci, int 
 int mmseg_conv3_wgrad(const void* dy, int lddy, const void* x, int ldx, float* grad, float* bias_grad, int Co, int Cip,
                       int Ci, int cpg_shift, long long V, int D, int H, int W, float* ws, long long ws_floats,
                       int accumulate, int dtype, void* stream);
+/* mmseg_conv_gemm_ex (without fused statistics) with the output columns [split, Ncols) written to a second
+ * tensor out2 (row pitch ldo2) as its columns 0..Ncols-split-1 (split, ldo, ldo2 multiples of 8, out2 16-B
+ * aligned; not the transposed-conv forward): the decoder's first-conv data gradient writes d(upsampled) and
+ * d(skip) as two dense tensors. */
+int mmseg_conv_gemm_split(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
+                          void* out2, int ldo2, int split, float* splitk_ws, int mode, int M, int Ncols, int Cpad,
+                          int KG, int cpg_shift, int D, int H, int W, int ksplit, int cin_real, int dtype,
+                          void* stream);
 /* Deferred InstanceNorm + ReLU of a 3^3 conv's input (the block's conv1 output is never written by its
  * normalisation pass): the input holds the PRE-norm activation and the kernels stage
  * relu((x - mean[n][c]) * rstd[n][c]) rounded to bf16, the values mmseg_instnorm_relu_fwd would write.

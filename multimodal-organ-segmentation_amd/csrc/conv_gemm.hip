@@ -56,7 +56,19 @@ struct GemmArgs {
   // activation, the kernel stages relu((a - nmean[n][c]) * nrstd[n][c]) rounded to T (in_relu_apply's values)
   const float* nmean;
   const float* nrstd;
+  // split output (mmseg_conv_gemm_split): columns >= split go to out2 (column - split, row pitch ldo2).  The
+  // decoder's first-conv data gradient writes d(upsampled) and d(skip) as two dense tensors instead of one
+  // [voxel][2F] tensor whose halves every later reader fetched at half a cache line per voxel.
+  void* out2;
+  int ldo2, split;
 };
+
+// Output element (row voxel, column) of a GEMM (split-aware; split is a multiple of 8).
+template <typename T>
+__device__ __forceinline__ T* out_at(const GemmArgs& g, long long vox, int col) {
+  if (g.out2 && col >= g.split) return reinterpret_cast<T*>(g.out2) + vox * g.ldo2 + (col - g.split);
+  return reinterpret_cast<T*>(g.out) + vox * g.ldo + col;
+}
 
 // The deferred norm of 8 staged channels: relu((v - mu) * rs) rounded to T, in_relu_apply's operations.
 template <typename T>
@@ -319,7 +331,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs g) {
         const int t = col / Cout, co = col - t * Cout;
         O[convt_child(row, t, g) * g.ldo + co] = El[lr * EPT + lc];
       } else {
-        O[row * g.ldo + col] = El[lr * EPT + lc];
+        *out_at<T>(g, row, col) = El[lr * EPT + lc];
       }
     }
     return;
@@ -335,7 +347,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs g) {
       const int t = col / Cout, co = col - t * Cout;
       o.store(O + convt_child(row, t, g) * g.ldo + co);
     } else {
-      o.store(O + row * g.ldo + col);
+      o.store(out_at<T>(g, row, col));
     }
   }
 }
@@ -498,7 +510,7 @@ __global__ __launch_bounds__(256) void conv3_brick_kernel(GemmArgs g) {
         const int row = kg * 4 + r;            // 0..15 within the tile
         const int y = y0 + 2 * i + (row >> 3), x = x0 + (row & 7), z = z0 + wave;
         const long long vox = nbase + z * HW + (long long)y * g.W + x;
-        O[vox * g.ldo + col] = from_f<T>(acc[i][j][r] + bv);
+        *out_at<T>(g, vox, col) = from_f<T>(acc[i][j][r] + bv);
       }
     }
 }
@@ -733,7 +745,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kern
       const int z = z0 + (v >> 6), y = y0 + ((v >> 3) & 7), x = x0 + (v & 7);
       V8<T> o;
       o.load(El + v * EP + cg * 8);
-      o.store(O + (nbase + z * HW + (long long)y * g.W + x) * g.ldo + col);
+      o.store(out_at<T>(g, nbase + z * HW + (long long)y * g.W + x, col));
     }
   }
 }
@@ -999,7 +1011,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kern
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
         const int z = cur.z0 + wave, y = cur.y0 + 2 * (i & 3) + (r16 >> 3), x = cur.x0 + (r16 & 7);
-        T* dst = O + (obase + (long long)(z * g.H + y) * g.W + x) * g.ldo + col;
+        T* dst = out_at<T>(g, obase + (long long)(z * g.H + y) * g.W + x, col);
         if constexpr (sizeof(T) == 2) {
           typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
           bf16x4 o;
@@ -1190,7 +1202,7 @@ __global__ __launch_bounds__(256, 1) void conv3_brick4_kernel(GemmArgs g, int up
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
         const int z = cur.z0 + wave, y = cur.y0 + 2 * i + (r16 >> 3), x = cur.x0 + (r16 & 7);
-        T* dst = O + (obase + (long long)(z * g.H + y) * g.W + x) * g.ldo + col;
+        T* dst = out_at<T>(g, obase + (long long)(z * g.H + y) * g.W + x, col);
         typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
         bf16x4 o;
 #pragma unroll
@@ -1405,7 +1417,7 @@ __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int up
 #pragma unroll
     for (int i = 0; i < BY; ++i) {
       const int z = q.z0 + wave, y = q.y0 + i, x = q.x0 + r16;
-      T* dst = O + (obase + (long long)(z * g.H + y) * g.W + x) * g.ldo + n0 + 8 * kg;
+      T* dst = out_at<T>(g, obase + (long long)(z * g.H + y) * g.W + x, n0 + 8 * kg);
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < RN; ++j)
@@ -1762,7 +1774,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kern
       if (col < g.Ncols) {
         V8<T> o;
         o.load(El + rr * EP + cg * 8);
-        o.store(O + row_vox(rr) * g.ldo + col);
+        o.store(out_at<T>(g, row_vox(rr), col));
       }
     }
   } else {
@@ -1919,7 +1931,7 @@ __global__ void gemm_splitk_reduce(GemmArgs g) {
     if (g.bias) {
       v.x += g.bias[col]; v.y += g.bias[col + 1]; v.z += g.bias[col + 2]; v.w += g.bias[col + 3];
     }
-    T* O = reinterpret_cast<T*>(g.out) + row * g.ldo + col;
+    T* O = out_at<T>(g, row, col);
     O[0] = from_f<T>(v.x); O[1] = from_f<T>(v.y); O[2] = from_f<T>(v.z); O[3] = from_f<T>(v.w);
     return;
   }
@@ -1937,7 +1949,7 @@ __global__ void gemm_splitk_reduce(GemmArgs g) {
     O[convt_child(row, t, g) * g.ldo + co] = from_f<T>(v);
   } else {
     if (g.bias) v += g.bias[col];
-    O[row * g.ldo + col] = from_f<T>(v);
+    *out_at<T>(g, row, col) = from_f<T>(v);
   }
 }
 
@@ -1978,7 +1990,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_s(GemmArgs g) {
   if (g.bias) {
     v.x += g.bias[col]; v.y += g.bias[col + 1]; v.z += g.bias[col + 2]; v.w += g.bias[col + 3];
   }
-  T* O = reinterpret_cast<T*>(g.out) + row * g.ldo + col;
+  T* O = out_at<T>(g, row, col);
   O[0] = from_f<T>(v.x); O[1] = from_f<T>(v.y); O[2] = from_f<T>(v.z); O[3] = from_f<T>(v.w);
 }
 
@@ -3803,9 +3815,34 @@ int mmseg_conv_gemm_stats(const void* a, int lda, const void* wpacked, const flo
 
 // mmseg_conv_gemm_stats for an A source whose channels past cin_real are padding (zero weights): the CONV3
 // brick kernels skip the 32-channel chunks wholly past cin_real.  cin_real = 0: every channel is real.
+int conv_gemm_impl(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo, void* out2,
+                   int ldo2, int split, float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift,
+                   int D, int H, int W, int ksplit, float* stats_part, int cin_real, int dtype, void* stream);
+
 int mmseg_conv_gemm_ex(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
                        float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H,
                        int W, int ksplit, float* stats_part, int cin_real, int dtype, void* stream) {
+  return conv_gemm_impl(a, lda, wpacked, bias, out, ldo, nullptr, 0, 0, splitk_ws, mode, M, Ncols, Cpad, KG,
+                        cpg_shift, D, H, W, ksplit, stats_part, cin_real, dtype, stream);
+}
+
+// mmseg_conv_gemm_ex (no fused statistics) whose output columns [split, Ncols) go to a second tensor out2 (row
+// pitch ldo2) as columns 0..: the decoder's first-conv data gradient writes d(upsampled) and d(skip) dense.
+int mmseg_conv_gemm_split(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
+                          void* out2, int ldo2, int split, float* splitk_ws, int mode, int M, int Ncols, int Cpad,
+                          int KG, int cpg_shift, int D, int H, int W, int ksplit, int cin_real, int dtype,
+                          void* stream) {
+  MMSEG_REQUIRE(out2 && split > 0 && split < Ncols && split % 8 == 0 && ldo2 % 8 == 0 && ldo % 8 == 0 &&
+                    (reinterpret_cast<uintptr_t>(out2) & 15) == 0 && mode != MODE_CONVT_FWD,
+                "conv_gemm_split: split %d must be a multiple of 8 inside (0, %d), ldo / ldo2 multiples of 8, out2 "
+                "16-B aligned", split, Ncols);
+  return conv_gemm_impl(a, lda, wpacked, bias, out, ldo, out2, ldo2, split, splitk_ws, mode, M, Ncols, Cpad, KG,
+                        cpg_shift, D, H, W, ksplit, nullptr, cin_real, dtype, stream);
+}
+
+int conv_gemm_impl(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo, void* out2,
+                   int ldo2, int split, float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift,
+                   int D, int H, int W, int ksplit, float* stats_part, int cin_real, int dtype, void* stream) {
   MMSEG_REQUIRE(cin_real >= 0 && cin_real <= (8 << cpg_shift), "conv_gemm: cin_real %d outside [0, %d]", cin_real,
                 8 << cpg_shift);
   MMSEG_REQUIRE(!stats_part || (mode == MODE_CONV3 && ksplit == 1 &&
@@ -3821,7 +3858,8 @@ int mmseg_conv_gemm_ex(const void* a, int lda, const void* wpacked, const float*
   ksplit = ceil_div(KGp, kps);
   GemmArgs g{a, lda, wpacked, bias, out, ldo, splitk_ws, M, Ncols, Cpad, KG, cpg_shift, D, H, W, ksplit, kps,
              knob("MMSEG_SWIZZLE", 1), stats_part,
-             (mode == MODE_CONV3 && knob("MMSEG_KCHUNKS", 1)) ? (cin_real + 31) / 32 : 0};
+             (mode == MODE_CONV3 && knob("MMSEG_KCHUNKS", 1)) ? (cin_real + 31) / 32 : 0, nullptr, nullptr, out2,
+             ldo2, split};
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16) return launch_gemm_mode<bf16_t>(g, mode, s);
   return launch_gemm_mode<float>(g, mode, s);

@@ -290,15 +290,23 @@ class Conv3:
                 wgrad.view(-1).copy_(self.wg_stage[:n])
         self.flat.mark(*[p for p in (self.conv.weight, self.conv.bias) if p is not None])
         if dx is not None:
+            # dx = (lo, hi): columns [0, lo.C) into lo, the rest into hi (two dense tensors, mmseg_conv_gemm_split)
+            split = isinstance(dx, tuple)
+            d0 = dx[0] if split else dx
             M = V
             nc = self.ncols_d
-            ks = L.mmseg_conv3_splits(M, nc, self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, dy.ld, dx.ld, code)
+            ks = L.mmseg_conv3_splits(M, nc, self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, dy.ld, d0.ld, code)
             ws = self.rt.ws(ks * M * nc) if ks > 1 else None
             with TIMER.region(_gemm_name(self.rt, nc, "conv3"), flops=2.0 * M * self.Co * 27 * self.Ci,
                               nbytes=_io_bytes(self.rt, M, self.Co, self.Cip, 27 * self.Cip * self.Co)):
-                L.mmseg_conv_gemm_ex(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, ptr(ws), MODE_CONV3, M, nc,
-                                     self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, ks, None, self.kreal_d, code,
-                                     s)
+                if split:
+                    L.mmseg_conv_gemm_split(dy.ptr, dy.ld, ptr(self.wd), None, d0.ptr, d0.ld, dx[1].ptr, dx[1].ld,
+                                            d0.C, ptr(ws), MODE_CONV3, M, nc, self.Cpad_d, self.KGd, self.dshift, x.D,
+                                            x.H, x.W, ks, self.kreal_d, code, s)
+                else:
+                    L.mmseg_conv_gemm_ex(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, ptr(ws), MODE_CONV3, M,
+                                         nc, self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, ks, None,
+                                         self.kreal_d, code, s)
 
 
 class ConvT2:

@@ -59,9 +59,24 @@ class _Decoder:
         rt, F = self.rt, self.F
         self.cat = [rt.act(N, *dims[l], 2 * F[l]) for l in range(len(F) - 1)]
         self.dout = [rt.act(N, *dims[l], F[l]) for l in range(len(F) - 1)]
+        # backward: d(cat) as two DENSE tensors over cat's memory (d(upsampled) in its first half, d(skip) in the
+        # second), written by the first conv's split data gradient.  Interleaved [voxel][2F], every reader of one
+        # half (the transposed conv's backward, the encoders' InstanceNorm backward) fetched full cache lines for
+        # half of them: 79 vs 39 us for the 96^3 IN backward partial pass (tools/inbench.py)
+        self.dsplit = []
+        for l in range(len(F) - 1):
+            c = self.cat[l]
+            half = c.N * c.V * F[l]
+            self.dsplit.append((Act(c.buf, 0, F[l], F[l], c.N, c.D, c.H, c.W),
+                                Act(c.buf, half, F[l], F[l], c.N, c.D, c.H, c.W)))
+        self.split_bwd = False
 
     def skip_slot(self, l: int) -> Act:
         return self.cat[l].slot(self.F[l], self.F[l])
+
+    def dskip(self, l: int) -> Act:
+        """Gradient of the skip input of decoder level l (valid after bwd)."""
+        return self.dsplit[l][1] if self.split_bwd else self.skip_slot(l)
 
     def fwd(self, bottom: Act, training: bool, loss=None):
         """-> logits; with loss = (labels, spec, class_w): the loss scalar (fused head + loss, no logits)."""
@@ -96,6 +111,7 @@ class _Decoder:
         """Returns the gradient of `bottom` (aliases `bottom`'s buffer).  gout (a device scalar) instead of
         dlogits: the fused head + loss backward of a forward that ran with `loss`."""
         nl = len(self.F) - 1
+        self.split_bwd = os.environ.get("MMSEG_SPLIT_DCAT", "1") != "0"
         dh = self.dout[0]
         if gout is not None:
             hx = self.blocks[nl - 1].out_stats()[0] if self.defer_head else self.dout[0]
@@ -104,9 +120,11 @@ class _Decoder:
             self.head.bwd(self.dout[0], dlogits, dh, accumulate)
         for j in reversed(range(nl)):
             l = nl - 1 - j
-            self.blocks[j].bwd(self.cat[l], DySpec(p1=dh), self.cat[l], accumulate)   # dcat aliases cat
+            dcat = self.dsplit[l] if self.split_bwd else self.cat[l]                  # aliases cat
+            self.blocks[j].bwd(self.cat[l], DySpec(p1=dh), dcat, accumulate)
             x_up = bottom if j == 0 else self.dout[l + 1]
-            self.ups[j].bwd(x_up, self.cat[l].slot(0, self.F[l]), x_up, accumulate)   # dd aliases x_up
+            dup = self.dsplit[l][0] if self.split_bwd else self.cat[l].slot(0, self.F[l])
+            self.ups[j].bwd(x_up, dup, x_up, accumulate)   # dd aliases x_up
             dh = x_up
         return bottom
 
@@ -178,7 +196,7 @@ class UNetProgram:
         dy = DySpec(p1=dbottom)
         for l in range(self.L - 1, 0, -1):
             self.enc[l - 1].bwd(self.pooled[l], dy, self.pooled[l], accumulate)   # dp aliases pooled
-            dy = DySpec(p1=self.dec.skip_slot(l - 1), pool_dy=self.pooled[l], pool_idx=self.idx[l])
+            dy = DySpec(p1=self.dec.dskip(l - 1), pool_dy=self.pooled[l], pool_idx=self.idx[l])
         self.init.bwd(self.xin_v, dy, None, accumulate)
 
 
@@ -251,6 +269,10 @@ class DualEncoderProgram:
 
     def fused_out(self, l: int) -> Act:
         return self.dec.skip_slot(l) if l < self.L - 1 else self.bottom
+
+    def dfused(self, l: int) -> Act:
+        """d(fused_l) after the decoder backward."""
+        return self.dec.dskip(l) if l < self.L - 1 else self.bottom
 
     def _fuse_fwd(self, l: int):
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
@@ -380,7 +402,7 @@ class DualEncoderProgram:
             self._encoders_bwd_streams(accumulate)
             return
         for l in range(self.L - 1, -1, -1):
-            dfused = self.fused_out(l)          # holds d(fused_l) now
+            dfused = self.dfused(l)
             N, V, C = dfused.N, dfused.V, dfused.C
             base: List[DySpec] = []
             if self.fusion == "concat":
@@ -427,7 +449,7 @@ class DualEncoderProgram:
 
         def levels(m, hi, lo):
             for l in range(hi - 1, lo - 1, -1):
-                dy = DySpec(p1=self.fused_out(l), scale1=sc)
+                dy = DySpec(p1=self.dfused(l), scale1=sc)
                 if l < self.L - 1:
                     dy.pool_dy = self.pooled[m][l + 1]
                     dy.pool_idx = self.idx[m][l + 1]

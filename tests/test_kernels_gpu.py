@@ -495,3 +495,38 @@ def test_conv3_channel_padded(dev, dtype, cin, cout, shape):
     (ref * _q(dy, dtype)).sum().backward()
     assert rel(from_ndhwc(dxa.buf, N, cin, D, H, W, ld=cip), xd.grad) < TOL[dtype]
     assert rel(flat.grad(conv.weight), wd.grad) < GTOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("knobs,cin,cout,shape", [
+    ({}, 64, 32, (2, 8, 8, 16)),                                    # dgrad Ncols 64 (brick2 / brick3)
+    ({"MMSEG_BRICK2_MINBLK": "0"}, 64, 32, (2, 8, 8, 16)),          # BN64 brick2
+    ({}, 128, 64, (2, 4, 8, 8)),                                    # two 64-column tiles
+    ({}, 256, 128, (2, 6, 6, 6)),                                   # runtime brick + split-K reduce
+    ({}, 64, 32, (1, 3, 5, 7)),                                     # generic GEMM
+])
+def test_conv3_dgrad_split_output(dev, dtype, knobs, cin, cout, shape, monkeypatch):
+    """mmseg_conv_gemm_split (the decoder's first-conv data gradient writing d(upsampled) and d(skip) as two
+    dense tensors) gives bitwise the columns of the single [voxel][Cin] output, for every kernel family."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    torch.manual_seed(cin + cout)
+    conv = nn.Conv3d(cin, cout, 3, padding=1).to(dev)
+    rt = Runtime(dev, dtype)
+    flat = FlatParams(list(conv.parameters()))
+    layer = Conv3(rt, conv, flat)
+    layer.pack()
+    N, D, H, W = shape
+    xa = _act(torch.randn(N, cin, D, H, W, device=dev), dtype)
+    dya = _act(torch.randn(N, cout, D, H, W, device=dev), dtype)
+    whole = rt.act(N, D, H, W, cin)
+    layer.bwd(xa, dya, whole, accumulate=False)
+    h = cin // 2
+    buf = torch.zeros(2 * N * D * H * W * h, dtype=rt.dtype, device=dev)
+    lo = Act(buf, 0, h, h, N, D, H, W)
+    hi = Act(buf, N * D * H * W * h, h, h, N, D, H, W)
+    layer.bwd(xa, dya, (lo, hi), accumulate=False)
+    torch.cuda.synchronize()
+    ref = whole.buf[: N * D * H * W * cin].view(-1, cin)
+    assert torch.equal(buf[: N * D * H * W * h].view(-1, h), ref[:, :h])
+    assert torch.equal(buf[N * D * H * W * h:].view(-1, h), ref[:, h:])
