@@ -155,6 +155,12 @@ int mmseg_conv3_wgrad_norm_ok(long long V, int Co, int Cip, int Ci, int cpg_shif
 int mmseg_conv3_wgrad_norm(const void* dy, int lddy, const void* x, int ldx, const float* nmean, const float* nrstd,
                            float* grad, float* bias_grad, int Co, int Cip, int Ci, int cpg_shift, long long V, int D,
                            int H, int W, float* ws, long long ws_floats, int accumulate, int dtype, void* stream);
+/* mmseg_conv3_wgrad (nmean / nrstd: optional deferred norm, as mmseg_conv3_wgrad_norm) in phases: bit 1 runs
+ * the weight-gradient kernel, bit 2 the split reduce (3 = both), so the kernel can be timed alone. */
+int mmseg_conv3_wgrad_ex(const void* dy, int lddy, const void* x, int ldx, const float* nmean, const float* nrstd,
+                         float* grad, float* bias_grad, int Co, int Cip, int Ci, int cpg_shift, long long V, int D,
+                         int H, int W, float* ws, long long ws_floats, int accumulate, int phase, int dtype,
+                         void* stream);
 /* Bias gradient out[c] (+)= sum_v dy[v][c] (convolution_backward grad_bias). */
 int mmseg_colsum(const void* dy, int ld, int C, long long V, float* part, int nblk, float* out, int accumulate,
                  int dtype, void* stream);

@@ -3975,7 +3975,7 @@ long long mmseg_conv3_wgrad_ws_floats(long long V, int Co, int Cip, int Ci, int 
 
 int conv3_wgrad_impl(const void* dy, int lddy, const void* x, int ldx, const float* nmean, const float* nrstd,
                      float* grad, float* bias_grad, int Co, int Cip, int Ci, int cpg_shift, long long V, int D, int H,
-                     int W, float* ws, long long ws_floats, int accumulate, int dtype, void* stream);
+                     int W, float* ws, long long ws_floats, int accumulate, int dtype, void* stream, int phase = 3);
 
 int mmseg_conv3_wgrad(const void* dy, int lddy, const void* x, int ldx, float* grad, float* bias_grad, int Co, int Cip,
                       int Ci, int cpg_shift, long long V, int D, int H, int W, float* ws, long long ws_floats,
@@ -4003,9 +4003,22 @@ int mmseg_conv3_wgrad_norm(const void* dy, int lddy, const void* x, int ldx, con
                           ws_floats, accumulate, dtype, stream);
 }
 
+// mmseg_conv3_wgrad in two phases (bit 1: the weight-gradient kernel, bit 2: the split reduce), so a caller can
+// time the kernel alone; nmean / nrstd optional (deferred norm of x, see mmseg_conv3_wgrad_norm).
+int mmseg_conv3_wgrad_ex(const void* dy, int lddy, const void* x, int ldx, const float* nmean, const float* nrstd,
+                         float* grad, float* bias_grad, int Co, int Cip, int Ci, int cpg_shift, long long V, int D,
+                         int H, int W, float* ws, long long ws_floats, int accumulate, int phase, int dtype,
+                         void* stream) {
+  MMSEG_REQUIRE(phase >= 1 && phase <= 3, "conv3_wgrad_ex: phase %d must be 1, 2 or 3", phase);
+  MMSEG_REQUIRE(!nmean || (nrstd && mmseg_conv3_wgrad_norm_ok(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype)),
+                "conv3_wgrad_ex: unsupported shape for the deferred norm (mmseg_conv3_wgrad_norm_ok)");
+  return conv3_wgrad_impl(dy, lddy, x, ldx, nmean, nrstd, grad, bias_grad, Co, Cip, Ci, cpg_shift, V, D, H, W, ws,
+                          ws_floats, accumulate, dtype, stream, phase);
+}
+
 int conv3_wgrad_impl(const void* dy, int lddy, const void* x, int ldx, const float* nmean, const float* nrstd,
                      float* grad, float* bias_grad, int Co, int Cip, int Ci, int cpg_shift, long long V, int D, int H,
-                     int W, float* ws, long long ws_floats, int accumulate, int dtype, void* stream) {
+                     int W, float* ws, long long ws_floats, int accumulate, int dtype, void* stream, int phase) {
   MMSEG_REQUIRE(Co % 8 == 0 && Cip % 8 == 0 && Ci <= Cip && (8 << cpg_shift) == Cip,
                 "conv3_wgrad: Co=%d, Cip=%d must be multiples of 8, Ci=%d <= Cip, Cip = 8 << cpg_shift", Co, Cip, Ci);
   const Conv3WgradPlan p = plan_conv3_wgrad(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype, ws_floats);
@@ -4020,8 +4033,11 @@ int conv3_wgrad_impl(const void* dy, int lddy, const void* x, int ldx, const flo
               knob("MMSEG_WGRAD_SWIZZLE", 0), p.kind, p.direct ? grad : nullptr, p.direct ? bias_grad : nullptr,
               accumulate, wgrad_kchunks(Cip, Ci), nmean, nrstd};
   hipStream_t s = (hipStream_t)stream;
-  const int rc = dtype == MMSEG_BF16 ? launch_wgrad<bf16_t, MODE_CONV3>(g, s) : launch_wgrad<float, MODE_CONV3>(g, s);
-  if (rc || p.direct) return rc;
+  if (phase & 1) {
+    const int rc = dtype == MMSEG_BF16 ? launch_wgrad<bf16_t, MODE_CONV3>(g, s) : launch_wgrad<float, MODE_CONV3>(g, s);
+    if (rc) return rc;
+  }
+  if (p.direct || !(phase & 2)) return 0;
   WReduceArgs r{part, grad, bpart, bias_grad, Co, ncols, p.ksplit, Cip, Ci, 27, accumulate, p.kind >= 2 ? 1 : 0};
   return launch_wgrad_reduce(r, stream);
 }

@@ -269,19 +269,17 @@ class Conv3:
                                             x.ld, code)
         ws = self.rt.ws(wsf) if wsf > 0 else None
         wgrad = self.flat.grad(self.conv.weight)
+        nm, nr = (ptr(norm[0]), ptr(norm[1])) if norm is not None else (None, None)
+        args = (dy.ptr, dy.ld, x.ptr, x.ld, nm, nr, ptr(self.wg_stage) if self.wg_stage is not None else ptr(wgrad),
+                ptr(self.flat.grad(self.conv.bias)) if self.conv.bias is not None else None, rows, self.Cip, self.Ci,
+                self.cpg_shift, V, x.D, x.H, x.W, ptr(ws), wsf, int(accumulate) if self.wg_stage is None else 0)
+        # the kernel and its split reduce are timed separately (the roofline family is the kernel alone, as in
+        # the rocprofv3 trace)
         with TIMER.region(_gemm_name(self.rt, 0, "conv3"), flops=2.0 * V * self.Co * 27 * self.Ci,
                           nbytes=_io_bytes(self.rt, V, self.Cip, self.Co, 27 * self.Cip * self.Co, 4)):
-            if norm is not None:
-                L.mmseg_conv3_wgrad_norm(dy.ptr, dy.ld, x.ptr, x.ld, ptr(norm[0]), ptr(norm[1]), ptr(wgrad),
-                                         ptr(self.flat.grad(self.conv.bias)) if self.conv.bias is not None else None,
-                                         rows, self.Cip, self.Ci, self.cpg_shift, V, x.D, x.H, x.W, ptr(ws), wsf,
-                                         int(accumulate), code, s)
-            else:
-                L.mmseg_conv3_wgrad(dy.ptr, dy.ld, x.ptr, x.ld,
-                                    ptr(self.wg_stage) if self.wg_stage is not None else ptr(wgrad),
-                                    ptr(self.flat.grad(self.conv.bias)) if self.conv.bias is not None else None, rows,
-                                    self.Cip, self.Ci, self.cpg_shift, V, x.D, x.H, x.W, ptr(ws), wsf,
-                                    int(accumulate) if self.wg_stage is None else 0, code, s)
+            L.mmseg_conv3_wgrad_ex(*args, 1, code, s)
+        with TIMER.region("wgrad_reduce_kernel"):
+            L.mmseg_conv3_wgrad_ex(*args, 2, code, s)
         if self.wg_stage is not None:     # rows [0, Co) of the staging are the gradient's storage order
             n = wgrad.numel()
             if accumulate:
