@@ -2494,6 +2494,40 @@ __device__ __forceinline__ void wgrad_store_chmajor(const f32x4 (&acc)[4][MT][2]
   }
 }
 
+// wgrad_store_chmajor for the balanced layout of wgrad_brick2_kernel<..., BAL>: accumulator slot uu of a wave
+// holds unit u_begin + uu = (tap, j) = ((u) >> 1, (u) & 1).
+template <int MT, int NU>
+__device__ __forceinline__ void wgrad_store_units(const f32x4 (&acc)[NU][MT], int u_begin, int u_cnt, float* L,
+                                                  const WgradArgs& g, int ks, int row0, int c0) {
+  const int tid = threadIdx.x, lane = tid & 63, g4 = lane >> 4, i16 = lane & 15;
+  const bool direct = g.grad != nullptr && g.ksplit == 1;
+  float* base = direct ? g.grad : g.part + (long long)ks * g.Ca * g.Ncols;
+  const bool accum = direct && g.accumulate;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    __syncthreads();
+#pragma unroll
+    for (int uu = 0; uu < NU; ++uu) {
+      if (uu >= u_cnt) continue;
+      const int u = u_begin + uu, tap = u >> 1, j = u & 1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) L[(g4 * 4 + r) * WEP_P + (j * 16 + i16) * 27 + tap] = acc[uu][i][r];
+    }
+    __syncthreads();
+    for (int e = tid; e < 16 * 216; e += 512) {
+      const int rr = e / 216, q = e - rr * 216;
+      const float4 v = *reinterpret_cast<const float4*>(L + rr * WEP_P + q * 4);
+      float4* d = reinterpret_cast<float4*>(base + (long long)(row0 + i * 16 + rr) * g.Ncols + c0 * 27 + q * 4);
+      if (accum) {
+        const float4 o = *d;
+        *d = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+      } else {
+        *d = v;
+      }
+    }
+  }
+}
+
 // Bias-gradient epilogue of the brick wgrad kernels: per-thread column sums of the staged dy rows
 // (8 channels of group tid % CG), reduced over the 512 threads in fixed order.
 template <int CG>
@@ -2529,7 +2563,11 @@ __device__ __forceinline__ void wgrad_store_bias(const float (&bsum)[8], float* 
 // with row pitches of 24 or 40 dwords (== 8 mod 16) 8 consecutive rows cover the 64 banks exactly once.
 // V = 2: the previous K order (x = j&3 + 4*(j>>2), y = g4) with 20-dword pitches, 2-way conflicted
 // (SQ_LDS_BANK_CONFLICT = half the LDS-active cycles at 96^3).
-template <typename T, int MT, int V>
+// BAL (balanced): the 27 taps x 2 column halves = 54 (tap, j) units are dealt 7,7,7,7,7,7,6,6 over the 8 waves
+// instead of 27 taps dealt 4,4,4,3,3,3,3,3 (the block waits for its 4-tap waves: 84 % of the MFMA issue used).
+// NORM: x holds a pre-norm activation (g.nmean / g.nrstd, mmseg_conv3_wgrad_norm); a separate instantiation so
+// the plain kernel does not carry the statistics' registers (256 VGPRs + spills for CO64 otherwise)
+template <typename T, int MT, int V, bool BAL = false, bool NORM = false>
 __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2_kernel(WgradArgs g) {
   constexpr int EP = 16 / sizeof(T);
   constexpr int CO = MT * 16, CG = CO / 8;       // output channels per block, 8-channel groups
@@ -2558,20 +2596,32 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
   const int t_begin = wave < 3 ? 4 * wave : 12 + 3 * (wave - 3);
   const int t_cnt = wave < 3 ? 4 : 3;
 
-  f32x4 acc[4][MT][2];
+  f32x4 acc[BAL ? 1 : 4][MT][2];
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
+  for (int t = 0; t < (BAL ? 1 : 4); ++t)
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[t][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  constexpr int NU = BAL ? 7 : 1;
+  const int u_begin = wave < 6 ? 7 * wave : 42 + 6 * (wave - 6), u_cnt = wave < 6 ? 7 : 6;
+  f32x4 accu[NU][MT];
+  int uoff[NU];   // per unit: halo offset of its tap (voxels) and column half (elements)
+#pragma unroll
+  for (int uu = 0; uu < NU; ++uu) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i) accu[uu][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int u = u_begin + uu, tap = u >> 1, jh = u & 1;
+    const int kz = tap / 9, ky = (tap / 3) % 3, kx = tap % 3;
+    uoff[uu] = ((kz * HLO_Y + ky) * HLO_X + kx) * XP + jh * 16;
+  }
   float bsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
   V8<T> dr[D_PER], xr[X_PER];
   uint32_t xin = 0;    // bit k: xr[k] is an in-volume voxel (padding stays 0 under the deferred norm)
   int xn = 0;          // sample of the staged brick
   int norm_n = -1;     // sample whose deferred-norm statistics nmu / nrs hold
-  float nmu[8], nrs[8];
+  float nmu[NORM ? 8 : 1], nrs[NORM ? 8 : 1];
   auto load = [&](long long b) {
     const int bx = (int)(b % bx_n);
     long long q = b / bx_n;
@@ -2597,7 +2647,7 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
         const int z = z0 - 1 + hz, y = y0 - 1 + hy, x = x0 - 1 + hx;
         if ((unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W) {
           xr[k].load(X + (nbase + z * HW + (long long)y * g.W + x) * g.ldb + c0 + cg * 8);
-          xin |= 1u << k;
+          if constexpr (NORM) xin |= 1u << k;
         } else {
           xr[k].zero();
         }
@@ -2616,7 +2666,7 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
         for (int j = 0; j < 8; ++j) bsum[j] += dr[k].get(j);
       }
     }
-    if (g.nmean) {   // deferred InstanceNorm + ReLU of x: channels c0 + 8 (tid & 3) .. of sample xn
+    if constexpr (NORM) {   // deferred InstanceNorm + ReLU of x: channels c0 + 8 (tid & 3) .. of sample xn
       if (xn != norm_n) {   // (the statistics change only when the brick range crosses into the next sample)
         norm_n = xn;
         const int cb = xn * cin + c0 + (tid & 3) * 8;
@@ -2662,6 +2712,20 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
         }
         const int hlo = ((v_lo >> 5) * HLO_Y + ((v_lo >> 3) & 3)) * HLO_X + (v_lo & 7);
         const int hhi = ((v_hi >> 5) * HLO_Y + ((v_hi >> 3) & 3)) * HLO_X + (v_hi & 7);
+        if constexpr (BAL) {
+#pragma unroll
+          for (int uu = 0; uu < NU; ++uu) {
+            if (uu < u_cnt) {
+              const bf16_t* pl = (const bf16_t*)Xl + hlo * XP + uoff[uu] + 4 * p4;
+              const bf16_t* ph = (const bf16_t*)Xl + hhi * XP + uoff[uu] + 4 * p4;
+              const bf16x8 bfr = tr_frag(pl, ph);
+#pragma unroll
+              for (int i = 0; i < MT; ++i)
+                accu[uu][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, accu[uu][i], 0, 0, 0);
+            }
+          }
+          continue;
+        }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           if (t < t_cnt) {
@@ -2711,7 +2775,10 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
 
   static_assert(sizeof(lds) >= 16 * WEP_P * sizeof(float) && sizeof(lds) >= 512 * 8 * sizeof(float),
                 "epilogue staging must fit the stage buffers");
-  wgrad_store_chmajor<MT>(acc, t_begin, t_cnt, reinterpret_cast<float*>(lds), g, ks, row0, c0);
+  if constexpr (BAL)
+    wgrad_store_units<MT, NU>(accu, u_begin, u_cnt, reinterpret_cast<float*>(lds), g, ks, row0, c0);
+  else
+    wgrad_store_chmajor<MT>(acc, t_begin, t_cnt, reinterpret_cast<float*>(lds), g, ks, row0, c0);
   if (do_bias) wgrad_store_bias<CG>(bsum, reinterpret_cast<float*>(lds), g, ks, row0);
 }
 
@@ -3562,14 +3629,24 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
       if (g.Ca % 64 == 0) {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 64) * g.ksplit);
         mmseg::note_kernel(v3 ? "wgrad_brick2_kernel<CO64,V3>" : "wgrad_brick2_kernel<CO64>");
-        if (v3)
+        if (v3 && g.nmean)
+          hipLaunchKernelGGL((wgrad_brick2_kernel<T, 4, 3, false, true>), grid, dim3(512), 0, s, g);
+        else if (v3 && knob("MMSEG_WGRAD_BAL", 0))
+          hipLaunchKernelGGL((wgrad_brick2_kernel<T, 4, 3, true>), grid, dim3(512), 0, s, g);
+        else if (v3)
           hipLaunchKernelGGL((wgrad_brick2_kernel<T, 4, 3>), grid, dim3(512), 0, s, g);
         else
           hipLaunchKernelGGL((wgrad_brick2_kernel<T, 4, 2>), grid, dim3(512), 0, s, g);
       } else {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 32) * g.ksplit);
         mmseg::note_kernel(v3 ? "wgrad_brick2_kernel<CO32,V3>" : "wgrad_brick2_kernel<CO32>");
-        if (v3)
+        if (v3 && g.nmean && knob("MMSEG_WGRAD_BAL", 0))
+          hipLaunchKernelGGL((wgrad_brick2_kernel<T, 2, 3, true, true>), grid, dim3(512), 0, s, g);
+        else if (v3 && g.nmean)
+          hipLaunchKernelGGL((wgrad_brick2_kernel<T, 2, 3, false, true>), grid, dim3(512), 0, s, g);
+        else if (v3 && knob("MMSEG_WGRAD_BAL", 0))
+          hipLaunchKernelGGL((wgrad_brick2_kernel<T, 2, 3, true>), grid, dim3(512), 0, s, g);
+        else if (v3)
           hipLaunchKernelGGL((wgrad_brick2_kernel<T, 2, 3>), grid, dim3(512), 0, s, g);
         else
           hipLaunchKernelGGL((wgrad_brick2_kernel<T, 2, 2>), grid, dim3(512), 0, s, g);
