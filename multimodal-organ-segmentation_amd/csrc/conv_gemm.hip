@@ -26,6 +26,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <vector>
 
@@ -2029,6 +2030,7 @@ struct WgradArgs {
   // activation, staged as relu((x - nmean[n][c]) * nrstd[n][c]) rounded to T
   const float* nmean;
   const float* nrstd;
+  int dbg;   // wgrad_brick2 timing probe (MMSEG_WGRAD_DBG): 1 = no global loads after the first brick, 2 = no MFMA
 };
 
 __host__ __device__ __forceinline__ int wgrad_nchunk(int cpg_shift, int kchunks) {
@@ -2298,11 +2300,12 @@ __global__ __launch_bounds__(256) void wgrad_brick_kernel(WgradArgs g) {
 
   V8<T> dr[D_PER], xr[X_PER];
   auto brick_origin = [&](long long b, long long& nbase, int& z0, int& y0, int& x0) {
-    const int bx = (int)(b % bx_n);
-    long long q = b / bx_n;
-    const int by = (int)(q % by_n);
+    int q = (int)b;   // brick index < V / 128 < 2^31 (mmseg_wgrad): 32-bit division
+    const int bx = q % bx_n;
+    q /= bx_n;
+    const int by = q % by_n;
     q /= by_n;
-    const int bz = (int)(q % bz_n);
+    const int bz = q % bz_n;
     const long long n = q / bz_n;
     nbase = n * g.D * HW;
     z0 = bz * BRK_Z;
@@ -2460,76 +2463,48 @@ __global__ __launch_bounds__(256) void wgrad_brick_kernel(WgradArgs g) {
 // split partial part[ks][Ca][Ncols] or, for a single split, straight into the gradient (= or +=).
 // LDS pitch 868 floats: a ds_write_b32 lane group (two co-rows x 16 ci, ci stride 27) hits 32 distinct banks.
 constexpr int WEP_P = 868;
-template <int MT>
+// RP rows of the 16-row MFMA tile per LDS pass (16: 55.5 KB of staging; 8: half that, two passes)
+template <int MT, int RP = 16>
 __device__ __forceinline__ void wgrad_store_chmajor(const f32x4 (&acc)[4][MT][2], int t_begin, int t_cnt, float* L,
                                                     const WgradArgs& g, int ks, int row0, int c0) {
   const int tid = threadIdx.x, lane = tid & 63, g4 = lane >> 4, i16 = lane & 15;
   const bool direct = g.grad != nullptr && g.ksplit == 1;
   float* base = direct ? g.grad : g.part + (long long)ks * g.Ca * g.Ncols;
   const bool accum = direct && g.accumulate;
+  constexpr int GP = RP / 4;   // lane groups per pass
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
-    __syncthreads();
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if (t >= t_cnt) continue;
-      const int tap = t_begin + t;
+    for (int hh = 0; hh < 16 / RP; ++hh) {
+      __syncthreads();
+      if (g4 / GP == hh) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+        for (int t = 0; t < 4; ++t) {
+          if (t >= t_cnt) continue;
+          const int tap = t_begin + t;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) L[(g4 * 4 + r) * WEP_P + (j * 16 + i16) * 27 + tap] = acc[t][i][j][r];
-    }
-    __syncthreads();
-    for (int e = tid; e < 16 * 216; e += 512) {
-      const int rr = e / 216, q = e - rr * 216;
-      const float4 v = *reinterpret_cast<const float4*>(L + rr * WEP_P + q * 4);
-      float4* d = reinterpret_cast<float4*>(base + (long long)(row0 + i * 16 + rr) * g.Ncols + c0 * 27 + q * 4);
-      if (accum) {
-        const float4 o = *d;
-        *d = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
-      } else {
-        *d = v;
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) L[((g4 % GP) * 4 + r) * WEP_P + (j * 16 + i16) * 27 + tap] = acc[t][i][j][r];
+        }
+      }
+      __syncthreads();
+      for (int e = tid; e < RP * 216; e += 512) {
+        const int rr = e / 216, q = e - rr * 216;
+        const float4 v = *reinterpret_cast<const float4*>(L + rr * WEP_P + q * 4);
+        float4* d = reinterpret_cast<float4*>(base + (long long)(row0 + i * 16 + hh * RP + rr) * g.Ncols + c0 * 27 +
+                                              q * 4);
+        if (accum) {
+          const float4 o = *d;
+          *d = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+        } else {
+          *d = v;
+        }
       }
     }
   }
 }
 
-// wgrad_store_chmajor for the balanced layout of wgrad_brick2_kernel<..., BAL>: accumulator slot uu of a wave
-// holds unit u_begin + uu = (tap, j) = ((u) >> 1, (u) & 1).
-template <int MT, int NU>
-__device__ __forceinline__ void wgrad_store_units(const f32x4 (&acc)[NU][MT], int u_begin, int u_cnt, float* L,
-                                                  const WgradArgs& g, int ks, int row0, int c0) {
-  const int tid = threadIdx.x, lane = tid & 63, g4 = lane >> 4, i16 = lane & 15;
-  const bool direct = g.grad != nullptr && g.ksplit == 1;
-  float* base = direct ? g.grad : g.part + (long long)ks * g.Ca * g.Ncols;
-  const bool accum = direct && g.accumulate;
-#pragma unroll
-  for (int i = 0; i < MT; ++i) {
-    __syncthreads();
-#pragma unroll
-    for (int uu = 0; uu < NU; ++uu) {
-      if (uu >= u_cnt) continue;
-      const int u = u_begin + uu, tap = u >> 1, j = u & 1;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) L[(g4 * 4 + r) * WEP_P + (j * 16 + i16) * 27 + tap] = acc[uu][i][r];
-    }
-    __syncthreads();
-    for (int e = tid; e < 16 * 216; e += 512) {
-      const int rr = e / 216, q = e - rr * 216;
-      const float4 v = *reinterpret_cast<const float4*>(L + rr * WEP_P + q * 4);
-      float4* d = reinterpret_cast<float4*>(base + (long long)(row0 + i * 16 + rr) * g.Ncols + c0 * 27 + q * 4);
-      if (accum) {
-        const float4 o = *d;
-        *d = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
-      } else {
-        *d = v;
-      }
-    }
-  }
-}
-
-// Bias-gradient epilogue of the brick wgrad kernels: per-thread column sums of the staged dy rows
-// (8 channels of group tid % CG), reduced over the 512 threads in fixed order.
 template <int CG>
 __device__ __forceinline__ void wgrad_store_bias(const float (&bsum)[8], float* red, const WgradArgs& g, int ks,
                                                  int row0) {
@@ -2563,11 +2538,9 @@ __device__ __forceinline__ void wgrad_store_bias(const float (&bsum)[8], float* 
 // with row pitches of 24 or 40 dwords (== 8 mod 16) 8 consecutive rows cover the 64 banks exactly once.
 // V = 2: the previous K order (x = j&3 + 4*(j>>2), y = g4) with 20-dword pitches, 2-way conflicted
 // (SQ_LDS_BANK_CONFLICT = half the LDS-active cycles at 96^3).
-// BAL (balanced): the 27 taps x 2 column halves = 54 (tap, j) units are dealt 7,7,7,7,7,7,6,6 over the 8 waves
-// instead of 27 taps dealt 4,4,4,3,3,3,3,3 (the block waits for its 4-tap waves: 84 % of the MFMA issue used).
 // NORM: x holds a pre-norm activation (g.nmean / g.nrstd, mmseg_conv3_wgrad_norm); a separate instantiation so
 // the plain kernel does not carry the statistics' registers (256 VGPRs + spills for CO64 otherwise)
-template <typename T, int MT, int V, bool BAL = false, bool NORM = false>
+template <typename T, int MT, int V, bool NORM = false>
 __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2_kernel(WgradArgs g) {
   constexpr int EP = 16 / sizeof(T);
   constexpr int CO = MT * 16, CG = CO / 8;       // output channels per block, 8-channel groups
@@ -2596,25 +2569,13 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
   const int t_begin = wave < 3 ? 4 * wave : 12 + 3 * (wave - 3);
   const int t_cnt = wave < 3 ? 4 : 3;
 
-  f32x4 acc[BAL ? 1 : 4][MT][2];
+  f32x4 acc[4][MT][2];
 #pragma unroll
-  for (int t = 0; t < (BAL ? 1 : 4); ++t)
+  for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[t][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  constexpr int NU = BAL ? 7 : 1;
-  const int u_begin = wave < 6 ? 7 * wave : 42 + 6 * (wave - 6), u_cnt = wave < 6 ? 7 : 6;
-  f32x4 accu[NU][MT];
-  int uoff[NU];   // per unit: halo offset of its tap (voxels) and column half (elements)
-#pragma unroll
-  for (int uu = 0; uu < NU; ++uu) {
-#pragma unroll
-    for (int i = 0; i < MT; ++i) accu[uu][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const int u = u_begin + uu, tap = u >> 1, jh = u & 1;
-    const int kz = tap / 9, ky = (tap / 3) % 3, kx = tap % 3;
-    uoff[uu] = ((kz * HLO_Y + ky) * HLO_X + kx) * XP + jh * 16;
-  }
   float bsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
   V8<T> dr[D_PER], xr[X_PER];
@@ -2622,13 +2583,14 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
   int xn = 0;          // sample of the staged brick
   int norm_n = -1;     // sample whose deferred-norm statistics nmu / nrs hold
   float nmu[NORM ? 8 : 1], nrs[NORM ? 8 : 1];
-  auto load = [&](long long b) {
-    const int bx = (int)(b % bx_n);
-    long long q = b / bx_n;
-    const int by = (int)(q % by_n);
+  auto load_into = [&](long long b, auto& dr, auto& xr, uint32_t& xin, int& xn) {
+    int q = (int)b;   // brick index < V / 128 < 2^31 (mmseg_wgrad): 32-bit division
+    const int bx = q % bx_n;
+    q /= bx_n;
+    const int by = q % by_n;
     q /= by_n;
-    const int bz = (int)(q % bz_n);
-    xn = (int)(q / bz_n);
+    const int bz = q % bz_n;
+    xn = q / bz_n;
     const long long nbase = (long long)xn * g.D * HW;
     const int z0 = bz * BRK_Z, y0 = by * BRK_Y, x0 = bx * BRK_X;
     xin = 0;
@@ -2654,7 +2616,7 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
       }
     }
   };
-  auto store = [&](int buf) {
+  auto store_from = [&](int buf, auto& dr, auto& xr, uint32_t xin, int xn) {
     T* Dl = lds + buf * (DS + XS);
     T* Xl = Dl + DS;
 #pragma unroll
@@ -2688,15 +2650,7 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
   };
 
   const int g4 = lane >> 4, i16 = lane & 15, q = i16 >> 2, p4 = i16 & 3;
-  int buf = 0;
-  if (b_begin < b_end) {
-    load(b_begin);
-    store(0);
-  }
-  __syncthreads();
-  for (long long b = b_begin; b < b_end; ++b) {
-    const bool more = b + 1 < b_end;
-    if (more) load(b + 1);
+  auto compute = [&](int buf) {
     const T* Dl = lds + buf * (DS + XS);
     const T* Xl = Dl + DS;
     if constexpr (sizeof(T) == 2) {
@@ -2712,20 +2666,6 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
         }
         const int hlo = ((v_lo >> 5) * HLO_Y + ((v_lo >> 3) & 3)) * HLO_X + (v_lo & 7);
         const int hhi = ((v_hi >> 5) * HLO_Y + ((v_hi >> 3) & 3)) * HLO_X + (v_hi & 7);
-        if constexpr (BAL) {
-#pragma unroll
-          for (int uu = 0; uu < NU; ++uu) {
-            if (uu < u_cnt) {
-              const bf16_t* pl = (const bf16_t*)Xl + hlo * XP + uoff[uu] + 4 * p4;
-              const bf16_t* ph = (const bf16_t*)Xl + hhi * XP + uoff[uu] + 4 * p4;
-              const bf16x8 bfr = tr_frag(pl, ph);
-#pragma unroll
-              for (int i = 0; i < MT; ++i)
-                accu[uu][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, accu[uu][i], 0, 0, 0);
-            }
-          }
-          continue;
-        }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           if (t < t_cnt) {
@@ -2768,18 +2708,307 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
         }
       }
     }
-    if (more) store(buf ^ 1);
+  };
+
+  {
+    int buf = 0;
+    if (b_begin < b_end) {
+      load_into(b_begin, dr, xr, xin, xn);
+      store_from(0, dr, xr, xin, xn);
+    }
     __syncthreads();
-    buf ^= 1;
+    for (long long b = b_begin; b < b_end; ++b) {
+      const bool more = b + 1 < b_end;
+      if (more && g.dbg != 1) load_into(b + 1, dr, xr, xin, xn);
+      if (g.dbg != 2) compute(buf);
+      if (more) store_from(buf ^ 1, dr, xr, xin, xn);
+      __syncthreads();
+      buf ^= 1;
+    }
   }
 
   static_assert(sizeof(lds) >= 16 * WEP_P * sizeof(float) && sizeof(lds) >= 512 * 8 * sizeof(float),
                 "epilogue staging must fit the stage buffers");
-  if constexpr (BAL)
-    wgrad_store_units<MT, NU>(accu, u_begin, u_cnt, reinterpret_cast<float*>(lds), g, ks, row0, c0);
-  else
-    wgrad_store_chmajor<MT>(acc, t_begin, t_cnt, reinterpret_cast<float*>(lds), g, ks, row0, c0);
+  wgrad_store_chmajor<MT>(acc, t_begin, t_cnt, reinterpret_cast<float*>(lds), g, ks, row0, c0);
   if (do_bias) wgrad_store_bias<CG>(bsum, reinterpret_cast<float*>(lds), g, ks, row0);
+}
+
+// ------------------------------------------ brick wgrad, LDS-DMA staging (3^3, bf16)
+// wgrad_brick2_kernel<bf16, MT, 3> with the stage images filled by buffer_load ... lds (no staging registers,
+// no ds_write) into THREE stage buffers: brick b + 2 is in flight while brick b is multiplied, so a load has two
+// brick periods to land instead of one (the register-staged kernel spends about a third of its time waiting
+// on its one-brick-ahead loads: 136 us with, 105 us without loads at 96^3 32->32).  The rows are unpadded and
+// XOR-swizzled at 32-byte granules instead (the DMA writes 64 contiguous 16-B chunks per wave-instruction; the
+// lane picks the global chunk that belongs at its LDS position), which keeps the transposed fragment reads
+// conflict-free:
+//   halo row (hz, hy, hx), 64 B:   granule j of channel half j lives at j ^ ((hx >> 2) & 1)
+//   dy row v, 64 B (32 co):        granule i at i ^ ((v >> 2) & 1)
+//   dy row v, 128 B (64 co):       granule i at i ^ ((v >> 1) & 3)
+// (8 consecutive halo x positions, or 8 aligned dy rows, then cover the 64 banks once).  The bias gradient
+// is one more MFMA chain against a ones fragment in wave 7's free tap slot.  NORM: the deferred InstanceNorm +
+// ReLU is applied in place to the landed halo (each thread its fixed channel group), one extra barrier.
+constexpr uint32_t WD_OOB = 0x80000000u;   // buffer offset past every tensor: the DMA writes zeros
+typedef int wd_rsrc_t __attribute__((ext_vector_type(4)));
+// raw buffer descriptor (base, stride 0, num_records bytes) in SGPRs
+__device__ __forceinline__ wd_rsrc_t wd_rsrc(const void* p, uint32_t bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  wd_rsrc_t r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32) & 0xffff);
+  r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
+  r[3] = 0x00020000;
+  return r;
+}
+// one wave-instruction of 16-B LDS-DMA: lane l's chunk lands at LDS byte lds + 16 l.  Issued through inline asm
+// so the compiler's waitcnt tracking does not see it: it would otherwise wait for every pending LDS-DMA before
+// any LDS read (it cannot tell the stage buffers apart), which serialises the prefetch.  The kernel waits for
+// these loads itself (s_waitcnt vmcnt).
+__device__ __forceinline__ void wd_dma16(uint32_t lds, uint32_t voff, wd_rsrc_t r) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds), "v"(voff), "s"(r)
+               : "memory", "m0");
+}
+template <int MT, bool NORM = false, int NST = 3>
+__global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
+  typedef bf16_t T;
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  constexpr int CO = MT * 16;
+  constexpr int DCH = CO / 8, XCH = CK / 8;             // 16-B chunks per dy / halo row
+  constexpr int NDI = 128 * DCH / 64;                   // dy wave-instructions per brick (8 / 16)
+  constexpr int NXI = (HLO_V * XCH + 63) / 64;          // halo wave-instructions (23, the last one half)
+  constexpr int NI = NDI + NXI, KI = (NI + 7) / 8;      // per brick; per wave (8 waves)
+  constexpr int DS = 128 * CO, XS = NXI * 64 * 8;       // elements per stage (halo padded to whole instructions)
+  constexpr int SS = DS + XS;
+  __shared__ __attribute__((aligned(16))) T st[NST * SS];   // ring of NST stage images
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cin = 8 << g.cpg_shift;
+  const int nchunk = wgrad_nchunk(g.cpg_shift, g.kchunks), rt_n = g.Ca / CO;
+  const int tile = blockIdx.x;
+  const int ct = tile % nchunk, rt = (tile / nchunk) % rt_n, ks = tile / (nchunk * rt_n);
+  const int bz_n = g.D / BRK_Z, by_n = g.H / BRK_Y, bx_n = g.W / BRK_X;
+  const int nbrick = (int)(g.V / ((long long)g.D * g.H * g.W)) * bz_n * by_n * bx_n;
+  const int bpk = (nbrick + g.ksplit - 1) / g.ksplit;
+  const int b_begin = ks * bpk;
+  const int b_end = b_begin + bpk < nbrick ? b_begin + bpk : nbrick;
+  const int HW = g.H * g.W;
+  const int row0 = rt * CO, c0 = ct * CK;
+  const bool do_bias = g.bias_part != nullptr && ct == 0;
+  const int t_begin = wave < 3 ? 4 * wave : 12 + 3 * (wave - 3);
+  const int t_cnt = wave < 3 ? 4 : 3;
+  const bool bias_wave = do_bias && wave == 7;
+
+  const wd_rsrc_t drsrc = wd_rsrc(g.a, (uint32_t)(g.V * g.lda * 2));
+  const wd_rsrc_t xrsrc = wd_rsrc(g.b, (uint32_t)(g.V * g.ldb * 2));
+
+  // per DMA slot k (wave-instruction m = wave + 8 k): the lane's byte offset from the brick origin and, for a
+  // halo chunk, its halo position (hz, hy, hx packed; 0xff: no chunk)
+  uint32_t rel[KI], hpos[KI];
+  int nw = 0;
+#pragma unroll
+  for (int k = 0; k < KI; ++k) {
+    const int m = wave + 8 * k;
+    rel[k] = 0;
+    hpos[k] = 0xffu;
+    if (m < NDI) {
+      const int p = m * 64 + lane, v = p / DCH, c = p % DCH;
+      const int gi = (c >> 1) ^ (DCH == 4 ? (v >> 2) & 1 : (v >> 1) & 3), cc = (gi << 1) | (c & 1);
+      rel[k] = (uint32_t)((((v >> 5) * HW + ((v >> 3) & 3) * g.W + (v & 7)) * g.lda + row0 + cc * 8) * 2);
+      ++nw;
+    } else if (m < NI) {
+      const int p = (m - NDI) * 64 + lane, h = p >> 2, c = p & 3;
+      if (h < HLO_V) {
+        const int hx = h % HLO_X, hy = (h / HLO_X) % HLO_Y, hz = h / (HLO_X * HLO_Y);
+        const int cc = (((c >> 1) ^ ((hx >> 2) & 1)) << 1) | (c & 1);
+        rel[k] = (uint32_t)(((hz * HW + hy * g.W + hx) * g.ldb + c0 + cc * 8) * 2);
+        hpos[k] = (uint32_t)(hz | (hy << 8) | (hx << 16));
+      }
+      ++nw;
+    }
+  }
+  auto issue = [&](T* dst, int b) __attribute__((always_inline)) {
+    int q = b;
+    const int bx = q % bx_n;
+    q /= bx_n;
+    const int by = q % by_n;
+    q /= by_n;
+    const int bz = q % bz_n;
+    const int n = q / bz_n;
+    const int z0 = bz * BRK_Z, y0 = by * BRK_Y, x0 = bx * BRK_X;
+    const int vb = (n * g.D + z0) * HW + y0 * g.W + x0;
+    const int dbase = vb * g.lda * 2;
+    const int xbase = (vb - HW - g.W - 1) * g.ldb * 2;
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+      const int m = wave + 8 * k;
+      if (m < NDI) {
+        wd_dma16(__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)(lds_ptr_t)(dst + m * 512)),
+                 (uint32_t)(dbase + (int)rel[k]), drsrc);
+      } else if (m < NI) {
+        const uint32_t hp = hpos[k];
+        const int z = z0 - 1 + (int)(hp & 0xff), y = y0 - 1 + (int)((hp >> 8) & 0xff), x = x0 - 1 + (int)(hp >> 16);
+        const bool ok = hp != 0xffu && (unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H &&
+                        (unsigned)x < (unsigned)g.W;
+        wd_dma16(__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)(lds_ptr_t)(dst + DS + (m - NDI) * 512)),
+                 ok ? (uint32_t)(xbase + (int)rel[k]) : WD_OOB, xrsrc);
+      }
+    }
+  };
+  // this wave's DMAs of all but the last brick issued have landed (vmcnt <= nw)
+  // wait until at most `later` bricks' DMAs of this wave are in flight (vmcnt <= later * nw)
+  auto wait_bricks = [&](int later) __attribute__((always_inline)) {
+    switch (later * nw) {
+#define MMSEG_WD_WAIT(N) \
+  case N: __builtin_amdgcn_s_waitcnt(0x0f70 | N); break;
+      MMSEG_WD_WAIT(1) MMSEG_WD_WAIT(2) MMSEG_WD_WAIT(3) MMSEG_WD_WAIT(4) MMSEG_WD_WAIT(5) MMSEG_WD_WAIT(6)
+      MMSEG_WD_WAIT(7) MMSEG_WD_WAIT(8) MMSEG_WD_WAIT(9) MMSEG_WD_WAIT(10) MMSEG_WD_WAIT(11) MMSEG_WD_WAIT(12)
+      MMSEG_WD_WAIT(13) MMSEG_WD_WAIT(14) MMSEG_WD_WAIT(15)
+#undef MMSEG_WD_WAIT
+      default: __builtin_amdgcn_s_waitcnt(0x0f70); break;
+    }
+  };
+
+  // NORM: thread owns channel group cg = tid & 3 of halo rows (tid >> 2) + 128 k
+  int norm_n = -1;
+  float nmu[NORM ? 8 : 1], nrs[NORM ? 8 : 1];
+  auto normalize = [&](T* dst, int b) __attribute__((always_inline)) {
+    if constexpr (NORM) {
+      int q = b;
+      const int bx = q % bx_n;
+      q /= bx_n;
+      const int by = q % by_n;
+      q /= by_n;
+      const int bz = q % bz_n;
+      const int n = q / bz_n;
+      if (n != norm_n) {
+        norm_n = n;
+        const int cb = n * cin + c0 + (tid & 3) * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          nmu[j] = g.nmean[cb + j];
+          nrs[j] = g.nrstd[cb + j];
+        }
+      }
+      const int z0 = bz * BRK_Z, y0 = by * BRK_Y, x0 = bx * BRK_X, cg = tid & 3;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int h = (tid >> 2) + 128 * k;
+        if (h < HLO_V) {
+          const int hx = h % HLO_X, hy = (h / HLO_X) % HLO_Y, hz = h / (HLO_X * HLO_Y);
+          if ((unsigned)(z0 - 1 + hz) < (unsigned)g.D && (unsigned)(y0 - 1 + hy) < (unsigned)g.H &&
+              (unsigned)(x0 - 1 + hx) < (unsigned)g.W) {
+            const int c = (((cg >> 1) ^ ((hx >> 2) & 1)) << 1) | (cg & 1);
+            T* p = dst + DS + h * CK + c * 8;
+            V8<T> v;
+            v.load(p);
+            norm_relu8<T>(v, nmu, nrs);
+            v.store(p);
+          }
+        }
+      }
+    }
+  };
+
+  f32x4 acc[4][MT][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[t][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // fragment addressing (bytes): dy rows v_lo = kk + 16 (g4 >> 1) + 4 (g4 & 1) + q and v_lo + 8 share the
+  // swizzle; halo rows hlo + tap offset share hx's
+  const int g4 = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
+  const int v0 = 16 * (g4 >> 1) + 4 * (g4 & 1) + q4;
+  const int dsw = DCH == 4 ? (v0 >> 2) & 1 : (v0 >> 1) & 3;
+  const int hx0 = 4 * (g4 & 1) + q4;   // x of v_lo; y = 2 (g4 >> 1)
+  const int hlo0 = (2 * (g4 >> 1)) * HLO_X + hx0;
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+  auto compute = [&](const T* S) __attribute__((always_inline)) {
+    const char* Db = reinterpret_cast<const char*>(S);
+    const char* Xb = reinterpret_cast<const char*>(S + DS);
+#pragma unroll
+    for (int kk = 0; kk < 128; kk += 32) {
+      bf16x8 af[MT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const bf16_t* base = reinterpret_cast<const bf16_t*>(Db + (kk + v0) * (CO * 2) + 32 * (i ^ dsw) + 8 * p4);
+        af[i] = tr_frag(base, base + 8 * CO);
+      }
+      const int hlo = hlo0 + (kk >> 5) * (HLO_Y * HLO_X);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (t < t_cnt) {
+          const int tap = t_begin + t;
+          const int kz = tap / 9, ky = (tap / 3) % 3, kx = tap % 3;
+          const int r = hlo + (kz * HLO_Y + ky) * HLO_X + kx;
+          const int xs = ((hx0 + kx) >> 2) & 1;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const bf16_t* pl = reinterpret_cast<const bf16_t*>(Xb + r * (CK * 2) + 32 * (j ^ xs) + 8 * p4);
+            const bf16x8 bfr = tr_frag(pl, pl + HLO_X * CK);
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+              acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[t][i][j], 0, 0, 0);
+          }
+        } else if (t == 3 && bias_wave) {
+#pragma unroll
+          for (int i = 0; i < MT; ++i)
+            acc[3][i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, acc[3][i][0], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  // prologue: bricks b_begin .. b_begin + NST - 2 in flight, the first one landed
+  for (int k = 0; k < NST - 1; ++k)
+    if (b_begin + k < b_end) issue(st + k * SS, b_begin + k);
+  {
+    const int inflight = b_end - b_begin - 1 < NST - 2 ? b_end - b_begin - 1 : NST - 2;
+    wait_bricks(inflight > 0 ? inflight : 0);
+  }
+  __syncthreads();
+  if constexpr (NORM) {
+    if (b_begin < b_end) {
+      normalize(st, b_begin);
+      __syncthreads();
+    }
+  }
+  for (int b = b_begin, sc = 0; b < b_end; ++b, sc = sc + 1 == NST ? 0 : sc + 1) {
+    // issue brick b + NST - 1 into the stage brick b - 1 used (every wave passed the barrier after it)
+    const int sn = sc == 0 ? NST - 1 : sc - 1;
+    if (b + NST - 1 < b_end && g.dbg != 1) issue(st + sn * SS, b + NST - 1);
+    if (g.dbg != 2) compute(st + sc * SS);
+    // brick b + 1 has landed once at most min(NST - 2, bricks issued after it) bricks are in flight
+    const int after = b_end - b - 2 < NST - 2 ? b_end - b - 2 : NST - 2;
+    wait_bricks(after > 0 ? after : 0);
+    __syncthreads();
+    if constexpr (NORM) {
+      if (b + 1 < b_end) {
+        normalize(st + (sc + 1 == NST ? 0 : sc + 1) * SS, b + 1);
+        __syncthreads();
+      }
+    }
+  }
+
+  static_assert(sizeof(st) >= 16 * WEP_P * sizeof(float), "epilogue staging must fit the stage ring");
+  wgrad_store_chmajor<MT>(acc, t_begin, t_cnt, reinterpret_cast<float*>(st), g, ks, row0, c0);
+  if (bias_wave && i16 == 0) {
+    // acc[3][i][0][r] = sum over the block's voxels of dy[.][row0 + 16 i + 4 g4 + r] (every column alike)
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = row0 + 16 * i + 4 * g4 + r;
+        const float s = acc[3][i][0][r];
+        if (g.bias_grad != nullptr && g.ksplit == 1)
+          g.bias_grad[co] = g.accumulate ? g.bias_grad[co] + s : s;
+        else
+          g.bias_part[(long long)ks * g.Ca + co] = s;
+      }
+  }
 }
 
 // ------------------------------------- runtime-brick wgrad (small volumes)
@@ -2840,12 +3069,13 @@ __global__ __launch_bounds__(512) void wgrad_brickr_kernel(WgradArgs g, int bz_r
 
   V8<T> dr[D_PER], xr[X_PER];
   auto load = [&](long long b) {
-    const int bxi = (int)(b % bx_n);
-    long long q = b / bx_n;
-    const int byi = (int)(q % by_n);
+    int q = (int)b;   // brick index < V < 2^31 (mmseg_wgrad): 32-bit division
+    const int bxi = q % bx_n;
+    q /= bx_n;
+    const int byi = q % by_n;
     q /= by_n;
-    const int bzi = (int)(q % bz_n);
-    const long long nbase = (q / bz_n) * g.D * HW;
+    const int bzi = q % bz_n;
+    const long long nbase = (long long)(q / bz_n) * g.D * HW;
     const int z0 = bzi * bz, y0 = byi * by, x0 = bxi * bx;
 #pragma unroll
     for (int k = 0; k < D_PER; ++k) {
@@ -3028,7 +3258,7 @@ struct WReduceArgs {
 // thousands), so every thread has a few independent loads in flight.  Bias
 // partials ([ks][Ca], after the weight columns) are summed by the blocks past
 // the weight range.
-template <int S>
+template <int S, int U = 4>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(WReduceArgs g) {
   constexpr int NC = 256 / S;                 // float4 columns per block
   __shared__ float4 red[S][NC];
@@ -3039,10 +3269,20 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(WReduceArgs g) {
   if (e0 < total) {
     const float4* p = reinterpret_cast<const float4*>(g.part + e0);
     const long long stride4 = total / 4;
-#pragma unroll 4
-    for (int k = sl; k < g.ksplit; k += S) {
-      const float4 a = p[(long long)k * stride4];
-      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    // U loads in flight per thread (the sum order stays k = sl, sl + S, ...)
+    for (int k0 = sl; k0 < g.ksplit; k0 += U * S) {
+      float4 a[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + u * S;
+        if (k < g.ksplit) a[u] = p[(long long)k * stride4];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (k0 + u * S < g.ksplit) {
+          v.x += a[u].x; v.y += a[u].y; v.z += a[u].z; v.w += a[u].w;
+        }
+      }
     }
   } else if (g.bias_part) {
     const long long r0 = e0 - total;   // bias rows r0 .. r0+3
@@ -3602,6 +3842,7 @@ int launch_gemm_mode(GemmArgs g, int mode, hipStream_t s) {
 
 template <typename T, int MODE>
 int launch_wgrad(WgradArgs g, hipStream_t s) {
+  g.dbg = knob("MMSEG_WGRAD_DBG", 0);
   dim3 block(256);
   if constexpr (sizeof(T) == 2) {
     if (MODE == MODE_CONV3 && g.brick == 3) {
@@ -3626,12 +3867,38 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
     }
     if (MODE == MODE_CONV3 && g.brick == 2) {
       const bool v3 = knob("MMSEG_WGRAD_V3", 1) != 0;
+      // LDS-DMA staging: bf16, byte offsets of both tensors within 31 bits
+      const bool dma = sizeof(T) == 2 && v3 && knob("MMSEG_WGRAD_DMA", 0) && g.V * g.lda * 2 < (1LL << 31) &&
+                       g.V * g.ldb * 2 < (1LL << 31) && (g.lda % 8) == 0 && (g.ldb % 8) == 0;
+      if (dma) {
+        const int mt = g.Ca % 64 == 0 ? 4 : 2;
+        dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / (16 * mt)) * g.ksplit);
+        const bool st4 = knob("MMSEG_WGRAD_DMA_ST", 3) >= 4;   // ring depth (4 x 38.5 KB fits at 64 co)
+        if (mt == 4) {
+          mmseg::note_kernel("wgrad_dma_kernel<CO64>");
+          if (g.nmean)
+            hipLaunchKernelGGL((wgrad_dma_kernel<4, true>), grid, dim3(512), 0, s, g);
+          else if (st4)
+            hipLaunchKernelGGL((wgrad_dma_kernel<4, false, 4>), grid, dim3(512), 0, s, g);
+          else
+            hipLaunchKernelGGL((wgrad_dma_kernel<4>), grid, dim3(512), 0, s, g);
+        } else {
+          mmseg::note_kernel("wgrad_dma_kernel<CO32>");
+          if (g.nmean && st4)
+            hipLaunchKernelGGL((wgrad_dma_kernel<2, true, 4>), grid, dim3(512), 0, s, g);
+          else if (g.nmean)
+            hipLaunchKernelGGL((wgrad_dma_kernel<2, true>), grid, dim3(512), 0, s, g);
+          else if (st4)
+            hipLaunchKernelGGL((wgrad_dma_kernel<2, false, 4>), grid, dim3(512), 0, s, g);
+          else
+            hipLaunchKernelGGL((wgrad_dma_kernel<2>), grid, dim3(512), 0, s, g);
+        }
+        return mmseg::check_launch("wgrad_dma");
+      }
       if (g.Ca % 64 == 0) {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 64) * g.ksplit);
         mmseg::note_kernel(v3 ? "wgrad_brick2_kernel<CO64,V3>" : "wgrad_brick2_kernel<CO64>");
         if (v3 && g.nmean)
-          hipLaunchKernelGGL((wgrad_brick2_kernel<T, 4, 3, false, true>), grid, dim3(512), 0, s, g);
-        else if (v3 && knob("MMSEG_WGRAD_BAL", 0))
           hipLaunchKernelGGL((wgrad_brick2_kernel<T, 4, 3, true>), grid, dim3(512), 0, s, g);
         else if (v3)
           hipLaunchKernelGGL((wgrad_brick2_kernel<T, 4, 3>), grid, dim3(512), 0, s, g);
@@ -3640,11 +3907,7 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
       } else {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 32) * g.ksplit);
         mmseg::note_kernel(v3 ? "wgrad_brick2_kernel<CO32,V3>" : "wgrad_brick2_kernel<CO32>");
-        if (v3 && g.nmean && knob("MMSEG_WGRAD_BAL", 0))
-          hipLaunchKernelGGL((wgrad_brick2_kernel<T, 2, 3, true, true>), grid, dim3(512), 0, s, g);
-        else if (v3 && g.nmean)
-          hipLaunchKernelGGL((wgrad_brick2_kernel<T, 2, 3, false, true>), grid, dim3(512), 0, s, g);
-        else if (v3 && knob("MMSEG_WGRAD_BAL", 0))
+        if (v3 && g.nmean)
           hipLaunchKernelGGL((wgrad_brick2_kernel<T, 2, 3, true>), grid, dim3(512), 0, s, g);
         else if (v3)
           hipLaunchKernelGGL((wgrad_brick2_kernel<T, 2, 3>), grid, dim3(512), 0, s, g);
@@ -3784,17 +4047,29 @@ int launch_wgrad_reduce(WReduceArgs g, void* stream) {
   // small gradients over many splits (the stem: 1,056 values x 1,024 splits): more slices until the grid
   // fills the chip, down to 2 loads per thread (S = 64 left it at 66 blocks, 12.8 us for 4 MB)
   while (S < 256 && (total * S + 1023) / 1024 < knob("MMSEG_WGRAD_RBLK", 512) && ksplit / (2 * S) >= 2) S *= 2;
+  const int U = knob("MMSEG_WRED_U", 4);
+#define MMSEG_WRED(SS, NB)                                                                             \
+  case SS:                                                                                             \
+    if (U >= 16)                                                                                       \
+      hipLaunchKernelGGL((wgrad_reduce_kernel<SS, 16>), dim3(ceil_div(total, NB)), dim3(256), 0, s, g); \
+    else if (U >= 8)                                                                                   \
+      hipLaunchKernelGGL((wgrad_reduce_kernel<SS, 8>), dim3(ceil_div(total, NB)), dim3(256), 0, s, g);  \
+    else                                                                                               \
+      hipLaunchKernelGGL((wgrad_reduce_kernel<SS, 4>), dim3(ceil_div(total, NB)), dim3(256), 0, s, g);  \
+    break;
   switch (S) {
-    case 256: hipLaunchKernelGGL(wgrad_reduce_kernel<256>, dim3(ceil_div(total, 4)), dim3(256), 0, s, g); break;
-    case 128: hipLaunchKernelGGL(wgrad_reduce_kernel<128>, dim3(ceil_div(total, 8)), dim3(256), 0, s, g); break;
-    case 64: hipLaunchKernelGGL(wgrad_reduce_kernel<64>, dim3(ceil_div(total, 16)), dim3(256), 0, s, g); break;
-    case 32: hipLaunchKernelGGL(wgrad_reduce_kernel<32>, dim3(ceil_div(total, 32)), dim3(256), 0, s, g); break;
-    case 16: hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(ceil_div(total, 64)), dim3(256), 0, s, g); break;
-    case 8: hipLaunchKernelGGL(wgrad_reduce_kernel<8>, dim3(ceil_div(total, 128)), dim3(256), 0, s, g); break;
-    case 4: hipLaunchKernelGGL(wgrad_reduce_kernel<4>, dim3(ceil_div(total, 256)), dim3(256), 0, s, g); break;
-    case 2: hipLaunchKernelGGL(wgrad_reduce_kernel<2>, dim3(ceil_div(total, 512)), dim3(256), 0, s, g); break;
-    default: hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(ceil_div(total, 1024)), dim3(256), 0, s, g); break;
+    MMSEG_WRED(256, 4)
+    MMSEG_WRED(128, 8)
+    MMSEG_WRED(64, 16)
+    MMSEG_WRED(32, 32)
+    MMSEG_WRED(16, 64)
+    MMSEG_WRED(8, 128)
+    MMSEG_WRED(4, 256)
+    MMSEG_WRED(2, 512)
+    default:
+      MMSEG_WRED(1, 1024)
   }
+#undef MMSEG_WRED
   return mmseg::check_launch("wgrad_reduce");
 }
 

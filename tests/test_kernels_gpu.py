@@ -72,6 +72,12 @@ def test_conv3_fwd_dgrad_wgrad(dev, dtype, cin, cout, shape):
     ({}, 32, 128, (1, 8, 4, 16)),                                    # v2 brick wgrad, 2 row tiles of 64 co
     ({}, 64, 32, (2, 4, 4, 16)),                                     # v2 brick wgrad, 32 co per block
     ({"MMSEG_WGRAD_BRICK2_CO32": "0"}, 64, 32, (2, 4, 4, 16)),       # v1 for 32 co
+    # v2 brick wgrad with LDS-DMA staging (bf16; f32 keeps the register-staged kernel): 3-stage ring, border
+    # halos, ragged brick ranges over the splits
+    ({"MMSEG_WGRAD_DMA": "1"}, 32, 128, (1, 8, 4, 16)),              # 64 co, 2 row tiles
+    ({"MMSEG_WGRAD_DMA": "1"}, 64, 32, (2, 4, 4, 16)),               # 32 co, 2 input chunks
+    ({"MMSEG_WGRAD_DMA": "1"}, 32, 32, (2, 12, 8, 24)),              # 32 co, 36 bricks
+    ({"MMSEG_WGRAD_DMA": "1"}, 64, 64, (1, 8, 12, 16)),              # 64 co, 24 bricks
     ({"MMSEG_BRICK": "1"}, 64, 64, (2, 8, 8, 8)),                   # v1 brick
     ({"MMSEG_BRICK": "0"}, 64, 64, (2, 8, 8, 8)),                   # per-lane gather GEMM
 ])

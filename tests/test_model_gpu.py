@@ -352,8 +352,9 @@ def test_deferred_head_norm_bitwise(dev, tag, dtype, monkeypatch):
     assert torch.equal(res[0][1], res[1][1])
 
 
+@pytest.mark.parametrize("wgrad_dma", ["0", "1"])
 @pytest.mark.parametrize("model", ["unet", "dual_encoder"])
-def test_deferred_conv_norm_bitwise(dev, model, monkeypatch):
+def test_deferred_conv_norm_bitwise(dev, model, wgrad_dma, monkeypatch):
     """bf16, 32-channel top level (the brick5 / brick2 kernels): conv1's InstanceNorm + ReLU applied by conv2's
     forward and weight-gradient kernels on staging (y1 never written) gives a bit-identical loss and gradients
     to the materialised path (MMSEG_DEFER_CONV_NORM=0)."""
@@ -363,6 +364,7 @@ def test_deferred_conv_norm_bitwise(dev, model, monkeypatch):
     x = torch.randn(2, 2, 32, 32, 32, generator=gen).to(dev)
     y = torch.randint(0, 3, (2, 32, 32, 32), generator=gen).to(dev)
     res = []
+    monkeypatch.setenv("MMSEG_WGRAD_DMA", wgrad_dma)   # register-staged / LDS-DMA weight-gradient kernels
     for defer in ("1", "0"):
         monkeypatch.setenv("MMSEG_DEFER_CONV_NORM", defer)
         cfg = make_config(model, ["CT", "PET"], 3, [32, 64, 128], dtype="bfloat16")
