@@ -2767,7 +2767,8 @@ __device__ __forceinline__ void wd_dma16(uint32_t lds, uint32_t voff, wd_rsrc_t 
   asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds), "v"(voff), "s"(r)
                : "memory", "m0");
 }
-template <int MT, bool NORM = false, int NST = 3>
+// PIPE: the fragment reads of the next (dy plane, tap) step are issued before the current step's MFMAs
+template <int MT, bool NORM = false, int NST = 3, bool PIPE = false>
 __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
   typedef bf16_t T;
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -2961,6 +2962,58 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
       }
     }
   };
+  // software-pipelined: steps s = (kk, t) over this wave's TC taps, fragments double-buffered
+  auto compute_pipe = [&](const T* S, auto tcc) __attribute__((always_inline)) {
+    constexpr int TC = decltype(tcc)::value;
+    const char* Db = reinterpret_cast<const char*>(S);
+    const char* Xb = reinterpret_cast<const char*>(S + DS);
+    constexpr int PD = 3;
+    bf16x8 af[2][MT], bf[PD][2];
+    auto load_a = [&](int kk, bf16x8(&a)[MT]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const bf16_t* base = reinterpret_cast<const bf16_t*>(Db + (kk + v0) * (CO * 2) + 32 * (i ^ dsw) + 8 * p4);
+        a[i] = tr_frag(base, base + 8 * CO);
+      }
+    };
+    auto load_b = [&](int kk, int t, bf16x8(&b)[2]) __attribute__((always_inline)) {
+      const int tap = t_begin + t;
+      const int kz = tap / 9, ky = (tap / 3) % 3, kx = tap % 3;
+      const int r = hlo0 + (kk >> 5) * (HLO_Y * HLO_X) + (kz * HLO_Y + ky) * HLO_X + kx;
+      const int xs = ((hx0 + kx) >> 2) & 1;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bf16_t* pl = reinterpret_cast<const bf16_t*>(Xb + r * (CK * 2) + 32 * (j ^ xs) + 8 * p4);
+        b[j] = tr_frag(pl, pl + HLO_X * CK);
+      }
+    };
+    // B fragments PD - 1 steps ahead (ring of PD), A one dy plane ahead
+    constexpr int NS = 4 * TC;
+    load_a(0, af[0]);
+#pragma unroll
+    for (int s0 = 0; s0 < PD - 1; ++s0)
+      if (s0 < NS) load_b(32 * (s0 / TC), s0 % TC, bf[s0 % PD]);
+#pragma unroll
+    for (int sidx = 0; sidx < NS; ++sidx) {
+      const int k4 = sidx / TC, t = sidx % TC;
+      const int sn = sidx + PD - 1;
+      if (sn < NS) load_b(32 * (sn / TC), sn % TC, bf[sn % PD]);
+      if (t == 0 && k4 + 1 < 4) load_a(32 * (k4 + 1), af[(k4 + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+          acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k4 & 1][i], bf[sidx % PD][j], acc[t][i][j], 0, 0,
+                                                                 0);
+      if (TC == 3 && t == 2 && bias_wave) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+          acc[3][i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k4 & 1][i], ones, acc[3][i][0], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
 
   // prologue: bricks b_begin .. b_begin + NST - 2 in flight, the first one landed
   for (int k = 0; k < NST - 1; ++k)
@@ -2980,7 +3033,16 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
     // issue brick b + NST - 1 into the stage brick b - 1 used (every wave passed the barrier after it)
     const int sn = sc == 0 ? NST - 1 : sc - 1;
     if (b + NST - 1 < b_end && g.dbg != 1) issue(st + sn * SS, b + NST - 1);
-    if (g.dbg != 2) compute(st + sc * SS);
+    if (g.dbg != 2) {
+      if constexpr (PIPE) {
+        if (t_cnt == 4)
+          compute_pipe(st + sc * SS, std::integral_constant<int, 4>{});
+        else
+          compute_pipe(st + sc * SS, std::integral_constant<int, 3>{});
+      } else {
+        compute(st + sc * SS);
+      }
+    }
     // brick b + 1 has landed once at most min(NST - 2, bricks issued after it) bricks are in flight
     const int after = b_end - b - 2 < NST - 2 ? b_end - b - 2 : NST - 2;
     wait_bricks(after > 0 ? after : 0);
@@ -3868,15 +3930,21 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
     if (MODE == MODE_CONV3 && g.brick == 2) {
       const bool v3 = knob("MMSEG_WGRAD_V3", 1) != 0;
       // LDS-DMA staging: bf16, byte offsets of both tensors within 31 bits
-      const bool dma = sizeof(T) == 2 && v3 && knob("MMSEG_WGRAD_DMA", 0) && g.V * g.lda * 2 < (1LL << 31) &&
+      // (the deferred-norm variant keeps register staging by default: its in-place LDS pass and extra barrier
+      // cost more than the DMA saves, 0.651 -> 0.682 ms/step for the 32-co family)
+      const bool dma = sizeof(T) == 2 && v3 && knob("MMSEG_WGRAD_DMA", 1) &&
+                       (g.nmean == nullptr || knob("MMSEG_WGRAD_DMA_NORM", 0)) && g.V * g.lda * 2 < (1LL << 31) &&
                        g.V * g.ldb * 2 < (1LL << 31) && (g.lda % 8) == 0 && (g.ldb % 8) == 0;
       if (dma) {
         const int mt = g.Ca % 64 == 0 ? 4 : 2;
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / (16 * mt)) * g.ksplit);
         const bool st4 = knob("MMSEG_WGRAD_DMA_ST", 3) >= 4;   // ring depth (4 x 38.5 KB fits at 64 co)
+        // fragment prefetch two steps ahead (32 co; at 64 co the extra registers spill: 59.5 -> 72.3 us)
+        const bool pipe = mt == 2 && knob("MMSEG_WGRAD_DMA_PIPE", 1) != 0;
+        const bool norm = g.nmean != nullptr;
         if (mt == 4) {
           mmseg::note_kernel("wgrad_dma_kernel<CO64>");
-          if (g.nmean)
+          if (norm)
             hipLaunchKernelGGL((wgrad_dma_kernel<4, true>), grid, dim3(512), 0, s, g);
           else if (st4)
             hipLaunchKernelGGL((wgrad_dma_kernel<4, false, 4>), grid, dim3(512), 0, s, g);
@@ -3884,10 +3952,12 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
             hipLaunchKernelGGL((wgrad_dma_kernel<4>), grid, dim3(512), 0, s, g);
         } else {
           mmseg::note_kernel("wgrad_dma_kernel<CO32>");
-          if (g.nmean && st4)
-            hipLaunchKernelGGL((wgrad_dma_kernel<2, true, 4>), grid, dim3(512), 0, s, g);
-          else if (g.nmean)
+          if (norm && pipe)
+            hipLaunchKernelGGL((wgrad_dma_kernel<2, true, 3, true>), grid, dim3(512), 0, s, g);
+          else if (norm)
             hipLaunchKernelGGL((wgrad_dma_kernel<2, true>), grid, dim3(512), 0, s, g);
+          else if (pipe)
+            hipLaunchKernelGGL((wgrad_dma_kernel<2, false, 3, true>), grid, dim3(512), 0, s, g);
           else if (st4)
             hipLaunchKernelGGL((wgrad_dma_kernel<2, false, 4>), grid, dim3(512), 0, s, g);
           else
