@@ -376,13 +376,16 @@ def test_dice_counts_from_logits_matches_argmax(dev):
     assert torch.equal(a.intersection, b.intersection) and torch.equal(a.union, b.union)
 
 
-def test_adamw_matches_torch(dev):
+@pytest.mark.parametrize("n0,n1", [(600, 400), (603, 402), (3, 0)])   # float4 body, + scalar tail, tail only
+def test_adamw_matches_torch(dev, n0, n1):
     from mmseg_amd.trainer.optim import FlatAdamW
     torch.manual_seed(0)
-    flat = torch.randn(1000, device=dev)
-    params = [torch.nn.Parameter(flat[:600].view(20, 30)), torch.nn.Parameter(flat[600:].view(400))]
-    gflat = torch.randn(1000, device=dev)
-    params[0].grad, params[1].grad = gflat[:600].view(20, 30), gflat[600:]
+    flat = torch.randn(n0 + n1, device=dev)
+    gflat = torch.randn(n0 + n1, device=dev)
+    params = [torch.nn.Parameter(flat[:n0].view(n0))] + ([torch.nn.Parameter(flat[n0:])] if n1 else [])
+    params[0].grad = gflat[:n0].view(n0)
+    if n1:
+        params[1].grad = gflat[n0:]
     ref = [torch.nn.Parameter(p.detach().cpu().clone()) for p in params]
     for r, p in zip(ref, params):
         r.grad = p.grad.detach().cpu().clone()
