@@ -364,7 +364,10 @@ def test_deferred_conv_norm_bitwise(dev, model, wgrad_dma, monkeypatch):
     x = torch.randn(2, 2, 32, 32, 32, generator=gen).to(dev)
     y = torch.randint(0, 3, (2, 32, 32, 32), generator=gen).to(dev)
     res = []
-    monkeypatch.setenv("MMSEG_WGRAD_DMA", wgrad_dma)   # register-staged / LDS-DMA weight-gradient kernels
+    # register-staged / LDS-DMA weight-gradient kernels, the same kind on both paths (their bias gradients sum
+    # in different orders)
+    monkeypatch.setenv("MMSEG_WGRAD_DMA", wgrad_dma)
+    monkeypatch.setenv("MMSEG_WGRAD_DMA_NORM", wgrad_dma)
     for defer in ("1", "0"):
         monkeypatch.setenv("MMSEG_DEFER_CONV_NORM", defer)
         cfg = make_config(model, ["CT", "PET"], 3, [32, 64, 128], dtype="bfloat16")
