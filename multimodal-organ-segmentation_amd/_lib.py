@@ -16,7 +16,8 @@ import torch  # noqa: F401  (must be imported first: loads torch's libamdhip64 s
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 _REPO_DIR = os.path.dirname(_PKG_DIR)
-LIB_PATH = os.path.join(_PKG_DIR, "libmmseg_hip.so")
+# MMSEG_LIB_PATH: another in-tree build of the same ABI (A/B of two builds in one GPU call, tools/ only)
+LIB_PATH = os.environ.get("MMSEG_LIB_PATH") or os.path.join(_PKG_DIR, "libmmseg_hip.so")
 HEADER_PATH = os.path.join(_REPO_DIR, "include", "mmseg_hip.h")
 
 _CTYPE = {
