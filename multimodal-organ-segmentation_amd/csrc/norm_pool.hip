@@ -295,19 +295,19 @@ __global__ void maxpool2_fwd(const T* __restrict__ x, int ldx, T* __restrict__ y
                              const float* __restrict__ mean = nullptr, const float* __restrict__ rstd = nullptr) {
   const int C8 = C >> 3;
   const int Do = D >> 1, Ho = H >> 1, Wo = W >> 1;
-  const long long Vo = (long long)Do * Ho * Wo;
-  const long long total = (long long)N * Vo * C8;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int cg = (int)(i % C8);
-    long long q = i / C8;
-    const int xo = (int)(q % Wo);
+  // 32-bit item index (the host requires N * Vo * C8 < 2^31): the former 64-bit divisions were most of the
+  // kernel's VALU work
+  const int total = N * Do * Ho * Wo * C8;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int cg = i % C8;
+    int q = i / C8;
+    const int xo = q % Wo;
     q /= Wo;
-    const int yo = (int)(q % Ho);
+    const int yo = q % Ho;
     q /= Ho;
-    const int zo = (int)(q % Do);
-    const long long n = q / Do;
-    const long long in0 = ((n * D + 2 * zo) * H + 2 * yo) * (long long)W + 2 * xo;
+    const int zo = q % Do;
+    const int n = q / Do;
+    const long long in0 = ((long long)(n * D + 2 * zo) * H + 2 * yo) * (long long)W + 2 * xo;
     float best[8];
     uint8_t bi[8];
     float mu[8], rs[8];
@@ -340,7 +340,7 @@ __global__ void maxpool2_fwd(const T* __restrict__ x, int ldx, T* __restrict__ y
     V8<T> o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) o.set(j, best[j]);
-    const long long vo = ((n * Do + zo) * Ho + yo) * Wo + xo;
+    const long long vo = ((long long)(n * Do + zo) * Ho + yo) * Wo + xo;
     o.store(y + vo * ldy + cg * 8);
     uint2 packed;
     packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
@@ -960,12 +960,11 @@ struct FuseSrc {
 template <typename T, bool NORM = false>
 __global__ void fuse_fwd(FuseSrc s, T* __restrict__ out, int ldo, long long V, int N, int C) {
   const int C8 = C >> 3;
-  const long long total = (long long)N * V * C8;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int cg = (int)(i % C8);
+  const int total = N * (int)V * C8;   // < 2^31 (host check): 32-bit index math
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int cg = i % C8;
     const long long nv = i / C8;
-    const int n = (int)(nv / V);
+    const int n = (int)(nv / (int)V);
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
@@ -1339,6 +1338,7 @@ int mmseg_instnorm_bwd(const void* x, int ldx, const float* mean, const float* r
 int mmseg_maxpool2_fwd(const void* x, int ldx, void* y, int ldy, uint8_t* idx, int N, int D, int H, int W, int C,
                        int dtype, void* stream) {
   MMSEG_REQUIRE(C % 8 == 0 && ((D | H | W) & 1) == 0, "maxpool2: C%%8==0 and even dims required");
+  MMSEG_REQUIRE((long long)N * (D / 2) * (H / 2) * (W / 2) * (C / 8) < (1LL << 31), "maxpool2: too many items");
   hipStream_t s = (hipStream_t)stream;
   const int grid = grid_for((long long)N * (D / 2) * (H / 2) * (W / 2) * (C / 8));
   if (dtype == MMSEG_BF16)
@@ -1355,6 +1355,7 @@ int mmseg_maxpool2_fwd(const void* x, int ldx, void* y, int ldy, uint8_t* idx, i
 int mmseg_maxpool2_norm_fwd(const void* x, int ldx, const float* mean, const float* rstd, void* y, int ldy,
                             uint8_t* idx, int N, int D, int H, int W, int C, int dtype, void* stream) {
   MMSEG_REQUIRE(C % 8 == 0 && ((D | H | W) & 1) == 0, "maxpool2: C%%8==0 and even dims required");
+  MMSEG_REQUIRE((long long)N * (D / 2) * (H / 2) * (W / 2) * (C / 8) < (1LL << 31), "maxpool2: too many items");
   hipStream_t s = (hipStream_t)stream;
   const int grid = grid_for((long long)N * (D / 2) * (H / 2) * (W / 2) * (C / 8));
   if (dtype == MMSEG_BF16)
@@ -1371,6 +1372,7 @@ int mmseg_fuse_norm_fwd(const void* const* srcs, const int* lds, const float* co
                         int M, float wconst, const float* wts, void* out, int ldo, int N, long long V, int C,
                         int dtype, void* stream) {
   MMSEG_REQUIRE(M >= 1 && M <= 4 && C % 8 == 0, "fuse: 1 <= M <= 4 and C%%8==0");
+  MMSEG_REQUIRE((long long)N * V * (C / 8) < (1LL << 31), "fuse: too many items");
   FuseSrc s{};
   for (int m = 0; m < M; ++m) {
     s.p[m] = srcs[m];
@@ -1394,6 +1396,7 @@ int mmseg_fuse_norm_fwd(const void* const* srcs, const int* lds, const float* co
 int mmseg_fuse_fwd(const void* const* srcs, const int* lds, int M, float wconst, const float* wts, void* out, int ldo,
                    int N, long long V, int C, int dtype, void* stream) {
   MMSEG_REQUIRE(M >= 1 && M <= 4 && C % 8 == 0, "fuse: 1 <= M <= 4 and C%%8==0");
+  MMSEG_REQUIRE((long long)N * V * (C / 8) < (1LL << 31), "fuse: too many items");
   FuseSrc s{};
   for (int m = 0; m < M; ++m) {
     s.p[m] = srcs[m];
