@@ -16,6 +16,8 @@
 // single-thread-per-output sweep), so results are bitwise reproducible.
 #include "mmseg_common.h"
 
+#include <algorithm>
+
 #include <stdlib.h>
 #include <type_traits>
 
@@ -1146,11 +1148,20 @@ int knob_small_t() {
   return e ? atoi(e) : 256;
 }
 
+// at least MMSEG_IN_MINCH chunks per sample (down to 2 voxels per thread): the 48^3 / 24^3 levels otherwise ran
+// 108..432 blocks of 16 voxels per thread, latency-bound
+int knob_in_minch() {
+  const char* e = getenv("MMSEG_IN_MINCH");
+  return e ? atoi(e) : 256;
+}
+
 int chunks_for(long long V, int C, long long* vpc) {
   // reduction passes: ~16 voxels per thread (lanes_v = 256 / C8 voxel lanes), at most 1024 chunks
   const int lanes_v = 256 / (C >> 3);
   long long want = (long long)lanes_v * 16;
   long long nch = (V + want - 1) / want;
+  const long long minch = std::min<long long>(knob_in_minch(), V / (2LL * lanes_v));
+  if (nch < minch) nch = minch;
   if (nch > 1024) nch = 1024;
   if (nch < 1) nch = 1;
   *vpc = (V + nch - 1) / nch;
@@ -1162,6 +1173,8 @@ int apply_chunks(long long V, int C, int* vpc) {
   const int lanes_v = 256 / (C >> 3);
   long long want = (long long)lanes_v * 2 * UNR;
   long long nch = (V + want - 1) / want;
+  const long long minch = std::min<long long>(knob_in_minch(), V / lanes_v);
+  if (nch < minch) nch = minch;
   if (nch < 1) nch = 1;
   *vpc = (int)((V + nch - 1) / nch);
   return (int)((V + *vpc - 1) / *vpc);
