@@ -1146,9 +1146,18 @@ int grid_for(long long total) {
   return (int)b;
 }
 
+int loss_vpc() {
+  static const int v = [] {
+    const char* e = getenv("MMSEG_LOSS_VPC");
+    return e ? atoi(e) : 2048;
+  }();
+  return v;
+}
+
 int loss_chunks(long long V, long long* vpc) {
-  long long nch = (V + 2047) / 2048;
-  if (nch > 1024) nch = 1024;
+  const int want = loss_vpc();
+  long long nch = (V + want - 1) / want;
+  if (nch > 4096) nch = 4096;
   if (nch < 1) nch = 1;
   *vpc = (V + nch - 1) / nch;
   return (int)((V + *vpc - 1) / *vpc);

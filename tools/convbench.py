@@ -1,6 +1,6 @@
 """Microbenchmark of one 3^3 conv layer on the engine (fwd, dgrad, wgrad), HIP-event timed.
 
-    python tools/convbench.py [--shape N,S,Cin,Cout ...] [--iters 20] [--only fwd,dgrad,wgrad]
+    python tools/convbench.py [--shape N,S,Cin,Cout | N,D,H,W,Cin,Cout ...] [--iters 20] [--only fwd,dgrad,wgrad]
 Env knobs (MMSEG_*) select kernel variants; prints one JSON line per (shape, op) with
 the kernel the library launched, us per launch and TFLOP/s (2*27*Cin*Cout per voxel).
 """
@@ -33,36 +33,41 @@ def main():
     rt = Runtime(dev, dt)
     ops = args.only.split(",")
     for sh in args.shape:
-        N, S, Ci, Co = (int(v) for v in sh.split(","))
+        vals = [int(v) for v in sh.split(",")]
+        if len(vals) == 4:
+            N, S, Ci, Co = vals
+            D = H = W = S
+        else:
+            N, D, H, W, Ci, Co = vals
         torch.manual_seed(0)
         conv = nn.Conv3d(Ci, Co, 3, padding=1).to(dev)
         flat = FlatParams(list(conv.parameters()))
         layer = Conv3(rt, conv, flat)
         layer.pack()
-        x = rt.act(N, S, S, S, Ci)
-        y = rt.act(N, S, S, S, Co)
-        dx = rt.act(N, S, S, S, Ci)
+        x = rt.act(N, D, H, W, Ci)
+        y = rt.act(N, D, H, W, Co)
+        dx = rt.act(N, D, H, W, Ci)
         x.buf.normal_()
         y.buf.normal_()
-        flops = 2.0 * N * S ** 3 * 27 * Ci * Co
+        flops = 2.0 * N * D * H * W * 27 * Ci * Co
         L, s, code = rt.lib, rt.stream, rt.code
 
         def run(op):
             if op == "fwd":
                 layer.fwd(x, y)
             elif op == "dgrad":
-                M = N * S ** 3
-                ks = L.mmseg_conv3_splits(M, Ci, layer.Cpad_d, layer.KGd, layer.dshift, S, S, S, y.ld, dx.ld, code)
+                M = N * D * H * W
+                ks = L.mmseg_conv3_splits(M, Ci, layer.Cpad_d, layer.KGd, layer.dshift, D, H, W, y.ld, dx.ld, code)
                 ws = rt.ws(ks * M * Ci) if ks > 1 else None
                 L.mmseg_conv_gemm(y.ptr, y.ld, layer.wd.data_ptr(), None, dx.ptr, dx.ld,
                                   ws.data_ptr() if ws is not None else None, 0, M, Ci, layer.Cpad_d, layer.KGd,
-                                  layer.dshift, S, S, S, ks, code, s)
+                                  layer.dshift, D, H, W, ks, code, s)
             else:
-                V = N * S ** 3
-                wsf = L.mmseg_conv3_wgrad_ws_floats(V, Co, layer.Cip, Ci, layer.cpg_shift, S, S, S, y.ld, x.ld, code)
+                V = N * D * H * W
+                wsf = L.mmseg_conv3_wgrad_ws_floats(V, Co, layer.Cip, Ci, layer.cpg_shift, D, H, W, y.ld, x.ld, code)
                 ws = rt.ws(wsf) if wsf > 0 else None
                 L.mmseg_conv3_wgrad(y.ptr, y.ld, x.ptr, x.ld, flat.grad(conv.weight).data_ptr(),
-                                    flat.grad(conv.bias).data_ptr(), Co, layer.Cip, Ci, layer.cpg_shift, V, S, S, S,
+                                    flat.grad(conv.bias).data_ptr(), Co, layer.Cip, Ci, layer.cpg_shift, V, D, H, W,
                                     ws.data_ptr() if ws is not None else None, wsf, 0, code, s)
 
         for op in ops:

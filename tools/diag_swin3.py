@@ -18,3 +18,6 @@ errs = sorted(((rel2(p.grad, grads[n]), n) for n, p in m.model.named_parameters(
               reverse=True)
 for e, n in errs:
     print(f"{n:60s} {e:.3e}")
+got = torch.cat([p.grad.reshape(-1).double().cpu() for n, p in m.model.named_parameters() if grads[n].norm() > 0])
+want = torch.cat([grads[n].reshape(-1).double() for n, p in m.model.named_parameters() if grads[n].norm() > 0])
+print("all-gradient L2", ((got - want).norm() / want.norm()).item())
