@@ -198,6 +198,13 @@ int mmseg_instnorm_bwd(const void* x, int ldx, const float* mean, const float* r
                        float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
                        const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N, int D,
                        int H, int W, int C, int relu, float* ws, int dtype, void* stream);
+/* mmseg_instnorm_bwd with the partial sums [N][nchunk][C][2] (sum g, sum g * xhat per chunk, g = dy [xhat > 0])
+ * already emitted by the producer of dy (mmseg_head_loss_bwd_in): finalize + apply only; ws holds 2 N C floats. */
+int mmseg_instnorm_bwd_part(const void* x, int ldx, const float* mean, const float* rstd, const void* p1, int ld1,
+                            float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
+                            const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N,
+                            int D, int H, int W, int C, int relu, const float* part, int nchunk, float* ws,
+                            int dtype, void* stream);
 /* MaxPool3d(2) forward + argmax (0..7, z-major; first max wins) (unet.py:73). */
 int mmseg_maxpool2_fwd(const void* x, int ldx, void* y, int ldy, uint8_t* idx, int N, int D, int H, int W, int C,
                        int dtype, void* stream);
@@ -407,6 +414,18 @@ int mmseg_head_loss_bwd(const void* x, int ldx, int Cin, const float* nmean, con
                         float smooth, float alpha, float beta, int include_bg, const float* class_w, const float* gout,
                         float gconst, const float* ws, void* dx, int lddx, float* gW, float* gb, float* wpart,
                         int accumulate, int dtype, void* stream);
+/* mmseg_head_loss_bwd that also emits the InstanceNorm-backward partial sums of the block feeding the head
+ * (inpart: [N][mmseg_head_loss_in_chunks()][Cin][2], the layout mmseg_instnorm_bwd_part reads): sums of
+ * g = dx [h > 0] and g h per chunk, with h the head's input feature (the normalised, ReLU'd value) and dx the
+ * stored data gradient.  Cin == 32 only (mmseg_head_loss_in_chunks() returns 0 otherwise), dx required, dscale
+ * (Dropout3d) null. */
+int mmseg_head_loss_in_chunks(int C, int Cin, long long V);
+int mmseg_head_loss_bwd_in(const void* x, int ldx, int Cin, const float* nmean, const float* nrstd, const float* W,
+                           const float* b, const float* dscale, int C,
+                           int N, long long V, const void* labels, int label_bytes, int type, float dice_w, float ce_w,
+                           float smooth, float alpha, float beta, int include_bg, const float* class_w,
+                           const float* gout, float gconst, const float* ws, void* dx, int lddx, float* gW, float* gb,
+                           float* wpart, float* inpart, int accumulate, int dtype, void* stream);
 /* argmax + per-class intersection / pred / target counts (trainer.py:290-291, metrics.py:42-67). */
 int mmseg_dice_counts(const float* logits, const void* labels, int label_bytes, int N, int C, long long V,
                       unsigned long long* counts, void* pred_out, void* stream);

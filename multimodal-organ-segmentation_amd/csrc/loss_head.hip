@@ -828,8 +828,8 @@ __global__ __launch_bounds__(256) void head_loss_stats_kernel(const T* __restric
 }
 
 // wpart: per block [C*Cin + C] weight / bias gradient partials (head_wgrad_reduce sums them over the blocks)
-template <typename T, int G, int NC, typename LT>
-__global__ __launch_bounds__(256) void head_loss_bwd_kernel(const T* __restrict__ x, int ldx,
+template <typename T, int G, int NC, typename LT, bool DS>
+__global__ __launch_bounds__(256, (NC <= 6 && sizeof(T) == 2) ? 2 : 1) void head_loss_bwd_kernel(const T* __restrict__ x, int ldx,
                                                             const float* __restrict__ nmean,
                                                             const float* __restrict__ nrstd,
                                                             const float* __restrict__ Wt,
@@ -838,10 +838,18 @@ __global__ __launch_bounds__(256) void head_loss_bwd_kernel(const T* __restrict_
                                                             const LT* __restrict__ labels, long long V, long long vpc,
                                                             LossCfg cfg, const float* __restrict__ coef,
                                                             const float* __restrict__ gout, float gconst,
-                                                            T* __restrict__ dx, int lddx, float* __restrict__ wpart) {
+                                                            T* __restrict__ dx, int lddx, float* __restrict__ wpart,
+                                                            float* __restrict__ inpart) {
   constexpr int Cin = 8 * G, TN = (Cin + 15) / 16;
   static_assert(NC <= 8, "dlogits gather covers 8 classes");
+  // G == 4: MFMA row r of dx tile t is channel 8 (r >> 2) + 4 t + (r & 3), so lane group g ends up holding the
+  // gradient of channels 8g..8g+7 of its voxel -- the channels of its own feature load: one 16-B store per voxel
+  // (two 8-B stores otherwise), and the InstanceNorm-backward partial sums below need no lane exchange
+  constexpr bool PERM = (G == 4);
+  if constexpr (!DS) dscale = nullptr;   // no Dropout3d scale: the compiler drops the scale registers
+  auto dx_chan = [](int t, int r) { return PERM ? 8 * (r >> 2) + 4 * t + (r & 3) : 16 * t + r; };
   __shared__ float red[4][NC * Cin + NC];
+  __shared__ float ired[4][2][Cin];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, v16 = lane & 15, g = lane >> 4;
   const int n = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
   float nmu[8], nrs[8];
@@ -866,9 +874,9 @@ __global__ __launch_bounds__(256) void head_loss_bwd_kernel(const T* __restrict_
   for (int t = 0; t < TN; ++t)
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
-      const int ci = 16 * t + v16, c = 4 * g + kb;
+      const int ci = dx_chan(t, v16), c = 4 * g + kb;
       wD[t][kb] = (ci < Cin && c < C) ? Wt[c * Cin + ci] : 0.f;
-      const int co = 16 * t + 4 * g + kb;     // the output channel of register kb
+      const int co = dx_chan(t, 4 * g + kb);   // the output channel of register kb
       sd[t][kb] = (dscale && co < Cin) ? dscale[n * Cin + co] : 1.f;
     }
   const float gsc = gout ? gout[0] * gconst : gconst;
@@ -880,6 +888,12 @@ __global__ __launch_bounds__(256) void head_loss_bwd_kernel(const T* __restrict_
     for (int j = 0; j < 8; ++j) acc[c][j] = 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) bacc[r] = 0.f;
+  // InstanceNorm-backward partials of the block feeding the head (inpart, PERM only): sums of g and g * h over
+  // the block's voxels, g = dx * [h > 0], h the head's input feature (relu of the normalised value)
+  float sg[8], sgx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sg[j] = sgx[j] = 0.f;
+  const bool do_in = PERM && !DS && inpart != nullptr;   // (with the Dropout3d scale the registers run out)
   const long long v0 = (long long)chunk * vpc;
   const long long v1 = v0 + vpc < V ? v0 + vpc : V;
   const long long base = (long long)n * V;
@@ -955,6 +969,27 @@ __global__ __launch_bounds__(256) void head_loss_bwd_kernel(const T* __restrict_
       bacc[r] += d[r];
     }
     // dx^T = W^T dlogits^T (exact fp32 MFMA), 4 channels of voxel v per lane and 16-channel tile
+    if constexpr (PERM) {
+      V8<T> dv;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) o = __builtin_amdgcn_mfma_f32_16x16x4f32(wD[t][kb], d[kb], o, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dv.set(4 * t + r, dscale ? o[r] * sd[t][r] : o[r]);
+      }
+      if (dx && ok) dv.store(dx + (base + v) * lddx + 8 * g);
+      if (do_in && ok) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float h = ld.a.get(j);
+          const float gg = h > 0.f ? dv.get(j) : 0.f;
+          sg[j] += gg;
+          sgx[j] = fmaf(gg, h, sgx[j]);
+        }
+      }
+    } else
 #pragma unroll
     for (int t = 0; t < TN; ++t) {
       f32x4 o = {0.f, 0.f, 0.f, 0.f};
@@ -1007,8 +1042,29 @@ __global__ __launch_bounds__(256) void head_loss_bwd_kernel(const T* __restrict_
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       if (4 * g + r < NC) red[wave][NC * Cin + 4 * g + r] = bacc[r];
+  if (do_in) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sg[j] += __shfl_xor(sg[j], o, 64);
+        sgx[j] += __shfl_xor(sgx[j], o, 64);
+      }
+    if (v16 == 0)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        ired[wave][0][8 * g + j] = sg[j];
+        ired[wave][1][8 * g + j] = sgx[j];
+      }
+  }
   __syncthreads();
   const long long blk = (long long)n * nchunk + chunk;
+  if (do_in && threadIdx.x < Cin) {   // in the layout of norm_pool.hip in_bwd_partial: [n][chunk][c][2]
+    const int c = threadIdx.x;
+    float* ip = inpart + (blk * Cin + c) * 2;
+    ip[0] = ired[0][0][c] + ired[1][0][c] + ired[2][0][c] + ired[3][0][c];
+    ip[1] = ired[0][1][c] + ired[1][1][c] + ired[2][1][c] + ired[3][1][c];
+  }
   const int npairs = C * Cin + C;
   for (int k = threadIdx.x; k < npairs; k += blockDim.x) {
     const int src = k < C * Cin ? k : NC * Cin + (k - C * Cin);
@@ -1370,14 +1426,41 @@ int mmseg_head_loss_fwd(const void* x, int ldx, int Cin, const float* nmean, con
 
 // After mmseg_head_loss_fwd with the same ws.  dx may alias x (each voxel's features are read before its
 // gradient is written); dx null skips the data gradient.  gW [C][Cin] / gb [C] (=, or += with accumulate).
+int mmseg_head_loss_bwd_in(const void* x, int ldx, int Cin, const float* nmean, const float* nrstd, const float* W,
+                           const float* b, const float* dscale, int C,
+                           int N, long long V, const void* labels, int label_bytes, int type, float dice_w, float ce_w,
+                           float smooth, float alpha, float beta, int include_bg, const float* class_w,
+                           const float* gout, float gconst, const float* ws, void* dx, int lddx, float* gW, float* gb,
+                           float* wpart, float* inpart, int accumulate, int dtype, void* stream);
+
 int mmseg_head_loss_bwd(const void* x, int ldx, int Cin, const float* nmean, const float* nrstd, const float* W,
                         const float* b, const float* dscale, int C,
                         int N, long long V, const void* labels, int label_bytes, int type, float dice_w, float ce_w,
                         float smooth, float alpha, float beta, int include_bg, const float* class_w, const float* gout,
                         float gconst, const float* ws, void* dx, int lddx, float* gW, float* gb, float* wpart,
                         int accumulate, int dtype, void* stream) {
+  return mmseg_head_loss_bwd_in(x, ldx, Cin, nmean, nrstd, W, b, dscale, C, N, V, labels, label_bytes, type, dice_w,
+                                ce_w, smooth, alpha, beta, include_bg, class_w, gout, gconst, ws, dx, lddx, gW, gb,
+                                wpart, nullptr, accumulate, dtype, stream);
+}
+
+int mmseg_head_loss_in_chunks(int C, int Cin, long long V) {
+  if (Cin != 32 || C < 2 || C > 8) return 0;
+  long long vpc;
+  return loss_chunks(V, &vpc);
+}
+
+int mmseg_head_loss_bwd_in(const void* x, int ldx, int Cin, const float* nmean, const float* nrstd, const float* W,
+                           const float* b, const float* dscale, int C,
+                           int N, long long V, const void* labels, int label_bytes, int type, float dice_w, float ce_w,
+                           float smooth, float alpha, float beta, int include_bg, const float* class_w,
+                           const float* gout, float gconst, const float* ws, void* dx, int lddx, float* gW, float* gb,
+                           float* wpart, float* inpart, int accumulate, int dtype, void* stream) {
   MMSEG_REQUIRE(mmseg_head_loss_ok(C, Cin, ldx, dtype) && (dx == nullptr || lddx % 8 == 0),
                 "head_loss_bwd: unsupported shape (C=%d, Cin=%d, ldx=%d, lddx=%d)", C, Cin, ldx, lddx);
+  MMSEG_REQUIRE(!inpart || (mmseg_head_loss_in_chunks(C, Cin, V) > 0 && dx != nullptr && !dscale),
+                "head_loss_bwd: InstanceNorm partials need Cin == 32, dx and no Dropout3d scale (C=%d, Cin=%d)", C,
+                Cin);
   MMSEG_REQUIRE(!nmean || dx != x, "head_loss_bwd: with the deferred norm x is the pre-norm input the "
                 "InstanceNorm backward still reads; dx must not alias it");
   LossCfg cfg{type, dice_w, ce_w, smooth, alpha, beta, include_bg, class_w};
@@ -1390,9 +1473,14 @@ int mmseg_head_loss_bwd(const void* x, int ldx, int Cin, const float* nmean, con
     using LT = decltype(lt);
     constexpr int G = decltype(g_c)::value, NC = decltype(nc_c)::value;
     mmseg::note_kernel("head_loss_bwd_kernel");
-    hipLaunchKernelGGL((head_loss_bwd_kernel<T, G, NC, LT>), dim3(nch, N), dim3(256), 0, s, (const T*)x, ldx, nmean,
-                       nrstd, W, b, dscale, C, (const LT*)labels, V, vpc, cfg, coef, gout, gconst, (T*)dx, lddx,
-                       wpart);
+    if (dscale)
+      hipLaunchKernelGGL((head_loss_bwd_kernel<T, G, NC, LT, true>), dim3(nch, N), dim3(256), 0, s, (const T*)x, ldx,
+                         nmean, nrstd, W, b, dscale, C, (const LT*)labels, V, vpc, cfg, coef, gout, gconst, (T*)dx,
+                         lddx, wpart, inpart);
+    else
+      hipLaunchKernelGGL((head_loss_bwd_kernel<T, G, NC, LT, false>), dim3(nch, N), dim3(256), 0, s, (const T*)x,
+                         ldx, nmean, nrstd, W, b, dscale, C, (const LT*)labels, V, vpc, cfg, coef, gout, gconst,
+                         (T*)dx, lddx, wpart, inpart);
   });
   if (mmseg::check_launch("head_loss_bwd")) return 1;
   hipLaunchKernelGGL(head_wgrad_reduce, dim3(ceil_div(C * Cin + C, 4)), dim3(256), 0, s, wpart, N * nch, C, Cin, gW,

@@ -1301,11 +1301,29 @@ int mmseg_instnorm_relu_bwd(const void* x, int ldx, const float* mean, const flo
                             pool_ld, pool_idx, dx, lddx, N, D, H, W, C, 1, ws, dtype, stream);
 }
 
+int mmseg_instnorm_bwd_part(const void* x, int ldx, const float* mean, const float* rstd, const void* p1, int ld1,
+                            float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
+                            const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N,
+                            int D, int H, int W, int C, int relu, const float* part_in, int nchunk_in, float* ws,
+                            int dtype, void* stream);
+
 int mmseg_instnorm_bwd(const void* x, int ldx, const float* mean, const float* rstd, const void* p1, int ld1,
                             float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
                             const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N,
                             int D, int H, int W, int C, int relu, float* ws, int dtype, void* stream) {
+  return mmseg_instnorm_bwd_part(x, ldx, mean, rstd, p1, ld1, scale1, alpha1, alpha_stride, beta, beta_stride, pool_dy,
+                                 pool_ld, pool_idx, dx, lddx, N, D, H, W, C, relu, nullptr, 0, ws, dtype, stream);
+}
+
+// mmseg_instnorm_bwd whose partial sums (g, g * xhat per chunk, [N][nchunk_in][C][2]) a producer of dy already
+// emitted (the fused head + loss backward, mmseg_head_loss_bwd_in): the partial pass is skipped.
+int mmseg_instnorm_bwd_part(const void* x, int ldx, const float* mean, const float* rstd, const void* p1, int ld1,
+                            float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
+                            const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N,
+                            int D, int H, int W, int C, int relu, const float* part_in, int nchunk_in, float* ws,
+                            int dtype, void* stream) {
   MMSEG_REQUIRE(C % 8 == 0 && C <= 2048, "instnorm_bwd: C=%d must be a multiple of 8 and <= 2048", C);
+  MMSEG_REQUIRE(!part_in || nchunk_in > 0, "instnorm_bwd: given partials need their chunk count");
   MMSEG_REQUIRE(!pool_dy || ((D | H | W) & 1) == 0, "instnorm_bwd: pooled gather needs even dims");
   const long long V = (long long)D * H * W;
   MMSEG_REQUIRE(V * (ldx > lddx ? ldx : lddx) < (1LL << 31) && V * (ld1 > pool_ld ? ld1 : pool_ld) < (1LL << 31),
@@ -1319,10 +1337,17 @@ int mmseg_instnorm_bwd(const void* x, int ldx, const float* mean, const float* r
   float* part = ws;
   float* coef = ws + (long long)N * nch * C * 2;
   dim3 grid(nch, N), agrid(anch, N);
-  const bool small = V <= knob_small_v();
+  const bool small = V <= knob_small_v() && !part_in;
+  if (part_in) coef = ws;
   auto run = [&](auto tag, auto relu_c) {
     using T = decltype(tag);
     constexpr bool R = decltype(relu_c)::value;
+    if (part_in) {
+      hipLaunchKernelGGL(in_bwd_finalize, dim3(N * C), dim3(256), 0, s, part_in, N, C, nchunk_in, V, coef);
+      hipLaunchKernelGGL((in_bwd_apply<T, R>), agrid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, coef,
+                         (T*)dx, lddx, (int)V, C, D, H, W, avpc);
+      return;
+    }
     if (small) {
       if (knob_small_t() == 1024)
         hipLaunchKernelGGL((in_small_bwd_1k<T, R>), dim3(C / 8, N), dim3(SMALL_T1K), 0, s, (const T*)x, ldx, mean, rstd,

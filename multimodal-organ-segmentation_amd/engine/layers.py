@@ -126,6 +126,9 @@ class DySpec:
     beta_stride: int = 0
     pool_dy: Optional[Act] = None
     pool_idx: Optional[torch.Tensor] = None
+    # (partials, nchunk): the InstanceNorm-backward partial sums [N][nchunk][C][2] the producer of p1 already
+    # emitted (fused head + loss backward), so the partial pass over x and dy is skipped
+    part: Optional[Tuple[torch.Tensor, int]] = None
 
 
 class Conv3:
@@ -473,6 +476,13 @@ class Block:
         es = 4
         alpha = None if dy.alpha is None else dy.alpha.data_ptr() + dy.alpha_off * es
         beta = None if dy.beta is None else dy.beta.data_ptr() + dy.beta_off * es
+        if dy.part is not None:
+            assert dy.pool_dy is None and alpha is None and beta is None
+            part, nch = dy.part
+            L.mmseg_instnorm_bwd_part(x.ptr, x.ld, ptr(m), ptr(r), p1.ptr, p1.ld, dy.scale1, None, 0, None, 0,
+                                      None, 0, None, dx.ptr, dx.ld, x.N, x.D, x.H, x.W, x.C, 1, ptr(part), nch,
+                                      ptr(ws), code, s)
+            return
         L.mmseg_instnorm_relu_bwd(x.ptr, x.ld, ptr(m), ptr(r),
                                   p1.ptr if p1 is not None else None, p1.ld if p1 is not None else 0, dy.scale1,
                                   alpha, dy.alpha_stride, beta, dy.beta_stride,
@@ -568,16 +578,26 @@ class Head:
         self.loss_state = (labels, args, ws, cw, dscale, (nm, nr))
         return loss, ws
 
-    def bwd_loss(self, x: Act, gout: torch.Tensor, dx: Optional[Act], accumulate: bool):
-        """dlogits (recomputed) -> head data + weight gradient, after fwd_loss."""
+    def in_chunks(self, x: Act) -> int:
+        """Chunks per sample of the InstanceNorm-backward partials bwd_loss can emit for the block feeding the head
+        (0: not available for this shape or with a Dropout3d scale, or switched off with MMSEG_HEAD_IN_PART=0).
+        Call between fwd_loss and bwd_loss."""
+        if os.environ.get("MMSEG_HEAD_IN_PART", "1") == "0" or self.loss_state[4] is not None:   # Dropout3d scale
+            return 0
+        return int(self.rt.lib.mmseg_head_loss_in_chunks(self.C, self.Cin, x.V))
+
+    def bwd_loss(self, x: Act, gout: torch.Tensor, dx: Optional[Act], accumulate: bool,
+                 inpart: Optional[torch.Tensor] = None):
+        """dlogits (recomputed) -> head data + weight gradient, after fwd_loss.  inpart: also write the
+        InstanceNorm-backward partial sums of the head's input block ([N][in_chunks()][Cin][2])."""
         L = self.rt.lib
         labels, args, ws, cw, dscale, (nm, nr) = self.loss_state
         wpart = self.rt.ws(L.mmseg_head_loss_wpart_floats(self.C, self.Cin, x.N, x.V))
-        L.mmseg_head_loss_bwd(x.ptr, x.ld, self.Cin, nm, nr, ptr(self.conv.weight), ptr(self.conv.bias), ptr(dscale),
-                              self.C, x.N, x.V, ptr(labels), labels.element_size(), *args, ptr(gout), 1.0, ptr(ws),
-                              dx.ptr if dx is not None else None, dx.ld if dx is not None else 0,
-                              ptr(self.flat.grad(self.conv.weight)), ptr(self.flat.grad(self.conv.bias)), ptr(wpart),
-                              int(accumulate), self.rt.code, self.rt.stream)
+        L.mmseg_head_loss_bwd_in(x.ptr, x.ld, self.Cin, nm, nr, ptr(self.conv.weight), ptr(self.conv.bias),
+                                 ptr(dscale), self.C, x.N, x.V, ptr(labels), labels.element_size(), *args, ptr(gout),
+                                 1.0, ptr(ws), dx.ptr if dx is not None else None, dx.ld if dx is not None else 0,
+                                 ptr(self.flat.grad(self.conv.weight)), ptr(self.flat.grad(self.conv.bias)),
+                                 ptr(wpart), ptr(inpart), int(accumulate), self.rt.code, self.rt.stream)
         self.flat.mark(self.conv.weight, self.conv.bias)
         self.loss_state = None
 

@@ -113,15 +113,24 @@ class _Decoder:
         nl = len(self.F) - 1
         self.split_bwd = os.environ.get("MMSEG_SPLIT_DCAT", "1") != "0"
         dh = self.dout[0]
+        hpart = None
         if gout is not None:
             hx = self.blocks[nl - 1].out_stats()[0] if self.defer_head else self.dout[0]
-            self.head.bwd_loss(hx, gout, dh, accumulate)
+            # the head backward also sums the last block's InstanceNorm-backward partials (no partial pass over
+            # its 113 MB x2 + dy at 96^3 B=2)
+            nch = self.head.in_chunks(hx)
+            if nch:
+                size = hx.N * nch * hx.C * 2
+                if getattr(self, "_hpart", None) is None or self._hpart.numel() != size:
+                    self._hpart = torch.empty(size, dtype=torch.float32, device=self.rt.device)
+                hpart = (self._hpart, nch)
+            self.head.bwd_loss(hx, gout, dh, accumulate, inpart=hpart[0] if hpart else None)
         else:
             self.head.bwd(self.dout[0], dlogits, dh, accumulate)
         for j in reversed(range(nl)):
             l = nl - 1 - j
             dcat = self.dsplit[l] if self.split_bwd else self.cat[l]                  # aliases cat
-            self.blocks[j].bwd(self.cat[l], DySpec(p1=dh), dcat, accumulate)
+            self.blocks[j].bwd(self.cat[l], DySpec(p1=dh, part=hpart if j == nl - 1 else None), dcat, accumulate)
             x_up = bottom if j == 0 else self.dout[l + 1]
             dup = self.dsplit[l][0] if self.split_bwd else self.cat[l].slot(0, self.F[l])
             self.ups[j].bwd(x_up, dup, x_up, accumulate)   # dd aliases x_up

@@ -386,6 +386,44 @@ def test_deferred_conv_norm_bitwise(dev, model, wgrad_dma, monkeypatch):
     assert torch.equal(res[0][1], res[1][1])
 
 
+@pytest.mark.parametrize("defer_head", ["1", "0"])
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("model", ["unet", "dual_encoder"])
+def test_head_in_partials(dev, model, dtype, defer_head, monkeypatch):
+    """32-channel top level: the fused head + loss backward also sums the last decoder block's InstanceNorm-backward
+    partials (mmseg_head_loss_bwd_in -> mmseg_instnorm_bwd_part, no partial pass).  Same loss bits; gradients
+    equal to the two-pass path (MMSEG_HEAD_IN_PART=0) up to the summation order of those partials (fp32 1e-5,
+    bf16 1e-2 normwise: a bf16 activation rounding on the other side moves by one ulp); the head's own weight
+    gradient is untouched (bitwise)."""
+    from mmseg_amd.engine.engine import fused_loss_supported, run_engine_loss
+    from mmseg_amd.trainer.losses import DiceCELoss
+    gen = torch.Generator().manual_seed(9)
+    x = torch.randn(2, 2, 32, 32, 32, generator=gen).to(dev)
+    y = torch.randint(0, 3, (2, 32, 32, 32), generator=gen).to(dev)
+    monkeypatch.setenv("MMSEG_DEFER_HEAD_NORM", defer_head)
+    res = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("MMSEG_HEAD_IN_PART", fused)
+        cfg = make_config(model, ["CT", "PET"], 3, [32, 64, 128], dtype=dtype)
+        torch.manual_seed(0)
+        m = build_model(cfg).to(dev)
+        m.train()
+        assert fused_loss_supported(m.backbone, model, x)
+        loss = run_engine_loss(m.backbone, model, x, y, DiceCELoss()._spec(), None)
+        loss.backward()
+        torch.cuda.synchronize()
+        prog = m.backbone.__dict__["_engine"].program
+        assert (getattr(prog.dec, "_hpart", None) is not None) == (fused == "1")
+        head = [p.grad.reshape(-1).clone() for n, p in m.named_parameters() if "out_conv" in n]
+        res.append((loss.detach().clone(), torch.cat([p.grad.reshape(-1) for p in m.parameters()]).clone(), head))
+    assert torch.equal(res[0][0], res[1][0])
+    for a, b in zip(res[0][2], res[1][2]):
+        assert torch.equal(a, b)
+    a, b = res[0][1].double(), res[1][1].double()
+    err = ((a - b).norm() / b.norm()).item()
+    assert err < (1e-5 if dtype == "float32" else 1e-2), err
+
+
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
 def test_deferred_encoder_norm_bitwise(dev, dtype, monkeypatch):
     """DualEncoder mean fusion: the encoders' output InstanceNorm + ReLU applied on load by the maxpool and the
