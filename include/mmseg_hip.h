@@ -65,6 +65,15 @@ int mmseg_pack_conv3_batched(const void* descs, int n, int nblocks, int dtype, v
 int mmseg_pack_desc_bytes(void);
 int mmseg_pack_weights_batched(const void* descs, int n, long long total, int dtype, void* stream);
 
+/* CONV3 data gradient (ksplit 1, no bias) that also writes the InstanceNorm-backward partial sums of its output:
+ * the output is dy of an InstanceNorm + ReLU with pre-norm input inx (pitch ldinx) and statistics inmean /
+ * inrstd [N][Ncols]; inpart [N][mmseg_conv3_dgrad_in_chunks()][Ncols][2] = (sum g, sum g xhat), g = dy [xhat > 0],
+ * the layout mmseg_instnorm_bwd_part reads.  bf16, the brick5 kernel's shapes only (chunks 0 otherwise). */
+int mmseg_conv3_dgrad_in_chunks(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda,
+                                int ldo, int dtype);
+int mmseg_conv3_dgrad_in(const void* a, int lda, const void* wpacked, void* out, int ldo, int M, int Ncols, int Cpad,
+                         int KG, int cpg_shift, int D, int H, int W, const void* inx, int ldinx, const float* inmean,
+                         const float* inrstd, float* inpart, int dtype, void* stream);
 /* Split count the CONV3 kernel choice wants for this shape (value-returning, not a status): the caller
  * allocates ksplit*M*Ncols fp32 of split-K workspace and passes ksplit to mmseg_conv_gemm. */
 int mmseg_conv3_splits(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,

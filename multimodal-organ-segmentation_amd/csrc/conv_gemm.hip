@@ -62,6 +62,14 @@ struct GemmArgs {
   // [voxel][2F] tensor whose halves every later reader fetched at half a cache line per voxel.
   void* out2;
   int ldo2, split;
+  // InstanceNorm-backward partials of the output (brick5 data gradient only, mmseg_conv3_dgrad_in): the output is
+  // the gradient dy of an InstanceNorm + ReLU whose PRE-norm input is inx (pitch ldinx, statistics inmean /
+  // inrstd [N][Ncols]); the kernel also writes inpart[n][block][col][2] = (sum g, sum g xhat), g = dy [xhat > 0]
+  const void* inx;
+  int ldinx;
+  const float* inmean;
+  const float* inrstd;
+  float* inpart;
 };
 
 // Output element (row voxel, column) of a GEMM (split-aware; split is a multiple of 8).
@@ -1225,7 +1233,9 @@ __global__ __launch_bounds__(256, 1) void conv3_brick4_kernel(GemmArgs g, int up
 // channel group kg at slot kg ^ (((hx >> 2) & 1) << 1), which makes the 16-lane groups of ds_read_b128
 // conflict-free for all three kx shifts; rows of 18 voxels, no padding.
 // Requirements (host): bf16, one 32-channel K chunk, Ncols % 32 == 0, D % 4, H % 4, W % 16, no fused stats.
-template <bool DBG = false, bool DMA = false>
+// INP (with DMA: the halo staging registers are free for it): the epilogue also sums the InstanceNorm-backward
+// partials of its output (GemmArgs::inpart); x of the brick is loaded during the brick's MFMA groups 4..5.
+template <bool DBG = false, bool DMA = false, bool INP = false>
 __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int upb, int blocks_per_nt,
                                                               long long* dbg = nullptr) {
   using T = bf16_t;
@@ -1410,11 +1420,64 @@ __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int up
     for (int r = 0; r < 4; ++r) bv[j][r] = g.bias ? g.bias[n0 + 8 * kg + 4 * j + r] : 0.f;
   T* O = reinterpret_cast<T*>(g.out);
 
+  // InstanceNorm-backward partials (INP): per lane the sums over its voxels of g and g (x - mean) for its 8
+  // channels n0 + 8 kg + (0..7) (times rstd at the flush), g = dy if x > mean (xhat > 0; rstd > 0) else 0
+  float isg[8], isgx[8], imu[8];
+  int in_n = -1;
+  V8<T> xin[BY];
+  __shared__ float ired[INP ? 4 : 1][2][32];
+  if constexpr (INP) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) isg[k] = isgx[k] = 0.f;
+  }
+  // block-wide: the sums of sample in_n -> inpart[in_n][blk][n0 + c] (fixed order: 16-lane tree, then waves 0..3)
+  auto in_flush = [&]() {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        isg[k] += __shfl_xor(isg[k], o, 64);
+        isgx[k] += __shfl_xor(isgx[k], o, 64);
+      }
+    if (r16 == 0)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        ired[wave][0][8 * kg + k] = isg[k];
+        ired[wave][1][8 * kg + k] = isgx[k];
+      }
+    __syncthreads();
+    if (tid < 32) {
+      const float a = ired[0][0][tid] + ired[1][0][tid] + ired[2][0][tid] + ired[3][0][tid];
+      const float c = ired[0][1][tid] + ired[1][1][tid] + ired[2][1][tid] + ired[3][1][tid];
+      float* p = g.inpart + (((long long)in_n * blocks_per_nt + blk) * g.Ncols + n0 + tid) * 2;
+      p[0] = a;
+      p[1] = c * g.inrstd[in_n * g.Ncols + n0 + tid];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) isg[k] = isgx[k] = 0.f;
+  };
+  auto in_load = [&](const Unit& q) {   // x of the lane's 4 output voxels (consumed by the brick's epilogue)
+    const T* X = reinterpret_cast<const T*>(g.inx) + (long long)q.n * vox_per_n * g.ldinx + n0 + 8 * kg;
+#pragma unroll
+    for (int i = 0; i < BY; ++i)
+      xin[i].load(X + (long long)((q.z0 + wave) * g.H + q.y0 + i) * g.W * g.ldinx +
+                  (long long)(q.x0 + r16) * g.ldinx);
+  };
+
   // epilogue of a finished brick (ev = its accumulators, copied out of the AGPRs): lane holds channels
   // n0 + 8*kg + 4*j + (0..3) of voxel (z0 + wave, y0 + i, x0 + r16): one 16-B store per row tile
   f32x4 ev[BY][RN];
   auto epilogue = [&](const Unit& q) {
     const long long obase = (long long)q.n * vox_per_n;
+    if constexpr (INP) {
+      if (q.n != in_n) {   // block-uniform
+        if (in_n >= 0) in_flush();
+        in_n = q.n;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) imu[k] = g.inmean[in_n * g.Ncols + n0 + 8 * kg + k];
+      }
+    }
 #pragma unroll
     for (int i = 0; i < BY; ++i) {
       const int z = q.z0 + wave, y = q.y0 + i, x = q.x0 + r16;
@@ -1425,6 +1488,15 @@ __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int up
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[4 * j + r] = (bf16_t)(ev[i][j][r] + bv[j][r]);
       *reinterpret_cast<bf16x8*>(dst) = o;
+      if constexpr (INP) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float d = xin[i].get(k) - imu[k];
+          const float gg = d > 0.f ? (float)o[k] : 0.f;
+          isg[k] += gg;
+          isgx[k] = fmaf(gg, d, isgx[k]);
+        }
+      }
     }
   };
   Unit cur = unit_of(u_begin), prev = cur;
@@ -1490,6 +1562,9 @@ __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int up
         }
       }
       if (q == 5) stamp();
+      if constexpr (INP) {
+        if (q == 4) in_load(cur);
+      }
       __builtin_amdgcn_sched_barrier(0);   // keep the next group's reads ahead of this group's MFMAs
       // the previous brick's outputs: their VALU work and stores fill the first group's MFMA shadow
       if (q == 0 && u > u_begin) epilogue(prev);
@@ -1516,6 +1591,7 @@ __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int up
     cur = nxt;
   }
   epilogue(prev);
+  if constexpr (INP) in_flush();
 }
 
 // ------------------------------------- runtime-brick conv (small volumes)
@@ -1895,6 +1971,11 @@ int launch_brick5(const GemmArgs& g, hipStream_t s, long long* dbg, bool dma) {
   const int bpn5 = ceil_div(nb5, upb5);
   mmseg::note_kernel("conv3_brick5_kernel<BN32>");
   const dim3 grid(bpn5 * nt_n), block(256);
+  if (g.inpart) {   // samples a block does not touch keep zero partials
+    hipMemsetAsync(g.inpart, 0, sizeof(float) * 2 * (size_t)(g.M / (g.D * g.H * g.W)) * bpn5 * g.Ncols, s);
+    hipLaunchKernelGGL((conv3_brick5_kernel<false, true, true>), grid, block, 0, s, g, upb5, bpn5, nullptr);
+    return upb5;
+  }
   if (dbg && dma) hipLaunchKernelGGL((conv3_brick5_kernel<true, true>), grid, block, 0, s, g, upb5, bpn5, dbg);
   else if (dbg) hipLaunchKernelGGL((conv3_brick5_kernel<true, false>), grid, block, 0, s, g, upb5, bpn5, dbg);
   else if (dma) hipLaunchKernelGGL((conv3_brick5_kernel<false, true>), grid, block, 0, s, g, upb5, bpn5, nullptr);
@@ -4312,6 +4393,45 @@ int mmseg_conv3_fwd_norm(const void* a, int lda, const float* nmean, const float
   GemmArgs g{a, lda, wpacked, bias, out, ldo, nullptr, M, Ncols, Cpad, KG, cpg_shift, D, H, W, 1, KGp,
              knob("MMSEG_SWIZZLE", 1), nullptr, 0, nmean, nrstd};
   return launch_gemm<bf16_t, MODE_CONV3>(g, (hipStream_t)stream);
+}
+
+// Chunks per sample of the InstanceNorm-backward partials mmseg_conv3_dgrad_in writes for this CONV3 data-gradient
+// shape (the brick5 kernel's blocks per column tile), or 0 when that kernel does not run it.
+int mmseg_conv3_dgrad_in_chunks(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda,
+                                int ldo, int dtype) {
+  if (dtype != MMSEG_BF16) return 0;
+  GemmArgs g{};
+  g.lda = lda; g.ldo = ldo; g.M = M; g.Ncols = Ncols; g.Cpad = Cpad; g.KG = KG; g.cpg_shift = cpg_shift;
+  g.D = D; g.H = H; g.W = W; g.ksplit = 1;
+  g.out = reinterpret_cast<void*>(static_cast<uintptr_t>(256));   // the caller's output is 16-B aligned (checked)
+  if (!brick5_selected(g, 2)) return 0;
+  const int nt_n = Ncols / 32;
+  const int per_nt = std::max(1, knob("MMSEG_BRICK4_BLOCKS", 256) / nt_n);
+  const int nb5 = (M / (D * H * W)) * (D / 4) * (H / 4) * (W / 16);
+  const int upb5 = ceil_div(nb5, std::min(per_nt, nb5));
+  return ceil_div(nb5, upb5);
+}
+
+// CONV3 data gradient (mmseg_conv_gemm_ex, ksplit 1, no bias) whose output dy feeds the backward of an InstanceNorm +
+// ReLU with pre-norm input inx (pitch ldinx) and statistics inmean / inrstd [N][Ncols]: the kernel also writes that
+// backward's partial sums inpart [N][mmseg_conv3_dgrad_in_chunks()][Ncols][2] (the layout mmseg_instnorm_bwd_part
+// reads), so its partial pass over x and dy is skipped.
+int mmseg_conv3_dgrad_in(const void* a, int lda, const void* wpacked, void* out, int ldo, int M, int Ncols, int Cpad,
+                         int KG, int cpg_shift, int D, int H, int W, const void* inx, int ldinx, const float* inmean,
+                         const float* inrstd, float* inpart, int dtype, void* stream) {
+  MMSEG_REQUIRE(inx && inmean && inrstd && inpart && ldinx % 8 == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
+                    mmseg_conv3_dgrad_in_chunks(M, Ncols, Cpad, KG, cpg_shift, D, H, W, lda, ldo, dtype) > 0,
+                "conv3_dgrad_in: unsupported shape (mmseg_conv3_dgrad_in_chunks)");
+  const int KGp = (KG + 3) & ~3;
+  GemmArgs g{a, lda, wpacked, nullptr, out, ldo, nullptr, M, Ncols, Cpad, KG, cpg_shift, D, H, W, 1, KGp,
+             knob("MMSEG_SWIZZLE", 1), nullptr, 0, nullptr, nullptr};
+  g.inx = inx;
+  g.ldinx = ldinx;
+  g.inmean = inmean;
+  g.inrstd = inrstd;
+  g.inpart = inpart;
+  launch_brick5(g, (hipStream_t)stream, nullptr, true);
+  return mmseg::check_launch("conv3_dgrad_in");
 }
 
 // Number of K splits the CONV3 path wants for this shape (callers size the

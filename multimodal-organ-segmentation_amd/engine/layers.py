@@ -246,9 +246,12 @@ class Conv3:
                                              self.cpg_shift, x.D, x.H, x.W, self.rt.code, self.rt.stream)
 
     def bwd(self, x: Act, dy: Act, dx: Optional[Act], accumulate: bool,
-            norm: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
+            norm: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+            inp: Optional[Tuple[Act, torch.Tensor, torch.Tensor]] = None):
         """norm = (mean, rstd): x is the pre-norm activation of an InstanceNorm + ReLU applied on staging by the
-        weight-gradient kernel (see fwd_norm)."""
+        weight-gradient kernel (see fwd_norm).  inp = (pre-norm x, mean, rstd) of the InstanceNorm + ReLU whose
+        output gradient dx is: when the data-gradient kernel can, it also writes that backward's partial sums;
+        returns (partials, chunks) for DySpec.part, or None."""
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
         V = x.N * x.V
         if dx is None and norm is None and self._stem(x, dy.ld):
@@ -300,6 +303,19 @@ class Conv3:
             ws = self.rt.ws(ks * M * nc) if ks > 1 else None
             with TIMER.region(_gemm_name(self.rt, nc, "conv3"), flops=2.0 * M * self.Co * 27 * self.Ci,
                               nbytes=_io_bytes(self.rt, M, self.Co, self.Cip, 27 * self.Cip * self.Co)):
+                nch = 0
+                if inp is not None and not split and ks == 1 and os.environ.get("MMSEG_DGRAD_IN_PART", "1") != "0":
+                    nch = L.mmseg_conv3_dgrad_in_chunks(M, nc, self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W,
+                                                        dy.ld, dx.ld, code)
+                if nch:
+                    xi, im, ir = inp
+                    size = x.N * nch * nc * 2
+                    if getattr(self, "_inpart", None) is None or self._inpart.numel() != size:
+                        self._inpart = torch.empty(size, dtype=torch.float32, device=self.rt.device)
+                    L.mmseg_conv3_dgrad_in(dy.ptr, dy.ld, ptr(self.wd), dx.ptr, dx.ld, M, nc, self.Cpad_d, self.KGd,
+                                           self.dshift, x.D, x.H, x.W, xi.ptr, xi.ld, ptr(im), ptr(ir),
+                                           ptr(self._inpart), code, s)
+                    return self._inpart, nch
                 if split:
                     L.mmseg_conv_gemm_split(dy.ptr, dy.ld, ptr(self.wd), None, d0.ptr, d0.ld, dx[1].ptr, dx[1].ld,
                                             d0.C, ptr(ws), MODE_CONV3, M, nc, self.Cpad_d, self.KGd, self.dshift, x.D,
@@ -536,12 +552,14 @@ class Block:
         g2 = self.x2                      # in place over x2
         self._norm_bwd(self.x2, st[2], st[3], dy, g2)
         dy1 = self.y1                     # conv2 wgrad reads y1 before dgrad overwrites it
+        # conv2's data gradient may also sum conv1's InstanceNorm-backward partials (brick5 shapes)
+        inp = (self.x1, st[0], st[1])
         if self.defer1:                   # (y1 was never written: the weight gradient normalises x1 itself)
-            self.c2.bwd(self.x1, g2, dy1, accumulate, norm=(st[0], st[1]))
+            part = self.c2.bwd(self.x1, g2, dy1, accumulate, norm=(st[0], st[1]), inp=inp)
         else:
-            self.c2.bwd(self.y1, g2, dy1, accumulate)
+            part = self.c2.bwd(self.y1, g2, dy1, accumulate, inp=inp)
         g1 = self.x1
-        self._norm_bwd(self.x1, st[0], st[1], DySpec(p1=dy1), g1)
+        self._norm_bwd(self.x1, st[0], st[1], DySpec(p1=dy1, part=part), g1)
         self.c1.bwd(xin, g1, dxin, accumulate)
 
 

@@ -386,15 +386,18 @@ def test_deferred_conv_norm_bitwise(dev, model, wgrad_dma, monkeypatch):
     assert torch.equal(res[0][1], res[1][1])
 
 
-@pytest.mark.parametrize("defer_head", ["1", "0"])
+@pytest.mark.parametrize("knob,defer_head", [("MMSEG_HEAD_IN_PART", "1"), ("MMSEG_HEAD_IN_PART", "0"),
+                                             ("MMSEG_DGRAD_IN_PART", "1")])
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
 @pytest.mark.parametrize("model", ["unet", "dual_encoder"])
-def test_head_in_partials(dev, model, dtype, defer_head, monkeypatch):
-    """32-channel top level: the fused head + loss backward also sums the last decoder block's InstanceNorm-backward
-    partials (mmseg_head_loss_bwd_in -> mmseg_instnorm_bwd_part, no partial pass).  Same loss bits; gradients
-    equal to the two-pass path (MMSEG_HEAD_IN_PART=0) up to the summation order of those partials (fp32 1e-5,
-    bf16 1e-2 normwise: a bf16 activation rounding on the other side moves by one ulp); the head's own weight
-    gradient is untouched (bitwise)."""
+def test_head_in_partials(dev, model, dtype, knob, defer_head, monkeypatch):
+    """32-channel top level: InstanceNorm-backward partial sums emitted by the producer of dy instead of a partial
+    pass over x and dy -- by the fused head + loss backward for the last decoder block's output norm
+    (MMSEG_HEAD_IN_PART, mmseg_head_loss_bwd_in) and by conv2's brick5 data gradient for conv1's norm in every
+    96^3-style block (MMSEG_DGRAD_IN_PART, mmseg_conv3_dgrad_in, bf16 only); both feed mmseg_instnorm_bwd_part.
+    Same loss bits; gradients equal to the two-pass path (knob=0) up to the summation order of those partials
+    (fp32 1e-5, bf16 1e-2 normwise: a bf16 activation rounding on the other side moves by one ulp); the head's own
+    weight gradient is untouched (bitwise)."""
     from mmseg_amd.engine.engine import fused_loss_supported, run_engine_loss
     from mmseg_amd.trainer.losses import DiceCELoss
     gen = torch.Generator().manual_seed(9)
@@ -403,7 +406,7 @@ def test_head_in_partials(dev, model, dtype, defer_head, monkeypatch):
     monkeypatch.setenv("MMSEG_DEFER_HEAD_NORM", defer_head)
     res = []
     for fused in ("1", "0"):
-        monkeypatch.setenv("MMSEG_HEAD_IN_PART", fused)
+        monkeypatch.setenv(knob, fused)
         cfg = make_config(model, ["CT", "PET"], 3, [32, 64, 128], dtype=dtype)
         torch.manual_seed(0)
         m = build_model(cfg).to(dev)
@@ -413,7 +416,11 @@ def test_head_in_partials(dev, model, dtype, defer_head, monkeypatch):
         loss.backward()
         torch.cuda.synchronize()
         prog = m.backbone.__dict__["_engine"].program
-        assert (getattr(prog.dec, "_hpart", None) is not None) == (fused == "1")
+        if knob == "MMSEG_HEAD_IN_PART":
+            assert (getattr(prog.dec, "_hpart", None) is not None) == (fused == "1")
+        else:
+            assert (getattr(prog.dec.blocks[-1].c2, "_inpart", None) is not None) == (fused == "1" and
+                                                                                   dtype == "bfloat16")
         head = [p.grad.reshape(-1).clone() for n, p in m.named_parameters() if "out_conv" in n]
         res.append((loss.detach().clone(), torch.cat([p.grad.reshape(-1) for p in m.parameters()]).clone(), head))
     assert torch.equal(res[0][0], res[1][0])
