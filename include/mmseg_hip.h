@@ -99,6 +99,13 @@ int mmseg_stem_fwd(const void* x, int ldx, int cr, const float* w, const float* 
                    int H, int W, int Co, int dtype, void* stream);
 int mmseg_stem_wgrad(const void* dy, int lddy, const void* x, int ldx, int cr, float* part, float* bias_part, int N,
                      int D, int H, int W, int Co, int ksplit, int dtype, void* stream);
+/* mmseg_stem_wgrad whose dy is the gradient of an InstanceNorm + ReLU OUTPUT: the norm's backward (pre-norm
+ * input inx with pitch ldinx, statistics inmean / inrstd [N][Co], coefficients incoef [N][Co][2] from
+ * mmseg_instnorm_bwd_coef) is applied while staging dy -- the values mmseg_instnorm_bwd would write, bit for bit --
+ * so the norm's input gradient is never materialised.  inx null: mmseg_stem_wgrad. */
+int mmseg_stem_wgrad_inb(const void* dy, int lddy, const void* x, int ldx, int cr, const void* inx, int ldinx,
+                         const float* inmean, const float* inrstd, const float* incoef, float* part, float* bias_part,
+                         int N, int D, int H, int W, int Co, int ksplit, int dtype, void* stream);
 
 /* Fused InstanceNorm statistics (unet.py:34 InstanceNorm3d following each Conv3d): when the CONV3 brick kernel
  * for a shape can emit them, mmseg_conv3_stats_bricks returns the bricks per sample (value-returning, 0 = not
@@ -214,6 +221,12 @@ int mmseg_instnorm_bwd_part(const void* x, int ldx, const float* mean, const flo
                             const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N,
                             int D, int H, int W, int C, int relu, const float* part, int nchunk, float* ws,
                             int dtype, void* stream);
+/* The coefficient half of mmseg_instnorm_bwd for dy = p1: coef [N][C][2] = (mean g, mean g xhat), from given
+ * partials (part, nchunk; as for mmseg_instnorm_bwd_part) or, part null, from a partial pass (ws:
+ * mmseg_instnorm_ws_floats floats).  Its apply half runs inside mmseg_stem_wgrad_inb. */
+int mmseg_instnorm_bwd_coef(const void* x, int ldx, const float* mean, const float* rstd, const void* p1, int ld1,
+                            int N, int D, int H, int W, int C, int relu, const float* part, int nchunk,
+                            float* coef, float* ws, int dtype, void* stream);
 /* MaxPool3d(2) forward + argmax (0..7, z-major; first max wins) (unet.py:73). */
 int mmseg_maxpool2_fwd(const void* x, int ldx, void* y, int ldy, uint8_t* idx, int N, int D, int H, int W, int C,
                        int dtype, void* stream);

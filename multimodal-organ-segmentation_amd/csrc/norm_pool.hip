@@ -1373,6 +1373,42 @@ int mmseg_instnorm_bwd_part(const void* x, int ldx, const float* mean, const flo
   return mmseg::check_launch("instnorm_relu_bwd");
 }
 
+// The first half of mmseg_instnorm_bwd for dy = p1 (scale 1): the finalised coefficients coef [N][C][2] =
+// (mean g, mean g xhat), from the partials a producer of dy emitted (part_in, nchunk_in) or from the partial pass
+// (part_in null; ws: mmseg_instnorm_ws_floats).  The apply half then runs inside the norm's only consumer
+// (mmseg_stem_wgrad_inb), which never writes the input gradient.
+int mmseg_instnorm_bwd_coef(const void* x, int ldx, const float* mean, const float* rstd, const void* p1, int ld1,
+                            int N, int D, int H, int W, int C, int relu, const float* part_in, int nchunk_in,
+                            float* coef, float* ws, int dtype, void* stream) {
+  MMSEG_REQUIRE(C % 8 == 0 && C <= 2048 && p1 && coef, "instnorm_bwd_coef: C=%d must be a multiple of 8", C);
+  const long long V = (long long)D * H * W;
+  MMSEG_REQUIRE(V * (ldx > ld1 ? ldx : ld1) < (1LL << 31), "instnorm_bwd_coef: per-sample extent must fit int32");
+  hipStream_t s = (hipStream_t)stream;
+  if (!part_in) {
+    long long vpc;
+    const int nch = chunks_for(V, C, &vpc);
+    DySrc src{p1, ld1, 1.f, nullptr, 0, nullptr, 0, nullptr, 0, nullptr};
+    const dim3 grid(nch, N);
+    auto run = [&](auto tag, auto relu_c) {
+      using T = decltype(tag);
+      constexpr bool R = decltype(relu_c)::value;
+      hipLaunchKernelGGL((in_bwd_partial<T, R>), grid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, (int)V, C,
+                         D, H, W, (int)vpc, ws);
+    };
+    if (dtype == MMSEG_BF16) {
+      if (relu) run(bf16_t{}, std::true_type{});
+      else run(bf16_t{}, std::false_type{});
+    } else {
+      if (relu) run(float{}, std::true_type{});
+      else run(float{}, std::false_type{});
+    }
+    part_in = ws;
+    nchunk_in = nch;
+  }
+  hipLaunchKernelGGL(in_bwd_finalize, dim3(N * C), dim3(256), 0, s, part_in, N, C, nchunk_in, V, coef);
+  return mmseg::check_launch("instnorm_bwd_coef");
+}
+
 int mmseg_maxpool2_fwd(const void* x, int ldx, void* y, int ldy, uint8_t* idx, int N, int D, int H, int W, int C,
                        int dtype, void* stream) {
   MMSEG_REQUIRE(C % 8 == 0 && ((D | H | W) & 1) == 0, "maxpool2: C%%8==0 and even dims required");

@@ -47,6 +47,12 @@ struct StemArgs {
   float* part; float* bias_part;        // wgrad partials [ks][Co][KP], [ks][Co]
   int N, D, H, W, Co, KP;
   int ksplit;
+  // wgrad with the InstanceNorm + ReLU backward applied on staging (mmseg_stem_wgrad_inb): dy is the gradient of
+  // the norm's OUTPUT, inx its pre-norm input (pitch ldinx), inmean / inrstd [N][Co] its statistics and incoef
+  // [N][Co][2] the finalised (mean g, mean g xhat); the staged value is in_bwd_apply's
+  // rstd (g - a - xhat b), g = dy [xhat > 0], rounded to T, so the norm's input gradient is never written
+  const void* inx; int ldinx;
+  const float* inmean; const float* inrstd; const float* incoef;
 };
 
 // Halo of a brick in LDS, compact: [600 halo voxels][CR channels] (the padded 8-channel input layout would
@@ -162,7 +168,7 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(StemArgs g) {
 // block = a contiguous range of bricks; wave w accumulates the brick's voxel
 // steps w, w+4 (2 x 32 voxels) into the full [CO][KP] tile; the 4 wave tiles
 // are added in order at the end (deterministic).
-template <typename T, int RM, int RNK, int CR>
+template <typename T, int RM, int RNK, int CR, bool INB = false>
 __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemArgs g) {
   constexpr int K = 27 * CR, KP = RNK * 16, CO = RM * 16, CGd = CO / 8;
   static_assert(KP == ((K + 31) / 32) * 32, "KP = 27 CR padded to 32");
@@ -192,6 +198,31 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemArgs g) {
     for (int j = 0; j < RNK; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;   // bias partial of channel tid % CO over voxel slice tid / CO
   int bko[RNK];       // this lane's im2col column per k tile (compact-halo offset), -1 = padding
+  // INB: the thread's 8 channels (group tid % CGd, the same in every staging item) and their statistics
+  float imu[8], irs[8], ica[8], icb[8];
+  int in_n = -1;
+  // dy (and, INB, the norm's pre-norm input) of the NEXT brick is loaded into registers before this brick's MFMA
+  // phase, so its HBM latency hides behind the MFMAs (thread item qq: voxel (tid + 256 qq) / CGd, channel group
+  // tid % CGd)
+  V8<T> pd[CGd], px[INB ? CGd : 1];
+  auto prefetch = [&](int b) {
+    int q = b;
+    const int bx = q % bx_n; q /= bx_n;
+    const int by = q % by_n; q /= by_n;
+    const int bz = q % bz_n;
+    const long long nb = (long long)(q / bz_n) * g.D * HW;
+    const int z0 = bz * SZ, y0 = by * SY, x0 = bx * SX;
+#pragma unroll
+    for (int qq = 0; qq < CGd; ++qq) {
+      const int e = tid + qq * 256;
+      const int v = e / CGd, cg = e % CGd;
+      const int z = z0 + (v >> 6), y = y0 + ((v >> 3) & 7), x = x0 + (v & 7);
+      const long long vox = nb + z * HW + (long long)y * g.W + x;
+      pd[qq].load(Dy + vox * g.lddy + cg * 8);
+      if constexpr (INB) px[qq].load(reinterpret_cast<const T*>(g.inx) + vox * g.ldinx + cg * 8);
+    }
+  };
+  if (b0 < b1) prefetch(b0);
   for (int b = b0; b < b1; ++b) {
     int q = b;
     const int bx = q % bx_n; q /= bx_n;
@@ -199,6 +230,20 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemArgs g) {
     const int bz = q % bz_n;
     const long long nbase = (long long)(q / bz_n) * g.D * HW;
     const int z0 = bz * SZ, y0 = by * SY, x0 = bx * SX;
+    if constexpr (INB) {
+      const int n = q / bz_n;
+      if (n != in_n) {
+        in_n = n;
+        const int c0 = n * CO + (tid % CGd) * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          imu[j] = g.inmean[c0 + j];
+          irs[j] = g.inrstd[c0 + j];
+          ica[j] = g.incoef[(c0 + j) * 2];
+          icb[j] = g.incoef[(c0 + j) * 2 + 1];
+        }
+      }
+    }
     __syncthreads();   // previous brick fully consumed (and, first time round, Kl written)
     if (b == b0) {
 #pragma unroll
@@ -209,11 +254,19 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemArgs g) {
     for (int qq = 0; qq < CGd; ++qq) {
       const int e = tid + qq * 256;
       const int v = e / CGd, cg = e % CGd;
-      const int z = z0 + (v >> 6), y = y0 + ((v >> 3) & 7), x = x0 + (v & 7);
-      V8<T> d;
-      d.load(Dy + (nbase + z * HW + (long long)y * g.W + x) * g.lddy + cg * 8);
+      V8<T> d = pd[qq];
+      if constexpr (INB) {   // in_bwd_apply's operations (DyCtx with p1 = dy, scale 1, no beta / pool)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float dyv = d.get(j) * 1.f + 0.f;
+          const float h = (px[qq].get(j) - imu[j]) * irs[j];
+          const float gg = h > 0.f ? dyv : 0.f;
+          d.set(j, irs[j] * (gg - ica[j] - h * icb[j]));
+        }
+      }
       d.store(Dl + v * DP + cg * 8);
     }
+    if (b + 1 < b1) prefetch(b + 1);
     __syncthreads();
     if (g.bias_part) {   // thread = (channel tid % CO, voxel slice tid / CO)
       const int c = tid % CO;
@@ -318,18 +371,44 @@ int mmseg_stem_wgrad_splits(int N, int D, int H, int W, int want) {
   return (int)((nbrick + bpk - 1) / bpk);
 }
 
+int mmseg_stem_wgrad_inb(const void* dy, int lddy, const void* x, int ldx, int cr, const void* inx, int ldinx,
+                         const float* inmean, const float* inrstd, const float* incoef, float* part, float* bias_part,
+                         int N, int D, int H, int W, int Co, int ksplit, int dtype, void* stream);
+
 // part[ks][Co][KP] (+ bias_part[ks][Co]); reduce with mmseg_wgrad_reduce(Ca=Co, Ncols=KP, cpad=cr, creal=cr, ntap=27)
 int mmseg_stem_wgrad(const void* dy, int lddy, const void* x, int ldx, int cr, float* part, float* bias_part, int N,
                      int D, int H, int W, int Co, int ksplit, int dtype, void* stream) {
+  return mmseg_stem_wgrad_inb(dy, lddy, x, ldx, cr, nullptr, 0, nullptr, nullptr, nullptr, part, bias_part, N, D, H,
+                              W, Co, ksplit, dtype, stream);
+}
+
+// mmseg_stem_wgrad whose dy is the gradient of an InstanceNorm + ReLU OUTPUT (pre-norm input inx, pitch ldinx,
+// statistics inmean / inrstd [N][Co], finalised coefficients incoef [N][Co][2] from mmseg_instnorm_bwd_coef): the
+// norm's backward is applied while staging dy (in_bwd_apply's values, bit for bit), so its input gradient -- read
+// by nothing but this weight gradient -- is never written.  inx null: plain mmseg_stem_wgrad.
+int mmseg_stem_wgrad_inb(const void* dy, int lddy, const void* x, int ldx, int cr, const void* inx, int ldinx,
+                         const float* inmean, const float* inrstd, const float* incoef, float* part, float* bias_part,
+                         int N, int D, int H, int W, int Co, int ksplit, int dtype, void* stream) {
   MMSEG_REQUIRE(mmseg_stem_ok(cr, Co, D, H, W, ldx, lddy), "stem_wgrad: unsupported shape");
+  MMSEG_REQUIRE(!inx || (inmean && inrstd && incoef && ldinx % 8 == 0),
+                "stem_wgrad_inb: the norm's statistics and coefficients are required, ldinx a multiple of 8");
   StemArgs g{x, ldx, cr, nullptr, nullptr, nullptr, 0, dy, lddy, part, bias_part, N, D, H, W, Co, stem_kp(cr),
-             ksplit};
+             ksplit, inx, ldinx, inmean, inrstd, incoef};
   hipStream_t s = (hipStream_t)stream;
   mmseg::note_kernel("stem_wgrad_kernel");
   const dim3 grid(ksplit), blk(256);
   auto run = [&](auto tag, auto rm) {
     using T = decltype(tag);
     constexpr int RM = decltype(rm)::value;
+    if (inx) {
+      switch (cr) {
+        case 1: hipLaunchKernelGGL((stem_wgrad_kernel<T, RM, 2, 1, true>), grid, blk, 0, s, g); break;
+        case 2: hipLaunchKernelGGL((stem_wgrad_kernel<T, RM, 4, 2, true>), grid, blk, 0, s, g); break;
+        case 3: hipLaunchKernelGGL((stem_wgrad_kernel<T, RM, 6, 3, true>), grid, blk, 0, s, g); break;
+        default: hipLaunchKernelGGL((stem_wgrad_kernel<T, RM, 8, 4, true>), grid, blk, 0, s, g); break;
+      }
+      return;
+    }
     switch (cr) {
       case 1: hipLaunchKernelGGL((stem_wgrad_kernel<T, RM, 2, 1>), grid, blk, 0, s, g); break;
       case 2: hipLaunchKernelGGL((stem_wgrad_kernel<T, RM, 4, 2>), grid, blk, 0, s, g); break;

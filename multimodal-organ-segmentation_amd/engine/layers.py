@@ -113,6 +113,9 @@ def _wgrad_ksplit(rows: int, ncols: int, V: int) -> int:
     return max(1, min(-(-TARGET_BLOCKS // tiles), V // 512))
 
 
+SMALL_IN_V = 4096   # norm_pool.hip knob_small_v(): at or below it InstanceNorm is one launch (stats + apply)
+
+
 @dataclass
 class DySpec:
     """Gradient sources of an InstanceNorm+ReLU output (see mmseg_instnorm_relu_bwd)."""
@@ -247,14 +250,17 @@ class Conv3:
 
     def bwd(self, x: Act, dy: Act, dx: Optional[Act], accumulate: bool,
             norm: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-            inp: Optional[Tuple[Act, torch.Tensor, torch.Tensor]] = None):
+            inp: Optional[Tuple[Act, torch.Tensor, torch.Tensor]] = None,
+            inb: Optional[Tuple[Act, torch.Tensor, torch.Tensor, torch.Tensor]] = None):
         """norm = (mean, rstd): x is the pre-norm activation of an InstanceNorm + ReLU applied on staging by the
         weight-gradient kernel (see fwd_norm).  inp = (pre-norm x, mean, rstd) of the InstanceNorm + ReLU whose
         output gradient dx is: when the data-gradient kernel can, it also writes that backward's partial sums;
-        returns (partials, chunks) for DySpec.part, or None."""
+        returns (partials, chunks) for DySpec.part, or None.  inb = (pre-norm x, mean, rstd, coef) (stem only, see
+        stem_inb_ok): dy is the gradient of that norm's OUTPUT and the stem weight gradient applies the norm's
+        backward while staging it (mmseg_stem_wgrad_inb)."""
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
         V = x.N * x.V
-        if dx is None and norm is None and self._stem(x, dy.ld):
+        if dx is None and norm is None and (inb is not None or self._stem(x, dy.ld)):
             # 1,024 splits: one round of resident blocks at 96^3 B=2 and half the partials of 2,048 (r02 stembench:
             # 42 + 12.8 us against 44 + 19.7 us with the reduce)
             ks = L.mmseg_stem_wgrad_splits(x.N, x.D, x.H, x.W, int(os.environ.get("MMSEG_STEM_SPLITS", "1024")))
@@ -263,8 +269,13 @@ class Conv3:
             bpart = part.data_ptr() + ks * self.Co * kp * 4
             with TIMER.region("stem_wgrad_kernel", flops=2.0 * V * self.Co * 27 * self.Ci,
                               nbytes=_io_bytes(self.rt, V, 8, self.Co, 27 * self.Ci * self.Co, 4)):
-                L.mmseg_stem_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, self.Ci, ptr(part), bpart, x.N, x.D, x.H, x.W, self.Co,
-                                   ks, code, s)
+                if inb is not None:
+                    xi, im, ir, cf = inb
+                    L.mmseg_stem_wgrad_inb(dy.ptr, dy.ld, x.ptr, x.ld, self.Ci, xi.ptr, xi.ld, ptr(im), ptr(ir),
+                                           ptr(cf), ptr(part), bpart, x.N, x.D, x.H, x.W, self.Co, ks, code, s)
+                else:
+                    L.mmseg_stem_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, self.Ci, ptr(part), bpart, x.N, x.D, x.H, x.W,
+                                       self.Co, ks, code, s)
             L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.conv.weight)), bpart,
                                  ptr(self.flat.grad(self.conv.bias)), self.Co, kp, ks, self.Ci, self.Ci, 27,
                                  int(accumulate), s)
@@ -559,8 +570,28 @@ class Block:
         else:
             part = self.c2.bwd(self.y1, g2, dy1, accumulate, inp=inp)
         g1 = self.x1
+        if dxin is None and self._stem_inb(xin):
+            # conv1 is the stem and its weight gradient is the only reader of conv1's InstanceNorm input gradient:
+            # only the norm's coefficients are formed here, the stem applies the backward while staging dy1
+            L, s, code = self.rt.lib, self.rt.stream, self.rt.code
+            x1 = self.x1
+            if getattr(self, "_coef", None) is None:
+                self._coef = torch.empty(x1.N * x1.C * 2, dtype=torch.float32, device=self.rt.device)
+            ws = self.rt.ws(L.mmseg_instnorm_ws_floats(x1.N, x1.V, x1.C)) if part is None else None
+            L.mmseg_instnorm_bwd_coef(x1.ptr, x1.ld, ptr(st[0]), ptr(st[1]), dy1.ptr, dy1.ld, x1.N, x1.D, x1.H,
+                                      x1.W, x1.C, 1, ptr(part[0]) if part else None, part[1] if part else 0,
+                                      ptr(self._coef), ptr(ws), code, s)
+            self.c1.bwd(xin, dy1, None, accumulate, inb=(x1, st[0], st[1], self._coef))
+            return
         self._norm_bwd(self.x1, st[0], st[1], DySpec(p1=dy1, part=part), g1)
         self.c1.bwd(xin, g1, dxin, accumulate)
+
+    def _stem_inb(self, xin: Act) -> bool:
+        """conv1's InstanceNorm backward applied inside the stem weight gradient (no input gradient written):
+        conv1 takes the stem path, has no data gradient, and the volume is above the one-launch small-IN size
+        (whose backward sums in another order)."""
+        return (os.environ.get("MMSEG_STEM_INB", "1") != "0" and not self.c1.need_dgrad
+                and self.x1.V > SMALL_IN_V and self.c1._stem(xin, self.x1.ld))
 
 
 class Head:

@@ -432,6 +432,36 @@ def test_head_in_partials(dev, model, dtype, knob, defer_head, monkeypatch):
 
 
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("model", ["unet", "dual_encoder"])
+def test_stem_inb_bitwise(dev, model, dtype, monkeypatch):
+    """The top block's conv1 is the stem: its InstanceNorm backward is applied by the stem weight gradient while it
+    stages dy (mmseg_instnorm_bwd_coef + mmseg_stem_wgrad_inb, the norm's input gradient never written) -- the
+    same loss and bit-identical gradients as the materialised path (MMSEG_STEM_INB=0)."""
+    from mmseg_amd.engine.engine import fused_loss_supported, run_engine_loss
+    from mmseg_amd.trainer.losses import DiceCELoss
+    gen = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 2, 32, 32, 32, generator=gen).to(dev)
+    y = torch.randint(0, 3, (2, 32, 32, 32), generator=gen).to(dev)
+    res = []
+    for inb in ("1", "0"):
+        monkeypatch.setenv("MMSEG_STEM_INB", inb)
+        cfg = make_config(model, ["CT", "PET"], 3, [32, 64, 128], dtype=dtype)
+        torch.manual_seed(0)
+        m = build_model(cfg).to(dev)
+        m.train()
+        assert fused_loss_supported(m.backbone, model, x)
+        loss = run_engine_loss(m.backbone, model, x, y, DiceCELoss()._spec(), None)
+        loss.backward()
+        torch.cuda.synchronize()
+        prog = m.backbone.__dict__["_engine"].program
+        top = prog.init if model == "unet" else prog.encs[0][0]
+        assert (getattr(top, "_coef", None) is not None) == (inb == "1")
+        res.append((loss.detach().clone(), torch.cat([p.grad.reshape(-1) for p in m.parameters()]).clone()))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
 def test_deferred_encoder_norm_bitwise(dev, dtype, monkeypatch):
     """DualEncoder mean fusion: the encoders' output InstanceNorm + ReLU applied on load by the maxpool and the
     fusion kernel (never written) gives bit-identical logits, gradients and return_features to the
