@@ -53,6 +53,9 @@ struct StemArgs {
   // rstd (g - a - xhat b), g = dy [xhat > 0], rounded to T, so the norm's input gradient is never written
   const void* inx; int ldinx;
   const float* inmean; const float* inrstd; const float* incoef;
+  // forward: per-brick InstanceNorm partials of the stored output, [brick][Co][2] = (mean, M2) over its 256 voxels
+  // (the layout of conv_gemm.hip brick_in_stats; merged by mmseg_instnorm_stats_bricks), or null
+  float* stats;
 };
 
 // Halo of a brick in LDS, compact: [600 halo voxels][CR channels] (the padded 8-channel input layout would
@@ -153,6 +156,10 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(StemArgs g) {
   __syncthreads();
   T* Y = reinterpret_cast<T*>(g.y);
   constexpr int CG = RN * 2;
+  // stats: Welford over the thread's CG voxels of its channel group tid % CG (the values as stored)
+  float smu[8], sm2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) smu[j] = sm2[j] = 0.f;
 #pragma unroll
   for (int q = 0; q < CG; ++q) {
     const int e = tid + q * 256;
@@ -161,6 +168,54 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(StemArgs g) {
     V8<T> o;
     o.load(El + v * EP + cg * 8);
     o.store(Y + (nbase + z * HW + (long long)y * g.W + x) * g.ldy + cg * 8);
+    if (g.stats) {
+      const float inv = 1.f / (float)(q + 1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xv = o.get(j), d = xv - smu[j];
+        smu[j] = fmaf(d, inv, smu[j]);
+        sm2[j] = fmaf(d, xv - smu[j], sm2[j]);
+      }
+    }
+  }
+  if (g.stats) {
+    // equal-count Chan merges, fixed order: the lanes of a wave holding the same channel group (xor CG .. 32,
+    // count per lane CG << level), then the 4 waves in order (64 voxels each)
+    float cnt = (float)CG;
+#pragma unroll
+    for (int o = CG; o < 64; o <<= 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float mb = __shfl_xor(smu[j], o, 64), m2b = __shfl_xor(sm2[j], o, 64);
+        const bool lo = (lane & o) == 0;   // both partners form the same value
+        const float m1 = lo ? smu[j] : mb, m2 = lo ? mb : smu[j];
+        const float d = m2 - m1;
+        sm2[j] = (lo ? sm2[j] + m2b : m2b + sm2[j]) + d * d * (0.5f * cnt);
+        smu[j] = m1 + 0.5f * d;
+      }
+      cnt *= 2.f;
+    }
+    __shared__ float sred[4][CO][2];
+    if (lane < CG)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sred[wave][lane * 8 + j][0] = smu[j];
+        sred[wave][lane * 8 + j][1] = sm2[j];
+      }
+    __syncthreads();
+    if (tid < CO) {
+      float mu = sred[0][tid][0], m2 = sred[0][tid][1], na = 64.f;
+#pragma unroll
+      for (int w = 1; w < 4; ++w) {
+        const float d = sred[w][tid][0] - mu, nn = na + 64.f;
+        mu += d * (64.f / nn);
+        m2 += sred[w][tid][1] + d * d * (na * 64.f / nn);
+        na = nn;
+      }
+      float* out = g.stats + ((long long)blockIdx.x * CO + tid) * 2;
+      out[0] = mu;
+      out[1] = m2;
+    }
   }
 }
 
@@ -332,11 +387,25 @@ int mmseg_stem_ok(int cr, int Co, int D, int H, int W, int ldx, int ldy) {
          H % SY == 0 && W % SX == 0;
 }
 
+int mmseg_stem_fwd_stats(const void* x, int ldx, int cr, const float* w, const float* bias, void* y, int ldy, int N,
+                         int D, int H, int W, int Co, float* stats, int dtype, void* stream);
+
 int mmseg_stem_fwd(const void* x, int ldx, int cr, const float* w, const float* bias, void* y, int ldy, int N, int D,
                    int H, int W, int Co, int dtype, void* stream) {
+  return mmseg_stem_fwd_stats(x, ldx, cr, w, bias, y, ldy, N, D, H, W, Co, nullptr, dtype, stream);
+}
+
+// Bricks per sample of the stem forward's fused InstanceNorm partials (each block is one 4x8x8 brick).
+int mmseg_stem_stats_bricks(int D, int H, int W) { return (D / SZ) * (H / SY) * (W / SX); }
+
+// mmseg_stem_fwd + per-brick InstanceNorm partials of its output (stats [N][mmseg_stem_stats_bricks()][Co][2] =
+// (mean, M2) of the stored values over each brick's 256 voxels; mmseg_instnorm_stats_bricks merges them).
+int mmseg_stem_fwd_stats(const void* x, int ldx, int cr, const float* w, const float* bias, void* y, int ldy, int N,
+                         int D, int H, int W, int Co, float* stats, int dtype, void* stream) {
   MMSEG_REQUIRE(mmseg_stem_ok(cr, Co, D, H, W, ldx, ldy), "stem_fwd: unsupported shape (cr=%d Co=%d %dx%dx%d)", cr,
                 Co, D, H, W);
   StemArgs g{x, ldx, cr, w, bias, y, ldy, nullptr, 0, nullptr, nullptr, N, D, H, W, Co, stem_kp(cr), 1};
+  g.stats = stats;
   const dim3 grid(N * (D / SZ) * (H / SY) * (W / SX));
   hipStream_t s = (hipStream_t)stream;
   mmseg::note_kernel("stem_fwd_kernel");
@@ -374,6 +443,8 @@ int mmseg_stem_wgrad_splits(int N, int D, int H, int W, int want) {
 int mmseg_stem_wgrad_inb(const void* dy, int lddy, const void* x, int ldx, int cr, const void* inx, int ldinx,
                          const float* inmean, const float* inrstd, const float* incoef, float* part, float* bias_part,
                          int N, int D, int H, int W, int Co, int ksplit, int dtype, void* stream);
+int mmseg_stem_fwd_stats(const void* x, int ldx, int cr, const float* w, const float* bias, void* y, int ldy, int N,
+                         int D, int H, int W, int Co, float* stats, int dtype, void* stream);
 
 // part[ks][Co][KP] (+ bias_part[ks][Co]); reduce with mmseg_wgrad_reduce(Ca=Co, Ncols=KP, cpad=cr, creal=cr, ntap=27)
 int mmseg_stem_wgrad(const void* dy, int lddy, const void* x, int ldx, int cr, float* part, float* bias_part, int N,

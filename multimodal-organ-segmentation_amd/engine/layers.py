@@ -199,11 +199,21 @@ class Conv3:
     def stats_bricks(self, x: Act, y: Act) -> int:
         """Bricks per sample for which fwd() can emit fused InstanceNorm partials (0 = not available)."""
         if self._stem(x, y.ld):
-            return 0
+            # the stem's blocks are single 4x8x8 bricks whose epilogue merges the tile's statistics
+            if os.environ.get("MMSEG_STEM_STATS", "1") == "0":
+                return 0
+            return self.rt.lib.mmseg_stem_stats_bricks(x.D, x.H, x.W)
         return self.rt.lib.mmseg_conv3_stats_bricks(x.N * x.V, self.Co, self.Cpad, self.KG, self.cpg_shift, x.D, x.H,
                                                     x.W, x.ld, y.ld, self.rt.code)
 
     def fwd(self, x: Act, y: Act, stats_part: Optional[torch.Tensor] = None):
+        if stats_part is not None and self._stem(x, y.ld):
+            with TIMER.region("stem_fwd_kernel", flops=2.0 * x.N * x.V * self.Co * 27 * self.Ci,
+                              nbytes=_io_bytes(self.rt, x.N * x.V, 8, self.Co, 27 * self.Ci * self.Co, 4)):
+                self.rt.lib.mmseg_stem_fwd_stats(x.ptr, x.ld, self.Ci, ptr(self.conv.weight), ptr(self.conv.bias),
+                                                 y.ptr, y.ld, x.N, x.D, x.H, x.W, self.Co, ptr(stats_part),
+                                                 self.rt.code, self.rt.stream)
+            return
         if stats_part is not None:
             with TIMER.region(_gemm_name(self.rt, self.Co, "conv3"), flops=2.0 * x.N * x.V * self.Co * 27 * self.Ci,
                               nbytes=_io_bytes(self.rt, x.N * x.V, self.Ci, self.Co, 27 * self.Ci * self.Co)):
