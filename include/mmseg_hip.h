@@ -97,9 +97,9 @@ int mmseg_stem_kp(int cr);
 int mmseg_stem_wgrad_splits(int N, int D, int H, int W, int want);
 int mmseg_stem_fwd(const void* x, int ldx, int cr, const float* w, const float* bias, void* y, int ldy, int N, int D,
                    int H, int W, int Co, int dtype, void* stream);
-/* mmseg_stem_fwd that also writes the per-brick InstanceNorm partials of its output: stats
- * [N][mmseg_stem_stats_bricks()][Co][2] = (mean, M2) of the stored values over each 4x8x8 brick (256 voxels), the
- * input of mmseg_instnorm_stats_bricks(stats, N, Co, bricks, 256, ...). */
+/* mmseg_stem_fwd that also writes InstanceNorm partials of its output: stats [N][mmseg_stem_stats_bricks()][Co][2]
+ * = (mean, M2) of the stored values over each 1x8x8 slice of its 4x8x8 bricks (64 voxels), the input of
+ * mmseg_instnorm_stats_bricks(stats, N, Co, slices, 64, ...). */
 int mmseg_stem_stats_bricks(int D, int H, int W);
 int mmseg_stem_fwd_stats(const void* x, int ldx, int cr, const float* w, const float* bias, void* y, int ldy, int N,
                          int D, int H, int W, int Co, float* stats, int dtype, void* stream);

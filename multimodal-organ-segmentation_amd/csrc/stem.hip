@@ -179,8 +179,9 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(StemArgs g) {
     }
   }
   if (g.stats) {
-    // equal-count Chan merges, fixed order: the lanes of a wave holding the same channel group (xor CG .. 32,
-    // count per lane CG << level), then the 4 waves in order (64 voxels each)
+    // equal-count Chan merges, fixed order, over the lanes of a wave holding the same channel group (xor CG .. 32,
+    // count per lane CG << level); each wave writes the partial of its brick z-slice (64 voxels), so the block
+    // needs no barrier or serial merge (a block-level merge made the kernel 16 us slower at 96^3 B=2)
     float cnt = (float)CG;
 #pragma unroll
     for (int o = CG; o < 64; o <<= 1) {
@@ -195,26 +196,13 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(StemArgs g) {
       }
       cnt *= 2.f;
     }
-    __shared__ float sred[4][CO][2];
-    if (lane < CG)
+    if (lane < CG) {
+      float* out = g.stats + (((long long)blockIdx.x * 4 + wave) * CO + lane * 8) * 2;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        sred[wave][lane * 8 + j][0] = smu[j];
-        sred[wave][lane * 8 + j][1] = sm2[j];
+        out[2 * j] = smu[j];
+        out[2 * j + 1] = sm2[j];
       }
-    __syncthreads();
-    if (tid < CO) {
-      float mu = sred[0][tid][0], m2 = sred[0][tid][1], na = 64.f;
-#pragma unroll
-      for (int w = 1; w < 4; ++w) {
-        const float d = sred[w][tid][0] - mu, nn = na + 64.f;
-        mu += d * (64.f / nn);
-        m2 += sred[w][tid][1] + d * d * (na * 64.f / nn);
-        na = nn;
-      }
-      float* out = g.stats + ((long long)blockIdx.x * CO + tid) * 2;
-      out[0] = mu;
-      out[1] = m2;
     }
   }
 }
@@ -395,11 +383,12 @@ int mmseg_stem_fwd(const void* x, int ldx, int cr, const float* w, const float* 
   return mmseg_stem_fwd_stats(x, ldx, cr, w, bias, y, ldy, N, D, H, W, Co, nullptr, dtype, stream);
 }
 
-// Bricks per sample of the stem forward's fused InstanceNorm partials (each block is one 4x8x8 brick).
-int mmseg_stem_stats_bricks(int D, int H, int W) { return (D / SZ) * (H / SY) * (W / SX); }
+// Partials per sample of the stem forward's fused InstanceNorm statistics: one per z-slice of each 4x8x8 brick
+// (a block is one brick, each of its 4 waves one 1x8x8 slice of 64 voxels).
+int mmseg_stem_stats_bricks(int D, int H, int W) { return 4 * (D / SZ) * (H / SY) * (W / SX); }
 
-// mmseg_stem_fwd + per-brick InstanceNorm partials of its output (stats [N][mmseg_stem_stats_bricks()][Co][2] =
-// (mean, M2) of the stored values over each brick's 256 voxels; mmseg_instnorm_stats_bricks merges them).
+// mmseg_stem_fwd + InstanceNorm partials of its output (stats [N][mmseg_stem_stats_bricks()][Co][2] = (mean, M2)
+// of the stored values over each 64-voxel brick slice; mmseg_instnorm_stats_bricks merges them).
 int mmseg_stem_fwd_stats(const void* x, int ldx, int cr, const float* w, const float* bias, void* y, int ldy, int N,
                          int D, int H, int W, int Co, float* stats, int dtype, void* stream) {
   MMSEG_REQUIRE(mmseg_stem_ok(cr, Co, D, H, W, ldx, ldy), "stem_fwd: unsupported shape (cr=%d Co=%d %dx%dx%d)", cr,

@@ -431,6 +431,38 @@ def test_head_in_partials(dev, model, dtype, knob, defer_head, monkeypatch):
     assert err < (1e-5 if dtype == "float32" else 1e-2), err
 
 
+@pytest.mark.parametrize("model", ["unet", "dual_encoder"])
+def test_fused_forward_stats(dev, model, monkeypatch):
+    """bf16, 32-channel top level: the InstanceNorm statistics of the top blocks' conv1 come from the stem forward's
+    epilogue (one (mean, M2) per 64-voxel brick slice) instead of a statistics pass.  Same math up to summation
+    order: loss 1e-5, gradients 1e-2 normwise (bf16 activations re-round near ties) against the statistics-pass
+    path (MMSEG_STEM_STATS=0)."""
+    knob = "MMSEG_STEM_STATS"
+    from mmseg_amd.engine.engine import fused_loss_supported, run_engine_loss
+    from mmseg_amd.trainer.losses import DiceCELoss
+    gen = torch.Generator().manual_seed(13)
+    x = torch.randn(2, 2, 32, 32, 32, generator=gen).to(dev)
+    y = torch.randint(0, 3, (2, 32, 32, 32), generator=gen).to(dev)
+    res = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv(knob, fused)
+        cfg = make_config(model, ["CT", "PET"], 3, [32, 64, 128], dtype="bfloat16")
+        torch.manual_seed(0)
+        m = build_model(cfg).to(dev)
+        m.train()
+        assert fused_loss_supported(m.backbone, model, x)
+        loss = run_engine_loss(m.backbone, model, x, y, DiceCELoss()._spec(), None)
+        loss.backward()
+        torch.cuda.synchronize()
+        prog = m.backbone.__dict__["_engine"].program
+        top = prog.init if model == "unet" else prog.encs[0][0]
+        assert bool(top.nb[0]) == (fused == "1")
+        res.append((loss.detach().double().item(), torch.cat([p.grad.reshape(-1) for p in m.parameters()]).clone()))
+    assert abs(res[0][0] - res[1][0]) <= 1e-5 * abs(res[1][0])
+    a, b = res[0][1].double(), res[1][1].double()
+    assert ((a - b).norm() / b.norm()).item() < 1e-2
+
+
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
 @pytest.mark.parametrize("model", ["unet", "dual_encoder"])
 def test_stem_inb_bitwise(dev, model, dtype, monkeypatch):
