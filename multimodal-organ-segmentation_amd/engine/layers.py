@@ -199,8 +199,10 @@ class Conv3:
     def stats_bricks(self, x: Act, y: Act) -> int:
         """Bricks per sample for which fwd() can emit fused InstanceNorm partials (0 = not available)."""
         if self._stem(x, y.ld):
-            # the stem's blocks are single 4x8x8 bricks whose epilogue merges the tile's statistics
-            if os.environ.get("MMSEG_STEM_STATS", "1") == "0":
+            # the stem's epilogue can emit its output's statistics per 64-voxel slice (MMSEG_STEM_STATS=1), but off by
+            # default: stem +14.5 us and the slice merge (in_stats_from_bricks, 13,824 slices per sample) 105 us per
+            # launch against a 20 + 5 us statistics pass (rocprofv3 r02h)
+            if os.environ.get("MMSEG_STEM_STATS", "0") != "1":
                 return 0
             return self.rt.lib.mmseg_stem_stats_bricks(x.D, x.H, x.W)
         return self.rt.lib.mmseg_conv3_stats_bricks(x.N * x.V, self.Co, self.Cpad, self.KG, self.cpg_shift, x.D, x.H,
