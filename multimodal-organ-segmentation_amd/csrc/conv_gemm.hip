@@ -550,7 +550,12 @@ struct Brick2Layout {
 
 __device__ __forceinline__ int w2_swz(int col) { return ((col >> 3) & 1) << 1; }
 
-template <typename T, int BN, int ZW, bool PF = false>
+template <typename T>
+__device__ __forceinline__ void buf_load_v8(V8<T>& v, __amdgpu_buffer_rsrc_t r, uint32_t off);
+
+// B32: the halo is staged with 32-bit offset buffer loads whose out-of-volume lanes read zeros (host: the A tensor
+// spans < 2^31 bytes), instead of 64-bit address arithmetic and a bounds branch per item.
+template <typename T, int BN, int ZW, bool PF = false, bool B32 = false>
 __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kernel(GemmArgs g) {
   using L = Brick2Layout<T>;
   constexpr int BZ = 4 * ZW, HZ = BZ + 2;
@@ -591,6 +596,9 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kern
   const int nstage = nchunk * 3;
 
   V8<T> xr[X_PER], wr[W_PER];
+  const int nvox = n * g.D * g.H * g.W;   // (B32 only: the host checked the extent)
+  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(g.a), 0, B32 ? (int)((long long)g.M * g.lda * (int)sizeof(T)) : 0, 0x00020000);
   auto load_x = [&](int c) {
 #pragma unroll
     for (int k = 0; k < X_PER; ++k) {
@@ -599,10 +607,18 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kern
         const int h = e >> 2, cg = e & 3;
         const int hx = h % H2_X, hy = (h / H2_X) % H2_Y, hz = h / (H2_X * H2_Y);
         const int z = z0 - 1 + hz, y = y0 - 1 + hy, x = x0 - 1 + hx;
-        if ((unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W)
-          xr[k].load(A + (nbase + z * HW + (long long)y * g.W + x) * g.lda + c * CK + cg * 8);
-        else
-          xr[k].zero();
+        const bool ok = (unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
+        if constexpr (B32) {
+          const uint32_t off = ok ? (uint32_t)(((nvox + (z * g.H + y) * g.W + x) * g.lda + c * CK + cg * 8) *
+                                               (int)sizeof(T))
+                                  : 0x80000000u;
+          buf_load_v8<T>(xr[k], arsrc, off);   // out-of-volume lanes read zeros
+        } else {
+          if (ok)
+            xr[k].load(A + (nbase + z * HW + (long long)y * g.W + x) * g.lda + c * CK + cg * 8);
+          else
+            xr[k].zero();
+        }
       }
     }
   };
@@ -3898,6 +3914,16 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
         hipLaunchKernelGGL((conv3_brick3_kernel<T, 32, false>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
     } else if (g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
       mmseg::note_kernel("conv3_brick2_kernel<BN64,ZW1>");
+      // (bf16 only: the fp32 instantiation of the 32-bit staging gave wrong results in the r02 GPU suite, cause not
+      // found; fp32 is the parity path and keeps the 64-bit staging)
+      const bool b32 = sizeof(T) == 2 && knob("MMSEG_BRICK2_B32", 1) &&
+                       (long long)g.M * g.lda * (long long)sizeof(T) < (1LL << 31);
+      if constexpr (sizeof(T) == 2) {
+        if (knob("MMSEG_TAP_PF", 1) && b32) {
+          hipLaunchKernelGGL((conv3_brick2_kernel<T, 64, 1, true, true>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
+          return mmseg::check_launch("conv3_brick2");
+        }
+      }
       if (knob("MMSEG_TAP_PF", 1))   // 2 % on the 48^3 64-channel layers (r02)
         hipLaunchKernelGGL((conv3_brick2_kernel<T, 64, 1, true>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
       else
