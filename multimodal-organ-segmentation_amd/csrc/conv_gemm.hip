@@ -3854,8 +3854,17 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     // persistent: at most one wave of resident blocks (2 per CU), each over a contiguous range of units
     const int maxblk = knob("MMSEG_BRICK3_BLOCKS", 512);
     // (BN64 stays on v2 unless asked for: at 256 VGPRs the v3 instantiation spills and measured no faster)
+    // 32-bit offset halo staging (brick2 B32; bf16 only, see the BN64 branch)
+    const bool b32 = sizeof(T) == 2 && knob("MMSEG_BRICK2_B32", 1) &&
+                     (long long)g.M * g.lda * (long long)sizeof(T) < (1LL << 31);
     if (g.Ncols % 32 != 0) {    // a multiple of 48 (plan_conv3)
       mmseg::note_kernel("conv3_brick2_kernel<BN48,ZW1>");
+      if constexpr (sizeof(T) == 2) {
+        if (b32) {
+          hipLaunchKernelGGL((conv3_brick2_kernel<T, 48, 1, false, true>), dim3(nb1 * (g.Ncols / 48)), block, 0, s, g);
+          return mmseg::check_launch("conv3_brick2");
+        }
+      }
       hipLaunchKernelGGL((conv3_brick2_kernel<T, 48, 1>), dim3(nb1 * (g.Ncols / 48)), block, 0, s, g);
     } else if (v3 && knob("MMSEG_BRICK3_BN64", 0) && g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
       const int units = nb1 * (g.Ncols / 64);
@@ -3914,10 +3923,8 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
         hipLaunchKernelGGL((conv3_brick3_kernel<T, 32, false>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
     } else if (g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
       mmseg::note_kernel("conv3_brick2_kernel<BN64,ZW1>");
-      // (bf16 only: the fp32 instantiation of the 32-bit staging gave wrong results in the r02 GPU suite, cause not
-      // found; fp32 is the parity path and keeps the 64-bit staging)
-      const bool b32 = sizeof(T) == 2 && knob("MMSEG_BRICK2_B32", 1) &&
-                       (long long)g.M * g.lda * (long long)sizeof(T) < (1LL << 31);
+      // (b32 is bf16 only: the fp32 instantiation of the 32-bit staging gave wrong results in the r02 GPU suite,
+      // cause not found; fp32 is the parity path and keeps the 64-bit staging)
       if constexpr (sizeof(T) == 2) {
         if (knob("MMSEG_TAP_PF", 1) && b32) {
           hipLaunchKernelGGL((conv3_brick2_kernel<T, 64, 1, true, true>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
