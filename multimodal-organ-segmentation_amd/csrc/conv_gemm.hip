@@ -1625,7 +1625,8 @@ __host__ __device__ constexpr int br_xq(int tsize) { return tsize == 2 ? 2560 : 
 // CB* > 0: the brick is known at compile time (6x6x6 at the 12^3 / 6^3 levels), so the halo / epilogue index
 // arithmetic divides by constants (mul-shift) instead of runtime integer divisions, which at one 32-channel
 // chunk per block were most of the kernel's VALU work (8.6 VALU instructions per MFMA, rocprofv3 r02).
-template <typename T, int BN, int CBZ = 0, int CBY = 0, int CBX = 0, int DBG = 0, bool PF = false>
+// B32 (bf16): the halo staged with 32-bit offset buffer loads, out-of-volume lanes reading zeros (conv3_brick2's B32).
+template <typename T, int BN, int CBZ = 0, int CBY = 0, int CBX = 0, int DBG = 0, bool PF = false, bool B32 = false>
 __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kernel(GemmArgs g, int bz_rt, int by_rt,
                                                                                    int bx_rt, long long* dbg = nullptr) {
   const int bz = CBZ > 0 ? CBZ : bz_rt, by = CBY > 0 ? CBY : by_rt, bx = CBX > 0 ? CBX : bx_rt;
@@ -1688,6 +1689,9 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kern
   const int c_end = c_begin + cps < nchunk ? c_begin + cps : nchunk;
 
   V8<T> xr[X_PER], wr[W_PER];
+  const int nvox = n * g.D * g.H * g.W;   // (B32 only: the host checked the extent)
+  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(g.a), 0, B32 ? (int)((long long)g.M * g.lda * (int)sizeof(T)) : 0, 0x00020000);
   auto load_x = [&](int c) {
 #pragma unroll
     for (int k = 0; k < X_PER; ++k) {
@@ -1697,10 +1701,18 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kern
         const int hx = h % HX, t = h / HX;
         const int hy = t % HY, hz = t / HY;
         const int z = z0 - 1 + hz, y = y0 - 1 + hy, x = x0 - 1 + hx;
-        if ((unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W)
-          xr[k].load(A + (nbase + z * HW + (long long)y * g.W + x) * g.lda + c * CK + cg * 8);
-        else
-          xr[k].zero();
+        const bool ok = (unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
+        if constexpr (B32) {
+          const uint32_t off = ok ? (uint32_t)(((nvox + (z * g.H + y) * g.W + x) * g.lda + c * CK + cg * 8) *
+                                               (int)sizeof(T))
+                                  : 0x80000000u;
+          buf_load_v8<T>(xr[k], arsrc, off);   // out-of-volume lanes read zeros
+        } else {
+          if (ok)
+            xr[k].load(A + (nbase + z * HW + (long long)y * g.W + x) * g.lda + c * CK + cg * 8);
+          else
+            xr[k].zero();
+        }
       }
     }
   };
@@ -3776,6 +3788,9 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     g.ksplit = (nchunk + cps - 1) / cps;
     const dim3 grid(nb * ((g.Ncols + plan.bn - 1) / plan.bn) * g.ksplit);
     const bool b666 = plan.bz == 6 && plan.by == 6 && plan.bx == 6 && knob("MMSEG_BRICKR_CT", 1);
+    // 32-bit offset halo staging (bf16 only, as conv3_brick2_kernel's B32)
+    const bool rb32 = sizeof(T) == 2 && knob("MMSEG_BRICKR_B32", 1) &&
+                      (long long)g.M * g.lda * (long long)sizeof(T) < (1LL << 31);
     if (plan.bn == 64) {
       if constexpr (sizeof(T) == 2) {
         mmseg::note_kernel("conv3_brickr_kernel<BN64>");
@@ -3823,11 +3838,16 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
         }
         else if (b666 && knob("MMSEG_BRICKR_PF", 0))
           hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6, 0, true>), grid, block, 0, s, g, 6, 6, 6);
+        else if (b666 && rb32)
+          hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6, 0, false, true>), grid, block, 0, s, g, 6, 6, 6);
         else if (b666)
           hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6>), grid, block, 0, s, g, 6, 6, 6);
         else if (knob("MMSEG_BRICKR_PF", 0))
           hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 0, 0, 0, 0, true>), grid, block, 0, s, g, plan.bz, plan.by,
                              plan.bx);
+        else if (rb32)
+          hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 0, 0, 0, 0, false, true>), grid, block, 0, s, g, plan.bz,
+                             plan.by, plan.bx);
         else
           hipLaunchKernelGGL((conv3_brickr_kernel<T, 64>), grid, block, 0, s, g, plan.bz, plan.by, plan.bx);
       }
