@@ -31,6 +31,11 @@ PEAK_BF16_TFLOPS = 2500.0    # dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
 
+# Whole-step algorithmic work per 96^3 sample (SURVEY §8d / BASELINE.md): FLOPs of forward + backward
+# (2 per MAC, torch FlopCounterMode on the reference) and compulsory HBM bytes with bf16 activations.
+STEP_WORK = {("unet", 2): (1206.2e9, 4.15e9), ("dual_encoder", 2): (1559.4e9, 6.31e9),
+             ("dual_encoder", 3): (1915.6e9, 8.20e9)}
+
 
 def make_config(model, batch, dtype, out_channels=6, modalities=("CT", "PET"), size=96, loss="dice_ce"):
     backbone = {"features": [32, 64, 128, 256, 512], "norm": "instance"}
@@ -54,24 +59,69 @@ def make_config(model, batch, dtype, out_channels=6, modalities=("CT", "PET"), s
     }
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*pmc_traffic*.json,
-    made by tools/rocprof_families.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench)."""
+def _pmc_summary():
+    """Newest committed PMC summary (profiles/*pmc_traffic*.json, made by tools/rocprof_families.py from separate
+    FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench): ({family: {...}}, path) or (None, None)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json")))
     if not files:
         return None, None
     with open(files[-1]) as f:
-        d = json.load(f)
-    if kernel not in d:
-        return None, os.path.relpath(files[-1], ROOT)
-    return d[kernel]["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+        return json.load(f), os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(model_name, batch, size, out_channels, modalities, threads):
-    """The oracle (torch-CPU fp32 restatement of the reference step) on the host cores:
-    1 warm-up step on a 32^3 patch, then ONE timed full-size step (bounded sample)."""
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the PMC summary."""
+    d, src = _pmc_summary()
+    if d is None or kernel not in d:
+        return None, src
+    return d[kernel]["hbm_bytes_per_launch"], src
+
+
+def pmc_step_bytes():
+    """HBM bytes of one whole training step from the PMC summary: every kernel's bytes per launch x launches,
+    over the steps the profiled run executed (its '_steps', else the AdamW launch count: one per step);
+    the runtime's buffer copies / fills (input staging, arena set-up) are not part of a step."""
+    d, src = _pmc_summary()
+    if d is None:
+        return None, None
+    steps = d.get("_steps") or d.get("adamw4_kernel", {}).get("launches")
+    if not steps:
+        return None, src
+    tot = sum(v["hbm_bytes_per_launch"] * v["launches"] for k, v in d.items()
+              if not k.startswith(("_", "__amd_rocclr")))
+    return tot / steps, src
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def cpu_threads() -> int:
+    """Threads for the CPU baseline: this process's CPU share (the GPU box's cgroup / OMP_NUM_THREADS: 16 per
+    GPU there), not os.cpu_count(), which reports the whole host."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(model_name, batch, size, out_channels, modalities, threads, loss="dice_ce", steps=3):
+    """The oracle (torch-CPU fp32 restatement of the reference step: forward, loss, backward, AdamW) on the
+    host cores, on the same seeded phantom batches as the GPU run: 1 warm-up step on a 32^3 patch, then `steps`
+    timed full-size steps (a bounded sample, ~10-30 s); value = patches / mean step time."""
     from oracle import mmseg_oracle as O
+    from mmseg_amd.data.synthetic import SyntheticSegDataset
     torch.set_num_threads(threads)
     M = len(modalities)
     feats = [32, 64, 128, 256, 512]
@@ -82,18 +132,23 @@ def cpu_baseline(model_name, batch, size, out_channels, modalities, threads):
     else:
         p = O.init_unet3d(M, out_channels, feats)
         fwd = O.unet3d_forward
-    st = O.OracleStep(p, fwd, O.dice_ce_loss)
+    st = O.OracleStep(p, fwd, O.tversky_loss if loss == "tversky" else O.dice_ce_loss)
     g = torch.Generator().manual_seed(5)
-    xw = torch.randn(1, M, 32, 32, 32, generator=g)
-    st.step(xw, torch.randint(0, out_channels, (1, 32, 32, 32), generator=g))
-    x = torch.randn(batch, M, size, size, size, generator=g)
-    y = torch.randint(0, out_channels, (batch, size, size, size), generator=g)
+    st.step(torch.randn(1, M, 32, 32, 32, generator=g), torch.randint(0, out_channels, (1, 32, 32, 32), generator=g))
+    ds = SyntheticSegDataset(steps * batch, size, out_channels, modalities, seed=1234)
+    batches = []
+    for i in range(steps):
+        items = [ds[i * batch + j] for j in range(batch)]
+        batches.append((torch.stack([it["image"] for it in items]), torch.stack([it["label"] for it in items])))
     t0 = time.perf_counter()
-    st.step(x, y)
-    dt = time.perf_counter() - t0
+    for x, y in batches:
+        st.step(x, y)
+    dt = (time.perf_counter() - t0) / steps
     return {"value": batch / dt, "unit": "patches/s", "cores": threads, "kind": "port",
-            "sample": f"1 oracle train step (fwd+DiceCE+bwd+AdamW), {model_name} B={batch} {size}^3 fp32, "
-                      f"{dt:.1f} s on {threads} threads ({platform.processor() or platform.machine()})"}
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
+            "sample": f"{steps} oracle train steps (fwd+{'Tversky' if loss == 'tversky' else 'DiceCE'}+bwd+AdamW), "
+                      f"{model_name} M={M} B={batch} {size}^3 fp32 on seeded phantoms, {dt:.2f} s/step on "
+                      f"{threads} threads"}
 
 
 def main():
@@ -109,7 +164,8 @@ def main():
     ap.add_argument("--modalities", default="CT,PET", help="c5: CT,PET,MRI")
     ap.add_argument("--loss", default="dice_ce", choices=["dice_ce", "tversky"], help="c5: tversky")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: this process's CPU share (cpu_threads())")
+    ap.add_argument("--cpu-steps", type=int, default=3, help="timed oracle steps in the CPU baseline")
     ap.add_argument("--timer-steps", type=int, default=3, help="extra steps timed per kernel family (roofline)")
     args = ap.parse_args()
 
@@ -196,10 +252,26 @@ def main():
     families = {k: {"ms_per_step": round(v["ms"] / args.timer_steps, 3),
                     "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1) if v["ms"] > 0 else None}
                 for k, v in sorted(fam.items(), key=lambda kv: -kv[1]["ms"])}
+    step = None
+    work = STEP_WORK.get((args.model, len(mods)))
+    if work is not None and args.size == 96 and args.dtype == "bf16":
+        F, Bt = work[0] * args.batch, work[1] * args.batch
+        t_mfma, t_hbm = F / (PEAK_BF16_TFLOPS * 1e12), Bt / (PEAK_HBM_GBS * 1e9)
+        t_roof = max(t_mfma, t_hbm)
+        counter, csrc = pmc_step_bytes()
+        step = {"bound": "hbm" if t_hbm >= t_mfma else "mfma", "algorithmic_tflop": round(F / 1e12, 3),
+                "compulsory_gb": round(Bt / 1e9, 3), "t_mfma_ms": round(t_mfma * 1e3, 3),
+                "t_hbm_ms": round(t_hbm * 1e3, 3), "t_roof_ms": round(t_roof * 1e3, 3),
+                "frac": round(t_roof * 1e3 / ms_per_step, 4),
+                "counter_gb": round(counter / 1e9, 3) if counter is not None else None,
+                "counter_source": csrc,
+                "counter_tbps": round(counter / (ms_per_step * 1e-3) / 1e12, 3) if counter is not None else None}
+        if roofline is not None:
+            roofline["step"] = step
     cpu = None
-    if (n_gpus == 1 and not args.no_cpu_baseline and args.model != "swin_unetr" and len(mods) == 2
-            and args.loss == "dice_ce"):
-        cpu = cpu_baseline(args.model, args.batch, args.size, 6, mods, args.cpu_threads)
+    if n_gpus == 1 and not args.no_cpu_baseline and args.model != "swin_unetr":
+        cpu = cpu_baseline(args.model, args.batch, args.size, 6, mods, args.cpu_threads or cpu_threads(),
+                           loss=args.loss, steps=args.cpu_steps)
     workload = {"dual_encoder": "DualEncoder fusion=cross_attention (mean, dual_encoder.py:193-195)",
                 "unet": "UNet3D early_fusion",
                 "swin_unetr": "SwinUNETR feature_size 48 (MONAI architecture; parity vs MONAI unpinned)"}[

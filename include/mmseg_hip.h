@@ -460,9 +460,19 @@ int mmseg_dice_counts(const float* logits, const void* labels, int label_bytes, 
 /* counts from class-index masks (DiceMetric.update(pred, target), metrics.py:42-67). */
 int mmseg_dice_counts_idx(const void* pred, int pred_bytes, const void* labels, int label_bytes, long long total, int C,
                           unsigned long long* counts, void* stream);
-/* AdamW step over flat fp32 buffers (torch.optim.AdamW op order, trainer.py:115-117). */
+/* AdamW step over flat fp32 buffers (torch.optim.AdamW op order, trainer.py:115-117).
+ * skip (nullable): one device float, the step's count of out-of-range labels (mmseg_loss_fwd's last workspace
+ * float, summed over the ranks under DP); when it is non-zero the kernel leaves p, m and v untouched, so a batch
+ * the trainer raises on (the reference raises in F.one_hot before its optimizer step) never updates the model. */
 int mmseg_adamw(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
-                float eps, float wd, int step, void* stream);
+                float eps, float wd, int step, const float* skip, void* stream);
+/* The same step with its hyper-parameters read from device memory (8 floats), so one launch can be captured
+ * in a HIP graph and replayed every step: mmseg_adamw_hyper (host only, no device work) fills the 8 floats for
+ * (lr, betas, eps, wd, step) exactly as mmseg_adamw derives them; the caller copies them to the device
+ * buffer before each replay. */
+int mmseg_adamw_hyper(float lr, float beta1, float beta2, float eps, float wd, int step, float* hyper);
+int mmseg_adamw_dev(float* p, const float* g, float* m, float* v, long long n, const float* hyper, const float* skip,
+                    void* stream);
 
 #ifdef __cplusplus
 }

@@ -3789,7 +3789,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     const dim3 grid(nb * ((g.Ncols + plan.bn - 1) / plan.bn) * g.ksplit);
     const bool b666 = plan.bz == 6 && plan.by == 6 && plan.bx == 6 && knob("MMSEG_BRICKR_CT", 1);
     // 32-bit offset halo staging (bf16 only, as conv3_brick2_kernel's B32)
-    const bool rb32 = sizeof(T) == 2 && knob("MMSEG_BRICKR_B32", 1) &&
+    const bool rb32 = (sizeof(T) == 2 || knob("MMSEG_B32_F32", 0)) && knob("MMSEG_BRICKR_B32", 1) &&
                       (long long)g.M * g.lda * (long long)sizeof(T) < (1LL << 31);
     if (plan.bn == 64) {
       if constexpr (sizeof(T) == 2) {
@@ -3853,10 +3853,17 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
       }
     } else if (b666) {
       mmseg::note_kernel("conv3_brickr_kernel<BN32>");
-      hipLaunchKernelGGL((conv3_brickr_kernel<T, 32, 6, 6, 6>), grid, block, 0, s, g, 6, 6, 6);
+      if (rb32)
+        hipLaunchKernelGGL((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, false, true>), grid, block, 0, s, g, 6, 6, 6);
+      else
+        hipLaunchKernelGGL((conv3_brickr_kernel<T, 32, 6, 6, 6>), grid, block, 0, s, g, 6, 6, 6);
     } else {
       mmseg::note_kernel("conv3_brickr_kernel<BN32>");
-      hipLaunchKernelGGL((conv3_brickr_kernel<T, 32>), grid, block, 0, s, g, plan.bz, plan.by, plan.bx);
+      if (rb32)
+        hipLaunchKernelGGL((conv3_brickr_kernel<T, 32, 0, 0, 0, 0, false, true>), grid, block, 0, s, g, plan.bz,
+                           plan.by, plan.bx);
+      else
+        hipLaunchKernelGGL((conv3_brickr_kernel<T, 32>), grid, block, 0, s, g, plan.bz, plan.by, plan.bx);
     }
     if (mmseg::check_launch("conv3_brickr")) return 1;
     if (g.ksplit > 1) return launch_splitk_reduce<T, MODE>(g, s);
@@ -3875,15 +3882,13 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     const int maxblk = knob("MMSEG_BRICK3_BLOCKS", 512);
     // (BN64 stays on v2 unless asked for: at 256 VGPRs the v3 instantiation spills and measured no faster)
     // 32-bit offset halo staging (brick2 B32; bf16 only, see the BN64 branch)
-    const bool b32 = sizeof(T) == 2 && knob("MMSEG_BRICK2_B32", 1) &&
+    const bool b32 = (sizeof(T) == 2 || knob("MMSEG_B32_F32", 0)) && knob("MMSEG_BRICK2_B32", 1) &&
                      (long long)g.M * g.lda * (long long)sizeof(T) < (1LL << 31);
     if (g.Ncols % 32 != 0) {    // a multiple of 48 (plan_conv3)
       mmseg::note_kernel("conv3_brick2_kernel<BN48,ZW1>");
-      if constexpr (sizeof(T) == 2) {
-        if (b32) {
-          hipLaunchKernelGGL((conv3_brick2_kernel<T, 48, 1, false, true>), dim3(nb1 * (g.Ncols / 48)), block, 0, s, g);
-          return mmseg::check_launch("conv3_brick2");
-        }
+      if (b32) {
+        hipLaunchKernelGGL((conv3_brick2_kernel<T, 48, 1, false, true>), dim3(nb1 * (g.Ncols / 48)), block, 0, s, g);
+        return mmseg::check_launch("conv3_brick2");
       }
       hipLaunchKernelGGL((conv3_brick2_kernel<T, 48, 1>), dim3(nb1 * (g.Ncols / 48)), block, 0, s, g);
     } else if (v3 && knob("MMSEG_BRICK3_BN64", 0) && g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
@@ -3943,13 +3948,9 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
         hipLaunchKernelGGL((conv3_brick3_kernel<T, 32, false>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
     } else if (g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
       mmseg::note_kernel("conv3_brick2_kernel<BN64,ZW1>");
-      // (b32 is bf16 only: the fp32 instantiation of the 32-bit staging gave wrong results in the r02 GPU suite,
-      // cause not found; fp32 is the parity path and keeps the 64-bit staging)
-      if constexpr (sizeof(T) == 2) {
-        if (knob("MMSEG_TAP_PF", 1) && b32) {
-          hipLaunchKernelGGL((conv3_brick2_kernel<T, 64, 1, true, true>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
-          return mmseg::check_launch("conv3_brick2");
-        }
+      if (knob("MMSEG_TAP_PF", 1) && b32) {
+        hipLaunchKernelGGL((conv3_brick2_kernel<T, 64, 1, true, true>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
+        return mmseg::check_launch("conv3_brick2");
       }
       if (knob("MMSEG_TAP_PF", 1))   // 2 % on the 48^3 64-channel layers (r02)
         hipLaunchKernelGGL((conv3_brick2_kernel<T, 64, 1, true>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);

@@ -14,6 +14,7 @@
 //   input:  NCDHW fp32 volume -> NDHWC (8-channel padded) engine layout.
 #include "mmseg_common.h"
 
+#include <cstring>
 #include <type_traits>
 
 namespace {
@@ -355,10 +356,12 @@ struct LossCfg {
 // Label validity (the reference raises in F.one_hot / cross_entropy on a label outside [0, C)): such a
 // voxel contributes nothing and is counted; the finalize pass then makes the loss NaN and publishes the
 // count at coef[2NC+1] for the host to raise on.  Pure CE (region weight 0) skips torch's default
-// ignore_index -100 without counting it, as nn.CrossEntropyLoss does.
+// ignore_index -100 without counting it, as nn.CrossEntropyLoss does.  Focal (type 2) skips it too: the
+// reference's F.cross_entropy(reduction='none') gives 0 there (losses.py:116), and its .mean() still counts
+// the voxel, so an ignored focal voxel adds 1 to the CE denominator and nothing else.
 __device__ __forceinline__ int label_state(int y, int C, const LossCfg& cfg) {
   if ((unsigned)y < (unsigned)C) return 0;                 // valid
-  return (y == -100 && cfg.type == 0 && cfg.dice_w == 0.f) ? 1 : 2;   // 1 = ignored, 2 = invalid
+  return (y == -100 && ((cfg.type == 0 && cfg.dice_w == 0.f) || cfg.type == 2)) ? 1 : 2;   // 1 ignored, 2 invalid
 }
 
 // One voxel's contribution to the loss statistics: softmax p over its C logits z, Sum p / Sum p*t / Sum t per
@@ -486,6 +489,7 @@ __global__ __launch_bounds__(256) void loss_stats_kernel(const float* __restrict
     const int ls = label_state(y, C, cfg);
     if (ls) {
       bad += ls == 2 ? 1.f : 0.f;
+      if (ls == 1 && cfg.type == 2) cden += 1.f;   // focal: ignored voxel, counted by the mean
       continue;
     }
     loss_voxel_stats<NC>(zu[u], C, y, cfg, P, I, Tc, ce, cden);
@@ -792,6 +796,8 @@ __global__ __launch_bounds__(256) void head_loss_stats_kernel(const T* __restric
       }
     } else if (ls == 2 && g == 0) {
       bad += 1.f;
+    } else if (ls == 1 && ok && cfg.type == 2 && g == 0) {
+      cden += 1.f;   // focal: ignored (-100) voxel, counted by the mean
     }
   }
   }
@@ -1128,10 +1134,29 @@ __global__ void dice_counts_idx_kernel(const PT* __restrict__ pred, const LT* __
 }
 
 // ------------------------------------------------------------------ AdamW
+// Hyper-parameters of one step, either by value (eager launches) or read from device memory (a captured step
+// graph replays the same launch every step; the host refreshes the 8 floats before each replay):
+// [decay, omb1, beta2, omb2, eps, step_size, bc2_sqrt, unused].  `skip` (nullable): a device float, the
+// step's count of out-of-range labels (summed over the ranks under DP); non-zero leaves p, m, v untouched,
+// so a batch the trainer is about to raise on never updates the model.
+struct AdamHyper {
+  float decay, omb1, beta2, omb2, eps, step_size, bc2_sqrt, pad;
+};
+__device__ __forceinline__ bool adamw_load(const AdamHyper& hv, const AdamHyper* hp, const float* skip,
+                                           AdamHyper& h) {
+  if (skip && *skip != 0.f) return false;
+  h = hp ? *hp : hv;
+  return true;
+}
+
 __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                             float* __restrict__ v, long long n, float decay, float beta1, float omb1, float beta2,
-                             float omb2, float eps, float step_size, float bc2_sqrt) {
+                             float* __restrict__ v, long long n, AdamHyper hv, const AdamHyper* __restrict__ hp,
+                             const float* __restrict__ skip) {
 #pragma clang fp contract(off)
+  AdamHyper h;
+  if (!adamw_load(hv, hp, skip, h)) return;
+  const float decay = h.decay, omb1 = h.omb1, beta2 = h.beta2, omb2 = h.omb2, eps = h.eps, step_size = h.step_size,
+              bc2_sqrt = h.bc2_sqrt;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     float pv = p[i];
     const float gv = g[i];
@@ -1163,8 +1188,12 @@ __device__ __forceinline__ float adamw_one(float& pv, float gv, float& mv, float
 }
 __global__ __launch_bounds__(256) void adamw4_kernel(float4* __restrict__ p, const float4* __restrict__ g,
                                                      float4* __restrict__ m, float4* __restrict__ v, long long n4,
-                                                     float decay, float omb1, float beta2, float omb2, float eps,
-                                                     float step_size, float bc2_sqrt) {
+                                                     AdamHyper hv, const AdamHyper* __restrict__ hp,
+                                                     const float* __restrict__ skip) {
+  AdamHyper h;
+  if (!adamw_load(hv, hp, skip, h)) return;
+  const float decay = h.decay, omb1 = h.omb1, beta2 = h.beta2, omb2 = h.omb2, eps = h.eps, step_size = h.step_size,
+              bc2_sqrt = h.bc2_sqrt;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += 2 * stride) {
     const long long i2 = i + stride;
@@ -1548,32 +1577,62 @@ int mmseg_dice_counts_idx(const void* pred, int pred_bytes, const void* labels, 
   return mmseg::check_launch("dice_counts_idx");
 }
 
-int mmseg_adamw(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
-                float eps, float wd, int step, void* stream) {
+static AdamHyper adamw_hyper(float lr, float beta1, float beta2, float eps, float wd, int step) {
+  // torch.optim.AdamW (single-tensor, foreach=False): bias corrections in double, as Python floats
   const double bc1 = 1.0 - pow((double)beta1, step);
   const double bc2 = 1.0 - pow((double)beta2, step);
-  const float step_size = (float)(lr / bc1);
-  const float bc2s = (float)sqrt(bc2);
-  const int grid = grid_for(n) > 4096 ? 4096 : grid_for(n);
-  const float decay = (float)(1.0 - (double)lr * (double)wd);
-  const float omb1 = (float)(1.0 - (double)beta1), omb2 = (float)(1.0 - (double)beta2);
+  AdamHyper h;
+  h.decay = (float)(1.0 - (double)lr * (double)wd);
+  h.omb1 = (float)(1.0 - (double)beta1);
+  h.beta2 = beta2;
+  h.omb2 = (float)(1.0 - (double)beta2);
+  h.eps = eps;
+  h.step_size = (float)(lr / bc1);
+  h.bc2_sqrt = (float)sqrt(bc2);
+  h.pad = 0.f;
+  return h;
+}
+
+static int adamw_launch(float* p, const float* g, float* m, float* v, long long n, const AdamHyper& hv,
+                        const AdamHyper* hp, const float* skip, hipStream_t stream) {
   const bool vec = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
                      reinterpret_cast<uintptr_t>(v)) & 15) == 0;
   if (vec && n >= 4) {
     const long long n4 = n / 4;
     long long b4 = (n4 + 511) / 512;   // 2 float4 per thread
     if (b4 > 8192) b4 = 8192;
-    hipLaunchKernelGGL(adamw4_kernel, dim3((int)b4), dim3(256), 0, (hipStream_t)stream, reinterpret_cast<float4*>(p),
+    hipLaunchKernelGGL(adamw4_kernel, dim3((int)b4), dim3(256), 0, stream, reinterpret_cast<float4*>(p),
                        reinterpret_cast<const float4*>(g), reinterpret_cast<float4*>(m), reinterpret_cast<float4*>(v),
-                       n4, decay, omb1, beta2, omb2, eps, step_size, bc2s);
+                       n4, hv, hp, skip);
     if (n % 4)
-      hipLaunchKernelGGL(adamw_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, p + 4 * n4, g + 4 * n4, m + 4 * n4,
-                         v + 4 * n4, n - 4 * n4, decay, beta1, omb1, beta2, omb2, eps, step_size, bc2s);
+      hipLaunchKernelGGL(adamw_kernel, dim3(1), dim3(64), 0, stream, p + 4 * n4, g + 4 * n4, m + 4 * n4, v + 4 * n4,
+                         n - 4 * n4, hv, hp, skip);
     return mmseg::check_launch("adamw");
   }
-  hipLaunchKernelGGL(adamw_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, decay, beta1, omb1,
-                     beta2, omb2, eps, step_size, bc2s);
+  const int grid = grid_for(n) > 4096 ? 4096 : grid_for(n);
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid), dim3(256), 0, stream, p, g, m, v, n, hv, hp, skip);
   return mmseg::check_launch("adamw");
+}
+
+int mmseg_adamw(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
+                float eps, float wd, int step, const float* skip, void* stream) {
+  MMSEG_REQUIRE(step >= 1, "adamw: step counts from 1");
+  return adamw_launch(p, g, m, v, n, adamw_hyper(lr, beta1, beta2, eps, wd, step), nullptr, skip,
+                      (hipStream_t)stream);
+}
+
+int mmseg_adamw_hyper(float lr, float beta1, float beta2, float eps, float wd, int step, float* hyper) {
+  MMSEG_REQUIRE(step >= 1 && hyper != nullptr, "adamw_hyper: step >= 1 and a host buffer of 8 floats");
+  const AdamHyper h = adamw_hyper(lr, beta1, beta2, eps, wd, step);
+  memcpy(hyper, &h, sizeof(h));
+  return 0;
+}
+
+int mmseg_adamw_dev(float* p, const float* g, float* m, float* v, long long n, const float* hyper, const float* skip,
+                    void* stream) {
+  MMSEG_REQUIRE(hyper != nullptr, "adamw_dev: hyper (8 device floats from mmseg_adamw_hyper) required");
+  AdamHyper unused{};
+  return adamw_launch(p, g, m, v, n, unused, reinterpret_cast<const AdamHyper*>(hyper), skip, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -1131,6 +1131,10 @@ __global__ void attn_gate_bwd(const float* __restrict__ dot_part, int nchunk, co
   }
 }
 
+// Kernels with a 32-bit grid-stride index (maxpool2_fwd, fuse_fwd) step i by up to 8192 * 256 = 2^21: the
+// item count must stay that far below INT_MAX so the last i += stride cannot wrap negative.
+constexpr long long kGridStrideMax = 2147483647LL - 8192LL * 256;
+
 int grid_for(long long total) {
   long long b = (total + 255) / 256;
   if (b > 8192) b = 8192;
@@ -1412,7 +1416,7 @@ int mmseg_instnorm_bwd_coef(const void* x, int ldx, const float* mean, const flo
 int mmseg_maxpool2_fwd(const void* x, int ldx, void* y, int ldy, uint8_t* idx, int N, int D, int H, int W, int C,
                        int dtype, void* stream) {
   MMSEG_REQUIRE(C % 8 == 0 && ((D | H | W) & 1) == 0, "maxpool2: C%%8==0 and even dims required");
-  MMSEG_REQUIRE((long long)N * (D / 2) * (H / 2) * (W / 2) * (C / 8) < (1LL << 31), "maxpool2: too many items");
+  MMSEG_REQUIRE((long long)N * (D / 2) * (H / 2) * (W / 2) * (C / 8) <= kGridStrideMax, "maxpool2: too many items");
   hipStream_t s = (hipStream_t)stream;
   const int grid = grid_for((long long)N * (D / 2) * (H / 2) * (W / 2) * (C / 8));
   if (dtype == MMSEG_BF16)
@@ -1429,7 +1433,7 @@ int mmseg_maxpool2_fwd(const void* x, int ldx, void* y, int ldy, uint8_t* idx, i
 int mmseg_maxpool2_norm_fwd(const void* x, int ldx, const float* mean, const float* rstd, void* y, int ldy,
                             uint8_t* idx, int N, int D, int H, int W, int C, int dtype, void* stream) {
   MMSEG_REQUIRE(C % 8 == 0 && ((D | H | W) & 1) == 0, "maxpool2: C%%8==0 and even dims required");
-  MMSEG_REQUIRE((long long)N * (D / 2) * (H / 2) * (W / 2) * (C / 8) < (1LL << 31), "maxpool2: too many items");
+  MMSEG_REQUIRE((long long)N * (D / 2) * (H / 2) * (W / 2) * (C / 8) <= kGridStrideMax, "maxpool2: too many items");
   hipStream_t s = (hipStream_t)stream;
   const int grid = grid_for((long long)N * (D / 2) * (H / 2) * (W / 2) * (C / 8));
   if (dtype == MMSEG_BF16)
@@ -1446,7 +1450,7 @@ int mmseg_fuse_norm_fwd(const void* const* srcs, const int* lds, const float* co
                         int M, float wconst, const float* wts, void* out, int ldo, int N, long long V, int C,
                         int dtype, void* stream) {
   MMSEG_REQUIRE(M >= 1 && M <= 4 && C % 8 == 0, "fuse: 1 <= M <= 4 and C%%8==0");
-  MMSEG_REQUIRE((long long)N * V * (C / 8) < (1LL << 31), "fuse: too many items");
+  MMSEG_REQUIRE((long long)N * V * (C / 8) <= kGridStrideMax, "fuse: too many items");
   FuseSrc s{};
   for (int m = 0; m < M; ++m) {
     s.p[m] = srcs[m];
@@ -1470,7 +1474,7 @@ int mmseg_fuse_norm_fwd(const void* const* srcs, const int* lds, const float* co
 int mmseg_fuse_fwd(const void* const* srcs, const int* lds, int M, float wconst, const float* wts, void* out, int ldo,
                    int N, long long V, int C, int dtype, void* stream) {
   MMSEG_REQUIRE(M >= 1 && M <= 4 && C % 8 == 0, "fuse: 1 <= M <= 4 and C%%8==0");
-  MMSEG_REQUIRE((long long)N * V * (C / 8) < (1LL << 31), "fuse: too many items");
+  MMSEG_REQUIRE((long long)N * V * (C / 8) <= kGridStrideMax, "fuse: too many items");
   FuseSrc s{};
   for (int m = 0; m < M; ++m) {
     s.p[m] = srcs[m];

@@ -37,11 +37,12 @@ def get_dataloader(config: Dict[str, Any], split: str = "train", shuffle=None, d
                                   seed=seed, preprocessing=config["data"].get("preprocessing"))
         return DeviceLoader(ds, config["training"]["batch_size"],
                             shuffle=split == "train" if shuffle is None else shuffle,
-                            drop_last=split == "train" if drop_last is None else drop_last, seed=seed)
+                            drop_last=split == "train" if drop_last is None else drop_last, seed=seed,
+                            pad=split == "train")
     ds = get_dataset(config, split)
     w, r = ddp.world(), ddp.rank()
-    if w > 1:
-        ds = Subset(ds, ddp.shard_indices(len(ds), r, w))
+    if w > 1:   # training shards are padded to equal length, validation shards are not (each sample once)
+        ds = Subset(ds, ddp.shard_indices(len(ds), r, w, pad=split == "train"))
     if shuffle is None:
         shuffle = split == "train"
     if drop_last is None:

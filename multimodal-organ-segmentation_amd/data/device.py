@@ -171,10 +171,12 @@ class DeviceLoader:
     """Batches of a DevicePhantomDataset (DistributedSampler semantics under DP: rank r takes r, r+W, ...)."""
 
     def __init__(self, ds: DevicePhantomDataset, batch_size: int, shuffle: bool = False, drop_last: bool = False,
-                 seed: int = 0):
+                 seed: int = 0, pad: bool = True):
         self.ds, self.B, self.shuffle, self.drop_last, self.seed = ds, batch_size, shuffle, drop_last, seed
         self.epoch = 0
-        self.idx = ddp.shard_indices(len(ds), ddp.rank(), ddp.world()) if ddp.world() > 1 else list(range(len(ds)))
+        # pad=True (training): equal-length shards; pad=False (validation): every sample scored once
+        self.idx = (ddp.shard_indices(len(ds), ddp.rank(), ddp.world(), pad=pad) if ddp.world() > 1
+                    else list(range(len(ds))))
 
     def __len__(self):
         n = len(self.idx)

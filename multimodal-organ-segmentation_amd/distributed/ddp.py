@@ -42,12 +42,16 @@ def init_from_env(backend: Optional[str] = None) -> int:
     return local
 
 
-def shard_indices(n_samples: int, r: int, w: int) -> List[int]:
+def shard_indices(n_samples: int, r: int, w: int, pad: bool = True) -> List[int]:
     """torch DistributedSampler(shuffle=False) order: pad the index list by wrapping around to
     ceil(n/W)*W, then rank r takes r, r+W, ...  Every rank gets the same count, so no rank runs
-    an extra train_step (which would wait forever in a gradient all-reduce)."""
+    an extra train_step (which would wait forever in a gradient all-reduce).  pad=False (validation):
+    plain r::W slicing, so every sample is scored exactly once (the validation all-reduce sums each
+    rank's real batch count, so unequal shards are fine there)."""
     if n_samples <= 0:
         return []
+    if not pad:
+        return list(range(r, n_samples, w))
     total = -(-n_samples // w) * w
     idx = list(range(n_samples))
     while len(idx) < total:
@@ -86,6 +90,11 @@ class GradBuckets:
         self.pending = [hi - lo for (lo, hi, _, _) in self.buckets]
         self.works = []
         self.events = [dict() for _ in self.buckets]   # bucket -> {stream handle: event after its last write}
+        # guard: one device float written by the step's loss forward (its count of out-of-range labels).  It is
+        # summed over the ranks together with the first bucket, so the optimizer kernel of EVERY rank sees a
+        # non-zero count and skips the update when any rank had a bad batch (the ranks stay identical)
+        self.guard: Optional[torch.Tensor] = None
+        self.guard_sent = False
 
     def _reduce(self, b: int):
         _, _, lo, hi = self.buckets[b]
@@ -106,9 +115,22 @@ class GradBuckets:
                     t.div_(self.w)
                     op = dist.ReduceOp.SUM
                 self.works.append(dist.all_reduce(t, op=op, group=self.group, async_op=True))
+                self._send_guard()
         else:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
             t.div_(self.w)
+            self._send_guard()
+
+    def _send_guard(self):
+        """All-reduce (SUM) the guard count on the comm stream, once per step; the loss forward that wrote it
+        precedes every gradient write, so the bucket events already order it."""
+        if self.guard is None or self.guard_sent:
+            return
+        self.guard_sent = True
+        if self.guard.is_cuda:
+            self.works.append(dist.all_reduce(self.guard, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+        else:
+            dist.all_reduce(self.guard, op=dist.ReduceOp.SUM, group=self.group)
 
     def param_ready(self, idx: int):
         if self.w == 1:
@@ -138,6 +160,12 @@ class GradBuckets:
         for b in late:         # a parameter the engine did not report: reduce anyway (correctness first)
             self.pending[b] = 0
             self._reduce(b)
+        if self.guard is not None and not self.guard_sent:
+            if self.grad.is_cuda:
+                with torch.cuda.stream(self.comm):
+                    self._send_guard()
+            else:
+                self._send_guard()
         for wk in self.works:
             wk.wait()      # makes the current (optimizer) stream wait for the collective
         self.reset()

@@ -31,6 +31,28 @@ class FlatAdamW(torch.optim.AdamW):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, **kw):
         super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, foreach=False, **kw)
         self._flat = {}
+        # guard: optional 1-element device tensor (the step's out-of-range label count, Trainer.train_step);
+        # the kernel skips the update when it is non-zero (no host sync)
+        self.guard: Optional[torch.Tensor] = None
+
+    def _group_step(self, group) -> torch.Tensor:
+        """The group's step counter: ONE CPU scalar tensor shared by every parameter's state['step'] (torch's
+        checkpoint format keeps a per-parameter 'step'), updated in place -- no per-parameter allocation per
+        step.  A state loaded from a checkpoint holds separate tensors; they are merged here."""
+        params = group["params"]
+        t = self.state[params[0]].get("step")
+        if t is None or any(self.state[p].get("step") is not t for p in params):
+            t = torch.tensor(float(t) if t is not None else 0.0)
+            for p in params:
+                self.state[p]["step"] = t
+        return t
+
+    def undo_step_count(self) -> None:
+        """Roll the step counters back by one: the kernel skipped an update (guard), so the bias corrections
+        of the next step must not advance."""
+        for group in self.param_groups:
+            t = self._group_step(group)
+            t.fill_(max(float(t) - 1.0, 0.0))
 
     def _moments(self, gi: int, group, numel: int, device):
         params = group["params"]
@@ -47,8 +69,6 @@ class FlatAdamW(torch.optim.AdamW):
             if "exp_avg" in st and st["exp_avg"].data_ptr() != mv.data_ptr():
                 mv.copy_(st["exp_avg"])      # state loaded from a checkpoint: move into the arena
                 vv.copy_(st["exp_avg_sq"])
-            if "step" not in st:
-                st["step"] = torch.tensor(0.0)
             st["exp_avg"], st["exp_avg_sq"] = mv, vv
             off += n
         return m, v
@@ -69,10 +89,11 @@ class FlatAdamW(torch.optim.AdamW):
                 raise NotImplementedError("FlatAdamW: amsgrad / maximize are not on the HIP path")
             base, n = arena
             m, v = self._moments(gi, group, n, params[0].device)
-            step = int(self.state[params[0]]["step"].item()) + 1
-            for p in params:
-                self.state[p]["step"] = torch.tensor(float(step))
+            st = self._group_step(group)
+            step = int(st.item()) + 1
+            st.fill_(float(step))
             b1, b2 = group["betas"]
             lib().mmseg_adamw(base, garena[0], ptr(m), ptr(v), n, float(group["lr"]), float(b1), float(b2),
-                              float(group["eps"]), float(group["weight_decay"]), step, stream_handle())
+                              float(group["eps"]), float(group["weight_decay"]), step, ptr(self.guard),
+                              stream_handle())
         return loss

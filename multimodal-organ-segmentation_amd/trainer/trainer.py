@@ -123,7 +123,7 @@ class Trainer:
         eng = bb.__dict__.get("_engine")
         return eng.flat if eng is not None else None
 
-    def _arm_buckets(self, communicate: bool):
+    def _arm_buckets(self, communicate: bool, guard: Optional[torch.Tensor] = None):
         if self.world == 1:
             return
         flat = self._engine_flat()
@@ -133,6 +133,7 @@ class Trainer:
             mb = float(self.config.get("distributed", {}).get("bucket_mb", 32))
             self._buckets = ddp.GradBuckets(flat.grad_flat, flat.offsets, flat.sizes, bucket_mb=mb)
         flat.on_ready = self._buckets.param_ready if communicate else None
+        self._buckets.guard = guard if communicate else None
 
     def _fused_loss(self, images: torch.Tensor, labels: torch.Tensor) -> Optional[torch.Tensor]:
         """The step's loss through the fused head + loss node when the model / loss / shape allow it, else None.
@@ -176,20 +177,36 @@ class Trainer:
         loss = self._fused_loss(images, labels)
         if loss is None:
             loss = self.criterion(self.model(images), labels)
+        # the loss kernels count labels outside [0, C) on the device (the reference raises in F.one_hot before
+        # any update): that count guards the optimizer kernel, which skips the update when it is non-zero, and
+        # under DP it is summed over the ranks with the first gradient bucket so every rank skips together
+        ws = self.criterion.__dict__.get("_last_ws")
+        guard = ws[-1:] if ws is not None else None
         loss = loss / self.accumulation_steps
-        self._arm_buckets(boundary)
+        self._arm_buckets(boundary, guard)
         loss.backward()
+        guarded = boundary and isinstance(self.optimizer, FlatAdamW)
         if boundary:
             if self._buckets is not None and self.world > 1:
                 self._buckets.finish()
+            if guarded:
+                self.optimizer.guard = guard
             self.optimizer.step()
+            if guarded:
+                self.optimizer.guard = None
             self.optimizer.zero_grad()
         out = loss.detach() * self.accumulation_steps
         if not sync:
             return out
         lv = out.item()
-        if lv != lv and hasattr(self.criterion, "check_labels"):
-            self.criterion.check_labels()      # NaN loss: raise if it came from out-of-range labels
+        if guard is not None and (lv != lv or self.world > 1):
+            if self.world > 1 and (not boundary or self._buckets is None):
+                ddp.allreduce_sum_(guard)      # no bucket carried it on this micro-step
+            if guard.item():                 # every rank sees the summed count and raises together
+                if guarded:
+                    self.optimizer.undo_step_count()    # the kernel skipped the update
+                self.optimizer.zero_grad()
+                self.criterion.check_labels()
         return lv
 
     def _train_epoch(self) -> float:

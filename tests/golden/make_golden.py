@@ -268,11 +268,176 @@ def full_case(tag, cfg, S, B, seed):
     print(tag, "loss", loss.item())
 
 
+def grad_sample_index(numel: int, k: int, seed: int) -> np.ndarray:
+    """Seeded positions at which a gradient tensor is sampled (all positions when it has <= k elements).
+    Tests regenerate the same positions from (numel, k, seed)."""
+    if numel <= k:
+        return np.arange(numel, dtype=np.int64)
+    rng = np.random.Generator(np.random.PCG64(seed))
+    return np.sort(rng.choice(numel, size=k, replace=False)).astype(np.int64)
+
+
+def full_inputs(S, B, M, C, seed):
+    """Data-only full-size inputs (shared by full_case / full_grad_case and the tests)."""
+    rng = np.random.Generator(np.random.PCG64(seed + 100))
+    x = torch.from_numpy(rng.standard_normal((B, M, S, S, S), dtype=np.float32))
+    y = torch.from_numpy(rng.integers(0, C, size=(B, S, S, S)).astype(np.int64))
+    idx = rng.integers(0, S ** 3, size=1024)
+    return x, y, idx
+
+
+def full_grad_case(tag, cfg, S, B, seed, k=4096):
+    """Full-size TRAINING step of the reference (trainer.py:250-254 with accumulation 1): train-mode forward,
+    the configured loss, backward.  Stored: loss, 1024 seeded voxels of every logit channel, the argmax
+    histogram, and per parameter gradient its L2 norm, sum and the values at k seeded positions (all of them
+    for tensors with <= k elements).  Initial weights are reproduced by torch.manual_seed(seed) + build_model."""
+    torch.manual_seed(seed)
+    model = build.build_model(cfg)
+    M = len(cfg["data"]["modalities"])
+    C = cfg["model"]["out_channels"]
+    x, y, idx = full_inputs(S, B, M, C, seed)
+    crit = losses.get_loss(cfg)
+    model.train()
+    out = model(x)
+    loss = crit(out, y)
+    loss.backward()
+    names, norms, sums, sidx, sval, soff = [], [], [], [], [], [0]
+    for i, (n, p) in enumerate(model.backbone.named_parameters()):
+        g = p.grad.detach().double().reshape(-1)
+        names.append(n)
+        norms.append(g.norm().item())
+        sums.append(g.sum().item())
+        gi = grad_sample_index(g.numel(), k, seed * 1000 + i)
+        sidx.append(gi)
+        sval.append(g[torch.from_numpy(gi)].numpy())
+        soff.append(soff[-1] + len(gi))
+    flat = out.detach().reshape(B, C, -1)
+    np.savez_compressed(os.path.join(OUT, f"{tag}.npz"), S=np.int64(S), B=np.int64(B), seed=np.int64(seed),
+                        k=np.int64(k), loss=np.float64(loss.item()), sample_idx=idx,
+                        sample_logits=flat[:, :, idx].numpy(),
+                        logits_sum=np.float64(out.detach().double().sum()),
+                        argmax_hist=np.bincount(out.detach().argmax(1).flatten().numpy(), minlength=C),
+                        param_names=np.array(names), grad_norm=np.array(norms), grad_sum=np.array(sums),
+                        gs_idx=np.concatenate(sidx), gs_val=np.concatenate(sval), gs_off=np.array(soff))
+    print(tag, "loss", loss.item(), "params", len(names))
+
+
+def _phantom_batch(seed, S, C, mods):
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(OUT)), "multimodal-organ-segmentation_amd",
+                                    "data"))
+    from synthetic import phantom    # the repo's seeded numpy phantom (plain data generation, SURVEY §8d)
+    p = phantom(seed, S, C, mods)
+    return {"image": torch.from_numpy(np.stack([p[m] for m in mods]))[None],
+            "label": torch.from_numpy(p["label"])[None]}
+
+
+def dice_heldout_case(K=16, V=2, S=64, lr=1e-4):
+    """north_star "Dice on a held-out synthetic set": config c1 (UNet3D, CT+PET, 3 classes, 64^3, batch 1,
+    DiceCE, AdamW lr 1e-4 = the c1 / default.yaml rate).  The reference Trainer runs one epoch over K phantom
+    batches (train seeds 1234..1234+K-1, trainer.py:222-263), then _validate (trainer.py:265-296: argmax +
+    DiceMetric, metrics.py:42-88) on V held-out phantoms (seeds 4321..).  The same run in fp64 is stored as the
+    reference's own rounding spread: a free-running K-step trajectory amplifies fp32 rounding (AdamW's first
+    steps move weights by ~lr * sign(g) wherever g is tiny), so two correct fp32 implementations differ by
+    about |ref32 - ref64| in held-out Dice."""
+    mods = ["CT", "PET"]
+    out = {"K": np.int64(K), "V": np.int64(V), "S": np.int64(S), "lr": np.float64(lr),
+           "train_seeds": np.arange(1234, 1234 + K), "val_seeds": np.arange(4321, 4321 + V)}
+    for dt, tag in ((torch.float32, "f32"), (torch.float64, "f64")):
+        cfg = base_config("unet", mods, 3, [32, 64, 128, 256, 512], lr=lr)
+        torch.manual_seed(42)
+        model = build.build_model(cfg).to(dt)
+        tr = trainer_mod.Trainer(config=cfg, model=model)
+        cast = lambda b: {"image": b["image"].to(dt), "label": b["label"]}  # noqa: E731
+        tr.train_loader = [cast(_phantom_batch(s, S, 3, mods)) for s in out["train_seeds"]]
+        tr.val_loader = [cast(_phantom_batch(s, S, 3, mods)) for s in out["val_seeds"]]
+        recorded = []
+        orig = tr.criterion
+
+        def rec(o, t, orig=orig, recorded=recorded):
+            lv = orig(o, t)
+            recorded.append(lv.item())
+            return lv
+        tr.criterion = rec
+        tr._train_epoch()
+        tr.criterion = orig
+        # _validate's DiceMetric is local: recompute its counts with the same calls to store I / U
+        dm = metrics.DiceMetric(num_classes=3)
+        model.eval()
+        with torch.no_grad():
+            for b in tr.val_loader:
+                dm.update(torch.argmax(model(b["image"]), dim=1), b["label"])
+        vloss, met = tr._validate()
+        out[f"{tag}_train_losses"] = np.array(recorded)
+        out[f"{tag}_val_loss"] = np.float64(vloss)
+        out[f"{tag}_dice"] = np.float64(met["dice"])
+        out[f"{tag}_dice_per_class"] = np.array(met["dice_per_class"])
+        out[f"{tag}_inter"] = dm.intersection.numpy()
+        out[f"{tag}_union"] = dm.union.numpy()
+        assert abs(dm.compute()["dice"] - met["dice"]) == 0.0
+        print("dice_heldout", tag, met, "val loss", vloss)
+    np.savez_compressed(os.path.join(OUT, "dice_heldout_c1.npz"), **out)
+
+
+def checkpoint_case():
+    """A checkpoint written by the reference (save_checkpoint, build.py:153-180: epoch, model_state_dict,
+    optimizer_state_dict (torch AdamW), best_metric, history) after 2 Trainer steps of a small UNet3D
+    (features [8, 16, 32], 32^3, B=2, 3 classes, lr 1e-3), and what the reference does next: a fresh model +
+    Trainer(resume_from=...) (trainer.py:150-164) trains one more batch; its loss and the resulting parameters
+    are stored.  The .pth holds only tensors / numbers / dicts / lists, so torch.load(weights_only=True)
+    reads it.  Also stored: the reference's c1 UNet3D and c3 DualEncoder state-dict key lists + shapes (the
+    checkpoint format an engine-written checkpoint must keep)."""
+    feats = [8, 16, 32]
+    cfg = base_config("unet", ["CT", "PET"], 3, feats, lr=1e-3)
+    g = torch.Generator().manual_seed(31)
+    xs = torch.randn(3, 2, 2, 32, 32, 32, generator=g)
+    ys = torch.randint(0, 3, (3, 2, 32, 32, 32), generator=g)
+    torch.manual_seed(0)
+    model = build.build_model(cfg)
+    tr = trainer_mod.Trainer(config=cfg, model=model)
+    tr.train_loader = [{"image": xs[i], "label": ys[i]} for i in range(2)]
+    tr._train_epoch()
+    path = os.path.join(OUT, "ref_ckpt_unet_small.pth")
+    build.save_checkpoint(model, tr.optimizer, epoch=3, checkpoint_path=path, best_metric=0.25,
+                          history={"train_loss": [1.0], "val_loss": [1.1], "val_dice": [0.25]})
+    torch.load(path, map_location="cpu", weights_only=True)     # the safe loader must accept it
+    torch.manual_seed(123)                                      # a different init: everything comes from the file
+    model2 = build.build_model(cfg)
+    tr2 = trainer_mod.Trainer(config=cfg, model=model2, resume_from=path)
+    recorded = []
+    orig = tr2.criterion
+    tr2.criterion = lambda o, t: recorded.append(orig(o, t)) or recorded[-1]
+    tr2.train_loader = [{"image": xs[2], "label": ys[2]}]
+    tr2._train_epoch()
+    names = [n for n, _ in model2.named_parameters()]
+    after = torch.cat([p.detach().reshape(-1) for p in model2.parameters()]).double()
+    keys = {}
+    for kind, mcfg in (("c1_unet", base_config("unet", ["CT", "PET"], 3, [32, 64, 128, 256, 512])),
+                       ("c3_dual", base_config("dual_encoder", ["CT", "PET"], 6, [32, 64, 128, 256, 512]))):
+        sd = build.build_model(mcfg).state_dict()
+        keys[f"{kind}_keys"] = np.array(list(sd))
+        keys[f"{kind}_shapes"] = np.array([",".join(map(str, v.shape)) for v in sd.values()])
+    np.savez_compressed(os.path.join(OUT, "ref_ckpt_unet_small.npz"), next_loss=np.float64(recorded[0].item()),
+                        resume_epoch=np.int64(tr2.current_epoch), after=after.numpy(), names=np.array(names),
+                        **keys)
+    print("checkpoint: next loss", recorded[0].item(), "resumed epoch", tr2.current_epoch)
+
+
+def full_grad_cases():
+    F = [32, 64, 128, 256, 512]
+    full_grad_case("fullgrad_unet_c2", base_config("unet", ["CT", "PET"], 6, F), S=96, B=2, seed=1234)
+    full_grad_case("fullgrad_dual_c3", base_config("dual_encoder", ["CT", "PET"], 6, F), S=96, B=2, seed=1234)
+    full_grad_case("fullgrad_dual_m3_c5", base_config("dual_encoder", ["CT", "PET", "MRI"], 6, F, loss="tversky"),
+                   S=96, B=2, seed=1234)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     if len(sys.argv) > 1:          # regenerate only the named cases, e.g. `make_golden.py bidirectional_case`
         for name in sys.argv[1:]:
-            globals()[name]()
+            if name == "full_grad_cases":
+                full_grad_cases()
+            else:
+                globals()[name]()
         sys.exit(0)
     feats = [8, 16, 32, 64, 128]
     model_case("unet_tiny", base_config("unet", ["CT", "PET"], 3, feats), S=32, B=2, full_logits=True)
@@ -287,3 +452,6 @@ if __name__ == "__main__":
     full_case("full_unet_c2", base_config("unet", ["CT", "PET"], 6, [32, 64, 128, 256, 512]), S=96, B=2, seed=1234)
     full_case("full_dual_c3", base_config("dual_encoder", ["CT", "PET"], 6, [32, 64, 128, 256, 512]),
               S=96, B=2, seed=1234)
+    full_grad_cases()
+    dice_heldout_case()
+    checkpoint_case()

@@ -161,3 +161,68 @@ def test_two_gloo_ranks_on_one_gpu_equal_one_rank_full_batch(dev):
     assert res[0]["vloss"] == res[1]["vloss"] and res[0]["dice"] == res[1]["dice"]
     assert abs(res[0]["vloss"] - single["vloss"]) < 1e-4
     assert np.abs(np.array(res[0]["dice"]) - np.array(single["dice"])).max() < 1e-3
+
+
+def _bad_label_worker(rank, world, port, q):
+    """Step 0 good on both ranks; step 1: rank 1's batch holds one label == C.  Every rank must raise at step
+    1 and keep the weights of step 0 (the summed guard makes every rank's AdamW kernel skip)."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world), LOCAL_RANK="0")
+        if ROOT not in sys.path:
+            sys.path.insert(0, ROOT)
+        import torch.distributed as dist
+        import mmseg_amd  # noqa: F401
+        from mmseg_amd.distributed import ddp
+        from mmseg_amd.models.build import build_model
+        from mmseg_amd.trainer.trainer import Trainer
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        cfg = _cfg(f"/tmp/mmseg_dpbad_{rank}")
+        torch.manual_seed(0)
+        model = build_model(cfg)
+        tr = Trainer(cfg, model)
+        xs, ys = _data()
+        idx = ddp.shard_indices(B_GLOBAL, rank, world)
+        tr.train_step({"image": xs[0][idx], "label": ys[0][idx]}, 0)
+        w0 = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()])
+        lab = ys[1][idx].clone()
+        if rank == 1:
+            lab[0, 0, 0, 0] = C
+        raised = False
+        try:
+            tr.train_step({"image": xs[1][idx], "label": lab}, 1)
+        except RuntimeError as e:
+            raised = "outside" in str(e)
+        w1 = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()])
+        dist.destroy_process_group()
+        q.put((rank, "ok", {"raised": raised, "unchanged": bool(torch.equal(w0, w1)), "w": w1.numpy()}))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_bad_labels_on_one_rank_raise_on_every_rank(dev):
+    """under DP only the rank with bad labels used to raise, and the others went on to the next
+    all-reduce and hung.  The guard count now rides with the first gradient bucket (SUM)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bad_label_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=300) for _ in procs]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in res:
+        assert r[1] == "ok", r[2]
+    res = {r[0]: r[2] for r in res}
+    for r in (0, 1):
+        assert res[r]["raised"], f"rank {r} did not raise"
+        assert res[r]["unchanged"], f"rank {r} updated its weights on the bad step"
+    assert np.array_equal(res[0]["w"], res[1]["w"])

@@ -87,6 +87,50 @@ def test_conv3_kernel_variants(dev, dtype, knobs, cin, cout, shape, monkeypatch)
     _check_conv3(dev, dtype, cin, cout, shape)
 
 
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("cin,cout,shape,extra,kernel", [
+    (64, 64, (2, 8, 16, 8), {"MMSEG_BRICK2_MINBLK": "0"}, "conv3_brick2_kernel<BN64,ZW1>"),
+    (64, 64, (1, 12, 8, 24), {"MMSEG_BRICK2_MINBLK": "0"}, "conv3_brick2_kernel<BN64,ZW1>"),  # border bricks
+    (32, 48, (1, 8, 8, 16), {}, "conv3_brick2_kernel<BN48,ZW1>"),
+    (256, 128, (2, 12, 12, 12), {}, "conv3_brickr_kernel"),        # runtime brick (3,6,12), split-K
+    (512, 256, (1, 6, 6, 6), {}, "conv3_brickr_kernel"),           # compile-time 6x6x6 brick, 16 chunks
+])
+def test_b32_halo_staging(dev, dtype, cin, cout, shape, extra, kernel, monkeypatch):
+    """The 32-bit-offset halo staging (MMSEG_BRICK2_B32 / MMSEG_BRICKR_B32: buffer loads whose out-of-volume lanes
+    read zeros) against the 64-bit staging, in BOTH storage types (fp32 through MMSEG_B32_F32=1), on shapes with
+    border bricks on every side: forward and data gradient bitwise equal (only the loads differ), and both against
+    the fp64 evaluation (_check_conv3)."""
+    for k, v in extra.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("MMSEG_B32_F32", "1")
+    torch.manual_seed(cin + cout)
+    conv = nn.Conv3d(cin, cout, 3, padding=1).to(dev)
+    N, D, H, W = shape
+    x = torch.randn(N, cin, D, H, W, device=dev)
+    dy = torch.randn(N, cout, D, H, W, device=dev)
+    res = []
+    for b32 in ("1", "0"):
+        monkeypatch.setenv("MMSEG_BRICK2_B32", b32)
+        monkeypatch.setenv("MMSEG_BRICKR_B32", b32)
+        rt = Runtime(dev, dtype)
+        flat = FlatParams(list(conv.parameters()))
+        layer = Conv3(rt, conv, flat)
+        layer.pack()
+        xa = _act(x, dtype)
+        ya = rt.act(N, D, H, W, cout)
+        layer.fwd(xa, ya)
+        torch.cuda.synchronize()
+        assert lib().mmseg_last_kernel().decode().startswith(kernel)
+        dxa = rt.act(N, D, H, W, cin)
+        layer.bwd(xa, _act(dy, dtype), dxa, accumulate=False)
+        torch.cuda.synchronize()
+        res.append((ya.buf.clone(), dxa.buf.clone()))
+        if b32 == "1":
+            _check_conv3(dev, dtype, cin, cout, shape)
+    assert torch.equal(res[0][0], res[1][0]), "forward differs between 32-bit and 64-bit staging"
+    assert torch.equal(res[0][1], res[1][1]), "data gradient differs between 32-bit and 64-bit staging"
+
+
 def _check_conv3(dev, dtype, cin, cout, shape):
     torch.manual_seed(cin + cout)
     conv = nn.Conv3d(cin, cout, 3, padding=1).to(dev)

@@ -269,16 +269,59 @@ def test_full_size_forward_matches_reference(dev, tag, model):
     assert np.abs(hist - g["argmax_hist"]).sum() <= 1e-4 * hist.sum()
 
 
-def test_train_step_raises_on_out_of_range_labels(dev):
-    """reference: F.one_hot raises on a class index >= num_classes; Trainer.train_step raises too
-    (the loss kernels count such voxels on the device; the step's loss.item() sees the NaN)."""
-    cfg, m, g, M, C = _build("unet_tiny")
-    xs, ys = _inputs(g, M, C)
-    tr = Trainer(cfg, m)
-    bad = ys[0].clone()
-    bad[0, 0, 0, 0] = C
-    with pytest.raises(RuntimeError, match="outside"):
-        tr.train_step({"image": xs[0], "label": bad}, 0)
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_train_step_raises_on_out_of_range_labels(dev, fused, monkeypatch):
+    """reference: F.one_hot raises on a class index >= num_classes BEFORE any update; Trainer.train_step raises
+    too, and the model is untouched: the loss kernels count such voxels on the device, the AdamW kernel skips
+    its update when that count is non-zero (no host sync), the step counter is rolled back, and the next good
+    step gives bitwise the state of a run that never saw the bad batch (fused head + loss and unfused)."""
+    monkeypatch.setenv("MMSEG_FUSED_HEAD_LOSS", fused)
+    xs = None
+    runs = []
+    for with_bad in (True, False):
+        cfg, m, g, M, C = _build("unet_tiny")
+        xs, ys = _inputs(g, M, C)
+        tr = Trainer(cfg, m)
+        tr.train_step({"image": xs[0], "label": ys[0]}, 0)
+        if with_bad:
+            before = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).clone()
+            mom = [t.clone() for t in tr.optimizer._flat[0]]
+            bad = ys[1].clone()
+            bad[0, 0, 0, 0] = C
+            with pytest.raises(RuntimeError, match="outside"):
+                tr.train_step({"image": xs[1], "label": bad}, 1)
+            after = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+            assert torch.equal(before, after), "a bad batch updated the parameters"
+            assert all(torch.equal(a, b) for a, b in zip(mom, tr.optimizer._flat[0])), "moments changed"
+            assert int(tr.optimizer.state[next(m.parameters())]["step"]) == 1
+        tr.train_step({"image": xs[2], "label": ys[2]}, 2)
+        runs.append(torch.cat([p.detach().reshape(-1) for p in m.parameters()]).clone())
+    assert torch.equal(runs[0], runs[1])
+
+
+def test_focal_ignores_minus_100(dev):
+    """FocalLoss (reference losses.py:83-125): F.cross_entropy(reduction='none') gives 0 at torch's default
+    ignore_index -100 and .mean() still counts those voxels; the HIP kernels do the same (loss and gradient vs
+    the reference formula evaluated by torch on the CPU in fp64).  No NaN, nothing raised."""
+    import torch.nn.functional as F
+    from mmseg_amd.trainer.losses import FocalLoss
+    g = torch.Generator().manual_seed(21)
+    for C in (3, 6):
+        logits = torch.randn(2, C, 6, 7, 8, generator=g) * 3
+        y = torch.randint(0, C, (2, 6, 7, 8), generator=g)
+        y[torch.rand(y.shape, generator=g) < 0.2] = -100
+        cw = torch.rand(C, generator=g) + 0.5
+        for alpha in (None, cw):
+            ref_in = logits.double().requires_grad_(True)
+            ce = F.cross_entropy(ref_in, y, weight=None if alpha is None else alpha.double(), reduction="none")
+            pt = torch.exp(-ce)
+            ref = ((1 - pt) ** 2.0 * ce).mean()
+            ref.backward()
+            x = logits.to(dev).requires_grad_(True)
+            loss = FocalLoss(alpha=alpha)(x, y.to(dev))
+            loss.backward()
+            assert abs(loss.item() - ref.item()) < 1e-5 * max(1.0, abs(ref.item())), (C, loss.item(), ref.item())
+            assert rel(x.grad.cpu(), ref_in.grad) < 1e-5
 
 
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])

@@ -1,7 +1,7 @@
 """Summarise rocprofv3 CSV output by the engine's kernel families.
 
     python tools/rocprof_families.py stats  <prof_kernel_stats.csv>  [steps]
-    python tools/rocprof_families.py traffic <fetch_counter_collection.csv> <write_counter_collection.csv> [out.json]
+    python tools/rocprof_families.py traffic <fetch_counter_collection.csv> <write_counter_collection.csv> [out.json [steps]]
 
 `stats` prints per-family calls / average duration (the same family names the
 in-process timer reports through mmseg_last_kernel(), so bench.py's
@@ -117,6 +117,8 @@ if __name__ == "__main__":
         stats(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 1)
     elif sys.argv[1] == "traffic":
         r = traffic(sys.argv[2], sys.argv[3])
+        if len(sys.argv) > 5:      # training steps the profiled run executed (bench: warmup + steps + timer)
+            r["_steps"] = int(sys.argv[5])
         js = json.dumps(r, indent=1)
         if len(sys.argv) > 4:
             with open(sys.argv[4], "w") as f:
