@@ -1,0 +1,175 @@
+"""The training step as a captured HIP graph (reference trainer.py:250-258: forward, loss, backward, optimizer
+step -- accumulation 1).
+
+Submitting one eager step costs ~4.3 ms of host time for ~300 launches through ctypes (DESIGN (d) "Host"), about
+as long as the GPU takes for the whole 96^3 step, so below that the step is bound by Python, not by the kernels.
+Every launch of the step goes through the enqueue-only C ABI on the current stream with buffers planned once
+per input shape, so the step is capturable as it stands: forward + fused head / loss (engine.forward_loss),
+backward (program.backward with a constant output gradient of 1) and the AdamW kernel are captured once per input
+(address, shape) and replayed with one host call.
+
+What changes per step lives in device memory, not in kernel arguments:
+  * the AdamW hyper-parameters (lr from the scheduler, the bias corrections of step t) -- mmseg_adamw_dev reads
+    8 floats that mmseg_adamw_hyper fills on the host; they go through a ring of pinned buffers (an event per
+    slot guards reuse) and one async copy before each replay;
+  * the inputs: a graph reads the images / labels at the addresses it was captured with, so graphs are cached
+    per (address, shape, dtype) of the batch (the pre-staged batches of a benchmark, or the few addresses a
+    caching allocator cycles through); past MAX_GRAPHS distinct inputs the batch is copied into the static
+    input buffers of one more graph.
+The replayed step runs the same kernels in the same order on the same buffers as the eager step, so it is
+bitwise equal to it (tests/test_step_graph_gpu.py).
+
+Used when the step has nothing per-step on the host side: one rank (the DP gradient buckets issue collectives
+from Python callbacks), accumulation_steps 1, the engine's fused head + loss, FlatAdamW (one group, no amsgrad),
+no Dropout3d in training, single-stream engine, kernel timer off.  hardware.step_graph: false or
+MMSEG_STEP_GRAPH=0 turns it off.
+"""
+from __future__ import annotations
+
+import os
+from collections import OrderedDict
+from typing import Optional, Tuple
+
+import torch
+
+from .._lib import lib, ptr, stream_handle
+
+
+class StepGraphs:
+    MAX_GRAPHS = 4       # pointer-keyed graphs (the bench pre-stages 4 batches)
+    RING = 16            # pinned hyper-parameter slots
+
+    def __init__(self, trainer):
+        self.tr = trainer
+        self.graphs: "OrderedDict[tuple, dict]" = OrderedDict()
+        self.copy_graph: Optional[dict] = None
+        self.dev = trainer.device
+        self.gout = torch.ones((), dtype=torch.float32, device=self.dev)
+        self.hyper_dev = torch.zeros(8, dtype=torch.float32, device=self.dev)
+        self.ring = [torch.zeros(8, dtype=torch.float32).pin_memory() for _ in range(self.RING)]
+        self.ring_ev = [None] * self.RING
+        self.slot = 0
+
+    # ------------------------------------------------------------------ eligibility
+    def usable(self, images: torch.Tensor, labels: torch.Tensor) -> bool:
+        env = os.environ.get("MMSEG_STEP_GRAPH")
+        if env == "0" or (env is None and not self.tr.config["hardware"].get("step_graph", True)):
+            return False
+        from ..engine.profiler import TIMER
+        from .optim import FlatAdamW
+        tr = self.tr
+        if TIMER.enabled or tr.world != 1 or tr.accumulation_steps != 1:
+            return False
+        if os.environ.get("MMSEG_MODALITY_STREAMS", "0") != "0":
+            return False
+        opt = tr.optimizer
+        if type(opt) is not FlatAdamW or len(opt.param_groups) != 1:
+            return False
+        grp = opt.param_groups[0]
+        if grp.get("amsgrad") or grp.get("maximize"):
+            return False
+        bb = getattr(tr.model, "backbone", tr.model)
+        if getattr(bb, "dropout_p", 0.0) > 0 and tr.model.training:
+            return False
+        if not tr.model.training or images.device.type != "cuda" or labels.device.type != "cuda":
+            return False
+        if images.dtype != torch.float32 or labels.dtype not in (torch.int64, torch.uint8):
+            return False
+        return images.is_contiguous() and labels.is_contiguous()
+
+    def _engine_key(self):
+        """Identity of every buffer a graph bakes in: a rebuilt engine (new arenas / activation plan) or newly
+        allocated optimizer moments invalidate the captured graphs."""
+        bb = getattr(self.tr.model, "backbone", self.tr.model)
+        eng = bb.__dict__.get("_engine")
+        if eng is None or eng.flat is None:
+            return None
+        mv = self.tr.optimizer._flat.get(0, (None, None))
+        return (id(eng.program), id(eng.flat), eng.flat.flat.data_ptr(), eng.flat.grad_flat.data_ptr(),
+                eng.program.shape, None if mv[0] is None else mv[0].data_ptr(),
+                None if mv[1] is None else mv[1].data_ptr())
+
+    # ------------------------------------------------------------------ capture
+    def _capture(self, x: torch.Tensor, y: torch.Tensor) -> dict:
+        tr = self.tr
+        bb = getattr(tr.model, "backbone", tr.model)
+        eng = bb.__dict__["_engine"]
+        crit = tr.criterion
+        spec = crit._spec()
+        cw = getattr(crit, "class_weights", None)
+        cw = None if cw is None else cw.to(self.dev, torch.float32).contiguous()
+        opt = tr.optimizer
+        grp = opt.param_groups[0]
+        flat = eng.flat
+        m, v = opt._moments(0, grp, flat.numel, self.dev)
+        L = lib()
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(self.dev)
+        with torch.cuda.graph(g):
+            loss = eng.forward_loss(x, True, y, spec, cw)
+            eng.program.backward(None, False, gout=self.gout)
+            ws = eng.loss_ws
+            L.mmseg_adamw_dev(ptr(flat.flat), ptr(flat.grad_flat), ptr(m), ptr(v), flat.numel, ptr(self.hyper_dev),
+                              ptr(ws[-1:]), stream_handle())
+        return {"graph": g, "loss": loss, "ws": ws, "x": x, "y": y, "cw": cw}
+
+    def _entry(self, images: torch.Tensor, labels: torch.Tensor) -> dict:
+        ek = self._engine_key()
+        if ek != getattr(self, "_ek", None):
+            self.graphs.clear()
+            self.copy_graph = None
+        key = (images.data_ptr(), tuple(images.shape), labels.data_ptr(), tuple(labels.shape), labels.dtype)
+        e = self.graphs.get(key)
+        if e is not None and ek == getattr(self, "_ek", None):
+            self.graphs.move_to_end(key)
+            return e
+        if len(self.graphs) < self.MAX_GRAPHS:
+            e = self._capture(images, labels)
+            self.graphs[key] = e
+            self._ek = self._engine_key()
+            return e
+        # more distinct inputs than pointer-keyed graphs: one graph over static input buffers (+ two D2D copies)
+        c = self.copy_graph
+        if c is None or c["x"].shape != images.shape or c["y"].shape != labels.shape or c["y"].dtype != labels.dtype:
+            sx, sy = torch.empty_like(images), torch.empty_like(labels)
+            sx.copy_(images)
+            sy.copy_(labels)
+            c = self._capture(sx, sy)
+            self.copy_graph = c
+            self._ek = self._engine_key()
+        else:
+            c["x"].copy_(images)
+            c["y"].copy_(labels)
+        return c
+
+    # ------------------------------------------------------------------ replay
+    def _push_hyper(self) -> int:
+        """Host: next step's AdamW hyper-parameters into a pinned slot, async copy to the device buffer."""
+        opt = self.tr.optimizer
+        grp = opt.param_groups[0]
+        st = opt._group_step(grp)
+        step = int(st.item()) + 1
+        st.fill_(float(step))
+        k = self.slot
+        self.slot = (k + 1) % self.RING
+        ev = self.ring_ev[k]
+        if ev is not None:
+            ev.synchronize()          # the copy that last read this slot has run (practically always already)
+        b1, b2 = grp["betas"]
+        buf = self.ring[k]
+        lib().mmseg_adamw_hyper(float(grp["lr"]), float(b1), float(b2), float(grp["eps"]),
+                                float(grp["weight_decay"]), step, buf.data_ptr())
+        self.hyper_dev.copy_(buf, non_blocking=True)
+        if ev is None:
+            ev = self.ring_ev[k] = torch.cuda.Event()
+        ev.record()
+        return step
+
+    def run(self, images: torch.Tensor, labels: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """One training step by graph replay; returns (loss, guard) -- both device tensors owned by the graph (the
+        loss is overwritten by the next replay of the same graph)."""
+        e = self._entry(images, labels)
+        self._push_hyper()
+        e["graph"].replay()
+        self.tr.criterion.__dict__["_last_ws"] = e["ws"]
+        return e["loss"], e["ws"][-1:]

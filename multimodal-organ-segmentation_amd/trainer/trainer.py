@@ -63,6 +63,10 @@ class Trainer:
         self.best_metric = 0.0
         self.history = {"train_loss": [], "val_loss": [], "val_dice": []}
         self._buckets = None
+        self._one = torch.ones((), dtype=torch.float32, device=self.device)
+        from .step_graph import StepGraphs
+        self._graphs = StepGraphs(self)
+        self._graph_ok = False
         # fused head + loss training step (engine.run_engine_loss): hardware.fused_head_loss (the
         # MMSEG_FUSED_HEAD_LOSS env var overrides it per step, for A/B runs)
         self.fused_head_loss = bool(config["hardware"].get("fused_head_loss", True))
@@ -174,7 +178,16 @@ class Trainer:
         images = batch["image"].to(self.device, non_blocking=True)
         labels = batch["label"].to(self.device, non_blocking=True)
         boundary = (batch_idx + 1) % self.accumulation_steps == 0
+        if self._graph_ok and self._graphs.usable(images, labels):
+            # the whole step (forward, fused loss, backward, AdamW) as one captured graph (trainer/step_graph.py)
+            if labels.dtype not in (torch.int64, torch.uint8):
+                labels = labels.long()
+            out, guard = self._graphs.run(images.contiguous(), labels.contiguous())
+            if not sync:
+                return out.clone()
+            return self._after_step(out.item(), guard, boundary=True, guarded=True)
         loss = self._fused_loss(images, labels)
+        fused = loss is not None
         if loss is None:
             loss = self.criterion(self.model(images), labels)
         # the loss kernels count labels outside [0, C) on the device (the reference raises in F.one_hot before
@@ -182,9 +195,10 @@ class Trainer:
         # under DP it is summed over the ranks with the first gradient bucket so every rank skips together
         ws = self.criterion.__dict__.get("_last_ws")
         guard = ws[-1:] if ws is not None else None
-        loss = loss / self.accumulation_steps
+        if self.accumulation_steps != 1:
+            loss = loss / self.accumulation_steps
         self._arm_buckets(boundary, guard)
-        loss.backward()
+        loss.backward(self._one)         # a constant output gradient: no fill kernel per step
         guarded = boundary and isinstance(self.optimizer, FlatAdamW)
         if boundary:
             if self._buckets is not None and self.world > 1:
@@ -195,10 +209,17 @@ class Trainer:
             if guarded:
                 self.optimizer.guard = None
             self.optimizer.zero_grad()
-        out = loss.detach() * self.accumulation_steps
+        # the first eager step planned every buffer and allocated the optimizer moments: later steps may replay
+        self._graph_ok = fused and boundary and self._graphs is not None
+        out = loss.detach()
+        if self.accumulation_steps != 1:
+            out = out * self.accumulation_steps
         if not sync:
             return out
-        lv = out.item()
+        return self._after_step(out.item(), guard, boundary, guarded)
+
+    def _after_step(self, lv: float, guard, boundary: bool, guarded: bool) -> float:
+        """Host side of a synchronous step: raise (on every rank) when the step's labels were out of range."""
         if guard is not None and (lv != lv or self.world > 1):
             if self.world > 1 and (not boundary or self._buckets is None):
                 ddp.allreduce_sum_(guard)      # no bucket carried it on this micro-step
