@@ -16,8 +16,7 @@ import torch  # noqa: F401  (must be imported first: loads torch's libamdhip64 s
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 _REPO_DIR = os.path.dirname(_PKG_DIR)
-# MMSEG_LIB_PATH: another in-tree build of the same ABI (A/B of two builds in one GPU call, tools/ only)
-LIB_PATH = os.environ.get("MMSEG_LIB_PATH") or os.path.join(_PKG_DIR, "libmmseg_hip.so")
+LIB_PATH = os.path.join(_PKG_DIR, "libmmseg_hip.so")
 HEADER_PATH = os.path.join(_REPO_DIR, "include", "mmseg_hip.h")
 
 _CTYPE = {
@@ -65,7 +64,8 @@ _VALUE_FUNCS = ("mmseg_abi_version", "mmseg_wgrad_splits", "mmseg_wgrad_splits_c
 
 
 class _Lib:
-    def __init__(self, path: str = LIB_PATH):
+    def __init__(self, path: Optional[str] = None):
+        path = path or LIB_PATH
         if not os.path.exists(path):
             raise ImportError(
                 f"{path} not found: the HIP kernels are not built. Run `python -c \"import __graft_entry__ as g; g.build()\"` "
@@ -106,6 +106,16 @@ def lib() -> _Lib:
     if _LIB is None:
         _LIB = _Lib()
     return _LIB
+
+
+def set_library_path(path: str) -> None:
+    """Bind another build of the same ABI (A/B of two in-tree builds from tools/); must precede the first
+    lib() call.  The package itself always loads the in-tree libmmseg_hip.so: no environment variable can
+    swap the library under a training run."""
+    global LIB_PATH
+    if _LIB is not None:
+        raise RuntimeError("set_library_path: the library is already loaded")
+    LIB_PATH = path
 
 
 def ptr(t) -> Optional[int]:

@@ -3794,7 +3794,9 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     if (plan.bn == 64) {
       if constexpr (sizeof(T) == 2) {
         mmseg::note_kernel("conv3_brickr_kernel<BN64>");
-        const int dbg = knob("MMSEG_BRICKR_DBG", 0);   // timing probes (diagnostics only, wrong results)
+#ifdef MMSEG_TIMING_PROBES
+        // timing probes (diagnostics only, wrong results): built only with -DMMSEG_TIMING_PROBES
+        const int dbg = knob("MMSEG_BRICKR_DBG", 0);
         if (b666 && dbg == 1)
           hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6, 1>), grid, block, 0, s, g, 6, 6, 6);
         else if (b666 && dbg == 2)
@@ -3835,8 +3837,9 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
           const long long* q = h.data() + 4 * 4096;
           for (int i = 1; i < 64 && q[i]; ++i) fprintf(stderr, " %lld", q[i] - q[i - 1]);
           fprintf(stderr, "\n");
-        }
-        else if (b666 && knob("MMSEG_BRICKR_PF", 0))
+        } else
+#endif
+        if (b666 && knob("MMSEG_BRICKR_PF", 0))
           hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6, 0, true>), grid, block, 0, s, g, 6, 6, 6);
         else if (b666 && rb32)
           hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6, 0, false, true>), grid, block, 0, s, g, 6, 6, 6);
@@ -3907,7 +3910,8 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
         if (g.H % 4 == 0 && g.W % 16 == 0 && g.ldo % 8 == 0 && (reinterpret_cast<uintptr_t>(g.out) & 15) == 0 &&
             knob("MMSEG_BRICK5", 1)) {   // (16-B output stores)
           const bool dma = knob("MMSEG_BRICK5_DMA", 0) != 0;
-          if (knob("MMSEG_BRICK5_DBG", 0)) {   // phase timing probe (diagnostics only)
+#ifdef MMSEG_TIMING_PROBES
+          if (knob("MMSEG_BRICK5_DBG", 0)) {   // phase timing probe (diagnostics only, -DMMSEG_TIMING_PROBES)
             static long long* dbg = nullptr;
             if (!dbg) hipMalloc(&dbg, 4 * 128 * sizeof(long long));
             hipMemsetAsync(dbg, 0, 4 * 128 * sizeof(long long), s);
@@ -3924,7 +3928,9 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
               for (int i = 1; i < n; ++i) fprintf(stderr, " %lld", q[i] - q[i - 1]);
               fprintf(stderr, "\n");
             }
-          } else {
+          } else
+#endif
+          {
             launch_brick5(g, s, nullptr, dma);
           }
         } else {
@@ -4039,7 +4045,11 @@ int launch_gemm_mode(GemmArgs g, int mode, hipStream_t s) {
 
 template <typename T, int MODE>
 int launch_wgrad(WgradArgs g, hipStream_t s) {
-  g.dbg = knob("MMSEG_WGRAD_DBG", 0);
+#ifdef MMSEG_TIMING_PROBES
+  g.dbg = knob("MMSEG_WGRAD_DBG", 0);   // 1 = no loads after the first brick, 2 = no MFMA (wrong results)
+#else
+  g.dbg = 0;
+#endif
   dim3 block(256);
   if constexpr (sizeof(T) == 2) {
     if (MODE == MODE_CONV3 && g.brick == 3) {

@@ -414,3 +414,42 @@ def test_swin_unetr_dropout_matches_oracle(dev, swin_case):
     m0 = _model(dev, torch.float32).eval()
     with torch.no_grad():
         assert torch.equal(m(x[:1].to(dev)), m0(x[:1].to(dev)))
+
+
+def test_swin_unetr_c4_size(dev):
+    """BASELINE config c4 at its own size: SwinUNETR feature_size 48, CT+PET 128^3, batch 1 (6 classes, as
+    bench.py --model swin_unetr).  fp32 engine forward against oracle/swin_oracle.py in fp32 on the host (1024
+    seeded voxels x every class, normwise 1e-3 -- the north_star logits tolerance; parity vs MONAI itself stays
+    unpinned), then three bf16 Trainer.train_step steps through build_model: finite and decreasing loss."""
+    import sys
+    sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__file__)))
+    from bench import make_config
+    from mmseg_amd.models.build import build_model
+    from mmseg_amd.trainer.trainer import Trainer
+    g = torch.Generator().manual_seed(48)
+    x = torch.randn(1, 2, 128, 128, 128, generator=g)
+    y = torch.randint(0, 6, (1, 128, 128, 128), generator=g)
+    idx = torch.randint(0, 128 ** 3, (1024,), generator=g)
+    cfg = make_config("swin_unetr", 1, "fp32", size=128)
+    torch.manual_seed(0)
+    m = build_model(cfg)
+    m.eval()
+    with torch.no_grad():
+        out = m(x.to(dev))
+        p = {k: v.detach().cpu().float() for k, v in m.backbone.model.named_parameters()}
+        ref = SO.swin_unetr_forward(p, x, m.backbone.depths, m.backbone.num_heads)
+    assert out.shape == (1, 6, 128, 128, 128)
+    e = rel(out.reshape(6, -1)[:, idx.to(dev)], ref.reshape(6, -1)[:, idx])
+    print(f"\nc4 fp32 forward vs oracle: {e:.2e}")
+    assert e < 1e-3
+    del out, ref, p
+    cfg = make_config("swin_unetr", 1, "bf16", size=128)
+    cfg["training"]["optimizer"]["lr"] = 1e-3
+    torch.manual_seed(0)
+    m = build_model(cfg)
+    tr = Trainer(cfg, m)
+    m.train()
+    batch = {"image": x.to(dev), "label": y.to(dev)}
+    losses = [tr.train_step(batch, i) for i in range(3)]
+    print("c4 bf16 losses", losses)
+    assert all(np.isfinite(losses)) and losses[-1] < losses[0]
