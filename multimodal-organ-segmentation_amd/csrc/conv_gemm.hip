@@ -797,15 +797,20 @@ __device__ __forceinline__ void buf_load_v8<bf16_t>(V8<bf16_t>& v, __amdgpu_buff
   const i32x4 t = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
   v.v = __builtin_bit_cast(bf16x8, t);
 }
+// The whole vector is bit-cast at once.  Casting element by element (__builtin_bit_cast(float, a[j])) is
+// miscompiled by hipcc (ROCm 7.2, gfx950): the b128 loads were narrowed to buffer_load_dword and element 0 was
+// copied into all four registers (v173..v175 = v172 in the disassembly), which is why the fp32 instantiation
+// of the 32-bit staging gave wrong results in r02 (tests/test_kernels_gpu.py::test_b32_halo_staging).
 template <>
 __device__ __forceinline__ void buf_load_v8<float>(V8<float>& v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
   typedef int i32x4 __attribute__((ext_vector_type(4)));
-  const i32x4 a = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-  const i32x4 b = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16, 0, 0);
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  const f32x4v a = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  const f32x4v b = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16, 0, 0));
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    v.v[j] = __builtin_bit_cast(float, a[j]);
-    v.v[4 + j] = __builtin_bit_cast(float, b[j]);
+    v.v[j] = a[j];
+    v.v[4 + j] = b[j];
   }
 }
 
@@ -2876,6 +2881,188 @@ __device__ __forceinline__ void wd_dma16(uint32_t lds, uint32_t voff, wd_rsrc_t 
   asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds), "v"(voff), "s"(r)
                : "memory", "m0");
 }
+
+// ------------------------------------------------- brick conv v8 (3^3, bf16, 8 waves, LDS-DMA staging)
+// conv3_brick2's BN-column tile with the block doubled to an 8 x 8 x 8 brick: 8 waves, wave w owns z plane w
+// (64 voxels = 4 row tiles of two 8-voxel x rows) x BN columns.  Both operands are staged by LDS-DMA
+// (buffer_load ... lds): no staging registers and no ds_write pass, which in conv3_brick2 were ~2 VALU + 0.7 SALU
+// per MFMA around a per-stage register round trip of the weights.  Per block:
+//   * the halo image of one 32-channel input chunk: 10 x 10 rows of 10 voxels x 4 quads + 2 pad quads (the pad
+//     keeps the 16-lane groups of the A-fragment ds_read_b128 on distinct banks), single buffer, re-filled
+//     between chunks (that refill is the one exposed load: 1 of 3 * nchunk stages);
+//   * the weight slice of one (chunk, kz) stage: 9 taps x BN columns x 32 channels in the B-operand order
+//     [tap][col][4 quads, channel group kg at slot kg ^ w2_swz(col)], double buffered: stage s + 1's slice
+//     lands while stage s is multiplied.
+// The lane-linear DMA destination is matched by computing, per lane, the source of the quad that belongs at its
+// LDS slot (pads and out-of-volume voxels read zeros through the OOB offset).  Each staged weight slice feeds
+// 8 waves x 9 taps x 4 x RN MFMAs (twice conv3_brick2's).  LDS 141 KB (BN 64): one block per CU, two waves
+// per SIMD.  Requirements (host): bf16, Cin % 32 == 0, Ncols % BN == 0, D % 8, H % 8, W % 8, ksplit == 1, no
+// fused stats / deferred norm / IN partials, the A and B extents < 2^31 bytes.
+template <int BN>
+__global__ __launch_bounds__(512, 1) void conv3_brick8_kernel(GemmArgs g) {
+  typedef bf16_t T;
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  constexpr int QV = 4;                                  // 16-B quads per halo voxel (32 channels)
+  constexpr int HXY = 10, HZ = 10;
+  constexpr int RY = HXY * QV + 2, RZ = HXY * RY;        // 42 quads per halo row, 420 per plane
+  constexpr int XQ = HZ * RZ;                            // 4200
+  constexpr int XI = (XQ + 63) / 64, XK = (XI + 7) / 8;  // 66 wave-instructions, <= 9 per wave
+  constexpr int XQP = XI * 64;
+  constexpr int WQ = 9 * BN * QV;                        // 2304 quads (BN 64)
+  constexpr int WI = WQ / 64, WK = (WI + 7) / 8;         // 36, <= 5 per wave
+  constexpr int RM = 4, RN = BN / 16;
+  constexpr int EPQ = 8;                                 // bf16 per quad
+  static_assert(WQ % 64 == 0, "weight slice must be whole wave-instructions");
+  __shared__ __attribute__((aligned(16))) float4 lds4[XQP + 2 * WQ];
+  T* Xl = reinterpret_cast<T*>(lds4);
+  T* Wl = reinterpret_cast<T*>(lds4 + XQP);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int bz_n = g.D >> 3, by_n = g.H >> 3, bx_n = g.W >> 3;
+  const int nbrick = (g.M / (g.D * g.H * g.W)) * bz_n * by_n * bx_n;
+  const int nt_n = g.Ncols / BN;
+  const int tile = g.swz ? xcd_swizzle(blockIdx.x, nbrick * nt_n) : (int)blockIdx.x;
+  int bidx = tile % nbrick;
+  const int nt = tile / nbrick;
+  const int bx = bidx % bx_n; bidx /= bx_n;
+  const int by = bidx % by_n; bidx /= by_n;
+  const int bz = bidx % bz_n;
+  const int n = bidx / bz_n;
+  const int z0 = bz * 8, y0 = by * 8, x0 = bx * 8;
+  const int n0 = nt * BN;
+  const int cin = 8 << g.cpg_shift;
+  const int nchunk = gemm_nchunk(g);
+  const int nstage = nchunk * 3;
+  const long long HW = (long long)g.H * g.W;
+  const long long nbase = (long long)n * g.D * HW;
+
+  const wd_rsrc_t arsrc = wd_rsrc(g.a, (uint32_t)((long long)g.M * g.lda * 2));
+  const int KGp = (g.KG + 3) & ~3;
+  const wd_rsrc_t brsrc = wd_rsrc(g.b, (uint32_t)((long long)KGp * g.Cpad * 16));
+
+  // per-lane halo sources: quad p = 64 m + lane of instruction m = wave + 8 kk, byte offset of chunk 0 or OOB
+  uint32_t xo[XK];
+#pragma unroll
+  for (int kk = 0; kk < XK; ++kk) {
+    const int p = (wave + 8 * kk) * 64 + lane;
+    const int row = p / RY, qi = p - row * RY;
+    const int hz = row / HXY, hy = row - hz * HXY, hx = qi >> 2, cg = qi & 3;
+    const int z = z0 - 1 + hz, y = y0 - 1 + hy, x = x0 - 1 + hx;
+    const bool ok = p < XQ && qi < HXY * QV && (unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H &&
+                    (unsigned)x < (unsigned)g.W;
+    xo[kk] = ok ? (uint32_t)((((n * g.D + z) * g.H + y) * g.W + x) * g.lda * 2 + cg * 16) : WD_OOB;
+  }
+  // per-lane weight sources: quad p = (t9 * BN + col) * 4 + slot, channel group slot ^ w2_swz(col)
+  uint32_t wo[WK];
+#pragma unroll
+  for (int kk = 0; kk < WK; ++kk) {
+    const int p = (wave + 8 * kk) * 64 + lane;
+    const int q = p >> 2, col = q % BN, t9 = q / BN;
+    const int cg = (p & 3) ^ w2_swz(col);
+    wo[kk] = (uint32_t)(((t9 * (cin / 8) + cg) * g.Cpad + n0 + col) * 16);
+  }
+  const uint32_t xl_base = (uint32_t)(uintptr_t)(lds_ptr_t)Xl;
+  const uint32_t wl_base = (uint32_t)(uintptr_t)(lds_ptr_t)Wl;
+  auto issue_x = [&](int c) {
+#pragma unroll
+    for (int kk = 0; kk < XK; ++kk) {
+      const int m = wave + 8 * kk;
+      if (m < XI)
+        wd_dma16(__builtin_amdgcn_readfirstlane((int)(xl_base + m * 1024)),
+                 xo[kk] == WD_OOB ? WD_OOB : xo[kk] + c * 64, arsrc);
+    }
+  };
+  auto issue_w = [&](int s, int buf) {
+    const int c = s / 3, kz = s - c * 3;
+    const uint32_t so = (uint32_t)((kz * 9 * (cin / 8) + c * 4) * g.Cpad * 16);
+#pragma unroll
+    for (int kk = 0; kk < WK; ++kk) {
+      const int m = wave + 8 * kk;
+      if (m < WI)
+        wd_dma16(__builtin_amdgcn_readfirstlane((int)(wl_base + (buf * WQ + m * 64) * 16)), wo[kk] + so, brsrc);
+    }
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int r16 = lane & 15, kg = lane >> 4;
+  int aq[RM];   // halo quad of the lane's row for tap (0,0,0), group kg: z plane = wave
+#pragma unroll
+  for (int i = 0; i < RM; ++i) aq[i] = wave * RZ + (2 * i + (r16 >> 3)) * RY + (r16 & 7) * QV + kg;
+  int bq[RN];
+#pragma unroll
+  for (int j = 0; j < RN; ++j) {
+    const int col = j * 16 + r16;
+    bq[j] = col * QV + (kg ^ w2_swz(col));
+  }
+
+  issue_x(0);
+  issue_w(0, 0);
+  __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): this wave's pieces have landed
+  __syncthreads();
+  for (int s = 0; s < nstage; ++s) {
+    const int kz = s % 3, b = s & 1;
+    const bool more = s + 1 < nstage;
+    if (more) issue_w(s + 1, b ^ 1);
+    const T* Wb = Wl + b * WQ * EPQ;
+    V8<T> af[2][RM], bf[2][RN];
+    auto rd = [&](int t9, int k) {
+      const int ky = t9 / 3, kx = t9 - ky * 3;
+      const int hoff = kz * RZ + ky * RY + kx * QV;
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bf[k][j].load(Wb + (t9 * BN * QV + bq[j]) * EPQ);
+#pragma unroll
+      for (int i = 0; i < RM; ++i) af[k][i].load(Xl + (aq[i] + hoff) * EPQ);
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int t9 = 0; t9 < 9; ++t9) {
+      if (t9 < 8) rd(t9 + 1, (t9 + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) mfma_step<T>(acc[i][j], af[t9 & 1][i], bf[t9 & 1][j]);
+    }
+    if (more) {
+      if ((s + 1) % 3 == 0) {           // next chunk: every wave is done with this halo, then refill it
+        __syncthreads();
+        issue_x((s + 1) / 3);
+      }
+      __builtin_amdgcn_s_waitcnt(0x0f70);
+      __syncthreads();
+    }
+  }
+
+  // epilogue: acc (+bias) -> LDS tile [512 voxels][BN + 8] -> 16-B stores
+  __syncthreads();
+  T* El = reinterpret_cast<T*>(lds4);
+  constexpr int EP = BN + 8;
+  static_assert(512 * EP * 2 <= (XQP + 2 * WQ) * 16, "epilogue tile must fit");
+#pragma unroll
+  for (int j = 0; j < RN; ++j) {
+    const int col = j * 16 + r16;
+    const float bv = (g.bias && n0 + col < g.Ncols) ? g.bias[n0 + col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) El[(wave * 64 + 16 * i + 4 * kg + r) * EP + col] = from_f<T>(acc[i][j][r] + bv);
+  }
+  __syncthreads();
+  constexpr int CG = BN / 8;
+#pragma unroll
+  for (int k = 0; k < 512 * CG / 512; ++k) {
+    const int e = tid + k * 512;
+    const int v = e / CG, cg = e % CG;
+    const int z = z0 + (v >> 6), y = y0 + ((v >> 3) & 7), x = x0 + (v & 7);
+    V8<T> o;
+    o.load(El + v * EP + cg * 8);
+    o.store(out_at<T>(g, nbase + z * HW + (long long)y * g.W + x, n0 + cg * 8));
+  }
+}
 // PIPE: the fragment reads of the next (dy plane, tap) step are issued before the current step's MFMAs
 template <int MT, bool NORM = false, int NST = 3, bool PIPE = false>
 __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
@@ -3875,6 +4062,19 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
   if (plan.kind == 1 && g.ksplit == 1) {
     const int nb1 = (g.M / (g.D * g.H * g.W)) * (g.D / 4) * (g.H / B2_Y) * (g.W / B2_X);
     const int min_blocks = knob("MMSEG_BRICK2_MINBLK", 512);
+    if constexpr (sizeof(T) == 2) {
+      // 8-wave 8x8x8 brick with LDS-DMA staging (conv3_brick8_kernel)
+      const int nb8 = nb1 / 2;   // 8-deep bricks
+      if (knob("MMSEG_BRICK8", 0) && g.Ncols % 64 == 0 && g.D % 8 == 0 && g.H % 8 == 0 && g.W % 8 == 0 &&
+          g.stats == nullptr && g.nmean == nullptr && g.inpart == nullptr && g.ldo % 8 == 0 &&
+          (!g.out2 || g.ldo2 % 8 == 0) && (reinterpret_cast<uintptr_t>(g.out) & 15) == 0 &&
+          nb8 * (g.Ncols / 64) >= knob("MMSEG_BRICK8_MINBLK", 256) &&
+          (long long)g.M * g.lda * 2 < (1LL << 31) && (long long)((g.KG + 3) & ~3) * g.Cpad * 16 < (1LL << 31)) {
+        mmseg::note_kernel("conv3_brick8_kernel<BN64>");
+        hipLaunchKernelGGL((conv3_brick8_kernel<64>), dim3(nb8 * (g.Ncols / 64)), dim3(512), 0, s, g);
+        return mmseg::check_launch("conv3_brick8");
+      }
+    }
     // v3 is bf16 only: its fp32 instantiation (f32 16x16x4 MFMA with swapped operands) returned the first
     // row of each 4-row accumulator group in all four registers (tools/diag_b3.py); the fp32 parity path
     // keeps the v2 kernel.

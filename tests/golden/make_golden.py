@@ -291,35 +291,65 @@ def full_grad_case(tag, cfg, S, B, seed, k=4096):
     the configured loss, backward.  Stored: loss, 1024 seeded voxels of every logit channel, the argmax
     histogram, and per parameter gradient its L2 norm, sum and the values at k seeded positions (all of them
     for tensors with <= k elements).  Initial weights are reproduced by torch.manual_seed(seed) + build_model."""
-    torch.manual_seed(seed)
-    model = build.build_model(cfg)
     M = len(cfg["data"]["modalities"])
     C = cfg["model"]["out_channels"]
     x, y, idx = full_inputs(S, B, M, C, seed)
     crit = losses.get_loss(cfg)
-    model.train()
-    out = model(x)
-    loss = crit(out, y)
-    loss.backward()
-    names, norms, sums, sidx, sval, soff = [], [], [], [], [], [0]
-    for i, (n, p) in enumerate(model.backbone.named_parameters()):
-        g = p.grad.detach().double().reshape(-1)
-        names.append(n)
-        norms.append(g.norm().item())
-        sums.append(g.sum().item())
-        gi = grad_sample_index(g.numel(), k, seed * 1000 + i)
-        sidx.append(gi)
-        sval.append(g[torch.from_numpy(gi)].numpy())
-        soff.append(soff[-1] + len(gi))
-    flat = out.detach().reshape(B, C, -1)
+
+    def run(mode):
+        """mode f32: the reference as it runs on CPU; f64: the same step in double (its rounding-free answer);
+        bf16: under torch.autocast("cpu", bfloat16), the CPU analogue of the reference's own mixed-precision
+        step (trainer.py:237-243 autocasts in fp16 on a GPU).  The f64 / bf16 runs measure how far rounding
+        alone moves these gradients: at 96^3 a few hundred ReLU / MaxPool decisions per layer sit within rounding
+        of their kink (fp32), tens of thousands at bf16, and every weight gradient is a heavily cancelling sum
+        over 1.8 M voxels."""
+        torch.manual_seed(seed)
+        model = build.build_model(cfg)
+        if mode == "f64":
+            model = model.double()
+        model.train()
+        xin = x.double() if mode == "f64" else x
+        if mode == "bf16":
+            with torch.autocast("cpu", dtype=torch.bfloat16):
+                out = model(xin)
+            loss = crit(out.float(), y)
+        else:
+            out = model(xin)
+            loss = crit(out, y)
+        loss.backward()
+        res = {"loss": loss.item(), "out": out.detach().float(), "names": [], "norms": [], "sums": [], "sidx": [],
+               "sval": []}
+        for i, (n, p) in enumerate(model.backbone.named_parameters()):
+            g = p.grad.detach().double().reshape(-1)
+            res["names"].append(n)
+            res["norms"].append(g.norm().item())
+            res["sums"].append(g.sum().item())
+            gi = grad_sample_index(g.numel(), k, seed * 1000 + i)
+            res["sidx"].append(gi)
+            res["sval"].append(g[torch.from_numpy(gi)].numpy())
+        return res
+
+    r32, r64, rbf = run("f32"), run("f64"), run("bf16")
+    out = r32["out"]
+    soff = np.cumsum([0] + [len(v) for v in r32["sidx"]])
+    flat = out.reshape(B, C, -1)
     np.savez_compressed(os.path.join(OUT, f"{tag}.npz"), S=np.int64(S), B=np.int64(B), seed=np.int64(seed),
-                        k=np.int64(k), loss=np.float64(loss.item()), sample_idx=idx,
+                        k=np.int64(k), loss=np.float64(r32["loss"]), loss64=np.float64(r64["loss"]),
+                        lossbf=np.float64(rbf["loss"]), sample_idx=idx,
                         sample_logits=flat[:, :, idx].numpy(),
-                        logits_sum=np.float64(out.detach().double().sum()),
-                        argmax_hist=np.bincount(out.detach().argmax(1).flatten().numpy(), minlength=C),
-                        param_names=np.array(names), grad_norm=np.array(norms), grad_sum=np.array(sums),
-                        gs_idx=np.concatenate(sidx), gs_val=np.concatenate(sval), gs_off=np.array(soff))
-    print(tag, "loss", loss.item(), "params", len(names))
+                        sample_logits64=r64["out"].reshape(B, C, -1)[:, :, idx].numpy(),
+                        logits_sum=np.float64(out.double().sum()),
+                        argmax_hist=np.bincount(out.argmax(1).flatten().numpy(), minlength=C),
+                        param_names=np.array(r32["names"]), grad_norm=np.array(r32["norms"]),
+                        grad_norm64=np.array(r64["norms"]), grad_sum=np.array(r32["sums"]),
+                        gs_idx=np.concatenate(r32["sidx"]), gs_val=np.concatenate(r32["sval"]),
+                        gs_val64=np.concatenate(r64["sval"]), gs_valbf=np.concatenate(rbf["sval"]),
+                        gs_off=soff)
+    e32 = [np.linalg.norm(a - b) / np.linalg.norm(b) for a, b in zip(r32["sval"], r64["sval"])]
+    ebf = [np.linalg.norm(a - b) / np.linalg.norm(b) for a, b in zip(rbf["sval"], r64["sval"])]
+    print(tag, "loss", r32["loss"], r64["loss"], rbf["loss"], "params", len(r32["names"]),
+          f"grad err vs f64: f32 median {np.median(e32):.2e} max {max(e32):.2e}; "
+          f"bf16 median {np.median(ebf):.2e} max {max(ebf):.2e}")
 
 
 def _phantom_batch(seed, S, C, mods):

@@ -76,6 +76,7 @@ def test_engine_checkpoint_matches_reference_format(dev, tmp_path):
     template), so the reference's load_checkpoint / _resume can read it."""
     ref = torch.load(REF_CKPT, map_location="cpu", weights_only=True)
     cfg = _small_cfg(tmp_path)
+    cfg["training"]["checkpoint"] = {"save_last": True, "save_best": True}
     torch.manual_seed(0)
     m = build_model(cfg)
     tr = Trainer(cfg, m)

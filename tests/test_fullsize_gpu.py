@@ -1,23 +1,28 @@
 """Full-size training-step parity: the engine's step at the BASELINE sizes (96^3, B=2) against the reference's
 own training step captured by tests/golden/make_golden.py (full_grad_case: reference train-mode forward + loss +
-backward, trainer.py:250-254).
+backward, trainer.py:250-254), run three ways on the CPU: as is (fp32), in fp64 (the rounding-free answer) and
+under torch.autocast("cpu", bfloat16) (the CPU analogue of the reference's own mixed-precision step,
+trainer.py:237-243).
 
 Cases: c2 UNet3D CT+PET 6 classes DiceCE; c3 DualEncoder "cross_attention" (= mean fusion, the bench
-workload) DiceCE; c5 DualEncoder CT+PET+MRI Tversky.  Each runs in fp32 (the parity path) and in bf16 (the
-path bench.py times: brick5 / brick3 / brick2-BN64 with 32-bit staging, wgrad_dma, the fused InstanceNorm
-partials, the fused head + loss), through Trainer._fused_loss exactly as Trainer.train_step does.
+workload) DiceCE; c5 DualEncoder CT+PET+MRI Tversky.  Each runs in fp32 (the parity path) and in bf16 (the path
+bench.py times: brick5 / brick3 / brick2-BN64 with 32-bit staging, wgrad_dma, the fused InstanceNorm partials,
+the fused head + loss), through Trainer._fused_loss exactly as Trainer.train_step does.
 
-Compared per parameter tensor, on the fixture's seeded gradient samples (k = 4096 positions, all of them for
-smaller tensors): normwise L2 error ||g - g_ref|| / ||g_ref||, and the full-tensor L2 norm against the
-reference's.  Conv biases in front of an InstanceNorm have a mathematically zero gradient (pure rounding
-noise) and are only bounded in size.
-
-Tolerances:
-  * fp32: loss 1e-5 relative; sampled logits 1e-3 normwise (north_star); every gradient 1e-3 normwise (the
-    transposed-conv bias, nearly dead, 1e-2); argmax histogram within 1e-4 of the voxels.
-  * bf16: activations are stored in bf16 (8 mantissa bits, relative rounding 2^-9 = 2e-3 per store, ~20
-    stores deep); loss 2e-3 relative; logits 3e-2 normwise; every gradient 8e-2 normwise and the median over
-    tensors 3e-2; gradient norms 5e-2.
+Why the gradient bounds are relative to the reference's own rounding error: at 96^3 every weight gradient is a
+heavily cancelling sum over 1.8 M voxels, and a ReLU / MaxPool decision within rounding of its kink routes one
+voxel's gradient discretely.  The reference's OWN fp32 gradients differ from its fp64 ones by 3e-3..8e-3
+(median over tensors), its bf16-autocast gradients by 0.43..0.50 -- on these random inputs the gradient is
+mostly noise that rounding re-draws.  So per parameter tensor (normwise L2 on the fixture's 4096 seeded
+positions, all of them for smaller tensors), with e(x) = ||x - ref_fp64|| / ||ref_fp64||:
+  * fp32 engine: e(engine) <= max(4 e(ref_fp32), 2 median e(ref_fp32)), and median e(engine) <= 2 median
+    e(ref_fp32);
+  * bf16 engine: e(engine) <= max(2 e(ref_bf16), median e(ref_bf16)), and median e(engine) <= 1.5 median
+    e(ref_bf16).
+A wiring error (a wrong buffer, a missing term) moves a gradient by O(1) and its norm by O(1); the gradient
+norms are held to 1e-3 (fp32) / 5e-2 (bf16) of the reference's.  Conv biases in front of an InstanceNorm
+have a mathematically zero gradient (rounding noise) and are only bounded in size.
+Loss: fp32 1e-5 relative to fp64; bf16 1e-3.  Sampled logits: 1e-3 normwise (north_star) / 3e-2 (bf16).
 """
 import numpy as np
 import pytest
@@ -34,11 +39,6 @@ CASES = {
     "fullgrad_unet_c2": ("unet", ["CT", "PET"], "dice_ce"),
     "fullgrad_dual_c3": ("dual_encoder", ["CT", "PET"], "dice_ce"),
     "fullgrad_dual_m3_c5": ("dual_encoder", ["CT", "PET", "MRI"], "tversky"),
-}
-
-TOL = {
-    "float32": dict(loss=1e-5, logits=1e-3, grad=1e-3, grad_near=1e-2, median=1e-3, norm=1e-3),
-    "bfloat16": dict(loss=2e-3, logits=3e-2, grad=8e-2, grad_near=8e-2, median=3e-2, norm=5e-2),
 }
 
 
@@ -68,6 +68,10 @@ def full_inputs(S, B, M, C, seed):
     return x, y, idx
 
 
+def _l2(a, b):
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
 @pytest.mark.parametrize("tag", list(CASES))
 def test_fullsize_training_step_matches_reference(dev, tag, dtype):
@@ -90,39 +94,47 @@ def test_fullsize_training_step_matches_reference(dev, tag, dtype):
     with torch.no_grad():
         logits = m(x)
     torch.cuda.synchronize()
-    t = TOL[dtype]
-    ref_loss = float(g["loss"])
-    err_loss = abs(lossv.item() - ref_loss) / abs(ref_loss)
+    bf = dtype == "bfloat16"
+    loss64 = float(g["loss64"])
+    err_loss = abs(lossv.item() - loss64) / abs(loss64)
     err_logits = rel(logits.reshape(B, C, -1)[:, :, torch.from_numpy(idx).to(dev)],
-                     torch.from_numpy(g["sample_logits"]))
-    errs, norm_errs, dead_sizes, typical = {}, {}, {}, []
+                     torch.from_numpy(g["sample_logits64"]))
     bb = dict(m.backbone.named_parameters())
     off = g["gs_off"]
+    ref_key = "gs_valbf" if bf else "gs_val"
+    e_eng, e_ref, norm_err, dead, typical = {}, {}, {}, {}, []
     for i, n in enumerate(names):
-        gi = torch.from_numpy(g["gs_idx"][off[i]:off[i + 1]]).to(dev)
-        gref = torch.from_numpy(g["gs_val"][off[i]:off[i + 1]])
-        geng = bb[n].grad.reshape(-1)[gi].double().cpu()
+        sl = slice(off[i], off[i + 1])
+        gi = torch.from_numpy(g["gs_idx"][sl]).to(dev)
+        g64 = g["gs_val64"][sl]
+        geng = bb[n].grad.reshape(-1)[gi].double().cpu().numpy()
         if n.endswith(("conv1.bias", "conv2.bias")):
-            dead_sizes[n] = float(geng.norm())
+            dead[n] = float(np.linalg.norm(geng))
             continue
-        errs[n] = float((geng - gref).norm() / gref.norm())
-        norm_errs[n] = abs(float(bb[n].grad.double().norm()) - float(g["grad_norm"][i])) / float(g["grad_norm"][i])
-        typical.append(float(g["grad_norm"][i]) / np.sqrt(bb[n].numel()))
-    med = float(np.median(list(errs.values())))
-    worst = sorted(((v, n) for n, v in errs.items()), reverse=True)[:5]
-    print(f"\n{tag} {dtype}: loss {lossv.item():.7f} vs {ref_loss:.7f} (rel {err_loss:.2e}), logits {err_logits:.2e}, "
-          f"grad median {med:.2e}, worst {[(round(v, 5), n) for v, n in worst]}, "
-          f"norm worst {max(norm_errs.values()):.2e}")
-    assert err_loss < t["loss"], err_loss
-    assert err_logits < t["logits"], err_logits
-    bad = {n: v for n, v in errs.items() if v > (t["grad_near"] if n.endswith("up.bias") else t["grad"])}
+        e_eng[n] = _l2(geng, g64)
+        e_ref[n] = _l2(g[ref_key][sl], g64)
+        norm_err[n] = abs(float(bb[n].grad.double().norm()) - float(g["grad_norm64"][i])) / float(g["grad_norm64"][i])
+        typical.append(float(g["grad_norm64"][i]) / np.sqrt(bb[n].numel()))
+    med_eng, med_ref = float(np.median(list(e_eng.values()))), float(np.median(list(e_ref.values())))
+    ratio = {n: e_eng[n] / e_ref[n] for n in e_eng}
+    worst = sorted(((r, n) for n, r in ratio.items()), reverse=True)[:4]
+    print(f"\n{tag} {dtype}: loss {lossv.item():.7f} vs fp64 {loss64:.7f} (rel {err_loss:.2e}), logits {err_logits:.2e}; "
+          f"grad error vs fp64: engine median {med_eng:.2e}, reference {'bf16' if bf else 'fp32'} median {med_ref:.2e}; "
+          f"worst engine/reference ratios {[(round(r, 2), nm) for r, nm in worst]}; "
+          f"norm worst {max(norm_err.values()):.2e}")
+    assert err_loss < (1e-3 if bf else 1e-5), err_loss
+    assert err_logits < (3e-2 if bf else 1e-3), err_logits
+    k, floor = (2.0, 1.0) if bf else (4.0, 2.0)
+    bad = {n: (round(e_eng[n], 5), round(e_ref[n], 5)) for n in e_eng
+           if e_eng[n] > max(k * e_ref[n], floor * med_ref)}
     assert not bad, bad
-    assert med < t["median"], med
-    bad = {n: v for n, v in norm_errs.items() if v > (t["grad_near"] if n.endswith("up.bias") else t["norm"])}
+    assert med_eng <= (1.5 if bf else 2.0) * med_ref, (med_eng, med_ref)
+    ntol = 5e-2 if bf else 1e-3
+    bad = {n: v for n, v in norm_err.items() if v > (10 * ntol if n.endswith("up.bias") else ntol)}
     assert not bad, bad
     # mathematically-zero gradients stay at the rounding-noise scale of the live ones
     scale = float(np.median(typical)) * np.sqrt(4096)
-    assert all(v < 1e-2 * scale for v in dead_sizes.values()), dead_sizes
-    if dtype == "float32":
+    assert all(v < 1e-2 * scale for v in dead.values()), dead
+    if not bf:
         hist = torch.bincount(logits.argmax(1).reshape(-1), minlength=C).cpu().numpy()
         assert np.abs(hist - g["argmax_hist"]).sum() <= 1e-4 * hist.sum()
