@@ -2883,8 +2883,9 @@ __device__ __forceinline__ void wd_dma16(uint32_t lds, uint32_t voff, wd_rsrc_t 
 }
 
 // ------------------------------------------------- brick conv v8 (3^3, bf16, 8 waves, LDS-DMA staging)
-// conv3_brick2's BN-column tile with the block doubled to an 8 x 8 x 8 brick: 8 waves, wave w owns z plane w
-// (64 voxels = 4 row tiles of two 8-voxel x rows) x BN columns.  Both operands are staged by LDS-DMA
+// conv3_brick2's BN-column tile with the block grown to an (8 ZP) x 8 x 8 brick: 8 waves, wave w owns z planes
+// w ZP .. w ZP + ZP - 1 (64 voxels each = 4 row tiles of two 8-voxel x rows) x BN columns (BN 64 with ZP 1; BN 32
+// with ZP 2, so a wave still runs 16 MFMAs per tap).  Both operands are staged by LDS-DMA
 // (buffer_load ... lds): no staging registers and no ds_write pass, which in conv3_brick2 were ~2 VALU + 0.7 SALU
 // per MFMA around a per-stage register round trip of the weights.  Per block:
 //   * the halo image of one 32-channel input chunk: 10 x 10 rows of 10 voxels x 4 quads + 2 pad quads (the pad
@@ -2895,22 +2896,23 @@ __device__ __forceinline__ void wd_dma16(uint32_t lds, uint32_t voff, wd_rsrc_t 
 //     lands while stage s is multiplied.
 // The lane-linear DMA destination is matched by computing, per lane, the source of the quad that belongs at its
 // LDS slot (pads and out-of-volume voxels read zeros through the OOB offset).  Each staged weight slice feeds
-// 8 waves x 9 taps x 4 x RN MFMAs (twice conv3_brick2's).  LDS 141 KB (BN 64): one block per CU, two waves
-// per SIMD.  Requirements (host): bf16, Cin % 32 == 0, Ncols % BN == 0, D % 8, H % 8, W % 8, ksplit == 1, no
+// 8 waves x 9 taps x 4 ZP x RN MFMAs (twice conv3_brick2's).  LDS 141 KB (BN 64) / 155 KB (BN 32): one block per
+// CU, two waves per SIMD.  Requirements (host): bf16, Cin % 32 == 0, Ncols % BN == 0, D % 8 ZP, H % 8, W % 8, ksplit == 1, no
 // fused stats / deferred norm / IN partials, the A and B extents < 2^31 bytes.
-template <int BN>
+template <int BN, int ZP>
 __global__ __launch_bounds__(512, 1) void conv3_brick8_kernel(GemmArgs g) {
   typedef bf16_t T;
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   constexpr int QV = 4;                                  // 16-B quads per halo voxel (32 channels)
-  constexpr int HXY = 10, HZ = 10;
+  constexpr int BZ = 8 * ZP;                            // z planes per brick (ZP per wave)
+  constexpr int HXY = 10, HZ = BZ + 2;
   constexpr int RY = HXY * QV + 2, RZ = HXY * RY;        // 42 quads per halo row, 420 per plane
-  constexpr int XQ = HZ * RZ;                            // 4200
-  constexpr int XI = (XQ + 63) / 64, XK = (XI + 7) / 8;  // 66 wave-instructions, <= 9 per wave
+  constexpr int XQ = HZ * RZ;                            // 4200 (ZP 1) / 7560 (ZP 2)
+  constexpr int XI = (XQ + 63) / 64, XK = (XI + 7) / 8;  // 66 / 119 wave-instructions
   constexpr int XQP = XI * 64;
   constexpr int WQ = 9 * BN * QV;                        // 2304 quads (BN 64)
   constexpr int WI = WQ / 64, WK = (WI + 7) / 8;         // 36, <= 5 per wave
-  constexpr int RM = 4, RN = BN / 16;
+  constexpr int RM = 4 * ZP, RN = BN / 16;
   constexpr int EPQ = 8;                                 // bf16 per quad
   static_assert(WQ % 64 == 0, "weight slice must be whole wave-instructions");
   __shared__ __attribute__((aligned(16))) float4 lds4[XQP + 2 * WQ];
@@ -2918,7 +2920,7 @@ __global__ __launch_bounds__(512, 1) void conv3_brick8_kernel(GemmArgs g) {
   T* Wl = reinterpret_cast<T*>(lds4 + XQP);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int bz_n = g.D >> 3, by_n = g.H >> 3, bx_n = g.W >> 3;
+  const int bz_n = g.D / BZ, by_n = g.H >> 3, bx_n = g.W >> 3;
   const int nbrick = (g.M / (g.D * g.H * g.W)) * bz_n * by_n * bx_n;
   const int nt_n = g.Ncols / BN;
   const int tile = g.swz ? xcd_swizzle(blockIdx.x, nbrick * nt_n) : (int)blockIdx.x;
@@ -2928,7 +2930,7 @@ __global__ __launch_bounds__(512, 1) void conv3_brick8_kernel(GemmArgs g) {
   const int by = bidx % by_n; bidx /= by_n;
   const int bz = bidx % bz_n;
   const int n = bidx / bz_n;
-  const int z0 = bz * 8, y0 = by * 8, x0 = bx * 8;
+  const int z0 = bz * BZ, y0 = by * 8, x0 = bx * 8;
   const int n0 = nt * BN;
   const int cin = 8 << g.cpg_shift;
   const int nchunk = gemm_nchunk(g);
@@ -2989,9 +2991,10 @@ __global__ __launch_bounds__(512, 1) void conv3_brick8_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const int r16 = lane & 15, kg = lane >> 4;
-  int aq[RM];   // halo quad of the lane's row for tap (0,0,0), group kg: z plane = wave
+  int aq[RM];   // halo quad of the lane's row for tap (0,0,0), group kg: z plane wave * ZP + i / 4
 #pragma unroll
-  for (int i = 0; i < RM; ++i) aq[i] = wave * RZ + (2 * i + (r16 >> 3)) * RY + (r16 & 7) * QV + kg;
+  for (int i = 0; i < RM; ++i)
+    aq[i] = (wave * ZP + (i >> 2)) * RZ + (2 * (i & 3) + (r16 >> 3)) * RY + (r16 & 7) * QV + kg;
   int bq[RN];
 #pragma unroll
   for (int j = 0; j < RN; ++j) {
@@ -3037,11 +3040,11 @@ __global__ __launch_bounds__(512, 1) void conv3_brick8_kernel(GemmArgs g) {
     }
   }
 
-  // epilogue: acc (+bias) -> LDS tile [512 voxels][BN + 8] -> 16-B stores
+  // epilogue: acc (+bias) -> LDS tile [512 ZP voxels][BN + 8] -> 16-B stores
   __syncthreads();
   T* El = reinterpret_cast<T*>(lds4);
   constexpr int EP = BN + 8;
-  static_assert(512 * EP * 2 <= (XQP + 2 * WQ) * 16, "epilogue tile must fit");
+  static_assert(512 * ZP * EP * 2 <= (XQP + 2 * WQ) * 16, "epilogue tile must fit");
 #pragma unroll
   for (int j = 0; j < RN; ++j) {
     const int col = j * 16 + r16;
@@ -3049,12 +3052,13 @@ __global__ __launch_bounds__(512, 1) void conv3_brick8_kernel(GemmArgs g) {
 #pragma unroll
     for (int i = 0; i < RM; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) El[(wave * 64 + 16 * i + 4 * kg + r) * EP + col] = from_f<T>(acc[i][j][r] + bv);
+      for (int r = 0; r < 4; ++r)
+        El[((wave * ZP + (i >> 2)) * 64 + 16 * (i & 3) + 4 * kg + r) * EP + col] = from_f<T>(acc[i][j][r] + bv);
   }
   __syncthreads();
   constexpr int CG = BN / 8;
 #pragma unroll
-  for (int k = 0; k < 512 * CG / 512; ++k) {
+  for (int k = 0; k < ZP * CG; ++k) {
     const int e = tid + k * 512;
     const int v = e / CG, cg = e % CG;
     const int z = z0 + (v >> 6), y = y0 + ((v >> 3) & 7), x = x0 + (v & 7);
@@ -4071,7 +4075,16 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
           nb8 * (g.Ncols / 64) >= knob("MMSEG_BRICK8_MINBLK", 256) &&
           (long long)g.M * g.lda * 2 < (1LL << 31) && (long long)((g.KG + 3) & ~3) * g.Cpad * 16 < (1LL << 31)) {
         mmseg::note_kernel("conv3_brick8_kernel<BN64>");
-        hipLaunchKernelGGL((conv3_brick8_kernel<64>), dim3(nb8 * (g.Ncols / 64)), dim3(512), 0, s, g);
+        hipLaunchKernelGGL((conv3_brick8_kernel<64, 1>), dim3(nb8 * (g.Ncols / 64)), dim3(512), 0, s, g);
+        return mmseg::check_launch("conv3_brick8");
+      }
+      if (knob("MMSEG_BRICK8", 0) && g.Ncols == 32 && g.D % 16 == 0 && g.H % 8 == 0 && g.W % 8 == 0 &&
+          g.stats == nullptr && g.nmean == nullptr && g.inpart == nullptr && g.ldo % 8 == 0 &&
+          (!g.out2 || g.ldo2 % 8 == 0) && (reinterpret_cast<uintptr_t>(g.out) & 15) == 0 &&
+          nb8 / 2 >= knob("MMSEG_BRICK8_MINBLK", 256) && (8 << g.cpg_shift) >= 64 &&
+          (long long)g.M * g.lda * 2 < (1LL << 31) && (long long)((g.KG + 3) & ~3) * g.Cpad * 16 < (1LL << 31)) {
+        mmseg::note_kernel("conv3_brick8_kernel<BN32>");
+        hipLaunchKernelGGL((conv3_brick8_kernel<32, 2>), dim3(nb8 / 2), dim3(512), 0, s, g);
         return mmseg::check_launch("conv3_brick8");
       }
     }

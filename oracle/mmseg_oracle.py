@@ -101,35 +101,72 @@ def init_dual_encoder(num_modalities: int, out_channels: int, features: Sequence
 
 
 # --------------------------------------------------------------------------
+# kink pins (parity tests only)
+# --------------------------------------------------------------------------
+class Pins:
+    """The piecewise-linear decisions of one forward, taken from the implementation under test: the ReLU mask
+    of every InstanceNorm + ReLU (in forward order) and the argmax code t = 4 dz + 2 dy + dx of every MaxPool3d(2)
+    window.  With them the oracle routes every gradient exactly as the implementation did, so an fp64 oracle
+    and an fp32 implementation differ by rounding alone -- not by which side of a kink a value within rounding
+    of it fell (at these decisions the true derivative jumps, so any two correct fp32 implementations disagree
+    there by O(1) on those voxels)."""
+
+    def __init__(self, relu_masks: List[Tensor], pool_codes: List[Tensor]):
+        self.relu_masks, self.pool_codes = list(relu_masks), list(pool_codes)
+        self.ri = self.pi = 0
+
+    def relu(self, x: Tensor) -> Tensor:
+        m = self.relu_masks[self.ri]
+        self.ri += 1
+        return x * m.to(x.dtype)
+
+    def pool(self, x: Tensor) -> Tensor:
+        code = self.pool_codes[self.pi]
+        self.pi += 1
+        N, C, D, H, W = x.shape
+        win = x.reshape(N, C, D // 2, 2, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 6, 3, 5, 7)
+        win = win.reshape(N, C, D // 2, H // 2, W // 2, 8)
+        return torch.gather(win, -1, code.long().unsqueeze(-1)).squeeze(-1)
+
+
+def _relu(x: Tensor, pins: Optional[Pins]) -> Tensor:
+    return torch.relu(x) if pins is None else pins.relu(x)
+
+
+def _pool(x: Tensor, pins: Optional[Pins]) -> Tensor:
+    return F.max_pool3d(x, 2) if pins is None else pins.pool(x)
+
+
+# --------------------------------------------------------------------------
 # forward restatements
 # --------------------------------------------------------------------------
-def conv_block(p: Params, prefix: str, x: Tensor) -> Tensor:
+def conv_block(p: Params, prefix: str, x: Tensor, pins: Optional[Pins] = None) -> Tensor:
     """ConvBlock3D.forward: (conv3^3 -> InstanceNorm3d -> ReLU) x 2 (reference unet.py:53-60)."""
     for c in ("conv1", "conv2"):
         x = F.conv3d(x, p[prefix + c + ".weight"], p[prefix + c + ".bias"], padding=1)
         x = F.instance_norm(x, eps=IN_EPS)
-        x = torch.relu(x)
+        x = _relu(x, pins)
     return x
 
 
-def up_block(p: Params, prefix: str, x: Tensor, skip: Tensor) -> Tensor:
+def up_block(p: Params, prefix: str, x: Tensor, skip: Tensor, pins: Optional[Pins] = None) -> Tensor:
     """UpBlock3D.forward: ConvTranspose3d(k2,s2) -> cat([up, skip]) -> ConvBlock (reference unet.py:104-113)."""
     x = F.conv_transpose3d(x, p[prefix + "up.weight"], p[prefix + "up.bias"], stride=2)
     if x.shape != skip.shape:  # dead for S divisible by 16 (reference unet.py:108-109)
         x = F.interpolate(x, size=skip.shape[2:], mode="trilinear", align_corners=True)
-    return conv_block(p, prefix + "conv.", torch.cat([x, skip], dim=1))
+    return conv_block(p, prefix + "conv.", torch.cat([x, skip], dim=1), pins)
 
 
-def unet3d_forward(p: Params, x: Tensor, n_levels: int = 5) -> Tensor:
+def unet3d_forward(p: Params, x: Tensor, n_levels: int = 5, pins: Optional[Pins] = None) -> Tensor:
     """UNet3D.forward (reference unet.py:165-200), dropout = identity."""
-    x = conv_block(p, "init_conv.", x)
+    x = conv_block(p, "init_conv.", x, pins)
     feats = [x]
     for i in range(n_levels - 1):
-        x = conv_block(p, f"encoders.{i}.conv.", F.max_pool3d(x, 2))
+        x = conv_block(p, f"encoders.{i}.conv.", _pool(x, pins), pins)
         feats.append(x)
     skips = feats[:-1]
     for j, skip in enumerate(reversed(skips)):
-        x = up_block(p, f"decoders.{j}.", x, skip)
+        x = up_block(p, f"decoders.{j}.", x, skip, pins)
     return F.conv3d(x, p["out_conv.weight"], p["out_conv.bias"])
 
 
@@ -157,21 +194,22 @@ def fuse_level(p: Params, fusion_type: str, level: int, feats: List[Tensor]) -> 
     return torch.stack(feats).mean(dim=0)
 
 
-def dual_encoder_forward(p: Params, x: Tensor, fusion_type: str, n_levels: int = 5) -> Tensor:
+def dual_encoder_forward(p: Params, x: Tensor, fusion_type: str, n_levels: int = 5,
+                         pins: Optional[Pins] = None) -> Tensor:
     """DualEncoder.forward (reference dual_encoder.py:112-165), dropout = identity."""
     M = x.shape[1]
     per_mod = []
     for m in range(M):
-        f = conv_block(p, f"encoders.{m}.init_conv.", x[:, m:m + 1])
+        f = conv_block(p, f"encoders.{m}.init_conv.", x[:, m:m + 1], pins)
         fl = [f]
         for i in range(n_levels - 1):
-            f = conv_block(p, f"encoders.{m}.blocks.{i}.conv.", F.max_pool3d(f, 2))
+            f = conv_block(p, f"encoders.{m}.blocks.{i}.conv.", _pool(f, pins), pins)
             fl.append(f)
         per_mod.append(fl)
     fused = [fuse_level(p, fusion_type, l, [pm[l] for pm in per_mod]) for l in range(n_levels)]
     y = fused[-1]
     for j, skip in enumerate(reversed(fused[:-1])):
-        y = up_block(p, f"decoder.{j}.", y, skip)
+        y = up_block(p, f"decoder.{j}.", y, skip, pins)
     return F.conv3d(y, p["out_conv.weight"], p["out_conv.bias"])
 
 

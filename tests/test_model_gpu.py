@@ -121,6 +121,85 @@ def test_tiny_trajectory_matches_reference_trainer(dev, tag):
     assert rel(after[torch.from_numpy(g["sample_idx"])], torch.from_numpy(g["after_sample"])) < 1e-1
 
 
+def _engine_pins(m, kind):
+    """The engine's kink decisions of the forward that just ran (call before the backward, which overwrites the
+    pre-norm buffers in place): each block's ReLU masks (pre-norm conv output > its InstanceNorm mean, i.e.
+    (x - mean) * rstd > 0, exactly the engine's test) and each MaxPool's argmax codes."""
+    from oracle import mmseg_oracle as O
+    prog = m.backbone.__dict__["_engine"].program
+
+    def masks(b):
+        res = []
+        for x, mean in ((b.x1, b.stats[0]), (b.x2, b.stats[2])):
+            mu = mean.view(x.N, x.C)[:, :, None, None, None]
+            res.append((x.to_ncdhw() > mu).cpu())
+        return res
+
+    def codes(idx, l, C):
+        D, H, W = prog.dims[l]
+        N = prog.shape[0]
+        return idx.view(N, D, H, W, C).permute(0, 4, 1, 2, 3).cpu()
+
+    F_ = prog.F
+    relu, pool = [], []
+    if kind == "unet":
+        for b in [prog.init] + prog.enc:
+            relu += masks(b)
+        pool = [codes(prog.idx[l], l, F_[l - 1]) for l in range(1, prog.L)]
+    else:
+        for blocks in prog.encs:
+            for b in blocks:
+                relu += masks(b)
+        pool = [codes(prog.idx[mm][l], l, F_[l - 1]) for mm in range(prog.M) for l in range(1, prog.L)]
+    for b in prog.dec.blocks:
+        relu += masks(b)
+    return O.Pins(relu, pool)
+
+
+@pytest.mark.parametrize("tag", ["unet_tiny", "dual_tiny_attention", "dual_tiny_concat", "dual_tiny_cross_attention",
+                                 "dual_tiny_add"])
+def test_teacher_forced_steps_pinned_to_oracle(dev, tag):
+    """At every step of a GPU training run (fp32) the oracle re-evaluates the step in fp64 from the engine's
+    current weights WITH THE ENGINE'S KINK DECISIONS (ReLU masks, MaxPool argmaxes; oracle.Pins): gradients
+    then differ by fp32 rounding alone, and every parameter gradient is held to 1e-4 normwise (max|a-b|/max|b|;
+    the conv biases in front of an InstanceNorm, whose true gradient is 0, only to the scale of the rest).
+    test_teacher_forced_steps_match_oracle below is the free-running form of the same check."""
+    from oracle import mmseg_oracle as O
+    cfg, m, g, M, C = _build(tag)
+    xs, ys = _inputs(g, M, C)
+    kind, _, _, fusion, lossname = TINY[tag]
+    L = len(g["features"])
+    fwd = ((lambda pp, x, pins: O.unet3d_forward(pp, x, L, pins=pins)) if kind == "unet" else
+           (lambda pp, x, pins: O.dual_encoder_forward(pp, x, fusion, L, pins=pins)))
+    lossf = O.dice_ce_loss if lossname == "dice_ce" else O.tversky_loss
+    tr = Trainer(cfg, m)
+    for i in range(3):
+        m.zero_grad(set_to_none=True)
+        m.train()
+        out = m(xs[i].to(dev))
+        pins = _engine_pins(m, kind)
+        loss = tr.criterion(out, ys[i].to(dev))
+        loss.backward()
+        params = {n: p.detach().cpu().double().requires_grad_(True) for n, p in m.backbone.named_parameters()}
+        ro = fwd(params, xs[i].double(), pins)
+        rl = lossf(ro, ys[i])
+        rl.backward()
+        assert pins.ri == len(pins.relu_masks) and pins.pi == len(pins.pool_codes)
+        assert rel(out, ro) < 1e-5
+        assert abs(loss.item() - rl.item()) < 1e-6
+        errs, dead = {}, {}
+        for n, p in m.backbone.named_parameters():
+            e = rel(p.grad, params[n].grad)
+            (dead if n.endswith(("conv1.bias", "conv2.bias")) else errs)[n] = e
+        worst = sorted(((v, n) for n, v in errs.items()), reverse=True)[:4]
+        print(f"step {i}: pinned grad errors median {np.median(list(errs.values())):.2e}, worst "
+              f"{[(float(f'{v:.2e}'), n) for v, n in worst]}")
+        assert max(errs.values()) < 1e-4, worst
+        gmax = max(float(p.grad.abs().max()) for n, p in m.backbone.named_parameters() if n in errs)
+        assert all(float(p.grad.abs().max()) < 1e-2 * gmax for n, p in m.backbone.named_parameters() if n in dead)
+        tr.optimizer.step()
+
+
 @pytest.mark.parametrize("tag", ["unet_tiny", "dual_tiny_attention", "dual_tiny_concat", "dual_tiny_cross_attention"])
 def test_teacher_forced_steps_match_oracle(dev, tag):
     """At every step of a GPU training run the oracle re-evaluates loss and gradients from the GPU's current

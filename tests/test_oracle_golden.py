@@ -130,3 +130,46 @@ def test_full_config_param_init_pinned():
              else O.init_dual_encoder(2, 6, [32, 64, 128, 256, 512], "cross_attention"))
         assert list(p) == list(g["param_names"])
         assert np.array_equal(np.array([v.double().sum().item() for v in p.values()]), g["param_sum"])
+
+
+class _RecordPins(O.Pins):
+    """Pins that record the oracle's own decisions (relu mask x > 0, MaxPool first argmax) while applying them."""
+
+    def __init__(self):
+        super().__init__([], [])
+
+    def relu(self, x):
+        self.relu_masks.append((x > 0).detach())
+        return super().relu(x)
+
+    def pool(self, x):
+        N, C, D, H, W = x.shape
+        win = x.detach().reshape(N, C, D // 2, 2, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 6, 3, 5, 7)
+        self.pool_codes.append(win.reshape(N, C, D // 2, H // 2, W // 2, 8).argmax(-1))
+        return super().pool(x)
+
+
+@pytest.mark.parametrize("kind", ["unet", "dual"])
+def test_oracle_pins_reproduce_free_forward(kind):
+    """Pinned with its own decisions, the oracle's forward and every gradient are bitwise the free oracle's:
+    the pins only fix WHICH side of each kink a value is on, the arithmetic is unchanged."""
+    feats = [8, 16, 32]
+    torch.manual_seed(0)
+    p = O.init_unet3d(2, 3, feats) if kind == "unet" else O.init_dual_encoder(2, 3, feats, "cross_attention")
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(2, 2, 16, 16, 16, generator=g, dtype=torch.float64)
+    y = torch.randint(0, 3, (2, 16, 16, 16), generator=g)
+    fwd = (lambda pp, xx, pins=None: O.unet3d_forward(pp, xx, 3, pins=pins)) if kind == "unet" else \
+        (lambda pp, xx, pins=None: O.dual_encoder_forward(pp, xx, "cross_attention", 3, pins=pins))
+    res = []
+    rec = _RecordPins()
+    for pins in (None, rec, "replay"):
+        if pins == "replay":
+            pins = O.Pins(rec.relu_masks, rec.pool_codes)
+        pp = {k: v.double().requires_grad_(True) for k, v in p.items()}
+        out = fwd(pp, x, pins)
+        O.dice_ce_loss(out, y).backward()
+        res.append((out.detach(), [pp[k].grad for k in p]))
+    for out, grads in res[1:]:
+        assert torch.equal(out, res[0][0])
+        assert all(torch.equal(a, b) for a, b in zip(grads, res[0][1]))
