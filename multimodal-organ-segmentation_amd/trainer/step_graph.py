@@ -26,7 +26,9 @@ MMSEG_STEP_GRAPH=0 turns it off.
 """
 from __future__ import annotations
 
+import gc
 import os
+import weakref
 from collections import OrderedDict
 from typing import Optional, Tuple
 
@@ -40,7 +42,10 @@ class StepGraphs:
     RING = 16            # pinned hyper-parameter slots
 
     def __init__(self, trainer):
-        self.tr = trainer
+        # a weak reference: no Trainer <-> StepGraphs cycle, so a dropped Trainer frees its graphs at once (by
+        # reference count) instead of whenever the cyclic collector runs -- which may be in the middle of another
+        # trainer's capture, where destroying a graph is an error (hipErrorStreamCaptureUnsupported)
+        self._tr = weakref.ref(trainer)
         self.graphs: "OrderedDict[tuple, dict]" = OrderedDict()
         self.copy_graph: Optional[dict] = None
         self.dev = trainer.device
@@ -49,6 +54,10 @@ class StepGraphs:
         self.ring = [torch.zeros(8, dtype=torch.float32).pin_memory() for _ in range(self.RING)]
         self.ring_ev = [None] * self.RING
         self.slot = 0
+
+    @property
+    def tr(self):
+        return self._tr()
 
     # ------------------------------------------------------------------ eligibility
     def usable(self, images: torch.Tensor, labels: torch.Tensor) -> bool:
@@ -105,12 +114,21 @@ class StepGraphs:
         L = lib()
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize(self.dev)
-        with torch.cuda.graph(g):
-            loss = eng.forward_loss(x, True, y, spec, cw)
-            eng.program.backward(None, False, gout=self.gout)
-            ws = eng.loss_ws
-            L.mmseg_adamw_dev(ptr(flat.flat), ptr(flat.grad_flat), ptr(m), ptr(v), flat.numel, ptr(self.hyper_dev),
-                              ptr(ws[-1:]), stream_handle())
+        # no cyclic garbage collection while capturing: a collected object owning a graph (or anything that frees
+        # device memory through the runtime) would be destroyed inside the capture
+        gc_on = gc.isenabled()
+        gc.collect()
+        gc.disable()
+        try:
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                loss = eng.forward_loss(x, True, y, spec, cw)
+                eng.program.backward(None, False, gout=self.gout)
+                ws = eng.loss_ws
+                L.mmseg_adamw_dev(ptr(flat.flat), ptr(flat.grad_flat), ptr(m), ptr(v), flat.numel,
+                                  ptr(self.hyper_dev), ptr(ws[-1:]), stream_handle())
+        finally:
+            if gc_on:
+                gc.enable()
         return {"graph": g, "loss": loss, "ws": ws, "x": x, "y": y, "cw": cw}
 
     def _entry(self, images: torch.Tensor, labels: torch.Tensor) -> dict:

@@ -211,43 +211,62 @@ def swin_transformer(p: Params, pre: str, x: Tensor, depths, heads, window, inde
     return outs
 
 
-def _lrelu(x: Tensor) -> Tensor:
-    return F.leaky_relu(x, LRELU_SLOPE)
+class LReluPins:
+    """The LeakyReLU decisions (pre-activation > 0, in forward order) of the implementation under test, so that
+    the oracle routes 1 or LRELU_SLOPE of every voxel's gradient exactly as it did (test infrastructure; the
+    same idea as mmseg_oracle.Pins)."""
+
+    def __init__(self, masks):
+        self.masks, self.i = list(masks), 0
+
+    def take(self) -> Tensor:
+        m = self.masks[self.i]
+        self.i += 1
+        return m
 
 
-def unet_res_block(p: Params, pre: str, x: Tensor) -> Tensor:
+def _lrelu(x: Tensor, pins: Optional[LReluPins] = None) -> Tensor:
+    if pins is None:
+        return F.leaky_relu(x, LRELU_SLOPE)
+    m = pins.take().to(torch.bool)
+    return x * torch.where(m, torch.ones((), dtype=x.dtype), torch.full((), LRELU_SLOPE, dtype=x.dtype))
+
+
+def unet_res_block(p: Params, pre: str, x: Tensor, pins: Optional[LReluPins] = None) -> Tensor:
     """UnetResBlock: conv1 -> IN -> LeakyReLU(0.01) -> conv2 -> IN, + residual (conv3 1x1 -> IN when the channel
     count changes), LeakyReLU.  Convs without bias, IN without affine."""
     out = F.conv3d(x, p[pre + "conv1.conv.weight"], padding=1)
-    out = _lrelu(F.instance_norm(out, eps=IN_EPS))
+    out = _lrelu(F.instance_norm(out, eps=IN_EPS), pins)
     out = F.conv3d(out, p[pre + "conv2.conv.weight"], padding=1)
     out = F.instance_norm(out, eps=IN_EPS)
     res = x
     if pre + "conv3.conv.weight" in p:
         res = F.instance_norm(F.conv3d(x, p[pre + "conv3.conv.weight"]), eps=IN_EPS)
-    return _lrelu(out + res)
+    return _lrelu(out + res, pins)
 
 
-def unetr_up_block(p: Params, pre: str, x: Tensor, skip: Tensor) -> Tensor:
+def unetr_up_block(p: Params, pre: str, x: Tensor, skip: Tensor, pins: Optional[LReluPins] = None) -> Tensor:
     """UnetrUpBlock: ConvTranspose3d(k2 s2, no bias) -> cat([up, skip]) -> UnetResBlock."""
     up = F.conv_transpose3d(x, p[pre + "transp_conv.conv.weight"], stride=2)
-    return unet_res_block(p, pre + "conv_block.", torch.cat([up, skip], 1))
+    return unet_res_block(p, pre + "conv_block.", torch.cat([up, skip], 1), pins)
 
 
 def swin_unetr_forward(p: Params, x: Tensor, depths=(2, 2, 2, 2), heads=(3, 6, 12, 24), window=(7, 7, 7),
-                       normalize: bool = True, prefix: str = "", drop: Optional[Callable] = None) -> Tensor:
+                       normalize: bool = True, prefix: str = "", drop: Optional[Callable] = None,
+                       pins: Optional[LReluPins] = None) -> Tensor:
     """MONAI SwinUNETR.forward: x [b, M, S^3] -> logits [b, C, S^3].  drop: the drop_rate sites in training
-    mode (make_drop), None = eval / drop_rate 0."""
+    mode (make_drop), None = eval / drop_rate 0.  pins: the LeakyReLU decisions of the ten residual blocks, in
+    this call order (encoder1/2/3/4/10, decoder5..1), two per block."""
     index = relative_position_index(window)
     hs = swin_transformer(p, prefix + "swinViT.", x, depths, heads, window, index, normalize, drop)
-    enc0 = unet_res_block(p, prefix + "encoder1.layer.", x)
-    enc1 = unet_res_block(p, prefix + "encoder2.layer.", hs[0])
-    enc2 = unet_res_block(p, prefix + "encoder3.layer.", hs[1])
-    enc3 = unet_res_block(p, prefix + "encoder4.layer.", hs[2])
-    dec4 = unet_res_block(p, prefix + "encoder10.layer.", hs[4])
-    dec3 = unetr_up_block(p, prefix + "decoder5.", dec4, hs[3])
-    dec2 = unetr_up_block(p, prefix + "decoder4.", dec3, enc3)
-    dec1 = unetr_up_block(p, prefix + "decoder3.", dec2, enc2)
-    dec0 = unetr_up_block(p, prefix + "decoder2.", dec1, enc1)
-    out = unetr_up_block(p, prefix + "decoder1.", dec0, enc0)
+    enc0 = unet_res_block(p, prefix + "encoder1.layer.", x, pins)
+    enc1 = unet_res_block(p, prefix + "encoder2.layer.", hs[0], pins)
+    enc2 = unet_res_block(p, prefix + "encoder3.layer.", hs[1], pins)
+    enc3 = unet_res_block(p, prefix + "encoder4.layer.", hs[2], pins)
+    dec4 = unet_res_block(p, prefix + "encoder10.layer.", hs[4], pins)
+    dec3 = unetr_up_block(p, prefix + "decoder5.", dec4, hs[3], pins)
+    dec2 = unetr_up_block(p, prefix + "decoder4.", dec3, enc3, pins)
+    dec1 = unetr_up_block(p, prefix + "decoder3.", dec2, enc2, pins)
+    dec0 = unetr_up_block(p, prefix + "decoder2.", dec1, enc1, pins)
+    out = unetr_up_block(p, prefix + "decoder1.", dec0, enc0, pins)
     return F.conv3d(out, p[prefix + "out.conv.conv.weight"], p[prefix + "out.conv.conv.bias"])

@@ -204,12 +204,25 @@ def _model(dev, dtype, fs=24, cin=2, cout=3, size=64, drop_rate=0.0):
     return m.to(dev)
 
 
-def _oracle(m, x, cot, dtype=torch.float64, drop=None):
+def _oracle(m, x, cot, dtype=torch.float64, drop=None, pins=None):
     p = {k: v.detach().cpu().to(dtype).requires_grad_(True) for k, v in m.model.named_parameters()}
     xr = x.to(dtype)
-    out = SO.swin_unetr_forward(p, xr, m.depths, m.num_heads, drop=drop)
+    out = SO.swin_unetr_forward(p, xr, m.depths, m.num_heads, drop=drop, pins=pins)
     (out * cot.to(dtype)).sum().backward()
     return out, {k: v.grad for k, v in p.items()}
+
+
+def _swin_pins(m):
+    """The engine's LeakyReLU decisions of the forward that just ran, in the oracle's call order (encoder1/2/3/4/
+    10, decoder5..1; per residual block the inner activation h1 and the block output): an activation is > 0
+    exactly where its pre-activation was (LeakyReLU keeps the sign)."""
+    prog = m.__dict__["_engine"].program
+    outs = [prog.dec[4].skip(), prog.dec[3].skip(), prog.dec[2].skip(), prog.dec[1].skip(), prog.dec4] + prog.dout
+    blocks = [prog.enc1, prog.enc2, prog.enc3, prog.enc4, prog.enc10] + [u.res for u in prog.dec]
+    masks = []
+    for b, y in zip(blocks, outs):
+        masks += [(b.h1.to_ncdhw() > 0).cpu(), (y.to_ncdhw() > 0).cpu()]
+    return SO.LReluPins(masks)
 
 
 @pytest.fixture(scope="module")
@@ -221,49 +234,56 @@ def swin_case():
 
 
 def test_swin_unetr_fp32_matches_oracle(dev, swin_case):
+    """fp32 engine vs the fp64 oracle given the engine's LeakyReLU decisions (_swin_pins): a pre-activation within
+    rounding of 0 otherwise routes 1 vs 0.01 of its voxel's gradient differently in the two (4 of 12.6 M voxels at
+    decoder1's output measured, tools/diag_swin2.py), which moved weight gradients upstream by up to 5e-2 of their
+    max; pinned, only rounding remains: every gradient within 1e-4 normwise (max|a-b|/max|b|), 1e-5 L2 overall."""
     x, cot = swin_case
     m = _model(dev, torch.float32)
     out = m(x.to(dev))
+    pins = _swin_pins(m)
     (out * cot.to(dev)).sum().backward()
-    ref, grads = _oracle(m, x, cot)
+    ref, grads = _oracle(m, x, cot, pins=pins)
+    assert pins.i == len(pins.masks)
     assert out.shape == (2, 3, 64, 64, 64)
     assert rel(out, ref) < 1e-4
-    bad = {}
+    errs = {}
     for name, prm in m.model.named_parameters():
         r = grads[name]
         if r.abs().max() == 0:
             assert prm.grad.abs().max().item() < 1e-6, name
             continue
-        e = rel(prm.grad, r)
-        if e > 5e-2:
-            bad[name] = e
-    assert not bad, bad
+        errs[name] = rel(prm.grad, r)
+    worst = sorted(((v, n) for n, v in errs.items()), reverse=True)[:4]
     got = torch.cat([p.grad.reshape(-1).double().cpu() for _, p in m.model.named_parameters()])
     want = torch.cat([grads[n].reshape(-1) for n, _ in m.model.named_parameters()])
-    assert ((got - want).norm() / want.norm()).item() < 1e-2
+    l2 = ((got - want).norm() / want.norm()).item()
+    print(f"\nswin fp32 pinned: worst {[(float(f'{v:.2e}'), n) for v, n in worst]}, L2 {l2:.2e}")
+    assert worst[0][0] < 1e-4, worst
+    assert l2 < 1e-5
 
 
 def test_swin_unetr_bf16_close_to_oracle(dev, swin_case):
+    """bf16 engine vs the fp64 oracle given the engine's LeakyReLU decisions.  Unpinned, bf16 activations put ~1 %
+    of the pre-activations on the other side of 0 than the oracle and each routes 1 vs 0.01 of its gradient: up
+    to 0.75 on one tensor, 0.10 L2 (tools/diag_swin3.py).  Pinned, what remains is bf16 storage rounding
+    (2^-9 per stored activation, a few dozen stores deep): every gradient within 5e-2 L2, 2e-2 overall."""
     x, cot = swin_case
     m = _model(dev, torch.bfloat16)
     out = m(x.to(dev))
+    pins = _swin_pins(m)
     (out * cot.to(dev)).sum().backward()
-    ref, grads = _oracle(m, x, cot, torch.float32)
+    ref, grads = _oracle(m, x, cot, torch.float64, pins=pins)
     assert rel2(out, ref) < 5e-2
-    # gradients: bf16 activations put ~1% of the LeakyReLU pre-activations on the other side of 0 than fp32
-    # does, and each such voxel routes 1 vs 0.01 of its gradient (the kink effect of the fp32 test, at bf16
-    # rounding size): the L2 error grows ~7% per residual block from the head (tools/diag_swin3.py:
-    # decoder1 7-9%, encoder10 26%, swinViT 25-38%); the head is exact to bf16 rounding
     errs = {n: rel2(p.grad, grads[n]) for n, p in m.model.named_parameters() if grads[n].norm() > 0}
-    assert errs["out.conv.conv.weight"] < 2e-2 and errs["out.conv.conv.bias"] < 2e-2
-    assert max(v for n, v in errs.items() if n.startswith("decoder1.")) < 0.12
-    # the worst single tensor (swinViT.layers1.0.blocks.0.norm1.bias) is kink noise: it measured 0.45 and 0.54
-    # under two InstanceNorm reduction chunkings (MMSEG_IN_MINCH 0 / 256) whose fp32 statistics differ only in
-    # summation order; the gradient as a whole stays at ~0.10 L2 (tools/diag_swin3.py)
-    assert max(errs.values()) < 0.75
     got = torch.cat([p.grad.reshape(-1).double().cpu() for n, p in m.model.named_parameters() if n in errs])
     want = torch.cat([grads[n].reshape(-1).double() for n, p in m.model.named_parameters() if n in errs])
-    assert ((got - want).norm() / want.norm()).item() < 0.2
+    l2 = ((got - want).norm() / want.norm()).item()
+    worst = sorted(((v, n) for n, v in errs.items()), reverse=True)[:4]
+    print(f"\nswin bf16 pinned: worst {[(float(f'{v:.2e}'), n) for v, n in worst]}, L2 {l2:.2e}")
+    assert errs["out.conv.conv.weight"] < 2e-2 and errs["out.conv.conv.bias"] < 2e-2
+    assert worst[0][0] < 5e-2, worst
+    assert l2 < 2e-2
 
 
 def test_swin_unetr_deterministic_and_features(dev, swin_case):
