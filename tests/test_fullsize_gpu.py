@@ -21,7 +21,7 @@ positions, all of them for smaller tensors), with e(x) = ||x - ref_fp64|| / ||re
     e(ref_bf16).
 A wiring error (a wrong buffer, a missing term) moves a gradient by O(1) and its norm by O(1); the gradient
 norms are held to 1e-3 (fp32) / 5e-2 (bf16) of the reference's.  Conv biases in front of an InstanceNorm
-have a mathematically zero gradient (rounding noise) and are only bounded in size.
+have a mathematically zero gradient (rounding noise): bounded by 10x the reference's own noise there.
 Loss: fp32 1e-5 relative to fp64; bf16 1e-3.  Sampled logits: 1e-3 normwise (north_star) / 3e-2 (bf16).
 """
 import numpy as np
@@ -102,19 +102,18 @@ def test_fullsize_training_step_matches_reference(dev, tag, dtype):
     bb = dict(m.backbone.named_parameters())
     off = g["gs_off"]
     ref_key = "gs_valbf" if bf else "gs_val"
-    e_eng, e_ref, norm_err, dead, typical = {}, {}, {}, {}, []
+    e_eng, e_ref, norm_err, dead = {}, {}, {}, {}
     for i, n in enumerate(names):
         sl = slice(off[i], off[i + 1])
         gi = torch.from_numpy(g["gs_idx"][sl]).to(dev)
         g64 = g["gs_val64"][sl]
         geng = bb[n].grad.reshape(-1)[gi].double().cpu().numpy()
         if n.endswith(("conv1.bias", "conv2.bias")):
-            dead[n] = float(np.linalg.norm(geng))
+            dead[n] = (float(np.linalg.norm(geng)), float(np.linalg.norm(g[ref_key][sl])))
             continue
         e_eng[n] = _l2(geng, g64)
         e_ref[n] = _l2(g[ref_key][sl], g64)
         norm_err[n] = abs(float(bb[n].grad.double().norm()) - float(g["grad_norm64"][i])) / float(g["grad_norm64"][i])
-        typical.append(float(g["grad_norm64"][i]) / np.sqrt(bb[n].numel()))
     med_eng, med_ref = float(np.median(list(e_eng.values()))), float(np.median(list(e_ref.values())))
     ratio = {n: e_eng[n] / e_ref[n] for n in e_eng}
     worst = sorted(((r, n) for n, r in ratio.items()), reverse=True)[:4]
@@ -132,9 +131,10 @@ def test_fullsize_training_step_matches_reference(dev, tag, dtype):
     ntol = 5e-2 if bf else 1e-3
     bad = {n: v for n, v in norm_err.items() if v > (10 * ntol if n.endswith("up.bias") else ntol)}
     assert not bad, bad
-    # mathematically-zero gradients stay at the rounding-noise scale of the live ones
-    scale = float(np.median(typical)) * np.sqrt(4096)
-    assert all(v < 1e-2 * scale for v in dead.values()), dead
+    # mathematically-zero gradients: rounding noise, no larger than the reference's own (fp32 / bf16-autocast) noise
+    # on the same biases (10x margin: it is noise, re-drawn by every summation order)
+    big = {n: v for n, v in dead.items() if v[0] > 10 * v[1] + 1e-12}
+    assert not big, big
     if not bf:
         hist = torch.bincount(logits.argmax(1).reshape(-1), minlength=C).cpu().numpy()
         assert np.abs(hist - g["argmax_hist"]).sum() <= 1e-4 * hist.sum()
