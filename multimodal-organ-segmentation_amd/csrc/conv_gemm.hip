@@ -40,6 +40,39 @@ int knob(const char* name, int dflt) {
 
 enum GatherMode { MODE_CONV3 = 0, MODE_POINT = 1, MODE_CONVT_FWD = 2, MODE_CONVT_DGRAD = 3 };
 
+// Block timeline probe (diagnostics, built only with -DMMSEG_TIMING_PROBES; tools/convbench.py --probe).
+// Per block b < PROBE_NB: [realtime start, realtime end, memtime start, memtime end, HW_ID, XCC_ID, -, -];
+// then for blocks < 32, every wave's lane 0 records up to 64 memtime stamps (PROBE_T) at phase boundaries.
+#ifdef MMSEG_TIMING_PROBES
+constexpr int PROBE_NB = 16384;
+__device__ long long* g_probe = nullptr;
+__device__ __forceinline__ void probe_block(bool end) {
+  long long* p = g_probe;
+  if (p && threadIdx.x == 0 && blockIdx.x < PROBE_NB) {
+    p += 8LL * blockIdx.x;
+    p[end ? 1 : 0] = (long long)__builtin_amdgcn_s_memrealtime();
+    p[end ? 3 : 2] = (long long)__builtin_amdgcn_s_memtime();
+    if (!end) {
+      p[4] = (long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+      p[5] = (long long)(unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20);   // HW_REG_XCC_ID
+    }
+  }
+}
+__device__ __forceinline__ void probe_stamp(int& k) {
+  long long* p = g_probe;
+  if (p && (threadIdx.x & 63) == 0 && blockIdx.x < 32 && k < 64)
+    p[8LL * PROBE_NB + ((blockIdx.x * 16 + (threadIdx.x >> 6)) * 64) + k] = (long long)__builtin_amdgcn_s_memtime();
+  ++k;
+}
+#define PROBE_BLOCK(e) probe_block(e)
+#define PROBE_T() probe_stamp(probe_k)
+#define PROBE_DECL() int probe_k = 0
+#else
+#define PROBE_BLOCK(e)
+#define PROBE_T()
+#define PROBE_DECL()
+#endif
+
 struct GemmArgs {
   const void* a;  int lda;   // A source (NDHWC)
   const void* b;             // packed weights [KGp][Cpad][8]
@@ -70,6 +103,10 @@ struct GemmArgs {
   const float* inmean;
   const float* inrstd;
   float* inpart;
+  // wave priority experiments (MMSEG_PRIO, A/B only): bit 0 = brick8 waves 4-7 at s_setprio 1 (the second-dispatched
+  // half of an 8-wave block loses every issue arbitration to its SIMD partner); bit 1 = s_setprio 1 around the tap
+  // loop's MFMAs (brick2 / brick8), so a co-resident wave in its staging phase yields issue to the MFMA stream
+  int prio;
 };
 
 // Output element (row voxel, column) of a GEMM (split-aware; split is a multiple of 8).
@@ -557,6 +594,8 @@ __device__ __forceinline__ void buf_load_v8(V8<T>& v, __amdgpu_buffer_rsrc_t r, 
 // spans < 2^31 bytes), instead of 64-bit address arithmetic and a bounds branch per item.
 template <typename T, int BN, int ZW, bool PF = false, bool B32 = false>
 __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kernel(GemmArgs g) {
+  PROBE_BLOCK(false);
+  PROBE_DECL();
   using L = Brick2Layout<T>;
   constexpr int BZ = 4 * ZW, HZ = BZ + 2;
   constexpr int RM = 4 * ZW, RN = BN / 16;
@@ -676,11 +715,13 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kern
     bq[j] = col * L::QV + (kg ^ w2_swz(col)) * L::QG;
   }
 
+  PROBE_T();
   load_x(0);
   load_w(0, 0);
   store_x();
   store_w();
   __syncthreads();
+  PROBE_T();
   for (int st = 0; st < nstage; ++st) {
     const int c = st / 3, kz = st - c * 3;
     const int sn = st + 1;
@@ -690,6 +731,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kern
       load_w(cn, kzn);
       if (kzn == 0) load_x(cn);
     }
+    if (g.prio & 2) __builtin_amdgcn_s_setprio(1);
     if constexpr (PF) {
       // fragments of tap t+1 are read while tap t's MFMAs run (one wave per SIMD cannot hide the LDS latency
       // behind another wave's MFMAs)
@@ -728,12 +770,15 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kern
           for (int j = 0; j < RN; ++j) mfma_step<T>(acc[i][j], af[i], bf[j]);
       }
     }
+    if (g.prio & 2) __builtin_amdgcn_s_setprio(0);
+    PROBE_T();
     __syncthreads();
     if (more) {
       store_w();
       if (kzn == 0) store_x();
       __syncthreads();
     }
+    PROBE_T();
   }
 
   // epilogue: acc (+bias) -> LDS tile [BZ*64 voxels][BN] -> 16-B vector stores
@@ -773,6 +818,8 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kern
       o.store(out_at<T>(g, nbase + z * HW + (long long)y * g.W + x, col));
     }
   }
+  PROBE_T();
+  PROBE_BLOCK(true);
 }
 
 
@@ -2901,6 +2948,8 @@ __device__ __forceinline__ void wd_dma16(uint32_t lds, uint32_t voff, wd_rsrc_t 
 // fused stats / deferred norm / IN partials, the A and B extents < 2^31 bytes.
 template <int BN, int ZP>
 __global__ __launch_bounds__(512, 1) void conv3_brick8_kernel(GemmArgs g) {
+  PROBE_BLOCK(false);
+  PROBE_DECL();
   typedef bf16_t T;
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   constexpr int QV = 4;                                  // 16-B quads per halo voxel (32 channels)
@@ -3002,10 +3051,13 @@ __global__ __launch_bounds__(512, 1) void conv3_brick8_kernel(GemmArgs g) {
     bq[j] = col * QV + (kg ^ w2_swz(col));
   }
 
+  PROBE_T();
   issue_x(0);
   issue_w(0, 0);
   __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): this wave's pieces have landed
   __syncthreads();
+  PROBE_T();
+  if ((g.prio & 1) && __builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);
   for (int s = 0; s < nstage; ++s) {
     const int kz = s % 3, b = s & 1;
     const bool more = s + 1 < nstage;
@@ -3020,6 +3072,7 @@ __global__ __launch_bounds__(512, 1) void conv3_brick8_kernel(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < RM; ++i) af[k][i].load(Xl + (aq[i] + hoff) * EPQ);
     };
+    if (g.prio & 2) __builtin_amdgcn_s_setprio(2);
     rd(0, 0);
 #pragma unroll
     for (int t9 = 0; t9 < 9; ++t9) {
@@ -3030,14 +3083,22 @@ __global__ __launch_bounds__(512, 1) void conv3_brick8_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < RN; ++j) mfma_step<T>(acc[i][j], af[t9 & 1][i], bf[t9 & 1][j]);
     }
+    if (g.prio & 2) {
+      if ((g.prio & 1) && __builtin_amdgcn_readfirstlane(wave) >= 4)
+        __builtin_amdgcn_s_setprio(1);
+      else
+        __builtin_amdgcn_s_setprio(0);
+    }
     if (more) {
       if ((s + 1) % 3 == 0) {           // next chunk: every wave is done with this halo, then refill it
         __syncthreads();
         issue_x((s + 1) / 3);
       }
+      PROBE_T();
       __builtin_amdgcn_s_waitcnt(0x0f70);
       __syncthreads();
     }
+    PROBE_T();
   }
 
   // epilogue: acc (+bias) -> LDS tile [512 ZP voxels][BN + 8] -> 16-B stores
@@ -3066,6 +3127,8 @@ __global__ __launch_bounds__(512, 1) void conv3_brick8_kernel(GemmArgs g) {
     o.load(El + v * EP + cg * 8);
     o.store(out_at<T>(g, nbase + z * HW + (long long)y * g.W + x, n0 + cg * 8));
   }
+  PROBE_T();
+  PROBE_BLOCK(true);
 }
 // PIPE: the fragment reads of the next (dy plane, tap) step are issued before the current step's MFMAs
 template <int MT, bool NORM = false, int NST = 3, bool PIPE = false>
@@ -3959,6 +4022,7 @@ int launch_splitk_reduce(const GemmArgs& g, hipStream_t s) {
 
 template <typename T, int MODE>
 int launch_gemm(GemmArgs g, hipStream_t s) {
+  g.prio = knob("MMSEG_PRIO", 0);
   if (g.nmean) {   // deferred InstanceNorm + ReLU of A: brick5 only (mmseg_conv3_norm_ok)
     MMSEG_REQUIRE(MODE == MODE_CONV3 && brick5_selected(g, (int)sizeof(T)),
                   "conv3 with a deferred norm needs the brick5 kernel for this shape (mmseg_conv3_norm_ok)");
@@ -4520,6 +4584,13 @@ int mmseg_pack_weight(const float* w, void* dst, int mode, int Co, int Ci, int C
 }
 
 int mmseg_pack3_desc_bytes(void) { return (int)sizeof(Pack3Desc); }
+
+#ifdef MMSEG_TIMING_PROBES
+// probe builds only (tools/convbench.py --probe): buffer of 8 * PROBE_NB + 32 * 16 * 64 longs, or null to stop
+int mmseg_probe_set(long long* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_probe), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 // descs: device array of n Pack3Desc sorted by block_begin; nblocks = total blocks
 // (sum over layers of Co/8 * ceil(Ci/32)).  The images must be zero-initialised once.

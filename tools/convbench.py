@@ -3,6 +3,9 @@
     python tools/convbench.py [--shape N,S,Cin,Cout | N,D,H,W,Cin,Cout ...] [--iters 20] [--only fwd,dgrad,wgrad]
 Env knobs (MMSEG_*) select kernel variants; prints one JSON line per (shape, op) with
 the kernel the library launched, us per launch and TFLOP/s (2*27*Cin*Cout per voxel).
+Ops: fwd, fwds (forward with the fused InstanceNorm partials, as ConvBlock3D runs it), dgrad, wgrad.
+--probe: load libmmseg_hip_probe.so (make -C csrc probe) and print the block timeline of one launch per op
+(per-CU residency, block lifetimes, per-phase cycles of block 0's waves; see conv_gemm.hip PROBE_*).
 """
 import argparse
 import json
@@ -23,7 +26,11 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="fwd,dgrad,wgrad")
     ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--probe", action="store_true")
     args = ap.parse_args()
+    if args.probe:
+        from mmseg_amd import _lib
+        _lib.set_library_path(os.path.join(ROOT, "multimodal-organ-segmentation_amd", "libmmseg_hip_probe.so"))
     import mmseg_amd  # noqa: F401
     from mmseg_amd.engine.layers import Conv3
     from mmseg_amd.engine.runtime import FlatParams, Runtime
@@ -52,9 +59,15 @@ def main():
         flops = 2.0 * N * D * H * W * 27 * Ci * Co
         L, s, code = rt.lib, rt.stream, rt.code
 
+        nb = layer.stats_bricks(x, y)
+        part = torch.empty(N * max(nb, 1) * Co * 2, dtype=torch.float32, device=dev)
+
         def run(op):
             if op == "fwd":
                 layer.fwd(x, y)
+            elif op == "fwds":
+                assert nb > 0, "no fused-statistics kernel for this shape (MMSEG_FUSED_STATS=1)"
+                layer.fwd(x, y, stats_part=part)
             elif op == "dgrad":
                 M = N * D * H * W
                 ks = L.mmseg_conv3_splits(M, Ci, layer.Cpad_d, layer.KGd, layer.dshift, D, H, W, y.ld, dx.ld, code)
@@ -84,6 +97,56 @@ def main():
             us = e0.elapsed_time(e1) * 1e3 / args.iters
             print(json.dumps({"shape": sh, "op": op, "kernel": kname, "us": round(us, 1),
                               "tflops": round(flops / (us * 1e-6) / 1e12, 1)}), flush=True)
+            if args.probe:
+                probe(L, lambda: run(op), dev)
+
+
+def probe(L, fn, dev):
+    """One launch with the block timeline probe on; prints residency and phase statistics."""
+    import ctypes
+    import numpy as np
+    nb_max = 16384
+    buf = torch.zeros(8 * nb_max + 32 * 16 * 64, dtype=torch.int64, device=dev)
+    setp = L.dll.mmseg_probe_set
+    setp.argtypes = [ctypes.c_void_p]
+    torch.cuda.synchronize()
+    assert setp(buf.data_ptr()) == 0
+    fn()
+    torch.cuda.synchronize()
+    assert setp(None) == 0
+    h = buf.cpu().numpy()
+    blk = h[:8 * nb_max].reshape(nb_max, 8)
+    nblk = int((blk[:, 0] != 0).sum())
+    if nblk == 0:
+        print("  probe: this kernel records no timeline", flush=True)
+        return
+    blk = blk[:nblk]
+    t0 = blk[:, 0].min()
+    st, en = (blk[:, 0] - t0) * 0.01, (blk[:, 1] - t0) * 0.01          # us (100 MHz realtime)
+    cyc = blk[:, 3] - blk[:, 2]
+    hw, xcc = blk[:, 4], blk[:, 5] & 0xF
+    cu = xcc * 4096 + ((hw >> 8) & 0xFF)                                   # XCC, SE / SH / CU
+    span = en.max()
+    ucu = np.unique(cu)
+    # per-CU concurrency sampled on a 0.1 us grid
+    grid = np.arange(0, span, 0.1)
+    conc = np.zeros((len(ucu), len(grid)))
+    for k, c in enumerate(ucu):
+        for s_, e_ in zip(st[cu == c], en[cu == c]):
+            conc[k, (grid >= s_) & (grid < e_)] += 1
+    per_cu = np.array([(cu == c).sum() for c in ucu])
+    print(f"  probe: {nblk} blocks on {len(ucu)} CUs (blocks/CU min {per_cu.min()} max {per_cu.max()}), span "
+          f"{span:.1f} us, last start {st.max():.1f} us; block lifetime mean {np.mean(en - st):.2f} us "
+          f"(p10 {np.percentile(en - st, 10):.2f} p90 {np.percentile(en - st, 90):.2f}), {np.mean(cyc):.0f} cycles "
+          f"-> clock {np.mean(cyc) / np.mean((en - st) * 1e3):.2f} GHz; mean resident blocks/CU {conc.mean():.2f} "
+          f"(max {conc.max():.0f}); CU-time with 0/1/2+ blocks {np.mean(conc == 0):.2f}/{np.mean(conc == 1):.2f}/"
+          f"{np.mean(conc >= 2):.2f}", flush=True)
+    ph = h[8 * nb_max:].reshape(32, 16, 64)
+    for w in (0, 1, 4, 7):
+        q = ph[0, w]
+        n = int((q != 0).sum())
+        if n > 1:
+            print(f"  block0 wave{w} phases (cycles): {list(np.diff(q[:n]))}", flush=True)
 
 
 if __name__ == "__main__":

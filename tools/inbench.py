@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--c", type=int, default=32)
     ap.add_argument("--n", type=int, default=2)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--cases", default="plain,pool_ld2,pool_ld1,plain_ld2")
+    ap.add_argument("--cases", default="stats,apply,plain,pool_ld2,pool_ld1,plain_ld2")
     args = ap.parse_args()
     import mmseg_amd  # noqa: F401
     from mmseg_amd._lib import lib, ptr
@@ -40,6 +40,15 @@ def main():
     rstd = torch.rand(N * C, device=dev) + 0.5
     ws = torch.empty(L.mmseg_instnorm_ws_floats(N, V, C), device=dev)
     for case in args.cases.split(","):
+        if case in ("stats", "apply"):
+            for _ in range(args.iters):
+                if case == "stats":
+                    L.mmseg_instnorm_stats(ptr(x), C, N, V, C, 1e-5, ptr(mean), C, ptr(rstd), ptr(ws), 1, s)
+                else:
+                    L.mmseg_instnorm_relu_fwd(ptr(x), C, ptr(dx), C, N, V, C, ptr(mean), ptr(rstd), 1, s)
+            torch.cuda.synchronize()
+            print("case", case, flush=True)
+            continue
         ld1 = 2 * C if "ld2" in case else C
         p1 = p1_wide if ld1 == 2 * C else p1_dense
         has_pool = case.startswith("pool")
