@@ -714,15 +714,23 @@ __global__ __launch_bounds__(SMALL_T) void in_small_fwd(const T* __restrict__ x,
     rs[j] = sfin[8 + j];
   }
   T* yn = y + (long long)n * V * ldy + cg * 8;
-  for (int v = tid; v < V; v += SMALL_T) {
-    V8<T> a, o;
-    a.load(xn + (long long)v * ldx);
+  // 4 (L2-resident) loads in flight per thread before the stores: one latency per 4 voxels
+  for (int v0 = tid; v0 < V; v0 += 4 * SMALL_T) {
+    V8<T> a[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float h = (a.get(j) - m[j]) * rs[j];
-      o.set(j, (!RELU || h > 0.f) ? h : 0.f);
+    for (int u = 0; u < 4; ++u)
+      if (v0 + u * SMALL_T < V) a[u].load(xn + (long long)(v0 + u * SMALL_T) * ldx);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (v0 + u * SMALL_T >= V) break;
+      V8<T> o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float h = (a[u].get(j) - m[j]) * rs[j];
+        o.set(j, (!RELU || h > 0.f) ? h : 0.f);
+      }
+      o.store(yn + (long long)(v0 + u * SMALL_T) * ldy);
     }
-    o.store(yn + (long long)v * ldy);
   }
 }
 
@@ -739,17 +747,203 @@ __global__ __launch_bounds__(SMALL_T) void in_small_bwd(const T* __restrict__ x,
   for (int j = 0; j < 8; ++j) ga[j] = gb[j] = 0.f;
   const DyCtx<T> dc(s, n, V, cg, C, D, H, W);
   const T* xn = x + (long long)n * V * ldx + cg * 8;
-  for (int v = tid; v < V; v += SMALL_T) {
-    V8<T> a;
-    typename DyCtx<T>::Raw r;
-    a.load(xn + (long long)v * ldx);
-    dc.load(v, r);
-    float dy[8];
-    dc.combine(r, dy);
+  // 4 voxels' loads in flight per thread, consumed in voxel order (the sums' order is unchanged)
+  for (int v0 = tid; v0 < V; v0 += 4 * SMALL_T) {
+    V8<T> a[4];
+    typename DyCtx<T>::Raw r[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (v0 + u * SMALL_T < V) {
+        a[u].load(xn + (long long)(v0 + u * SMALL_T) * ldx);
+        dc.load(v0 + u * SMALL_T, r[u]);
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (v0 + u * SMALL_T >= V) break;
+      float dy[8];
+      dc.combine(r[u], dy);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float h = (a[u].get(j) - mu[j]) * rs[j];
+        const float g = (!RELU || h > 0.f) ? dy[j] : 0.f;
+        ga[j] += g;
+        gb[j] = fmaf(g, h, gb[j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ga[j] = wave_sum(ga[j]);
+    gb[j] = wave_sum(gb[j]);
+  }
+  if (lane == 0) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float h = (a.get(j) - mu[j]) * rs[j];
-      const float g = (!RELU || h > 0.f) ? dy[j] : 0.f;
+      sa[wave][j] = ga[j];
+      sb[wave][j] = gb[j];
+    }
+  }
+  __syncthreads();
+  if (tid < 8) {
+    sfin[tid] = (((sa[0][tid] + sa[1][tid]) + sa[2][tid]) + sa[3][tid]) / (float)V;
+    sfin[8 + tid] = (((sb[0][tid] + sb[1][tid]) + sb[2][tid]) + sb[3][tid]) / (float)V;
+  }
+  __syncthreads();
+  float ca[8], cb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ca[j] = sfin[j];
+    cb[j] = sfin[8 + j];
+  }
+  T* dxn = dx + (long long)n * V * lddx + cg * 8;
+  for (int v0 = tid; v0 < V; v0 += 4 * SMALL_T) {
+    V8<T> a[4];
+    typename DyCtx<T>::Raw r[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (v0 + u * SMALL_T < V) {
+        a[u].load(xn + (long long)(v0 + u * SMALL_T) * ldx);
+        dc.load(v0 + u * SMALL_T, r[u]);
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (v0 + u * SMALL_T >= V) break;
+      float dy[8];
+      dc.combine(r[u], dy);
+      V8<T> o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float h = (a[u].get(j) - mu[j]) * rs[j];
+        const float g = (!RELU || h > 0.f) ? dy[j] : 0.f;
+        o.set(j, rs[j] * (g - ca[j] - h * cb[j]));
+      }
+      o.store(dxn + (long long)(v0 + u * SMALL_T) * lddx);
+    }
+  }
+}
+
+// Register-resident forms for V <= VPT * 256 (the 12^3 and 6^3 levels): every voxel of the thread is loaded
+// once, up front (one memory latency instead of one per pass and per 4 voxels), kept in registers through the
+// statistics and applied from there.  The per-thread accumulation order (voxels tid, tid + 256, ...) and the
+// merge trees are those of in_small_fwd / in_small_bwd, so the results are bitwise the same.
+template <typename T, bool RELU, int VPT>
+__global__ __launch_bounds__(SMALL_T) void in_small_fwd_r(const T* __restrict__ x, int ldx, T* __restrict__ y,
+                                                         int ldy, int V, int C, float eps, float* __restrict__ mean,
+                                                         int mean_ld, float* __restrict__ rstd) {
+  __shared__ float smu[4][8], sm2[4][8], scnt[4], sfin[16];
+  const int cg = blockIdx.x, n = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const T* xn = x + (long long)n * V * ldx + cg * 8;
+  V8<T> a[VPT];
+#pragma unroll
+  for (int u = 0; u < VPT; ++u)
+    if (tid + u * SMALL_T < V) a[u].load(xn + (long long)(tid + u * SMALL_T) * ldx);
+  float mu[8], m2[8], cnt = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) mu[j] = m2[j] = 0.f;
+#pragma unroll
+  for (int u = 0; u < VPT; ++u) {
+    if (tid + u * SMALL_T >= V) break;
+    cnt += 1.f;
+    const float inv = 1.f / cnt;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xv = a[u].get(j), d = xv - mu[j];
+      mu[j] = fmaf(d, inv, mu[j]);
+      m2[j] = fmaf(d, xv - mu[j], m2[j]);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float mb[8], m2b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mb[j] = __shfl_xor(mu[j], o, 64);
+      m2b[j] = __shfl_xor(m2[j], o, 64);
+    }
+    chan_merge(cnt, mu, m2, __shfl_xor(cnt, o, 64), mb, m2b);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      smu[wave][j] = mu[j];
+      sm2[wave][j] = m2[j];
+    }
+    scnt[wave] = cnt;
+  }
+  __syncthreads();
+  if (tid < 8) {
+    float c0 = scnt[0], m0 = smu[0][tid], q0 = sm2[0][tid];
+    for (int w = 1; w < 4; ++w) {
+      const float nb = scnt[w], nn = c0 + nb;
+      if (nb > 0.f) {
+        const float dl = smu[w][tid] - m0;
+        m0 = m0 + dl * (nb / nn);
+        q0 = q0 + sm2[w][tid] + dl * dl * (c0 * nb / nn);
+        c0 = nn;
+      }
+    }
+    const float rs = 1.f / sqrtf(q0 / (float)V + eps);
+    sfin[tid] = m0;
+    sfin[8 + tid] = rs;
+    mean[(long long)n * mean_ld + cg * 8 + tid] = m0;
+    rstd[n * C + cg * 8 + tid] = rs;
+  }
+  __syncthreads();
+  float m[8], rs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    m[j] = sfin[j];
+    rs[j] = sfin[8 + j];
+  }
+  T* yn = y + (long long)n * V * ldy + cg * 8;
+#pragma unroll
+  for (int u = 0; u < VPT; ++u) {
+    if (tid + u * SMALL_T >= V) break;
+    V8<T> o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float h = (a[u].get(j) - m[j]) * rs[j];
+      o.set(j, (!RELU || h > 0.f) ? h : 0.f);
+    }
+    o.store(yn + (long long)(tid + u * SMALL_T) * ldy);
+  }
+}
+
+template <typename T, bool RELU, int VPT>
+__global__ __launch_bounds__(SMALL_T) void in_small_bwd_r(const T* __restrict__ x, int ldx,
+                                                         const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                         DySrc s, T* __restrict__ dx, int lddx, int V, int C, int D,
+                                                         int H, int W) {
+  __shared__ float sa[4][8], sb[4][8], sfin[16];
+  const int cg = blockIdx.x, n = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const DyCtx<T> dc(s, n, V, cg, C, D, H, W);
+  const T* xn = x + (long long)n * V * ldx + cg * 8;
+  V8<T> a[VPT];
+  float dy[VPT][8];
+  {
+    typename DyCtx<T>::Raw r[VPT];
+#pragma unroll
+    for (int u = 0; u < VPT; ++u)
+      if (tid + u * SMALL_T < V) {
+        a[u].load(xn + (long long)(tid + u * SMALL_T) * ldx);
+        dc.load(tid + u * SMALL_T, r[u]);
+      }
+#pragma unroll
+    for (int u = 0; u < VPT; ++u)
+      if (tid + u * SMALL_T < V) dc.combine(r[u], dy[u]);
+  }
+  float mu[8], rs[8], ga[8], gb[8];
+  load8f(mean + n * C + cg * 8, mu);
+  load8f(rstd + n * C + cg * 8, rs);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ga[j] = gb[j] = 0.f;
+#pragma unroll
+  for (int u = 0; u < VPT; ++u) {
+    if (tid + u * SMALL_T >= V) break;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float h = (a[u].get(j) - mu[j]) * rs[j];
+      const float g = (!RELU || h > 0.f) ? dy[u][j] : 0.f;
       ga[j] += g;
       gb[j] = fmaf(g, h, gb[j]);
     }
@@ -779,21 +973,17 @@ __global__ __launch_bounds__(SMALL_T) void in_small_bwd(const T* __restrict__ x,
     cb[j] = sfin[8 + j];
   }
   T* dxn = dx + (long long)n * V * lddx + cg * 8;
-  for (int v = tid; v < V; v += SMALL_T) {
-    V8<T> a;
-    typename DyCtx<T>::Raw r;
-    a.load(xn + (long long)v * ldx);
-    dc.load(v, r);
-    float dy[8];
-    dc.combine(r, dy);
+#pragma unroll
+  for (int u = 0; u < VPT; ++u) {
+    if (tid + u * SMALL_T >= V) break;
     V8<T> o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float h = (a.get(j) - mu[j]) * rs[j];
-      const float g = (!RELU || h > 0.f) ? dy[j] : 0.f;
+      const float h = (a[u].get(j) - mu[j]) * rs[j];
+      const float g = (!RELU || h > 0.f) ? dy[u][j] : 0.f;
       o.set(j, rs[j] * (g - ca[j] - h * cb[j]));
     }
-    o.store(dxn + (long long)v * lddx);
+    o.store(dxn + (long long)(tid + u * SMALL_T) * lddx);
   }
 }
 
@@ -1147,6 +1337,11 @@ int knob_small_v() {   // read per call (A/B runs and tests flip it in-process)
   return e ? atoi(e) : 4096;
 }
 
+int knob_small_reg() {   // register-resident small-volume kernels (in_small_fwd_r / in_small_bwd_r)
+  const char* e = getenv("MMSEG_IN_SMALL_REG");
+  return e ? atoi(e) : 1;
+}
+
 int knob_small_t() {
   const char* e = getenv("MMSEG_IN_SMALL_T");
   return e ? atoi(e) : 256;
@@ -1252,6 +1447,12 @@ int mmseg_instnorm_fwd(const void* x, int ldx, void* y, int ldy, int N, long lon
     if (knob_small_t() == 1024)
       hipLaunchKernelGGL((in_small_fwd_1k<T, R>), grid, dim3(SMALL_T1K), 0, s, (const T*)x, ldx, (T*)y, ldy, (int)V, C,
                          eps, mean, mean_ld, rstd);
+    else if (knob_small_reg() && V <= SMALL_T)
+      hipLaunchKernelGGL((in_small_fwd_r<T, R, 1>), grid, dim3(SMALL_T), 0, s, (const T*)x, ldx, (T*)y, ldy, (int)V, C,
+                         eps, mean, mean_ld, rstd);
+    else if (knob_small_reg() && V <= 8 * SMALL_T)
+      hipLaunchKernelGGL((in_small_fwd_r<T, R, 8>), grid, dim3(SMALL_T), 0, s, (const T*)x, ldx, (T*)y, ldy, (int)V, C,
+                         eps, mean, mean_ld, rstd);
     else
       hipLaunchKernelGGL((in_small_fwd<T, R>), grid, dim3(SMALL_T), 0, s, (const T*)x, ldx, (T*)y, ldy, (int)V, C, eps,
                          mean, mean_ld, rstd);
@@ -1355,6 +1556,12 @@ int mmseg_instnorm_bwd_part(const void* x, int ldx, const float* mean, const flo
     if (small) {
       if (knob_small_t() == 1024)
         hipLaunchKernelGGL((in_small_bwd_1k<T, R>), dim3(C / 8, N), dim3(SMALL_T1K), 0, s, (const T*)x, ldx, mean, rstd,
+                           src, (T*)dx, lddx, (int)V, C, D, H, W);
+      else if (knob_small_reg() && V <= SMALL_T)
+        hipLaunchKernelGGL((in_small_bwd_r<T, R, 1>), dim3(C / 8, N), dim3(SMALL_T), 0, s, (const T*)x, ldx, mean, rstd,
+                           src, (T*)dx, lddx, (int)V, C, D, H, W);
+      else if (knob_small_reg() && V <= 8 * SMALL_T)
+        hipLaunchKernelGGL((in_small_bwd_r<T, R, 8>), dim3(C / 8, N), dim3(SMALL_T), 0, s, (const T*)x, ldx, mean, rstd,
                            src, (T*)dx, lddx, (int)V, C, D, H, W);
       else
         hipLaunchKernelGGL((in_small_bwd<T, R>), dim3(C / 8, N), dim3(SMALL_T), 0, s, (const T*)x, ldx, mean, rstd, src,

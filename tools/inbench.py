@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--c", type=int, default=32)
     ap.add_argument("--n", type=int, default=2)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--cases", default="stats,apply,plain,pool_ld2,pool_ld1,plain_ld2")
+    ap.add_argument("--cases", default="copy,fwd,stats,apply,plain,pool_ld2,pool_ld1,plain_ld2")
     args = ap.parse_args()
     import mmseg_amd  # noqa: F401
     from mmseg_amd._lib import lib, ptr
@@ -40,9 +40,17 @@ def main():
     rstd = torch.rand(N * C, device=dev) + 0.5
     ws = torch.empty(L.mmseg_instnorm_ws_floats(N, V, C), device=dev)
     for case in args.cases.split(","):
-        if case in ("stats", "apply"):
+        if case == "copy":   # torch's bf16 copy of the same tensor: the box's streaming reference
             for _ in range(args.iters):
-                if case == "stats":
+                dx.copy_(x)
+            torch.cuda.synchronize()
+            print("case", case, flush=True)
+            continue
+        if case in ("stats", "apply", "fwd"):
+            for _ in range(args.iters):
+                if case == "fwd":
+                    L.mmseg_instnorm_fwd(ptr(x), C, ptr(dx), C, N, V, C, 1e-5, ptr(mean), C, ptr(rstd), 1, ptr(ws), 1, s)
+                elif case == "stats":
                     L.mmseg_instnorm_stats(ptr(x), C, N, V, C, 1e-5, ptr(mean), C, ptr(rstd), ptr(ws), 1, s)
                 else:
                     L.mmseg_instnorm_relu_fwd(ptr(x), C, ptr(dx), C, N, V, C, ptr(mean), ptr(rstd), 1, s)
