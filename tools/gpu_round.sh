@@ -9,7 +9,7 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 if [ "${2:-tests}" = "tests" ]; then
-  timeout -k 10 1200 python3 -m pytest $R/tests -m gpu -q > $O/gpu_tests.log 2>&1
+  timeout -k 10 700 python3 -u -m pytest $R/tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.log 2>&1
   rc=$?
   tail -3 $O/gpu_tests.log
   # 1 = some test assertions failed (keep measuring); anything else (abort, segfault, timeout) ends the call
@@ -20,5 +20,6 @@ tail -1 $O/bench.log
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o prof -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/prof.log 2>&1 || { echo "prof failed"; tail -20 $O/prof.log; exit 1; }
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o pmc -- python3 $R/bench.py --steps 2 --warmup 1 --timer-steps 1 --no-cpu-baseline > $O/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; tail -20 $O/pmc_fetch.log; exit 1; }
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o pmc -- python3 $R/bench.py --steps 2 --warmup 1 --timer-steps 1 --no-cpu-baseline > $O/pmc_write.log 2>&1 || { echo "pmc write failed"; tail -20 $O/pmc_write.log; exit 1; }
-find $O -name "*.csv" | head -20
+python3 $R/tools/rocprof_families.py stats $O/trace/prof_kernel_stats.csv 16 > $O/families.txt
+python3 $R/tools/rocprof_families.py traffic $O/pmc_fetch/pmc_counter_collection.csv $O/pmc_write/pmc_counter_collection.csv $O/pmc_traffic.json 4 > /dev/null
 echo done
