@@ -4133,7 +4133,12 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     if constexpr (sizeof(T) == 2) {
       // 8-wave 8x8x8 brick with LDS-DMA staging (conv3_brick8_kernel)
       const int nb8 = nb1 / 2;   // 8-deep bricks
-      if (knob("MMSEG_BRICK8", 0) && g.Ncols % 64 == 0 && g.D % 8 == 0 && g.H % 8 == 0 && g.W % 8 == 0 &&
+      // (BN64: one 64-column tile over >= 2 input chunks, where it measured faster than brick2 BN64 -- 48^3
+      // 64->64 fwd / dgrad 61 -> 55.5 us, 128->64 fwd 111 -> 98 us; with one chunk, or two column tiles, it was
+      // slower: profiles/r03c_brick8_convbench.txt)
+      const int b8 = knob("MMSEG_BRICK8", 1);
+      if (b8 && g.Ncols % 64 == 0 && (b8 == 2 || (g.Ncols == 64 && gemm_nchunk(g) >= 2)) && g.D % 8 == 0 &&
+          g.H % 8 == 0 && g.W % 8 == 0 &&
           g.stats == nullptr && g.nmean == nullptr && g.inpart == nullptr && g.ldo % 8 == 0 &&
           (!g.out2 || g.ldo2 % 8 == 0) && (reinterpret_cast<uintptr_t>(g.out) & 15) == 0 &&
           nb8 * (g.Ncols / 64) >= knob("MMSEG_BRICK8_MINBLK", 256) &&
@@ -4142,7 +4147,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
         hipLaunchKernelGGL((conv3_brick8_kernel<64, 1>), dim3(nb8 * (g.Ncols / 64)), dim3(512), 0, s, g);
         return mmseg::check_launch("conv3_brick8");
       }
-      if (knob("MMSEG_BRICK8", 0) && g.Ncols == 32 && g.D % 16 == 0 && g.H % 8 == 0 && g.W % 8 == 0 &&
+      if (b8 && g.Ncols == 32 && g.D % 16 == 0 && g.H % 8 == 0 && g.W % 8 == 0 &&
           g.stats == nullptr && g.nmean == nullptr && g.inpart == nullptr && g.ldo % 8 == 0 &&
           (!g.out2 || g.ldo2 % 8 == 0) && (reinterpret_cast<uintptr_t>(g.out) & 15) == 0 &&
           nb8 / 2 >= knob("MMSEG_BRICK8_MINBLK", 256) && (8 << g.cpg_shift) >= 64 &&

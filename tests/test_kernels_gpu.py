@@ -81,11 +81,11 @@ def test_conv3_fwd_dgrad_wgrad(dev, dtype, cin, cout, shape):
     ({"MMSEG_BRICK": "1"}, 64, 64, (2, 8, 8, 8)),                   # v1 brick
     ({"MMSEG_BRICK": "0"}, 64, 64, (2, 8, 8, 8)),                   # per-lane gather GEMM
     # brick v8 (bf16; f32 ignores the knob): 8 waves over an 8x8x8 brick, LDS-DMA halo + double-buffered weights
-    ({"MMSEG_BRICK8": "1", "MMSEG_BRICK8_MINBLK": "0"}, 64, 64, (2, 8, 16, 8)),     # 2 chunks (halo refill)
-    ({"MMSEG_BRICK8": "1", "MMSEG_BRICK8_MINBLK": "0"}, 32, 64, (1, 16, 8, 24)),    # 1 chunk, border bricks
-    ({"MMSEG_BRICK8": "1", "MMSEG_BRICK8_MINBLK": "0"}, 128, 128, (1, 8, 8, 16)),   # 4 chunks, 2 column tiles
-    ({"MMSEG_BRICK8": "1", "MMSEG_BRICK8_MINBLK": "0"}, 64, 32, (1, 16, 8, 16)),    # BN32: 2 planes per wave
-    ({"MMSEG_BRICK8": "1", "MMSEG_BRICK8_MINBLK": "0"}, 128, 32, (2, 16, 16, 8)),   # BN32, 4 chunks, border
+    ({"MMSEG_BRICK8": "2", "MMSEG_BRICK8_MINBLK": "0"}, 64, 64, (2, 8, 16, 8)),     # 2 chunks (halo refill)
+    ({"MMSEG_BRICK8": "2", "MMSEG_BRICK8_MINBLK": "0"}, 32, 64, (1, 16, 8, 24)),    # 1 chunk, border bricks
+    ({"MMSEG_BRICK8": "2", "MMSEG_BRICK8_MINBLK": "0"}, 128, 128, (1, 8, 8, 16)),   # 4 chunks, 2 column tiles
+    ({"MMSEG_BRICK8": "2", "MMSEG_BRICK8_MINBLK": "0"}, 64, 32, (1, 16, 8, 16)),    # BN32: 2 planes per wave
+    ({"MMSEG_BRICK8": "2", "MMSEG_BRICK8_MINBLK": "0"}, 128, 32, (2, 16, 16, 8)),   # BN32, 4 chunks, border
 ])
 def test_conv3_kernel_variants(dev, dtype, knobs, cin, cout, shape, monkeypatch):
     for k, v in knobs.items():
