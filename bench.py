@@ -71,11 +71,15 @@ def _pmc_summary():
 
 
 def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the PMC summary."""
+    """HBM bytes per launch of `kernel` from the PMC summary (the trace names some families without the timer's
+    template suffix: conv3_brick5_kernel<BN32>[bf16] is conv3_brick5_kernel there)."""
     d, src = _pmc_summary()
-    if d is None or kernel not in d:
+    if d is None:
         return None, src
-    return d[kernel]["hbm_bytes_per_launch"], src
+    key = kernel if kernel in d else kernel.split("<")[0]
+    if key not in d:
+        return None, src
+    return d[key]["hbm_bytes_per_launch"], src
 
 
 def pmc_step_bytes():

@@ -21,8 +21,8 @@ bitwise equal to it (tests/test_step_graph_gpu.py).
 
 Used when the step has nothing per-step on the host side: one rank (the DP gradient buckets issue collectives
 from Python callbacks), accumulation_steps 1, the engine's fused head + loss, FlatAdamW (one group, no amsgrad),
-no Dropout3d in training, single-stream engine, kernel timer off.  hardware.step_graph: false or
-MMSEG_STEP_GRAPH=0 turns it off.
+no Dropout3d in training, single-stream engine, kernel timer off, optimizer.step / zero_grad not wrapped by the
+caller (a replay does not call them).  hardware.step_graph: false or MMSEG_STEP_GRAPH=0 turns it off.
 """
 from __future__ import annotations
 
@@ -74,6 +74,8 @@ class StepGraphs:
         opt = tr.optimizer
         if type(opt) is not FlatAdamW or len(opt.param_groups) != 1:
             return False
+        if "step" in opt.__dict__ or "zero_grad" in opt.__dict__:
+            return False   # a caller wrapped the optimizer's step: a replayed step would not call it
         grp = opt.param_groups[0]
         if grp.get("amsgrad") or grp.get("maximize"):
             return False

@@ -40,7 +40,9 @@ def _cfg(tmp):
                      "loss": {"name": "dice_ce", "dice_weight": 0.5, "ce_weight": 0.5, "class_weights": None},
                      "checkpoint": {"save_last": False, "save_best": False}},
         "distributed": {"bucket_mb": 0.25},      # many buckets: most reduce while the backward still runs
-        "hardware": {"device": "cuda", "mixed_precision": False, "engine_dtype": "float32"},
+        # eager steps: the test reads the gradient arena inside optimizer.step, which a replayed captured step
+        # (world size 1, trainer/step_graph.py) does not call
+        "hardware": {"device": "cuda", "mixed_precision": False, "engine_dtype": "float32", "step_graph": False},
     }
 
 
