@@ -37,7 +37,8 @@ STEP_WORK = {("unet", 2): (1206.2e9, 4.15e9), ("dual_encoder", 2): (1559.4e9, 6.
              ("dual_encoder", 3): (1915.6e9, 8.20e9)}
 
 
-def make_config(model, batch, dtype, out_channels=6, modalities=("CT", "PET"), size=96, loss="dice_ce"):
+def make_config(model, batch, dtype, out_channels=6, modalities=("CT", "PET"), size=96, loss="dice_ce",
+                kernels="hip", amp="bf16"):
     backbone = {"features": [32, 64, 128, 256, 512], "norm": "instance"}
     if model == "swin_unetr":     # config c4: SwinUNETR feature_size 48 (swin_unetr.py:180-200 defaults otherwise)
         backbone = {"img_size": [size] * 3, "feature_size": 48}
@@ -53,8 +54,10 @@ def make_config(model, batch, dtype, out_channels=6, modalities=("CT", "PET"), s
                      "loss": {"name": loss, "dice_weight": 0.5, "ce_weight": 0.5, "class_weights": None,
                               "tversky_alpha": 0.5, "tversky_beta": 0.5},
                      "checkpoint": {"save_last": False, "save_best": False}},
-        "hardware": {"device": "cuda", "mixed_precision": dtype == "bf16",
-                     "engine_dtype": "bfloat16" if dtype == "bf16" else "float32"},
+        "hardware": {"device": "cuda", "mixed_precision": dtype == "bf16", "kernels": kernels,
+                     # torch-op backend: bf16 autocast, or the reference's own fp16 autocast + GradScaler
+                     "engine_dtype": "bfloat16" if dtype == "bf16" and not (kernels == "torch" and amp == "fp16")
+                     else "float32"},
         "distributed": {"bucket_mb": 32},
     }
 
@@ -171,6 +174,10 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: this process's CPU share (cpu_threads())")
     ap.add_argument("--cpu-steps", type=int, default=3, help="timed oracle steps in the CPU baseline")
     ap.add_argument("--timer-steps", type=int, default=3, help="extra steps timed per kernel family (roofline)")
+    ap.add_argument("--kernels", default="hip", choices=["hip", "torch"],
+                    help="torch: the same model / step through PyTorch-ROCm ops (MIOpen convs; hardware.kernels A/B)")
+    ap.add_argument("--amp", default="bf16", choices=["bf16", "fp16"],
+                    help="--kernels torch autocast dtype (fp16 + GradScaler = the reference's GPU mode)")
     args = ap.parse_args()
 
     import mmseg_amd  # noqa: F401
@@ -188,7 +195,11 @@ def main():
     n_gpus = world
 
     mods = args.modalities.split(",")
-    cfg = make_config(args.model, args.batch, args.dtype, size=args.size, modalities=mods, loss=args.loss)
+    cfg = make_config(args.model, args.batch, args.dtype, size=args.size, modalities=mods, loss=args.loss,
+                      kernels=args.kernels, amp=args.amp)
+    if args.kernels == "torch":
+        args.no_cpu_baseline = True
+        args.timer_steps = 0
     torch.manual_seed(42)
     model = build_model(cfg)
     trainer = Trainer(cfg, model)
@@ -272,6 +283,8 @@ def main():
                 "counter_tbps": round(counter / (ms_per_step * 1e-3) / 1e12, 3) if counter is not None else None}
         if roofline is not None:
             roofline["step"] = step
+        else:
+            roofline = {"step": step}
     cpu = None
     if n_gpus == 1 and not args.no_cpu_baseline and args.model != "swin_unetr":
         cpu = cpu_baseline(args.model, args.batch, args.size, 6, mods, args.cpu_threads or cpu_threads(),
@@ -284,12 +297,13 @@ def main():
         "metric": f"{args.size}^3 {len(mods)}-modality patches/sec/node (train step)",
         "value": round(value, 3), "unit": "patches/s", "n_gpus": n_gpus, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": args.dtype,
+        "vs_baseline": None,
+        "dtype": args.dtype if args.kernels == "hip" else f"{args.amp if args.dtype == 'bf16' else 'fp32'}-autocast",
         "data": f"synthetic (seeded {'/'.join(mods)} phantoms, pre-staged in HBM)",
         "config": {"workload": f"{workload} {args.size}^3, modalities {'+'.join(mods)}, 6 classes, "
                                f"{'DiceCE' if args.loss == 'dice_ce' else 'Tversky'}, AdamW, per-GPU batch {args.batch}",
                    "model": args.model, "global_batch": args.batch * n_gpus, "patch": [args.size] * 3,
-                   "parallelism": f"dp{n_gpus}"},
+                   "parallelism": f"dp{n_gpus}", "kernels": args.kernels},
         "loss": round(loss_val, 5),
         "roofline": roofline,
         "cpu_baseline": cpu,

@@ -8,6 +8,9 @@ Fusion semantics follow the reference exactly (dual_encoder.py:167-199):
 parameters.  The real Q.K^T cross-attention (CrossAttentionFusion) is not
 reachable from build_model in the reference either; it lives in
 models/fusion/attention_fusion.py.
+
+`hardware.kernels: torch` runs the reference forward (dual_encoder.py:112-199,
+243-254) over the same containers in PyTorch-ROCm ops (A/B backend).
 """
 from __future__ import annotations
 
@@ -17,7 +20,7 @@ import torch
 import torch.nn as nn
 
 from ...engine import run_engine
-from .unet import ConvBlock3D, DownBlock3D, UpBlock3D
+from .unet import ConvBlock3D, DownBlock3D, UpBlock3D, check_torch_backend_input
 
 
 def fusion_kind(fusion_type: str) -> str:
@@ -38,8 +41,11 @@ class CrossModalAttention(nn.Module):
                                        nn.ReLU(inplace=True), nn.Linear(mc // reduction, num_modalities),
                                        nn.Softmax(dim=1))
 
-    def forward(self, x):  # pragma: no cover - executed inside the DualEncoder program
-        raise RuntimeError("CrossModalAttention is executed as part of the DualEncoder HIP program")
+    def forward(self, x):
+        """torch-op backend only (reference dual_encoder.py:243-254): x [B, M, C, H, W, D] -> [B, C, H, W, D]."""
+        B, M, C = x.shape[:3]
+        w = self.attention(x.reshape(B, M * C, *x.shape[3:]))
+        return (x * w.view(B, M, 1, 1, 1, 1)).sum(dim=1)
 
 
 class DualEncoder(nn.Module):
@@ -71,6 +77,7 @@ class DualEncoder(nn.Module):
         self.dropout = nn.Dropout3d(dropout) if dropout > 0 else nn.Identity()
         self.out_conv = nn.Conv3d(features[0], out_channels, kernel_size=1)
         self.engine_dtype = torch.float32
+        self.kernels = "hip"
 
     @staticmethod
     def _encoder(features: List[int], norm: str) -> nn.ModuleDict:
@@ -81,6 +88,9 @@ class DualEncoder(nn.Module):
 
     def forward(self, x: torch.Tensor, return_features: bool = False
                 ) -> Union[torch.Tensor, Tuple[torch.Tensor, Dict[str, List]]]:
+        if self.kernels == "torch":
+            check_torch_backend_input(x)
+            return self.torch_forward(x, return_features)
         logits = run_engine(self, "dual_encoder", x)
         if return_features:
             prog = self.__dict__["_engine"].program
@@ -89,6 +99,35 @@ class DualEncoder(nn.Module):
             fused = [prog.fused_out(l).to_ncdhw() for l in range(len(self.features))]
             return logits, {"encoder_features": enc, "fused_features": fused}
         return logits
+
+    def torch_forward(self, x: torch.Tensor, return_features: bool = False):
+        """The reference forward (dual_encoder.py:112-199) over these containers in PyTorch ops."""
+        allf = []
+        for i, enc in enumerate(self.encoders):
+            f = enc["init_conv"](x[:, i:i + 1])
+            mf = [f]
+            for blk in enc["blocks"]:
+                f, _ = blk(f)
+                mf.append(f)
+            allf.append(mf)
+        fused = []
+        for l in range(len(allf[0])):
+            lf = [f[l] for f in allf]
+            if self.fusion_type == "concat":
+                fused.append(self.fusion_proj[l](torch.cat(lf, dim=1)))
+            elif self.fusion_type == "add":
+                fused.append(sum(lf))
+            elif self.fusion_type == "attention":
+                fused.append(self.fusion_layers[l](torch.stack(lf, dim=1)))
+            else:
+                fused.append(torch.stack(lf).mean(dim=0))
+        h = fused[-1]
+        for dec, skip in zip(self.decoder, reversed(fused[:-1])):
+            h = dec(h, skip)
+        h = self.out_conv(self.dropout(h))
+        if return_features:
+            return h, {"encoder_features": allf, "fused_features": fused}
+        return h
 
     @property
     def encoder_channels(self) -> List[int]:

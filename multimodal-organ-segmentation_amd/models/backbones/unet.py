@@ -15,6 +15,7 @@ from typing import Any, Dict, List, Tuple, Union
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from ...engine import run_engine
 
@@ -39,8 +40,10 @@ class ConvBlock3D(nn.Module):
         self.norm2 = nn.InstanceNorm3d(out_channels)
         self.act = nn.ReLU(inplace=True)
 
-    def forward(self, x):  # pragma: no cover - container only
-        raise RuntimeError("ConvBlock3D is executed as part of the whole-network HIP program")
+    def forward(self, x):
+        """torch-op backend only (reference unet.py:53-60); the HIP backend runs the block inside its program."""
+        x = self.act(self.norm1(self.conv1(x)))
+        return self.act(self.norm2(self.conv2(x)))
 
 
 class DownBlock3D(nn.Module):
@@ -51,8 +54,10 @@ class DownBlock3D(nn.Module):
         self.pool = nn.MaxPool3d(2)
         self.conv = ConvBlock3D(in_channels, out_channels, norm=norm)
 
-    def forward(self, x):  # pragma: no cover
-        raise RuntimeError("DownBlock3D is executed as part of the whole-network HIP program")
+    def forward(self, x):
+        """torch-op backend only (reference unet.py:74-79): (conv(pool(x)), pool(x))."""
+        x_pool = self.pool(x)
+        return self.conv(x_pool), x_pool
 
 
 class UpBlock3D(nn.Module):
@@ -65,8 +70,12 @@ class UpBlock3D(nn.Module):
         self.up = nn.ConvTranspose3d(in_channels, in_channels // 2, kernel_size=2, stride=2)
         self.conv = ConvBlock3D(in_channels, out_channels, norm=norm)
 
-    def forward(self, x, skip):  # pragma: no cover
-        raise RuntimeError("UpBlock3D is executed as part of the whole-network HIP program")
+    def forward(self, x, skip):
+        """torch-op backend only (reference unet.py:104-113)."""
+        x = self.up(x)
+        if x.shape != skip.shape:
+            x = F.interpolate(x, size=skip.shape[2:], mode="trilinear", align_corners=True)
+        return self.conv(torch.cat([x, skip], dim=1))
 
 
 class UNet3D(nn.Module):
@@ -89,9 +98,13 @@ class UNet3D(nn.Module):
         self.dropout = nn.Dropout3d(dropout) if dropout > 0 else nn.Identity()
         self.out_conv = nn.Conv3d(features[0], out_channels, kernel_size=1)
         self.engine_dtype = torch.float32
+        self.kernels = "hip"
 
     def forward(self, x: torch.Tensor, return_features: bool = False
                 ) -> Union[torch.Tensor, Tuple[torch.Tensor, List[torch.Tensor]]]:
+        if self.kernels == "torch":
+            check_torch_backend_input(x)
+            return self.torch_forward(x, return_features)
         logits = run_engine(self, "unet", x)
         if return_features:
             prog = self.__dict__["_engine"].program
@@ -99,9 +112,28 @@ class UNet3D(nn.Module):
             return logits, feats
         return logits
 
+    def torch_forward(self, x: torch.Tensor, return_features: bool = False):
+        """The reference forward (unet.py:165-200) over these containers in PyTorch ops."""
+        x = self.init_conv(x)
+        feats = [x]
+        for enc in self.encoders:
+            x, _ = enc(x)
+            feats.append(x)
+        feats = feats[:-1]
+        for dec, skip in zip(self.decoders, reversed(feats)):
+            x = dec(x, skip)
+        x = self.out_conv(self.dropout(x))
+        return (x, feats) if return_features else x
+
     @property
     def encoder_channels(self) -> List[int]:
         return self.features
+
+
+def check_torch_backend_input(x: torch.Tensor) -> None:
+    """The torch-op backend is an A/B backend on the GPU, like the HIP one: no CPU path."""
+    if x.device.type != "cuda":
+        raise RuntimeError("hardware.kernels: torch runs on a ROCm device; there is no CPU path")
 
 
 def build_unet3d(config: Dict[str, Any]) -> UNet3D:

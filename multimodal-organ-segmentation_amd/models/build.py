@@ -6,6 +6,12 @@ Differences, all additive:
     activation storage; if absent, `hardware.mixed_precision: true` (the
     reference's fp16-autocast switch) maps to bfloat16 and false to float32.
     Parameters, gradients and optimizer state stay fp32 either way.
+  * `hardware.kernels` ("hip" | "torch", default "hip") selects the backend
+    (SURVEY §8b): "hip" runs the whole network as one HIP program; "torch"
+    runs the same parameter containers through plain PyTorch-ROCm ops (MIOpen
+    convolutions), the reference's own module forward, for A/B runs on the
+    GPU.  It is chosen explicitly, never as a fallback, and needs a ROCm device
+    like the HIP backend.
 """
 from __future__ import annotations
 
@@ -37,6 +43,16 @@ def engine_dtype_from_config(config: Dict[str, Any]) -> torch.dtype:
     return table[name]
 
 
+KERNELS = ("hip", "torch")
+
+
+def kernels_from_config(config: Dict[str, Any]) -> str:
+    name = str(config.get("hardware", {}).get("kernels", "hip")).lower()
+    if name not in KERNELS:
+        raise ValueError(f"hardware.kernels must be one of {list(KERNELS)}, got {name!r}")
+    return name
+
+
 class MultiModalSegmentationModel(nn.Module):
     """Pass-through wrapper (reference build.py:24-74): forward(x, return_features)."""
 
@@ -63,8 +79,12 @@ def build_model(config: Dict[str, Any]) -> nn.Module:
     n_mod = len(config["data"]["modalities"])
     if name in ("swin_unetr", "unet", "unet3d"):
         config["model"]["in_channels"] = n_mod          # reference build.py:97-99
+    kernels = kernels_from_config(config)
+    if kernels == "torch" and name == "swin_unetr":
+        raise ValueError("hardware.kernels: torch covers unet / dual_encoder, not swin_unetr (MONAI is absent)")
     backbone = MODEL_REGISTRY[name](config)
     backbone.engine_dtype = engine_dtype_from_config(config)
+    backbone.kernels = kernels
     model = MultiModalSegmentationModel(backbone, config)
     if config.get("hardware", {}).get("device", "cuda") == "cuda" and torch.cuda.is_available():
         model = model.cuda()

@@ -13,6 +13,7 @@ from typing import Any, Dict, Optional
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from .._lib import lib, ptr, stream_handle
 
@@ -74,7 +75,16 @@ class _HipLoss(nn.Module):
             raise RuntimeError(f"{n} target voxels hold a class index outside [0, num_classes) "
                                "(the reference raises in F.one_hot / cross_entropy on such labels)")
 
+    kernels = "hip"
+
+    def torch_forward(self, pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError
+
     def forward(self, pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+        if self.kernels == "torch":
+            if pred.device.type != "cuda":
+                raise RuntimeError("hardware.kernels: torch runs on a ROCm device; there is no CPU path")
+            return self.torch_forward(pred, target)
         if getattr(self, "reduction", "mean") != "mean":
             raise NotImplementedError("HIP losses implement reduction='mean' (the reference's default)")
         return _SegLoss.apply(pred, target, self._spec(), getattr(self, "class_weights", None), self)
@@ -94,6 +104,17 @@ class DiceLoss(_HipLoss):
         return dict(type=TYPE_DICE, dice_w=1.0, ce_w=0.0, smooth=self.smooth, alpha=0.0, beta=0.0,
                     include_bg=self.include_background)
 
+    def torch_forward(self, pred, target):
+        """reference losses.py:47-80."""
+        C = pred.shape[1]
+        p = F.softmax(pred, dim=1)
+        t = F.one_hot(target.long(), C).permute(0, 4, 1, 2, 3).float()
+        if not self.include_background:
+            p, t = p[:, 1:], t[:, 1:]
+        p, t = p.flatten(2), t.flatten(2)
+        dice = (2.0 * (p * t).sum(-1) + self.smooth) / (p.sum(-1) + t.sum(-1) + self.smooth)
+        return _reduce(1.0 - dice, self.reduction)
+
 
 class CrossEntropyLoss(_HipLoss):
     """nn.CrossEntropyLoss(weight) with mean reduction over B*H*W*D (reference losses.py:214)."""
@@ -104,6 +125,10 @@ class CrossEntropyLoss(_HipLoss):
 
     def _spec(self):
         return dict(type=TYPE_DICE, dice_w=0.0, ce_w=1.0, smooth=1.0, alpha=0.0, beta=0.0, include_bg=True)
+
+    def torch_forward(self, pred, target):
+        w = None if self.class_weights is None else self.class_weights.to(pred.device)
+        return F.cross_entropy(pred, target.long(), weight=w)
 
 
 class TverskyLoss(_HipLoss):
@@ -116,6 +141,17 @@ class TverskyLoss(_HipLoss):
     def _spec(self):
         return dict(type=TYPE_TVERSKY, dice_w=1.0, ce_w=0.0, smooth=self.smooth, alpha=self.alpha, beta=self.beta,
                     include_bg=True)
+
+    def torch_forward(self, pred, target):
+        """reference losses.py:160-185."""
+        C = pred.shape[1]
+        p = F.softmax(pred, dim=1).flatten(2)
+        t = F.one_hot(target.long(), C).permute(0, 4, 1, 2, 3).float().flatten(2)
+        tp = (p * t).sum(-1)
+        fp = (p * (1 - t)).sum(-1)
+        fn = ((1 - p) * t).sum(-1)
+        tv = (tp + self.smooth) / (tp + self.alpha * fp + self.beta * fn + self.smooth)
+        return _reduce(1.0 - tv, self.reduction)
 
 
 class FocalLoss(_HipLoss):
@@ -130,6 +166,12 @@ class FocalLoss(_HipLoss):
     def _spec(self):
         return dict(type=TYPE_FOCAL, dice_w=0.0, ce_w=1.0, smooth=1.0, alpha=float(self.gamma), beta=0.0,
                     include_bg=True)
+
+    def torch_forward(self, pred, target):
+        """reference losses.py:109-125."""
+        w = None if self.alpha is None else self.alpha.to(pred.device)
+        ce = F.cross_entropy(pred, target.long(), weight=w, reduction="none")
+        return _reduce((1 - torch.exp(-ce)) ** self.gamma * ce, self.reduction)
 
 
 class DiceCELoss(_HipLoss):
@@ -146,9 +188,30 @@ class DiceCELoss(_HipLoss):
         return dict(type=TYPE_DICE, dice_w=self.dice_weight, ce_w=self.ce_weight, smooth=1.0, alpha=0.0, beta=0.0,
                     include_bg=self.include_background)
 
+    def torch_forward(self, pred, target):
+        """reference losses.py:216-228."""
+        dice = DiceLoss(include_background=self.include_background).torch_forward(pred, target)
+        w = None if self.class_weights is None else self.class_weights.to(pred.device)
+        return self.dice_weight * dice + self.ce_weight * F.cross_entropy(pred, target.long(), weight=w)
+
+
+def _reduce(x: torch.Tensor, reduction: str) -> torch.Tensor:
+    if reduction == "mean":
+        return x.mean()
+    if reduction == "sum":
+        return x.sum()
+    return x
+
 
 def get_loss(config: Dict[str, Any]) -> nn.Module:
-    """reference losses.py:231-267."""
+    """reference losses.py:231-267 (+ the hardware.kernels backend, models/build.py)."""
+    from ..models.build import kernels_from_config
+    loss = _get_loss(config)
+    loss.kernels = kernels_from_config(config)
+    return loss
+
+
+def _get_loss(config: Dict[str, Any]) -> nn.Module:
     lc = config["training"]["loss"]
     name = lc["name"].lower()
     cw = lc.get("class_weights")

@@ -14,6 +14,12 @@ MI355X-specific behaviour:
     accumulation boundary micro-step communicates; rank 0 logs/checkpoints;
   * validation accumulates Dice counts on the device (fused argmax + counts),
     one host sync per validation pass instead of one per batch.
+
+`hardware.kernels: torch` (models/build.py) is the A/B backend: the model's
+and the losses' own PyTorch-ROCm forwards, torch.optim.AdamW, and the
+reference's step body verbatim in behaviour (trainer.py:236-258: autocast fp16
++ GradScaler when mixed_precision, or bf16 autocast without a scaler when
+hardware.engine_dtype is bfloat16).  Never a fallback: selected explicitly.
 """
 from __future__ import annotations
 
@@ -25,7 +31,7 @@ import torch
 import torch.nn as nn
 
 from ..distributed import ddp
-from ..models.build import load_checkpoint, save_checkpoint
+from ..models.build import kernels_from_config, load_checkpoint, save_checkpoint
 from .losses import get_loss
 from .metrics import DiceMetric, get_metrics
 from .optim import FlatAdamW
@@ -48,12 +54,19 @@ class Trainer:
         self.epochs = config["training"]["epochs"]
         self.device = self._get_device()
         self.model = self.model.to(self.device)
+        self.kernels = kernels_from_config(config)
         self.optimizer = self._setup_optimizer()
         self.scheduler = self._setup_scheduler()
         self.criterion = get_loss(config)
         self.metrics = get_metrics(config)
         self.use_amp = config["hardware"].get("mixed_precision", False)
         self.scaler = None  # bf16 engine: no loss scaling needed (see module docstring)
+        self._amp_dtype = None
+        if self.kernels == "torch" and self.use_amp:
+            bf16 = str(config["hardware"].get("engine_dtype", "")).lower() in ("bfloat16", "bf16")
+            self._amp_dtype = torch.bfloat16 if bf16 else torch.float16
+            if not bf16:
+                self.scaler = torch.amp.GradScaler("cuda")
         self.accumulation_steps = config["training"].get("accumulation_steps", 1)
         self.rank, self.world = ddp.rank(), ddp.world()
         self.output_dir = Path(config["experiment"]["output_dir"]) / config["experiment"]["name"]
@@ -85,6 +98,13 @@ class Trainer:
         name = oc["name"].lower()
         lr, wd = oc["lr"], oc.get("weight_decay", 0)
         params = list(self.model.parameters())
+        if self.kernels == "torch":      # reference trainer.py:104-122
+            if name == "adam":
+                return torch.optim.Adam(params, lr=lr, weight_decay=wd)
+            if name == "sgd":
+                return torch.optim.SGD(params, lr=lr, momentum=oc.get("momentum", 0.9), weight_decay=wd)
+            betas = tuple(oc.get("betas", [0.9, 0.999])) if name == "adamw" else (0.9, 0.999)
+            return torch.optim.AdamW(params, lr=lr, weight_decay=wd, betas=betas)
         if name == "adamw":
             return FlatAdamW(params, lr=lr, weight_decay=wd, betas=tuple(oc.get("betas", [0.9, 0.999])))
         if name == "adam":
@@ -178,6 +198,8 @@ class Trainer:
         images = batch["image"].to(self.device, non_blocking=True)
         labels = batch["label"].to(self.device, non_blocking=True)
         boundary = (batch_idx + 1) % self.accumulation_steps == 0
+        if self.kernels == "torch":
+            return self._torch_step(images, labels, boundary, sync)
         if self._graph_ok and self._graphs.usable(images, labels):
             # the whole step (forward, fused loss, backward, AdamW) as one captured graph (trainer/step_graph.py)
             if labels.dtype not in (torch.int64, torch.uint8):
@@ -217,6 +239,32 @@ class Trainer:
         if not sync:
             return out
         return self._after_step(out.item(), guard, boundary, guarded)
+
+    def _torch_step(self, images, labels, boundary: bool, sync: bool):
+        """The reference's per-batch body (trainer.py:236-258) on the torch-op backend."""
+        if self._amp_dtype is not None:
+            with torch.autocast("cuda", dtype=self._amp_dtype):
+                loss = self.criterion(self.model(images), labels) / self.accumulation_steps
+        else:
+            loss = self.criterion(self.model(images), labels) / self.accumulation_steps
+        if self.scaler is not None:
+            self.scaler.scale(loss).backward()
+        else:
+            loss.backward()
+        if boundary:
+            if self.world > 1:           # plain per-tensor averaging (the reference is single-process)
+                for p in self.model.parameters():
+                    if p.grad is not None:
+                        ddp.allreduce_sum_(p.grad)
+                        p.grad.div_(self.world)
+            if self.scaler is not None:
+                self.scaler.step(self.optimizer)
+                self.scaler.update()
+            else:
+                self.optimizer.step()
+            self.optimizer.zero_grad()
+        out = loss.detach() * self.accumulation_steps
+        return out.item() if sync else out
 
     def _after_step(self, lv: float, guard, boundary: bool, guarded: bool) -> float:
         """Host side of a synchronous step: raise (on every rank) when the step's labels were out of range."""
