@@ -1662,6 +1662,266 @@ __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int up
   if constexpr (INP) in_flush();
 }
 
+// ------------------------------------------------- brick conv v6 (brick5 with its other work between the MFMAs)
+// Stamps and the .s of brick5 (r03s, 96^3 B=2 32->32 forward, one wave per SIMD): ~8,000 cycles per brick against
+// 3,456 of MFMA issue.  hipcc emitted each group's halo staging (the deferred norm's VALU work and its ds_writes),
+// the next group's fragment reads and the previous brick's epilogue as blocks BETWEEN the groups' MFMA runs, and
+// an MFMA run at one wave per SIMD leaves only 8 of every 16 cycles to other instructions -- when those come as a
+// block, the matrix pipe idles for the whole block.  v6 is brick5's register-staged path (same layout, same
+// arithmetic, bitwise the same outputs) with every group cut into 8 chunks of 3 MFMAs separated by
+// sched_barrier(0), each chunk carrying a fixed share of the rest: one of the next group's 6 fragment reads, a row
+// of the next brick's halo loads (groups 0-1), one 2-channel pair of a staged row's deferred norm (groups SG0..8,
+// row written to LDS with its fourth pair) or one row of the previous brick's epilogue (group 0).  The steady state
+// has no branches: NORM is a template parameter, out-of-volume rows are zeroed by a mask instead of a branch, the
+// 40 threads without a halo column write a dummy LDS slot, the last brick re-stages itself, and the first brick's
+// group-0 epilogue writes bias-only values that the next brick's epilogue (same lanes, same addresses) overwrites.
+// DBG (timing probes only, wrong results): 1 = MFMAs + fragment reads only after the prologue, 2 = MFMAs only.
+template <bool NORM, int SG0 = 3, int DBG = 0>
+__global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int upb, int blocks_per_nt) {
+  using T = bf16_t;
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  constexpr int BZ = 4, BY = 4, BX = 16;
+  constexpr int HZ = BZ + 2, HY = BY + 2, HX = BX + 2;
+  constexpr int RY = HX * 4, RZ = HY * RY;             // quads per halo row / plane
+  constexpr int XQ = HZ * RZ;                          // 2592 quads = 41.5 KB
+  constexpr int RN = 2;
+  constexpr int XROWS = HZ * HY;                       // 36 (z, y) halo rows
+  constexpr int XK = XROWS / 3;                        // rows per thread (3 rows per pass of 216 threads)
+  constexpr int NSG = 9 - SG0;                         // groups that write staged rows
+  constexpr int RPG = (XK + NSG - 1) / NSG;            // rows per such group
+  constexpr int PPC = RPG / 2;                         // norm pairs per chunk (4 pairs per row, 8 chunks)
+  static_assert(RPG % 2 == 0 && NSG * RPG >= XK && SG0 >= 2, "SG0: 3, 6 or 7");
+  constexpr int EPQ = 8;
+  __shared__ __attribute__((aligned(16))) float4 lds4[2 * XQ + 64];
+  T* Xl = reinterpret_cast<T*>(lds4);
+
+  const T* Bw = reinterpret_cast<const T*>(g.b);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int bz_n = g.D / BZ, by_n = g.H / BY, bx_n = g.W / BX;
+  const int nbrick = (g.M / (g.D * g.H * g.W)) * bz_n * by_n * bx_n;
+  const int blk_all = g.swz ? xcd_swizzle(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int nt = blk_all / blocks_per_nt, blk = blk_all - nt * blocks_per_nt;
+  const int n0 = nt * 32;
+  const int u_begin = blk * upb;
+  const int u_end = u_begin + upb < nbrick ? u_begin + upb : nbrick;
+  if (u_begin >= u_end || n0 >= g.Ncols) return;
+  const int HW = g.H * g.W;
+  const int cin = 8 << g.cpg_shift;
+  const int ldb = g.lda * (int)sizeof(T);
+  const int vox_per_n = g.D * HW;
+  const int r16 = lane & 15, kg = lane >> 4;
+
+  V8<T> wf[27][RN];
+#pragma unroll
+  for (int t = 0; t < 27; ++t)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+      wf[t][j].load(Bw + ((long long)(t * (cin / 8) + kg) * g.Cpad + n0 + 8 * (r16 >> 2) + 4 * j + (r16 & 3)) * 8);
+#pragma unroll
+  for (int t = 0; t < 27; ++t) brick4_wfence(wf[t][0].v, wf[t][1].v);
+
+  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(g.a), 0, (int)((long long)(g.M / vox_per_n) * vox_per_n * ldb), 0x00020000);
+  const bool xact = tid < 216;
+  const int xq = tid % 72, r0 = tid / 72;
+  const int hx = xq >> 2, cg = xq & 3;
+  const int xlds0 = (hx * 4 + (cg ^ (((hx >> 2) & 1) << 1))) * EPQ;
+  // LDS destination of staged row k in buffer b: xs0 + b * xsb + k * xsk (idle threads: a dummy slot)
+  const int xs0 = xact ? xlds0 + r0 * RY * EPQ : (2 * XQ + (tid & 63)) * EPQ;
+  const int xsk = xact ? 3 * RY * EPQ : 0;
+  const int xsb = xact ? XQ * EPQ : 0;
+  struct Unit { int n, z0, y0, x0; };
+  auto unit_of = [&](int b) {
+    Unit r;
+    const int bx = b % bx_n; b /= bx_n;
+    const int by = b % by_n; b /= by_n;
+    r.z0 = (b % bz_n) * BZ;
+    r.n = b / bz_n;
+    r.y0 = by * BY;
+    r.x0 = bx * BX;
+    return r;
+  };
+  V8<T> xr[XK];
+  uint32_t rel[XK];
+#pragma unroll
+  for (int k = 0; k < XK; ++k) {
+    const int row = r0 + 3 * k, hz = row / HY, hy = row - hz * HY;
+    rel[k] = (uint32_t)((hz * HW + hy * g.W + hx) * ldb + cg * 16);
+  }
+  uint32_t xo[XK], om[XK];
+  float nmu[8], nrs[8];
+  int norm_n = -1;
+  auto set_x = [&](const Unit& q) {
+    if constexpr (NORM) {
+      if (q.n != norm_n) {
+        norm_n = q.n;
+        const int cb = q.n * cin + cg * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          nmu[j] = g.nmean[cb + j];
+          nrs[j] = g.nrstd[cb + j];
+        }
+      }
+    }
+    const int xx = q.x0 - 1 + hx;
+    const bool xok = xact && (unsigned)xx < (unsigned)g.W;
+    const int ob = ((q.n * g.D + q.z0 - 1) * g.H + q.y0 - 1) * g.W + q.x0 - 1;
+    const uint32_t base = (uint32_t)(ob * ldb);
+    if (q.z0 >= 1 && q.z0 + BZ < g.D && q.y0 >= 1 && q.y0 + BY < g.H) {
+#pragma unroll
+      for (int k = 0; k < XK; ++k) xo[k] = xok ? base + rel[k] : 0x80000000u;
+    } else {
+#pragma unroll
+      for (int k = 0; k < XK; ++k) {
+        const int row = r0 + 3 * k, hz = row / HY, hy = row - hz * HY;
+        const int zz = q.z0 - 1 + hz, yy = q.y0 - 1 + hy;
+        const bool ok = xok && (unsigned)zz < (unsigned)g.D && (unsigned)yy < (unsigned)g.H;
+        xo[k] = ok ? base + rel[k] : 0x80000000u;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < XK; ++k) om[k] = xo[k] != 0x80000000u ? ~0u : 0u;
+  };
+  auto load_row = [&](int k) { buf_load_v8<T>(xr[k], arsrc, xo[k]); };
+  // deferred norm of channels 2p, 2p+1 of staged row k: in_relu_apply's operations; out-of-volume rows stay 0
+  u32x4 sv[RPG];
+  auto norm_pair = [&](int k, int p, u32x4& o) {
+    float ha = (xr[k].get(2 * p) - nmu[2 * p]) * nrs[2 * p];
+    float hb = (xr[k].get(2 * p + 1) - nmu[2 * p + 1]) * nrs[2 * p + 1];
+    ha = ha > 0.f ? ha : 0.f;
+    hb = hb > 0.f ? hb : 0.f;
+    const bf16x2 h2 = {(__bf16)ha, (__bf16)hb};
+    o[p] = __builtin_bit_cast(uint32_t, h2) & om[k];
+  };
+  auto store_row = [&](int buf, int k, const u32x4& o) {
+    *reinterpret_cast<u32x4*>(Xl + buf * xsb + xs0 + k * xsk) = o;
+  };
+  auto stage_row = [&](int buf, int k) {   // whole row (prologue)
+    u32x4 o;
+    if constexpr (NORM) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) norm_pair(k, p, o);
+    } else {
+      o = __builtin_bit_cast(u32x4, xr[k].v);
+    }
+    store_row(buf, k, o);
+  };
+  int ao[3];
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) {
+    const int h = r16 + kx;
+    ao[kx] = wave * RZ + h * 4 + (kg ^ (((h >> 2) & 1) << 1));
+  }
+  float bv[RN][4];
+#pragma unroll
+  for (int j = 0; j < RN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[j][r] = g.bias ? g.bias[n0 + 8 * kg + 4 * j + r] : 0.f;
+
+  f32x4 ev[BY][RN];
+#pragma unroll
+  for (int i = 0; i < BY; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) ev[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // row i of a finished brick: lane holds channels n0 + 8 kg + 4 j + (0..3) of voxel (z0 + wave, y0 + i, x0 + r16)
+  auto epi_row = [&](const Unit& q, int i) {
+    const long long obase = (long long)q.n * vox_per_n;
+    const int z = q.z0 + wave, y = q.y0 + i, x = q.x0 + r16;
+    T* dst = out_at<T>(g, obase + (long long)(z * g.H + y) * g.W + x, n0 + 8 * kg);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[4 * j + r] = (bf16_t)(ev[i][j][r] + bv[j][r]);
+    *reinterpret_cast<bf16x8*>(dst) = o;
+  };
+
+  Unit cur = unit_of(u_begin), prev = cur;
+  set_x(cur);
+#pragma unroll
+  for (int k = 0; k < XK; ++k) load_row(k);
+#pragma unroll
+  for (int k = 0; k < XK; ++k) stage_row(0, k);
+  __syncthreads();
+  int b = 0;
+  for (int u = u_begin; u < u_end; ++u) {
+    f32x4 acc[BY][RN];
+#pragma unroll
+    for (int i = 0; i < BY; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    Unit nxt = cur;
+    if (u + 1 < u_end) {   // (the last brick re-stages itself into the idle buffer)
+      nxt.x0 += BX;
+      if (nxt.x0 == g.W) {
+        nxt.x0 = 0;
+        nxt.y0 += BY;
+        if (nxt.y0 == g.H) {
+          nxt.y0 = 0;
+          nxt.z0 += BZ;
+          if (nxt.z0 == g.D) {
+            nxt.z0 = 0;
+            ++nxt.n;
+          }
+        }
+      }
+    }
+    set_x(nxt);
+    const T* Xb = Xl + b * XQ * EPQ;
+    V8<T> af[2][HY];
+#pragma unroll
+    for (int h = 0; h < HY; ++h) af[0][h].load(Xb + (ao[0] + h * RY) * EPQ);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      const int kz = q / 3, kx = q - kz * 3;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        if (q + 1 < 9 && c < HY && DBG < 2) {     // fragment c of the next group
+          const int qn = q + 1, kzn = qn / 3, kxn = qn - kzn * 3;
+          af[qn & 1][c].load(Xb + (ao[kxn] + kzn * RZ + c * RY) * EPQ);
+        }
+        if (q == 0 && DBG == 0) {
+          load_row(c);                  // next brick's halo rows 0..7
+          if ((c & 1) == 0) epi_row(prev, c >> 1);
+        }
+        if (q == 1 && c < XK - 8 && DBG == 0) load_row(8 + c);
+        if (q >= SG0 && DBG == 0) {
+#pragma unroll
+          for (int pp = 0; pp < PPC; ++pp) {
+            const int pi = c * PPC + pp;            // pair index inside the group: row slot pi / 4, pair pi % 4
+            const int k = (q - SG0) * RPG + pi / 4;
+            if (k < XK) {
+              if constexpr (NORM) norm_pair(k, pi % 4, sv[pi / 4]);
+              else if (pi % 4 == 0) sv[pi / 4] = __builtin_bit_cast(u32x4, xr[k].v);
+              if (pi % 4 == 3) store_row(b ^ 1, k, sv[pi / 4]);
+            }
+          }
+        }
+#pragma unroll
+        for (int m = 3 * c; m < 3 * c + 3; ++m) {
+          const int ky = m >> 3, i = (m >> 1) & 3, j = m & 1;
+          mfma_aw(acc[i][j], wf[kz * 9 + ky * 3 + kx][j].v, af[q & 1][i + ky].v);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BY; ++i) brick4_fence(acc[i][0], acc[i][1]);
+#pragma unroll
+    for (int i = 0; i < BY; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) ev[i][j] = acc[i][j];
+    prev = cur;
+    __syncthreads();   // buffer b^1 is complete; buffer b is free for the brick after next
+    b ^= 1;
+    cur = nxt;
+  }
+#pragma unroll
+  for (int i = 0; i < BY; ++i) epi_row(prev, i);
+}
+
 // ------------------------------------- runtime-brick conv (small volumes)
 // conv3_brick2_kernel for volumes whose sides are not multiples of 8 (the
 // 12^3 and 6^3 levels): the brick (bz, by, bx), <= 256 voxels, is chosen on the
@@ -2054,6 +2314,28 @@ int launch_brick5(const GemmArgs& g, hipStream_t s, long long* dbg, bool dma) {
   if (g.inpart) {   // samples a block does not touch keep zero partials
     hipMemsetAsync(g.inpart, 0, sizeof(float) * 2 * (size_t)(g.M / (g.D * g.H * g.W)) * bpn5 * g.Ncols, s);
     hipLaunchKernelGGL((conv3_brick5_kernel<false, true, true>), grid, block, 0, s, g, upb5, bpn5, nullptr);
+    return upb5;
+  }
+  if (!dbg && !dma && knob("MMSEG_BRICK6", 1)) {
+    const int sg = knob("MMSEG_BRICK6_SG0", 6);
+    mmseg::note_kernel("conv3_brick6_kernel<BN32>");
+#ifdef MMSEG_TIMING_PROBES
+    if (knob("MMSEG_BRICK6_DBG", 0) == 1) {
+      hipLaunchKernelGGL((conv3_brick6_kernel<false, 3, 1>), grid, block, 0, s, g, upb5, bpn5);
+      return upb5;
+    }
+    if (knob("MMSEG_BRICK6_DBG", 0) == 2) {
+      hipLaunchKernelGGL((conv3_brick6_kernel<false, 3, 2>), grid, block, 0, s, g, upb5, bpn5);
+      return upb5;
+    }
+#endif
+#define MMSEG_B6(N, S) hipLaunchKernelGGL((conv3_brick6_kernel<N, S>), grid, block, 0, s, g, upb5, bpn5)
+    if (g.nmean) {
+      if (sg == 6) MMSEG_B6(true, 6); else if (sg == 7) MMSEG_B6(true, 7); else MMSEG_B6(true, 3);
+    } else {
+      if (sg == 6) MMSEG_B6(false, 6); else if (sg == 7) MMSEG_B6(false, 7); else MMSEG_B6(false, 3);
+    }
+#undef MMSEG_B6
     return upb5;
   }
   if (dbg && dma) hipLaunchKernelGGL((conv3_brick5_kernel<true, true>), grid, block, 0, s, g, upb5, bpn5, dbg);

@@ -60,6 +60,12 @@ def test_conv3_fwd_dgrad_wgrad(dev, dtype, cin, cout, shape):
     ({"MMSEG_BRICK4_BLOCKS": "3"}, 32, 32, (2, 8, 8, 32)),           # 16 bricks over 3 blocks, ragged ranges
     ({}, 32, 32, (1, 12, 12, 16)),                                   # border bricks on every side
     ({"MMSEG_BRICK4_BLOCKS": "4"}, 32, 64, (1, 4, 4, 32)),           # 2 column tiles
+    # brick v6 (v5's register-staged path with the staging interleaved between the MFMAs; default) against v5,
+    # and with the staged rows written from group 6 / 7 on
+    ({"MMSEG_BRICK6": "0", "MMSEG_BRICK4_BLOCKS": "3"}, 32, 32, (2, 8, 8, 32)),
+    ({"MMSEG_BRICK6_SG0": "6", "MMSEG_BRICK4_BLOCKS": "3"}, 32, 32, (2, 8, 8, 32)),
+    ({"MMSEG_BRICK6_SG0": "7"}, 32, 32, (1, 12, 12, 16)),
+    ({"MMSEG_BRICK6_SG0": "6", "MMSEG_BRICK4_BLOCKS": "1"}, 32, 32, (2, 4, 4, 16)),   # one brick per sample
     ({"MMSEG_BRICK3_BN64": "1", "MMSEG_BRICK2_MINBLK": "0", "MMSEG_BRICK3_BLOCKS": "2"}, 64, 64, (2, 8, 8, 8)),
     ({"MMSEG_BRICK2_ZW": "2"}, 32, 32, (1, 8, 8, 16)),              # BN32 ZW2 (bf16 only; f32 takes ZW1)
     ({"MMSEG_BRICK2_ZW": "2"}, 64, 32, (2, 8, 8, 8)),               # BN32 ZW2, dgrad with 2 input chunks

@@ -3,7 +3,9 @@
     python tools/convbench.py [--shape N,S,Cin,Cout | N,D,H,W,Cin,Cout ...] [--iters 20] [--only fwd,dgrad,wgrad]
 Env knobs (MMSEG_*) select kernel variants; prints one JSON line per (shape, op) with
 the kernel the library launched, us per launch and TFLOP/s (2*27*Cin*Cout per voxel).
-Ops: fwd, fwds (forward with the fused InstanceNorm partials, as ConvBlock3D runs it), dgrad, wgrad.
+Ops: fwd, fwds (forward with the fused InstanceNorm partials, as ConvBlock3D runs it), fwdn (forward of
+relu(IN(x)) with the norm applied on staging: Block.defer1's conv2), dgrad, dgradin (data gradient that also sums
+the InstanceNorm-backward partials of its output: Block.bwd's conv2 at 96^3), wgrad.
 --probe: load libmmseg_hip_probe.so (make -C csrc probe) and print the block timeline of one launch per op
 (per-CU residency, block lifetimes, per-phase cycles of block 0's waves; see conv_gemm.hip PROBE_*).
 """
@@ -61,6 +63,9 @@ def main():
 
         nb = layer.stats_bricks(x, y)
         part = torch.empty(N * max(nb, 1) * Co * 2, dtype=torch.float32, device=dev)
+        mean = torch.zeros(N * Ci, dtype=torch.float32, device=dev)
+        rstd = torch.ones(N * Ci, dtype=torch.float32, device=dev)
+        inpart = torch.empty(N * 4096 * Ci * 2, dtype=torch.float32, device=dev)
 
         def run(op):
             if op == "fwd":
@@ -68,6 +73,16 @@ def main():
             elif op == "fwds":
                 assert nb > 0, "no fused-statistics kernel for this shape (MMSEG_FUSED_STATS=1)"
                 layer.fwd(x, y, stats_part=part)
+            elif op == "fwdn":
+                layer.fwd_norm(x, mean, rstd, y)
+            elif op == "dgradin":
+                M = N * D * H * W
+                nch = L.mmseg_conv3_dgrad_in_chunks(M, Ci, layer.Cpad_d, layer.KGd, layer.dshift, D, H, W, y.ld,
+                                                    dx.ld, code)
+                assert nch > 0 and N * nch * Ci * 2 <= inpart.numel(), "no INP data-gradient kernel for this shape"
+                L.mmseg_conv3_dgrad_in(y.ptr, y.ld, layer.wd.data_ptr(), dx.ptr, dx.ld, M, Ci, layer.Cpad_d,
+                                       layer.KGd, layer.dshift, D, H, W, x.ptr, x.ld, mean.data_ptr(),
+                                       rstd.data_ptr(), inpart.data_ptr(), code, s)
             elif op == "dgrad":
                 M = N * D * H * W
                 ks = L.mmseg_conv3_splits(M, Ci, layer.Cpad_d, layer.KGd, layer.dshift, D, H, W, y.ld, dx.ld, code)
