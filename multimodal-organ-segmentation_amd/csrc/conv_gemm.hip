@@ -1129,6 +1129,10 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kern
 __device__ __forceinline__ void mfma_aw(f32x4& acc, const bf16x8& w, const bf16x8& x) {
   asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "a"(w), "v"(x));
 }
+// first MFMA of an accumulation chain: C = 0 (no accumulator zeroing per brick)
+__device__ __forceinline__ void mfma_aw0(f32x4& acc, const bf16x8& w, const bf16x8& x) {
+  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "a"(w), "v"(x));
+}
 __device__ __forceinline__ void brick4_fence(f32x4& a, f32x4& b) {
   asm volatile("s_nop 7\n\ts_nop 7" : "+a"(a), "+a"(b));
 }
@@ -1678,6 +1682,7 @@ __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int up
 // DBG (timing probes only, wrong results): 1 = MFMAs + fragment reads only after the prologue, 2 = MFMAs only.
 template <bool NORM, int SG0 = 3, int DBG = 0>
 __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int upb, int blocks_per_nt) {
+  PROBE_BLOCK(false);
   using T = bf16_t;
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -1846,11 +1851,7 @@ __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int up
   __syncthreads();
   int b = 0;
   for (int u = u_begin; u < u_end; ++u) {
-    f32x4 acc[BY][RN];
-#pragma unroll
-    for (int i = 0; i < BY; ++i)
-#pragma unroll
-      for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    f32x4 acc[BY][RN];   // (first written by the C = 0 MFMAs of group 0)
     Unit nxt = cur;
     if (u + 1 < u_end) {   // (the last brick re-stages itself into the idle buffer)
       nxt.x0 += BX;
@@ -1902,13 +1903,15 @@ __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int up
 #pragma unroll
         for (int m = 3 * c; m < 3 * c + 3; ++m) {
           const int ky = m >> 3, i = (m >> 1) & 3, j = m & 1;
-          mfma_aw(acc[i][j], wf[kz * 9 + ky * 3 + kx][j].v, af[q & 1][i + ky].v);
+          if (q == 0 && ky == 0) mfma_aw0(acc[i][j], wf[kx][j].v, af[0][i].v);
+          else mfma_aw(acc[i][j], wf[kz * 9 + ky * 3 + kx][j].v, af[q & 1][i + ky].v);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-#pragma unroll
-    for (int i = 0; i < BY; ++i) brick4_fence(acc[i][0], acc[i][1]);
+    // one MFMA-result hazard fence over all 8 accumulators before they are copied
+    asm volatile("s_nop 7\n\ts_nop 7" : "+a"(acc[0][0]), "+a"(acc[0][1]), "+a"(acc[1][0]), "+a"(acc[1][1]),
+                 "+a"(acc[2][0]), "+a"(acc[2][1]), "+a"(acc[3][0]), "+a"(acc[3][1]));
 #pragma unroll
     for (int i = 0; i < BY; ++i)
 #pragma unroll
@@ -1920,6 +1923,7 @@ __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int up
   }
 #pragma unroll
   for (int i = 0; i < BY; ++i) epi_row(prev, i);
+  PROBE_BLOCK(true);
 }
 
 // ------------------------------------- runtime-brick conv (small volumes)

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--layers", action="store_true", help="also print every timed launch of the last step")
     args = ap.parse_args()
+    # eager steps: a captured step graph would replay the first variant's kernels for every variant
+    os.environ.setdefault("MMSEG_STEP_GRAPH", "0")
     import mmseg_amd  # noqa: F401
     from bench import make_config
     from mmseg_amd.data import device_batches
