@@ -1680,7 +1680,10 @@ __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int up
 // 40 threads without a halo column write a dummy LDS slot, the last brick re-stages itself, and the first brick's
 // group-0 epilogue writes bias-only values that the next brick's epilogue (same lanes, same addresses) overwrites.
 // DBG (timing probes only, wrong results): 1 = MFMAs + fragment reads only after the prologue, 2 = MFMAs only.
-template <bool NORM, int SG0 = 3, int DBG = 0>
+// INP (data gradient, no bias): the epilogue also sums the InstanceNorm-backward partials of its output, as brick5's
+// INP variant (same per-lane order: bitwise the same partials); the x of a brick's output voxels is loaded in its
+// group 4, its partial sums are formed in the next brick's group 1.
+template <bool NORM, int SG0 = 3, int DBG = 0, bool INP = false>
 __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int upb, int blocks_per_nt) {
   PROBE_BLOCK(false);
   using T = bf16_t;
@@ -1830,16 +1833,78 @@ __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int up
 #pragma unroll
     for (int j = 0; j < RN; ++j) ev[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   // row i of a finished brick: lane holds channels n0 + 8 kg + 4 j + (0..3) of voxel (z0 + wave, y0 + i, x0 + r16)
+  bf16x8 eo[BY];   // the stored rows (INP: their partial sums follow one group later)
   auto epi_row = [&](const Unit& q, int i) {
     const long long obase = (long long)q.n * vox_per_n;
     const int z = q.z0 + wave, y = q.y0 + i, x = q.x0 + r16;
     T* dst = out_at<T>(g, obase + (long long)(z * g.H + y) * g.W + x, n0 + 8 * kg);
-    bf16x8 o;
 #pragma unroll
     for (int j = 0; j < RN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[4 * j + r] = (bf16_t)(ev[i][j][r] + bv[j][r]);
-    *reinterpret_cast<bf16x8*>(dst) = o;
+      for (int r = 0; r < 4; ++r) eo[i][4 * j + r] = (bf16_t)(ev[i][j][r] + bv[j][r]);
+    *reinterpret_cast<bf16x8*>(dst) = eo[i];
+  };
+  // InstanceNorm-backward partials (INP): per lane the sums over its voxels of g and g (x - mean) for channels
+  // n0 + 8 kg + (0..7), g = dy if x > mean else 0 (times rstd at the flush); the first brick's epilogue runs on
+  // zeroed accumulators and x and adds 0
+  __shared__ float ired[INP ? 4 : 1][2][32];
+  float isg[8], isgx[8], imu[8];
+  int in_n = -1;
+  V8<T> xin[BY];
+  if constexpr (INP) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) isg[k] = isgx[k] = imu[k] = 0.f;
+#pragma unroll
+    for (int i = 0; i < BY; ++i) xin[i].zero();
+  }
+  auto in_flush = [&]() {   // block-wide, fixed order: 16-lane tree, then waves 0..3
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        isg[k] += __shfl_xor(isg[k], o, 64);
+        isgx[k] += __shfl_xor(isgx[k], o, 64);
+      }
+    if (r16 == 0)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        ired[wave][0][8 * kg + k] = isg[k];
+        ired[wave][1][8 * kg + k] = isgx[k];
+      }
+    __syncthreads();
+    if (tid < 32) {
+      const float a = ired[0][0][tid] + ired[1][0][tid] + ired[2][0][tid] + ired[3][0][tid];
+      const float c = ired[0][1][tid] + ired[1][1][tid] + ired[2][1][tid] + ired[3][1][tid];
+      float* p = g.inpart + (((long long)in_n * blocks_per_nt + blk) * g.Ncols + n0 + tid) * 2;
+      p[0] = a;
+      p[1] = c * g.inrstd[in_n * g.Ncols + n0 + tid];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) isg[k] = isgx[k] = 0.f;
+  };
+  auto in_begin = [&](const Unit& q) {   // block-uniform: the sample of the epilogue's brick
+    if constexpr (INP) {
+      if (q.n != in_n) {
+        if (in_n >= 0) in_flush();
+        in_n = q.n;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) imu[k] = g.inmean[in_n * g.Ncols + n0 + 8 * kg + k];
+      }
+    }
+  };
+  auto in_load_row = [&](const Unit& q, int i) {   // x of the lane's output voxel of row i
+    const T* X = reinterpret_cast<const T*>(g.inx) + (long long)q.n * vox_per_n * g.ldinx + n0 + 8 * kg;
+    xin[i].load(X + (long long)((q.z0 + wave) * g.H + q.y0 + i) * g.W * g.ldinx + (long long)(q.x0 + r16) * g.ldinx);
+  };
+  auto epi_inp = [&](int i, int half) {
+#pragma unroll
+    for (int k = 4 * half; k < 4 * half + 4; ++k) {
+      const float d = xin[i].get(k) - imu[k];
+      const float gg = d > 0.f ? (float)eo[i][k] : 0.f;
+      isg[k] += gg;
+      isgx[k] = fmaf(gg, d, isgx[k]);
+    }
   };
 
   Unit cur = unit_of(u_begin), prev = cur;
@@ -1869,6 +1934,7 @@ __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int up
       }
     }
     set_x(nxt);
+    in_begin(prev);
     const T* Xb = Xl + b * XQ * EPQ;
     V8<T> af[2][HY];
 #pragma unroll
@@ -1888,6 +1954,10 @@ __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int up
           if ((c & 1) == 0) epi_row(prev, c >> 1);
         }
         if (q == 1 && c < XK - 8 && DBG == 0) load_row(8 + c);
+        if constexpr (INP) {
+          if (q == 1 && DBG == 0) epi_inp(c >> 1, c & 1);
+          if (q == 4 && c < BY && DBG == 0) in_load_row(cur, c);
+        }
         if (q >= SG0 && DBG == 0) {
 #pragma unroll
           for (int pp = 0; pp < PPC; ++pp) {
@@ -1921,8 +1991,16 @@ __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int up
     b ^= 1;
     cur = nxt;
   }
+  in_begin(prev);
 #pragma unroll
-  for (int i = 0; i < BY; ++i) epi_row(prev, i);
+  for (int i = 0; i < BY; ++i) {
+    epi_row(prev, i);
+    if constexpr (INP) {
+      epi_inp(i, 0);
+      epi_inp(i, 1);
+    }
+  }
+  if constexpr (INP) in_flush();
   PROBE_BLOCK(true);
 }
 
@@ -2317,6 +2395,11 @@ int launch_brick5(const GemmArgs& g, hipStream_t s, long long* dbg, bool dma) {
   const dim3 grid(bpn5 * nt_n), block(256);
   if (g.inpart) {   // samples a block does not touch keep zero partials
     hipMemsetAsync(g.inpart, 0, sizeof(float) * 2 * (size_t)(g.M / (g.D * g.H * g.W)) * bpn5 * g.Ncols, s);
+    if (!g.bias && knob("MMSEG_BRICK6", 1) && knob("MMSEG_BRICK6_INP", 1)) {
+      mmseg::note_kernel("conv3_brick6_kernel<BN32,INP>");
+      hipLaunchKernelGGL((conv3_brick6_kernel<false, 6, 0, true>), grid, block, 0, s, g, upb5, bpn5);
+      return upb5;
+    }
     hipLaunchKernelGGL((conv3_brick5_kernel<false, true, true>), grid, block, 0, s, g, upb5, bpn5, nullptr);
     return upb5;
   }
