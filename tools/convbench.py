@@ -29,10 +29,12 @@ def main():
     ap.add_argument("--only", default="fwd,dgrad,wgrad")
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--probe", action="store_true")
+    ap.add_argument("--lib", default=None, help="another in-tree build of the library (A/B), e.g. libmmseg_hip_old.so")
     args = ap.parse_args()
-    if args.probe:
+    if args.probe or args.lib:
         from mmseg_amd import _lib
-        _lib.set_library_path(os.path.join(ROOT, "multimodal-organ-segmentation_amd", "libmmseg_hip_probe.so"))
+        _lib.set_library_path(os.path.join(ROOT, "multimodal-organ-segmentation_amd",
+                                           args.lib or "libmmseg_hip_probe.so"))
     import mmseg_amd  # noqa: F401
     from mmseg_amd.engine.layers import Conv3
     from mmseg_amd.engine.runtime import FlatParams, Runtime
