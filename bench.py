@@ -38,7 +38,7 @@ STEP_WORK = {("unet", 2): (1206.2e9, 4.15e9), ("dual_encoder", 2): (1559.4e9, 6.
 
 
 def make_config(model, batch, dtype, out_channels=6, modalities=("CT", "PET"), size=96, loss="dice_ce",
-                kernels="hip", amp="bf16"):
+                kernels="hip", amp="bf16", fp8=False):
     backbone = {"features": [32, 64, 128, 256, 512], "norm": "instance"}
     if model == "swin_unetr":     # config c4: SwinUNETR feature_size 48 (swin_unetr.py:180-200 defaults otherwise)
         backbone = {"img_size": [size] * 3, "feature_size": 48}
@@ -54,7 +54,7 @@ def make_config(model, batch, dtype, out_channels=6, modalities=("CT", "PET"), s
                      "loss": {"name": loss, "dice_weight": 0.5, "ce_weight": 0.5, "class_weights": None,
                               "tversky_alpha": 0.5, "tversky_beta": 0.5},
                      "checkpoint": {"save_last": False, "save_best": False}},
-        "hardware": {"device": "cuda", "mixed_precision": dtype == "bf16", "kernels": kernels,
+        "hardware": {"device": "cuda", "mixed_precision": dtype == "bf16", "kernels": kernels, "fp8": fp8,
                      # torch-op backend: bf16 autocast, or the reference's own fp16 autocast + GradScaler
                      "engine_dtype": "bfloat16" if dtype == "bf16" and not (kernels == "torch" and amp == "fp16")
                      else "float32"},
@@ -176,6 +176,8 @@ def main():
     ap.add_argument("--timer-steps", type=int, default=3, help="extra steps timed per kernel family (roofline)")
     ap.add_argument("--kernels", default="hip", choices=["hip", "torch"],
                     help="torch: the same model / step through PyTorch-ROCm ops (MIOpen convs; hardware.kernels A/B)")
+    ap.add_argument("--fp8", action="store_true",
+                    help="config c5's mixed bf16/fp8: e4m3 forward convolutions where the kernel takes them")
     ap.add_argument("--amp", default="bf16", choices=["bf16", "fp16"],
                     help="--kernels torch autocast dtype (fp16 + GradScaler = the reference's GPU mode)")
     args = ap.parse_args()
@@ -196,7 +198,7 @@ def main():
 
     mods = args.modalities.split(",")
     cfg = make_config(args.model, args.batch, args.dtype, size=args.size, modalities=mods, loss=args.loss,
-                      kernels=args.kernels, amp=args.amp)
+                      kernels=args.kernels, amp=args.amp, fp8=args.fp8)
     if args.kernels == "torch":
         args.no_cpu_baseline = True
         args.timer_steps = 0
@@ -273,7 +275,7 @@ def main():
         F, Bt = work[0] * args.batch, work[1] * args.batch
         t_mfma, t_hbm = F / (PEAK_BF16_TFLOPS * 1e12), Bt / (PEAK_HBM_GBS * 1e9)
         t_roof = max(t_mfma, t_hbm)
-        counter, csrc = pmc_step_bytes()
+        counter, csrc = pmc_step_bytes() if args.kernels == "hip" and not args.fp8 else (None, None)
         step = {"bound": "hbm" if t_hbm >= t_mfma else "mfma", "algorithmic_tflop": round(F / 1e12, 3),
                 "compulsory_gb": round(Bt / 1e9, 3), "t_mfma_ms": round(t_mfma * 1e3, 3),
                 "t_hbm_ms": round(t_hbm * 1e3, 3), "t_roof_ms": round(t_roof * 1e3, 3),
@@ -298,7 +300,8 @@ def main():
         "value": round(value, 3), "unit": "patches/s", "n_gpus": n_gpus, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None,
-        "dtype": args.dtype if args.kernels == "hip" else f"{args.amp if args.dtype == 'bf16' else 'fp32'}-autocast",
+        "dtype": (args.dtype + ("+fp8" if args.fp8 else "")) if args.kernels == "hip"
+        else f"{args.amp if args.dtype == 'bf16' else 'fp32'}-autocast",
         "data": f"synthetic (seeded {'/'.join(mods)} phantoms, pre-staged in HBM)",
         "config": {"workload": f"{workload} {args.size}^3, modalities {'+'.join(mods)}, 6 classes, "
                                f"{'DiceCE' if args.loss == 'dice_ce' else 'Tversky'}, AdamW, per-GPU batch {args.batch}",

@@ -172,6 +172,17 @@ int mmseg_conv3_norm_ok(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D
 int mmseg_conv3_fwd_norm(const void* a, int lda, const float* nmean, const float* nrstd, const void* wpacked,
                          const float* bias, void* out, int ldo, int M, int Ncols, int Cpad, int KG, int cpg_shift,
                          int D, int H, int W, int dtype, void* stream);
+/* Mixed bf16/fp8 forward (config c5, "mixed bf16/fp8"): the 3^3 convs the brick kernels take with one 32-channel
+ * input chunk run with OCP e4m3 operands and fp32 accumulation.  mmseg_pack_conv3_fp8 writes the e4m3 image of
+ * w[co] * s[co], s[co] = 448 / max|w[co]|, and wdq[co] = 1 / s[co]; mmseg_conv3_fwd_fp8 stages the (optionally
+ * normalised, as mmseg_conv3_fwd_norm) bf16 input as e4m3 at unit scale and writes bf16.  Replaces the
+ * reference's Conv3d forward (unet.py:26-27, 53-60) under its mixed-precision mode. */
+int mmseg_conv3_fp8_ok(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo);
+int mmseg_pack_conv3_fp8(const float* w, int Co, int Ci, int Cip, int KGp, int Cpad, void* dst, float* wdq,
+                         void* stream);
+int mmseg_conv3_fwd_fp8(const void* a, int lda, const float* nmean, const float* nrstd, const void* w8,
+                        const float* wdq, const float* bias, void* out, int ldo, int M, int Ncols, int Cpad, int KG,
+                        int cpg_shift, int D, int H, int W, void* stream);
 int mmseg_conv3_wgrad_norm_ok(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W, int lddy,
                               int ldx, int dtype);
 int mmseg_conv3_wgrad_norm(const void* dy, int lddy, const void* x, int ldx, const float* nmean, const float* nrstd,

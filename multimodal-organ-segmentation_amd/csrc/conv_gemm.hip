@@ -107,6 +107,9 @@ struct GemmArgs {
   // half of an 8-wave block loses every issue arbitration to its SIMD partner); bit 1 = s_setprio 1 around the tap
   // loop's MFMAs (brick2 / brick8), so a co-resident wave in its staging phase yields issue to the MFMA stream
   int prio;
+  // fp8 forward (brick6 F8, mmseg_conv3_fwd_fp8): b holds e4m3 weights w * s[co] (s = 448 / max |w[co]|), wdq[co] =
+  // 1 / s[co] restores the scale in the epilogue; the staged activations are e4m3 at unit scale
+  const float* wdq;
 };
 
 // Output element (row voxel, column) of a GEMM (split-aware; split is a multiple of 8).
@@ -1129,6 +1132,13 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kern
 __device__ __forceinline__ void mfma_aw(f32x4& acc, const bf16x8& w, const bf16x8& x) {
   asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "a"(w), "v"(x));
 }
+// e4m3 x e4m3 -> f32 (K = 32: a lane holds 8 fp8 = 8 bytes of A and of B, the bf16 form's lane map)
+__device__ __forceinline__ void mfma_aw8(f32x4& acc, const long& w, const long& x) {
+  asm("v_mfma_f32_16x16x32_fp8_fp8 %0, %1, %2, %0" : "+a"(acc) : "a"(w), "v"(x));
+}
+__device__ __forceinline__ void mfma_aw80(f32x4& acc, const long& w, const long& x) {
+  asm("v_mfma_f32_16x16x32_fp8_fp8 %0, %1, %2, 0" : "=a"(acc) : "a"(w), "v"(x));
+}
 // first MFMA of an accumulation chain: C = 0 (no accumulator zeroing per brick)
 __device__ __forceinline__ void mfma_aw0(f32x4& acc, const bf16x8& w, const bf16x8& x) {
   asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "a"(w), "v"(x));
@@ -1683,7 +1693,10 @@ __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int up
 // INP (data gradient, no bias): the epilogue also sums the InstanceNorm-backward partials of its output, as brick5's
 // INP variant (same per-lane order: bitwise the same partials); the x of a brick's output voxels is loaded in its
 // group 4, its partial sums are formed in the next brick's group 1.
-template <bool NORM, int SG0 = 3, int DBG = 0, bool INP = false>
+// F8 (forward only; mixed bf16/fp8 of config c5): the halo is staged as OCP e4m3 (the first 8 bytes of each 16-B
+// quad, read by ds_read_b64), the weights come as e4m3 w * s[co] (mmseg_pack_conv3_fp8) and the MFMA is
+// v_mfma_f32_16x16x32_fp8_fp8 with fp32 accumulation; the epilogue multiplies by g.wdq[co] = 1 / s[co].
+template <bool NORM, int SG0 = 3, int DBG = 0, bool INP = false, bool F8 = false>
 __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int upb, int blocks_per_nt) {
   PROBE_BLOCK(false);
   using T = bf16_t;
@@ -1720,14 +1733,26 @@ __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int up
   const int vox_per_n = g.D * HW;
   const int r16 = lane & 15, kg = lane >> 4;
 
-  V8<T> wf[27][RN];
+  V8<T> wf[F8 ? 1 : 27][RN];
+  long wf8[F8 ? 27 : 1][RN];
+  if constexpr (F8) {
+    const long* B8 = reinterpret_cast<const long*>(g.b);
 #pragma unroll
-  for (int t = 0; t < 27; ++t)
+    for (int t = 0; t < 27; ++t)
 #pragma unroll
-    for (int j = 0; j < RN; ++j)
-      wf[t][j].load(Bw + ((long long)(t * (cin / 8) + kg) * g.Cpad + n0 + 8 * (r16 >> 2) + 4 * j + (r16 & 3)) * 8);
+      for (int j = 0; j < RN; ++j)
+        wf8[t][j] = B8[(long long)(t * (cin / 8) + kg) * g.Cpad + n0 + 8 * (r16 >> 2) + 4 * j + (r16 & 3)];
 #pragma unroll
-  for (int t = 0; t < 27; ++t) brick4_wfence(wf[t][0].v, wf[t][1].v);
+    for (int t = 0; t < 27; ++t) asm volatile("s_nop 2" : "+a"(wf8[t][0]), "+a"(wf8[t][1]));
+  } else {
+#pragma unroll
+    for (int t = 0; t < 27; ++t)
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+        wf[t][j].load(Bw + ((long long)(t * (cin / 8) + kg) * g.Cpad + n0 + 8 * (r16 >> 2) + 4 * j + (r16 & 3)) * 8);
+#pragma unroll
+    for (int t = 0; t < 27; ++t) brick4_wfence(wf[t][0].v, wf[t][1].v);
+  }
 
   const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(g.a), 0, (int)((long long)(g.M / vox_per_n) * vox_per_n * ldb), 0x00020000);
@@ -1799,17 +1824,36 @@ __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int up
     float hb = (xr[k].get(2 * p + 1) - nmu[2 * p + 1]) * nrs[2 * p + 1];
     ha = ha > 0.f ? ha : 0.f;
     hb = hb > 0.f ? hb : 0.f;
-    const bf16x2 h2 = {(__bf16)ha, (__bf16)hb};
-    o[p] = __builtin_bit_cast(uint32_t, h2) & om[k];
+    if constexpr (F8) {   // pairs 0, 1 -> dword 0 (low, high word), 2, 3 -> dword 1
+      if (p & 1) o[p >> 1] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(ha, hb, (int)o[p >> 1], true) & om[k];
+      else o[p >> 1] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(ha, hb, 0, false);
+    } else {
+      const bf16x2 h2 = {(__bf16)ha, (__bf16)hb};
+      o[p] = __builtin_bit_cast(uint32_t, h2) & om[k];
+    }
+  };
+  auto to_f8 = [&](int k, u32x4& o) {   // raw staged row (no norm) -> e4m3 (out-of-volume lanes read 0 -> 0)
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      const int lo = __builtin_amdgcn_cvt_pk_fp8_f32(xr[k].get(4 * d), xr[k].get(4 * d + 1), 0, false);
+      o[d] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(xr[k].get(4 * d + 2), xr[k].get(4 * d + 3), lo, true);
+    }
   };
   auto store_row = [&](int buf, int k, const u32x4& o) {
-    *reinterpret_cast<u32x4*>(Xl + buf * xsb + xs0 + k * xsk) = o;
+    if constexpr (F8) {
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<u32x2*>(Xl + buf * xsb + xs0 + k * xsk) = (u32x2){o[0], o[1]};
+    } else {
+      *reinterpret_cast<u32x4*>(Xl + buf * xsb + xs0 + k * xsk) = o;
+    }
   };
   auto stage_row = [&](int buf, int k) {   // whole row (prologue)
     u32x4 o;
     if constexpr (NORM) {
 #pragma unroll
       for (int p = 0; p < 4; ++p) norm_pair(k, p, o);
+    } else if constexpr (F8) {
+      to_f8(k, o);
     } else {
       o = __builtin_bit_cast(u32x4, xr[k].v);
     }
@@ -1821,11 +1865,14 @@ __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int up
     const int h = r16 + kx;
     ao[kx] = wave * RZ + h * 4 + (kg ^ (((h >> 2) & 1) << 1));
   }
-  float bv[RN][4];
+  float bv[RN][4], dq[F8 ? RN : 1][4];
 #pragma unroll
   for (int j = 0; j < RN; ++j)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bv[j][r] = g.bias ? g.bias[n0 + 8 * kg + 4 * j + r] : 0.f;
+    for (int r = 0; r < 4; ++r) {
+      bv[j][r] = g.bias ? g.bias[n0 + 8 * kg + 4 * j + r] : 0.f;
+      if constexpr (F8) dq[j][r] = g.wdq[n0 + 8 * kg + 4 * j + r];
+    }
 
   f32x4 ev[BY][RN];
 #pragma unroll
@@ -1841,7 +1888,10 @@ __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int up
 #pragma unroll
     for (int j = 0; j < RN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) eo[i][4 * j + r] = (bf16_t)(ev[i][j][r] + bv[j][r]);
+      for (int r = 0; r < 4; ++r) {
+        if constexpr (F8) eo[i][4 * j + r] = (bf16_t)fmaf(ev[i][j][r], dq[j][r], bv[j][r]);
+        else eo[i][4 * j + r] = (bf16_t)(ev[i][j][r] + bv[j][r]);
+      }
     *reinterpret_cast<bf16x8*>(dst) = eo[i];
   };
   // InstanceNorm-backward partials (INP): per lane the sums over its voxels of g and g (x - mean) for channels
@@ -1936,9 +1986,13 @@ __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int up
     set_x(nxt);
     in_begin(prev);
     const T* Xb = Xl + b * XQ * EPQ;
-    V8<T> af[2][HY];
+    V8<T> af[F8 ? 1 : 2][HY];
+    long af8[F8 ? 2 : 1][HY];
 #pragma unroll
-    for (int h = 0; h < HY; ++h) af[0][h].load(Xb + (ao[0] + h * RY) * EPQ);
+    for (int h = 0; h < HY; ++h) {
+      if constexpr (F8) af8[0][h] = *reinterpret_cast<const long*>(Xb + (ao[0] + h * RY) * EPQ);
+      else af[0][h].load(Xb + (ao[0] + h * RY) * EPQ);
+    }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int q = 0; q < 9; ++q) {
@@ -1947,7 +2001,8 @@ __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int up
       for (int c = 0; c < 8; ++c) {
         if (q + 1 < 9 && c < HY && DBG < 2) {     // fragment c of the next group
           const int qn = q + 1, kzn = qn / 3, kxn = qn - kzn * 3;
-          af[qn & 1][c].load(Xb + (ao[kxn] + kzn * RZ + c * RY) * EPQ);
+          if constexpr (F8) af8[qn & 1][c] = *reinterpret_cast<const long*>(Xb + (ao[kxn] + kzn * RZ + c * RY) * EPQ);
+          else af[qn & 1][c].load(Xb + (ao[kxn] + kzn * RZ + c * RY) * EPQ);
         }
         if (q == 0 && DBG == 0) {
           load_row(c);                  // next brick's halo rows 0..7
@@ -1965,6 +2020,7 @@ __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int up
             const int k = (q - SG0) * RPG + pi / 4;
             if (k < XK) {
               if constexpr (NORM) norm_pair(k, pi % 4, sv[pi / 4]);
+              else if constexpr (F8) { if (pi % 4 == 0) to_f8(k, sv[pi / 4]); }
               else if (pi % 4 == 0) sv[pi / 4] = __builtin_bit_cast(u32x4, xr[k].v);
               if (pi % 4 == 3) store_row(b ^ 1, k, sv[pi / 4]);
             }
@@ -1973,8 +2029,13 @@ __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int up
 #pragma unroll
         for (int m = 3 * c; m < 3 * c + 3; ++m) {
           const int ky = m >> 3, i = (m >> 1) & 3, j = m & 1;
-          if (q == 0 && ky == 0) mfma_aw0(acc[i][j], wf[kx][j].v, af[0][i].v);
-          else mfma_aw(acc[i][j], wf[kz * 9 + ky * 3 + kx][j].v, af[q & 1][i + ky].v);
+          if constexpr (F8) {
+            if (q == 0 && ky == 0) mfma_aw80(acc[i][j], wf8[kx][j], af8[0][i]);
+            else mfma_aw8(acc[i][j], wf8[kz * 9 + ky * 3 + kx][j], af8[q & 1][i + ky]);
+          } else {
+            if (q == 0 && ky == 0) mfma_aw0(acc[i][j], wf[kx][j].v, af[0][i].v);
+            else mfma_aw(acc[i][j], wf[kz * 9 + ky * 3 + kx][j].v, af[q & 1][i + ky].v);
+          }
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -2393,6 +2454,12 @@ int launch_brick5(const GemmArgs& g, hipStream_t s, long long* dbg, bool dma) {
   const int bpn5 = ceil_div(nb5, upb5);
   mmseg::note_kernel("conv3_brick5_kernel<BN32>");
   const dim3 grid(bpn5 * nt_n), block(256);
+  if (g.wdq) {   // e4m3 forward (mmseg_conv3_fwd_fp8)
+    mmseg::note_kernel("conv3_brick6_kernel<BN32,F8>");
+    if (g.nmean) hipLaunchKernelGGL((conv3_brick6_kernel<true, 6, 0, false, true>), grid, block, 0, s, g, upb5, bpn5);
+    else hipLaunchKernelGGL((conv3_brick6_kernel<false, 6, 0, false, true>), grid, block, 0, s, g, upb5, bpn5);
+    return upb5;
+  }
   if (g.inpart) {   // samples a block does not touch keep zero partials
     hipMemsetAsync(g.inpart, 0, sizeof(float) * 2 * (size_t)(g.M / (g.D * g.H * g.W)) * bpn5 * g.Ncols, s);
     if (!g.bias && knob("MMSEG_BRICK6", 1) && knob("MMSEG_BRICK6_INP", 1)) {
@@ -4941,6 +5008,33 @@ int launch_wgrad_reduce(WReduceArgs g, void* stream) {
 
 }  // namespace
 
+// e4m3 B-operand image of a 3^3 conv for brick6 F8 ([KGp][Cpad][8] bytes, the bf16 image's geometry): one block
+// per output channel: s = 448 / max |w[co]| (1 for an all-zero row; 448 = e4m3fn's largest finite value), the
+// entries w[co][ci][tap] * s rounded to e4m3 (v_cvt_pk_fp8_f32: round to nearest even), wdq[co] = 1 / s.
+__global__ __launch_bounds__(256) void pack_conv3_fp8_kernel(const float* __restrict__ w, int Ci, int Cip, int Cpad,
+                                                             unsigned char* __restrict__ dst, float* __restrict__ wdq) {
+  const int co = blockIdx.x, tid = threadIdx.x;
+  const int n = Ci * 27;
+  const float* wr = w + (long long)co * n;
+  float m = 0.f;
+  for (int e = tid; e < n; e += 256) m = fmaxf(m, fabsf(wr[e]));
+  __shared__ float red[4];
+  m = fmaxf(m, __shfl_xor(m, 1, 64));
+#pragma unroll
+  for (int o = 2; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((tid & 63) == 0) red[tid >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float sc = m > 0.f ? 448.f / m : 1.f;
+  if (tid == 0) wdq[co] = 1.f / sc;
+  for (int e = tid; e < n; e += 256) {
+    const int ci = e / 27, tap = e - ci * 27;
+    const int kgi = tap * (Cip / 8) + ci / 8;
+    const int v = __builtin_amdgcn_cvt_pk_fp8_f32(wr[e] * sc, 0.f, 0, false);
+    dst[((long long)kgi * Cpad + co) * 8 + (ci & 7)] = (unsigned char)(v & 0xff);
+  }
+}
+
 // =================================================================== C ABI
 extern "C" {
 
@@ -5115,6 +5209,43 @@ int mmseg_conv3_fwd_norm(const void* a, int lda, const float* nmean, const float
   GemmArgs g{a, lda, wpacked, bias, out, ldo, nullptr, M, Ncols, Cpad, KG, cpg_shift, D, H, W, 1, KGp,
              knob("MMSEG_SWIZZLE", 1), nullptr, 0, nmean, nrstd};
   return launch_gemm<bf16_t, MODE_CONV3>(g, (hipStream_t)stream);
+}
+
+// Mixed bf16/fp8 forward (config c5): the brick6 shapes of a 3^3 conv with e4m3 operands and fp32 accumulation.
+int mmseg_conv3_fp8_ok(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo) {
+  if (!knob("MMSEG_FP8", 1)) return 0;
+  GemmArgs g{};
+  g.lda = lda; g.ldo = ldo; g.M = M; g.Ncols = Ncols; g.Cpad = Cpad; g.KG = KG; g.cpg_shift = cpg_shift;
+  g.D = D; g.H = H; g.W = W; g.ksplit = 1;
+  g.out = reinterpret_cast<void*>(static_cast<uintptr_t>(256));
+  return brick5_selected(g, 2) ? 1 : 0;
+}
+
+int mmseg_pack_conv3_fp8(const float* w, int Co, int Ci, int Cip, int KGp, int Cpad, void* dst, float* wdq,
+                         void* stream) {
+  MMSEG_REQUIRE(w && dst && wdq && Co > 0 && Co <= Cpad && Ci <= Cip && Cip % 8 == 0 && KGp * 8 >= 27 * Cip,
+                "pack_conv3_fp8: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  hipMemsetAsync(dst, 0, (size_t)KGp * Cpad * 8, s);   // K / column padding stays e4m3 zero
+  hipLaunchKernelGGL(pack_conv3_fp8_kernel, dim3(Co), dim3(256), 0, s, w, Ci, Cip, Cpad, (unsigned char*)dst, wdq);
+  return mmseg::check_launch("pack_conv3_fp8");
+}
+
+// out = conv3(A) with e4m3 operands (A: bf16 NDHWC, staged as e4m3; with nmean / nrstd: relu((a - mean) * rstd)
+// first, as mmseg_conv3_fwd_norm), bf16 output; w8 / wdq from mmseg_pack_conv3_fp8 (requires mmseg_conv3_fp8_ok).
+int mmseg_conv3_fwd_fp8(const void* a, int lda, const float* nmean, const float* nrstd, const void* w8,
+                        const float* wdq, const float* bias, void* out, int ldo, int M, int Ncols, int Cpad, int KG,
+                        int cpg_shift, int D, int H, int W, void* stream) {
+  MMSEG_REQUIRE(a && w8 && wdq && out && (nmean == nullptr) == (nrstd == nullptr) &&
+                    (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
+                    mmseg_conv3_fp8_ok(M, Ncols, Cpad, KG, cpg_shift, D, H, W, lda, ldo),
+                "conv3_fwd_fp8: unsupported shape (mmseg_conv3_fp8_ok)");
+  const int KGp = (KG + 3) & ~3;
+  GemmArgs g{a, lda, w8, bias, out, ldo, nullptr, M, Ncols, Cpad, KG, cpg_shift, D, H, W, 1, KGp,
+             knob("MMSEG_SWIZZLE", 1), nullptr, 0, nmean, nrstd};
+  g.wdq = wdq;
+  launch_brick5(g, (hipStream_t)stream, nullptr, false);
+  return mmseg::check_launch("conv3_fwd_fp8");
 }
 
 // Chunks per sample of the InstanceNorm-backward partials mmseg_conv3_dgrad_in writes for this CONV3 data-gradient

@@ -33,9 +33,10 @@ class SegEngine:
         params = list(self.module.parameters())
         if any(p.device != device for p in params):
             raise RuntimeError(f"model parameters are not on {device}; call model.to({device}) first")
-        if (self.rt is None or self.rt.device != device or self.rt.dtype != self.dtype
+        fp8 = bool(getattr(self.module, "fp8_convs", False))
+        if (self.rt is None or self.rt.device != device or self.rt.dtype != self.dtype or self.rt.fp8 != fp8
                 or self.flat is None or not self.flat.intact()):
-            self.rt = Runtime(device, self.dtype)
+            self.rt = Runtime(device, self.dtype, fp8)
             self.flat = FlatParams(params)
             if self.kind == "swin_unetr":
                 from .swin import SwinUNETRProgram

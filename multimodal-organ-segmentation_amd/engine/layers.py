@@ -176,6 +176,34 @@ class Conv3:
         # 32-channel chunks past them
         self.kreal_f = self.Ci if self.Cip > self.Ci else 0
         self.kreal_d = self.Co if self.Cop > self.Co else 0
+        self._f8 = None   # (e4m3 weight image, per-output-channel dequant) when the fp8 forward applies
+
+    def fp8_ok(self, x: Act, y: Act) -> bool:
+        """Mixed bf16/fp8: this conv's forward runs on e4m3 operands (Runtime.fp8 and the kernel takes the shape)."""
+        if not getattr(self.rt, "fp8", False) or self.pad_cols or self.Cip != self.Ci or self.ncols_f != self.Co:
+            return False
+        return bool(self.rt.lib.mmseg_conv3_fp8_ok(x.N * x.V, self.ncols_f, self.Cpad, self.KG, self.cpg_shift, x.D,
+                                                   x.H, x.W, x.ld, y.ld))
+
+    def _fp8_weights(self):
+        """e4m3 image of the CURRENT fp32 weights (re-packed every forward, like the bf16 images)."""
+        if self._f8 is None:
+            self._f8 = (torch.empty(self.KGp * self.Cpad * 8, dtype=torch.uint8, device=self.rt.device),
+                        torch.empty(self.Co, dtype=torch.float32, device=self.rt.device))
+        w8, dq = self._f8
+        self.rt.lib.mmseg_pack_conv3_fp8(ptr(self.conv.weight), self.Co, self.Ci, self.Cip, self.KGp, self.Cpad,
+                                         ptr(w8), ptr(dq), self.rt.stream)
+        return w8, dq
+
+    def fwd_fp8(self, x: Act, y: Act, norm: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
+        """fwd() / fwd_norm() on e4m3 operands (requires fp8_ok)."""
+        w8, dq = self._fp8_weights()
+        nm, nr = (ptr(norm[0]), ptr(norm[1])) if norm is not None else (None, None)
+        with TIMER.region("conv3_brick6_kernel<BN32,F8>[fp8]", flops=2.0 * x.N * x.V * self.Co * 27 * self.Ci,
+                          nbytes=_io_bytes(self.rt, x.N * x.V, self.Cip, self.Co, 27 * self.Cip * self.Co, 1)):
+            self.rt.lib.mmseg_conv3_fwd_fp8(x.ptr, x.ld, nm, nr, ptr(w8), ptr(dq), ptr(self.conv.bias), y.ptr, y.ld,
+                                            x.N * x.V, self.ncols_f, self.Cpad, self.KG, self.cpg_shift, x.D, x.H,
+                                            x.W, self.rt.stream)
 
     def descs(self):
         w = self.conv.weight
@@ -230,6 +258,9 @@ class Conv3:
                 self.rt.lib.mmseg_stem_fwd(x.ptr, x.ld, self.Ci, ptr(self.conv.weight), ptr(self.conv.bias), y.ptr,
                                            y.ld, x.N, x.D, x.H, x.W, self.Co, self.rt.code, self.rt.stream)
             return
+        if self.fp8_ok(x, y):
+            self.fwd_fp8(x, y)
+            return
         M = x.N * x.V
         nc = self.ncols_f
         ks = self.rt.lib.mmseg_conv3_splits(M, nc, self.Cpad, self.KG, self.cpg_shift, x.D, x.H, x.W, x.ld, y.ld,
@@ -254,6 +285,9 @@ class Conv3:
 
     def fwd_norm(self, x: Act, mean: torch.Tensor, rstd: torch.Tensor, y: Act):
         """fwd() of relu(InstanceNorm(x)) with x the pre-norm activation (requires norm_ok)."""
+        if self.fp8_ok(x, y):
+            self.fwd_fp8(x, y, norm=(mean, rstd))
+            return
         with TIMER.region(_gemm_name(self.rt, self.ncols_f, "conv3"), flops=2.0 * x.N * x.V * self.Co * 27 * self.Ci,
                           nbytes=_io_bytes(self.rt, x.N * x.V, self.Cip, self.Co, 27 * self.Cip * self.Co)):
             self.rt.lib.mmseg_conv3_fwd_norm(x.ptr, x.ld, ptr(mean), ptr(rstd), ptr(self.wf), ptr(self.conv.bias),

@@ -54,7 +54,7 @@ class Act:
 class Runtime:
     """Per-model device context: dtype, workspace arena, flat param/grad arenas."""
 
-    def __init__(self, device: torch.device, dtype: torch.dtype):
+    def __init__(self, device: torch.device, dtype: torch.dtype, fp8: bool = False):
         if device.type != "cuda":
             raise RuntimeError(
                 "the MI355X segmentation engine runs on a ROCm device only (got %s); "
@@ -64,6 +64,11 @@ class Runtime:
         self.device = device
         self.dtype = dtype
         self.code = DTYPE_CODE[dtype]
+        # mixed bf16/fp8 (hardware.fp8, config c5): the forward 3^3 convs that mmseg_conv3_fp8_ok accepts run with
+        # e4m3 operands (layers.Conv3); everything else keeps the bf16 storage
+        if fp8 and dtype != torch.bfloat16:
+            raise ValueError("hardware.fp8 needs hardware.engine_dtype: bfloat16 (the rest of the step stays bf16)")
+        self.fp8 = fp8
         self.lib = lib()
         self._ws: Dict[int, torch.Tensor] = {}      # one scratch arena per HIP stream
 

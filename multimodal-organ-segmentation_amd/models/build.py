@@ -12,6 +12,10 @@ Differences, all additive:
     convolutions), the reference's own module forward, for A/B runs on the
     GPU.  It is chosen explicitly, never as a fallback, and needs a ROCm device
     like the HIP backend.
+  * `hardware.fp8: true` (with engine_dtype bfloat16; config c5's "mixed
+    bf16/fp8") runs the forward 3^3 convolutions the fp8 kernel takes (one
+    32-channel input chunk: the 96^3 conv2 layers) with OCP e4m3 operands and
+    fp32 accumulation; backward, norms, fusion and loss stay bf16 / fp32.
 """
 from __future__ import annotations
 
@@ -85,6 +89,10 @@ def build_model(config: Dict[str, Any]) -> nn.Module:
     backbone = MODEL_REGISTRY[name](config)
     backbone.engine_dtype = engine_dtype_from_config(config)
     backbone.kernels = kernels
+    # hardware.fp8 (config c5 "mixed bf16/fp8"): e4m3 forward convolutions where the kernels take them
+    backbone.fp8_convs = bool(config.get("hardware", {}).get("fp8", False))
+    if backbone.fp8_convs and (kernels != "hip" or backbone.engine_dtype != torch.bfloat16):
+        raise ValueError("hardware.fp8 needs hardware.kernels: hip and engine_dtype: bfloat16")
     model = MultiModalSegmentationModel(backbone, config)
     if config.get("hardware", {}).get("device", "cuda") == "cuda" and torch.cuda.is_available():
         model = model.cuda()

@@ -140,3 +140,16 @@ def test_torch_backend_amp_step_runs(dev):
         losses = [tr.train_step({"image": xs[1], "label": ys[1]}, i) for i in range(3)]
         assert all(np.isfinite(losses))
         assert abs(losses[0] - float(g["loss"])) < 5e-2
+
+
+def test_fp8_config_checks():
+    """hardware.fp8 (config c5's mixed bf16/fp8) needs the HIP backend with bf16 storage."""
+    cfg = make_config("dual_encoder", ["CT", "PET", "MRI"], 4, [32, 64], loss="tversky", dtype="float32")
+    cfg["hardware"]["fp8"] = True
+    cfg["hardware"]["device"] = "cpu"
+    with pytest.raises(ValueError, match="fp8"):
+        build_model(cfg)
+    cfg["hardware"]["engine_dtype"] = "bfloat16"
+    cfg["hardware"]["kernels"] = "torch"
+    with pytest.raises(ValueError, match="fp8"):
+        build_model(cfg)
