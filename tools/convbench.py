@@ -5,7 +5,8 @@ Env knobs (MMSEG_*) select kernel variants; prints one JSON line per (shape, op)
 the kernel the library launched, us per launch and TFLOP/s (2*27*Cin*Cout per voxel).
 Ops: fwd, fwds (forward with the fused InstanceNorm partials, as ConvBlock3D runs it), fwdn (forward of
 relu(IN(x)) with the norm applied on staging: Block.defer1's conv2), dgrad, dgradin (data gradient that also sums
-the InstanceNorm-backward partials of its output: Block.bwd's conv2 at 96^3), wgrad.
+the InstanceNorm-backward partials of its output: Block.bwd's conv2 at 96^3), wgrad, wgradn (weight gradient with
+the deferred norm of x).
 --probe: load libmmseg_hip_probe.so (make -C csrc probe) and print the block timeline of one launch per op
 (per-CU residency, block lifetimes, per-phase cycles of block 0's waves; see conv_gemm.hip PROBE_*).
 """
@@ -92,6 +93,14 @@ def main():
                 L.mmseg_conv_gemm(y.ptr, y.ld, layer.wd.data_ptr(), None, dx.ptr, dx.ld,
                                   ws.data_ptr() if ws is not None else None, 0, M, Ci, layer.Cpad_d, layer.KGd,
                                   layer.dshift, D, H, W, ks, code, s)
+            elif op == "wgradn":   # deferred-norm weight gradient (Block.defer1's conv2 backward)
+                V = N * D * H * W
+                wsf = L.mmseg_conv3_wgrad_ws_floats(V, Co, layer.Cip, Ci, layer.cpg_shift, D, H, W, y.ld, x.ld, code)
+                ws = rt.ws(wsf) if wsf > 0 else None
+                L.mmseg_conv3_wgrad_norm(y.ptr, y.ld, x.ptr, x.ld, mean.data_ptr(), rstd.data_ptr(),
+                                         flat.grad(conv.weight).data_ptr(), flat.grad(conv.bias).data_ptr(), Co,
+                                         layer.Cip, Ci, layer.cpg_shift, V, D, H, W,
+                                         ws.data_ptr() if ws is not None else None, wsf, 0, code, s)
             else:
                 V = N * D * H * W
                 wsf = L.mmseg_conv3_wgrad_ws_floats(V, Co, layer.Cip, Ci, layer.cpg_shift, D, H, W, y.ld, x.ld, code)
