@@ -8,4 +8,5 @@ run() { n=$1; shift; timeout -k 10 600 python3 $R/bench.py --no-cpu-baseline --t
 run c3 --steps 20 --warmup 5
 run c2 --model unet --steps 20 --warmup 5
 run c5 --modalities CT,PET,MRI --loss tversky --steps 20 --warmup 5
+run c5fp8 --modalities CT,PET,MRI --loss tversky --fp8 --steps 20 --warmup 5
 run c4 --model swin_unetr --size 128 --batch 1 --steps 5 --warmup 2
