@@ -683,6 +683,19 @@ __device__ __forceinline__ bool head_norm_stats(const float* nmean, const float*
 
 constexpr int HU = 4;   // 16-voxel tiles per wave step in the fused head + loss kernels
 
+// The wave's step loop over [vb, v1) in strides of `step`: fetch(regs, labels, vb) issues one step's loads,
+// body(regs, labels, vb) consumes them.  (Issuing step k + 1's loads before step k's body, two register sets,
+// measured slower: statistics pass 83 -> 94 us at 96^3 B=2, the backward spilled.)
+template <typename T, int G, typename F, typename B>
+__device__ __forceinline__ void head_steps(F& fetch, B& body, long long vb, long long v1, long long step) {
+  for (; vb < v1; vb += step) {
+    HeadLoad<T, G> l[HU];
+    int y[HU];
+    fetch(l, y, vb);
+    body(l, y, vb);
+  }
+}
+
 template <int G>
 __device__ __forceinline__ f32x4 head_logits_t(const float* wA, const float* xs, const float* bz) {
   f32x4 acc = {bz[0], bz[1], bz[2], bz[3]};
@@ -723,15 +736,15 @@ __global__ __launch_bounds__(256) void head_loss_stats_kernel(const T* __restric
   const long long base = (long long)n * V;
   // HU tiles of 16 voxels per wave step, all their loads in flight before the first is used (one 16-B load
   // per lane and tile is too little memory parallelism on its own)
-  for (long long vb = v0 + wave * 16 * HU; vb < v1; vb += 64 * HU) {
-  HeadLoad<T, G> lds_[HU];
-  int ys_[HU];
+  auto fetch = [&](HeadLoad<T, G>(&lds_)[HU], int(&ys_)[HU], long long vb) {
 #pragma unroll
-  for (int u = 0; u < HU; ++u) {
-    const long long v = vb + 16 * u + v16;
-    lds_[u].load(x, ldx, base + v, v < v1, g);
-    ys_[u] = v < v1 ? (int)labels[base + v] : 0;
-  }
+    for (int u = 0; u < HU; ++u) {
+      const long long v = vb + 16 * u + v16;
+      lds_[u].load(x, ldx, base + v, v < v1, g);
+      ys_[u] = v < v1 ? (int)labels[base + v] : 0;
+    }
+  };
+  auto body = [&](HeadLoad<T, G>(&lds_)[HU], const int(&ys_)[HU], long long vb) {
   if (donorm) {
 #pragma unroll
     for (int u = 0; u < HU; ++u) lds_[u].norm(nmu, nrs);
@@ -800,7 +813,8 @@ __global__ __launch_bounds__(256) void head_loss_stats_kernel(const T* __restric
       cden += 1.f;   // focal: ignored (-100) voxel, counted by the mean
     }
   }
-  }
+  };
+  head_steps<T, G>(fetch, body, v0 + wave * 16 * HU, v1, 64 * HU);
   // sums over the 16 voxel lanes of each group (fixed tree); lane 16g then holds classes 4g..4g+3
 #pragma unroll
   for (int o = 1; o < 16; o <<= 1)
@@ -903,15 +917,15 @@ __global__ __launch_bounds__(256, (NC <= 6 && sizeof(T) == 2) ? 2 : 1) void head
   const long long v0 = (long long)chunk * vpc;
   const long long v1 = v0 + vpc < V ? v0 + vpc : V;
   const long long base = (long long)n * V;
-  for (long long vb = v0 + wave * 16 * HU; vb < v1; vb += 64 * HU) {
-  HeadLoad<T, G> lds_[HU];
-  int ys_[HU];
+  auto fetch = [&](HeadLoad<T, G>(&lds_)[HU], int(&ys_)[HU], long long vb) {
 #pragma unroll
-  for (int u = 0; u < HU; ++u) {
-    const long long v = vb + 16 * u + v16;
-    lds_[u].load(x, ldx, base + v, v < v1, g);
-    ys_[u] = v < v1 ? (int)labels[base + v] : 0;
-  }
+    for (int u = 0; u < HU; ++u) {
+      const long long v = vb + 16 * u + v16;
+      lds_[u].load(x, ldx, base + v, v < v1, g);
+      ys_[u] = v < v1 ? (int)labels[base + v] : 0;
+    }
+  };
+  auto body = [&](HeadLoad<T, G>(&lds_)[HU], const int(&ys_)[HU], long long vb) {
   if (donorm) {
 #pragma unroll
     for (int u = 0; u < HU; ++u) lds_[u].norm(nmu, nrs);
@@ -1028,7 +1042,8 @@ __global__ __launch_bounds__(256, (NC <= 6 && sizeof(T) == 2) ? 2 : 1) void head
       for (int j = 0; j < 8; ++j) acc[c][j] = fmaf(dc, xs[j], acc[c][j]);
     }
   }
-  }
+  };
+  head_steps<T, G>(fetch, body, v0 + wave * 16 * HU, v1, 64 * HU);
   // fixed-order sums over the 16 voxel lanes of each group, then the 4 waves in order
 #pragma unroll
   for (int o = 1; o < 16; o <<= 1) {
@@ -1233,14 +1248,32 @@ int grid_for(long long total) {
 
 int loss_vpc() {
   static const int v = [] {
+    // 1,728 voxels: 1,024 blocks at 96^3 B=2, one full round of the fused statistics kernel (118 VGPRs: 4 blocks
+    // per CU); 2,048 left 864 blocks, 3-4 per CU (83 -> 75 us, tools/headbench.py)
     const char* e = getenv("MMSEG_LOSS_VPC");
-    return e ? atoi(e) : 2048;
+    return e ? atoi(e) : 1728;
   }();
   return v;
 }
 
 int loss_chunks(long long V, long long* vpc) {
   const int want = loss_vpc();
+  long long nch = (V + want - 1) / want;
+  if (nch > 4096) nch = 4096;
+  if (nch < 1) nch = 1;
+  *vpc = (V + nch - 1) / nch;
+  return (int)((V + *vpc - 1) / *vpc);
+}
+
+// Voxel chunks of the fused head + loss backward, its own grid: 249 VGPRs hold it at two waves per SIMD, so
+// 3,456 voxels (512 blocks at 96^3 B=2) are one full round of 256 CUs x 2 blocks; the statistics pass's 1,024 /
+// 864 blocks took two (114 / 129 -> 110 us, tools/headbench.py).  MMSEG_HEAD_BWD_VPC, 0 = the statistics chunking.
+int head_bwd_chunks(long long V, long long* vpc) {
+  static const int want = [] {
+    const char* e = getenv("MMSEG_HEAD_BWD_VPC");
+    return e ? atoi(e) : 3456;
+  }();
+  if (want <= 0) return loss_chunks(V, vpc);
   long long nch = (V + want - 1) / want;
   if (nch > 4096) nch = 4096;
   if (nch < 1) nch = 1;
@@ -1419,7 +1452,7 @@ int mmseg_head_loss_ok(int C, int Cin, int ldx, int dtype) {
 
 long long mmseg_head_loss_wpart_floats(int C, int Cin, int N, long long V) {
   long long vpc;
-  const int nch = loss_chunks(V, &vpc);
+  const int nch = head_bwd_chunks(V, &vpc);
   return (long long)N * nch * (C * Cin + C);
 }
 
@@ -1476,7 +1509,7 @@ int mmseg_head_loss_bwd(const void* x, int ldx, int Cin, const float* nmean, con
 int mmseg_head_loss_in_chunks(int C, int Cin, long long V) {
   if (Cin != 32 || C < 2 || C > 8) return 0;
   long long vpc;
-  return loss_chunks(V, &vpc);
+  return head_bwd_chunks(V, &vpc);
 }
 
 int mmseg_head_loss_bwd_in(const void* x, int ldx, int Cin, const float* nmean, const float* nrstd, const float* W,
@@ -1493,9 +1526,10 @@ int mmseg_head_loss_bwd_in(const void* x, int ldx, int Cin, const float* nmean, 
   MMSEG_REQUIRE(!nmean || dx != x, "head_loss_bwd: with the deferred norm x is the pre-norm input the "
                 "InstanceNorm backward still reads; dx must not alias it");
   LossCfg cfg{type, dice_w, ce_w, smooth, alpha, beta, include_bg, class_w};
-  long long vpc;
-  const int nch = loss_chunks(V, &vpc);
-  const float* coef = ws + (long long)N * nch * (3 * C + 3);
+  long long svpc, vpc;
+  const int snch = loss_chunks(V, &svpc);   // the statistics pass's layout of ws
+  const int nch = head_bwd_chunks(V, &vpc);
+  const float* coef = ws + (long long)N * snch * (3 * C + 3);
   hipStream_t s = (hipStream_t)stream;
   head_loss_dispatch(C, Cin, dtype, label_bytes, [&](auto tag, auto g_c, auto nc_c, auto lt) {
     using T = decltype(tag);

@@ -1,7 +1,10 @@
 """Head + loss microbenchmark at the bench's shape (96^3, B=2, 32 -> 6, DiceCE, bf16): the unfused sequence
 (head_fwd, loss stats + finalize, loss_bwd, head_bwd) against the fused head + loss kernels, HIP-event timed.
 
-    python tools/headbench.py [--iters 20]
+    python tools/headbench.py [--iters 20] [--step-only]
+
+The step form (deferred InstanceNorm input, InstanceNorm-backward partials) is timed too; its loss / checksums
+let A/B runs of the kernel variants (MMSEG_HEAD_PF, MMSEG_LOSS_VPC, MMSEG_HEAD_BWD_VPC) be compared.
 """
 import argparse
 import json
@@ -18,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--size", type=int, default=96)
+    ap.add_argument("--step-only", action="store_true", help="only the training step's form (deferred norm + IN partials)")
     args = ap.parse_args()
     import mmseg_amd  # noqa: F401
     from mmseg_amd._lib import lib, ptr
@@ -59,6 +63,20 @@ def main():
         L.mmseg_head_loss_bwd(ptr(x), Cin, Cin, None, None, ptr(W), ptr(b), None, C, N, V, ptr(y), 8, *args8, ptr(g), 1.0,
                               ptr(ws), ptr(dx), Cin, ptr(gW), ptr(gb), ptr(wpart), 0, 1, s)
 
+    # the training step's form: deferred InstanceNorm + ReLU of the input on load, InstanceNorm-backward partials
+    nmean = (torch.randn(N * Cin, device=dev) * 0.1).contiguous()
+    nrstd = (torch.rand(N * Cin, device=dev) + 0.5).contiguous()
+    inpart = torch.empty(N * max(L.mmseg_head_loss_in_chunks(C, Cin, V), 1) * Cin * 2, device=dev)
+
+    def step_fwd():
+        L.mmseg_head_loss_fwd(ptr(x), Cin, Cin, ptr(nmean), ptr(nrstd), ptr(W), ptr(b), None, C, N, V, ptr(y), 8,
+                              *args8, ptr(loss), ptr(ws), 1, s)
+
+    def step_bwd():
+        L.mmseg_head_loss_bwd_in(ptr(x), Cin, Cin, ptr(nmean), ptr(nrstd), ptr(W), ptr(b), None, C, N, V, ptr(y), 8,
+                                 *args8, ptr(g), 1.0, ptr(ws), ptr(dx), Cin, ptr(gW), ptr(gb), ptr(wpart), ptr(inpart),
+                                 0, 1, s)
+
     def timeit(fn):
         for _ in range(3):
             fn()
@@ -79,8 +97,16 @@ def main():
     torch.cuda.synchronize()
     err = {"loss": abs(loss.item() - ref[0]), "dx": ((dx.float() - ref[1]).abs().max() / ref[1].abs().max()).item(),
            "gW": ((gW - ref[2]).abs().max() / ref[2].abs().max()).item()}
-    res = {"unfused_fwd_us": timeit(unfused_fwd), "unfused_bwd_us": timeit(unfused_bwd),
-           "fused_fwd_us": timeit(fused_fwd), "fused_bwd_us": timeit(fused_bwd), "err": err}
+    res = {"env": {k: v for k, v in os.environ.items() if k.startswith("MMSEG_")}}
+    if not args.step_only:
+        res.update({"unfused_fwd_us": timeit(unfused_fwd), "unfused_bwd_us": timeit(unfused_bwd),
+                    "fused_fwd_us": timeit(fused_fwd), "fused_bwd_us": timeit(fused_bwd), "err": err})
+    step_fwd()
+    step_bwd()
+    torch.cuda.synchronize()
+    res.update({"step_fwd_us": timeit(step_fwd), "step_bwd_us": timeit(step_bwd), "step_loss": loss.item(),
+                "step_dx_sum": dx.float().sum().item(), "step_gW_sum": gW.sum().item(),
+                "step_in_sum": inpart.sum().item()})
     print(json.dumps({k: (round(v, 1) if isinstance(v, float) else v) for k, v in res.items()}))
 
 
