@@ -52,3 +52,18 @@ def test_value_returning_entry_points_do_not_raise():
     assert L.mmseg_wgrad_splits_conv3(2 * 96 ** 3, 512, 32, 2, 96, 96, 96, 32, 32, 1) >= 1
     assert L.mmseg_conv3_splits(2 * 12 ** 3, 256, 256, 27 * 32, 5, 12, 12, 12, 256, 256, 1) >= 1
     assert L.mmseg_pack_desc_bytes() == 56
+
+
+def test_head_loss_size_queries_agree():
+    """The fused head + loss backward has its own voxel chunking (whole rounds of its 2-blocks-per-CU grid); the
+    weight-gradient partials it writes and the InstanceNorm partials it hands to mmseg_instnorm_bwd_part must be
+    counted over the same chunks, and the loss workspace over the statistics pass's."""
+    L = _lib.lib()
+    for N, V in ((2, 96 ** 3), (1, 64 ** 3), (2, 32 ** 3), (1, 7)):
+        for C in (3, 6, 7):
+            nch = L.mmseg_head_loss_in_chunks(C, 32, V)
+            assert nch >= 1
+            assert L.mmseg_head_loss_wpart_floats(C, 32, N, V) == N * nch * (C * 32 + C)
+            assert L.mmseg_loss_ws_floats(N, C, V) >= N * (3 * C + 3) + 2 * N * C + 2
+    assert L.mmseg_head_loss_in_chunks(6, 32, 96 ** 3) == 256   # 3,456 voxels per block at 96^3
+    assert L.mmseg_head_loss_in_chunks(6, 16, 96 ** 3) == 0     # partials only for Cin = 32
