@@ -1184,6 +1184,54 @@ __global__ void fuse_fwd(FuseSrc s, T* __restrict__ out, int ldo, long long V, i
   }
 }
 
+// fuse_fwd<NORM> with the source count MM known at compile time: the MM feature loads of an item are issued
+// together (the runtime-M loop waited a memory latency per source), and since the grid stride is a multiple of
+// C / 8 a thread's channel group never changes, so the sources' statistics are loaded once per sample instead
+// of once per item.  Same operations in the same order as fuse_fwd<NORM>: bitwise equal.
+template <typename T, int MM>
+__global__ void fuse_norm_fwd_m(FuseSrc s, T* __restrict__ out, int ldo, long long V, int N, int C) {
+  const int C8 = C >> 3;
+  const int total = N * (int)V * C8;   // < 2^31 (host check): 32-bit index math
+  const int stride = gridDim.x * blockDim.x;   // a multiple of C8 (host check)
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int cg = i % C8;
+  int cur_n = -1;
+  float mu[MM][8], rs[MM][8];
+  for (; i < total; i += stride) {
+    const long long nv = i / C8;
+    const int n = (int)(nv / (int)V);
+    V8<T> a[MM];
+#pragma unroll
+    for (int m = 0; m < MM; ++m) a[m].load(reinterpret_cast<const T*>(s.p[m]) + nv * s.ld[m] + cg * 8);
+    if (n != cur_n) {
+#pragma unroll
+      for (int m = 0; m < MM; ++m) {
+        load8f(s.mean[m] + n * C + cg * 8, mu[m]);
+        load8f(s.rstd[m] + n * C + cg * 8, rs[m]);
+      }
+      cur_n = n;
+    }
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int m = 0; m < MM; ++m) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float h = (a[m].get(j) - mu[m][j]) * rs[m][j];
+        a[m].set(j, h > 0.f ? h : 0.f);
+      }
+      const float w = s.wts ? s.wts[n * s.M + m] : 1.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = s.wts ? fmaf(a[m].get(j), w, acc[j]) : acc[j] + a[m].get(j);
+    }
+    V8<T> o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o.set(j, s.wts ? acc[j] : acc[j] * s.wconst);
+    o.store(out + nv * ldo + cg * 8);
+  }
+}
+
 // dots[n][m] partial: sum_{v,c} dfused[n,v,c] * src_m[n,v,c]
 template <typename T>
 __global__ void fuse_dot_partial(FuseSrc s, const T* __restrict__ dfused, int ldd, long long V, int C, long long vpc,
@@ -1670,10 +1718,19 @@ int mmseg_fuse_norm_fwd(const void* const* srcs, const int* lds, const float* co
   s.wts = wts;
   hipStream_t st = (hipStream_t)stream;
   const int grid = grid_for((long long)N * V * (C / 8));
-  if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL((fuse_fwd<bf16_t, true>), dim3(grid), dim3(256), 0, st, s, (bf16_t*)out, ldo, V, N, C);
-  else
-    hipLaunchKernelGGL((fuse_fwd<float, true>), dim3(grid), dim3(256), 0, st, s, (float*)out, ldo, V, N, C);
+  const char* e = getenv("MMSEG_FUSE_M");   // 0: the runtime-M kernel (A/B); M = 4 spilled, stays runtime-M
+  const bool cm = (!e || atoi(e) != 0) && M >= 2 && ((long long)grid * 256) % (C / 8) == 0;
+  auto run = [&](auto tag) {
+    using T = decltype(tag);
+    if (cm && M == 2)
+      hipLaunchKernelGGL((fuse_norm_fwd_m<T, 2>), dim3(grid), dim3(256), 0, st, s, (T*)out, ldo, V, N, C);
+    else if (cm && M == 3)
+      hipLaunchKernelGGL((fuse_norm_fwd_m<T, 3>), dim3(grid), dim3(256), 0, st, s, (T*)out, ldo, V, N, C);
+    else
+      hipLaunchKernelGGL((fuse_fwd<T, true>), dim3(grid), dim3(256), 0, st, s, (T*)out, ldo, V, N, C);
+  };
+  if (dtype == MMSEG_BF16) run(bf16_t{});
+  else run(float{});
   return mmseg::check_launch("fuse_norm_fwd");
 }
 
