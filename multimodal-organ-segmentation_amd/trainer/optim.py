@@ -47,6 +47,16 @@ class FlatAdamW(torch.optim.AdamW):
                 self.state[p]["step"] = t
         return t
 
+    def state_dict(self):
+        """torch's format with one 'step' tensor PER PARAMETER.  _group_step shares a single counter across a
+        group; torch.optim.AdamW (the reference's optimizer, or hardware.kernels: torch resuming an engine
+        checkpoint) would otherwise load that sharing and advance the shared tensor once per parameter per
+        step, breaking the bias corrections (reference trainer.py:115-117, build.py:170-180)."""
+        sd = super().state_dict()
+        sd["state"] = {k: ({**st, "step": st["step"].clone()} if torch.is_tensor(st.get("step")) else st)
+                       for k, st in sd["state"].items()}
+        return sd
+
     def undo_step_count(self) -> None:
         """Roll the step counters back by one: the kernel skipped an update (guard), so the bias corrections
         of the next step must not advance."""

@@ -74,8 +74,10 @@ class StepGraphs:
         opt = tr.optimizer
         if type(opt) is not FlatAdamW or len(opt.param_groups) != 1:
             return False
-        if "step" in opt.__dict__ or "zero_grad" in opt.__dict__:
+        wrapped = opt.__dict__.get("step")
+        if (wrapped is not None and not getattr(wrapped, "_wrapped_by_lr_sched", False)) or "zero_grad" in opt.__dict__:
             return False   # a caller wrapped the optimizer's step: a replayed step would not call it
+        # (an LR scheduler's wrapper only records that step() ran -- run() sets that flag itself)
         grp = opt.param_groups[0]
         if grp.get("amsgrad") or grp.get("maximize"):
             return False
@@ -191,5 +193,8 @@ class StepGraphs:
         e = self._entry(images, labels)
         self._push_hyper()
         e["graph"].replay()
+        # what torch's LRScheduler step wrapper records (lr_scheduler.py patch_track_step_called): the optimizer
+        # stepped before the scheduler does, so scheduler.step() raises no "called before optimizer.step()" warning
+        self.tr.optimizer.__dict__["_opt_called"] = True
         self.tr.criterion.__dict__["_last_ws"] = e["ws"]
         return e["loss"], e["ws"][-1:]

@@ -76,6 +76,7 @@ class Trainer:
         self.best_metric = 0.0
         self.history = {"train_loss": [], "val_loss": [], "val_dice": []}
         self._buckets = None
+        self._deferred_bad = None       # device count of sync=False steps whose labels were out of range
         self._one = torch.ones((), dtype=torch.float32, device=self.device)
         from .step_graph import StepGraphs
         self._graphs = StepGraphs(self)
@@ -206,6 +207,7 @@ class Trainer:
                 labels = labels.long()
             out, guard = self._graphs.run(images.contiguous(), labels.contiguous())
             if not sync:
+                self._defer_guard(guard)
                 return out.clone()
             return self._after_step(out.item(), guard, boundary=True, guarded=True)
         loss = self._fused_loss(images, labels)
@@ -237,8 +239,35 @@ class Trainer:
         if self.accumulation_steps != 1:
             out = out * self.accumulation_steps
         if not sync:
+            if guarded:
+                self._defer_guard(guard)
             return out
         return self._after_step(out.item(), guard, boundary, guarded)
+
+    def _defer_guard(self, guard: Optional[torch.Tensor]) -> None:
+        """sync=False (bench.py's timed loop, anything that batches its host syncs): no host read per step.  The
+        AdamW kernel has already skipped the update of a step whose labels were out of range (the guard); such
+        steps are counted on the device and check_deferred() -- called by the next synchronous train_step and by
+        _validate -- rolls their step counts back and raises, as the synchronous step would have at once.  Steps
+        that ran between the bad one and the check used the advanced step count in their bias corrections."""
+        if guard is None:
+            return
+        bad = guard.reshape(()).sign()
+        self._deferred_bad = bad if self._deferred_bad is None else self._deferred_bad.add_(bad)
+
+    def check_deferred(self) -> None:
+        if self._deferred_bad is None:
+            return
+        # under DP each step's guard was summed over the ranks by the first gradient bucket, so every rank
+        # counts the same steps and raises together
+        nbad, self._deferred_bad = int(self._deferred_bad.item()), None
+        if nbad:
+            for _ in range(nbad):
+                self.optimizer.undo_step_count()
+            self.optimizer.zero_grad()
+            raise RuntimeError(f"{nbad} earlier training step(s) had target voxels with a class index outside "
+                               "[0, num_classes) (the reference raises in F.one_hot / cross_entropy on such "
+                               "labels); their updates were skipped")
 
     def _torch_step(self, images, labels, boundary: bool, sync: bool):
         """The reference's per-batch body (trainer.py:236-258) on the torch-op backend."""
@@ -268,6 +297,7 @@ class Trainer:
 
     def _after_step(self, lv: float, guard, boundary: bool, guarded: bool) -> float:
         """Host side of a synchronous step: raise (on every rank) when the step's labels were out of range."""
+        self.check_deferred()
         if guard is not None and (lv != lv or self.world > 1):
             if self.world > 1 and (not boundary or self._buckets is None):
                 ddp.allreduce_sum_(guard)      # no bucket carried it on this micro-step
@@ -292,6 +322,7 @@ class Trainer:
         return total / n
 
     def _validate(self) -> Tuple[float, Dict[str, float]]:
+        self.check_deferred()
         self.model.eval()
         dm = DiceMetric(num_classes=self.config["model"]["out_channels"], device=self.device)
         total = torch.zeros((), dtype=torch.float64, device=self.device)

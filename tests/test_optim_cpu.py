@@ -1,0 +1,82 @@
+"""Host-side logic of the optimizer and the captured step that needs no GPU.
+
+* FlatAdamW keeps ONE step counter per parameter group (trainer/optim.py _group_step), but its state_dict must
+  hold one 'step' tensor per parameter, as torch.optim.AdamW writes it (reference trainer.py:115-117, checkpoint
+  format build.py:170-180): torch.optim.AdamW loading an engine checkpoint then advances every parameter's step
+  by exactly one per optimizer step.
+* StepGraphs.usable accepts an optimizer whose step() an LR scheduler wrapped (every shipped config uses the
+  cosine scheduler) and still refuses any other wrapper."""
+import types
+
+import torch
+
+import mmseg_amd  # noqa: F401
+from mmseg_amd.trainer.optim import FlatAdamW
+from mmseg_amd.trainer.step_graph import StepGraphs
+
+
+def _params(n=3):
+    g = torch.Generator().manual_seed(0)
+    return [torch.nn.Parameter(torch.randn(4, 5, generator=g)) for _ in range(n)]
+
+
+def test_flat_adamw_state_dict_has_per_parameter_steps():
+    ps = _params()
+    opt = FlatAdamW(ps, lr=1e-3)
+    st = opt._group_step(opt.param_groups[0])
+    st.fill_(7.0)
+    for p in ps:                       # what the kernel path leaves in the state besides the shared counter
+        opt.state[p]["exp_avg"] = torch.zeros_like(p)
+        opt.state[p]["exp_avg_sq"] = torch.zeros_like(p)
+    sd = opt.state_dict()
+    steps = [sd["state"][i]["step"] for i in range(len(ps))]
+    assert all(float(s) == 7.0 for s in steps)
+    assert len({id(s) for s in steps}) == len(ps), "state_dict shares one step tensor across parameters"
+    # the optimizer's own counter is still shared (and untouched by state_dict)
+    assert all(opt.state[p]["step"] is st for p in ps)
+
+    ref_ps = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    ref = torch.optim.AdamW(ref_ps, lr=1e-3)
+    ref.load_state_dict(sd)
+    for p in ref_ps:
+        p.grad = torch.ones_like(p)
+    ref.step()
+    assert [float(ref.state[p]["step"]) for p in ref_ps] == [8.0] * len(ps)
+    # and our counter did not move through the loaded copy
+    assert float(st) == 7.0
+
+
+def test_flat_adamw_round_trip_through_its_own_state_dict():
+    ps = _params()
+    opt = FlatAdamW(ps, lr=1e-3)
+    opt._group_step(opt.param_groups[0]).fill_(3.0)
+    sd = opt.state_dict()
+    opt2 = FlatAdamW([torch.nn.Parameter(p.detach().clone()) for p in ps], lr=1e-3)
+    opt2.load_state_dict(sd)
+    t = opt2._group_step(opt2.param_groups[0])      # separate loaded tensors are merged into one counter
+    assert float(t) == 3.0 and all(opt2.state[p]["step"] is t for p in opt2.param_groups[0]["params"])
+
+
+def _fake_trainer(opt):
+    model = types.SimpleNamespace(training=True, backbone=types.SimpleNamespace(dropout_p=0.0))
+    return types.SimpleNamespace(config={"hardware": {}}, world=1, accumulation_steps=1, optimizer=opt,
+                                 model=model)
+
+
+def _fake_input(dtype):
+    return types.SimpleNamespace(device=types.SimpleNamespace(type="cuda"), dtype=dtype, is_contiguous=lambda: True)
+
+
+def test_step_graph_accepts_lr_scheduler_wrapper(monkeypatch):
+    monkeypatch.delenv("MMSEG_STEP_GRAPH", raising=False)
+    opt = FlatAdamW(_params(), lr=1e-3)
+    tr = _fake_trainer(opt)
+    sg = StepGraphs.__new__(StepGraphs)          # no device buffers: only the eligibility logic
+    sg._tr = lambda: tr
+    x, y = _fake_input(torch.float32), _fake_input(torch.int64)
+    assert sg.usable(x, y)
+    torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=4)
+    assert getattr(opt.step, "_wrapped_by_lr_sched", False)
+    assert sg.usable(x, y), "the cosine scheduler's step wrapper must not disable the captured step"
+    opt.step = lambda *a, **k: None              # any other wrapper: a replay would not call it
+    assert not sg.usable(x, y)

@@ -35,7 +35,7 @@ def _batches(dev, n, S, M, C, seed=3):
              "label": torch.randint(0, C, (2, S, S, S), generator=g).to(dev)} for _ in range(n)]
 
 
-def _run(cfg, batches, steps, graph, monkeypatch, sync=True):
+def _run(cfg, batches, steps, graph, monkeypatch, sync=True, sched_every=0):
     monkeypatch.setenv("MMSEG_STEP_GRAPH", "1" if graph else "0")
     torch.manual_seed(0)
     m = build_model(cfg)
@@ -44,6 +44,8 @@ def _run(cfg, batches, steps, graph, monkeypatch, sync=True):
     for i in range(steps):
         lv = tr.train_step(batches[i % len(batches)], i, sync=sync)
         losses.append(lv if sync else lv.item())
+        if sched_every and (i + 1) % sched_every == 0:
+            tr.scheduler.step()
     torch.cuda.synchronize()
     params = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).clone()
     mv = [t.clone() for t in tr.optimizer._flat[0]]
@@ -62,6 +64,27 @@ def test_step_graph_bitwise_equal_to_eager(dev, model, dtype, monkeypatch):
     assert torch.equal(p0, p1)
     assert all(torch.equal(a, b) for a, b in zip(mv0, mv1))
     assert int(tr.optimizer.state[next(tr.model.parameters())]["step"]) == 6
+
+
+def test_step_graph_with_cosine_scheduler(dev, monkeypatch):
+    """The shipped configs use a cosine LR scheduler, which wraps optimizer.step (torch lr_scheduler.py
+    patch_track_step_called): the captured step must still engage, follow the scheduler's lr (a device
+    hyper-parameter refreshed before each replay) and stay bitwise equal to the eager step."""
+    cfg = _cfg("unet", 3, [8, 16, 32, 64, 128], "float32")
+    cfg["training"]["epochs"] = 4
+    cfg["training"]["scheduler"] = {"name": "cosine", "warmup_epochs": 0, "min_lr": 1e-6}
+    batches = _batches(dev, 2, 32, 2, 3, seed=5)
+    import warnings
+    with warnings.catch_warnings():
+        warnings.filterwarnings("error", message=".*lr_scheduler.step.*before.*optimizer.step")
+        _, l0, p0, mv0 = _run(cfg, batches, 6, False, monkeypatch, sched_every=2)
+        tr, l1, p1, mv1 = _run(cfg, batches, 6, True, monkeypatch, sched_every=2)
+    assert getattr(tr.optimizer.step, "_wrapped_by_lr_sched", False)
+    assert len(tr._graphs.graphs) == 2, "graph replay did not engage under the cosine scheduler"
+    assert tr.optimizer.param_groups[0]["lr"] < 1e-3
+    assert l0 == l1
+    assert torch.equal(p0, p1)
+    assert all(torch.equal(a, b) for a, b in zip(mv0, mv1))
 
 
 def test_step_graph_bench_workload_bitwise(dev, monkeypatch):
@@ -106,3 +129,28 @@ def test_step_graph_bad_labels(dev, monkeypatch):
     assert len(tr._graphs.graphs) == 2
     assert torch.equal(before, torch.cat([p.detach().reshape(-1) for p in m.parameters()]))
     assert int(tr.optimizer.state[next(m.parameters())]["step"]) == 2
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_deferred_bad_labels_raise_at_next_sync(dev, monkeypatch, graph):
+    """sync=False (no host read per step): a bad-label step skips its update on the device, returns a NaN loss,
+    and the trainer raises at its next synchronisation point with the step count rolled back."""
+    cfg = _cfg("unet", 3, [8, 16, 32, 64, 128], "float32")
+    batches = _batches(dev, 2, 32, 2, 3, seed=4)
+    monkeypatch.setenv("MMSEG_STEP_GRAPH", "1" if graph else "0")
+    torch.manual_seed(0)
+    m = build_model(cfg)
+    tr = Trainer(cfg, m)
+    tr.train_step(batches[0], 0)
+    tr.train_step(batches[1], 1, sync=False)
+    torch.cuda.synchronize()
+    before = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).clone()
+    bad = {"image": batches[0]["image"], "label": batches[0]["label"].clone()}
+    bad["label"][0, 1, 2, 3] = 9
+    lv = tr.train_step(bad, 2, sync=False)
+    assert torch.isnan(lv).item()
+    assert torch.equal(before, torch.cat([p.detach().reshape(-1) for p in m.parameters()]))
+    with pytest.raises(RuntimeError, match="outside"):
+        tr.check_deferred()
+    assert int(tr.optimizer.state[next(m.parameters())]["step"]) == 2
+    tr.check_deferred()                 # cleared: no second raise
