@@ -73,16 +73,51 @@ def _pmc_summary():
         return json.load(f), os.path.relpath(files[-1], ROOT)
 
 
+def _family_key(d: dict, kernel: str):
+    """The timer's family name (mmseg_last_kernel(), e.g. conv3_brickr_kernel<BN64>) as a key of a rocprofv3
+    summary (tools/rocprof_families.py: the same name, possibly with a [bf16] / [f32] suffix, or the bare kernel
+    name for families the trace does not split by template)."""
+    if kernel in d:
+        return kernel
+    for suf in ("[bf16]", "[f32]"):
+        if kernel + suf in d:
+            return kernel + suf
+    base = kernel.split("<")[0]
+    return base if base in d else None
+
+
 def pmc_traffic(kernel: str):
     """HBM bytes per launch of `kernel` from the PMC summary (the trace names some families without the timer's
     template suffix: conv3_brick5_kernel<BN32>[bf16] is conv3_brick5_kernel there)."""
     d, src = _pmc_summary()
     if d is None:
         return None, src
-    key = kernel if kernel in d else kernel.split("<")[0]
-    if key not in d:
+    key = _family_key(d, kernel)
+    if key is None:
         return None, src
     return d[key]["hbm_bytes_per_launch"], src
+
+
+def pmc_mfma_busy(kernel: str):
+    """MFMA-pipe busy fraction of `kernel` from the newest committed SQ counter summary (profiles/*pmc_sq*.json,
+    tools/rocprof_families.py sq, from a separate rocprofv3 --pmc pass over this bench): SQ_VALU_MFMA_BUSY_CYCLES
+    (summed over the 1,024 SIMDs) / (1,024 x GRBM_GUI_ACTIVE / 8 XCDs), with the VALU / LDS instructions issued
+    per MFMA."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_sq*.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    key = _family_key(d, kernel)
+    if key is None:
+        return None, os.path.relpath(files[-1], ROOT)
+    v = d[key]
+    out = {"mfma_busy": round(v["mfma_busy"], 4)}
+    for k in ("valu_per_mfma", "lds_per_mfma", "clock_ghz"):
+        if v.get(k) is not None:
+            out[k] = round(v[k], 3)
+    return out, os.path.relpath(files[-1], ROOT)
 
 
 def pmc_step_bytes():
@@ -98,6 +133,20 @@ def pmc_step_bytes():
     tot = sum(v["hbm_bytes_per_launch"] * v["launches"] for k, v in d.items()
               if not k.startswith(("_", "__amd_rocclr")))
     return tot / steps, src
+
+
+def hold_cycles(timer_steps: int, ms_per_timer_step: float = 40.0) -> int:
+    """Cycles of torch.cuda._sleep that keep the GPU busy while the host submits `timer_steps` eager steps with
+    per-launch events (~10 ms each at 96^3; 40 ms of margin per step).  The spin kernel's clock is measured here
+    rather than assumed (the shader clock moves with DVFS)."""
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 2_000_000
+    s.record()
+    torch.cuda._sleep(n)
+    e.record()
+    e.synchronize()
+    cyc_per_ms = n / max(s.elapsed_time(e), 1e-3)
+    return int(cyc_per_ms * ms_per_timer_step * timer_steps)
 
 
 def cpu_model() -> str:
@@ -233,12 +282,24 @@ def main():
         elapsed = t.item()
     loss_val = float(last.item()) if last is not None else float("nan")
 
-    # per-kernel-family timing over a separate live window (HIP events on the launching stream)
+    # per-kernel-family timing over a separate live window (HIP events on the launching stream).  The window's
+    # steps are eager (a captured graph has no per-launch events), and an eager step with two events per launch
+    # takes the host longer to submit than the GPU to run: with the queue drained, each start event would fire
+    # before its kernel was even submitted and short kernels would read long (round-3 review: the 12^3 conv read
+    # 28.7 us against rocprofv3's 20.5).  So the GPU is first held in a spin kernel long enough for the host to
+    # submit the whole window; the events then bracket back-to-back kernels, as in the profiler's trace.
+    held = torch.cuda.Event()
+    if args.timer_steps:
+        torch.cuda.synchronize()
+        torch.cuda._sleep(hold_cycles(args.timer_steps))
+        held.record()
     TIMER.start()
     for _ in range(args.timer_steps):
         trainer.train_step(batches[step % len(batches)], step, sync=False)
         step += 1
     TIMER.stop()
+    # True when the GPU was still in the spin kernel after the host had submitted the whole window
+    host_ahead = bool(args.timer_steps) and not held.query()
     fam = TIMER.summary()
     dom = max(fam.items(), key=lambda kv: kv[1]["ms"]) if fam else None
 
@@ -265,7 +326,13 @@ def main():
                     "traffic_source": tsrc,
                     "avg_launch_ms": round(avg_ms, 4), "launches_per_step": a["launches"] // max(args.timer_steps, 1),
                     "algorithmic_gflop_per_launch": round(flops_per_launch / 1e9, 3),
-                    "algorithmic_bytes_per_launch": round(bytes_per_launch)}
+                    "algorithmic_bytes_per_launch": round(bytes_per_launch),
+                    "timer": "HIP events on the launching stream, queue pre-filled (host ahead of GPU: "
+                             f"{host_ahead})"}
+        busy, bsrc = pmc_mfma_busy(name)
+        if busy is not None:
+            roofline.update(busy)
+            roofline["mfma_busy_source"] = bsrc
     families = {k: {"ms_per_step": round(v["ms"] / args.timer_steps, 3),
                     "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1) if v["ms"] > 0 else None}
                 for k, v in sorted(fam.items(), key=lambda kv: -kv[1]["ms"])}

@@ -12,14 +12,19 @@ reference's NIfTI datasets for benchmarking and parity runs.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Sequence
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
 
 
-def phantom(seed: int, size: int, num_classes: int, modalities: Sequence[str]) -> Dict[str, np.ndarray]:
+def phantom(seed: int, size: int, num_classes: int, modalities: Sequence[str],
+            class_seed: Optional[int] = None) -> Dict[str, np.ndarray]:
+    """class_seed: None (default) draws each organ's intensities per phantom, so only shape and contrast tell the
+    organs apart; an integer draws them once from that seed for every phantom ("organ-consistent" phantoms, on
+    which a model learns which organ is which -- used for the held-out Dice parity set)."""
     rng = np.random.Generator(np.random.PCG64(seed))
+    crng = rng if class_seed is None else np.random.Generator(np.random.PCG64(class_seed))
     S = size
     z, y, x = np.meshgrid(*(np.arange(S, dtype=np.float32),) * 3, indexing="ij")
     label = np.zeros((S, S, S), dtype=np.int64)
@@ -32,15 +37,15 @@ def phantom(seed: int, size: int, num_classes: int, modalities: Sequence[str]) -
     for mod in modalities:
         m = mod.upper()
         if m == "CT":
-            hu = rng.uniform(-200, 200, num_classes).astype(np.float32)
+            hu = crng.uniform(-200, 200, num_classes).astype(np.float32)
             img = hu[label] + rng.normal(0, 20, label.shape).astype(np.float32)
             img = (np.clip(img, -450.0, 250.0) + 450.0) / 700.0
         elif m == "PET":
-            suv = rng.uniform(0.5, 8.0, num_classes).astype(np.float32)
+            suv = crng.uniform(0.5, 8.0, num_classes).astype(np.float32)
             img = suv[label] + np.abs(rng.normal(0, 0.3, label.shape)).astype(np.float32)
             img = img / img.max()
         else:
-            mu = rng.uniform(0.0, 1.0, num_classes).astype(np.float32)
+            mu = crng.uniform(0.0, 1.0, num_classes).astype(np.float32)
             img = mu[label] + rng.normal(0, 0.1, label.shape).astype(np.float32)
             img = (img - img.mean()) / (img.std() + 1e-8)
         out[mod] = img.astype(np.float32)

@@ -10,7 +10,10 @@ this is new work whose oracle is "N ranks x B == 1 rank x N*B".
     all-reduces each bucket with ReduceOp.AVG as soon as the engine has
     written every gradient in it, so RCCL traffic over xGMI overlaps the rest
     of the backward; `finish()` joins them before the optimizer step;
-  * validation counts (Dice I/U) are summed with one all_reduce.
+  * validation counts (Dice I/U) are summed with one all_reduce;
+  * over RCCL the whole step, collectives included, is captured as one HIP graph (trainer/step_graph.py):
+    the bucket all-reduces are recorded at the points of the backward where their gradients become final,
+    on the comm stream forked from the capture stream, and joined before the AdamW kernel.
 """
 from __future__ import annotations
 
@@ -19,6 +22,14 @@ from typing import List, Optional
 
 import torch
 import torch.distributed as dist
+
+
+def initialized() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
+def backend() -> Optional[str]:
+    return dist.get_backend() if initialized() else None
 
 
 def world() -> int:
@@ -63,10 +74,13 @@ class GradBuckets:
     """Bucketed, backward-overlapped gradient averaging over a flat arena."""
 
     def __init__(self, grad_flat: torch.Tensor, param_offsets: List[int], param_sizes: List[int],
-                 bucket_mb: float = 32.0, group=None):
+                 bucket_mb: float = 32.0, group=None, force: bool = False):
         self.grad = grad_flat
         self.group = group
         self.w = world()
+        # force: issue the collectives at world size 1 too (distributed.reduce_single_rank) -- the one-GPU box
+        # runs the real RCCL + AVG (+ graph capture) path that way; at one rank AVG is the identity
+        self.active = self.w > 1 or force
         nbytes = int(bucket_mb * 1024 * 1024)
         # buckets over parameter index ranges, from the END of the arena (backward order)
         self.buckets = []          # (lo_param, hi_param, lo_elem, hi_elem)
@@ -133,7 +147,7 @@ class GradBuckets:
             dist.all_reduce(self.guard, op=dist.ReduceOp.SUM, group=self.group)
 
     def param_ready(self, idx: int):
-        if self.w == 1:
+        if not self.active:
             return
         b = self.owner[idx]
         if self.grad.is_cuda:
@@ -146,7 +160,7 @@ class GradBuckets:
             self._reduce(b)
 
     def finish(self):
-        if self.w == 1:
+        if not self.active:
             return
         late = [b for b, n in enumerate(self.pending) if n > 0]
         if late and self.grad.is_cuda:

@@ -19,8 +19,13 @@ What changes per step lives in device memory, not in kernel arguments:
 The replayed step runs the same kernels in the same order on the same buffers as the eager step, so it is
 bitwise equal to it (tests/test_step_graph_gpu.py).
 
-Used when the step has nothing per-step on the host side: one rank (the DP gradient buckets issue collectives
-from Python callbacks), accumulation_steps 1, the engine's fused head + loss, FlatAdamW (one group, no amsgrad),
+Data parallel over RCCL: the bucket all-reduces (ddp.GradBuckets, issued from the engine's gradient-ready
+callbacks) are recorded into the same graph at the points of the backward where they were issued, on the comm
+stream forked from the capture stream, so the replayed DP step overlaps them with the rest of the backward
+exactly as the eager step does, without ~4 ms of host submission per step.  gloo (host-side collectives) stays
+eager.
+
+Used when the step has nothing per-step on the host side: accumulation_steps 1, the engine's fused head + loss, FlatAdamW (one group, no amsgrad),
 no Dropout3d in training, single-stream engine, kernel timer off, optimizer.step / zero_grad not wrapped by the
 caller (a replay does not call them).  hardware.step_graph: false or MMSEG_STEP_GRAPH=0 turns it off.
 """
@@ -67,8 +72,14 @@ class StepGraphs:
         from ..engine.profiler import TIMER
         from .optim import FlatAdamW
         tr = self.tr
-        if TIMER.enabled or tr.world != 1 or tr.accumulation_steps != 1:
+        if TIMER.enabled or tr.accumulation_steps != 1:
             return False
+        if tr.dp:
+            # RCCL collectives are capturable (recorded on the comm stream forked from the capture stream); gloo's
+            # run on the host and are not.  MMSEG_STEP_GRAPH_DP=0 keeps the DP step eager.
+            from ..distributed import ddp
+            if ddp.backend() != "nccl" or os.environ.get("MMSEG_STEP_GRAPH_DP", "1") == "0":
+                return False
         if os.environ.get("MMSEG_MODALITY_STREAMS", "0") != "0":
             return False
         opt = tr.optimizer
@@ -126,8 +137,14 @@ class StepGraphs:
         try:
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 loss = eng.forward_loss(x, True, y, spec, cw)
-                eng.program.backward(None, False, gout=self.gout)
                 ws = eng.loss_ws
+                # DP: the bucket all-reduces are issued by the engine's gradient-ready callbacks during the backward
+                # (recorded into the graph on the comm stream), the guard count travels with the first bucket,
+                # and finish() joins every collective into the capture stream before the AdamW kernel
+                tr._arm_buckets(True, ws[-1:])
+                eng.program.backward(None, False, gout=self.gout)
+                if tr.dp and tr._buckets is not None:
+                    tr._buckets.finish()
                 L.mmseg_adamw_dev(ptr(flat.flat), ptr(flat.grad_flat), ptr(m), ptr(v), flat.numel,
                                   ptr(self.hyper_dev), ptr(ws[-1:]), stream_handle())
         finally:

@@ -69,6 +69,10 @@ class Trainer:
                 self.scaler = torch.amp.GradScaler("cuda")
         self.accumulation_steps = config["training"].get("accumulation_steps", 1)
         self.rank, self.world = ddp.rank(), ddp.world()
+        # gradient all-reduce active: more than one rank, or distributed.reduce_single_rank with a process group
+        # (the one-GPU rehearsal of the RCCL path, ddp.GradBuckets force)
+        self.dp = self.world > 1 or (bool(config.get("distributed", {}).get("reduce_single_rank", False))
+                                     and ddp.initialized())
         self.output_dir = Path(config["experiment"]["output_dir"]) / config["experiment"]["name"]
         if self.rank == 0:
             self.output_dir.mkdir(parents=True, exist_ok=True)
@@ -149,14 +153,14 @@ class Trainer:
         return eng.flat if eng is not None else None
 
     def _arm_buckets(self, communicate: bool, guard: Optional[torch.Tensor] = None):
-        if self.world == 1:
+        if not self.dp:
             return
         flat = self._engine_flat()
         if flat is None:
             return
         if self._buckets is None or self._buckets.grad is not flat.grad_flat:
             mb = float(self.config.get("distributed", {}).get("bucket_mb", 32))
-            self._buckets = ddp.GradBuckets(flat.grad_flat, flat.offsets, flat.sizes, bucket_mb=mb)
+            self._buckets = ddp.GradBuckets(flat.grad_flat, flat.offsets, flat.sizes, bucket_mb=mb, force=True)
         flat.on_ready = self._buckets.param_ready if communicate else None
         self._buckets.guard = guard if communicate else None
 
@@ -225,7 +229,7 @@ class Trainer:
         loss.backward(self._one)         # a constant output gradient: no fill kernel per step
         guarded = boundary and isinstance(self.optimizer, FlatAdamW)
         if boundary:
-            if self._buckets is not None and self.world > 1:
+            if self._buckets is not None and self.dp:
                 self._buckets.finish()
             if guarded:
                 self.optimizer.guard = guard

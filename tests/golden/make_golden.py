@@ -352,11 +352,11 @@ def full_grad_case(tag, cfg, S, B, seed, k=4096):
           f"bf16 median {np.median(ebf):.2e} max {max(ebf):.2e}")
 
 
-def _phantom_batch(seed, S, C, mods):
+def _phantom_batch(seed, S, C, mods, class_seed=None):
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(OUT)), "multimodal-organ-segmentation_amd",
                                     "data"))
     from synthetic import phantom    # the repo's seeded numpy phantom (plain data generation)
-    p = phantom(seed, S, C, mods)
+    p = phantom(int(seed), S, C, mods, class_seed=class_seed)
     return {"image": torch.from_numpy(np.stack([p[m] for m in mods]))[None],
             "label": torch.from_numpy(p["label"])[None]}
 
@@ -406,6 +406,64 @@ def dice_heldout_case(K=16, V=2, S=64, lr=1e-4):
         assert abs(dm.compute()["dice"] - met["dice"]) == 0.0
         print("dice_heldout", tag, met, "val loss", vloss)
     np.savez_compressed(os.path.join(OUT, "dice_heldout_c1.npz"), **out)
+
+
+def dice_heldout_trained_case(K=160, V=16, S=64, lr=2e-3, class_seed=77, feats=(8, 16, 32, 64, 128)):
+    """Held-out Dice on the REFERENCE's trained weights (north_star "Dice on a held-out synthetic set matching
+    reference +-1e-4").  UNet3D CT+PET, 3 classes, 64^3, batch 1, DiceCE, AdamW: the reference Trainer runs one
+    epoch over K organ-consistent phantoms (class_seed: the organs' intensities are the same in every phantom,
+    so the model learns which organ is which; train seeds 1234.., trainer.py:222-263), then _validate
+    (trainer.py:265-296, DiceMetric metrics.py:42-88) on V held-out phantoms (seeds 4321..).  Stored: the
+    trained weights (fp32, plain arrays -- the network is the c1 UNet3D at features 8..128 so they stay a
+    small fixture), the reference's held-out Dice / per-class Dice / I / U / loss on them, its argmax masks
+    (uint8) for flip counting, its training losses, and the same run in fp64 (the reference's own spread for
+    the free-running comparison)."""
+    mods = ["CT", "PET"]
+    out = {"K": np.int64(K), "V": np.int64(V), "S": np.int64(S), "lr": np.float64(lr),
+           "class_seed": np.int64(class_seed), "features": np.array(feats),
+           "train_seeds": np.arange(1234, 1234 + K), "val_seeds": np.arange(4321, 4321 + V)}
+    for dt, tag in ((torch.float32, "f32"), (torch.float64, "f64")):
+        cfg = base_config("unet", mods, 3, list(feats), lr=lr)
+        torch.manual_seed(42)
+        model = build.build_model(cfg).to(dt)
+        tr = trainer_mod.Trainer(config=cfg, model=model)
+        cast = lambda b: {"image": b["image"].to(dt), "label": b["label"]}  # noqa: E731
+        tr.train_loader = [cast(_phantom_batch(s, S, 3, mods, class_seed)) for s in out["train_seeds"]]
+        tr.val_loader = [cast(_phantom_batch(s, S, 3, mods, class_seed)) for s in out["val_seeds"]]
+        recorded = []
+        orig = tr.criterion
+
+        def rec(o, t, orig=orig, recorded=recorded):
+            lv = orig(o, t)
+            recorded.append(lv.item())
+            return lv
+        tr.criterion = rec
+        tr._train_epoch()
+        tr.criterion = orig
+        dm = metrics.DiceMetric(num_classes=3)
+        masks = []
+        model.eval()
+        with torch.no_grad():
+            for b in tr.val_loader:
+                pred = torch.argmax(model(b["image"]), dim=1)
+                masks.append(pred[0].to(torch.uint8).numpy())
+                dm.update(pred, b["label"])
+        vloss, met = tr._validate()
+        assert abs(dm.compute()["dice"] - met["dice"]) == 0.0
+        out[f"{tag}_train_losses"] = np.array(recorded)
+        out[f"{tag}_val_loss"] = np.float64(vloss)
+        out[f"{tag}_dice"] = np.float64(met["dice"])
+        out[f"{tag}_dice_per_class"] = np.array(met["dice_per_class"])
+        out[f"{tag}_inter"] = dm.intersection.numpy()
+        out[f"{tag}_union"] = dm.union.numpy()
+        if tag == "f32":
+            out["masks"] = np.stack(masks)
+            names = [n for n, _ in model.named_parameters()]
+            out["param_names"] = np.array(names)
+            for i, (n, p) in enumerate(model.named_parameters()):
+                out[f"w{i}"] = p.detach().numpy().astype(np.float32)
+        print("dice_heldout_trained", tag, met, "val loss", vloss)
+    np.savez_compressed(os.path.join(OUT, "dice_heldout_trained.npz"), **out)
 
 
 def checkpoint_case():

@@ -96,3 +96,79 @@ def test_heldout_dice_matches_reference(dev):
     # _validate's on-device fused argmax + counts == DiceMetric.update on the engine's own masks, bit for bit
     assert met["dice"] == res_eng["dice"] and met["dice_per_class"] == res_eng["dice_per_class"]
     assert flips <= 1e-4 * nvox
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# Held-out Dice on the REFERENCE's trained weights (make_golden.py dice_heldout_trained_case)
+# ---------------------------------------------------------------------------------------------------------------
+def _trained_cfg(g):
+    cfg = _cfg()
+    cfg["model"]["backbone"]["features"] = [int(f) for f in g["features"]]
+    cfg["training"]["optimizer"]["lr"] = float(g["lr"])
+    return cfg
+
+
+def _trained_batch(g, seed):
+    p = phantom(int(seed), int(g["S"]), 3, ["CT", "PET"], class_seed=int(g["class_seed"]))
+    return {"image": torch.from_numpy(np.stack([p["CT"], p["PET"]]))[None],
+            "label": torch.from_numpy(p["label"])[None]}
+
+
+def test_heldout_dice_on_reference_weights(dev):
+    """The reference trained a UNet3D (CT+PET, 3 classes, 64^3, features 8..128) for K = 160 AdamW steps on
+    organ-consistent phantoms (the organs' intensities are the same in every phantom, so it learns which organ
+    is which: held-out foreground Dice 0.93) and scored V = 16 held-out phantoms (4.2 M voxels) with its own
+    _validate (trainer.py:265-296, DiceMetric metrics.py:42-88).  The engine loads those weights and runs ITS
+    _validate (fused on-device argmax + counts): the Dice must match to +-1e-4 (north_star); argmax flips against
+    the reference's stored masks are counted and reported."""
+    g = golden("dice_heldout_trained")
+    cfg = _trained_cfg(g)
+    torch.manual_seed(0)
+    m = build_model(cfg)
+    names = [n for n, _ in m.named_parameters()]
+    assert names == list(g["param_names"])
+    with torch.no_grad():
+        for i, (n, p) in enumerate(m.named_parameters()):
+            p.copy_(torch.from_numpy(g[f"w{i}"]).to(dev))
+    val = [_trained_batch(g, s) for s in g["val_seeds"]]
+    tr = Trainer(cfg, m, val_loader=val)
+    vloss, met = tr._validate()
+    flips = 0
+    m.eval()
+    with torch.no_grad():
+        for i, b in enumerate(val):
+            pe = m(b["image"].to(dev)).argmax(1)[0].to(torch.uint8).cpu().numpy()
+            flips += int((pe != g["masks"][i]).sum())
+    ref = float(g["f32_dice"])
+    nvox = len(val) * int(g["S"]) ** 3
+    print(f"\nheld-out Dice on the reference's weights: engine {met['dice']:.7f} vs reference {ref:.7f} "
+          f"(|d| {abs(met['dice'] - ref):.2e}); per class {np.round(met['dice_per_class'], 7).tolist()} vs "
+          f"{np.round(g['f32_dice_per_class'], 7).tolist()}; val loss {vloss:.8f} vs {float(g['f32_val_loss']):.8f}; "
+          f"argmax flips {flips} of {nvox} voxels")
+    assert ref > 0.5
+    assert abs(met["dice"] - ref) <= 1e-4
+    assert np.allclose(met["dice_per_class"], g["f32_dice_per_class"], rtol=0, atol=1e-4)
+    assert abs(vloss - float(g["f32_val_loss"])) < 1e-5
+    assert flips <= 1e-5 * nvox
+
+
+def test_heldout_dice_free_running_trained(dev):
+    """The same K = 160-step epoch trained BY THE ENGINE from the reference's initial weights (torch.manual_seed
+    42 + the reference's registration order), then validated: a free-running trajectory, so the bound is the
+    reference's own fp32-vs-fp64 spread on the same run, max(1e-4, 2 |ref32 - ref64|)."""
+    g = golden("dice_heldout_trained")
+    cfg = _trained_cfg(g)
+    torch.manual_seed(42)
+    m = build_model(cfg)
+    train = [_trained_batch(g, s) for s in g["train_seeds"]]
+    val = [_trained_batch(g, s) for s in g["val_seeds"]]
+    tr = Trainer(cfg, m, val_loader=val)
+    m.train()
+    losses = np.array([tr.train_step(b, i) for i, b in enumerate(train)])
+    vloss, met = tr._validate()
+    ref, ref64 = float(g["f32_dice"]), float(g["f64_dice"])
+    spread = abs(ref - ref64)
+    print(f"\nfree-running 160 steps: engine Dice {met['dice']:.7f}, reference fp32 {ref:.7f}, fp64 {ref64:.7f} "
+          f"(|engine - ref| {abs(met['dice'] - ref):.2e}, reference spread {spread:.2e}); train loss max diff "
+          f"{np.abs(losses - g['f32_train_losses']).max():.2e}")
+    assert abs(met["dice"] - ref) <= max(1e-4, 2 * spread)

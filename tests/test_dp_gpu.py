@@ -228,3 +228,70 @@ def test_bad_labels_on_one_rank_raise_on_every_rank(dev):
         assert res[r]["raised"], f"rank {r} did not raise"
         assert res[r]["unchanged"], f"rank {r} updated its weights on the bad step"
     assert np.array_equal(res[0]["w"], res[1]["w"])
+
+
+def _rccl_graph_worker(port, q):
+    """One process, RCCL (backend "nccl") at world size 1 with distributed.reduce_single_rank: the bucket
+    all-reduces (ReduceOp.AVG on the comm stream) really run, eagerly and recorded inside the captured step.
+    Three runs of the same steps: eager DP, captured DP, captured without DP."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+        if ROOT not in sys.path:
+            sys.path.insert(0, ROOT)
+        import torch.distributed as dist
+        import mmseg_amd  # noqa: F401
+        from mmseg_amd.models.build import build_model
+        from mmseg_amd.trainer.trainer import Trainer
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1)
+        xs, ys = _data()
+        dev = torch.device("cuda", 0)
+        batches = [{"image": xs[s].to(dev), "label": ys[s].to(dev)} for s in range(STEPS)]
+        out = {}
+        for tag, graph, dp in (("eager_dp", False, True), ("graph_dp", True, True), ("graph", True, False)):
+            os.environ["MMSEG_STEP_GRAPH"] = "1" if graph else "0"
+            cfg = _cfg(f"/tmp/mmseg_rccl_{tag}")
+            cfg["hardware"]["step_graph"] = True
+            cfg["distributed"]["reduce_single_rank"] = dp
+            torch.manual_seed(0)
+            model = build_model(cfg)
+            tr = Trainer(cfg, model)
+            losses = [tr.train_step(batches[s % STEPS], s) for s in range(5)]
+            torch.cuda.synchronize()
+            w = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()])
+            out[tag] = {"losses": losses, "w": w.numpy(), "graphs": len(tr._graphs.graphs), "dp": tr.dp,
+                        "buckets": 0 if tr._buckets is None else len(tr._buckets.buckets),
+                        "backend": dist.get_backend()}
+        dist.destroy_process_group()
+        q.put((0, "ok", out))
+    except Exception:
+        import traceback
+        q.put((0, "error", traceback.format_exc()))
+
+
+def test_rccl_dp_step_captured_bitwise_equal_to_eager(dev):
+    """The DP step as one captured graph over RCCL (trainer/step_graph.py): bitwise equal to the eager DP step,
+    which at one rank (AVG = identity) is bitwise equal to the step without DP.  RCCL with more than one rank
+    needs one GPU per rank (the driver's 8-GPU node); this runs the same code path -- collectives recorded on
+    the comm stream inside the capture, guard with the first bucket, finish() joined before AdamW."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_graph_worker, args=(_free_port(), q))
+    p.start()
+    try:
+        r = q.get(timeout=300)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert r[1] == "ok", r[2]
+    res = r[2]
+    print("\n", {k: (v["losses"][-1], v["graphs"], v["dp"], v["buckets"], v["backend"]) for k, v in res.items()})
+    assert res["graph_dp"]["backend"] == "nccl"
+    assert res["eager_dp"]["dp"] and res["graph_dp"]["dp"] and not res["graph"]["dp"]
+    assert res["graph_dp"]["buckets"] > 4, "bucketing did not engage"
+    assert res["graph_dp"]["graphs"] == STEPS and res["eager_dp"]["graphs"] == 0
+    assert res["eager_dp"]["losses"] == res["graph_dp"]["losses"] == res["graph"]["losses"]
+    assert np.array_equal(res["eager_dp"]["w"], res["graph_dp"]["w"])
+    assert np.array_equal(res["graph"]["w"], res["graph_dp"]["w"])

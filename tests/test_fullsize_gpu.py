@@ -138,3 +138,83 @@ def test_fullsize_training_step_matches_reference(dev, tag, dtype):
     if not bf:
         hist = torch.bincount(logits.argmax(1).reshape(-1), minlength=C).cpu().numpy()
         assert np.abs(hist - g["argmax_hist"]).sum() <= 1e-4 * hist.sum()
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# The same 96^3 B=2 steps against the fp64 oracle PINNED to the engine's own kink decisions
+# ---------------------------------------------------------------------------------------------------------------
+PINNED_TOL = {  # per parameter tensor, max|engine - oracle| / max|oracle| (tests.helpers.rel)
+    "float32": 1e-4,   # fp32 storage, fp32 accumulation: rounding alone
+    "bfloat16": 6e-2,  # bf16 activation / weight storage (2^-9 relative per rounding, ~40 roundings deep)
+}
+PINNED_MEDIAN = {"float32": 2e-5, "bfloat16": 1.5e-2}
+
+
+def _oracle_fwd(kind, mods):
+    from oracle import mmseg_oracle as O
+    if kind == "unet":
+        return lambda p, x, pins: O.unet3d_forward(p, x, 5, pins=pins)
+    return lambda p, x, pins: O.dual_encoder_forward(p, x, "cross_attention", 5, pins=pins)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("tag,dtype", [("fullgrad_dual_c3", "float32"), ("fullgrad_dual_c3", "bfloat16"),
+                                       ("fullgrad_unet_c2", "float32"), ("fullgrad_dual_m3_c5", "float32"),
+                                       ("fullgrad_dual_m3_c5", "bfloat16")])
+def test_fullsize_step_pinned_to_fp64_oracle(dev, tag, dtype):
+    """The benched step at full size (96^3, B=2; trainer.py:250-254) against oracle/mmseg_oracle.py evaluated in
+    fp64 ON THE GPU (torch ops) with the engine's own ReLU masks and MaxPool argmax codes (oracle.Pins, as
+    tests/test_model_gpu.py does for the tiny configs).  At 96^3 a ReLU / MaxPool decision within rounding of its
+    kink re-routes one voxel's gradient discretely, which is why the free comparison above needs bounds relative
+    to the reference's own noise; with the decisions pinned the oracle and the engine differ by rounding alone,
+    so EVERY parameter gradient is held to PINNED_TOL (fp32: 1e-4), including the ConvTranspose biases; the conv
+    biases in front of an InstanceNorm (true gradient 0) to 1e-5 (fp32) / 1e-2 (bf16) of the largest gradient."""
+    from tests.test_model_gpu import _engine_pins
+    g = golden(tag)
+    model, mods, loss = CASES[tag]
+    S, B, seed, C = int(g["S"]), int(g["B"]), int(g["seed"]), 6
+    cfg = _config(model, mods, loss, dtype)
+    torch.manual_seed(seed)
+    m = build_model(cfg)
+    x, y, _ = full_inputs(S, B, len(mods), C, seed)
+    x, y = x.to(dev), y.to(dev)
+    tr = Trainer(cfg, m)
+    m.train()
+    lossv = tr._fused_loss(x, y)
+    assert lossv is not None, "fused head + loss path not taken"
+    pins = _engine_pins(m, model)
+    pins.relu_masks = [r.to(dev) for r in pins.relu_masks]
+    pins.pool_codes = [c.to(dev) for c in pins.pool_codes]
+    lossv.backward()
+    torch.cuda.synchronize()
+    import time
+    t0 = time.time()
+    from oracle import mmseg_oracle as O
+    params = {n: p.detach().double().requires_grad_(True) for n, p in m.backbone.named_parameters()}
+    lossf = O.dice_ce_loss if loss == "dice_ce" else O.tversky_loss
+    with torch.backends.cudnn.flags(enabled=False):
+        ro = _oracle_fwd(model, mods)(params, x.double(), pins)
+        rl = lossf(ro, y)
+        rl.backward()
+    torch.cuda.synchronize()
+    t_orc = time.time() - t0
+    assert pins.ri == len(pins.relu_masks) and pins.pi == len(pins.pool_codes)
+    errs, dead = {}, {}
+    gmax = max(float(p.grad.abs().max()) for p in params.values())
+    for n, p in m.backbone.named_parameters():
+        if n.endswith(("conv1.bias", "conv2.bias")):
+            dead[n] = float(p.grad.abs().max()) / gmax
+        else:
+            errs[n] = rel(p.grad, params[n].grad)
+    del ro, params
+    med = float(np.median(list(errs.values())))
+    worst = sorted(((v, n) for n, v in errs.items()), reverse=True)[:4]
+    err_loss = abs(lossv.item() - rl.item()) / abs(rl.item())
+    print(f"\n{tag} {dtype} pinned fp64 oracle ({t_orc:.0f} s on the GPU): loss rel {err_loss:.2e}; grad errors "
+          f"median {med:.2e}, worst {[(float(f'{v:.2e}'), n) for v, n in worst]}; dead-bias max "
+          f"{max(dead.values()):.2e} of the largest gradient")
+    tol = PINNED_TOL[dtype]
+    assert err_loss < (1e-6 if dtype == "float32" else 1e-3), err_loss
+    assert max(errs.values()) < tol, worst
+    assert med < PINNED_MEDIAN[dtype], med
+    assert max(dead.values()) < (1e-5 if dtype == "float32" else 1e-2), dead

@@ -59,7 +59,7 @@ def test_flat_adamw_round_trip_through_its_own_state_dict():
 
 def _fake_trainer(opt):
     model = types.SimpleNamespace(training=True, backbone=types.SimpleNamespace(dropout_p=0.0))
-    return types.SimpleNamespace(config={"hardware": {}}, world=1, accumulation_steps=1, optimizer=opt,
+    return types.SimpleNamespace(config={"hardware": {}}, world=1, dp=False, accumulation_steps=1, optimizer=opt,
                                  model=model)
 
 

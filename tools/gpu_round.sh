@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU call: parity tests, the default bench, a rocprofv3 kernel-trace profile
-# and two PMC passes (FETCH_SIZE, WRITE_SIZE; separate runs, no trace domains).
+# and three PMC passes (FETCH_SIZE, WRITE_SIZE, SQ MFMA-busy; separate runs, no trace domains).
 # usage: bash tools/gpu_round.sh TAG [tests|notests]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -20,6 +20,8 @@ tail -1 $O/bench.log
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o prof -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/prof.log 2>&1 || { echo "prof failed"; tail -20 $O/prof.log; exit 1; }
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o pmc -- python3 $R/bench.py --steps 2 --warmup 1 --timer-steps 1 --no-cpu-baseline > $O/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; tail -20 $O/pmc_fetch.log; exit 1; }
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o pmc -- python3 $R/bench.py --steps 2 --warmup 1 --timer-steps 1 --no-cpu-baseline > $O/pmc_write.log 2>&1 || { echo "pmc write failed"; tail -20 $O/pmc_write.log; exit 1; }
+timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d $O/pmc_sq -o pmc -- python3 $R/bench.py --steps 2 --warmup 1 --timer-steps 1 --no-cpu-baseline > $O/pmc_sq.log 2>&1 || { echo "pmc sq failed"; tail -20 $O/pmc_sq.log; exit 1; }
+python3 $R/tools/rocprof_families.py sq $O/pmc_sq/pmc_counter_collection.csv $O/pmc_sq.json > /dev/null
 python3 $R/tools/rocprof_families.py stats $O/trace/prof_kernel_stats.csv 16 > $O/families.txt
 python3 $R/tools/rocprof_families.py traffic $O/pmc_fetch/pmc_counter_collection.csv $O/pmc_write/pmc_counter_collection.csv $O/pmc_traffic.json 4 > /dev/null
 echo done

@@ -2,6 +2,7 @@
 
     python tools/rocprof_families.py stats  <prof_kernel_stats.csv>  [steps]
     python tools/rocprof_families.py traffic <fetch_counter_collection.csv> <write_counter_collection.csv> [out.json [steps]]
+    python tools/rocprof_families.py sq <sq_counter_collection.csv> [out.json]
 
 `stats` prints per-family calls / average duration (the same family names the
 in-process timer reports through mmseg_last_kernel(), so bench.py's
@@ -48,6 +49,9 @@ def family(name: str) -> str:
     if m:
         v3 = ",V3" if m.group(3) == "3" else ""
         return f"wgrad_brick{m.group(1)}_kernel<CO{int(m.group(2)) * 16}{v3}>[{dt}]"
+    m = re.search(r"wgrad_dma_kernelILi(\d+)E|wgrad_dma_kernel<(\d+)", name)
+    if m:
+        return f"wgrad_dma_kernel<CO{int(m.group(1) or m.group(2)) * 16}>"
     m = re.search(r"wgrad_reduce_kernelILi(\d+)E|wgrad_reduce_kernel<(\d+)>", name)
     if m:
         return f"wgrad_reduce_kernel<{m.group(1) or m.group(2)}>"
@@ -112,9 +116,55 @@ def traffic(fetch_csv: str, write_csv: str):
     return res
 
 
+SQ_COUNTERS = ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "SQ_INSTS_MFMA", "SQ_INSTS_VALU", "SQ_INSTS_LDS",
+               "GRBM_GUI_ACTIVE")
+N_SIMD, N_XCD = 1024, 8
+
+
+def sq(csv_path: str, trace_stats: str = None):
+    """Per family, averaged over its dispatches: MFMA-pipe busy = SQ_VALU_MFMA_BUSY_CYCLES (summed over the SIMDs)
+    / (1,024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs), the VALU and LDS instructions issued per MFMA, and -- when the
+    rows carry timestamps -- the effective clock GRBM_GUI_ACTIVE / 8 / duration (MI355X_MICROARCH.md DVFS)."""
+    per = defaultdict(lambda: defaultdict(float))
+    fam_of, dur = {}, {}
+    with open(csv_path) as f:
+        for r in csv.DictReader(f):
+            did = r.get("Dispatch_Id") or r.get("Correlation_Id")
+            fam_of[did] = family(r["Kernel_Name"])
+            per[did][r["Counter_Name"]] += float(r["Counter_Value"])
+            if r.get("Start_Timestamp") and r.get("End_Timestamp"):
+                dur[did] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    acc = defaultdict(lambda: defaultdict(list))
+    for did, c in per.items():
+        gui = c.get("GRBM_GUI_ACTIVE", 0.0)
+        if gui <= 0:
+            continue
+        a = acc[fam_of[did]]
+        a["mfma_busy"].append(c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (N_SIMD * gui / N_XCD))
+        nm = c.get("SQ_INSTS_MFMA", 0.0)
+        if nm > 0:
+            a["valu_per_mfma"].append(c.get("SQ_INSTS_VALU", 0.0) / nm)
+            a["lds_per_mfma"].append(c.get("SQ_INSTS_LDS", 0.0) / nm)
+        a["mfma_insts"].append(nm)
+        if did in dur and dur[did] > 0:
+            a["clock_ghz"].append(gui / N_XCD / dur[did] / 1e9)
+    res = {}
+    for fam, a in sorted(acc.items()):
+        res[fam] = {k: (sum(v) / len(v) if v else None) for k, v in a.items()}
+        res[fam]["launches"] = len(a["mfma_busy"])
+    return res
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 1)
+    elif sys.argv[1] == "sq":
+        r = sq(sys.argv[2])
+        js = json.dumps(r, indent=1)
+        if len(sys.argv) > 3:
+            with open(sys.argv[3], "w") as f:
+                f.write(js + "\n")
+        print(js)
     elif sys.argv[1] == "traffic":
         r = traffic(sys.argv[2], sys.argv[3])
         if len(sys.argv) > 5:      # training steps the profiled run executed (bench: warmup + steps + timer)
