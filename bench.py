@@ -135,20 +135,6 @@ def pmc_step_bytes():
     return tot / steps, src
 
 
-def hold_cycles(timer_steps: int, ms_per_timer_step: float = 40.0) -> int:
-    """Cycles of torch.cuda._sleep that keep the GPU busy while the host submits `timer_steps` eager steps with
-    per-launch events (~10 ms each at 96^3; 40 ms of margin per step).  The spin kernel's clock is measured here
-    rather than assumed (the shader clock moves with DVFS)."""
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    n = 2_000_000
-    s.record()
-    torch.cuda._sleep(n)
-    e.record()
-    e.synchronize()
-    cyc_per_ms = n / max(s.elapsed_time(e), 1e-3)
-    return int(cyc_per_ms * ms_per_timer_step * timer_steps)
-
-
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -282,24 +268,14 @@ def main():
         elapsed = t.item()
     loss_val = float(last.item()) if last is not None else float("nan")
 
-    # per-kernel-family timing over a separate live window (HIP events on the launching stream).  The window's
-    # steps are eager (a captured graph has no per-launch events), and an eager step with two events per launch
-    # takes the host longer to submit than the GPU to run: with the queue drained, each start event would fire
-    # before its kernel was even submitted and short kernels would read long (round-3 review: the 12^3 conv read
-    # 28.7 us against rocprofv3's 20.5).  So the GPU is first held in a spin kernel long enough for the host to
-    # submit the whole window; the events then bracket back-to-back kernels, as in the profiler's trace.
-    held = torch.cuda.Event()
-    if args.timer_steps:
-        torch.cuda.synchronize()
-        torch.cuda._sleep(hold_cycles(args.timer_steps))
-        held.record()
+    # per-kernel-family timing over a separate live window: eager steps (a captured graph has no per-launch
+    # timing) whose every library kernel is launched with hipExtLaunchKernelGGL start / stop events, stamped by
+    # the runtime from the dispatch itself -- the interval rocprofv3's kernel trace reports (engine/profiler.py)
     TIMER.start()
     for _ in range(args.timer_steps):
         trainer.train_step(batches[step % len(batches)], step, sync=False)
         step += 1
     TIMER.stop()
-    # True when the GPU was still in the spin kernel after the host had submitted the whole window
-    host_ahead = bool(args.timer_steps) and not held.query()
     fam = TIMER.summary()
     dom = max(fam.items(), key=lambda kv: kv[1]["ms"]) if fam else None
 
@@ -327,8 +303,8 @@ def main():
                     "avg_launch_ms": round(avg_ms, 4), "launches_per_step": a["launches"] // max(args.timer_steps, 1),
                     "algorithmic_gflop_per_launch": round(flops_per_launch / 1e9, 3),
                     "algorithmic_bytes_per_launch": round(bytes_per_launch),
-                    "timer": "HIP events on the launching stream, queue pre-filled (host ahead of GPU: "
-                             f"{host_ahead})"}
+                    "timer": "hipExtLaunchKernelGGL start/stop events on the launching stream (dispatch "
+                             "timestamps, the rocprofv3 kernel-trace interval)"}
         busy, bsrc = pmc_mfma_busy(name)
         if busy is not None:
             roofline.update(busy)

@@ -38,6 +38,14 @@ const char* mmseg_last_error(void);
 /* Name of the main kernel the last conv/wgrad entry point launched on this thread (for the per-kernel timer). */
 const char* mmseg_last_kernel(void);
 int mmseg_abi_version(void);
+/* Launch timing for the per-kernel timer (bench.py's roofline): between begin and end every kernel of the
+ * library is launched with hipExtLaunchKernelGGL start / stop events, which the runtime stamps from the
+ * dispatch itself (the kernel's own begin / end, as rocprofv3's kernel trace reports them).  After the work
+ * has completed, mmseg_timing_get(i) gives launch i's duration and its launch-site kernel expression. */
+int mmseg_timing_begin(void);
+int mmseg_timing_end(void);
+long long mmseg_timing_count(void);
+int mmseg_timing_get(long long i, float* ms, const char** name);
 
 /* --------------------------------------------------------- GEMM family */
 /* Gather modes: 0 CONV3 (3x3x3, pad 1), 1 POINT (1x1x1), 2 CONVT_FWD (k2 s2,

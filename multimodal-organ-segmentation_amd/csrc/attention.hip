@@ -274,11 +274,11 @@ int mmseg_bgemm_nt(const void* a, long long sa_outer, long long sa_inner, int ld
   const dim3 grid(ceil_div(M, 64) * ceil_div(N, 64), batch);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16) {
-    if (c_dtype == MMSEG_BF16) hipLaunchKernelGGL((bgemm_nt_kernel<bf16_t, bf16_t>), grid, dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((bgemm_nt_kernel<bf16_t, float>), grid, dim3(256), 0, s, g);
+    if (c_dtype == MMSEG_BF16) MMSEG_LAUNCH((bgemm_nt_kernel<bf16_t, bf16_t>), grid, dim3(256), 0, s, g);
+    else MMSEG_LAUNCH((bgemm_nt_kernel<bf16_t, float>), grid, dim3(256), 0, s, g);
   } else {
     MMSEG_REQUIRE(c_dtype == MMSEG_F32, "bgemm_nt: fp32 operands need an fp32 C");
-    hipLaunchKernelGGL((bgemm_nt_kernel<float, float>), grid, dim3(256), 0, s, g);
+    MMSEG_LAUNCH((bgemm_nt_kernel<float, float>), grid, dim3(256), 0, s, g);
   }
   mmseg::note_kernel("bgemm_nt_kernel");
   return mmseg::check_launch("bgemm_nt");
@@ -292,7 +292,7 @@ int mmseg_transpose(const void* src, long long s_outer, long long s_inner, int l
   const dim3 grid(ceil_div(rows, 32) * ceil_div(cols, 32), batch);
   hipStream_t s = (hipStream_t)stream;
 #define MMSEG_TR(TS, TD)                                                                                          \
-  hipLaunchKernelGGL((transpose_kernel<TS, TD>), grid, dim3(256), 0, s, (const TS*)src, s_outer, s_inner, lds,    \
+  MMSEG_LAUNCH((transpose_kernel<TS, TD>), grid, dim3(256), 0, s, (const TS*)src, s_outer, s_inner, lds,    \
                      (TD*)dst, d_outer, d_inner, ldd, inner, rows, cols)
   if (src_dtype == MMSEG_F32 && dst_dtype == MMSEG_F32) MMSEG_TR(float, float);
   else if (src_dtype == MMSEG_F32) MMSEG_TR(float, bf16_t);
@@ -306,9 +306,9 @@ int mmseg_softmax_rows(const float* S, int lds, void* P, int ldp, long long rows
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)((rows + 3) / 4));
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(softmax_rows_kernel<bf16_t>, grid, dim3(256), 0, s, S, lds, (bf16_t*)P, ldp, rows, N);
+    MMSEG_LAUNCH(softmax_rows_kernel<bf16_t>, grid, dim3(256), 0, s, S, lds, (bf16_t*)P, ldp, rows, N);
   else
-    hipLaunchKernelGGL(softmax_rows_kernel<float>, grid, dim3(256), 0, s, S, lds, (float*)P, ldp, rows, N);
+    MMSEG_LAUNCH(softmax_rows_kernel<float>, grid, dim3(256), 0, s, S, lds, (float*)P, ldp, rows, N);
   return mmseg::check_launch("softmax_rows");
 }
 
@@ -317,17 +317,17 @@ int mmseg_softmax_bwd_rows(const void* P, int ldp, const float* dP, int lddp, vo
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)((rows + 3) / 4));
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(softmax_bwd_rows_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)P, ldp, dP, lddp,
+    MMSEG_LAUNCH(softmax_bwd_rows_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)P, ldp, dP, lddp,
                        (bf16_t*)dS, ldds, rows, N);
   else
-    hipLaunchKernelGGL(softmax_bwd_rows_kernel<float>, grid, dim3(256), 0, s, (const float*)P, ldp, dP, lddp,
+    MMSEG_LAUNCH(softmax_bwd_rows_kernel<float>, grid, dim3(256), 0, s, (const float*)P, ldp, dP, lddp,
                        (float*)dS, ldds, rows, N);
   return mmseg::check_launch("softmax_bwd_rows");
 }
 
 int mmseg_relpos_bias(const float* table, const int* index, int heads, int N, float* bias, void* stream) {
   const long long total = (long long)heads * N * N;
-  hipLaunchKernelGGL(relpos_bias_kernel, dim3((unsigned)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192)),
+  MMSEG_LAUNCH(relpos_bias_kernel, dim3((unsigned)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192)),
                      dim3(256), 0, (hipStream_t)stream, table, index, heads, N, bias);
   return mmseg::check_launch("relpos_bias");
 }
@@ -339,10 +339,10 @@ int mmseg_softmax_bias_rows(const float* S, int lds, const float* bias, const fl
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)((rows + 3) / 4));
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(softmax_bias_rows_kernel<bf16_t>, grid, dim3(256), 0, s, S, lds, bias, mask, nw, heads,
+    MMSEG_LAUNCH(softmax_bias_rows_kernel<bf16_t>, grid, dim3(256), 0, s, S, lds, bias, mask, nw, heads,
                        (bf16_t*)P, ldp, rows, N);
   else
-    hipLaunchKernelGGL(softmax_bias_rows_kernel<float>, grid, dim3(256), 0, s, S, lds, bias, mask, nw, heads,
+    MMSEG_LAUNCH(softmax_bias_rows_kernel<float>, grid, dim3(256), 0, s, S, lds, bias, mask, nw, heads,
                        (float*)P, ldp, rows, N);
   return mmseg::check_launch("softmax_bias_rows");
 }
@@ -353,14 +353,14 @@ int mmseg_relpos_table_grad(const void* dS, int ldn, int B, int heads, int N, fl
   const long long hnm = (long long)heads * N * N;
   const unsigned g1 = (unsigned)((hnm + 255) / 256 < 8192 ? (hnm + 255) / 256 : 8192);
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(bias_grad_sum_kernel<bf16_t>, dim3(g1), dim3(256), 0, s, (const bf16_t*)dS, ldn, B, heads, N,
+    MMSEG_LAUNCH(bias_grad_sum_kernel<bf16_t>, dim3(g1), dim3(256), 0, s, (const bf16_t*)dS, ldn, B, heads, N,
                        dB);
   else
-    hipLaunchKernelGGL(bias_grad_sum_kernel<float>, dim3(g1), dim3(256), 0, s, (const float*)dS, ldn, B, heads, N,
+    MMSEG_LAUNCH(bias_grad_sum_kernel<float>, dim3(g1), dim3(256), 0, s, (const float*)dS, ldn, B, heads, N,
                        dB);
   if (mmseg::check_launch("bias_grad_sum")) return 1;
   const long long th = (long long)T * heads;
-  hipLaunchKernelGGL(relpos_table_grad_kernel, dim3((unsigned)std::min<long long>((th + 3) / 4, 8192)), dim3(256), 0, s,
+  MMSEG_LAUNCH(relpos_table_grad_kernel, dim3((unsigned)std::min<long long>((th + 3) / 4, 8192)), dim3(256), 0, s,
                      dB, offs, pairs, T,
                      heads, N, gtable, accumulate);
   return mmseg::check_launch("relpos_table_grad");

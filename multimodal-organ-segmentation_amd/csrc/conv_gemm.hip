@@ -2456,18 +2456,18 @@ int launch_brick5(const GemmArgs& g, hipStream_t s, long long* dbg, bool dma) {
   const dim3 grid(bpn5 * nt_n), block(256);
   if (g.wdq) {   // e4m3 forward (mmseg_conv3_fwd_fp8)
     mmseg::note_kernel("conv3_brick6_kernel<BN32,F8>");
-    if (g.nmean) hipLaunchKernelGGL((conv3_brick6_kernel<true, 6, 0, false, true>), grid, block, 0, s, g, upb5, bpn5);
-    else hipLaunchKernelGGL((conv3_brick6_kernel<false, 6, 0, false, true>), grid, block, 0, s, g, upb5, bpn5);
+    if (g.nmean) MMSEG_LAUNCH((conv3_brick6_kernel<true, 6, 0, false, true>), grid, block, 0, s, g, upb5, bpn5);
+    else MMSEG_LAUNCH((conv3_brick6_kernel<false, 6, 0, false, true>), grid, block, 0, s, g, upb5, bpn5);
     return upb5;
   }
   if (g.inpart) {   // samples a block does not touch keep zero partials
     hipMemsetAsync(g.inpart, 0, sizeof(float) * 2 * (size_t)(g.M / (g.D * g.H * g.W)) * bpn5 * g.Ncols, s);
     if (!g.bias && knob("MMSEG_BRICK6", 1) && knob("MMSEG_BRICK6_INP", 1)) {
       mmseg::note_kernel("conv3_brick6_kernel<BN32,INP>");
-      hipLaunchKernelGGL((conv3_brick6_kernel<false, 6, 0, true>), grid, block, 0, s, g, upb5, bpn5);
+      MMSEG_LAUNCH((conv3_brick6_kernel<false, 6, 0, true>), grid, block, 0, s, g, upb5, bpn5);
       return upb5;
     }
-    hipLaunchKernelGGL((conv3_brick5_kernel<false, true, true>), grid, block, 0, s, g, upb5, bpn5, nullptr);
+    MMSEG_LAUNCH((conv3_brick5_kernel<false, true, true>), grid, block, 0, s, g, upb5, bpn5, nullptr);
     return upb5;
   }
   if (!dbg && !dma && knob("MMSEG_BRICK6", 1)) {
@@ -2475,15 +2475,15 @@ int launch_brick5(const GemmArgs& g, hipStream_t s, long long* dbg, bool dma) {
     mmseg::note_kernel("conv3_brick6_kernel<BN32>");
 #ifdef MMSEG_TIMING_PROBES
     if (knob("MMSEG_BRICK6_DBG", 0) == 1) {
-      hipLaunchKernelGGL((conv3_brick6_kernel<false, 3, 1>), grid, block, 0, s, g, upb5, bpn5);
+      MMSEG_LAUNCH((conv3_brick6_kernel<false, 3, 1>), grid, block, 0, s, g, upb5, bpn5);
       return upb5;
     }
     if (knob("MMSEG_BRICK6_DBG", 0) == 2) {
-      hipLaunchKernelGGL((conv3_brick6_kernel<false, 3, 2>), grid, block, 0, s, g, upb5, bpn5);
+      MMSEG_LAUNCH((conv3_brick6_kernel<false, 3, 2>), grid, block, 0, s, g, upb5, bpn5);
       return upb5;
     }
 #endif
-#define MMSEG_B6(N, S) hipLaunchKernelGGL((conv3_brick6_kernel<N, S>), grid, block, 0, s, g, upb5, bpn5)
+#define MMSEG_B6(N, S) MMSEG_LAUNCH((conv3_brick6_kernel<N, S>), grid, block, 0, s, g, upb5, bpn5)
     if (g.nmean) {
       if (sg == 6) MMSEG_B6(true, 6); else if (sg == 7) MMSEG_B6(true, 7); else MMSEG_B6(true, 3);
     } else {
@@ -2492,10 +2492,10 @@ int launch_brick5(const GemmArgs& g, hipStream_t s, long long* dbg, bool dma) {
 #undef MMSEG_B6
     return upb5;
   }
-  if (dbg && dma) hipLaunchKernelGGL((conv3_brick5_kernel<true, true>), grid, block, 0, s, g, upb5, bpn5, dbg);
-  else if (dbg) hipLaunchKernelGGL((conv3_brick5_kernel<true, false>), grid, block, 0, s, g, upb5, bpn5, dbg);
-  else if (dma) hipLaunchKernelGGL((conv3_brick5_kernel<false, true>), grid, block, 0, s, g, upb5, bpn5, nullptr);
-  else hipLaunchKernelGGL((conv3_brick5_kernel<false, false>), grid, block, 0, s, g, upb5, bpn5, nullptr);
+  if (dbg && dma) MMSEG_LAUNCH((conv3_brick5_kernel<true, true>), grid, block, 0, s, g, upb5, bpn5, dbg);
+  else if (dbg) MMSEG_LAUNCH((conv3_brick5_kernel<true, false>), grid, block, 0, s, g, upb5, bpn5, dbg);
+  else if (dma) MMSEG_LAUNCH((conv3_brick5_kernel<false, true>), grid, block, 0, s, g, upb5, bpn5, nullptr);
+  else MMSEG_LAUNCH((conv3_brick5_kernel<false, false>), grid, block, 0, s, g, upb5, bpn5, nullptr);
   return upb5;
 }
 
@@ -4446,12 +4446,12 @@ int launch_splitk_reduce(const GemmArgs& g, hipStream_t s) {
   while (S < 16 && g.ksplit / (2 * S) >= rpt) S *= 2;
   if (vec && S > 1) {
     const int nb = ceil_div(total / 4, 256 / S);
-    if (S == 16) hipLaunchKernelGGL((gemm_splitk_reduce_s<T, 16>), dim3(nb), dim3(256), 0, s, g);
-    else if (S == 8) hipLaunchKernelGGL((gemm_splitk_reduce_s<T, 8>), dim3(nb), dim3(256), 0, s, g);
-    else if (S == 4) hipLaunchKernelGGL((gemm_splitk_reduce_s<T, 4>), dim3(nb), dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((gemm_splitk_reduce_s<T, 2>), dim3(nb), dim3(256), 0, s, g);
+    if (S == 16) MMSEG_LAUNCH((gemm_splitk_reduce_s<T, 16>), dim3(nb), dim3(256), 0, s, g);
+    else if (S == 8) MMSEG_LAUNCH((gemm_splitk_reduce_s<T, 8>), dim3(nb), dim3(256), 0, s, g);
+    else if (S == 4) MMSEG_LAUNCH((gemm_splitk_reduce_s<T, 4>), dim3(nb), dim3(256), 0, s, g);
+    else MMSEG_LAUNCH((gemm_splitk_reduce_s<T, 2>), dim3(nb), dim3(256), 0, s, g);
   } else {
-    hipLaunchKernelGGL((gemm_splitk_reduce<T, MODE>), dim3(splitk_reduce_blocks<MODE>(g)), dim3(256), 0, s, g);
+    MMSEG_LAUNCH((gemm_splitk_reduce<T, MODE>), dim3(splitk_reduce_blocks<MODE>(g)), dim3(256), 0, s, g);
   }
   return mmseg::check_launch("gemm_splitk_reduce");
 }
@@ -4489,11 +4489,11 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
         // timing probes (diagnostics only, wrong results): built only with -DMMSEG_TIMING_PROBES
         const int dbg = knob("MMSEG_BRICKR_DBG", 0);
         if (b666 && dbg == 1)
-          hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6, 1>), grid, block, 0, s, g, 6, 6, 6);
+          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 1>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
         else if (b666 && dbg == 2)
-          hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6, 2>), grid, block, 0, s, g, 6, 6, 6);
+          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 2>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
         else if (b666 && dbg == 3)
-          hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6, 3>), grid, block, 0, s, g, 6, 6, 6);
+          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 3>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
         else if (dbg == 4) {
           static long long* dp = nullptr;
           const int nlong = 4 * 4096 + 64;
@@ -4501,14 +4501,14 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
           hipMemsetAsync(dp, 0, nlong * sizeof(long long), s);
           const bool pf = knob("MMSEG_BRICKR_PF", 0);
           if (b666 && pf)
-            hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6, 4, true>), grid, block, 0, s, g, 6, 6, 6, dp);
+            MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 4, true>), grid, block, 0, s, g, 6, 6, 6, dp);
           else if (b666)
-            hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6, 4>), grid, block, 0, s, g, 6, 6, 6, dp);
+            MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 4>), grid, block, 0, s, g, 6, 6, 6, dp);
           else if (pf)
-            hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 0, 0, 0, 4, true>), grid, block, 0, s, g, plan.bz, plan.by,
+            MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 0, 0, 0, 4, true>), grid, block, 0, s, g, plan.bz, plan.by,
                                plan.bx, dp);
           else
-            hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 0, 0, 0, 4>), grid, block, 0, s, g, plan.bz, plan.by,
+            MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 0, 0, 0, 4>), grid, block, 0, s, g, plan.bz, plan.by,
                                plan.bx, dp);
           std::vector<long long> h(nlong);
           hipStreamSynchronize(s);
@@ -4531,33 +4531,33 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
         } else
 #endif
         if (b666 && knob("MMSEG_BRICKR_PF", 0))
-          hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6, 0, true>), grid, block, 0, s, g, 6, 6, 6);
+          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 0, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
         else if (b666 && rb32)
-          hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6, 0, false, true>), grid, block, 0, s, g, 6, 6, 6);
+          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 0, false, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
         else if (b666)
-          hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 6, 6, 6>), grid, block, 0, s, g, 6, 6, 6);
+          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
         else if (knob("MMSEG_BRICKR_PF", 0))
-          hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 0, 0, 0, 0, true>), grid, block, 0, s, g, plan.bz, plan.by,
-                             plan.bx);
+          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 0, 0, 0, 0, true>), grid, block, 0, s, g, plan.bz, plan.by,
+                             plan.bx, (long long*)nullptr);
         else if (rb32)
-          hipLaunchKernelGGL((conv3_brickr_kernel<T, 64, 0, 0, 0, 0, false, true>), grid, block, 0, s, g, plan.bz,
-                             plan.by, plan.bx);
+          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 0, 0, 0, 0, false, true>), grid, block, 0, s, g, plan.bz,
+                             plan.by, plan.bx, (long long*)nullptr);
         else
-          hipLaunchKernelGGL((conv3_brickr_kernel<T, 64>), grid, block, 0, s, g, plan.bz, plan.by, plan.bx);
+          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64>), grid, block, 0, s, g, plan.bz, plan.by, plan.bx, (long long*)nullptr);
       }
     } else if (b666) {
       mmseg::note_kernel("conv3_brickr_kernel<BN32>");
       if (rb32)
-        hipLaunchKernelGGL((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, false, true>), grid, block, 0, s, g, 6, 6, 6);
+        MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, false, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
       else
-        hipLaunchKernelGGL((conv3_brickr_kernel<T, 32, 6, 6, 6>), grid, block, 0, s, g, 6, 6, 6);
+        MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
     } else {
       mmseg::note_kernel("conv3_brickr_kernel<BN32>");
       if (rb32)
-        hipLaunchKernelGGL((conv3_brickr_kernel<T, 32, 0, 0, 0, 0, false, true>), grid, block, 0, s, g, plan.bz,
-                           plan.by, plan.bx);
+        MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 0, 0, 0, 0, false, true>), grid, block, 0, s, g, plan.bz,
+                           plan.by, plan.bx, (long long*)nullptr);
       else
-        hipLaunchKernelGGL((conv3_brickr_kernel<T, 32>), grid, block, 0, s, g, plan.bz, plan.by, plan.bx);
+        MMSEG_LAUNCH((conv3_brickr_kernel<T, 32>), grid, block, 0, s, g, plan.bz, plan.by, plan.bx, (long long*)nullptr);
     }
     if (mmseg::check_launch("conv3_brickr")) return 1;
     if (g.ksplit > 1) return launch_splitk_reduce<T, MODE>(g, s);
@@ -4580,7 +4580,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
           nb8 * (g.Ncols / 64) >= knob("MMSEG_BRICK8_MINBLK", 256) &&
           (long long)g.M * g.lda * 2 < (1LL << 31) && (long long)((g.KG + 3) & ~3) * g.Cpad * 16 < (1LL << 31)) {
         mmseg::note_kernel("conv3_brick8_kernel<BN64>");
-        hipLaunchKernelGGL((conv3_brick8_kernel<64, 1>), dim3(nb8 * (g.Ncols / 64)), dim3(512), 0, s, g);
+        MMSEG_LAUNCH((conv3_brick8_kernel<64, 1>), dim3(nb8 * (g.Ncols / 64)), dim3(512), 0, s, g);
         return mmseg::check_launch("conv3_brick8");
       }
       if (b8 && g.Ncols == 32 && g.D % 16 == 0 && g.H % 8 == 0 && g.W % 8 == 0 &&
@@ -4589,7 +4589,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
           nb8 / 2 >= knob("MMSEG_BRICK8_MINBLK", 256) && (8 << g.cpg_shift) >= 64 &&
           (long long)g.M * g.lda * 2 < (1LL << 31) && (long long)((g.KG + 3) & ~3) * g.Cpad * 16 < (1LL << 31)) {
         mmseg::note_kernel("conv3_brick8_kernel<BN32>");
-        hipLaunchKernelGGL((conv3_brick8_kernel<32, 2>), dim3(nb8 / 2), dim3(512), 0, s, g);
+        MMSEG_LAUNCH((conv3_brick8_kernel<32, 2>), dim3(nb8 / 2), dim3(512), 0, s, g);
         return mmseg::check_launch("conv3_brick8");
       }
     }
@@ -4608,15 +4608,15 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     if (g.Ncols % 32 != 0) {    // a multiple of 48 (plan_conv3)
       mmseg::note_kernel("conv3_brick2_kernel<BN48,ZW1>");
       if (b32) {
-        hipLaunchKernelGGL((conv3_brick2_kernel<T, 48, 1, false, true>), dim3(nb1 * (g.Ncols / 48)), block, 0, s, g);
+        MMSEG_LAUNCH((conv3_brick2_kernel<T, 48, 1, false, true>), dim3(nb1 * (g.Ncols / 48)), block, 0, s, g);
         return mmseg::check_launch("conv3_brick2");
       }
-      hipLaunchKernelGGL((conv3_brick2_kernel<T, 48, 1>), dim3(nb1 * (g.Ncols / 48)), block, 0, s, g);
+      MMSEG_LAUNCH((conv3_brick2_kernel<T, 48, 1>), dim3(nb1 * (g.Ncols / 48)), block, 0, s, g);
     } else if (v3 && knob("MMSEG_BRICK3_BN64", 0) && g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
       const int units = nb1 * (g.Ncols / 64);
       const int upb = maxblk > 0 ? ceil_div(units, maxblk) : 1;
       mmseg::note_kernel("conv3_brick3_kernel<BN64>");
-      hipLaunchKernelGGL((conv3_brick3_kernel<T, 64>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
+      MMSEG_LAUNCH((conv3_brick3_kernel<T, 64>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
     } else if (v3 && gemm_nchunk(g) == 1 && g.Ncols % 32 == 0 && knob("MMSEG_BRICK4", 1) &&
                !(g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks)) {
       if constexpr (sizeof(T) == 2) {
@@ -4653,7 +4653,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
           }
         } else {
           mmseg::note_kernel("conv3_brick4_kernel<BN32>");
-          hipLaunchKernelGGL(conv3_brick4_kernel, dim3(bpn * nt_n), block, 0, s, g, upb, bpn);
+          MMSEG_LAUNCH(conv3_brick4_kernel, dim3(bpn * nt_n), block, 0, s, g, upb, bpn);
         }
       }
     } else if (v3 && !(g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks)) {
@@ -4661,33 +4661,33 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
       const int upb = maxblk > 0 ? ceil_div(units, maxblk) : 1;
       mmseg::note_kernel("conv3_brick3_kernel<BN32>");
       if (knob("MMSEG_BRICK3_WU", 0))
-        hipLaunchKernelGGL((conv3_brick3_kernel<T, 32, true>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
+        MMSEG_LAUNCH((conv3_brick3_kernel<T, 32, true>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
       else if (knob("MMSEG_BRICK3_XP", 0))
-        hipLaunchKernelGGL((conv3_brick3_kernel<T, 32, false, false, true>), dim3(ceil_div(units, upb)), block, 0, s,
+        MMSEG_LAUNCH((conv3_brick3_kernel<T, 32, false, false, true>), dim3(ceil_div(units, upb)), block, 0, s,
                            g, upb);
       else if (knob("MMSEG_BRICK3_WDB", 0))
-        hipLaunchKernelGGL((conv3_brick3_kernel<T, 32, false, true>), dim3(ceil_div(units, upb)), block, 0, s, g,
+        MMSEG_LAUNCH((conv3_brick3_kernel<T, 32, false, true>), dim3(ceil_div(units, upb)), block, 0, s, g,
                            upb);
       else
-        hipLaunchKernelGGL((conv3_brick3_kernel<T, 32, false>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
+        MMSEG_LAUNCH((conv3_brick3_kernel<T, 32, false>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
     } else if (g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
       mmseg::note_kernel("conv3_brick2_kernel<BN64,ZW1>");
       if (knob("MMSEG_TAP_PF", 1) && b32) {
-        hipLaunchKernelGGL((conv3_brick2_kernel<T, 64, 1, true, true>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
+        MMSEG_LAUNCH((conv3_brick2_kernel<T, 64, 1, true, true>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
         return mmseg::check_launch("conv3_brick2");
       }
       if (knob("MMSEG_TAP_PF", 1))   // 2 % on the 48^3 64-channel layers (r02)
-        hipLaunchKernelGGL((conv3_brick2_kernel<T, 64, 1, true>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
+        MMSEG_LAUNCH((conv3_brick2_kernel<T, 64, 1, true>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
       else
-        hipLaunchKernelGGL((conv3_brick2_kernel<T, 64, 1>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
+        MMSEG_LAUNCH((conv3_brick2_kernel<T, 64, 1>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
     } else if (sizeof(T) == 2 && g.D % 8 == 0 && knob("MMSEG_BRICK2_ZW", 1) == 2) {
       if constexpr (sizeof(T) == 2) {
         mmseg::note_kernel("conv3_brick2_kernel<BN32,ZW2>");
-        hipLaunchKernelGGL((conv3_brick2_kernel<T, 32, 2>), dim3(nb1 / 2 * (g.Ncols / 32)), block, 0, s, g);
+        MMSEG_LAUNCH((conv3_brick2_kernel<T, 32, 2>), dim3(nb1 / 2 * (g.Ncols / 32)), block, 0, s, g);
       }
     } else {
       mmseg::note_kernel("conv3_brick2_kernel<BN32,ZW1>");
-      hipLaunchKernelGGL((conv3_brick2_kernel<T, 32, 1>), dim3(nb1 * (g.Ncols / 32)), block, 0, s, g);
+      MMSEG_LAUNCH((conv3_brick2_kernel<T, 32, 1>), dim3(nb1 * (g.Ncols / 32)), block, 0, s, g);
     }
     return mmseg::check_launch("conv3_brick2");
   }
@@ -4697,9 +4697,9 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     const int bn = (g.Ncols >= 64 && knob("MMSEG_BRICK_BN", 64) == 64) ? 64 : 32;
     mmseg::note_kernel(bn == 64 ? "conv3_brick_kernel<BN64>" : "conv3_brick_kernel<BN32>");
     if (bn == 64) {
-      hipLaunchKernelGGL((conv3_brick_kernel<T, 64>), dim3(nb * ceil_div(g.Ncols, 64)), block, 0, s, g);
+      MMSEG_LAUNCH((conv3_brick_kernel<T, 64>), dim3(nb * ceil_div(g.Ncols, 64)), block, 0, s, g);
     } else {
-      hipLaunchKernelGGL((conv3_brick_kernel<T, 32>), dim3(nb * ceil_div(g.Ncols, 32)), block, 0, s, g);
+      MMSEG_LAUNCH((conv3_brick_kernel<T, 32>), dim3(nb * ceil_div(g.Ncols, 32)), block, 0, s, g);
     }
     return mmseg::check_launch("conv3_brick");
   }
@@ -4708,7 +4708,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     // voxels, so each input row is read by one block instead of by Ncols / 64 column tiles
     mmseg::note_kernel("conv_gemm_kernel<convT_fwd,64x256>");
     dim3 grid(ceil_div(g.M, 64) * (g.Ncols / 256) * g.ksplit);
-    hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, 1, 4, 4, 4>), grid, block, 0, s, g);
+    MMSEG_LAUNCH((conv_gemm_kernel<T, MODE, 1, 4, 4, 4>), grid, block, 0, s, g);
     if (mmseg::check_launch("conv_gemm")) return 1;
     if (g.ksplit > 1) return launch_splitk_reduce<T, MODE>(g, s);
     return 0;
@@ -4716,7 +4716,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
   if (MODE == MODE_CONVT_DGRAD && g.Ncols % 64 == 0 && knob("MMSEG_CONVT_DGRAD_TILE", 0) == 1) {
     mmseg::note_kernel("conv_gemm_kernel<convT_dgrad,64x64>");
     dim3 grid(ceil_div(g.M, 64) * (g.Ncols / 64) * g.ksplit);
-    hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, 2, 2, 2, 2>), grid, block, 0, s, g);
+    MMSEG_LAUNCH((conv_gemm_kernel<T, MODE, 2, 2, 2, 2>), grid, block, 0, s, g);
     if (mmseg::check_launch("conv_gemm")) return 1;
     if (g.ksplit > 1) return launch_splitk_reduce<T, MODE>(g, s);
     return 0;
@@ -4724,7 +4724,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
   if (MODE == MODE_CONVT_DGRAD && g.Ncols % 128 == 0 && knob("MMSEG_CONVT_DGRAD_TILE", 0) == 2) {
     mmseg::note_kernel("conv_gemm_kernel<convT_dgrad,64x128>");
     dim3 grid(ceil_div(g.M, 64) * (g.Ncols / 128) * g.ksplit);
-    hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, 1, 4, 4, 2>), grid, block, 0, s, g);
+    MMSEG_LAUNCH((conv_gemm_kernel<T, MODE, 1, 4, 4, 2>), grid, block, 0, s, g);
     if (mmseg::check_launch("conv_gemm")) return 1;
     if (g.ksplit > 1) return launch_splitk_reduce<T, MODE>(g, s);
     return 0;
@@ -4735,14 +4735,14 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
                                 "conv_gemm_kernel<convT_fwd,128x32>", "conv_gemm_kernel<convT_dgrad,128x32>"};
     mmseg::note_kernel(nm[MODE]);
     dim3 grid(ceil_div(g.M, 128) * ceil_div(g.Ncols, 32) * g.ksplit);
-    hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, 4, 1, 2, 2>), grid, block, 0, s, g);
+    MMSEG_LAUNCH((conv_gemm_kernel<T, MODE, 4, 1, 2, 2>), grid, block, 0, s, g);
   } else {
     // BM=128, BN=64
     static const char* nm[4] = {"conv_gemm_kernel<conv3,128x64>", "conv_gemm_kernel<point,128x64>",
                                 "conv_gemm_kernel<convT_fwd,128x64>", "conv_gemm_kernel<convT_dgrad,128x64>"};
     mmseg::note_kernel(nm[MODE]);
     dim3 grid(ceil_div(g.M, 128) * ceil_div(g.Ncols, 64) * g.ksplit);
-    hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, 2, 2, 4, 2>), grid, block, 0, s, g);
+    MMSEG_LAUNCH((conv_gemm_kernel<T, MODE, 2, 2, 4, 2>), grid, block, 0, s, g);
   }
   if (mmseg::check_launch("conv_gemm")) return 1;
   if (g.ksplit > 1) return launch_splitk_reduce<T, MODE>(g, s);
@@ -4777,16 +4777,16 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 64) * g.ksplit);
         mmseg::note_kernel("wgrad_brickr_kernel<CO64>");
         if (b366)
-          hipLaunchKernelGGL((wgrad_brickr_kernel<T, 4, 3, 6, 6>), grid, dim3(512), 0, s, g, 3, 6, 6);
+          MMSEG_LAUNCH((wgrad_brickr_kernel<T, 4, 3, 6, 6>), grid, dim3(512), 0, s, g, 3, 6, 6);
         else
-          hipLaunchKernelGGL((wgrad_brickr_kernel<T, 4>), grid, dim3(512), 0, s, g, wb.bz, wb.by, wb.bx);
+          MMSEG_LAUNCH((wgrad_brickr_kernel<T, 4>), grid, dim3(512), 0, s, g, wb.bz, wb.by, wb.bx);
       } else {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 32) * g.ksplit);
         mmseg::note_kernel("wgrad_brickr_kernel<CO32>");
         if (b366)
-          hipLaunchKernelGGL((wgrad_brickr_kernel<T, 2, 3, 6, 6>), grid, dim3(512), 0, s, g, 3, 6, 6);
+          MMSEG_LAUNCH((wgrad_brickr_kernel<T, 2, 3, 6, 6>), grid, dim3(512), 0, s, g, 3, 6, 6);
         else
-          hipLaunchKernelGGL((wgrad_brickr_kernel<T, 2>), grid, dim3(512), 0, s, g, wb.bz, wb.by, wb.bx);
+          MMSEG_LAUNCH((wgrad_brickr_kernel<T, 2>), grid, dim3(512), 0, s, g, wb.bz, wb.by, wb.bx);
       }
       return mmseg::check_launch("wgrad_brickr");
     }
@@ -4808,23 +4808,23 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
         if (mt == 4) {
           mmseg::note_kernel("wgrad_dma_kernel<CO64>");
           if (norm)
-            hipLaunchKernelGGL((wgrad_dma_kernel<4, true>), grid, dim3(512), 0, s, g);
+            MMSEG_LAUNCH((wgrad_dma_kernel<4, true>), grid, dim3(512), 0, s, g);
           else if (st4)
-            hipLaunchKernelGGL((wgrad_dma_kernel<4, false, 4>), grid, dim3(512), 0, s, g);
+            MMSEG_LAUNCH((wgrad_dma_kernel<4, false, 4>), grid, dim3(512), 0, s, g);
           else
-            hipLaunchKernelGGL((wgrad_dma_kernel<4>), grid, dim3(512), 0, s, g);
+            MMSEG_LAUNCH((wgrad_dma_kernel<4>), grid, dim3(512), 0, s, g);
         } else {
           mmseg::note_kernel("wgrad_dma_kernel<CO32>");
           if (norm && pipe)
-            hipLaunchKernelGGL((wgrad_dma_kernel<2, true, 3, true>), grid, dim3(512), 0, s, g);
+            MMSEG_LAUNCH((wgrad_dma_kernel<2, true, 3, true>), grid, dim3(512), 0, s, g);
           else if (norm)
-            hipLaunchKernelGGL((wgrad_dma_kernel<2, true>), grid, dim3(512), 0, s, g);
+            MMSEG_LAUNCH((wgrad_dma_kernel<2, true>), grid, dim3(512), 0, s, g);
           else if (pipe)
-            hipLaunchKernelGGL((wgrad_dma_kernel<2, false, 3, true>), grid, dim3(512), 0, s, g);
+            MMSEG_LAUNCH((wgrad_dma_kernel<2, false, 3, true>), grid, dim3(512), 0, s, g);
           else if (st4)
-            hipLaunchKernelGGL((wgrad_dma_kernel<2, false, 4>), grid, dim3(512), 0, s, g);
+            MMSEG_LAUNCH((wgrad_dma_kernel<2, false, 4>), grid, dim3(512), 0, s, g);
           else
-            hipLaunchKernelGGL((wgrad_dma_kernel<2>), grid, dim3(512), 0, s, g);
+            MMSEG_LAUNCH((wgrad_dma_kernel<2>), grid, dim3(512), 0, s, g);
         }
         return mmseg::check_launch("wgrad_dma");
       }
@@ -4832,20 +4832,20 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 64) * g.ksplit);
         mmseg::note_kernel(v3 ? "wgrad_brick2_kernel<CO64,V3>" : "wgrad_brick2_kernel<CO64>");
         if (v3 && g.nmean)
-          hipLaunchKernelGGL((wgrad_brick2_kernel<T, 4, 3, true>), grid, dim3(512), 0, s, g);
+          MMSEG_LAUNCH((wgrad_brick2_kernel<T, 4, 3, true>), grid, dim3(512), 0, s, g);
         else if (v3)
-          hipLaunchKernelGGL((wgrad_brick2_kernel<T, 4, 3>), grid, dim3(512), 0, s, g);
+          MMSEG_LAUNCH((wgrad_brick2_kernel<T, 4, 3>), grid, dim3(512), 0, s, g);
         else
-          hipLaunchKernelGGL((wgrad_brick2_kernel<T, 4, 2>), grid, dim3(512), 0, s, g);
+          MMSEG_LAUNCH((wgrad_brick2_kernel<T, 4, 2>), grid, dim3(512), 0, s, g);
       } else {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 32) * g.ksplit);
         mmseg::note_kernel(v3 ? "wgrad_brick2_kernel<CO32,V3>" : "wgrad_brick2_kernel<CO32>");
         if (v3 && g.nmean)
-          hipLaunchKernelGGL((wgrad_brick2_kernel<T, 2, 3, true>), grid, dim3(512), 0, s, g);
+          MMSEG_LAUNCH((wgrad_brick2_kernel<T, 2, 3, true>), grid, dim3(512), 0, s, g);
         else if (v3)
-          hipLaunchKernelGGL((wgrad_brick2_kernel<T, 2, 3>), grid, dim3(512), 0, s, g);
+          MMSEG_LAUNCH((wgrad_brick2_kernel<T, 2, 3>), grid, dim3(512), 0, s, g);
         else
-          hipLaunchKernelGGL((wgrad_brick2_kernel<T, 2, 2>), grid, dim3(512), 0, s, g);
+          MMSEG_LAUNCH((wgrad_brick2_kernel<T, 2, 2>), grid, dim3(512), 0, s, g);
       }
       return mmseg::check_launch("wgrad_brick2");
     }
@@ -4853,7 +4853,7 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
   if (MODE == MODE_CONV3 && g.brick) {
     dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 32) * g.ksplit);
     mmseg::note_kernel("wgrad_brick_kernel");
-    hipLaunchKernelGGL((wgrad_brick_kernel<T>), grid, block, 0, s, g);
+    MMSEG_LAUNCH((wgrad_brick_kernel<T>), grid, block, 0, s, g);
     return mmseg::check_launch("wgrad_brick");
   }
   const int bn = knob("MMSEG_WGRAD_BN", 64);
@@ -4863,18 +4863,18 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
   if (g.Ca % 64 == 0) {
     if (bn == 128) {
       dim3 grid(ceil_div(g.Ncols, 128) * (g.Ca / 64) * g.ksplit);
-      hipLaunchKernelGGL((wgrad_kernel<T, MODE, 2, 2, 2, 4, 64>), grid, block, 0, s, g);
+      MMSEG_LAUNCH((wgrad_kernel<T, MODE, 2, 2, 2, 4, 64>), grid, block, 0, s, g);
     } else {
       dim3 grid(ceil_div(g.Ncols, 64) * (g.Ca / 64) * g.ksplit);
-      hipLaunchKernelGGL((wgrad_kernel<T, MODE, 2, 2, 2, 2, 64>), grid, block, 0, s, g);
+      MMSEG_LAUNCH((wgrad_kernel<T, MODE, 2, 2, 2, 2, 64>), grid, block, 0, s, g);
     }
   } else {
     if (bn == 128) {
       dim3 grid(ceil_div(g.Ncols, 128) * ceil_div(g.Ca, 32) * g.ksplit);
-      hipLaunchKernelGGL((wgrad_kernel<T, MODE, 1, 4, 2, 2, 64>), grid, block, 0, s, g);
+      MMSEG_LAUNCH((wgrad_kernel<T, MODE, 1, 4, 2, 2, 64>), grid, block, 0, s, g);
     } else {
       dim3 grid(ceil_div(g.Ncols, 64) * ceil_div(g.Ca, 32) * g.ksplit);
-      hipLaunchKernelGGL((wgrad_kernel<T, MODE, 1, 4, 2, 1, 64>), grid, block, 0, s, g);
+      MMSEG_LAUNCH((wgrad_kernel<T, MODE, 1, 4, 2, 1, 64>), grid, block, 0, s, g);
     }
   }
   return mmseg::check_launch("wgrad");
@@ -4984,11 +4984,11 @@ int launch_wgrad_reduce(WReduceArgs g, void* stream) {
 #define MMSEG_WRED(SS, NB)                                                                             \
   case SS:                                                                                             \
     if (U >= 16)                                                                                       \
-      hipLaunchKernelGGL((wgrad_reduce_kernel<SS, 16>), dim3(ceil_div(total, NB)), dim3(256), 0, s, g); \
+      MMSEG_LAUNCH((wgrad_reduce_kernel<SS, 16>), dim3(ceil_div(total, NB)), dim3(256), 0, s, g); \
     else if (U >= 8)                                                                                   \
-      hipLaunchKernelGGL((wgrad_reduce_kernel<SS, 8>), dim3(ceil_div(total, NB)), dim3(256), 0, s, g);  \
+      MMSEG_LAUNCH((wgrad_reduce_kernel<SS, 8>), dim3(ceil_div(total, NB)), dim3(256), 0, s, g);  \
     else                                                                                               \
-      hipLaunchKernelGGL((wgrad_reduce_kernel<SS, 4>), dim3(ceil_div(total, NB)), dim3(256), 0, s, g);  \
+      MMSEG_LAUNCH((wgrad_reduce_kernel<SS, 4>), dim3(ceil_div(total, NB)), dim3(256), 0, s, g);  \
     break;
   switch (S) {
     MMSEG_WRED(256, 4)
@@ -5045,9 +5045,9 @@ int mmseg_pack_weight(const float* w, void* dst, int mode, int Co, int Ci, int C
   long long total = (long long)KGp * Cpad * 8;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(pack_weight_kernel<bf16_t>, dim3(ceil_div(total, 256)), dim3(256), 0, s, g, mode);
+    MMSEG_LAUNCH(pack_weight_kernel<bf16_t>, dim3(ceil_div(total, 256)), dim3(256), 0, s, g, mode);
   else
-    hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(ceil_div(total, 256)), dim3(256), 0, s, g, mode);
+    MMSEG_LAUNCH(pack_weight_kernel<float>, dim3(ceil_div(total, 256)), dim3(256), 0, s, g, mode);
   return mmseg::check_launch("pack_weight");
 }
 
@@ -5066,9 +5066,9 @@ int mmseg_pack_conv3_batched(const void* descs, int n, int nblocks, int dtype, v
   MMSEG_REQUIRE(n >= 1 && nblocks >= 1, "pack_conv3_batched: empty table");
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(pack_conv3_batched_kernel<bf16_t>, dim3(nblocks), dim3(256), 0, s, (const Pack3Desc*)descs, n);
+    MMSEG_LAUNCH(pack_conv3_batched_kernel<bf16_t>, dim3(nblocks), dim3(256), 0, s, (const Pack3Desc*)descs, n);
   else
-    hipLaunchKernelGGL(pack_conv3_batched_kernel<float>, dim3(nblocks), dim3(256), 0, s, (const Pack3Desc*)descs, n);
+    MMSEG_LAUNCH(pack_conv3_batched_kernel<float>, dim3(nblocks), dim3(256), 0, s, (const Pack3Desc*)descs, n);
   return mmseg::check_launch("pack_conv3_batched");
 }
 
@@ -5081,10 +5081,10 @@ int mmseg_pack_weights_batched(const void* descs, int n, long long total, int dt
   long long blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(pack_weight_batched_kernel<bf16_t>, dim3((int)blocks), dim3(256), 0, s, (const PackDesc*)descs,
+    MMSEG_LAUNCH(pack_weight_batched_kernel<bf16_t>, dim3((int)blocks), dim3(256), 0, s, (const PackDesc*)descs,
                        n, total);
   else
-    hipLaunchKernelGGL(pack_weight_batched_kernel<float>, dim3((int)blocks), dim3(256), 0, s, (const PackDesc*)descs,
+    MMSEG_LAUNCH(pack_weight_batched_kernel<float>, dim3((int)blocks), dim3(256), 0, s, (const PackDesc*)descs,
                        n, total);
   return mmseg::check_launch("pack_weights_batched");
 }
@@ -5227,7 +5227,7 @@ int mmseg_pack_conv3_fp8(const float* w, int Co, int Ci, int Cip, int KGp, int C
                 "pack_conv3_fp8: bad arguments");
   hipStream_t s = (hipStream_t)stream;
   hipMemsetAsync(dst, 0, (size_t)KGp * Cpad * 8, s);   // K / column padding stays e4m3 zero
-  hipLaunchKernelGGL(pack_conv3_fp8_kernel, dim3(Co), dim3(256), 0, s, w, Ci, Cip, Cpad, (unsigned char*)dst, wdq);
+  MMSEG_LAUNCH(pack_conv3_fp8_kernel, dim3(Co), dim3(256), 0, s, w, Ci, Cip, Cpad, (unsigned char*)dst, wdq);
   return mmseg::check_launch("pack_conv3_fp8");
 }
 
@@ -5445,13 +5445,13 @@ int mmseg_colsum(const void* dy, int ld, int C, long long V, float* part, int nb
   nblk = (int)((V + vps - 1) / vps);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(colsum_partial_kernel<bf16_t>, dim3(nblk), dim3(256), 0, s, (const bf16_t*)dy, ld, C, V, vps,
+    MMSEG_LAUNCH(colsum_partial_kernel<bf16_t>, dim3(nblk), dim3(256), 0, s, (const bf16_t*)dy, ld, C, V, vps,
                        part);
   else
-    hipLaunchKernelGGL(colsum_partial_kernel<float>, dim3(nblk), dim3(256), 0, s, (const float*)dy, ld, C, V, vps,
+    MMSEG_LAUNCH(colsum_partial_kernel<float>, dim3(nblk), dim3(256), 0, s, (const float*)dy, ld, C, V, vps,
                        part);
   if (mmseg::check_launch("colsum_partial")) return 1;
-  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(C), dim3(256), 0, s, part, nblk, C, out, accumulate);
+  MMSEG_LAUNCH(colsum_reduce_kernel, dim3(C), dim3(256), 0, s, part, nblk, C, out, accumulate);
   return mmseg::check_launch("colsum_reduce");
 }
 
@@ -5459,7 +5459,7 @@ int mmseg_colsum(const void* dy, int ld, int C, long long V, float* part, int nb
 // gradient from mmseg_wgrad's CONVT column-sum partials is mmseg_colsum_reduce(bias_part, 8 * ksplit, Cout, ...).
 int mmseg_colsum_reduce(const float* part, int nblk, int C, float* out, int accumulate, void* stream) {
   MMSEG_REQUIRE(nblk >= 1 && C >= 1, "colsum_reduce: nblk, C >= 1");
-  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part, nblk, C, out,
+  MMSEG_LAUNCH(colsum_reduce_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part, nblk, C, out,
                      accumulate);
   return mmseg::check_launch("colsum_reduce");
 }

@@ -248,7 +248,7 @@ int mmseg_modality_normalize(float* x, long long V, int kind, double lo, double 
   hipStream_t s = (hipStream_t)stream;
   if (kind == 0) {
     MMSEG_REQUIRE(hi > lo, "modality_normalize: CT window width must be > 0");
-    hipLaunchKernelGGL(ct_window_kernel, dim3(grid_of(V)), dim3(256), 0, s, x, V, (float)lo, (float)hi,
+    MMSEG_LAUNCH(ct_window_kernel, dim3(grid_of(V)), dim3(256), 0, s, x, V, (float)lo, (float)hi,
                        (float)(hi - lo));
     return mmseg::check_launch("ct_window");
   }
@@ -257,15 +257,15 @@ int mmseg_modality_normalize(float* x, long long V, int kind, double lo, double 
   double* part = (double*)ws;
   double* stats = part + NB;
   if (kind == 1) {
-    hipLaunchKernelGGL(stat_partial_kernel, dim3(NB), dim3(256), 0, s, x, V, 0, stats, part);
-    hipLaunchKernelGGL(stat_final_kernel, dim3(1), dim3(64), 0, s, part, NB, 0, V, stats);
-    hipLaunchKernelGGL(scale_kernel, dim3(grid_of(V)), dim3(256), 0, s, x, V, 0, stats);
+    MMSEG_LAUNCH(stat_partial_kernel, dim3(NB), dim3(256), 0, s, x, V, 0, stats, part);
+    MMSEG_LAUNCH(stat_final_kernel, dim3(1), dim3(64), 0, s, part, NB, 0, V, stats);
+    MMSEG_LAUNCH(scale_kernel, dim3(grid_of(V)), dim3(256), 0, s, x, V, 0, stats);
   } else {
-    hipLaunchKernelGGL(stat_partial_kernel, dim3(NB), dim3(256), 0, s, x, V, 1, stats, part);
-    hipLaunchKernelGGL(stat_final_kernel, dim3(1), dim3(64), 0, s, part, NB, 1, V, stats);
-    hipLaunchKernelGGL(stat_partial_kernel, dim3(NB), dim3(256), 0, s, x, V, 2, stats, part);
-    hipLaunchKernelGGL(stat_final_kernel, dim3(1), dim3(64), 0, s, part, NB, 2, V, stats);
-    hipLaunchKernelGGL(scale_kernel, dim3(grid_of(V)), dim3(256), 0, s, x, V, 1, stats);
+    MMSEG_LAUNCH(stat_partial_kernel, dim3(NB), dim3(256), 0, s, x, V, 1, stats, part);
+    MMSEG_LAUNCH(stat_final_kernel, dim3(1), dim3(64), 0, s, part, NB, 1, V, stats);
+    MMSEG_LAUNCH(stat_partial_kernel, dim3(NB), dim3(256), 0, s, x, V, 2, stats, part);
+    MMSEG_LAUNCH(stat_final_kernel, dim3(1), dim3(64), 0, s, part, NB, 2, V, stats);
+    MMSEG_LAUNCH(scale_kernel, dim3(grid_of(V)), dim3(256), 0, s, x, V, 1, stats);
   }
   return mmseg::check_launch("modality_normalize");
 }
@@ -273,7 +273,7 @@ int mmseg_modality_normalize(float* x, long long V, int kind, double lo, double 
 int mmseg_resize_linear(const float* src, int C, int D, int H, int W, float* dst, int d, int h, int w, void* stream) {
   MMSEG_REQUIRE(C >= 1 && D >= 1 && H >= 1 && W >= 1 && d >= 1 && h >= 1 && w >= 1, "resize_linear: empty shape");
   const long long total = (long long)C * d * h * w;
-  hipLaunchKernelGGL(resize_linear_kernel, dim3(grid_of(total)), dim3(256), 0, (hipStream_t)stream, src, C, D, H, W,
+  MMSEG_LAUNCH(resize_linear_kernel, dim3(grid_of(total)), dim3(256), 0, (hipStream_t)stream, src, C, D, H, W,
                      dst, d, h, w);
   return mmseg::check_launch("resize_linear");
 }
@@ -284,10 +284,10 @@ int mmseg_resize_nearest(const void* src, int label_bytes, int C, int D, int H, 
   const long long total = (long long)C * d * h * w;
   hipStream_t s = (hipStream_t)stream;
   if (label_bytes == 8)
-    hipLaunchKernelGGL(resize_nearest_kernel<int64_t>, dim3(grid_of(total)), dim3(256), 0, s, (const int64_t*)src, D,
+    MMSEG_LAUNCH(resize_nearest_kernel<int64_t>, dim3(grid_of(total)), dim3(256), 0, s, (const int64_t*)src, D,
                        H, W, (int64_t*)dst, d, h, w, total);
   else
-    hipLaunchKernelGGL(resize_nearest_kernel<uint8_t>, dim3(grid_of(total)), dim3(256), 0, s, (const uint8_t*)src, D,
+    MMSEG_LAUNCH(resize_nearest_kernel<uint8_t>, dim3(grid_of(total)), dim3(256), 0, s, (const uint8_t*)src, D,
                        H, W, (uint8_t*)dst, d, h, w, total);
   return mmseg::check_launch("resize_nearest");
 }
@@ -313,9 +313,9 @@ int mmseg_phantom(int S, int ncls, const double* geo, int M, const float* class_
   const long long V = (long long)S * S * S;
   hipStream_t s = (hipStream_t)stream;
   if (label_bytes == 8)
-    hipLaunchKernelGGL(phantom_kernel<int64_t>, dim3(grid_of(V)), dim3(256), 0, s, a, (int64_t*)label, image);
+    MMSEG_LAUNCH(phantom_kernel<int64_t>, dim3(grid_of(V)), dim3(256), 0, s, a, (int64_t*)label, image);
   else
-    hipLaunchKernelGGL(phantom_kernel<uint8_t>, dim3(grid_of(V)), dim3(256), 0, s, a, (uint8_t*)label, image);
+    MMSEG_LAUNCH(phantom_kernel<uint8_t>, dim3(grid_of(V)), dim3(256), 0, s, a, (uint8_t*)label, image);
   return mmseg::check_launch("phantom");
 }
 

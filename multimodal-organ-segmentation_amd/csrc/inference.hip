@@ -90,7 +90,7 @@ int mmseg_window_gather(const float* vol, int N, int C, int D, int H, int W, con
                         int r2, float* out, void* stream) {
   MMSEG_REQUIRE(nw >= 1 && r0 > 0 && r1 > 0 && r2 > 0, "window_gather: empty window set");
   WinGeom g{N, C, D, H, W, r0, r1, r2};
-  hipLaunchKernelGGL(window_gather_kernel, dim3(grid_for((long long)nw * C * r0 * r1 * r2)), dim3(256), 0,
+  MMSEG_LAUNCH(window_gather_kernel, dim3(grid_for((long long)nw * C * r0 * r1 * r2)), dim3(256), 0,
                      (hipStream_t)stream, vol, g, win, nw, out);
   return mmseg::check_launch("window_gather");
 }
@@ -99,7 +99,7 @@ int mmseg_window_accum(const float* logits, int N, int C, int D, int H, int W, i
                        int r1, int r2, float* out, void* stream) {
   MMSEG_REQUIRE(n >= 0 && n < N, "window_accum: sample %d out of range", n);
   WinGeom g{N, C, D, H, W, r0, r1, r2};
-  hipLaunchKernelGGL(window_accum_kernel, dim3(grid_for((long long)C * r0 * r1 * r2)), dim3(256), 0,
+  MMSEG_LAUNCH(window_accum_kernel, dim3(grid_for((long long)C * r0 * r1 * r2)), dim3(256), 0,
                      (hipStream_t)stream, logits, g, n, z0, y0, x0, out);
   return mmseg::check_launch("window_accum");
 }
@@ -107,7 +107,7 @@ int mmseg_window_accum(const float* logits, int N, int C, int D, int H, int W, i
 int mmseg_window_norm(float* out, int N, int C, int D, int H, int W, const float* cz, const float* cy, const float* cx,
                       void* stream) {
   WinGeom g{N, C, D, H, W, 1, 1, 1};
-  hipLaunchKernelGGL(window_norm_kernel, dim3(grid_for((long long)N * C * D * H * W)), dim3(256), 0,
+  MMSEG_LAUNCH(window_norm_kernel, dim3(grid_for((long long)N * C * D * H * W)), dim3(256), 0,
                      (hipStream_t)stream, out, g, cz, cy, cx);
   return mmseg::check_launch("window_norm");
 }

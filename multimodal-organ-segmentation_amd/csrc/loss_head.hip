@@ -1315,9 +1315,9 @@ int mmseg_pack_input(const float* x, int Ctot, int c0, int cnt, int N, long long
   hipStream_t s = (hipStream_t)stream;
   const int grid = grid_for((long long)N * V);
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(pack_input_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, x, Ctot, c0, cnt, V, N, (bf16_t*)out);
+    MMSEG_LAUNCH(pack_input_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, x, Ctot, c0, cnt, V, N, (bf16_t*)out);
   else
-    hipLaunchKernelGGL(pack_input_kernel<float>, dim3(grid), dim3(256), 0, s, x, Ctot, c0, cnt, V, N, (float*)out);
+    MMSEG_LAUNCH(pack_input_kernel<float>, dim3(grid), dim3(256), 0, s, x, Ctot, c0, cnt, V, N, (float*)out);
   return mmseg::check_launch("pack_input");
 }
 
@@ -1327,10 +1327,10 @@ int mmseg_pack_input_compact(const float* x, int Ctot, int c0, int cnt, int N, l
   hipStream_t s = (hipStream_t)stream;
   const int grid = grid_for((long long)N * V);
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(pack_input_compact_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, x, Ctot, c0, cnt, V, N,
+    MMSEG_LAUNCH(pack_input_compact_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, x, Ctot, c0, cnt, V, N,
                        (bf16_t*)out);
   else
-    hipLaunchKernelGGL(pack_input_compact_kernel<float>, dim3(grid), dim3(256), 0, s, x, Ctot, c0, cnt, V, N,
+    MMSEG_LAUNCH(pack_input_compact_kernel<float>, dim3(grid), dim3(256), 0, s, x, Ctot, c0, cnt, V, N,
                        (float*)out);
   return mmseg::check_launch("pack_input_compact");
 }
@@ -1344,7 +1344,7 @@ int mmseg_head_fwd(const void* x, int ldx, int Cin, const float* W, const float*
     using T = decltype(tag);
     constexpr int CG = decltype(cg_c)::value, CC = decltype(cc_c)::value;
     if (Cin != CG * 8 || C != CC) return false;
-    hipLaunchKernelGGL((head_fwd_u_kernel<T, CG, CC>), dim3(ugrid), dim3(256), 0, s, (const T*)x, ldx, W, b, dscale,
+    MMSEG_LAUNCH((head_fwd_u_kernel<T, CG, CC>), dim3(ugrid), dim3(256), 0, s, (const T*)x, ldx, W, b, dscale,
                        V, N, logits);
     return true;
   };
@@ -1361,10 +1361,10 @@ int mmseg_head_fwd(const void* x, int ldx, int Cin, const float* W, const float*
   const int grid = grid_for((long long)N * V);
   const size_t shm = (size_t)C * Cin * sizeof(float);
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(head_fwd_kernel<bf16_t>, dim3(grid), dim3(256), shm, s, (const bf16_t*)x, ldx, Cin, W, b, dscale,
+    MMSEG_LAUNCH(head_fwd_kernel<bf16_t>, dim3(grid), dim3(256), shm, s, (const bf16_t*)x, ldx, Cin, W, b, dscale,
                        C, V, N, logits);
   else
-    hipLaunchKernelGGL(head_fwd_kernel<float>, dim3(grid), dim3(256), shm, s, (const float*)x, ldx, Cin, W, b, dscale,
+    MMSEG_LAUNCH(head_fwd_kernel<float>, dim3(grid), dim3(256), shm, s, (const float*)x, ldx, Cin, W, b, dscale,
                        C, V, N, logits);
   return mmseg::check_launch("head_fwd");
 }
@@ -1388,20 +1388,20 @@ int mmseg_head_bwd(const void* x, int ldx, int Cin, const float* W, const float*
   const size_t shm2 = 0;
   // weight-gradient partials first: dx may alias x (the engine reuses the feature buffer)
   if (dtype == MMSEG_BF16) {
-    hipLaunchKernelGGL(head_wgrad_partial<bf16_t>, dim3((int)nblk), dim3(256), shm2, s, (const bf16_t*)x, ldx, dlogits,
+    MMSEG_LAUNCH(head_wgrad_partial<bf16_t>, dim3((int)nblk), dim3(256), shm2, s, (const bf16_t*)x, ldx, dlogits,
                        dscale, C, Cin, V, N, vpc, ws);
     if (dx)
-      hipLaunchKernelGGL(head_dgrad_q_kernel<bf16_t>, dim3(qgrid), dim3(256), shm, s, dlogits, W, dscale, C, Cin, V,
+      MMSEG_LAUNCH(head_dgrad_q_kernel<bf16_t>, dim3(qgrid), dim3(256), shm, s, dlogits, W, dscale, C, Cin, V,
                          N, (bf16_t*)dx, lddx);
   } else {
-    hipLaunchKernelGGL(head_wgrad_partial<float>, dim3((int)nblk), dim3(256), shm2, s, (const float*)x, ldx, dlogits,
+    MMSEG_LAUNCH(head_wgrad_partial<float>, dim3((int)nblk), dim3(256), shm2, s, (const float*)x, ldx, dlogits,
                        dscale, C, Cin, V, N, vpc, ws);
     if (dx)
-      hipLaunchKernelGGL(head_dgrad_q_kernel<float>, dim3(qgrid), dim3(256), shm, s, dlogits, W, dscale, C, Cin, V, N,
+      MMSEG_LAUNCH(head_dgrad_q_kernel<float>, dim3(qgrid), dim3(256), shm, s, dlogits, W, dscale, C, Cin, V, N,
                          (float*)dx, lddx);
   }
   if (mmseg::check_launch("head_bwd")) return 1;
-  hipLaunchKernelGGL(head_wgrad_reduce, dim3(ceil_div(C * Cin + C, 4)), dim3(256), 0, s, ws, (int)nblk, C, Cin, gW,
+  MMSEG_LAUNCH(head_wgrad_reduce, dim3(ceil_div(C * Cin + C, 4)), dim3(256), 0, s, ws, (int)nblk, C, Cin, gW,
                      gb, accumulate);
   return mmseg::check_launch("head_wgrad_reduce");
 }
@@ -1426,7 +1426,7 @@ int mmseg_loss_fwd(const float* logits, const void* labels, int label_bytes, int
   hipStream_t s = (hipStream_t)stream;
   auto stats = [&](auto lt, auto cc) {
     using LT = decltype(lt);
-    hipLaunchKernelGGL((loss_stats_kernel<LT, decltype(cc)::value>), dim3(nch, N), dim3(256), 0, s, logits,
+    MMSEG_LAUNCH((loss_stats_kernel<LT, decltype(cc)::value>), dim3(nch, N), dim3(256), 0, s, logits,
                        (const LT*)labels, C, V, vpc, cfg, part);
   };
   auto stats_c = [&](auto lt) {
@@ -1440,7 +1440,7 @@ int mmseg_loss_fwd(const float* logits, const void* labels, int label_bytes, int
   if (mmseg::check_launch("loss_stats")) return 1;
   const size_t shm = sizeof(double) * ((size_t)N * (3 * C + 3) + (size_t)N * C);
   MMSEG_REQUIRE(shm <= 64 * 1024, "loss: batch too large for the finalize pass (N=%d, C=%d)", N, C);
-  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), shm, s, part, N, C, nch, cfg, loss_out, coef);
+  MMSEG_LAUNCH(loss_finalize_kernel, dim3(1), dim3(1024), shm, s, part, N, C, nch, cfg, loss_out, coef);
   return mmseg::check_launch("loss_finalize");
 }
 
@@ -1476,13 +1476,13 @@ int mmseg_head_loss_fwd(const void* x, int ldx, int Cin, const float* nmean, con
     constexpr int G = decltype(g_c)::value, NC = decltype(nc_c)::value;
     (void)NC;                 // the statistics kernel does not depend on NC: one instance per (T, G, LT)
     mmseg::note_kernel("head_loss_stats_kernel");
-    hipLaunchKernelGGL((head_loss_stats_kernel<T, G, LT>), dim3(nch, N), dim3(256), 0, s, (const T*)x, ldx, nmean,
+    MMSEG_LAUNCH((head_loss_stats_kernel<T, G, LT>), dim3(nch, N), dim3(256), 0, s, (const T*)x, ldx, nmean,
                        nrstd, W, b, dscale, C, (const LT*)labels, V, vpc, cfg, part);
   });
   if (mmseg::check_launch("head_loss_stats")) return 1;
   const size_t shm = sizeof(double) * ((size_t)N * (3 * C + 3) + (size_t)N * C);
   MMSEG_REQUIRE(shm <= 64 * 1024, "head_loss: batch too large for the finalize pass (N=%d, C=%d)", N, C);
-  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), shm, s, part, N, C, nch, cfg, loss_out, coef);
+  MMSEG_LAUNCH(loss_finalize_kernel, dim3(1), dim3(1024), shm, s, part, N, C, nch, cfg, loss_out, coef);
   return mmseg::check_launch("loss_finalize");
 }
 
@@ -1537,16 +1537,16 @@ int mmseg_head_loss_bwd_in(const void* x, int ldx, int Cin, const float* nmean, 
     constexpr int G = decltype(g_c)::value, NC = decltype(nc_c)::value;
     mmseg::note_kernel("head_loss_bwd_kernel");
     if (dscale)
-      hipLaunchKernelGGL((head_loss_bwd_kernel<T, G, NC, LT, true>), dim3(nch, N), dim3(256), 0, s, (const T*)x, ldx,
+      MMSEG_LAUNCH((head_loss_bwd_kernel<T, G, NC, LT, true>), dim3(nch, N), dim3(256), 0, s, (const T*)x, ldx,
                          nmean, nrstd, W, b, dscale, C, (const LT*)labels, V, vpc, cfg, coef, gout, gconst, (T*)dx,
                          lddx, wpart, inpart);
     else
-      hipLaunchKernelGGL((head_loss_bwd_kernel<T, G, NC, LT, false>), dim3(nch, N), dim3(256), 0, s, (const T*)x,
+      MMSEG_LAUNCH((head_loss_bwd_kernel<T, G, NC, LT, false>), dim3(nch, N), dim3(256), 0, s, (const T*)x,
                          ldx, nmean, nrstd, W, b, dscale, C, (const LT*)labels, V, vpc, cfg, coef, gout, gconst,
                          (T*)dx, lddx, wpart, inpart);
   });
   if (mmseg::check_launch("head_loss_bwd")) return 1;
-  hipLaunchKernelGGL(head_wgrad_reduce, dim3(ceil_div(C * Cin + C, 4)), dim3(256), 0, s, wpart, N * nch, C, Cin, gW,
+  MMSEG_LAUNCH(head_wgrad_reduce, dim3(ceil_div(C * Cin + C, 4)), dim3(256), 0, s, wpart, N * nch, C, Cin, gW,
                      gb, accumulate);
   return mmseg::check_launch("head_wgrad_reduce");
 }
@@ -1565,7 +1565,7 @@ int mmseg_loss_bwd(const float* logits, const void* labels, int label_bytes, int
     using LT = decltype(lt);
     constexpr int CC = decltype(cc)::value;
     const int grid = grid_for(CC > 0 ? ceil_div((long long)N * V, 4) : (long long)N * V);
-    hipLaunchKernelGGL((loss_bwd_kernel<LT, CC>), dim3(grid), dim3(256), 0, s, logits, (const LT*)labels, C, V, N, cfg,
+    MMSEG_LAUNCH((loss_bwd_kernel<LT, CC>), dim3(grid), dim3(256), 0, s, logits, (const LT*)labels, C, V, N, cfg,
                        coef, gout, gconst, dlogits);
   };
   auto bwd_c = [&](auto lt) {
@@ -1586,10 +1586,10 @@ int mmseg_dice_counts(const float* logits, const void* labels, int label_bytes, 
   hipStream_t s = (hipStream_t)stream;
   const int grid = grid_for((long long)N * V) > 2048 ? 2048 : grid_for((long long)N * V);
   if (label_bytes == 8)
-    hipLaunchKernelGGL(dice_counts_kernel<int64_t>, dim3(grid), dim3(256), 0, s, logits, (const int64_t*)labels, C, V,
+    MMSEG_LAUNCH(dice_counts_kernel<int64_t>, dim3(grid), dim3(256), 0, s, logits, (const int64_t*)labels, C, V,
                        N, counts, (int64_t*)pred_out);
   else
-    hipLaunchKernelGGL(dice_counts_kernel<uint8_t>, dim3(grid), dim3(256), 0, s, logits, (const uint8_t*)labels, C, V,
+    MMSEG_LAUNCH(dice_counts_kernel<uint8_t>, dim3(grid), dim3(256), 0, s, logits, (const uint8_t*)labels, C, V,
                        N, counts, (uint8_t*)pred_out);
   return mmseg::check_launch("dice_counts");
 }
@@ -1602,7 +1602,7 @@ int mmseg_dice_counts_idx(const void* pred, int pred_bytes, const void* labels, 
   hipStream_t s = (hipStream_t)stream;
   const int grid = grid_for(total) > 2048 ? 2048 : grid_for(total);
 #define DCI(PT, LT) \
-  hipLaunchKernelGGL((dice_counts_idx_kernel<PT, LT>), dim3(grid), dim3(256), 0, s, (const PT*)pred, (const LT*)labels, C, total, counts)
+  MMSEG_LAUNCH((dice_counts_idx_kernel<PT, LT>), dim3(grid), dim3(256), 0, s, (const PT*)pred, (const LT*)labels, C, total, counts)
   if (pred_bytes == 8 && label_bytes == 8) DCI(int64_t, int64_t);
   else if (pred_bytes == 8) DCI(int64_t, uint8_t);
   else if (label_bytes == 8) DCI(uint8_t, int64_t);
@@ -1635,16 +1635,16 @@ static int adamw_launch(float* p, const float* g, float* m, float* v, long long 
     const long long n4 = n / 4;
     long long b4 = (n4 + 511) / 512;   // 2 float4 per thread
     if (b4 > 8192) b4 = 8192;
-    hipLaunchKernelGGL(adamw4_kernel, dim3((int)b4), dim3(256), 0, stream, reinterpret_cast<float4*>(p),
+    MMSEG_LAUNCH(adamw4_kernel, dim3((int)b4), dim3(256), 0, stream, reinterpret_cast<float4*>(p),
                        reinterpret_cast<const float4*>(g), reinterpret_cast<float4*>(m), reinterpret_cast<float4*>(v),
                        n4, hv, hp, skip);
     if (n % 4)
-      hipLaunchKernelGGL(adamw_kernel, dim3(1), dim3(64), 0, stream, p + 4 * n4, g + 4 * n4, m + 4 * n4, v + 4 * n4,
+      MMSEG_LAUNCH(adamw_kernel, dim3(1), dim3(64), 0, stream, p + 4 * n4, g + 4 * n4, m + 4 * n4, v + 4 * n4,
                          n - 4 * n4, hv, hp, skip);
     return mmseg::check_launch("adamw");
   }
   const int grid = grid_for(n) > 4096 ? 4096 : grid_for(n);
-  hipLaunchKernelGGL(adamw_kernel, dim3(grid), dim3(256), 0, stream, p, g, m, v, n, hv, hp, skip);
+  MMSEG_LAUNCH(adamw_kernel, dim3(grid), dim3(256), 0, stream, p, g, m, v, n, hv, hp, skip);
   return mmseg::check_launch("adamw");
 }
 

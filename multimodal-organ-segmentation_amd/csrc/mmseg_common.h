@@ -10,6 +10,7 @@
 // accumulation is fp32.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <stddef.h>
 
@@ -29,7 +30,25 @@ int check_launch(const char* what);
 // Record the main kernel an entry point launched (mmseg_last_kernel(); the
 // per-kernel timer names its regions with it, matching rocprofv3's names).
 void note_kernel(const char* name);
+// Launch timing (mmseg_timing_begin / _end / _count / _get): while it is on, every kernel goes through
+// hipExtLaunchKernelGGL with a start / stop event pair that the runtime stamps from the dispatch itself --
+// the kernel's own begin / end, as rocprofv3's kernel trace reports them -- instead of event-record packets
+// around the launch, which add the barrier / dispatch latency between them to every kernel.
+bool timing_on();
+void timing_events(const char* name, hipEvent_t* start, hipEvent_t* stop);
 }  // namespace mmseg
+
+// Every kernel launch of the library: hipLaunchKernelGGL, or the timed form while launch timing is on.
+#define MMSEG_LAUNCH(K, GRID, BLOCK, SHM, STRM, ...)                                         \
+  do {                                                                                     \
+    if (mmseg::timing_on()) {                                                              \
+      hipEvent_t mmseg_ts_, mmseg_te_;                                                     \
+      mmseg::timing_events(#K, &mmseg_ts_, &mmseg_te_);                                    \
+      hipExtLaunchKernelGGL(K, GRID, BLOCK, SHM, STRM, mmseg_ts_, mmseg_te_, 0, ##__VA_ARGS__); \
+    } else {                                                                               \
+      hipLaunchKernelGGL(K, GRID, BLOCK, SHM, STRM, ##__VA_ARGS__);                        \
+    }                                                                                      \
+  } while (0)
 
 #define MMSEG_REQUIRE(cond, ...)              \
   do {                                        \

@@ -1448,13 +1448,13 @@ int mmseg_instnorm_stats(const void* x, int ldx, int N, long long V, int C, floa
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(nch, N);
   if (dtype == MMSEG_BF16) {
-    hipLaunchKernelGGL(in_stats_partial<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, (int)V, C, (int)vpc,
+    MMSEG_LAUNCH(in_stats_partial<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, (int)V, C, (int)vpc,
                        ws);
-    hipLaunchKernelGGL(in_stats_finalize<bf16_t>, dim3(N * C), dim3(256), 0, s, (const bf16_t*)x, ldx,
+    MMSEG_LAUNCH(in_stats_finalize<bf16_t>, dim3(N * C), dim3(256), 0, s, (const bf16_t*)x, ldx,
                        V, N, C, nch, vpc, ws, eps, mean, mean_ld, rstd);
   } else {
-    hipLaunchKernelGGL(in_stats_partial<float>, grid, dim3(256), 0, s, (const float*)x, ldx, (int)V, C, (int)vpc, ws);
-    hipLaunchKernelGGL(in_stats_finalize<float>, dim3(N * C), dim3(256), 0, s, (const float*)x, ldx, V,
+    MMSEG_LAUNCH(in_stats_partial<float>, grid, dim3(256), 0, s, (const float*)x, ldx, (int)V, C, (int)vpc, ws);
+    MMSEG_LAUNCH(in_stats_finalize<float>, dim3(N * C), dim3(256), 0, s, (const float*)x, ldx, V,
                        N, C, nch, vpc, ws, eps, mean, mean_ld, rstd);
   }
   return mmseg::check_launch("instnorm_stats");
@@ -1464,7 +1464,7 @@ int mmseg_instnorm_stats(const void* x, int ldx, int N, long long V, int C, floa
 int mmseg_instnorm_stats_bricks(const float* part, int N, int C, int nb, int cnt, float eps, float* mean, int mean_ld,
                                 float* rstd, void* stream) {
   MMSEG_REQUIRE(nb >= 1 && cnt >= 1, "instnorm_stats_bricks: nb, cnt >= 1");
-  hipLaunchKernelGGL(in_stats_from_bricks, dim3(ceil_div(N * C, 4)), dim3(256), 0, (hipStream_t)stream, part, N, C,
+  MMSEG_LAUNCH(in_stats_from_bricks, dim3(ceil_div(N * C, 4)), dim3(256), 0, (hipStream_t)stream, part, N, C,
                      nb, cnt, eps, mean, mean_ld, rstd);
   return mmseg::check_launch("instnorm_stats_bricks");
 }
@@ -1493,16 +1493,16 @@ int mmseg_instnorm_fwd(const void* x, int ldx, void* y, int ldy, int N, long lon
     using T = decltype(tag);
     constexpr bool R = decltype(relu_c)::value;
     if (knob_small_t() == 1024)
-      hipLaunchKernelGGL((in_small_fwd_1k<T, R>), grid, dim3(SMALL_T1K), 0, s, (const T*)x, ldx, (T*)y, ldy, (int)V, C,
+      MMSEG_LAUNCH((in_small_fwd_1k<T, R>), grid, dim3(SMALL_T1K), 0, s, (const T*)x, ldx, (T*)y, ldy, (int)V, C,
                          eps, mean, mean_ld, rstd);
     else if (knob_small_reg() && V <= SMALL_T)
-      hipLaunchKernelGGL((in_small_fwd_r<T, R, 1>), grid, dim3(SMALL_T), 0, s, (const T*)x, ldx, (T*)y, ldy, (int)V, C,
+      MMSEG_LAUNCH((in_small_fwd_r<T, R, 1>), grid, dim3(SMALL_T), 0, s, (const T*)x, ldx, (T*)y, ldy, (int)V, C,
                          eps, mean, mean_ld, rstd);
     else if (knob_small_reg() && V <= 8 * SMALL_T)
-      hipLaunchKernelGGL((in_small_fwd_r<T, R, 8>), grid, dim3(SMALL_T), 0, s, (const T*)x, ldx, (T*)y, ldy, (int)V, C,
+      MMSEG_LAUNCH((in_small_fwd_r<T, R, 8>), grid, dim3(SMALL_T), 0, s, (const T*)x, ldx, (T*)y, ldy, (int)V, C,
                          eps, mean, mean_ld, rstd);
     else
-      hipLaunchKernelGGL((in_small_fwd<T, R>), grid, dim3(SMALL_T), 0, s, (const T*)x, ldx, (T*)y, ldy, (int)V, C, eps,
+      MMSEG_LAUNCH((in_small_fwd<T, R>), grid, dim3(SMALL_T), 0, s, (const T*)x, ldx, (T*)y, ldy, (int)V, C, eps,
                          mean, mean_ld, rstd);
   };
   if (dtype == MMSEG_BF16) {
@@ -1529,17 +1529,17 @@ int mmseg_instnorm_apply(const void* x, int ldx, void* y, int ldy, int N, long l
   const dim3 grid(apply_chunks(V, C, &vpc), N);
   if (dtype == MMSEG_BF16) {
     if (relu)
-      hipLaunchKernelGGL((in_relu_apply<bf16_t, true>), grid, dim3(256), 0, s, (const bf16_t*)x, ldx, (bf16_t*)y, ldy,
+      MMSEG_LAUNCH((in_relu_apply<bf16_t, true>), grid, dim3(256), 0, s, (const bf16_t*)x, ldx, (bf16_t*)y, ldy,
                          (int)V, C, vpc, mean, rstd);
     else
-      hipLaunchKernelGGL((in_relu_apply<bf16_t, false>), grid, dim3(256), 0, s, (const bf16_t*)x, ldx, (bf16_t*)y,
+      MMSEG_LAUNCH((in_relu_apply<bf16_t, false>), grid, dim3(256), 0, s, (const bf16_t*)x, ldx, (bf16_t*)y,
                          ldy, (int)V, C, vpc, mean, rstd);
   } else {
     if (relu)
-      hipLaunchKernelGGL((in_relu_apply<float, true>), grid, dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy,
+      MMSEG_LAUNCH((in_relu_apply<float, true>), grid, dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy,
                          (int)V, C, vpc, mean, rstd);
     else
-      hipLaunchKernelGGL((in_relu_apply<float, false>), grid, dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy,
+      MMSEG_LAUNCH((in_relu_apply<float, false>), grid, dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy,
                          (int)V, C, vpc, mean, rstd);
   }
   return mmseg::check_launch("instnorm_apply");
@@ -1596,30 +1596,30 @@ int mmseg_instnorm_bwd_part(const void* x, int ldx, const float* mean, const flo
     using T = decltype(tag);
     constexpr bool R = decltype(relu_c)::value;
     if (part_in) {
-      hipLaunchKernelGGL(in_bwd_finalize, dim3(N * C), dim3(256), 0, s, part_in, N, C, nchunk_in, V, coef);
-      hipLaunchKernelGGL((in_bwd_apply<T, R>), agrid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, coef,
+      MMSEG_LAUNCH(in_bwd_finalize, dim3(N * C), dim3(256), 0, s, part_in, N, C, nchunk_in, V, coef);
+      MMSEG_LAUNCH((in_bwd_apply<T, R>), agrid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, coef,
                          (T*)dx, lddx, (int)V, C, D, H, W, avpc);
       return;
     }
     if (small) {
       if (knob_small_t() == 1024)
-        hipLaunchKernelGGL((in_small_bwd_1k<T, R>), dim3(C / 8, N), dim3(SMALL_T1K), 0, s, (const T*)x, ldx, mean, rstd,
+        MMSEG_LAUNCH((in_small_bwd_1k<T, R>), dim3(C / 8, N), dim3(SMALL_T1K), 0, s, (const T*)x, ldx, mean, rstd,
                            src, (T*)dx, lddx, (int)V, C, D, H, W);
       else if (knob_small_reg() && V <= SMALL_T)
-        hipLaunchKernelGGL((in_small_bwd_r<T, R, 1>), dim3(C / 8, N), dim3(SMALL_T), 0, s, (const T*)x, ldx, mean, rstd,
+        MMSEG_LAUNCH((in_small_bwd_r<T, R, 1>), dim3(C / 8, N), dim3(SMALL_T), 0, s, (const T*)x, ldx, mean, rstd,
                            src, (T*)dx, lddx, (int)V, C, D, H, W);
       else if (knob_small_reg() && V <= 8 * SMALL_T)
-        hipLaunchKernelGGL((in_small_bwd_r<T, R, 8>), dim3(C / 8, N), dim3(SMALL_T), 0, s, (const T*)x, ldx, mean, rstd,
+        MMSEG_LAUNCH((in_small_bwd_r<T, R, 8>), dim3(C / 8, N), dim3(SMALL_T), 0, s, (const T*)x, ldx, mean, rstd,
                            src, (T*)dx, lddx, (int)V, C, D, H, W);
       else
-        hipLaunchKernelGGL((in_small_bwd<T, R>), dim3(C / 8, N), dim3(SMALL_T), 0, s, (const T*)x, ldx, mean, rstd, src,
+        MMSEG_LAUNCH((in_small_bwd<T, R>), dim3(C / 8, N), dim3(SMALL_T), 0, s, (const T*)x, ldx, mean, rstd, src,
                            (T*)dx, lddx, (int)V, C, D, H, W);
       return;
     }
-    hipLaunchKernelGGL((in_bwd_partial<T, R>), grid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, (int)V, C, D,
+    MMSEG_LAUNCH((in_bwd_partial<T, R>), grid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, (int)V, C, D,
                        H, W, (int)vpc, part);
-    hipLaunchKernelGGL(in_bwd_finalize, dim3(N * C), dim3(256), 0, s, part, N, C, nch, V, coef);
-    hipLaunchKernelGGL((in_bwd_apply<T, R>), agrid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, coef, (T*)dx,
+    MMSEG_LAUNCH(in_bwd_finalize, dim3(N * C), dim3(256), 0, s, part, N, C, nch, V, coef);
+    MMSEG_LAUNCH((in_bwd_apply<T, R>), agrid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, coef, (T*)dx,
                        lddx, (int)V, C, D, H, W, avpc);
   };
   if (dtype == MMSEG_BF16) {
@@ -1651,7 +1651,7 @@ int mmseg_instnorm_bwd_coef(const void* x, int ldx, const float* mean, const flo
     auto run = [&](auto tag, auto relu_c) {
       using T = decltype(tag);
       constexpr bool R = decltype(relu_c)::value;
-      hipLaunchKernelGGL((in_bwd_partial<T, R>), grid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, (int)V, C,
+      MMSEG_LAUNCH((in_bwd_partial<T, R>), grid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, (int)V, C,
                          D, H, W, (int)vpc, ws);
     };
     if (dtype == MMSEG_BF16) {
@@ -1664,7 +1664,7 @@ int mmseg_instnorm_bwd_coef(const void* x, int ldx, const float* mean, const flo
     part_in = ws;
     nchunk_in = nch;
   }
-  hipLaunchKernelGGL(in_bwd_finalize, dim3(N * C), dim3(256), 0, s, part_in, N, C, nchunk_in, V, coef);
+  MMSEG_LAUNCH(in_bwd_finalize, dim3(N * C), dim3(256), 0, s, part_in, N, C, nchunk_in, V, coef);
   return mmseg::check_launch("instnorm_bwd_coef");
 }
 
@@ -1675,11 +1675,11 @@ int mmseg_maxpool2_fwd(const void* x, int ldx, void* y, int ldy, uint8_t* idx, i
   hipStream_t s = (hipStream_t)stream;
   const int grid = grid_for((long long)N * (D / 2) * (H / 2) * (W / 2) * (C / 8));
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(maxpool2_fwd<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, ldx, (bf16_t*)y, ldy, idx,
-                       N, D, H, W, C);
+    MMSEG_LAUNCH(maxpool2_fwd<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, ldx, (bf16_t*)y, ldy, idx,
+                       N, D, H, W, C, (const float*)nullptr, (const float*)nullptr);
   else
-    hipLaunchKernelGGL(maxpool2_fwd<float>, dim3(grid), dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy, idx, N,
-                       D, H, W, C);
+    MMSEG_LAUNCH(maxpool2_fwd<float>, dim3(grid), dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy, idx, N,
+                       D, H, W, C, (const float*)nullptr, (const float*)nullptr);
   return mmseg::check_launch("maxpool2_fwd");
 }
 
@@ -1692,10 +1692,10 @@ int mmseg_maxpool2_norm_fwd(const void* x, int ldx, const float* mean, const flo
   hipStream_t s = (hipStream_t)stream;
   const int grid = grid_for((long long)N * (D / 2) * (H / 2) * (W / 2) * (C / 8));
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL((maxpool2_fwd<bf16_t, true>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x, ldx, (bf16_t*)y,
+    MMSEG_LAUNCH((maxpool2_fwd<bf16_t, true>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x, ldx, (bf16_t*)y,
                        ldy, idx, N, D, H, W, C, mean, rstd);
   else
-    hipLaunchKernelGGL((maxpool2_fwd<float, true>), dim3(grid), dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy,
+    MMSEG_LAUNCH((maxpool2_fwd<float, true>), dim3(grid), dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy,
                        idx, N, D, H, W, C, mean, rstd);
   return mmseg::check_launch("maxpool2_norm_fwd");
 }
@@ -1723,11 +1723,11 @@ int mmseg_fuse_norm_fwd(const void* const* srcs, const int* lds, const float* co
   auto run = [&](auto tag) {
     using T = decltype(tag);
     if (cm && M == 2)
-      hipLaunchKernelGGL((fuse_norm_fwd_m<T, 2>), dim3(grid), dim3(256), 0, st, s, (T*)out, ldo, V, N, C);
+      MMSEG_LAUNCH((fuse_norm_fwd_m<T, 2>), dim3(grid), dim3(256), 0, st, s, (T*)out, ldo, V, N, C);
     else if (cm && M == 3)
-      hipLaunchKernelGGL((fuse_norm_fwd_m<T, 3>), dim3(grid), dim3(256), 0, st, s, (T*)out, ldo, V, N, C);
+      MMSEG_LAUNCH((fuse_norm_fwd_m<T, 3>), dim3(grid), dim3(256), 0, st, s, (T*)out, ldo, V, N, C);
     else
-      hipLaunchKernelGGL((fuse_fwd<T, true>), dim3(grid), dim3(256), 0, st, s, (T*)out, ldo, V, N, C);
+      MMSEG_LAUNCH((fuse_fwd<T, true>), dim3(grid), dim3(256), 0, st, s, (T*)out, ldo, V, N, C);
   };
   if (dtype == MMSEG_BF16) run(bf16_t{});
   else run(float{});
@@ -1750,16 +1750,16 @@ int mmseg_fuse_fwd(const void* const* srcs, const int* lds, int M, float wconst,
   hipStream_t st = (hipStream_t)stream;
   const int grid = grid_for((long long)N * V * (C / 8));
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(fuse_fwd<bf16_t>, dim3(grid), dim3(256), 0, st, s, (bf16_t*)out, ldo, V, N, C);
+    MMSEG_LAUNCH(fuse_fwd<bf16_t>, dim3(grid), dim3(256), 0, st, s, (bf16_t*)out, ldo, V, N, C);
   else
-    hipLaunchKernelGGL(fuse_fwd<float>, dim3(grid), dim3(256), 0, st, s, (float*)out, ldo, V, N, C);
+    MMSEG_LAUNCH(fuse_fwd<float>, dim3(grid), dim3(256), 0, st, s, (float*)out, ldo, V, N, C);
   return mmseg::check_launch("fuse_fwd");
 }
 
 int mmseg_attn_gate_fwd(const float* pooled, const float* W1, const float* b1, const float* W2, const float* b2,
                         float* hbuf, float* wts, int N, int MC, int Hd, int M, void* stream) {
   MMSEG_REQUIRE(M <= 4, "attn gate: M <= 4");
-  hipLaunchKernelGGL(attn_gate_fwd, dim3(N), dim3(256), Hd * sizeof(float), (hipStream_t)stream, pooled, W1, b1, W2,
+  MMSEG_LAUNCH(attn_gate_fwd, dim3(N), dim3(256), Hd * sizeof(float), (hipStream_t)stream, pooled, W1, b1, W2,
                      b2, hbuf, wts, MC, Hd, M);
   return mmseg::check_launch("attn_gate_fwd");
 }
@@ -1784,15 +1784,15 @@ int mmseg_attn_gate_bwd(const void* const* srcs, const int* lds, int M, const vo
   nch = (V + vpc - 1) / vpc;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(fuse_dot_partial<bf16_t>, dim3((int)nch, N), dim3(256), 0, st, s, (const bf16_t*)dfused, ldd, V,
+    MMSEG_LAUNCH(fuse_dot_partial<bf16_t>, dim3((int)nch, N), dim3(256), 0, st, s, (const bf16_t*)dfused, ldd, V,
                        C, vpc, ws);
   else
-    hipLaunchKernelGGL(fuse_dot_partial<float>, dim3((int)nch, N), dim3(256), 0, st, s, (const float*)dfused, ldd, V, C,
+    MMSEG_LAUNCH(fuse_dot_partial<float>, dim3((int)nch, N), dim3(256), 0, st, s, (const float*)dfused, ldd, V, C,
                        vpc, ws);
   if (mmseg::check_launch("fuse_dot_partial")) return 1;
   const int MC = M * C;
   const size_t shm = (size_t)(N * M + N * Hd) * sizeof(float);
-  hipLaunchKernelGGL(attn_gate_bwd, dim3(1), dim3(256), shm, st, ws, (int)nch, pooled, W1, W2, hbuf, wts, beta, gW1,
+  MMSEG_LAUNCH(attn_gate_bwd, dim3(1), dim3(256), shm, st, ws, (int)nch, pooled, W1, W2, hbuf, wts, beta, gW1,
                      gb1, gW2, gb2, N, MC, Hd, M, V, accumulate);
   return mmseg::check_launch("attn_gate_bwd");
 }

@@ -402,10 +402,10 @@ int mmseg_stem_fwd_stats(const void* x, int ldx, int cr, const float* w, const f
     using T = decltype(tag);
     constexpr int RN = decltype(rn)::value;
     switch (cr) {
-      case 1: hipLaunchKernelGGL((stem_fwd_kernel<T, RN, 1>), grid, dim3(256), 0, s, g); break;
-      case 2: hipLaunchKernelGGL((stem_fwd_kernel<T, RN, 2>), grid, dim3(256), 0, s, g); break;
-      case 3: hipLaunchKernelGGL((stem_fwd_kernel<T, RN, 3>), grid, dim3(256), 0, s, g); break;
-      default: hipLaunchKernelGGL((stem_fwd_kernel<T, RN, 4>), grid, dim3(256), 0, s, g); break;
+      case 1: MMSEG_LAUNCH((stem_fwd_kernel<T, RN, 1>), grid, dim3(256), 0, s, g); break;
+      case 2: MMSEG_LAUNCH((stem_fwd_kernel<T, RN, 2>), grid, dim3(256), 0, s, g); break;
+      case 3: MMSEG_LAUNCH((stem_fwd_kernel<T, RN, 3>), grid, dim3(256), 0, s, g); break;
+      default: MMSEG_LAUNCH((stem_fwd_kernel<T, RN, 4>), grid, dim3(256), 0, s, g); break;
     }
   };
   if (dtype == MMSEG_BF16) {
@@ -462,18 +462,18 @@ int mmseg_stem_wgrad_inb(const void* dy, int lddy, const void* x, int ldx, int c
     constexpr int RM = decltype(rm)::value;
     if (inx) {
       switch (cr) {
-        case 1: hipLaunchKernelGGL((stem_wgrad_kernel<T, RM, 2, 1, true>), grid, blk, 0, s, g); break;
-        case 2: hipLaunchKernelGGL((stem_wgrad_kernel<T, RM, 4, 2, true>), grid, blk, 0, s, g); break;
-        case 3: hipLaunchKernelGGL((stem_wgrad_kernel<T, RM, 6, 3, true>), grid, blk, 0, s, g); break;
-        default: hipLaunchKernelGGL((stem_wgrad_kernel<T, RM, 8, 4, true>), grid, blk, 0, s, g); break;
+        case 1: MMSEG_LAUNCH((stem_wgrad_kernel<T, RM, 2, 1, true>), grid, blk, 0, s, g); break;
+        case 2: MMSEG_LAUNCH((stem_wgrad_kernel<T, RM, 4, 2, true>), grid, blk, 0, s, g); break;
+        case 3: MMSEG_LAUNCH((stem_wgrad_kernel<T, RM, 6, 3, true>), grid, blk, 0, s, g); break;
+        default: MMSEG_LAUNCH((stem_wgrad_kernel<T, RM, 8, 4, true>), grid, blk, 0, s, g); break;
       }
       return;
     }
     switch (cr) {
-      case 1: hipLaunchKernelGGL((stem_wgrad_kernel<T, RM, 2, 1>), grid, blk, 0, s, g); break;
-      case 2: hipLaunchKernelGGL((stem_wgrad_kernel<T, RM, 4, 2>), grid, blk, 0, s, g); break;
-      case 3: hipLaunchKernelGGL((stem_wgrad_kernel<T, RM, 6, 3>), grid, blk, 0, s, g); break;
-      default: hipLaunchKernelGGL((stem_wgrad_kernel<T, RM, 8, 4>), grid, blk, 0, s, g); break;
+      case 1: MMSEG_LAUNCH((stem_wgrad_kernel<T, RM, 2, 1>), grid, blk, 0, s, g); break;
+      case 2: MMSEG_LAUNCH((stem_wgrad_kernel<T, RM, 4, 2>), grid, blk, 0, s, g); break;
+      case 3: MMSEG_LAUNCH((stem_wgrad_kernel<T, RM, 6, 3>), grid, blk, 0, s, g); break;
+      default: MMSEG_LAUNCH((stem_wgrad_kernel<T, RM, 8, 4>), grid, blk, 0, s, g); break;
     }
   };
   if (dtype == MMSEG_BF16) {

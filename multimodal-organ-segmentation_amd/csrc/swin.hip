@@ -508,7 +508,7 @@ int ln_fwd_t(const void* x, int ldx, void* y, int ldy, long long rows, int C, co
   const int nl = ln_nl(C), nb = ln_blocks(rows);
   auto X = (const T*)x;
   auto Y = (T*)y;
-#define LNF(NL) hipLaunchKernelGGL((layernorm_fwd_kernel<T, NL>), dim3(nb), dim3(256), 0, s, X, ldx, Y, ldy, rows, C, \
+#define LNF(NL) MMSEG_LAUNCH((layernorm_fwd_kernel<T, NL>), dim3(nb), dim3(256), 0, s, X, ldx, Y, ldy, rows, C, \
                                    gamma, beta, eps, mean, rstd)
   switch (nl) {
     case 1: LNF(1); break;
@@ -530,7 +530,7 @@ int ln_bwd_t(const void* x, int ldx, const void* dy, int lddy, void* dx, int ldd
   auto X = (const T*)x;
   auto G = (const T*)dy;
   auto O = (T*)dx;
-#define LNB(NL) hipLaunchKernelGGL((layernorm_bwd_kernel<T, NL>), dim3(nb), dim3(256), 0, s, X, ldx, G, lddy, O, lddx, \
+#define LNB(NL) MMSEG_LAUNCH((layernorm_bwd_kernel<T, NL>), dim3(nb), dim3(256), 0, s, X, ldx, G, lddy, O, lddx, \
                                    rows, C, gamma, mean, rstd, add, part)
   switch (nl) {
     case 1: LNB(1); break;
@@ -576,7 +576,7 @@ int mmseg_layernorm_bwd(const void* x, int ldx, const void* dy, int lddy, void* 
                     : ln_bwd_t<float>(x, ldx, dy, lddy, dx, lddx, rows, C, gamma, mean, rstd, add_dx, part, s);
   if (r || !part) return r;
   const int nb = ln_blocks(rows) * (64 * ln_nl(C) <= 1024 ? 1 : LN_WAVES);
-  hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(ceil_div(2LL * C, 64)), dim3(64 * LNR_WAVES), 0, s, part, nb, C,
+  MMSEG_LAUNCH(ln_param_reduce_kernel, dim3(ceil_div(2LL * C, 64)), dim3(64 * LNR_WAVES), 0, s, part, nb, C,
                      dgamma, dbeta, accumulate);
   return mmseg::check_launch("ln_param_reduce");
 }
@@ -585,10 +585,10 @@ int mmseg_gelu_fwd(const void* h, void* y, long long n, int dtype, void* stream)
   MMSEG_REQUIRE(n % 8 == 0, "gelu: n %% 8 == 0");
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(gelu_fwd_kernel<bf16_t>, dim3(grid_of(n / 8)), dim3(256), 0, s, (const bf16_t*)h, (bf16_t*)y,
+    MMSEG_LAUNCH(gelu_fwd_kernel<bf16_t>, dim3(grid_of(n / 8)), dim3(256), 0, s, (const bf16_t*)h, (bf16_t*)y,
                        n / 8);
   else
-    hipLaunchKernelGGL(gelu_fwd_kernel<float>, dim3(grid_of(n / 8)), dim3(256), 0, s, (const float*)h, (float*)y,
+    MMSEG_LAUNCH(gelu_fwd_kernel<float>, dim3(grid_of(n / 8)), dim3(256), 0, s, (const float*)h, (float*)y,
                        n / 8);
   return mmseg::check_launch("gelu_fwd");
 }
@@ -597,10 +597,10 @@ int mmseg_gelu_bwd(const void* h, const void* dy, void* dh, long long n, int dty
   MMSEG_REQUIRE(n % 8 == 0, "gelu_bwd: n %% 8 == 0");
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(gelu_bwd_kernel<bf16_t>, dim3(grid_of(n / 8)), dim3(256), 0, s, (const bf16_t*)h,
+    MMSEG_LAUNCH(gelu_bwd_kernel<bf16_t>, dim3(grid_of(n / 8)), dim3(256), 0, s, (const bf16_t*)h,
                        (const bf16_t*)dy, (bf16_t*)dh, n / 8);
   else
-    hipLaunchKernelGGL(gelu_bwd_kernel<float>, dim3(grid_of(n / 8)), dim3(256), 0, s, (const float*)h,
+    MMSEG_LAUNCH(gelu_bwd_kernel<float>, dim3(grid_of(n / 8)), dim3(256), 0, s, (const float*)h,
                        (const float*)dy, (float*)dh, n / 8);
   return mmseg::check_launch("gelu_bwd");
 }
@@ -615,10 +615,10 @@ int mmseg_dropout(const void* x, void* y, long long rows, int C, long long V, in
   const unsigned int thr = t >= 4294967295.0 ? 0xffffffffu : (unsigned int)t;
   const float scale = (float)(1.0 / (1.0 - (double)p));
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(dropout_kernel<bf16_t>, dim3(grid_of(n8)), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, n8,
+    MMSEG_LAUNCH(dropout_kernel<bf16_t>, dim3(grid_of(n8)), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, n8,
                        C, V, ncdhw, (unsigned long long)seed, thr, scale);
   else
-    hipLaunchKernelGGL(dropout_kernel<float>, dim3(grid_of(n8)), dim3(256), 0, s, (const float*)x, (float*)y, n8, C,
+    MMSEG_LAUNCH(dropout_kernel<float>, dim3(grid_of(n8)), dim3(256), 0, s, (const float*)x, (float*)y, n8, C,
                        V, ncdhw, (unsigned long long)seed, thr, scale);
   return mmseg::check_launch("dropout");
 }
@@ -627,10 +627,10 @@ int mmseg_add(const void* a, const void* b, void* out, long long n, int dtype, v
   MMSEG_REQUIRE(n % 8 == 0, "add: n %% 8 == 0");
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(add_kernel<bf16_t>, dim3(grid_of(n / 8)), dim3(256), 0, s, (const bf16_t*)a, (const bf16_t*)b,
+    MMSEG_LAUNCH(add_kernel<bf16_t>, dim3(grid_of(n / 8)), dim3(256), 0, s, (const bf16_t*)a, (const bf16_t*)b,
                        (bf16_t*)out, n / 8);
   else
-    hipLaunchKernelGGL(add_kernel<float>, dim3(grid_of(n / 8)), dim3(256), 0, s, (const float*)a, (const float*)b,
+    MMSEG_LAUNCH(add_kernel<float>, dim3(grid_of(n / 8)), dim3(256), 0, s, (const float*)a, (const float*)b,
                        (float*)out, n / 8);
   return mmseg::check_launch("add");
 }
@@ -650,10 +650,10 @@ int mmseg_window_partition(const void* src, int ldx, int B, int D, int H, int W,
   const long long total8 = (long long)B * Dp * Hp * Wp * (C / 8);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(window_partition_kernel<bf16_t>, dim3(grid_of(total8)), dim3(256), 0, s, (const bf16_t*)src, a,
+    MMSEG_LAUNCH(window_partition_kernel<bf16_t>, dim3(grid_of(total8)), dim3(256), 0, s, (const bf16_t*)src, a,
                        (bf16_t*)dst, total8);
   else
-    hipLaunchKernelGGL(window_partition_kernel<float>, dim3(grid_of(total8)), dim3(256), 0, s, (const float*)src, a,
+    MMSEG_LAUNCH(window_partition_kernel<float>, dim3(grid_of(total8)), dim3(256), 0, s, (const float*)src, a,
                        (float*)dst, total8);
   return mmseg::check_launch("window_partition");
 }
@@ -666,10 +666,10 @@ int mmseg_window_reverse(const void* win, int B, int D, int H, int W, int C, int
   const long long total8 = (long long)B * D * H * W * (C / 8);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(window_reverse_kernel<bf16_t>, dim3(grid_of(total8)), dim3(256), 0, s, (const bf16_t*)win, a,
+    MMSEG_LAUNCH(window_reverse_kernel<bf16_t>, dim3(grid_of(total8)), dim3(256), 0, s, (const bf16_t*)win, a,
                        (const bf16_t*)add_src, ld_add, (bf16_t*)dst, ld_dst, total8);
   else
-    hipLaunchKernelGGL(window_reverse_kernel<float>, dim3(grid_of(total8)), dim3(256), 0, s, (const float*)win, a,
+    MMSEG_LAUNCH(window_reverse_kernel<float>, dim3(grid_of(total8)), dim3(256), 0, s, (const float*)win, a,
                        (const float*)add_src, ld_add, (float*)dst, ld_dst, total8);
   return mmseg::check_launch("window_reverse");
 }
@@ -679,10 +679,10 @@ int mmseg_merge_gather(const void* x, int ldx, int B, int D, int H, int W, int C
   const long long total8 = (long long)B * ((D + 1) / 2) * ((H + 1) / 2) * ((W + 1) / 2) * 8 * (C / 8);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(merge_gather_kernel<bf16_t>, dim3(grid_of(total8)), dim3(256), 0, s, (const bf16_t*)x, ldx, B,
+    MMSEG_LAUNCH(merge_gather_kernel<bf16_t>, dim3(grid_of(total8)), dim3(256), 0, s, (const bf16_t*)x, ldx, B,
                        D, H, W, C, (bf16_t*)out, total8);
   else
-    hipLaunchKernelGGL(merge_gather_kernel<float>, dim3(grid_of(total8)), dim3(256), 0, s, (const float*)x, ldx, B, D,
+    MMSEG_LAUNCH(merge_gather_kernel<float>, dim3(grid_of(total8)), dim3(256), 0, s, (const float*)x, ldx, B, D,
                        H, W, C, (float*)out, total8);
   return mmseg::check_launch("merge_gather");
 }
@@ -693,10 +693,10 @@ int mmseg_merge_scatter(const void* dout, int B, int D, int H, int W, int C, voi
   const long long total8 = (long long)B * D * H * W * (C / 8);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(merge_scatter_kernel<bf16_t>, dim3(grid_of(total8)), dim3(256), 0, s, (const bf16_t*)dout, B,
+    MMSEG_LAUNCH(merge_scatter_kernel<bf16_t>, dim3(grid_of(total8)), dim3(256), 0, s, (const bf16_t*)dout, B,
                        D, H, W, C, (bf16_t*)dx, lddx, total8);
   else
-    hipLaunchKernelGGL(merge_scatter_kernel<float>, dim3(grid_of(total8)), dim3(256), 0, s, (const float*)dout, B, D,
+    MMSEG_LAUNCH(merge_scatter_kernel<float>, dim3(grid_of(total8)), dim3(256), 0, s, (const float*)dout, B, D,
                        H, W, C, (float*)dx, lddx, total8);
   return mmseg::check_launch("merge_scatter");
 }
@@ -707,10 +707,10 @@ int mmseg_patchify(const float* x, int B, int Cin, int D, int H, int W, int Kp, 
   const long long total = (long long)B * (D / 2) * (H / 2) * (W / 2) * Kp;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(patchify_kernel<bf16_t>, dim3(grid_of(total)), dim3(256), 0, s, x, B, Cin, D, H, W, Kp,
+    MMSEG_LAUNCH(patchify_kernel<bf16_t>, dim3(grid_of(total)), dim3(256), 0, s, x, B, Cin, D, H, W, Kp,
                        (bf16_t*)out, total);
   else
-    hipLaunchKernelGGL(patchify_kernel<float>, dim3(grid_of(total)), dim3(256), 0, s, x, B, Cin, D, H, W, Kp,
+    MMSEG_LAUNCH(patchify_kernel<float>, dim3(grid_of(total)), dim3(256), 0, s, x, B, Cin, D, H, W, Kp,
                        (float*)out, total);
   return mmseg::check_launch("patchify");
 }
@@ -723,10 +723,10 @@ int mmseg_res_apply(const void* a, int lda, const float* ma, const float* ra, co
   const long long total8 = (long long)N * V * (C / 8);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(res_apply_kernel<bf16_t>, dim3(grid_of(total8)), dim3(256), 0, s, (const bf16_t*)a, lda, ma,
+    MMSEG_LAUNCH(res_apply_kernel<bf16_t>, dim3(grid_of(total8)), dim3(256), 0, s, (const bf16_t*)a, lda, ma,
                        ra, (const bf16_t*)b, ldb, mb, rb, (bf16_t*)y, ldy, V, C, slope, total8);
   else
-    hipLaunchKernelGGL(res_apply_kernel<float>, dim3(grid_of(total8)), dim3(256), 0, s, (const float*)a, lda, ma, ra,
+    MMSEG_LAUNCH(res_apply_kernel<float>, dim3(grid_of(total8)), dim3(256), 0, s, (const float*)a, lda, ma, ra,
                        (const float*)b, ldb, mb, rb, (float*)y, ldy, V, C, slope, total8);
   return mmseg::check_launch("res_apply");
 }
@@ -737,10 +737,10 @@ int mmseg_lrelu_bwd(const void* y, int ldy, const void* dy, int lddy, void* g, i
   const long long total8 = rows * (C / 8);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16)
-    hipLaunchKernelGGL(lrelu_bwd_kernel<bf16_t>, dim3(grid_of(total8)), dim3(256), 0, s, (const bf16_t*)y, ldy,
+    MMSEG_LAUNCH(lrelu_bwd_kernel<bf16_t>, dim3(grid_of(total8)), dim3(256), 0, s, (const bf16_t*)y, ldy,
                        (const bf16_t*)dy, lddy, (bf16_t*)g, ldg, C, slope, total8);
   else
-    hipLaunchKernelGGL(lrelu_bwd_kernel<float>, dim3(grid_of(total8)), dim3(256), 0, s, (const float*)y, ldy,
+    MMSEG_LAUNCH(lrelu_bwd_kernel<float>, dim3(grid_of(total8)), dim3(256), 0, s, (const float*)y, ldy,
                        (const float*)dy, lddy, (float*)g, ldg, C, slope, total8);
   return mmseg::check_launch("lrelu_bwd");
 }

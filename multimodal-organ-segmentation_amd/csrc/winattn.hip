@@ -391,7 +391,7 @@ int mmseg_winattn_fwd(const void* qkv, int B, int N, int C, int heads, const flo
   WinAttnArgs a{(const bf16_t*)qkv, nullptr, nullptr, (bf16_t*)O, lse, nullptr, table, region,
                 B, N, C, heads, C / heads, nw, T, 0, w0, w1, w2, scale};
   if (check_args(a)) return 1;
-  hipLaunchKernelGGL(winattn_fwd_kernel, dim3(B * heads), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+  MMSEG_LAUNCH(winattn_fwd_kernel, dim3(B * heads), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
   return mmseg::check_launch("winattn_fwd");
 }
 
@@ -403,9 +403,9 @@ int mmseg_winattn_bwd(const void* qkv, const void* O, const void* dO, const floa
   if (check_args(a)) return 1;
   MMSEG_REQUIRE(ldn >= N && ldn % 8 == 0, "winattn_bwd: ldn >= N, multiple of 8");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(winattn_bwd_kv_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  MMSEG_LAUNCH(winattn_bwd_kv_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
   if (mmseg::check_launch("winattn_bwd_kv")) return 1;
-  hipLaunchKernelGGL(winattn_bwd_q_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  MMSEG_LAUNCH(winattn_bwd_q_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
   return mmseg::check_launch("winattn_bwd_q");
 }
 
