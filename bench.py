@@ -213,6 +213,7 @@ def main():
                     help="torch: the same model / step through PyTorch-ROCm ops (MIOpen convs; hardware.kernels A/B)")
     ap.add_argument("--fp8", action="store_true",
                     help="config c5's mixed bf16/fp8: e4m3 forward convolutions where the kernel takes them")
+    ap.add_argument("--timer-dump", default="", help="write every timed launch (family, site, ms, flops) as JSON")
     ap.add_argument("--amp", default="bf16", choices=["bf16", "fp16"],
                     help="--kernels torch autocast dtype (fp16 + GradScaler = the reference's GPU mode)")
     args = ap.parse_args()
@@ -276,6 +277,9 @@ def main():
         trainer.train_step(batches[step % len(batches)], step, sync=False)
         step += 1
     TIMER.stop()
+    if args.timer_dump and rank == 0:
+        with open(args.timer_dump, "w") as f:
+            json.dump({"timer_steps": args.timer_steps, "launches": TIMER.records()}, f)
     fam = TIMER.summary()
     dom = max(fam.items(), key=lambda kv: kv[1]["ms"]) if fam else None
 

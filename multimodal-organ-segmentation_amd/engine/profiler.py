@@ -71,9 +71,9 @@ class KernelTimer:
             out.append((nm.value.decode(), float(ms.value)))
         return out
 
-    def summary(self):
+    def records(self):
+        """Per launch, in issue order: (family, launch-site kernel, ms, flops, bytes)."""
         launches = self.launches()
-        agg = defaultdict(lambda: {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
         owner = {}
         for name, fl, nb, i0, i1 in self.regions:
             if i1 <= i0:
@@ -83,8 +83,15 @@ class KernelTimer:
                         max(range(i0, i1), key=lambda i: launches[i][1]))
             for i in range(i0, i1):
                 owner[i] = (name, fl, nb) if i == main else (_base(launches[i][0]), 0.0, 0.0)
+        out = []
         for i, (site, ms) in enumerate(launches):
             name, fl, nb = owner.get(i, (_base(site), 0.0, 0.0))
+            out.append((name, site, ms, fl, nb))
+        return out
+
+    def summary(self):
+        agg = defaultdict(lambda: {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
+        for name, _, ms, fl, nb in self.records():
             a = agg[name]
             a["launches"] += 1
             a["ms"] += ms

@@ -225,3 +225,67 @@ def test_fullsize_step_pinned_to_fp64_oracle(dev, tag, dtype):
     assert max(errs.values()) < tol, worst
     assert med < PINNED_MEDIAN[dtype], med
     assert max(dead.values()) < PINNED_DEAD[dtype], dead
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# c5 in mixed bf16 / fp8 (hardware.fp8: true) at full size
+# ---------------------------------------------------------------------------------------------------------------
+def test_fullsize_c5_fp8_step(dev):
+    """Config c5 (DualEncoder CT+PET+MRI, Tversky, 96^3, B=2) with the e4m3 forward convolutions (bench.py
+    --fp8), against the reference's own step on the same inputs (tests/golden/fullgrad_dual_m3_c5.npz) and
+    against the engine's bf16 step.  e4m3 keeps 3 mantissa bits, so the bound is stated against the
+    reference's own mixed precision: per parameter tensor e(x) = ||x - ref_fp64|| / ||ref_fp64|| on the
+    fixture's sampled positions; the fp8 step's median e within 1.5x the reference bf16-autocast step's median
+    (which is 0.46 here: the reference's mixed precision re-draws most of these random-input gradients), the
+    loss within 1e-2 of fp64, the sampled logits within 0.2 normwise of fp64 and of the bf16 engine."""
+    tag = "fullgrad_dual_m3_c5"
+    g = golden(tag)
+    model, mods, loss = CASES[tag]
+    S, B, seed, C = int(g["S"]), int(g["B"]), int(g["seed"]), 6
+    x, y, idx = full_inputs(S, B, len(mods), C, seed)
+    x, y = x.to(dev), y.to(dev)
+    res = {}
+    for fp8 in (False, True):
+        cfg = _config(model, mods, loss, "bfloat16")
+        cfg["hardware"]["fp8"] = fp8
+        torch.manual_seed(seed)
+        m = build_model(cfg)
+        tr = Trainer(cfg, m)
+        m.train()
+        lossv = tr._fused_loss(x, y)
+        assert lossv is not None
+        lossv.backward()
+        if fp8:
+            prog = m.backbone.__dict__["_engine"].program
+            assert all(prog.encs[k][0].c2._f8 is not None for k in range(3)) and prog.dec.blocks[-1].c2._f8 is not None
+        with torch.no_grad():
+            logits = m(x)
+        torch.cuda.synchronize()
+        names = [n for n, _ in m.backbone.named_parameters()]
+        bb = dict(m.backbone.named_parameters())
+        off = g["gs_off"]
+        e = {}
+        for i, n in enumerate(names):
+            if n.endswith(("conv1.bias", "conv2.bias")):
+                continue
+            sl = slice(off[i], off[i + 1])
+            gi = torch.from_numpy(g["gs_idx"][sl]).to(dev)
+            e[n] = _l2(bb[n].grad.reshape(-1)[gi].double().cpu().numpy(), g["gs_val64"][sl])
+        samp = logits.reshape(B, C, -1)[:, :, torch.from_numpy(idx).to(dev)].double().cpu()
+        res[fp8] = (lossv.item(), samp, e)
+        del m, tr
+    loss64 = float(g["loss64"])
+    ref_bf = {n: _l2(g["gs_valbf"][slice(g["gs_off"][i], g["gs_off"][i + 1])],
+                     g["gs_val64"][slice(g["gs_off"][i], g["gs_off"][i + 1])])
+              for i, n in enumerate(g["param_names"]) if n in res[True][2]}
+    l64 = torch.from_numpy(g["sample_logits64"])
+    nrel = lambda a, b: float((a - b).norm() / b.norm())  # noqa: E731
+    med8, medb, medr = (float(np.median(list(res[True][2].values()))), float(np.median(list(res[False][2].values()))),
+                        float(np.median(list(ref_bf.values()))))
+    print(f"\nc5 96^3 fp8: loss {res[True][0]:.6f} (bf16 {res[False][0]:.6f}, fp64 {loss64:.6f}); sampled logits vs fp64 "
+          f"{nrel(res[True][1], l64):.3f} (bf16 engine {nrel(res[False][1], l64):.4f}), fp8 vs bf16 engine "
+          f"{nrel(res[True][1], res[False][1]):.3f}; gradient error vs fp64, median over tensors: fp8 {med8:.3f}, "
+          f"bf16 engine {medb:.3f}, reference bf16 autocast {medr:.3f}")
+    assert abs(res[True][0] - loss64) < 1e-2 * abs(loss64)
+    assert nrel(res[True][1], l64) < 0.2 and nrel(res[True][1], res[False][1]) < 0.2
+    assert med8 <= 1.5 * medr, (med8, medr)

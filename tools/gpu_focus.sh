@@ -17,7 +17,7 @@ if [ -n "$2" ]; then
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "tests ended with $rc"; tail -30 $O/gpu_tests.log; exit 1; fi
 fi
 if [ "${3:-bench}" = "bench" ]; then
-  timeout -k 10 600 python3 $R/bench.py > $O/bench.log 2>&1 || { echo "bench failed"; tail -20 $O/bench.log; exit 1; }
+  timeout -k 10 600 python3 $R/bench.py --timer-dump $O/timer.json > $O/bench.log 2>&1 || { echo "bench failed"; tail -20 $O/bench.log; exit 1; }
   tail -1 $O/bench.log
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o prof -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/prof.log 2>&1 || { echo "prof failed"; tail -20 $O/prof.log; exit 1; }
   tail -1 $O/prof.log

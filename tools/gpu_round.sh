@@ -15,7 +15,7 @@ if [ "${2:-tests}" = "tests" ]; then
   # 1 = some test assertions failed (keep measuring); anything else (abort, segfault, timeout) ends the call
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "tests ended with $rc"; tail -30 $O/gpu_tests.log; exit 1; fi
 fi
-timeout -k 10 600 python3 $R/bench.py > $O/bench.log 2>&1 || { echo "bench failed"; tail -20 $O/bench.log; exit 1; }
+timeout -k 10 600 python3 $R/bench.py --timer-dump $O/timer.json > $O/bench.log 2>&1 || { echo "bench failed"; tail -20 $O/bench.log; exit 1; }
 tail -1 $O/bench.log
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o prof -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/prof.log 2>&1 || { echo "prof failed"; tail -20 $O/prof.log; exit 1; }
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o pmc -- python3 $R/bench.py --steps 2 --warmup 1 --timer-steps 1 --no-cpu-baseline > $O/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; tail -20 $O/pmc_fetch.log; exit 1; }
