@@ -2628,6 +2628,7 @@ struct WgradArgs {
   const float* nmean;
   const float* nrstd;
   int dbg;   // wgrad_brick2 timing probe (MMSEG_WGRAD_DBG): 1 = no global loads after the first brick, 2 = no MFMA
+  int frag;  // wgrad_dma: split partials in the fragment-native layout (wgrad_dma_mt, WReduceArgs::frag_mt)
 };
 
 __host__ __device__ __forceinline__ int wgrad_nchunk(int cpg_shift, int kchunks) {
@@ -3855,7 +3856,25 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
   }
 
   static_assert(sizeof(st) >= 16 * WEP_P * sizeof(float), "epilogue staging must fit the stage ring");
-  wgrad_store_chmajor<MT>(acc, t_begin, t_cnt, reinterpret_cast<float*>(st), g, ks, row0, c0);
+  if (g.frag && !(g.grad != nullptr && g.ksplit == 1)) {
+    // split partials in the accumulators' own layout: every (tap, i, j) fragment is 1 KB contiguous (lane l's
+    // f32x4 at 16 l), so each wave stores straight from registers with 16-B lanes -- no LDS transpose, no
+    // barriers; wgrad_reduce_kernel (frag_mt) maps the layout to the torch order and sums in the same fixed
+    // split order as before (bitwise the same gradient)
+    float* base = g.part + (long long)ks * g.Ca * g.Ncols + (long long)(rt * nchunk + ct) * (CO * 27 * CK);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (t >= t_cnt) continue;
+      const int tap = t_begin + t;
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          *reinterpret_cast<f32x4*>(base + ((tap * MT + i) * 2 + j) * 256 + lane * 4) = acc[t][i][j];
+    }
+  } else {
+    wgrad_store_chmajor<MT>(acc, t_begin, t_cnt, reinterpret_cast<float*>(st), g, ks, row0, c0);
+  }
   if (bias_wave && i16 == 0) {
     // acc[3][i][0][r] = sum over the block's voxels of dy[.][row0 + 16 i + 4 g4 + r] (every column alike)
 #pragma unroll
@@ -4111,6 +4130,8 @@ struct WReduceArgs {
   int ntap;           // 27 (CONV3), 1 (POINT), 8 (CONVT)
   int accumulate;
   int chmajor;        // cols are channel-major (col = c*ntap + tap, brick2/brickr partials) instead of tap-major
+  int frag_mt;        // > 0: wgrad_dma's fragment-native partials (MT 16-row tiles per block), see wgrad_dma_kernel
+  int nchunk;         // frag_mt > 0: 32-channel chunks per tile row
 };
 
 // 256 threads = (256/S) float4 columns x S split slices: slice s sums splits
@@ -4181,9 +4202,25 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(WReduceArgs g) {
       g.bias_grad[row] = g.accumulate ? g.bias_grad[row] + val : val;
       continue;
     }
-    const int row = (int)(idx / g.Ncols);
+    int row, tt, c;
+    if (g.frag_mt > 0) {
+      // tile (rt, ct) of CO x (27 taps x 32 channels), inside it ((tap * MT + i) * 2 + j) * 256 + lane * 4 + r
+      const int CO = g.frag_mt * 16, tsz = CO * 27 * 32;
+      const int tile = (int)(idx / tsz), loc = (int)(idx - (long long)tile * tsz);
+      const int rt = tile / g.nchunk, ct = tile - rt * g.nchunk;
+      const int f = loc >> 8, e = loc & 255, lane = e >> 2, r = e & 3;
+      const int j = f & 1, i = (f >> 1) % g.frag_mt;
+      tt = (f >> 1) / g.frag_mt;
+      row = rt * CO + 16 * i + 4 * (lane >> 4) + r;
+      c = ct * 32 + 16 * j + (lane & 15);
+      if (row >= g.Ca || c >= g.creal) continue;   // past the tiles (channel padding): never written, sum dropped
+      const long long dst = ((long long)row * g.creal + c) * g.ntap + tt;
+      if (g.accumulate) g.grad[dst] += val;
+      else g.grad[dst] = val;
+      continue;
+    }
+    row = (int)(idx / g.Ncols);
     const int col = (int)(idx - (long long)row * g.Ncols);
-    int tt, c;
     if (g.chmajor) {
       c = col / g.ntap;
       tt = col - c * g.ntap;
@@ -4761,6 +4798,17 @@ int launch_gemm_mode(GemmArgs g, int mode, hipStream_t s) {
   return 1;
 }
 
+// The LDS-DMA weight-gradient kernel's row tile (4 = 64 co, 2 = 32 co) when it takes this CONV3 brick2 launch,
+// else 0: bf16, byte offsets of both tensors within 31 bits (the deferred-norm variant keeps register staging by
+// default: its in-place LDS pass and extra barrier cost more than the DMA saves, 0.651 -> 0.682 ms/step for the
+// 32-co family)
+int wgrad_dma_mt(const WgradArgs& g, int elem_bytes) {
+  const bool dma = elem_bytes == 2 && g.brick == 2 && knob("MMSEG_WGRAD_V3", 1) != 0 && knob("MMSEG_WGRAD_DMA", 1) &&
+                   (g.nmean == nullptr || knob("MMSEG_WGRAD_DMA_NORM", 0)) && g.V * g.lda * 2 < (1LL << 31) &&
+                   g.V * g.ldb * 2 < (1LL << 31) && (g.lda % 8) == 0 && (g.ldb % 8) == 0;
+  return dma ? (g.Ca % 64 == 0 ? 4 : 2) : 0;
+}
+
 template <typename T, int MODE>
 int launch_wgrad(WgradArgs g, hipStream_t s) {
 #ifdef MMSEG_TIMING_PROBES
@@ -4792,14 +4840,7 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
     }
     if (MODE == MODE_CONV3 && g.brick == 2) {
       const bool v3 = knob("MMSEG_WGRAD_V3", 1) != 0;
-      // LDS-DMA staging: bf16, byte offsets of both tensors within 31 bits
-      // (the deferred-norm variant keeps register staging by default: its in-place LDS pass and extra barrier
-      // cost more than the DMA saves, 0.651 -> 0.682 ms/step for the 32-co family)
-      const bool dma = sizeof(T) == 2 && v3 && knob("MMSEG_WGRAD_DMA", 1) &&
-                       (g.nmean == nullptr || knob("MMSEG_WGRAD_DMA_NORM", 0)) && g.V * g.lda * 2 < (1LL << 31) &&
-                       g.V * g.ldb * 2 < (1LL << 31) && (g.lda % 8) == 0 && (g.ldb % 8) == 0;
-      if (dma) {
-        const int mt = g.Ca % 64 == 0 ? 4 : 2;
+      if (const int mt = wgrad_dma_mt(g, (int)sizeof(T))) {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / (16 * mt)) * g.ksplit);
         const bool st4 = knob("MMSEG_WGRAD_DMA_ST", 3) >= 4;   // ring depth (4 x 38.5 KB fits at 64 co)
         // fragment prefetch two steps ahead (32 co; at 64 co the extra registers spill: 59.5 -> 72.3 us)
@@ -5428,12 +5469,15 @@ int conv3_wgrad_impl(const void* dy, int lddy, const void* x, int ldx, const flo
               knob("MMSEG_WGRAD_SWIZZLE", 0), p.kind, p.direct ? grad : nullptr, p.direct ? bias_grad : nullptr,
               accumulate, wgrad_kchunks(Cip, Ci), nmean, nrstd};
   hipStream_t s = (hipStream_t)stream;
+  const int fmt = knob("MMSEG_WGRAD_FRAG", 1) ? wgrad_dma_mt(g, dtype == MMSEG_BF16 ? 2 : 4) : 0;
+  g.frag = fmt > 0;
   if (phase & 1) {
     const int rc = dtype == MMSEG_BF16 ? launch_wgrad<bf16_t, MODE_CONV3>(g, s) : launch_wgrad<float, MODE_CONV3>(g, s);
     if (rc) return rc;
   }
   if (p.direct || !(phase & 2)) return 0;
-  WReduceArgs r{part, grad, bpart, bias_grad, Co, ncols, p.ksplit, Cip, Ci, 27, accumulate, p.kind >= 2 ? 1 : 0};
+  WReduceArgs r{part, grad, bpart, bias_grad, Co, ncols, p.ksplit, Cip, Ci, 27, accumulate, p.kind >= 2 ? 1 : 0,
+                fmt, wgrad_nchunk(cpg_shift, g.kchunks)};
   return launch_wgrad_reduce(r, stream);
 }
 

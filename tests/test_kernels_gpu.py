@@ -595,3 +595,41 @@ def test_conv3_dgrad_split_output(dev, dtype, knobs, cin, cout, shape, monkeypat
     ref = whole.buf[: N * D * H * W * cin].view(-1, cin)
     assert torch.equal(buf[: N * D * H * W * h].view(-1, h), ref[:, :h])
     assert torch.equal(buf[N * D * H * W * h:].view(-1, h), ref[:, h:])
+
+
+@pytest.mark.parametrize("cin,cout,shape,accumulate", [
+    (64, 64, (2, 8, 12, 16), 0), (32, 128, (2, 8, 8, 16), 1), (64, 32, (2, 8, 4, 16), 0),
+    (128, 64, (2, 8, 8, 16), 1), (32, 32, (2, 12, 8, 24), 0)])
+def test_wgrad_dma_fragment_partials_bitwise(dev, cin, cout, shape, accumulate, monkeypatch):
+    """wgrad_dma's split partials in the accumulators' own layout (MMSEG_WGRAD_FRAG=1, direct 16-B stores from
+    registers) against the channel-major layout through the LDS transpose (=0): the reduce sums every element
+    over the same splits in the same fixed order, so weight and bias gradients must be BITWISE equal."""
+    N, D, H, W = shape
+    V = N * D * H * W
+    g = torch.Generator().manual_seed(cin + cout + V)
+    dy = torch.randn(V, cout, generator=g).to(dev, torch.bfloat16).reshape(-1)
+    x = torch.randn(V, cin, generator=g).to(dev, torch.bfloat16).reshape(-1)
+    gw0 = torch.randn(cout * cin * 27, generator=g).to(dev) if accumulate else torch.zeros(cout * cin * 27, device=dev)
+    gb0 = torch.ones(cout, device=dev) if accumulate else torch.zeros(cout, device=dev)
+    L = lib()
+    shift = int(np.log2(cin // 8))
+    wsf = L.mmseg_conv3_wgrad_ws_floats(V, cout, cin, cin, shift, D, H, W, cout, cin, 1)
+    assert wsf > 0, "single split: nothing to reduce"
+    out = {}
+    for frag in ("0", "1"):
+        monkeypatch.setenv("MMSEG_WGRAD_FRAG", frag)
+        ws = torch.full((wsf,), float("nan"), device=dev)
+        gw, gb = gw0.clone(), gb0.clone()
+        L.mmseg_conv3_wgrad(ptr(dy), cout, ptr(x), cin, ptr(gw), ptr(gb), cout, cin, cin, shift, V, D, H, W,
+                            ptr(ws), wsf, accumulate, 1, stream_handle())
+        assert L.mmseg_last_kernel().decode().startswith("wgrad_dma_kernel")
+        torch.cuda.synchronize()
+        out[frag] = (gw, gb)
+    assert torch.equal(out["0"][0], out["1"][0]) and torch.equal(out["0"][1], out["1"][1])
+    # and against fp64 (the torch layout the reduce writes)
+    xr = x.double().cpu().reshape(N, D, H, W, cin).permute(0, 4, 1, 2, 3)
+    dyr = dy.double().cpu().reshape(N, D, H, W, cout).permute(0, 4, 1, 2, 3)
+    ref = torch.nn.grad.conv3d_weight(xr, (cout, cin, 3, 3, 3), dyr, padding=1).reshape(-1)
+    got = out["1"][0].double().cpu() - gw0.double().cpu()
+    assert rel(got, ref) < GTOL[torch.bfloat16]
+    assert rel(out["1"][1].double().cpu() - gb0.double().cpu(), dyr.sum(dim=(0, 2, 3, 4))) < GTOL[torch.bfloat16]
