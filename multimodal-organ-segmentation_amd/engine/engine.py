@@ -56,6 +56,7 @@ class SegEngine:
     def backward(self, dlogits: torch.Tensor) -> None:
         accumulate = self.flat.begin_backward()
         self.program.backward(dlogits.float().contiguous(), accumulate)
+        self.rt.join_side()
         self.flat.end_backward()
 
     # ---- fused head + loss (Trainer fast path)
@@ -72,6 +73,7 @@ class SegEngine:
     def backward_loss(self, gout: torch.Tensor) -> None:
         accumulate = self.flat.begin_backward()
         self.program.backward(None, accumulate, gout=gout.float().contiguous())
+        self.rt.join_side()
         self.flat.end_backward()
 
 

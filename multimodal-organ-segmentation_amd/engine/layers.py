@@ -294,7 +294,35 @@ class Conv3:
                                              y.ptr, y.ld, x.N * x.V, self.ncols_f, self.Cpad, self.KG,
                                              self.cpg_shift, x.D, x.H, x.W, self.rt.code, self.rt.stream)
 
-    def bwd(self, x: Act, dy: Act, dx: Optional[Act], accumulate: bool,
+    def _part(self, nfloats: int) -> torch.Tensor:
+        """Split partials of this layer's weight gradient: the shared scratch, or with the side-stream reduce
+        (Runtime.async_wred) a buffer of the layer's own, since its reduce may still run while the data-gradient
+        kernel takes scratch (the partials of a whole backward, ~1.2 GB for the 96^3 DualEncoder, fit HBM many
+        times over)."""
+        if not self.rt.async_wred:
+            return self.rt.ws(nfloats)
+        buf = getattr(self, "_wpart", None)
+        if buf is None or buf.numel() < nfloats:
+            buf = self._wpart = torch.empty(int(nfloats), dtype=torch.float32, device=self.rt.device)
+        return buf
+
+    def _reduce_after(self, fn) -> None:
+        """Run fn(stream) -- the split reduce, the staging copy and the DP readiness mark -- after the weight-gradient
+        kernel: on the side stream, beside this layer's data-gradient kernel (the mark then records the DP bucket
+        event there; bwd joins the side stream before it returns), or in line."""
+        if self.rt.async_wred:
+            with self.rt.fork_side():
+                fn(self.rt.stream)
+        else:
+            fn(self.rt.stream)
+
+    def bwd(self, *args, **kw):
+        try:
+            return self._bwd(*args, **kw)
+        finally:
+            self.rt.join_side()
+
+    def _bwd(self, x: Act, dy: Act, dx: Optional[Act], accumulate: bool,
             norm: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
             inp: Optional[Tuple[Act, torch.Tensor, torch.Tensor]] = None,
             inb: Optional[Tuple[Act, torch.Tensor, torch.Tensor, torch.Tensor]] = None):
@@ -330,7 +358,7 @@ class Conv3:
         rows = self.Cop if self.wg_stage is not None else self.Co
         wsf = L.mmseg_conv3_wgrad_ws_floats(V, rows, self.Cip, self.Ci, self.cpg_shift, x.D, x.H, x.W, dy.ld,
                                             x.ld, code)
-        ws = self.rt.ws(wsf) if wsf > 0 else None
+        ws = self._part(wsf) if wsf > 0 else None
         wgrad = self.flat.grad(self.conv.weight)
         nm, nr = (ptr(norm[0]), ptr(norm[1])) if norm is not None else (None, None)
         args = (dy.ptr, dy.ld, x.ptr, x.ld, nm, nr, ptr(self.wg_stage) if self.wg_stage is not None else ptr(wgrad),
@@ -341,15 +369,21 @@ class Conv3:
         with TIMER.region(_gemm_name(self.rt, 0, "conv3"), flops=2.0 * V * self.Co * 27 * self.Ci,
                           nbytes=_io_bytes(self.rt, V, self.Cip, self.Co, 27 * self.Cip * self.Co, 4)):
             L.mmseg_conv3_wgrad_ex(*args, 1, code, s)
-        with TIMER.region("wgrad_reduce_kernel"):
-            L.mmseg_conv3_wgrad_ex(*args, 2, code, s)
-        if self.wg_stage is not None:     # rows [0, Co) of the staging are the gradient's storage order
-            n = wgrad.numel()
-            if accumulate:
-                L.mmseg_add(ptr(wgrad), ptr(self.wg_stage), ptr(wgrad), n, 0, s)
-            else:
-                wgrad.view(-1).copy_(self.wg_stage[:n])
-        self.flat.mark(*[p for p in (self.conv.weight, self.conv.bias) if p is not None])
+
+        def reduce(s2):
+            with TIMER.region("wgrad_reduce_kernel"):
+                L.mmseg_conv3_wgrad_ex(*args, 2, code, s2)
+            if self.wg_stage is not None:     # rows [0, Co) of the staging are the gradient's storage order
+                n = wgrad.numel()
+                if accumulate:
+                    L.mmseg_add(ptr(wgrad), ptr(self.wg_stage), ptr(wgrad), n, 0, s2)
+                else:
+                    wgrad.view(-1).copy_(self.wg_stage[:n])
+            self.flat.mark(*[p for p in (self.conv.weight, self.conv.bias) if p is not None])
+        if wsf > 0:
+            self._reduce_after(reduce)
+        else:
+            reduce(s)
         if dx is not None:
             # dx = (lo, hi): columns [0, lo.C) into lo, the rest into hi (two dense tensors, mmseg_conv_gemm_split)
             split = isinstance(dx, tuple)

@@ -14,6 +14,7 @@ Design (MI355X-first, not a translation of the reference's module graph):
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -71,6 +72,12 @@ class Runtime:
         self.fp8 = fp8
         self.lib = lib()
         self._ws: Dict[int, torch.Tensor] = {}      # one scratch arena per HIP stream
+        # weight-gradient split reduces on a side stream (MMSEG_ASYNC_WRED): each reduce waits for its own
+        # weight-gradient kernel only, so it can run beside the next data-gradient / conv kernels (a memory-bound
+        # sum beside MFMA-bound tiles); the backward joins the side stream before anything reads the gradients
+        self.async_wred = os.environ.get("MMSEG_ASYNC_WRED", "1") != "0"
+        self._side: Optional[torch.cuda.Stream] = None
+        self._side_pending = False
 
     # ---------------------------------------------------------------- alloc
     def act(self, N: int, D: int, H: int, W: int, C: int, ld: Optional[int] = None) -> Act:
@@ -92,6 +99,22 @@ class Runtime:
     @property
     def stream(self) -> int:
         return stream_handle()
+
+    def fork_side(self):
+        """Context: the side stream, after everything issued so far on the current stream (a fork of the capture
+        stream when a step graph is being captured)."""
+        main = torch.cuda.current_stream(self.device)
+        if self._side is None:
+            self._side = torch.cuda.Stream(self.device)
+        self._side.wait_stream(main)
+        self._side_pending = True
+        return torch.cuda.stream(self._side)
+
+    def join_side(self) -> None:
+        """The current stream waits for all side-stream work (end of the backward: the gradients are final)."""
+        if self._side_pending:
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
+            self._side_pending = False
 
 
 class FlatParams:

@@ -143,6 +143,7 @@ class StepGraphs:
                 # and finish() joins every collective into the capture stream before the AdamW kernel
                 tr._arm_buckets(True, ws[-1:])
                 eng.program.backward(None, False, gout=self.gout)
+                eng.rt.join_side()
                 if tr.dp and tr._buckets is not None:
                     tr._buckets.finish()
                 L.mmseg_adamw_dev(ptr(flat.flat), ptr(flat.grad_flat), ptr(m), ptr(v), flat.numel,
