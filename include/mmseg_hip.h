@@ -196,6 +196,27 @@ int mmseg_conv3_wgrad_norm_ok(long long V, int Co, int Cip, int Ci, int cpg_shif
 int mmseg_conv3_wgrad_norm(const void* dy, int lddy, const void* x, int ldx, const float* nmean, const float* nrstd,
                            float* grad, float* bias_grad, int Co, int Cip, int Ci, int cpg_shift, long long V, int D,
                            int H, int W, float* ws, long long ws_floats, int accumulate, int dtype, void* stream);
+/* Grouped forms for `groups` same-shape layers over equal sample groups of one activation tensor (group gi:
+ * samples [gi N / groups, (gi + 1) N / groups)), each with its own weights: the M modality encoders' small levels
+ * (12^3 / 6^3, runtime-brick kernels) as one launch instead of M.  Replace the same ATen ops as mmseg_conv_gemm_ex /
+ * mmseg_conv3_wgrad (reference unet.py:26-27, run once per modality encoder, dual_encoder.py:112-165).
+ * conv_gemm_group: group gi reads wpacked + gi * w_gstride (elements) and bias + gi * b_gstride.
+ * conv3_wgrad_group: group gi's gradients go to grad + gi * grad_gstride / bias_grad + gi * bias_gstride floats;
+ * ws holds mmseg_conv3_wgrad_group_ws_floats() floats; phase as mmseg_conv3_wgrad_ex. */
+int mmseg_conv_gemm_group(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
+                          float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H,
+                          int W, int ksplit, int cin_real, int groups, long long w_gstride, int b_gstride, int dtype,
+                          void* stream);
+int mmseg_conv3_group_ok(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,
+                         int dtype);
+int mmseg_conv3_wgrad_group_ok(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W, int lddy,
+                               int ldx, int dtype);
+long long mmseg_conv3_wgrad_group_ws_floats(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W,
+                                            int lddy, int ldx, int groups, int dtype);
+int mmseg_conv3_wgrad_group(const void* dy, int lddy, const void* x, int ldx, float* grad, float* bias_grad, int Co,
+                            int Cip, int Ci, int cpg_shift, long long V, int D, int H, int W, float* ws,
+                            long long ws_floats, int accumulate, int groups, long long grad_gstride,
+                            int bias_gstride, int phase, int dtype, void* stream);
 /* mmseg_conv3_wgrad (nmean / nrstd: optional deferred norm, as mmseg_conv3_wgrad_norm) in phases: bit 1 runs
  * the weight-gradient kernel, bit 2 the split reduce (3 = both), so the kernel can be timed alone. */
 int mmseg_conv3_wgrad_ex(const void* dy, int lddy, const void* x, int ldx, const float* nmean, const float* nrstd,

@@ -110,6 +110,12 @@ struct GemmArgs {
   // fp8 forward (brick6 F8, mmseg_conv3_fwd_fp8): b holds e4m3 weights w * s[co] (s = 448 / max |w[co]|), wdq[co] =
   // 1 / s[co] restores the scale in the epilogue; the staged activations are e4m3 at unit scale
   const float* wdq;
+  // grouped launch (mmseg_conv_gemm_group, runtime-brick kernel only): the samples are grp_n-sample groups with
+  // their own weights / bias -- group gi reads b + gi * w_gstride (elements) and bias + gi * b_gstride; the M
+  // modality encoders' small levels run as ONE launch over M x N samples
+  int grp_n;
+  long long w_gstride;
+  int b_gstride;
 };
 
 // Output element (row voxel, column) of a GEMM (split-aware; split is a multiple of 8).
@@ -2136,6 +2142,9 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kern
   const int z0 = bzi * bz, y0 = byi * by, x0 = bxi * bx;
   const long long HW = (long long)g.H * g.W;
   const long long nbase = (long long)n * g.D * HW;
+  const int grp = g.grp_n > 0 ? n / g.grp_n : 0;     // grouped launch: this brick's weight / bias group
+  if (grp) Bw += (long long)grp * g.w_gstride;
+  const float* biasp = (g.bias && grp) ? g.bias + grp * g.b_gstride : g.bias;
   const int n0 = nt * BN;
   const int cin = 8 << g.cpg_shift;
   const int nchunk = gemm_nchunk(g);
@@ -2314,7 +2323,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kern
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
       const int col = j * 16 + r16;
-      const float bv = (g.bias && n0 + col < g.Ncols) ? g.bias[n0 + col] : 0.f;
+      const float bv = (biasp && n0 + col < g.Ncols) ? biasp[n0 + col] : 0.f;
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -2527,7 +2536,9 @@ __global__ void gemm_splitk_reduce(GemmArgs g) {
       v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
     }
     if (g.bias) {
-      v.x += g.bias[col]; v.y += g.bias[col + 1]; v.z += g.bias[col + 2]; v.w += g.bias[col + 3];
+      const float* bp = g.grp_n > 0 ? g.bias + (int)(row / ((long long)g.D * g.H * g.W) / g.grp_n) * g.b_gstride
+                                    : g.bias;
+      v.x += bp[col]; v.y += bp[col + 1]; v.z += bp[col + 2]; v.w += bp[col + 3];
     }
     T* O = out_at<T>(g, row, col);
     O[0] = from_f<T>(v.x); O[1] = from_f<T>(v.y); O[2] = from_f<T>(v.z); O[3] = from_f<T>(v.w);
@@ -2546,7 +2557,8 @@ __global__ void gemm_splitk_reduce(GemmArgs g) {
     if (g.bias) v += g.bias[co];
     O[convt_child(row, t, g) * g.ldo + co] = from_f<T>(v);
   } else {
-    if (g.bias) v += g.bias[col];
+    if (g.bias)
+      v += (g.grp_n > 0 ? g.bias + (int)(row / ((long long)g.D * g.H * g.W) / g.grp_n) * g.b_gstride : g.bias)[col];
     *out_at<T>(g, row, col) = from_f<T>(v);
   }
 }
@@ -2586,7 +2598,9 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_s(GemmArgs g) {
   const long long row = idx4 / g.Ncols;
   const int col = (int)(idx4 - row * g.Ncols);
   if (g.bias) {
-    v.x += g.bias[col]; v.y += g.bias[col + 1]; v.z += g.bias[col + 2]; v.w += g.bias[col + 3];
+    const float* bp = g.grp_n > 0 ? g.bias + (int)(row / ((long long)g.D * g.H * g.W) / g.grp_n) * g.b_gstride
+                                  : g.bias;
+    v.x += bp[col]; v.y += bp[col + 1]; v.z += bp[col + 2]; v.w += bp[col + 3];
   }
   T* O = out_at<T>(g, row, col);
   O[0] = from_f<T>(v.x); O[1] = from_f<T>(v.y); O[2] = from_f<T>(v.z); O[3] = from_f<T>(v.w);
@@ -2629,6 +2643,8 @@ struct WgradArgs {
   const float* nrstd;
   int dbg;   // wgrad_brick2 timing probe (MMSEG_WGRAD_DBG): 1 = no global loads after the first brick, 2 = no MFMA
   int frag;  // wgrad_dma: split partials in the fragment-native layout (wgrad_dma_mt, WReduceArgs::frag_mt)
+  int groups;  // grouped launch (wgrad_brickr only): the bricks are `groups` equal sample groups, splits
+               // [gi * ksplit / groups, (gi + 1) * ksplit / groups) cover group gi's bricks only
 };
 
 __host__ __device__ __forceinline__ int wgrad_nchunk(int cpg_shift, int kchunks) {
@@ -3923,9 +3939,13 @@ __global__ __launch_bounds__(512) void wgrad_brickr_kernel(WgradArgs g, int bz_r
   const int HV = HZ * HY * HX, rows = bz * by * bx;
   const int bz_n = g.D / bz, by_n = g.H / by, bx_n = g.W / bx;
   const long long nbrick = (g.V / ((long long)g.D * g.H * g.W)) * bz_n * by_n * bx_n;
-  const long long bpk = (nbrick + g.ksplit - 1) / g.ksplit;
-  const long long b_begin = ks * bpk;
-  const long long b_end = b_begin + bpk < nbrick ? b_begin + bpk : nbrick;
+  // grouped: group gi's bricks (contiguous, sample-major) over its own ksplit / groups splits
+  const int ngrp = g.groups > 1 ? g.groups : 1;
+  const int ks_g = g.ksplit / ngrp, gi = ks / ks_g, kl = ks - gi * ks_g;
+  const long long nb_g = nbrick / ngrp;
+  const long long bpk = (nb_g + ks_g - 1) / ks_g;
+  const long long b_begin = gi * nb_g + kl * bpk;
+  const long long b_end = b_begin + bpk < (gi + 1) * nb_g ? b_begin + bpk : (gi + 1) * nb_g;
   const long long HW = (long long)g.H * g.W;
   const int row0 = rt * CO, c0 = ct * CK;
   const bool do_bias = g.bias_part != nullptr && ct == 0;
@@ -4132,6 +4152,10 @@ struct WReduceArgs {
   int chmajor;        // cols are channel-major (col = c*ntap + tap, brick2/brickr partials) instead of tap-major
   int frag_mt;        // > 0: wgrad_dma's fragment-native partials (MT 16-row tiles per block), see wgrad_dma_kernel
   int nchunk;         // frag_mt > 0: 32-channel chunks per tile row
+  // grouped (blockIdx.y = group gi < gridDim.y): splits [gi * ksplit, (gi + 1) * ksplit) of the partials (ksplit
+  // counts one group's splits), written to grad + gi * grad_gstride / bias_grad + gi * bias_gstride
+  long long grad_gstride;
+  int bias_gstride;
 };
 
 // 256 threads = (256/S) float4 columns x S split slices: slice s sums splits
@@ -4142,6 +4166,13 @@ struct WReduceArgs {
 // the weight range.
 template <int S, int U = 4>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(WReduceArgs g) {
+  if (blockIdx.y) {                           // grouped: this group's splits and gradient
+    const long long gi = blockIdx.y;
+    g.part += gi * g.ksplit * ((long long)g.Ca * g.Ncols);
+    if (g.bias_part) g.bias_part += gi * g.ksplit * g.Ca;
+    g.grad += gi * g.grad_gstride;
+    if (g.bias_grad) g.bias_grad += gi * g.bias_gstride;
+  }
   constexpr int NC = 256 / S;                 // float4 columns per block
   __shared__ float4 red[S][NC];
   const int col4 = threadIdx.x % NC, sl = threadIdx.x / NC;
@@ -4508,6 +4539,8 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
   const Conv3Plan plan = MODE == MODE_CONV3 ? plan_conv3(g.M, g.Ncols, 8 << g.cpg_shift, g.D, g.H, g.W, g.lda, g.ldo,
                                                          (int)sizeof(T))
                                             : Conv3Plan{0, 0, 0, 0, 1, 32};
+  MMSEG_REQUIRE(g.grp_n == 0 || (MODE == MODE_CONV3 && plan.kind == 2),
+                "grouped conv: only the runtime-brick kernel takes per-group weights (small volumes)");
   if (plan.kind == 2) {
     const int nb = (g.M / (g.D * g.H * g.W)) * (g.D / plan.bz) * (g.H / plan.by) * (g.W / plan.bx);
     const int nchunk = gemm_nchunk(g);
@@ -5010,7 +5043,7 @@ Conv3WgradPlan plan_conv3_wgrad(long long V, int Co, int Cip, int Ci, int cpg_sh
   return p;
 }
 
-int launch_wgrad_reduce(WReduceArgs g, void* stream) {
+int launch_wgrad_reduce(WReduceArgs g, void* stream, int groups = 1) {
   const int ksplit = g.ksplit;
   const long long total = (long long)g.Ca * g.Ncols + (g.bias_part ? g.Ca : 0);
   hipStream_t s = (hipStream_t)stream;
@@ -5025,11 +5058,11 @@ int launch_wgrad_reduce(WReduceArgs g, void* stream) {
 #define MMSEG_WRED(SS, NB)                                                                             \
   case SS:                                                                                             \
     if (U >= 16)                                                                                       \
-      MMSEG_LAUNCH((wgrad_reduce_kernel<SS, 16>), dim3(ceil_div(total, NB)), dim3(256), 0, s, g); \
+      MMSEG_LAUNCH((wgrad_reduce_kernel<SS, 16>), dim3(ceil_div(total, NB), groups), dim3(256), 0, s, g); \
     else if (U >= 8)                                                                                   \
-      MMSEG_LAUNCH((wgrad_reduce_kernel<SS, 8>), dim3(ceil_div(total, NB)), dim3(256), 0, s, g);  \
+      MMSEG_LAUNCH((wgrad_reduce_kernel<SS, 8>), dim3(ceil_div(total, NB), groups), dim3(256), 0, s, g);  \
     else                                                                                               \
-      MMSEG_LAUNCH((wgrad_reduce_kernel<SS, 4>), dim3(ceil_div(total, NB)), dim3(256), 0, s, g);  \
+      MMSEG_LAUNCH((wgrad_reduce_kernel<SS, 4>), dim3(ceil_div(total, NB), groups), dim3(256), 0, s, g);  \
     break;
   switch (S) {
     MMSEG_WRED(256, 4)
@@ -5177,7 +5210,21 @@ int mmseg_conv_gemm_stats(const void* a, int lda, const void* wpacked, const flo
 // brick kernels skip the 32-channel chunks wholly past cin_real.  cin_real = 0: every channel is real.
 int conv_gemm_impl(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo, void* out2,
                    int ldo2, int split, float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift,
-                   int D, int H, int W, int ksplit, float* stats_part, int cin_real, int dtype, void* stream);
+                   int D, int H, int W, int ksplit, float* stats_part, int cin_real, int dtype, void* stream,
+                   int groups = 1, long long w_gstride = 0, int b_gstride = 0);
+
+// mmseg_conv_gemm_ex over `groups` equal sample groups of A / out with their own packed weights (group gi:
+// wpacked + gi * w_gstride elements) and bias (bias + gi * b_gstride): the modality encoders' small levels as one
+// launch (+ one split-K reduce).  Runtime-brick CONV3 shapes only (small volumes).
+int mmseg_conv_gemm_group(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
+                          float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H,
+                          int W, int ksplit, int cin_real, int groups, long long w_gstride, int b_gstride, int dtype,
+                          void* stream) {
+  MMSEG_REQUIRE(mode == MODE_CONV3 && groups >= 1 && M % (groups * D * H * W) == 0,
+                "conv_gemm_group: CONV3 over groups x whole samples");
+  return conv_gemm_impl(a, lda, wpacked, bias, out, ldo, nullptr, 0, 0, splitk_ws, mode, M, Ncols, Cpad, KG, cpg_shift,
+                        D, H, W, ksplit, nullptr, cin_real, dtype, stream, groups, w_gstride, b_gstride);
+}
 
 int mmseg_conv_gemm_ex(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
                        float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H,
@@ -5202,7 +5249,8 @@ int mmseg_conv_gemm_split(const void* a, int lda, const void* wpacked, const flo
 
 int conv_gemm_impl(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo, void* out2,
                    int ldo2, int split, float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift,
-                   int D, int H, int W, int ksplit, float* stats_part, int cin_real, int dtype, void* stream) {
+                   int D, int H, int W, int ksplit, float* stats_part, int cin_real, int dtype, void* stream,
+                   int groups, long long w_gstride, int b_gstride) {
   MMSEG_REQUIRE(cin_real >= 0 && cin_real <= (8 << cpg_shift), "conv_gemm: cin_real %d outside [0, %d]", cin_real,
                 8 << cpg_shift);
   MMSEG_REQUIRE(!stats_part || (mode == MODE_CONV3 && ksplit == 1 &&
@@ -5220,6 +5268,11 @@ int conv_gemm_impl(const void* a, int lda, const void* wpacked, const float* bia
              knob("MMSEG_SWIZZLE", 1), stats_part,
              (mode == MODE_CONV3 && knob("MMSEG_KCHUNKS", 1)) ? (cin_real + 31) / 32 : 0, nullptr, nullptr, out2,
              ldo2, split};
+  if (groups > 1) {
+    g.grp_n = M / (D * H * W) / groups;
+    g.w_gstride = w_gstride;
+    g.b_gstride = b_gstride;
+  }
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16) return launch_gemm_mode<bf16_t>(g, mode, s);
   return launch_gemm_mode<float>(g, mode, s);
@@ -5330,6 +5383,19 @@ int mmseg_conv3_dgrad_in(const void* a, int lda, const void* wpacked, void* out,
 
 // Number of K splits the CONV3 path wants for this shape (callers size the
 // split-K workspace, ksplit*M*Ncols floats, with it and pass it as ksplit).
+// 1 when mmseg_conv_gemm_group / mmseg_conv3_wgrad_group take this shape: the runtime-brick conv (plan kind 2)
+// and, for the weight gradient, the runtime-brick weight-gradient kernel (kind 3).
+int mmseg_conv3_group_ok(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,
+                         int dtype) {
+  if (!knob("MMSEG_GROUP_SMALL", 1)) return 0;
+  return plan_conv3(M, Ncols, 8 << cpg_shift, D, H, W, lda, ldo, dtype == MMSEG_BF16 ? 2 : 4).kind == 2 ? 1 : 0;
+}
+int mmseg_conv3_wgrad_group_ok(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W, int lddy,
+                               int ldx, int dtype) {
+  if (!knob("MMSEG_GROUP_SMALL", 1)) return 0;
+  return plan_conv3_wgrad(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype, 1LL << 40).kind == 3 ? 1 : 0;
+}
+
 int mmseg_conv3_splits(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,
                        int dtype) {
   const int tsize = dtype == MMSEG_BF16 ? 2 : 4;
@@ -5409,9 +5475,43 @@ long long mmseg_conv3_wgrad_ws_floats(long long V, int Co, int Cip, int Ci, int 
   return plan_conv3_wgrad(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype, cap).ws;
 }
 
+// Grouped weight gradient (mmseg_conv3_wgrad_group): the plan of the whole V, its split count rounded down to a
+// multiple of `groups` (at least one split per group), never direct.
+Conv3WgradPlan plan_conv3_wgrad_grouped(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W,
+                                        int lda, int ldb, int dtype, long long ws_cap, int groups) {
+  Conv3WgradPlan p = plan_conv3_wgrad(V, Co, Cip, Ci, cpg_shift, D, H, W, lda, ldb, dtype, ws_cap);
+  if (groups <= 1) return p;
+  p.ksplit = p.ksplit / groups * groups;
+  if (p.ksplit < groups) p.ksplit = groups;
+  p.direct = 0;
+  p.ws = (long long)p.ksplit * ((long long)Co * 27 * Cip + Co);
+  return p;
+}
+
+long long mmseg_conv3_wgrad_group_ws_floats(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W,
+                                            int lddy, int ldx, int groups, int dtype) {
+  const long long cap = (long long)knob("MMSEG_WGRAD_CAP_MF", 16) << 20;
+  return plan_conv3_wgrad_grouped(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype, cap, groups).ws;
+}
+
 int conv3_wgrad_impl(const void* dy, int lddy, const void* x, int ldx, const float* nmean, const float* nrstd,
                      float* grad, float* bias_grad, int Co, int Cip, int Ci, int cpg_shift, long long V, int D, int H,
-                     int W, float* ws, long long ws_floats, int accumulate, int dtype, void* stream, int phase = 3);
+                     int W, float* ws, long long ws_floats, int accumulate, int dtype, void* stream, int phase = 3,
+                     int groups = 1, long long grad_gstride = 0, int bias_gstride = 0);
+
+// The weight / bias gradients of `groups` same-shape 3^3 convs over equal sample groups of one activation pair
+// (group gi: samples [gi N / groups, (gi + 1) N / groups) of dy / x, gradient at grad + gi * grad_gstride and
+// bias_grad + gi * bias_gstride floats) in one weight-gradient launch and one reduce -- the modality encoders'
+// small levels.  Runtime-brick weight-gradient shapes only; ws: mmseg_conv3_wgrad_group_ws_floats().
+int mmseg_conv3_wgrad_group(const void* dy, int lddy, const void* x, int ldx, float* grad, float* bias_grad, int Co,
+                            int Cip, int Ci, int cpg_shift, long long V, int D, int H, int W, float* ws,
+                            long long ws_floats, int accumulate, int groups, long long grad_gstride,
+                            int bias_gstride, int phase, int dtype, void* stream) {
+  MMSEG_REQUIRE(groups >= 1 && V % ((long long)groups * D * H * W) == 0 && phase >= 1 && phase <= 3,
+                "conv3_wgrad_group: V must hold groups x whole samples, phase 1..3");
+  return conv3_wgrad_impl(dy, lddy, x, ldx, nullptr, nullptr, grad, bias_grad, Co, Cip, Ci, cpg_shift, V, D, H, W, ws,
+                          ws_floats, accumulate, dtype, stream, phase, groups, grad_gstride, bias_gstride);
+}
 
 int mmseg_conv3_wgrad(const void* dy, int lddy, const void* x, int ldx, float* grad, float* bias_grad, int Co, int Cip,
                       int Ci, int cpg_shift, long long V, int D, int H, int W, float* ws, long long ws_floats,
@@ -5454,11 +5554,14 @@ int mmseg_conv3_wgrad_ex(const void* dy, int lddy, const void* x, int ldx, const
 
 int conv3_wgrad_impl(const void* dy, int lddy, const void* x, int ldx, const float* nmean, const float* nrstd,
                      float* grad, float* bias_grad, int Co, int Cip, int Ci, int cpg_shift, long long V, int D, int H,
-                     int W, float* ws, long long ws_floats, int accumulate, int dtype, void* stream, int phase) {
+                     int W, float* ws, long long ws_floats, int accumulate, int dtype, void* stream, int phase,
+                     int groups, long long grad_gstride, int bias_gstride) {
   MMSEG_REQUIRE(Co % 8 == 0 && Cip % 8 == 0 && Ci <= Cip && (8 << cpg_shift) == Cip,
                 "conv3_wgrad: Co=%d, Cip=%d must be multiples of 8, Ci=%d <= Cip, Cip = 8 << cpg_shift", Co, Cip, Ci);
-  const Conv3WgradPlan p = plan_conv3_wgrad(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype, ws_floats);
+  const Conv3WgradPlan p = plan_conv3_wgrad_grouped(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype, ws_floats,
+                                                    groups);
   MMSEG_REQUIRE(!nmean || p.kind == 2, "conv3_wgrad: a deferred norm needs the brick2 weight-gradient kernel");
+  MMSEG_REQUIRE(groups <= 1 || p.kind == 3, "conv3_wgrad_group: only the runtime-brick weight gradient is grouped");
   MMSEG_REQUIRE(p.ws <= ws_floats && (p.ws == 0 || ws != nullptr), "conv3_wgrad: workspace of %lld floats < %lld",
                 ws_floats, p.ws);
   const int ncols = 27 * Cip;
@@ -5471,14 +5574,16 @@ int conv3_wgrad_impl(const void* dy, int lddy, const void* x, int ldx, const flo
   hipStream_t s = (hipStream_t)stream;
   const int fmt = knob("MMSEG_WGRAD_FRAG", 1) ? wgrad_dma_mt(g, dtype == MMSEG_BF16 ? 2 : 4) : 0;
   g.frag = fmt > 0;
+  g.groups = groups > 1 ? groups : 0;
   if (phase & 1) {
     const int rc = dtype == MMSEG_BF16 ? launch_wgrad<bf16_t, MODE_CONV3>(g, s) : launch_wgrad<float, MODE_CONV3>(g, s);
     if (rc) return rc;
   }
   if (p.direct || !(phase & 2)) return 0;
-  WReduceArgs r{part, grad, bpart, bias_grad, Co, ncols, p.ksplit, Cip, Ci, 27, accumulate, p.kind >= 2 ? 1 : 0,
-                fmt, wgrad_nchunk(cpg_shift, g.kchunks)};
-  return launch_wgrad_reduce(r, stream);
+  const int ng = groups > 1 ? groups : 1;
+  WReduceArgs r{part, grad, bpart, bias_grad, Co, ncols, p.ksplit / ng, Cip, Ci, 27, accumulate, p.kind >= 2 ? 1 : 0,
+                fmt, wgrad_nchunk(cpg_shift, g.kchunks), grad_gstride, bias_gstride};
+  return launch_wgrad_reduce(r, stream, ng);
 }
 
 // Bias gradient: out[c] (+)= sum_v dy[v][c]; part must hold nblk*C floats.

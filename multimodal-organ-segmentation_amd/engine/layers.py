@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import os
 from dataclasses import dataclass
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -672,6 +672,156 @@ class Block:
         (whose backward sums in another order)."""
         return (os.environ.get("MMSEG_STEM_INB", "1") != "0" and not self.c1.need_dgrad
                 and self.x1.V > SMALL_IN_V and self.c1._stem(xin, self.x1.ld))
+
+
+class ConvGroup:
+    """G same-shape Conv3 layers (the M modality encoders' copies of one layer) run as ONE launch over the G x N
+    samples of a combined activation (mmseg_conv_gemm_group / mmseg_conv3_wgrad_group): group g reads its own
+    packed weights (the layers' images are laid out at a fixed stride, DualEncoderProgram) and bias, and writes its
+    own gradients (the encoders' parameters sit at a fixed stride in the flat arena).  At the 12^3 / 6^3 levels a
+    modality's launch fills a fraction of the CUs; the grouped one does twice (M = 2) the work per launch."""
+
+    def __init__(self, convs: List["Conv3"]):
+        self.convs = list(convs)
+        self.G = len(self.convs)
+        c0 = self.convs[0]
+        self.c0, self.rt, self.flat = c0, c0.rt, c0.flat
+
+        def stride(get, es):
+            p = [get(c) for c in self.convs]
+            d = {(p[i + 1] - p[i]) for i in range(len(p) - 1)}
+            if len(d) != 1 or next(iter(d)) % es:
+                return None
+            return next(iter(d)) // es
+        es = self.rt.dtype.itemsize
+        self.w_gs = stride(lambda c: ptr(c.wf), es)
+        self.wd_gs = stride(lambda c: ptr(c.wd), es) if c0.need_dgrad else 0
+        fl = self.flat
+        self.b_gs = stride(lambda c: ptr(c.conv.bias), 4) if c0.conv.bias is not None else 0
+        self.gw_gs = stride(lambda c: ptr(fl.grad(c.conv.weight)), 4)
+        self.gb_gs = stride(lambda c: ptr(fl.grad(c.conv.bias)), 4) if c0.conv.bias is not None else 0
+        self.layout_ok = (None not in (self.w_gs, self.wd_gs, self.b_gs, self.gw_gs, self.gb_gs)
+                          and all(c.wg_stage is None and c.Cip == c.Ci and not c.pad_cols and c.need_dgrad
+                                  for c in self.convs))
+
+    def ok(self, x: Act, y: Act) -> bool:
+        """x / y: the combined (G x N sample) input and output of the layer's forward."""
+        if not self.layout_ok:
+            return False
+        c, L, code = self.c0, self.rt.lib, self.rt.code
+        M = x.N * x.V
+        return (bool(L.mmseg_conv3_group_ok(M, c.ncols_f, c.Cpad, c.KG, c.cpg_shift, x.D, x.H, x.W, x.ld, y.ld, code))
+                and bool(L.mmseg_conv3_group_ok(M, c.ncols_d, c.Cpad_d, c.KGd, c.dshift, x.D, x.H, x.W, y.ld, x.ld,
+                                                code))
+                and bool(L.mmseg_conv3_wgrad_group_ok(M, c.Co, c.Cip, c.Ci, c.cpg_shift, x.D, x.H, x.W, y.ld, x.ld,
+                                                      code)))
+
+    def fwd(self, x: Act, y: Act):
+        c, L = self.c0, self.rt.lib
+        M, nc = x.N * x.V, c.ncols_f
+        ks = L.mmseg_conv3_splits(M, nc, c.Cpad, c.KG, c.cpg_shift, x.D, x.H, x.W, x.ld, y.ld, self.rt.code)
+        ws = self.rt.ws(ks * M * nc) if ks > 1 else None
+        with TIMER.region(_gemm_name(self.rt, nc, "conv3"), flops=2.0 * M * c.Co * 27 * c.Ci,
+                          nbytes=_io_bytes(self.rt, M, c.Cip, c.Co, self.G * 27 * c.Cip * c.Co)):
+            L.mmseg_conv_gemm_group(x.ptr, x.ld, ptr(c.wf), ptr(c.conv.bias), y.ptr, y.ld, ptr(ws), MODE_CONV3, M, nc,
+                                    c.Cpad, c.KG, c.cpg_shift, x.D, x.H, x.W, ks, c.kreal_f, self.G, self.w_gs,
+                                    self.b_gs, self.rt.code, self.rt.stream)
+
+    def bwd(self, x: Act, dy: Act, dx: Optional[Act], accumulate: bool):
+        """Weight / bias gradients of every group (one weight-gradient launch, one reduce -- on the side stream
+        beside the data gradient, as Conv3.bwd), then the data gradient dx (one launch)."""
+        c, L, code = self.c0, self.rt.lib, self.rt.code
+        V = x.N * x.V
+        wsf = L.mmseg_conv3_wgrad_group_ws_floats(V, c.Co, c.Cip, c.Ci, c.cpg_shift, x.D, x.H, x.W, dy.ld, x.ld,
+                                                  self.G, code)
+        ws = c._part(wsf)
+        gw = ptr(self.flat.grad(c.conv.weight))
+        gb = ptr(self.flat.grad(c.conv.bias)) if c.conv.bias is not None else None
+        args = (dy.ptr, dy.ld, x.ptr, x.ld, gw, gb, c.Co, c.Cip, c.Ci, c.cpg_shift, V, x.D, x.H, x.W, ptr(ws), wsf,
+                int(accumulate), self.G, self.gw_gs, self.gb_gs)
+        with TIMER.region(_gemm_name(self.rt, 0, "conv3"), flops=2.0 * V * c.Co * 27 * c.Ci,
+                          nbytes=_io_bytes(self.rt, V, c.Cip, c.Co, self.G * 27 * c.Cip * c.Co, 4)):
+            L.mmseg_conv3_wgrad_group(*args, 1, code, self.rt.stream)
+
+        def reduce(s2):
+            with TIMER.region("wgrad_reduce_kernel"):
+                L.mmseg_conv3_wgrad_group(*args, 2, code, s2)
+            for cc in self.convs:
+                self.flat.mark(*[p for p in (cc.conv.weight, cc.conv.bias) if p is not None])
+        c._reduce_after(reduce)
+        try:
+            if dx is None:
+                return
+            M, nc = V, c.ncols_d
+            ks = L.mmseg_conv3_splits(M, nc, c.Cpad_d, c.KGd, c.dshift, x.D, x.H, x.W, dy.ld, dx.ld, code)
+            ws2 = self.rt.ws(ks * M * nc) if ks > 1 else None
+            with TIMER.region(_gemm_name(self.rt, nc, "conv3"), flops=2.0 * M * c.Co * 27 * c.Ci,
+                              nbytes=_io_bytes(self.rt, M, c.Co, c.Cip, self.G * 27 * c.Cip * c.Co)):
+                L.mmseg_conv_gemm_group(dy.ptr, dy.ld, ptr(c.wd), None, dx.ptr, dx.ld, ptr(ws2), MODE_CONV3, M, nc,
+                                        c.Cpad_d, c.KGd, c.dshift, x.D, x.H, x.W, ks, c.kreal_d, self.G, self.wd_gs, 0,
+                                        code, self.rt.stream)
+        finally:
+            self.rt.join_side()
+
+
+def act_group_view(a: Act, g: int, n: int) -> Act:
+    """Samples [g n, (g + 1) n) of a combined activation as an Act of its own (same buffer)."""
+    return Act(a.buf, a.off + g * n * a.V * a.ld, a.C, a.ld, n, a.D, a.H, a.W)
+
+
+class GroupBlock(Block):
+    """The M modality encoders' ConvBlock3D of one small level as one block over M x N samples (ConvGroup convs,
+    one-launch InstanceNorm over all M x N samples).  The per-modality Block objects keep views of the combined
+    activations and statistics (x1 / y1 / x2 / stats), so everything that reads a modality's block still does."""
+
+    def __init__(self, blocks: List[Block]):
+        self.rt = blocks[0].rt
+        self.blocks = list(blocks)
+        self.G = len(blocks)
+        self.g1 = ConvGroup([b.c1 for b in blocks])
+        self.g2 = ConvGroup([b.c2 for b in blocks])
+        self.c1, self.c2 = blocks[0].c1, blocks[0].c2
+        self.Co = blocks[0].Co
+        self.shape = None
+        self.defer_out = False
+        self.defer1 = False
+        self.norm1_ok = False
+
+    def setup(self, N, D, H, W):
+        """N: samples per modality."""
+        if self.shape == (N, D, H, W):
+            return
+        self.shape = (N, D, H, W)
+        rt, C, G = self.rt, self.Co, self.G
+        self.x1 = rt.act(G * N, D, H, W, C)
+        self.y1 = rt.act(G * N, D, H, W, C)
+        self.x2 = rt.act(G * N, D, H, W, C)
+        self.stats = torch.empty(4, G * N * C, dtype=torch.float32, device=rt.device)
+        for g, b in enumerate(self.blocks):
+            b.shape = (N, D, H, W)
+            b.x1, b.y1, b.x2 = (act_group_view(t, g, N) for t in (self.x1, self.y1, self.x2))
+            b.stats = self.stats[:, g * N * C:(g + 1) * N * C]
+            b.nb, b.norm1_ok, b.defer1, b.defer_out = (0, 0), False, False, False
+
+    def ok(self, xin: Act) -> bool:
+        return self.g1.ok(xin, self.x1) and self.g2.ok(self.x1, self.x2) and self.x1.V <= SMALL_IN_V
+
+    def fwd(self, xin: Act, out: Act):
+        st = self.stats
+        self.g1.fwd(xin, self.x1)
+        self._norm_fwd(self.x1, self.y1, st[0], st[1])
+        self.g2.fwd(self.y1, self.x2)
+        self._norm_fwd(self.x2, out, st[2], st[3])
+
+    def bwd(self, xin: Act, dy: DySpec, dxin: Optional[Act], accumulate: bool):
+        st = self.stats
+        g2 = self.x2
+        self._norm_bwd(self.x2, st[2], st[3], dy, g2)
+        dy1 = self.y1                     # the weight gradient reads y1 before the data gradient overwrites it
+        self.g2.bwd(self.y1, g2, dy1, accumulate)
+        g1 = self.x1
+        self._norm_bwd(self.x1, st[0], st[1], DySpec(p1=dy1), g1)
+        self.g1.bwd(xin, g1, dxin, accumulate)
 
 
 class Head:

@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from .._lib import ptr
-from .layers import Block, ConvT2, DySpec, Head, Packer, Point
+from .layers import Block, ConvT2, DySpec, GroupBlock, Head, Packer, Point, act_group_view
 from .runtime import Act, FlatParams, Runtime
 
 
@@ -232,6 +232,22 @@ class DualEncoderProgram:
         self.dec = _Decoder(rt, m.decoder, m.out_conv, m.dropout_p, flat, self.F)
         self.flat = flat
         self.shape = None
+        # modality-grouped small levels (mean / add fusion): each level's M copies of a conv keep their packed
+        # weight images at one fixed stride, so one launch can serve all M encoders (layers.ConvGroup)
+        self.gblocks = {}
+        if self.M > 1 and self.fusion in ("mean", "add"):
+            for l in range(1, self.L):
+                for attr in ("c1", "c2"):
+                    convs = [self.encs[mm][l].__dict__[attr] for mm in range(self.M)]
+                    for img in ("wf", "wd"):
+                        ts = [c.__dict__[img] for c in convs]
+                        if any(t.numel() != ts[0].numel() for t in ts):
+                            continue
+                        comb = torch.zeros(self.M * ts[0].numel(), dtype=ts[0].dtype, device=ts[0].device)
+                        for c, k in zip(convs, range(self.M)):
+                            c.__dict__[img] = comb[k * ts[0].numel():(k + 1) * ts[0].numel()]
+                self.gblocks[l] = GroupBlock([self.encs[mm][l] for mm in range(self.M)])
+        self.l0 = self.L          # first grouped level (setup)
 
     def _all_descs(self):
         d = []
@@ -270,11 +286,46 @@ class DualEncoderProgram:
         self.idx = [[None] + [torch.empty(N * dims[l][0] * dims[l][1] * dims[l][2] * F[l - 1], dtype=torch.uint8,
                                           device=rt.device) for l in range(1, self.L)] for _ in range(M)]
         self.bottom = rt.act(N, *dims[-1], F[-1])
+        self._setup_groups(N)
         if self.fusion == "attention":
             self.pooled_mean = [torch.empty(N, M * F[l], dtype=torch.float32, device=rt.device) for l in range(self.L)]
             self.gate_h = [torch.empty(N, M * F[l] // 4, dtype=torch.float32, device=rt.device) for l in range(self.L)]
             self.gate_w = [torch.empty(N, M, dtype=torch.float32, device=rt.device) for l in range(self.L)]
             self.gate_beta = [torch.empty(N, M * F[l], dtype=torch.float32, device=rt.device) for l in range(self.L)]
+
+    def _setup_groups(self, N: int):
+        """Grouped levels: the deepest levels whose M encoder blocks take the grouped kernels (12^3 / 6^3 at a
+        96^3 input).  Their pooled inputs, outputs and argmax codes are combined [M x N] tensors; the modality
+        views (self.pooled / y / idx [m][l]) keep every other reader unchanged."""
+        rt, F, M, dims = self.rt, self.F, self.M, self.dims
+        self.l0 = self.L
+        self.pooled_g, self.y_g, self.idx_g, self.rep = {}, {}, {}, {}
+        if not self.gblocks or self.multistream or os.environ.get("MMSEG_GROUP_SMALL", "1") == "0":
+            return
+        for l in range(self.L - 1, 0, -1):
+            gb = self.gblocks[l]
+            gb.setup(N, *dims[l])
+            xin = rt.act(M * N, *dims[l], F[l - 1])
+            if not gb.ok(xin):
+                break
+            self.pooled_g[l] = xin
+            self.y_g[l] = rt.act(M * N, *dims[l], F[l])
+            self.rep[l] = rt.act(M * N, *dims[l], F[l])
+            V = dims[l][0] * dims[l][1] * dims[l][2]
+            self.idx_g[l] = torch.empty(M * N * V * F[l - 1], dtype=torch.uint8, device=rt.device)
+            for mm in range(M):
+                self.pooled[mm][l] = act_group_view(xin, mm, N)
+                self.y[mm][l] = act_group_view(self.y_g[l], mm, N)
+                self.idx[mm][l] = self.idx_g[l][mm * N * V * F[l - 1]:(mm + 1) * N * V * F[l - 1]]
+            self.l0 = l
+
+    def _replicate(self, src: Act, dst: Act):
+        """dst (M x N samples) = src (N samples) repeated M times: the fused level's gradient, which every modality's
+        InstanceNorm backward reads (scaled 1/M), for the grouped one-launch backward."""
+        N, V, C = src.N, src.V, src.C
+        s = src.buf[:N * V * src.ld].view(N * V, src.ld)[:, src.off:src.off + C]
+        d = dst.buf[:dst.N * V * dst.ld].view(self.M, N * V, dst.ld)[:, :, dst.off:dst.off + C]
+        d.copy_(s.unsqueeze(0).expand(self.M, N * V, C))
 
     def fused_out(self, l: int) -> Act:
         return self.dec.skip_slot(l) if l < self.L - 1 else self.bottom
@@ -353,7 +404,18 @@ class DualEncoderProgram:
         on their own (run concurrently they only contend for L2 / Infinity Cache), the smaller ones do not."""
         return int(os.environ.get("MMSEG_STREAM_FROM_LEVEL", "2"))
 
-    def _enc_fwd_levels(self, m: int, x: torch.Tensor, lo: int, hi: int):
+    def _group_fwd_levels(self):
+        """Levels l0 .. L-1 for all modalities at once (the maxpool into l0 ran per modality, into the views)."""
+        L, code, s = self.rt.lib, self.rt.code, self.rt.stream
+        for l in range(self.l0, self.L):
+            if l > self.l0:
+                prev = self.y_g[l - 1]
+                L.mmseg_maxpool2_fwd(prev.ptr, prev.ld, self.pooled_g[l].ptr, self.pooled_g[l].ld,
+                                     ptr(self.idx_g[l]), prev.N, *self.dims[l - 1], prev.C, code, s)
+            self.gblocks[l].fwd(self.pooled_g[l], self.y_g[l])
+
+    def _enc_fwd_levels(self, m: int, x: torch.Tensor, lo: int, hi: int, group_from: Optional[int] = None):
+        """Levels [lo, hi) of modality m; at level group_from only the maxpool runs (its block is grouped)."""
         L, code, s = self.rt.lib, self.rt.code, self.rt.stream
         N, Cx, D, H, W = x.shape
         blocks = self.encs[m]
@@ -371,6 +433,8 @@ class DualEncoderProgram:
             else:
                 L.mmseg_maxpool2_fwd(prev.ptr, prev.ld, self.pooled[m][l].ptr, self.pooled[m][l].ld,
                                      ptr(self.idx[m][l]), N, *self.dims[l - 1], prev.C, code, s)
+            if l == group_from:
+                continue
             blocks[l].fwd(self.pooled[m][l], self.y[m][l])
 
     def forward(self, x: torch.Tensor, training: bool, loss=None) -> torch.Tensor:
@@ -388,11 +452,18 @@ class DualEncoderProgram:
                 self.encs[m][l].defer_out = defer and d[0] * d[1] * d[2] > SMALL_IN_V
         streams = self._streams()
         split = min(max(self.stream_level, 0), self.L)
-        for m in range(self.M):                      # big levels: one stream, modality after modality
-            self._enc_fwd_levels(m, x, 0, split)
-        for m in range(self.M):                      # small levels: modality m on stream m
-            with self._on(streams, m):
-                self._enc_fwd_levels(m, x, split, self.L)
+        if self.l0 < self.L:
+            # grouped small levels: modality after modality down to the maxpool into level l0, then every op of
+            # levels l0 .. L-1 as one launch for all modalities
+            for m in range(self.M):
+                self._enc_fwd_levels(m, x, 0, self.l0 + 1, group_from=self.l0)
+            self._group_fwd_levels()
+        else:
+            for m in range(self.M):                  # big levels: one stream, modality after modality
+                self._enc_fwd_levels(m, x, 0, split)
+            for m in range(self.M):                  # small levels: modality m on stream m
+                with self._on(streams, m):
+                    self._enc_fwd_levels(m, x, split, self.L)
         for m in range(1, self.M):
             if streams[m] is not streams[0]:
                 streams[0].wait_stream(streams[m])
@@ -468,6 +539,17 @@ class DualEncoderProgram:
                 else:
                     blk.bwd(self.xin_v[m], dy, None, accumulate)
 
+        if self.l0 < self.L:                          # grouped small levels: all modalities per launch
+            for l in range(self.L - 1, self.l0 - 1, -1):
+                self._replicate(self.dfused(l), self.rep[l])
+                dy = DySpec(p1=self.rep[l], scale1=sc)
+                if l < self.L - 1:
+                    dy.pool_dy = self.pooled_g[l + 1]
+                    dy.pool_idx = self.idx_g[l + 1]
+                self.gblocks[l].bwd(self.pooled_g[l], dy, self.pooled_g[l], accumulate)   # dp aliases pooled
+            for m in range(M):
+                levels(m, self.l0, 0)
+            return
         for m in range(M):                           # small levels: modality m on stream m
             with self._on(streams, m):
                 levels(m, self.L, split)

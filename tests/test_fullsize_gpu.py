@@ -163,10 +163,11 @@ def _oracle_fwd(kind, mods):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("tag,dtype", [("fullgrad_dual_c3", "float32"), ("fullgrad_dual_c3", "bfloat16"),
-                                       ("fullgrad_unet_c2", "float32"), ("fullgrad_dual_m3_c5", "float32"),
-                                       ("fullgrad_dual_m3_c5", "bfloat16")])
-def test_fullsize_step_pinned_to_fp64_oracle(dev, tag, dtype):
+@pytest.mark.parametrize("tag,dtype,group", [("fullgrad_dual_c3", "float32", "1"), ("fullgrad_dual_c3", "bfloat16", "1"),
+                                             ("fullgrad_unet_c2", "float32", "1"), ("fullgrad_dual_m3_c5", "float32", "1"),
+                                             ("fullgrad_dual_m3_c5", "bfloat16", "1"),
+                                             ("fullgrad_dual_c3", "float32", "0")])
+def test_fullsize_step_pinned_to_fp64_oracle(dev, tag, dtype, group, monkeypatch):
     """The benched step at full size (96^3, B=2; trainer.py:250-254) against oracle/mmseg_oracle.py evaluated in
     fp64 ON THE GPU (torch ops) with the engine's own ReLU masks and MaxPool argmax codes (oracle.Pins, as
     tests/test_model_gpu.py does for the tiny configs).  At 96^3 a ReLU / MaxPool decision within rounding of its
@@ -175,6 +176,7 @@ def test_fullsize_step_pinned_to_fp64_oracle(dev, tag, dtype):
     so EVERY parameter gradient is held to PINNED_TOL (fp32: 1e-4), including the ConvTranspose biases; the conv
     biases in front of an InstanceNorm (true gradient 0) to PINNED_DEAD of the largest gradient."""
     from tests.test_model_gpu import _engine_pins
+    monkeypatch.setenv("MMSEG_GROUP_SMALL", group)   # "1": the modality-grouped 12^3 / 6^3 levels (default)
     g = golden(tag)
     model, mods, loss = CASES[tag]
     S, B, seed, C = int(g["S"]), int(g["B"]), int(g["seed"]), 6
@@ -187,6 +189,9 @@ def test_fullsize_step_pinned_to_fp64_oracle(dev, tag, dtype):
     m.train()
     lossv = tr._fused_loss(x, y)
     assert lossv is not None, "fused head + loss path not taken"
+    if model == "dual_encoder":
+        prog = m.backbone.__dict__["_engine"].program
+        assert prog.l0 == (3 if group == "1" else prog.L), prog.l0    # 12^3 and 6^3 grouped over the modalities
     pins = _engine_pins(m, model)
     pins.relu_masks = [r.to(dev) for r in pins.relu_masks]
     pins.pool_codes = [c.to(dev) for c in pins.pool_codes]
@@ -216,7 +221,7 @@ def test_fullsize_step_pinned_to_fp64_oracle(dev, tag, dtype):
     med = float(np.median(list(errs.values())))
     worst = sorted(((v, n) for n, v in errs.items()), reverse=True)[:4]
     err_loss = abs(lossv.item() - rl.item()) / abs(rl.item())
-    print(f"\n{tag} {dtype} pinned fp64 oracle ({t_orc:.0f} s on the GPU): loss rel {err_loss:.2e}; grad errors "
+    print(f"\n{tag} {dtype} group={group} pinned fp64 oracle ({t_orc:.0f} s on the GPU): loss rel {err_loss:.2e}; grad errors "
           f"median {med:.2e}, worst {[(float(f'{v:.2e}'), n) for v, n in worst]}; L2 median "
           f"{float(np.median(list(l2.values()))):.2e} max {max(l2.values()):.2e}; dead-bias max "
           f"{max(dead.values()):.2e} of the largest gradient")
