@@ -134,6 +134,12 @@ class DySpec:
     part: Optional[Tuple[torch.Tensor, int]] = None
 
 
+def _aliases(x: Act, dx) -> bool:
+    """True when the data-gradient output(s) dx share a buffer with the weight gradient's input x."""
+    outs = dx if isinstance(dx, tuple) else (dx,)
+    return any(o.buf.data_ptr() == x.buf.data_ptr() for o in outs)
+
+
 class Conv3:
     def __init__(self, rt: Runtime, conv: nn.Conv3d, flat: FlatParams, cin_pad: Optional[int] = None,
                  need_dgrad: bool = True, cout_pad: Optional[int] = None, pad_cols: bool = False):
@@ -366,9 +372,22 @@ class Conv3:
                 self.cpg_shift, V, x.D, x.H, x.W, ptr(ws), wsf, int(accumulate) if self.wg_stage is None else 0)
         # the kernel and its split reduce are timed separately (the roofline family is the kernel alone, as in
         # the rocprofv3 trace)
-        with TIMER.region(_gemm_name(self.rt, 0, "conv3"), flops=2.0 * V * self.Co * 27 * self.Ci,
-                          nbytes=_io_bytes(self.rt, V, self.Cip, self.Co, 27 * self.Cip * self.Co, 4)):
-            L.mmseg_conv3_wgrad_ex(*args, 1, code, s)
+        def wkernel(s1):
+            with TIMER.region(_gemm_name(self.rt, 0, "conv3"), flops=2.0 * V * self.Co * 27 * self.Ci,
+                              nbytes=_io_bytes(self.rt, V, self.Cip, self.Co, 27 * self.Cip * self.Co, 4)):
+                L.mmseg_conv3_wgrad_ex(*args, 1, code, s1)
+
+        # weight gradient (kernel + reduce) beside the data gradient (MMSEG_WD_CONC): both only read dy, so when dx
+        # does not overwrite x the two MFMA launches can share the chip -- the tail of one (a partial last round of
+        # blocks, the partials' write burst) overlaps the other
+        conc = (wsf > 0 and dx is not None and self.rt.async_wred and os.environ.get("MMSEG_WD_CONC", "0") != "0"
+                and not _aliases(x, dx))
+        if conc:
+            def both(s2):
+                wkernel(s2)
+                reduce(s2)
+        else:
+            wkernel(s)
 
         def reduce(s2):
             with TIMER.region("wgrad_reduce_kernel"):
@@ -380,7 +399,9 @@ class Conv3:
                 else:
                     wgrad.view(-1).copy_(self.wg_stage[:n])
             self.flat.mark(*[p for p in (self.conv.weight, self.conv.bias) if p is not None])
-        if wsf > 0:
+        if conc:
+            self._reduce_after(both)
+        elif wsf > 0:
             self._reduce_after(reduce)
         else:
             reduce(s)
@@ -643,6 +664,12 @@ class Block:
         g2 = self.x2                      # in place over x2
         self._norm_bwd(self.x2, st[2], st[3], dy, g2)
         dy1 = self.y1                     # conv2 wgrad reads y1 before dgrad overwrites it
+        if not self.defer1 and os.environ.get("MMSEG_WD_CONC", "0") != "0":
+            # a buffer of its own, so conv2's weight and data gradients can run side by side (Conv3.bwd)
+            if getattr(self, "_dy1b", None) is None or self._dy1b.buf.numel() != self.y1.buf.numel():
+                y1 = self.y1
+                self._dy1b = self.rt.act(y1.N, y1.D, y1.H, y1.W, y1.C, y1.ld)
+            dy1 = self._dy1b
         # conv2's data gradient may also sum conv1's InstanceNorm-backward partials (brick5 shapes)
         inp = (self.x1, st[0], st[1])
         if self.defer1:                   # (y1 was never written: the weight gradient normalises x1 itself)
@@ -739,16 +766,23 @@ class ConvGroup:
         gb = ptr(self.flat.grad(c.conv.bias)) if c.conv.bias is not None else None
         args = (dy.ptr, dy.ld, x.ptr, x.ld, gw, gb, c.Co, c.Cip, c.Ci, c.cpg_shift, V, x.D, x.H, x.W, ptr(ws), wsf,
                 int(accumulate), self.G, self.gw_gs, self.gb_gs)
-        with TIMER.region(_gemm_name(self.rt, 0, "conv3"), flops=2.0 * V * c.Co * 27 * c.Ci,
-                          nbytes=_io_bytes(self.rt, V, c.Cip, c.Co, self.G * 27 * c.Cip * c.Co, 4)):
-            L.mmseg_conv3_wgrad_group(*args, 1, code, self.rt.stream)
+        def wkernel(s1):
+            with TIMER.region(_gemm_name(self.rt, 0, "conv3"), flops=2.0 * V * c.Co * 27 * c.Ci,
+                              nbytes=_io_bytes(self.rt, V, c.Cip, c.Co, self.G * 27 * c.Cip * c.Co, 4)):
+                L.mmseg_conv3_wgrad_group(*args, 1, code, s1)
 
         def reduce(s2):
             with TIMER.region("wgrad_reduce_kernel"):
                 L.mmseg_conv3_wgrad_group(*args, 2, code, s2)
             for cc in self.convs:
                 self.flat.mark(*[p for p in (cc.conv.weight, cc.conv.bias) if p is not None])
-        c._reduce_after(reduce)
+        conc = (dx is not None and self.rt.async_wred and os.environ.get("MMSEG_WD_CONC", "0") != "0"
+                and not _aliases(x, dx))
+        if conc:                          # weight gradient beside the data gradient (Conv3.bwd)
+            c._reduce_after(lambda s2: (wkernel(s2), reduce(s2)))
+        else:
+            wkernel(self.rt.stream)
+            c._reduce_after(reduce)
         try:
             if dx is None:
                 return
@@ -818,6 +852,11 @@ class GroupBlock(Block):
         g2 = self.x2
         self._norm_bwd(self.x2, st[2], st[3], dy, g2)
         dy1 = self.y1                     # the weight gradient reads y1 before the data gradient overwrites it
+        if os.environ.get("MMSEG_WD_CONC", "0") != "0":
+            if getattr(self, "_dy1b", None) is None or self._dy1b.buf.numel() != self.y1.buf.numel():
+                y1 = self.y1
+                self._dy1b = self.rt.act(y1.N, y1.D, y1.H, y1.W, y1.C, y1.ld)
+            dy1 = self._dy1b
         self.g2.bwd(self.y1, g2, dy1, accumulate)
         g1 = self.x1
         self._norm_bwd(self.x1, st[0], st[1], DySpec(p1=dy1), g1)
