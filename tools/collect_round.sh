@@ -1,0 +1,15 @@
+#!/bin/bash
+# Copy the judged summaries of one gpu_round.sh call from gpurun_out/TAG into profiles/TAG_* (run locally).
+# usage: bash tools/collect_round.sh TAG
+set -e
+T=$1
+O=gpurun_out/$T
+P=profiles
+[ -f $O/bench.log ] && tail -1 $O/bench.log > $P/${T}_bench.json
+[ -f $O/families.txt ] && cp $O/families.txt $P/${T}_families.txt
+[ -f $O/trace/prof_kernel_stats.csv ] && cp $O/trace/prof_kernel_stats.csv $P/${T}_kernel_stats.csv
+[ -f $O/pmc_traffic.json ] && cp $O/pmc_traffic.json $P/${T}_pmc_traffic.json
+[ -f $O/pmc_sq.json ] && cp $O/pmc_sq.json $P/${T}_pmc_sq.json
+[ -f $O/timer.json ] && python3 tools/timer_dump.py $O/timer.json 40 > $P/${T}_timer.txt
+[ -f $O/gpu_tests.log ] && grep -E "passed|failed|PASSED|FAILED|pinned fp64|held-out|free-running|c5 96|fp8 vs|grouped|Error" $O/gpu_tests.log | cut -c1-400 > $P/${T}_gpu_tests.txt || true
+ls -la $P/${T}_*

@@ -9,7 +9,7 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 if [ "${2:-tests}" = "tests" ]; then
-  timeout -k 10 700 python3 -u -m pytest $R/tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.log 2>&1
+  timeout -k 10 900 python3 -u -m pytest $R/tests -m gpu -q -s --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.log 2>&1
   rc=$?
   tail -3 $O/gpu_tests.log
   # 1 = some test assertions failed (keep measuring); anything else (abort, segfault, timeout) ends the call
