@@ -169,6 +169,10 @@ class UNetProgram:
         self.xin = rt.act(N, *dims[0], 8)
         self.dec.setup(N, dims)
         self.pooled = [None] + [rt.act(N, *dims[l], F[l - 1]) for l in range(1, self.L)]
+        # d(pooled): over pooled itself, or (MMSEG_WD_CONC) buffers of their own so that a block's conv1 weight and
+        # data gradients do not alias and can run side by side (layers.Conv3.bwd)
+        self.dpooled = ([None] + [rt.act(N, *dims[l], F[l - 1]) for l in range(1, self.L)] if _wd_conc()
+                        else self.pooled)
         self.idx = [None] + [torch.empty(N * dims[l][0] * dims[l][1] * dims[l][2] * F[l - 1], dtype=torch.uint8,
                                          device=rt.device) for l in range(1, self.L)]
         self.bottom = rt.act(N, *dims[-1], F[-1])
@@ -204,8 +208,8 @@ class UNetProgram:
         dbottom = self.dec.bwd(self.bottom, dlogits, accumulate, gout)
         dy = DySpec(p1=dbottom)
         for l in range(self.L - 1, 0, -1):
-            self.enc[l - 1].bwd(self.pooled[l], dy, self.pooled[l], accumulate)   # dp aliases pooled
-            dy = DySpec(p1=self.dec.dskip(l - 1), pool_dy=self.pooled[l], pool_idx=self.idx[l])
+            self.enc[l - 1].bwd(self.pooled[l], dy, self.dpooled[l], accumulate)   # dp aliases pooled (default)
+            dy = DySpec(p1=self.dec.dskip(l - 1), pool_dy=self.dpooled[l], pool_idx=self.idx[l])
         self.init.bwd(self.xin_v, dy, None, accumulate)
 
 
@@ -282,6 +286,8 @@ class DualEncoderProgram:
         else:
             self.y = [[rt.act(N, *dims[l], F[l]) for l in range(self.L)] for _ in range(M)]
         self.pooled = [[None] + [rt.act(N, *dims[l], F[l - 1]) for l in range(1, self.L)] for _ in range(M)]
+        self.dpooled = ([[None] + [rt.act(N, *dims[l], F[l - 1]) for l in range(1, self.L)] for _ in range(M)]
+                        if _wd_conc() else self.pooled)
 
         self.idx = [[None] + [torch.empty(N * dims[l][0] * dims[l][1] * dims[l][2] * F[l - 1], dtype=torch.uint8,
                                           device=rt.device) for l in range(1, self.L)] for _ in range(M)]
@@ -299,7 +305,7 @@ class DualEncoderProgram:
         views (self.pooled / y / idx [m][l]) keep every other reader unchanged."""
         rt, F, M, dims = self.rt, self.F, self.M, self.dims
         self.l0 = self.L
-        self.pooled_g, self.y_g, self.idx_g, self.rep = {}, {}, {}, {}
+        self.pooled_g, self.dpooled_g, self.y_g, self.idx_g, self.rep = {}, {}, {}, {}, {}
         if not self.gblocks or self.multistream or os.environ.get("MMSEG_GROUP_SMALL", "1") == "0":
             return
         for l in range(self.L - 1, 0, -1):
@@ -309,12 +315,15 @@ class DualEncoderProgram:
             if not gb.ok(xin):
                 break
             self.pooled_g[l] = xin
+            self.dpooled_g[l] = rt.act(M * N, *dims[l], F[l - 1]) if _wd_conc() else xin
             self.y_g[l] = rt.act(M * N, *dims[l], F[l])
             self.rep[l] = rt.act(M * N, *dims[l], F[l])
             V = dims[l][0] * dims[l][1] * dims[l][2]
             self.idx_g[l] = torch.empty(M * N * V * F[l - 1], dtype=torch.uint8, device=rt.device)
             for mm in range(M):
                 self.pooled[mm][l] = act_group_view(xin, mm, N)
+                if self.dpooled is not self.pooled:
+                    self.dpooled[mm][l] = act_group_view(self.dpooled_g[l], mm, N)
                 self.y[mm][l] = act_group_view(self.y_g[l], mm, N)
                 self.idx[mm][l] = self.idx_g[l][mm * N * V * F[l - 1]:(mm + 1) * N * V * F[l - 1]]
             self.l0 = l
@@ -510,11 +519,11 @@ class DualEncoderProgram:
             for m in range(M):
                 dy = base[m]
                 if l < self.L - 1:
-                    dy.pool_dy = self.pooled[m][l + 1]
+                    dy.pool_dy = self.dpooled[m][l + 1]
                     dy.pool_idx = self.idx[m][l + 1]
                 blk = self.encs[m][l]
                 if l > 0:
-                    blk.bwd(self.pooled[m][l], dy, self.pooled[m][l], accumulate)
+                    blk.bwd(self.pooled[m][l], dy, self.dpooled[m][l], accumulate)
                 else:
                     blk.bwd(self.xin_v[m], dy, None, accumulate)
 
@@ -531,11 +540,11 @@ class DualEncoderProgram:
             for l in range(hi - 1, lo - 1, -1):
                 dy = DySpec(p1=self.dfused(l), scale1=sc)
                 if l < self.L - 1:
-                    dy.pool_dy = self.pooled[m][l + 1]
+                    dy.pool_dy = self.dpooled[m][l + 1]
                     dy.pool_idx = self.idx[m][l + 1]
                 blk = self.encs[m][l]
                 if l > 0:
-                    blk.bwd(self.pooled[m][l], dy, self.pooled[m][l], accumulate)
+                    blk.bwd(self.pooled[m][l], dy, self.dpooled[m][l], accumulate)
                 else:
                     blk.bwd(self.xin_v[m], dy, None, accumulate)
 
@@ -544,9 +553,9 @@ class DualEncoderProgram:
                 self._replicate(self.dfused(l), self.rep[l])
                 dy = DySpec(p1=self.rep[l], scale1=sc)
                 if l < self.L - 1:
-                    dy.pool_dy = self.pooled_g[l + 1]
+                    dy.pool_dy = self.dpooled_g[l + 1]
                     dy.pool_idx = self.idx_g[l + 1]
-                self.gblocks[l].bwd(self.pooled_g[l], dy, self.pooled_g[l], accumulate)   # dp aliases pooled
+                self.gblocks[l].bwd(self.pooled_g[l], dy, self.dpooled_g[l], accumulate)   # dp aliases pooled
             for m in range(M):
                 levels(m, self.l0, 0)
             return
@@ -558,6 +567,10 @@ class DualEncoderProgram:
                 streams[0].wait_stream(streams[m])
         for m in range(M):                           # big levels: one stream
             levels(m, split, 0)
+
+
+def _wd_conc() -> bool:
+    return os.environ.get("MMSEG_WD_CONC", "0") != "0"
 
 
 def _ptr_array(ptrs):
