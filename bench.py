@@ -213,6 +213,9 @@ def main():
                     help="torch: the same model / step through PyTorch-ROCm ops (MIOpen convs; hardware.kernels A/B)")
     ap.add_argument("--fp8", action="store_true",
                     help="config c5's mixed bf16/fp8: e4m3 forward convolutions where the kernel takes them")
+    ap.add_argument("--fresh-inputs", action="store_true",
+                    help="every step's batch at a new device address (a DataLoader's pattern): the captured step "
+                         "runs its copy-graph path (trainer/step_graph.py) instead of a pointer-keyed graph")
     ap.add_argument("--timer-dump", default="", help="write every timed launch (family, site, ms, flops) as JSON")
     ap.add_argument("--amp", default="bf16", choices=["bf16", "fp16"],
                     help="--kernels torch autocast dtype (fp16 + GradScaler = the reference's GPU mode)")
@@ -247,6 +250,10 @@ def main():
         if world > 1:
             dist.barrier()
 
+    if args.fresh_inputs:
+        # no pointer-keyed graphs: every replay first copies its batch into the static input buffers of the copy
+        # graph, as it does for a loader that hands over a new address every step
+        trainer._graphs.MAX_GRAPHS = 0
     step = 0
     for _ in range(args.warmup):
         trainer.train_step(batches[step % len(batches)], step, sync=False)
@@ -349,7 +356,8 @@ def main():
         "vs_baseline": None,
         "dtype": (args.dtype + ("+fp8" if args.fp8 else "")) if args.kernels == "hip"
         else f"{args.amp if args.dtype == 'bf16' else 'fp32'}-autocast",
-        "data": f"synthetic (seeded {'/'.join(mods)} phantoms, pre-staged in HBM)",
+        "data": f"synthetic (seeded {'/'.join(mods)} phantoms, pre-staged in HBM"
+                f"{', a new address every step (copy-graph path)' if args.fresh_inputs else ''})",
         "config": {"workload": f"{workload} {args.size}^3, modalities {'+'.join(mods)}, 6 classes, "
                                f"{'DiceCE' if args.loss == 'dice_ce' else 'Tversky'}, AdamW, per-GPU batch {args.batch}",
                    "model": args.model, "global_batch": args.batch * n_gpus, "patch": [args.size] * 3,
