@@ -239,6 +239,13 @@ int mmseg_instnorm_stats(const void* x, int ldx, int N, long long V, int C, floa
 /* y = relu((x - mean) * rstd)  (InstanceNorm3d + ReLU(inplace), unet.py:54-59). */
 int mmseg_instnorm_relu_fwd(const void* x, int ldx, void* y, int ldy, int N, long long V, int C, const float* mean,
                             const float* rstd, int dtype, void* stream);
+/* mmseg_instnorm_relu_bwd over G modality groups of one combined tensor (N = G x n samples): p1 holds n samples and
+ * sample k reads p1 sample k % p1_nmod (p1_nmod = n) -- the fused level's gradient, read once for all G encoders
+ * (reference dual_encoder.py:193-195 / 184-186 fusion backward + unet.py:34-35 InstanceNorm + ReLU backward). */
+int mmseg_instnorm_relu_bwd_group(const void* x, int ldx, const float* mean, const float* rstd, const void* p1,
+                                  int ld1, float scale1, int p1_nmod, const void* pool_dy, int pool_ld,
+                                  const uint8_t* pool_idx, void* dx, int lddx, int N, int D, int H, int W, int C,
+                                  float* ws, int dtype, void* stream);
 /* Backward of InstanceNorm3d + ReLU with dy gathered as
  *   dy = scale1*alpha1[n]*p1 + beta[n][c] + maxpool_bwd(pool_dy, pool_idx)
  * (MaxPool3d backward unet.py:73 and the DualEncoder fusion backward

@@ -365,6 +365,8 @@ struct DySrc {
   const void* pool_dy;   // [N][Vo][C] with ld pool_ld, or null
   int pool_ld;
   const uint8_t* pool_idx;  // [N][Vo][C]
+  int p1_nmod;           // > 0: p1 holds p1_nmod samples, sample n reads p1 sample n % p1_nmod (the fused level's
+                         // gradient shared by the M modality groups of a grouped backward)
 };
 
 // Per-thread view of a DySrc for one sample and one 8-channel group: the
@@ -386,7 +388,8 @@ struct DyCtx {
     C = C_;
     H = H_;
     W = W_;
-    p1 = s.p1 ? reinterpret_cast<const T*>(s.p1) + (long long)n * V * s.ld1 + cg * 8 : nullptr;
+    const int n1 = s.p1_nmod > 0 ? n % s.p1_nmod : n;
+    p1 = s.p1 ? reinterpret_cast<const T*>(s.p1) + (long long)n1 * V * s.ld1 + cg * 8 : nullptr;
     ld1 = s.ld1;
     sc = s.scale1 * (s.alpha1 ? s.alpha1[n * s.alpha_stride] : 1.f);
     has_beta = s.beta != nullptr;
@@ -1559,6 +1562,25 @@ int mmseg_instnorm_bwd_part(const void* x, int ldx, const float* mean, const flo
                             const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N,
                             int D, int H, int W, int C, int relu, const float* part_in, int nchunk_in, float* ws,
                             int dtype, void* stream);
+int instnorm_bwd_impl(const void* x, int ldx, const float* mean, const float* rstd, const void* p1, int ld1,
+                      float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
+                      const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N, int D,
+                      int H, int W, int C, int relu, const float* part_in, int nchunk_in, float* ws, int dtype,
+                      void* stream, int p1_nmod);
+
+// The InstanceNorm + ReLU backward of G modality encoders' level outputs at once (N = G x n samples of one
+// combined pre-norm tensor / statistics / pooled gradient): every sample reads the fused level's gradient p1 of
+// its own sample index modulo p1_nmod = n -- once per fused sample for all G modalities (reference
+// dual_encoder.py:193-195 mean / 184-186 add fusion backward, unet.py:34-35 InstanceNorm + ReLU).
+int mmseg_instnorm_relu_bwd_group(const void* x, int ldx, const float* mean, const float* rstd, const void* p1,
+                                  int ld1, float scale1, int p1_nmod, const void* pool_dy, int pool_ld,
+                                  const uint8_t* pool_idx, void* dx, int lddx, int N, int D, int H, int W, int C,
+                                  float* ws, int dtype, void* stream) {
+  MMSEG_REQUIRE(p1_nmod >= 1 && N % p1_nmod == 0, "instnorm_relu_bwd_group: N=%d must be a multiple of p1_nmod=%d",
+                N, p1_nmod);
+  return instnorm_bwd_impl(x, ldx, mean, rstd, p1, ld1, scale1, nullptr, 0, nullptr, 0, pool_dy, pool_ld, pool_idx,
+                           dx, lddx, N, D, H, W, C, 1, nullptr, 0, ws, dtype, stream, p1_nmod);
+}
 
 int mmseg_instnorm_bwd(const void* x, int ldx, const float* mean, const float* rstd, const void* p1, int ld1,
                             float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
@@ -1575,6 +1597,15 @@ int mmseg_instnorm_bwd_part(const void* x, int ldx, const float* mean, const flo
                             const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N,
                             int D, int H, int W, int C, int relu, const float* part_in, int nchunk_in, float* ws,
                             int dtype, void* stream) {
+  return instnorm_bwd_impl(x, ldx, mean, rstd, p1, ld1, scale1, alpha1, alpha_stride, beta, beta_stride, pool_dy,
+                           pool_ld, pool_idx, dx, lddx, N, D, H, W, C, relu, part_in, nchunk_in, ws, dtype, stream, 0);
+}
+
+int instnorm_bwd_impl(const void* x, int ldx, const float* mean, const float* rstd, const void* p1, int ld1,
+                      float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
+                      const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N, int D,
+                      int H, int W, int C, int relu, const float* part_in, int nchunk_in, float* ws, int dtype,
+                      void* stream, int p1_nmod) {
   MMSEG_REQUIRE(C % 8 == 0 && C <= 2048, "instnorm_bwd: C=%d must be a multiple of 8 and <= 2048", C);
   MMSEG_REQUIRE(!part_in || nchunk_in > 0, "instnorm_bwd: given partials need their chunk count");
   MMSEG_REQUIRE(!pool_dy || ((D | H | W) & 1) == 0, "instnorm_bwd: pooled gather needs even dims");
@@ -1585,7 +1616,7 @@ int mmseg_instnorm_bwd_part(const void* x, int ldx, const float* mean, const flo
   const int nch = chunks_for(V, C, &vpc);
   int avpc;
   const int anch = apply_chunks(V, C, &avpc);
-  DySrc src{p1, ld1, scale1, alpha1, alpha_stride, beta, beta_stride, pool_dy, pool_ld, pool_idx};
+  DySrc src{p1, ld1, scale1, alpha1, alpha_stride, beta, beta_stride, pool_dy, pool_ld, pool_idx, p1_nmod};
   hipStream_t s = (hipStream_t)stream;
   float* part = ws;
   float* coef = ws + (long long)N * nch * C * 2;
