@@ -659,10 +659,12 @@ class Block:
         L.mmseg_instnorm_relu_fwd(self.x2.ptr, self.x2.ld, out.ptr, out.ld, self.x2.N, self.x2.V, self.x2.C,
                                   ptr(self.stats[2]), ptr(self.stats[3]), self.rt.code, self.rt.stream)
 
-    def bwd(self, xin: Act, dy: DySpec, dxin: Optional[Act], accumulate: bool):
+    def bwd(self, xin: Act, dy: Optional[DySpec], dxin: Optional[Act], accumulate: bool, out_done: bool = False):
+        """out_done: the output InstanceNorm's backward already ran (grouped over the modalities, in place over x2)."""
         st = self.stats
         g2 = self.x2                      # in place over x2
-        self._norm_bwd(self.x2, st[2], st[3], dy, g2)
+        if not out_done:
+            self._norm_bwd(self.x2, st[2], st[3], dy, g2)
         dy1 = self.y1                     # conv2 wgrad reads y1 before dgrad overwrites it
         if not self.defer1 and os.environ.get("MMSEG_WD_CONC", "0") != "0":
             # a buffer of its own, so conv2's weight and data gradients can run side by side (Conv3.bwd)

@@ -285,14 +285,22 @@ class DualEncoderProgram:
             self.y = [[self.ycat[l].slot(m * F[l], F[l]) for l in range(self.L)] for m in range(M)]
         else:
             self.y = [[rt.act(N, *dims[l], F[l]) for l in range(self.L)] for _ in range(M)]
-        self.pooled = [[None] + [rt.act(N, *dims[l], F[l - 1]) for l in range(1, self.L)] for _ in range(M)]
-        self.dpooled = ([[None] + [rt.act(N, *dims[l], F[l - 1]) for l in range(1, self.L)] for _ in range(M)]
-                        if _wd_conc() else self.pooled)
-
-        self.idx = [[None] + [torch.empty(N * dims[l][0] * dims[l][1] * dims[l][2] * F[l - 1], dtype=torch.uint8,
-                                          device=rt.device) for l in range(1, self.L)] for _ in range(M)]
+        # pooled inputs, their gradients and the argmax codes: one [M x N]-sample tensor per level, the modalities'
+        # views of it (a grouped op reads all modalities at once, everything else its own view)
+        vol = [d[0] * d[1] * d[2] for d in dims]
+        self.pooled_c = [None] + [rt.act(M * N, *dims[l], F[l - 1]) for l in range(1, self.L)]
+        self.dpooled_c = ([None] + [rt.act(M * N, *dims[l], F[l - 1]) for l in range(1, self.L)] if _wd_conc()
+                          else self.pooled_c)
+        self.idx_c = [None] + [torch.empty(M * N * vol[l] * F[l - 1], dtype=torch.uint8, device=rt.device)
+                               for l in range(1, self.L)]
+        self.pooled = [[None] + [act_group_view(self.pooled_c[l], m, N) for l in range(1, self.L)] for m in range(M)]
+        self.dpooled = ([[None] + [act_group_view(self.dpooled_c[l], m, N) for l in range(1, self.L)]
+                         for m in range(M)] if _wd_conc() else self.pooled)
+        self.idx = [[None] + [self.idx_c[l][m * N * vol[l] * F[l - 1]:(m + 1) * N * vol[l] * F[l - 1]]
+                              for l in range(1, self.L)] for m in range(M)]
         self.bottom = rt.act(N, *dims[-1], F[-1])
         self._setup_groups(N)
+        self._setup_outnorm(N)
         if self.fusion == "attention":
             self.pooled_mean = [torch.empty(N, M * F[l], dtype=torch.float32, device=rt.device) for l in range(self.L)]
             self.gate_h = [torch.empty(N, M * F[l] // 4, dtype=torch.float32, device=rt.device) for l in range(self.L)]
@@ -311,22 +319,39 @@ class DualEncoderProgram:
         for l in range(self.L - 1, 0, -1):
             gb = self.gblocks[l]
             gb.setup(N, *dims[l])
-            xin = rt.act(M * N, *dims[l], F[l - 1])
+            xin = self.pooled_c[l]
             if not gb.ok(xin):
                 break
             self.pooled_g[l] = xin
-            self.dpooled_g[l] = rt.act(M * N, *dims[l], F[l - 1]) if _wd_conc() else xin
+            self.dpooled_g[l] = self.dpooled_c[l]
             self.y_g[l] = rt.act(M * N, *dims[l], F[l])
             self.rep[l] = rt.act(M * N, *dims[l], F[l])
-            V = dims[l][0] * dims[l][1] * dims[l][2]
-            self.idx_g[l] = torch.empty(M * N * V * F[l - 1], dtype=torch.uint8, device=rt.device)
+            self.idx_g[l] = self.idx_c[l]
             for mm in range(M):
-                self.pooled[mm][l] = act_group_view(xin, mm, N)
-                if self.dpooled is not self.pooled:
-                    self.dpooled[mm][l] = act_group_view(self.dpooled_g[l], mm, N)
                 self.y[mm][l] = act_group_view(self.y_g[l], mm, N)
-                self.idx[mm][l] = self.idx_g[l][mm * N * V * F[l - 1]:(mm + 1) * N * V * F[l - 1]]
             self.l0 = l
+
+    def _setup_outnorm(self, N: int):
+        """Levels above the grouped ones (mean / add fusion): each encoder block's output InstanceNorm backward runs
+        for all M modalities as one launch sequence (mmseg_instnorm_relu_bwd_group), reading the fused level's
+        gradient once instead of M times.  The blocks' pre-norm outputs x2 and statistics become views of one
+        [M x N]-sample tensor per level (self.x2c / self.statsc)."""
+        rt, F, M, dims = self.rt, self.F, self.M, self.dims
+        self.x2c, self.statsc = {}, {}
+        self.group_outnorm = (M > 1 and self.fusion in ("mean", "add") and not self.multistream
+                              and os.environ.get("MMSEG_GROUP_OUTNORM", "1") != "0")
+        if not self.group_outnorm:
+            return
+        for l in range(min(self.l0, self.L)):
+            C = F[l]
+            x2c = rt.act(M * N, *dims[l], C)
+            stc = torch.empty(4, M * N * C, dtype=torch.float32, device=rt.device)
+            for m in range(M):
+                b = self.encs[m][l]
+                b.setup(N, *dims[l])
+                b.x2 = act_group_view(x2c, m, N)
+                b.stats = stc[:, m * N * C:(m + 1) * N * C]
+            self.x2c[l], self.statsc[l] = x2c, stc
 
     def _replicate(self, src: Act, dst: Act):
         """dst (M x N samples) = src (N samples) repeated M times: the fused level's gradient, which every modality's
@@ -556,8 +581,28 @@ class DualEncoderProgram:
                     dy.pool_dy = self.dpooled_g[l + 1]
                     dy.pool_idx = self.idx_g[l + 1]
                 self.gblocks[l].bwd(self.pooled_g[l], dy, self.dpooled_g[l], accumulate)   # dp aliases pooled
-            for m in range(M):
-                levels(m, self.l0, 0)
+            if not self.group_outnorm:
+                for m in range(M):
+                    levels(m, self.l0, 0)
+                return
+        if self.group_outnorm:
+            L, s, code = self.rt.lib, self.rt.stream, self.rt.code
+            for l in range(min(self.l0, self.L) - 1, -1, -1):
+                # the M output-norm backwards of level l at once, in place over the combined pre-norm outputs
+                x2c, stc, p1 = self.x2c[l], self.statsc[l], self.dfused(l)
+                NG = x2c.N
+                ws = self.rt.ws(L.mmseg_instnorm_ws_floats(NG, x2c.V, x2c.C))
+                pdy = self.dpooled_c[l + 1] if l < self.L - 1 else None
+                L.mmseg_instnorm_relu_bwd_group(x2c.ptr, x2c.ld, ptr(stc[2]), ptr(stc[3]), p1.ptr, p1.ld, sc, p1.N,
+                                                pdy.ptr if pdy is not None else None, pdy.ld if pdy is not None else 0,
+                                                ptr(self.idx_c[l + 1]) if pdy is not None else None, x2c.ptr, x2c.ld,
+                                                NG, *self.dims[l], x2c.C, ptr(ws), code, s)
+                for m in range(M):
+                    blk = self.encs[m][l]
+                    if l > 0:
+                        blk.bwd(self.pooled[m][l], None, self.dpooled[m][l], accumulate, out_done=True)
+                    else:
+                        blk.bwd(self.xin_v[m], None, None, accumulate, out_done=True)
             return
         for m in range(M):                           # small levels: modality m on stream m
             with self._on(streams, m):
