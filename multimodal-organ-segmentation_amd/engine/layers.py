@@ -801,8 +801,10 @@ class ConvGroup:
 
 
 def act_group_view(a: Act, g: int, n: int) -> Act:
-    """Samples [g n, (g + 1) n) of a combined activation as an Act of its own (same buffer)."""
-    return Act(a.buf, a.off + g * n * a.V * a.ld, a.C, a.ld, n, a.D, a.H, a.W)
+    """Samples [g n, (g + 1) n) of a combined activation as an Act of its own: a view of the same memory whose
+    buffer starts at the group's first sample (Act.off stays the offset inside a voxel row)."""
+    span = n * a.V * a.ld
+    return Act(a.buf[g * span:(g + 1) * span], a.off, a.C, a.ld, n, a.D, a.H, a.W)
 
 
 class GroupBlock(Block):

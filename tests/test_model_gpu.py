@@ -636,3 +636,41 @@ def test_deferred_encoder_norm_bitwise(dev, dtype, monkeypatch):
     assert torch.equal(res[0][0], res[1][0])
     assert torch.equal(res[0][1], res[1][1])
     assert all(torch.equal(a, b) for a, b in zip(res[0][2], res[1][2]))
+
+
+@pytest.mark.parametrize("tag", ["dual_tiny_cross_attention", "dual_tiny_add", "dual_tiny_m3_tversky"])
+def test_grouped_modalities_match_per_modality(dev, tag, monkeypatch):
+    """bf16 (the dtype whose small levels take the runtime-brick kernels): the modality-grouped small levels and the
+    grouped encoder output-norm backward (MMSEG_GROUP_SMALL / MMSEG_GROUP_OUTNORM, programs.DualEncoderProgram)
+    against the per-modality launches on the same weights and batch.  The grouped launches split the reductions
+    differently (one launch over M x N samples), so the two differ by bf16 rounding: loss within 1e-3 relative,
+    logits within 2e-2 and every gradient within 5e-2 normwise (L2)."""
+    kind, mods, C, fusion, lossname = TINY[tag]
+    g = golden(tag)
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("MMSEG_GROUP_SMALL", flag)
+        monkeypatch.setenv("MMSEG_GROUP_OUTNORM", flag)
+        cfg = make_config(kind, mods, C, list(g["features"]), fusion=fusion, loss=lossname, dtype="bfloat16")
+        torch.manual_seed(int(g["seed"]))
+        m = build_model(cfg)
+        xs, ys = _inputs(g, len(mods), C)
+        tr = Trainer(cfg, m)
+        m.train()
+        loss = tr.criterion(m(xs[0].to(dev)), ys[0].to(dev))
+        loss.backward()
+        prog = m.backbone.__dict__["_engine"].program
+        with torch.no_grad():
+            logits = m(xs[0].to(dev)).float().cpu()
+        res[flag] = (loss.item(), logits, {n: p.grad.detach().double().cpu().clone()
+                                           for n, p in m.backbone.named_parameters()}, prog.l0, prog.L,
+                     prog.group_outnorm)
+    (l1, lg1, g1, l0, L, go), (l2, lg2, g2, l0b, _, gob) = res["1"], res["0"]
+    print(f"\n{tag}: grouped from level {l0} of {L} (output norm grouped: {go}); loss {l1:.6f} vs {l2:.6f}")
+    assert l0 < L and go and l0b == L and not gob
+    assert abs(l1 - l2) < 1e-3 * abs(l2)
+    assert float((lg1 - lg2).norm() / lg2.norm()) < 2e-2
+    bad = {n: float((g1[n] - g2[n]).norm() / g2[n].norm()) for n in g2
+           if not n.endswith(("conv1.bias", "conv2.bias")) and g2[n].norm() > 0
+           and float((g1[n] - g2[n]).norm() / g2[n].norm()) > 5e-2}
+    assert not bad, bad
