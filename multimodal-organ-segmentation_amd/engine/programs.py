@@ -357,8 +357,9 @@ class DualEncoderProgram:
         """dst (M x N samples) = src (N samples) repeated M times: the fused level's gradient, which every modality's
         InstanceNorm backward reads (scaled 1/M), for the grouped one-launch backward."""
         N, V, C = src.N, src.V, src.C
-        s = src.buf[:N * V * src.ld].view(N * V, src.ld)[:, src.off:src.off + C]
-        d = dst.buf[:dst.N * V * dst.ld].view(self.M, N * V, dst.ld)[:, :, dst.off:dst.off + C]
+        # element (n, v, c) at buf[(n V + v) ld + off + c] (off may reach past the first row: decoder dsplit halves)
+        s = src.buf.as_strided((N * V, C), (src.ld, 1), src.buf.storage_offset() + src.off)
+        d = dst.buf.as_strided((self.M, N * V, C), (N * V * dst.ld, dst.ld, 1), dst.buf.storage_offset() + dst.off)
         d.copy_(s.unsqueeze(0).expand(self.M, N * V, C))
 
     def fused_out(self, l: int) -> Act:
