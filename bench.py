@@ -288,7 +288,10 @@ def main():
         with open(args.timer_dump, "w") as f:
             json.dump({"timer_steps": args.timer_steps, "launches": TIMER.records()}, f)
     fam = TIMER.summary()
-    dom = max(fam.items(), key=lambda kv: kv[1]["ms"]) if fam else None
+    # the dominant MFMA kernel: the family with algorithmic FLOPs and the largest time per step (helper launches
+    # without FLOPs -- split reduces, packing, norms -- are HBM-bound and listed in kernel_families)
+    mfma = {k: v for k, v in fam.items() if v["flops"] > 0}
+    dom = max(mfma.items(), key=lambda kv: kv[1]["ms"]) if mfma else None
 
     if rank != 0:
         if world > 1:

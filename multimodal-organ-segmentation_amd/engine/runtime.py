@@ -72,10 +72,11 @@ class Runtime:
         self.fp8 = fp8
         self.lib = lib()
         self._ws: Dict[int, torch.Tensor] = {}      # one scratch arena per HIP stream
-        # weight-gradient split reduces on a side stream (MMSEG_ASYNC_WRED): each reduce waits for its own
-        # weight-gradient kernel only, so it can run beside the next data-gradient / conv kernels (a memory-bound
-        # sum beside MFMA-bound tiles); the backward joins the side stream before anything reads the gradients
-        self.async_wred = os.environ.get("MMSEG_ASYNC_WRED", "1") != "0"
+        # weight-gradient split reduces on a side stream (MMSEG_ASYNC_WRED=1): each reduce waits for its own
+        # weight-gradient kernel only, so it can run beside the layer's data-gradient kernel.  Off by default:
+        # measured +0.3 ms per 96^3 step (6.45 -> 6.75 ms, r04c A/B) -- in the captured graph every fork / join
+        # is a cross-queue dependency that costs more than the overlap wins
+        self.async_wred = os.environ.get("MMSEG_ASYNC_WRED", "0") != "0"
         self._side: Optional[torch.cuda.Stream] = None
         self._side_pending = False
 

@@ -260,7 +260,8 @@ def test_fullsize_c5_fp8_step(dev):
         tr = Trainer(cfg, m)
         m.train()
         lossv = tr._fused_loss(x, y)
-        assert lossv is not None
+        if lossv is None:                 # the e4m3 forward keeps the unfused head + loss
+            lossv = tr.criterion(m(x), y)
         lossv.backward()
         if fp8:
             prog = m.backbone.__dict__["_engine"].program
