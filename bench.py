@@ -82,6 +82,8 @@ def _family_key(d: dict, kernel: str):
     for suf in ("[bf16]", "[f32]"):
         if kernel + suf in d:
             return kernel + suf
+        if kernel.endswith(suf) and kernel[:-len(suf)] in d:
+            return kernel[:-len(suf)]
     base = kernel.split("<")[0]
     return base if base in d else None
 
@@ -114,7 +116,7 @@ def pmc_mfma_busy(kernel: str):
         return None, os.path.relpath(files[-1], ROOT)
     v = d[key]
     out = {"mfma_busy": round(v["mfma_busy"], 4)}
-    for k in ("valu_per_mfma", "lds_per_mfma", "clock_ghz"):
+    for k in ("valu_per_mfma", "lds_per_mfma", "clock_ghz", "counter_gflop"):
         if v.get(k) is not None:
             out[k] = round(v[k], 3)
     return out, os.path.relpath(files[-1], ROOT)
@@ -321,6 +323,11 @@ def main():
                              "timestamps, the rocprofv3 kernel-trace interval)"}
         busy, bsrc = pmc_mfma_busy(name)
         if busy is not None:
+            # SQ_VALU_MFMA_BUSY_CYCLES x 1,024 FLOPs / SIMD-cycle re-counts the MFMA work from the counters alone:
+            # counter_gflop / algorithmic_gflop ~ 1 (above 1 only by K padding) pins the FLOPs `achieved` divides
+            if busy.get("counter_gflop") is not None:
+                busy["counter_gflop_per_launch"] = round(busy.pop("counter_gflop"), 3)
+                busy["counter_vs_algorithmic"] = round(busy["counter_gflop_per_launch"] * 1e9 / flops_per_launch, 4)
             roofline.update(busy)
             roofline["mfma_busy_source"] = bsrc
     families = {k: {"ms_per_step": round(v["ms"] / args.timer_steps, 3),

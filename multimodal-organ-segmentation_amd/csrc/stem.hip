@@ -211,18 +211,22 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(StemArgs g) {
 // block = a contiguous range of bricks; wave w accumulates the brick's voxel
 // steps w, w+4 (2 x 32 voxels) into the full [CO][KP] tile; the 4 wave tiles
 // are added in order at the end (deterministic).
+// CR = 1 (the DualEncoder stems): held to 128 VGPRs, 4 waves / SIMD, so all 1,024 blocks of the 96^3 B=2 grid
+// are resident at once (at 3 waves / SIMD the last 256 ran as a second round); wider CR would spill.
 template <typename T, int RM, int RNK, int CR, bool INB = false>
-__global__ __launch_bounds__(256) void stem_wgrad_kernel(StemArgs g) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CR == 1 ? 4 : 1))) void stem_wgrad_kernel(StemArgs g) {
   constexpr int K = 27 * CR, KP = RNK * 16, CO = RM * 16, CGd = CO / 8;
   static_assert(KP == ((K + 31) / 32) * 32, "KP = 27 CR padded to 32");
   constexpr int DP = CO + 8;
   constexpr int HB = ((SHV * CR * (int)sizeof(T) + 15) / 16) * 16, DB = 256 * DP * (int)sizeof(T);
   constexpr int RB = 4 * CO * (KP + 1) * 4;
-  constexpr int LB = (HB + DB + KP * 4) > RB ? (HB + DB + KP * 4) : RB;
+  constexpr int SB = INB ? CO * 16 : 0;   // INB: the sample's norm statistics [CO] x (mean, rstd, a, b)
+  constexpr int LB = (HB + DB + KP * 4 + SB) > RB ? (HB + DB + KP * 4 + SB) : RB;
   __shared__ __attribute__((aligned(16))) unsigned char lds_raw[LB];
   T* Hl = reinterpret_cast<T*>(lds_raw);
   T* Dl = reinterpret_cast<T*>(lds_raw + HB);
   int* Kl = reinterpret_cast<int*>(lds_raw + HB + DB);
+  float4* Sl = reinterpret_cast<float4*>(lds_raw + HB + DB + KP * 4);
   float (*red)[CO][KP + 1] = reinterpret_cast<float (*)[CO][KP + 1]>(lds_raw);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bz_n = g.D / SZ, by_n = g.H / SY, bx_n = g.W / SX;
@@ -241,8 +245,8 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemArgs g) {
     for (int j = 0; j < RNK; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;   // bias partial of channel tid % CO over voxel slice tid / CO
   int bko[RNK];       // this lane's im2col column per k tile (compact-halo offset), -1 = padding
-  // INB: the thread's 8 channels (group tid % CGd, the same in every staging item) and their statistics
-  float imu[8], irs[8], ica[8], icb[8];
+  // INB: the statistics of the current sample live in LDS (Sl), read per channel while staging -- in registers
+  // (32 VGPRs) they held the kernel at 3 waves / SIMD, 768 resident blocks for the 1,024-split grid
   int in_n = -1;
   // dy (and, INB, the norm's pre-norm input) of the NEXT brick is loaded into registers before this brick's MFMA
   // phase, so its HBM latency hides behind the MFMAs (thread item qq: voxel (tid + 256 qq) / CGd, channel group
@@ -274,16 +278,13 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemArgs g) {
     const long long nbase = (long long)(q / bz_n) * g.D * HW;
     const int z0 = bz * SZ, y0 = by * SY, x0 = bx * SX;
     if constexpr (INB) {
+      // (the previous brick's staging read Sl before its second barrier)
       const int n = q / bz_n;
       if (n != in_n) {
         in_n = n;
-        const int c0 = n * CO + (tid % CGd) * 8;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          imu[j] = g.inmean[c0 + j];
-          irs[j] = g.inrstd[c0 + j];
-          ica[j] = g.incoef[(c0 + j) * 2];
-          icb[j] = g.incoef[(c0 + j) * 2 + 1];
+        if (tid < CO) {
+          const int c = n * CO + tid;
+          Sl[tid] = make_float4(g.inmean[c], g.inrstd[c], g.incoef[c * 2], g.incoef[c * 2 + 1]);
         }
       }
     }
@@ -301,10 +302,11 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemArgs g) {
       if constexpr (INB) {   // in_bwd_apply's operations (DyCtx with p1 = dy, scale 1, no beta / pool)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
+          const float4 st = Sl[cg * 8 + j];   // (mean, rstd, a, b)
           const float dyv = d.get(j) * 1.f + 0.f;
-          const float h = (px[qq].get(j) - imu[j]) * irs[j];
+          const float h = (px[qq].get(j) - st.x) * st.y;
           const float gg = h > 0.f ? dyv : 0.f;
-          d.set(j, irs[j] * (gg - ica[j] - h * icb[j]));
+          d.set(j, st.y * (gg - st.z - h * st.w));
         }
       }
       d.store(Dl + v * DP + cg * 8);

@@ -123,8 +123,11 @@ N_SIMD, N_XCD = 1024, 8
 
 def sq(csv_path: str, trace_stats: str = None):
     """Per family, averaged over its dispatches: MFMA-pipe busy = SQ_VALU_MFMA_BUSY_CYCLES (summed over the SIMDs)
-    / (1,024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs), the VALU and LDS instructions issued per MFMA, and -- when the
-    rows carry timestamps -- the effective clock GRBM_GUI_ACTIVE / 8 / duration (MI355X_MICROARCH.md DVFS)."""
+    / (1,024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs), the VALU and LDS instructions issued per MFMA, the MFMA FLOPs the
+    busy cycles account for (counter_gflop, bf16 rate: divided by the kernel-trace duration this is the kernel's
+    TFLOP/s from rocprofv3 alone), and -- when the rows carry timestamps -- the effective clock GRBM_GUI_ACTIVE /
+    8 / duration (MI355X_MICROARCH.md DVFS; it reads high on dispatches under ~0.3 ms, so the busy fraction reads
+    low there)."""
     per = defaultdict(lambda: defaultdict(float))
     fam_of, dur = {}, {}
     with open(csv_path) as f:
@@ -146,6 +149,10 @@ def sq(csv_path: str, trace_stats: str = None):
             a["valu_per_mfma"].append(c.get("SQ_INSTS_VALU", 0.0) / nm)
             a["lds_per_mfma"].append(c.get("SQ_INSTS_LDS", 0.0) / nm)
         a["mfma_insts"].append(nm)
+        # dense bf16 MFMA: 1,024 FLOPs per SIMD per busy cycle (16x16x32 = 16,384 FLOPs in 16 cycles,
+        # MI355X_MICROARCH.md: 32 cycles per 32x32x16), so the busy cycles re-count the kernel's MFMA FLOPs
+        a["mfma_busy_cycles"].append(c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0))
+        a["counter_gflop"].append(c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) * 1024 / 1e9)
         if did in dur and dur[did] > 0:
             a["clock_ghz"].append(gui / N_XCD / dur[did] / 1e9)
     res = {}
