@@ -2645,7 +2645,16 @@ struct WgradArgs {
   int frag;  // wgrad_dma: split partials in the fragment-native layout (wgrad_dma_mt, WReduceArgs::frag_mt)
   int groups;  // grouped launch (wgrad_brickr only): the bricks are `groups` equal sample groups, splits
                // [gi * ksplit / groups, (gi + 1) * ksplit / groups) cover group gi's bricks only
+  // grouped with one split per group (ksplit == groups) and grad != null: split gi writes group gi's gradient
+  // straight to grad + gi * grad_gstride (bias_grad + gi * bias_gstride), no partials and no reduce
+  long long grad_gstride;
+  int bias_gstride;
 };
+
+// the launch writes the gradient itself: one split, or one split per group of a grouped launch
+__device__ __forceinline__ bool wgrad_direct(const WgradArgs& g) {
+  return g.ksplit == 1 || (g.groups > 1 && g.ksplit == g.groups);
+}
 
 __host__ __device__ __forceinline__ int wgrad_nchunk(int cpg_shift, int kchunks) {
   const int n = (8 << cpg_shift) / 32;
@@ -3082,8 +3091,9 @@ template <int MT, int RP = 16>
 __device__ __forceinline__ void wgrad_store_chmajor(const f32x4 (&acc)[4][MT][2], int t_begin, int t_cnt, float* L,
                                                     const WgradArgs& g, int ks, int row0, int c0) {
   const int tid = threadIdx.x, lane = tid & 63, g4 = lane >> 4, i16 = lane & 15;
-  const bool direct = g.grad != nullptr && g.ksplit == 1;
-  float* base = direct ? g.grad : g.part + (long long)ks * g.Ca * g.Ncols;
+  const bool direct = g.grad != nullptr && wgrad_direct(g);
+  float* base = direct ? g.grad + (g.ksplit > 1 ? (long long)ks * g.grad_gstride : 0LL)
+                       : g.part + (long long)ks * g.Ca * g.Ncols;
   const bool accum = direct && g.accumulate;
   constexpr int GP = RP / 4;   // lane groups per pass
 #pragma unroll
@@ -3132,10 +3142,12 @@ __device__ __forceinline__ void wgrad_store_bias(const float (&bsum)[8], float* 
     const int cg = tid >> 3, j = tid & 7;
     float sacc = 0.f;
     for (int t = cg; t < 512; t += CG) sacc += red[t * 8 + j];
-    if (g.bias_grad != nullptr && g.ksplit == 1)
-      g.bias_grad[row0 + tid] = g.accumulate ? g.bias_grad[row0 + tid] + sacc : sacc;
-    else
+    if (g.bias_grad != nullptr && wgrad_direct(g)) {
+      float* bg = g.bias_grad + (g.ksplit > 1 ? ks * g.bias_gstride : 0) + row0 + tid;
+      *bg = g.accumulate ? *bg + sacc : sacc;
+    } else {
       g.bias_part[(long long)ks * g.Ca + row0 + tid] = sacc;
+    }
   }
 }
 
@@ -3170,7 +3182,7 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cin = 8 << g.cpg_shift;
   const int nchunk = wgrad_nchunk(g.cpg_shift, g.kchunks), rt_n = g.Ca / CO;
-  const int tile = blockIdx.x;
+  const int tile = g.swz ? xcd_swizzle(blockIdx.x, gridDim.x) : (int)blockIdx.x;
   const int ct = tile % nchunk, rt = (tile / nchunk) % rt_n, ks = tile / (nchunk * rt_n);
   const int bz_n = g.D / BRK_Z, by_n = g.H / BRK_Y, bx_n = g.W / BRK_X;
   const long long nbrick = (g.V / ((long long)g.D * g.H * g.W)) * bz_n * by_n * bx_n;
@@ -3600,7 +3612,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cin = 8 << g.cpg_shift;
   const int nchunk = wgrad_nchunk(g.cpg_shift, g.kchunks), rt_n = g.Ca / CO;
-  const int tile = blockIdx.x;
+  const int tile = g.swz ? xcd_swizzle(blockIdx.x, gridDim.x) : (int)blockIdx.x;
   const int ct = tile % nchunk, rt = (tile / nchunk) % rt_n, ks = tile / (nchunk * rt_n);
   const int bz_n = g.D / BRK_Z, by_n = g.H / BRK_Y, bx_n = g.W / BRK_X;
   const int nbrick = (int)(g.V / ((long long)g.D * g.H * g.W)) * bz_n * by_n * bx_n;
@@ -3933,7 +3945,7 @@ __global__ __launch_bounds__(512) void wgrad_brickr_kernel(WgradArgs g, int bz_r
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cin = 8 << g.cpg_shift;
   const int nchunk = wgrad_nchunk(g.cpg_shift, g.kchunks), rt_n = g.Ca / CO;
-  const int tile = blockIdx.x;
+  const int tile = g.swz ? xcd_swizzle(blockIdx.x, gridDim.x) : (int)blockIdx.x;
   const int ct = tile % nchunk, rt = (tile / nchunk) % rt_n, ks = tile / (nchunk * rt_n);
   const int HX = bx + 2, HY = by + 2, HZ = bz + 2;
   const int HV = HZ * HY * HX, rows = bz * by * bx;
@@ -5483,8 +5495,10 @@ Conv3WgradPlan plan_conv3_wgrad_grouped(long long V, int Co, int Cip, int Ci, in
   if (groups <= 1) return p;
   p.ksplit = p.ksplit / groups * groups;
   if (p.ksplit < groups) p.ksplit = groups;
-  p.direct = 0;
-  p.ws = (long long)p.ksplit * ((long long)Co * 27 * Cip + Co);
+  // one split per group (the deepest levels): each writes its group's gradient directly, as the ungrouped
+  // single-split launch does -- a reduce would only copy 2 x 28 MB there (28.8 us, r04d)
+  p.direct = p.kind >= 2 && p.ksplit == groups && Ci == Cip && knob("MMSEG_WGRAD_GDIRECT", 1);
+  p.ws = p.direct ? 0 : (long long)p.ksplit * ((long long)Co * 27 * Cip + Co);
   return p;
 }
 
@@ -5575,6 +5589,8 @@ int conv3_wgrad_impl(const void* dy, int lddy, const void* x, int ldx, const flo
   const int fmt = knob("MMSEG_WGRAD_FRAG", 1) ? wgrad_dma_mt(g, dtype == MMSEG_BF16 ? 2 : 4) : 0;
   g.frag = fmt > 0;
   g.groups = groups > 1 ? groups : 0;
+  g.grad_gstride = grad_gstride;
+  g.bias_gstride = bias_gstride;
   if (phase & 1) {
     const int rc = dtype == MMSEG_BF16 ? launch_wgrad<bf16_t, MODE_CONV3>(g, s) : launch_wgrad<float, MODE_CONV3>(g, s);
     if (rc) return rc;
