@@ -5439,7 +5439,7 @@ int mmseg_wgrad(const void* a, int lda, const void* b, int ldb, float* part, flo
     ksplit = (int)((V + vps - 1) / vps);
   }
   WgradArgs g{a, lda, b, ldb, part, bias_part, Ca, Ncols, cpg_shift, V, D, H, W, ksplit, vps,
-              knob("MMSEG_WGRAD_SWIZZLE", 0), brick, nullptr, nullptr, 0};
+              knob("MMSEG_WGRAD_SWIZZLE", 1), brick, nullptr, nullptr, 0};
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16) {
     switch (mode) {
@@ -5582,8 +5582,11 @@ int conv3_wgrad_impl(const void* dy, int lddy, const void* x, int ldx, const flo
   float* part = p.direct ? nullptr : ws;
   float* bpart = (p.direct || bias_grad == nullptr) ? nullptr : ws + (long long)p.ksplit * Co * ncols;
   const long long vps = ((V + p.ksplit - 1) / p.ksplit + 63) / 64 * 64;
+  // XCD swizzle (MMSEG_WGRAD_SWIZZLE): each XCD walks a contiguous range of (split, row tile, channel chunk) tiles,
+  // so the chunks of one brick range -- which all read the same dy -- and neighbouring brick ranges -- which share
+  // halo planes -- meet in one L2 (r04e A/B: 6.38 -> 6.35 ms/step)
   WgradArgs g{dy, lddy, x, ldx, part, p.direct ? bias_grad : bpart, Co, ncols, cpg_shift, V, D, H, W, p.ksplit, vps,
-              knob("MMSEG_WGRAD_SWIZZLE", 0), p.kind, p.direct ? grad : nullptr, p.direct ? bias_grad : nullptr,
+              knob("MMSEG_WGRAD_SWIZZLE", 1), p.kind, p.direct ? grad : nullptr, p.direct ? bias_grad : nullptr,
               accumulate, wgrad_kchunks(Cip, Ci), nmean, nrstd};
   hipStream_t s = (hipStream_t)stream;
   const int fmt = knob("MMSEG_WGRAD_FRAG", 1) ? wgrad_dma_mt(g, dtype == MMSEG_BF16 ? 2 : 4) : 0;
