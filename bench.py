@@ -122,6 +122,21 @@ def pmc_mfma_busy(kernel: str):
     return out, os.path.relpath(files[-1], ROOT)
 
 
+def rocprof_steady(kernel: str):
+    """The kernel's steady-state average launch duration from the newest committed rocprofv3 kernel-trace summary
+    (profiles/*steady*.json: tools/rocprof_families.py steady over the last steps of a traced run of this bench),
+    to set beside the live timer's."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*steady*.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    key = _family_key(d, kernel)
+    src = os.path.relpath(files[-1], ROOT)
+    return (d[key]["avg_launch_ms"] if key is not None else None), src
+
+
 def pmc_step_bytes():
     """HBM bytes of one whole training step from the PMC summary: every kernel's bytes per launch x launches,
     over the steps the profiled run executed (its '_steps', else the AdamW launch count: one per step);
@@ -321,6 +336,13 @@ def main():
                     "algorithmic_bytes_per_launch": round(bytes_per_launch),
                     "timer": "hipExtLaunchKernelGGL start/stop events on the launching stream (dispatch "
                              "timestamps, the rocprofv3 kernel-trace interval)"}
+        rp, rsrc = rocprof_steady(name)
+        if rp is not None:
+            # the same family in the committed rocprofv3 trace (steady-state steps): frac from its duration
+            roofline["rocprof_avg_launch_ms"] = round(rp, 4)
+            roofline["rocprof_frac"] = round(flops_per_launch / (rp * 1e-3) / 1e12 / peak, 4)
+            roofline["rocprof_vs_timer"] = round(rp / avg_ms, 4)
+            roofline["rocprof_source"] = rsrc
         busy, bsrc = pmc_mfma_busy(name)
         if busy is not None:
             # SQ_VALU_MFMA_BUSY_CYCLES x 1,024 FLOPs / SIMD-cycle re-counts the MFMA work from the counters alone:

@@ -8,6 +8,7 @@ P=profiles
 [ -f $O/bench.log ] && tail -1 $O/bench.log > $P/${T}_bench.json
 [ -f $O/families.txt ] && cp $O/families.txt $P/${T}_families.txt
 [ -f $O/trace/prof_kernel_stats.csv ] && cp $O/trace/prof_kernel_stats.csv $P/${T}_kernel_stats.csv
+[ -f $O/steady.json ] && cp $O/steady.json $P/${T}_steady.json && cp $O/families_steady.txt $P/${T}_families_steady.txt
 [ -f $O/pmc_traffic.json ] && cp $O/pmc_traffic.json $P/${T}_pmc_traffic.json
 [ -f $O/pmc_sq.json ] && cp $O/pmc_sq.json $P/${T}_pmc_sq.json
 [ -f $O/timer.json ] && python3 tools/timer_dump.py $O/timer.json 40 > $P/${T}_timer.txt

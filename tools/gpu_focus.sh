@@ -24,5 +24,6 @@ if [ "${3:-bench}" = "bench" ]; then
   timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d $O/pmc_sq -o pmc -- python3 $R/bench.py --steps 2 --warmup 1 --timer-steps 1 --no-cpu-baseline > $O/pmc_sq.log 2>&1 || { echo "pmc sq failed"; tail -20 $O/pmc_sq.log; exit 1; }
   python3 $R/tools/rocprof_families.py sq $O/pmc_sq/pmc_counter_collection.csv $O/pmc_sq.json > /dev/null
   python3 $R/tools/rocprof_families.py stats $O/trace/prof_kernel_stats.csv 16 > $O/families.txt
+  python3 $R/tools/rocprof_families.py steady $O/trace/prof_kernel_trace.csv $O/steady.json 8 > $O/families_steady.txt
 fi
 echo done

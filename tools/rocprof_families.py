@@ -3,6 +3,7 @@
     python tools/rocprof_families.py stats  <prof_kernel_stats.csv>  [steps]
     python tools/rocprof_families.py traffic <fetch_counter_collection.csv> <write_counter_collection.csv> [out.json [steps]]
     python tools/rocprof_families.py sq <sq_counter_collection.csv> [out.json]
+    python tools/rocprof_families.py steady <prof_kernel_trace.csv> <out.json> [last_steps]
 
 `stats` prints per-family calls / average duration (the same family names the
 in-process timer reports through mmseg_last_kernel(), so bench.py's
@@ -78,6 +79,33 @@ def stats(path: str, steps: int = 1):
     print(f"{'family':48s} {'calls':>7s} {'avg_us':>9s} {'ms/step':>8s} {'%':>6s}")
     for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
         print(f"{k:48s} {c:7d} {t / c / 1e3:9.1f} {t / steps / 1e6:8.3f} {100 * t / tot:6.2f}")
+
+
+def steady(trace_csv: str, last: int = 8):
+    """Per family over the LAST `last` training steps of a rocprofv3 kernel trace (a step ends with its AdamW
+    launch): average duration per launch and launches per step.  The first steps of a bench run (warm-up, graph
+    capture) run at ramping clocks -- wgrad_dma 47 us there against 42 us in steady state (r04d) -- and would
+    bias prof_kernel_stats.csv's all-dispatch averages; bench.py's timer window runs after the timed steps."""
+    with open(trace_csv) as f:
+        rows = sorted(csv.DictReader(f), key=lambda r: int(r["Start_Timestamp"]))
+    ends = [i for i, r in enumerate(rows) if family(r["Kernel_Name"]) in ("adamw4_kernel", "adamw_kernel")]
+    # one AdamW family per step: with both kernels present (large + small parameter groups) keep adamw4's
+    if any(family(rows[i]["Kernel_Name"]) == "adamw4_kernel" for i in ends):
+        ends = [i for i in ends if family(rows[i]["Kernel_Name"]) == "adamw4_kernel"]
+    if len(ends) < 2:
+        raise SystemExit("steady: fewer than two AdamW launches in the trace")
+    last = min(last, len(ends) - 1)
+    lo, hi = ends[-last - 1], ends[-1]
+    agg = defaultdict(lambda: [0, 0.0])
+    for r in rows[lo + 1:hi + 1]:
+        a = agg[family(r["Kernel_Name"])]
+        a[0] += 1
+        a[1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6   # ms
+    span = (int(rows[hi]["End_Timestamp"]) - int(rows[lo]["End_Timestamp"])) * 1e-6
+    res = {"_steps": last, "_span_ms_per_step": span / last}
+    for k, (n, ms) in agg.items():
+        res[k] = {"launches_per_step": n / last, "avg_launch_ms": ms / n, "ms_per_step": ms / last}
+    return res
 
 
 def _counter_rows(path: str, counter: str):
@@ -165,6 +193,17 @@ def sq(csv_path: str, trace_stats: str = None):
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 1)
+    elif sys.argv[1] == "steady":
+        r = steady(sys.argv[2], int(sys.argv[4]) if len(sys.argv) > 4 else 8)
+        with open(sys.argv[3], "w") as f:
+            f.write(json.dumps(r, indent=1) + "\n")
+        fam = {k: v for k, v in r.items() if not k.startswith("_")}
+        tot = sum(v["ms_per_step"] for v in fam.values())
+        print(f"last {r['_steps']} steps, {r['_span_ms_per_step']:.3f} ms/step wall, {tot:.3f} ms/step of kernels")
+        print(f"{'family':48s} {'n/step':>7s} {'avg_us':>9s} {'ms/step':>8s} {'%':>6s}")
+        for k, v in sorted(fam.items(), key=lambda kv: -kv[1]["ms_per_step"]):
+            print(f"{k:48s} {v['launches_per_step']:7.1f} {v['avg_launch_ms'] * 1e3:9.1f} {v['ms_per_step']:8.3f} "
+                  f"{100 * v['ms_per_step'] / tot:6.2f}")
     elif sys.argv[1] == "sq":
         r = sq(sys.argv[2])
         js = json.dumps(r, indent=1)
