@@ -4847,11 +4847,13 @@ int launch_gemm_mode(GemmArgs g, int mode, hipStream_t s) {
 // else 0: bf16, byte offsets of both tensors within 31 bits (the deferred-norm variant keeps register staging by
 // default: its in-place LDS pass and extra barrier cost more than the DMA saves, 0.651 -> 0.682 ms/step for the
 // 32-co family)
+bool wgrad_co64(int Ca, long long V, int kind);
+
 int wgrad_dma_mt(const WgradArgs& g, int elem_bytes) {
   const bool dma = elem_bytes == 2 && g.brick == 2 && knob("MMSEG_WGRAD_V3", 1) != 0 && knob("MMSEG_WGRAD_DMA", 1) &&
                    (g.nmean == nullptr || knob("MMSEG_WGRAD_DMA_NORM", 0)) && g.V * g.lda * 2 < (1LL << 31) &&
                    g.V * g.ldb * 2 < (1LL << 31) && (g.lda % 8) == 0 && (g.ldb % 8) == 0;
-  return dma ? (g.Ca % 64 == 0 ? 4 : 2) : 0;
+  return dma ? (wgrad_co64(g.Ca, g.V, 2) ? 4 : 2) : 0;
 }
 
 template <typename T, int MODE>
@@ -4866,7 +4868,7 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
     if (MODE == MODE_CONV3 && g.brick == 3) {
       const WBrick wb = plan_wgrad_brickr(g.D, g.H, g.W);
       const bool b366 = wb.bz == 3 && wb.by == 6 && wb.bx == 6 && knob("MMSEG_BRICKR_CT", 1);
-      if (g.Ca % 64 == 0) {
+      if (wgrad_co64(g.Ca, g.V, 3)) {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 64) * g.ksplit);
         mmseg::note_kernel("wgrad_brickr_kernel<CO64>");
         if (b366)
@@ -4914,7 +4916,7 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
         }
         return mmseg::check_launch("wgrad_dma");
       }
-      if (g.Ca % 64 == 0) {
+      if (wgrad_co64(g.Ca, g.V, 2)) {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 64) * g.ksplit);
         mmseg::note_kernel(v3 ? "wgrad_brick2_kernel<CO64,V3>" : "wgrad_brick2_kernel<CO64>");
         if (v3 && g.nmean)
@@ -4980,10 +4982,20 @@ int wgrad_brick_ok(int Ca, int cpg_shift, int D, int H, int W, int lda, int ldb,
 
 // Split count of the CONV3 brick wgrad: enough blocks to fill the chip, capped by
 // the caller's workspace (cap) and by one brick per split.
+// 64-co row tiles for the brick weight-gradient kernels (kind 2: brick2 / LDS-DMA, 3: runtime brick), else 32-co.
+// A block's split partial is its whole tile, so at small volumes -- where the ~256 resident blocks each see a
+// few bricks -- the partials outweigh the inputs (24^3: 54 MB written and re-read per launch against 35-65 MB
+// of input); 32-co tiles halve them at the price of reading the halo once per row tile.  Below V voxels
+// MMSEG_WGRAD_CO64_MINV (kind 2) / MMSEG_WGRAD_RCO64_MINV (kind 3) the 32-co tiles are used.
+bool wgrad_co64(int Ca, long long V, int kind) {
+  if (Ca % 64 != 0) return false;
+  return V >= (long long)knob(kind == 3 ? "MMSEG_WGRAD_RCO64_MINV" : "MMSEG_WGRAD_CO64_MINV", 0);
+}
+
 int brick_wgrad_splits(long long V, int cap, int Ca, int cpg_shift, int kind, int D, int H, int W,
                        int kchunks = 0) {
   const int nchunk = wgrad_nchunk(cpg_shift, kchunks);
-  const int tiles = nchunk * (Ca / ((kind >= 2 && Ca % 64 == 0) ? 64 : 32));
+  const int tiles = nchunk * (Ca / ((kind >= 2 && wgrad_co64(Ca, V, kind)) ? 64 : 32));
   // v2 / runtime-brick kernels: one wave of resident blocks (256 CUs x blocks per CU: 2 for the 32-co brick2
   // kernel, 1 for the 64-co and runtime-brick kernels, whose stage buffers take > 80 KB of LDS), never more:
   // a partial second wave of 512-thread blocks costs a whole block time.
