@@ -357,6 +357,13 @@ int mmseg_winattn_fwd(const void* qkv, int B, int N, int C, int heads, const flo
 int mmseg_winattn_bwd(const void* qkv, const void* O, const void* dO, const float* lse, int B, int N, int C, int heads,
                       const float* table, int T, int w0, int w1, int w2, const uint8_t* region, int nw, float scale,
                       void* dqkv, void* dS, int ldn, void* stream);
+/* winattn_bwd_sum: mmseg_winattn_bwd with the score gradient summed over groups of windows on chip (dqkv bitwise
+ * the same): dsum [groups][heads][N][ldn] fp32, groups = mmseg_winattn_sum_groups(B, N, heads) (0 = not worth it,
+ * use mmseg_winattn_bwd); fold with mmseg_relpos_table_grad(dsum, ldn, groups, ..., dtype f32). */
+int mmseg_winattn_sum_groups(int B, int N, int heads);
+int mmseg_winattn_bwd_sum(const void* qkv, const void* O, const void* dO, const float* lse, int B, int N, int C,
+                          int heads, const float* table, int T, int w0, int w1, int w2, const uint8_t* region, int nw,
+                          float scale, void* dqkv, float* dsum, int ldn, void* stream);
 
 /* ---------------------------------------------------- SwinUNETR tokens */
 /* The SwinTransformer stages and UNETR residual blocks of MONAI SwinUNETR (built by the reference's

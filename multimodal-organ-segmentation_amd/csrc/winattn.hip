@@ -372,6 +372,134 @@ __global__ __launch_bounds__(512) void winattn_bwd_q_kernel(WinAttnArgs a) {
   }
 }
 
+// ------------------------------------- backward: dQ and the window-summed dS
+// bwd_q for many windows per block: block = (window group wg of wpg windows, head h, query-tile group qg of 8
+// tiles); wave w owns query tile qg * 8 + w of every window in the group.  Per window it computes dQ as bwd_q
+// does (the same MFMAs on the same operands, so dQ is bitwise bwd_q's) and adds its fp32 dS[q][keys] into
+// registers; after the group it writes the sum once, dsum[wg][h][q][ldn] (fp32, keys >= N zero).  The bias-table
+// gradient then folds nwg window sums instead of B bf16 score gradients: at SwinUNETR stage 0 (1,000 windows of
+// 343 tokens, 3 heads) 79 MB instead of 708 MB written and read back per attention layer.
+constexpr int QB_TILES = 8;                        // query tiles per block (one per wave)
+
+__global__ __launch_bounds__(512) void winattn_bwd_qb_kernel(WinAttnArgs a, int wpg, int nqg, float* dsum) {
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Kt[16][TP];
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[QB_TILES * 16][16];
+  __shared__ __attribute__((aligned(16))) bf16_t dOs[QB_TILES * 16][16];
+  __shared__ float tab[TMAX];
+  __shared__ float lse[QB_TILES * 16];
+  __shared__ float Dq[QB_TILES * 16];
+  __shared__ __attribute__((aligned(16))) int code[NPMAX];
+  __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
+  const int qg = blockIdx.x % nqg, h = (blockIdx.x / nqg) % a.heads, wg = blockIdx.x / (nqg * a.heads);
+  const int np = (a.N + 15) & ~15, nt = np / 16;
+  const int q0 = qg * QB_TILES * 16;
+  const int C3 = 3 * a.C, hoff = h * a.hd;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const int qt = qg * QB_TILES + wave;
+  const int q = qt * 16 + r16;
+  const bool qv = q < a.N;
+  stage_table(tab, a, h);
+  stage_codes(code, a, np);
+  const float* ctab = tab + code_off(a);
+  float acc[NTMAX][4];
+#pragma unroll
+  for (int kt = 0; kt < NTMAX; ++kt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[kt][r] = 0.f;
+  const int b0 = wg * wpg, b1 = b0 + wpg < a.B ? b0 + wpg : a.B;
+  for (int b = b0; b < b1; ++b) {
+    const int bh = b * a.heads + h;
+    const Stage st{b, h, a.N, np};
+    __syncthreads();   // the previous window's operands are consumed
+    stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, Kt);
+    stage_rows(Vs, a.qkv, C3, 2 * a.C + hoff, st, a.hd, nullptr);
+    stage_region(reg, a, b);
+    // this group's queries (zeros past N): rows q0 .. q0 + 127 of Q, dO; their lse and D = dO . O
+    for (int e = threadIdx.x; e < QB_TILES * 16 * 2; e += blockDim.x) {
+      const int n = e >> 1, half = e & 1, qq = q0 + n;
+      V8<bf16_t> vq, vo;
+      vq.zero();
+      vo.zero();
+      if (qq < a.N && half * 8 < a.hd) {
+        vq.load(a.qkv + (long long)(b * a.N + qq) * C3 + hoff + half * 8);
+        vo.load(a.dO + (long long)(b * a.N + qq) * a.C + hoff + half * 8);
+      }
+      vq.store(&Qs[n][half * 8]);
+      vo.store(&dOs[n][half * 8]);
+    }
+    for (int n = threadIdx.x; n < QB_TILES * 16; n += blockDim.x) {
+      const int qq = q0 + n;
+      float d = 0.f, l = 0.f;
+      if (qq < a.N) {
+        const long long base = (long long)(b * a.N + qq) * a.C + hoff;
+        for (int j = 0; j < a.hd; ++j) d += (float)a.dO[base + j] * (float)a.O[base + j];
+        l = a.lse[(long long)bh * NPMAX + qq];
+      }
+      Dq[n] = d;
+      lse[n] = l;
+    }
+    __syncthreads();
+    if (qt < nt) {
+      const int ql = wave * 16 + r16;
+      const s4 bq = ld4(&Qs[ql][4 * g4]);
+      const s4 bdo = ld4(&dOs[ql][4 * g4]);
+      const float lq = lse[ql], dq_ = Dq[ql];
+      const float* tq = ctab + code[q];
+      const uint32_t rq = reg[q];
+      f32x4 dq = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kt = 0; kt < NTMAX; ++kt) {
+        if (kt < nt) {
+          const f32x4 sc = mma(ld4(&Ks[kt * 16 + r16][4 * g4]), bq, (f32x4){0.f, 0.f, 0.f, 0.f});
+          const f32x4 dp = mma(ld4(&Vs[kt * 16 + r16][4 * g4]), bdo, (f32x4){0.f, 0.f, 0.f, 0.f});
+          float ds[4];
+          scores_q(sc, qv, tq, rq, kt * 16 + 4 * g4, a, code, reg, ds);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float p = ds[r] == -INFINITY ? 0.f : __expf(ds[r] - lq);
+            ds[r] = p * (dp[r] - dq_);
+            acc[kt][r] += ds[r];
+          }
+          dq = mma(pack4(ds[0], ds[1], ds[2], ds[3]), ld4(&Kt[r16][kt * 16 + 4 * g4]), dq);
+        }
+      }
+      if (r16 < a.hd) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qq = qt * 16 + 4 * g4 + r;
+          if (qq < a.N) a.out[(long long)(b * a.N + qq) * C3 + hoff + r16] = (bf16_t)(dq[r] * a.scale);
+        }
+      }
+    }
+  }
+  if (qt < nt && qv) {
+    float* row = dsum + (((long long)wg * a.heads + h) * a.N + q) * a.ldn;
+#pragma unroll
+    for (int kt = 0; kt < NTMAX; ++kt) {
+      const int k0 = kt * 16 + 4 * g4;
+      if (kt < nt && k0 < a.ldn) {
+        if (k0 + 3 < a.ldn) {
+          *reinterpret_cast<float4*>(row + k0) = make_float4(acc[kt][0], acc[kt][1], acc[kt][2], acc[kt][3]);
+        } else {
+          for (int r = 0; r < 4 && k0 + r < a.ldn; ++r) row[k0 + r] = acc[kt][r];
+        }
+      }
+    }
+  }
+}
+
+// windows per block of winattn_bwd_qb: about two resident blocks per CU over (window group, head, query group)
+int qb_windows_per_group(int B, int N, int heads) {
+  const int nt = ((N + 15) & ~15) / 16, nqg = (nt + QB_TILES - 1) / QB_TILES;
+  int nwg = (512 + heads * nqg - 1) / (heads * nqg);
+  if (nwg > B) nwg = B;
+  if (nwg < 1) nwg = 1;
+  return (B + nwg - 1) / nwg;
+}
+
 int check_args(const WinAttnArgs& a) {
   MMSEG_REQUIRE(a.N >= 1 && a.N <= NPMAX && a.hd >= 1 && a.hd <= 16 && a.hd % 8 == 0 && a.C == a.heads * a.hd &&
                     a.T <= TMAX && a.T == (2 * a.w0 - 1) * (2 * a.w1 - 1) * (2 * a.w2 - 1) &&
@@ -407,6 +535,32 @@ int mmseg_winattn_bwd(const void* qkv, const void* O, const void* dO, const floa
   if (mmseg::check_launch("winattn_bwd_kv")) return 1;
   MMSEG_LAUNCH(winattn_bwd_q_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
   return mmseg::check_launch("winattn_bwd_q");
+}
+
+// Window groups of mmseg_winattn_bwd_sum (0: too few windows per group to pay -- use mmseg_winattn_bwd).
+int mmseg_winattn_sum_groups(int B, int N, int heads) {
+  const int wpg = qb_windows_per_group(B, N, heads);
+  return wpg >= 4 ? (B + wpg - 1) / wpg : 0;
+}
+
+// mmseg_winattn_bwd with the score gradient summed over groups of windows on chip: dsum [groups][heads][N][ldn]
+// fp32 (groups = mmseg_winattn_sum_groups(), keys >= N zero) replaces dS [B][heads][N][ldn]; fold it with
+// mmseg_relpos_table_grad(dsum, ldn, groups, ..., dtype = f32).  dqkv is bitwise mmseg_winattn_bwd's.
+int mmseg_winattn_bwd_sum(const void* qkv, const void* O, const void* dO, const float* lse, int B, int N, int C,
+                          int heads, const float* table, int T, int w0, int w1, int w2, const uint8_t* region, int nw,
+                          float scale, void* dqkv, float* dsum, int ldn, void* stream) {
+  WinAttnArgs a{(const bf16_t*)qkv, (const bf16_t*)O, (const bf16_t*)dO, (bf16_t*)dqkv, const_cast<float*>(lse),
+                nullptr, table, region, B, N, C, heads, C / heads, nw, T, ldn, w0, w1, w2, scale};
+  if (check_args(a)) return 1;
+  MMSEG_REQUIRE(ldn >= N && ldn % 8 == 0 && mmseg_winattn_sum_groups(B, N, heads) > 0,
+                "winattn_bwd_sum: ldn >= N (multiple of 8) and enough windows (mmseg_winattn_sum_groups)");
+  hipStream_t s = (hipStream_t)stream;
+  MMSEG_LAUNCH(winattn_bwd_kv_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  if (mmseg::check_launch("winattn_bwd_kv")) return 1;
+  const int wpg = qb_windows_per_group(B, N, heads);
+  const int nt = ((N + 15) & ~15) / 16, nqg = (nt + QB_TILES - 1) / QB_TILES, nwg = (B + wpg - 1) / wpg;
+  MMSEG_LAUNCH(winattn_bwd_qb_kernel, dim3(nwg * heads * nqg), dim3(64 * WAVES), 0, s, a, wpg, nqg, dsum);
+  return mmseg::check_launch("winattn_bwd_qb");
 }
 
 }  // extern "C"

@@ -24,6 +24,7 @@ norm_pool.hip, the LeakyReLU residual tail (mmseg_res_apply / _lrelu_bwd).
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Tuple
 
 import numpy as np
@@ -311,18 +312,30 @@ class SwinBlockProg:
         if st["fused"]:
             dqkv = self._empty(Mw * 3 * C)
             ldn = (Nw + 7) // 8 * 8
-            dS = self._empty(B * self.heads * Nw * ldn)
             region = geo["region"] if any(sh) else None
             nw = region.shape[0] if region is not None else 0
             w0, w1, w2 = geo["window"]
-            L.mmseg_winattn_bwd(ptr(st["qkv"]), ptr(st["O"]), ptr(dO), ptr(st["P"]), B, Nw, C, self.heads,
-                                ptr(self._table_t()), self.table.shape[0], w0, w1, w2, ptr(region), nw,
-                                self.core.scale, ptr(dqkv), ptr(dS), ldn, s)
             dB = torch.empty(self.heads * Nw * Nw, dtype=torch.float32, device=rt.device)
             offs, pairs, T = geo["csr"]
-            L.mmseg_relpos_table_grad(ptr(dS), ldn, B, self.heads, Nw, ptr(dB), ptr(offs), ptr(pairs), T,
-                                      ptr(self.flat.grad(self.table)), int(accumulate), code, s)
-            del dS
+            # many windows: the score gradient summed over window groups on chip (fp32, mmseg_winattn_bwd_sum),
+            # so the bias-table gradient folds a few group sums instead of every window's bf16 dS
+            ng = L.mmseg_winattn_sum_groups(B, Nw, self.heads) if os.environ.get("MMSEG_WINATTN_SUM", "1") != "0" else 0
+            if ng > 0:
+                dsum = torch.empty(ng * self.heads * Nw * ldn, dtype=torch.float32, device=rt.device)
+                L.mmseg_winattn_bwd_sum(ptr(st["qkv"]), ptr(st["O"]), ptr(dO), ptr(st["P"]), B, Nw, C, self.heads,
+                                        ptr(self._table_t()), self.table.shape[0], w0, w1, w2, ptr(region), nw,
+                                        self.core.scale, ptr(dqkv), ptr(dsum), ldn, s)
+                L.mmseg_relpos_table_grad(ptr(dsum), ldn, ng, self.heads, Nw, ptr(dB), ptr(offs), ptr(pairs), T,
+                                          ptr(self.flat.grad(self.table)), int(accumulate), 0, s)   # dsum: fp32
+                del dsum
+            else:
+                dS = self._empty(B * self.heads * Nw * ldn)
+                L.mmseg_winattn_bwd(ptr(st["qkv"]), ptr(st["O"]), ptr(dO), ptr(st["P"]), B, Nw, C, self.heads,
+                                    ptr(self._table_t()), self.table.shape[0], w0, w1, w2, ptr(region), nw,
+                                    self.core.scale, ptr(dqkv), ptr(dS), ldn, s)
+                L.mmseg_relpos_table_grad(ptr(dS), ldn, B, self.heads, Nw, ptr(dB), ptr(offs), ptr(pairs), T,
+                                          ptr(self.flat.grad(self.table)), int(accumulate), code, s)
+                del dS
         else:
             dqkv = self.core.core_bwd(dO, st["qkv"], st["P"], B, Nw, self.flat.grad(self.table), geo["csr"],
                                       accumulate)

@@ -371,6 +371,77 @@ def test_fused_window_attention_vs_torch(dev, N, hd, heads, nwin, masked):
     assert torch.equal(dS.view(B, heads, N, ldn)[..., N:].cpu(), torch.zeros(B, heads, N, ldn - N, dtype=torch.bfloat16))
 
 
+@pytest.mark.parametrize("masked", [True, False])
+def test_window_attention_summed_score_gradient(dev, masked):
+    """mmseg_winattn_bwd_sum (score gradient summed over window groups on chip, fp32) against mmseg_winattn_bwd
+    (per-window bf16 dS) on the same operands: dqkv bitwise equal; the bias-table gradient folded from the group
+    sums (relpos_table_grad over the groups, fp32) against a torch fp64 evaluation on the GPU (table rows summed over
+    windows and index pairs) within 1e-2 normwise, and no further from it than the per-window path's."""
+    N, hd, heads, nwin = 343, 16, 2, 4
+    C, B = heads * hd, 360
+    L, s = lib(), stream_handle()
+    ng = L.mmseg_winattn_sum_groups(B, N, heads)
+    assert ng > 0 and L.mmseg_winattn_sum_groups(8, N, heads) == 0
+    g = torch.Generator().manual_seed(5)
+    qkv = torch.randn(B * N, 3 * C, generator=g).to(torch.bfloat16).to(dev)
+    table = (torch.randn(13 ** 3, heads, generator=g) * 0.5).to(dev)
+    region = torch.randint(0, 4, (nwin, N), generator=g).to(torch.uint8).to(dev) if masked else None
+    dO = torch.randn(B * N, C, generator=g).to(torch.bfloat16).to(dev)
+    tabt = table.t().contiguous()
+    scale = hd ** -0.5
+    nwm = nwin if masked else 0
+    O = torch.empty(B * N, C, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(L.mmseg_winattn_lse_floats(B, heads), device=dev)
+    L.mmseg_winattn_fwd(ptr(qkv), B, N, C, heads, ptr(tabt), 13 ** 3, 7, 7, 7, ptr(region), nwm, scale, ptr(O),
+                        ptr(lse), s)
+    ldn = (N + 7) // 8 * 8
+    idx = SO.relative_position_index((7, 7, 7))[:N, :N]
+    offs, pairs = [], []
+    flat = idx.reshape(-1).numpy()
+    order = np.argsort(flat, kind="stable")
+    counts = np.bincount(flat, minlength=13 ** 3)
+    offs = torch.from_numpy(np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)).to(dev)
+    pairs = torch.from_numpy(order.astype(np.int32)).to(dev)
+    dB = torch.empty(heads * N * N, device=dev)
+    res = {}
+    for mode in ("sum", "win"):
+        dqkv = torch.empty(B * N, 3 * C, dtype=torch.bfloat16, device=dev)
+        gt = torch.empty(13 ** 3, heads, device=dev)
+        if mode == "sum":
+            dsum = torch.empty(ng * heads * N * ldn, device=dev)
+            L.mmseg_winattn_bwd_sum(ptr(qkv), ptr(O), ptr(dO), ptr(lse), B, N, C, heads, ptr(tabt), 13 ** 3, 7, 7, 7,
+                                    ptr(region), nwm, scale, ptr(dqkv), ptr(dsum), ldn, s)
+            L.mmseg_relpos_table_grad(ptr(dsum), ldn, ng, heads, N, ptr(dB), ptr(offs), ptr(pairs), 13 ** 3,
+                                      ptr(gt), 0, 0, s)
+        else:
+            dS = torch.empty(B * heads * N * ldn, dtype=torch.bfloat16, device=dev)
+            L.mmseg_winattn_bwd(ptr(qkv), ptr(O), ptr(dO), ptr(lse), B, N, C, heads, ptr(tabt), 13 ** 3, 7, 7, 7,
+                                ptr(region), nwm, scale, ptr(dqkv), ptr(dS), ldn, s)
+            L.mmseg_relpos_table_grad(ptr(dS), ldn, B, heads, N, ptr(dB), ptr(offs), ptr(pairs), 13 ** 3, ptr(gt), 0,
+                                      1, s)
+        torch.cuda.synchronize()
+        res[mode] = (dqkv.clone(), gt.clone())
+    assert torch.equal(res["sum"][0], res["win"][0])
+    # fp64 reference of the table gradient on the GPU
+    x = qkv.double().view(B, N, 3, heads, hd).permute(2, 0, 3, 1, 4)
+    q, k, v = [t.clone().requires_grad_(True) for t in x]
+    bias = table.double()[idx.reshape(-1).to(dev)].view(N, N, heads).permute(2, 0, 1)
+    S = (q * scale) @ k.transpose(-1, -2) + bias
+    if masked:
+        m = torch.where(region[:, :, None] == region[:, None, :], 0.0, -100.0).double()
+        S = (S.view(B // nwin, nwin, heads, N, N) + m[None, :, None]).view(B, heads, N, N)
+    S.retain_grad()
+    out = (torch.softmax(S, -1) @ v).transpose(1, 2).reshape(B * N, C)
+    out.backward(dO.double())
+    dsw = S.grad.sum(0).reshape(heads, N * N)                        # [h][n*N+m]
+    ref = torch.zeros(13 ** 3, heads, dtype=torch.float64, device=dev)
+    ref.index_add_(0, idx.reshape(-1).to(dev), dsw.t())
+    e_sum, e_win = rel2(res["sum"][1], ref), rel2(res["win"][1], ref)
+    print(f"\nwindow-summed score gradient (masked={masked}, {ng} groups of {B} windows): table grad vs fp64 "
+          f"{e_sum:.2e} (per-window bf16 dS path {e_win:.2e})")
+    assert e_sum < 1e-2 and e_sum <= e_win * 1.05
+
+
 def test_fused_attention_network_matches_unfused(dev, swin_case, monkeypatch):
     """Whole bf16 SwinUNETR: the fused window attention vs the batched-GEMM path (MMSEG_WINATTN=0)."""
     x, cot = swin_case
