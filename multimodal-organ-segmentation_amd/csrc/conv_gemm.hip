@@ -3596,7 +3596,14 @@ __global__ __launch_bounds__(512, 1) void conv3_brick8_kernel(GemmArgs g) {
   PROBE_BLOCK(true);
 }
 // PIPE: the fragment reads of the next (dy plane, tap) step are issued before the current step's MFMAs
-template <int MT, bool NORM = false, int NST = 3, bool PIPE = false>
+// RING: the halo is a ring of z-plane slots and a block walks its bricks z-fastest, so a brick that continues the
+// previous one's (x, y) column reuses the two halo planes they share and stages only its four new ones: halo
+// bytes per brick 1.875x the brick's voxels instead of 2.81x (6 x 6 x 10 of 4 x 4 x 8).  Slot of the halo's first
+// plane: sb(b) = 4 (b - b_begin) + 2 (column starts in (b_begin, b]) mod RSLOT -- a brick starting a column takes
+// six fresh slots; with NST = 3 the bricks in flight span at most 18 of the 24 slots.
+constexpr int RSLOT = 24;                 // halo plane slots
+constexpr int RPLANE_I = 4;               // DMA wave-instructions per plane slot (6 x 10 voxels x 4 chunks = 240 lanes)
+template <int MT, bool NORM = false, int NST = 3, bool PIPE = false, bool RING = false>
 __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
   typedef bf16_t T;
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -3606,8 +3613,11 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
   constexpr int NXI = (HLO_V * XCH + 63) / 64;          // halo wave-instructions (23, the last one half)
   constexpr int NI = NDI + NXI, KI = (NI + 7) / 8;      // per brick; per wave (8 waves)
   constexpr int DS = 128 * CO, XS = NXI * 64 * 8;       // elements per stage (halo padded to whole instructions)
-  constexpr int SS = DS + XS;
-  __shared__ __attribute__((aligned(16))) T st[NST * SS];   // ring of NST stage images
+  constexpr int SS = RING ? DS : DS + XS;
+  constexpr int PLANE_E = RPLANE_I * 512;               // elements per halo plane slot (4 KB)
+  static_assert(!RING || (!NORM && NST == 3), "RING: no deferred norm, three stages");
+  __shared__ __attribute__((aligned(16))) T st[NST * SS];   // ring of NST stage images (RING: dy only)
+  __shared__ __attribute__((aligned(16))) T xr[RING ? RSLOT * PLANE_E : 8];   // RING: halo plane slots
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cin = 8 << g.cpg_shift;
@@ -3654,15 +3664,85 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
       ++nw;
     }
   }
-  auto issue = [&](T* dst, int b) __attribute__((always_inline)) {
+  // RING: per plane-slot instruction j4 (0..3) the lane's byte offset within the plane and its (hy, hx)
+  uint32_t prel[RING ? RPLANE_I : 1], ppos[RING ? RPLANE_I : 1];
+  if constexpr (RING) {
+#pragma unroll
+    for (int j4 = 0; j4 < RPLANE_I; ++j4) {
+      const int p = j4 * 64 + lane, h = p >> 2, c = p & 3;
+      prel[j4] = 0;
+      ppos[j4] = 0xffu;
+      if (h < HLO_Y * HLO_X) {
+        const int hx = h % HLO_X, hy = h / HLO_X;
+        const int cc = (((c >> 1) ^ ((hx >> 2) & 1)) << 1) | (c & 1);
+        prel[j4] = (uint32_t)(((hy * g.W + hx) * g.ldb + c0 + cc * 8) * 2);
+        ppos[j4] = (uint32_t)(hy | (hx << 8));
+      }
+    }
+  }
+  // brick b's origin: x fastest, or (RING) z fastest so consecutive bricks of a block share halo planes
+  auto brick_at = [&](int b, int& n, int& z0, int& y0, int& x0) __attribute__((always_inline)) {
     int q = b;
-    const int bx = q % bx_n;
-    q /= bx_n;
-    const int by = q % by_n;
-    q /= by_n;
-    const int bz = q % bz_n;
-    const int n = q / bz_n;
-    const int z0 = bz * BRK_Z, y0 = by * BRK_Y, x0 = bx * BRK_X;
+    if constexpr (RING) {
+      const int bz = q % bz_n;
+      q /= bz_n;
+      const int bx = q % bx_n;
+      q /= bx_n;
+      const int by = q % by_n;
+      n = q / by_n;
+      z0 = bz * BRK_Z, y0 = by * BRK_Y, x0 = bx * BRK_X;
+    } else {
+      const int bx = q % bx_n;
+      q /= bx_n;
+      const int by = q % by_n;
+      q /= by_n;
+      const int bz = q % bz_n;
+      n = q / bz_n;
+      z0 = bz * BRK_Z, y0 = by * BRK_Y, x0 = bx * BRK_X;
+    }
+  };
+  auto ring_cont = [&](int b) __attribute__((always_inline)) { return b > b_begin && b % bz_n != 0; };
+  auto ring_sb = [&](int b) __attribute__((always_inline)) {
+    return (4 * (b - b_begin) + 2 * (b / bz_n - b_begin / bz_n)) % RSLOT;
+  };
+  // this wave's DMA instructions for brick b (RING: dy + 4 or 6 planes x 4, dealt round-robin over the waves)
+  auto ring_count = [&](int b) __attribute__((always_inline)) {
+    const int tot = NDI + RPLANE_I * (ring_cont(b) ? 4 : 6);
+    return tot > wave ? (tot - 1 - wave) / 8 + 1 : 0;
+  };
+  auto issue_ring = [&](T* dst, int b) __attribute__((always_inline)) {
+    int n, z0, y0, x0;
+    brick_at(b, n, z0, y0, x0);
+    const int vb = (n * g.D + z0) * HW + y0 * g.W + x0;
+    const int dbase = vb * g.lda * 2;
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+      const int m = wave + 8 * k;
+      if (m < NDI)
+        wd_dma16(__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)(lds_ptr_t)(dst + m * 512)),
+                 (uint32_t)(dbase + (int)rel[k]), drsrc);
+    }
+    const int p0 = ring_cont(b) ? 2 : 0, sb = ring_sb(b);
+    const int tot = NDI + RPLANE_I * (6 - p0);
+    for (int m = NDI + ((wave - NDI) & 7); m < tot; m += 8) {   // this wave's halo instructions
+      const int hi = m - NDI, p = p0 + (hi >> 2), j4 = hi & 3;
+      int slot = sb + p;
+      if (slot >= RSLOT) slot -= RSLOT;
+      const int z = z0 - 1 + p;
+      // the lane's (hy, hx) for instruction j4 (j4 is wave-uniform: select among the four precomputed values)
+      const uint32_t hp = j4 == 0 ? ppos[0] : j4 == 1 ? ppos[1] : j4 == 2 ? ppos[2] : ppos[3];
+      const uint32_t rl = j4 == 0 ? prel[0] : j4 == 1 ? prel[1] : j4 == 2 ? prel[2] : prel[3];
+      const int y = y0 - 1 + (int)(hp & 0xff), x = x0 - 1 + (int)(hp >> 8);
+      const bool ok = hp != 0xffu && (unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H &&
+                      (unsigned)x < (unsigned)g.W;
+      const int pbase = (((n * g.D + z) * g.H + (y0 - 1)) * g.W + (x0 - 1)) * g.ldb * 2;
+      wd_dma16(__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)(lds_ptr_t)(xr + slot * PLANE_E + j4 * 512)),
+               ok ? (uint32_t)(pbase + (int)rl) : WD_OOB, xrsrc);
+    }
+  };
+  auto issue = [&](T* dst, int b) __attribute__((always_inline)) {
+    int n, z0, y0, x0;
+    brick_at(b, n, z0, y0, x0);
     const int vb = (n * g.D + z0) * HW + y0 * g.W + x0;
     const int dbase = vb * g.lda * 2;
     const int xbase = (vb - HW - g.W - 1) * g.ldb * 2;
@@ -3686,6 +3766,18 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
   // wait until at most `later` bricks' DMAs of this wave are in flight (vmcnt <= later * nw)
   auto wait_bricks = [&](int later) __attribute__((always_inline)) {
     switch (later * nw) {
+#define MMSEG_WD_WAIT(N) \
+  case N: __builtin_amdgcn_s_waitcnt(0x0f70 | N); break;
+      MMSEG_WD_WAIT(1) MMSEG_WD_WAIT(2) MMSEG_WD_WAIT(3) MMSEG_WD_WAIT(4) MMSEG_WD_WAIT(5) MMSEG_WD_WAIT(6)
+      MMSEG_WD_WAIT(7) MMSEG_WD_WAIT(8) MMSEG_WD_WAIT(9) MMSEG_WD_WAIT(10) MMSEG_WD_WAIT(11) MMSEG_WD_WAIT(12)
+      MMSEG_WD_WAIT(13) MMSEG_WD_WAIT(14) MMSEG_WD_WAIT(15)
+#undef MMSEG_WD_WAIT
+      default: __builtin_amdgcn_s_waitcnt(0x0f70); break;
+    }
+  };
+  // wait until at most `cnt` of this wave's DMA instructions are in flight
+  auto wait_cnt = [&](int cnt) __attribute__((always_inline)) {
+    switch (cnt) {
 #define MMSEG_WD_WAIT(N) \
   case N: __builtin_amdgcn_s_waitcnt(0x0f70 | N); break;
       MMSEG_WD_WAIT(1) MMSEG_WD_WAIT(2) MMSEG_WD_WAIT(3) MMSEG_WD_WAIT(4) MMSEG_WD_WAIT(5) MMSEG_WD_WAIT(6)
@@ -3755,7 +3847,17 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
   bf16x8 ones;
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
-  auto compute = [&](const T* S) __attribute__((always_inline)) {
+  // halo row of tap (kz, ky, kx) for the lane's voxels in brick z-plane vz (RING: plane slot sb + vz + kz)
+  auto xrow = [&](const char* Xb, int sb, int vz, int kz, int ky, int kx) __attribute__((always_inline)) {
+    if constexpr (RING) {
+      int slot = sb + vz + kz;
+      if (slot >= RSLOT) slot -= RSLOT;
+      return reinterpret_cast<const char*>(xr) + slot * (PLANE_E * 2) + (hlo0 + ky * HLO_X + kx) * (CK * 2);
+    } else {
+      return Xb + (hlo0 + (vz + kz) * (HLO_Y * HLO_X) + ky * HLO_X + kx) * (CK * 2);
+    }
+  };
+  auto compute = [&](const T* S, int sb) __attribute__((always_inline)) {
     const char* Db = reinterpret_cast<const char*>(S);
     const char* Xb = reinterpret_cast<const char*>(S + DS);
 #pragma unroll
@@ -3766,17 +3868,16 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
         const bf16_t* base = reinterpret_cast<const bf16_t*>(Db + (kk + v0) * (CO * 2) + 32 * (i ^ dsw) + 8 * p4);
         af[i] = tr_frag(base, base + 8 * CO);
       }
-      const int hlo = hlo0 + (kk >> 5) * (HLO_Y * HLO_X);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         if (t < t_cnt) {
           const int tap = t_begin + t;
           const int kz = tap / 9, ky = (tap / 3) % 3, kx = tap % 3;
-          const int r = hlo + (kz * HLO_Y + ky) * HLO_X + kx;
+          const char* row = xrow(Xb, sb, kk >> 5, kz, ky, kx);
           const int xs = ((hx0 + kx) >> 2) & 1;
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            const bf16_t* pl = reinterpret_cast<const bf16_t*>(Xb + r * (CK * 2) + 32 * (j ^ xs) + 8 * p4);
+            const bf16_t* pl = reinterpret_cast<const bf16_t*>(row + 32 * (j ^ xs) + 8 * p4);
             const bf16x8 bfr = tr_frag(pl, pl + HLO_X * CK);
 #pragma unroll
             for (int i = 0; i < MT; ++i)
@@ -3791,7 +3892,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
     }
   };
   // software-pipelined: steps s = (kk, t) over this wave's TC taps, fragments double-buffered
-  auto compute_pipe = [&](const T* S, auto tcc) __attribute__((always_inline)) {
+  auto compute_pipe = [&](const T* S, int sb, auto tcc) __attribute__((always_inline)) {
     constexpr int TC = decltype(tcc)::value;
     const char* Db = reinterpret_cast<const char*>(S);
     const char* Xb = reinterpret_cast<const char*>(S + DS);
@@ -3807,11 +3908,11 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
     auto load_b = [&](int kk, int t, bf16x8(&b)[2]) __attribute__((always_inline)) {
       const int tap = t_begin + t;
       const int kz = tap / 9, ky = (tap / 3) % 3, kx = tap % 3;
-      const int r = hlo0 + (kk >> 5) * (HLO_Y * HLO_X) + (kz * HLO_Y + ky) * HLO_X + kx;
+      const char* row = xrow(Xb, sb, kk >> 5, kz, ky, kx);
       const int xs = ((hx0 + kx) >> 2) & 1;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const bf16_t* pl = reinterpret_cast<const bf16_t*>(Xb + r * (CK * 2) + 32 * (j ^ xs) + 8 * p4);
+        const bf16_t* pl = reinterpret_cast<const bf16_t*>(row + 32 * (j ^ xs) + 8 * p4);
         b[j] = tr_frag(pl, pl + HLO_X * CK);
       }
     };
@@ -3844,9 +3945,17 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
   };
 
   // prologue: bricks b_begin .. b_begin + NST - 2 in flight, the first one landed
-  for (int k = 0; k < NST - 1; ++k)
-    if (b_begin + k < b_end) issue(st + k * SS, b_begin + k);
-  {
+  for (int k = 0; k < NST - 1; ++k) {
+    if (b_begin + k < b_end) {
+      if constexpr (RING)
+        issue_ring(st + k * SS, b_begin + k);
+      else
+        issue(st + k * SS, b_begin + k);
+    }
+  }
+  if constexpr (RING) {
+    wait_cnt(b_begin + 1 < b_end ? ring_count(b_begin + 1) : 0);   // NST = 3: only brick b_begin + 1 may follow
+  } else {
     const int inflight = b_end - b_begin - 1 < NST - 2 ? b_end - b_begin - 1 : NST - 2;
     wait_bricks(inflight > 0 ? inflight : 0);
   }
@@ -3860,20 +3969,30 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
   for (int b = b_begin, sc = 0; b < b_end; ++b, sc = sc + 1 == NST ? 0 : sc + 1) {
     // issue brick b + NST - 1 into the stage brick b - 1 used (every wave passed the barrier after it)
     const int sn = sc == 0 ? NST - 1 : sc - 1;
-    if (b + NST - 1 < b_end && g.dbg != 1) issue(st + sn * SS, b + NST - 1);
+    if (b + NST - 1 < b_end && g.dbg != 1) {
+      if constexpr (RING)
+        issue_ring(st + sn * SS, b + NST - 1);
+      else
+        issue(st + sn * SS, b + NST - 1);
+    }
+    const int sb = RING ? ring_sb(b) : 0;
     if (g.dbg != 2) {
       if constexpr (PIPE) {
         if (t_cnt == 4)
-          compute_pipe(st + sc * SS, std::integral_constant<int, 4>{});
+          compute_pipe(st + sc * SS, sb, std::integral_constant<int, 4>{});
         else
-          compute_pipe(st + sc * SS, std::integral_constant<int, 3>{});
+          compute_pipe(st + sc * SS, sb, std::integral_constant<int, 3>{});
       } else {
-        compute(st + sc * SS);
+        compute(st + sc * SS, sb);
       }
     }
     // brick b + 1 has landed once at most min(NST - 2, bricks issued after it) bricks are in flight
-    const int after = b_end - b - 2 < NST - 2 ? b_end - b - 2 : NST - 2;
-    wait_bricks(after > 0 ? after : 0);
+    if constexpr (RING) {
+      wait_cnt(b + 2 < b_end ? ring_count(b + 2) : 0);
+    } else {
+      const int after = b_end - b - 2 < NST - 2 ? b_end - b - 2 : NST - 2;
+      wait_bricks(after > 0 ? after : 0);
+    }
     __syncthreads();
     if constexpr (NORM) {
       if (b + 1 < b_end) {
@@ -3883,7 +4002,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
     }
   }
 
-  static_assert(sizeof(st) >= 16 * WEP_P * sizeof(float), "epilogue staging must fit the stage ring");
+  static_assert((RING ? sizeof(xr) : sizeof(st)) >= 16 * WEP_P * sizeof(float),
+                "epilogue staging must fit the stage ring");
   if (g.frag && !(g.grad != nullptr && g.ksplit == 1)) {
     // split partials in the accumulators' own layout: every (tap, i, j) fragment is 1 KB contiguous (lane l's
     // f32x4 at 16 l), so each wave stores straight from registers with 16-B lanes -- no LDS transpose, no
@@ -3901,7 +4021,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
           *reinterpret_cast<f32x4*>(base + ((tap * MT + i) * 2 + j) * 256 + lane * 4) = acc[t][i][j];
     }
   } else {
-    wgrad_store_chmajor<MT>(acc, t_begin, t_cnt, reinterpret_cast<float*>(st), g, ks, row0, c0);
+    __syncthreads();   // (RING: the halo slots are the epilogue's staging)
+    wgrad_store_chmajor<MT>(acc, t_begin, t_cnt, RING ? reinterpret_cast<float*>(xr) : reinterpret_cast<float*>(st),
+                            g, ks, row0, c0);
   }
   if (bias_wave && i16 == 0) {
     // acc[3][i][0][r] = sum over the block's voxels of dy[.][row0 + 16 i + 4 g4 + r] (every column alike)
@@ -4893,10 +5015,14 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
         // fragment prefetch two steps ahead (32 co; at 64 co the extra registers spill: 59.5 -> 72.3 us)
         const bool pipe = mt == 2 && knob("MMSEG_WGRAD_DMA_PIPE", 1) != 0;
         const bool norm = g.nmean != nullptr;
+        // z-plane halo ring (MMSEG_WGRAD_RING): no deferred norm, three stages
+        const bool ring = !norm && !st4 && knob("MMSEG_WGRAD_RING", 0) != 0;
         if (mt == 4) {
           mmseg::note_kernel("wgrad_dma_kernel<CO64>");
           if (norm)
             MMSEG_LAUNCH((wgrad_dma_kernel<4, true>), grid, dim3(512), 0, s, g);
+          else if (ring)
+            MMSEG_LAUNCH((wgrad_dma_kernel<4, false, 3, false, true>), grid, dim3(512), 0, s, g);
           else if (st4)
             MMSEG_LAUNCH((wgrad_dma_kernel<4, false, 4>), grid, dim3(512), 0, s, g);
           else
@@ -4907,6 +5033,10 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
             MMSEG_LAUNCH((wgrad_dma_kernel<2, true, 3, true>), grid, dim3(512), 0, s, g);
           else if (norm)
             MMSEG_LAUNCH((wgrad_dma_kernel<2, true>), grid, dim3(512), 0, s, g);
+          else if (ring && pipe)
+            MMSEG_LAUNCH((wgrad_dma_kernel<2, false, 3, true, true>), grid, dim3(512), 0, s, g);
+          else if (ring)
+            MMSEG_LAUNCH((wgrad_dma_kernel<2, false, 3, false, true>), grid, dim3(512), 0, s, g);
           else if (pipe)
             MMSEG_LAUNCH((wgrad_dma_kernel<2, false, 3, true>), grid, dim3(512), 0, s, g);
           else if (st4)

@@ -598,6 +598,43 @@ def test_conv3_dgrad_split_output(dev, dtype, knobs, cin, cout, shape, monkeypat
 
 
 @pytest.mark.parametrize("cin,cout,shape,accumulate", [
+    (64, 64, (2, 8, 12, 16), 0), (32, 128, (2, 8, 8, 16), 1), (64, 32, (2, 8, 4, 16), 1),
+    (32, 32, (2, 12, 8, 24), 0), (64, 64, (2, 24, 24, 24), 1), (64, 32, (2, 24, 24, 24), 0)])
+def test_wgrad_dma_halo_ring(dev, cin, cout, shape, accumulate, monkeypatch):
+    """wgrad_dma with the z-plane halo ring (MMSEG_WGRAD_RING=1: bricks walked z-fastest, a column's next brick
+    stages only its four new halo planes into rotating slots) against the per-brick halo (=0) and against fp64.
+    The ring changes which bricks a split sums and in what order, so the two agree to bf16-input rounding of the
+    fp32 sums, not bitwise; both held to the fp64 weight / bias gradient."""
+    N, D, H, W = shape
+    V = N * D * H * W
+    g = torch.Generator().manual_seed(7 * cin + cout + V)
+    dy = torch.randn(V, cout, generator=g).to(dev, torch.bfloat16).reshape(-1)
+    x = torch.randn(V, cin, generator=g).to(dev, torch.bfloat16).reshape(-1)
+    gw0 = torch.randn(cout * cin * 27, generator=g).to(dev) if accumulate else torch.zeros(cout * cin * 27, device=dev)
+    gb0 = torch.ones(cout, device=dev) if accumulate else torch.zeros(cout, device=dev)
+    L = lib()
+    shift = int(np.log2(cin // 8))
+    wsf = L.mmseg_conv3_wgrad_ws_floats(V, cout, cin, cin, shift, D, H, W, cout, cin, 1)
+    out = {}
+    for ring in ("0", "1"):
+        monkeypatch.setenv("MMSEG_WGRAD_RING", ring)
+        ws = torch.full((max(wsf, 1),), float("nan"), device=dev)
+        gw, gb = gw0.clone(), gb0.clone()
+        L.mmseg_conv3_wgrad(ptr(dy), cout, ptr(x), cin, ptr(gw), ptr(gb), cout, cin, cin, shift, V, D, H, W,
+                            ptr(ws), wsf, accumulate, 1, stream_handle())
+        assert L.mmseg_last_kernel().decode().startswith("wgrad_dma_kernel")
+        torch.cuda.synchronize()
+        out[ring] = (gw.double().cpu() - gw0.double().cpu(), gb.double().cpu() - gb0.double().cpu())
+    xr = x.double().cpu().reshape(N, D, H, W, cin).permute(0, 4, 1, 2, 3)
+    dyr = dy.double().cpu().reshape(N, D, H, W, cout).permute(0, 4, 1, 2, 3)
+    ref = torch.nn.grad.conv3d_weight(xr, (cout, cin, 3, 3, 3), dyr, padding=1).reshape(-1)
+    refb = dyr.sum(dim=(0, 2, 3, 4))
+    for ring in ("0", "1"):
+        assert rel(out[ring][0], ref) < 1e-4 and rel(out[ring][1], refb) < 1e-4, ring
+    assert rel(out["1"][0], out["0"][0]) < 1e-4
+
+
+@pytest.mark.parametrize("cin,cout,shape,accumulate", [
     (64, 64, (2, 8, 12, 16), 0), (32, 128, (2, 8, 8, 16), 1), (64, 32, (2, 8, 4, 16), 0),
     (128, 64, (2, 8, 8, 16), 1), (32, 32, (2, 12, 8, 24), 0)])
 def test_wgrad_dma_fragment_partials_bitwise(dev, cin, cout, shape, accumulate, monkeypatch):
