@@ -218,7 +218,13 @@ int mmseg_conv3_wgrad_group(const void* dy, int lddy, const void* x, int ldx, fl
                             long long ws_floats, int accumulate, int groups, long long grad_gstride,
                             int bias_gstride, int phase, int dtype, void* stream);
 /* mmseg_conv3_wgrad (nmean / nrstd: optional deferred norm, as mmseg_conv3_wgrad_norm) in phases: bit 1 runs
- * the weight-gradient kernel, bit 2 the split reduce (3 = both), so the kernel can be timed alone. */
+ * the weight-gradient kernel, bit 2 the split reduce (3 = both), so the kernel can be timed alone.  Bit 4 with
+ * bit 2 defers the reduce: its arguments are queued until mmseg_wgrad_reduce_flush(stream), which sums every
+ * queued reduce of that stream in one launch (bitwise the same gradients); the partials (ws) must stay untouched
+ * until then. */
+int mmseg_wgrad_reduce_flush(void* stream);
+int mmseg_wgrad_reduce_pending(void);
+int mmseg_wgrad_reduce_discard(void* stream);
 int mmseg_conv3_wgrad_ex(const void* dy, int lddy, const void* x, int ldx, const float* nmean, const float* nrstd,
                          float* grad, float* bias_grad, int Co, int Cip, int Ci, int cpg_shift, long long V, int D,
                          int H, int W, float* ws, long long ws_floats, int accumulate, int phase, int dtype,

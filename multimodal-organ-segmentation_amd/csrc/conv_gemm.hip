@@ -4298,20 +4298,19 @@ struct WReduceArgs {
 // thousands), so every thread has a few independent loads in flight.  Bias
 // partials ([ks][Ca], after the weight columns) are summed by the blocks past
 // the weight range.
-template <int S, int U = 4>
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(WReduceArgs g) {
-  if (blockIdx.y) {                           // grouped: this group's splits and gradient
-    const long long gi = blockIdx.y;
+template <int U>
+__device__ __forceinline__ void wred_body(WReduceArgs g, const int S, const int bx, const int gy, float4* red) {
+  if (gy) {                                   // grouped: this group's splits and gradient
+    const long long gi = gy;
     g.part += gi * g.ksplit * ((long long)g.Ca * g.Ncols);
     if (g.bias_part) g.bias_part += gi * g.ksplit * g.Ca;
     g.grad += gi * g.grad_gstride;
     if (g.bias_grad) g.bias_grad += gi * g.bias_gstride;
   }
-  constexpr int NC = 256 / S;                 // float4 columns per block
-  __shared__ float4 red[S][NC];
+  const int NC = 256 / S;                     // float4 columns per block
   const int col4 = threadIdx.x % NC, sl = threadIdx.x / NC;
   const long long total = (long long)g.Ca * g.Ncols;   // multiple of 4
-  const long long e0 = ((long long)blockIdx.x * NC + col4) * 4;
+  const long long e0 = ((long long)bx * NC + col4) * 4;
   float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
   if (e0 < total) {
     const float4* p = reinterpret_cast<const float4*>(g.part + e0);
@@ -4344,14 +4343,14 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(WReduceArgs g) {
   if (S > 1) {
     // slice sums: a fixed pairwise tree (S = 16..64 made the former serial sweep of one thread per column the
     // kernel's critical path)
-    red[sl][col4] = v;
+    red[sl * NC + col4] = v;
     __syncthreads();
 #pragma unroll
     for (int h = S / 2; h > 0; h >>= 1) {
       if (sl < h) {
-        const float4 a = red[sl + h][col4];
+        const float4 a = red[(sl + h) * NC + col4];
         v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
-        red[sl][col4] = v;
+        red[sl * NC + col4] = v;
       }
       __syncthreads();
     }
@@ -4398,6 +4397,32 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(WReduceArgs g) {
     if (g.accumulate) g.grad[dst] += val;
     else g.grad[dst] = val;
   }
+}
+
+template <int S, int U = 4>
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(WReduceArgs g) {
+  __shared__ float4 red[256];
+  wred_body<U>(g, S, blockIdx.x, blockIdx.y, red);
+}
+
+// Several layers' split reduces in one launch (mmseg_wgrad_reduce_flush): descriptor k owns blocks
+// [blk0[k], blk0[k + 1]) = groups x nbx[k], each summed exactly as its own wgrad_reduce_kernel<S[k]> launch would
+// (same slices, same fixed order: bitwise the same gradient).
+constexpr int WRB_MAX = 30;
+struct WReduceBatch {
+  int n;
+  int blk0[WRB_MAX + 1];
+  int nbx[WRB_MAX];
+  int S[WRB_MAX];
+  WReduceArgs d[WRB_MAX];
+};
+__global__ __launch_bounds__(256) void wgrad_reduce_batch_kernel(WReduceBatch b) {
+  __shared__ float4 red[256];
+  const int bid = blockIdx.x;
+  int k = 0;
+  while (k + 1 < b.n && bid >= b.blk0[k + 1]) ++k;
+  const int local = bid - b.blk0[k];
+  wred_body<4>(b.d[k], b.S[k], local % b.nbx[k], local / b.nbx[k], red);
 }
 
 // Column sums (bias gradient): db[c] = sum_v dy[v][c], split over voxels.
@@ -5197,17 +5222,31 @@ Conv3WgradPlan plan_conv3_wgrad(long long V, int Co, int Cip, int Ci, int cpg_sh
   return p;
 }
 
-int launch_wgrad_reduce(WReduceArgs g, void* stream, int groups = 1) {
+// split slices S of a reduce: about MMSEG_WGRAD_RPT (default 8) split loads per thread, the slice sums a pairwise
+// LDS tree; small gradients over many splits (the stem: 1,056 values x 1,024 splits) take more slices until the
+// grid fills the chip, down to 2 loads per thread (S = 64 left it at 66 blocks, 12.8 us for 4 MB)
+int wred_slices(const WReduceArgs& g) {
   const int ksplit = g.ksplit;
   const long long total = (long long)g.Ca * g.Ncols + (g.bias_part ? g.Ca : 0);
-  hipStream_t s = (hipStream_t)stream;
-  // slices S: about MMSEG_WGRAD_RPT (default 8) split loads per thread, the slice sums a pairwise LDS tree
   const int rpt = knob("MMSEG_WGRAD_RPT", 8);
   int S = 1;
   while (S < 64 && ksplit / (2 * S) >= rpt) S *= 2;
-  // small gradients over many splits (the stem: 1,056 values x 1,024 splits): more slices until the grid
-  // fills the chip, down to 2 loads per thread (S = 64 left it at 66 blocks, 12.8 us for 4 MB)
   while (S < 256 && (total * S + 1023) / 1024 < knob("MMSEG_WGRAD_RBLK", 512) && ksplit / (2 * S) >= 2) S *= 2;
+  return S;
+}
+
+// reduces deferred by conv3_wgrad_impl (phase bit 4) until mmseg_wgrad_reduce_flush
+struct PendingWred {
+  WReduceArgs r;
+  int groups;
+  void* stream;
+};
+std::vector<PendingWred> g_wred_pending;
+
+int launch_wgrad_reduce(WReduceArgs g, void* stream, int groups = 1) {
+  const long long total = (long long)g.Ca * g.Ncols + (g.bias_part ? g.Ca : 0);
+  hipStream_t s = (hipStream_t)stream;
+  const int S = wred_slices(g);
   const int U = knob("MMSEG_WRED_U", 4);
 #define MMSEG_WRED(SS, NB)                                                                             \
   case SS:                                                                                             \
@@ -5663,8 +5702,8 @@ int mmseg_conv3_wgrad_group(const void* dy, int lddy, const void* x, int ldx, fl
                             int Cip, int Ci, int cpg_shift, long long V, int D, int H, int W, float* ws,
                             long long ws_floats, int accumulate, int groups, long long grad_gstride,
                             int bias_gstride, int phase, int dtype, void* stream) {
-  MMSEG_REQUIRE(groups >= 1 && V % ((long long)groups * D * H * W) == 0 && phase >= 1 && phase <= 3,
-                "conv3_wgrad_group: V must hold groups x whole samples, phase 1..3");
+  MMSEG_REQUIRE(groups >= 1 && V % ((long long)groups * D * H * W) == 0 && phase >= 1 && phase <= 7 && (phase & 3),
+                "conv3_wgrad_group: V must hold groups x whole samples, phase bits 1 | 2 (| 4 defer)");
   return conv3_wgrad_impl(dy, lddy, x, ldx, nullptr, nullptr, grad, bias_grad, Co, Cip, Ci, cpg_shift, V, D, H, W, ws,
                           ws_floats, accumulate, dtype, stream, phase, groups, grad_gstride, bias_gstride);
 }
@@ -5701,11 +5740,53 @@ int mmseg_conv3_wgrad_ex(const void* dy, int lddy, const void* x, int ldx, const
                          float* grad, float* bias_grad, int Co, int Cip, int Ci, int cpg_shift, long long V, int D,
                          int H, int W, float* ws, long long ws_floats, int accumulate, int phase, int dtype,
                          void* stream) {
-  MMSEG_REQUIRE(phase >= 1 && phase <= 3, "conv3_wgrad_ex: phase %d must be 1, 2 or 3", phase);
+  MMSEG_REQUIRE(phase >= 1 && phase <= 7 && (phase & 3), "conv3_wgrad_ex: phase %d: bits 1 | 2 (| 4 defer)", phase);
   MMSEG_REQUIRE(!nmean || (nrstd && mmseg_conv3_wgrad_norm_ok(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype)),
                 "conv3_wgrad_ex: unsupported shape for the deferred norm (mmseg_conv3_wgrad_norm_ok)");
   return conv3_wgrad_impl(dy, lddy, x, ldx, nmean, nrstd, grad, bias_grad, Co, Cip, Ci, cpg_shift, V, D, H, W, ws,
                           ws_floats, accumulate, dtype, stream, phase);
+}
+
+// Launch the reduces deferred with phase bit 4 (in the order they were deferred, at most WRB_MAX per launch) on
+// `stream`; each gradient is bitwise what its own reduce would have written.  Returns the number flushed.
+int mmseg_wgrad_reduce_flush(void* stream) {
+  int done = 0;
+  std::vector<PendingWred> keep;
+  std::vector<PendingWred> mine;
+  for (auto& e : g_wred_pending) (e.stream == stream ? mine : keep).push_back(e);
+  g_wred_pending.swap(keep);
+  for (size_t i0 = 0; i0 < mine.size(); i0 += WRB_MAX) {
+    WReduceBatch b{};
+    b.n = (int)std::min<size_t>(WRB_MAX, mine.size() - i0);
+    int blk = 0;
+    for (int k = 0; k < b.n; ++k) {
+      const PendingWred& e = mine[i0 + k];
+      const long long total = (long long)e.r.Ca * e.r.Ncols + (e.r.bias_part ? e.r.Ca : 0);
+      b.d[k] = e.r;
+      b.S[k] = wred_slices(e.r);
+      b.nbx[k] = ceil_div(total, 1024 / b.S[k]);
+      b.blk0[k] = blk;
+      blk += b.nbx[k] * e.groups;
+    }
+    b.blk0[b.n] = blk;
+    mmseg::note_kernel("wgrad_reduce_batch_kernel");
+    MMSEG_LAUNCH(wgrad_reduce_batch_kernel, dim3(blk), dim3(256), 0, (hipStream_t)stream, b);
+    if (mmseg::check_launch("wgrad_reduce_batch")) return -1;
+    done += b.n;
+  }
+  return done;
+}
+
+// number of deferred reduces not yet flushed (all streams)
+int mmseg_wgrad_reduce_pending(void) { return (int)g_wred_pending.size(); }
+
+// drop the deferred reduces of `stream` (a backward that failed half way); returns how many
+int mmseg_wgrad_reduce_discard(void* stream) {
+  const size_t n0 = g_wred_pending.size();
+  g_wred_pending.erase(std::remove_if(g_wred_pending.begin(), g_wred_pending.end(),
+                                      [&](const PendingWred& e) { return e.stream == stream; }),
+                       g_wred_pending.end());
+  return (int)(n0 - g_wred_pending.size());
 }
 
 int conv3_wgrad_impl(const void* dy, int lddy, const void* x, int ldx, const float* nmean, const float* nrstd,
@@ -5744,6 +5825,10 @@ int conv3_wgrad_impl(const void* dy, int lddy, const void* x, int ldx, const flo
   const int ng = groups > 1 ? groups : 1;
   WReduceArgs r{part, grad, bpart, bias_grad, Co, ncols, p.ksplit / ng, Cip, Ci, 27, accumulate, p.kind >= 2 ? 1 : 0,
                 fmt, wgrad_nchunk(cpg_shift, g.kchunks), grad_gstride, bias_gstride};
+  if (phase & 4) {   // deferred: summed by the next mmseg_wgrad_reduce_flush on this stream
+    g_wred_pending.push_back({r, ng, stream});
+    return 0;
+  }
   return launch_wgrad_reduce(r, stream, ng);
 }
 

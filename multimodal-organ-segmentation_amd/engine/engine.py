@@ -55,7 +55,8 @@ class SegEngine:
 
     def backward(self, dlogits: torch.Tensor) -> None:
         accumulate = self.flat.begin_backward()
-        self.program.backward(dlogits.float().contiguous(), accumulate)
+        with self.rt.wred_session():
+            self.program.backward(dlogits.float().contiguous(), accumulate)
         self.rt.join_side()
         self.flat.end_backward()
 
@@ -72,7 +73,8 @@ class SegEngine:
 
     def backward_loss(self, gout: torch.Tensor) -> None:
         accumulate = self.flat.begin_backward()
-        self.program.backward(None, accumulate, gout=gout.float().contiguous())
+        with self.rt.wred_session():
+            self.program.backward(None, accumulate, gout=gout.float().contiguous())
         self.rt.join_side()
         self.flat.end_backward()
 

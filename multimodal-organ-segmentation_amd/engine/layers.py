@@ -300,12 +300,12 @@ class Conv3:
                                              y.ptr, y.ld, x.N * x.V, self.ncols_f, self.Cpad, self.KG,
                                              self.cpg_shift, x.D, x.H, x.W, self.rt.code, self.rt.stream)
 
-    def _part(self, nfloats: int) -> torch.Tensor:
+    def _part(self, nfloats: int, own: bool = False) -> torch.Tensor:
         """Split partials of this layer's weight gradient: the shared scratch, or with the side-stream reduce
-        (Runtime.async_wred) a buffer of the layer's own, since its reduce may still run while the data-gradient
-        kernel takes scratch (the partials of a whole backward, ~1.2 GB for the 96^3 DualEncoder, fit HBM many
-        times over)."""
-        if not self.rt.async_wred:
+        (Runtime.async_wred) or a deferred one (own: Runtime.defer_wred) a buffer of the layer's own, since its
+        reduce may still run while later kernels take scratch (the partials of a whole backward, ~1.2 GB for the
+        96^3 DualEncoder, fit HBM many times over)."""
+        if not self.rt.async_wred and not own:
             return self.rt.ws(nfloats)
         buf = getattr(self, "_wpart", None)
         if buf is None or buf.numel() < nfloats:
@@ -364,7 +364,10 @@ class Conv3:
         rows = self.Cop if self.wg_stage is not None else self.Co
         wsf = L.mmseg_conv3_wgrad_ws_floats(V, rows, self.Cip, self.Ci, self.cpg_shift, x.D, x.H, x.W, dy.ld,
                                             x.ld, code)
-        ws = self._part(wsf) if wsf > 0 else None
+        # a batched backward queues the split reduce (its partials then need a buffer of their own); not with a
+        # staging buffer, whose copy into the arena must follow the reduce
+        defer = wsf > 0 and self.wg_stage is None and self.rt.defer_wred(self.flat)
+        ws = self._part(wsf, own=defer) if wsf > 0 else None
         wgrad = self.flat.grad(self.conv.weight)
         nm, nr = (ptr(norm[0]), ptr(norm[1])) if norm is not None else (None, None)
         args = (dy.ptr, dy.ld, x.ptr, x.ld, nm, nr, ptr(self.wg_stage) if self.wg_stage is not None else ptr(wgrad),
@@ -391,7 +394,7 @@ class Conv3:
 
         def reduce(s2):
             with TIMER.region("wgrad_reduce_kernel"):
-                L.mmseg_conv3_wgrad_ex(*args, 2, code, s2)
+                L.mmseg_conv3_wgrad_ex(*args, 6 if defer else 2, code, s2)
             if self.wg_stage is not None:     # rows [0, Co) of the staging are the gradient's storage order
                 n = wgrad.numel()
                 if accumulate:
@@ -763,7 +766,8 @@ class ConvGroup:
         V = x.N * x.V
         wsf = L.mmseg_conv3_wgrad_group_ws_floats(V, c.Co, c.Cip, c.Ci, c.cpg_shift, x.D, x.H, x.W, dy.ld, x.ld,
                                                   self.G, code)
-        ws = c._part(wsf)
+        defer = wsf > 0 and self.rt.defer_wred(self.flat)
+        ws = c._part(wsf, own=defer)
         gw = ptr(self.flat.grad(c.conv.weight))
         gb = ptr(self.flat.grad(c.conv.bias)) if c.conv.bias is not None else None
         args = (dy.ptr, dy.ld, x.ptr, x.ld, gw, gb, c.Co, c.Cip, c.Ci, c.cpg_shift, V, x.D, x.H, x.W, ptr(ws), wsf,
@@ -775,7 +779,7 @@ class ConvGroup:
 
         def reduce(s2):
             with TIMER.region("wgrad_reduce_kernel"):
-                L.mmseg_conv3_wgrad_group(*args, 2, code, s2)
+                L.mmseg_conv3_wgrad_group(*args, 6 if defer else 2, code, s2)
             for cc in self.convs:
                 self.flat.mark(*[p for p in (cc.conv.weight, cc.conv.bias) if p is not None])
         conc = (dx is not None and self.rt.async_wred and os.environ.get("MMSEG_WD_CONC", "0") != "0"

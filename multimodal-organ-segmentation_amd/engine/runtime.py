@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import math
 import os
+from contextlib import contextmanager
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -79,6 +80,12 @@ class Runtime:
         self.async_wred = os.environ.get("MMSEG_ASYNC_WRED", "0") != "0"
         self._side: Optional[torch.cuda.Stream] = None
         self._side_pending = False
+        # weight-gradient split reduces batched (MMSEG_WRED_BATCH): inside a backward session (`wred_session`) each
+        # layer's reduce is queued in the library (its partials in a buffer of the layer's own) and the whole
+        # backward's reduces run as one launch at the end of the session -- bitwise the same gradients, ~28 fewer
+        # launches per 96^3 step.  Not with DP gradient buckets (they need each gradient as soon as it is final)
+        self.batch_wred = os.environ.get("MMSEG_WRED_BATCH", "0") != "0"
+        self._wred_active = False
 
     # ---------------------------------------------------------------- alloc
     def act(self, N: int, D: int, H: int, W: int, C: int, ld: Optional[int] = None) -> Act:
@@ -110,6 +117,27 @@ class Runtime:
         self._side.wait_stream(main)
         self._side_pending = True
         return torch.cuda.stream(self._side)
+
+    def defer_wred(self, flat: Optional["FlatParams"]) -> bool:
+        """Queue this layer's split reduce until the session ends (see batch_wred)."""
+        return (self._wred_active and not self.async_wred
+                and (flat is None or flat.on_ready is None))
+
+    @contextmanager
+    def wred_session(self):
+        """A backward whose split reduces may be batched; flushed (one launch) on exit."""
+        self._wred_active = self.batch_wred
+        try:
+            yield
+        except BaseException:
+            self.lib.mmseg_wgrad_reduce_discard(self.stream)
+            raise
+        finally:
+            self._wred_active = False
+        if self.batch_wred:
+            n = self.lib.mmseg_wgrad_reduce_flush(self.stream)
+            if n < 0:
+                raise RuntimeError("mmseg_wgrad_reduce_flush: " + self.lib.mmseg_last_error().decode(errors="replace"))
 
     def join_side(self) -> None:
         """The current stream waits for all side-stream work (end of the backward: the gradients are final)."""

@@ -142,7 +142,8 @@ class StepGraphs:
                 # (recorded into the graph on the comm stream), the guard count travels with the first bucket,
                 # and finish() joins every collective into the capture stream before the AdamW kernel
                 tr._arm_buckets(True, ws[-1:])
-                eng.program.backward(None, False, gout=self.gout)
+                with eng.rt.wred_session():
+                    eng.program.backward(None, False, gout=self.gout)
                 eng.rt.join_side()
                 if tr.dp and tr._buckets is not None:
                     tr._buckets.finish()

@@ -18,6 +18,7 @@ import pytest
 import torch
 
 import mmseg_amd  # noqa: F401
+from mmseg_amd._lib import lib
 from mmseg_amd.models.build import build_model
 from mmseg_amd.trainer.losses import get_loss
 from mmseg_amd.trainer.trainer import Trainer
@@ -636,6 +637,34 @@ def test_deferred_encoder_norm_bitwise(dev, dtype, monkeypatch):
     assert torch.equal(res[0][0], res[1][0])
     assert torch.equal(res[0][1], res[1][1])
     assert all(torch.equal(a, b) for a, b in zip(res[0][2], res[1][2]))
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
+def test_batched_weight_gradient_reduce_bitwise(dev, dtype, monkeypatch):
+    """MMSEG_WRED_BATCH=1 queues every 3^3 weight-gradient split reduce of the backward and sums them in one launch
+    at its end (wgrad_reduce_batch_kernel): each gradient is summed over the same splits in the same order as its
+    own reduce, so the whole step's gradients are BITWISE the unbatched ones; the queue is empty afterwards."""
+    kind, mods, C, fusion, lossname = TINY["dual_tiny_cross_attention"]
+    g = golden("dual_tiny_cross_attention")
+    gen = torch.Generator().manual_seed(3)
+    x = torch.randn(2, len(mods), 96, 96, 96, generator=gen)
+    y = torch.randint(0, C, (2, 96, 96, 96), generator=gen)
+    res = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("MMSEG_WRED_BATCH", flag)
+        cfg = make_config(kind, mods, C, list(g["features"]), fusion=fusion, loss=lossname, dtype=dtype)
+        torch.manual_seed(int(g["seed"]))
+        m = build_model(cfg)
+        tr = Trainer(cfg, m)
+        m.train()
+        loss = tr.criterion(m(x.to(dev)), y.to(dev))
+        loss.backward()
+        torch.cuda.synchronize()
+        res[flag] = (loss.item(), {n: p.grad.detach().clone() for n, p in m.backbone.named_parameters()})
+        assert lib().mmseg_wgrad_reduce_pending() == 0
+    assert res["0"][0] == res["1"][0]
+    diff = [n for n in res["0"][1] if not torch.equal(res["0"][1][n], res["1"][1][n])]
+    assert not diff, diff
 
 
 @pytest.mark.parametrize("tag", ["dual_tiny_cross_attention", "dual_tiny_add", "dual_tiny_m3_tversky"])
