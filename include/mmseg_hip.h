@@ -211,6 +211,8 @@ int mmseg_conv3_group_ok(int M, int Ncols, int Cpad, int KG, int cpg_shift, int 
                          int dtype);
 int mmseg_conv3_wgrad_group_ok(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W, int lddy,
                                int ldx, int dtype);
+int mmseg_conv3_group_splits(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,
+                             int dtype);
 long long mmseg_conv3_wgrad_group_ws_floats(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W,
                                             int lddy, int ldx, int groups, int dtype);
 int mmseg_conv3_wgrad_group(const void* dy, int lddy, const void* x, int ldx, float* grad, float* bias_grad, int Co,

@@ -2386,13 +2386,16 @@ struct Conv3Plan {
   int bn;            // kind 2 column tile
 };
 
-Conv3Plan plan_conv3(int M, int Ncols, int cin, int D, int H, int W, int lda, int ldo, int tsize) {
+// force_r: the runtime-brick kernel even where the (4, 8, 8)-brick family fits -- the modality-grouped launches,
+// whose per-group weights only the runtime-brick kernel reads (24^3 with MMSEG_GROUP_FORCE_R)
+Conv3Plan plan_conv3(int M, int Ncols, int cin, int D, int H, int W, int lda, int ldo, int tsize,
+                     bool force_r = false) {
   Conv3Plan p{0, 0, 0, 0, 1, 32};
   const int brick = knob("MMSEG_BRICK", 2);
   const bool base_ok = cin % CK == 0 && lda % 8 == 0 && ldo % 8 == 0 && Ncols % 32 == 0;
   // 48-column multiples (SwinUNETR's feature_size 48) run the brick2 kernel with 48-column tiles
   const bool ok48 = cin % CK == 0 && lda % 8 == 0 && ldo % 8 == 0 && Ncols % 48 == 0 && knob("MMSEG_BRICK2_BN48", 1);
-  if (brick == 2 && (base_ok || ok48) && D % 4 == 0 && H % B2_Y == 0 && W % B2_X == 0) {
+  if (!force_r && brick == 2 && (base_ok || ok48) && D % 4 == 0 && H % B2_Y == 0 && W % B2_X == 0) {
     p.kind = 1;
     return p;
   }
@@ -4696,7 +4699,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
   dim3 block(256);
   const int brick = knob("MMSEG_BRICK", 2);
   const Conv3Plan plan = MODE == MODE_CONV3 ? plan_conv3(g.M, g.Ncols, 8 << g.cpg_shift, g.D, g.H, g.W, g.lda, g.ldo,
-                                                         (int)sizeof(T))
+                                                         (int)sizeof(T), g.grp_n > 0)
                                             : Conv3Plan{0, 0, 0, 0, 1, 32};
   MMSEG_REQUIRE(g.grp_n == 0 || (MODE == MODE_CONV3 && plan.kind == 2),
                 "grouped conv: only the runtime-brick kernel takes per-group weights (small volumes)");
@@ -5126,9 +5129,11 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
 // 0: generic wgrad_kernel, 1: wgrad_brick_kernel (32 co), 2: wgrad_brick2_kernel (64 / 32 co),
 // 3: wgrad_brickr_kernel (runtime brick, small volumes).
 // (v2 / runtime brick are bf16 only: their two fp32 stage buffers would not fit in LDS)
-int wgrad_brick_ok(int Ca, int cpg_shift, int D, int H, int W, int lda, int ldb, int dtype) {
+int wgrad_brick_ok(int Ca, int cpg_shift, int D, int H, int W, int lda, int ldb, int dtype, bool force_r = false) {
   const int k = knob("MMSEG_WGRAD_BRICK", 2);
   if (!(k && Ca % 32 == 0 && (8 << cpg_shift) % CK == 0 && lda % 8 == 0 && ldb % 8 == 0)) return 0;
+  if (force_r)   // grouped launches: only the runtime-brick weight gradient splits by sample group
+    return (k >= 2 && dtype == MMSEG_BF16 && knob("MMSEG_WGRAD_BRICKR", 1) && plan_wgrad_brickr(D, H, W).bz) ? 3 : 0;
   if (D % BRK_Z == 0 && H % BRK_Y == 0 && W % BRK_X == 0)
     return (k >= 2 && dtype == MMSEG_BF16 && (Ca % 64 == 0 || knob("MMSEG_WGRAD_BRICK2_CO32", 1))) ? 2 : 1;
   if (k >= 2 && dtype == MMSEG_BF16 && knob("MMSEG_WGRAD_BRICKR", 1) && plan_wgrad_brickr(D, H, W).bz) return 3;
@@ -5199,13 +5204,13 @@ struct Conv3WgradPlan {
 };
 
 Conv3WgradPlan plan_conv3_wgrad(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W, int lda,
-                                int ldb, int dtype, long long ws_cap) {
+                                int ldb, int dtype, long long ws_cap, bool force_r = false) {
   Conv3WgradPlan p{0, 1, 0, 0};
   const long long ncols = 27LL * Cip;
   const long long per_split = (long long)Co * ncols + Co;
   int cap = (int)(ws_cap / per_split);
   if (cap < 1) cap = 1;
-  p.kind = wgrad_brick_ok(Co, cpg_shift, D, H, W, lda, ldb, dtype);
+  p.kind = wgrad_brick_ok(Co, cpg_shift, D, H, W, lda, ldb, dtype, force_r);
   if (p.kind) {
     p.ksplit = brick_wgrad_splits(V, cap, Co, cpg_shift, p.kind, D, H, W, wgrad_kchunks(Cip, Ci));
   } else {
@@ -5578,15 +5583,29 @@ int mmseg_conv3_dgrad_in(const void* a, int lda, const void* wpacked, void* out,
 // split-K workspace, ksplit*M*Ncols floats, with it and pass it as ksplit).
 // 1 when mmseg_conv_gemm_group / mmseg_conv3_wgrad_group take this shape: the runtime-brick conv (plan kind 2)
 // and, for the weight gradient, the runtime-brick weight-gradient kernel (kind 3).
+// (a grouped launch takes the runtime-brick kernels; MMSEG_GROUP_FORCE_R=1 also groups shapes that would otherwise
+// take the (4, 8, 8)-brick family -- the 24^3 level)
 int mmseg_conv3_group_ok(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,
                          int dtype) {
   if (!knob("MMSEG_GROUP_SMALL", 1)) return 0;
-  return plan_conv3(M, Ncols, 8 << cpg_shift, D, H, W, lda, ldo, dtype == MMSEG_BF16 ? 2 : 4).kind == 2 ? 1 : 0;
+  const int ts = dtype == MMSEG_BF16 ? 2 : 4;
+  if (plan_conv3(M, Ncols, 8 << cpg_shift, D, H, W, lda, ldo, ts).kind == 2) return 1;
+  return knob("MMSEG_GROUP_FORCE_R", 0) && plan_conv3(M, Ncols, 8 << cpg_shift, D, H, W, lda, ldo, ts, true).kind == 2
+             ? 1 : 0;
 }
 int mmseg_conv3_wgrad_group_ok(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W, int lddy,
                                int ldx, int dtype) {
   if (!knob("MMSEG_GROUP_SMALL", 1)) return 0;
-  return plan_conv3_wgrad(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype, 1LL << 40).kind == 3 ? 1 : 0;
+  if (plan_conv3_wgrad(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype, 1LL << 40).kind == 3) return 1;
+  return knob("MMSEG_GROUP_FORCE_R", 0) &&
+                 plan_conv3_wgrad(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype, 1LL << 40, true).kind == 3
+             ? 1 : 0;
+}
+// split count of a grouped conv (mmseg_conv_gemm_group): the runtime-brick plan's
+int mmseg_conv3_group_splits(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,
+                             int dtype) {
+  const Conv3Plan p = plan_conv3(M, Ncols, 8 << cpg_shift, D, H, W, lda, ldo, dtype == MMSEG_BF16 ? 2 : 4, true);
+  return p.kind == 2 ? p.ks : 1;
 }
 
 int mmseg_conv3_splits(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,
@@ -5672,7 +5691,7 @@ long long mmseg_conv3_wgrad_ws_floats(long long V, int Co, int Cip, int Ci, int 
 // multiple of `groups` (at least one split per group), never direct.
 Conv3WgradPlan plan_conv3_wgrad_grouped(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W,
                                         int lda, int ldb, int dtype, long long ws_cap, int groups) {
-  Conv3WgradPlan p = plan_conv3_wgrad(V, Co, Cip, Ci, cpg_shift, D, H, W, lda, ldb, dtype, ws_cap);
+  Conv3WgradPlan p = plan_conv3_wgrad(V, Co, Cip, Ci, cpg_shift, D, H, W, lda, ldb, dtype, ws_cap, groups > 1);
   if (groups <= 1) return p;
   p.ksplit = p.ksplit / groups * groups;
   if (p.ksplit < groups) p.ksplit = groups;

@@ -751,7 +751,7 @@ class ConvGroup:
     def fwd(self, x: Act, y: Act):
         c, L = self.c0, self.rt.lib
         M, nc = x.N * x.V, c.ncols_f
-        ks = L.mmseg_conv3_splits(M, nc, c.Cpad, c.KG, c.cpg_shift, x.D, x.H, x.W, x.ld, y.ld, self.rt.code)
+        ks = L.mmseg_conv3_group_splits(M, nc, c.Cpad, c.KG, c.cpg_shift, x.D, x.H, x.W, x.ld, y.ld, self.rt.code)
         ws = self.rt.ws(ks * M * nc) if ks > 1 else None
         with TIMER.region(_gemm_name(self.rt, nc, "conv3"), flops=2.0 * M * c.Co * 27 * c.Ci,
                           nbytes=_io_bytes(self.rt, M, c.Cip, c.Co, self.G * 27 * c.Cip * c.Co)):
@@ -793,7 +793,7 @@ class ConvGroup:
             if dx is None:
                 return
             M, nc = V, c.ncols_d
-            ks = L.mmseg_conv3_splits(M, nc, c.Cpad_d, c.KGd, c.dshift, x.D, x.H, x.W, dy.ld, dx.ld, code)
+            ks = L.mmseg_conv3_group_splits(M, nc, c.Cpad_d, c.KGd, c.dshift, x.D, x.H, x.W, dy.ld, dx.ld, code)
             ws2 = self.rt.ws(ks * M * nc) if ks > 1 else None
             with TIMER.region(_gemm_name(self.rt, nc, "conv3"), flops=2.0 * M * c.Co * 27 * c.Ci,
                               nbytes=_io_bytes(self.rt, M, c.Co, c.Cip, self.G * 27 * c.Cip * c.Co)):

@@ -667,13 +667,17 @@ def test_batched_weight_gradient_reduce_bitwise(dev, dtype, monkeypatch):
     assert not diff, diff
 
 
-@pytest.mark.parametrize("tag", ["dual_tiny_cross_attention", "dual_tiny_add", "dual_tiny_m3_tversky"])
-def test_grouped_modalities_match_per_modality(dev, tag, monkeypatch):
+@pytest.mark.parametrize("tag,force", [("dual_tiny_cross_attention", "0"), ("dual_tiny_add", "0"),
+                                       ("dual_tiny_m3_tversky", "0"), ("dual_tiny_cross_attention", "1"),
+                                       ("dual_tiny_m3_tversky", "1")])
+def test_grouped_modalities_match_per_modality(dev, tag, force, monkeypatch):
     """bf16 (the dtype whose small levels take the runtime-brick kernels): the modality-grouped small levels and the
     grouped encoder output-norm backward (MMSEG_GROUP_SMALL / MMSEG_GROUP_OUTNORM, programs.DualEncoderProgram)
     against the per-modality launches on the same weights and batch.  The grouped launches split the reductions
     differently (one launch over M x N samples), so the two differ by bf16 rounding: loss within 1e-3 relative,
-    logits within 2e-2 and every gradient within 5e-2 normwise (L2)."""
+    logits within 2e-2 and every gradient within 5e-2 normwise (L2).  force=1 (MMSEG_GROUP_FORCE_R): the 24^3
+    level is grouped too, on the runtime-brick kernels instead of the (4, 8, 8)-brick family."""
+    monkeypatch.setenv("MMSEG_GROUP_FORCE_R", force)
     kind, mods, C, fusion, lossname = TINY[tag]
     g = golden(tag)
     # 96^3 (B = 1, the tiny features): levels 12^3 / 6^3 take the runtime-brick kernels, as in the bench
@@ -699,7 +703,7 @@ def test_grouped_modalities_match_per_modality(dev, tag, monkeypatch):
                      prog.group_outnorm)
     (l1, lg1, g1, l0, L, go), (l2, lg2, g2, l0b, _, gob) = res["1"], res["0"]
     print(f"\n{tag}: grouped from level {l0} of {L} (output norm grouped: {go}); loss {l1:.6f} vs {l2:.6f}")
-    assert l0 == 3 and go and l0b == L and not gob
+    assert l0 == (2 if force == "1" else 3) and go and l0b == L and not gob
     assert abs(l1 - l2) < 1e-3 * abs(l2)
     assert float((lg1 - lg2).norm() / lg2.norm()) < 2e-2
     bad = {n: float((g1[n] - g2[n]).norm() / g2[n].norm()) for n in g2
