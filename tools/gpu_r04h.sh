@@ -5,7 +5,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/r04h
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 python3 -u -m pytest $R/tests/test_model_gpu.py::test_batched_weight_gradient_reduce_bitwise $R/tests/test_step_graph_gpu.py -m gpu -v -s --timeout 300 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1
+timeout -k 10 600 python3 -u -m pytest $R/tests/test_model_gpu.py::test_batched_weight_gradient_reduce_bitwise $R/tests/test_model_gpu.py::test_grouped_modalities_match_per_modality $R/tests/test_step_graph_gpu.py -m gpu -v -s --timeout 300 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1
 rc=$?
 tail -3 $O/tests.log
 [ $rc -ne 0 ] && { grep -E "^E |Error" $O/tests.log | head -20; exit 1; }
