@@ -82,9 +82,10 @@ class Runtime:
         self._side_pending = False
         # weight-gradient split reduces batched (MMSEG_WRED_BATCH): inside a backward session (`wred_session`) each
         # layer's reduce is queued in the library (its partials in a buffer of the layer's own) and the whole
-        # backward's reduces run as one launch at the end of the session -- bitwise the same gradients, ~28 fewer
-        # launches per 96^3 step.  Not with DP gradient buckets (they need each gradient as soon as it is final)
-        self.batch_wred = os.environ.get("MMSEG_WRED_BATCH", "0") != "0"
+        # backward's reduces run as one launch at the end of the session -- bitwise the same gradients, 22 fewer
+        # launches per 96^3 step (r04h A/B: 6.37 -> 6.31 ms).  Not with DP gradient buckets (they need each
+        # gradient as soon as it is final); MMSEG_WRED_BATCH=0 restores one reduce per layer
+        self.batch_wred = os.environ.get("MMSEG_WRED_BATCH", "1") != "0"
         self._wred_active = False
 
     # ---------------------------------------------------------------- alloc
