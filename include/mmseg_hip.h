@@ -225,6 +225,9 @@ int mmseg_conv3_wgrad_group(const void* dy, int lddy, const void* x, int ldx, fl
  * queued reduce of that stream in one launch (bitwise the same gradients); the partials (ws) must stay untouched
  * until then. */
 int mmseg_wgrad_reduce_flush(void* stream);
+/* mmseg_wgrad_reduce queued for the next mmseg_wgrad_reduce_flush on `stream` (part untouched until then) */
+int mmseg_wgrad_reduce_defer(const float* part, float* grad, const float* bias_part, float* bias_grad, int Ca,
+                             int Ncols, int ksplit, int cpad, int creal, int ntap, int accumulate, void* stream);
 int mmseg_wgrad_reduce_pending(void);
 int mmseg_wgrad_reduce_discard(void* stream);
 int mmseg_conv3_wgrad_ex(const void* dy, int lddy, const void* x, int ldx, const float* nmean, const float* nrstd,

@@ -5678,6 +5678,16 @@ int mmseg_wgrad_reduce(const float* part, float* grad, const float* bias_part, f
   return launch_wgrad_reduce(g, stream);
 }
 
+// mmseg_wgrad_reduce queued until mmseg_wgrad_reduce_flush(stream) (part must stay untouched until then)
+int mmseg_wgrad_reduce_defer(const float* part, float* grad, const float* bias_part, float* bias_grad, int Ca,
+                             int Ncols, int ksplit, int cpad, int creal, int ntap, int accumulate, void* stream) {
+  MMSEG_REQUIRE(((long long)Ca * Ncols) % 4 == 0 && (reinterpret_cast<uintptr_t>(part) & 15) == 0,
+                "wgrad_reduce: Ca*Ncols %% 4 == 0 and a 16-B aligned partial buffer");
+  WReduceArgs g{part, grad, bias_part, bias_grad, Ca, Ncols, ksplit, cpad, creal, ntap, accumulate, 0};
+  g_wred_pending.push_back({g, 1, stream});
+  return 0;
+}
+
 // Weight (+ bias) gradient of a 3^3 conv straight into the torch-layout fp32 gradient
 // grad[Co][Ci][27] (+ bias_grad[Co]), = or += (accumulate).  The library picks kernel and split;
 // ws holds mmseg_conv3_wgrad_ws_floats() floats (more lets it split further, fewer is clamped).
@@ -5774,9 +5784,20 @@ int mmseg_wgrad_reduce_flush(void* stream) {
   std::vector<PendingWred> mine;
   for (auto& e : g_wred_pending) (e.stream == stream ? mine : keep).push_back(e);
   g_wred_pending.swap(keep);
-  for (size_t i0 = 0; i0 < mine.size(); i0 += WRB_MAX) {
+  for (size_t i0 = 0; i0 < mine.size(); i0 += 0) {
     WReduceBatch b{};
-    b.n = (int)std::min<size_t>(WRB_MAX, mine.size() - i0);
+    // at most WRB_MAX per launch, and a gradient written by two queued reduces (an accumulating second use) starts
+    // a new launch, so the two stay ordered
+    size_t i1 = i0;
+    while (i1 < mine.size() && i1 - i0 < (size_t)WRB_MAX) {
+      bool clash = false;
+      for (size_t j = i0; j < i1; ++j)
+        clash = clash || mine[j].r.grad == mine[i1].r.grad ||
+                (mine[i1].r.bias_grad != nullptr && mine[j].r.bias_grad == mine[i1].r.bias_grad);
+      if (clash) break;
+      ++i1;
+    }
+    b.n = (int)(i1 - i0);
     int blk = 0;
     for (int k = 0; k < b.n; ++k) {
       const PendingWred& e = mine[i0 + k];
@@ -5792,6 +5813,7 @@ int mmseg_wgrad_reduce_flush(void* stream) {
     MMSEG_LAUNCH(wgrad_reduce_batch_kernel, dim3(blk), dim3(256), 0, (hipStream_t)stream, b);
     if (mmseg::check_launch("wgrad_reduce_batch")) return -1;
     done += b.n;
+    i0 = i1;
   }
   return done;
 }

@@ -30,6 +30,14 @@ IN_EPS = 1e-5
 TARGET_BLOCKS = 1024
 
 
+def _own_part(obj, rt: Runtime, nfloats: int) -> torch.Tensor:
+    """A split-partial buffer of obj's own (its reduce is queued: Runtime.defer_wred)."""
+    buf = getattr(obj, "_wpart", None)
+    if buf is None or buf.numel() < nfloats:
+        buf = obj._wpart = torch.empty(int(nfloats), dtype=torch.float32, device=rt.device)
+    return buf
+
+
 def _gemm_name(rt: Runtime, ncols: int, mode: str):
     """Timer family = the kernel the library actually launched (same name as in rocprofv3 traces)."""
     return lambda: f"{rt.lib.mmseg_last_kernel().decode()}[{'bf16' if rt.code else 'f32'}]"
@@ -345,7 +353,8 @@ class Conv3:
             # 42 + 12.8 us against 44 + 19.7 us with the reduce)
             ks = L.mmseg_stem_wgrad_splits(x.N, x.D, x.H, x.W, int(os.environ.get("MMSEG_STEM_SPLITS", "1024")))
             kp = L.mmseg_stem_kp(self.Ci)
-            part = self.rt.ws(ks * self.Co * kp + ks * self.Co)
+            defer = self.rt.defer_wred(self.flat)
+            part = self._part(ks * self.Co * kp + ks * self.Co, own=defer)
             bpart = part.data_ptr() + ks * self.Co * kp * 4
             with TIMER.region("stem_wgrad_kernel", flops=2.0 * V * self.Co * 27 * self.Ci,
                               nbytes=_io_bytes(self.rt, V, 8, self.Co, 27 * self.Ci * self.Co, 4)):
@@ -356,9 +365,9 @@ class Conv3:
                 else:
                     L.mmseg_stem_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, self.Ci, ptr(part), bpart, x.N, x.D, x.H, x.W,
                                        self.Co, ks, code, s)
-            L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.conv.weight)), bpart,
-                                 ptr(self.flat.grad(self.conv.bias)), self.Co, kp, ks, self.Ci, self.Ci, 27,
-                                 int(accumulate), s)
+            (L.mmseg_wgrad_reduce_defer if defer else L.mmseg_wgrad_reduce)(
+                ptr(part), ptr(self.flat.grad(self.conv.weight)), bpart, ptr(self.flat.grad(self.conv.bias)), self.Co,
+                kp, ks, self.Ci, self.Ci, 27, int(accumulate), s)
             self.flat.mark(self.conv.weight, self.conv.bias)
             return
         rows = self.Cop if self.wg_stage is not None else self.Co
@@ -490,14 +499,18 @@ class ConvT2:
         # bias gradient: column sums of the gathered dy tile emitted by the weight-gradient kernel itself
         # ([ks][8 Cop] after the weight partials, folded over (split, tap)), so dy is read once
         fused_bias = self.up.bias is not None and self.Cop == self.Co
-        part = self.rt.ws(max(ks * self.Ci * ncols + (ks * ncols if fused_bias else 0), 256 * self.Co))
+        # (the unfused bias sums reuse the partial buffer after the reduce: that reduce stays in line)
+        defer = (fused_bias or self.up.bias is None) and self.rt.defer_wred(self.flat)
+        nfl = max(ks * self.Ci * ncols + (ks * ncols if fused_bias else 0), 256 * self.Co)
+        part = _own_part(self, self.rt, nfl) if defer else self.rt.ws(nfl)
         bpart = part.data_ptr() + ks * self.Ci * ncols * 4 if fused_bias else None
         with TIMER.region(_gemm_name(self.rt, 0, "convT"), flops=2.0 * V * self.Ci * 8 * self.Co,
                           nbytes=_io_bytes(self.rt, V, self.Ci, 8 * self.Co, 8 * self.Ci * self.Co, 4)):
             L.mmseg_wgrad(x.ptr, x.ld, dy.ptr, dy.ld, ptr(part), bpart, MODE_CONVT_DGRAD, self.Ci, ncols,
                           self.dshift, V, x.D, x.H, x.W, ks, code, s)
-        L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.up.weight)), None, None, self.Ci, ncols, ks, self.Cop,
-                             self.Co, 8, int(accumulate), s)
+        (L.mmseg_wgrad_reduce_defer if defer else L.mmseg_wgrad_reduce)(
+            ptr(part), ptr(self.flat.grad(self.up.weight)), None, None, self.Ci, ncols, ks, self.Cop, self.Co, 8,
+            int(accumulate), s)
         if fused_bias:
             L.mmseg_colsum_reduce(bpart, 8 * ks, self.Co, ptr(self.flat.grad(self.up.bias)), int(accumulate), s)
         elif self.up.bias is not None:
@@ -540,13 +553,15 @@ class Point:
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
         V = x.N * x.V
         ks = L.mmseg_wgrad_splits(V, _wgrad_ksplit(self.Co, self.Ci, V))
-        part = self.rt.ws(ks * self.Co * self.Ci + ks * self.Co)
+        defer = self.rt.defer_wred(self.flat)
+        nfl = ks * self.Co * self.Ci + ks * self.Co
+        part = _own_part(self, self.rt, nfl) if defer else self.rt.ws(nfl)
         bpart = part.data_ptr() + ks * self.Co * self.Ci * 4
         L.mmseg_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, ptr(part), bpart, MODE_POINT, self.Co, self.Ci, 0, V, x.D, x.H, x.W,
                       ks, code, s)
-        L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.conv.weight)), bpart,
-                             ptr(self.flat.grad(self.conv.bias)), self.Co, self.Ci, ks, self.Ci, self.Ci, 1,
-                             int(accumulate), s)
+        (L.mmseg_wgrad_reduce_defer if defer else L.mmseg_wgrad_reduce)(
+            ptr(part), ptr(self.flat.grad(self.conv.weight)), bpart, ptr(self.flat.grad(self.conv.bias)), self.Co,
+            self.Ci, ks, self.Ci, self.Ci, 1, int(accumulate), s)
         self.flat.mark(self.conv.weight, self.conv.bias)
         if dx is not None:
             L.mmseg_conv_gemm(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, None, MODE_POINT, V, self.Ci,

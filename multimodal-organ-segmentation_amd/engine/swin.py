@@ -33,7 +33,7 @@ import torch.nn as nn
 
 from .._lib import ptr
 from .attention import WindowAttentionEngine
-from .layers import MODE_POINT, Conv3, ConvT2, Head, Packer, _col_tile, _gemm_ksplit, _wgrad_ksplit
+from .layers import MODE_POINT, Conv3, ConvT2, Head, Packer, _col_tile, _gemm_ksplit, _own_part, _wgrad_ksplit
 from .runtime import Act, FlatParams, Runtime, round_up
 
 LN_EPS = 1e-5
@@ -124,13 +124,15 @@ class Lin:
             lddx: int, accumulate: bool):
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
         ks = L.mmseg_wgrad_splits(M, _wgrad_ksplit(self.Co, self.Cip, M))
-        part = self.rt.ws(ks * self.Co * self.Cip + ks * self.Co + 4)
+        defer = self.rt.defer_wred(self.flat)
+        nfl = ks * self.Co * self.Cip + ks * self.Co + 4
+        part = _own_part(self, self.rt, nfl) if defer else self.rt.ws(nfl)
         bpart = part.data_ptr() + round_up(ks * self.Co * self.Cip, 4) * 4 if self.b is not None else None
         L.mmseg_wgrad(ptr(dy), lddy, ptr(x), ldx, ptr(part), bpart, MODE_POINT, self.Co, self.Cip, 0, M, 1, 1, 1, ks,
                       code, s)
-        L.mmseg_wgrad_reduce(ptr(part), ptr(self.flat.grad(self.w)), bpart,
-                             ptr(self.flat.grad(self.b)) if self.b is not None else None, self.Co, self.Cip, ks,
-                             self.Cip, self.Ci, 1, int(accumulate), s)
+        (L.mmseg_wgrad_reduce_defer if defer else L.mmseg_wgrad_reduce)(
+            ptr(part), ptr(self.flat.grad(self.w)), bpart, ptr(self.flat.grad(self.b)) if self.b is not None else None,
+            self.Co, self.Cip, ks, self.Cip, self.Ci, 1, int(accumulate), s)
         self.flat.mark(*[p for p in (self.w, self.b) if p is not None])
         if dx is not None:
             kd = _gemm_ksplit(M, self.Ci, self.KGd)
