@@ -233,9 +233,9 @@ __device__ __forceinline__ long long tap_offset(int t, const GemmArgs& g) {
     int dz, dy, dx;
     tap_delta(t, dz, dy, dx);
     return ((long long)dz * g.H + dy) * g.W + dx;
-  } else {
-    int a = t >> 2, b = (t >> 1) & 1, c = t & 1;
-    return ((long long)a * (2LL * g.H) + b) * (2LL * g.W) + c;
+  } else {   // 32-bit: the child grid's voxel count is < 2^31 (host: M * lda)
+    const int a = t >> 2, b = (t >> 1) & 1, c = t & 1;
+    return (long long)(a * (4 * g.H * g.W) + b * (2 * g.W) + c);
   }
 }
 
@@ -391,6 +391,43 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs g) {
     }
     return;
   }
+  if constexpr (MODE == MODE_CONVT_FWD) {
+    // a thread's 8-column group (tap t, channels co..co+7) is the same in every pass (256 % CG == 0) and its rows
+    // step by 256 / CG: the child voxel's coordinates are decomposed once and then stepped, instead of three
+    // runtime divisions per store (the epilogue was ~28 VALU per MFMA, r04i PMC)
+    static_assert(256 % CG == 0, "fixed column group per thread");
+    constexpr int LSTEP = 256 / CG;
+    const int cg = threadIdx.x % CG;
+    const int col = nt0 + cg * 8;
+    if (col >= g.Ncols) return;
+    const int t = col / Cout, co = col - t * Cout;
+    const int tz = t >> 2, ty = (t >> 1) & 1, tx = t & 1;
+    int lr = threadIdx.x / CG;
+    const unsigned mu = (unsigned)(mt0 + lr);
+    const unsigned q = mu / (unsigned)g.W, q2 = q / (unsigned)g.H;
+    int x = (int)(mu - q * (unsigned)g.W), y = (int)(q - q2 * (unsigned)g.H);
+    int n = (int)(q2 / (unsigned)g.D), z = (int)(q2 - (unsigned)n * (unsigned)g.D);
+    const long long W2 = 2LL * g.W, H2 = 2LL * g.H, D2 = 2LL * g.D;
+    for (; lr < BM; lr += LSTEP) {
+      if (mt0 + lr >= g.M) break;
+      V8<T> o;
+      o.load(El + lr * EPT + cg * 8);
+      const long long child = (((long long)n * D2 + 2 * z + tz) * H2 + 2 * y + ty) * W2 + 2 * x + tx;
+      o.store(O + child * g.ldo + co);
+      x += LSTEP;
+      while (x >= g.W) {
+        x -= g.W;
+        if (++y == g.H) {
+          y = 0;
+          if (++z == g.D) {
+            z = 0;
+            ++n;
+          }
+        }
+      }
+    }
+    return;
+  }
   for (int e = threadIdx.x; e < BM * CG; e += 256) {
     const int lr = e / CG, cg = e % CG;
     const long long row = mt0 + lr;
@@ -398,12 +435,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs g) {
     if (row >= g.M || col >= g.Ncols) continue;
     V8<T> o;
     o.load(El + lr * EPT + cg * 8);
-    if (MODE == MODE_CONVT_FWD) {
-      const int t = col / Cout, co = col - t * Cout;
-      o.store(O + convt_child(row, t, g) * g.ldo + co);
-    } else {
-      o.store(out_at<T>(g, row, col));
-    }
+    o.store(out_at<T>(g, row, col));
   }
 }
 
@@ -2511,20 +2543,46 @@ int launch_brick5(const GemmArgs& g, hipStream_t s, long long* dbg, bool dma) {
   return upb5;
 }
 
+// 4 consecutive columns per thread in gemm_splitk_reduce (for the transposed conv: 4 channels of one child voxel,
+// Cout % 4 == 0)
+template <int MODE>
+__host__ __device__ __forceinline__ bool splitk_vec(const GemmArgs& g) {
+  const bool al = (g.Ncols & 3) == 0 && (g.ldo & 3) == 0 && (reinterpret_cast<uintptr_t>(g.part) & 15) == 0;
+  return MODE == MODE_CONVT_FWD ? al && ((g.Ncols >> 3) & 3) == 0 : al;
+}
 template <int MODE>
 int splitk_reduce_blocks(const GemmArgs& g) {
   const long long total = (long long)g.M * g.Ncols;
-  const bool vec = MODE != MODE_CONVT_FWD && (g.Ncols & 3) == 0 && (g.ldo & 3) == 0 &&
-      (reinterpret_cast<uintptr_t>(g.part) & 15) == 0;
-  return ceil_div(vec ? (total + 3) / 4 : total, 256);
+  return ceil_div(splitk_vec<MODE>(g) ? (total + 3) / 4 : total, 256);
 }
 
 // Fixed-order split-K reduction for the forward GEMM: out = sum_k part[k] (+bias).
 template <typename T, int MODE>
 __global__ void gemm_splitk_reduce(GemmArgs g) {
   long long total = (long long)g.M * g.Ncols;
-  if (MODE != MODE_CONVT_FWD && (g.Ncols & 3) == 0 && (g.ldo & 3) == 0 &&
-      (reinterpret_cast<uintptr_t>(g.part) & 15) == 0) {
+  if (MODE == MODE_CONVT_FWD && splitk_vec<MODE>(g)) {
+    // 4 channels of one child voxel per thread: one child-index computation per 4 values (was one per value)
+    const long long idx4 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (idx4 >= total) return;
+    const long long row = idx4 / g.Ncols;
+    const int col = (int)(idx4 - row * g.Ncols);
+    const int Cout = g.Ncols >> 3, t = col / Cout, co = col - t * Cout;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4* p = reinterpret_cast<const float4*>(g.part + idx4);
+    const long long st = total / 4;
+#pragma unroll 4
+    for (int k = 0; k < g.ksplit; ++k) {
+      const float4 a = p[(long long)k * st];
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+    if (g.bias) {
+      v.x += g.bias[co]; v.y += g.bias[co + 1]; v.z += g.bias[co + 2]; v.w += g.bias[co + 3];
+    }
+    T* O = reinterpret_cast<T*>(g.out) + convt_child(row, t, g) * g.ldo + co;
+    O[0] = from_f<T>(v.x); O[1] = from_f<T>(v.y); O[2] = from_f<T>(v.z); O[3] = from_f<T>(v.w);
+    return;
+  }
+  if (MODE != MODE_CONVT_FWD && splitk_vec<MODE>(g)) {
     // 4 consecutive columns per thread: 16-B partial loads, 4 splits' loads in flight, fixed split order
     const long long idx4 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
     if (idx4 >= total) return;
@@ -2748,6 +2806,21 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs g) {
   float bsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
   V8<T> ra[A_PER], rb[B_PER];
+  // transposed conv: the thread's B voxels step by KV per stage, so their (n, z, y, x) are decomposed once and
+  // stepped (gather_src's three runtime divisions per load were ~29 VALU per MFMA, r04i PMC)
+  int cx[B_PER], cy[B_PER], cz[B_PER], cn[B_PER];
+  const int t_b = kgi_b >> g.cpg_shift, c8_b = kgi_b & ((1 << g.cpg_shift) - 1);
+  if constexpr (MODE == MODE_CONVT_DGRAD) {
+#pragma unroll
+    for (int k = 0; k < B_PER; ++k) {
+      const unsigned vu = (unsigned)(v_begin + (tid + k * 256) / BG);
+      const unsigned q = vu / (unsigned)g.W, q2 = q / (unsigned)g.H;
+      cn[k] = (int)(q2 / (unsigned)g.D);
+      cz[k] = (int)(q2 - (unsigned)cn[k] * (unsigned)g.D);
+      cy[k] = (int)(q - q2 * (unsigned)g.H);
+      cx[k] = (int)(vu - q * (unsigned)g.W);
+    }
+  }
   auto load_stage = [&](long long vb) {
 #pragma unroll
     for (int k = 0; k < A_PER; ++k) {
@@ -2760,11 +2833,30 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs g) {
     for (int k = 0; k < B_PER; ++k) {
       const int v = (tid + k * 256) / BG;
       const long long vox = vb + v;
-      long long src;
-      int c8;
-      const bool ok = vox < v_end && col_ok && gather_src<MODE>(vox, kgi_b, g.cpg_shift, g, src, c8);
-      if (ok) rb[k].load(B + src * g.ldb + c8 * 8);
-      else rb[k].zero();
+      if constexpr (MODE == MODE_CONVT_DGRAD) {
+        const unsigned src = (((unsigned)cn[k] * 2u * g.D + 2u * cz[k] + (t_b >> 2)) * 2u * g.H + 2u * cy[k] +
+                              ((t_b >> 1) & 1)) * 2u * g.W + 2u * cx[k] + (t_b & 1);
+        if (vox < v_end && col_ok) rb[k].load(B + (long long)src * g.ldb + c8_b * 8);
+        else rb[k].zero();
+        // step to the voxel KV further on (the next stage)
+        cx[k] += KV;
+        while (cx[k] >= g.W) {
+          cx[k] -= g.W;
+          if (++cy[k] == g.H) {
+            cy[k] = 0;
+            if (++cz[k] == g.D) {
+              cz[k] = 0;
+              ++cn[k];
+            }
+          }
+        }
+      } else {
+        long long src;
+        int c8;
+        const bool ok = vox < v_end && col_ok && gather_src<MODE>(vox, kgi_b, g.cpg_shift, g, src, c8);
+        if (ok) rb[k].load(B + src * g.ldb + c8 * 8);
+        else rb[k].zero();
+      }
     }
   };
   auto write_stage = [&](int buf) {
@@ -4669,8 +4761,7 @@ __global__ void pack_weight_batched_kernel(const PackDesc* __restrict__ descs, i
 template <typename T, int MODE>
 int launch_splitk_reduce(const GemmArgs& g, hipStream_t s) {
   const long long total = (long long)g.M * g.Ncols;
-  const bool vec = MODE != MODE_CONVT_FWD && (g.Ncols & 3) == 0 && (g.ldo & 3) == 0 &&
-                   (reinterpret_cast<uintptr_t>(g.part) & 15) == 0;
+  const bool vec = MODE != MODE_CONVT_FWD && splitk_vec<MODE>(g);   // (the sliced reduce: not the transposed conv)
   int S = 1;
   const int rpt = knob("MMSEG_SPLITK_RPT", 4);
   while (S < 16 && g.ksplit / (2 * S) >= rpt) S *= 2;
