@@ -13,4 +13,6 @@ P=profiles
 [ -f $O/pmc_sq.json ] && cp $O/pmc_sq.json $P/${T}_pmc_sq.json
 [ -f $O/timer.json ] && python3 tools/timer_dump.py $O/timer.json 40 > $P/${T}_timer.txt
 [ -f $O/gpu_tests.log ] && grep -E "passed|failed|PASSED|FAILED|pinned fp64|held-out|free-running|c5 96|fp8 vs|grouped|Error" $O/gpu_tests.log | cut -c1-400 > $P/${T}_gpu_tests.txt || true
+C=gpurun_out/${T}_cfg
+if [ -d $C ]; then for f in $C/c*.log; do n=$(basename $f .log); tail -1 $f > $P/${T}_config_$n.json; done; fi
 ls -la $P/${T}_*
