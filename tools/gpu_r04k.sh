@@ -12,3 +12,4 @@ tail -3 $O/tests.log
 timeout -k 10 600 python3 $R/bench.py --timer-dump $O/timer.json --no-cpu-baseline > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
 tail -1 $O/bench.log | cut -c1-200
 python3 $R/tools/timer_dump.py $O/timer.json 10 | head -45
+AB_STEPS=40 bash $R/tools/gpu_ab.sh r04k_ab - MMSEG_BRICKR_SLOTS=128 MMSEG_BRICKR_SLOTS=64 - MMSEG_BRICKR_SLOTS=128 MMSEG_BRICKR_SLOTS=64
