@@ -2838,12 +2838,15 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs g) {
                               ((t_b >> 1) & 1)) * 2u * g.W + 2u * cx[k] + (t_b & 1);
         if (vox < v_end && col_ok) rb[k].load(B + (long long)src * g.ldb + c8_b * 8);
         else rb[k].zero();
-        // step to the voxel KV further on (the next stage)
+        // step to the voxel KV further on (the next stage): one division for the x carry (KV may span several
+        // rows of a small grid), then y / z wrap at most a few times
         cx[k] += KV;
-        while (cx[k] >= g.W) {
-          cx[k] -= g.W;
-          if (++cy[k] == g.H) {
-            cy[k] = 0;
+        if (cx[k] >= g.W) {
+          const int qy = (int)((unsigned)cx[k] / (unsigned)g.W);
+          cx[k] -= qy * g.W;
+          cy[k] += qy;
+          while (cy[k] >= g.H) {
+            cy[k] -= g.H;
             if (++cz[k] == g.D) {
               cz[k] = 0;
               ++cn[k];
