@@ -197,8 +197,10 @@ def test_fullsize_step_pinned_to_fp64_oracle(dev, tag, dtype, group, monkeypatch
         # bf16: the 12^3 and 6^3 levels grouped over the modalities (the runtime-brick kernels are bf16-only, so
         # the fp32 parity mode keeps per-modality launches there)
         prog = m.backbone.__dict__["_engine"].program
-        want = prog.L if group == "0" or dtype != "bfloat16" else (2 if group == "force" else 3)
-        assert prog.l0 == want, prog.l0
+        if group == "force":            # 24^3 and (c3 features) 48^3 grouped as well
+            assert prog.l0 <= 2, prog.l0
+        else:
+            assert prog.l0 == (prog.L if group == "0" or dtype != "bfloat16" else 3), prog.l0
     pins = _engine_pins(m, model)
     pins.relu_masks = [r.to(dev) for r in pins.relu_masks]
     pins.pool_codes = [c.to(dev) for c in pins.pool_codes]
