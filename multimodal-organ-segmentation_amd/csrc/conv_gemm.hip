@@ -5677,21 +5677,22 @@ int mmseg_conv3_dgrad_in(const void* a, int lda, const void* wpacked, void* out,
 // split-K workspace, ksplit*M*Ncols floats, with it and pass it as ksplit).
 // 1 when mmseg_conv_gemm_group / mmseg_conv3_wgrad_group take this shape: the runtime-brick conv (plan kind 2)
 // and, for the weight gradient, the runtime-brick weight-gradient kernel (kind 3).
-// (a grouped launch takes the runtime-brick kernels; MMSEG_GROUP_FORCE_R=1 also groups shapes that would otherwise
-// take the (4, 8, 8)-brick family -- the 24^3 level)
+// (a grouped launch takes the runtime-brick kernels; MMSEG_GROUP_FORCE_R (default on) also groups shapes that would
+// otherwise take the (4, 8, 8)-brick family -- the 24^3 / 48^3 levels: one launch over both modalities on the
+// runtime-brick kernels beat two on the brick family there, r04j / r04l / r04n A/B -0.05..-0.07 ms per step)
 int mmseg_conv3_group_ok(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,
                          int dtype) {
   if (!knob("MMSEG_GROUP_SMALL", 1)) return 0;
   const int ts = dtype == MMSEG_BF16 ? 2 : 4;
   if (plan_conv3(M, Ncols, 8 << cpg_shift, D, H, W, lda, ldo, ts).kind == 2) return 1;
-  return knob("MMSEG_GROUP_FORCE_R", 0) && plan_conv3(M, Ncols, 8 << cpg_shift, D, H, W, lda, ldo, ts, true).kind == 2
+  return knob("MMSEG_GROUP_FORCE_R", 1) && plan_conv3(M, Ncols, 8 << cpg_shift, D, H, W, lda, ldo, ts, true).kind == 2
              ? 1 : 0;
 }
 int mmseg_conv3_wgrad_group_ok(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W, int lddy,
                                int ldx, int dtype) {
   if (!knob("MMSEG_GROUP_SMALL", 1)) return 0;
   if (plan_conv3_wgrad(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype, 1LL << 40).kind == 3) return 1;
-  return knob("MMSEG_GROUP_FORCE_R", 0) &&
+  return knob("MMSEG_GROUP_FORCE_R", 1) &&
                  plan_conv3_wgrad(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype, 1LL << 40, true).kind == 3
              ? 1 : 0;
 }

@@ -861,9 +861,9 @@ class GroupBlock(Block):
             b.nb, b.norm1_ok, b.defer1, b.defer_out = (0, 0), False, False, False
 
     def ok(self, xin: Act) -> bool:
-        # levels above the one-launch InstanceNorm size group only with MMSEG_GROUP_FORCE_R (the 24^3 level on the
-        # runtime-brick kernels; the InstanceNorm passes take the multi-pass path over the M x N samples)
-        small = self.x1.V <= SMALL_IN_V or os.environ.get("MMSEG_GROUP_FORCE_R", "0") == "1"
+        # levels above the one-launch InstanceNorm size group with MMSEG_GROUP_FORCE_R (default on: the 24^3 / 48^3
+        # levels on the runtime-brick kernels; the InstanceNorm passes take the multi-pass path over M x N samples)
+        small = self.x1.V <= SMALL_IN_V or os.environ.get("MMSEG_GROUP_FORCE_R", "1") != "0"
         return self.g1.ok(xin, self.x1) and self.g2.ok(self.x1, self.x2) and small
 
     def fwd(self, xin: Act, out: Act):

@@ -167,7 +167,7 @@ def _oracle_fwd(kind, mods):
                                              ("fullgrad_unet_c2", "float32", "1"), ("fullgrad_dual_m3_c5", "float32", "1"),
                                              ("fullgrad_dual_m3_c5", "bfloat16", "1"),
                                              ("fullgrad_dual_c3", "bfloat16", "0"),
-                                             ("fullgrad_dual_c3", "bfloat16", "force")])
+                                             ("fullgrad_dual_c3", "bfloat16", "noforce")])
 def test_fullsize_step_pinned_to_fp64_oracle(dev, tag, dtype, group, monkeypatch):
     """The benched step at full size (96^3, B=2; trainer.py:250-254) against oracle/mmseg_oracle.py evaluated in
     fp64 ON THE GPU (torch ops) with the engine's own ReLU masks and MaxPool argmax codes (oracle.Pins, as
@@ -177,10 +177,10 @@ def test_fullsize_step_pinned_to_fp64_oracle(dev, tag, dtype, group, monkeypatch
     so EVERY parameter gradient is held to PINNED_TOL (fp32: 1e-4), including the ConvTranspose biases; the conv
     biases in front of an InstanceNorm (true gradient 0) to PINNED_DEAD of the largest gradient."""
     from tests.test_model_gpu import _engine_pins
-    # "1": the modality-grouped 12^3 / 6^3 levels (default); "force": the 24^3 level grouped too, on the runtime-brick
-    # kernels (MMSEG_GROUP_FORCE_R) -- other kernels than the per-modality step, so it is held to the oracle here
+    # "1" (default): the modality-grouped levels -- 12^3 / 6^3, and with MMSEG_GROUP_FORCE_R (default on) 24^3 / 48^3
+    # on the runtime-brick kernels; "noforce": only 12^3 / 6^3; "0": every level per modality
     monkeypatch.setenv("MMSEG_GROUP_SMALL", "0" if group == "0" else "1")
-    monkeypatch.setenv("MMSEG_GROUP_FORCE_R", "1" if group == "force" else "0")
+    monkeypatch.setenv("MMSEG_GROUP_FORCE_R", "0" if group == "noforce" else "1")
     g = golden(tag)
     model, mods, loss = CASES[tag]
     S, B, seed, C = int(g["S"]), int(g["B"]), int(g["seed"]), 6
@@ -197,10 +197,12 @@ def test_fullsize_step_pinned_to_fp64_oracle(dev, tag, dtype, group, monkeypatch
         # bf16: the 12^3 and 6^3 levels grouped over the modalities (the runtime-brick kernels are bf16-only, so
         # the fp32 parity mode keeps per-modality launches there)
         prog = m.backbone.__dict__["_engine"].program
-        if group == "force":            # 24^3 and (c3 features) 48^3 grouped as well
+        if group == "0" or dtype != "bfloat16":
+            assert prog.l0 == prog.L, prog.l0
+        elif group == "noforce":
+            assert prog.l0 == 3, prog.l0
+        else:                           # 24^3 and (c3 / c5 features) 48^3 grouped as well
             assert prog.l0 <= 2, prog.l0
-        else:
-            assert prog.l0 == (prog.L if group == "0" or dtype != "bfloat16" else 3), prog.l0
     pins = _engine_pins(m, model)
     pins.relu_masks = [r.to(dev) for r in pins.relu_masks]
     pins.pool_codes = [c.to(dev) for c in pins.pool_codes]
