@@ -4805,6 +4805,8 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     g.ksplit = (nchunk + cps - 1) / cps;
     const dim3 grid(nb * ((g.Ncols + plan.bn - 1) / plan.bn) * g.ksplit);
     const bool b666 = plan.bz == 6 && plan.by == 6 && plan.bx == 6 && knob("MMSEG_BRICKR_CT", 1);
+    // 4 x 8 x 8: the grouped 48^3 / 24^3 levels (MMSEG_GROUP_FORCE_R), compile-time as 6 x 6 x 6
+    const bool b488 = plan.bz == 4 && plan.by == 8 && plan.bx == 8 && knob("MMSEG_BRICKR_CT488", 1);
     // 32-bit offset halo staging (bf16 only, as conv3_brick2_kernel's B32)
     const bool rb32 = (sizeof(T) == 2 || knob("MMSEG_B32_F32", 0)) && knob("MMSEG_BRICKR_B32", 1) &&
                       (long long)g.M * g.lda * (long long)sizeof(T) < (1LL << 31);
@@ -4862,6 +4864,10 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
           MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 0, false, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
         else if (b666)
           MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
+        else if (b488 && rb32)
+          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 4, 8, 8, 0, false, true>), grid, block, 0, s, g, 4, 8, 8, (long long*)nullptr);
+        else if (b488)
+          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 4, 8, 8>), grid, block, 0, s, g, 4, 8, 8, (long long*)nullptr);
         else if (knob("MMSEG_BRICKR_PF", 0))
           MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 0, 0, 0, 0, true>), grid, block, 0, s, g, plan.bz, plan.by,
                              plan.bx, (long long*)nullptr);
@@ -4877,6 +4883,12 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
         MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, false, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
       else
         MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
+    } else if (b488) {
+      mmseg::note_kernel("conv3_brickr_kernel<BN32>");
+      if (rb32)
+        MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 4, 8, 8, 0, false, true>), grid, block, 0, s, g, 4, 8, 8, (long long*)nullptr);
+      else
+        MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 4, 8, 8>), grid, block, 0, s, g, 4, 8, 8, (long long*)nullptr);
     } else {
       mmseg::note_kernel("conv3_brickr_kernel<BN32>");
       if (rb32)
@@ -5112,11 +5124,14 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
     if (MODE == MODE_CONV3 && g.brick == 3) {
       const WBrick wb = plan_wgrad_brickr(g.D, g.H, g.W);
       const bool b366 = wb.bz == 3 && wb.by == 6 && wb.bx == 6 && knob("MMSEG_BRICKR_CT", 1);
+      const bool b448 = wb.bz == 4 && wb.by == 4 && wb.bx == 8 && knob("MMSEG_BRICKR_CT488", 1);   // grouped 48^3 / 24^3
       if (wgrad_co64(g.Ca, g.V, 3)) {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 64) * g.ksplit);
         mmseg::note_kernel("wgrad_brickr_kernel<CO64>");
         if (b366)
           MMSEG_LAUNCH((wgrad_brickr_kernel<T, 4, 3, 6, 6>), grid, dim3(512), 0, s, g, 3, 6, 6);
+        else if (b448)
+          MMSEG_LAUNCH((wgrad_brickr_kernel<T, 4, 4, 4, 8>), grid, dim3(512), 0, s, g, 4, 4, 8);
         else
           MMSEG_LAUNCH((wgrad_brickr_kernel<T, 4>), grid, dim3(512), 0, s, g, wb.bz, wb.by, wb.bx);
       } else {
@@ -5124,6 +5139,8 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
         mmseg::note_kernel("wgrad_brickr_kernel<CO32>");
         if (b366)
           MMSEG_LAUNCH((wgrad_brickr_kernel<T, 2, 3, 6, 6>), grid, dim3(512), 0, s, g, 3, 6, 6);
+        else if (b448)
+          MMSEG_LAUNCH((wgrad_brickr_kernel<T, 2, 4, 4, 8>), grid, dim3(512), 0, s, g, 4, 4, 8);
         else
           MMSEG_LAUNCH((wgrad_brickr_kernel<T, 2>), grid, dim3(512), 0, s, g, wb.bz, wb.by, wb.bx);
       }

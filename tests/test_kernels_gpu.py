@@ -105,6 +105,9 @@ def test_conv3_kernel_variants(dev, dtype, knobs, cin, cout, shape, monkeypatch)
     (64, 64, (1, 12, 8, 24), {"MMSEG_BRICK2_MINBLK": "0"}, "conv3_brick2_kernel<BN64,ZW1>"),  # border bricks
     (256, 128, (2, 12, 12, 12), {}, "conv3_brickr_kernel"),        # runtime brick (3,6,12), split-K
     (512, 256, (1, 6, 6, 6), {}, "conv3_brickr_kernel"),           # compile-time 6x6x6 brick, 16 chunks
+    # compile-time 4x8x8 brick (the grouped 48^3 / 24^3 levels); MMSEG_BRICK=3 skips the brick2 family
+    (128, 64, (2, 8, 16, 16), {"MMSEG_BRICK": "3"}, "conv3_brickr_kernel"),   # BN64 in bf16
+    (64, 32, (1, 8, 16, 24), {"MMSEG_BRICK": "3"}, "conv3_brickr_kernel<BN32>"),
 ])
 def test_b32_halo_staging(dev, dtype, cin, cout, shape, extra, kernel, monkeypatch):
     """The 32-bit-offset halo staging (MMSEG_BRICK2_B32 / MMSEG_BRICKR_B32: buffer loads whose out-of-volume lanes
