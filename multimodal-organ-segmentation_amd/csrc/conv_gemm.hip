@@ -2462,6 +2462,10 @@ Conv3Plan plan_conv3(int M, int Ncols, int cin, int D, int H, int W, int lda, in
       const int nchunk = cin / CK;
       const int slots = knob("MMSEG_BRICKR_SLOTS", 256);   // 512 measured 2-10 % slower at 12^3 / 6^3 (r02)
       int ks = (slots + nb * nt - 1) / (nb * nt);
+      // at least this many (brick, column-tile) blocks: no chunk split (24^3 grouped data gradient, 216 blocks:
+      // 42.8 us split in two against 35.3 us whole, r04p)
+      const int nosplit = knob("MMSEG_BRICKR_NOSPLIT", 0);
+      if (nosplit > 0 && nb * nt >= nosplit) ks = 1;
       if (ks > nchunk) ks = nchunk;
       if (ks < 1) ks = 1;
       const int cps = (nchunk + ks - 1) / ks;
@@ -5321,6 +5325,8 @@ Conv3WgradPlan plan_conv3_wgrad(long long V, int Co, int Cip, int Ci, int cpg_sh
   const long long per_split = (long long)Co * ncols + Co;
   int cap = (int)(ws_cap / per_split);
   if (cap < 1) cap = 1;
+  // MMSEG_WGRAD_FORCE_R=1: the runtime-brick weight gradient for ungrouped launches too (microbenchmarks)
+  if (knob("MMSEG_WGRAD_FORCE_R", 0)) force_r = true;
   p.kind = wgrad_brick_ok(Co, cpg_shift, D, H, W, lda, ldb, dtype, force_r);
   if (p.kind) {
     p.ksplit = brick_wgrad_splits(V, cap, Co, cpg_shift, p.kind, D, H, W, wgrad_kchunks(Cip, Ci));
@@ -5358,6 +5364,20 @@ struct PendingWred {
   void* stream;
 };
 std::vector<PendingWred> g_wred_pending;
+extern "C" int mmseg_wgrad_reduce_flush(void* stream);
+
+// Queue a deferred reduce; once the partials queued on its stream pass MMSEG_WRED_FLUSH_MB (0: never), flush them
+// there and then, while they may still sit in the Infinity Cache (the whole step's partials do not).
+int wred_push(const WReduceArgs& r, int groups, void* stream) {
+  g_wred_pending.push_back({r, groups, stream});
+  const long long cap = (long long)knob("MMSEG_WRED_FLUSH_MB", 0) << 20;
+  if (cap <= 0) return 0;
+  long long bytes = 0;
+  for (const auto& e : g_wred_pending)
+    if (e.stream == stream)
+      bytes += 4LL * e.r.ksplit * e.groups * ((long long)e.r.Ca * e.r.Ncols + (e.r.bias_part ? e.r.Ca : 0));
+  return bytes >= cap && mmseg_wgrad_reduce_flush(stream) < 0 ? -1 : 0;
+}
 
 int launch_wgrad_reduce(WReduceArgs g, void* stream, int groups = 1) {
   const long long total = (long long)g.Ca * g.Ncols + (g.bias_part ? g.Ca : 0);
@@ -5796,8 +5816,7 @@ int mmseg_wgrad_reduce_defer(const float* part, float* grad, const float* bias_p
   MMSEG_REQUIRE(((long long)Ca * Ncols) % 4 == 0 && (reinterpret_cast<uintptr_t>(part) & 15) == 0,
                 "wgrad_reduce: Ca*Ncols %% 4 == 0 and a 16-B aligned partial buffer");
   WReduceArgs g{part, grad, bias_part, bias_grad, Ca, Ncols, ksplit, cpad, creal, ntap, accumulate, 0};
-  g_wred_pending.push_back({g, 1, stream});
-  return 0;
+  return wred_push(g, 1, stream);
 }
 
 // Weight (+ bias) gradient of a 3^3 conv straight into the torch-layout fp32 gradient
@@ -5979,8 +5998,7 @@ int conv3_wgrad_impl(const void* dy, int lddy, const void* x, int ldx, const flo
   WReduceArgs r{part, grad, bpart, bias_grad, Co, ncols, p.ksplit / ng, Cip, Ci, 27, accumulate, p.kind >= 2 ? 1 : 0,
                 fmt, wgrad_nchunk(cpg_shift, g.kchunks), grad_gstride, bias_gstride};
   if (phase & 4) {   // deferred: summed by the next mmseg_wgrad_reduce_flush on this stream
-    g_wred_pending.push_back({r, ng, stream});
-    return 0;
+    return wred_push(r, ng, stream);
   }
   return launch_wgrad_reduce(r, stream, ng);
 }

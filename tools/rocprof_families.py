@@ -48,7 +48,8 @@ def family(name: str) -> str:
         return f"conv3_brick3_kernel<BN{m.group(1)}>[{dt}]"
     m = re.search(r"wgrad_brick([2r])_kernelI(?:DF16b|f)Li(\d+)E(?:Li(\d)E)?", name)
     if m:
-        v3 = ",V3" if m.group(3) == "3" else ""
+        # compile-time bricks of the runtime-brick kernel: 3x6x6 (12^3 / 6^3, "V3"), 4x4x8 (grouped 48^3 / 24^3)
+        v3 = {"3": ",V3", "4": ",B448"}.get(m.group(3), "")
         return f"wgrad_brick{m.group(1)}_kernel<CO{int(m.group(2)) * 16}{v3}>[{dt}]"
     m = re.search(r"wgrad_dma_kernelILi(\d+)E|wgrad_dma_kernel<(\d+)", name)
     if m:
