@@ -2458,6 +2458,10 @@ Conv3Plan plan_conv3(int M, int Ncols, int cin, int D, int H, int W, int lda, in
       p.kind = 2;
       p.bn = (tsize == 2 && Ncols % 64 == 0) ? 64 : 32;
       const int nb = (M / (D * H * W)) * (D / p.bz) * (H / p.by) * (W / p.bx);
+      // 32-column tiles where 64-column ones leave fewer than MMSEG_BRICKR_BN32_BLK blocks: twice the blocks
+      // instead of a chunk split (no fp32 partials, no reduce launch); 12^3 / 6^3 grouped: 2-8 us per launch
+      // (r04v convbench), -0.02 ms per step
+      if (p.bn == 64 && nb * (Ncols / 64) < knob("MMSEG_BRICKR_BN32_BLK", 256)) p.bn = 32;
       const int nt = (Ncols + p.bn - 1) / p.bn;
       const int nchunk = cin / CK;
       const int slots = knob("MMSEG_BRICKR_SLOTS", 256);   // 512 measured 2-10 % slower at 12^3 / 6^3 (r02)

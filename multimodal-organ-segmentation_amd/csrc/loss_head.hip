@@ -704,7 +704,26 @@ __device__ __forceinline__ f32x4 head_logits_t(const float* wA, const float* xs,
   return acc;
 }
 
-template <typename T, int G, typename LT>
+// BFL (bf16 storage, no Dropout3d scale): the same logits from two bf16 MFMAs (K = 32 = the lane's 8 channels x
+// 4 lane groups, the load layout as is), W split into bf16 hi + lo parts: x is exact in bf16 and the products
+// are exact, so the logits keep ~2^-17 of W (fp32 accumulation in another order) -- 32 MFMA cycles per 16
+// voxels instead of 256 for the eight fp32 16x16x4 steps.
+__device__ __forceinline__ void head_w_split(const float* wA, bf16x8& wh, bf16x8& wl) {
+#pragma unroll
+  for (int kb = 0; kb < 8; ++kb) {
+    const bf16_t h = (bf16_t)wA[kb];
+    wh[kb] = h;
+    wl[kb] = (bf16_t)(wA[kb] - (float)h);
+  }
+}
+__device__ __forceinline__ f32x4 head_logits_bf(const bf16x8& wh, const bf16x8& wl, const bf16x8& xa,
+                                                const float* bz) {
+  f32x4 acc = {bz[0], bz[1], bz[2], bz[3]};
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xa, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, xa, acc, 0, 0, 0);
+}
+
+template <typename T, int G, typename LT, bool BFL = false>
 __global__ __launch_bounds__(256) void head_loss_stats_kernel(const T* __restrict__ x, int ldx,
                                                               const float* __restrict__ nmean,
                                                               const float* __restrict__ nrstd,
@@ -727,6 +746,8 @@ __global__ __launch_bounds__(256) void head_loss_stats_kernel(const T* __restric
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) bz[r] = 4 * g + r < C ? bias[4 * g + r] : 0.f;
+  bf16x8 wAh, wAl;
+  if constexpr (BFL) head_w_split(wA, wAh, wAl);
   float P[4], I[4], Tc[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) P[r] = I[r] = Tc[r] = 0.f;
@@ -755,10 +776,15 @@ __global__ __launch_bounds__(256) void head_loss_stats_kernel(const T* __restric
     const bool ok = v < v1;
     const HeadLoad<T, G>& ld = lds_[u];
     const int y = ys_[u];
-    float xs[8];
+    f32x4 acc;
+    if constexpr (BFL) {
+      acc = head_logits_bf(wAh, wAl, ld.a.v, bz);
+    } else {
+      float xs[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) xs[j] = dscale ? ld.a.get(j) * sc[j] : ld.a.get(j);
-    const f32x4 acc = head_logits_t<G>(wA, xs, bz);
+      for (int j = 0; j < 8; ++j) xs[j] = dscale ? ld.a.get(j) * sc[j] : ld.a.get(j);
+      acc = head_logits_t<G>(wA, xs, bz);
+    }
     float z[4], e[4];
     float mx = -INFINITY;
 #pragma unroll
@@ -848,7 +874,7 @@ __global__ __launch_bounds__(256) void head_loss_stats_kernel(const T* __restric
 }
 
 // wpart: per block [C*Cin + C] weight / bias gradient partials (head_wgrad_reduce sums them over the blocks)
-template <typename T, int G, int NC, typename LT, bool DS>
+template <typename T, int G, int NC, typename LT, bool DS, bool BFL = false>
 __global__ __launch_bounds__(256, (NC <= 6 && sizeof(T) == 2) ? 2 : 1) void head_loss_bwd_kernel(const T* __restrict__ x, int ldx,
                                                             const float* __restrict__ nmean,
                                                             const float* __restrict__ nrstd,
@@ -880,6 +906,8 @@ __global__ __launch_bounds__(256, (NC <= 6 && sizeof(T) == 2) ? 2 : 1) void head
     wA[kb] = (v16 < C && g < G) ? Wt[v16 * Cin + 8 * g + kb] : 0.f;
     sc[kb] = (dscale && g < G) ? dscale[n * Cin + 8 * g + kb] : 1.f;
   }
+  bf16x8 wAh, wAl;
+  if constexpr (BFL) head_w_split(wA, wAh, wAl);
   const float* cf = coef + (long long)n * C * 2;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -939,7 +967,9 @@ __global__ __launch_bounds__(256, (NC <= 6 && sizeof(T) == 2) ? 2 : 1) void head
     float xs[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) xs[j] = dscale ? ld.a.get(j) * sc[j] : ld.a.get(j);
-    const f32x4 acc_l = head_logits_t<G>(wA, xs, bz);
+    f32x4 acc_l;
+    if constexpr (BFL) acc_l = head_logits_bf(wAh, wAl, ld.a.v, bz);
+    else acc_l = head_logits_t<G>(wA, xs, bz);
     float z[4], p[4];
     float mx = -INFINITY;
 #pragma unroll
@@ -1246,6 +1276,13 @@ int grid_for(long long total) {
   return (int)b;
 }
 
+// MMSEG_HEAD_BF16 (default 1): the fused head + loss kernels' logits from bf16 hi + lo MFMAs (head_logits_bf);
+// read per call, so A/B runs and tests can flip it in-process
+bool head_bf16() {
+  const char* e = getenv("MMSEG_HEAD_BF16");
+  return e ? atoi(e) != 0 : true;
+}
+
 int loss_vpc() {
   static const int v = [] {
     // 1,728 voxels: 1,024 blocks at 96^3 B=2, one full round of the fused statistics kernel (118 VGPRs: 4 blocks
@@ -1476,8 +1513,12 @@ int mmseg_head_loss_fwd(const void* x, int ldx, int Cin, const float* nmean, con
     constexpr int G = decltype(g_c)::value, NC = decltype(nc_c)::value;
     (void)NC;                 // the statistics kernel does not depend on NC: one instance per (T, G, LT)
     mmseg::note_kernel("head_loss_stats_kernel");
-    MMSEG_LAUNCH((head_loss_stats_kernel<T, G, LT>), dim3(nch, N), dim3(256), 0, s, (const T*)x, ldx, nmean,
-                       nrstd, W, b, dscale, C, (const LT*)labels, V, vpc, cfg, part);
+    if (sizeof(T) == 2 && !dscale && head_bf16())
+      MMSEG_LAUNCH((head_loss_stats_kernel<T, G, LT, sizeof(T) == 2>), dim3(nch, N), dim3(256), 0, s, (const T*)x,
+                   ldx, nmean, nrstd, W, b, dscale, C, (const LT*)labels, V, vpc, cfg, part);
+    else
+      MMSEG_LAUNCH((head_loss_stats_kernel<T, G, LT>), dim3(nch, N), dim3(256), 0, s, (const T*)x, ldx, nmean,
+                   nrstd, W, b, dscale, C, (const LT*)labels, V, vpc, cfg, part);
   });
   if (mmseg::check_launch("head_loss_stats")) return 1;
   const size_t shm = sizeof(double) * ((size_t)N * (3 * C + 3) + (size_t)N * C);
@@ -1540,6 +1581,10 @@ int mmseg_head_loss_bwd_in(const void* x, int ldx, int Cin, const float* nmean, 
       MMSEG_LAUNCH((head_loss_bwd_kernel<T, G, NC, LT, true>), dim3(nch, N), dim3(256), 0, s, (const T*)x, ldx,
                          nmean, nrstd, W, b, dscale, C, (const LT*)labels, V, vpc, cfg, coef, gout, gconst, (T*)dx,
                          lddx, wpart, inpart);
+    else if (sizeof(T) == 2 && head_bf16())   // the statistics pass's logits (same switch)
+      MMSEG_LAUNCH((head_loss_bwd_kernel<T, G, NC, LT, false, sizeof(T) == 2>), dim3(nch, N), dim3(256), 0, s,
+                   (const T*)x, ldx, nmean, nrstd, W, b, dscale, C, (const LT*)labels, V, vpc, cfg, coef, gout,
+                   gconst, (T*)dx, lddx, wpart, inpart);
     else
       MMSEG_LAUNCH((head_loss_bwd_kernel<T, G, NC, LT, false>), dim3(nch, N), dim3(256), 0, s, (const T*)x,
                          ldx, nmean, nrstd, W, b, dscale, C, (const LT*)labels, V, vpc, cfg, coef, gout, gconst,

@@ -404,16 +404,18 @@ def test_focal_ignores_minus_100(dev):
             assert rel(x.grad.cpu(), ref_in.grad) < 1e-5
 
 
+@pytest.mark.parametrize("dropout", [0.3, 0.0])
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
 @pytest.mark.parametrize("tag", ["unet_tiny", "dual_tiny_cross_attention"])
-def test_fused_head_loss_matches_unfused(dev, tag, dtype):
+def test_fused_head_loss_matches_unfused(dev, tag, dtype, dropout):
     """Trainer's fused head + loss node (engine.run_engine_loss: no logits / dlogits tensors, logits recomputed
-    in the backward) against model(x) -> criterion -> backward, for every HIP loss, class weights, uint8 labels
-    and an active Dropout3d (same device RNG state for both runs)."""
+    in the backward) against model(x) -> criterion -> backward, for every HIP loss, class weights, uint8 labels,
+    with an active Dropout3d (same device RNG state for both runs) and without one -- in bf16 the fused kernels'
+    logits then come from the bf16 hi + lo MFMAs (MMSEG_HEAD_BF16, loss_head.hip head_logits_bf)."""
     from mmseg_amd.engine.engine import fused_loss_supported, run_engine_loss
     from mmseg_amd.trainer.losses import CrossEntropyLoss, DiceCELoss, DiceLoss, FocalLoss, TverskyLoss
     cfg, m, g, M, C = _build(tag, dtype)
-    m.backbone.dropout_p = 0.3
+    m.backbone.dropout_p = dropout
     m.train()
     xs, ys = _inputs(g, M, C)
     x, y = xs[0].to(dev), ys[0].to(dev)
@@ -446,6 +448,37 @@ def test_fused_head_loss_matches_unfused(dev, tag, dtype):
             assert abs(lu - lf) <= 1e-5 * max(1.0, abs(lu)), (name, lu, lf)
             for a, b in zip(gf, gu):
                 assert ((a - b).norm() / b.norm()).item() < tol, (name, dtype)
+
+
+@pytest.mark.parametrize("tag", ["unet_tiny", "dual_tiny_cross_attention"])
+def test_head_bf16_logits_match_fp32_logits(dev, tag, monkeypatch):
+    """bf16 storage, no Dropout3d: the fused head + loss kernels' logits from bf16 hi + lo MFMAs (x exact in bf16,
+    W to ~2^-17) against the exact fp32 MFMA chain (MMSEG_HEAD_BF16=0): loss to 1e-5, gradients to the bf16
+    fused-vs-unfused bound (2e-2: a logit change of ~1e-6 can move a bf16 rounding downstream)."""
+    from mmseg_amd.engine.engine import fused_loss_supported, run_engine_loss
+    from mmseg_amd.trainer.losses import DiceCELoss, TverskyLoss
+    cfg, m, g, M, C = _build(tag, "bfloat16")
+    m.backbone.dropout_p = 0.0
+    m.train()
+    xs, ys = _inputs(g, M, C)
+    x, y = xs[0].to(dev), ys[0].to(dev)
+    kind = "unet" if tag == "unet_tiny" else "dual_encoder"
+    assert fused_loss_supported(m.backbone, kind, x)
+    for crit in (DiceCELoss(), TverskyLoss(0.3, 0.7)):
+        res = []
+        for bf in ("0", "1"):
+            monkeypatch.setenv("MMSEG_HEAD_BF16", bf)
+            m.zero_grad(set_to_none=True)
+            loss = run_engine_loss(m.backbone, kind, x, y, crit._spec(), None)
+            loss.backward()
+            torch.cuda.synchronize()
+            res.append((loss.item(), [p.grad.detach().double().cpu().clone() for n, p in m.named_parameters()
+                                      if not n.endswith("bias") or "out_conv" in n]))
+        (l0, g0), (l1, g1) = res
+        assert abs(l0 - l1) <= 1e-5 * max(1.0, abs(l0)), (l0, l1)
+        worst = max(((a - b).norm() / max(b.norm(), 1e-30)).item() for a, b in zip(g1, g0))
+        print(f"{tag} {type(crit).__name__}: loss {l0:.7f} vs {l1:.7f}, worst gradient rel {worst:.2e}")
+        assert worst < 2e-2
 
 
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
