@@ -908,6 +908,24 @@ __global__ __launch_bounds__(256, (NC <= 6 && sizeof(T) == 2) ? 2 : 1) void head
   }
   bf16x8 wAh, wAl;
   if constexpr (BFL) head_w_split(wA, wAh, wAl);
+  // BFL, PERM: dx^T from bf16 MFMAs too.  Lane group g's k-slots 0..3 carry classes 4g..4g+3 (hi parts of dlogits),
+  // slots 4..7 the same classes' lo parts; A = (W hi, W hi) then (W lo, W lo): two 16x16x32 MFMAs per 16-channel
+  // tile give (Whi + Wlo)(dhi + dlo) with exact products and fp32 sums -- instead of four fp32 16x16x4 steps
+  bf16x8 wDh[TN], wDl[TN];
+  if constexpr (BFL && PERM) {
+#pragma unroll
+    for (int t = 0; t < TN; ++t)
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const int ci = dx_chan(t, v16), c = 4 * g + kb;
+        const float w = (ci < Cin && c < C) ? Wt[c * Cin + ci] : 0.f;
+        const bf16_t h = (bf16_t)w, l = (bf16_t)(w - (float)h);
+        wDh[t][kb] = h;
+        wDh[t][kb + 4] = h;
+        wDl[t][kb] = l;
+        wDl[t][kb + 4] = l;
+      }
+  }
   const float* cf = coef + (long long)n * C * 2;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -1021,11 +1039,25 @@ __global__ __launch_bounds__(256, (NC <= 6 && sizeof(T) == 2) ? 2 : 1) void head
     // dx^T = W^T dlogits^T (exact fp32 MFMA), 4 channels of voxel v per lane and 16-channel tile
     if constexpr (PERM) {
       V8<T> dv;
+      bf16x8 db;
+      if constexpr (BFL) {
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+          const bf16_t h = (bf16_t)d[kb];
+          db[kb] = h;
+          db[kb + 4] = (bf16_t)(d[kb] - (float)h);
+        }
+      }
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         f32x4 o = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (BFL) {
+          o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wDh[t], db, o, 0, 0, 0);
+          o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wDl[t], db, o, 0, 0, 0);
+        } else {
 #pragma unroll
-        for (int kb = 0; kb < 4; ++kb) o = __builtin_amdgcn_mfma_f32_16x16x4f32(wD[t][kb], d[kb], o, 0, 0, 0);
+          for (int kb = 0; kb < 4; ++kb) o = __builtin_amdgcn_mfma_f32_16x16x4f32(wD[t][kb], d[kb], o, 0, 0, 0);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) dv.set(4 * t + r, dscale ? o[r] * sd[t][r] : o[r]);
       }
