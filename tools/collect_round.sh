@@ -6,6 +6,8 @@ T=$1
 O=gpurun_out/$T
 P=profiles
 [ -f $O/bench.log ] && tail -1 $O/bench.log > $P/${T}_bench.json
+# (gpu_round.sh's last bench run reads the call's own trace / counter summaries: the judged line)
+[ -f $O/bench_final.log ] && tail -1 $O/bench_final.log > $P/${T}_bench.json
 [ -f $O/families.txt ] && cp $O/families.txt $P/${T}_families.txt
 [ -f $O/trace/prof_kernel_stats.csv ] && cp $O/trace/prof_kernel_stats.csv $P/${T}_kernel_stats.csv
 [ -f $O/steady.json ] && cp $O/steady.json $P/${T}_steady.json && cp $O/families_steady.txt $P/${T}_families_steady.txt

@@ -25,4 +25,9 @@ python3 $R/tools/rocprof_families.py sq $O/pmc_sq/pmc_counter_collection.csv $O/
 python3 $R/tools/rocprof_families.py stats $O/trace/prof_kernel_stats.csv 16 > $O/families.txt
 python3 $R/tools/rocprof_families.py steady $O/trace/prof_kernel_trace.csv $O/steady.json 8 > $O/families_steady.txt
 python3 $R/tools/rocprof_families.py traffic $O/pmc_fetch/pmc_counter_collection.csv $O/pmc_write/pmc_counter_collection.csv $O/pmc_traffic.json 4 > /dev/null
+# the bench line again, now reading THIS call's trace / counter summaries (the names collect_round.sh gives them
+# under profiles/), so its rocprof_* / traffic / mfma_busy fields come from the same tree and box
+cp $O/steady.json $R/profiles/${TAG}_steady.json && cp $O/pmc_traffic.json $R/profiles/${TAG}_pmc_traffic.json && cp $O/pmc_sq.json $R/profiles/${TAG}_pmc_sq.json
+timeout -k 10 600 python3 $R/bench.py > $O/bench_final.log 2>&1 || { echo "final bench failed"; tail -20 $O/bench_final.log; exit 1; }
+tail -1 $O/bench_final.log
 echo done
