@@ -1764,7 +1764,24 @@ __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int up
   const int n0 = nt * 32;
   const int u_begin = blk * upb;
   const int u_end = u_begin + upb < nbrick ? u_begin + upb : nbrick;
-  if (u_begin >= u_end || n0 >= g.Ncols) return;
+  // INP: zero partials for the samples outside the block's unit range [n_lo, n_hi] (the consumer sums every
+  // block's slot of every sample; this replaces a memset of the whole partial buffer before the launch)
+  auto inp_zero = [&](int n_lo, int n_hi) {
+    if constexpr (INP) {
+      const int nsamp = g.M / (g.D * g.H * g.W);
+      if (tid < 32 && n0 + tid < g.Ncols)
+        for (int n = 0; n < nsamp; ++n)
+          if (n < n_lo || n > n_hi) {
+            float* p = g.inpart + (((long long)n * blocks_per_nt + blk) * g.Ncols + n0 + tid) * 2;
+            p[0] = 0.f;
+            p[1] = 0.f;
+          }
+    }
+  };
+  if (u_begin >= u_end || n0 >= g.Ncols) {
+    inp_zero(0, -1);
+    return;
+  }
   const int HW = g.H * g.W;
   const int cin = 8 << g.cpg_shift;
   const int ldb = g.lda * (int)sizeof(T);
@@ -2099,7 +2116,10 @@ __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int up
       epi_inp(i, 1);
     }
   }
-  if constexpr (INP) in_flush();
+  if constexpr (INP) {
+    in_flush();
+    inp_zero(u_begin / (nbrick / (g.M / vox_per_n)), in_n);
+  }
   PROBE_BLOCK(true);
 }
 
@@ -2513,12 +2533,12 @@ int launch_brick5(const GemmArgs& g, hipStream_t s, long long* dbg, bool dma) {
     return upb5;
   }
   if (g.inpart) {   // samples a block does not touch keep zero partials
-    hipMemsetAsync(g.inpart, 0, sizeof(float) * 2 * (size_t)(g.M / (g.D * g.H * g.W)) * bpn5 * g.Ncols, s);
-    if (!g.bias && knob("MMSEG_BRICK6", 1) && knob("MMSEG_BRICK6_INP", 1)) {
+    if (!g.bias && knob("MMSEG_BRICK6", 1) && knob("MMSEG_BRICK6_INP", 1)) {   // (brick6 writes those zeros itself)
       mmseg::note_kernel("conv3_brick6_kernel<BN32,INP>");
       MMSEG_LAUNCH((conv3_brick6_kernel<false, 6, 0, true>), grid, block, 0, s, g, upb5, bpn5);
       return upb5;
     }
+    hipMemsetAsync(g.inpart, 0, sizeof(float) * 2 * (size_t)(g.M / (g.D * g.H * g.W)) * bpn5 * g.Ncols, s);
     MMSEG_LAUNCH((conv3_brick5_kernel<false, true, true>), grid, block, 0, s, g, upb5, bpn5, nullptr);
     return upb5;
   }
@@ -4866,7 +4886,9 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
           fprintf(stderr, "\n");
         } else
 #endif
-        if (b666 && knob("MMSEG_BRICKR_PF", 0))
+        if (b666 && rb32 && knob("MMSEG_BRICKR_PF", 0))
+          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 0, true, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
+        else if (b666 && knob("MMSEG_BRICKR_PF", 0))
           MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 0, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
         else if (b666 && rb32)
           MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 0, false, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
@@ -4887,7 +4909,10 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
       }
     } else if (b666) {
       mmseg::note_kernel("conv3_brickr_kernel<BN32>");
-      if (rb32)
+      // (MMSEG_BRICKR_PF: tap t+1's fragments read during tap t's MFMAs -- at 12^3 / 6^3 a CU holds one block)
+      if (rb32 && knob("MMSEG_BRICKR_PF", 0))
+        MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, true, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
+      else if (rb32)
         MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, false, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
       else
         MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
@@ -5135,7 +5160,9 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
       const bool b448 = wb.bz == 4 && wb.by == 4 && wb.bx == 8 && knob("MMSEG_BRICKR_CT488", 1);   // grouped 48^3 / 24^3
       if (wgrad_co64(g.Ca, g.V, 3)) {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 64) * g.ksplit);
-        mmseg::note_kernel("wgrad_brickr_kernel<CO64>");
+        // (the compile-time bricks under their rocprofv3 family names, tools/rocprof_families.py)
+        mmseg::note_kernel(b366 ? "wgrad_brickr_kernel<CO64,V3>" : b448 ? "wgrad_brickr_kernel<CO64,B448>"
+                                                                         : "wgrad_brickr_kernel<CO64>");
         if (b366)
           MMSEG_LAUNCH((wgrad_brickr_kernel<T, 4, 3, 6, 6>), grid, dim3(512), 0, s, g, 3, 6, 6);
         else if (b448)
@@ -5144,7 +5171,8 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
           MMSEG_LAUNCH((wgrad_brickr_kernel<T, 4>), grid, dim3(512), 0, s, g, wb.bz, wb.by, wb.bx);
       } else {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 32) * g.ksplit);
-        mmseg::note_kernel("wgrad_brickr_kernel<CO32>");
+        mmseg::note_kernel(b366 ? "wgrad_brickr_kernel<CO32,V3>" : b448 ? "wgrad_brickr_kernel<CO32,B448>"
+                                                                         : "wgrad_brickr_kernel<CO32>");
         if (b366)
           MMSEG_LAUNCH((wgrad_brickr_kernel<T, 2, 3, 6, 6>), grid, dim3(512), 0, s, g, 3, 6, 6);
         else if (b448)

@@ -140,6 +140,9 @@ class DySpec:
     # (partials, nchunk): the InstanceNorm-backward partial sums [N][nchunk][C][2] the producer of p1 already
     # emitted (fused head + loss backward), so the partial pass over x and dy is skipped
     part: Optional[Tuple[torch.Tensor, int]] = None
+    # > 0: p1 holds p1_nmod samples and sample n reads p1's sample n % p1_nmod -- the fused level's gradient shared
+    # by the M modality groups of a grouped block (mmseg_instnorm_relu_bwd_group), instead of an M-fold copy
+    p1_nmod: int = 0
 
 
 def _aliases(x: Act, dx) -> bool:
@@ -622,6 +625,13 @@ class Block:
         es = 4
         alpha = None if dy.alpha is None else dy.alpha.data_ptr() + dy.alpha_off * es
         beta = None if dy.beta is None else dy.beta.data_ptr() + dy.beta_off * es
+        if dy.p1_nmod:
+            assert dy.part is None and alpha is None and beta is None and p1 is not None
+            L.mmseg_instnorm_relu_bwd_group(x.ptr, x.ld, ptr(m), ptr(r), p1.ptr, p1.ld, dy.scale1, dy.p1_nmod,
+                                            dy.pool_dy.ptr if dy.pool_dy is not None else None,
+                                            dy.pool_dy.ld if dy.pool_dy is not None else 0, ptr(dy.pool_idx),
+                                            dx.ptr, dx.ld, x.N, x.D, x.H, x.W, x.C, ptr(ws), code, s)
+            return
         if dy.part is not None:
             assert dy.pool_dy is None and alpha is None and beta is None
             part, nch = dy.part

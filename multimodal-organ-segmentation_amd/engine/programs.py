@@ -325,7 +325,8 @@ class DualEncoderProgram:
             self.pooled_g[l] = xin
             self.dpooled_g[l] = self.dpooled_c[l]
             self.y_g[l] = rt.act(M * N, *dims[l], F[l])
-            self.rep[l] = rt.act(M * N, *dims[l], F[l])
+            if os.environ.get("MMSEG_GROUP_REPLICATE", "0") != "0":
+                self.rep[l] = rt.act(M * N, *dims[l], F[l])
             self.idx_g[l] = self.idx_c[l]
             for mm in range(M):
                 self.y[mm][l] = act_group_view(self.y_g[l], mm, N)
@@ -576,8 +577,12 @@ class DualEncoderProgram:
 
         if self.l0 < self.L:                          # grouped small levels: all modalities per launch
             for l in range(self.L - 1, self.l0 - 1, -1):
-                self._replicate(self.dfused(l), self.rep[l])
-                dy = DySpec(p1=self.rep[l], scale1=sc)
+                if os.environ.get("MMSEG_GROUP_REPLICATE", "0") != "0":   # the previous M-fold copy (A/B)
+                    self._replicate(self.dfused(l), self.rep[l])
+                    dy = DySpec(p1=self.rep[l], scale1=sc)
+                else:   # every modality group reads the fused gradient's sample n % N (no copy)
+                    p1 = self.dfused(l)
+                    dy = DySpec(p1=p1, scale1=sc, p1_nmod=p1.N)
                 if l < self.L - 1:
                     dy.pool_dy = self.dpooled_g[l + 1]
                     dy.pool_idx = self.idx_g[l + 1]
