@@ -4909,8 +4909,9 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
       }
     } else if (b666) {
       mmseg::note_kernel("conv3_brickr_kernel<BN32>");
-      // (MMSEG_BRICKR_PF: tap t+1's fragments read during tap t's MFMAs -- at 12^3 / 6^3 a CU holds one block)
-      if (rb32 && knob("MMSEG_BRICKR_PF", 0))
+      // (MMSEG_BRICKR_PF32: tap t+1's fragments read during tap t's MFMAs -- at 12^3 / 6^3 a CU holds one block;
+      // 5-10 % per launch, r04ab convbench)
+      if (rb32 && knob("MMSEG_BRICKR_PF32", 1))
         MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, true, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
       else if (rb32)
         MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, false, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
