@@ -4894,6 +4894,8 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
           MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 0, false, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
         else if (b666)
           MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
+        else if (b488 && rb32 && knob("MMSEG_BRICKR_PF488", 0))
+          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 4, 8, 8, 0, true, true>), grid, block, 0, s, g, 4, 8, 8, (long long*)nullptr);
         else if (b488 && rb32)
           MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 4, 8, 8, 0, false, true>), grid, block, 0, s, g, 4, 8, 8, (long long*)nullptr);
         else if (b488)
@@ -4919,7 +4921,9 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
         MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
     } else if (b488) {
       mmseg::note_kernel("conv3_brickr_kernel<BN32>");
-      if (rb32)
+      if (rb32 && knob("MMSEG_BRICKR_PF488", 0))
+        MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 4, 8, 8, 0, true, true>), grid, block, 0, s, g, 4, 8, 8, (long long*)nullptr);
+      else if (rb32)
         MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 4, 8, 8, 0, false, true>), grid, block, 0, s, g, 4, 8, 8, (long long*)nullptr);
       else
         MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 4, 8, 8>), grid, block, 0, s, g, 4, 8, 8, (long long*)nullptr);
