@@ -41,6 +41,16 @@ def family(name: str) -> str:
     if m:
         tile = "128x32" if (m.group(2), m.group(3)) == ("4", "1") else "128x64"
         return f"conv_gemm_kernel<{_MODES[m.group(1)]},{tile}>[{dt}]"
+    # brick6 / brick8 under the timer's family names (engine/profiler.py: mmseg_last_kernel()), so a family
+    # means the same launches in the live timer and in the trace: brick6 split by its INP / F8 forms, brick8 by BN
+    m = (re.search(r"conv3_brick6_kernelILb[01]ELi\d+ELi\d+ELb([01])ELb([01])E", name) or
+         re.search(r"conv3_brick6_kernel<(?:true|false), \d+, \d+, (true|false), (true|false)>", name))
+    if m:
+        inp, f8 = (m.group(1) in ("1", "true")), (m.group(2) in ("1", "true"))
+        return "conv3_brick6_kernel<BN32" + (",INP" if inp else "") + (",F8" if f8 else "") + ">[bf16]"   # bf16 only
+    m = re.search(r"conv3_brick8_kernelILi(\d+)E", name) or re.search(r"conv3_brick8_kernel<(\d+),", name)
+    if m:
+        return f"conv3_brick8_kernel<BN{m.group(1)}>[bf16]"   # bf16 only
     if "conv3_brick4_kernel" in name:
         return "conv3_brick4_kernel<BN32>[bf16]"
     m = re.search(r"conv3_brick3_kernelI(?:DF16b|f)Li(\d+)E", name)
