@@ -213,6 +213,15 @@ int mmseg_conv3_wgrad_group_ok(long long V, int Co, int Cip, int Ci, int cpg_shi
                                int ldx, int dtype);
 int mmseg_conv3_group_splits(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,
                              int dtype);
+/* conv_gemm_group + the output's per-brick InstanceNorm partials (the runtime-brick epilogue; one split): stats_part
+ * [M / (D H W)][conv3_group_stats_bricks()][Ncols][2] (mean, M2), merged by mmseg_instnorm_stats_bricks -- the
+ * grouped 48^3 / 24^3 levels' statistics without a pass over the output (reference unet.py:28-29 InstanceNorm). */
+int mmseg_conv3_group_stats_bricks(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda,
+                                   int ldo, int dtype);
+int mmseg_conv_gemm_group_stats(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
+                                int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W,
+                                int cin_real, int groups, long long w_gstride, int b_gstride, float* stats_part,
+                                int dtype, void* stream);
 long long mmseg_conv3_wgrad_group_ws_floats(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W,
                                             int lddy, int ldx, int groups, int dtype);
 int mmseg_conv3_wgrad_group(const void* dy, int lddy, const void* x, int ldx, float* grad, float* bias_grad, int Co,

@@ -5578,6 +5578,22 @@ int conv_gemm_impl(const void* a, int lda, const void* wpacked, const float* bia
                    int ldo2, int split, float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift,
                    int D, int H, int W, int ksplit, float* stats_part, int cin_real, int dtype, void* stream,
                    int groups = 1, long long w_gstride = 0, int b_gstride = 0);
+int mmseg_conv3_group_stats_bricks(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda,
+                                   int ldo, int dtype);
+
+// mmseg_conv_gemm_group + the per-brick InstanceNorm partials of the output (stats_part [M / (D H W)]
+// [mmseg_conv3_group_stats_bricks()][Ncols][2], (mean, M2) per brick; mmseg_instnorm_stats_bricks merges them)
+// from the runtime-brick kernel's epilogue -- the grouped 48^3 / 24^3 levels' statistics without a pass over
+// the conv output.
+int mmseg_conv_gemm_group_stats(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
+                                int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W,
+                                int cin_real, int groups, long long w_gstride, int b_gstride, float* stats_part,
+                                int dtype, void* stream) {
+  MMSEG_REQUIRE(mode == MODE_CONV3 && groups >= 1 && M % (groups * D * H * W) == 0 && stats_part != nullptr,
+                "conv_gemm_group_stats: CONV3 over groups x whole samples, with a statistics buffer");
+  return conv_gemm_impl(a, lda, wpacked, bias, out, ldo, nullptr, 0, 0, nullptr, mode, M, Ncols, Cpad, KG, cpg_shift,
+                        D, H, W, 1, stats_part, cin_real, dtype, stream, groups, w_gstride, b_gstride);
+}
 
 // mmseg_conv_gemm_ex over `groups` equal sample groups of A / out with their own packed weights (group gi:
 // wpacked + gi * w_gstride elements) and bias (bias + gi * b_gstride): the modality encoders' small levels as one
@@ -5620,7 +5636,10 @@ int conv_gemm_impl(const void* a, int lda, const void* wpacked, const float* bia
   MMSEG_REQUIRE(cin_real >= 0 && cin_real <= (8 << cpg_shift), "conv_gemm: cin_real %d outside [0, %d]", cin_real,
                 8 << cpg_shift);
   MMSEG_REQUIRE(!stats_part || (mode == MODE_CONV3 && ksplit == 1 &&
-                                mmseg_conv3_stats_bricks(M, Ncols, Cpad, KG, cpg_shift, D, H, W, lda, ldo, dtype) > 0),
+                                (groups > 1 ? mmseg_conv3_group_stats_bricks(M, Ncols, Cpad, KG, cpg_shift, D, H, W, lda,
+                                                                             ldo, dtype)
+                                            : mmseg_conv3_stats_bricks(M, Ncols, Cpad, KG, cpg_shift, D, H, W, lda, ldo,
+                                                                       dtype)) > 0),
                 "conv_gemm_stats: fused statistics need a brick kernel without split-K for this shape");
   MMSEG_REQUIRE(lda % 8 == 0 && ldo >= 1, "conv_gemm: lda must be a multiple of 8 (got %d)", lda);
   MMSEG_REQUIRE(Cpad >= ((Ncols + (Ncols >= 64 ? 63 : 31)) / (Ncols >= 64 ? 64 : 32)) * (Ncols >= 64 ? 64 : 32),
@@ -5771,6 +5790,16 @@ int mmseg_conv3_wgrad_group_ok(long long V, int Co, int Cip, int Ci, int cpg_shi
              ? 1 : 0;
 }
 // split count of a grouped conv (mmseg_conv_gemm_group): the runtime-brick plan's
+// Bricks per sample for which the grouped (forced runtime-brick) conv can emit fused InstanceNorm partials
+// (mmseg_conv_gemm_group_stats): the plan runs one split; 0 otherwise or without MMSEG_GROUP_STATS=1.
+int mmseg_conv3_group_stats_bricks(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda,
+                                   int ldo, int dtype) {
+  if (!knob("MMSEG_GROUP_STATS", 0)) return 0;   // off: equal per step (r04ad), the epilogue costs what the pass did
+  const Conv3Plan p = plan_conv3(M, Ncols, 8 << cpg_shift, D, H, W, lda, ldo, dtype == MMSEG_BF16 ? 2 : 4, true);
+  if (p.kind != 2 || p.ks != 1) return 0;
+  return (D / p.bz) * (H / p.by) * (W / p.bx);
+}
+
 int mmseg_conv3_group_splits(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,
                              int dtype) {
   const Conv3Plan p = plan_conv3(M, Ncols, 8 << cpg_shift, D, H, W, lda, ldo, dtype == MMSEG_BF16 ? 2 : 4, true);

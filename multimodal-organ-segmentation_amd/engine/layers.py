@@ -773,9 +773,22 @@ class ConvGroup:
                 and bool(L.mmseg_conv3_wgrad_group_ok(M, c.Co, c.Cip, c.Ci, c.cpg_shift, x.D, x.H, x.W, y.ld, x.ld,
                                                       code)))
 
-    def fwd(self, x: Act, y: Act):
+    def stats_bricks(self, x: Act, y: Act) -> int:
+        """Bricks per sample for which fwd() can emit fused InstanceNorm partials (0 = not available)."""
+        c = self.c0
+        return self.rt.lib.mmseg_conv3_group_stats_bricks(x.N * x.V, c.ncols_f, c.Cpad, c.KG, c.cpg_shift, x.D, x.H,
+                                                          x.W, x.ld, y.ld, self.rt.code)
+
+    def fwd(self, x: Act, y: Act, stats_part: Optional[torch.Tensor] = None):
         c, L = self.c0, self.rt.lib
         M, nc = x.N * x.V, c.ncols_f
+        if stats_part is not None:
+            with TIMER.region(_gemm_name(self.rt, nc, "conv3"), flops=2.0 * M * c.Co * 27 * c.Ci,
+                              nbytes=_io_bytes(self.rt, M, c.Cip, c.Co, self.G * 27 * c.Cip * c.Co)):
+                L.mmseg_conv_gemm_group_stats(x.ptr, x.ld, ptr(c.wf), ptr(c.conv.bias), y.ptr, y.ld, MODE_CONV3, M, nc,
+                                              c.Cpad, c.KG, c.cpg_shift, x.D, x.H, x.W, c.kreal_f, self.G, self.w_gs,
+                                              self.b_gs, ptr(stats_part), self.rt.code, self.rt.stream)
+            return
         ks = L.mmseg_conv3_group_splits(M, nc, c.Cpad, c.KG, c.cpg_shift, x.D, x.H, x.W, x.ld, y.ld, self.rt.code)
         ws = self.rt.ws(ks * M * nc) if ks > 1 else None
         with TIMER.region(_gemm_name(self.rt, nc, "conv3"), flops=2.0 * M * c.Co * 27 * c.Ci,
@@ -864,6 +877,7 @@ class GroupBlock(Block):
         self.y1 = rt.act(G * N, D, H, W, C)
         self.x2 = rt.act(G * N, D, H, W, C)
         self.stats = torch.empty(4, G * N * C, dtype=torch.float32, device=rt.device)
+        self.gnb = None   # fused-statistics bricks per sample of (g1, g2), set on the first forward
         for g, b in enumerate(self.blocks):
             b.shape = (N, D, H, W)
             b.x1, b.y1, b.x2 = (act_group_view(t, g, N) for t in (self.x1, self.y1, self.x2))
@@ -878,10 +892,21 @@ class GroupBlock(Block):
 
     def fwd(self, xin: Act, out: Act):
         st = self.stats
-        self.g1.fwd(xin, self.x1)
-        self._norm_fwd(self.x1, self.y1, st[0], st[1])
-        self.g2.fwd(self.y1, self.x2)
-        self._norm_fwd(self.x2, out, st[2], st[3])
+        if self.gnb is None:
+            # the statistics from the conv epilogue above the one-launch InstanceNorm size (48^3 / 24^3 with forced
+            # grouping); the register-resident small form needs no statistics pass to replace
+            big = self.x1.V > SMALL_IN_V
+            self.gnb = (self.g1.stats_bricks(xin, self.x1) if big else 0,
+                        self.g2.stats_bricks(self.y1, self.x2) if big else 0)
+            n = max(self.gnb)
+            self.gpart = (torch.empty(self.x1.N * n * self.Co * 2, dtype=torch.float32, device=self.rt.device)
+                          if n else None)
+        p1 = self.gpart if self.gnb[0] else None
+        p2 = self.gpart if self.gnb[1] else None
+        self.g1.fwd(xin, self.x1, stats_part=p1)
+        self._norm_fwd(self.x1, self.y1, st[0], st[1], p1, self.gnb[0])
+        self.g2.fwd(self.y1, self.x2, stats_part=p2)
+        self._norm_fwd(self.x2, out, st[2], st[3], p2, self.gnb[1])
 
     def bwd(self, xin: Act, dy: DySpec, dxin: Optional[Act], accumulate: bool):
         st = self.stats

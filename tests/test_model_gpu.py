@@ -702,28 +702,32 @@ def test_batched_weight_gradient_reduce_bitwise(dev, dtype, monkeypatch):
 
 @pytest.mark.parametrize("tag,force", [("dual_tiny_cross_attention", "0"), ("dual_tiny_add", "0"),
                                        ("dual_tiny_m3_tversky", "0"), ("dual_tiny_cross_attention", "1"),
-                                       ("dual_tiny_m3_tversky", "1"), ("dual_tiny_cross_attention", "w")])
+                                       ("dual_tiny_m3_tversky", "1"), ("dual_tiny_cross_attention", "w"),
+                                       ("dual_tiny_cross_attention", "s")])
 def test_grouped_modalities_match_per_modality(dev, tag, force, monkeypatch):
     """bf16 (the dtype whose small levels take the runtime-brick kernels): the modality-grouped small levels and the
     grouped encoder output-norm backward (MMSEG_GROUP_SMALL / MMSEG_GROUP_OUTNORM, programs.DualEncoderProgram)
     against the per-modality launches on the same weights and batch.  The grouped launches split the reductions
     differently (one launch over M x N samples), so the two differ by bf16 rounding: loss within 1e-3 relative,
     logits within 2e-2 and every gradient within 5e-2 normwise (L2).  force=1 (MMSEG_GROUP_FORCE_R): the 24^3
-    level is grouped too, on the runtime-brick kernels instead of the (4, 8, 8)-brick family."""
-    monkeypatch.setenv("MMSEG_GROUP_FORCE_R", "1" if force == "1" else "0")
+    level is grouped too, on the runtime-brick kernels instead of the (4, 8, 8)-brick family; force=s: the same
+    with that level's InstanceNorm statistics from the conv epilogue (MMSEG_GROUP_STATS, mmseg_conv_gemm_group_stats)."""
+    monkeypatch.setenv("MMSEG_GROUP_FORCE_R", "1" if force in ("1", "s") else "0")
+    monkeypatch.setenv("MMSEG_GROUP_STATS", "1" if force == "s" else "0")
     kind, mods, C, fusion, lossname = TINY[tag]
     g = golden(tag)
     # 96^3 (B = 1, the tiny features): levels 12^3 / 6^3 take the runtime-brick kernels, as in the bench
     gen = torch.Generator().manual_seed(11)
-    x = torch.randn(1, len(mods), 96, 96, 96, generator=gen)
-    y = torch.randint(0, C, (1, 96, 96, 96), generator=gen)
+    B = 2 if force == "s" else 1   # (s: 4 samples at 24^3 leave the runtime-brick conv one split, as in the bench)
+    x = torch.randn(B, len(mods), 96, 96, 96, generator=gen)
+    y = torch.randint(0, C, (B, 96, 96, 96), generator=gen)
     res = {}
     for flag in ("1", "0"):
         monkeypatch.setenv("MMSEG_GROUP_SMALL", flag)
         monkeypatch.setenv("MMSEG_GROUP_OUTNORM", flag)
         # (force: features whose 24^3 convs have unpadded channels -- the tiny fixture's 16 -> 32 conv pads its
         # input channels, which keeps that level per modality)
-        feats = [16, 32, 64, 128, 256] if force in ("1", "w") else list(g["features"])
+        feats = [16, 32, 64, 128, 256] if force in ("1", "w", "s") else list(g["features"])
         cfg = make_config(kind, mods, C, feats, fusion=fusion, loss=lossname, dtype="bfloat16")
         torch.manual_seed(int(g["seed"]))
         m = build_model(cfg)
@@ -737,14 +741,17 @@ def test_grouped_modalities_match_per_modality(dev, tag, force, monkeypatch):
         res[flag] = (loss.item(), logits, {n: p.grad.detach().double().cpu().clone()
                                            for n, p in m.backbone.named_parameters()}, prog.l0, prog.L,
                      prog.group_outnorm)
+        if flag == "1":
+            gnb = tuple(getattr(prog.gblocks[prog.l0], "gnb", None) or (0, 0))
     (l1, lg1, g1, l0, L, go), (l2, lg2, g2, l0b, _, gob) = res["1"], res["0"]
     print(f"\n{tag}: grouped from level {l0} of {L} (output norm grouped: {go}); loss {l1:.6f} vs {l2:.6f}")
-    assert l0 == (2 if force == "1" else 3) and go and l0b == L and not gob
+    assert l0 == (2 if force in ("1", "s") else 3) and go and l0b == L and not gob
+    assert (min(gnb) > 0) == (force == "s"), gnb   # force=s: the 24^3 statistics came from the conv epilogue
     bad_all = {n: float((g1[n] - g2[n]).norm() / g2[n].norm()) for n in g2 if g2[n].norm() > 0}
     print("largest gradient differences:", sorted(bad_all.items(), key=lambda kv: -kv[1])[:6])
     assert abs(l1 - l2) < 1e-3 * abs(l2)
     assert float((lg1 - lg2).norm() / lg2.norm()) < 2e-2
-    if force == "1":
+    if force in ("1", "s"):
         # the forced 24^3 level runs other kernels (runtime-brick) than the per-modality step, so the two bf16
         # steps differ by rounding amplified through kink flips (up to ~0.15 on these random-input gradients, the
         # size of any two bf16 kernel paths here); its parity is held to the pinned fp64 oracle instead
