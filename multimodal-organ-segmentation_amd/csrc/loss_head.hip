@@ -1263,14 +1263,27 @@ __device__ __forceinline__ float adamw_one(float& pv, float gv, float& mv, float
   pv = pv + (-step_size) * (mv / denom);
   return pv;
 }
+// ntail (< 4): the scalar elements after the last float4, done by block 0's first threads (the same
+// per-element operations as adamw_kernel, so bitwise its results) -- no second launch per step for them.
 __global__ __launch_bounds__(256) void adamw4_kernel(float4* __restrict__ p, const float4* __restrict__ g,
                                                      float4* __restrict__ m, float4* __restrict__ v, long long n4,
                                                      AdamHyper hv, const AdamHyper* __restrict__ hp,
-                                                     const float* __restrict__ skip) {
+                                                     const float* __restrict__ skip, int ntail) {
   AdamHyper h;
   if (!adamw_load(hv, hp, skip, h)) return;
   const float decay = h.decay, omb1 = h.omb1, beta2 = h.beta2, omb2 = h.omb2, eps = h.eps, step_size = h.step_size,
               bc2_sqrt = h.bc2_sqrt;
+  if (blockIdx.x == 0 && (int)threadIdx.x < ntail) {
+    const long long k = 4 * n4 + threadIdx.x;
+    float* ps = reinterpret_cast<float*>(p);
+    float* ms = reinterpret_cast<float*>(m);
+    float* vs = reinterpret_cast<float*>(v);
+    float pv = ps[k], mv = ms[k], vv = vs[k];
+    adamw_one(pv, reinterpret_cast<const float*>(g)[k], mv, vv, decay, omb1, beta2, omb2, eps, step_size, bc2_sqrt);
+    ps[k] = pv;
+    ms[k] = mv;
+    vs[k] = vv;
+  }
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += 2 * stride) {
     const long long i2 = i + stride;
@@ -1714,10 +1727,7 @@ static int adamw_launch(float* p, const float* g, float* m, float* v, long long 
     if (b4 > 8192) b4 = 8192;
     MMSEG_LAUNCH(adamw4_kernel, dim3((int)b4), dim3(256), 0, stream, reinterpret_cast<float4*>(p),
                        reinterpret_cast<const float4*>(g), reinterpret_cast<float4*>(m), reinterpret_cast<float4*>(v),
-                       n4, hv, hp, skip);
-    if (n % 4)
-      MMSEG_LAUNCH(adamw_kernel, dim3(1), dim3(64), 0, stream, p + 4 * n4, g + 4 * n4, m + 4 * n4, v + 4 * n4,
-                         n - 4 * n4, hv, hp, skip);
+                       n4, hv, hp, skip, (int)(n % 4));
     return mmseg::check_launch("adamw");
   }
   const int grid = grid_for(n) > 4096 ? 4096 : grid_for(n);
