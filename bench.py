@@ -62,15 +62,62 @@ def make_config(model, batch, dtype, out_channels=6, modalities=("CT", "PET"), s
     }
 
 
-def _pmc_summary():
-    """Newest committed PMC summary (profiles/*pmc_traffic*.json, made by tools/rocprof_families.py from separate
-    FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench): ({family: {...}}, path) or (None, None)."""
+# ---------------------------------------------------------------------------------------------------------------
+# Committed rocprofv3 summaries (profiles/*_steady.json, *_pmc_traffic.json, *_pmc_sq.json; tools/rocprof_families.py)
+# carry the workload they were measured on ("_workload": workload_key() of the profiled bench run) and when
+# ("_created").  A bench line reads only summaries of ITS OWN workload -- the newest by "_created" -- and leaves
+# the rocprof / PMC fields null when none matches (then the dominant family comes from the live timer alone).
+# ---------------------------------------------------------------------------------------------------------------
+CONFIG_TAGS = {  # BASELINE.json configs (1 GPU per-rank shapes) -> tag used in profile file names
+    ("dual_encoder", 2, 96, 2, "bf16", "dice_ce", False): "c3",
+    ("unet", 2, 96, 2, "bf16", "dice_ce", False): "c2",
+    ("swin_unetr", 2, 128, 1, "bf16", "dice_ce", False): "c4",
+    ("dual_encoder", 3, 96, 2, "bf16", "tversky", False): "c5",
+    ("dual_encoder", 3, 96, 2, "bf16", "tversky", True): "c5fp8",
+}
+
+WORKLOAD = None      # set by main(): workload_key(args)
+
+
+def workload_key(model: str, modalities: int, size: int, batch: int, dtype: str, loss: str, fp8: bool,
+                 kernels: str = "hip") -> dict:
+    """What a profile summary must match to be used on a bench line: the per-GPU step's shape and arithmetic."""
+    return {"model": model, "modalities": int(modalities), "size": int(size), "batch": int(batch), "dtype": dtype,
+            "loss": loss, "fp8": bool(fp8), "kernels": kernels}
+
+
+def workload_tag(w: dict) -> str:
+    t = CONFIG_TAGS.get((w["model"], w["modalities"], w["size"], w["batch"], w["dtype"], w["loss"], w["fp8"]))
+    if t is not None and w.get("kernels", "hip") == "hip":
+        return t
+    return f"{w['model']}-m{w['modalities']}-s{w['size']}-b{w['batch']}-{w['dtype']}-{w['loss']}" + \
+        ("-fp8" if w["fp8"] else "") + ("" if w.get("kernels", "hip") == "hip" else "-" + w["kernels"])
+
+
+_PROFILE_CACHE = {}
+
+
+def _profile(kind: str):
+    """(summary dict, repo-relative path) of the newest committed `kind` summary measured on WORKLOAD, else
+    (None, None).  kind: steady | pmc_traffic | pmc_sq."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        return json.load(f), os.path.relpath(files[-1], ROOT)
+    if kind in _PROFILE_CACHE:
+        return _PROFILE_CACHE[kind]
+    best = (None, None, "")
+    if WORKLOAD is not None:
+        for f in glob.glob(os.path.join(ROOT, "profiles", f"*_{kind}.json")):
+            try:
+                with open(f) as fh:
+                    d = json.load(fh)
+            except (OSError, ValueError):
+                continue
+            if not isinstance(d, dict) or d.get("_workload") != WORKLOAD:
+                continue
+            created = str(d.get("_created", ""))
+            if best[0] is None or created > best[2]:
+                best = (d, os.path.relpath(f, ROOT), created)
+    _PROFILE_CACHE[kind] = best[:2]
+    return best[:2]
 
 
 def _family_key(d: dict, kernel: str):
@@ -89,9 +136,8 @@ def _family_key(d: dict, kernel: str):
 
 
 def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the PMC summary (the trace names some families without the timer's
-    template suffix: conv3_brick5_kernel<BN32>[bf16] is conv3_brick5_kernel there)."""
-    d, src = _pmc_summary()
+    """HBM bytes per launch of `kernel` from this workload's PMC summary (FETCH_SIZE x 2 + WRITE_SIZE)."""
+    d, src = _profile("pmc_traffic")
     if d is None:
         return None, src
     key = _family_key(d, kernel)
@@ -101,64 +147,47 @@ def pmc_traffic(kernel: str):
 
 
 def pmc_mfma_busy(kernel: str):
-    """MFMA-pipe busy fraction of `kernel` from the newest committed SQ counter summary (profiles/*pmc_sq*.json,
+    """MFMA-pipe busy fraction of `kernel` from this workload's SQ counter summary (profiles/*_pmc_sq.json,
     tools/rocprof_families.py sq, from a separate rocprofv3 --pmc pass over this bench): SQ_VALU_MFMA_BUSY_CYCLES
     (summed over the 1,024 SIMDs) / (1,024 x GRBM_GUI_ACTIVE / 8 XCDs), with the VALU / LDS instructions issued
     per MFMA."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_sq*.json")))
-    if not files:
+    d, src = _profile("pmc_sq")
+    if d is None:
         return None, None
-    with open(files[-1]) as f:
-        d = json.load(f)
     key = _family_key(d, kernel)
     if key is None:
-        return None, os.path.relpath(files[-1], ROOT)
+        return None, src
     v = d[key]
     out = {"mfma_busy": round(v["mfma_busy"], 4)}
     for k in ("valu_per_mfma", "lds_per_mfma", "clock_ghz", "counter_gflop"):
         if v.get(k) is not None:
             out[k] = round(v[k], 3)
-    return out, os.path.relpath(files[-1], ROOT)
-
-
-def _steady_summary():
-    """Newest committed steady-state rocprofv3 family summary (profiles/*steady*.json): (dict, path) or (None, None)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*steady*.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        return json.load(f), os.path.relpath(files[-1], ROOT)
+    return out, src
 
 
 def rocprof_steady(kernel: str):
-    """The kernel's steady-state average launch duration from the newest committed rocprofv3 kernel-trace summary
-    (profiles/*steady*.json: tools/rocprof_families.py steady over the last steps of a traced run of this bench),
+    """The kernel's steady-state average launch duration from this workload's rocprofv3 kernel-trace summary
+    (profiles/*_steady.json: tools/rocprof_families.py steady over the last steps of a traced run of this bench),
     to set beside the live timer's."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*steady*.json")))
-    if not files:
+    d, src = _profile("steady")
+    if d is None:
         return None, None
-    with open(files[-1]) as f:
-        d = json.load(f)
     key = _family_key(d, kernel)
-    src = os.path.relpath(files[-1], ROOT)
     return (d[key]["avg_launch_ms"] if key is not None else None), src
 
 
 def pmc_step_bytes():
-    """HBM bytes of one whole training step from the PMC summary: every kernel's bytes per launch x launches,
-    over the steps the profiled run executed (its '_steps', else the AdamW launch count: one per step);
+    """HBM bytes of one whole training step from this workload's PMC summary: every kernel's bytes per launch x
+    launches, over the steps the profiled run executed (its '_steps', else the AdamW launch count: one per step);
     the runtime's buffer copies / fills (input staging, arena set-up) are not part of a step."""
-    d, src = _pmc_summary()
+    d, src = _profile("pmc_traffic")
     if d is None:
         return None, None
     steps = d.get("_steps") or d.get("adamw4_kernel", {}).get("launches")
     if not steps:
         return None, src
     tot = sum(v["hbm_bytes_per_launch"] * v["launches"] for k, v in d.items()
-              if not k.startswith(("_", "__amd_rocclr")))
+              if not k.startswith(("_", "__amd_rocclr")) and isinstance(v, dict))
     return tot / steps, src
 
 
@@ -183,6 +212,36 @@ def cpu_threads() -> int:
         return len(os.sched_getaffinity(0))
     except AttributeError:
         return os.cpu_count() or 1
+
+
+def cpu_baseline_swin(model, batch, size, out_channels, modalities, threads, steps=1):
+    """Config c4 on the host: oracle/swin_oracle.py (torch-CPU fp32 restatement of MONAI 1.3's SwinUNETR forward;
+    parity vs MONAI itself unpinned) + the reference's DiceCE + backward + AdamW, from the GPU model's initial
+    weights, on the same seeded phantoms: 1 warm-up step on a 64^3 patch, then `steps` timed full-size steps."""
+    from oracle import mmseg_oracle as O
+    from oracle import swin_oracle as SO
+    from mmseg_amd.data.synthetic import SyntheticSegDataset
+    torch.set_num_threads(threads)
+    M = len(modalities)
+    bb = model.backbone
+    p = {k: v.detach().float().cpu() for k, v in bb.model.named_parameters()}
+    fwd = lambda pp, x: SO.swin_unetr_forward(pp, x, bb.depths, bb.num_heads)  # noqa: E731
+    st = O.OracleStep(p, fwd, O.dice_ce_loss)
+    g = torch.Generator().manual_seed(5)
+    st.step(torch.randn(1, M, 64, 64, 64, generator=g), torch.randint(0, out_channels, (1, 64, 64, 64), generator=g))
+    ds = SyntheticSegDataset(steps * batch, size, out_channels, modalities, seed=1234)
+    batches = []
+    for i in range(steps):
+        items = [ds[i * batch + j] for j in range(batch)]
+        batches.append((torch.stack([it["image"] for it in items]), torch.stack([it["label"] for it in items])))
+    t0 = time.perf_counter()
+    for x, y in batches:
+        st.step(x, y)
+    dt = (time.perf_counter() - t0) / steps
+    return {"value": batch / dt, "unit": "patches/s", "cores": threads, "kind": "port",
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
+            "sample": f"{steps} oracle train step(s) (oracle/swin_oracle.py fwd + DiceCE + bwd + AdamW), swin_unetr "
+                      f"fs=48 M={M} B={batch} {size}^3 fp32 on seeded phantoms, {dt:.2f} s/step on {threads} threads"}
 
 
 def cpu_baseline(model_name, batch, size, out_channels, modalities, threads, loss="dice_ce", steps=3):
@@ -246,7 +305,19 @@ def main():
     ap.add_argument("--timer-dump", default="", help="write every timed launch (family, site, ms, flops) as JSON")
     ap.add_argument("--amp", default="bf16", choices=["bf16", "fp16"],
                     help="--kernels torch autocast dtype (fp16 + GradScaler = the reference's GPU mode)")
+    ap.add_argument("--dp-rehearsal", action="store_true",
+                    help="one GPU, the data-parallel step: an RCCL process group of world size 1 with "
+                         "distributed.reduce_single_rank, so the bucket all-reduces (AVG) really run through RCCL "
+                         "inside the captured step, exactly as each rank of the N-GPU job runs them")
+    ap.add_argument("--workload-out", default="", help="write this run's workload key (JSON) for the profile "
+                                                       "summaries of tools/rocprof_families.py")
     args = ap.parse_args()
+    global WORKLOAD
+    WORKLOAD = workload_key(args.model, len(args.modalities.split(",")), args.size, args.batch, args.dtype, args.loss,
+                            args.fp8, args.kernels)
+    if args.workload_out:
+        with open(args.workload_out, "w") as f:
+            json.dump(WORKLOAD, f)
 
     import mmseg_amd  # noqa: F401
     from mmseg_amd.data import device_batches
@@ -261,10 +332,18 @@ def main():
     torch.cuda.set_device(dev)
     rank, world = ddp.rank(), ddp.world()
     n_gpus = world
+    if args.dp_rehearsal:
+        if world != 1:
+            raise SystemExit("--dp-rehearsal is the one-GPU rehearsal of the DP step (world size 1)")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
 
     mods = args.modalities.split(",")
     cfg = make_config(args.model, args.batch, args.dtype, size=args.size, modalities=mods, loss=args.loss,
                       kernels=args.kernels, amp=args.amp, fp8=args.fp8)
+    if args.dp_rehearsal:
+        cfg["distributed"]["reduce_single_rank"] = True
     if args.kernels == "torch":
         args.no_cpu_baseline = True
         args.timer_steps = 0
@@ -321,7 +400,7 @@ def main():
     dom = max(mfma.items(), key=lambda kv: kv[1]["ms"]) if mfma else None
     # ... chosen by rocprofv3 time per step of the captured step where a committed steady-state trace summary
     # names the family (tools/rocprof_families.py uses the timer's family names), else by the timer's own time
-    steady, _ = _steady_summary()
+    steady, _ = _profile("steady")
     if mfma and steady:
         def _rp_ms(kv):
             key = _family_key(steady, kv[0])
@@ -375,6 +454,27 @@ def main():
     families = {k: {"ms_per_step": round(v["ms"] / args.timer_steps, 3),
                     "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1) if v["ms"] > 0 else None}
                 for k, v in sorted(fam.items(), key=lambda kv: -kv[1]["ms"])}
+    # every MFMA family of the step with its algorithmic work, frac of the dense peak (live timer), and -- from this
+    # workload's committed rocprofv3 summaries -- its trace duration and SQ counters
+    peak_f = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
+    mfma_families = {}
+    for k, v in sorted(mfma.items(), key=lambda kv: -kv[1]["ms"]):
+        fl = v["flops"] / v["launches"]
+        e = {"ms_per_step": round(v["ms"] / max(args.timer_steps, 1), 4), "launches_per_step":
+             round(v["launches"] / max(args.timer_steps, 1), 2), "gflop_per_launch": round(fl / 1e9, 4),
+             "avg_launch_ms": round(v["ms"] / v["launches"], 4),
+             "frac": round(fl / (v["ms"] / v["launches"] * 1e-3) / 1e12 / peak_f, 4)}
+        rp, _ = rocprof_steady(k)
+        if rp:
+            e["rocprof_avg_launch_ms"] = round(rp, 4)
+            e["rocprof_frac"] = round(fl / (rp * 1e-3) / 1e12 / peak_f, 4)
+        busy, _ = pmc_mfma_busy(k)
+        if busy is not None:
+            e.update({kk: busy[kk] for kk in ("mfma_busy", "valu_per_mfma", "lds_per_mfma") if kk in busy})
+        tr, _ = pmc_traffic(k)
+        if tr is not None:
+            e["traffic_vs_algorithmic"] = round(tr / max(v["bytes"] / v["launches"], 1.0), 3)
+        mfma_families[k] = e
     step = None
     work = STEP_WORK.get((args.model, len(mods)))
     if work is not None and args.size == 96 and args.dtype == "bf16":
@@ -394,7 +494,10 @@ def main():
         else:
             roofline = {"step": step}
     cpu = None
-    if n_gpus == 1 and not args.no_cpu_baseline and args.model != "swin_unetr":
+    if n_gpus == 1 and not args.no_cpu_baseline and args.model == "swin_unetr":
+        cpu = cpu_baseline_swin(model, args.batch, args.size, 6, mods, args.cpu_threads or cpu_threads(),
+                                steps=max(1, min(args.cpu_steps, 1)))
+    elif n_gpus == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.model, args.batch, args.size, 6, mods, args.cpu_threads or cpu_threads(),
                            loss=args.loss, steps=args.cpu_steps)
     workload = {"dual_encoder": "DualEncoder fusion=cross_attention (mean, dual_encoder.py:193-195)",
@@ -413,15 +516,20 @@ def main():
         "config": {"workload": f"{workload} {args.size}^3, modalities {'+'.join(mods)}, 6 classes, "
                                f"{'DiceCE' if args.loss == 'dice_ce' else 'Tversky'}, AdamW, per-GPU batch {args.batch}",
                    "model": args.model, "global_batch": args.batch * n_gpus, "patch": [args.size] * 3,
-                   "parallelism": f"dp{n_gpus}", "kernels": args.kernels},
+                   "parallelism": f"dp{n_gpus}" + ("-rccl-rehearsal" if args.dp_rehearsal else ""),
+                   "kernels": args.kernels, "tag": workload_tag(WORKLOAD)},
         "loss": round(loss_val, 5),
         "roofline": roofline,
         "cpu_baseline": cpu,
         "kernel_families": families,
+        "mfma_families": mfma_families,
+        "profiles": {kind: _profile(kind)[1] for kind in ("steady", "pmc_traffic", "pmc_sq")},
     }
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
+        dist.destroy_process_group()
+    elif args.dp_rehearsal:
         dist.destroy_process_group()
 
 

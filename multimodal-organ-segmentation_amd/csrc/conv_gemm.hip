@@ -2139,9 +2139,15 @@ __host__ __device__ constexpr int br_xq(int tsize) { return tsize == 2 ? 2560 : 
 // arithmetic divides by constants (mul-shift) instead of runtime integer divisions, which at one 32-channel
 // chunk per block were most of the kernel's VALU work (8.6 VALU instructions per MFMA, rocprofv3 r02).
 // B32 (bf16): the halo staged with 32-bit offset buffer loads, out-of-volume lanes reading zeros (conv3_brick2's B32).
-template <typename T, int BN, int CBZ = 0, int CBY = 0, int CBX = 0, int DBG = 0, bool PF = false, bool B32 = false>
-__global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kernel(GemmArgs g, int bz_rt, int by_rt,
-                                                                                   int bx_rt, long long* dbg = nullptr) {
+// KW = 2 (12^3 / 6^3, r05): 512-thread blocks whose two 256-thread halves split the block's 32-channel chunks
+// (half 0 the first ceil(n/2), half 1 the rest), each with its own halo / weight stage buffers, in lockstep through
+// the same barriers; half 1's accumulators are added to half 0's through LDS (fixed order) before the epilogue.
+// At these levels a launch has ~256 blocks, one per CU, so the KW = 1 form runs ONE wave per SIMD and nothing
+// hides a wave's staging and LDS latency; two K-halves give every SIMD a second wave without a global split.
+template <typename T, int BN, int CBZ = 0, int CBY = 0, int CBX = 0, int DBG = 0, bool PF = false, bool B32 = false,
+          int KW = 1>
+__global__ __launch_bounds__(256 * KW, (sizeof(T) == 2 && KW == 1) ? 2 : 1) void conv3_brickr_kernel(
+    GemmArgs g, int bz_rt, int by_rt, int bx_rt, long long* dbg = nullptr) {
   const int bz = CBZ > 0 ? CBZ : bz_rt, by = CBY > 0 ? CBY : by_rt, bx = CBX > 0 ? CBX : bx_rt;
   // DBG 4: every block's (realtime, memtime) at start / end, block 0 wave 0's per-phase memtime stamps
   int dn = 0;
@@ -2162,10 +2168,12 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kern
   constexpr int XQ = br_xq(sizeof(T));
   constexpr int WQ = 9 * BN * L::QV;
   constexpr int EQ = (256 * (BN + 4) * 4 + 15) / 16;   // fp32 epilogue tile
-  constexpr int LQ = (XQ + WQ) > EQ ? (XQ + WQ) : EQ;
+  constexpr int RQ = KW > 1 ? 256 * BN / 4 : 0;           // half 1's accumulators (fp32), after the epilogue tile
+  constexpr int LQ = (KW * (XQ + WQ)) > (EQ + RQ) ? (KW * (XQ + WQ)) : (EQ + RQ);
   __shared__ __attribute__((aligned(16))) float4 lds4[LQ];
-  T* Xl = reinterpret_cast<T*>(lds4);
-  T* Wl = reinterpret_cast<T*>(lds4 + XQ);
+  const int half = KW > 1 ? (int)(threadIdx.x >> 8) : 0;
+  T* Xl = reinterpret_cast<T*>(lds4 + half * (XQ + WQ));
+  T* Wl = reinterpret_cast<T*>(lds4 + half * (XQ + WQ) + XQ);
   constexpr int EPQ = 16 / sizeof(T);
   constexpr int X_PER = (BR_MAXHV * 4 + 255) / 256;
   constexpr int W_ITEMS = 9 * BN * 4;
@@ -2179,7 +2187,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kern
 
   const T* A = reinterpret_cast<const T*>(g.a);
   const T* Bw = reinterpret_cast<const T*>(g.b);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
   const int bz_n = g.D / bz, by_n = g.H / by, bx_n = g.W / bx;
   const int nbrick = (g.M / (g.D * g.H * g.W)) * bz_n * by_n * bx_n;
   const int nt_n = (g.Ncols + BN - 1) / BN;
@@ -2201,8 +2209,14 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kern
   const int cin = 8 << g.cpg_shift;
   const int nchunk = gemm_nchunk(g);
   const int cps = (nchunk + g.ksplit - 1) / g.ksplit;
-  const int c_begin = ks * cps;
-  const int c_end = c_begin + cps < nchunk ? c_begin + cps : nchunk;
+  const int cb0 = ks * cps;
+  const int ce0 = cb0 + cps < nchunk ? cb0 + cps : nchunk;
+  // KW = 2: this half's chunks of the block's range (half 0 takes the larger share when it is odd)
+  const int cmid = cb0 + (ce0 - cb0 + 1) / 2;
+  const int c_begin = KW > 1 && half ? cmid : cb0;
+  const int c_end = KW > 1 ? (half ? ce0 : cmid) : ce0;
+  // iterations every thread of the block runs (the barriers inside the loop are block-wide): half 0's count
+  const int n_iter = ((KW > 1 ? cmid : ce0) - cb0) * 3;
 
   V8<T> xr[X_PER], wr[W_PER];
   const int nvox = n * g.D * g.H * g.W;   // (B32 only: the host checked the extent)
@@ -2299,7 +2313,9 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kern
   }
   __syncthreads();
   stamp();
-  for (int st = st_begin; st < st_end; ++st) {
+  for (int it = 0; it < n_iter; ++it) {
+    const int st = st_begin + it;
+    const bool active = st < st_end;   // (KW = 2: half 1 may own one chunk fewer; it still joins every barrier)
     const int kz = st % 3;
     const int sn = st + 1;
     const bool more = sn < st_end;
@@ -2308,7 +2324,8 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kern
       load_w(cn, kzn);
       if (kzn == 0) load_x(cn);
     }
-    if constexpr (PF) {
+    if (!active) {
+    } else if constexpr (PF) {
       // fragments of tap t+1 are read while tap t's MFMAs run: at one block per CU (one wave per SIMD) nothing
       // else hides the LDS latency (s_memtime: ~4,200 cycles per 9-tap stage against 2,304 of MFMA)
       V8<T> af[2][RM], bf[2][RN];
@@ -2358,38 +2375,63 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kern
     if (more && DBG != 3) {
       store_w();
       if (kzn == 0) store_x();
-      __syncthreads();
     }
+    if (KW > 1 || (more && DBG != 3)) __syncthreads();   // (KW = 2: the halves' `more` may differ)
     stamp();
   }
 
-  // epilogue through LDS: rows < bz*by*bx only
+  // KW = 2: half 1's accumulators added to half 0's (the loop ended with a barrier: the stage buffers are free)
+  if constexpr (KW > 1) {
+    f32x4* R4 = reinterpret_cast<f32x4*>(lds4 + EQ);
+    if (half) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) R4[((wave * RM + i) * RN + j) * 64 + lane] = acc[i][j];
+    }
+    __syncthreads();
+    if (!half) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          const f32x4 o = R4[((wave * RM + i) * RN + j) * 64 + lane];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
+        }
+    }
+  }
+  // epilogue through LDS: rows < bz*by*bx only (KW = 2: half 0 fills the tile, all 512 threads store it)
   auto row_vox = [&](int rr) {
     const int rx = rr % bx, t = rr / bx;
     const int ry = t % by, rz = t / by;
     return nbase + (z0 + rz) * HW + (long long)(y0 + ry) * g.W + (x0 + rx);
   };
+  const int etid = threadIdx.x;
+  constexpr int ET = 256 * KW;
   if (g.ksplit == 1) {
     T* El = reinterpret_cast<T*>(lds4);
     constexpr int EP = BN + 8;
+    if (!half) {
 #pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      const int col = j * 16 + r16;
-      const float bv = (biasp && n0 + col < g.Ncols) ? biasp[n0 + col] : 0.f;
+      for (int j = 0; j < RN; ++j) {
+        const int col = j * 16 + r16;
+        const float bv = (biasp && n0 + col < g.Ncols) ? biasp[n0 + col] : 0.f;
 #pragma unroll
-      for (int i = 0; i < RM; ++i)
+        for (int i = 0; i < RM; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) El[(wave * 64 + i * 16 + kg * 4 + r) * EP + col] = from_f<T>(acc[i][j][r] + bv);
+          for (int r = 0; r < 4; ++r) El[(wave * 64 + i * 16 + kg * 4 + r) * EP + col] = from_f<T>(acc[i][j][r] + bv);
+      }
     }
     __syncthreads();
-    if (g.stats) {
+    if (KW == 1 && g.stats) {
       float* red = reinterpret_cast<float*>(El + 256 * EP);
       const long long brick = (long long)n * (bz_n * by_n * bx_n) + ((long long)bzi * by_n + byi) * bx_n + bxi;
       brick_in_stats<T, BN>(El, EP, rows, red, g.stats, brick, n0, g.Ncols);
     }
     T* O = reinterpret_cast<T*>(g.out);
     constexpr int CG = BN / 8;
-    for (int e = tid; e < rows * CG; e += 256) {
+    for (int e = etid; e < rows * CG; e += ET) {
       const int rr = e / CG, cg = e % CG;
       const int col = n0 + cg * 8;
       if (col < g.Ncols) {
@@ -2401,17 +2443,19 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brickr_kern
   } else {
     float* El = reinterpret_cast<float*>(lds4);
     constexpr int EP = BN + 4;
+    if (!half) {
 #pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      const int col = j * 16 + r16;
+      for (int j = 0; j < RN; ++j) {
+        const int col = j * 16 + r16;
 #pragma unroll
-      for (int i = 0; i < RM; ++i)
+        for (int i = 0; i < RM; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) El[(wave * 64 + i * 16 + kg * 4 + r) * EP + col] = acc[i][j][r];
+          for (int r = 0; r < 4; ++r) El[(wave * 64 + i * 16 + kg * 4 + r) * EP + col] = acc[i][j][r];
+      }
     }
     __syncthreads();
     constexpr int CG = BN / 4;
-    for (int e = tid; e < rows * CG; e += 256) {
+    for (int e = etid; e < rows * CG; e += ET) {
       const int rr = e / CG, cg = e % CG;
       const int col = n0 + cg * 4;
       if (col < g.Ncols) {
@@ -4910,10 +4954,27 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
           MMSEG_LAUNCH((conv3_brickr_kernel<T, 64>), grid, block, 0, s, g, plan.bz, plan.by, plan.bx, (long long*)nullptr);
       }
     } else if (b666) {
-      mmseg::note_kernel("conv3_brickr_kernel<BN32>");
+      // KW = 2 (MMSEG_BRICKR_KW, default 2): two waves per SIMD from an in-block split of the chunks (see the kernel)
+      const bool kw2 = sizeof(T) == 2 && !g.stats && cps >= 2 && knob("MMSEG_BRICKR_KW", 2) == 2;
+      mmseg::note_kernel(kw2 ? "conv3_brickr_kernel<BN32,KW2>" : "conv3_brickr_kernel<BN32>");
       // (MMSEG_BRICKR_PF32: tap t+1's fragments read during tap t's MFMAs -- at 12^3 / 6^3 a CU holds one block;
       // 5-10 % per launch, r04ab convbench)
-      if (rb32 && knob("MMSEG_BRICKR_PF32", 1))
+      bool done = false;
+      if constexpr (sizeof(T) == 2) {   // (the fp32 form's two stage sets exceed the LDS)
+        const bool pf = knob("MMSEG_BRICKR_PF32", 1);
+        const dim3 b2(512);
+        if (kw2 && pf && rb32)
+          MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, true, true, 2>), grid, b2, 0, s, g, 6, 6, 6, nullptr);
+        else if (kw2 && rb32)
+          MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, false, true, 2>), grid, b2, 0, s, g, 6, 6, 6, nullptr);
+        else if (kw2 && pf)
+          MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, true, false, 2>), grid, b2, 0, s, g, 6, 6, 6, nullptr);
+        else if (kw2)
+          MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, false, false, 2>), grid, b2, 0, s, g, 6, 6, 6, nullptr);
+        done = kw2;
+      }
+      if (done) {
+      } else if (rb32 && knob("MMSEG_BRICKR_PF32", 1))
         MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, true, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
       else if (rb32)
         MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, false, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
@@ -5406,6 +5467,14 @@ extern "C" int mmseg_wgrad_reduce_flush(void* stream);
 // Queue a deferred reduce; once the partials queued on its stream pass MMSEG_WRED_FLUSH_MB (0: never), flush them
 // there and then, while they may still sit in the Infinity Cache (the whole step's partials do not).
 int wred_push(const WReduceArgs& r, int groups, void* stream) {
+  // a queued reduce reads its partials when the queue is flushed: a second weight-gradient kernel into the same
+  // partial buffer before that would have overwritten them (the engine flushes first: Runtime.own_part)
+  for (const auto& e : g_wred_pending)
+    if (e.stream == stream && (e.r.part == r.part || (r.bias_part && e.r.bias_part == r.bias_part))) {
+      mmseg::set_error("deferred weight-gradient reduce: its partial buffer is already queued on this stream "
+                       "(flush the queue before reusing it)");
+      return -1;
+    }
   g_wred_pending.push_back({r, groups, stream});
   const long long cap = (long long)knob("MMSEG_WRED_FLUSH_MB", 0) << 20;
   if (cap <= 0) return 0;

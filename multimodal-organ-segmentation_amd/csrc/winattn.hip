@@ -219,6 +219,117 @@ __global__ __launch_bounds__(512) void winattn_fwd_kernel(WinAttnArgs a) {
   }
 }
 
+// ------------------------------------------------------ forward, one pass
+// (r05; default, MMSEG_WINATTN_FWD1=0 restores winattn_fwd_kernel.)  A query tile's whole score row stays in
+// registers (22 key tiles x 4 keys per lane = 88 VGPRs), so the scores, their bias / mask and the exponentials are
+// computed ONCE instead of twice (the two-pass form recomputed S^T and exp for P V): the kernel was VALU-issue-bound
+// at ~50 VALU instructions per MFMA (r05a SQ counters).  Scores are taken in the log2 domain (the table and the scale
+// pre-multiplied by log2 e, so a score is one FMA and its exponential one v_exp_f32), P V runs on the full-rate
+// 16x16x32 MFMA (two key tiles per instruction, keys permuted identically in P and V), and O is divided by the row
+// sum after the product (4 multiplies per lane instead of one per score).  The stored lse is the natural-log one the
+// backward expects.
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+__device__ __forceinline__ bf16x8 cat44(s4 a, s4 b) {
+  typedef short s8 __attribute__((ext_vector_type(8)));
+  const s8 t = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, t);
+}
+
+__global__ __launch_bounds__(512) void winattn_fwd1_kernel(WinAttnArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Vt[16][TP];
+  __shared__ float tab[TMAX];
+  __shared__ __attribute__((aligned(16))) int code[NPMAX];
+  __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
+  const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads;
+  const int np = (a.N + 15) & ~15, nt = np / 16;
+  const Stage st{b, h, a.N, np};
+  const int C3 = 3 * a.C, hoff = h * a.hd;
+  stage_rows(Qs, a.qkv, C3, hoff, st, a.hd, nullptr);
+  stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, nullptr);
+  stage_rows(nullptr, a.qkv, C3, 2 * a.C + hoff, st, a.hd, Vt);
+  {
+    const float* row = a.table + (long long)h * a.T;
+    for (int t = threadIdx.x; t < a.T; t += blockDim.x) tab[t] = row[t] * LOG2E;
+  }
+  stage_codes(code, a, np);
+  stage_region(reg, a, b);
+  __syncthreads();
+  const float* ctab = tab + code_off(a);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const float sc2 = a.scale * LOG2E, pen2 = 100.0f * LOG2E;
+  const s4 z4 = {0, 0, 0, 0};
+  for (int qt = wave; qt < nt; qt += WAVES) {
+    const int q = qt * 16 + r16;
+    const s4 bq = ld4(&Qs[q][4 * g4]);
+    const bool qv = q < a.N;
+    const float* tq = ctab + code[q];
+    const uint32_t rq = reg[q];
+    float v[NTMAX][4];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NTMAX; ++kt) {
+      if (kt < nt) {
+        const f32x4 acc = mma(ld4(&Ks[kt * 16 + r16][4 * g4]), bq, (f32x4){0.f, 0.f, 0.f, 0.f});
+        const int k0 = kt * 16 + 4 * g4;
+        const int4 ck = *reinterpret_cast<const int4*>(code + k0);
+        const uint32_t rk = a.region ? *reinterpret_cast<const uint32_t*>(reg + k0) : 0u;
+        const int c[4] = {ck.x, ck.y, ck.z, ck.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float t = fmaf(acc[r], sc2, tq[-c[r]]);
+          if (a.region && ((rk >> (8 * r)) & 255u) != rq) t -= pen2;
+          v[kt][r] = (qv && k0 + r < a.N) ? t : -INFINITY;
+          mx = fmaxf(mx, v[kt][r]);
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NTMAX; ++kt) {
+      if (kt < nt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = v[kt][r] == -INFINITY ? 0.f : exp2f(v[kt][r] - mx);
+          v[kt][r] = p;
+          sum += p;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) sum += __shfl_xor(sum, o, 64);
+    if (g4 == 0 && qv) a.lse[(long long)bh * NPMAX + q] = (mx + log2f(sum)) * LN2;
+    const float inv = sum > 0.f ? 1.f / sum : 0.f;
+    f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c2 = 0; c2 < NTMAX / 2; ++c2) {
+      const int k0 = 2 * c2;
+      if (k0 < nt) {
+        const bool hi = k0 + 1 < nt;
+        const s4 pa = pack4(v[k0][0], v[k0][1], v[k0][2], v[k0][3]);
+        const s4 pb = hi ? pack4(v[k0 + 1][0], v[k0 + 1][1], v[k0 + 1][2], v[k0 + 1][3]) : z4;
+        const s4 va = ld4(&Vt[r16][k0 * 16 + 4 * g4]);
+        const s4 vb = hi ? ld4(&Vt[r16][(k0 + 1) * 16 + 4 * g4]) : z4;
+        o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat44(pa, pb), cat44(va, vb), o, 0, 0, 0);
+      }
+    }
+    if (r16 < a.hd) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = qt * 16 + 4 * g4 + r;
+        const float ir = __shfl(inv, 4 * g4 + r, 64);   // the row sum of query qq (held by lane qq % 16)
+        if (qq < a.N) a.out[(long long)(b * a.N + qq) * a.C + hoff + r16] = (bf16_t)(o[r] * ir);
+      }
+    }
+  }
+}
+
 // D[q] = sum_d dO[q][d] O[q][d] of this head (fp32), staged into LDS
 __device__ __forceinline__ void stage_D(float* Dq, const WinAttnArgs& a, const Stage& s) {
   for (int n = threadIdx.x; n < s.np; n += blockDim.x) {
@@ -500,6 +611,11 @@ int qb_windows_per_group(int B, int N, int heads) {
   return (B + nwg - 1) / nwg;
 }
 
+int knob_i(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
 int check_args(const WinAttnArgs& a) {
   MMSEG_REQUIRE(a.N >= 1 && a.N <= NPMAX && a.hd >= 1 && a.hd <= 16 && a.hd % 8 == 0 && a.C == a.heads * a.hd &&
                     a.T <= TMAX && a.T == (2 * a.w0 - 1) * (2 * a.w1 - 1) * (2 * a.w2 - 1) &&
@@ -519,7 +635,13 @@ int mmseg_winattn_fwd(const void* qkv, int B, int N, int C, int heads, const flo
   WinAttnArgs a{(const bf16_t*)qkv, nullptr, nullptr, (bf16_t*)O, lse, nullptr, table, region,
                 B, N, C, heads, C / heads, nw, T, 0, w0, w1, w2, scale};
   if (check_args(a)) return 1;
-  MMSEG_LAUNCH(winattn_fwd_kernel, dim3(B * heads), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+  if (knob_i("MMSEG_WINATTN_FWD1", 1)) {
+    mmseg::note_kernel("winattn_fwd1_kernel");
+    MMSEG_LAUNCH(winattn_fwd1_kernel, dim3(B * heads), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+  } else {
+    mmseg::note_kernel("winattn_fwd_kernel");
+    MMSEG_LAUNCH(winattn_fwd_kernel, dim3(B * heads), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+  }
   return mmseg::check_launch("winattn_fwd");
 }
 

@@ -94,6 +94,9 @@ class GradBuckets:
             self.buckets.append((lo, hi, param_offsets[lo], param_offsets[hi - 1] + param_sizes[hi - 1]))
             hi = lo
         self.comm = None
+        # called on the compute stream right before a bucket's collective is issued: the engine's batched
+        # weight-gradient reduces (Runtime.flush_wred) still queued then write that bucket's gradients first
+        self.pre_reduce = None
         self.owner = [0] * len(param_offsets)
         for b, (lo, hi, _, _) in enumerate(self.buckets):
             for i in range(lo, hi):
@@ -150,12 +153,14 @@ class GradBuckets:
         if not self.active:
             return
         b = self.owner[idx]
+        self.pending[b] -= 1
+        if self.pending[b] == 0 and self.pre_reduce is not None:
+            self.pre_reduce()
         if self.grad.is_cuda:
             cur = torch.cuda.current_stream(self.grad.device)
             ev = torch.cuda.Event()
             ev.record(cur)
             self.events[b][cur.cuda_stream] = ev
-        self.pending[b] -= 1
         if self.pending[b] == 0:
             self._reduce(b)
 
@@ -163,6 +168,8 @@ class GradBuckets:
         if not self.active:
             return
         late = [b for b, n in enumerate(self.pending) if n > 0]
+        if late and self.pre_reduce is not None:
+            self.pre_reduce()
         if late and self.grad.is_cuda:
             # writes to unreported parameters may still be queued on the current stream: the late
             # collectives wait for everything issued on it so far

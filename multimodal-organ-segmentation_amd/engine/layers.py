@@ -31,11 +31,8 @@ TARGET_BLOCKS = 1024
 
 
 def _own_part(obj, rt: Runtime, nfloats: int) -> torch.Tensor:
-    """A split-partial buffer of obj's own (its reduce is queued: Runtime.defer_wred)."""
-    buf = getattr(obj, "_wpart", None)
-    if buf is None or buf.numel() < nfloats:
-        buf = obj._wpart = torch.empty(int(nfloats), dtype=torch.float32, device=rt.device)
-    return buf
+    """A split-partial buffer of obj's own (its reduce is queued: Runtime.defer_wred / Runtime.own_part)."""
+    return rt.own_part(obj, nfloats)
 
 
 def _gemm_name(rt: Runtime, ncols: int, mode: str):
@@ -318,6 +315,8 @@ class Conv3:
         96^3 DualEncoder, fit HBM many times over)."""
         if not self.rt.async_wred and not own:
             return self.rt.ws(nfloats)
+        if own:
+            return self.rt.own_part(self, nfloats)
         buf = getattr(self, "_wpart", None)
         if buf is None or buf.numel() < nfloats:
             buf = self._wpart = torch.empty(int(nfloats), dtype=torch.float32, device=self.rt.device)
@@ -489,9 +488,11 @@ class ConvT2:
         ncols = 8 * self.Co
         ks = _gemm_ksplit(M, ncols, self.KG)
         ws = self.rt.ws(ks * M * ncols) if ks > 1 else None
-        self.rt.lib.mmseg_conv_gemm(x.ptr, x.ld, ptr(self.wf), ptr(self.up.bias), y.ptr, y.ld, ptr(ws),
-                                    MODE_CONVT_FWD, M, ncols, self.Cpad, self.KG, 0, x.D, x.H, x.W, ks, self.rt.code,
-                                    self.rt.stream)
+        with TIMER.region(_gemm_name(self.rt, 0, "convT"), flops=2.0 * M * self.Ci * 8 * self.Co,
+                          nbytes=_io_bytes(self.rt, M, self.Ci, 8 * self.Co, 8 * self.Ci * self.Co)):
+            self.rt.lib.mmseg_conv_gemm(x.ptr, x.ld, ptr(self.wf), ptr(self.up.bias), y.ptr, y.ld, ptr(ws),
+                                        MODE_CONVT_FWD, M, ncols, self.Cpad, self.KG, 0, x.D, x.H, x.W, ks,
+                                        self.rt.code, self.rt.stream)
 
     def bwd(self, x: Act, dy: Act, dx: Optional[Act], accumulate: bool):
         """x: input grid (D,H,W); dy: output grid (2D,2H,2W)."""
@@ -523,8 +524,10 @@ class ConvT2:
         if dx is not None:
             ks = _gemm_ksplit(V, self.Ci, self.KGd)
             ws = self.rt.ws(ks * V * self.Ci) if ks > 1 else None
-            L.mmseg_conv_gemm(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, ptr(ws), MODE_CONVT_DGRAD, V, self.Ci,
-                              self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, ks, code, s)
+            with TIMER.region(_gemm_name(self.rt, 0, "convT"), flops=2.0 * V * self.Ci * 8 * self.Co,
+                              nbytes=_io_bytes(self.rt, V, 8 * self.Co, self.Ci, 8 * self.Ci * self.Co)):
+                L.mmseg_conv_gemm(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, ptr(ws), MODE_CONVT_DGRAD, V,
+                                  self.Ci, self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, ks, code, s)
 
 
 class Point:
@@ -549,8 +552,11 @@ class Point:
 
     def fwd(self, x: Act, y: Act):
         M = x.N * x.V
-        self.rt.lib.mmseg_conv_gemm(x.ptr, x.ld, ptr(self.wf), ptr(self.conv.bias), y.ptr, y.ld, None, MODE_POINT, M,
-                                    self.Co, self.Cpad, self.KG, 0, x.D, x.H, x.W, 1, self.rt.code, self.rt.stream)
+        with TIMER.region(_gemm_name(self.rt, 0, "point"), flops=2.0 * M * self.Ci * self.Co,
+                          nbytes=_io_bytes(self.rt, M, self.Ci, self.Co, self.Ci * self.Co)):
+            self.rt.lib.mmseg_conv_gemm(x.ptr, x.ld, ptr(self.wf), ptr(self.conv.bias), y.ptr, y.ld, None, MODE_POINT,
+                                        M, self.Co, self.Cpad, self.KG, 0, x.D, x.H, x.W, 1, self.rt.code,
+                                        self.rt.stream)
 
     def bwd(self, x: Act, dy: Act, dx: Optional[Act], accumulate: bool):
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
@@ -560,15 +566,19 @@ class Point:
         nfl = ks * self.Co * self.Ci + ks * self.Co
         part = _own_part(self, self.rt, nfl) if defer else self.rt.ws(nfl)
         bpart = part.data_ptr() + ks * self.Co * self.Ci * 4
-        L.mmseg_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, ptr(part), bpart, MODE_POINT, self.Co, self.Ci, 0, V, x.D, x.H, x.W,
-                      ks, code, s)
+        with TIMER.region(_gemm_name(self.rt, 0, "point"), flops=2.0 * V * self.Ci * self.Co,
+                          nbytes=_io_bytes(self.rt, V, self.Ci, self.Co, self.Ci * self.Co, 4)):
+            L.mmseg_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, ptr(part), bpart, MODE_POINT, self.Co, self.Ci, 0, V, x.D, x.H,
+                          x.W, ks, code, s)
         (L.mmseg_wgrad_reduce_defer if defer else L.mmseg_wgrad_reduce)(
             ptr(part), ptr(self.flat.grad(self.conv.weight)), bpart, ptr(self.flat.grad(self.conv.bias)), self.Co,
             self.Ci, ks, self.Ci, self.Ci, 1, int(accumulate), s)
         self.flat.mark(self.conv.weight, self.conv.bias)
         if dx is not None:
-            L.mmseg_conv_gemm(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, None, MODE_POINT, V, self.Ci,
-                              self.Cpad_d, self.KGd, 0, x.D, x.H, x.W, 1, code, s)
+            with TIMER.region(_gemm_name(self.rt, 0, "point"), flops=2.0 * V * self.Ci * self.Co,
+                              nbytes=_io_bytes(self.rt, V, self.Co, self.Ci, self.Ci * self.Co)):
+                L.mmseg_conv_gemm(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, None, MODE_POINT, V, self.Ci,
+                                  self.Cpad_d, self.KGd, 0, x.D, x.H, x.W, 1, code, s)
 
 
 class Block:

@@ -49,15 +49,20 @@ class KernelTimer:
         self._lib().mmseg_timing_end()
 
     @contextmanager
-    def region(self, name, flops: float = 0.0, nbytes: float = 0.0):
-        """`name` may be a callable evaluated after the launch (e.g. the kernel the library chose)."""
+    def region(self, name, flops: float = 0.0, nbytes: float = 0.0, more=()):
+        """`name` may be a callable evaluated after the launch (e.g. the kernel the library chose).  `more`:
+        further (name, flops, bytes) of other main kernels of the same entry point (an entry that launches two
+        MFMA kernels, e.g. the window-attention backward), each matched to its own launch."""
         if not self.enabled:
             yield
             return
         L = self._lib()
         i0 = L.mmseg_timing_count()
         yield
-        self.regions.append((name() if callable(name) else name, flops, nbytes, i0, L.mmseg_timing_count()))
+        i1 = L.mmseg_timing_count()
+        self.regions.append((name() if callable(name) else name, flops, nbytes, i0, i1))
+        for nm, fl, nb in more:
+            self.regions.append((nm, fl, nb, i0, i1))
 
     def launches(self):
         """[(launch-site kernel expression, ms)] of every library launch in the window."""
@@ -75,14 +80,19 @@ class KernelTimer:
         """Per launch, in issue order: (family, launch-site kernel, ms, flops, bytes)."""
         launches = self.launches()
         owner = {}
+        mains = set()
         for name, fl, nb, i0, i1 in self.regions:
             if i1 <= i0:
                 continue
             want = _base(name)
-            main = next((i for i in range(i0, i1) if _base(launches[i][0]) == want),
+            main = next((i for i in range(i0, i1) if _base(launches[i][0]) == want and i not in mains),
                         max(range(i0, i1), key=lambda i: launches[i][1]))
+            mains.add(main)
             for i in range(i0, i1):
-                owner[i] = (name, fl, nb) if i == main else (_base(launches[i][0]), 0.0, 0.0)
+                if i == main:
+                    owner[i] = (name, fl, nb)
+                elif i not in mains:
+                    owner[i] = (_base(launches[i][0]), 0.0, 0.0)
         out = []
         for i, (site, ms) in enumerate(launches):
             name, fl, nb = owner.get(i, (_base(site), 0.0, 0.0))

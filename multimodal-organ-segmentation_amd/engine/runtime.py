@@ -87,6 +87,8 @@ class Runtime:
         # gradient as soon as it is final); MMSEG_WRED_BATCH=0 restores one reduce per layer
         self.batch_wred = os.environ.get("MMSEG_WRED_BATCH", "1") != "0"
         self._wred_active = False
+        self._wred_session = 0          # id of the current backward session (own_part's reuse check)
+        self._wred_flush_hook = None    # DP: flushes the queued reduces before a gradient bucket is reduced
 
     # ---------------------------------------------------------------- alloc
     def act(self, N: int, D: int, H: int, W: int, C: int, ld: Optional[int] = None) -> Act:
@@ -120,14 +122,38 @@ class Runtime:
         return torch.cuda.stream(self._side)
 
     def defer_wred(self, flat: Optional["FlatParams"]) -> bool:
-        """Queue this layer's split reduce until the session ends (see batch_wred)."""
+        """Queue this layer's split reduce until the session ends (see batch_wred).  Under DP gradient buckets the
+        queue is flushed before each bucket's collective (FlatParams.flush_before_ready), so the bucketed step
+        runs the same batched reduces as the single-GPU one."""
         return (self._wred_active and not self.async_wred
-                and (flat is None or flat.on_ready is None))
+                and (flat is None or flat.on_ready is None or flat.flush_before_ready is not None))
+
+    def own_part(self, obj, nfloats: int) -> torch.Tensor:
+        """The split-partial buffer of `obj`'s own for a queued (deferred) reduce.  If obj already queued a reduce
+        in this session (a layer whose backward runs twice before the flush), that reduce still has to read the
+        buffer: flush the queue first, so the new weight-gradient kernel cannot overwrite partials a queued reduce
+        has not summed yet."""
+        if getattr(obj, "_wpart_session", None) == self._wred_session and self._wred_active:
+            self.flush_wred()
+        obj._wpart_session = self._wred_session
+        buf = getattr(obj, "_wpart", None)
+        if buf is None or buf.numel() < nfloats:
+            buf = obj._wpart = torch.empty(int(nfloats), dtype=torch.float32, device=self.device)
+        return buf
+
+    def flush_wred(self) -> None:
+        """Launch every queued reduce of the current stream now (one batched launch)."""
+        n = self.lib.mmseg_wgrad_reduce_flush(self.stream)
+        if n < 0:
+            raise RuntimeError("mmseg_wgrad_reduce_flush: " + self.lib.mmseg_last_error().decode(errors="replace"))
+        # every earlier queued buffer is free again: a layer may defer once more in this session
+        self._wred_session += 1
 
     @contextmanager
     def wred_session(self):
         """A backward whose split reduces may be batched; flushed (one launch) on exit."""
         self._wred_active = self.batch_wred
+        self._wred_session += 1
         try:
             yield
         except BaseException:
@@ -136,9 +162,7 @@ class Runtime:
         finally:
             self._wred_active = False
         if self.batch_wred:
-            n = self.lib.mmseg_wgrad_reduce_flush(self.stream)
-            if n < 0:
-                raise RuntimeError("mmseg_wgrad_reduce_flush: " + self.lib.mmseg_last_error().decode(errors="replace"))
+            self.flush_wred()
 
     def join_side(self) -> None:
         """The current stream waits for all side-stream work (end of the backward: the gradients are final)."""
@@ -171,6 +195,9 @@ class FlatParams:
         self.index: Dict[int, int] = {id(p): i for i, p in enumerate(self.params)}
         self.sizes = [p.numel() for p in self.params]
         self.on_ready = None      # callback(param_index) once the param's gradient is final (DP buckets)
+        # DP with batched weight-gradient reduces: called (by the buckets) right before a bucket's collective is
+        # issued, so the reduces still queued in the library have written that bucket's gradients
+        self.flush_before_ready = None
 
     def mark(self, *params: torch.nn.Parameter) -> None:
         if self.on_ready is not None:

@@ -33,7 +33,9 @@ import torch.nn as nn
 
 from .._lib import ptr
 from .attention import WindowAttentionEngine
-from .layers import MODE_POINT, Conv3, ConvT2, Head, Packer, _col_tile, _gemm_ksplit, _own_part, _wgrad_ksplit
+from .layers import (MODE_POINT, Conv3, ConvT2, Head, Packer, _col_tile, _gemm_ksplit, _gemm_name, _io_bytes,
+                     _own_part, _wgrad_ksplit)
+from .profiler import TIMER
 from .runtime import Act, FlatParams, Runtime, round_up
 
 LN_EPS = 1e-5
@@ -117,8 +119,10 @@ class Lin:
     def fwd(self, x: torch.Tensor, ldx: int, M: int, y: torch.Tensor, ldy: int):
         ks = _gemm_ksplit(M, self.Co, self.KG)
         ws = self.rt.ws(ks * M * self.Co) if ks > 1 else None
-        self.rt.lib.mmseg_conv_gemm(ptr(x), ldx, ptr(self.wf), ptr(self.b), ptr(y), ldy, ptr(ws), MODE_POINT, M,
-                                    self.Co, self.Cpad, self.KG, 0, 1, 1, 1, ks, self.rt.code, self.rt.stream)
+        with TIMER.region(_gemm_name(self.rt, 0, "point"), flops=2.0 * M * self.Ci * self.Co,
+                          nbytes=_io_bytes(self.rt, M, self.Cip, self.Co, self.Ci * self.Co)):
+            self.rt.lib.mmseg_conv_gemm(ptr(x), ldx, ptr(self.wf), ptr(self.b), ptr(y), ldy, ptr(ws), MODE_POINT, M,
+                                        self.Co, self.Cpad, self.KG, 0, 1, 1, 1, ks, self.rt.code, self.rt.stream)
 
     def bwd(self, x: torch.Tensor, ldx: int, dy: torch.Tensor, lddy: int, M: int, dx: Optional[torch.Tensor],
             lddx: int, accumulate: bool):
@@ -128,8 +132,10 @@ class Lin:
         nfl = ks * self.Co * self.Cip + ks * self.Co + 4
         part = _own_part(self, self.rt, nfl) if defer else self.rt.ws(nfl)
         bpart = part.data_ptr() + round_up(ks * self.Co * self.Cip, 4) * 4 if self.b is not None else None
-        L.mmseg_wgrad(ptr(dy), lddy, ptr(x), ldx, ptr(part), bpart, MODE_POINT, self.Co, self.Cip, 0, M, 1, 1, 1, ks,
-                      code, s)
+        with TIMER.region(_gemm_name(self.rt, 0, "point"), flops=2.0 * M * self.Ci * self.Co,
+                          nbytes=_io_bytes(self.rt, M, self.Cip, self.Co, self.Ci * self.Co, 4)):
+            L.mmseg_wgrad(ptr(dy), lddy, ptr(x), ldx, ptr(part), bpart, MODE_POINT, self.Co, self.Cip, 0, M, 1, 1, 1,
+                          ks, code, s)
         (L.mmseg_wgrad_reduce_defer if defer else L.mmseg_wgrad_reduce)(
             ptr(part), ptr(self.flat.grad(self.w)), bpart, ptr(self.flat.grad(self.b)) if self.b is not None else None,
             self.Co, self.Cip, ks, self.Cip, self.Ci, 1, int(accumulate), s)
@@ -137,8 +143,10 @@ class Lin:
         if dx is not None:
             kd = _gemm_ksplit(M, self.Ci, self.KGd)
             ws = self.rt.ws(kd * M * self.Ci) if kd > 1 else None
-            L.mmseg_conv_gemm(ptr(dy), lddy, ptr(self.wd), None, ptr(dx), lddx, ptr(ws), MODE_POINT, M, self.Ci,
-                              self.Cpad_d, self.KGd, 0, 1, 1, 1, kd, code, s)
+            with TIMER.region(_gemm_name(self.rt, 0, "point"), flops=2.0 * M * self.Ci * self.Co,
+                              nbytes=_io_bytes(self.rt, M, self.Co, self.Ci, self.Ci * self.Co)):
+                L.mmseg_conv_gemm(ptr(dy), lddy, ptr(self.wd), None, ptr(dx), lddx, ptr(ws), MODE_POINT, M, self.Ci,
+                                  self.Cpad_d, self.KGd, 0, 1, 1, 1, kd, code, s)
 
 
 class LN:
@@ -252,8 +260,11 @@ class SwinBlockProg:
             nw = region.shape[0] if region is not None else 0
             w0, w1, w2 = geo["window"]
             tabT = self._table_t()
-            L.mmseg_winattn_fwd(ptr(qkv), B, Nw, C, self.heads, ptr(tabT), self.table.shape[0], w0, w1, w2,
-                                ptr(region), nw, self.core.scale, ptr(O), ptr(P), s)
+            # algorithmic work: S = Q K^T and O = P V, 2 * 2 * Nw^2 * hd per (window, head); bytes: q, k, v in, O out
+            with TIMER.region(lambda: L.mmseg_last_kernel().decode(), flops=4.0 * B * Nw * Nw * C,
+                              nbytes=2.0 * Mw * 4 * C):
+                L.mmseg_winattn_fwd(ptr(qkv), B, Nw, C, self.heads, ptr(tabT), self.table.shape[0], w0, w1, w2,
+                                    ptr(region), nw, self.core.scale, ptr(O), ptr(P), s)
         else:
             O, P = self.core.core_fwd(qkv, B, Nw, mask, self.table, geo["index"])
         aw = self._empty(Mw * C)
@@ -322,19 +333,24 @@ class SwinBlockProg:
             # many windows: the score gradient summed over window groups on chip (fp32, mmseg_winattn_bwd_sum),
             # so the bias-table gradient folds a few group sums instead of every window's bf16 dS
             ng = L.mmseg_winattn_sum_groups(B, Nw, self.heads) if os.environ.get("MMSEG_WINATTN_SUM", "1") != "0" else 0
+            # algorithmic backward work: dP = dO V^T, dV = P^T dO, dK = dS^T Q (the key pass, 3 x 2 Nw^2 hd) and
+            # dQ = dS K (the query pass, 2 Nw^2 hd); the recomputed scores are not counted
+            kv_w = ("winattn_bwd_kv_kernel", 6.0 * B * Nw * Nw * C, 2.0 * Mw * 8 * C)
             if ng > 0:
                 dsum = torch.empty(ng * self.heads * Nw * ldn, dtype=torch.float32, device=rt.device)
-                L.mmseg_winattn_bwd_sum(ptr(st["qkv"]), ptr(st["O"]), ptr(dO), ptr(st["P"]), B, Nw, C, self.heads,
-                                        ptr(self._table_t()), self.table.shape[0], w0, w1, w2, ptr(region), nw,
-                                        self.core.scale, ptr(dqkv), ptr(dsum), ldn, s)
+                with TIMER.region(*kv_w, more=[("winattn_bwd_qb_kernel", 2.0 * B * Nw * Nw * C, 2.0 * Mw * 7 * C)]):
+                    L.mmseg_winattn_bwd_sum(ptr(st["qkv"]), ptr(st["O"]), ptr(dO), ptr(st["P"]), B, Nw, C,
+                                            self.heads, ptr(self._table_t()), self.table.shape[0], w0, w1, w2,
+                                            ptr(region), nw, self.core.scale, ptr(dqkv), ptr(dsum), ldn, s)
                 L.mmseg_relpos_table_grad(ptr(dsum), ldn, ng, self.heads, Nw, ptr(dB), ptr(offs), ptr(pairs), T,
                                           ptr(self.flat.grad(self.table)), int(accumulate), 0, s)   # dsum: fp32
                 del dsum
             else:
                 dS = self._empty(B * self.heads * Nw * ldn)
-                L.mmseg_winattn_bwd(ptr(st["qkv"]), ptr(st["O"]), ptr(dO), ptr(st["P"]), B, Nw, C, self.heads,
-                                    ptr(self._table_t()), self.table.shape[0], w0, w1, w2, ptr(region), nw,
-                                    self.core.scale, ptr(dqkv), ptr(dS), ldn, s)
+                with TIMER.region(*kv_w, more=[("winattn_bwd_q_kernel", 2.0 * B * Nw * Nw * C, 2.0 * Mw * 7 * C)]):
+                    L.mmseg_winattn_bwd(ptr(st["qkv"]), ptr(st["O"]), ptr(dO), ptr(st["P"]), B, Nw, C, self.heads,
+                                        ptr(self._table_t()), self.table.shape[0], w0, w1, w2, ptr(region), nw,
+                                        self.core.scale, ptr(dqkv), ptr(dS), ldn, s)
                 L.mmseg_relpos_table_grad(ptr(dS), ldn, B, self.heads, Nw, ptr(dB), ptr(offs), ptr(pairs), T,
                                           ptr(self.flat.grad(self.table)), int(accumulate), code, s)
                 del dS

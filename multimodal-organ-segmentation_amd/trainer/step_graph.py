@@ -80,6 +80,14 @@ class StepGraphs:
             from ..distributed import ddp
             if ddp.backend() != "nccl" or os.environ.get("MMSEG_STEP_GRAPH_DP", "1") == "0":
                 return False
+            if ddp.world() > 1 and not getattr(self, "_warned_dp", False):
+                # bitwise-tested at world size 1 over RCCL (test_rccl_dp_step_captured_bitwise_equal_to_eager);
+                # across several ranks (collectives recorded in each rank's graph, every rank capturing at the same
+                # step because all key their graphs on the same batch sequence) it has not run on hardware yet
+                import warnings
+                warnings.warn("captured data-parallel step over RCCL with world size > 1: verified at world size 1 "
+                              "only; MMSEG_STEP_GRAPH_DP=0 keeps the DP step eager", RuntimeWarning, stacklevel=2)
+                self._warned_dp = True
         if os.environ.get("MMSEG_MODALITY_STREAMS", "0") != "0":
             return False
         opt = tr.optimizer

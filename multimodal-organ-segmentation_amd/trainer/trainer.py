@@ -163,6 +163,18 @@ class Trainer:
             self._buckets = ddp.GradBuckets(flat.grad_flat, flat.offsets, flat.sizes, bucket_mb=mb, force=True)
         flat.on_ready = self._buckets.param_ready if communicate else None
         self._buckets.guard = guard if communicate else None
+        # the batched weight-gradient reduces stay on under DP: the queue is flushed right before each bucket's
+        # collective (one batched launch per bucket instead of one reduce launch per layer)
+        bb = getattr(self.model, "backbone", self.model)
+        rt = getattr(bb.__dict__.get("_engine"), "rt", None)
+        batched = (communicate and rt is not None and rt.batch_wred
+                   and os.environ.get("MMSEG_DP_WRED_BATCH", "1") != "0")
+        flat.flush_before_ready = rt.flush_wred if batched else None
+
+        def pre_reduce():
+            if rt._wred_active:       # inside the backward session: the queue may hold this bucket's reduces
+                rt.flush_wred()
+        self._buckets.pre_reduce = pre_reduce if batched else None
 
     def _fused_loss(self, images: torch.Tensor, labels: torch.Tensor) -> Optional[torch.Tensor]:
         """The step's loss through the fused head + loss node when the model / loss / shape allow it, else None.
@@ -259,9 +271,11 @@ class Trainer:
         bad = guard.reshape(()).sign()
         self._deferred_bad = bad if self._deferred_bad is None else self._deferred_bad.add_(bad)
 
-    def check_deferred(self) -> None:
+    def _take_deferred(self) -> int:
+        """Count of earlier sync=False steps whose labels were out of range (their step counts rolled back,
+        gradients cleared); resets the device counter."""
         if self._deferred_bad is None:
-            return
+            return 0
         # under DP each step's guard was summed over the ranks by the first gradient bucket, so every rank
         # counts the same steps and raises together
         nbad, self._deferred_bad = int(self._deferred_bad.item()), None
@@ -269,9 +283,18 @@ class Trainer:
             for _ in range(nbad):
                 self.optimizer.undo_step_count()
             self.optimizer.zero_grad()
-            raise RuntimeError(f"{nbad} earlier training step(s) had target voxels with a class index outside "
-                               "[0, num_classes) (the reference raises in F.one_hot / cross_entropy on such "
-                               "labels); their updates were skipped")
+        return nbad
+
+    @staticmethod
+    def _deferred_error(nbad: int) -> RuntimeError:
+        return RuntimeError(f"{nbad} earlier training step(s) had target voxels with a class index outside "
+                            "[0, num_classes) (the reference raises in F.one_hot / cross_entropy on such "
+                            "labels); their updates were skipped")
+
+    def check_deferred(self) -> None:
+        nbad = self._take_deferred()
+        if nbad:
+            raise self._deferred_error(nbad)
 
     def _torch_step(self, images, labels, boundary: bool, sync: bool):
         """The reference's per-batch body (trainer.py:236-258) on the torch-op backend."""
@@ -300,16 +323,28 @@ class Trainer:
         return out.item() if sync else out
 
     def _after_step(self, lv: float, guard, boundary: bool, guarded: bool) -> float:
-        """Host side of a synchronous step: raise (on every rank) when the step's labels were out of range."""
-        self.check_deferred()
+        """Host side of a synchronous step: raise (on every rank) when the step's labels were out of range.
+        The current step's guard is handled first (its step count rolled back when the kernel skipped it), then
+        the earlier deferred steps', so one raise reports both and neither's bookkeeping is skipped."""
+        cur_bad = False
         if guard is not None and (lv != lv or self.world > 1):
             if self.world > 1 and (not boundary or self._buckets is None):
                 ddp.allreduce_sum_(guard)      # no bucket carried it on this micro-step
             if guard.item():                 # every rank sees the summed count and raises together
+                cur_bad = True
                 if guarded:
                     self.optimizer.undo_step_count()    # the kernel skipped the update
                 self.optimizer.zero_grad()
+        nbad = self._take_deferred()
+        if cur_bad:
+            try:
                 self.criterion.check_labels()
+            except RuntimeError as e:
+                if nbad:
+                    raise RuntimeError(f"{e}; and {self._deferred_error(nbad)}") from None
+                raise
+        if nbad:
+            raise self._deferred_error(nbad)
         return lv
 
     def _train_epoch(self) -> float:

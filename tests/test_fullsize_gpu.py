@@ -243,6 +243,49 @@ def test_fullsize_step_pinned_to_fp64_oracle(dev, tag, dtype, group, monkeypatch
     assert max(dead.values()) < PINNED_DEAD[dtype], dead
 
 
+def test_group_force_runs_other_kernels(dev, monkeypatch):
+    """Why group=1 and group=noforce above are two checks, not one: forced grouping (MMSEG_GROUP_FORCE_R, default)
+    runs the 48^3 / 24^3 encoder levels as ONE launch over both modalities on the runtime-brick kernels
+    (conv3_brickr / wgrad_brickr), while noforce runs them per modality on the (4, 8, 8)-brick family (brick2 /
+    brick8 / brick3 / wgrad_dma), whose split-K and accumulation orders differ.  Same bf16 c3 step, both modes in
+    one process on the same inputs and weights: the launched kernel families differ, and so (by rounding, not
+    bitwise) do the gradients -- each mode is then held to the pinned fp64 oracle by the parametrized test."""
+    from mmseg_amd.engine.profiler import TIMER
+    model, mods, loss = CASES["fullgrad_dual_c3"]
+    x, y, _ = full_inputs(96, 2, 2, 6, 11)
+    x, y = x.to(dev), y.to(dev)
+    out = {}
+    for mode in ("1", "noforce"):
+        monkeypatch.setenv("MMSEG_GROUP_FORCE_R", "0" if mode == "noforce" else "1")
+        cfg = _config(model, mods, loss, "bfloat16")
+        torch.manual_seed(3)
+        m = build_model(cfg)
+        tr = Trainer(cfg, m)
+        m.train()
+        TIMER.start()
+        lossv = tr._fused_loss(x, y)
+        lossv.backward()
+        TIMER.stop()
+        fams = {}
+        for fam, *_ in TIMER.records():
+            fams[fam] = fams.get(fam, 0) + 1
+        prog = m.backbone.__dict__["_engine"].program
+        out[mode] = (prog.l0, fams, torch.cat([p.grad.reshape(-1).float() for p in m.parameters()]).clone(),
+                     float(lossv))
+        del m, tr
+    (l0f, ff, gf, lf), (l0n, fn, gn, ln) = out["1"], out["noforce"]
+    only_f = sorted(k for k in ff if ff[k] != fn.get(k, 0))
+    only_n = sorted(k for k in fn if fn[k] != ff.get(k, 0))
+    d = float((gf - gn).norm() / gn.norm())
+    print(f"\nforced grouping: l0 {l0f} vs {l0n}; launch counts that differ: force {[(k, ff[k]) for k in only_f]} / "
+          f"noforce {[(k, fn[k]) for k in only_n]}; loss {lf:.6f} vs {ln:.6f}; gradient L2 difference {d:.2e}")
+    assert l0f <= 2 and l0n == 3
+    assert any(k.startswith("conv3_brickr_kernel<BN64>") for k in only_f)
+    assert any(k.startswith(("conv3_brick2_kernel", "conv3_brick8_kernel", "wgrad_dma_kernel")) for k in only_n)
+    assert d > 0.0, "different kernels gave bitwise-equal gradients"
+    assert d < 1.0 and abs(lf - ln) / abs(ln) < 1e-3     # kink flips amplify rounding in bf16 (DESIGN (c))
+
+
 # ---------------------------------------------------------------------------------------------------------------
 # c5 in mixed bf16 / fp8 (hardware.fp8: true) at full size
 # ---------------------------------------------------------------------------------------------------------------

@@ -73,6 +73,12 @@ def test_conv3_fwd_dgrad_wgrad(dev, dtype, cin, cout, shape):
     ({}, 256, 128, (2, 12, 12, 12)),                                 # runtime brick (3,6,12) + chunk split-K
     ({}, 512, 256, (1, 6, 6, 6)),                                    # runtime brick (6,6,6), 16 chunks
     ({"MMSEG_BRICKR": "0"}, 256, 128, (2, 12, 12, 12)),              # same through the gather GEMM
+    # runtime brick 6x6x6 with the in-block K split over two 256-thread halves (KW = 2, bf16; r05) against KW = 1,
+    # and an odd chunk count per block (2 + 1: half 1 idles through the last stages' barriers)
+    ({"MMSEG_BRICKR_KW": "1"}, 512, 256, (1, 6, 6, 6)),
+    ({}, 256, 256, (4, 12, 12, 12)),                                 # the grouped 12^3 shape (N = M x B = 4)
+    ({"MMSEG_BRICKR_SLOTS": "6"}, 256, 32, (2, 6, 6, 6)),           # 8 chunks over 3 splits: 3 (2 + 1), 3, 2
+    ({"MMSEG_BRICKR_SLOTS": "1", "MMSEG_BRICKR_PF32": "0"}, 128, 32, (2, 6, 6, 6)),
     ({"MMSEG_WGRAD_BRICK": "1"}, 64, 128, (2, 4, 8, 8)),             # v1 brick wgrad (32 co per block)
     ({"MMSEG_WGRAD_BRICK": "0"}, 64, 64, (1, 4, 8, 8)),              # generic wgrad
     ({}, 32, 128, (1, 8, 4, 16)),                                    # v2 brick wgrad, 2 row tiles of 64 co

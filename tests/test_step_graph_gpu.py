@@ -154,3 +154,28 @@ def test_deferred_bad_labels_raise_at_next_sync(dev, monkeypatch, graph):
         tr.check_deferred()
     assert int(tr.optimizer.state[next(m.parameters())]["step"]) == 2
     tr.check_deferred()                 # cleared: no second raise
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_deferred_bad_then_sync_bad(dev, monkeypatch, graph):
+    """A bad sync=False step followed by a bad sync=True step: one raise reports both, and BOTH step counts are
+    rolled back (the current step's guard is handled before the deferred raise)."""
+    cfg = _cfg("unet", 3, [8, 16, 32, 64, 128], "float32")
+    batches = _batches(dev, 2, 32, 2, 3, seed=4)
+    monkeypatch.setenv("MMSEG_STEP_GRAPH", "1" if graph else "0")
+    torch.manual_seed(0)
+    m = build_model(cfg)
+    tr = Trainer(cfg, m)
+    tr.train_step(batches[0], 0)
+    tr.train_step(batches[1], 1)
+    before = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).clone()
+    bad = {"image": batches[0]["image"], "label": batches[0]["label"].clone()}
+    bad["label"][0, 1, 2, 3] = 9
+    assert torch.isnan(tr.train_step(bad, 2, sync=False)).item()
+    with pytest.raises(RuntimeError, match="outside.*earlier training step"):
+        tr.train_step(bad, 3)
+    assert torch.equal(before, torch.cat([p.detach().reshape(-1) for p in m.parameters()]))
+    assert int(tr.optimizer.state[next(m.parameters())]["step"]) == 2
+    tr.check_deferred()                 # nothing left to raise
+    tr.train_step(batches[1], 4)        # and training continues
+    assert int(tr.optimizer.state[next(m.parameters())]["step"]) == 3

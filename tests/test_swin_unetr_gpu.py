@@ -544,3 +544,32 @@ def test_swin_unetr_c4_size(dev):
     losses = [tr.train_step(batch, i) for i in range(3)]
     print("c4 bf16 losses", losses)
     assert all(np.isfinite(losses)) and losses[-1] < losses[0]
+
+
+@pytest.mark.parametrize("N,hd,heads,masked", [(343, 16, 3, True), (343, 8, 2, False), (8, 16, 1, False),
+                                               (100, 16, 2, True)])
+def test_window_attention_one_pass_forward(dev, N, hd, heads, masked, monkeypatch):
+    """The one-pass forward (winattn_fwd1_kernel: scores kept in registers, log2-domain exponentials, P V on the
+    16x16x32 MFMA, division by the row sum after the product; default) against the two-pass kernel
+    (MMSEG_WINATTN_FWD1=0) on the same operands: the stored log-sum-exp (which the backward consumes) to 1e-5
+    and O to bf16 rounding (both are held to torch fp64 by test_fused_window_attention_vs_torch)."""
+    C, nwin = heads * hd, 2
+    B = 2 * nwin
+    g = torch.Generator().manual_seed(7 * N + hd)
+    qkv = torch.randn(B * N, 3 * C, generator=g).to(torch.bfloat16).to(dev)
+    tab = (torch.randn(13 ** 3, heads, generator=g) * 0.5).t().contiguous().to(dev)
+    reg = torch.randint(0, 4, (nwin, N), generator=g).to(torch.uint8).to(dev) if masked else None
+    L, s = lib(), stream_handle()
+    res = []
+    for fwd1 in ("1", "0"):
+        monkeypatch.setenv("MMSEG_WINATTN_FWD1", fwd1)
+        O = torch.empty(B * N, C, dtype=torch.bfloat16, device=dev)
+        lse = torch.zeros(L.mmseg_winattn_lse_floats(B, heads), device=dev)
+        L.mmseg_winattn_fwd(ptr(qkv), B, N, C, heads, ptr(tab), 13 ** 3, 7, 7, 7, ptr(reg), nwin if masked else 0,
+                            hd ** -0.5, ptr(O), ptr(lse), s)
+        torch.cuda.synchronize()
+        assert L.mmseg_last_kernel().decode() == ("winattn_fwd1_kernel" if fwd1 == "1" else "winattn_fwd_kernel")
+        res.append((O.float(), lse.view(B * heads, -1)[:, :N].clone()))
+    (o1, l1), (o0, l0) = res
+    assert (l1 - l0).abs().max().item() < 1e-5 * max(1.0, l0.abs().max().item())
+    assert rel2(o1, o0) < 1e-2

@@ -4,6 +4,8 @@
     python tools/rocprof_families.py traffic <fetch_counter_collection.csv> <write_counter_collection.csv> [out.json [steps]]
     python tools/rocprof_families.py sq <sq_counter_collection.csv> [out.json]
     python tools/rocprof_families.py steady <prof_kernel_trace.csv> <out.json> [last_steps]
+    (any of them: --workload <file> written by `bench.py --workload-out`, stamped into the summary as
+    "_workload" with "_created"; bench.py uses only the summaries of its own workload)
 
 `stats` prints per-family calls / average duration (the same family names the
 in-process timer reports through mmseg_last_kernel(), so bench.py's
@@ -23,6 +25,25 @@ import sys
 from collections import defaultdict
 
 _MODES = {"0": "conv3", "1": "point", "2": "convT_fwd", "3": "convT_dgrad"}
+_GEMM_TILES = {("4", "1", "2", "2"): "128x32", ("2", "2", "4", "2"): "128x64", ("1", "4", "4", "4"): "64x256",
+               ("2", "2", "2", "2"): "64x64", ("1", "4", "4", "2"): "64x128"}
+
+
+def _mangled_base(name: str):
+    """Function name of an Itanium-mangled kernel symbol (the traces are taken with rocprofv3 -M: its demangler
+    garbles the __bf16 template arguments, DF16b): the last <length><identifier> of the nested name,
+    _ZN12_GLOBAL__N_115conv_gemm_kernelI... -> conv_gemm_kernel."""
+    if not name.startswith("_Z"):
+        return None
+    i = 3 if name.startswith("_ZN") else 2
+    last = None
+    while i < len(name) and name[i].isdigit():
+        j = i
+        while j < len(name) and name[j].isdigit():
+            j += 1
+        n = int(name[i:j])
+        last, i = name[j:j + n], j + n
+    return last
 
 
 def family(name: str) -> str:
@@ -31,6 +52,9 @@ def family(name: str) -> str:
     m = re.search(r"conv3_brick2_kernelI(?:DF16b|f)Li(\d+)ELi(\d+)E", name)
     if m:
         return f"conv3_brick2_kernel<BN{m.group(1)},ZW{m.group(2)}>[{dt}]"
+    m = re.search(r"conv3_brickr_kernelI(?:DF16b|f)Li(\d+)E(?:Li\d+E){4}Lb[01]ELb[01]ELi(\d+)E", name)
+    if m and m.group(2) != "1":   # the in-block K split (template KW), as mmseg_last_kernel() names it
+        return f"conv3_brickr_kernel<BN{m.group(1)},KW{m.group(2)}>[{dt}]"
     m = re.search(r"conv3_brickr_kernelI(?:DF16b|f)Li(\d+)E", name)
     if m:
         return f"conv3_brickr_kernel<BN{m.group(1)}>[{dt}]"
@@ -39,7 +63,8 @@ def family(name: str) -> str:
         return f"conv3_brick_kernel<BN{m.group(1)}>[{dt}]"
     m = re.search(r"conv_gemm_kernelI(?:DF16b|f)Li(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d)E", name)
     if m:
-        tile = "128x32" if (m.group(2), m.group(3)) == ("4", "1") else "128x64"
+        # (WM, WN, TM, TN) template arguments -> the tile name mmseg_last_kernel() reports (conv_gemm.hip)
+        tile = _GEMM_TILES.get(m.group(2, 3, 4, 5), "128x64")
         return f"conv_gemm_kernel<{_MODES[m.group(1)]},{tile}>[{dt}]"
     # brick6 / brick8 under the timer's family names (engine/profiler.py: mmseg_last_kernel()), so a family
     # means the same launches in the live timer and in the trace: brick6 split by its INP / F8 forms, brick8 by BN
@@ -75,6 +100,9 @@ def family(name: str) -> str:
     m = re.search(r"\(anonymous namespace\)::([A-Za-z_][A-Za-z0-9_]*)[<(]", name)
     if m:
         return m.group(1)
+    base = _mangled_base(name)
+    if base:
+        return base
     m = re.search(r"(?:_GLOBAL__N_1\d+|::)([A-Za-z_][A-Za-z0-9_]*?)(?:I|\(|E|$)", name)
     return m.group(1) if m else name
 
@@ -201,14 +229,33 @@ def sq(csv_path: str, trace_stats: str = None):
     return res
 
 
+def _stamp(res: dict) -> dict:
+    """Tag a summary with the workload of the profiled bench run (--workload FILE, written by bench.py
+    --workload-out) and its creation time: bench.py reads only summaries of its own workload, newest first."""
+    if WORKLOAD_FILE:
+        with open(WORKLOAD_FILE) as f:
+            res["_workload"] = json.load(f)
+    import datetime
+    res["_created"] = datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
+    return res
+
+
+WORKLOAD_FILE = None
+
 if __name__ == "__main__":
+    if "--workload" in sys.argv:
+        i = sys.argv.index("--workload")
+        WORKLOAD_FILE = sys.argv[i + 1]
+        del sys.argv[i:i + 2]
     if sys.argv[1] == "stats":
         stats(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 1)
     elif sys.argv[1] == "steady":
-        r = steady(sys.argv[2], int(sys.argv[4]) if len(sys.argv) > 4 else 8)
+        r = _stamp(steady(sys.argv[2], int(sys.argv[4]) if len(sys.argv) > 4 else 8))
         with open(sys.argv[3], "w") as f:
             f.write(json.dumps(r, indent=1) + "\n")
         fam = {k: v for k, v in r.items() if not k.startswith("_")}
+        if r.get("_workload"):
+            print("workload", json.dumps(r["_workload"]))
         tot = sum(v["ms_per_step"] for v in fam.values())
         print(f"last {r['_steps']} steps, {r['_span_ms_per_step']:.3f} ms/step wall, {tot:.3f} ms/step of kernels")
         print(f"{'family':48s} {'n/step':>7s} {'avg_us':>9s} {'ms/step':>8s} {'%':>6s}")
@@ -216,7 +263,7 @@ if __name__ == "__main__":
             print(f"{k:48s} {v['launches_per_step']:7.1f} {v['avg_launch_ms'] * 1e3:9.1f} {v['ms_per_step']:8.3f} "
                   f"{100 * v['ms_per_step'] / tot:6.2f}")
     elif sys.argv[1] == "sq":
-        r = sq(sys.argv[2])
+        r = _stamp(sq(sys.argv[2]))
         js = json.dumps(r, indent=1)
         if len(sys.argv) > 3:
             with open(sys.argv[3], "w") as f:
@@ -226,6 +273,7 @@ if __name__ == "__main__":
         r = traffic(sys.argv[2], sys.argv[3])
         if len(sys.argv) > 5:      # training steps the profiled run executed (bench: warmup + steps + timer)
             r["_steps"] = int(sys.argv[5])
+        r = _stamp(r)
         js = json.dumps(r, indent=1)
         if len(sys.argv) > 4:
             with open(sys.argv[4], "w") as f:
