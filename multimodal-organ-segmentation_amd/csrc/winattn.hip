@@ -60,9 +60,13 @@ __device__ __forceinline__ f32x4 mma(s4 a, s4 b, f32x4 c) {
 // relative-position table row of tokens (n, m) in the full window's numbering:
 // ((dz + w0-1)(2w1-1) + dy + w1-1)(2w2-1) + dx + w2-1 = code(n) - code(m) + code_off with
 // code(n) = (z (2w1-1) + y)(2w2-1) + x, so a per-token code staged in LDS gives the row with one subtraction
+// Padding tokens (n >= N) take token 0's code, so every lookup code(n) - code(m) + code_off stays inside the table
+// (a real pair's difference): the r05 backward kernels compute those scores unmasked (their probability is zeroed
+// by lse = +inf, or the score gradient by a select), and a lookup past the staged table read stale LDS.
 __device__ __forceinline__ void stage_codes(int* code, const WinAttnArgs& a, int np) {
   for (int n = threadIdx.x; n < np; n += blockDim.x) {
-    const int z = n / (a.w1 * a.w2), y = (n / a.w2) % a.w1, x = n % a.w2;
+    const int m = n < a.N ? n : 0;
+    const int z = m / (a.w1 * a.w2), y = (m / a.w2) % a.w1, x = m % a.w2;
     code[n] = (z * (2 * a.w1 - 1) + y) * (2 * a.w2 - 1) + x;
   }
 }
@@ -296,7 +300,7 @@ __global__ __launch_bounds__(512) void winattn_fwd1_kernel(WinAttnArgs a) {
       if (kt < nt) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = v[kt][r] == -INFINITY ? 0.f : exp2f(v[kt][r] - mx);
+          const float p = v[kt][r] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(v[kt][r] - mx);
           v[kt][r] = p;
           sum += p;
         }
@@ -304,7 +308,7 @@ __global__ __launch_bounds__(512) void winattn_fwd1_kernel(WinAttnArgs a) {
     }
 #pragma unroll
     for (int o = 16; o <= 32; o <<= 1) sum += __shfl_xor(sum, o, 64);
-    if (g4 == 0 && qv) a.lse[(long long)bh * NPMAX + q] = (mx + log2f(sum)) * LN2;
+    if (g4 == 0 && qv) a.lse[(long long)bh * NPMAX + q] = (mx + __builtin_amdgcn_logf(sum)) * LN2;
     const float inv = sum > 0.f ? 1.f / sum : 0.f;
     f32x4 o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -319,12 +323,14 @@ __global__ __launch_bounds__(512) void winattn_fwd1_kernel(WinAttnArgs a) {
         o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat44(pa, pb), cat44(va, vb), o, 0, 0, 0);
       }
     }
+    float ir[4];   // 1 / row sum of query 4 g4 + r (held by lane 4 g4 + r): shuffled with every lane active
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ir[r] = __shfl(inv, 4 * g4 + r, 64);
     if (r16 < a.hd) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qq = qt * 16 + 4 * g4 + r;
-        const float ir = __shfl(inv, 4 * g4 + r, 64);   // the row sum of query qq (held by lane qq % 16)
-        if (qq < a.N) a.out[(long long)(b * a.N + qq) * a.C + hoff + r16] = (bf16_t)(o[r] * ir);
+        if (qq < a.N) a.out[(long long)(b * a.N + qq) * a.C + hoff + r16] = (bf16_t)(o[r] * ir[r]);
       }
     }
   }
@@ -602,6 +608,340 @@ __global__ __launch_bounds__(512) void winattn_bwd_qb_kernel(WinAttnArgs a, int 
   }
 }
 
+// ----------------------------------------------- backward, r05 forms (default)
+// (MMSEG_WINATTN_BWD2=0 restores winattn_bwd_kv_kernel / winattn_bwd_qb_kernel.)  Same decomposition as the r04
+// kernels (key pass: dV, dK; query pass: dQ and the window-summed dS), with what the VALU-issue-bound loops spent
+// per score cut: scores in the log2 domain (table and scale pre-multiplied by log2 e, lse staged as lse * log2 e,
+// one FMA + one v_exp_f32 per probability); in the key pass invalid queries carry lse = +inf (p = 0 with no select)
+// and invalid keys need no mask (their dV / dK rows are never stored); the products that contract over tokens
+// (dV, dK over queries; dQ over keys) run on the 16x16x32 MFMA, two token tiles per instruction with the tokens
+// permuted identically in both operands.
+__device__ __forceinline__ f32x4 mma32(s4 a0, s4 a1, s4 b0, s4 b1, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat44(a0, a1), cat44(b0, b1), c, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(512) void winattn_bwd_kv2_kernel(WinAttnArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t dOs[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Qt[16][TP];
+  __shared__ __attribute__((aligned(16))) bf16_t dOt[16][TP];
+  __shared__ float tab[TMAX];
+  __shared__ __attribute__((aligned(16))) float lse2[NPMAX];
+  __shared__ __attribute__((aligned(16))) float Dq[NPMAX];
+  __shared__ __attribute__((aligned(16))) int code[NPMAX];
+  __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
+  const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads;
+  const int np = (a.N + 15) & ~15, nt = np / 16;
+  const Stage st{b, h, a.N, np};
+  const int C3 = 3 * a.C, hoff = h * a.hd;
+  stage_rows(Qs, a.qkv, C3, hoff, st, a.hd, Qt);
+  stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, nullptr);
+  stage_rows(Vs, a.qkv, C3, 2 * a.C + hoff, st, a.hd, nullptr);
+  stage_rows(dOs, a.dO, a.C, hoff, st, a.hd, dOt);
+  {
+    const float* row = a.table + (long long)h * a.T;
+    for (int t = threadIdx.x; t < a.T; t += blockDim.x) tab[t] = row[t] * LOG2E;
+  }
+  stage_codes(code, a, np);
+  stage_region(reg, a, b);
+  stage_D(Dq, a, st);
+  for (int n = threadIdx.x; n < np; n += blockDim.x)
+    lse2[n] = n < a.N ? a.lse[(long long)bh * NPMAX + n] * LOG2E : INFINITY;
+  __syncthreads();
+  const float* ctab = tab + code_off(a);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const float sc2 = a.scale * LOG2E, pen2 = 100.0f * LOG2E;
+  const s4 z4 = {0, 0, 0, 0};
+  for (int kt = wave; kt < nt; kt += WAVES) {
+    const int key = kt * 16 + r16;
+    const s4 bk = ld4(&Ks[key][4 * g4]);
+    const s4 bv = ld4(&Vs[key][4 * g4]);
+    const float* tk = ctab - code[key];
+    const uint32_t rk = reg[key];
+    f32x4 dk = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
+    for (int qt = 0; qt < nt; qt += 2) {
+      s4 pp[2], dd[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int qq = qt + u;
+        if (qq < nt) {
+          const f32x4 sc = mma(ld4(&Qs[qq * 16 + r16][4 * g4]), bk, (f32x4){0.f, 0.f, 0.f, 0.f});   // S[q][key]
+          const f32x4 dp = mma(ld4(&dOs[qq * 16 + r16][4 * g4]), bv, (f32x4){0.f, 0.f, 0.f, 0.f}); // dP[q][key]
+          const int q0 = qq * 16 + 4 * g4;
+          const int4 cq = *reinterpret_cast<const int4*>(code + q0);
+          const uint32_t rq = a.region ? *reinterpret_cast<const uint32_t*>(reg + q0) : 0u;
+          const float4 l4 = *reinterpret_cast<const float4*>(lse2 + q0);
+          const float4 d4 = *reinterpret_cast<const float4*>(Dq + q0);
+          const int c[4] = {cq.x, cq.y, cq.z, cq.w};
+          const float lq[4] = {l4.x, l4.y, l4.z, l4.w}, dq4[4] = {d4.x, d4.y, d4.z, d4.w};
+          float p[4], ds[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float t = fmaf(sc[r], sc2, tk[c[r]]);
+            if (a.region && ((rq >> (8 * r)) & 255u) != rk) t -= pen2;
+            p[r] = __builtin_amdgcn_exp2f(t - lq[r]);
+            ds[r] = p[r] * (dp[r] - dq4[r]);
+          }
+          pp[u] = pack4(p[0], p[1], p[2], p[3]);
+          dd[u] = pack4(ds[0], ds[1], ds[2], ds[3]);
+        } else {
+          pp[u] = z4;
+          dd[u] = z4;
+        }
+      }
+      const bool hi = qt + 1 < nt;
+      const s4 o0 = ld4(&dOt[r16][qt * 16 + 4 * g4]), o1 = hi ? ld4(&dOt[r16][(qt + 1) * 16 + 4 * g4]) : z4;
+      const s4 q0 = ld4(&Qt[r16][qt * 16 + 4 * g4]), q1 = hi ? ld4(&Qt[r16][(qt + 1) * 16 + 4 * g4]) : z4;
+      dv = mma32(pp[0], pp[1], o0, o1, dv);
+      dk = mma32(dd[0], dd[1], q0, q1, dk);
+    }
+    if (r16 < a.hd) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kk = kt * 16 + 4 * g4 + r;
+        if (kk < a.N) {
+          bf16_t* row = a.out + (long long)(b * a.N + kk) * C3;
+          row[a.C + hoff + r16] = (bf16_t)(dk[r] * a.scale);
+          row[2 * a.C + hoff + r16] = (bf16_t)dv[r];
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(512) void winattn_bwd_qb2_kernel(WinAttnArgs a, int wpg, int nqg, float* dsum) {
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Kt[16][TP];
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[QB_TILES * 16][16];
+  __shared__ __attribute__((aligned(16))) bf16_t dOs[QB_TILES * 16][16];
+  __shared__ float tab[TMAX];
+  __shared__ float lse2[QB_TILES * 16];
+  __shared__ float Dq[QB_TILES * 16];
+  __shared__ __attribute__((aligned(16))) int code[NPMAX];
+  __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
+  const int qg = blockIdx.x % nqg, h = (blockIdx.x / nqg) % a.heads, wg = blockIdx.x / (nqg * a.heads);
+  const int np = (a.N + 15) & ~15, nt = np / 16;
+  const int q0 = qg * QB_TILES * 16;
+  const int C3 = 3 * a.C, hoff = h * a.hd;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const int qt = qg * QB_TILES + wave;
+  const int q = qt * 16 + r16;
+  const bool qv = q < a.N;
+  {
+    const float* row = a.table + (long long)h * a.T;
+    for (int t = threadIdx.x; t < a.T; t += blockDim.x) tab[t] = row[t] * LOG2E;
+  }
+  stage_codes(code, a, np);
+  const float* ctab = tab + code_off(a);
+  const float sc2 = a.scale * LOG2E, pen2 = 100.0f * LOG2E;
+  const s4 z4 = {0, 0, 0, 0};
+  float acc[NTMAX][4];
+#pragma unroll
+  for (int kt = 0; kt < NTMAX; ++kt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[kt][r] = 0.f;
+  const int b0 = wg * wpg, b1 = b0 + wpg < a.B ? b0 + wpg : a.B;
+  for (int b = b0; b < b1; ++b) {
+    const int bh = b * a.heads + h;
+    const Stage st{b, h, a.N, np};
+    __syncthreads();   // the previous window's operands are consumed
+    stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, Kt);
+    stage_rows(Vs, a.qkv, C3, 2 * a.C + hoff, st, a.hd, nullptr);
+    stage_region(reg, a, b);
+    for (int e = threadIdx.x; e < QB_TILES * 16 * 2; e += blockDim.x) {
+      const int n = e >> 1, half = e & 1, qq = q0 + n;
+      V8<bf16_t> vq, vo;
+      vq.zero();
+      vo.zero();
+      if (qq < a.N && half * 8 < a.hd) {
+        vq.load(a.qkv + (long long)(b * a.N + qq) * C3 + hoff + half * 8);
+        vo.load(a.dO + (long long)(b * a.N + qq) * a.C + hoff + half * 8);
+      }
+      vq.store(&Qs[n][half * 8]);
+      vo.store(&dOs[n][half * 8]);
+    }
+    for (int n = threadIdx.x; n < QB_TILES * 16; n += blockDim.x) {
+      const int qq = q0 + n;
+      float d = 0.f, l = 0.f;
+      if (qq < a.N) {
+        const long long base = (long long)(b * a.N + qq) * a.C + hoff;
+        for (int j = 0; j < a.hd; ++j) d += (float)a.dO[base + j] * (float)a.O[base + j];
+        l = a.lse[(long long)bh * NPMAX + qq];
+      }
+      Dq[n] = d;
+      lse2[n] = l * LOG2E;
+    }
+    __syncthreads();
+    if (qt < nt) {
+      const int ql = wave * 16 + r16;
+      const s4 bq = ld4(&Qs[ql][4 * g4]);
+      const s4 bdo = ld4(&dOs[ql][4 * g4]);
+      const float lq = lse2[ql], dq_ = Dq[ql];
+      const float* tq = ctab + code[q];
+      const uint32_t rq = reg[q];
+      f32x4 dq = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k2 = 0; k2 < NTMAX / 2; ++k2) {
+        s4 dd[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int kt = 2 * k2 + u;
+          if (kt < nt) {
+            const f32x4 sc = mma(ld4(&Ks[kt * 16 + r16][4 * g4]), bq, (f32x4){0.f, 0.f, 0.f, 0.f});
+            const f32x4 dp = mma(ld4(&Vs[kt * 16 + r16][4 * g4]), bdo, (f32x4){0.f, 0.f, 0.f, 0.f});
+            const int k0 = kt * 16 + 4 * g4;
+            const int4 ck = *reinterpret_cast<const int4*>(code + k0);
+            const uint32_t rk = a.region ? *reinterpret_cast<const uint32_t*>(reg + k0) : 0u;
+            const int c[4] = {ck.x, ck.y, ck.z, ck.w};
+            float ds[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float t = fmaf(sc[r], sc2, tq[-c[r]]);
+              if (a.region && ((rk >> (8 * r)) & 255u) != rq) t -= pen2;
+              const float p = __builtin_amdgcn_exp2f(t - lq);
+              ds[r] = p * (dp[r] - dq_);
+              if (kt == nt - 1 && k0 + r >= a.N) ds[r] = 0.f;   // keys past N (only in the last tile)
+              acc[kt][r] += ds[r];
+            }
+            dd[u] = pack4(ds[0], ds[1], ds[2], ds[3]);
+          } else {
+            dd[u] = z4;
+          }
+        }
+        const int kt0 = 2 * k2;
+        if (kt0 < nt) {
+          const bool hi = kt0 + 1 < nt;
+          const s4 k0v = ld4(&Kt[r16][kt0 * 16 + 4 * g4]), k1v = hi ? ld4(&Kt[r16][(kt0 + 1) * 16 + 4 * g4]) : z4;
+          dq = mma32(dd[0], dd[1], k0v, k1v, dq);
+        }
+      }
+      if (r16 < a.hd) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qq = qt * 16 + 4 * g4 + r;
+          if (qq < a.N) a.out[(long long)(b * a.N + qq) * C3 + hoff + r16] = (bf16_t)(dq[r] * a.scale);
+        }
+      }
+    }
+  }
+  if (qt < nt && qv) {
+    float* row = dsum + (((long long)wg * a.heads + h) * a.N + q) * a.ldn;
+#pragma unroll
+    for (int kt = 0; kt < NTMAX; ++kt) {
+      const int k0 = kt * 16 + 4 * g4;
+      if (kt < nt && k0 < a.ldn) {
+        if (k0 + 3 < a.ldn) {
+          *reinterpret_cast<float4*>(row + k0) = make_float4(acc[kt][0], acc[kt][1], acc[kt][2], acc[kt][3]);
+        } else {
+          for (int r = 0; r < 4 && k0 + r < a.ldn; ++r) row[k0 + r] = acc[kt][r];
+        }
+      }
+    }
+  }
+}
+
+// bwd_q in the r05 form (one window per block, dS written per window in bf16 for mmseg_relpos_table_grad): the
+// same per-score arithmetic and MFMA order as winattn_bwd_qb2_kernel, so dQ is bitwise the summed path's.
+__global__ __launch_bounds__(512) void winattn_bwd_q2_kernel(WinAttnArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t dOs[NPMAX][16];
+  __shared__ __attribute__((aligned(16))) bf16_t Kt[16][TP];
+  __shared__ float tab[TMAX];
+  __shared__ __attribute__((aligned(16))) float lse2[NPMAX];
+  __shared__ __attribute__((aligned(16))) float Dq[NPMAX];
+  __shared__ __attribute__((aligned(16))) int code[NPMAX];
+  __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
+  const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads;
+  const int np = (a.N + 15) & ~15, nt = np / 16;
+  const Stage st{b, h, a.N, np};
+  const int C3 = 3 * a.C, hoff = h * a.hd;
+  stage_rows(Qs, a.qkv, C3, hoff, st, a.hd, nullptr);
+  stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, Kt);
+  stage_rows(Vs, a.qkv, C3, 2 * a.C + hoff, st, a.hd, nullptr);
+  stage_rows(dOs, a.dO, a.C, hoff, st, a.hd, nullptr);
+  {
+    const float* row = a.table + (long long)h * a.T;
+    for (int t = threadIdx.x; t < a.T; t += blockDim.x) tab[t] = row[t] * LOG2E;
+  }
+  stage_codes(code, a, np);
+  stage_region(reg, a, b);
+  stage_D(Dq, a, st);
+  for (int n = threadIdx.x; n < np; n += blockDim.x) lse2[n] = n < a.N ? a.lse[(long long)bh * NPMAX + n] * LOG2E : 0.f;
+  __syncthreads();
+  const float* ctab = tab + code_off(a);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const float sc2 = a.scale * LOG2E, pen2 = 100.0f * LOG2E;
+  const s4 z4 = {0, 0, 0, 0};
+  for (int qt = wave; qt < nt; qt += WAVES) {
+    const int q = qt * 16 + r16;
+    const s4 bq = ld4(&Qs[q][4 * g4]);
+    const s4 bdo = ld4(&dOs[q][4 * g4]);
+    const float lq = lse2[q], dq_ = Dq[q];
+    const float* tq = ctab + code[q];
+    const uint32_t rq = reg[q];
+    f32x4 dq = {0.f, 0.f, 0.f, 0.f};
+    bf16_t* dsrow = a.dS + ((long long)bh * a.N + q) * a.ldn;
+#pragma unroll
+    for (int k2 = 0; k2 < NTMAX / 2; ++k2) {
+      s4 dd[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int kt = 2 * k2 + u;
+        if (kt < nt) {
+          const f32x4 sc = mma(ld4(&Ks[kt * 16 + r16][4 * g4]), bq, (f32x4){0.f, 0.f, 0.f, 0.f});
+          const f32x4 dp = mma(ld4(&Vs[kt * 16 + r16][4 * g4]), bdo, (f32x4){0.f, 0.f, 0.f, 0.f});
+          const int k0 = kt * 16 + 4 * g4;
+          const int4 ck = *reinterpret_cast<const int4*>(code + k0);
+          const uint32_t rk = a.region ? *reinterpret_cast<const uint32_t*>(reg + k0) : 0u;
+          const int c[4] = {ck.x, ck.y, ck.z, ck.w};
+          float ds[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float t = fmaf(sc[r], sc2, tq[-c[r]]);
+            if (a.region && ((rk >> (8 * r)) & 255u) != rq) t -= pen2;
+            const float p = __builtin_amdgcn_exp2f(t - lq);
+            ds[r] = p * (dp[r] - dq_);
+            if (kt == nt - 1 && k0 + r >= a.N) ds[r] = 0.f;
+          }
+          dd[u] = pack4(ds[0], ds[1], ds[2], ds[3]);
+          if (q < a.N) {
+            if (k0 + 3 < a.ldn) {
+              *reinterpret_cast<s4*>(dsrow + k0) = dd[u];
+            } else {
+              typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+              const b4 v = __builtin_bit_cast(b4, dd[u]);
+              for (int r = 0; r < 4 && k0 + r < a.ldn; ++r) dsrow[k0 + r] = v[r];
+            }
+          }
+        } else {
+          dd[u] = z4;
+        }
+      }
+      const int kt0 = 2 * k2;
+      if (kt0 < nt) {
+        const bool hi = kt0 + 1 < nt;
+        const s4 k0v = ld4(&Kt[r16][kt0 * 16 + 4 * g4]), k1v = hi ? ld4(&Kt[r16][(kt0 + 1) * 16 + 4 * g4]) : z4;
+        dq = mma32(dd[0], dd[1], k0v, k1v, dq);
+      }
+    }
+    if (r16 < a.hd) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = qt * 16 + 4 * g4 + r;
+        if (qq < a.N) a.out[(long long)(b * a.N + qq) * C3 + hoff + r16] = (bf16_t)(dq[r] * a.scale);
+      }
+    }
+  }
+}
+
 // windows per block of winattn_bwd_qb: about two resident blocks per CU over (window group, head, query group)
 int qb_windows_per_group(int B, int N, int heads) {
   const int nt = ((N + 15) & ~15) / 16, nqg = (nt + QB_TILES - 1) / QB_TILES;
@@ -653,9 +993,13 @@ int mmseg_winattn_bwd(const void* qkv, const void* O, const void* dO, const floa
   if (check_args(a)) return 1;
   MMSEG_REQUIRE(ldn >= N && ldn % 8 == 0, "winattn_bwd: ldn >= N, multiple of 8");
   hipStream_t s = (hipStream_t)stream;
-  MMSEG_LAUNCH(winattn_bwd_kv_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  const bool v2 = knob_i("MMSEG_WINATTN_BWD2", 1) != 0;
+  if (v2) MMSEG_LAUNCH(winattn_bwd_kv2_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  else MMSEG_LAUNCH(winattn_bwd_kv_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
   if (mmseg::check_launch("winattn_bwd_kv")) return 1;
-  MMSEG_LAUNCH(winattn_bwd_q_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  if (v2) MMSEG_LAUNCH(winattn_bwd_q2_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  else MMSEG_LAUNCH(winattn_bwd_q_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  mmseg::note_kernel(v2 ? "winattn_bwd_kv2_kernel" : "winattn_bwd_kv_kernel");
   return mmseg::check_launch("winattn_bwd_q");
 }
 
@@ -677,11 +1021,15 @@ int mmseg_winattn_bwd_sum(const void* qkv, const void* O, const void* dO, const 
   MMSEG_REQUIRE(ldn >= N && ldn % 8 == 0 && mmseg_winattn_sum_groups(B, N, heads) > 0,
                 "winattn_bwd_sum: ldn >= N (multiple of 8) and enough windows (mmseg_winattn_sum_groups)");
   hipStream_t s = (hipStream_t)stream;
-  MMSEG_LAUNCH(winattn_bwd_kv_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  const bool v2 = knob_i("MMSEG_WINATTN_BWD2", 1) != 0;
+  if (v2) MMSEG_LAUNCH(winattn_bwd_kv2_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  else MMSEG_LAUNCH(winattn_bwd_kv_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
   if (mmseg::check_launch("winattn_bwd_kv")) return 1;
   const int wpg = qb_windows_per_group(B, N, heads);
   const int nt = ((N + 15) & ~15) / 16, nqg = (nt + QB_TILES - 1) / QB_TILES, nwg = (B + wpg - 1) / wpg;
-  MMSEG_LAUNCH(winattn_bwd_qb_kernel, dim3(nwg * heads * nqg), dim3(64 * WAVES), 0, s, a, wpg, nqg, dsum);
+  if (v2) MMSEG_LAUNCH(winattn_bwd_qb2_kernel, dim3(nwg * heads * nqg), dim3(64 * WAVES), 0, s, a, wpg, nqg, dsum);
+  else MMSEG_LAUNCH(winattn_bwd_qb_kernel, dim3(nwg * heads * nqg), dim3(64 * WAVES), 0, s, a, wpg, nqg, dsum);
+  mmseg::note_kernel(v2 ? "winattn_bwd_kv2_kernel" : "winattn_bwd_kv_kernel");
   return mmseg::check_launch("winattn_bwd_qb");
 }
 

@@ -113,6 +113,14 @@ class GradBuckets:
         self.guard: Optional[torch.Tensor] = None
         self.guard_sent = False
 
+    def _record(self, b: int):
+        """Replace the bucket's writer streams by events recorded on them now (after their last write)."""
+        for key, st in list(self.events[b].items()):
+            if isinstance(st, torch.cuda.Stream):
+                ev = torch.cuda.Event()
+                ev.record(st)
+                self.events[b][key] = ev
+
     def _reduce(self, b: int):
         _, _, lo, hi = self.buckets[b]
         t = self.grad[lo:hi]
@@ -154,14 +162,15 @@ class GradBuckets:
             return
         b = self.owner[idx]
         self.pending[b] -= 1
-        if self.pending[b] == 0 and self.pre_reduce is not None:
-            self.pre_reduce()
         if self.grad.is_cuda:
+            # the streams that wrote this bucket; their events are recorded once the bucket is complete (one event
+            # per stream and bucket, not one per parameter: inside a captured step each is a graph dependency)
             cur = torch.cuda.current_stream(self.grad.device)
-            ev = torch.cuda.Event()
-            ev.record(cur)
-            self.events[b][cur.cuda_stream] = ev
+            self.events[b].setdefault(cur.cuda_stream, cur)
         if self.pending[b] == 0:
+            if self.pre_reduce is not None:
+                self.pre_reduce()
+            self._record(b)
             self._reduce(b)
 
     def finish(self):
@@ -174,10 +183,9 @@ class GradBuckets:
             # writes to unreported parameters may still be queued on the current stream: the late
             # collectives wait for everything issued on it so far
             cur = torch.cuda.current_stream(self.grad.device)
-            ev = torch.cuda.Event()
-            ev.record(cur)
             for b in late:
-                self.events[b][cur.cuda_stream] = ev
+                self.events[b][cur.cuda_stream] = cur
+                self._record(b)
         for b in late:         # a parameter the engine did not report: reduce anyway (correctness first)
             self.pending[b] = 0
             self._reduce(b)

@@ -85,8 +85,9 @@ class KernelTimer:
             if i1 <= i0:
                 continue
             want = _base(name)
-            main = next((i for i in range(i0, i1) if _base(launches[i][0]) == want and i not in mains),
-                        max(range(i0, i1), key=lambda i: launches[i][1]))
+            free = [i for i in range(i0, i1) if i not in mains] or list(range(i0, i1))
+            main = next((i for i in free if _base(launches[i][0]) == want),
+                        max(free, key=lambda i: launches[i][1]))
             mains.add(main)
             for i in range(i0, i1):
                 if i == main:

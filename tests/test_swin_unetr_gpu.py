@@ -391,7 +391,8 @@ def test_window_attention_summed_score_gradient(dev, masked):
     scale = hd ** -0.5
     nwm = nwin if masked else 0
     O = torch.empty(B * N, C, dtype=torch.bfloat16, device=dev)
-    lse = torch.empty(L.mmseg_winattn_lse_floats(B, heads), device=dev)
+    # NaN past each window's N tokens: no kernel may read the log-sum-exp of a padding token (r05 regression)
+    lse = torch.full((L.mmseg_winattn_lse_floats(B, heads),), float("nan"), device=dev)
     L.mmseg_winattn_fwd(ptr(qkv), B, N, C, heads, ptr(tabt), 13 ** 3, 7, 7, 7, ptr(region), nwm, scale, ptr(O),
                         ptr(lse), s)
     ldn = (N + 7) // 8 * 8
@@ -421,6 +422,11 @@ def test_window_attention_summed_score_gradient(dev, masked):
                                       1, s)
         torch.cuda.synchronize()
         res[mode] = (dqkv.clone(), gt.clone())
+    dd = (res["sum"][0].float() - res["win"][0].float()).abs()
+    C3 = 3 * C
+    print("\ndqkv |sum - win|: dq", float(dd[:, :C].max()), "dk", float(dd[:, C:2 * C].max()), "dv",
+          float(dd[:, 2 * C:C3].max()), "differing", int((dd > 0).sum()), "nan", int(torch.isnan(dd).sum()))
+    assert not torch.isnan(res["sum"][0].float()).any()
     assert torch.equal(res["sum"][0], res["win"][0])
     # fp64 reference of the table gradient on the GPU
     x = qkv.double().view(B, N, 3, heads, hd).permute(2, 0, 3, 1, 4)
@@ -573,3 +579,36 @@ def test_window_attention_one_pass_forward(dev, N, hd, heads, masked, monkeypatc
     (o1, l1), (o0, l0) = res
     assert (l1 - l0).abs().max().item() < 1e-5 * max(1.0, l0.abs().max().item())
     assert rel2(o1, o0) < 1e-2
+
+
+@pytest.mark.parametrize("N,hd,heads,masked", [(343, 16, 3, True), (100, 8, 2, False)])
+def test_window_attention_backward_r05_forms(dev, N, hd, heads, masked, monkeypatch):
+    """The r05 backward kernels (log2-domain scores, dV / dK / dQ on the 16x16x32 MFMA; default) against the r04
+    ones (MMSEG_WINATTN_BWD2=0) on the same operands and forward: dqkv and the per-window dS to bf16 rounding of
+    each other (both are held to torch fp64 by test_fused_window_attention_vs_torch)."""
+    C, nwin = heads * hd, 2
+    B = 2 * nwin
+    g = torch.Generator().manual_seed(11 * N + hd)
+    qkv = torch.randn(B * N, 3 * C, generator=g).to(torch.bfloat16).to(dev)
+    tab = (torch.randn(13 ** 3, heads, generator=g) * 0.5).t().contiguous().to(dev)
+    reg = torch.randint(0, 4, (nwin, N), generator=g).to(torch.uint8).to(dev) if masked else None
+    dO = torch.randn(B * N, C, generator=g).to(torch.bfloat16).to(dev)
+    L, s = lib(), stream_handle()
+    O = torch.empty(B * N, C, dtype=torch.bfloat16, device=dev)
+    lse = torch.zeros(L.mmseg_winattn_lse_floats(B, heads), device=dev)
+    nw = nwin if masked else 0
+    L.mmseg_winattn_fwd(ptr(qkv), B, N, C, heads, ptr(tab), 13 ** 3, 7, 7, 7, ptr(reg), nw, hd ** -0.5, ptr(O),
+                        ptr(lse), s)
+    ldn = (N + 7) // 8 * 8
+    res = []
+    for v2 in ("1", "0"):
+        monkeypatch.setenv("MMSEG_WINATTN_BWD2", v2)
+        dqkv = torch.empty(B * N, 3 * C, dtype=torch.bfloat16, device=dev)
+        dS = torch.zeros(B * heads * N * ldn, dtype=torch.bfloat16, device=dev)
+        L.mmseg_winattn_bwd(ptr(qkv), ptr(O), ptr(dO), ptr(lse), B, N, C, heads, ptr(tab), 13 ** 3, 7, 7, 7,
+                            ptr(reg), nw, hd ** -0.5, ptr(dqkv), ptr(dS), ldn, s)
+        torch.cuda.synchronize()
+        res.append((dqkv.float(), dS.float().view(B, heads, N, ldn)))
+    (d1, s1), (d0, s0) = res
+    assert rel2(d1, d0) < 2e-2 and rel2(s1, s0) < 2e-2
+    assert torch.equal(s1[..., N:], torch.zeros_like(s1[..., N:]))
