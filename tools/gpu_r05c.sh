@@ -1,0 +1,8 @@
+# r05c: per-config rocprofv3 trace + PMC summaries (workload-stamped) and judged bench lines, c3 c2 c5 c4
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+bash $R/tools/gpu_profile.sh r05c c3 || exit 1
+bash $R/tools/gpu_profile.sh r05c c2 --model unet || exit 1
+bash $R/tools/gpu_profile.sh r05c c5 --modalities CT,PET,MRI --loss tversky || exit 1
+PROF_STEPS=6 BENCH_STEPS="--steps 5 --warmup 2 --cpu-steps 1" bash $R/tools/gpu_profile.sh r05c c4 --model swin_unetr --size 128 --batch 1 || exit 1
+echo all done
