@@ -248,8 +248,9 @@ def test_group_force_runs_other_kernels(dev, monkeypatch):
     runs the 48^3 / 24^3 encoder levels as ONE launch over both modalities on the runtime-brick kernels
     (conv3_brickr / wgrad_brickr), while noforce runs them per modality on the (4, 8, 8)-brick family (brick2 /
     brick8 / brick3 / wgrad_dma), whose split-K and accumulation orders differ.  Same bf16 c3 step, both modes in
-    one process on the same inputs and weights: the launched kernel families differ, and so (by rounding, not
-    bitwise) do the gradients -- each mode is then held to the pinned fp64 oracle by the parametrized test."""
+    one process on the same inputs and weights: the launched kernel families differ, and the gradients differ by
+    fp32 accumulation order only (not bitwise; L2 ~1e-7) -- each mode is held to the pinned fp64 oracle by the
+    parametrized test, whose printed error profiles therefore agree to the digits shown."""
     from mmseg_amd.engine.profiler import TIMER
     model, mods, loss = CASES["fullgrad_dual_c3"]
     x, y, _ = full_inputs(96, 2, 2, 6, 11)
@@ -282,8 +283,10 @@ def test_group_force_runs_other_kernels(dev, monkeypatch):
     assert l0f <= 2 and l0n == 3
     assert any(k.startswith("conv3_brickr_kernel<BN64>") for k in only_f)
     assert any(k.startswith(("conv3_brick2_kernel", "conv3_brick8_kernel", "wgrad_dma_kernel")) for k in only_n)
-    assert d > 0.0, "different kernels gave bitwise-equal gradients"
-    assert d < 1.0 and abs(lf - ln) / abs(ln) < 1e-3     # kink flips amplify rounding in bf16 (DESIGN (c))
+    # measured (r05d): 9.1e-8 -- the two kernel families differ only in fp32 accumulation order, which almost never
+    # moves a bf16-rounded activation, so the pinned test above prints the same digits for both modes
+    assert 0.0 < d < 1e-5, d
+    assert abs(lf - ln) / abs(ln) < 1e-5
 
 
 # ---------------------------------------------------------------------------------------------------------------
