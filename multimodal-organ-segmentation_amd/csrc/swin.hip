@@ -23,6 +23,9 @@
 //                          the LeakyReLU mask of its backward
 #include "mmseg_common.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace {
 
 constexpr int LN_WAVES = 4;   // rows per block pass
@@ -148,6 +151,224 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const T* __restrict_
       if (c < C) {
         part[((long long)(blockIdx.x * LN_WAVES + wave) * 2) * C + c] = pg[i];
         part[((long long)(blockIdx.x * LN_WAVES + wave) * 2 + 1) * C + c] = pb[i];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------- LayerNorm, row groups (r05)
+// The kernels above give each token row a whole wave with one 2-byte element per lane: at the SwinUNETR widths
+// (C = 48 at stage 0: 48 active lanes of 64, 96 B per row) a wave spends two dependent wave-wide reductions and
+// two memory latencies on 96 bytes, and the launch ran at 0.75 (fwd) / 1.1 (bwd) TB/s (r05c c4 PMC).  Here a row
+// belongs to G lanes (G = the power of two >= C / 8, <= 64), each holding V vectors of 8 channels (16-B loads),
+// so a wave carries 64 / G rows; the row sums are xor-shuffle trees over the G lanes, and every lane keeps two
+// rows in flight.  Same two-pass mean / variance in fp32 (not the same summation order as the wave-per-row form).
+// The backward writes per-wave dgamma / dbeta partials part[(block * 4 + wave)][2][C] (ln_param_reduce sums them
+// in a fixed order).
+constexpr int LNG_LDS_C = 768;   // widest row whose per-block dgamma / dbeta partial is reduced in LDS
+
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T, int G, int V>
+__global__ __launch_bounds__(256) void layernorm_fwd_g_kernel(const T* __restrict__ x, int ldx, T* __restrict__ y,
+                                                              int ldy, long long rows, int C,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta, float eps,
+                                                              float* __restrict__ mean_out,
+                                                              float* __restrict__ rstd_out) {
+  constexpr int RPW = 64 / G, U = 2;                 // rows per wave, row iterations in flight per lane
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int gl = lane & (G - 1), gr = lane / G;
+  float ga[V][8], be[V][8];
+  bool cok[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const int c = (gl + G * v) * 8;
+    cok[v] = c < C;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ga[v][j] = (gamma && cok[v]) ? gamma[c + j] : 1.f;
+      be[v][j] = (beta && cok[v]) ? beta[c + j] : 0.f;
+    }
+  }
+  const float invC = 1.f / (float)C;
+  const long long step = (long long)gridDim.x * 4 * RPW;
+  for (long long base = ((long long)blockIdx.x * 4 + wave) * RPW; base < rows; base += U * step) {
+    V8<T> xv[U][V];
+    long long r[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      r[u] = base + u * step + gr;
+      ok[u] = r[u] < rows;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        if (ok[u] && cok[v]) xv[u][v].load(x + r[u] * ldx + (gl + G * v) * 8);
+        else xv[u][v].zero();
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float s = 0.f;
+#pragma unroll
+      for (int v = 0; v < V; ++v)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += xv[u][v].get(j);
+      const float mean = group_sum<G>(s) * invC;
+      float q = 0.f;
+#pragma unroll
+      for (int v = 0; v < V; ++v)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = cok[v] ? xv[u][v].get(j) - mean : 0.f;
+          q += d * d;
+        }
+      const float rs = rsqrtf(group_sum<G>(q) * invC + eps);
+      if (ok[u]) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          if (!cok[v]) continue;
+          V8<T> o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o.set(j, (xv[u][v].get(j) - mean) * rs * ga[v][j] + be[v][j]);
+          o.store(y + r[u] * ldy + (gl + G * v) * 8);
+        }
+        if (gl == 0 && mean_out) {
+          mean_out[r[u]] = mean;
+          rstd_out[r[u]] = rs;
+        }
+      }
+    }
+  }
+}
+
+template <typename T, int G, int V>
+__global__ __launch_bounds__(256) void layernorm_bwd_g_kernel(const T* __restrict__ x, int ldx,
+                                                              const T* __restrict__ dy, int lddy, T* __restrict__ dx,
+                                                              int lddx, long long rows, int C,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ rstd, int add,
+                                                              float* __restrict__ part) {
+  constexpr int RPW = 64 / G, U = 2;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int gl = lane & (G - 1), gr = lane / G;
+  float ga[V][8], pg[V][8], pb[V][8];
+  bool cok[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const int c = (gl + G * v) * 8;
+    cok[v] = c < C;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ga[v][j] = (gamma && cok[v]) ? gamma[c + j] : 1.f;
+      pg[v][j] = pb[v][j] = 0.f;
+    }
+  }
+  const float invC = 1.f / (float)C;
+  const long long step = (long long)gridDim.x * 4 * RPW;
+  for (long long base = ((long long)blockIdx.x * 4 + wave) * RPW; base < rows; base += U * step) {
+    V8<T> xv[U][V], dv[U][V];
+    long long r[U];
+    bool ok[U];
+    float mu[U], rs[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      r[u] = base + u * step + gr;
+      ok[u] = r[u] < rows;
+      mu[u] = ok[u] ? mean[r[u]] : 0.f;
+      rs[u] = ok[u] ? rstd[r[u]] : 0.f;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        if (ok[u] && cok[v]) {
+          xv[u][v].load(x + r[u] * ldx + (gl + G * v) * 8);
+          dv[u][v].load(dy + r[u] * lddy + (gl + G * v) * 8);
+        } else {
+          xv[u][v].zero();
+          dv[u][v].zero();
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float sg = 0.f, sgx = 0.f;
+#pragma unroll
+      for (int v = 0; v < V; ++v)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = dv[u][v].get(j), h = (xv[u][v].get(j) - mu[u]) * rs[u];
+          pg[v][j] += d * h;      // (padding rows / channels: d = 0)
+          pb[v][j] += d;
+          const float gg = d * ga[v][j];
+          sg += gg;
+          sgx += gg * h;
+        }
+      const float mg = group_sum<G>(sg) * invC, mgx = group_sum<G>(sgx) * invC;
+      if (!ok[u]) continue;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        if (!cok[v]) continue;
+        T* o = dx + r[u] * lddx + (gl + G * v) * 8;
+        V8<T> prev, out;
+        if (add) prev.load(o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float h = (xv[u][v].get(j) - mu[u]) * rs[u];
+          float w = rs[u] * (dv[u][v].get(j) * ga[v][j] - mg - h * mgx);
+          if (add) w += prev.get(j);
+          out.set(j, w);
+        }
+        out.store(o);
+      }
+    }
+  }
+  if (part == nullptr) return;
+  // partials of the wave: the RPW row groups of the wave hold the same channels -- fixed xor tree over them
+#pragma unroll
+  for (int v = 0; v < V; ++v)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+      for (int o = G; o < 64; o <<= 1) {
+        pg[v][j] += __shfl_xor(pg[v][j], o, 64);
+        pb[v][j] += __shfl_xor(pb[v][j], o, 64);
+      }
+    }
+  if constexpr (G * V * 8 <= LNG_LDS_C) {
+    // C <= 768: the 4 waves' partials summed in LDS (wave order), one partial row pair per block
+    __shared__ float red[4][2][LNG_LDS_C];
+    if (gr == 0) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const int c = (gl + G * v) * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          red[wave][0][c + j] = pg[v][j];
+          red[wave][1][c + j] = pb[v][j];
+        }
+      }
+    }
+    __syncthreads();
+    float* pw = part + (long long)blockIdx.x * 2 * C;
+    for (int e = threadIdx.x; e < 2 * C; e += 256) {
+      const int k = e >= C, c = e - k * C;
+      pw[e] = ((red[0][k][c] + red[1][k][c]) + red[2][k][c]) + red[3][k][c];
+    }
+  } else if (gr == 0) {
+    float* pw = part + (long long)(blockIdx.x * 4 + wave) * 2 * C;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      if (!cok[v]) continue;
+      const int c = (gl + G * v) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        pw[c + j] = pg[v][j];
+        pw[C + c + j] = pb[v][j];
       }
     }
   }
@@ -502,9 +723,44 @@ int ln_blocks(long long rows) {
   return (int)(b < 1024 ? (b < 1 ? 1 : b) : 1024);
 }
 
+// (G, V) of the row-group LayerNorm kernels for C (0: not covered -> the wave-per-row kernels); MMSEG_LN_G=0 too
+int ln_gv(int C, int ldx, int ldy, int* V) {
+  const char* e = getenv("MMSEG_LN_G");
+  if ((e && atoi(e) == 0) || C % 8 || ldx % 8 || ldy % 8) return 0;
+  const int c8 = C / 8;
+  int G = 8;
+  while (G < c8 && G < 64) G *= 2;
+  *V = (c8 + G - 1) / G;
+  if (c8 < 4) return 0;
+  return (*V == 1 || *V == 2 || *V == 3 || *V == 6) ? G : 0;
+}
+
+int ln_g_blocks(long long rows, int G) {
+  const long long per = 4LL * (64 / G) * 2;   // rows per block per loop iteration (U = 2)
+  long long b = (rows + per - 1) / per;
+  return (int)(b < 1024 ? (b < 1 ? 1 : b) : 1024);
+}
+
 template <typename T>
 int ln_fwd_t(const void* x, int ldx, void* y, int ldy, long long rows, int C, const float* gamma, const float* beta,
              float eps, float* mean, float* rstd, hipStream_t s) {
+  int V = 0;
+  const int G = ln_gv(C, ldx, ldy, &V);
+  if (G) {
+    const int nb = ln_g_blocks(rows, G);
+    mmseg::note_kernel("layernorm_fwd_g_kernel");
+#define LNG(GG, VV) MMSEG_LAUNCH((layernorm_fwd_g_kernel<T, GG, VV>), dim3(nb), dim3(256), 0, s, (const T*)x, ldx, \
+                                 (T*)y, ldy, rows, C, gamma, beta, eps, mean, rstd)
+    if (G == 8) LNG(8, 1);
+    else if (G == 16) LNG(16, 1);
+    else if (G == 32) LNG(32, 1);
+    else if (V == 1) LNG(64, 1);
+    else if (V == 2) LNG(64, 2);
+    else if (V == 3) LNG(64, 3);
+    else LNG(64, 6);
+#undef LNG
+    return mmseg::check_launch("layernorm_fwd_g");
+  }
   const int nl = ln_nl(C), nb = ln_blocks(rows);
   auto X = (const T*)x;
   auto Y = (T*)y;
@@ -525,12 +781,32 @@ int ln_fwd_t(const void* x, int ldx, void* y, int ldy, long long rows, int C, co
 
 template <typename T>
 int ln_bwd_t(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, long long rows, int C,
-             const float* gamma, const float* mean, const float* rstd, int add, float* part, hipStream_t s) {
+             const float* gamma, const float* mean, const float* rstd, int add, float* part, hipStream_t s,
+             int* part_rows) {
+  int V = 0;
+  const int G = (lddy % 8 == 0) ? ln_gv(C, ldx, lddx, &V) : 0;
+  if (G) {
+    const int nb = ln_g_blocks(rows, G);
+    *part_rows = G * V * 8 <= LNG_LDS_C ? nb : nb * 4;
+    mmseg::note_kernel("layernorm_bwd_g_kernel");
+#define LNGB(GG, VV) MMSEG_LAUNCH((layernorm_bwd_g_kernel<T, GG, VV>), dim3(nb), dim3(256), 0, s, (const T*)x, ldx, \
+                                  (const T*)dy, lddy, (T*)dx, lddx, rows, C, gamma, mean, rstd, add, part)
+    if (G == 8) LNGB(8, 1);
+    else if (G == 16) LNGB(16, 1);
+    else if (G == 32) LNGB(32, 1);
+    else if (V == 1) LNGB(64, 1);
+    else if (V == 2) LNGB(64, 2);
+    else if (V == 3) LNGB(64, 3);
+    else LNGB(64, 6);
+#undef LNGB
+    return mmseg::check_launch("layernorm_bwd_g");
+  }
   const int nl = ln_nl(C), nb = ln_blocks(rows);
+  *part_rows = nb * (64 * ln_nl(C) <= 1024 ? 1 : LN_WAVES);
   auto X = (const T*)x;
-  auto G = (const T*)dy;
+  auto Gd = (const T*)dy;
   auto O = (T*)dx;
-#define LNB(NL) MMSEG_LAUNCH((layernorm_bwd_kernel<T, NL>), dim3(nb), dim3(256), 0, s, X, ldx, G, lddy, O, lddx, \
+#define LNB(NL) MMSEG_LAUNCH((layernorm_bwd_kernel<T, NL>), dim3(nb), dim3(256), 0, s, X, ldx, Gd, lddy, O, lddx, \
                                    rows, C, gamma, mean, rstd, add, part)
   switch (nl) {
     case 1: LNB(1); break;
@@ -561,7 +837,8 @@ int mmseg_layernorm_fwd(const void* x, int ldx, void* y, int ldy, long long rows
 
 long long mmseg_layernorm_bwd_ws_floats(long long rows, int C) {
   const long long nb = ln_blocks(rows);
-  return nb * LN_WAVES * 2LL * C;
+  // (the row-group kernels: at most 1,024 blocks x 4 per-wave partials)
+  return std::max<long long>(nb * LN_WAVES, 1024LL * 4) * 2LL * C;
 }
 
 int mmseg_layernorm_bwd(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, long long rows, int C,
@@ -571,11 +848,11 @@ int mmseg_layernorm_bwd(const void* x, int ldx, const void* dy, int lddy, void* 
   MMSEG_REQUIRE(!(dgamma || dbeta) || ws != nullptr, "layernorm_bwd: parameter gradients need the workspace");
   hipStream_t s = (hipStream_t)stream;
   float* part = (dgamma || dbeta) ? ws : nullptr;
+  int nb = 0;
   const int r = dtype == MMSEG_BF16
-                    ? ln_bwd_t<bf16_t>(x, ldx, dy, lddy, dx, lddx, rows, C, gamma, mean, rstd, add_dx, part, s)
-                    : ln_bwd_t<float>(x, ldx, dy, lddy, dx, lddx, rows, C, gamma, mean, rstd, add_dx, part, s);
+                    ? ln_bwd_t<bf16_t>(x, ldx, dy, lddy, dx, lddx, rows, C, gamma, mean, rstd, add_dx, part, s, &nb)
+                    : ln_bwd_t<float>(x, ldx, dy, lddy, dx, lddx, rows, C, gamma, mean, rstd, add_dx, part, s, &nb);
   if (r || !part) return r;
-  const int nb = ln_blocks(rows) * (64 * ln_nl(C) <= 1024 ? 1 : LN_WAVES);
   MMSEG_LAUNCH(ln_param_reduce_kernel, dim3(ceil_div(2LL * C, 64)), dim3(64 * LNR_WAVES), 0, s, part, nb, C,
                      dgamma, dbeta, accumulate);
   return mmseg::check_launch("ln_param_reduce");

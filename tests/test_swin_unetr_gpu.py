@@ -34,9 +34,12 @@ def rel2(a, b):
     return ((a - b).norm() / b.norm()).item()
 
 
+@pytest.mark.parametrize("ln_g", ["1", "0"])   # r05 row-group kernels (default) / the wave-per-row kernels
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("C,affine", [(48, True), (96, False), (384, True), (1536, True), (3072, True)])
-def test_layernorm(dev, dtype, C, affine):
+@pytest.mark.parametrize("C,affine", [(48, True), (96, False), (192, True), (384, True), (768, False), (1536, True),
+                                      (3072, True)])
+def test_layernorm(dev, dtype, C, affine, ln_g, monkeypatch):
+    monkeypatch.setenv("MMSEG_LN_G", ln_g)
     g = torch.Generator().manual_seed(C)
     rows, ld = 300, C + 16
     x = (torch.randn(rows, ld, generator=g) * 3 + 1).to(dtype)
