@@ -283,15 +283,18 @@ __global__ __launch_bounds__(512) void winattn_fwd1_kernel(WinAttnArgs a) {
         const int4 ck = *reinterpret_cast<const int4*>(code + k0);
         const uint32_t rk = a.region ? *reinterpret_cast<const uint32_t*>(reg + k0) : 0u;
         const int c[4] = {ck.x, ck.y, ck.z, ck.w};
+        const bool last = kt == nt - 1;   // (wave-uniform) only the last key tile holds keys past N
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float t = fmaf(acc[r], sc2, tq[-c[r]]);
           if (a.region && ((rk >> (8 * r)) & 255u) != rq) t -= pen2;
-          v[kt][r] = (qv && k0 + r < a.N) ? t : -INFINITY;
-          mx = fmaxf(mx, v[kt][r]);
+          if (last && k0 + r >= a.N) t = -INFINITY;
+          v[kt][r] = t;
+          mx = fmaxf(mx, t);
         }
       }
     }
+    // (a padding query's row is finite -- its table codes are token 0's -- and is never stored: no select)
 #pragma unroll
     for (int o = 16; o <= 32; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
     float sum = 0.f;
@@ -300,7 +303,7 @@ __global__ __launch_bounds__(512) void winattn_fwd1_kernel(WinAttnArgs a) {
       if (kt < nt) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = v[kt][r] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(v[kt][r] - mx);
+          const float p = __builtin_amdgcn_exp2f(v[kt][r] - mx);   // exp2(-inf) = 0
           v[kt][r] = p;
           sum += p;
         }
