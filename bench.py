@@ -309,6 +309,7 @@ def main():
                     help="one GPU, the data-parallel step: an RCCL process group of world size 1 with "
                          "distributed.reduce_single_rank, so the bucket all-reduces (AVG) really run through RCCL "
                          "inside the captured step, exactly as each rank of the N-GPU job runs them")
+    ap.add_argument("--bucket-mb", type=float, default=32.0, help="DP gradient bucket size (distributed.bucket_mb)")
     ap.add_argument("--workload-out", default="", help="write this run's workload key (JSON) for the profile "
                                                        "summaries of tools/rocprof_families.py")
     args = ap.parse_args()
@@ -342,6 +343,7 @@ def main():
     mods = args.modalities.split(",")
     cfg = make_config(args.model, args.batch, args.dtype, size=args.size, modalities=mods, loss=args.loss,
                       kernels=args.kernels, amp=args.amp, fp8=args.fp8)
+    cfg["distributed"]["bucket_mb"] = args.bucket_mb
     if args.dp_rehearsal:
         cfg["distributed"]["reduce_single_rank"] = True
     if args.kernels == "torch":
