@@ -171,6 +171,12 @@ int mmseg_conv_gemm_split(const void* a, int lda, const void* wpacked, const flo
                           void* out2, int ldo2, int split, float* splitk_ws, int mode, int M, int Ncols, int Cpad,
                           int KG, int cpg_shift, int D, int H, int W, int ksplit, int cin_real, int dtype,
                           void* stream);
+/* 1x1 GEMM (MODE_POINT, no split-K) with a residual epilogue: out = round(round(A W^T + bias) + res) -- bitwise the
+ * GEMM into a temporary followed by mmseg_add(res, temporary, out); res may alias out; ldo, ldres, Ncols multiples
+ * of 8, out / res 16-B aligned.  SwinUNETR's residual sums (UnetResBlock dx += d(conv3 branch), MLP x + fc2(.);
+ * reference swin_unetr.py:80-96 -> MONAI) without their own pass. */
+int mmseg_conv_gemm_res(const void* a, int lda, const void* wpacked, const float* bias, const void* res, int ldres,
+                        void* out, int ldo, int M, int Ncols, int Cpad, int KG, int dtype, void* stream);
 /* Deferred InstanceNorm + ReLU of a 3^3 conv's input (the block's conv1 output is never written by its
  * normalisation pass): the input holds the PRE-norm activation and the kernels stage
  * relu((x - mean[n][c]) * rstd[n][c]) rounded to bf16, the values mmseg_instnorm_relu_fwd would write.
@@ -274,6 +280,22 @@ int mmseg_instnorm_relu_bwd(const void* x, int ldx, const float* mean, const flo
                             float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
                             const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N,
                             int D, int H, int W, int C, float* ws, int dtype, void* stream);
+/* Backward of InstanceNorm3d (no affine) + LeakyReLU(slope): g is the gradient of the activation's output, dx that
+ * of the norm's input x (MONAI UnetResBlock conv1 -> norm1 -> lrelu, reference swin_unetr.py:80-96); the
+ * activation's backward runs inside the norm's passes.  ws: mmseg_instnorm_ws_floats. */
+int mmseg_instnorm_lrelu_bwd(const void* x, int ldx, const float* mean, const float* rstd, const void* g, int ldg,
+                             void* dx, int lddx, int N, int D, int H, int W, int C, float slope, float* ws, int dtype,
+                             void* stream);
+/* Chunks per sample of the InstanceNorm-backward partial sums over V voxels x C channels (0: unsupported shape). */
+int mmseg_instnorm_part_chunks(long long V, int C);
+/* UnetResBlock tail backward, first pass (y = LeakyReLU(IN(xa) + IN(xb)) or LeakyReLU(IN(xa) + residual)):
+ * g = dy * (y > 0 ? 1 : slope), stored, and in the same pass the InstanceNorm-backward partial sums of xa (and of xb
+ * if non-NULL) over g: pa / pb [N][mmseg_instnorm_part_chunks(V, C)][C][2], the layout mmseg_instnorm_bwd_part
+ * finalises and applies.  Bitwise what mmseg_lrelu_bwd + the norms' own partial passes give. */
+int mmseg_lrelu_bwd_in_part(const void* y, int ldy, const void* dy, int lddy, void* g, int ldg, float slope,
+                            const void* xa, int lda, const float* ma, const float* ra, float* pa, const void* xb,
+                            int ldb, const float* mb, const float* rb, float* pb, int N, long long V, int C, int dtype,
+                            void* stream);
 /* Statistics + normalisation (+ ReLU if relu) in one call: y = [relu]((x - mean) * rstd), mean / rstd written as
  * by mmseg_instnorm_stats (mean_ld == C).  Volumes of <= 4096 voxels per sample take one fused launch (one block
  * per 8-channel group and sample, the 12^3 / 6^3 levels); larger ones the stats + apply passes. */

@@ -62,7 +62,7 @@ _VALUE_FUNCS = ("mmseg_abi_version", "mmseg_wgrad_splits", "mmseg_wgrad_splits_c
                 "mmseg_head_loss_ok", "mmseg_conv3_norm_ok", "mmseg_conv3_wgrad_norm_ok", "mmseg_head_loss_in_chunks",
                 "mmseg_conv3_dgrad_in_chunks", "mmseg_stem_stats_bricks", "mmseg_conv3_fp8_ok",
                 "mmseg_conv3_group_ok", "mmseg_conv3_wgrad_group_ok", "mmseg_conv3_group_splits", "mmseg_winattn_sum_groups",
-                "mmseg_conv3_group_stats_bricks",
+                "mmseg_conv3_group_stats_bricks", "mmseg_instnorm_part_chunks",
                 "mmseg_wgrad_reduce_flush", "mmseg_wgrad_reduce_pending", "mmseg_wgrad_reduce_discard")
 
 

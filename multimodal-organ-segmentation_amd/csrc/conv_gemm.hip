@@ -116,6 +116,11 @@ struct GemmArgs {
   int grp_n;
   long long w_gstride;
   int b_gstride;
+  // residual epilogue (MODE_POINT, ksplit 1, vector stores; mmseg_conv_gemm_res): out = round(round(acc + bias) +
+  // res), the values of the GEMM followed by mmseg_add(res, out) -- a residual sum without its own pass (res may
+  // alias out)
+  const void* res;
+  int ldres;
 };
 
 // Output element (row voxel, column) of a GEMM (split-aware; split is a multiple of 8).
@@ -435,6 +440,12 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs g) {
     if (row >= g.M || col >= g.Ncols) continue;
     V8<T> o;
     o.load(El + lr * EPT + cg * 8);
+    if (MODE == MODE_POINT && g.res) {
+      V8<T> rv;
+      rv.load(reinterpret_cast<const T*>(g.res) + row * g.ldres + col);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o.set(j, o.get(j) + rv.get(j));
+    }
     o.store(out_at<T>(g, row, col));
   }
 }
@@ -5646,7 +5657,8 @@ int mmseg_conv_gemm_stats(const void* a, int lda, const void* wpacked, const flo
 int conv_gemm_impl(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo, void* out2,
                    int ldo2, int split, float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift,
                    int D, int H, int W, int ksplit, float* stats_part, int cin_real, int dtype, void* stream,
-                   int groups = 1, long long w_gstride = 0, int b_gstride = 0);
+                   int groups = 1, long long w_gstride = 0, int b_gstride = 0, const void* res = nullptr,
+                   int ldres = 0);
 int mmseg_conv3_group_stats_bricks(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda,
                                    int ldo, int dtype);
 
@@ -5684,6 +5696,16 @@ int mmseg_conv_gemm_ex(const void* a, int lda, const void* wpacked, const float*
                         cpg_shift, D, H, W, ksplit, stats_part, cin_real, dtype, stream);
 }
 
+// 1x1 GEMM (MODE_POINT, ksplit 1) whose epilogue adds a residual: out = round(round(A W^T + bias) + res), bitwise
+// mmseg_conv_gemm into a temporary followed by mmseg_add(res, temporary, out); res may alias out.  The SwinUNETR
+// residual sums (UnetResBlock input gradient dx += d(conv3 branch), the MLP residual x + fc2(.)) without a pass.
+int mmseg_conv_gemm_res(const void* a, int lda, const void* wpacked, const float* bias, const void* res, int ldres,
+                        void* out, int ldo, int M, int Ncols, int Cpad, int KG, int dtype, void* stream) {
+  MMSEG_REQUIRE(res != nullptr, "conv_gemm_res: residual required");
+  return conv_gemm_impl(a, lda, wpacked, bias, out, ldo, nullptr, 0, 0, nullptr, MODE_POINT, M, Ncols, Cpad, KG, 0, 1,
+                        1, 1, 1, nullptr, 0, dtype, stream, 1, 0, 0, res, ldres);
+}
+
 // mmseg_conv_gemm_ex (no fused statistics) whose output columns [split, Ncols) go to a second tensor out2 (row
 // pitch ldo2) as columns 0..: the decoder's first-conv data gradient writes d(upsampled) and d(skip) dense.
 int mmseg_conv_gemm_split(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
@@ -5701,7 +5723,11 @@ int mmseg_conv_gemm_split(const void* a, int lda, const void* wpacked, const flo
 int conv_gemm_impl(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo, void* out2,
                    int ldo2, int split, float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift,
                    int D, int H, int W, int ksplit, float* stats_part, int cin_real, int dtype, void* stream,
-                   int groups, long long w_gstride, int b_gstride) {
+                   int groups, long long w_gstride, int b_gstride, const void* res, int ldres) {
+  MMSEG_REQUIRE(!res || (mode == MODE_POINT && ksplit == 1 && !out2 && ldo % 8 == 0 && ldres % 8 == 0 &&
+                         Ncols % 8 == 0 && ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(res)) &
+                                            15) == 0),
+                "conv_gemm_res: MODE_POINT, ksplit 1, pitches and Ncols multiples of 8, 16-B aligned out / res");
   MMSEG_REQUIRE(cin_real >= 0 && cin_real <= (8 << cpg_shift), "conv_gemm: cin_real %d outside [0, %d]", cin_real,
                 8 << cpg_shift);
   MMSEG_REQUIRE(!stats_part || (mode == MODE_CONV3 && ksplit == 1 &&
@@ -5727,6 +5753,8 @@ int conv_gemm_impl(const void* a, int lda, const void* wpacked, const float* bia
     g.w_gstride = w_gstride;
     g.b_gstride = b_gstride;
   }
+  g.res = res;
+  g.ldres = ldres;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16) return launch_gemm_mode<bf16_t>(g, mode, s);
   return launch_gemm_mode<float>(g, mode, s);

@@ -367,7 +367,17 @@ struct DySrc {
   const uint8_t* pool_idx;  // [N][Vo][C]
   int p1_nmod;           // > 0: p1 holds p1_nmod samples, sample n reads p1 sample n % p1_nmod (the fused level's
                          // gradient shared by the M modality groups of a grouped backward)
+  float slope;           // ACT 2: the LeakyReLU's negative slope
 };
+
+// gradient through the activation that follows the norm (h: the normalised value; an activation keeps the sign,
+// so h > 0 is where its output is > 0): ACT 0 none, 1 ReLU, 2 LeakyReLU
+template <int ACT>
+__device__ __forceinline__ float act_grad(float h, float dy, float slope) {
+  if constexpr (ACT == 0) return dy;
+  else if constexpr (ACT == 1) return h > 0.f ? dy : 0.f;
+  else return h > 0.f ? dy : dy * slope;
+}
 
 // Per-thread view of a DySrc for one sample and one 8-channel group: the
 // scale, beta and base pointers are resolved once, the per-voxel work is the
@@ -437,7 +447,7 @@ struct DyCtx {
 };
 
 // partial sums of g and g*xhat, g = dy * [xhat > 0]
-template <typename T, bool RELU = true>
+template <typename T, int ACT = 1>
 __global__ void in_bwd_partial(const T* __restrict__ x, int ldx, const float* __restrict__ mean,
                                const float* __restrict__ rstd, DySrc s, int V, int C, int D, int H, int W, int vpc,
                                float* __restrict__ part) {
@@ -476,7 +486,7 @@ __global__ void in_bwd_partial(const T* __restrict__ x, int ldx, const float* __
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float h = (a[u].get(j) - mu[j]) * rs[j];
-          const float g = (!RELU || h > 0.f) ? dy[j] : 0.f;
+          const float g = act_grad<ACT>(h, dy[j], s.slope);
           sg[j] += g;
           sgx[j] = fmaf(g, h, sgx[j]);
         }
@@ -564,7 +574,7 @@ __global__ void in_bwd_finalize(const float* __restrict__ part, int N, int C, in
 }
 
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)); same thread layout as the apply kernels
-template <typename T, bool RELU = true>
+template <typename T, int ACT = 1>
 __global__ void in_bwd_apply(const T* __restrict__ x, int ldx, const float* __restrict__ mean,
                              const float* __restrict__ rstd, DySrc s, const float* __restrict__ coef, T* __restrict__ dx,
                              int lddx, int V, int C, int D, int H, int W, int vpc) {
@@ -608,7 +618,7 @@ __global__ void in_bwd_apply(const T* __restrict__ x, int ldx, const float* __re
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float h = (a[u].get(j) - mu[j]) * rs[j];
-        const float g = (!RELU || h > 0.f) ? dy[j] : 0.f;
+        const float g = act_grad<ACT>(h, dy[j], s.slope);
         o.set(j, rs[j] * (g - ca[j] - h * cb[j]));
       }
       o.store(dxn + (long long)(vb + u * lanes_v) * lddx);
@@ -616,6 +626,127 @@ __global__ void in_bwd_apply(const T* __restrict__ x, int ldx, const float* __re
   }
 }
 
+// The UnetResBlock tail's backward, first pass (y = lrelu(IN(xa) + IN(xb) | + residual)): g = dy * (y > 0 ? 1 :
+// slope), stored (the norms' apply passes and the residual branch read it), and in the same pass the partial sums
+// (sum g, sum g xhat) of the InstanceNorm backward of xa and, NX = 2, of xb -- over g as stored, with
+// in_bwd_partial's chunks, per-thread voxel order and reduction tree, so the partials and everything after them
+// are those of lrelu_bwd_kernel + in_bwd_partial bit for bit, without the separate passes over g.
+template <typename T, int NX>
+__global__ __launch_bounds__(256) void lrelu_bwd_in_partial(const T* __restrict__ y, int ldy,
+                                                            const T* __restrict__ dy, int lddy, T* __restrict__ g,
+                                                            int ldg, float slope, const T* __restrict__ xa, int lda,
+                                                            const float* __restrict__ ma, const float* __restrict__ ra,
+                                                            float* __restrict__ pa, const T* __restrict__ xb, int ldb,
+                                                            const float* __restrict__ mb, const float* __restrict__ rb,
+                                                            float* __restrict__ pb, int V, int C, int vpc) {
+  constexpr int K = 1 + NX;    // sum g, sum g xhat_a (, sum g xhat_b)
+  const int n = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
+  const int C8 = C >> 3, lanes_v = 256 / C8;
+  const int tid = threadIdx.x, cg = tid % C8, vl = tid / C8;
+  float acc[K][8], mua[8], rsa[8], mub[8], rsb[8];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
+  load8f(ma + n * C + cg * 8, mua);
+  load8f(ra + n * C + cg * 8, rsa);
+  if constexpr (NX > 1) {
+    load8f(mb + n * C + cg * 8, mub);
+    load8f(rb + n * C + cg * 8, rsb);
+  }
+  const long long row0 = (long long)n * V;
+  const int v0 = chunk * vpc;
+  const int v1 = v0 + vpc < V ? v0 + vpc : V;
+  if (vl < lanes_v) {
+    for (int vb = v0 + vl; vb < v1; vb += UNR * lanes_v) {
+      V8<T> vy[UNR], vd[UNR], va[UNR], vx[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+        if (vb + u * lanes_v < v1) {
+          const long long t = row0 + vb + u * lanes_v;
+          vy[u].load(y + t * ldy + cg * 8);
+          vd[u].load(dy + t * lddy + cg * 8);
+          va[u].load(xa + t * lda + cg * 8);
+          if constexpr (NX > 1) vx[u].load(xb + t * ldb + cg * 8);
+        }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        if (vb + u * lanes_v >= v1) break;
+        const long long t = row0 + vb + u * lanes_v;
+        V8<T> gv;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gv.set(j, vy[u].get(j) > 0.f ? vd[u].get(j) : vd[u].get(j) * slope);
+        gv.store(g + t * ldg + cg * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float gg = gv.get(j);
+          const float h = (va[u].get(j) - mua[j]) * rsa[j];
+          acc[0][j] += gg;
+          acc[1][j] = fmaf(gg, h, acc[1][j]);
+          if constexpr (NX > 1) {
+            const float h2 = (vx[u].get(j) - mub[j]) * rsb[j];
+            acc[2][j] = fmaf(gg, h2, acc[2][j]);
+          }
+        }
+      }
+    }
+  }
+  // in_bwd_partial's reduction, K sums at once
+  __shared__ float red[K][256 * 8];
+  float* const pout[2] = {pa + ((long long)n * nchunk + chunk) * C * 2,
+                          NX > 1 ? pb + ((long long)n * nchunk + chunk) * C * 2 : nullptr};
+  if ((C8 & (C8 - 1)) == 0 && C8 <= 32) {
+    for (int o = 32; o >= C8; o >>= 1) {
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[k][j] += __shfl_down(acc[k][j], o, 64);
+    }
+    const int lane = tid & 63, wave = tid >> 6;
+    if (lane < C8) {
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) red[k][(wave * C8 + lane) * 8 + j] = acc[k][j];
+    }
+    __syncthreads();
+    if (tid < C) {
+      const int gi = tid >> 3, j = tid & 7;
+      float s[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        s[k] = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) s[k] += red[k][(w * C8 + gi) * 8 + j];
+      }
+#pragma unroll
+      for (int x = 0; x < NX; ++x) {
+        pout[x][tid * 2] = s[0];
+        pout[x][tid * 2 + 1] = s[1 + x];
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[k][tid * 8 + j] = acc[k][j];
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    const int gi = c >> 3, j = c & 7;
+    float s[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) s[k] = 0.f;
+    for (int l = 0; l < lanes_v; ++l)
+#pragma unroll
+      for (int k = 0; k < K; ++k) s[k] += red[k][(l * C8 + gi) * 8 + j];
+#pragma unroll
+    for (int x = 0; x < NX; ++x) {
+      pout[x][c * 2] = s[0];
+      pout[x][c * 2 + 1] = s[1 + x];
+    }
+  }
+}
 
 // ------------------------------------------------- small-volume fused IN
 // The 12^3 / 6^3 levels (V <= 4096 voxels per sample): one 256-thread block per (8-channel group, sample)
@@ -737,7 +868,7 @@ __global__ __launch_bounds__(SMALL_T) void in_small_fwd(const T* __restrict__ x,
   }
 }
 
-template <typename T, bool RELU>
+template <typename T, int ACT>
 __global__ __launch_bounds__(SMALL_T) void in_small_bwd(const T* __restrict__ x, int ldx, const float* __restrict__ mean,
                                                        const float* __restrict__ rstd, DySrc s, T* __restrict__ dx,
                                                        int lddx, int V, int C, int D, int H, int W) {
@@ -768,7 +899,7 @@ __global__ __launch_bounds__(SMALL_T) void in_small_bwd(const T* __restrict__ x,
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float h = (a[u].get(j) - mu[j]) * rs[j];
-        const float g = (!RELU || h > 0.f) ? dy[j] : 0.f;
+        const float g = act_grad<ACT>(h, dy[j], s.slope);
         ga[j] += g;
         gb[j] = fmaf(g, h, gb[j]);
       }
@@ -817,7 +948,7 @@ __global__ __launch_bounds__(SMALL_T) void in_small_bwd(const T* __restrict__ x,
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float h = (a[u].get(j) - mu[j]) * rs[j];
-        const float g = (!RELU || h > 0.f) ? dy[j] : 0.f;
+        const float g = act_grad<ACT>(h, dy[j], s.slope);
         o.set(j, rs[j] * (g - ca[j] - h * cb[j]));
       }
       o.store(dxn + (long long)(v0 + u * SMALL_T) * lddx);
@@ -912,7 +1043,7 @@ __global__ __launch_bounds__(SMALL_T) void in_small_fwd_r(const T* __restrict__ 
   }
 }
 
-template <typename T, bool RELU, int VPT>
+template <typename T, int ACT, int VPT>
 __global__ __launch_bounds__(SMALL_T) void in_small_bwd_r(const T* __restrict__ x, int ldx,
                                                          const float* __restrict__ mean, const float* __restrict__ rstd,
                                                          DySrc s, T* __restrict__ dx, int lddx, int V, int C, int D,
@@ -946,7 +1077,7 @@ __global__ __launch_bounds__(SMALL_T) void in_small_bwd_r(const T* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float h = (a[u].get(j) - mu[j]) * rs[j];
-      const float g = (!RELU || h > 0.f) ? dy[u][j] : 0.f;
+      const float g = act_grad<ACT>(h, dy[u][j], s.slope);
       ga[j] += g;
       gb[j] = fmaf(g, h, gb[j]);
     }
@@ -983,7 +1114,7 @@ __global__ __launch_bounds__(SMALL_T) void in_small_bwd_r(const T* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float h = (a[u].get(j) - mu[j]) * rs[j];
-      const float g = (!RELU || h > 0.f) ? dy[u][j] : 0.f;
+      const float g = act_grad<ACT>(h, dy[u][j], s.slope);
       o.set(j, rs[j] * (g - ca[j] - h * cb[j]));
     }
     o.store(dxn + (long long)(tid + u * SMALL_T) * lddx);
@@ -1071,7 +1202,7 @@ __global__ __launch_bounds__(SMALL_T1K) void in_small_fwd_1k(const T* __restrict
   }
 }
 
-template <typename T, bool RELU>
+template <typename T, int ACT>
 __global__ __launch_bounds__(SMALL_T1K) void in_small_bwd_1k(const T* __restrict__ x, int ldx, const float* __restrict__ mean,
                                                        const float* __restrict__ rstd, DySrc s, T* __restrict__ dx,
                                                        int lddx, int V, int C, int D, int H, int W) {
@@ -1094,7 +1225,7 @@ __global__ __launch_bounds__(SMALL_T1K) void in_small_bwd_1k(const T* __restrict
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float h = (a.get(j) - mu[j]) * rs[j];
-      const float g = (!RELU || h > 0.f) ? dy[j] : 0.f;
+      const float g = act_grad<ACT>(h, dy[j], s.slope);
       ga[j] += g;
       gb[j] = fmaf(g, h, gb[j]);
     }
@@ -1133,7 +1264,7 @@ __global__ __launch_bounds__(SMALL_T1K) void in_small_bwd_1k(const T* __restrict
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float h = (a.get(j) - mu[j]) * rs[j];
-      const float g = (!RELU || h > 0.f) ? dy[j] : 0.f;
+      const float g = act_grad<ACT>(h, dy[j], s.slope);
       o.set(j, rs[j] * (g - ca[j] - h * cb[j]));
     }
     o.store(dxn + (long long)v * lddx);
@@ -1566,7 +1697,7 @@ int instnorm_bwd_impl(const void* x, int ldx, const float* mean, const float* rs
                       float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
                       const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N, int D,
                       int H, int W, int C, int relu, const float* part_in, int nchunk_in, float* ws, int dtype,
-                      void* stream, int p1_nmod);
+                      void* stream, int p1_nmod, float slope = 0.f);
 
 // The InstanceNorm + ReLU backward of G modality encoders' level outputs at once (N = G x n samples of one
 // combined pre-norm tensor / statistics / pooled gradient): every sample reads the fused level's gradient p1 of
@@ -1580,6 +1711,52 @@ int mmseg_instnorm_relu_bwd_group(const void* x, int ldx, const float* mean, con
                 N, p1_nmod);
   return instnorm_bwd_impl(x, ldx, mean, rstd, p1, ld1, scale1, nullptr, 0, nullptr, 0, pool_dy, pool_ld, pool_idx,
                            dx, lddx, N, D, H, W, C, 1, nullptr, 0, ws, dtype, stream, p1_nmod);
+}
+
+// The InstanceNorm + LeakyReLU backward (SwinUNETR's UnetResBlock conv1 -> IN -> LeakyReLU, MONAI
+// get_norm_layer("instance") + get_act_layer(("leakyrelu", {"negative_slope": 0.01}))): g is the gradient of the
+// activation's OUTPUT; the activation's backward (g, or slope * g where the normalised value is <= 0) is applied
+// in the norm's passes instead of a separate pass over g.
+int mmseg_instnorm_lrelu_bwd(const void* x, int ldx, const float* mean, const float* rstd, const void* g, int ldg,
+                             void* dx, int lddx, int N, int D, int H, int W, int C, float slope, float* ws, int dtype,
+                             void* stream) {
+  return instnorm_bwd_impl(x, ldx, mean, rstd, g, ldg, 1.f, nullptr, 0, nullptr, 0, nullptr, 0, nullptr, dx, lddx, N,
+                           D, H, W, C, 2, nullptr, 0, ws, dtype, stream, 0, slope);
+}
+
+int mmseg_instnorm_part_chunks(long long V, int C) {
+  long long vpc;
+  return (C % 8 == 0 && C <= 2048 && V > 0) ? chunks_for(V, C, &vpc) : 0;
+}
+
+int mmseg_lrelu_bwd_in_part(const void* y, int ldy, const void* dy, int lddy, void* g, int ldg, float slope,
+                            const void* xa, int lda, const float* ma, const float* ra, float* pa, const void* xb,
+                            int ldb, const float* mb, const float* rb, float* pb, int N, long long V, int C, int dtype,
+                            void* stream) {
+  MMSEG_REQUIRE(C % 8 == 0 && C <= 2048 && V > 0, "lrelu_bwd_in_part: C=%d must be a multiple of 8", C);
+  MMSEG_REQUIRE(y && dy && g && xa && ma && ra && pa, "lrelu_bwd_in_part: null operand");
+  MMSEG_REQUIRE(!xb || (mb && rb && pb), "lrelu_bwd_in_part: xb needs its statistics and partial buffer");
+  const int ldmax = std::max(std::max(ldy, lddy), std::max(std::max(ldg, lda), xb ? ldb : 0));
+  MMSEG_REQUIRE(V * ldmax < (1LL << 31), "lrelu_bwd_in_part: per-sample extent must fit int32");
+  MMSEG_REQUIRE(ldy % 8 == 0 && lddy % 8 == 0 && ldg % 8 == 0 && lda % 8 == 0 && (!xb || ldb % 8 == 0),
+                "lrelu_bwd_in_part: pitches must be multiples of 8");
+  long long vpc;
+  const int nch = chunks_for(V, C, &vpc);
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid(nch, N);
+  auto run = [&](auto tag) {
+    using T = decltype(tag);
+    if (xb)
+      MMSEG_LAUNCH((lrelu_bwd_in_partial<T, 2>), grid, dim3(256), 0, s, (const T*)y, ldy, (const T*)dy, lddy, (T*)g,
+                   ldg, slope, (const T*)xa, lda, ma, ra, pa, (const T*)xb, ldb, mb, rb, pb, (int)V, C, (int)vpc);
+    else
+      MMSEG_LAUNCH((lrelu_bwd_in_partial<T, 1>), grid, dim3(256), 0, s, (const T*)y, ldy, (const T*)dy, lddy, (T*)g,
+                   ldg, slope, (const T*)xa, lda, ma, ra, pa, (const T*)nullptr, 0, nullptr, nullptr, nullptr, (int)V,
+                   C, (int)vpc);
+  };
+  if (dtype == MMSEG_BF16) run(bf16_t{});
+  else run(float{});
+  return mmseg::check_launch("lrelu_bwd_in_part");
 }
 
 int mmseg_instnorm_bwd(const void* x, int ldx, const float* mean, const float* rstd, const void* p1, int ld1,
@@ -1605,7 +1782,8 @@ int instnorm_bwd_impl(const void* x, int ldx, const float* mean, const float* rs
                       float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
                       const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N, int D,
                       int H, int W, int C, int relu, const float* part_in, int nchunk_in, float* ws, int dtype,
-                      void* stream, int p1_nmod) {
+                      void* stream, int p1_nmod, float slope) {
+  MMSEG_REQUIRE(relu >= 0 && relu <= 2, "instnorm_bwd: activation %d (0 none, 1 ReLU, 2 LeakyReLU)", relu);
   MMSEG_REQUIRE(C % 8 == 0 && C <= 2048, "instnorm_bwd: C=%d must be a multiple of 8 and <= 2048", C);
   MMSEG_REQUIRE(!part_in || nchunk_in > 0, "instnorm_bwd: given partials need their chunk count");
   MMSEG_REQUIRE(!pool_dy || ((D | H | W) & 1) == 0, "instnorm_bwd: pooled gather needs even dims");
@@ -1616,16 +1794,16 @@ int instnorm_bwd_impl(const void* x, int ldx, const float* mean, const float* rs
   const int nch = chunks_for(V, C, &vpc);
   int avpc;
   const int anch = apply_chunks(V, C, &avpc);
-  DySrc src{p1, ld1, scale1, alpha1, alpha_stride, beta, beta_stride, pool_dy, pool_ld, pool_idx, p1_nmod};
+  DySrc src{p1, ld1, scale1, alpha1, alpha_stride, beta, beta_stride, pool_dy, pool_ld, pool_idx, p1_nmod, slope};
   hipStream_t s = (hipStream_t)stream;
   float* part = ws;
   float* coef = ws + (long long)N * nch * C * 2;
   dim3 grid(nch, N), agrid(anch, N);
   const bool small = V <= knob_small_v() && !part_in;
   if (part_in) coef = ws;
-  auto run = [&](auto tag, auto relu_c) {
+  auto run = [&](auto tag, auto act_c) {
     using T = decltype(tag);
-    constexpr bool R = decltype(relu_c)::value;
+    constexpr int R = decltype(act_c)::value;
     if (part_in) {
       MMSEG_LAUNCH(in_bwd_finalize, dim3(N * C), dim3(256), 0, s, part_in, N, C, nchunk_in, V, coef);
       MMSEG_LAUNCH((in_bwd_apply<T, R>), agrid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, coef,
@@ -1653,13 +1831,13 @@ int instnorm_bwd_impl(const void* x, int ldx, const float* mean, const float* rs
     MMSEG_LAUNCH((in_bwd_apply<T, R>), agrid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, coef, (T*)dx,
                        lddx, (int)V, C, D, H, W, avpc);
   };
-  if (dtype == MMSEG_BF16) {
-    if (relu) run(bf16_t{}, std::true_type{});
-    else run(bf16_t{}, std::false_type{});
-  } else {
-    if (relu) run(float{}, std::true_type{});
-    else run(float{}, std::false_type{});
-  }
+  auto act = [&](auto tag) {
+    if (relu == 2) run(tag, std::integral_constant<int, 2>{});
+    else if (relu == 1) run(tag, std::integral_constant<int, 1>{});
+    else run(tag, std::integral_constant<int, 0>{});
+  };
+  if (dtype == MMSEG_BF16) act(bf16_t{});
+  else act(float{});
   return mmseg::check_launch("instnorm_relu_bwd");
 }
 
@@ -1679,18 +1857,18 @@ int mmseg_instnorm_bwd_coef(const void* x, int ldx, const float* mean, const flo
     const int nch = chunks_for(V, C, &vpc);
     DySrc src{p1, ld1, 1.f, nullptr, 0, nullptr, 0, nullptr, 0, nullptr};
     const dim3 grid(nch, N);
-    auto run = [&](auto tag, auto relu_c) {
+    auto run = [&](auto tag, auto act_c) {
       using T = decltype(tag);
-      constexpr bool R = decltype(relu_c)::value;
+      constexpr int R = decltype(act_c)::value;
       MMSEG_LAUNCH((in_bwd_partial<T, R>), grid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, (int)V, C,
                          D, H, W, (int)vpc, ws);
     };
     if (dtype == MMSEG_BF16) {
-      if (relu) run(bf16_t{}, std::true_type{});
-      else run(bf16_t{}, std::false_type{});
+      if (relu) run(bf16_t{}, std::integral_constant<int, 1>{});
+      else run(bf16_t{}, std::integral_constant<int, 0>{});
     } else {
-      if (relu) run(float{}, std::true_type{});
-      else run(float{}, std::false_type{});
+      if (relu) run(float{}, std::integral_constant<int, 1>{});
+      else run(float{}, std::integral_constant<int, 0>{});
     }
     part_in = ws;
     nchunk_in = nch;

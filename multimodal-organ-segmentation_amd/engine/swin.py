@@ -88,6 +88,12 @@ def shift_mask(dims_p, ws, ss) -> np.ndarray:
     return np.where(m != 0, np.float32(-100.0), np.float32(0.0)).astype(np.float32)
 
 
+def _res_fuse() -> bool:
+    """The residual sums folded into their producers (mmseg_conv_gemm_res, mmseg_lrelu_bwd_in_part); MMSEG_RES_FUSE=0
+    keeps the separate passes (bitwise the same results)."""
+    return os.environ.get("MMSEG_RES_FUSE", "1") != "0"
+
+
 class Lin:
     """Token linear y[M][Co] = x[M][Cip] W^T (+ b) as a 1x1 implicit GEMM (MODE_POINT), weight [Co][Ci...]
     (trailing dims flattened: the PatchEmbed kernel [Co][Cin][2][2][2] is a [Co][8 Cin] linear over the
@@ -116,16 +122,31 @@ class Lin:
             d.append((ptr(self.w), ptr(self.wd), 3, self.Co, self.Ci, self.Ci, self.KGd, self.KGdp, self.Cpad_d))
         return d
 
-    def fwd(self, x: torch.Tensor, ldx: int, M: int, y: torch.Tensor, ldy: int):
+    def fwd(self, x: torch.Tensor, ldx: int, M: int, y: torch.Tensor, ldy: int, res: Optional[torch.Tensor] = None):
+        """res (pitch ldy, may be y): y = res + x W^T (+ b), from the GEMM's epilogue when it runs without split-K
+        (mmseg_conv_gemm_res), else through a temporary and mmseg_add -- bitwise the same."""
+        L = self.rt.lib
         ks = _gemm_ksplit(M, self.Co, self.KG)
+        fuse = res is not None and ks == 1 and _res_fuse()
+        out = y if res is None or fuse else torch.empty(M * ldy, dtype=self.rt.dtype, device=self.rt.device)
         ws = self.rt.ws(ks * M * self.Co) if ks > 1 else None
         with TIMER.region(_gemm_name(self.rt, 0, "point"), flops=2.0 * M * self.Ci * self.Co,
                           nbytes=_io_bytes(self.rt, M, self.Cip, self.Co, self.Ci * self.Co)):
-            self.rt.lib.mmseg_conv_gemm(ptr(x), ldx, ptr(self.wf), ptr(self.b), ptr(y), ldy, ptr(ws), MODE_POINT, M,
-                                        self.Co, self.Cpad, self.KG, 0, 1, 1, 1, ks, self.rt.code, self.rt.stream)
+            if fuse:
+                L.mmseg_conv_gemm_res(ptr(x), ldx, ptr(self.wf), ptr(self.b), ptr(res), ldy, ptr(y), ldy, M, self.Co,
+                                      self.Cpad, self.KG, self.rt.code, self.rt.stream)
+            else:
+                L.mmseg_conv_gemm(ptr(x), ldx, ptr(self.wf), ptr(self.b), ptr(out), ldy, ptr(ws), MODE_POINT, M,
+                                  self.Co, self.Cpad, self.KG, 0, 1, 1, 1, ks, self.rt.code, self.rt.stream)
+        if res is not None and not fuse:
+            if ldy != self.Co:
+                raise ValueError("token linear with a residual: dense rows only on the unfused path")
+            L.mmseg_add(ptr(res), ptr(out), ptr(y), M * ldy, self.rt.code, self.rt.stream)
 
     def bwd(self, x: torch.Tensor, ldx: int, dy: torch.Tensor, lddy: int, M: int, dx: Optional[torch.Tensor],
-            lddx: int, accumulate: bool):
+            lddx: int, accumulate: bool, dx_add: bool = False):
+        """dx_add: dx += the data gradient (a residual branch's; the GEMM's epilogue adds it, mmseg_conv_gemm_res,
+        when it runs without split-K), instead of dx := it."""
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
         ks = L.mmseg_wgrad_splits(M, _wgrad_ksplit(self.Co, self.Cip, M))
         defer = self.rt.defer_wred(self.flat)
@@ -142,11 +163,20 @@ class Lin:
         self.flat.mark(*[p for p in (self.w, self.b) if p is not None])
         if dx is not None:
             kd = _gemm_ksplit(M, self.Ci, self.KGd)
+            if dx_add and (kd > 1 or not _res_fuse()):
+                raise ValueError("Lin.bwd(dx_add): the residual epilogue needs the unsplit GEMM")
             ws = self.rt.ws(kd * M * self.Ci) if kd > 1 else None
             with TIMER.region(_gemm_name(self.rt, 0, "point"), flops=2.0 * M * self.Ci * self.Co,
                               nbytes=_io_bytes(self.rt, M, self.Co, self.Ci, self.Ci * self.Co)):
-                L.mmseg_conv_gemm(ptr(dy), lddy, ptr(self.wd), None, ptr(dx), lddx, ptr(ws), MODE_POINT, M, self.Ci,
-                                  self.Cpad_d, self.KGd, 0, 1, 1, 1, kd, code, s)
+                if dx_add:
+                    L.mmseg_conv_gemm_res(ptr(dy), lddy, ptr(self.wd), None, ptr(dx), lddx, ptr(dx), lddx, M, self.Ci,
+                                          self.Cpad_d, self.KGd, code, s)
+                else:
+                    L.mmseg_conv_gemm(ptr(dy), lddy, ptr(self.wd), None, ptr(dx), lddx, ptr(ws), MODE_POINT, M,
+                                      self.Ci, self.Cpad_d, self.KGd, 0, 1, 1, 1, kd, code, s)
+
+    def dgrad_splits(self, M: int) -> int:
+        return _gemm_ksplit(M, self.Ci, self.KGd)
 
 
 class LN:
@@ -283,12 +313,14 @@ class SwinBlockProg:
         L.mmseg_gelu_fwd(ptr(hbuf), ptr(g), M * hdim, code, s)
         if seeds:                         # MLPBlock drop1 (after the activation)
             drop(g, g, M, hdim, seeds[1])
-        z = self._empty(M * C)
-        self.fc2.fwd(g, hdim, M, z, C)
-        if seeds:                         # MLPBlock drop2 (after linear2)
-            drop(z, z, M, C, seeds[2])
         out = self._empty(M * C)
-        L.mmseg_add(ptr(xm), ptr(z), ptr(out), M * C, code, s)
+        if seeds:
+            z = self._empty(M * C)
+            self.fc2.fwd(g, hdim, M, z, C)
+            drop(z, z, M, C, seeds[2])    # MLPBlock drop2 (after linear2)
+            L.mmseg_add(ptr(xm), ptr(z), ptr(out), M * C, code, s)
+        else:
+            self.fc2.fwd(g, hdim, M, out, C, res=xm)     # out = xm + linear2(.)
         st = dict(x=x, st1=st1, xw=xw, qkv=qkv, O=O, P=P, xm=xm, st2=st2, ln2=ln2, h=hbuf, g=g, B=B, Nw=Nw, Mw=Mw,
                   M=M, sh=sh, fused=fused, drop=drop, seeds=seeds)
         return out, st
@@ -478,6 +510,14 @@ class ResBlockProg:
         if not self.first:
             self.dres = Act(torch.zeros(N * D * H * W * self.cip, dtype=rt.dtype, device=rt.device), 0, self.cin,
                             self.cip, N, D, H, W) if self.has3 else None
+        # the tail's LeakyReLU backward and the norms' partial sums in one pass (mmseg_lrelu_bwd_in_part) above the
+        # one-launch small-volume norms; MMSEG_RES_FUSE=0 keeps the separate passes (bitwise the same)
+        V = D * H * W
+        nch = rt.lib.mmseg_instnorm_part_chunks(V, self.cout) if V > 4096 else 0
+        self.res_nch = nch if _res_fuse() else 0
+        if self.res_nch:
+            p = lambda: torch.empty(N * nch * self.cout * 2, dtype=torch.float32, device=rt.device)
+            self.pa, self.pb = p(), (p() if self.has3 else None)
 
     def _stats(self, a: Act, m, r):
         L = self.rt.lib
@@ -485,9 +525,15 @@ class ResBlockProg:
         L.mmseg_instnorm_stats(a.ptr, a.ld, a.N, a.V, a.C, IN_EPS, ptr(m), a.C, ptr(r), ptr(ws), self.rt.code,
                                self.rt.stream)
 
-    def _in_bwd(self, a: Act, m, r, g: Act, dx: Act):
+    def _in_bwd(self, a: Act, m, r, g: Act, dx: Act, part: Optional[torch.Tensor] = None):
+        """part: the partial sums mmseg_lrelu_bwd_in_part emitted (finalize + apply only)."""
         L = self.rt.lib
         ws = self.rt.ws(L.mmseg_instnorm_ws_floats(a.N, a.V, a.C))
+        if part is not None:
+            L.mmseg_instnorm_bwd_part(a.ptr, a.ld, ptr(m), ptr(r), g.ptr, g.ld, 1.0, None, 0, None, 0, None, 0, None,
+                                      dx.ptr, dx.ld, a.N, a.D, a.H, a.W, a.C, 0, ptr(part), self.res_nch, ptr(ws),
+                                      self.rt.code, self.rt.stream)
+            return
         L.mmseg_instnorm_bwd(a.ptr, a.ld, ptr(m), ptr(r), g.ptr, g.ld, 1.0, None, 0, None, 0, None, 0, None, dx.ptr,
                              dx.ld, a.N, a.D, a.H, a.W, a.C, 0, ptr(ws), self.rt.code, self.rt.stream)
 
@@ -512,19 +558,33 @@ class ResBlockProg:
         """dx (if not None) := the input gradient (it must not alias dy)."""
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
         rows = x.N * x.V
-        L.mmseg_lrelu_bwd(y.ptr, y.ld, dy.ptr, dy.ld, self.g.ptr, self.g.ld, rows, self.cout, SLOPE, code, s)
-        self._in_bwd(self.a2, self.m2, self.r2, self.g, self.da)
+        pa = pb = None
+        if self.res_nch:
+            a2, a3 = self.a2, self.a3
+            pa, pb = self.pa, self.pb
+            L.mmseg_lrelu_bwd_in_part(y.ptr, y.ld, dy.ptr, dy.ld, self.g.ptr, self.g.ld, SLOPE, a2.ptr, a2.ld,
+                                      ptr(self.m2), ptr(self.r2), ptr(pa), a3.ptr if a3 else None, a3.ld if a3 else 0,
+                                      ptr(self.m3), ptr(self.r3), ptr(pb), x.N, x.V, self.cout, code, s)
+        else:
+            L.mmseg_lrelu_bwd(y.ptr, y.ld, dy.ptr, dy.ld, self.g.ptr, self.g.ld, rows, self.cout, SLOPE, code, s)
+        self._in_bwd(self.a2, self.m2, self.r2, self.g, self.da, pa)
         self.c2.bwd(self.h1, self.da, self.dh, accumulate)
-        L.mmseg_lrelu_bwd(self.h1.ptr, self.h1.ld, self.dh.ptr, self.dh.ld, self.dh.ptr, self.dh.ld, rows, self.cout,
-                          SLOPE, code, s)
-        self._in_bwd(self.a1, self.m1, self.r1, self.dh, self.da)
+        # h1 = lrelu(IN(a1)): the LeakyReLU's backward inside the norm's passes (h1 > 0 exactly where a1 > mean)
+        a1 = self.a1
+        ws = self.rt.ws(L.mmseg_instnorm_ws_floats(a1.N, a1.V, a1.C))
+        L.mmseg_instnorm_lrelu_bwd(a1.ptr, a1.ld, ptr(self.m1), ptr(self.r1), self.dh.ptr, self.dh.ld, self.da.ptr,
+                                   self.da.ld, a1.N, a1.D, a1.H, a1.W, a1.C, SLOPE, ptr(ws), code, s)
         self.c1.bwd(x, self.da, dx, accumulate)
         if self.has3:
-            self._in_bwd(self.a3, self.m3, self.r3, self.g, self.da)
-            self.c3.bwd(x.ptr, x.ld, self.da.ptr, self.da.ld, rows, self.dres.ptr if dx is not None else None,
-                        self.dres.ld if dx is not None else 0, accumulate)
-            if dx is not None:
-                _add_act(self.rt, dx, self.dres)
+            self._in_bwd(self.a3, self.m3, self.r3, self.g, self.da, pb)
+            if dx is not None and self.c3.dgrad_splits(rows) == 1 and _res_fuse():
+                # dx += d(conv3 branch) from the 1x1 data-gradient GEMM's epilogue (no dres buffer, no add pass)
+                self.c3.bwd(x.ptr, x.ld, self.da.ptr, self.da.ld, rows, dx.ptr, dx.ld, accumulate, dx_add=True)
+            else:
+                self.c3.bwd(x.ptr, x.ld, self.da.ptr, self.da.ld, rows, self.dres.ptr if dx is not None else None,
+                            self.dres.ld if dx is not None else 0, accumulate)
+                if dx is not None:
+                    _add_act(self.rt, dx, self.dres)
         elif dx is not None:
             _add_act(self.rt, dx, self.g)
 

@@ -8,7 +8,8 @@ use_v2=False, normalize=True, qkv_bias=True, mlp_ratio 4, window 7, patch 2).
 MONAI is not installed and not on disk, so this file restates the
 MONAI 1.3 SwinUNETR forward from its published architecture in functional
 torch-CPU fp32.  **Parity vs MONAI itself is unpinned**: the engine is checked
-against this restatement only.
+against this restatement only.  The functions follow their inputs' device: the
+128^3 c4 backward check evaluates them in fp64 on the GPU (tests only).
 
 Parameters are a flat ``{name: tensor}`` dict keyed by the MONAI state-dict
 names below a prefix (``swinViT.layers1.0.blocks.0.attn.qkv.weight`` ...), so
@@ -68,7 +69,7 @@ def make_drop(p: float, seeds: Dict[str, object]) -> Callable[[Tensor, str], Ten
         else:
             pre, which = site.rsplit(".", 1)
             seed = seeds[pre + "."][{"proj": 0, "drop1": 1, "drop2": 2}[which]]
-        keep = torch.from_numpy(dropout_keep(int(seed), t.numel(), p)).view(t.shape)
+        keep = torch.from_numpy(dropout_keep(int(seed), t.numel(), p)).view(t.shape).to(t.device)
         return torch.where(keep, t * scale.to(t.dtype), torch.zeros((), dtype=t.dtype))
 
     return drop
@@ -181,7 +182,7 @@ def basic_layer(p: Params, pre: str, x: Tensor, depth: int, heads: int, window, 
     ws, ss = get_window_size((d, h, w), window, shift_full)
     x = x.permute(0, 2, 3, 4, 1)
     dp, hp, wp = [-(-s // ws[i]) * ws[i] for i, s in enumerate((d, h, w))]
-    mask = compute_mask((dp, hp, wp), ws, ss)
+    mask = compute_mask((dp, hp, wp), ws, ss).to(x.device)
     for i in range(depth):
         x = swin_block(p, f"{pre}blocks.{i}.", x, mask, window, (0, 0, 0) if i % 2 == 0 else shift_full, heads,
                        index, drop)
@@ -228,7 +229,7 @@ class LReluPins:
 def _lrelu(x: Tensor, pins: Optional[LReluPins] = None) -> Tensor:
     if pins is None:
         return F.leaky_relu(x, LRELU_SLOPE)
-    m = pins.take().to(torch.bool)
+    m = pins.take().to(device=x.device, dtype=torch.bool)
     return x * torch.where(m, torch.ones((), dtype=x.dtype), torch.full((), LRELU_SLOPE, dtype=x.dtype))
 
 
@@ -257,7 +258,7 @@ def swin_unetr_forward(p: Params, x: Tensor, depths=(2, 2, 2, 2), heads=(3, 6, 1
     """MONAI SwinUNETR.forward: x [b, M, S^3] -> logits [b, C, S^3].  drop: the drop_rate sites in training
     mode (make_drop), None = eval / drop_rate 0.  pins: the LeakyReLU decisions of the ten residual blocks, in
     this call order (encoder1/2/3/4/10, decoder5..1), two per block."""
-    index = relative_position_index(window)
+    index = relative_position_index(window).to(x.device)
     hs = swin_transformer(p, prefix + "swinViT.", x, depths, heads, window, index, normalize, drop)
     enc0 = unet_res_block(p, prefix + "encoder1.layer.", x, pins)
     enc1 = unet_res_block(p, prefix + "encoder2.layer.", hs[0], pins)

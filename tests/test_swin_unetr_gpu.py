@@ -195,6 +195,140 @@ def test_res_apply_and_lrelu_bwd(dev, dtype):
     assert rel(gd[:, :C], refg) < 1e-6
 
 
+def _in_stats(x, N, V, C, ld, dtype):
+    L = lib()
+    m = torch.empty(N * C, device=x.device)
+    r = torch.empty(N * C, device=x.device)
+    ws = torch.empty(L.mmseg_instnorm_ws_floats(N, V, C), device=x.device)
+    L.mmseg_instnorm_stats(ptr(x), ld, N, V, C, 1e-5, ptr(m), C, ptr(r), ptr(ws), CODE[dtype], stream_handle())
+    return m, r
+
+
+@pytest.mark.parametrize("dims", [(20, 20, 20), (8, 8, 8)])     # partial + apply passes / the one-launch small form
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_instnorm_lrelu_bwd(dev, dtype, dims):
+    """mmseg_instnorm_lrelu_bwd (UnetResBlock conv1 -> IN -> LeakyReLU(0.01), the activation's backward inside the
+    norm's passes) against torch fp64 autograd of leaky_relu(instance_norm(x)) on the same (rounded) x."""
+    N, C, ld = 2, 48, 64
+    D, H, W = dims
+    V = D * H * W
+    gen = torch.Generator().manual_seed(31)
+    x = (torch.randn(N * V, ld, generator=gen) * 2 + 0.5).to(dtype)
+    gy = torch.randn(N * V, ld, generator=gen).to(dtype)
+    xd, gd = x.to(dev), gy.to(dev)
+    m, r = _in_stats(xd, N, V, C, ld, dtype)
+    L = lib()
+    dx = torch.zeros(N * V, ld, dtype=dtype, device=dev)
+    ws = torch.empty(L.mmseg_instnorm_ws_floats(N, V, C), device=dev)
+    L.mmseg_instnorm_lrelu_bwd(ptr(xd), ld, ptr(m), ptr(r), ptr(gd), ld, ptr(dx), ld, N, D, H, W, C, 0.01, ptr(ws),
+                               CODE[dtype], stream_handle())
+    xr = x[:, :C].double().view(N, V, C).permute(0, 2, 1).reshape(N, C, D, H, W).requires_grad_(True)
+    y = F.leaky_relu(F.instance_norm(xr, eps=1e-5), 0.01)
+    y.backward(gy[:, :C].double().view(N, V, C).permute(0, 2, 1).reshape(N, C, D, H, W))
+    ref = xr.grad.reshape(N, C, V).permute(0, 2, 1)
+    got = dx[:, :C].view(N, V, C)
+    e = rel(got, ref)
+    print(f"\ninstnorm_lrelu_bwd {dtype} {dims}: {e:.2e}")
+    assert e < (1e-5 if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("C,ld,has_b", [(48, 64, True), (48, 64, False), (64, 64, True), (96, 128, False)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_lrelu_bwd_in_part_bitwise(dev, dtype, C, ld, has_b):
+    """mmseg_lrelu_bwd_in_part + mmseg_instnorm_bwd_part (the tail's LeakyReLU backward with the norms' partial sums
+    in its pass) bit for bit against mmseg_lrelu_bwd + mmseg_instnorm_bwd (separate passes): g and both input
+    gradients, over the strided (C8 = 6 / 12) and shuffle-tree (C8 = 8) reductions."""
+    N, D, H, W = 2, 24, 20, 18
+    V = D * H * W
+    gen = torch.Generator().manual_seed(32)
+    mk = lambda: (torch.randn(N * V, ld, generator=gen) * 1.5 + 0.2).to(dtype).to(dev)   # noqa: E731
+    a, b, y, dy = mk(), mk(), mk(), mk()
+    L, s, code = lib(), stream_handle(), CODE[dtype]
+    ma, ra = _in_stats(a, N, V, C, ld, dtype)
+    mb, rb = _in_stats(b, N, V, C, ld, dtype)
+    ws = torch.empty(L.mmseg_instnorm_ws_floats(N, V, C), device=dev)
+    g0 = torch.zeros(N * V, ld, dtype=dtype, device=dev)
+    L.mmseg_lrelu_bwd(ptr(y), ld, ptr(dy), ld, ptr(g0), ld, N * V, C, 0.01, code, s)
+    ref = []
+    for x, m, r in [(a, ma, ra)] + ([(b, mb, rb)] if has_b else []):
+        d = torch.zeros(N * V, ld, dtype=dtype, device=dev)
+        L.mmseg_instnorm_bwd(ptr(x), ld, ptr(m), ptr(r), ptr(g0), ld, 1.0, None, 0, None, 0, None, 0, None, ptr(d), ld,
+                             N, D, H, W, C, 0, ptr(ws), code, s)
+        ref.append(d)
+    nch = L.mmseg_instnorm_part_chunks(V, C)
+    assert nch > 0
+    pa = torch.empty(N * nch * C * 2, device=dev)
+    pb = torch.empty(N * nch * C * 2, device=dev)
+    g1 = torch.zeros(N * V, ld, dtype=dtype, device=dev)
+    assert L.mmseg_lrelu_bwd_in_part(ptr(y), ld, ptr(dy), ld, ptr(g1), ld, 0.01, ptr(a), ld, ptr(ma), ptr(ra), ptr(pa),
+                                     ptr(b) if has_b else None, ld, ptr(mb), ptr(rb), ptr(pb), N, V, C, code, s) == 0
+    assert torch.equal(g1, g0)
+    for (x, m, r), part, want in zip([(a, ma, ra), (b, mb, rb)], [pa, pb], ref):
+        d = torch.zeros(N * V, ld, dtype=dtype, device=dev)
+        L.mmseg_instnorm_bwd_part(ptr(x), ld, ptr(m), ptr(r), ptr(g1), ld, 1.0, None, 0, None, 0, None, 0, None, ptr(d),
+                                  ld, N, D, H, W, C, 0, ptr(part), nch, ptr(ws), code, s)
+        assert torch.equal(d, want)
+
+
+@pytest.mark.parametrize("Co,Ci,M", [(48, 192, 3000), (96, 64, 5000), (384, 1536, 700)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_point_gemm_residual_epilogue_bitwise(dev, dtype, Co, Ci, M, monkeypatch):
+    """mmseg_conv_gemm_res (the token linear / 1x1 data gradient with the residual added in its epilogue, out may
+    alias the residual) bit for bit against the GEMM into a temporary followed by mmseg_add."""
+    from mmseg_amd.engine.runtime import FlatParams, Runtime
+    from mmseg_amd.engine.swin import Lin
+    torch.manual_seed(4)
+    rt = Runtime(dev, dtype)
+    lin = torch.nn.Linear(Ci, Co).to(dev)
+    flat = FlatParams(list(lin.parameters()))
+    L = Lin(rt, lin.weight, lin.bias, flat)
+    for d in L.descs():
+        lib().mmseg_pack_weight(*d, rt.code, rt.stream)
+    x = torch.randn(M * Ci, device=dev).to(dtype)
+    res = torch.randn(M * Co, device=dev).to(dtype)
+    ys = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("MMSEG_RES_FUSE", fuse)
+        y = torch.full((M * Co,), float("nan"), device=dev, dtype=dtype)
+        L.fwd(x, Ci, M, y, Co, res=res)
+        ys.append(y)
+    assert torch.equal(ys[0], ys[1])
+    assert rel(ys[0].view(M, Co), (x.view(M, Ci).double() @ lin.weight.double().t() + lin.bias.double()
+                                   + res.view(M, Co).double())) < (1e-5 if dtype == torch.float32 else 1e-2)
+    inplace = res.clone()                       # y aliasing the residual (the MLP's in-place form)
+    monkeypatch.setenv("MMSEG_RES_FUSE", "1")
+    L.fwd(x, Ci, M, inplace, Co, res=inplace)
+    assert torch.equal(inplace, ys[0])
+    # data gradient: dx += dy W (dx_add) vs dgrad into a temporary + mmseg_add
+    dy = torch.randn(M * Co, device=dev).to(dtype)
+    dx0 = torch.randn(M * Ci, device=dev).to(dtype)
+    dx1 = dx0.clone()
+    tmp = torch.empty_like(dx0)
+    if L.dgrad_splits(M) == 1:
+        L.bwd(x, Ci, dy, Co, M, dx1, Ci, False, dx_add=True)
+        L.bwd(x, Ci, dy, Co, M, tmp, Ci, False)
+        lib().mmseg_add(ptr(dx0), ptr(tmp), ptr(dx0), M * Ci, rt.code, rt.stream)
+        assert torch.equal(dx1, dx0)
+    else:
+        with pytest.raises(ValueError):
+            L.bwd(x, Ci, dy, Co, M, dx1, Ci, False, dx_add=True)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_swin_res_fuse_bitwise(dev, swin_case, dtype, monkeypatch):
+    """The network with the fused tail backward (default) and with MMSEG_RES_FUSE=0: bitwise equal gradients."""
+    x, cot = swin_case
+    grads = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("MMSEG_RES_FUSE", fuse)
+        m = _model(dev, dtype)
+        out = m(x.to(dev))
+        (out * cot.to(dev)).sum().backward()
+        grads.append([p.grad.clone() for p in m.model.parameters()])
+        del m, out
+    assert all(torch.equal(a, b) for a, b in zip(*grads))
+
+
 # --------------------------------------------------------------------- whole network
 def _model(dev, dtype, fs=24, cin=2, cout=3, size=64, drop_rate=0.0):
     torch.manual_seed(1)
@@ -553,6 +687,45 @@ def test_swin_unetr_c4_size(dev):
     losses = [tr.train_step(batch, i) for i in range(3)]
     print("c4 bf16 losses", losses)
     assert all(np.isfinite(losses)) and losses[-1] < losses[0]
+
+
+def test_swin_unetr_c4_size_backward_pinned(dev):
+    """c4's network at its own size (feature_size 48, CT+PET 128^3, batch 1, 6 classes): the fp32 engine's logits and
+    EVERY parameter gradient against oracle/swin_oracle.py in fp64, evaluated on the GPU (the oracle is plain torch and
+    follows its inputs' device; on the host the 128^3 fp64 backward takes minutes), given the engine's LeakyReLU
+    decisions (_swin_pins) as in the 64^3 test above.  Bounds as at 64^3: every gradient within 1e-4 normwise
+    (max|a-b|/max|b|), 1e-5 L2 over all of them."""
+    m = _model(dev, torch.float32, fs=48, cout=6, size=128)
+    g = torch.Generator().manual_seed(49)
+    x = torch.randn(1, 2, 128, 128, 128, generator=g)
+    cot = torch.randn(1, 6, 128, 128, 128, generator=g)
+    out = m(x.to(dev))
+    pins = _swin_pins(m)
+    (out * cot.to(dev)).sum().backward()
+    out = out.detach()
+    p = {k: v.detach().double().requires_grad_(True) for k, v in m.model.named_parameters()}
+    ref = SO.swin_unetr_forward(p, x.to(dev, torch.float64), m.depths, m.num_heads, pins=pins)
+    (ref * cot.to(dev, torch.float64)).sum().backward()
+    assert pins.i == len(pins.masks)
+    e_out = rel(out, ref)
+    del ref
+    errs, got, want = {}, [], []
+    for name, prm in m.model.named_parameters():
+        r = p[name].grad
+        got.append(prm.grad.reshape(-1).double())
+        want.append(r.reshape(-1))
+        if r.abs().max() == 0:
+            assert prm.grad.abs().max().item() < 1e-6, name
+            continue
+        errs[name] = rel(prm.grad, r)
+    got, want = torch.cat(got), torch.cat(want)
+    l2 = ((got - want).norm() / want.norm()).item()
+    worst = sorted(((v, n) for n, v in errs.items()), reverse=True)[:4]
+    print(f"\nc4 128^3 fp32 pinned: logits {e_out:.2e}, {len(errs)} gradients, worst "
+          f"{[(float(f'{v:.2e}'), n) for v, n in worst]}, L2 {l2:.2e}")
+    assert e_out < 1e-4
+    assert worst[0][0] < 1e-4, worst
+    assert l2 < 1e-5
 
 
 @pytest.mark.parametrize("N,hd,heads,masked", [(343, 16, 3, True), (343, 8, 2, False), (8, 16, 1, False),
