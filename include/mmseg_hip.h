@@ -280,22 +280,25 @@ int mmseg_instnorm_relu_bwd(const void* x, int ldx, const float* mean, const flo
                             float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
                             const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N,
                             int D, int H, int W, int C, float* ws, int dtype, void* stream);
-/* Backward of InstanceNorm3d (no affine) + LeakyReLU(slope): g is the gradient of the activation's output, dx that
- * of the norm's input x (MONAI UnetResBlock conv1 -> norm1 -> lrelu, reference swin_unetr.py:80-96); the
- * activation's backward runs inside the norm's passes.  ws: mmseg_instnorm_ws_floats. */
-int mmseg_instnorm_lrelu_bwd(const void* x, int ldx, const float* mean, const float* rstd, const void* g, int ldg,
-                             void* dx, int lddx, int N, int D, int H, int W, int C, float slope, float* ws, int dtype,
-                             void* stream);
+/* Backward of InstanceNorm3d (no affine) with the activation after it folded in: act 0 none, 1 ReLU, 2
+ * LeakyReLU(slope); g is the gradient of the activation's OUTPUT, dx that of the norm's input x (MONAI UnetResBlock
+ * norms, reference swin_unetr.py:80-96).  part / nchunk: partial sums a producer of g emitted
+ * (mmseg_lrelu_bwd_in_part; finalize + apply only) or NULL / 0.  Cw (C <= Cw <= min(2 C, lddx), multiple of 8, or 0
+ * = C): dx's channels [C, Cw) are written as zeros (whole-row writes).  ws: mmseg_instnorm_ws_floats. */
+int mmseg_instnorm_act_bwd(const void* x, int ldx, const float* mean, const float* rstd, const void* g, int ldg,
+                           void* dx, int lddx, int N, int D, int H, int W, int C, int Cw, int act, float slope,
+                           const float* part, int nchunk, float* ws, int dtype, void* stream);
 /* Chunks per sample of the InstanceNorm-backward partial sums over V voxels x C channels (0: unsupported shape). */
 int mmseg_instnorm_part_chunks(long long V, int C);
 /* UnetResBlock tail backward, first pass (y = LeakyReLU(IN(xa) + IN(xb)) or LeakyReLU(IN(xa) + residual)):
  * g = dy * (y > 0 ? 1 : slope), stored, and in the same pass the InstanceNorm-backward partial sums of xa (and of xb
  * if non-NULL) over g: pa / pb [N][mmseg_instnorm_part_chunks(V, C)][C][2], the layout mmseg_instnorm_bwd_part
- * finalises and applies.  Bitwise what mmseg_lrelu_bwd + the norms' own partial passes give. */
+ * finalises and applies.  Bitwise what mmseg_lrelu_bwd + the norms' own partial passes give.  Cw: g's channels
+ * [C, Cw) written as zeros (as mmseg_lrelu_bwd). */
 int mmseg_lrelu_bwd_in_part(const void* y, int ldy, const void* dy, int lddy, void* g, int ldg, float slope,
                             const void* xa, int lda, const float* ma, const float* ra, float* pa, const void* xb,
-                            int ldb, const float* mb, const float* rb, float* pb, int N, long long V, int C, int dtype,
-                            void* stream);
+                            int ldb, const float* mb, const float* rb, float* pb, int N, long long V, int C, int Cw,
+                            int dtype, void* stream);
 /* Statistics + normalisation (+ ReLU if relu) in one call: y = [relu]((x - mean) * rstd), mean / rstd written as
  * by mmseg_instnorm_stats (mean_ld == C).  Volumes of <= 4096 voxels per sample take one fused launch (one block
  * per 8-channel group and sample, the 12^3 / 6^3 levels); larger ones the stats + apply passes. */
@@ -448,11 +451,13 @@ int mmseg_merge_scatter(const void* dout, int B, int D, int H, int W, int C, voi
  * column ci*8 + kz*4 + ky*2 + kx (the weight's own flattening), columns >= 8*Cin zero. */
 int mmseg_patchify(const float* x, int B, int Cin, int D, int H, int W, int Kp, void* out, int dtype, void* stream);
 /* UnetResBlock tail: y = lrelu((a - ma) * ra + R), R = (b - mb) * rb (b normalised), b (identity
- * residual, mb = rb = NULL) or 0 (b = NULL); stats [N][C].  lrelu_bwd: g = dy * (y > 0 ? 1 : slope). */
+ * residual, mb = rb = NULL) or 0 (b = NULL); stats [N][C].  lrelu_bwd: g = dy * (y > 0 ? 1 : slope).
+ * Cw (C <= Cw <= min(2 C, output pitch), multiple of 8): the output's channels [C, Cw) are written as zeros, so a
+ * row padded past C (48 channels at pitch 64) is written whole -- partial-row writes run at ~60 % of the rate. */
 int mmseg_res_apply(const void* a, int lda, const float* ma, const float* ra, const void* b, int ldb, const float* mb,
-                    const float* rb, void* y, int ldy, int N, long long V, int C, float slope, int dtype,
+                    const float* rb, void* y, int ldy, int N, long long V, int C, int Cw, float slope, int dtype,
                     void* stream);
-int mmseg_lrelu_bwd(const void* y, int ldy, const void* dy, int lddy, void* g, int ldg, long long rows, int C,
+int mmseg_lrelu_bwd(const void* y, int ldy, const void* dy, int lddy, void* g, int ldg, long long rows, int C, int Cw,
                     float slope, int dtype, void* stream);
 
 /* ------------------------------------------------------- device data path */

@@ -5053,7 +5053,12 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     // 32-bit offset halo staging (brick2 B32; bf16 only, see the BN64 branch)
     const bool b32 = (sizeof(T) == 2 || knob("MMSEG_B32_F32", 0)) && knob("MMSEG_BRICK2_B32", 1) &&
                      (long long)g.M * g.lda * (long long)sizeof(T) < (1LL << 31);
-    if (g.Ncols % 32 != 0) {    // a multiple of 48 (plan_conv3)
+    // 48-column tiles also for multiples of 96 that are not of 64 (SwinUNETR's 96-column convs: two 48-column tiles
+    // read the A halo twice, three 32-column brick3 tiles three times -- 128^3 96-column dgrad 0.74 ms at 706 TF/s
+    // on brick3, r05c timer)
+    const bool bn48 = g.Ncols % 32 != 0 ||
+                      (g.Ncols % 96 == 0 && g.Ncols % 64 != 0 && g.stats == nullptr && knob("MMSEG_BRICK2_BN48X", 1));
+    if (bn48) {    // a multiple of 48 (plan_conv3)
       mmseg::note_kernel("conv3_brick2_kernel<BN48,ZW1>");
       if (b32) {
         MMSEG_LAUNCH((conv3_brick2_kernel<T, 48, 1, false, true>), dim3(nb1 * (g.Ncols / 48)), block, 0, s, g);

@@ -379,6 +379,15 @@ __device__ __forceinline__ float act_grad(float h, float dy, float slope) {
   else return h > 0.f ? dy : dy * slope;
 }
 
+// 8 zeros into a row's channel padding (whole-row writes; see mmseg_instnorm_act_bwd)
+template <typename T>
+__device__ __forceinline__ void store_zero8(T* p) {
+  V8<T> z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z.set(j, 0.f);
+  z.store(p);
+}
+
 // Per-thread view of a DySrc for one sample and one 8-channel group: the
 // scale, beta and base pointers are resolved once, the per-voxel work is the
 // loads and the pool-window test.
@@ -577,7 +586,7 @@ __global__ void in_bwd_finalize(const float* __restrict__ part, int N, int C, in
 template <typename T, int ACT = 1>
 __global__ void in_bwd_apply(const T* __restrict__ x, int ldx, const float* __restrict__ mean,
                              const float* __restrict__ rstd, DySrc s, const float* __restrict__ coef, T* __restrict__ dx,
-                             int lddx, int V, int C, int D, int H, int W, int vpc) {
+                             int lddx, int V, int C, int D, int H, int W, int vpc, int npad) {
   const int n = blockIdx.y;
   const int C8 = C >> 3, lanes_v = 256 / C8;
   const int cg = threadIdx.x % C8, vl = threadIdx.x / C8;
@@ -622,6 +631,7 @@ __global__ void in_bwd_apply(const T* __restrict__ x, int ldx, const float* __re
         o.set(j, rs[j] * (g - ca[j] - h * cb[j]));
       }
       o.store(dxn + (long long)(vb + u * lanes_v) * lddx);
+      if (cg < npad) store_zero8(dxn + (long long)(vb + u * lanes_v) * lddx + C);   // (dxn is at channel 8 cg)
     }
   }
 }
@@ -638,7 +648,8 @@ __global__ __launch_bounds__(256) void lrelu_bwd_in_partial(const T* __restrict_
                                                             const float* __restrict__ ma, const float* __restrict__ ra,
                                                             float* __restrict__ pa, const T* __restrict__ xb, int ldb,
                                                             const float* __restrict__ mb, const float* __restrict__ rb,
-                                                            float* __restrict__ pb, int V, int C, int vpc) {
+                                                            float* __restrict__ pb, int V, int C, int vpc,
+                                                            int npad) {
   constexpr int K = 1 + NX;    // sum g, sum g xhat_a (, sum g xhat_b)
   const int n = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
   const int C8 = C >> 3, lanes_v = 256 / C8;
@@ -677,6 +688,7 @@ __global__ __launch_bounds__(256) void lrelu_bwd_in_partial(const T* __restrict_
 #pragma unroll
         for (int j = 0; j < 8; ++j) gv.set(j, vy[u].get(j) > 0.f ? vd[u].get(j) : vd[u].get(j) * slope);
         gv.store(g + t * ldg + cg * 8);
+        if (cg < npad) store_zero8(g + t * ldg + C + cg * 8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float gg = gv.get(j);
@@ -1697,7 +1709,7 @@ int instnorm_bwd_impl(const void* x, int ldx, const float* mean, const float* rs
                       float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
                       const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N, int D,
                       int H, int W, int C, int relu, const float* part_in, int nchunk_in, float* ws, int dtype,
-                      void* stream, int p1_nmod, float slope = 0.f);
+                      void* stream, int p1_nmod, float slope = 0.f, int Cw = 0);
 
 // The InstanceNorm + ReLU backward of G modality encoders' level outputs at once (N = G x n samples of one
 // combined pre-norm tensor / statistics / pooled gradient): every sample reads the fused level's gradient p1 of
@@ -1713,15 +1725,17 @@ int mmseg_instnorm_relu_bwd_group(const void* x, int ldx, const float* mean, con
                            dx, lddx, N, D, H, W, C, 1, nullptr, 0, ws, dtype, stream, p1_nmod);
 }
 
-// The InstanceNorm + LeakyReLU backward (SwinUNETR's UnetResBlock conv1 -> IN -> LeakyReLU, MONAI
-// get_norm_layer("instance") + get_act_layer(("leakyrelu", {"negative_slope": 0.01}))): g is the gradient of the
-// activation's OUTPUT; the activation's backward (g, or slope * g where the normalised value is <= 0) is applied
-// in the norm's passes instead of a separate pass over g.
-int mmseg_instnorm_lrelu_bwd(const void* x, int ldx, const float* mean, const float* rstd, const void* g, int ldg,
-                             void* dx, int lddx, int N, int D, int H, int W, int C, float slope, float* ws, int dtype,
-                             void* stream) {
+// The InstanceNorm backward (no affine) with the activation after the norm folded in (act 0 none, 1 ReLU, 2
+// LeakyReLU(slope); g: the gradient of the activation's OUTPUT), dy = g: SwinUNETR's UnetResBlock norms (MONAI
+// get_norm_layer("instance") + LeakyReLU(0.01) for conv1's, none for conv2 / conv3's, whose LeakyReLU follows the
+// residual sum -- mmseg_lrelu_bwd_in_part).  part / nchunk: partial sums a producer of g emitted (finalize + apply
+// only), or null.  Cw: dx's channels [C, Cw) are written as zeros (whole-row writes at pitch lddx > C) on the
+// partial / apply path (V > the small-volume bound).
+int mmseg_instnorm_act_bwd(const void* x, int ldx, const float* mean, const float* rstd, const void* g, int ldg,
+                           void* dx, int lddx, int N, int D, int H, int W, int C, int Cw, int act, float slope,
+                           const float* part, int nchunk, float* ws, int dtype, void* stream) {
   return instnorm_bwd_impl(x, ldx, mean, rstd, g, ldg, 1.f, nullptr, 0, nullptr, 0, nullptr, 0, nullptr, dx, lddx, N,
-                           D, H, W, C, 2, nullptr, 0, ws, dtype, stream, 0, slope);
+                           D, H, W, C, act, part, nchunk, ws, dtype, stream, 0, slope, Cw);
 }
 
 int mmseg_instnorm_part_chunks(long long V, int C) {
@@ -1731,9 +1745,11 @@ int mmseg_instnorm_part_chunks(long long V, int C) {
 
 int mmseg_lrelu_bwd_in_part(const void* y, int ldy, const void* dy, int lddy, void* g, int ldg, float slope,
                             const void* xa, int lda, const float* ma, const float* ra, float* pa, const void* xb,
-                            int ldb, const float* mb, const float* rb, float* pb, int N, long long V, int C, int dtype,
-                            void* stream) {
+                            int ldb, const float* mb, const float* rb, float* pb, int N, long long V, int C, int Cw,
+                            int dtype, void* stream) {
   MMSEG_REQUIRE(C % 8 == 0 && C <= 2048 && V > 0, "lrelu_bwd_in_part: C=%d must be a multiple of 8", C);
+  MMSEG_REQUIRE(Cw % 8 == 0 && Cw >= C && Cw <= 2 * C && Cw <= ldg, "lrelu_bwd_in_part: C <= Cw <= min(2 C, ldg)");
+  const int npad = (Cw - C) / 8;
   MMSEG_REQUIRE(y && dy && g && xa && ma && ra && pa, "lrelu_bwd_in_part: null operand");
   MMSEG_REQUIRE(!xb || (mb && rb && pb), "lrelu_bwd_in_part: xb needs its statistics and partial buffer");
   const int ldmax = std::max(std::max(ldy, lddy), std::max(std::max(ldg, lda), xb ? ldb : 0));
@@ -1748,11 +1764,12 @@ int mmseg_lrelu_bwd_in_part(const void* y, int ldy, const void* dy, int lddy, vo
     using T = decltype(tag);
     if (xb)
       MMSEG_LAUNCH((lrelu_bwd_in_partial<T, 2>), grid, dim3(256), 0, s, (const T*)y, ldy, (const T*)dy, lddy, (T*)g,
-                   ldg, slope, (const T*)xa, lda, ma, ra, pa, (const T*)xb, ldb, mb, rb, pb, (int)V, C, (int)vpc);
+                   ldg, slope, (const T*)xa, lda, ma, ra, pa, (const T*)xb, ldb, mb, rb, pb, (int)V, C, (int)vpc,
+                   npad);
     else
       MMSEG_LAUNCH((lrelu_bwd_in_partial<T, 1>), grid, dim3(256), 0, s, (const T*)y, ldy, (const T*)dy, lddy, (T*)g,
                    ldg, slope, (const T*)xa, lda, ma, ra, pa, (const T*)nullptr, 0, nullptr, nullptr, nullptr, (int)V,
-                   C, (int)vpc);
+                   C, (int)vpc, npad);
   };
   if (dtype == MMSEG_BF16) run(bf16_t{});
   else run(float{});
@@ -1782,8 +1799,12 @@ int instnorm_bwd_impl(const void* x, int ldx, const float* mean, const float* rs
                       float scale1, const float* alpha1, int alpha_stride, const float* beta, int beta_stride,
                       const void* pool_dy, int pool_ld, const uint8_t* pool_idx, void* dx, int lddx, int N, int D,
                       int H, int W, int C, int relu, const float* part_in, int nchunk_in, float* ws, int dtype,
-                      void* stream, int p1_nmod, float slope) {
+                      void* stream, int p1_nmod, float slope, int Cw) {
   MMSEG_REQUIRE(relu >= 0 && relu <= 2, "instnorm_bwd: activation %d (0 none, 1 ReLU, 2 LeakyReLU)", relu);
+  if (Cw == 0) Cw = C;
+  MMSEG_REQUIRE(Cw % 8 == 0 && Cw >= C && Cw <= 2 * C && Cw <= lddx,
+                "instnorm_bwd: write extent Cw=%d outside [C, min(2 C, lddx)] or not a multiple of 8", Cw);
+  const int npad = (Cw - C) / 8;
   MMSEG_REQUIRE(C % 8 == 0 && C <= 2048, "instnorm_bwd: C=%d must be a multiple of 8 and <= 2048", C);
   MMSEG_REQUIRE(!part_in || nchunk_in > 0, "instnorm_bwd: given partials need their chunk count");
   MMSEG_REQUIRE(!pool_dy || ((D | H | W) & 1) == 0, "instnorm_bwd: pooled gather needs even dims");
@@ -1807,7 +1828,7 @@ int instnorm_bwd_impl(const void* x, int ldx, const float* mean, const float* rs
     if (part_in) {
       MMSEG_LAUNCH(in_bwd_finalize, dim3(N * C), dim3(256), 0, s, part_in, N, C, nchunk_in, V, coef);
       MMSEG_LAUNCH((in_bwd_apply<T, R>), agrid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, coef,
-                         (T*)dx, lddx, (int)V, C, D, H, W, avpc);
+                         (T*)dx, lddx, (int)V, C, D, H, W, avpc, npad);
       return;
     }
     if (small) {
@@ -1829,7 +1850,7 @@ int instnorm_bwd_impl(const void* x, int ldx, const float* mean, const float* rs
                        H, W, (int)vpc, part);
     MMSEG_LAUNCH(in_bwd_finalize, dim3(N * C), dim3(256), 0, s, part, N, C, nch, V, coef);
     MMSEG_LAUNCH((in_bwd_apply<T, R>), agrid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, coef, (T*)dx,
-                       lddx, (int)V, C, D, H, W, avpc);
+                       lddx, (int)V, C, D, H, W, avpc, npad);
   };
   auto act = [&](auto tag) {
     if (relu == 2) run(tag, std::integral_constant<int, 2>{});

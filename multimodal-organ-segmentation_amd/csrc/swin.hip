@@ -651,58 +651,108 @@ __global__ void patchify_kernel(const float* __restrict__ x, int B, int Cin, int
 }
 
 // ------------------------------------------------------ UnetResBlock tail
-// y = lrelu((a - ma) * ra + R), R = (b - mb) * rb | b | 0; stats [n][C]
+constexpr int RU = 4;   // rows in flight per thread
+// Whole-row writes: a pass over C real channels of rows with pitch ld > C (SwinUNETR's 48 / 96 channels stored as 64
+// / 128) also writes zeros into the row's padding [C, Cw) (npad = (Cw - C) / 8 <= C / 8 groups, one per thread of the
+// row's first groups), so every 128-B line is written whole: a pass writing 96 B of each 128-B row ran at ~60 % of
+// the whole-row rate (tools/diag_rows.py, r05k: res_apply 235 us at 48 / 64 vs 178 us at 64 / 64 real channels).
+// The padding holds zeros anyway (zero-filled buffers whose pad columns nothing else writes).
 template <typename T>
-__global__ void res_apply_kernel(const T* __restrict__ a, int lda, const float* __restrict__ ma,
-                                 const float* __restrict__ ra, const T* __restrict__ b, int ldb,
-                                 const float* __restrict__ mb, const float* __restrict__ rb, T* __restrict__ y, int ldy,
-                                 long long V, int C, float slope, long long total8) {
-  const int c8n = C / 8;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total8;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int c8 = (int)(e % c8n);
-    const long long t = e / c8n;
-    const int n = (int)(t / V);
-    V8<T> va;
-    va.load(a + t * lda + c8 * 8);
-    float o[8];
+__device__ __forceinline__ void store_zero8(T* p) {
+  V8<T> z;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = c8 * 8 + j;
-      o[j] = (va.get(j) - ma[n * C + c]) * ra[n * C + c];
-    }
-    if (b) {
-      V8<T> vb;
-      vb.load(b + t * ldb + c8 * 8);
+  for (int j = 0; j < 8; ++j) z.set(j, 0.f);
+  z.store(p);
+}
+// Row-group layout: thread = (row lane tr, 8-channel group c8), rpb = 256 / (C / 8) rows per block pass, so the
+// (row, channel) split is one 32-bit division per thread instead of two 64-bit divisions per 16-B access (which
+// held these passes to ~2.7 TB/s at 128^3, r05c timer).
+// y = lrelu((a - ma) * ra + R), R = (b - mb) * rb | b | 0; stats [n][C]; grid (row blocks, N)
+template <typename T>
+__global__ __launch_bounds__(256) void res_apply_kernel(const T* __restrict__ a, int lda, const float* __restrict__ ma,
+                                                        const float* __restrict__ ra, const T* __restrict__ b, int ldb,
+                                                        const float* __restrict__ mb, const float* __restrict__ rb,
+                                                        T* __restrict__ y, int ldy, int V, int C, float slope,
+                                                        int npad) {
+  const int c8n = C >> 3, rpb = 256 / c8n;
+  const int tr = threadIdx.x / c8n, c8 = threadIdx.x - tr * c8n;
+  if (tr >= rpb) return;
+  const int n = blockIdx.y, c0 = n * C + c8 * 8;
+  float mua[8], rsa[8], mub[8], rsb[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = c8 * 8 + j;
-        o[j] += mb ? (vb.get(j) - mb[n * C + c]) * rb[n * C + c] : vb.get(j);
+  for (int j = 0; j < 8; ++j) {
+    mua[j] = ma[c0 + j];
+    rsa[j] = ra[c0 + j];
+    mub[j] = mb ? mb[c0 + j] : 0.f;
+    rsb[j] = mb ? rb[c0 + j] : 0.f;
+  }
+  const long long base = (long long)n * V;
+  const int step = gridDim.x * rpb;
+  // RU rows in flight per thread: all their loads issue before the first is used
+  for (int v0 = blockIdx.x * rpb + tr; v0 < V; v0 += RU * step) {
+    V8<T> va[RU], vb[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u)
+      if (v0 + u * step < V) {
+        const long long t = base + v0 + u * step;
+        va[u].load(a + t * lda + c8 * 8);
+        if (b) vb[u].load(b + t * ldb + c8 * 8);
       }
-    }
-    V8<T> vy;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) vy.set(j, o[j] > 0.f ? o[j] : o[j] * slope);
-    vy.store(y + t * ldy + c8 * 8);
+    for (int u = 0; u < RU; ++u) {
+      if (v0 + u * step >= V) break;
+      const long long t = base + v0 + u * step;
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (va[u].get(j) - mua[j]) * rsa[j];
+      if (b) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += mb ? (vb[u].get(j) - mub[j]) * rsb[j] : vb[u].get(j);
+      }
+      V8<T> vy;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vy.set(j, o[j] > 0.f ? o[j] : o[j] * slope);
+      vy.store(y + t * ldy + c8 * 8);
+      if (c8 < npad) store_zero8(y + t * ldy + C + c8 * 8);
+    }
   }
 }
 
-// g = dy * (y > 0 ? 1 : slope)   (g may alias dy)
+// g = dy * (y > 0 ? 1 : slope)   (g may alias dy); same row-group layout over rows rows
 template <typename T>
-__global__ void lrelu_bwd_kernel(const T* __restrict__ y, int ldy, const T* dy, int lddy, T* g, int ldg, int C,
-                                 float slope, long long total8) {
-  const int c8n = C / 8;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total8;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int c8 = (int)(e % c8n);
-    const long long t = e / c8n;
-    V8<T> vy, vd;
-    vy.load(y + t * ldy + c8 * 8);
-    vd.load(dy + t * lddy + c8 * 8);
+__global__ __launch_bounds__(256) void lrelu_bwd_kernel(const T* __restrict__ y, int ldy, const T* dy, int lddy, T* g,
+                                                        int ldg, int C, float slope, int rows, int npad) {
+  const int c8n = C >> 3, rpb = 256 / c8n;
+  const int tr = threadIdx.x / c8n, c8 = threadIdx.x - tr * c8n;
+  if (tr >= rpb) return;
+  const int step = gridDim.x * rpb;
+  for (int r0 = blockIdx.x * rpb + tr; r0 < rows; r0 += RU * step) {
+    V8<T> vy[RU], vd[RU];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) vd.set(j, vy.get(j) > 0.f ? vd.get(j) : vd.get(j) * slope);
-    vd.store(g + t * ldg + c8 * 8);
+    for (int u = 0; u < RU; ++u)
+      if (r0 + u * step < rows) {
+        const long long t = r0 + u * step;
+        vy[u].load(y + t * ldy + c8 * 8);
+        vd[u].load(dy + t * lddy + c8 * 8);
+      }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      if (r0 + u * step >= rows) break;
+      const long long t = r0 + u * step;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vd[u].set(j, vy[u].get(j) > 0.f ? vd[u].get(j) : vd[u].get(j) * slope);
+      vd[u].store(g + t * ldg + c8 * 8);
+      if (c8 < npad) store_zero8(g + t * ldg + C + c8 * 8);
+    }
   }
+}
+
+// row blocks of the row-group layout: enough for ~16 K blocks in all, at least RU rows per thread
+int row_blocks(long long rows, int C, int nsplit) {
+  const int rpb = 256 / (C / 8);
+  const long long need = (rows + (long long)rpb * RU - 1) / ((long long)rpb * RU);
+  const long long cap = std::max(1, 16384 / std::max(1, nsplit));
+  return (int)std::max(1LL, std::min(need, cap));
 }
 
 int grid_of(long long total) {
@@ -993,32 +1043,36 @@ int mmseg_patchify(const float* x, int B, int Cin, int D, int H, int W, int Kp, 
 }
 
 int mmseg_res_apply(const void* a, int lda, const float* ma, const float* ra, const void* b, int ldb, const float* mb,
-                    const float* rb, void* y, int ldy, int N, long long V, int C, float slope, int dtype,
+                    const float* rb, void* y, int ldy, int N, long long V, int C, int Cw, float slope, int dtype,
                     void* stream) {
-  MMSEG_REQUIRE(C % 8 == 0, "res_apply: C %% 8 == 0");
+  MMSEG_REQUIRE(C % 8 == 0 && C <= 2048, "res_apply: C %% 8 == 0 and C <= 2048");
+  MMSEG_REQUIRE(Cw % 8 == 0 && Cw >= C && Cw <= 2 * C && Cw <= ldy, "res_apply: C <= Cw <= min(2 C, ldy), Cw %% 8 == 0");
   MMSEG_REQUIRE((mb == nullptr) == (rb == nullptr), "res_apply: mb and rb together or neither");
-  const long long total8 = (long long)N * V * (C / 8);
+  MMSEG_REQUIRE(V < (1LL << 31), "res_apply: V must fit int32");
   hipStream_t s = (hipStream_t)stream;
+  const dim3 grid(row_blocks(V, C, N), N);
   if (dtype == MMSEG_BF16)
-    MMSEG_LAUNCH(res_apply_kernel<bf16_t>, dim3(grid_of(total8)), dim3(256), 0, s, (const bf16_t*)a, lda, ma,
-                       ra, (const bf16_t*)b, ldb, mb, rb, (bf16_t*)y, ldy, V, C, slope, total8);
+    MMSEG_LAUNCH(res_apply_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)a, lda, ma, ra, (const bf16_t*)b,
+                       ldb, mb, rb, (bf16_t*)y, ldy, (int)V, C, slope, (Cw - C) / 8);
   else
-    MMSEG_LAUNCH(res_apply_kernel<float>, dim3(grid_of(total8)), dim3(256), 0, s, (const float*)a, lda, ma, ra,
-                       (const float*)b, ldb, mb, rb, (float*)y, ldy, V, C, slope, total8);
+    MMSEG_LAUNCH(res_apply_kernel<float>, grid, dim3(256), 0, s, (const float*)a, lda, ma, ra, (const float*)b, ldb,
+                       mb, rb, (float*)y, ldy, (int)V, C, slope, (Cw - C) / 8);
   return mmseg::check_launch("res_apply");
 }
 
-int mmseg_lrelu_bwd(const void* y, int ldy, const void* dy, int lddy, void* g, int ldg, long long rows, int C,
+int mmseg_lrelu_bwd(const void* y, int ldy, const void* dy, int lddy, void* g, int ldg, long long rows, int C, int Cw,
                     float slope, int dtype, void* stream) {
-  MMSEG_REQUIRE(C % 8 == 0, "lrelu_bwd: C %% 8 == 0");
-  const long long total8 = rows * (C / 8);
+  MMSEG_REQUIRE(C % 8 == 0 && C <= 2048, "lrelu_bwd: C %% 8 == 0 and C <= 2048");
+  MMSEG_REQUIRE(Cw % 8 == 0 && Cw >= C && Cw <= 2 * C && Cw <= ldg, "lrelu_bwd: C <= Cw <= min(2 C, ldg), Cw %% 8 == 0");
+  MMSEG_REQUIRE(rows < (1LL << 31), "lrelu_bwd: rows must fit int32");
   hipStream_t s = (hipStream_t)stream;
+  const dim3 grid(row_blocks(rows, C, 1));
   if (dtype == MMSEG_BF16)
-    MMSEG_LAUNCH(lrelu_bwd_kernel<bf16_t>, dim3(grid_of(total8)), dim3(256), 0, s, (const bf16_t*)y, ldy,
-                       (const bf16_t*)dy, lddy, (bf16_t*)g, ldg, C, slope, total8);
+    MMSEG_LAUNCH(lrelu_bwd_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)y, ldy, (const bf16_t*)dy, lddy,
+                       (bf16_t*)g, ldg, C, slope, (int)rows, (Cw - C) / 8);
   else
-    MMSEG_LAUNCH(lrelu_bwd_kernel<float>, dim3(grid_of(total8)), dim3(256), 0, s, (const float*)y, ldy,
-                       (const float*)dy, lddy, (float*)g, ldg, C, slope, total8);
+    MMSEG_LAUNCH(lrelu_bwd_kernel<float>, grid, dim3(256), 0, s, (const float*)y, ldy, (const float*)dy, lddy,
+                       (float*)g, ldg, C, slope, (int)rows, (Cw - C) / 8);
   return mmseg::check_launch("lrelu_bwd");
 }
 

@@ -35,6 +35,20 @@ class Act:
     D: int
     H: int
     W: int
+    # the view owns its rows' padding [off + C, ld) (a buffer of its own, not a slot of a wider concat): passes that
+    # write it may write zeros there so the rows are written whole (SwinUNETR's 48 / 96-channel tensors at pitch 64 /
+    # 128; see mmseg_res_apply's Cw)
+    whole: bool = False
+
+    @property
+    def wcols(self) -> int:
+        """Channels a pass may write: C, or (a view owning its rows) C rounded up to whole 128-B lines of bf16 (64
+        channels) within the pitch -- zeros past C, at most C of them (the kernels' one zero store per real 8-channel
+        group)."""
+        if not self.whole or self.off:
+            return self.C
+        w = min(self.ld, -(-self.C // 64) * 64)
+        return w if w <= 2 * self.C else self.C
 
     @property
     def V(self) -> int:

@@ -122,14 +122,20 @@ class Lin:
             d.append((ptr(self.w), ptr(self.wd), 3, self.Co, self.Ci, self.Ci, self.KGd, self.KGdp, self.Cpad_d))
         return d
 
-    def fwd(self, x: torch.Tensor, ldx: int, M: int, y: torch.Tensor, ldy: int, res: Optional[torch.Tensor] = None):
+    def fwd(self, x: torch.Tensor, ldx: int, M: int, y: torch.Tensor, ldy: int, res: Optional[torch.Tensor] = None,
+            ncols: Optional[int] = None):
         """res (pitch ldy, may be y): y = res + x W^T (+ b), from the GEMM's epilogue when it runs without split-K
-        (mmseg_conv_gemm_res), else through a temporary and mmseg_add -- bitwise the same."""
+        (mmseg_conv_gemm_res), else through a temporary and mmseg_add -- bitwise the same.  ncols (> Co, bias-free,
+        <= the packed column tile): the GEMM also writes the zero columns [Co, ncols) of its zero-padded weights, so
+        y's padded rows are written whole (Act.wcols) and one column tile covers 48 real columns."""
         L = self.rt.lib
-        ks = _gemm_ksplit(M, self.Co, self.KG)
+        nc = self.Co if ncols is None else ncols
+        if nc != self.Co and (self.b is not None or nc > self.Cpad or nc % 8 or res is not None):
+            raise ValueError(f"token linear: {nc} output columns need a bias-free layer within its packed tile")
+        ks = _gemm_ksplit(M, nc, self.KG)
         fuse = res is not None and ks == 1 and _res_fuse()
         out = y if res is None or fuse else torch.empty(M * ldy, dtype=self.rt.dtype, device=self.rt.device)
-        ws = self.rt.ws(ks * M * self.Co) if ks > 1 else None
+        ws = self.rt.ws(ks * M * nc) if ks > 1 else None
         with TIMER.region(_gemm_name(self.rt, 0, "point"), flops=2.0 * M * self.Ci * self.Co,
                           nbytes=_io_bytes(self.rt, M, self.Cip, self.Co, self.Ci * self.Co)):
             if fuse:
@@ -137,16 +143,17 @@ class Lin:
                                       self.Cpad, self.KG, self.rt.code, self.rt.stream)
             else:
                 L.mmseg_conv_gemm(ptr(x), ldx, ptr(self.wf), ptr(self.b), ptr(out), ldy, ptr(ws), MODE_POINT, M,
-                                  self.Co, self.Cpad, self.KG, 0, 1, 1, 1, ks, self.rt.code, self.rt.stream)
+                                  nc, self.Cpad, self.KG, 0, 1, 1, 1, ks, self.rt.code, self.rt.stream)
         if res is not None and not fuse:
             if ldy != self.Co:
                 raise ValueError("token linear with a residual: dense rows only on the unfused path")
             L.mmseg_add(ptr(res), ptr(out), ptr(y), M * ldy, self.rt.code, self.rt.stream)
 
     def bwd(self, x: torch.Tensor, ldx: int, dy: torch.Tensor, lddy: int, M: int, dx: Optional[torch.Tensor],
-            lddx: int, accumulate: bool, dx_add: bool = False):
+            lddx: int, accumulate: bool, dx_add: bool = False, dx_cols: Optional[int] = None):
         """dx_add: dx += the data gradient (a residual branch's; the GEMM's epilogue adds it, mmseg_conv_gemm_res,
-        when it runs without split-K), instead of dx := it."""
+        when it runs without split-K), instead of dx := it.  dx_cols: as fwd's ncols for dx (zero columns
+        [Ci, dx_cols) from the zero-padded data-gradient image: whole-row writes)."""
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
         ks = L.mmseg_wgrad_splits(M, _wgrad_ksplit(self.Co, self.Cip, M))
         defer = self.rt.defer_wred(self.flat)
@@ -162,21 +169,24 @@ class Lin:
             self.Co, self.Cip, ks, self.Cip, self.Ci, 1, int(accumulate), s)
         self.flat.mark(*[p for p in (self.w, self.b) if p is not None])
         if dx is not None:
-            kd = _gemm_ksplit(M, self.Ci, self.KGd)
+            ncd = self.Ci if dx_cols is None else dx_cols
+            if ncd != self.Ci and (ncd > self.Cpad_d or ncd % 8):
+                raise ValueError(f"token linear: {ncd} data-gradient columns exceed the packed tile {self.Cpad_d}")
+            kd = _gemm_ksplit(M, ncd, self.KGd)
             if dx_add and (kd > 1 or not _res_fuse()):
                 raise ValueError("Lin.bwd(dx_add): the residual epilogue needs the unsplit GEMM")
-            ws = self.rt.ws(kd * M * self.Ci) if kd > 1 else None
+            ws = self.rt.ws(kd * M * ncd) if kd > 1 else None
             with TIMER.region(_gemm_name(self.rt, 0, "point"), flops=2.0 * M * self.Ci * self.Co,
                               nbytes=_io_bytes(self.rt, M, self.Co, self.Ci, self.Ci * self.Co)):
                 if dx_add:
-                    L.mmseg_conv_gemm_res(ptr(dy), lddy, ptr(self.wd), None, ptr(dx), lddx, ptr(dx), lddx, M, self.Ci,
+                    L.mmseg_conv_gemm_res(ptr(dy), lddy, ptr(self.wd), None, ptr(dx), lddx, ptr(dx), lddx, M, ncd,
                                           self.Cpad_d, self.KGd, code, s)
                 else:
                     L.mmseg_conv_gemm(ptr(dy), lddy, ptr(self.wd), None, ptr(dx), lddx, ptr(ws), MODE_POINT, M,
-                                      self.Ci, self.Cpad_d, self.KGd, 0, 1, 1, 1, kd, code, s)
+                                      ncd, self.Cpad_d, self.KGd, 0, 1, 1, 1, kd, code, s)
 
-    def dgrad_splits(self, M: int) -> int:
-        return _gemm_ksplit(M, self.Ci, self.KGd)
+    def dgrad_splits(self, M: int, ncols: Optional[int] = None) -> int:
+        return _gemm_ksplit(M, self.Ci if ncols is None else ncols, self.KGd)
 
 
 class LN:
@@ -501,7 +511,7 @@ class ResBlockProg:
     def setup(self, N, D, H, W):
         rt = self.rt
         z = lambda: Act(torch.zeros(N * D * H * W * self.cop, dtype=rt.dtype, device=rt.device), 0, self.cout,
-                        self.cop, N, D, H, W)
+                        self.cop, N, D, H, W, whole=True)
         self.a1, self.h1, self.a2, self.g, self.da, self.dh = z(), z(), z(), z(), z(), z()
         self.a3 = z() if self.has3 else None
         f = lambda: torch.empty(N * self.cout, dtype=torch.float32, device=rt.device)
@@ -527,32 +537,32 @@ class ResBlockProg:
 
     def _in_bwd(self, a: Act, m, r, g: Act, dx: Act, part: Optional[torch.Tensor] = None):
         """part: the partial sums mmseg_lrelu_bwd_in_part emitted (finalize + apply only)."""
+        self._in_act_bwd(a, m, r, g, dx, 0, part)
+
+    def _in_act_bwd(self, a: Act, m, r, g: Act, dx: Act, act: int, part: Optional[torch.Tensor] = None):
+        """The norm's backward with the activation after it (0 none, 2 LeakyReLU) folded in; dx written whole-row."""
         L = self.rt.lib
         ws = self.rt.ws(L.mmseg_instnorm_ws_floats(a.N, a.V, a.C))
-        if part is not None:
-            L.mmseg_instnorm_bwd_part(a.ptr, a.ld, ptr(m), ptr(r), g.ptr, g.ld, 1.0, None, 0, None, 0, None, 0, None,
-                                      dx.ptr, dx.ld, a.N, a.D, a.H, a.W, a.C, 0, ptr(part), self.res_nch, ptr(ws),
-                                      self.rt.code, self.rt.stream)
-            return
-        L.mmseg_instnorm_bwd(a.ptr, a.ld, ptr(m), ptr(r), g.ptr, g.ld, 1.0, None, 0, None, 0, None, 0, None, dx.ptr,
-                             dx.ld, a.N, a.D, a.H, a.W, a.C, 0, ptr(ws), self.rt.code, self.rt.stream)
+        L.mmseg_instnorm_act_bwd(a.ptr, a.ld, ptr(m), ptr(r), g.ptr, g.ld, dx.ptr, dx.ld, a.N, a.D, a.H, a.W, a.C,
+                                 dx.wcols if _res_fuse() else a.C, act, SLOPE, ptr(part),
+                                 self.res_nch if part is not None else 0, ptr(ws), self.rt.code, self.rt.stream)
 
     def fwd(self, x: Act, y: Act):
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
         self.c1.fwd(x, self.a1)
         self._stats(self.a1, self.m1, self.r1)
         L.mmseg_res_apply(self.a1.ptr, self.a1.ld, ptr(self.m1), ptr(self.r1), None, 0, None, None, self.h1.ptr,
-                          self.h1.ld, x.N, x.V, self.cout, SLOPE, code, s)
+                          self.h1.ld, x.N, x.V, self.cout, _wc(self.h1), SLOPE, code, s)
         self.c2.fwd(self.h1, self.a2)
         self._stats(self.a2, self.m2, self.r2)
         if self.has3:
-            self.c3.fwd(x.ptr, x.ld, x.N * x.V, self.a3.ptr, self.a3.ld)
+            self.c3.fwd(x.ptr, x.ld, x.N * x.V, self.a3.ptr, self.a3.ld, ncols=_wc(self.a3))
             self._stats(self.a3, self.m3, self.r3)
             L.mmseg_res_apply(self.a2.ptr, self.a2.ld, ptr(self.m2), ptr(self.r2), self.a3.ptr, self.a3.ld,
-                              ptr(self.m3), ptr(self.r3), y.ptr, y.ld, x.N, x.V, self.cout, SLOPE, code, s)
+                              ptr(self.m3), ptr(self.r3), y.ptr, y.ld, x.N, x.V, self.cout, _wc(y), SLOPE, code, s)
         else:
             L.mmseg_res_apply(self.a2.ptr, self.a2.ld, ptr(self.m2), ptr(self.r2), x.ptr, x.ld, None, None, y.ptr,
-                              y.ld, x.N, x.V, self.cout, SLOPE, code, s)
+                              y.ld, x.N, x.V, self.cout, _wc(y), SLOPE, code, s)
 
     def bwd(self, x: Act, y: Act, dy: Act, dx: Optional[Act], accumulate: bool):
         """dx (if not None) := the input gradient (it must not alias dy)."""
@@ -564,22 +574,21 @@ class ResBlockProg:
             pa, pb = self.pa, self.pb
             L.mmseg_lrelu_bwd_in_part(y.ptr, y.ld, dy.ptr, dy.ld, self.g.ptr, self.g.ld, SLOPE, a2.ptr, a2.ld,
                                       ptr(self.m2), ptr(self.r2), ptr(pa), a3.ptr if a3 else None, a3.ld if a3 else 0,
-                                      ptr(self.m3), ptr(self.r3), ptr(pb), x.N, x.V, self.cout, code, s)
+                                      ptr(self.m3), ptr(self.r3), ptr(pb), x.N, x.V, self.cout, _wc(self.g), code, s)
         else:
-            L.mmseg_lrelu_bwd(y.ptr, y.ld, dy.ptr, dy.ld, self.g.ptr, self.g.ld, rows, self.cout, SLOPE, code, s)
+            L.mmseg_lrelu_bwd(y.ptr, y.ld, dy.ptr, dy.ld, self.g.ptr, self.g.ld, rows, self.cout, _wc(self.g), SLOPE,
+                              code, s)
         self._in_bwd(self.a2, self.m2, self.r2, self.g, self.da, pa)
         self.c2.bwd(self.h1, self.da, self.dh, accumulate)
         # h1 = lrelu(IN(a1)): the LeakyReLU's backward inside the norm's passes (h1 > 0 exactly where a1 > mean)
-        a1 = self.a1
-        ws = self.rt.ws(L.mmseg_instnorm_ws_floats(a1.N, a1.V, a1.C))
-        L.mmseg_instnorm_lrelu_bwd(a1.ptr, a1.ld, ptr(self.m1), ptr(self.r1), self.dh.ptr, self.dh.ld, self.da.ptr,
-                                   self.da.ld, a1.N, a1.D, a1.H, a1.W, a1.C, SLOPE, ptr(ws), code, s)
+        self._in_act_bwd(self.a1, self.m1, self.r1, self.dh, self.da, 2)
         self.c1.bwd(x, self.da, dx, accumulate)
         if self.has3:
             self._in_bwd(self.a3, self.m3, self.r3, self.g, self.da, pb)
-            if dx is not None and self.c3.dgrad_splits(rows) == 1 and _res_fuse():
+            if dx is not None and self.c3.dgrad_splits(rows, _wc(dx)) == 1 and _res_fuse():
                 # dx += d(conv3 branch) from the 1x1 data-gradient GEMM's epilogue (no dres buffer, no add pass)
-                self.c3.bwd(x.ptr, x.ld, self.da.ptr, self.da.ld, rows, dx.ptr, dx.ld, accumulate, dx_add=True)
+                self.c3.bwd(x.ptr, x.ld, self.da.ptr, self.da.ld, rows, dx.ptr, dx.ld, accumulate, dx_add=True,
+                            dx_cols=_wc(dx))
             else:
                 self.c3.bwd(x.ptr, x.ld, self.da.ptr, self.da.ld, rows, self.dres.ptr if dx is not None else None,
                             self.dres.ld if dx is not None else 0, accumulate)
@@ -587,6 +596,12 @@ class ResBlockProg:
                     _add_act(self.rt, dx, self.dres)
         elif dx is not None:
             _add_act(self.rt, dx, self.g)
+
+
+def _wc(a: Act) -> int:
+    """Channels the pass writing a writes (Act.wcols: whole rows, zeros in the padding), or only the real ones
+    (MMSEG_RES_FUSE=0)."""
+    return a.wcols if _res_fuse() else a.C
 
 
 def _add_act(rt: Runtime, dst: Act, src: Act):
@@ -612,7 +627,8 @@ class UpBlockProg:
     def setup(self, N, D, H, W):
         rt, c, ld = self.rt, self.cout, cpad(2 * self.cout)
         self.cat = Act(torch.zeros(N * D * H * W * ld, dtype=rt.dtype, device=rt.device), 0, 2 * c, ld, N, D, H, W)
-        self.dcat = Act(torch.zeros(N * D * H * W * ld, dtype=rt.dtype, device=rt.device), 0, 2 * c, ld, N, D, H, W)
+        self.dcat = Act(torch.zeros(N * D * H * W * ld, dtype=rt.dtype, device=rt.device), 0, 2 * c, ld, N, D, H, W,
+                        whole=True)
         self.res.setup(N, D, H, W)
 
     def skip(self) -> Act:
@@ -690,7 +706,7 @@ class SwinUNETRProgram:
         for i, st in enumerate(self.stages):
             st.setup(N, *g[i])
         z = lambda dims, c: Act(torch.zeros(N * dims[0] * dims[1] * dims[2] * cpad(c), dtype=rt.dtype,
-                                            device=rt.device), 0, c, cpad(c), N, *dims)
+                                            device=rt.device), 0, c, cpad(c), N, *dims, whole=True)
         full = (D, H, W)
         self.xin = Act(torch.zeros(N * D * H * W * 8, dtype=rt.dtype, device=rt.device), 0, self.cin, 8, N, *full)
         # decoder k (5..1) runs at grid of hs[k-2] x2 = g[k-2] for k >= 2 ... decoder1 at full res

@@ -170,26 +170,30 @@ def test_patchify(dev):
     assert rel(got.view(2, 4, 3, 2, 5).permute(0, 4, 1, 2, 3), ref) < 1e-5
 
 
+@pytest.mark.parametrize("whole", [False, True])    # Cw = C, or whole rows (zeros written into [C, ld))
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_res_apply_and_lrelu_bwd(dev, dtype):
+def test_res_apply_and_lrelu_bwd(dev, dtype, whole):
     N, V, C, ld = 2, 100, 24, 32
+    cw = ld if whole else C
     g = torch.Generator().manual_seed(9)
     a, b = torch.randn(N * V, ld, generator=g).to(dtype), torch.randn(N * V, ld, generator=g).to(dtype)
     ma, ra, mb, rb = [torch.randn(N, C, generator=g) for _ in range(4)]
     L, s = lib(), stream_handle()
-    y = torch.zeros(N * V, ld, dtype=dtype, device=dev)
+    y = torch.full((N * V, ld), float("nan"), dtype=dtype, device=dev)
     ad, mad, rad, bd, mbd, rbd = [t.to(dev) for t in (a, ma, ra, b, mb, rb)]
-    L.mmseg_res_apply(ptr(ad), ld, ptr(mad), ptr(rad), ptr(bd), ld, ptr(mbd), ptr(rbd), ptr(y), ld, N, V, C, 0.01,
+    L.mmseg_res_apply(ptr(ad), ld, ptr(mad), ptr(rad), ptr(bd), ld, ptr(mbd), ptr(rbd), ptr(y), ld, N, V, C, cw, 0.01,
                       CODE[dtype], s)
+    assert (torch.all(y[:, C:] == 0) if whole else torch.all(torch.isnan(y[:, C:]))).item()
     av, bv = a[:, :C].double().view(N, V, C), b[:, :C].double().view(N, V, C)
     pre = (av - ma.double()[:, None]) * ra.double()[:, None] + (bv - mb.double()[:, None]) * rb.double()[:, None]
     ref = F.leaky_relu(pre, 0.01)
     tol = 1e-6 if dtype == torch.float32 else 1e-2
     assert rel(y[:, :C].view(N, V, C), ref) < tol
     dy = torch.randn(N * V, ld, generator=g).to(dtype)
-    gd = torch.empty(N * V, ld, dtype=dtype, device=dev)
+    gd = torch.full((N * V, ld), float("nan"), dtype=dtype, device=dev)
     dyd = dy.to(dev)
-    L.mmseg_lrelu_bwd(ptr(y), ld, ptr(dyd), ld, ptr(gd), ld, N * V, C, 0.01, CODE[dtype], s)
+    L.mmseg_lrelu_bwd(ptr(y), ld, ptr(dyd), ld, ptr(gd), ld, N * V, C, cw, 0.01, CODE[dtype], s)
+    assert (torch.all(gd[:, C:] == 0) if whole else torch.all(torch.isnan(gd[:, C:]))).item()
     yv = y[:, :C].float().cpu()
     refg = torch.where(yv > 0, dy[:, :C].float(), dy[:, :C].float() * 0.01).to(dtype)
     assert rel(gd[:, :C], refg) < 1e-6
@@ -207,8 +211,9 @@ def _in_stats(x, N, V, C, ld, dtype):
 @pytest.mark.parametrize("dims", [(20, 20, 20), (8, 8, 8)])     # partial + apply passes / the one-launch small form
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_instnorm_lrelu_bwd(dev, dtype, dims):
-    """mmseg_instnorm_lrelu_bwd (UnetResBlock conv1 -> IN -> LeakyReLU(0.01), the activation's backward inside the
-    norm's passes) against torch fp64 autograd of leaky_relu(instance_norm(x)) on the same (rounded) x."""
+    """mmseg_instnorm_act_bwd(act 2) (UnetResBlock conv1 -> IN -> LeakyReLU(0.01), the activation's backward inside
+    the norm's passes) against torch fp64 autograd of leaky_relu(instance_norm(x)) on the same (rounded) x; on the
+    partial / apply path with whole-row writes (Cw = ld: zeros in dx's padding)."""
     N, C, ld = 2, 48, 64
     D, H, W = dims
     V = D * H * W
@@ -218,10 +223,13 @@ def test_instnorm_lrelu_bwd(dev, dtype, dims):
     xd, gd = x.to(dev), gy.to(dev)
     m, r = _in_stats(xd, N, V, C, ld, dtype)
     L = lib()
-    dx = torch.zeros(N * V, ld, dtype=dtype, device=dev)
+    small = V <= 4096
+    dx = torch.full((N * V, ld), float("nan"), dtype=dtype, device=dev)
     ws = torch.empty(L.mmseg_instnorm_ws_floats(N, V, C), device=dev)
-    L.mmseg_instnorm_lrelu_bwd(ptr(xd), ld, ptr(m), ptr(r), ptr(gd), ld, ptr(dx), ld, N, D, H, W, C, 0.01, ptr(ws),
-                               CODE[dtype], stream_handle())
+    L.mmseg_instnorm_act_bwd(ptr(xd), ld, ptr(m), ptr(r), ptr(gd), ld, ptr(dx), ld, N, D, H, W, C,
+                             C if small else ld, 2, 0.01, None, 0, ptr(ws), CODE[dtype], stream_handle())
+    if not small:
+        assert torch.all(dx[:, C:] == 0).item()
     xr = x[:, :C].double().view(N, V, C).permute(0, 2, 1).reshape(N, C, D, H, W).requires_grad_(True)
     y = F.leaky_relu(F.instance_norm(xr, eps=1e-5), 0.01)
     y.backward(gy[:, :C].double().view(N, V, C).permute(0, 2, 1).reshape(N, C, D, H, W))
@@ -248,7 +256,7 @@ def test_lrelu_bwd_in_part_bitwise(dev, dtype, C, ld, has_b):
     mb, rb = _in_stats(b, N, V, C, ld, dtype)
     ws = torch.empty(L.mmseg_instnorm_ws_floats(N, V, C), device=dev)
     g0 = torch.zeros(N * V, ld, dtype=dtype, device=dev)
-    L.mmseg_lrelu_bwd(ptr(y), ld, ptr(dy), ld, ptr(g0), ld, N * V, C, 0.01, code, s)
+    L.mmseg_lrelu_bwd(ptr(y), ld, ptr(dy), ld, ptr(g0), ld, N * V, C, C, 0.01, code, s)
     ref = []
     for x, m, r in [(a, ma, ra)] + ([(b, mb, rb)] if has_b else []):
         d = torch.zeros(N * V, ld, dtype=dtype, device=dev)
@@ -261,7 +269,8 @@ def test_lrelu_bwd_in_part_bitwise(dev, dtype, C, ld, has_b):
     pb = torch.empty(N * nch * C * 2, device=dev)
     g1 = torch.zeros(N * V, ld, dtype=dtype, device=dev)
     assert L.mmseg_lrelu_bwd_in_part(ptr(y), ld, ptr(dy), ld, ptr(g1), ld, 0.01, ptr(a), ld, ptr(ma), ptr(ra), ptr(pa),
-                                     ptr(b) if has_b else None, ld, ptr(mb), ptr(rb), ptr(pb), N, V, C, code, s) == 0
+                                     ptr(b) if has_b else None, ld, ptr(mb), ptr(rb), ptr(pb), N, V, C, C, code,
+                                     s) == 0
     assert torch.equal(g1, g0)
     for (x, m, r), part, want in zip([(a, ma, ra), (b, mb, rb)], [pa, pb], ref):
         d = torch.zeros(N * V, ld, dtype=dtype, device=dev)
