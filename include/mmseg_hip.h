@@ -137,6 +137,12 @@ int mmseg_conv_gemm_stats(const void* a, int lda, const void* wpacked, const flo
 int mmseg_conv_gemm_ex(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
                        float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H,
                        int W, int ksplit, float* stats_part, int cin_real, int dtype, void* stream);
+/* mmseg_conv_gemm_ex (no statistics) with a whole-row output hint: the brick2 conv kernels also write zeros into
+ * columns [Ncols, zcols) of the output rows (zcols <= min(ldo, Ncols + 48), multiple of 8; 0 = none), so 48 / 96
+ * real columns at pitch 64 / 128 are written in whole 128-B lines; other kernels leave those columns alone. */
+int mmseg_conv_gemm_zw(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
+                       float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H,
+                       int W, int ksplit, int cin_real, int zcols, int dtype, void* stream);
 int mmseg_instnorm_stats_bricks(const float* part, int N, int C, int nb, int cnt, float eps, float* mean, int mean_ld,
                                 float* rstd, void* stream);
 
@@ -177,6 +183,13 @@ int mmseg_conv_gemm_split(const void* a, int lda, const void* wpacked, const flo
  * reference swin_unetr.py:80-96 -> MONAI) without their own pass. */
 int mmseg_conv_gemm_res(const void* a, int lda, const void* wpacked, const float* bias, const void* res, int ldres,
                         void* out, int ldo, int M, int Ncols, int Cpad, int KG, int dtype, void* stream);
+/* 1x1 GEMM (MODE_POINT, no split-K) with the MLP's GELU (exact erf) in its epilogue: epi 1, out = h = A W^T + bias
+ * and gelu_out = gelu(h) (MLPBlock linear1 + GELU); epi 2, out = (A W^T) * gelu'(gelu_in) (linear2's data gradient
+ * through the GELU, gelu_in = h) -- bitwise the GEMM followed by mmseg_gelu_fwd / mmseg_gelu_bwd; every buffer at
+ * pitch ldo (multiple of 8), 16-B aligned (reference swin_unetr.py:80-96 -> MONAI MLPBlock). */
+int mmseg_conv_gemm_gelu(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
+                         const void* gelu_in, void* gelu_out, int epi, int M, int Ncols, int Cpad, int KG, int dtype,
+                         void* stream);
 /* Deferred InstanceNorm + ReLU of a 3^3 conv's input (the block's conv1 output is never written by its
  * normalisation pass): the input holds the PRE-norm activation and the kernels stage
  * relu((x - mean[n][c]) * rstd[n][c]) rounded to bf16, the values mmseg_instnorm_relu_fwd would write.

@@ -121,6 +121,16 @@ struct GemmArgs {
   // alias out)
   const void* res;
   int ldres;
+  // whole-row output hint (brick2 kernels; others ignore it): the last column tile also writes zeros into columns
+  // [Ncols, zcols) (<= Ncols + BN) of the output rows -- SwinUNETR's 48 / 96-column outputs at pitch 64 / 128 are
+  // then written in whole 128-B lines (partial-line writes ran at ~60 % of the whole-row rate, r05k)
+  int zcols;
+  // token-GEMM epilogue (MODE_POINT, ksplit 1, vector stores; mmseg_conv_gemm_gelu): epi 1 = GELU forward, out = h
+  // (the pre-activation the backward reads) and aux_out = gelu(h); epi 2 = GELU backward, out = round(round(acc) *
+  // gelu'(aux)) with aux = h -- the values of the GEMM followed by mmseg_gelu_fwd / mmseg_gelu_bwd (pitch ldo)
+  int epi;
+  const void* aux;
+  void* aux_out;
 };
 
 // Output element (row voxel, column) of a GEMM (split-aware; split is a multiple of 8).
@@ -445,6 +455,17 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs g) {
       rv.load(reinterpret_cast<const T*>(g.res) + row * g.ldres + col);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o.set(j, o.get(j) + rv.get(j));
+    }
+    if (MODE == MODE_POINT && g.epi == 1) {
+      V8<T> gv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gv.set(j, mmseg_gelu(o.get(j)));
+      gv.store(reinterpret_cast<T*>(g.aux_out) + row * g.ldo + col);
+    } else if (MODE == MODE_POINT && g.epi == 2) {
+      V8<T> hv;
+      hv.load(reinterpret_cast<const T*>(g.aux) + row * g.ldo + col);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o.set(j, o.get(j) * mmseg_gelu_grad(hv.get(j)));
     }
     o.store(out_at<T>(g, row, col));
   }
@@ -858,16 +879,23 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kern
   T* O = reinterpret_cast<T*>(g.out);
   constexpr int CG = BN / 8;                  // 8-column groups per voxel
   constexpr int O_ITEMS = BZ * 64 * CG;
+  // zero groups past Ncols (whole-row hint), written by the last column tile's first groups
+  const int zg = (g.zcols > g.Ncols && n0 + BN >= g.Ncols) ? (g.zcols - g.Ncols) >> 3 : 0;
 #pragma unroll
   for (int k = 0; k < O_ITEMS / 256; ++k) {
     const int e = tid + k * 256;
     const int v = e / CG, cg = e % CG;
     const int col = n0 + cg * 8;
+    const int z = z0 + (v >> 6), y = y0 + ((v >> 3) & 7), x = x0 + (v & 7);
     if (col < g.Ncols) {
-      const int z = z0 + (v >> 6), y = y0 + ((v >> 3) & 7), x = x0 + (v & 7);
       V8<T> o;
       o.load(El + v * EP + cg * 8);
       o.store(out_at<T>(g, nbase + z * HW + (long long)y * g.W + x, col));
+    }
+    for (int zc = cg; zc < zg; zc += CG) {
+      V8<T> zv;
+      zv.zero();
+      zv.store(O + (nbase + z * HW + (long long)y * g.W + x) * g.ldo + g.Ncols + zc * 8);
     }
   }
   PROBE_T();
@@ -5663,7 +5691,7 @@ int conv_gemm_impl(const void* a, int lda, const void* wpacked, const float* bia
                    int ldo2, int split, float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift,
                    int D, int H, int W, int ksplit, float* stats_part, int cin_real, int dtype, void* stream,
                    int groups = 1, long long w_gstride = 0, int b_gstride = 0, const void* res = nullptr,
-                   int ldres = 0);
+                   int ldres = 0, int zcols = 0);
 int mmseg_conv3_group_stats_bricks(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda,
                                    int ldo, int dtype);
 
@@ -5701,6 +5729,41 @@ int mmseg_conv_gemm_ex(const void* a, int lda, const void* wpacked, const float*
                         cpg_shift, D, H, W, ksplit, stats_part, cin_real, dtype, stream);
 }
 
+// mmseg_conv_gemm_ex (no statistics) with the whole-row output hint: columns [Ncols, zcols) of the output rows are
+// written as zeros by the kernels that support it (the brick2 conv kernels), left alone by the others.
+int mmseg_conv_gemm_zw(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
+                       float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H,
+                       int W, int ksplit, int cin_real, int zcols, int dtype, void* stream) {
+  return conv_gemm_impl(a, lda, wpacked, bias, out, ldo, nullptr, 0, 0, splitk_ws, mode, M, Ncols, Cpad, KG,
+                        cpg_shift, D, H, W, ksplit, nullptr, cin_real, dtype, stream, 1, 0, 0, nullptr, 0, zcols);
+}
+
+// 1x1 GEMM (MODE_POINT, ksplit 1) with the MLP's GELU in its epilogue: epi 1, out = h = A W^T + bias and gelu_out
+// = gelu(h) (linear1 + GELU); epi 2, out = (A W^T) * gelu'(h) with h = gelu_in (linear2's data gradient through the
+// GELU) -- bitwise the GEMM followed by mmseg_gelu_fwd / mmseg_gelu_bwd.  out, gelu_in / gelu_out at pitch ldo.
+int mmseg_conv_gemm_gelu(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo,
+                         const void* gelu_in, void* gelu_out, int epi, int M, int Ncols, int Cpad, int KG, int dtype,
+                         void* stream) {
+  MMSEG_REQUIRE((epi == 1 && gelu_out && !gelu_in) || (epi == 2 && gelu_in && !gelu_out),
+                "conv_gemm_gelu: epi 1 (forward, gelu_out) or 2 (backward, gelu_in)");
+  MMSEG_REQUIRE(ldo % 8 == 0 && Ncols % 8 == 0 &&
+                    ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(gelu_in) |
+                      reinterpret_cast<uintptr_t>(gelu_out)) & 15) == 0,
+                "conv_gemm_gelu: ldo, Ncols multiples of 8, 16-B aligned buffers");
+  const int KGp = (KG + 3) & ~3;
+  GemmArgs g{a, lda, wpacked, bias, out, ldo, nullptr, M, Ncols, Cpad, KG, 0, 1, 1, 1, 1, KGp,
+             knob("MMSEG_SWIZZLE", 1), nullptr, 0, nullptr, nullptr};
+  MMSEG_REQUIRE(lda % 8 == 0, "conv_gemm_gelu: lda must be a multiple of 8");
+  MMSEG_REQUIRE(Cpad >= ((Ncols + (Ncols >= 64 ? 63 : 31)) / (Ncols >= 64 ? 64 : 32)) * (Ncols >= 64 ? 64 : 32),
+                "conv_gemm_gelu: packed weights must be padded to the column tile (Cpad=%d, Ncols=%d)", Cpad, Ncols);
+  g.epi = epi;
+  g.aux = gelu_in;
+  g.aux_out = gelu_out;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MMSEG_BF16) return launch_gemm<bf16_t, MODE_POINT>(g, s);
+  return launch_gemm<float, MODE_POINT>(g, s);
+}
+
 // 1x1 GEMM (MODE_POINT, ksplit 1) whose epilogue adds a residual: out = round(round(A W^T + bias) + res), bitwise
 // mmseg_conv_gemm into a temporary followed by mmseg_add(res, temporary, out); res may alias out.  The SwinUNETR
 // residual sums (UnetResBlock input gradient dx += d(conv3 branch), the MLP residual x + fc2(.)) without a pass.
@@ -5728,7 +5791,10 @@ int mmseg_conv_gemm_split(const void* a, int lda, const void* wpacked, const flo
 int conv_gemm_impl(const void* a, int lda, const void* wpacked, const float* bias, void* out, int ldo, void* out2,
                    int ldo2, int split, float* splitk_ws, int mode, int M, int Ncols, int Cpad, int KG, int cpg_shift,
                    int D, int H, int W, int ksplit, float* stats_part, int cin_real, int dtype, void* stream,
-                   int groups, long long w_gstride, int b_gstride, const void* res, int ldres) {
+                   int groups, long long w_gstride, int b_gstride, const void* res, int ldres, int zcols) {
+  MMSEG_REQUIRE(zcols == 0 || (zcols >= Ncols && zcols % 8 == 0 && zcols <= ldo && !out2 && Ncols % 8 == 0 &&
+                               zcols - Ncols <= 48),
+                "conv_gemm: whole-row extent zcols=%d must lie in [Ncols, min(ldo, Ncols + 48)]", zcols);
   MMSEG_REQUIRE(!res || (mode == MODE_POINT && ksplit == 1 && !out2 && ldo % 8 == 0 && ldres % 8 == 0 &&
                          Ncols % 8 == 0 && ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(res)) &
                                             15) == 0),
@@ -5760,6 +5826,7 @@ int conv_gemm_impl(const void* a, int lda, const void* wpacked, const float* bia
   }
   g.res = res;
   g.ldres = ldres;
+  g.zcols = zcols;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16) return launch_gemm_mode<bf16_t>(g, mode, s);
   return launch_gemm_mode<float>(g, mode, s);

@@ -138,3 +138,10 @@ __device__ __forceinline__ int xcd_swizzle(int b, int T) {
   const int xcd = b & 7, j = b >> 3, q = T >> 3, r = T & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
 }
+
+// nn.GELU() (exact erf) and its derivative, shared by the elementwise kernels (swin.hip) and the token GEMMs'
+// fused epilogues (conv_gemm.hip) so both give the same bits.
+__device__ __forceinline__ float mmseg_gelu(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float mmseg_gelu_grad(float x) {
+  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+}

@@ -410,10 +410,8 @@ __global__ __launch_bounds__(1024) void ln_param_reduce_kernel(const float* __re
 }
 
 // ------------------------------------------------------------------ GELU
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_grad(float x) {
-  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
-}
+__device__ __forceinline__ float gelu_f(float x) { return mmseg_gelu(x); }
+__device__ __forceinline__ float gelu_grad(float x) { return mmseg_gelu_grad(x); }
 
 template <typename T>
 __global__ void gelu_fwd_kernel(const T* __restrict__ h, T* __restrict__ y, long long n8) {

@@ -47,6 +47,13 @@ def _io_bytes(rt: Runtime, vox: int, cin: int, cout: int, wcount: int, wbytes: i
     return float(vox * (cin + cout) * es + wcount * wbytes)
 
 
+def _zcols(a: Act, ncols: int) -> int:
+    """Whole-row extent for a GEMM writing ncols columns of a (mmseg_conv_gemm_zw): a's Act.wcols when it reaches past
+    ncols, else 0 (no zero columns)."""
+    w = a.wcols
+    return w if w > ncols and w - ncols <= 48 else 0
+
+
 def _col_tile(n: int) -> int:
     return round_up(n, 64 if n >= 64 else 32)
 
@@ -282,9 +289,10 @@ class Conv3:
         ws = self.rt.ws(ks * M * nc) if ks > 1 else None
         with TIMER.region(_gemm_name(self.rt, nc, "conv3"), flops=2.0 * M * self.Co * 27 * self.Ci,
                           nbytes=_io_bytes(self.rt, M, self.Cip, self.Co, 27 * self.Cip * self.Co)):
-            self.rt.lib.mmseg_conv_gemm_ex(x.ptr, x.ld, ptr(self.wf), ptr(self.conv.bias), y.ptr, y.ld, ptr(ws),
+            # (an output owning its padded rows is written whole: Act.wcols, mmseg_conv_gemm_zw)
+            self.rt.lib.mmseg_conv_gemm_zw(x.ptr, x.ld, ptr(self.wf), ptr(self.conv.bias), y.ptr, y.ld, ptr(ws),
                                            MODE_CONV3, M, nc, self.Cpad, self.KG, self.cpg_shift, x.D, x.H, x.W, ks,
-                                           None, self.kreal_f, self.rt.code, self.rt.stream)
+                                           self.kreal_f, _zcols(y, nc), self.rt.code, self.rt.stream)
 
     def norm_ok(self, x: Act, y: Act) -> bool:
         """True when this conv can take its input as the PRE-norm activation of an InstanceNorm + ReLU and apply
@@ -447,9 +455,9 @@ class Conv3:
                                             d0.C, ptr(ws), MODE_CONV3, M, nc, self.Cpad_d, self.KGd, self.dshift, x.D,
                                             x.H, x.W, ks, self.kreal_d, code, s)
                 else:
-                    L.mmseg_conv_gemm_ex(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, ptr(ws), MODE_CONV3, M,
-                                         nc, self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, ks, None,
-                                         self.kreal_d, code, s)
+                    L.mmseg_conv_gemm_zw(dy.ptr, dy.ld, ptr(self.wd), None, dx.ptr, dx.ld, ptr(ws), MODE_CONV3, M,
+                                         nc, self.Cpad_d, self.KGd, self.dshift, x.D, x.H, x.W, ks, self.kreal_d,
+                                         _zcols(dx, nc), code, s)
 
 
 class ConvT2:

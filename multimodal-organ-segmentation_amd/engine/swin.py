@@ -122,6 +122,19 @@ class Lin:
             d.append((ptr(self.w), ptr(self.wd), 3, self.Co, self.Ci, self.Ci, self.KGd, self.KGdp, self.Cpad_d))
         return d
 
+    def fwd_gelu(self, x: torch.Tensor, ldx: int, M: int, h: torch.Tensor, g: torch.Tensor) -> None:
+        """h = x W^T + b and g = gelu(h) (MLPBlock linear1 + GELU; dense rows of Co): from the GEMM's epilogue
+        (mmseg_conv_gemm_gelu) when it runs without split-K, else the GEMM + mmseg_gelu_fwd -- bitwise the same."""
+        L = self.rt.lib
+        if _gemm_ksplit(M, self.Co, self.KG) == 1 and _res_fuse():
+            with TIMER.region(_gemm_name(self.rt, 0, "point"), flops=2.0 * M * self.Ci * self.Co,
+                              nbytes=_io_bytes(self.rt, M, self.Cip, 2 * self.Co, self.Ci * self.Co)):
+                L.mmseg_conv_gemm_gelu(ptr(x), ldx, ptr(self.wf), ptr(self.b), ptr(h), self.Co, None, ptr(g), 1, M,
+                                       self.Co, self.Cpad, self.KG, self.rt.code, self.rt.stream)
+            return
+        self.fwd(x, ldx, M, h, self.Co)
+        L.mmseg_gelu_fwd(ptr(h), ptr(g), M * self.Co, self.rt.code, self.rt.stream)
+
     def fwd(self, x: torch.Tensor, ldx: int, M: int, y: torch.Tensor, ldy: int, res: Optional[torch.Tensor] = None,
             ncols: Optional[int] = None):
         """res (pitch ldy, may be y): y = res + x W^T (+ b), from the GEMM's epilogue when it runs without split-K
@@ -150,10 +163,13 @@ class Lin:
             L.mmseg_add(ptr(res), ptr(out), ptr(y), M * ldy, self.rt.code, self.rt.stream)
 
     def bwd(self, x: torch.Tensor, ldx: int, dy: torch.Tensor, lddy: int, M: int, dx: Optional[torch.Tensor],
-            lddx: int, accumulate: bool, dx_add: bool = False, dx_cols: Optional[int] = None):
+            lddx: int, accumulate: bool, dx_add: bool = False, dx_cols: Optional[int] = None,
+            gelu_h: Optional[torch.Tensor] = None):
         """dx_add: dx += the data gradient (a residual branch's; the GEMM's epilogue adds it, mmseg_conv_gemm_res,
         when it runs without split-K), instead of dx := it.  dx_cols: as fwd's ncols for dx (zero columns
-        [Ci, dx_cols) from the zero-padded data-gradient image: whole-row writes)."""
+        [Ci, dx_cols) from the zero-padded data-gradient image: whole-row writes).  gelu_h: dx := (dy W) * gelu'(gelu_h)
+        (the data gradient through the GELU that produced this layer's input; dense rows), in the GEMM's epilogue
+        when it runs without split-K, else the GEMM + mmseg_gelu_bwd -- bitwise the same."""
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code
         ks = L.mmseg_wgrad_splits(M, _wgrad_ksplit(self.Co, self.Cip, M))
         defer = self.rt.defer_wred(self.flat)
@@ -176,14 +192,22 @@ class Lin:
             if dx_add and (kd > 1 or not _res_fuse()):
                 raise ValueError("Lin.bwd(dx_add): the residual epilogue needs the unsplit GEMM")
             ws = self.rt.ws(kd * M * ncd) if kd > 1 else None
+            gelu_fused = gelu_h is not None and kd == 1 and _res_fuse()
             with TIMER.region(_gemm_name(self.rt, 0, "point"), flops=2.0 * M * self.Ci * self.Co,
                               nbytes=_io_bytes(self.rt, M, self.Co, self.Ci, self.Ci * self.Co)):
-                if dx_add:
+                if gelu_fused:
+                    if dx_add or ncd != self.Ci or lddx != self.Ci:
+                        raise ValueError("Lin.bwd(gelu_h): dense data gradient only")
+                    L.mmseg_conv_gemm_gelu(ptr(dy), lddy, ptr(self.wd), None, ptr(dx), lddx, ptr(gelu_h), None, 2, M,
+                                           self.Ci, self.Cpad_d, self.KGd, code, s)
+                elif dx_add:
                     L.mmseg_conv_gemm_res(ptr(dy), lddy, ptr(self.wd), None, ptr(dx), lddx, ptr(dx), lddx, M, ncd,
                                           self.Cpad_d, self.KGd, code, s)
                 else:
                     L.mmseg_conv_gemm(ptr(dy), lddy, ptr(self.wd), None, ptr(dx), lddx, ptr(ws), MODE_POINT, M,
                                       ncd, self.Cpad_d, self.KGd, 0, 1, 1, 1, kd, code, s)
+            if gelu_h is not None and not gelu_fused:
+                L.mmseg_gelu_bwd(ptr(gelu_h), ptr(dx), ptr(dx), M * self.Ci, code, s)
 
     def dgrad_splits(self, M: int, ncols: Optional[int] = None) -> int:
         return _gemm_ksplit(M, self.Ci if ncols is None else ncols, self.KGd)
@@ -318,9 +342,8 @@ class SwinBlockProg:
         st2 = self.ln2.fwd(xm, C, M, ln2, C)
         hdim = self.fc1.Co
         hbuf = self._empty(M * hdim)
-        self.fc1.fwd(ln2, C, M, hbuf, hdim)
         g = self._empty(M * hdim)
-        L.mmseg_gelu_fwd(ptr(hbuf), ptr(g), M * hdim, code, s)
+        self.fc1.fwd_gelu(ln2, C, M, hbuf, g)          # h = linear1(.), g = GELU(h)
         if seeds:                         # MLPBlock drop1 (after the activation)
             drop(g, g, M, hdim, seeds[1])
         out = self._empty(M * C)
@@ -348,11 +371,13 @@ class SwinBlockProg:
             dz = self._empty(M * C)
             drop(dout, dz, M, C, seeds[2])
         dg = self._empty(M * hdim)
-        self.fc2.bwd(st["g"], hdim, dz, C, M, dg, hdim, accumulate)
-        del dz
         if seeds:
+            self.fc2.bwd(st["g"], hdim, dz, C, M, dg, hdim, accumulate)
             drop(dg, dg, M, hdim, seeds[1])
-        L.mmseg_gelu_bwd(ptr(st["h"]), ptr(dg), ptr(dg), M * hdim, code, s)
+            L.mmseg_gelu_bwd(ptr(st["h"]), ptr(dg), ptr(dg), M * hdim, code, s)
+        else:                             # d(linear1 output) = (dz W2) * GELU'(h)
+            self.fc2.bwd(st["g"], hdim, dz, C, M, dg, hdim, accumulate, gelu_h=st["h"])
+        del dz
         dln2 = self._empty(M * C)
         self.fc1.bwd(st["ln2"], C, dg, hdim, M, dln2, C, accumulate)
         del dg

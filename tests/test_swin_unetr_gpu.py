@@ -323,6 +323,42 @@ def test_point_gemm_residual_epilogue_bitwise(dev, dtype, Co, Ci, M, monkeypatch
             L.bwd(x, Ci, dy, Co, M, dx1, Ci, False, dx_add=True)
 
 
+@pytest.mark.parametrize("Co,Ci,M", [(192, 48, 4000), (384, 96, 2500)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_point_gemm_gelu_epilogue_bitwise(dev, dtype, Co, Ci, M, monkeypatch):
+    """mmseg_conv_gemm_gelu (MLPBlock linear1 + GELU forward, linear2's data gradient through the GELU) bit for bit
+    against the GEMM followed by mmseg_gelu_fwd / mmseg_gelu_bwd, and close to torch fp64."""
+    from mmseg_amd.engine.runtime import FlatParams, Runtime
+    from mmseg_amd.engine.swin import Lin
+    torch.manual_seed(5)
+    rt = Runtime(dev, dtype)
+    fc1, fc2 = torch.nn.Linear(Ci, Co).to(dev), torch.nn.Linear(Co, Ci).to(dev)
+    flat = FlatParams(list(fc1.parameters()) + list(fc2.parameters()))
+    l1, l2 = Lin(rt, fc1.weight, fc1.bias, flat), Lin(rt, fc2.weight, fc2.bias, flat)
+    for d in l1.descs() + l2.descs():
+        lib().mmseg_pack_weight(*d, rt.code, rt.stream)
+    x = torch.randn(M * Ci, device=dev).to(dtype)
+    dz = torch.randn(M * Ci, device=dev).to(dtype)
+    outs = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("MMSEG_RES_FUSE", fuse)
+        h = torch.empty(M * Co, device=dev, dtype=dtype)
+        g = torch.empty(M * Co, device=dev, dtype=dtype)
+        l1.fwd_gelu(x, Ci, M, h, g)
+        dg = torch.empty(M * Co, device=dev, dtype=dtype)
+        l2.bwd(g, Co, dz, Ci, M, dg, Co, False, gelu_h=h)
+        outs.append((h, g, dg))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    h, g, dg = outs[0]
+    hr = x.view(M, Ci).double() @ fc1.weight.double().t() + fc1.bias.double()
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert rel(g.view(M, Co), F.gelu(hr)) < tol
+    hq = h.view(M, Co).double().requires_grad_(True)
+    F.gelu(hq).backward(dz.view(M, Ci).double() @ fc2.weight.double())
+    assert rel(dg.view(M, Co), hq.grad) < tol
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_swin_res_fuse_bitwise(dev, swin_case, dtype, monkeypatch):
     """The network with the fused tail backward (default) and with MMSEG_RES_FUSE=0: bitwise equal gradients."""
