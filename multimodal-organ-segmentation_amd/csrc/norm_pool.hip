@@ -583,7 +583,7 @@ __global__ void in_bwd_finalize(const float* __restrict__ part, int N, int C, in
 }
 
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)); same thread layout as the apply kernels
-template <typename T, int ACT = 1>
+template <typename T, int ACT = 1, bool ZP = false>
 __global__ void in_bwd_apply(const T* __restrict__ x, int ldx, const float* __restrict__ mean,
                              const float* __restrict__ rstd, DySrc s, const float* __restrict__ coef, T* __restrict__ dx,
                              int lddx, int V, int C, int D, int H, int W, int vpc, int npad) {
@@ -631,7 +631,9 @@ __global__ void in_bwd_apply(const T* __restrict__ x, int ldx, const float* __re
         o.set(j, rs[j] * (g - ca[j] - h * cb[j]));
       }
       o.store(dxn + (long long)(vb + u * lanes_v) * lddx);
-      if (cg < npad) store_zero8(dxn + (long long)(vb + u * lanes_v) * lddx + C);   // (dxn is at channel 8 cg)
+      if constexpr (ZP) {   // whole-row writes (a separate instantiation: the plain one keeps its code)
+        if (cg < npad) store_zero8(dxn + (long long)(vb + u * lanes_v) * lddx + C);   // (dxn is at channel 8 cg)
+      }
     }
   }
 }
@@ -1827,8 +1829,12 @@ int instnorm_bwd_impl(const void* x, int ldx, const float* mean, const float* rs
     constexpr int R = decltype(act_c)::value;
     if (part_in) {
       MMSEG_LAUNCH(in_bwd_finalize, dim3(N * C), dim3(256), 0, s, part_in, N, C, nchunk_in, V, coef);
-      MMSEG_LAUNCH((in_bwd_apply<T, R>), agrid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, coef,
-                         (T*)dx, lddx, (int)V, C, D, H, W, avpc, npad);
+      if (npad)
+        MMSEG_LAUNCH((in_bwd_apply<T, R, true>), agrid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, coef,
+                           (T*)dx, lddx, (int)V, C, D, H, W, avpc, npad);
+      else
+        MMSEG_LAUNCH((in_bwd_apply<T, R>), agrid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, coef,
+                           (T*)dx, lddx, (int)V, C, D, H, W, avpc, 0);
       return;
     }
     if (small) {
@@ -1849,8 +1855,12 @@ int instnorm_bwd_impl(const void* x, int ldx, const float* mean, const float* rs
     MMSEG_LAUNCH((in_bwd_partial<T, R>), grid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, (int)V, C, D,
                        H, W, (int)vpc, part);
     MMSEG_LAUNCH(in_bwd_finalize, dim3(N * C), dim3(256), 0, s, part, N, C, nch, V, coef);
-    MMSEG_LAUNCH((in_bwd_apply<T, R>), agrid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, coef, (T*)dx,
-                       lddx, (int)V, C, D, H, W, avpc, npad);
+    if (npad)
+      MMSEG_LAUNCH((in_bwd_apply<T, R, true>), agrid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, coef,
+                         (T*)dx, lddx, (int)V, C, D, H, W, avpc, npad);
+    else
+      MMSEG_LAUNCH((in_bwd_apply<T, R>), agrid, dim3(256), 0, s, (const T*)x, ldx, mean, rstd, src, coef, (T*)dx,
+                         lddx, (int)V, C, D, H, W, avpc, 0);
   };
   auto act = [&](auto tag) {
     if (relu == 2) run(tag, std::integral_constant<int, 2>{});

@@ -217,15 +217,26 @@ class Trainer:
         boundary = (batch_idx + 1) % self.accumulation_steps == 0
         if self.kernels == "torch":
             return self._torch_step(images, labels, boundary, sync)
-        if self._graph_ok and self._graphs.usable(images, labels):
+        if self._graph_ok and self._graphs is not None and self._graphs.usable(images, labels):
             # the whole step (forward, fused loss, backward, AdamW) as one captured graph (trainer/step_graph.py)
             if labels.dtype not in (torch.int64, torch.uint8):
                 labels = labels.long()
-            out, guard = self._graphs.run(images.contiguous(), labels.contiguous())
-            if not sync:
-                self._defer_guard(guard)
-                return out.clone()
-            return self._after_step(out.item(), guard, boundary=True, guarded=True)
+            try:
+                out, guard = self._graphs.run(images.contiguous(), labels.contiguous())
+            except RuntimeError as e:
+                # the captured data-parallel step over several ranks has not run on hardware (step_graph.py): if its
+                # first capture fails -- on every rank alike, they run the same code -- the step stays eager
+                if not (self.dp and self._graphs.graphs == {} and self._graphs.copy_graph is None):
+                    raise
+                import warnings
+                warnings.warn(f"captured data-parallel step failed to capture ({e}); the DP step runs eagerly",
+                              RuntimeWarning, stacklevel=2)
+                self._graphs, self._graph_ok = None, False
+            else:
+                if not sync:
+                    self._defer_guard(guard)
+                    return out.clone()
+                return self._after_step(out.item(), guard, boundary=True, guarded=True)
         loss = self._fused_loss(images, labels)
         fused = loss is not None
         if loss is None:

@@ -247,19 +247,30 @@ def _rccl_graph_worker(port, q):
         xs, ys = _data()
         dev = torch.device("cuda", 0)
         batches = [{"image": xs[s].to(dev), "label": ys[s].to(dev)} for s in range(STEPS)]
+        from mmseg_amd.trainer import step_graph as SG
         out = {}
-        for tag, graph, dp in (("eager_dp", False, True), ("graph_dp", True, True), ("graph", True, False)):
+        for tag, graph, dp, fail in (("eager_dp", False, True, False), ("graph_dp", True, True, False),
+                                     ("graph", True, False, False), ("graph_dp_fail", True, True, True)):
             os.environ["MMSEG_STEP_GRAPH"] = "1" if graph else "0"
             cfg = _cfg(f"/tmp/mmseg_rccl_{tag}")
             cfg["hardware"]["step_graph"] = True
             cfg["distributed"]["reduce_single_rank"] = dp
             torch.manual_seed(0)
-            model = build_model(cfg)
-            tr = Trainer(cfg, model)
-            losses = [tr.train_step(batches[s % STEPS], s) for s in range(5)]
+            orig = SG.StepGraphs._capture
+            if fail:      # a DP capture that fails: the trainer must fall back to the eager DP step
+                def _boom(self, x, y):
+                    raise RuntimeError("injected capture failure")
+                SG.StepGraphs._capture = _boom
+            try:
+                model = build_model(cfg)
+                tr = Trainer(cfg, model)
+                losses = [tr.train_step(batches[s % STEPS], s) for s in range(5)]
+            finally:
+                SG.StepGraphs._capture = orig
             torch.cuda.synchronize()
             w = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()])
-            out[tag] = {"losses": losses, "w": w.numpy(), "graphs": len(tr._graphs.graphs), "dp": tr.dp,
+            out[tag] = {"losses": losses, "w": w.numpy(),
+                        "graphs": len(tr._graphs.graphs) if tr._graphs is not None else -1, "dp": tr.dp,
                         "buckets": 0 if tr._buckets is None else len(tr._buckets.buckets),
                         "backend": dist.get_backend()}
         dist.destroy_process_group()
@@ -295,3 +306,7 @@ def test_rccl_dp_step_captured_bitwise_equal_to_eager(dev):
     assert res["eager_dp"]["losses"] == res["graph_dp"]["losses"] == res["graph"]["losses"]
     assert np.array_equal(res["eager_dp"]["w"], res["graph_dp"]["w"])
     assert np.array_equal(res["graph"]["w"], res["graph_dp"]["w"])
+    # a failed first capture of the DP step: eager from then on, bitwise the eager DP run
+    assert res["graph_dp_fail"]["graphs"] == -1
+    assert res["graph_dp_fail"]["losses"] == res["eager_dp"]["losses"]
+    assert np.array_equal(res["graph_dp_fail"]["w"], res["eager_dp"]["w"])
