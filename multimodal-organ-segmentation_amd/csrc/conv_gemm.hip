@@ -2526,13 +2526,22 @@ struct Conv3Plan {
 Conv3Plan plan_conv3(int M, int Ncols, int cin, int D, int H, int W, int lda, int ldo, int tsize,
                      bool force_r = false) {
   Conv3Plan p{0, 0, 0, 0, 1, 32};
+  bool k1_ok = false;   // the brick2 family can take the shape (used when the runtime brick cannot)
   const int brick = knob("MMSEG_BRICK", 2);
   const bool base_ok = cin % CK == 0 && lda % 8 == 0 && ldo % 8 == 0 && Ncols % 32 == 0;
   // 48-column multiples (SwinUNETR's feature_size 48) run the brick2 kernel with 48-column tiles
   const bool ok48 = cin % CK == 0 && lda % 8 == 0 && ldo % 8 == 0 && Ncols % 48 == 0 && knob("MMSEG_BRICK2_BN48", 1);
   if (!force_r && brick == 2 && (base_ok || ok48) && D % 4 == 0 && H % B2_Y == 0 && W % B2_X == 0) {
-    p.kind = 1;
-    return p;
+    // a brick2-family launch has one block per (4x8x8 brick, column tile): at SwinUNETR's 8^3 / 16^3 levels
+    // (384 / 192 channels) that is 12-48 blocks for the whole chip (brick3 at 75-290 TF/s, r05m).  Below
+    // MMSEG_BRICK2_MINUNITS such shapes take the runtime-brick kernel, whose chunk splits fill the CUs.
+    const long long units = (long long)(M / (D * H * W)) * (D / 4) * (H / B2_Y) * (W / B2_X) *
+                            ((Ncols + 63) / 64);
+    if (!(base_ok && units < knob("MMSEG_BRICK2_MINUNITS", 128))) {
+      p.kind = 1;
+      return p;
+    }
+    k1_ok = true;
   }
   if (brick >= 2 && base_ok && knob("MMSEG_BRICKR", 1)) {
     int best = 0;
@@ -2580,6 +2589,7 @@ Conv3Plan plan_conv3(int M, int Ncols, int cin, int D, int H, int W, int lda, in
       return p;
     }
   }
+  if (k1_ok) p.kind = 1;
   return p;
 }
 

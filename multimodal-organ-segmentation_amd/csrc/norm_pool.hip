@@ -643,7 +643,7 @@ __global__ void in_bwd_apply(const T* __restrict__ x, int ldx, const float* __re
 // (sum g, sum g xhat) of the InstanceNorm backward of xa and, NX = 2, of xb -- over g as stored, with
 // in_bwd_partial's chunks, per-thread voxel order and reduction tree, so the partials and everything after them
 // are those of lrelu_bwd_kernel + in_bwd_partial bit for bit, without the separate passes over g.
-template <typename T, int NX>
+template <typename T, int NX, bool ZP>
 __global__ __launch_bounds__(256) void lrelu_bwd_in_partial(const T* __restrict__ y, int ldy,
                                                             const T* __restrict__ dy, int lddy, T* __restrict__ g,
                                                             int ldg, float slope, const T* __restrict__ xa, int lda,
@@ -690,7 +690,9 @@ __global__ __launch_bounds__(256) void lrelu_bwd_in_partial(const T* __restrict_
 #pragma unroll
         for (int j = 0; j < 8; ++j) gv.set(j, vy[u].get(j) > 0.f ? vd[u].get(j) : vd[u].get(j) * slope);
         gv.store(g + t * ldg + cg * 8);
-        if (cg < npad) store_zero8(g + t * ldg + C + cg * 8);
+        if constexpr (ZP) {
+          if (cg < npad) store_zero8(g + t * ldg + C + cg * 8);
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float gg = gv.get(j);
@@ -1762,19 +1764,24 @@ int mmseg_lrelu_bwd_in_part(const void* y, int ldy, const void* dy, int lddy, vo
   const int nch = chunks_for(V, C, &vpc);
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(nch, N);
-  auto run = [&](auto tag) {
+  auto run = [&](auto tag, auto zp) {
     using T = decltype(tag);
+    constexpr bool Z = decltype(zp)::value;
     if (xb)
-      MMSEG_LAUNCH((lrelu_bwd_in_partial<T, 2>), grid, dim3(256), 0, s, (const T*)y, ldy, (const T*)dy, lddy, (T*)g,
+      MMSEG_LAUNCH((lrelu_bwd_in_partial<T, 2, Z>), grid, dim3(256), 0, s, (const T*)y, ldy, (const T*)dy, lddy, (T*)g,
                    ldg, slope, (const T*)xa, lda, ma, ra, pa, (const T*)xb, ldb, mb, rb, pb, (int)V, C, (int)vpc,
                    npad);
     else
-      MMSEG_LAUNCH((lrelu_bwd_in_partial<T, 1>), grid, dim3(256), 0, s, (const T*)y, ldy, (const T*)dy, lddy, (T*)g,
+      MMSEG_LAUNCH((lrelu_bwd_in_partial<T, 1, Z>), grid, dim3(256), 0, s, (const T*)y, ldy, (const T*)dy, lddy, (T*)g,
                    ldg, slope, (const T*)xa, lda, ma, ra, pa, (const T*)nullptr, 0, nullptr, nullptr, nullptr, (int)V,
                    C, (int)vpc, npad);
   };
-  if (dtype == MMSEG_BF16) run(bf16_t{});
-  else run(float{});
+  auto zrun = [&](auto tag) {
+    if (npad) run(tag, std::true_type{});
+    else run(tag, std::false_type{});
+  };
+  if (dtype == MMSEG_BF16) zrun(bf16_t{});
+  else zrun(float{});
   return mmseg::check_launch("lrelu_bwd_in_part");
 }
 

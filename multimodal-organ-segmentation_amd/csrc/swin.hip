@@ -24,6 +24,7 @@
 #include "mmseg_common.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 namespace {
@@ -666,7 +667,7 @@ __device__ __forceinline__ void store_zero8(T* p) {
 // (row, channel) split is one 32-bit division per thread instead of two 64-bit divisions per 16-B access (which
 // held these passes to ~2.7 TB/s at 128^3, r05c timer).
 // y = lrelu((a - ma) * ra + R), R = (b - mb) * rb | b | 0; stats [n][C]; grid (row blocks, N)
-template <typename T>
+template <typename T, bool ZP>
 __global__ __launch_bounds__(256) void res_apply_kernel(const T* __restrict__ a, int lda, const float* __restrict__ ma,
                                                         const float* __restrict__ ra, const T* __restrict__ b, int ldb,
                                                         const float* __restrict__ mb, const float* __restrict__ rb,
@@ -711,13 +712,15 @@ __global__ __launch_bounds__(256) void res_apply_kernel(const T* __restrict__ a,
 #pragma unroll
       for (int j = 0; j < 8; ++j) vy.set(j, o[j] > 0.f ? o[j] : o[j] * slope);
       vy.store(y + t * ldy + c8 * 8);
-      if (c8 < npad) store_zero8(y + t * ldy + C + c8 * 8);
+      if constexpr (ZP) {
+        if (c8 < npad) store_zero8(y + t * ldy + C + c8 * 8);
+      }
     }
   }
 }
 
 // g = dy * (y > 0 ? 1 : slope)   (g may alias dy); same row-group layout over rows rows
-template <typename T>
+template <typename T, bool ZP>
 __global__ __launch_bounds__(256) void lrelu_bwd_kernel(const T* __restrict__ y, int ldy, const T* dy, int lddy, T* g,
                                                         int ldg, int C, float slope, int rows, int npad) {
   const int c8n = C >> 3, rpb = 256 / c8n;
@@ -740,7 +743,9 @@ __global__ __launch_bounds__(256) void lrelu_bwd_kernel(const T* __restrict__ y,
 #pragma unroll
       for (int j = 0; j < 8; ++j) vd[u].set(j, vy[u].get(j) > 0.f ? vd[u].get(j) : vd[u].get(j) * slope);
       vd[u].store(g + t * ldg + c8 * 8);
-      if (c8 < npad) store_zero8(g + t * ldg + C + c8 * 8);
+      if constexpr (ZP) {
+        if (c8 < npad) store_zero8(g + t * ldg + C + c8 * 8);
+      }
     }
   }
 }
@@ -1049,12 +1054,18 @@ int mmseg_res_apply(const void* a, int lda, const float* ma, const float* ra, co
   MMSEG_REQUIRE(V < (1LL << 31), "res_apply: V must fit int32");
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(row_blocks(V, C, N), N);
-  if (dtype == MMSEG_BF16)
-    MMSEG_LAUNCH(res_apply_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)a, lda, ma, ra, (const bf16_t*)b,
-                       ldb, mb, rb, (bf16_t*)y, ldy, (int)V, C, slope, (Cw - C) / 8);
-  else
-    MMSEG_LAUNCH(res_apply_kernel<float>, grid, dim3(256), 0, s, (const float*)a, lda, ma, ra, (const float*)b, ldb,
-                       mb, rb, (float*)y, ldy, (int)V, C, slope, (Cw - C) / 8);
+  auto run = [&](auto tag, auto zp) {
+    using T = decltype(tag);
+    MMSEG_LAUNCH((res_apply_kernel<T, decltype(zp)::value>), grid, dim3(256), 0, s, (const T*)a, lda, ma, ra,
+                 (const T*)b, ldb, mb, rb, (T*)y, ldy, (int)V, C, slope, (Cw - C) / 8);
+  };
+  if (dtype == MMSEG_BF16) {
+    if (Cw > C) run(bf16_t{}, std::true_type{});
+    else run(bf16_t{}, std::false_type{});
+  } else {
+    if (Cw > C) run(float{}, std::true_type{});
+    else run(float{}, std::false_type{});
+  }
   return mmseg::check_launch("res_apply");
 }
 
@@ -1065,12 +1076,18 @@ int mmseg_lrelu_bwd(const void* y, int ldy, const void* dy, int lddy, void* g, i
   MMSEG_REQUIRE(rows < (1LL << 31), "lrelu_bwd: rows must fit int32");
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(row_blocks(rows, C, 1));
-  if (dtype == MMSEG_BF16)
-    MMSEG_LAUNCH(lrelu_bwd_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)y, ldy, (const bf16_t*)dy, lddy,
-                       (bf16_t*)g, ldg, C, slope, (int)rows, (Cw - C) / 8);
-  else
-    MMSEG_LAUNCH(lrelu_bwd_kernel<float>, grid, dim3(256), 0, s, (const float*)y, ldy, (const float*)dy, lddy,
-                       (float*)g, ldg, C, slope, (int)rows, (Cw - C) / 8);
+  auto run = [&](auto tag, auto zp) {
+    using T = decltype(tag);
+    MMSEG_LAUNCH((lrelu_bwd_kernel<T, decltype(zp)::value>), grid, dim3(256), 0, s, (const T*)y, ldy, (const T*)dy,
+                 lddy, (T*)g, ldg, C, slope, (int)rows, (Cw - C) / 8);
+  };
+  if (dtype == MMSEG_BF16) {
+    if (Cw > C) run(bf16_t{}, std::true_type{});
+    else run(bf16_t{}, std::false_type{});
+  } else {
+    if (Cw > C) run(float{}, std::true_type{});
+    else run(float{}, std::false_type{});
+  }
   return mmseg::check_launch("lrelu_bwd");
 }
 

@@ -16,6 +16,14 @@ from tests.helpers import from_ndhwc, golden, rel, to_ndhwc
 
 pytestmark = pytest.mark.gpu
 DTYPES = [torch.float32, torch.bfloat16]
+@pytest.fixture(autouse=True)
+def _brick2_small_volumes(monkeypatch):
+    """These tests pin brick2-family kernels on small volumes; by default the engine sends conv launches of fewer
+    than MMSEG_BRICK2_MINUNITS (4x8x8 brick, 64-column) units to the runtime-brick kernel instead
+    (test_conv3_few_brick_units_take_runtime_brick covers that routing)."""
+    monkeypatch.setenv("MMSEG_BRICK2_MINUNITS", "0")
+
+
 TOL = {torch.float32: 2e-5, torch.bfloat16: 1.2e-2}
 GTOL = {torch.float32: 2e-5, torch.bfloat16: 2e-3}   # fp32-accumulated gradient outputs
 
@@ -679,3 +687,38 @@ def test_wgrad_dma_fragment_partials_bitwise(dev, cin, cout, shape, accumulate, 
     got = out["1"][0].double().cpu() - gw0.double().cpu()
     assert rel(got, ref) < GTOL[torch.bfloat16]
     assert rel(out["1"][1].double().cpu() - gb0.double().cpu(), dyr.sum(dim=(0, 2, 3, 4))) < GTOL[torch.bfloat16]
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("cin,cout,shape", [(384, 384, (1, 8, 8, 8)), (768, 384, (1, 8, 8, 8)), (192, 192, (1, 16, 16, 16))])
+def test_conv3_few_brick_units_take_runtime_brick(dev, dtype, cin, cout, shape, monkeypatch):
+    """SwinUNETR's 8^3 / 16^3 convs (384 / 768 / 192 channels at pitch 512 / 1024 / 256) are 12-48 brick2 blocks for
+    the whole chip; below MMSEG_BRICK2_MINUNITS (default 128) the plan takes the runtime-brick kernel with chunk
+    splits.  Forward, data gradient and weight gradient against fp64 (as test_conv3_channel_padded)."""
+    monkeypatch.delenv("MMSEG_BRICK2_MINUNITS", raising=False)
+    from mmseg_amd.engine.swin import cpad
+    torch.manual_seed(cin + cout)
+    conv = nn.Conv3d(cin, cout, 3, padding=1, bias=False).to(dev)
+    rt = Runtime(dev, dtype)
+    flat = FlatParams(list(conv.parameters()))
+    cip, cop = cpad(cin), cpad(cout)
+    layer = Conv3(rt, conv, flat, cin_pad=cip, cout_pad=cop, pad_cols=True)
+    N, D, H, W = shape
+    x = torch.randn(N, cin, D, H, W, device=dev)
+    xa = Act(to_ndhwc(x, dtype, ld=cip), 0, cin, cip, N, D, H, W)
+    ya = Act(torch.zeros(N * D * H * W * cop, dtype=dtype, device=dev), 0, cout, cop, N, D, H, W)
+    layer.pack()
+    layer.fwd(xa, ya)
+    torch.cuda.synchronize()
+    assert lib().mmseg_last_kernel().decode().startswith("conv3_brickr_kernel")
+    xd = _q(x, dtype).requires_grad_(True)
+    wd = _q(conv.weight, dtype).requires_grad_(True)
+    ref = F.conv3d(xd, wd, padding=1)
+    assert rel(from_ndhwc(ya.buf, N, cout, D, H, W, ld=cop), ref) < TOL[dtype]
+    dy = torch.randn(ref.shape, device=dev)
+    dya = Act(to_ndhwc(dy, dtype, ld=cop), 0, cout, cop, N, D, H, W)
+    dxa = Act(torch.zeros(N * D * H * W * cip, dtype=dtype, device=dev), 0, cin, cip, N, D, H, W)
+    layer.bwd(xa, dya, dxa, accumulate=False)
+    (ref * _q(dy, dtype)).sum().backward()
+    assert rel(from_ndhwc(dxa.buf, N, cin, D, H, W, ld=cip), xd.grad) < TOL[dtype]
+    assert rel(flat.grad(conv.weight), wd.grad) < GTOL[dtype]
