@@ -373,8 +373,9 @@ int stem_kp(int cr) { return ((27 * cr + 31) / 32) * 32; }
 extern "C" {
 
 int mmseg_stem_ok(int cr, int Co, int D, int H, int W, int ldx, int ldy) {
-  return cr >= 1 && cr <= 4 && (ldx == SCR || ldx == cr) && (Co == 16 || Co == 32) && ldy % 8 == 0 && D % SZ == 0 &&
-         H % SY == 0 && W % SX == 0;
+  // Co 48: SwinUNETR's encoder1 conv1 (2 -> 48 at 128^3), no bias, no fused statistics
+  return cr >= 1 && cr <= 4 && (ldx == SCR || ldx == cr) && (Co == 16 || Co == 32 || Co == 48) && ldy % 8 == 0 &&
+         D % SZ == 0 && H % SY == 0 && W % SX == 0;
 }
 
 int mmseg_stem_fwd_stats(const void* x, int ldx, int cr, const float* w, const float* bias, void* y, int ldy, int N,
@@ -395,6 +396,7 @@ int mmseg_stem_fwd_stats(const void* x, int ldx, int cr, const float* w, const f
                          int D, int H, int W, int Co, float* stats, int dtype, void* stream) {
   MMSEG_REQUIRE(mmseg_stem_ok(cr, Co, D, H, W, ldx, ldy), "stem_fwd: unsupported shape (cr=%d Co=%d %dx%dx%d)", cr,
                 Co, D, H, W);
+  MMSEG_REQUIRE(Co != 48 || !stats, "stem_fwd: fused statistics need Co = 16 / 32 (power-of-two lane merges)");
   StemArgs g{x, ldx, cr, w, bias, y, ldy, nullptr, 0, nullptr, nullptr, N, D, H, W, Co, stem_kp(cr), 1};
   g.stats = stats;
   const dim3 grid(N * (D / SZ) * (H / SY) * (W / SX));
@@ -412,9 +414,11 @@ int mmseg_stem_fwd_stats(const void* x, int ldx, int cr, const float* w, const f
   };
   if (dtype == MMSEG_BF16) {
     if (Co == 16) run(bf16_t{}, std::integral_constant<int, 1>{});
+    else if (Co == 48) run(bf16_t{}, std::integral_constant<int, 3>{});
     else run(bf16_t{}, std::integral_constant<int, 2>{});
   } else {
     if (Co == 16) run(float{}, std::integral_constant<int, 1>{});
+    else if (Co == 48) run(float{}, std::integral_constant<int, 3>{});
     else run(float{}, std::integral_constant<int, 2>{});
   }
   return mmseg::check_launch("stem_fwd");
@@ -452,6 +456,7 @@ int mmseg_stem_wgrad_inb(const void* dy, int lddy, const void* x, int ldx, int c
                          const float* inmean, const float* inrstd, const float* incoef, float* part, float* bias_part,
                          int N, int D, int H, int W, int Co, int ksplit, int dtype, void* stream) {
   MMSEG_REQUIRE(mmseg_stem_ok(cr, Co, D, H, W, ldx, lddy), "stem_wgrad: unsupported shape");
+  MMSEG_REQUIRE(Co != 48 || (!bias_part && !inx), "stem_wgrad: Co = 48 without bias / fused norm backward only");
   MMSEG_REQUIRE(!inx || (inmean && inrstd && incoef && ldinx % 8 == 0),
                 "stem_wgrad_inb: the norm's statistics and coefficients are required, ldinx a multiple of 8");
   StemArgs g{x, ldx, cr, nullptr, nullptr, nullptr, 0, dy, lddy, part, bias_part, N, D, H, W, Co, stem_kp(cr),
@@ -480,9 +485,11 @@ int mmseg_stem_wgrad_inb(const void* dy, int lddy, const void* x, int ldx, int c
   };
   if (dtype == MMSEG_BF16) {
     if (Co == 16) run(bf16_t{}, std::integral_constant<int, 1>{});
+    else if (Co == 48) run(bf16_t{}, std::integral_constant<int, 3>{});
     else run(bf16_t{}, std::integral_constant<int, 2>{});
   } else {
     if (Co == 16) run(float{}, std::integral_constant<int, 1>{});
+    else if (Co == 48) run(float{}, std::integral_constant<int, 3>{});
     else run(float{}, std::integral_constant<int, 2>{});
   }
   return mmseg::check_launch("stem_wgrad");

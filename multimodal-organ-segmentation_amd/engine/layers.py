@@ -365,7 +365,8 @@ class Conv3:
             kp = L.mmseg_stem_kp(self.Ci)
             defer = self.rt.defer_wred(self.flat)
             part = self._part(ks * self.Co * kp + ks * self.Co, own=defer)
-            bpart = part.data_ptr() + ks * self.Co * kp * 4
+            has_b = self.conv.bias is not None
+            bpart = part.data_ptr() + ks * self.Co * kp * 4 if has_b else None
             with TIMER.region("stem_wgrad_kernel", flops=2.0 * V * self.Co * 27 * self.Ci,
                               nbytes=_io_bytes(self.rt, V, 8, self.Co, 27 * self.Ci * self.Co, 4)):
                 if inb is not None:
@@ -376,9 +377,10 @@ class Conv3:
                     L.mmseg_stem_wgrad(dy.ptr, dy.ld, x.ptr, x.ld, self.Ci, ptr(part), bpart, x.N, x.D, x.H, x.W,
                                        self.Co, ks, code, s)
             (L.mmseg_wgrad_reduce_defer if defer else L.mmseg_wgrad_reduce)(
-                ptr(part), ptr(self.flat.grad(self.conv.weight)), bpart, ptr(self.flat.grad(self.conv.bias)), self.Co,
-                kp, ks, self.Ci, self.Ci, 27, int(accumulate), s)
-            self.flat.mark(self.conv.weight, self.conv.bias)
+                ptr(part), ptr(self.flat.grad(self.conv.weight)), bpart,
+                ptr(self.flat.grad(self.conv.bias)) if has_b else None, self.Co, kp, ks, self.Ci, self.Ci, 27,
+                int(accumulate), s)
+            self.flat.mark(*[p for p in (self.conv.weight, self.conv.bias) if p is not None])
             return
         rows = self.Cop if self.wg_stage is not None else self.Co
         wsf = L.mmseg_conv3_wgrad_ws_floats(V, rows, self.Cip, self.Ci, self.cpg_shift, x.D, x.H, x.W, dy.ld,
