@@ -14,6 +14,8 @@
 //   input:  NCDHW fp32 volume -> NDHWC (8-channel padded) engine layout.
 #include "mmseg_common.h"
 
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 
@@ -138,6 +140,60 @@ __global__ __launch_bounds__(256) void head_fwd_u_kernel(const T* __restrict__ x
     const long long n = i / V, v = i - n * V;
 #pragma unroll
     for (int c = 0; c < CC; ++c) logits[(n * CC + c) * V + v] = acc[u][c];
+  }
+}
+
+// Tile-staged head for padded feature rows (SwinUNETR: 48 channels at pitch 64).  head_fwd_u gives each lane one
+// voxel, so a wave's 16-B loads touch 64 rows 128 B apart (225 us at 128^3, ~1.4 TB/s, r05s).  Here a block stages
+// HT_V consecutive voxels' CG 16-B groups with lanes on consecutive groups (each row's 96 B read by neighbouring
+// lanes), converts them to fp32 in LDS, and then thread (voxel v = tid % HT_V, class slice) takes its classes'
+// dot products from LDS: the logit stores of a class are consecutive voxels.  Same per-logit fma order as
+// head_fwd_u (bias, then channels 0..Cin-1), so the logits are bitwise head_fwd_u's.
+constexpr int HT_V = 128;
+int head_knob(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+template <typename T, int CG, int CC>
+__global__ __launch_bounds__(256) void head_fwd_t_kernel(const T* __restrict__ x, int ldx,
+                                                         const float* __restrict__ Wt, const float* __restrict__ bias,
+                                                         long long V, int N, float* __restrict__ logits) {
+  constexpr int Cin = CG * 8, XP = Cin + 1;                  // fp32 row pitch (odd: conflict-free column reads)
+  constexpr int CS = (CC + 1) / 2;                           // classes per thread (two class slices)
+  __shared__ float sw[CC * Cin];
+  __shared__ float xs[HT_V * XP];
+  for (int i = threadIdx.x; i < CC * Cin; i += blockDim.x) sw[i] = Wt[i];
+  const long long total = (long long)N * V;
+  const int v = threadIdx.x % HT_V, half = threadIdx.x / HT_V;
+  for (long long t0 = (long long)blockIdx.x * HT_V; t0 < total; t0 += (long long)gridDim.x * HT_V) {
+    __syncthreads();   // the previous tile's reads are done (and, first time round, sw is written)
+#pragma unroll
+    for (int k = 0; k < (HT_V * CG + 255) / 256; ++k) {
+      const int e = threadIdx.x + 256 * k;
+      if (e < HT_V * CG) {
+        const int r = e / CG, cg = e - r * CG;
+        V8<T> a;
+        if (t0 + r < total) a.load(x + (t0 + r) * ldx + cg * 8);
+        else a.zero();
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xs[r * XP + cg * 8 + j] = a.get(j);
+      }
+    }
+    __syncthreads();
+    const long long i = t0 + v;
+    if (i < total) {
+      const long long n = i / V, vv = i - n * V;
+#pragma unroll
+      for (int cc = 0; cc < CS; ++cc) {
+        const int c = half * CS + cc;
+        if (c < CC) {
+          float acc = bias[c];
+#pragma unroll 8
+          for (int ci = 0; ci < Cin; ++ci) acc = fmaf(sw[c * Cin + ci], xs[v * XP + ci], acc);
+          logits[(n * CC + c) * V + vv] = acc;
+        }
+      }
+    }
   }
 }
 
@@ -1426,6 +1482,12 @@ int mmseg_head_fwd(const void* x, int ldx, int Cin, const float* W, const float*
     using T = decltype(tag);
     constexpr int CG = decltype(cg_c)::value, CC = decltype(cc_c)::value;
     if (Cin != CG * 8 || C != CC) return false;
+    if (CG == 6 && !dscale && head_knob("MMSEG_HEAD_TILE", 1)) {   // padded 48-channel rows: the tile-staged form
+      const int tgrid = (int)std::min<long long>(ceil_div((long long)N * V, (long long)HT_V), 4096LL);
+      MMSEG_LAUNCH((head_fwd_t_kernel<T, CG, CC>), dim3(tgrid), dim3(256), 0, s, (const T*)x, ldx, W, b, V, N,
+                   logits);
+      return true;
+    }
     MMSEG_LAUNCH((head_fwd_u_kernel<T, CG, CC>), dim3(ugrid), dim3(256), 0, s, (const T*)x, ldx, W, b, dscale,
                        V, N, logits);
     return true;

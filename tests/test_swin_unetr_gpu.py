@@ -833,3 +833,26 @@ def test_window_attention_backward_r05_forms(dev, N, hd, heads, masked, monkeypa
     (d1, s1), (d0, s0) = res
     assert rel2(d1, d0) < 2e-2 and rel2(s1, s0) < 2e-2
     assert torch.equal(s1[..., N:], torch.zeros_like(s1[..., N:]))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_head_48_channels_tile(dev, dtype, monkeypatch):
+    """SwinUNETR's 1x1 head on 48 channels at pitch 64: the tile-staged forward (MMSEG_HEAD_TILE, default) is bitwise
+    the one-voxel-per-lane kernel, and both match torch fp64."""
+    N, V, Cin, ld, C = 1, 3000, 48, 64, 6
+    g = torch.Generator().manual_seed(41)
+    x = torch.randn(N * V, ld, generator=g).to(dtype)
+    x[:, Cin:] = 0
+    W = torch.randn(C, Cin, generator=g) * 0.2
+    b = torch.randn(C, generator=g)
+    xd, Wd, bd = x.to(dev), W.to(dev), b.to(dev)
+    L, s = lib(), stream_handle()
+    outs = []
+    for tile in ("1", "0"):
+        monkeypatch.setenv("MMSEG_HEAD_TILE", tile)
+        lg = torch.empty(N * C * V, device=dev)
+        L.mmseg_head_fwd(ptr(xd), ld, Cin, ptr(Wd), ptr(bd), None, C, N, V, ptr(lg), CODE[dtype], s)
+        outs.append(lg)
+    assert torch.equal(outs[0], outs[1])
+    ref = x[:, :Cin].double() @ W.double().t() + b.double()
+    assert rel(outs[0].view(C, V).t(), ref) < 1e-5
