@@ -339,14 +339,35 @@ __global__ __launch_bounds__(512) void winattn_fwd1_kernel(WinAttnArgs a) {
   }
 }
 
+// sum_d dO[row][d] O[row][d] of one head (fp32, d in order): head_dim 16 / 8 from 16-B vector loads issued
+// together (a scalar loop over head_dim waited on each 2-B load in turn), any other head_dim element-wise
+__device__ __forceinline__ float dot_dO_O(const WinAttnArgs& a, long long base) {
+  float d = 0.f;
+  if (a.hd == 16 || a.hd == 8) {
+    V8<bf16_t> g0, g1, o0, o1;
+    g0.load(a.dO + base);
+    o0.load(a.O + base);
+    if (a.hd == 16) {
+      g1.load(a.dO + base + 8);
+      o1.load(a.O + base + 8);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d += g0.get(j) * o0.get(j);
+    if (a.hd == 16) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d += g1.get(j) * o1.get(j);
+    }
+    return d;
+  }
+  for (int j = 0; j < a.hd; ++j) d += (float)a.dO[base + j] * (float)a.O[base + j];
+  return d;
+}
+
 // D[q] = sum_d dO[q][d] O[q][d] of this head (fp32), staged into LDS
 __device__ __forceinline__ void stage_D(float* Dq, const WinAttnArgs& a, const Stage& s) {
   for (int n = threadIdx.x; n < s.np; n += blockDim.x) {
     float d = 0.f;
-    if (n < s.N) {
-      const long long base = (long long)(s.b * s.N + n) * a.C + s.h * a.hd;
-      for (int j = 0; j < a.hd; ++j) d += (float)a.dO[base + j] * (float)a.O[base + j];
-    }
+    if (n < s.N) d = dot_dO_O(a, (long long)(s.b * s.N + n) * a.C + s.h * a.hd);
     Dq[n] = d;
   }
 }
@@ -554,8 +575,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_qb_kernel(WinAttnArgs a, int 
       const int qq = q0 + n;
       float d = 0.f, l = 0.f;
       if (qq < a.N) {
-        const long long base = (long long)(b * a.N + qq) * a.C + hoff;
-        for (int j = 0; j < a.hd; ++j) d += (float)a.dO[base + j] * (float)a.O[base + j];
+        d = dot_dO_O(a, (long long)(b * a.N + qq) * a.C + hoff);
         l = a.lse[(long long)bh * NPMAX + qq];
       }
       Dq[n] = d;
@@ -772,8 +792,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_qb2_kernel(WinAttnArgs a, int
       const int qq = q0 + n;
       float d = 0.f, l = 0.f;
       if (qq < a.N) {
-        const long long base = (long long)(b * a.N + qq) * a.C + hoff;
-        for (int j = 0; j < a.hd; ++j) d += (float)a.dO[base + j] * (float)a.O[base + j];
+        d = dot_dO_O(a, (long long)(b * a.N + qq) * a.C + hoff);
         l = a.lse[(long long)bh * NPMAX + qq];
       }
       Dq[n] = d;
