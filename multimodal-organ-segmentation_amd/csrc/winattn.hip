@@ -81,32 +81,62 @@ struct Stage {
 
 __device__ __forceinline__ void stage_rows(bf16_t (*dst)[16], const bf16_t* src, int ld, int col0, const Stage& s,
                                            int hd, bf16_t (*dstT)[TP]) {
-  // thread per (token, 8-channel half); zeros past N and past hd
-  for (int e = threadIdx.x; e < s.np * 2; e += blockDim.x) {
-    const int n = e >> 1, half = e & 1;
-    V8<bf16_t> v;
-    if (n < s.N && half * 8 < hd) {
-      if (hd >= half * 8 + 8) {
-        v.load(src + (long long)(s.b * s.N + n) * ld + col0 + half * 8);
+  // thread per (token, 8-channel half); zeros past N and past hd.  SU items per thread per pass, all their loads
+  // issued before the first LDS store (one global round trip per pass instead of one per item)
+  constexpr int SU = 2;
+  for (int e0 = threadIdx.x; e0 < s.np * 2; e0 += SU * blockDim.x) {
+    V8<bf16_t> v[SU];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const int e = e0 + u * blockDim.x;
+      const int n = e >> 1, half = e & 1;
+      if (e < s.np * 2 && n < s.N && half * 8 < hd) {
+        if (hd >= half * 8 + 8) {
+          v[u].load(src + (long long)(s.b * s.N + n) * ld + col0 + half * 8);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            v[u].set(j, half * 8 + j < hd ? (float)src[(long long)(s.b * s.N + n) * ld + col0 + half * 8 + j] : 0.f);
+        }
       } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          v.set(j, half * 8 + j < hd ? (float)src[(long long)(s.b * s.N + n) * ld + col0 + half * 8 + j] : 0.f);
+        v[u].zero();
       }
-    } else {
-      v.zero();
     }
-    if (dst) v.store(&dst[n][half * 8]);
-    if (dstT) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dstT[half * 8 + j][n] = v.v[j];
+    for (int u = 0; u < SU; ++u) {
+      const int e = e0 + u * blockDim.x;
+      if (e >= s.np * 2) break;
+      const int n = e >> 1, half = e & 1;
+      if (dst) v[u].store(&dst[n][half * 8]);
+      if (dstT) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dstT[half * 8 + j][n] = v[u].v[j];
+      }
+    }
+  }
+}
+
+// the head's relative-position table row (times mul) into LDS: TU loads per thread in flight (a 7^3 window's
+// 2,197-entry table is one pass of 512 threads)
+__device__ __forceinline__ void stage_table_m(float* tab, const float* row, int T, float mul) {
+  constexpr int TU = 5;
+  for (int t0 = threadIdx.x; t0 < T; t0 += TU * blockDim.x) {
+    float v[TU];
+#pragma unroll
+    for (int u = 0; u < TU; ++u) {
+      const int tt = t0 + u * blockDim.x;
+      v[u] = tt < T ? row[tt] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < TU; ++u) {
+      const int tt = t0 + u * blockDim.x;
+      if (tt < T) tab[tt] = v[u] * mul;
     }
   }
 }
 
 __device__ __forceinline__ void stage_table(float* tab, const WinAttnArgs& a, int h) {
-  const float* row = a.table + (long long)h * a.T;
-  for (int t = threadIdx.x; t < a.T; t += blockDim.x) tab[t] = row[t];
+  stage_table_m(tab, a.table + (long long)h * a.T, a.T, 1.f);
 }
 
 __device__ __forceinline__ void stage_region(uint8_t* reg, const WinAttnArgs& a, int b) {
@@ -256,8 +286,7 @@ __global__ __launch_bounds__(512) void winattn_fwd1_kernel(WinAttnArgs a) {
   stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, nullptr);
   stage_rows(nullptr, a.qkv, C3, 2 * a.C + hoff, st, a.hd, Vt);
   {
-    const float* row = a.table + (long long)h * a.T;
-    for (int t = threadIdx.x; t < a.T; t += blockDim.x) tab[t] = row[t] * LOG2E;
+    stage_table_m(tab, a.table + (long long)h * a.T, a.T, LOG2E);
   }
   stage_codes(code, a, np);
   stage_region(reg, a, b);
@@ -664,8 +693,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_kv2_kernel(WinAttnArgs a) {
   stage_rows(Vs, a.qkv, C3, 2 * a.C + hoff, st, a.hd, nullptr);
   stage_rows(dOs, a.dO, a.C, hoff, st, a.hd, dOt);
   {
-    const float* row = a.table + (long long)h * a.T;
-    for (int t = threadIdx.x; t < a.T; t += blockDim.x) tab[t] = row[t] * LOG2E;
+    stage_table_m(tab, a.table + (long long)h * a.T, a.T, LOG2E);
   }
   stage_codes(code, a, np);
   stage_region(reg, a, b);
@@ -756,8 +784,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_qb2_kernel(WinAttnArgs a, int
   const int q = qt * 16 + r16;
   const bool qv = q < a.N;
   {
-    const float* row = a.table + (long long)h * a.T;
-    for (int t = threadIdx.x; t < a.T; t += blockDim.x) tab[t] = row[t] * LOG2E;
+    stage_table_m(tab, a.table + (long long)h * a.T, a.T, LOG2E);
   }
   stage_codes(code, a, np);
   const float* ctab = tab + code_off(a);
@@ -889,8 +916,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_q2_kernel(WinAttnArgs a) {
   stage_rows(Vs, a.qkv, C3, 2 * a.C + hoff, st, a.hd, nullptr);
   stage_rows(dOs, a.dO, a.C, hoff, st, a.hd, nullptr);
   {
-    const float* row = a.table + (long long)h * a.T;
-    for (int t = threadIdx.x; t < a.T; t += blockDim.x) tab[t] = row[t] * LOG2E;
+    stage_table_m(tab, a.table + (long long)h * a.T, a.T, LOG2E);
   }
   stage_codes(code, a, np);
   stage_region(reg, a, b);

@@ -1,4 +1,4 @@
-# r05w: vectorised dO.O dot products in the window-attention backward; swin tests + c4 bench
+# r05w: window-attention staging (dO.O vector dots, loads in flight before LDS stores); swin tests + c4 bench
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r05w; mkdir -p $O; cd /tmp; export TMPDIR=/tmp
 timeout -k 10 900 python3 -u -m pytest $R/tests/test_swin_unetr_gpu.py -x -q --timeout 600 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1; rc=$?
