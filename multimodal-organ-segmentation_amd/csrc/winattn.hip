@@ -139,10 +139,20 @@ __device__ __forceinline__ void stage_table(float* tab, const WinAttnArgs& a, in
   stage_table_m(tab, a.table + (long long)h * a.T, a.T, 1.f);
 }
 
-__device__ __forceinline__ void stage_region(uint8_t* reg, const WinAttnArgs& a, int b) {
-  if (!a.region) return;
+// the window's region labels (shifted windows) into LDS; returns whether they differ within the window -- only the
+// windows along the far faces of the shifted grid mix regions (271 of stage 0's 1,000), the others need no mask.
+// Every thread of the block must call it (block-wide vote).
+__device__ __forceinline__ bool stage_region(uint8_t* reg, const WinAttnArgs& a, int b) {
+  if (!a.region) return false;
   const uint8_t* r = a.region + (long long)(b % a.nw) * a.N;
-  for (int n = threadIdx.x; n < NPMAX; n += blockDim.x) reg[n] = n < a.N ? r[n] : 0;
+  const uint8_t r0 = r[0];
+  int mixed = 0;
+  for (int n = threadIdx.x; n < NPMAX; n += blockDim.x) {
+    const uint8_t v = n < a.N ? r[n] : 0;
+    reg[n] = v;
+    mixed |= (n < a.N && v != r0) ? 1 : 0;
+  }
+  return __syncthreads_or(mixed) != 0;
 }
 
 // bias + mask of one query against 4 consecutive keys k0..k0+3 (the S^T lane layout), -inf past N
@@ -289,7 +299,7 @@ __global__ __launch_bounds__(512) void winattn_fwd1_kernel(WinAttnArgs a) {
     stage_table_m(tab, a.table + (long long)h * a.T, a.T, LOG2E);
   }
   stage_codes(code, a, np);
-  stage_region(reg, a, b);
+  const bool rmix = stage_region(reg, a, b);
   __syncthreads();
   const float* ctab = tab + code_off(a);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -310,13 +320,13 @@ __global__ __launch_bounds__(512) void winattn_fwd1_kernel(WinAttnArgs a) {
         const f32x4 acc = mma(ld4(&Ks[kt * 16 + r16][4 * g4]), bq, (f32x4){0.f, 0.f, 0.f, 0.f});
         const int k0 = kt * 16 + 4 * g4;
         const int4 ck = *reinterpret_cast<const int4*>(code + k0);
-        const uint32_t rk = a.region ? *reinterpret_cast<const uint32_t*>(reg + k0) : 0u;
+        const uint32_t rk = rmix ? *reinterpret_cast<const uint32_t*>(reg + k0) : 0u;
         const int c[4] = {ck.x, ck.y, ck.z, ck.w};
         const bool last = kt == nt - 1;   // (wave-uniform) only the last key tile holds keys past N
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float t = fmaf(acc[r], sc2, tq[-c[r]]);
-          if (a.region && ((rk >> (8 * r)) & 255u) != rq) t -= pen2;
+          if (rmix && ((rk >> (8 * r)) & 255u) != rq) t -= pen2;
           if (last && k0 + r >= a.N) t = -INFINITY;
           v[kt][r] = t;
           mx = fmaxf(mx, t);
@@ -696,7 +706,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_kv2_kernel(WinAttnArgs a) {
     stage_table_m(tab, a.table + (long long)h * a.T, a.T, LOG2E);
   }
   stage_codes(code, a, np);
-  stage_region(reg, a, b);
+  const bool rmix = stage_region(reg, a, b);
   stage_D(Dq, a, st);
   for (int n = threadIdx.x; n < np; n += blockDim.x)
     lse2[n] = n < a.N ? a.lse[(long long)bh * NPMAX + n] * LOG2E : INFINITY;
@@ -723,7 +733,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_kv2_kernel(WinAttnArgs a) {
           const f32x4 dp = mma(ld4(&dOs[qq * 16 + r16][4 * g4]), bv, (f32x4){0.f, 0.f, 0.f, 0.f}); // dP[q][key]
           const int q0 = qq * 16 + 4 * g4;
           const int4 cq = *reinterpret_cast<const int4*>(code + q0);
-          const uint32_t rq = a.region ? *reinterpret_cast<const uint32_t*>(reg + q0) : 0u;
+          const uint32_t rq = rmix ? *reinterpret_cast<const uint32_t*>(reg + q0) : 0u;
           const float4 l4 = *reinterpret_cast<const float4*>(lse2 + q0);
           const float4 d4 = *reinterpret_cast<const float4*>(Dq + q0);
           const int c[4] = {cq.x, cq.y, cq.z, cq.w};
@@ -732,7 +742,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_kv2_kernel(WinAttnArgs a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float t = fmaf(sc[r], sc2, tk[c[r]]);
-            if (a.region && ((rq >> (8 * r)) & 255u) != rk) t -= pen2;
+            if (rmix && ((rq >> (8 * r)) & 255u) != rk) t -= pen2;
             p[r] = __builtin_amdgcn_exp2f(t - lq[r]);
             ds[r] = p[r] * (dp[r] - dq4[r]);
           }
@@ -802,7 +812,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_qb2_kernel(WinAttnArgs a, int
     __syncthreads();   // the previous window's operands are consumed
     stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, Kt);
     stage_rows(Vs, a.qkv, C3, 2 * a.C + hoff, st, a.hd, nullptr);
-    stage_region(reg, a, b);
+    const bool rmix = stage_region(reg, a, b);
     for (int e = threadIdx.x; e < QB_TILES * 16 * 2; e += blockDim.x) {
       const int n = e >> 1, half = e & 1, qq = q0 + n;
       V8<bf16_t> vq, vo;
@@ -845,13 +855,13 @@ __global__ __launch_bounds__(512) void winattn_bwd_qb2_kernel(WinAttnArgs a, int
             const f32x4 dp = mma(ld4(&Vs[kt * 16 + r16][4 * g4]), bdo, (f32x4){0.f, 0.f, 0.f, 0.f});
             const int k0 = kt * 16 + 4 * g4;
             const int4 ck = *reinterpret_cast<const int4*>(code + k0);
-            const uint32_t rk = a.region ? *reinterpret_cast<const uint32_t*>(reg + k0) : 0u;
+            const uint32_t rk = rmix ? *reinterpret_cast<const uint32_t*>(reg + k0) : 0u;
             const int c[4] = {ck.x, ck.y, ck.z, ck.w};
             float ds[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               float t = fmaf(sc[r], sc2, tq[-c[r]]);
-              if (a.region && ((rk >> (8 * r)) & 255u) != rq) t -= pen2;
+              if (rmix && ((rk >> (8 * r)) & 255u) != rq) t -= pen2;
               const float p = __builtin_amdgcn_exp2f(t - lq);
               ds[r] = p * (dp[r] - dq_);
               if (kt == nt - 1 && k0 + r >= a.N) ds[r] = 0.f;   // keys past N (only in the last tile)
@@ -919,7 +929,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_q2_kernel(WinAttnArgs a) {
     stage_table_m(tab, a.table + (long long)h * a.T, a.T, LOG2E);
   }
   stage_codes(code, a, np);
-  stage_region(reg, a, b);
+  const bool rmix = stage_region(reg, a, b);
   stage_D(Dq, a, st);
   for (int n = threadIdx.x; n < np; n += blockDim.x) lse2[n] = n < a.N ? a.lse[(long long)bh * NPMAX + n] * LOG2E : 0.f;
   __syncthreads();
@@ -948,13 +958,13 @@ __global__ __launch_bounds__(512) void winattn_bwd_q2_kernel(WinAttnArgs a) {
           const f32x4 dp = mma(ld4(&Vs[kt * 16 + r16][4 * g4]), bdo, (f32x4){0.f, 0.f, 0.f, 0.f});
           const int k0 = kt * 16 + 4 * g4;
           const int4 ck = *reinterpret_cast<const int4*>(code + k0);
-          const uint32_t rk = a.region ? *reinterpret_cast<const uint32_t*>(reg + k0) : 0u;
+          const uint32_t rk = rmix ? *reinterpret_cast<const uint32_t*>(reg + k0) : 0u;
           const int c[4] = {ck.x, ck.y, ck.z, ck.w};
           float ds[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float t = fmaf(sc[r], sc2, tq[-c[r]]);
-            if (a.region && ((rk >> (8 * r)) & 255u) != rq) t -= pen2;
+            if (rmix && ((rk >> (8 * r)) & 255u) != rq) t -= pen2;
             const float p = __builtin_amdgcn_exp2f(t - lq);
             ds[r] = p * (dp[r] - dq_);
             if (kt == nt - 1 && k0 + r >= a.N) ds[r] = 0.f;

@@ -1,0 +1,9 @@
+# r05y: window attention skips the region mask in single-region windows; swin tests + c4 bench
+set -o pipefail
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r05y; mkdir -p $O; cd /tmp; export TMPDIR=/tmp
+timeout -k 10 900 python3 -u -m pytest $R/tests/test_swin_unetr_gpu.py -x -q --timeout 600 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1; rc=$?
+tail -2 $O/tests.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/tests.log | head -20; exit 1; }
+timeout -k 10 600 python3 $R/bench.py --model swin_unetr --size 128 --batch 1 --steps 10 --warmup 3 --no-cpu-baseline --timer-steps 1 --timer-dump $O/timer.json > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
+python3 -c "
+import json; d=json.loads(open('$O/bench.log').read().strip().splitlines()[-1]); print('c4', d['ms_per_step'], d['value'])"
+python3 $R/tools/timer_families.py $O/timer.json 60 | grep -E "winattn|launches"
