@@ -3385,8 +3385,12 @@ __device__ __forceinline__ void wgrad_store_bias(const float (&bsum)[8], float* 
 // (SQ_LDS_BANK_CONFLICT = half the LDS-active cycles at 96^3).
 // NORM: x holds a pre-norm activation (g.nmean / g.nrstd, mmseg_conv3_wgrad_norm); a separate instantiation so
 // the plain kernel does not carry the statistics' registers (256 VGPRs + spills for CO64 otherwise)
-template <typename T, int MT, int V, bool NORM = false>
+// PIPE (bf16, V = 3): the software-pipelined multiply of wgrad_dma_kernel's PIPE form -- halo fragments two
+// (dy plane, tap) steps ahead in a ring of three, dy fragments one plane ahead -- instead of reading each tap's
+// fragments into the registers the previous tap's MFMAs just released (read, wait, 4 MFMAs, per tap).
+template <typename T, int MT, int V, bool NORM = false, bool PIPE = false>
 __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2_kernel(WgradArgs g) {
+  static_assert(!PIPE || (V == 3 && sizeof(T) == 2), "PIPE: bf16 with the V = 3 fragment order");
   constexpr int EP = 16 / sizeof(T);
   constexpr int CO = MT * 16, CG = CO / 8;       // output channels per block, 8-channel groups
   constexpr int DP = V == 3 ? (MT == 2 ? 48 : 80) : CO + EP;   // dy tile pitch (elements)
@@ -3411,8 +3415,9 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
   const long long HW = (long long)g.H * g.W;
   const int row0 = rt * CO, c0 = ct * CK;
   const bool do_bias = g.bias_part != nullptr && ct == 0;
-  const int t_begin = wave < 3 ? 4 * wave : 12 + 3 * (wave - 3);
-  const int t_cnt = wave < 3 ? 4 : 3;
+  // wave-uniform (SGPRs): the per-tap halo offsets are scalar, and the pipelined multiply branches on t_cnt
+  const int t_begin = __builtin_amdgcn_readfirstlane(wave < 3 ? 4 * wave : 12 + 3 * (wave - 3));
+  const int t_cnt = __builtin_amdgcn_readfirstlane(wave < 3 ? 4 : 3);
 
   f32x4 acc[4][MT][2];
 #pragma unroll
@@ -3555,7 +3560,59 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
     }
   };
 
-  {
+  // PIPE: steps s = (dy plane k4, tap t) over this wave's TC taps; lane rows v_lo = 32 k4 + v0 and v_lo + 8 (halo
+  // rows hlo and hlo + HLO_X of the tap's shifted window)
+  const int v0 = 16 * (g4 >> 1) + 4 * (g4 & 1) + q;
+  const int hlo0 = ((v0 >> 3) & 3) * HLO_X + (v0 & 7);
+  auto compute_pipe = [&](int buf, auto tcc) __attribute__((always_inline)) {
+    if constexpr (PIPE) {
+      constexpr int TC = decltype(tcc)::value;
+      constexpr int PD = 3, NS = 4 * TC;
+      const bf16_t* Dl = reinterpret_cast<const bf16_t*>(lds + buf * (DS + XS));
+      const bf16_t* Xl = Dl + DS;
+      bf16x8 af[2][MT], bf[PD][2];
+      auto load_a = [&](int k4, bf16x8(&a)[MT]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          const bf16_t* base = Dl + (32 * k4 + v0) * DP + i * 16 + 4 * p4;
+          a[i] = tr_frag(base, base + 8 * DP);
+        }
+      };
+      auto load_b = [&](int k4, int t, bf16x8(&b)[2]) __attribute__((always_inline)) {
+        const int tap = t_begin + t;
+        const int kz = tap / 9, ky = (tap / 3) % 3, kx = tap % 3;
+        const int h = k4 * (HLO_Y * HLO_X) + hlo0 + (kz * HLO_Y + ky) * HLO_X + kx;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const bf16_t* pl = Xl + h * XP + j * 16 + 4 * p4;
+          b[j] = tr_frag(pl, pl + HLO_X * XP);
+        }
+      };
+      load_a(0, af[0]);
+#pragma unroll
+      for (int s0 = 0; s0 < PD - 1; ++s0)
+        if (s0 < NS) load_b(s0 / TC, s0 % TC, bf[s0 % PD]);
+#pragma unroll
+      for (int sidx = 0; sidx < NS; ++sidx) {
+        const int k4 = sidx / TC, t = sidx % TC;
+        const int sn = sidx + PD - 1;
+        if (sn < NS) load_b(sn / TC, sn % TC, bf[sn % PD]);
+        if (t == 0 && k4 + 1 < 4) load_a(k4 + 1, af[(k4 + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int i = 0; i < MT; ++i)
+            acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k4 & 1][i], bf[sidx % PD][j], acc[t][i][j], 0,
+                                                                   0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+
+  // PIPE: the brick loop is instantiated per tap count (a branch inside it would merge the two multiplies'
+  // accumulator registers at every brick: copies, and 256 VGPRs with spills)
+  auto brick_loop = [&](auto tcc) __attribute__((always_inline)) {
     int buf = 0;
     if (b_begin < b_end) {
       load_into(b_begin, dr, xr, xin, xn);
@@ -3565,12 +3622,21 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
     for (long long b = b_begin; b < b_end; ++b) {
       const bool more = b + 1 < b_end;
       if (more && g.dbg != 1) load_into(b + 1, dr, xr, xin, xn);
-      if (g.dbg != 2) compute(buf);
+      if (g.dbg != 2) {
+        if constexpr (PIPE)
+          compute_pipe(buf, tcc);
+        else
+          compute(buf);
+      }
       if (more) store_from(buf ^ 1, dr, xr, xin, xn);
       __syncthreads();
       buf ^= 1;
     }
-  }
+  };
+  if (!PIPE || t_cnt == 4)
+    brick_loop(std::integral_constant<int, 4>{});
+  else
+    brick_loop(std::integral_constant<int, 3>{});
 
   static_assert(sizeof(lds) >= 16 * WEP_P * sizeof(float) && sizeof(lds) >= 512 * 8 * sizeof(float),
                 "epilogue staging must fit the stage buffers");
@@ -4185,6 +4251,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
       __syncthreads();
     }
   }
+  // PIPE: the brick loop is instantiated per tap count (a branch on t_cnt inside it merges the two multiplies'
+  // accumulator registers at every brick: copies around every MFMA group)
+  auto brick_loop = [&](auto tcc) __attribute__((always_inline)) {
   for (int b = b_begin, sc = 0; b < b_end; ++b, sc = sc + 1 == NST ? 0 : sc + 1) {
     // issue brick b + NST - 1 into the stage brick b - 1 used (every wave passed the barrier after it)
     const int sn = sc == 0 ? NST - 1 : sc - 1;
@@ -4196,14 +4265,10 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
     }
     const int sb = RING ? ring_sb(b) : 0;
     if (g.dbg != 2) {
-      if constexpr (PIPE) {
-        if (t_cnt == 4)
-          compute_pipe(st + sc * SS, sb, std::integral_constant<int, 4>{});
-        else
-          compute_pipe(st + sc * SS, sb, std::integral_constant<int, 3>{});
-      } else {
+      if constexpr (PIPE)
+        compute_pipe(st + sc * SS, sb, tcc);
+      else
         compute(st + sc * SS, sb);
-      }
     }
     // brick b + 1 has landed once at most min(NST - 2, bricks issued after it) bricks are in flight
     if constexpr (RING) {
@@ -4220,6 +4285,11 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
       }
     }
   }
+  };
+  if (!PIPE || t_cnt == 4)
+    brick_loop(std::integral_constant<int, 4>{});
+  else
+    brick_loop(std::integral_constant<int, 3>{});
 
   static_assert((RING ? sizeof(xr) : sizeof(st)) >= 16 * WEP_P * sizeof(float),
                 "epilogue staging must fit the stage ring");
@@ -5353,8 +5423,13 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
       } else {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 32) * g.ksplit);
         mmseg::note_kernel(v3 ? "wgrad_brick2_kernel<CO32,V3>" : "wgrad_brick2_kernel<CO32>");
-        if (v3 && g.nmean)
+        const bool pipe = knob("MMSEG_WGRAD_B2_PIPE", 1) != 0;
+        if (v3 && g.nmean && pipe)
+          MMSEG_LAUNCH((wgrad_brick2_kernel<T, 2, 3, true, true>), grid, dim3(512), 0, s, g);
+        else if (v3 && g.nmean)
           MMSEG_LAUNCH((wgrad_brick2_kernel<T, 2, 3, true>), grid, dim3(512), 0, s, g);
+        else if (v3 && pipe)
+          MMSEG_LAUNCH((wgrad_brick2_kernel<T, 2, 3, false, true>), grid, dim3(512), 0, s, g);
         else if (v3)
           MMSEG_LAUNCH((wgrad_brick2_kernel<T, 2, 3>), grid, dim3(512), 0, s, g);
         else

@@ -689,6 +689,56 @@ def test_wgrad_dma_fragment_partials_bitwise(dev, cin, cout, shape, accumulate, 
     assert rel(out["1"][1].double().cpu() - gb0.double().cpu(), dyr.sum(dim=(0, 2, 3, 4))) < GTOL[torch.bfloat16]
 
 
+@pytest.mark.parametrize("norm", [False, True])
+@pytest.mark.parametrize("cin,cout,shape,accumulate", [
+    (32, 32, (2, 12, 8, 24), 0), (64, 32, (2, 8, 4, 16), 1), (32, 32, (1, 8, 8, 8), 1), (32, 32, (2, 24, 24, 24), 0)])
+def test_wgrad_brick2_pipelined_bitwise(dev, cin, cout, shape, accumulate, norm, monkeypatch):
+    """The 32-co register-staged brick wgrad (the deferred-norm form is the c3 step's 96^3 32 -> 32 layers) with its
+    fragment reads software-pipelined (MMSEG_WGRAD_B2_PIPE=1, default) against the read-then-multiply form (=0):
+    every accumulator sums the same products in the same order, so weight and bias gradients are BITWISE equal;
+    and both against fp64 (the deferred norm: relu((x - mean) * rstd) of the bf16 x, rounded to bf16)."""
+    monkeypatch.setenv("MMSEG_WGRAD_DMA", "0")
+    N, D, H, W = shape
+    V = N * D * H * W
+    g = torch.Generator().manual_seed(11 * cin + cout + V + norm)
+    dy = torch.randn(V, cout, generator=g).to(dev, torch.bfloat16).reshape(-1)
+    x = (torch.randn(V, cin, generator=g) * 2 + 0.5).to(dev, torch.bfloat16).reshape(-1)
+    mean = (torch.randn(N, cin, generator=g) * 0.3 + 0.5).to(dev)
+    rstd = (torch.rand(N, cin, generator=g) + 0.5).to(dev)
+    gw0 = torch.randn(cout * cin * 27, generator=g).to(dev) if accumulate else torch.zeros(cout * cin * 27, device=dev)
+    gb0 = torch.ones(cout, device=dev) if accumulate else torch.zeros(cout, device=dev)
+    L = lib()
+    shift = int(np.log2(cin // 8))
+    if norm:
+        assert L.mmseg_conv3_wgrad_norm_ok(V, cout, cin, cin, shift, D, H, W, cout, cin, 1)
+    wsf = L.mmseg_conv3_wgrad_ws_floats(V, cout, cin, cin, shift, D, H, W, cout, cin, 1)
+    out = {}
+    for pipe in ("0", "1"):
+        monkeypatch.setenv("MMSEG_WGRAD_B2_PIPE", pipe)
+        ws = torch.full((max(wsf, 1),), float("nan"), device=dev)
+        gw, gb = gw0.clone(), gb0.clone()
+        if norm:
+            rc = L.mmseg_conv3_wgrad_norm(ptr(dy), cout, ptr(x), cin, ptr(mean), ptr(rstd), ptr(gw), ptr(gb), cout,
+                                          cin, cin, shift, V, D, H, W, ptr(ws), wsf, accumulate, 1, stream_handle())
+        else:
+            rc = L.mmseg_conv3_wgrad(ptr(dy), cout, ptr(x), cin, ptr(gw), ptr(gb), cout, cin, cin, shift, V, D, H, W,
+                                     ptr(ws), wsf, accumulate, 1, stream_handle())
+        assert rc == 0
+        assert L.mmseg_last_kernel().decode().startswith("wgrad_brick2_kernel<CO32,V3>")
+        torch.cuda.synchronize()
+        out[pipe] = (gw, gb)
+    assert torch.equal(out["0"][0], out["1"][0]) and torch.equal(out["0"][1], out["1"][1])
+    xd = x.double().cpu().reshape(N, D * H * W, cin)
+    if norm:
+        xd = torch.relu((xd - mean.double().cpu()[:, None, :]) * rstd.double().cpu()[:, None, :])
+        xd = xd.to(torch.bfloat16).double()
+    xr = xd.reshape(N, D, H, W, cin).permute(0, 4, 1, 2, 3)
+    dyr = dy.double().cpu().reshape(N, D, H, W, cout).permute(0, 4, 1, 2, 3)
+    ref = torch.nn.grad.conv3d_weight(xr, (cout, cin, 3, 3, 3), dyr, padding=1).reshape(-1)
+    assert rel(out["1"][0].double().cpu() - gw0.double().cpu(), ref) < GTOL[torch.bfloat16]
+    assert rel(out["1"][1].double().cpu() - gb0.double().cpu(), dyr.sum(dim=(0, 2, 3, 4))) < 1e-4
+
+
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("cin,cout,shape", [(384, 384, (1, 8, 8, 8)), (768, 384, (1, 8, 8, 8)), (192, 192, (1, 16, 16, 16))])
 def test_conv3_few_brick_units_take_runtime_brick(dev, dtype, cin, cout, shape, monkeypatch):

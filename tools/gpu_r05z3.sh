@@ -1,0 +1,12 @@
+# r05z3: brick loops instantiated per tap count in the pipelined wgrad kernels; wgrad kernel tests, c3 + c2 benches
+set -o pipefail
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r05z3; mkdir -p $O; cd /tmp; export TMPDIR=/tmp
+timeout -k 10 600 python3 -u -m pytest $R/tests/test_kernels_gpu.py -x -q -k "wgrad" --timeout 300 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1; rc=$?
+tail -2 $O/tests.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/tests.log | head -20; exit 1; }
+for c in c3 c2; do
+  a=""; [ $c = c2 ] && a="--model unet"
+  timeout -k 10 300 python3 $R/bench.py $a --steps 20 --warmup 5 --no-cpu-baseline --timer-steps 1 --timer-dump $O/timer_$c.json > $O/bench_$c.log 2>&1 || { tail -20 $O/bench_$c.log; exit 1; }
+  python3 -c "
+import json; d=json.loads(open('$O/bench_$c.log').read().strip().splitlines()[-1]); print('$c', d['ms_per_step'], d['value'], d['roofline']['kernel'], d['roofline']['avg_launch_ms'], d['roofline']['frac'])"
+  python3 $R/tools/timer_families.py $O/timer_$c.json 60 | grep -E "wgrad_brick2|wgrad_dma|launches"
+done
