@@ -258,6 +258,9 @@ int mmseg_wgrad_reduce_defer(const float* part, float* grad, const float* bias_p
                              int Ncols, int ksplit, int cpad, int creal, int ntap, int accumulate, void* stream);
 int mmseg_wgrad_reduce_pending(void);
 int mmseg_wgrad_reduce_discard(void* stream);
+/* phase bit 8 (with bit 1): rows [Co - 16, Co) of dy / the gradient are output-channel padding (SwinUNETR's 48 real
+ * channels in 64-row tiles): the 64-row LDS-DMA weight-gradient kernel multiplies 48 rows and writes zeros there
+ * (other kernels ignore the bit); the real rows are bitwise unchanged. */
 int mmseg_conv3_wgrad_ex(const void* dy, int lddy, const void* x, int ldx, const float* nmean, const float* nrstd,
                          float* grad, float* bias_grad, int Co, int Cip, int Ci, int cpg_shift, long long V, int D,
                          int H, int W, float* ws, long long ws_floats, int accumulate, int phase, int dtype,

@@ -2831,6 +2831,9 @@ struct WgradArgs {
   // straight to grad + gi * grad_gstride (bias_grad + gi * bias_gstride), no partials and no reduce
   long long grad_gstride;
   int bias_gstride;
+  int grad_ld;   // direct gradient row pitch (27 x real input channels; 0 = Ncols), wgrad_direct_ok
+  int pad16;   // mmseg_conv3_wgrad_ex phase bit 8: rows [Ca - 16, Ca) are output-channel padding (48 real of 64: the
+               // SwinUNETR 48-channel levels); wgrad_dma's 64-co tile then runs 3 of its 4 MFMA row tiles, zero rows
 };
 
 // the launch writes the gradient itself: one split, or one split per group of a grouped launch
@@ -3313,6 +3316,7 @@ __device__ __forceinline__ void wgrad_store_chmajor(const f32x4 (&acc)[4][MT][2]
   const bool direct = g.grad != nullptr && wgrad_direct(g);
   float* base = direct ? g.grad + (g.ksplit > 1 ? (long long)ks * g.grad_gstride : 0LL)
                        : g.part + (long long)ks * g.Ca * g.Ncols;
+  const long long ldg = direct && g.grad_ld > 0 ? g.grad_ld : g.Ncols;   // gradient row pitch (real channels)
   const bool accum = direct && g.accumulate;
   constexpr int GP = RP / 4;   // lane groups per pass
 #pragma unroll
@@ -3335,7 +3339,7 @@ __device__ __forceinline__ void wgrad_store_chmajor(const f32x4 (&acc)[4][MT][2]
       for (int e = tid; e < RP * 216; e += 512) {
         const int rr = e / 216, q = e - rr * 216;
         const float4 v = *reinterpret_cast<const float4*>(L + rr * WEP_P + q * 4);
-        float4* d = reinterpret_cast<float4*>(base + (long long)(row0 + i * 16 + hh * RP + rr) * g.Ncols + c0 * 27 +
+        float4* d = reinterpret_cast<float4*>(base + (long long)(row0 + i * 16 + hh * RP + rr) * ldg + c0 * 27 +
                                               q * 4);
         if (accum) {
           const float4 o = *d;
@@ -3888,7 +3892,9 @@ __global__ __launch_bounds__(512, 1) void conv3_brick8_kernel(GemmArgs g) {
 // six fresh slots; with NST = 3 the bricks in flight span at most 18 of the 24 slots.
 constexpr int RSLOT = 24;                 // halo plane slots
 constexpr int RPLANE_I = 4;               // DMA wave-instructions per plane slot (6 x 10 voxels x 4 chunks = 240 lanes)
-template <int MT, bool NORM = false, int NST = 3, bool PIPE = false, bool RING = false>
+// MTC < MT: only the first MTC 16-row tiles are multiplied (the rest are output-channel padding, WgradArgs::pad16);
+// staging and the epilogue keep the MT-row layout, the skipped rows' accumulators stay zero
+template <int MT, bool NORM = false, int NST = 3, bool PIPE = false, bool RING = false, int MTC = MT>
 __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
   typedef bf16_t T;
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -4149,7 +4155,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
     for (int kk = 0; kk < 128; kk += 32) {
       bf16x8 af[MT];
 #pragma unroll
-      for (int i = 0; i < MT; ++i) {
+      for (int i = 0; i < MTC; ++i) {
         const bf16_t* base = reinterpret_cast<const bf16_t*>(Db + (kk + v0) * (CO * 2) + 32 * (i ^ dsw) + 8 * p4);
         af[i] = tr_frag(base, base + 8 * CO);
       }
@@ -4165,12 +4171,12 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
             const bf16_t* pl = reinterpret_cast<const bf16_t*>(row + 32 * (j ^ xs) + 8 * p4);
             const bf16x8 bfr = tr_frag(pl, pl + HLO_X * CK);
 #pragma unroll
-            for (int i = 0; i < MT; ++i)
+            for (int i = 0; i < MTC; ++i)
               acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[t][i][j], 0, 0, 0);
           }
         } else if (t == 3 && bias_wave) {
 #pragma unroll
-          for (int i = 0; i < MT; ++i)
+          for (int i = 0; i < MTC; ++i)
             acc[3][i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, acc[3][i][0], 0, 0, 0);
         }
       }
@@ -4185,7 +4191,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
     bf16x8 af[2][MT], bf[PD][2];
     auto load_a = [&](int kk, bf16x8(&a)[MT]) __attribute__((always_inline)) {
 #pragma unroll
-      for (int i = 0; i < MT; ++i) {
+      for (int i = 0; i < MTC; ++i) {
         const bf16_t* base = reinterpret_cast<const bf16_t*>(Db + (kk + v0) * (CO * 2) + 32 * (i ^ dsw) + 8 * p4);
         a[i] = tr_frag(base, base + 8 * CO);
       }
@@ -4217,12 +4223,12 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int i = 0; i < MT; ++i)
+        for (int i = 0; i < MTC; ++i)
           acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k4 & 1][i], bf[sidx % PD][j], acc[t][i][j], 0, 0,
                                                                  0);
       if (TC == 3 && t == 2 && bias_wave) {
 #pragma unroll
-        for (int i = 0; i < MT; ++i)
+        for (int i = 0; i < MTC; ++i)
           acc[3][i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k4 & 1][i], ones, acc[3][i][0], 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -4579,6 +4585,7 @@ struct WReduceArgs {
   // counts one group's splits), written to grad + gi * grad_gstride / bias_grad + gi * bias_gstride
   long long grad_gstride;
   int bias_gstride;
+  int vec4;           // host-set (wred_vec4): channel-major sums as 16-B stores
 };
 
 // 256 threads = (256/S) float4 columns x S split slices: slice s sums splits
@@ -4644,6 +4651,21 @@ __device__ __forceinline__ void wred_body(WReduceArgs g, const int S, const int 
       __syncthreads();
     }
     if (sl != 0) return;
+  }
+  // channel-major partials: the four sums are four consecutive gradient floats (col = c ntap + tap and the torch
+  // offset (row creal + c) ntap + tap differ by row (Ncols - creal ntap), a multiple of 4, and the real-channel
+  // boundary col = creal ntap is one too) -- one 16-B store instead of four 4-B ones
+  if (g.vec4 && e0 < total && g.frag_mt == 0 && g.chmajor) {
+    const long long row = e0 / g.Ncols;
+    const long long col = e0 - row * g.Ncols;
+    if (col >= (long long)g.creal * g.ntap) return;   // channel padding: dropped
+    float4* d = reinterpret_cast<float4*>(g.grad + row * ((long long)g.creal * g.ntap) + col);
+    if (g.accumulate) {
+      const float4 o = *d;
+      v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+    }
+    *d = v;
+    return;
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -5290,7 +5312,15 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     if (g.ksplit > 1) return launch_splitk_reduce<T, MODE>(g, s);
     return 0;
   }
-  if (!Cbig) {
+  if (MODE == MODE_POINT && g.Ncols % 96 == 0 && g.Ncols % 64 != 0 && knob("MMSEG_POINT_BN96", 1)) {
+    // BM=128, BN=96: the 96 / 288 / 480-column 1x1 GEMMs (SwinUNETR's 96-channel stage, the 96 -> 48 residual
+    // conv's data gradient) in whole tiles -- BN=64 left a half-empty last column tile that re-read every A row
+    if constexpr (MODE == MODE_POINT) {
+      mmseg::note_kernel("conv_gemm_kernel<point,128x96>");
+      dim3 grid(ceil_div(g.M, 128) * (g.Ncols / 96) * g.ksplit);
+      MMSEG_LAUNCH((conv_gemm_kernel<T, MODE, 2, 2, 4, 3>), grid, block, 0, s, g);
+    }
+  } else if (!Cbig) {
     // BM=128, BN=32
     static const char* nm[4] = {"conv_gemm_kernel<conv3,128x32>", "conv_gemm_kernel<point,128x32>",
                                 "conv_gemm_kernel<convT_fwd,128x32>", "conv_gemm_kernel<convT_dgrad,128x32>"};
@@ -5384,7 +5414,12 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
         const bool ring = !norm && !st4 && knob("MMSEG_WGRAD_RING", 0) != 0;
         if (mt == 4) {
           mmseg::note_kernel("wgrad_dma_kernel<CO64>");
-          if (norm)
+          const bool p16 = g.pad16 && !norm && !ring && !st4 && g.Ca == 64 && knob("MMSEG_WGRAD_PAD16", 1);
+          if (p16 && knob("MMSEG_WGRAD_PAD16_PIPE", 1))   // 48 rows leave room for the pipelined multiply
+            MMSEG_LAUNCH((wgrad_dma_kernel<4, false, 3, true, false, 3>), grid, dim3(512), 0, s, g);
+          else if (p16)
+            MMSEG_LAUNCH((wgrad_dma_kernel<4, false, 3, false, false, 3>), grid, dim3(512), 0, s, g);
+          else if (norm)
             MMSEG_LAUNCH((wgrad_dma_kernel<4, true>), grid, dim3(512), 0, s, g);
           else if (ring)
             MMSEG_LAUNCH((wgrad_dma_kernel<4, false, 3, false, true>), grid, dim3(512), 0, s, g);
@@ -5537,6 +5572,14 @@ int mmseg_wgrad_splits_impl(long long V, int ksplit) {
 // split reduction never reads the skipped columns' partials into the gradient).
 int wgrad_kchunks(int Cip, int Ci) { return (Ci < Cip && knob("MMSEG_KCHUNKS", 1)) ? (Ci + 31) / 32 : 0; }
 
+// A single-split brick weight gradient writes the torch-layout gradient [co][ci][27] itself when its input
+// channels are unpadded, or padded past whole real 32-channel chunks (Ci % 32 == 0: SwinUNETR's 768 of 1024): the
+// kernel computes only the real chunks (wgrad_kchunks), whose rows then land at pitch 27 Ci (WgradArgs::grad_ld)
+// -- no partial, no relayout reduce (MMSEG_WGRAD_PDIRECT=0: through the partial as before).
+bool wgrad_direct_ok(int Cip, int Ci) {
+  return Ci == Cip || (Ci % 32 == 0 && wgrad_kchunks(Cip, Ci) == Ci / 32 && knob("MMSEG_WGRAD_PDIRECT", 1));
+}
+
 // CONV3 weight-gradient plan (mmseg_conv3_wgrad): kernel kind (wgrad_brick_ok), split count, whether the
 // kernel writes the torch-layout gradient itself (brick2 / brickr, one split, unpadded input channels),
 // and the workspace (floats) of the split partials + bias partials otherwise.
@@ -5566,7 +5609,7 @@ Conv3WgradPlan plan_conv3_wgrad(long long V, int Co, int Cip, int Ci, int cpg_sh
     if (want < 1) want = 1;
     p.ksplit = mmseg_wgrad_splits_impl(V, (int)want);
   }
-  p.direct = p.kind >= 2 && p.ksplit == 1 && Ci == Cip;
+  p.direct = p.kind >= 2 && p.ksplit == 1 && wgrad_direct_ok(Cip, Ci);
   p.ws = p.direct ? 0 : p.ksplit * per_split;
   return p;
 }
@@ -6220,7 +6263,8 @@ int mmseg_conv3_wgrad_ex(const void* dy, int lddy, const void* x, int ldx, const
                          float* grad, float* bias_grad, int Co, int Cip, int Ci, int cpg_shift, long long V, int D,
                          int H, int W, float* ws, long long ws_floats, int accumulate, int phase, int dtype,
                          void* stream) {
-  MMSEG_REQUIRE(phase >= 1 && phase <= 7 && (phase & 3), "conv3_wgrad_ex: phase %d: bits 1 | 2 (| 4 defer)", phase);
+  MMSEG_REQUIRE(phase >= 1 && phase <= 15 && (phase & 3) && (!(phase & 8) || (Co >= 16 && Co % 16 == 0)),
+                "conv3_wgrad_ex: phase %d: bits 1 | 2 (| 4 defer, | 8 last 16 rows padding)", phase);
   MMSEG_REQUIRE(!nmean || (nrstd && mmseg_conv3_wgrad_norm_ok(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype)),
                 "conv3_wgrad_ex: unsupported shape for the deferred norm (mmseg_conv3_wgrad_norm_ok)");
   return conv3_wgrad_impl(dy, lddy, x, ldx, nmean, nrstd, grad, bias_grad, Co, Cip, Ci, cpg_shift, V, D, H, W, ws,
@@ -6260,6 +6304,11 @@ int mmseg_wgrad_reduce_flush(void* stream) {
       blk += b.nbx[k] * e.groups;
     }
     b.blk0[b.n] = blk;
+    if (knob("MMSEG_WRED_LOG", 0))   // diagnostics: what each batched launch sums
+      for (int k = 0; k < b.n; ++k)
+        fprintf(stderr, "wred_batch %zu.%d: Ca %d Ncols %d ksplit %d groups %d S %d MB %.1f\n", i0, k, b.d[k].Ca,
+                b.d[k].Ncols, b.d[k].ksplit, mine[i0 + k].groups, b.S[k],
+                4.0 * b.d[k].ksplit * mine[i0 + k].groups * b.d[k].Ca * b.d[k].Ncols / 1048576.0);
     mmseg::note_kernel("wgrad_reduce_batch_kernel");
     MMSEG_LAUNCH(wgrad_reduce_batch_kernel, dim3(blk), dim3(256), 0, (hipStream_t)stream, b);
     if (mmseg::check_launch("wgrad_reduce_batch")) return -1;
@@ -6309,6 +6358,8 @@ int conv3_wgrad_impl(const void* dy, int lddy, const void* x, int ldx, const flo
   g.groups = groups > 1 ? groups : 0;
   g.grad_gstride = grad_gstride;
   g.bias_gstride = bias_gstride;
+  g.pad16 = (phase & 8) ? 1 : 0;
+  g.grad_ld = p.direct ? 27 * Ci : 0;
   if (phase & 1) {
     const int rc = dtype == MMSEG_BF16 ? launch_wgrad<bf16_t, MODE_CONV3>(g, s) : launch_wgrad<float, MODE_CONV3>(g, s);
     if (rc) return rc;
@@ -6317,6 +6368,8 @@ int conv3_wgrad_impl(const void* dy, int lddy, const void* x, int ldx, const flo
   const int ng = groups > 1 ? groups : 1;
   WReduceArgs r{part, grad, bpart, bias_grad, Co, ncols, p.ksplit / ng, Cip, Ci, 27, accumulate, p.kind >= 2 ? 1 : 0,
                 fmt, wgrad_nchunk(cpg_shift, g.kchunks), grad_gstride, bias_gstride};
+  r.vec4 = knob("MMSEG_WRED_V4", 1) && r.chmajor && !r.frag_mt && ((uintptr_t)grad & 15) == 0 &&
+           (ng == 1 || grad_gstride % 4 == 0) && r.Ncols % 4 == 0 && ((long long)r.creal * r.ntap) % 4 == 0;
   if (phase & 4) {   // deferred: summed by the next mmseg_wgrad_reduce_flush on this stream
     return wred_push(r, ng, stream);
   }

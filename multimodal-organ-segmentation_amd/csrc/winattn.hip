@@ -43,7 +43,13 @@ struct WinAttnArgs {
   int B, N, C, heads, hd, nw, T, ldn;
   int w0, w1, w2;        // the module's full window
   float scale;
+  int swz;               // XCD-aware block order (MMSEG_WINATTN_SWZ, default on): a window's heads / query groups,
+                         // which stage the same qkv rows (a head's 32-B slice of each), run on one XCD and share its L2
 };
+
+__device__ __forceinline__ int wa_block(const WinAttnArgs& a) {
+  return a.swz ? xcd_swizzle((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+}
 
 __device__ __forceinline__ s4 ld4(const bf16_t* p) { return *reinterpret_cast<const s4*>(p); }
 
@@ -193,7 +199,7 @@ __global__ __launch_bounds__(512) void winattn_fwd_kernel(WinAttnArgs a) {
   __shared__ float tab[TMAX];
   __shared__ __attribute__((aligned(16))) int code[NPMAX];
   __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
-  const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads;
+  const int bh = wa_block(a), b = bh / a.heads, h = bh % a.heads;
   const int np = (a.N + 15) & ~15, nt = np / 16;
   const Stage st{b, h, a.N, np};
   const int C3 = 3 * a.C, hoff = h * a.hd;
@@ -288,7 +294,7 @@ __global__ __launch_bounds__(512) void winattn_fwd1_kernel(WinAttnArgs a) {
   __shared__ float tab[TMAX];
   __shared__ __attribute__((aligned(16))) int code[NPMAX];
   __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
-  const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads;
+  const int bh = wa_block(a), b = bh / a.heads, h = bh % a.heads;
   const int np = (a.N + 15) & ~15, nt = np / 16;
   const Stage st{b, h, a.N, np};
   const int C3 = 3 * a.C, hoff = h * a.hd;
@@ -424,7 +430,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_kv_kernel(WinAttnArgs a) {
   __shared__ __attribute__((aligned(16))) float Dq[NPMAX];
   __shared__ __attribute__((aligned(16))) int code[NPMAX];
   __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
-  const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads;
+  const int bh = wa_block(a), b = bh / a.heads, h = bh % a.heads;
   const int np = (a.N + 15) & ~15, nt = np / 16;
   const Stage st{b, h, a.N, np};
   const int C3 = 3 * a.C, hoff = h * a.hd;
@@ -492,7 +498,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_q_kernel(WinAttnArgs a) {
   __shared__ __attribute__((aligned(16))) float Dq[NPMAX];
   __shared__ __attribute__((aligned(16))) int code[NPMAX];
   __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
-  const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads;
+  const int bh = wa_block(a), b = bh / a.heads, h = bh % a.heads;
   const int np = (a.N + 15) & ~15, nt = np / 16;
   const Stage st{b, h, a.N, np};
   const int C3 = 3 * a.C, hoff = h * a.hd;
@@ -572,7 +578,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_qb_kernel(WinAttnArgs a, int 
   __shared__ float Dq[QB_TILES * 16];
   __shared__ __attribute__((aligned(16))) int code[NPMAX];
   __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
-  const int qg = blockIdx.x % nqg, h = (blockIdx.x / nqg) % a.heads, wg = blockIdx.x / (nqg * a.heads);
+  const int blk = wa_block(a), qg = blk % nqg, h = (blk / nqg) % a.heads, wg = blk / (nqg * a.heads);
   const int np = (a.N + 15) & ~15, nt = np / 16;
   const int q0 = qg * QB_TILES * 16;
   const int C3 = 3 * a.C, hoff = h * a.hd;
@@ -694,7 +700,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_kv2_kernel(WinAttnArgs a) {
   __shared__ __attribute__((aligned(16))) float Dq[NPMAX];
   __shared__ __attribute__((aligned(16))) int code[NPMAX];
   __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
-  const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads;
+  const int bh = wa_block(a), b = bh / a.heads, h = bh % a.heads;
   const int np = (a.N + 15) & ~15, nt = np / 16;
   const Stage st{b, h, a.N, np};
   const int C3 = 3 * a.C, hoff = h * a.hd;
@@ -784,7 +790,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_qb2_kernel(WinAttnArgs a, int
   __shared__ float Dq[QB_TILES * 16];
   __shared__ __attribute__((aligned(16))) int code[NPMAX];
   __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
-  const int qg = blockIdx.x % nqg, h = (blockIdx.x / nqg) % a.heads, wg = blockIdx.x / (nqg * a.heads);
+  const int blk = wa_block(a), qg = blk % nqg, h = (blk / nqg) % a.heads, wg = blk / (nqg * a.heads);
   const int np = (a.N + 15) & ~15, nt = np / 16;
   const int q0 = qg * QB_TILES * 16;
   const int C3 = 3 * a.C, hoff = h * a.hd;
@@ -917,7 +923,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_q2_kernel(WinAttnArgs a) {
   __shared__ __attribute__((aligned(16))) float Dq[NPMAX];
   __shared__ __attribute__((aligned(16))) int code[NPMAX];
   __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
-  const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads;
+  const int bh = wa_block(a), b = bh / a.heads, h = bh % a.heads;
   const int np = (a.N + 15) & ~15, nt = np / 16;
   const Stage st{b, h, a.N, np};
   const int C3 = 3 * a.C, hoff = h * a.hd;
@@ -1032,6 +1038,7 @@ int mmseg_winattn_fwd(const void* qkv, int B, int N, int C, int heads, const flo
                       int w2, const uint8_t* region, int nw, float scale, void* O, float* lse, void* stream) {
   WinAttnArgs a{(const bf16_t*)qkv, nullptr, nullptr, (bf16_t*)O, lse, nullptr, table, region,
                 B, N, C, heads, C / heads, nw, T, 0, w0, w1, w2, scale};
+  a.swz = knob_i("MMSEG_WINATTN_SWZ", 1);
   if (check_args(a)) return 1;
   if (knob_i("MMSEG_WINATTN_FWD1", 1)) {
     mmseg::note_kernel("winattn_fwd1_kernel");
@@ -1048,6 +1055,7 @@ int mmseg_winattn_bwd(const void* qkv, const void* O, const void* dO, const floa
                       void* dqkv, void* dS, int ldn, void* stream) {
   WinAttnArgs a{(const bf16_t*)qkv, (const bf16_t*)O, (const bf16_t*)dO, (bf16_t*)dqkv, const_cast<float*>(lse),
                 (bf16_t*)dS, table, region, B, N, C, heads, C / heads, nw, T, ldn, w0, w1, w2, scale};
+  a.swz = knob_i("MMSEG_WINATTN_SWZ", 1);
   if (check_args(a)) return 1;
   MMSEG_REQUIRE(ldn >= N && ldn % 8 == 0, "winattn_bwd: ldn >= N, multiple of 8");
   hipStream_t s = (hipStream_t)stream;
@@ -1075,6 +1083,7 @@ int mmseg_winattn_bwd_sum(const void* qkv, const void* O, const void* dO, const 
                           float scale, void* dqkv, float* dsum, int ldn, void* stream) {
   WinAttnArgs a{(const bf16_t*)qkv, (const bf16_t*)O, (const bf16_t*)dO, (bf16_t*)dqkv, const_cast<float*>(lse),
                 nullptr, table, region, B, N, C, heads, C / heads, nw, T, ldn, w0, w1, w2, scale};
+  a.swz = knob_i("MMSEG_WINATTN_SWZ", 1);
   if (check_args(a)) return 1;
   MMSEG_REQUIRE(ldn >= N && ldn % 8 == 0 && mmseg_winattn_sum_groups(B, N, heads) > 0,
                 "winattn_bwd_sum: ldn >= N (multiple of 8) and enough windows (mmseg_winattn_sum_groups)");

@@ -396,10 +396,14 @@ class Conv3:
                 self.cpg_shift, V, x.D, x.H, x.W, ptr(ws), wsf, int(accumulate) if self.wg_stage is None else 0)
         # the kernel and its split reduce are timed separately (the roofline family is the kernel alone, as in
         # the rocprofv3 trace)
+        # the staged gradient's last 16 rows are output-channel padding (48 of 64): the 64-row kernel skips them
+        pad16 = 8 if (self.wg_stage is not None and rows - self.Co == 16
+                      and os.environ.get("MMSEG_WGRAD_PAD16", "1") != "0") else 0
+
         def wkernel(s1):
             with TIMER.region(_gemm_name(self.rt, 0, "conv3"), flops=2.0 * V * self.Co * 27 * self.Ci,
                               nbytes=_io_bytes(self.rt, V, self.Cip, self.Co, 27 * self.Cip * self.Co, 4)):
-                L.mmseg_conv3_wgrad_ex(*args, 1, code, s1)
+                L.mmseg_conv3_wgrad_ex(*args, 1 | pad16, code, s1)
 
         # weight gradient (kernel + reduce) beside the data gradient (MMSEG_WD_CONC): both only read dy, so when dx
         # does not overwrite x the two MFMA launches can share the chip -- the tail of one (a partial last round of

@@ -739,6 +739,126 @@ def test_wgrad_brick2_pipelined_bitwise(dev, cin, cout, shape, accumulate, norm,
     assert rel(out["1"][1].double().cpu() - gb0.double().cpu(), dyr.sum(dim=(0, 2, 3, 4))) < 1e-4
 
 
+@pytest.mark.parametrize("cip,ci,cout,shape,accumulate", [
+    (32, 32, 32, (2, 12, 8, 24), 0), (64, 48, 64, (1, 8, 8, 16), 1), (128, 96, 64, (1, 12, 12, 12), 0),
+    (64, 64, 128, (2, 12, 12, 12), 1), (1024, 768, 64, (1, 8, 8, 8), 0)])
+def test_wgrad_reduce_vec4_bitwise(dev, cip, ci, cout, shape, accumulate, monkeypatch):
+    """The split reduce of channel-major weight-gradient partials (brick2 / runtime-brick kernels) storing each
+    thread's four sums as one 16-B store (MMSEG_WRED_V4=1, default) against four 4-B stores (=0): the same sums to
+    the same torch offsets, padded input channels (ci < cip) dropped -- weight and bias gradients BITWISE equal; and
+    against fp64."""
+    monkeypatch.setenv("MMSEG_WGRAD_DMA", "0")
+    N, D, H, W = shape
+    V = N * D * H * W
+    g = torch.Generator().manual_seed(cip + ci + cout + V)
+    dy = torch.randn(V, cout, generator=g).to(dev, torch.bfloat16).reshape(-1)
+    x = torch.randn(V, cip, generator=g)
+    x[:, ci:] = 0
+    x = x.to(dev, torch.bfloat16).reshape(-1)
+    gw0 = torch.randn(cout * ci * 27, generator=g).to(dev) if accumulate else torch.zeros(cout * ci * 27, device=dev)
+    gb0 = torch.ones(cout, device=dev) if accumulate else torch.zeros(cout, device=dev)
+    L = lib()
+    shift = int(np.log2(cip // 8))
+    wsf = L.mmseg_conv3_wgrad_ws_floats(V, cout, cip, ci, shift, D, H, W, cout, cip, 1)
+    assert wsf > 0, "a direct single-split gradient has no reduce"
+    out = {}
+    for v4 in ("0", "1"):
+        monkeypatch.setenv("MMSEG_WRED_V4", v4)
+        ws = torch.full((wsf,), float("nan"), device=dev)
+        gw, gb = gw0.clone(), gb0.clone()
+        assert L.mmseg_conv3_wgrad(ptr(dy), cout, ptr(x), cip, ptr(gw), ptr(gb), cout, cip, ci, shift, V, D, H, W,
+                                   ptr(ws), wsf, accumulate, 1, stream_handle()) == 0
+        assert not L.mmseg_last_kernel().decode().startswith("wgrad_dma")
+        torch.cuda.synchronize()
+        out[v4] = (gw, gb)
+    assert torch.equal(out["0"][0], out["1"][0]) and torch.equal(out["0"][1], out["1"][1])
+    xr = x.double().cpu().reshape(N, D, H, W, cip)[..., :ci].permute(0, 4, 1, 2, 3)
+    dyr = dy.double().cpu().reshape(N, D, H, W, cout).permute(0, 4, 1, 2, 3)
+    ref = torch.nn.grad.conv3d_weight(xr, (cout, ci, 3, 3, 3), dyr, padding=1).reshape(-1)
+    assert rel(out["1"][0].double().cpu() - gw0.double().cpu(), ref) < GTOL[torch.bfloat16]
+    assert rel(out["1"][1].double().cpu() - gb0.double().cpu(), dyr.sum(dim=(0, 2, 3, 4))) < GTOL[torch.bfloat16]
+
+
+@pytest.mark.parametrize("cip,ci,cout,shape,accumulate", [
+    (1024, 768, 64, (1, 4, 4, 4), 0), (1024, 768, 384, (1, 8, 8, 8), 1), (128, 96, 64, (1, 4, 4, 8), 1),
+    (64, 32, 64, (1, 4, 4, 8), 0)])
+def test_wgrad_direct_chunk_padded_bitwise(dev, cip, ci, cout, shape, accumulate, monkeypatch):
+    """A single-split brick weight gradient over chunk-padded input channels (ci % 32 == 0 < cip: SwinUNETR's 768 of
+    1024) writes the torch-layout gradient itself at row pitch 27 ci (MMSEG_WGRAD_PDIRECT=1, default: no workspace)
+    instead of a partial + relayout reduce (=0): BITWISE the same weight and bias gradients; and against fp64."""
+    N, D, H, W = shape
+    V = N * D * H * W
+    g = torch.Generator().manual_seed(cip + ci + cout + V)
+    dy = torch.randn(V, cout, generator=g).to(dev, torch.bfloat16).reshape(-1)
+    x = torch.randn(V, cip, generator=g)
+    x[:, ci:] = 0
+    x = x.to(dev, torch.bfloat16).reshape(-1)
+    gw0 = torch.randn(cout * ci * 27, generator=g).to(dev) if accumulate else torch.zeros(cout * ci * 27, device=dev)
+    gb0 = torch.ones(cout, device=dev) if accumulate else torch.zeros(cout, device=dev)
+    L = lib()
+    shift = int(np.log2(cip // 8))
+    out = {}
+    for pd in ("0", "1"):
+        monkeypatch.setenv("MMSEG_WGRAD_PDIRECT", pd)
+        wsf = L.mmseg_conv3_wgrad_ws_floats(V, cout, cip, ci, shift, D, H, W, cout, cip, 1)
+        assert (wsf == 0) == (pd == "1")
+        ws = torch.full((max(wsf, 1),), float("nan"), device=dev)
+        gw, gb = gw0.clone(), gb0.clone()
+        assert L.mmseg_conv3_wgrad(ptr(dy), cout, ptr(x), cip, ptr(gw), ptr(gb), cout, cip, ci, shift, V, D, H, W,
+                                   ptr(ws) if wsf else None, wsf, accumulate, 1, stream_handle()) == 0
+        torch.cuda.synchronize()
+        out[pd] = (gw, gb)
+    assert torch.equal(out["0"][0], out["1"][0]) and torch.equal(out["0"][1], out["1"][1])
+    xr = x.double().cpu().reshape(N, D, H, W, cip)[..., :ci].permute(0, 4, 1, 2, 3)
+    dyr = dy.double().cpu().reshape(N, D, H, W, cout).permute(0, 4, 1, 2, 3)
+    ref = torch.nn.grad.conv3d_weight(xr, (cout, ci, 3, 3, 3), dyr, padding=1).reshape(-1)
+    assert rel(out["1"][0].double().cpu() - gw0.double().cpu(), ref) < GTOL[torch.bfloat16]
+    assert rel(out["1"][1].double().cpu() - gb0.double().cpu(), dyr.sum(dim=(0, 2, 3, 4))) < GTOL[torch.bfloat16]
+
+
+@pytest.mark.parametrize("pipe", ["0", "1"])
+@pytest.mark.parametrize("cip,ci,shape,accumulate", [
+    (64, 48, (1, 16, 16, 16), 0), (128, 96, (1, 8, 16, 16), 1), (64, 48, (2, 8, 8, 16), 1), (64, 64, (1, 12, 8, 24), 0)])
+def test_wgrad_pad16_rows_bitwise(dev, cip, ci, shape, accumulate, pipe, monkeypatch):
+    """mmseg_conv3_wgrad_ex phase bit 8 (SwinUNETR's 48 real output channels in 64-row tiles): the LDS-DMA kernel
+    multiplies 3 of its 4 row tiles (MMSEG_WGRAD_PAD16_PIPE: with / without the pipelined multiply).  Rows 0..47 of
+    the weight and bias gradients are BITWISE those of the full 64-row launch; rows 48..63 receive zeros."""
+    monkeypatch.setenv("MMSEG_WGRAD_PAD16_PIPE", pipe)
+    N, D, H, W = shape
+    V = N * D * H * W
+    co = 64
+    g = torch.Generator().manual_seed(cip + ci + V + accumulate)
+    dy = torch.randn(V, co, generator=g)
+    dy[:, 48:] = 0
+    dy = dy.to(dev, torch.bfloat16).reshape(-1)
+    x = torch.randn(V, cip, generator=g)
+    x[:, ci:] = 0
+    x = x.to(dev, torch.bfloat16).reshape(-1)
+    gw0 = torch.randn(co * ci * 27, generator=g).to(dev) if accumulate else torch.zeros(co * ci * 27, device=dev)
+    gb0 = torch.ones(co, device=dev) if accumulate else torch.zeros(co, device=dev)
+    L = lib()
+    shift = int(np.log2(cip // 8))
+    wsf = L.mmseg_conv3_wgrad_ws_floats(V, co, cip, ci, shift, D, H, W, co, cip, 1)
+    out = {}
+    for phase in (3, 11):
+        ws = torch.full((max(wsf, 1),), float("nan"), device=dev)
+        gw, gb = gw0.clone(), gb0.clone()
+        args = (ptr(dy), co, ptr(x), cip, None, None, ptr(gw), ptr(gb), co, cip, ci, shift, V, D, H, W, ptr(ws), wsf,
+                accumulate)
+        assert L.mmseg_conv3_wgrad_ex(*args, phase & ~2, 1, stream_handle()) == 0   # the kernel
+        assert L.mmseg_last_kernel().decode() == "wgrad_dma_kernel<CO64>"
+        assert L.mmseg_conv3_wgrad_ex(*args, 2, 1, stream_handle()) == 0            # its split reduce
+        torch.cuda.synchronize()
+        out[phase] = (gw.view(co, -1), gb)
+    r = 48
+    assert torch.equal(out[3][0][:r], out[11][0][:r]) and torch.equal(out[3][1][:r], out[11][1][:r])
+    assert torch.equal(out[11][0][r:], gw0.view(co, -1)[r:]) and torch.equal(out[11][1][r:], gb0[r:])
+    xr = x.double().cpu().reshape(N, D, H, W, cip)[..., :ci].permute(0, 4, 1, 2, 3)
+    dyr = dy.double().cpu().reshape(N, D, H, W, co).permute(0, 4, 1, 2, 3)
+    ref = torch.nn.grad.conv3d_weight(xr, (co, ci, 3, 3, 3), dyr, padding=1).reshape(co, -1)
+    assert rel(out[11][0][:r].double().cpu() - gw0.view(co, -1)[:r].double().cpu(), ref[:r]) < GTOL[torch.bfloat16]
+
+
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("cin,cout,shape", [(384, 384, (1, 8, 8, 8)), (768, 384, (1, 8, 8, 8)), (192, 192, (1, 16, 16, 16))])
 def test_conv3_few_brick_units_take_runtime_brick(dev, dtype, cin, cout, shape, monkeypatch):

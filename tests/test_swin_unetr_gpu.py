@@ -279,6 +279,52 @@ def test_lrelu_bwd_in_part_bitwise(dev, dtype, C, ld, has_b):
         assert torch.equal(d, want)
 
 
+@pytest.mark.parametrize("Co,Ci,M", [(96, 48, 3000), (288, 96, 2000), (96, 384, 1000), (96, 96, 70000)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_point_gemm_96_column_tile_bitwise(dev, dtype, Co, Ci, M, monkeypatch):
+    """96 / 288-column 1x1 GEMMs on the 128x96 tile (MMSEG_POINT_BN96=1, default) against the 128x64 tile (=0):
+    every output sums the same K products in the same order, so the forward (plain, residual and GELU epilogues)
+    and the data gradient (into 96 columns, plain and dx +=) are BITWISE equal; and against fp64."""
+    from mmseg_amd.engine.runtime import FlatParams, Runtime
+    from mmseg_amd.engine.swin import Lin
+    torch.manual_seed(Co + Ci)
+    rt = Runtime(dev, dtype)
+    lin = torch.nn.Linear(Ci, Co).to(dev)
+    flat = FlatParams(list(lin.parameters()))
+    L = Lin(rt, lin.weight, lin.bias, flat)
+    for d in L.descs():
+        lib().mmseg_pack_weight(*d, rt.code, rt.stream)
+    x = torch.randn(M * Ci, device=dev).to(dtype)
+    res = torch.randn(M * Co, device=dev).to(dtype)
+    dy = torch.randn(M * Co, device=dev).to(dtype)
+    dx0 = torch.randn(M * Ci, device=dev).to(dtype)
+    outs = {}
+    for bn in ("1", "0"):
+        monkeypatch.setenv("MMSEG_POINT_BN96", bn)
+        y = torch.full((M * Co,), float("nan"), device=dev, dtype=dtype)
+        L.fwd(x, Ci, M, y, Co)
+        if bn == "1" and Co % 64:
+            assert lib().mmseg_last_kernel().decode() == "conv_gemm_kernel<point,128x96>"
+        yr = torch.full((M * Co,), float("nan"), device=dev, dtype=dtype)
+        L.fwd(x, Ci, M, yr, Co, res=res)
+        h = torch.full((M * Co,), float("nan"), device=dev, dtype=dtype)
+        gl = torch.full((M * Co,), float("nan"), device=dev, dtype=dtype)
+        L.fwd_gelu(x, Ci, M, h, gl)
+        dx = torch.full((M * Ci,), float("nan"), device=dev, dtype=dtype)
+        L.bwd(x, Ci, dy, Co, M, dx, Ci, False)
+        dxa = dx0.clone()
+        if L.dgrad_splits(M) == 1:
+            L.bwd(x, Ci, dy, Co, M, dxa, Ci, False, dx_add=True)
+        torch.cuda.synchronize()
+        outs[bn] = (y, yr, h, gl, dx, dxa)
+    for a, b in zip(outs["1"], outs["0"]):
+        assert torch.equal(a, b)
+    ref = x.view(M, Ci).double() @ lin.weight.double().t() + lin.bias.double()
+    assert rel(outs["1"][0].view(M, Co), ref) < (1e-5 if dtype == torch.float32 else 1e-2)
+    refd = dy.view(M, Co).double() @ lin.weight.double()
+    assert rel(outs["1"][4].view(M, Ci), refd) < (1e-5 if dtype == torch.float32 else 1e-2)
+
+
 @pytest.mark.parametrize("Co,Ci,M", [(48, 192, 3000), (96, 64, 5000), (384, 1536, 700)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_point_gemm_residual_epilogue_bitwise(dev, dtype, Co, Ci, M, monkeypatch):
