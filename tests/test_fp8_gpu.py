@@ -28,6 +28,14 @@ from tests.test_model_gpu import make_config
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _brick2_small_volumes(monkeypatch):
+    """The e4m3 forward is a brick2-family kernel; these small test volumes would otherwise fall under
+    MMSEG_BRICK2_MINUNITS and take the runtime-brick kernel, which has no fp8 form (the 96^3 layers fp8 serves
+    are far above it)."""
+    monkeypatch.setenv("MMSEG_BRICK2_MINUNITS", "0")
+
+
 def _e4m3(t):
     return t.float().to(torch.float8_e4m3fn).double()
 
