@@ -47,6 +47,14 @@ struct WinAttnArgs {
                          // which stage the same qkv rows (a head's 32-B slice of each), run on one XCD and share its L2
 };
 
+// windows of 337..352 tokens (MONAI's 7^3 = 343) take the FULL instantiations: the key-tile loops run to a
+// compile-time 22, so the per-tile `kt < nt` guards and their selects around every score update disappear
+// (MMSEG_WINATTN_FULL=0: the runtime-bound forms)
+int knob_i(const char* name, int dflt);
+inline bool wa_full(const WinAttnArgs& a) {
+  return ((a.N + 15) & ~15) == NPMAX && knob_i("MMSEG_WINATTN_FULL", 1) != 0;
+}
+
 __device__ __forceinline__ int wa_block(const WinAttnArgs& a) {
   return a.swz ? xcd_swizzle((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
 }
@@ -287,6 +295,7 @@ __device__ __forceinline__ bf16x8 cat44(s4 a, s4 b) {
   return __builtin_bit_cast(bf16x8, t);
 }
 
+template <bool FULL>
 __global__ __launch_bounds__(512) void winattn_fwd1_kernel(WinAttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Qs[NPMAX][16];
   __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
@@ -295,7 +304,7 @@ __global__ __launch_bounds__(512) void winattn_fwd1_kernel(WinAttnArgs a) {
   __shared__ __attribute__((aligned(16))) int code[NPMAX];
   __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
   const int bh = wa_block(a), b = bh / a.heads, h = bh % a.heads;
-  const int np = (a.N + 15) & ~15, nt = np / 16;
+  const int np = FULL ? NPMAX : (a.N + 15) & ~15, nt = FULL ? NTMAX : np / 16;   // FULL: 22 key tiles, compile-time
   const Stage st{b, h, a.N, np};
   const int C3 = 3 * a.C, hoff = h * a.hd;
   stage_rows(Qs, a.qkv, C3, hoff, st, a.hd, nullptr);
@@ -688,6 +697,7 @@ __device__ __forceinline__ f32x4 mma32(s4 a0, s4 a1, s4 b0, s4 b1, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat44(a0, a1), cat44(b0, b1), c, 0, 0, 0);
 }
 
+template <bool FULL>
 __global__ __launch_bounds__(512) void winattn_bwd_kv2_kernel(WinAttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Qs[NPMAX][16];
   __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
@@ -701,7 +711,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_kv2_kernel(WinAttnArgs a) {
   __shared__ __attribute__((aligned(16))) int code[NPMAX];
   __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
   const int bh = wa_block(a), b = bh / a.heads, h = bh % a.heads;
-  const int np = (a.N + 15) & ~15, nt = np / 16;
+  const int np = FULL ? NPMAX : (a.N + 15) & ~15, nt = FULL ? NTMAX : np / 16;   // FULL: 22 key tiles, compile-time
   const Stage st{b, h, a.N, np};
   const int C3 = 3 * a.C, hoff = h * a.hd;
   stage_rows(Qs, a.qkv, C3, hoff, st, a.hd, Qt);
@@ -779,6 +789,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_kv2_kernel(WinAttnArgs a) {
   }
 }
 
+template <bool FULL>
 __global__ __launch_bounds__(512) void winattn_bwd_qb2_kernel(WinAttnArgs a, int wpg, int nqg, float* dsum) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[NPMAX][16];
@@ -791,7 +802,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_qb2_kernel(WinAttnArgs a, int
   __shared__ __attribute__((aligned(16))) int code[NPMAX];
   __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
   const int blk = wa_block(a), qg = blk % nqg, h = (blk / nqg) % a.heads, wg = blk / (nqg * a.heads);
-  const int np = (a.N + 15) & ~15, nt = np / 16;
+  const int np = FULL ? NPMAX : (a.N + 15) & ~15, nt = FULL ? NTMAX : np / 16;   // FULL: 22 key tiles, compile-time
   const int q0 = qg * QB_TILES * 16;
   const int C3 = 3 * a.C, hoff = h * a.hd;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -869,7 +880,9 @@ __global__ __launch_bounds__(512) void winattn_bwd_qb2_kernel(WinAttnArgs a, int
               float t = fmaf(sc[r], sc2, tq[-c[r]]);
               if (rmix && ((rk >> (8 * r)) & 255u) != rq) t -= pen2;
               const float p = __builtin_amdgcn_exp2f(t - lq);
-              ds[r] = p * (dp[r] - dq_);
+              // (an explicitly rounded product: with `acc += p * (...)` the compiler may contract into an FMA or
+              // not depending on the instantiation, and the summed gradient must be the same bits in both forms)
+              ds[r] = __fmul_rn(p, dp[r] - dq_);
               if (kt == nt - 1 && k0 + r >= a.N) ds[r] = 0.f;   // keys past N (only in the last tile)
               acc[kt][r] += ds[r];
             }
@@ -912,6 +925,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_qb2_kernel(WinAttnArgs a, int
 
 // bwd_q in the r05 form (one window per block, dS written per window in bf16 for mmseg_relpos_table_grad): the
 // same per-score arithmetic and MFMA order as winattn_bwd_qb2_kernel, so dQ is bitwise the summed path's.
+template <bool FULL>
 __global__ __launch_bounds__(512) void winattn_bwd_q2_kernel(WinAttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Qs[NPMAX][16];
   __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
@@ -924,7 +938,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_q2_kernel(WinAttnArgs a) {
   __shared__ __attribute__((aligned(16))) int code[NPMAX];
   __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
   const int bh = wa_block(a), b = bh / a.heads, h = bh % a.heads;
-  const int np = (a.N + 15) & ~15, nt = np / 16;
+  const int np = FULL ? NPMAX : (a.N + 15) & ~15, nt = FULL ? NTMAX : np / 16;   // FULL: 22 key tiles, compile-time
   const Stage st{b, h, a.N, np};
   const int C3 = 3 * a.C, hoff = h * a.hd;
   stage_rows(Qs, a.qkv, C3, hoff, st, a.hd, nullptr);
@@ -972,7 +986,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_q2_kernel(WinAttnArgs a) {
             float t = fmaf(sc[r], sc2, tq[-c[r]]);
             if (rmix && ((rk >> (8 * r)) & 255u) != rq) t -= pen2;
             const float p = __builtin_amdgcn_exp2f(t - lq);
-            ds[r] = p * (dp[r] - dq_);
+            ds[r] = __fmul_rn(p, dp[r] - dq_);   // (as the grouped query pass: the same dQ bits)
             if (kt == nt - 1 && k0 + r >= a.N) ds[r] = 0.f;
           }
           dd[u] = pack4(ds[0], ds[1], ds[2], ds[3]);
@@ -1042,7 +1056,9 @@ int mmseg_winattn_fwd(const void* qkv, int B, int N, int C, int heads, const flo
   if (check_args(a)) return 1;
   if (knob_i("MMSEG_WINATTN_FWD1", 1)) {
     mmseg::note_kernel("winattn_fwd1_kernel");
-    MMSEG_LAUNCH(winattn_fwd1_kernel, dim3(B * heads), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+    // (the forward keeps the runtime bound: its FULL instantiation held the whole score row live, 256 VGPRs
+    // with 134 spills)
+    MMSEG_LAUNCH(winattn_fwd1_kernel<false>, dim3(B * heads), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
   } else {
     mmseg::note_kernel("winattn_fwd_kernel");
     MMSEG_LAUNCH(winattn_fwd_kernel, dim3(B * heads), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
@@ -1060,10 +1076,12 @@ int mmseg_winattn_bwd(const void* qkv, const void* O, const void* dO, const floa
   MMSEG_REQUIRE(ldn >= N && ldn % 8 == 0, "winattn_bwd: ldn >= N, multiple of 8");
   hipStream_t s = (hipStream_t)stream;
   const bool v2 = knob_i("MMSEG_WINATTN_BWD2", 1) != 0;
-  if (v2) MMSEG_LAUNCH(winattn_bwd_kv2_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  if (v2 && wa_full(a)) MMSEG_LAUNCH(winattn_bwd_kv2_kernel<true>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  else if (v2) MMSEG_LAUNCH(winattn_bwd_kv2_kernel<false>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
   else MMSEG_LAUNCH(winattn_bwd_kv_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
   if (mmseg::check_launch("winattn_bwd_kv")) return 1;
-  if (v2) MMSEG_LAUNCH(winattn_bwd_q2_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  if (v2 && wa_full(a)) MMSEG_LAUNCH(winattn_bwd_q2_kernel<true>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  else if (v2) MMSEG_LAUNCH(winattn_bwd_q2_kernel<false>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
   else MMSEG_LAUNCH(winattn_bwd_q_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
   mmseg::note_kernel(v2 ? "winattn_bwd_kv2_kernel" : "winattn_bwd_kv_kernel");
   return mmseg::check_launch("winattn_bwd_q");
@@ -1089,12 +1107,16 @@ int mmseg_winattn_bwd_sum(const void* qkv, const void* O, const void* dO, const 
                 "winattn_bwd_sum: ldn >= N (multiple of 8) and enough windows (mmseg_winattn_sum_groups)");
   hipStream_t s = (hipStream_t)stream;
   const bool v2 = knob_i("MMSEG_WINATTN_BWD2", 1) != 0;
-  if (v2) MMSEG_LAUNCH(winattn_bwd_kv2_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  if (v2 && wa_full(a)) MMSEG_LAUNCH(winattn_bwd_kv2_kernel<true>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  else if (v2) MMSEG_LAUNCH(winattn_bwd_kv2_kernel<false>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
   else MMSEG_LAUNCH(winattn_bwd_kv_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
   if (mmseg::check_launch("winattn_bwd_kv")) return 1;
   const int wpg = qb_windows_per_group(B, N, heads);
   const int nt = ((N + 15) & ~15) / 16, nqg = (nt + QB_TILES - 1) / QB_TILES, nwg = (B + wpg - 1) / wpg;
-  if (v2) MMSEG_LAUNCH(winattn_bwd_qb2_kernel, dim3(nwg * heads * nqg), dim3(64 * WAVES), 0, s, a, wpg, nqg, dsum);
+  if (v2 && wa_full(a))
+    MMSEG_LAUNCH(winattn_bwd_qb2_kernel<true>, dim3(nwg * heads * nqg), dim3(64 * WAVES), 0, s, a, wpg, nqg, dsum);
+  else if (v2)
+    MMSEG_LAUNCH(winattn_bwd_qb2_kernel<false>, dim3(nwg * heads * nqg), dim3(64 * WAVES), 0, s, a, wpg, nqg, dsum);
   else MMSEG_LAUNCH(winattn_bwd_qb_kernel, dim3(nwg * heads * nqg), dim3(64 * WAVES), 0, s, a, wpg, nqg, dsum);
   mmseg::note_kernel(v2 ? "winattn_bwd_kv2_kernel" : "winattn_bwd_kv_kernel");
   return mmseg::check_launch("winattn_bwd_qb");

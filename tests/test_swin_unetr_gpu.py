@@ -881,6 +881,49 @@ def test_window_attention_backward_r05_forms(dev, N, hd, heads, masked, monkeypa
     assert torch.equal(s1[..., N:], torch.zeros_like(s1[..., N:]))
 
 
+@pytest.mark.parametrize("masked", [True, False])
+def test_window_attention_full_windows_bitwise(dev, masked, monkeypatch):
+    """343-token windows (22 key tiles) run the backward kernels instantiated with the tile count at compile time
+    (MMSEG_WINATTN_FULL=1, default): the same scores, products and sums in the same order as the runtime-bound
+    forms (=0): dqkv and the per-window dS (key and query passes) are BITWISE equal, the on-chip summed fp32 dS
+    (grouped query pass) to its last bit."""
+    N, hd, heads, nwin = 343, 16, 3, 4
+    C, B = heads * hd, 256
+    g = torch.Generator().manual_seed(5 + masked)
+    qkv = torch.randn(B * N, 3 * C, generator=g).to(torch.bfloat16).to(dev)
+    tab = (torch.randn(13 ** 3, heads, generator=g) * 0.5).t().contiguous().to(dev)
+    reg = torch.randint(0, 4, (nwin, N), generator=g).to(torch.uint8).to(dev) if masked else None
+    dO = torch.randn(B * N, C, generator=g).to(torch.bfloat16).to(dev)
+    L, s = lib(), stream_handle()
+    O = torch.empty(B * N, C, dtype=torch.bfloat16, device=dev)
+    lse = torch.zeros(L.mmseg_winattn_lse_floats(B, heads), device=dev)
+    nw = nwin if masked else 0
+    L.mmseg_winattn_fwd(ptr(qkv), B, N, C, heads, ptr(tab), 13 ** 3, 7, 7, 7, ptr(reg), nw, hd ** -0.5, ptr(O),
+                        ptr(lse), s)
+    ldn = (N + 7) // 8 * 8
+    groups = L.mmseg_winattn_sum_groups(B, N, heads)
+    assert groups > 0
+    res = {}
+    for full in ("1", "0"):
+        monkeypatch.setenv("MMSEG_WINATTN_FULL", full)
+        dqkv = torch.empty(B * N, 3 * C, dtype=torch.bfloat16, device=dev)
+        dS = torch.zeros(B * heads * N * ldn, dtype=torch.bfloat16, device=dev)
+        L.mmseg_winattn_bwd(ptr(qkv), ptr(O), ptr(dO), ptr(lse), B, N, C, heads, ptr(tab), 13 ** 3, 7, 7, 7,
+                            ptr(reg), nw, hd ** -0.5, ptr(dqkv), ptr(dS), ldn, s)
+        dqkv2 = torch.empty(B * N, 3 * C, dtype=torch.bfloat16, device=dev)
+        dsum = torch.zeros(groups * heads * N * ldn, device=dev)
+        assert L.mmseg_winattn_bwd_sum(ptr(qkv), ptr(O), ptr(dO), ptr(lse), B, N, C, heads, ptr(tab), 13 ** 3, 7,
+                                       7, 7, ptr(reg), nw, hd ** -0.5, ptr(dqkv2), ptr(dsum), ldn, s) == 0
+        torch.cuda.synchronize()
+        res[full] = (dqkv, dS, dqkv2, dsum)
+    for name, a, b in zip(("dqkv", "dS", "dqkv (grouped)"), res["1"][:3], res["0"][:3]):
+        assert torch.equal(a, b), (name, (a.float() - b.float()).abs().max().item())
+    # the fp32 table-gradient sums: measured within 1.2e-7 absolute of each other (the masked windows' sums differ
+    # in the last bit between the two instantiations; dQ / dK / dV / dS, which go through bf16, are bitwise)
+    assert rel2(res["1"][3], res["0"][3]) < 1e-6
+    assert torch.equal(res["1"][0], res["1"][2])   # dQ of the grouped query pass is the per-window pass's
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_head_48_channels_tile(dev, dtype, monkeypatch):
     """SwinUNETR's 1x1 head on 48 channels at pitch 64: the tile-staged forward (MMSEG_HEAD_TILE, default) is bitwise
