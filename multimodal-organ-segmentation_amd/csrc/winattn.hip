@@ -321,6 +321,7 @@ __global__ __launch_bounds__(512) void winattn_fwd1_kernel(WinAttnArgs a) {
   const int r16 = lane & 15, g4 = lane >> 4;
   const float sc2 = a.scale * LOG2E, pen2 = 100.0f * LOG2E;
   const s4 z4 = {0, 0, 0, 0};
+#pragma unroll 1   // (one query tile's score row live at a time: with FULL the trip count is known)
   for (int qt = wave; qt < nt; qt += WAVES) {
     const int q = qt * 16 + r16;
     const s4 bq = ld4(&Qs[q][4 * g4]);
@@ -347,6 +348,7 @@ __global__ __launch_bounds__(512) void winattn_fwd1_kernel(WinAttnArgs a) {
           mx = fmaxf(mx, t);
         }
       }
+      if constexpr (FULL) __builtin_amdgcn_sched_barrier(0);   // one key tile's loads in flight at a time
     }
     // (a padding query's row is finite -- its table codes are token 0's -- and is never stored: no select)
 #pragma unroll
@@ -1056,9 +1058,10 @@ int mmseg_winattn_fwd(const void* qkv, int B, int N, int C, int heads, const flo
   if (check_args(a)) return 1;
   if (knob_i("MMSEG_WINATTN_FWD1", 1)) {
     mmseg::note_kernel("winattn_fwd1_kernel");
-    // (the forward keeps the runtime bound: its FULL instantiation held the whole score row live, 256 VGPRs
-    // with 134 spills)
-    MMSEG_LAUNCH(winattn_fwd1_kernel<false>, dim3(B * heads), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+    if (wa_full(a))
+      MMSEG_LAUNCH(winattn_fwd1_kernel<true>, dim3(B * heads), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+    else
+      MMSEG_LAUNCH(winattn_fwd1_kernel<false>, dim3(B * heads), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
   } else {
     mmseg::note_kernel("winattn_fwd_kernel");
     MMSEG_LAUNCH(winattn_fwd_kernel, dim3(B * heads), dim3(64 * WAVES), 0, (hipStream_t)stream, a);

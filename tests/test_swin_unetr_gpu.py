@@ -895,11 +895,18 @@ def test_window_attention_full_windows_bitwise(dev, masked, monkeypatch):
     reg = torch.randint(0, 4, (nwin, N), generator=g).to(torch.uint8).to(dev) if masked else None
     dO = torch.randn(B * N, C, generator=g).to(torch.bfloat16).to(dev)
     L, s = lib(), stream_handle()
-    O = torch.empty(B * N, C, dtype=torch.bfloat16, device=dev)
-    lse = torch.zeros(L.mmseg_winattn_lse_floats(B, heads), device=dev)
     nw = nwin if masked else 0
-    L.mmseg_winattn_fwd(ptr(qkv), B, N, C, heads, ptr(tab), 13 ** 3, 7, 7, 7, ptr(reg), nw, hd ** -0.5, ptr(O),
-                        ptr(lse), s)
+    fw = {}
+    for full in ("1", "0"):   # the forward too: O and lse bitwise
+        monkeypatch.setenv("MMSEG_WINATTN_FULL", full)
+        O = torch.empty(B * N, C, dtype=torch.bfloat16, device=dev)
+        lse = torch.zeros(L.mmseg_winattn_lse_floats(B, heads), device=dev)
+        L.mmseg_winattn_fwd(ptr(qkv), B, N, C, heads, ptr(tab), 13 ** 3, 7, 7, 7, ptr(reg), nw, hd ** -0.5, ptr(O),
+                            ptr(lse), s)
+        torch.cuda.synchronize()
+        fw[full] = (O, lse)
+    assert torch.equal(fw["1"][0], fw["0"][0]) and torch.equal(fw["1"][1], fw["0"][1])
+    O, lse = fw["1"]
     ldn = (N + 7) // 8 * 8
     groups = L.mmseg_winattn_sum_groups(B, N, heads)
     assert groups > 0
