@@ -43,6 +43,7 @@ struct WinAttnArgs {
   int B, N, C, heads, hd, nw, T, ldn;
   int w0, w1, w2;        // the module's full window
   float scale;
+  int mixall;            // MMSEG_WINATTN_MIXALL=1: every window takes the mixed-region score code (A/B only)
   int swz;               // XCD-aware block order (MMSEG_WINATTN_SWZ, default on): a window's heads / query groups,
                          // which stage the same qkv rows (a head's 32-B slice of each), run on one XCD and share its L2
 };
@@ -330,26 +331,36 @@ __global__ __launch_bounds__(512) void winattn_fwd1_kernel(WinAttnArgs a) {
     const uint32_t rq = reg[q];
     float v[NTMAX][4];
     float mx = -INFINITY;
+    // the score row, instantiated for mixed-region windows and for the rest (no per-score mask compare or select)
+    auto scores = [&](auto mixc) __attribute__((always_inline)) {
+      constexpr bool MIX = decltype(mixc)::value;
 #pragma unroll
-    for (int kt = 0; kt < NTMAX; ++kt) {
-      if (kt < nt) {
-        const f32x4 acc = mma(ld4(&Ks[kt * 16 + r16][4 * g4]), bq, (f32x4){0.f, 0.f, 0.f, 0.f});
-        const int k0 = kt * 16 + 4 * g4;
-        const int4 ck = *reinterpret_cast<const int4*>(code + k0);
-        const uint32_t rk = rmix ? *reinterpret_cast<const uint32_t*>(reg + k0) : 0u;
-        const int c[4] = {ck.x, ck.y, ck.z, ck.w};
-        const bool last = kt == nt - 1;   // (wave-uniform) only the last key tile holds keys past N
+      for (int kt = 0; kt < NTMAX; ++kt) {
+        if (kt < nt) {
+          const f32x4 acc = mma(ld4(&Ks[kt * 16 + r16][4 * g4]), bq, (f32x4){0.f, 0.f, 0.f, 0.f});
+          const int k0 = kt * 16 + 4 * g4;
+          const int4 ck = *reinterpret_cast<const int4*>(code + k0);
+          const uint32_t rk = MIX ? *reinterpret_cast<const uint32_t*>(reg + k0) : 0u;
+          const int c[4] = {ck.x, ck.y, ck.z, ck.w};
+          const bool last = kt == nt - 1;   // (wave-uniform) only the last key tile holds keys past N
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float t = fmaf(acc[r], sc2, tq[-c[r]]);
-          if (rmix && ((rk >> (8 * r)) & 255u) != rq) t -= pen2;
-          if (last && k0 + r >= a.N) t = -INFINITY;
-          v[kt][r] = t;
-          mx = fmaxf(mx, t);
+          for (int r = 0; r < 4; ++r) {
+            float t = fmaf(acc[r], sc2, tq[-c[r]]);
+            if constexpr (MIX) {
+              if (((rk >> (8 * r)) & 255u) != rq) t -= pen2;
+            }
+            if (last && k0 + r >= a.N) t = -INFINITY;
+            v[kt][r] = t;
+            mx = fmaxf(mx, t);
+          }
         }
+        if constexpr (FULL) __builtin_amdgcn_sched_barrier(0);   // one key tile's loads in flight at a time
       }
-      if constexpr (FULL) __builtin_amdgcn_sched_barrier(0);   // one key tile's loads in flight at a time
-    }
+    };
+    if (rmix || a.mixall)
+      scores(std::true_type{});
+    else
+      scores(std::false_type{});
     // (a padding query's row is finite -- its table codes are token 0's -- and is never stored: no select)
 #pragma unroll
     for (int o = 16; o <= 32; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
@@ -863,43 +874,53 @@ __global__ __launch_bounds__(512) void winattn_bwd_qb2_kernel(WinAttnArgs a, int
       const float* tq = ctab + code[q];
       const uint32_t rq = reg[q];
       f32x4 dq = {0.f, 0.f, 0.f, 0.f};
+      // instantiated for mixed-region windows and for the rest (no per-score mask compare or select)
+      auto tiles = [&](auto mixc) __attribute__((always_inline)) {
+        constexpr bool MIX = decltype(mixc)::value;
 #pragma unroll
-      for (int k2 = 0; k2 < NTMAX / 2; ++k2) {
-        s4 dd[2];
+        for (int k2 = 0; k2 < NTMAX / 2; ++k2) {
+          s4 dd[2];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int kt = 2 * k2 + u;
-          if (kt < nt) {
-            const f32x4 sc = mma(ld4(&Ks[kt * 16 + r16][4 * g4]), bq, (f32x4){0.f, 0.f, 0.f, 0.f});
-            const f32x4 dp = mma(ld4(&Vs[kt * 16 + r16][4 * g4]), bdo, (f32x4){0.f, 0.f, 0.f, 0.f});
-            const int k0 = kt * 16 + 4 * g4;
-            const int4 ck = *reinterpret_cast<const int4*>(code + k0);
-            const uint32_t rk = rmix ? *reinterpret_cast<const uint32_t*>(reg + k0) : 0u;
-            const int c[4] = {ck.x, ck.y, ck.z, ck.w};
-            float ds[4];
+          for (int u = 0; u < 2; ++u) {
+            const int kt = 2 * k2 + u;
+            if (kt < nt) {
+              const f32x4 sc = mma(ld4(&Ks[kt * 16 + r16][4 * g4]), bq, (f32x4){0.f, 0.f, 0.f, 0.f});
+              const f32x4 dp = mma(ld4(&Vs[kt * 16 + r16][4 * g4]), bdo, (f32x4){0.f, 0.f, 0.f, 0.f});
+              const int k0 = kt * 16 + 4 * g4;
+              const int4 ck = *reinterpret_cast<const int4*>(code + k0);
+              const uint32_t rk = MIX ? *reinterpret_cast<const uint32_t*>(reg + k0) : 0u;
+              const int c[4] = {ck.x, ck.y, ck.z, ck.w};
+              float ds[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              float t = fmaf(sc[r], sc2, tq[-c[r]]);
-              if (rmix && ((rk >> (8 * r)) & 255u) != rq) t -= pen2;
-              const float p = __builtin_amdgcn_exp2f(t - lq);
-              // (an explicitly rounded product: with `acc += p * (...)` the compiler may contract into an FMA or
-              // not depending on the instantiation, and the summed gradient must be the same bits in both forms)
-              ds[r] = __fmul_rn(p, dp[r] - dq_);
-              if (kt == nt - 1 && k0 + r >= a.N) ds[r] = 0.f;   // keys past N (only in the last tile)
-              acc[kt][r] += ds[r];
+              for (int r = 0; r < 4; ++r) {
+                float t = fmaf(sc[r], sc2, tq[-c[r]]);
+                if constexpr (MIX) {
+                  if (((rk >> (8 * r)) & 255u) != rq) t -= pen2;
+                }
+                const float p = __builtin_amdgcn_exp2f(t - lq);
+                // (an explicitly rounded product: with `acc += p * (...)` the compiler may contract into an FMA
+                // or not depending on the instantiation, and the summed gradient must be the same bits in both)
+                ds[r] = __fmul_rn(p, dp[r] - dq_);
+                if (kt == nt - 1 && k0 + r >= a.N) ds[r] = 0.f;   // keys past N (only in the last tile)
+                acc[kt][r] += ds[r];
+              }
+              dd[u] = pack4(ds[0], ds[1], ds[2], ds[3]);
+            } else {
+              dd[u] = z4;
             }
-            dd[u] = pack4(ds[0], ds[1], ds[2], ds[3]);
-          } else {
-            dd[u] = z4;
+          }
+          const int kt0 = 2 * k2;
+          if (kt0 < nt) {
+            const bool hi = kt0 + 1 < nt;
+            const s4 k0v = ld4(&Kt[r16][kt0 * 16 + 4 * g4]), k1v = hi ? ld4(&Kt[r16][(kt0 + 1) * 16 + 4 * g4]) : z4;
+            dq = mma32(dd[0], dd[1], k0v, k1v, dq);
           }
         }
-        const int kt0 = 2 * k2;
-        if (kt0 < nt) {
-          const bool hi = kt0 + 1 < nt;
-          const s4 k0v = ld4(&Kt[r16][kt0 * 16 + 4 * g4]), k1v = hi ? ld4(&Kt[r16][(kt0 + 1) * 16 + 4 * g4]) : z4;
-          dq = mma32(dd[0], dd[1], k0v, k1v, dq);
-        }
-      }
+      };
+      if (rmix || a.mixall)
+        tiles(std::true_type{});
+      else
+        tiles(std::false_type{});
       if (r16 < a.hd) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1055,6 +1076,7 @@ int mmseg_winattn_fwd(const void* qkv, int B, int N, int C, int heads, const flo
   WinAttnArgs a{(const bf16_t*)qkv, nullptr, nullptr, (bf16_t*)O, lse, nullptr, table, region,
                 B, N, C, heads, C / heads, nw, T, 0, w0, w1, w2, scale};
   a.swz = knob_i("MMSEG_WINATTN_SWZ", 1);
+  a.mixall = knob_i("MMSEG_WINATTN_MIXALL", 0);
   if (check_args(a)) return 1;
   if (knob_i("MMSEG_WINATTN_FWD1", 1)) {
     mmseg::note_kernel("winattn_fwd1_kernel");
@@ -1075,6 +1097,7 @@ int mmseg_winattn_bwd(const void* qkv, const void* O, const void* dO, const floa
   WinAttnArgs a{(const bf16_t*)qkv, (const bf16_t*)O, (const bf16_t*)dO, (bf16_t*)dqkv, const_cast<float*>(lse),
                 (bf16_t*)dS, table, region, B, N, C, heads, C / heads, nw, T, ldn, w0, w1, w2, scale};
   a.swz = knob_i("MMSEG_WINATTN_SWZ", 1);
+  a.mixall = knob_i("MMSEG_WINATTN_MIXALL", 0);
   if (check_args(a)) return 1;
   MMSEG_REQUIRE(ldn >= N && ldn % 8 == 0, "winattn_bwd: ldn >= N, multiple of 8");
   hipStream_t s = (hipStream_t)stream;
@@ -1105,6 +1128,7 @@ int mmseg_winattn_bwd_sum(const void* qkv, const void* O, const void* dO, const 
   WinAttnArgs a{(const bf16_t*)qkv, (const bf16_t*)O, (const bf16_t*)dO, (bf16_t*)dqkv, const_cast<float*>(lse),
                 nullptr, table, region, B, N, C, heads, C / heads, nw, T, ldn, w0, w1, w2, scale};
   a.swz = knob_i("MMSEG_WINATTN_SWZ", 1);
+  a.mixall = knob_i("MMSEG_WINATTN_MIXALL", 0);
   if (check_args(a)) return 1;
   MMSEG_REQUIRE(ldn >= N && ldn % 8 == 0 && mmseg_winattn_sum_groups(B, N, heads) > 0,
                 "winattn_bwd_sum: ldn >= N (multiple of 8) and enough windows (mmseg_winattn_sum_groups)");
