@@ -752,42 +752,52 @@ __global__ __launch_bounds__(512) void winattn_bwd_kv2_kernel(WinAttnArgs a) {
     const float* tk = ctab - code[key];
     const uint32_t rk = reg[key];
     f32x4 dk = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
-    for (int qt = 0; qt < nt; qt += 2) {
-      s4 pp[2], dd[2];
+    // instantiated for mixed-region windows and for the rest (no per-score mask compare or select)
+    auto pairs = [&](auto mixc) __attribute__((always_inline)) {
+      constexpr bool MIX = decltype(mixc)::value;
+      for (int qt = 0; qt < nt; qt += 2) {
+        s4 pp[2], dd[2];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int qq = qt + u;
-        if (qq < nt) {
-          const f32x4 sc = mma(ld4(&Qs[qq * 16 + r16][4 * g4]), bk, (f32x4){0.f, 0.f, 0.f, 0.f});   // S[q][key]
-          const f32x4 dp = mma(ld4(&dOs[qq * 16 + r16][4 * g4]), bv, (f32x4){0.f, 0.f, 0.f, 0.f}); // dP[q][key]
-          const int q0 = qq * 16 + 4 * g4;
-          const int4 cq = *reinterpret_cast<const int4*>(code + q0);
-          const uint32_t rq = rmix ? *reinterpret_cast<const uint32_t*>(reg + q0) : 0u;
-          const float4 l4 = *reinterpret_cast<const float4*>(lse2 + q0);
-          const float4 d4 = *reinterpret_cast<const float4*>(Dq + q0);
-          const int c[4] = {cq.x, cq.y, cq.z, cq.w};
-          const float lq[4] = {l4.x, l4.y, l4.z, l4.w}, dq4[4] = {d4.x, d4.y, d4.z, d4.w};
-          float p[4], ds[4];
+        for (int u = 0; u < 2; ++u) {
+          const int qq = qt + u;
+          if (qq < nt) {
+            const f32x4 sc = mma(ld4(&Qs[qq * 16 + r16][4 * g4]), bk, (f32x4){0.f, 0.f, 0.f, 0.f});   // S[q][key]
+            const f32x4 dp = mma(ld4(&dOs[qq * 16 + r16][4 * g4]), bv, (f32x4){0.f, 0.f, 0.f, 0.f}); // dP[q][key]
+            const int q0 = qq * 16 + 4 * g4;
+            const int4 cq = *reinterpret_cast<const int4*>(code + q0);
+            const uint32_t rq = MIX ? *reinterpret_cast<const uint32_t*>(reg + q0) : 0u;
+            const float4 l4 = *reinterpret_cast<const float4*>(lse2 + q0);
+            const float4 d4 = *reinterpret_cast<const float4*>(Dq + q0);
+            const int c[4] = {cq.x, cq.y, cq.z, cq.w};
+            const float lq[4] = {l4.x, l4.y, l4.z, l4.w}, dq4[4] = {d4.x, d4.y, d4.z, d4.w};
+            float p[4], ds[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float t = fmaf(sc[r], sc2, tk[c[r]]);
-            if (rmix && ((rq >> (8 * r)) & 255u) != rk) t -= pen2;
-            p[r] = __builtin_amdgcn_exp2f(t - lq[r]);
-            ds[r] = p[r] * (dp[r] - dq4[r]);
+            for (int r = 0; r < 4; ++r) {
+              float t = fmaf(sc[r], sc2, tk[c[r]]);
+              if constexpr (MIX) {
+                if (((rq >> (8 * r)) & 255u) != rk) t -= pen2;
+              }
+              p[r] = __builtin_amdgcn_exp2f(t - lq[r]);
+              ds[r] = p[r] * (dp[r] - dq4[r]);
+            }
+            pp[u] = pack4(p[0], p[1], p[2], p[3]);
+            dd[u] = pack4(ds[0], ds[1], ds[2], ds[3]);
+          } else {
+            pp[u] = z4;
+            dd[u] = z4;
           }
-          pp[u] = pack4(p[0], p[1], p[2], p[3]);
-          dd[u] = pack4(ds[0], ds[1], ds[2], ds[3]);
-        } else {
-          pp[u] = z4;
-          dd[u] = z4;
         }
+        const bool hi = qt + 1 < nt;
+        const s4 o0 = ld4(&dOt[r16][qt * 16 + 4 * g4]), o1 = hi ? ld4(&dOt[r16][(qt + 1) * 16 + 4 * g4]) : z4;
+        const s4 q0 = ld4(&Qt[r16][qt * 16 + 4 * g4]), q1 = hi ? ld4(&Qt[r16][(qt + 1) * 16 + 4 * g4]) : z4;
+        dv = mma32(pp[0], pp[1], o0, o1, dv);
+        dk = mma32(dd[0], dd[1], q0, q1, dk);
       }
-      const bool hi = qt + 1 < nt;
-      const s4 o0 = ld4(&dOt[r16][qt * 16 + 4 * g4]), o1 = hi ? ld4(&dOt[r16][(qt + 1) * 16 + 4 * g4]) : z4;
-      const s4 q0 = ld4(&Qt[r16][qt * 16 + 4 * g4]), q1 = hi ? ld4(&Qt[r16][(qt + 1) * 16 + 4 * g4]) : z4;
-      dv = mma32(pp[0], pp[1], o0, o1, dv);
-      dk = mma32(dd[0], dd[1], q0, q1, dk);
-    }
+    };
+    if (rmix || a.mixall)
+      pairs(std::true_type{});
+    else
+      pairs(std::false_type{});
     if (r16 < a.hd) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
