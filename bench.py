@@ -279,6 +279,41 @@ def cpu_baseline(model_name, batch, size, out_channels, modalities, threads, los
                       f"{threads} threads"}
 
 
+def bench_infer(args, trainer, model, mods, dev):
+    """Sliding-window inference at the config's window (roi 96^3, sw_batch 4, overlap 0.5): --infer-volumes
+    seeded phantom volumes of --infer-size^3 resident in HBM, one warm-up call, then --steps timed calls."""
+    from mmseg_amd.data import device_batches
+    model.eval()
+    S, V = args.infer_size, args.infer_volumes
+    img = device_batches(1, V, S, 6, mods, dev, seed=4321)[0]["image"]
+    with torch.no_grad():
+        for _ in range(max(args.warmup, 1)):
+            out = trainer._sliding_window_inference(img)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = trainer._sliding_window_inference(img)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    import math
+    nwin = 1
+    for _ in range(3):
+        iv = int(96 * 0.5)
+        num = int(math.ceil(S / iv))
+        nwin *= next((i for i in range(num) if i * iv + 96 >= S), num - 1) + 1
+    ms_vol = el / (args.steps * V) * 1e3
+    print(json.dumps({
+        "metric": f"sliding-window inference {S}^3 {len(mods)}-modality volumes/sec (roi 96^3, sw_batch 4, "
+                  f"overlap 0.5)", "value": round(1e3 / ms_vol, 3), "unit": "volumes/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": max(args.warmup, 1), "ms_per_volume": round(ms_vol, 3),
+        "higher_is_better": True, "dtype": args.dtype, "data": "synthetic (seeded phantoms, resident in HBM)",
+        "windows_per_volume": nwin, "ms_per_window": round(ms_vol / nwin, 3),
+        "config": {"workload": f"{args.model} sliding_window_inference, {V} x {S}^3, 6 classes",
+                   "model": args.model, "volumes": V, "size": S, "roi": [96, 96, 96], "sw_batch": 4,
+                   "overlap": 0.5},
+        "out_finite": bool(torch.isfinite(out).all().item())}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -307,9 +342,18 @@ def main():
                     help="--kernels torch autocast dtype (fp16 + GradScaler = the reference's GPU mode)")
     ap.add_argument("--dp-rehearsal", action="store_true",
                     help="one GPU, the data-parallel step: an RCCL process group of world size 1 with "
-                         "distributed.reduce_single_rank, so the bucket all-reduces (AVG) really run through RCCL "
-                         "inside the captured step, exactly as each rank of the N-GPU job runs them")
+                         "distributed.reduce_single_rank, so the bucket all-reduces really run through RCCL inside the "
+                         "captured step at the points each rank of the N-GPU job issues them.  At world size 1 the "
+                         "collective is SUM (AVG is the identity there; RCCL's single-rank AVG adds a scaling pass, "
+                         "~0.24 ms/step, that an N-rank AVG folds into the reduction), so that pass is not in the "
+                         "rehearsed time (MMSEG_DP_AVG1=1 keeps AVG)")
     ap.add_argument("--bucket-mb", type=float, default=32.0, help="DP gradient bucket size (distributed.bucket_mb)")
+    ap.add_argument("--infer", action="store_true",
+                    help="secondary line: sliding-window inference (Trainer._sliding_window_inference, reference "
+                         "trainer.py:370-395 with default.yaml's roi 96^3 / sw_batch 4 / overlap 0.5) over "
+                         "--infer-volumes volumes of --infer-size^3, timed per volume; not the headline metric")
+    ap.add_argument("--infer-size", type=int, default=160)
+    ap.add_argument("--infer-volumes", type=int, default=2)
     ap.add_argument("--workload-out", default="", help="write this run's workload key (JSON) for the profile "
                                                        "summaries of tools/rocprof_families.py")
     args = ap.parse_args()
@@ -349,6 +393,13 @@ def main():
     if args.kernels == "torch":
         args.no_cpu_baseline = True
         args.timer_steps = 0
+    if args.infer:
+        cfg["inference"] = {"sliding_window": {"roi_size": [96, 96, 96], "overlap": 0.5}, "batch_size": 4}
+        torch.manual_seed(42)
+        model = build_model(cfg)
+        trainer = Trainer(cfg, model)
+        bench_infer(args, trainer, model, mods, dev)
+        return
     torch.manual_seed(42)
     model = build_model(cfg)
     trainer = Trainer(cfg, model)
@@ -476,6 +527,14 @@ def main():
         tr, _ = pmc_traffic(k)
         if tr is not None:
             e["traffic_vs_algorithmic"] = round(tr / max(v["bytes"] / v["launches"], 1.0), 3)
+        # the family's own roofline: below the ridge (peak FLOP/s / peak B/s = 312.5 FLOP/B for bf16) a launch is
+        # bound by its compulsory HBM bytes, not by the matrix cores (the SwinUNETR token GEMMs, K = 48..192)
+        nb = v["bytes"] / v["launches"]
+        if nb > 0:
+            e["gbyte_per_launch"] = round(nb / 1e9, 5)
+            e["gbps"] = round(nb / (v["ms"] / v["launches"] * 1e-3) / 1e9, 1)
+            e["hbm_frac"] = round(e["gbps"] / PEAK_HBM_GBS, 4)
+            e["bound"] = "hbm" if fl / nb < peak_f / (PEAK_HBM_GBS / 1e3) else "mfma"
         mfma_families[k] = e
     step = None
     work = STEP_WORK.get((args.model, len(mods)))
@@ -491,6 +550,28 @@ def main():
                 "counter_gb": round(counter / 1e9, 3) if counter is not None else None,
                 "counter_source": csrc,
                 "counter_tbps": round(counter / (ms_per_step * 1e-3) / 1e12, 3) if counter is not None else None}
+    elif args.dtype == "bf16" and args.timer_steps > 0 and fam:
+        # no SURVEY 8(d) whole-step model for this workload (c4 SwinUNETR 128^3): the step's algorithmic work is
+        # the sum over every timed launch of its region's algorithmic FLOPs and compulsory bytes (each kernel's
+        # inputs + outputs once, engine/layers.py / swin.py regions) -- per-kernel compulsory traffic, so an
+        # upper bound on the whole-step compulsory bytes (tensors passed between kernels are counted twice)
+        F = sum(v["flops"] for v in fam.values()) / args.timer_steps
+        Bt = sum(v["bytes"] for v in fam.values()) / args.timer_steps
+        t_mfma, t_hbm = F / (PEAK_BF16_TFLOPS * 1e12), Bt / (PEAK_HBM_GBS * 1e9)
+        t_roof = max(t_mfma, t_hbm)
+        counter, csrc = pmc_step_bytes() if args.kernels == "hip" and not args.fp8 else (None, None)
+        step = {"bound": "hbm" if t_hbm >= t_mfma else "mfma", "algorithmic_tflop": round(F / 1e12, 3),
+                "compulsory_gb": round(Bt / 1e9, 3), "t_mfma_ms": round(t_mfma * 1e3, 3),
+                "t_hbm_ms": round(t_hbm * 1e3, 3), "t_roof_ms": round(t_roof * 1e3, 3),
+                "frac": round(t_roof * 1e3 / ms_per_step, 4),
+                "work_source": "sum of the timed launches' algorithmic FLOPs / per-kernel compulsory bytes",
+                "counter_gb": round(counter / 1e9, 3) if counter is not None else None,
+                "counter_source": csrc,
+                "counter_tbps": round(counter / (ms_per_step * 1e-3) / 1e12, 3) if counter is not None else None}
+    if step is not None:
+        if args.timer_steps > 0 and fam:
+            step["timer_sum_tflop"] = round(sum(v["flops"] for v in fam.values()) / args.timer_steps / 1e12, 3)
+            step["timer_sum_gb"] = round(sum(v["bytes"] for v in fam.values()) / args.timer_steps / 1e9, 3)
         if roofline is not None:
             roofline["step"] = step
         else:

@@ -5,6 +5,8 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include "../../include/mmseg_hip.h"
+
 #include <vector>
 
 namespace mmseg {

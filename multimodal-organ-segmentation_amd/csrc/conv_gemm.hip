@@ -2611,23 +2611,34 @@ bool brick5_selected(const GemmArgs& g, int tsize) {
          knob("MMSEG_BRICK5", 1);
 }
 
+// Every column tile of a conv launch reads weight columns [n0, n0 + BN) of the packed image [KGp][Cpad][8]: all of
+// them must lie inside the image's pitch Cpad (the r05f GPU fault: a 192-column tile over a 96-column layer's
+// 128-column image read 64 columns past it).  Checked on the host before each launch, with the kernel's name noted.
+inline bool tile_in_pitch(const GemmArgs& g, int BN) { return (long long)((g.Ncols + BN - 1) / BN) * BN <= g.Cpad; }
+#define MMSEG_TILE(G, NAME, BN)                                                                                   \
+  do {                                                                                                           \
+    MMSEG_REQUIRE(tile_in_pitch((G), (BN)), "%s: %d-column tiles over %d columns exceed the packed pitch %d", \
+                  (const char*)(NAME), (int)(BN), (G).Ncols, (G).Cpad);                                          \
+    mmseg::note_kernel(NAME);                                                                                    \
+  } while (0)
+
 int launch_brick5(const GemmArgs& g, hipStream_t s, long long* dbg, bool dma) {
   const int nt_n = g.Ncols / 32;
   const int per_nt = std::max(1, knob("MMSEG_BRICK4_BLOCKS", 256) / nt_n);
   const int nb5 = (g.M / (g.D * g.H * g.W)) * (g.D / 4) * (g.H / 4) * (g.W / 16);
   const int upb5 = ceil_div(nb5, std::min(per_nt, nb5));
   const int bpn5 = ceil_div(nb5, upb5);
-  mmseg::note_kernel("conv3_brick5_kernel<BN32>");
+  MMSEG_TILE(g, "conv3_brick5_kernel<BN32>", 32);
   const dim3 grid(bpn5 * nt_n), block(256);
   if (g.wdq) {   // e4m3 forward (mmseg_conv3_fwd_fp8)
-    mmseg::note_kernel("conv3_brick6_kernel<BN32,F8>");
+    MMSEG_TILE(g, "conv3_brick6_kernel<BN32,F8>", 32);
     if (g.nmean) MMSEG_LAUNCH((conv3_brick6_kernel<true, 6, 0, false, true>), grid, block, 0, s, g, upb5, bpn5);
     else MMSEG_LAUNCH((conv3_brick6_kernel<false, 6, 0, false, true>), grid, block, 0, s, g, upb5, bpn5);
     return upb5;
   }
   if (g.inpart) {   // samples a block does not touch keep zero partials
     if (!g.bias && knob("MMSEG_BRICK6", 1) && knob("MMSEG_BRICK6_INP", 1)) {   // (brick6 writes those zeros itself)
-      mmseg::note_kernel("conv3_brick6_kernel<BN32,INP>");
+      MMSEG_TILE(g, "conv3_brick6_kernel<BN32,INP>", 32);
       MMSEG_LAUNCH((conv3_brick6_kernel<false, 6, 0, true>), grid, block, 0, s, g, upb5, bpn5);
       return upb5;
     }
@@ -2637,7 +2648,7 @@ int launch_brick5(const GemmArgs& g, hipStream_t s, long long* dbg, bool dma) {
   }
   if (!dbg && !dma && knob("MMSEG_BRICK6", 1)) {
     const int sg = knob("MMSEG_BRICK6_SG0", 6);
-    mmseg::note_kernel("conv3_brick6_kernel<BN32>");
+    MMSEG_TILE(g, "conv3_brick6_kernel<BN32>", 32);
 #ifdef MMSEG_TIMING_PROBES
     if (knob("MMSEG_BRICK6_DBG", 0) == 1) {
       MMSEG_LAUNCH((conv3_brick6_kernel<false, 3, 1>), grid, block, 0, s, g, upb5, bpn5);
@@ -5025,7 +5036,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
                       (long long)g.M * g.lda * (long long)sizeof(T) < (1LL << 31);
     if (plan.bn == 64) {
       if constexpr (sizeof(T) == 2) {
-        mmseg::note_kernel("conv3_brickr_kernel<BN64>");
+        MMSEG_TILE(g, "conv3_brickr_kernel<BN64>", 64);
 #ifdef MMSEG_TIMING_PROBES
         // timing probes (diagnostics only, wrong results): built only with -DMMSEG_TIMING_PROBES
         const int dbg = knob("MMSEG_BRICKR_DBG", 0);
@@ -5122,7 +5133,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
       else
         MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
     } else if (b488) {
-      mmseg::note_kernel("conv3_brickr_kernel<BN32>");
+      MMSEG_TILE(g, "conv3_brickr_kernel<BN32>", 32);
       if (rb32 && knob("MMSEG_BRICKR_PF488", 0))
         MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 4, 8, 8, 0, true, true>), grid, block, 0, s, g, 4, 8, 8, (long long*)nullptr);
       else if (rb32)
@@ -5130,7 +5141,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
       else
         MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 4, 8, 8>), grid, block, 0, s, g, 4, 8, 8, (long long*)nullptr);
     } else {
-      mmseg::note_kernel("conv3_brickr_kernel<BN32>");
+      MMSEG_TILE(g, "conv3_brickr_kernel<BN32>", 32);
       if (rb32)
         MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 0, 0, 0, 0, false, true>), grid, block, 0, s, g, plan.bz,
                            plan.by, plan.bx, (long long*)nullptr);
@@ -5157,7 +5168,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
           (!g.out2 || g.ldo2 % 8 == 0) && (reinterpret_cast<uintptr_t>(g.out) & 15) == 0 &&
           nb8 * (g.Ncols / 64) >= knob("MMSEG_BRICK8_MINBLK", 256) &&
           (long long)g.M * g.lda * 2 < (1LL << 31) && (long long)((g.KG + 3) & ~3) * g.Cpad * 16 < (1LL << 31)) {
-        mmseg::note_kernel("conv3_brick8_kernel<BN64>");
+        MMSEG_TILE(g, "conv3_brick8_kernel<BN64>", 64);
         MMSEG_LAUNCH((conv3_brick8_kernel<64, 1>), dim3(nb8 * (g.Ncols / 64)), dim3(512), 0, s, g);
         return mmseg::check_launch("conv3_brick8");
       }
@@ -5166,7 +5177,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
           (!g.out2 || g.ldo2 % 8 == 0) && (reinterpret_cast<uintptr_t>(g.out) & 15) == 0 &&
           nb8 / 2 >= knob("MMSEG_BRICK8_MINBLK", 256) && (8 << g.cpg_shift) >= 64 &&
           (long long)g.M * g.lda * 2 < (1LL << 31) && (long long)((g.KG + 3) & ~3) * g.Cpad * 16 < (1LL << 31)) {
-        mmseg::note_kernel("conv3_brick8_kernel<BN32>");
+        MMSEG_TILE(g, "conv3_brick8_kernel<BN32>", 32);
         MMSEG_LAUNCH((conv3_brick8_kernel<32, 2>), dim3(nb8 / 2), dim3(512), 0, s, g);
         return mmseg::check_launch("conv3_brick8");
       }
@@ -5189,7 +5200,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     const bool bn48 = g.Ncols % 32 != 0 ||
                       (g.Ncols % 96 == 0 && g.Ncols % 64 != 0 && g.stats == nullptr && knob("MMSEG_BRICK2_BN48X", 1));
     if (bn48) {    // a multiple of 48 (plan_conv3)
-      mmseg::note_kernel("conv3_brick2_kernel<BN48,ZW1>");
+      MMSEG_TILE(g, "conv3_brick2_kernel<BN48,ZW1>", 48);
       if (b32) {
         MMSEG_LAUNCH((conv3_brick2_kernel<T, 48, 1, false, true>), dim3(nb1 * (g.Ncols / 48)), block, 0, s, g);
         return mmseg::check_launch("conv3_brick2");
@@ -5198,7 +5209,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     } else if (v3 && knob("MMSEG_BRICK3_BN64", 0) && g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
       const int units = nb1 * (g.Ncols / 64);
       const int upb = maxblk > 0 ? ceil_div(units, maxblk) : 1;
-      mmseg::note_kernel("conv3_brick3_kernel<BN64>");
+      MMSEG_TILE(g, "conv3_brick3_kernel<BN64>", 64);
       MMSEG_LAUNCH((conv3_brick3_kernel<T, 64>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
     } else if (v3 && gemm_nchunk(g) == 1 && g.Ncols % 32 == 0 && knob("MMSEG_BRICK4", 1) &&
                !(g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks)) {
@@ -5235,14 +5246,14 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
             launch_brick5(g, s, nullptr, dma);
           }
         } else {
-          mmseg::note_kernel("conv3_brick4_kernel<BN32>");
+          MMSEG_TILE(g, "conv3_brick4_kernel<BN32>", 32);
           MMSEG_LAUNCH(conv3_brick4_kernel, dim3(bpn * nt_n), block, 0, s, g, upb, bpn);
         }
       }
     } else if (v3 && !(g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks)) {
       const int units = nb1 * (g.Ncols / 32);
       const int upb = maxblk > 0 ? ceil_div(units, maxblk) : 1;
-      mmseg::note_kernel("conv3_brick3_kernel<BN32>");
+      MMSEG_TILE(g, "conv3_brick3_kernel<BN32>", 32);
       if (knob("MMSEG_BRICK3_WU", 0))
         MMSEG_LAUNCH((conv3_brick3_kernel<T, 32, true>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
       else if (knob("MMSEG_BRICK3_XP", 0))
@@ -5254,7 +5265,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
       else
         MMSEG_LAUNCH((conv3_brick3_kernel<T, 32, false>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
     } else if (g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
-      mmseg::note_kernel("conv3_brick2_kernel<BN64,ZW1>");
+      MMSEG_TILE(g, "conv3_brick2_kernel<BN64,ZW1>", 64);
       if (knob("MMSEG_TAP_PF", 1) && b32) {
         MMSEG_LAUNCH((conv3_brick2_kernel<T, 64, 1, true, true>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
         return mmseg::check_launch("conv3_brick2");
@@ -5265,11 +5276,11 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
         MMSEG_LAUNCH((conv3_brick2_kernel<T, 64, 1>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
     } else if (sizeof(T) == 2 && g.D % 8 == 0 && knob("MMSEG_BRICK2_ZW", 1) == 2) {
       if constexpr (sizeof(T) == 2) {
-        mmseg::note_kernel("conv3_brick2_kernel<BN32,ZW2>");
+        MMSEG_TILE(g, "conv3_brick2_kernel<BN32,ZW2>", 32);
         MMSEG_LAUNCH((conv3_brick2_kernel<T, 32, 2>), dim3(nb1 / 2 * (g.Ncols / 32)), block, 0, s, g);
       }
     } else {
-      mmseg::note_kernel("conv3_brick2_kernel<BN32,ZW1>");
+      MMSEG_TILE(g, "conv3_brick2_kernel<BN32,ZW1>", 32);
       MMSEG_LAUNCH((conv3_brick2_kernel<T, 32, 1>), dim3(nb1 * (g.Ncols / 32)), block, 0, s, g);
     }
     return mmseg::check_launch("conv3_brick2");
@@ -5278,7 +5289,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
       g.D % BRK_Z == 0 && g.H % BRK_Y == 0 && g.W % BRK_X == 0 && g.lda % 8 == 0) {
     const int nb = (g.M / (g.D * g.H * g.W)) * (g.D / BRK_Z) * (g.H / BRK_Y) * (g.W / BRK_X);
     const int bn = (g.Ncols >= 64 && knob("MMSEG_BRICK_BN", 64) == 64) ? 64 : 32;
-    mmseg::note_kernel(bn == 64 ? "conv3_brick_kernel<BN64>" : "conv3_brick_kernel<BN32>");
+    MMSEG_TILE(g, bn == 64 ? "conv3_brick_kernel<BN64>" : "conv3_brick_kernel<BN32>", bn);
     if (bn == 64) {
       MMSEG_LAUNCH((conv3_brick_kernel<T, 64>), dim3(nb * ceil_div(g.Ncols, 64)), block, 0, s, g);
     } else {
@@ -5289,7 +5300,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
   if (MODE == MODE_CONVT_FWD && g.Ncols % 256 == 0 && knob("MMSEG_CONVT_FWD_WIDE", 1)) {
     // BM=64, BN=256: a block writes all 8 taps x 32 (or a quarter of 8 x 128 ...) output channels of its 64 input
     // voxels, so each input row is read by one block instead of by Ncols / 64 column tiles
-    mmseg::note_kernel("conv_gemm_kernel<convT_fwd,64x256>");
+    MMSEG_TILE(g, "conv_gemm_kernel<convT_fwd,64x256>", 256);
     dim3 grid(ceil_div(g.M, 64) * (g.Ncols / 256) * g.ksplit);
     MMSEG_LAUNCH((conv_gemm_kernel<T, MODE, 1, 4, 4, 4>), grid, block, 0, s, g);
     if (mmseg::check_launch("conv_gemm")) return 1;
@@ -5297,7 +5308,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     return 0;
   }
   if (MODE == MODE_CONVT_DGRAD && g.Ncols % 64 == 0 && knob("MMSEG_CONVT_DGRAD_TILE", 0) == 1) {
-    mmseg::note_kernel("conv_gemm_kernel<convT_dgrad,64x64>");
+    MMSEG_TILE(g, "conv_gemm_kernel<convT_dgrad,64x64>", 64);
     dim3 grid(ceil_div(g.M, 64) * (g.Ncols / 64) * g.ksplit);
     MMSEG_LAUNCH((conv_gemm_kernel<T, MODE, 2, 2, 2, 2>), grid, block, 0, s, g);
     if (mmseg::check_launch("conv_gemm")) return 1;
@@ -5305,7 +5316,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     return 0;
   }
   if (MODE == MODE_CONVT_DGRAD && g.Ncols % 128 == 0 && knob("MMSEG_CONVT_DGRAD_TILE", 0) == 2) {
-    mmseg::note_kernel("conv_gemm_kernel<convT_dgrad,64x128>");
+    MMSEG_TILE(g, "conv_gemm_kernel<convT_dgrad,64x128>", 128);
     dim3 grid(ceil_div(g.M, 64) * (g.Ncols / 128) * g.ksplit);
     MMSEG_LAUNCH((conv_gemm_kernel<T, MODE, 1, 4, 4, 2>), grid, block, 0, s, g);
     if (mmseg::check_launch("conv_gemm")) return 1;
@@ -5316,7 +5327,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     // BM=128, BN=96: the 96 / 288 / 480-column 1x1 GEMMs (SwinUNETR's 96-channel stage, the 96 -> 48 residual
     // conv's data gradient) in whole tiles -- BN=64 left a half-empty last column tile that re-read every A row
     if constexpr (MODE == MODE_POINT) {
-      mmseg::note_kernel("conv_gemm_kernel<point,128x96>");
+      MMSEG_TILE(g, "conv_gemm_kernel<point,128x96>", 96);
       dim3 grid(ceil_div(g.M, 128) * (g.Ncols / 96) * g.ksplit);
       MMSEG_LAUNCH((conv_gemm_kernel<T, MODE, 2, 2, 4, 3>), grid, block, 0, s, g);
     }
@@ -5324,14 +5335,14 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     // BM=128, BN=32
     static const char* nm[4] = {"conv_gemm_kernel<conv3,128x32>", "conv_gemm_kernel<point,128x32>",
                                 "conv_gemm_kernel<convT_fwd,128x32>", "conv_gemm_kernel<convT_dgrad,128x32>"};
-    mmseg::note_kernel(nm[MODE]);
+    MMSEG_TILE(g, nm[MODE], 32);
     dim3 grid(ceil_div(g.M, 128) * ceil_div(g.Ncols, 32) * g.ksplit);
     MMSEG_LAUNCH((conv_gemm_kernel<T, MODE, 4, 1, 2, 2>), grid, block, 0, s, g);
   } else {
     // BM=128, BN=64
     static const char* nm[4] = {"conv_gemm_kernel<conv3,128x64>", "conv_gemm_kernel<point,128x64>",
                                 "conv_gemm_kernel<convT_fwd,128x64>", "conv_gemm_kernel<convT_dgrad,128x64>"};
-    mmseg::note_kernel(nm[MODE]);
+    MMSEG_TILE(g, nm[MODE], 64);
     dim3 grid(ceil_div(g.M, 128) * ceil_div(g.Ncols, 64) * g.ksplit);
     MMSEG_LAUNCH((conv_gemm_kernel<T, MODE, 2, 2, 4, 2>), grid, block, 0, s, g);
   }

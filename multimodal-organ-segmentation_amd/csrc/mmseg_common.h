@@ -13,6 +13,8 @@
 #include <hip/hip_ext.h>
 #include <stdint.h>
 #include <stddef.h>
+// the C ABI's declarations: every extern "C" definition in these sources is checked against its prototype
+#include "../../include/mmseg_hip.h"
 
 typedef __bf16 bf16_t;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));

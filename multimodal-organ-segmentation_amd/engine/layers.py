@@ -241,13 +241,20 @@ class Conv3:
             self.rt.lib.mmseg_pack_weight(*d, self.rt.code, self.rt.stream)
 
     def _stem(self, x: Act, y_ld: int) -> bool:
-        """First conv on the packed input: K = 27*Ci real taps*channels (stem.hip)."""
+        """First conv on the packed input: K = 27*Ci real taps*channels (stem.hip).  The 48-output-channel stem is
+        SwinUNETR's bias-free encoder1 conv only: its weight gradient has no bias term, fused statistics or fused
+        norm backward, so a biased 48-channel first conv (a UNet3D / DualEncoder with features[0] = 48) takes the
+        implicit-GEMM path."""
+        if self.Co == 48 and self.conv.bias is not None:
+            return False
         return (not self.need_dgrad and self.Cip == 8 and os.environ.get("MMSEG_STEM", "1") != "0"
                 and bool(self.rt.lib.mmseg_stem_ok(self.Ci, self.Co, x.D, x.H, x.W, x.ld, y_ld)))
 
     def stats_bricks(self, x: Act, y: Act) -> int:
         """Bricks per sample for which fwd() can emit fused InstanceNorm partials (0 = not available)."""
         if self._stem(x, y.ld):
+            if self.Co == 48:   # the 48-channel stem has no fused statistics (power-of-two lane merges only)
+                return 0
             # the stem's epilogue can emit its output's statistics per 64-voxel slice (MMSEG_STEM_STATS=1), but off by
             # default: stem +14.5 us and the slice merge (in_stats_from_bricks, 13,824 slices per sample) 105 us per
             # launch against a 20 + 5 us statistics pass (rocprofv3 r02h)
@@ -751,7 +758,7 @@ class Block:
         """conv1's InstanceNorm backward applied inside the stem weight gradient (no input gradient written):
         conv1 takes the stem path, has no data gradient, and the volume is above the one-launch small-IN size
         (whose backward sums in another order)."""
-        return (os.environ.get("MMSEG_STEM_INB", "1") != "0" and not self.c1.need_dgrad
+        return (os.environ.get("MMSEG_STEM_INB", "1") != "0" and not self.c1.need_dgrad and self.c1.Co != 48
                 and self.x1.V > SMALL_IN_V and self.c1._stem(xin, self.x1.ld))
 
 

@@ -37,7 +37,10 @@ class Act:
     W: int
     # the view owns its rows' padding [off + C, ld) (a buffer of its own, not a slot of a wider concat): passes that
     # write it may write zeros there so the rows are written whole (SwinUNETR's 48 / 96-channel tensors at pitch 64 /
-    # 128; see mmseg_res_apply's Cw)
+    # 128; see mmseg_res_apply's Cw).  CONTRACT: the padding of a whole view holds zeros at all times -- every writer
+    # either writes zeros there or leaves it alone, never another value -- because consumers read it as real K
+    # columns (the zero-padded weight images multiply it) and the fused dx_add epilogue computes dx_pad + 0.
+    # tests/test_swin_unetr_gpu.py::test_swin_whole_act_padding_stays_zero checks it after a forward + backward.
     whole: bool = False
 
     @property
@@ -49,6 +52,13 @@ class Act:
             return self.C
         w = min(self.ld, -(-self.C // 64) * 64)
         return w if w <= 2 * self.C else self.C
+
+    def pad_max_abs(self) -> float:
+        """max |value| in the rows' padding [off + C, ld) over the view's N*V rows (0.0 when there is none)."""
+        if self.off + self.C >= self.ld:
+            return 0.0
+        rows = self.buf[: self.N * self.V * self.ld].view(self.N * self.V, self.ld)
+        return rows[:, self.off + self.C:].float().abs().max().item()
 
     @property
     def V(self) -> int:

@@ -157,6 +157,13 @@ class StepGraphs:
                     tr._buckets.finish()
                 L.mmseg_adamw_dev(ptr(flat.flat), ptr(flat.grad_flat), ptr(m), ptr(v), flat.numel,
                                   ptr(self.hyper_dev), ptr(ws[-1:]), stream_handle())
+        except BaseException:
+            # a capture that fails part-way through the backward (e.g. a collective RCCL cannot capture) has
+            # already decremented bucket counts and stored works / events: drop them so the eager fallback
+            # fires every bucket exactly once
+            if tr._buckets is not None:
+                tr._buckets.reset()
+            raise
         finally:
             if gc_on:
                 gc.enable()

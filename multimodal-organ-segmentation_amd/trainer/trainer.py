@@ -232,6 +232,11 @@ class Trainer:
                 warnings.warn(f"captured data-parallel step failed to capture ({e}); the DP step runs eagerly",
                               RuntimeWarning, stacklevel=2)
                 self._graphs, self._graph_ok = None, False
+                if self._buckets is not None:
+                    # a capture that failed mid-backward left decremented pending counts, stored works and
+                    # events: the eager step must start from a clean bucket state (StepGraphs._capture resets
+                    # too; this covers a failure raised outside it)
+                    self._buckets.reset()
             else:
                 if not sync:
                     self._defer_guard(guard)

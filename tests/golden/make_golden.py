@@ -466,6 +466,49 @@ def dice_heldout_trained_case(K=160, V=16, S=64, lr=2e-3, class_seed=77, feats=(
     np.savez_compressed(os.path.join(OUT, "dice_heldout_trained.npz"), **out)
 
 
+def dice_heldout_envelope_case(threads=(1, 2, 4, 6)):
+    """The reference's own reproducibility envelope for the two free-running held-out Dice checks
+    (test_dice_heldout_gpu.py): the SAME reference runs as dice_heldout_case / dice_heldout_trained_case (stored
+    there at 8 threads, fp32 and fp64), repeated in fp32 at other intra-op thread counts.  Each thread count
+    changes the CPU kernels' summation order (blocked reductions in mkldnn convolutions and the loss), i.e. is
+    another legitimate fp32 ordering of the same algorithm; the spread of held-out Dice over these orderings
+    and fp64 is what a correct fp32 implementation with yet another summation order (the HIP engine) can
+    differ by.  Stored per case: the thread counts and the Dice / train-loss trajectories of each run."""
+    mods = ["CT", "PET"]
+    cases = {"c1": dict(K=16, V=2, S=64, lr=1e-4, feats=[32, 64, 128, 256, 512], class_seed=None),
+             "trained": dict(K=160, V=16, S=64, lr=2e-3, feats=[8, 16, 32, 64, 128], class_seed=77)}
+    out = {"threads": np.array(threads)}
+    for cname, c in cases.items():
+        train = [_phantom_batch(s, c["S"], 3, mods, c["class_seed"]) for s in range(1234, 1234 + c["K"])]
+        val = [_phantom_batch(s, c["S"], 3, mods, c["class_seed"]) for s in range(4321, 4321 + c["V"])]
+        dices, losses = [], []
+        for t in threads:
+            torch.set_num_threads(int(t))
+            cfg = base_config("unet", mods, 3, c["feats"], lr=c["lr"])
+            torch.manual_seed(42)
+            model = build.build_model(cfg)
+            tr = trainer_mod.Trainer(config=cfg, model=model)
+            tr.train_loader, tr.val_loader = train, val
+            recorded = []
+            orig = tr.criterion
+
+            def rec(o, tt, orig=orig, recorded=recorded):
+                lv = orig(o, tt)
+                recorded.append(lv.item())
+                return lv
+            tr.criterion = rec
+            tr._train_epoch()
+            tr.criterion = orig
+            vloss, met = tr._validate()
+            dices.append(met["dice"])
+            losses.append(recorded)
+            print("dice_heldout_envelope", cname, "threads", t, met["dice"], "val loss", vloss, flush=True)
+        out[f"{cname}_f32_dice"] = np.array(dices, dtype=np.float64)
+        out[f"{cname}_f32_train_losses"] = np.array(losses, dtype=np.float64)
+    torch.set_num_threads(8)
+    np.savez_compressed(os.path.join(OUT, "dice_heldout_envelope.npz"), **out)
+
+
 def checkpoint_case():
     """A checkpoint written by the reference (save_checkpoint, build.py:153-180: epoch, model_state_dict,
     optimizer_state_dict (torch AdamW), best_metric, history) after 2 Trainer steps of a small UNet3D

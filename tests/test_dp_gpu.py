@@ -256,23 +256,31 @@ def _rccl_graph_worker(port, q):
             cfg["hardware"]["step_graph"] = True
             cfg["distributed"]["reduce_single_rank"] = dp
             torch.manual_seed(0)
-            orig = SG.StepGraphs._capture
-            if fail:      # a DP capture that fails: the trainer must fall back to the eager DP step
-                def _boom(self, x, y):
-                    raise RuntimeError("injected capture failure")
-                SG.StepGraphs._capture = _boom
+            from mmseg_amd.distributed import ddp
+            orig = ddp.GradBuckets._reduce
+            calls = []
+            if fail:
+                # a DP capture that fails MID-BACKWARD (advisor r05): the first bucket's collective raises inside
+                # the capture, after the engine has already reported gradients; the trainer must fall back to the
+                # eager DP step with a clean bucket state, every bucket reduced exactly once per eager step
+                def _boom(self, b):
+                    if torch.cuda.is_current_stream_capturing():
+                        raise RuntimeError("injected capture failure")
+                    calls.append(b)
+                    return orig(self, b)
+                ddp.GradBuckets._reduce = _boom
             try:
                 model = build_model(cfg)
                 tr = Trainer(cfg, model)
                 losses = [tr.train_step(batches[s % STEPS], s) for s in range(5)]
             finally:
-                SG.StepGraphs._capture = orig
+                ddp.GradBuckets._reduce = orig
             torch.cuda.synchronize()
             w = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()])
             out[tag] = {"losses": losses, "w": w.numpy(),
                         "graphs": len(tr._graphs.graphs) if tr._graphs is not None else -1, "dp": tr.dp,
                         "buckets": 0 if tr._buckets is None else len(tr._buckets.buckets),
-                        "backend": dist.get_backend()}
+                        "backend": dist.get_backend(), "calls": list(calls)}
         dist.destroy_process_group()
         q.put((0, "ok", out))
     except Exception:
@@ -308,5 +316,8 @@ def test_rccl_dp_step_captured_bitwise_equal_to_eager(dev):
     assert np.array_equal(res["graph"]["w"], res["graph_dp"]["w"])
     # a failed first capture of the DP step: eager from then on, bitwise the eager DP run
     assert res["graph_dp_fail"]["graphs"] == -1
+    nb = res["graph_dp_fail"]["buckets"]
+    calls = res["graph_dp_fail"]["calls"]
+    assert sorted(calls) == sorted(list(range(nb)) * 5), "eager DP steps after the failed capture mis-fired buckets"
     assert res["graph_dp_fail"]["losses"] == res["eager_dp"]["losses"]
     assert np.array_equal(res["graph_dp_fail"]["w"], res["eager_dp"]["w"])

@@ -514,6 +514,44 @@ def test_swin_unetr_bf16_close_to_oracle(dev, swin_case):
     assert l2 < 2e-2
 
 
+def _whole_acts(root):
+    """Every Act reachable from the program that owns its padded rows (whole=True, a buffer of its own)."""
+    from mmseg_amd.engine.runtime import Act
+    seen, found, stack = set(), {}, [root]
+    while stack:
+        o = stack.pop()
+        if id(o) in seen or isinstance(o, (torch.Tensor, str, int, float, bool, type(None))):
+            continue
+        seen.add(id(o))
+        if isinstance(o, Act):
+            if o.whole and o.off == 0 and o.ld > o.C:
+                found[id(o)] = o
+            continue
+        if isinstance(o, dict):
+            stack.extend(o.values())
+        elif isinstance(o, (list, tuple)):
+            stack.extend(o)
+        elif hasattr(o, "__dict__") and type(o).__module__.startswith("mmseg_amd.engine"):
+            stack.extend(vars(o).values())
+    return list(found.values())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_swin_whole_act_padding_stays_zero(dev, swin_case, dtype):
+    """Act's whole-row contract (runtime.py, advisor r05): after a forward and a backward every whole=True view's
+    padding [C, ld) is still exactly zero -- no writer (brick2 zcols, brickr, split reduces, the dx_add epilogue,
+    the norm / residual passes) left a non-zero value there."""
+    x, cot = swin_case
+    m = _model(dev, dtype)
+    out = m(x.to(dev))
+    (out * cot.to(dev)).sum().backward()
+    torch.cuda.synchronize()
+    acts = _whole_acts(m.__dict__["_engine"].program)
+    assert len(acts) >= 4, "no whole-row activations found"
+    bad = [(a.C, a.ld, a.D, a.pad_max_abs()) for a in acts if a.pad_max_abs() != 0.0]
+    assert not bad, bad
+
+
 def test_swin_unetr_deterministic_and_features(dev, swin_case):
     x, _ = swin_case
     m = _model(dev, torch.bfloat16)
@@ -952,3 +990,46 @@ def test_head_48_channels_tile(dev, dtype, monkeypatch):
     assert torch.equal(outs[0], outs[1])
     ref = x[:, :Cin].double() @ W.double().t() + b.double()
     assert rel(outs[0].view(C, V).t(), ref) < 1e-5
+
+
+def test_swin_sliding_window_c4_at_size(dev):
+    """BASELINE config c4's inference leg at the config's size (reference trainer.py:370-395, configs/default.yaml
+    inference: roi 96^3, sw_batch 4, overlap 0.5): Trainer._sliding_window_inference on the feature_size 48
+    SwinUNETR over a 2 x 160^3 CT+PET volume (27 overlapping windows per image, batches of 4 crossing the image
+    boundary, a clamped last window per axis), fp32, against the MONAI-algorithm restatement
+    (oracle.sliding_window_inference) driving the SwinUNETR restatement (oracle/swin_oracle.py) in fp32 on the GPU
+    as its predictor.  Both sides differ only by the predictors' fp32 summation orders: 1e-4 normwise (measured
+    ~1e-6).  Parity vs MONAI itself stays unpinned (MONAI absent)."""
+    import os
+    import sys
+    import time
+    sys.path.insert(0, os.path.dirname(os.path.dirname(__file__)))
+    from bench import make_config
+    from mmseg_amd.models.build import build_model
+    from mmseg_amd.trainer.trainer import Trainer
+    from oracle import mmseg_oracle as O
+    cfg = make_config("swin_unetr", 1, "fp32", size=96)
+    cfg["inference"] = {"sliding_window": {"roi_size": [96, 96, 96], "overlap": 0.5}, "batch_size": 4}
+    torch.manual_seed(0)
+    m = build_model(cfg)
+    tr = Trainer(cfg, m)
+    m.eval()
+    g = torch.Generator().manual_seed(160)
+    x = torch.randn(2, 2, 160, 160, 160, generator=g).to(dev)
+    with torch.no_grad():
+        got = tr._sliding_window_inference(x)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        got2 = tr._sliding_window_inference(x)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1e3
+        p = {k: v.detach().float() for k, v in m.backbone.model.named_parameters()}
+        bb = m.backbone
+        ref = O.sliding_window_inference(x, (96, 96, 96), 4,
+                                         lambda b: SO.swin_unetr_forward(p, b, bb.depths, bb.num_heads), 0.5)
+    assert got.shape == (2, 6, 160, 160, 160)
+    assert torch.equal(got, got2)
+    e = rel(got, ref)
+    print(f"\nc4 sliding window 2 x 160^3 (roi 96^3, sw_batch 4, overlap 0.5) fp32 vs oracle: {e:.2e}; "
+          f"{ms:.1f} ms for 2 volumes")
+    assert e < 1e-4
