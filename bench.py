@@ -602,6 +602,9 @@ def main():
                    "parallelism": f"dp{n_gpus}" + ("-rccl-rehearsal" if args.dp_rehearsal else ""),
                    "kernels": args.kernels, "tag": workload_tag(WORKLOAD)},
         "loss": round(loss_val, 5),
+        # the timed steps replay captured graphs (trainer/step_graph.py): how many were captured (0: eager steps)
+        "captured_graphs": (len(trainer._graphs.graphs) + (trainer._graphs.copy_graph is not None))
+        if getattr(trainer, "_graphs", None) is not None else 0,
         "roofline": roofline,
         "cpu_baseline": cpu,
         "kernel_families": families,

@@ -4347,6 +4347,299 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
   }
 }
 
+// ------------------------------------------- row-slab weight gradient (3^3, bf16, 32 co, W % 32 == 0)
+// The 96^3 32-output-channel layers' weight gradient as long-lived blocks that walk columns of x rows.
+// GEMM view: dW[co][ci][tap] = sum_v dy[v][co] x[v + tap][ci].  One MFMA K-slab is 32 CONSECUTIVE x voxels of one
+// (z, y) row.  The B fragment of tap (kz, ky, kx) for the dy row at (z, y) is then the halo row at (z + kz - 1,
+// y + ky - 1) shifted by kx: the same fragment serves every (dy row, kz, ky) pair that lands on the same halo row.
+// A wave owns one kx, one 16-channel ci half and one 16-channel co half (12 waves) and ALL nine (kz, ky) of it, so
+// each halo-row fragment it reads from LDS feeds up to nine MFMAs and each dy fragment (kept in registers while
+// its plane is in the 3-plane tap window) up to nine: ~0.28 LDS fragments per MFMA against 0.65 for the brick
+// kernels (wgrad_brick2 / wgrad_dma: each halo fragment feeds 2 MFMAs, DESIGN (d) 8a).
+// A block owns a contiguous range of dy-plane steps: columns (sample n, 4 y rows, 32 x) walked along z, so a
+// halo plane is staged ONCE per column (6 rows x 34 voxels for 4 x 32 dy voxels: 1.6x the x bytes, against 2.8x
+// for a 4 x 4 x 8 brick's halo).  Step u of a column segment stages halo plane z_a - 1 + u and dy plane z_a + u
+// into one slot of a 4-slot LDS ring by LDS-DMA (buffer_load ... lds; the same 32-B XOR swizzle as wgrad_dma,
+// conflict-free for every kx shift) three steps ahead; the multiply pairs the halo plane with the dy planes
+// u, u - 1, u - 2 (kz = 0, 1, 2), whose fragments rotate through three register sets.  One barrier per step.
+// NORM (deferred InstanceNorm + ReLU of x): each wave normalises, in place, the halo chunks its OWN DMA
+// instructions brought in (its own vmcnt orders them), one step before they are multiplied: no extra barrier.
+// Bias gradient: dy fragments times a ones fragment, dealt round-robin over the six waves of a co half.
+// Partials: the fragment-native layout of wgrad_dma (WReduceArgs::frag_mt = 2), summed by the same reduce.
+constexpr int WROW_RY = 4;                                   // dy rows (y) per plane step
+constexpr int WROW_HY = WROW_RY + 2, WROW_HX = 34;           // halo rows per plane, voxels per halo row
+constexpr int WROW_HI = (WROW_HY * WROW_HX * 4 + 63) / 64;   // halo DMA wave-instructions per plane (13)
+constexpr int WROW_DI = WROW_RY * 32 * 4 / 64;               // dy DMA wave-instructions per plane (8)
+constexpr int WROW_NI = WROW_HI + WROW_DI;                   // 21 per step
+constexpr int WROW_DOFF = WROW_HI * 1024;                    // dy image offset in a slot (bytes)
+constexpr int WROW_SLOT = WROW_NI * 1024;                    // bytes per ring slot
+constexpr int WROW_NST = 4;                                  // ring: computed, two landing, one being issued
+constexpr int WROW_WAVES = 12;                               // (kx, ci half, co half)
+constexpr int WROW_MAXN = 16;                                // samples whose norm statistics fit the LDS table
+
+// a column segment of a block's step range: column col (sample, 4 y rows, 32 x), dy planes [za, za + L)
+struct WRowSeg {
+  int s, col, za, L;
+};
+
+template <bool NORM>
+__global__ __launch_bounds__(768, 1) void wgrad_row_kernel(WgradArgs g) {
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  __shared__ __attribute__((aligned(16))) char ring[WROW_NST * WROW_SLOT];
+  __shared__ __attribute__((aligned(16))) float ntab[NORM ? 2 * WROW_MAXN * CK : 4];
+  __shared__ float bred[WROW_WAVES * 16];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kx = wave >> 2, jh = (wave >> 1) & 1, ih = wave & 1;   // the wave's tap column, ci half, co half
+  const int cin = 8 << g.cpg_shift;
+  const int nchunk = wgrad_nchunk(g.cpg_shift, g.kchunks);
+  const int tile = g.swz ? xcd_swizzle(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int ct = tile % nchunk, ks = tile / nchunk;
+  const int c0 = ct * CK;
+  const int D = g.D, H = g.H, W = g.W;
+  const int ncx = W / 32, ncol = (H / WROW_RY) * ncx;
+  const int N = (int)(g.V / ((long long)D * H * W));
+  const int s_tot = N * ncol * D;
+  const int spb = (s_tot + g.ksplit - 1) / g.ksplit;
+  const int s_begin = min(ks * spb, s_tot), s_end = min(s_begin + spb, s_tot);
+  const bool do_bias = g.bias_part != nullptr && ct == 0;
+  const wd_rsrc_t drsrc = wd_rsrc(g.a, (uint32_t)(g.V * g.lda * 2));
+  const wd_rsrc_t xrsrc = wd_rsrc(g.b, (uint32_t)(g.V * g.ldb * 2));
+
+  // segments and halo steps: a segment of L dy planes takes L + 2 halo steps
+  auto seg_at = [&](int s) __attribute__((always_inline)) {
+    WRowSeg q;
+    q.s = s;
+    q.col = s / D;
+    q.za = s - q.col * D;
+    q.L = min(D, s_end - q.col * D) - q.za;
+    return q;
+  };
+  int h_tot = 0;
+  for (int s = s_begin; s < s_end;) {
+    const WRowSeg q = seg_at(s);
+    h_tot += q.L + 2;
+    s += q.L;
+  }
+
+  // the wave's DMA instructions (m = wave, wave + 12 < WROW_NI): m < WROW_HI halo chunks, else dy chunks.  Per
+  // instruction: the lane's byte offset from the plane origin and its (y, x) position in the plane
+  const int nw = wave + 12 < WROW_NI ? 2 : 1;
+  int rel[2], py[2], px[2], ncc[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int m = wave + 12 * k;
+    rel[k] = 0, py[k] = 0xff, px[k] = 0, ncc[k] = 0;
+    if (m < WROW_HI) {
+      const int p = m * 64 + lane, hy = p / (WROW_HX * 4), r = p - hy * (WROW_HX * 4), xh = r >> 2, cs = r & 3;
+      const int cc = (((cs >> 1) ^ ((xh >> 2) & 1)) << 1) | (cs & 1);
+      if (hy < WROW_HY) {
+        rel[k] = ((hy * W + xh) * g.ldb + c0 + cc * 8) * 2;
+        py[k] = hy, px[k] = xh, ncc[k] = cc;
+      }
+    } else if (m < WROW_NI) {
+      const int p = (m - WROW_HI) * 64 + lane, ry = p >> 7, r = p & 127, x = r >> 2, cs = r & 3;
+      const int cc = (((cs >> 1) ^ ((x >> 2) & 1)) << 1) | (cs & 1);
+      rel[k] = ((ry * W + x) * g.lda + cc * 8) * 2;
+    }
+  }
+  // DMA of halo step (segment q, step u) into ring slot `slot`
+  auto issue = [&](int slot, const WRowSeg& q, int u) __attribute__((always_inline)) {
+    const int n = q.col / ncol, cr = q.col - n * ncol, by = cr / ncx;
+    const int y0 = by * WROW_RY, x0 = (cr - by * ncx) * 32;
+    const int zh = q.za - 1 + u, zd = q.za + u;
+    const bool zh_ok = (unsigned)zh < (unsigned)D, zd_ok = u < q.L;
+    const int hb = (((n * D + zh) * H + (y0 - 1)) * W + (x0 - 1)) * g.ldb * 2;
+    const int db = (((n * D + zd) * H + y0) * W + x0) * g.lda * 2;
+    const uint32_t lbase = (uint32_t)(uintptr_t)(lds_ptr_t)(ring + slot * WROW_SLOT);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int m = wave + 12 * k;
+      if (m < WROW_HI) {
+        const int y = y0 - 1 + py[k], x = x0 - 1 + px[k];
+        const bool ok = zh_ok && py[k] != 0xff && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+        wd_dma16(__builtin_amdgcn_readfirstlane(lbase + m * 1024), ok ? (uint32_t)(hb + rel[k]) : WD_OOB, xrsrc);
+      } else if (m < WROW_NI) {
+        wd_dma16(__builtin_amdgcn_readfirstlane(lbase + m * 1024), zd_ok ? (uint32_t)(db + rel[k]) : WD_OOB, drsrc);
+      }
+    }
+  };
+  auto wait_cnt = [&](int cnt) __attribute__((always_inline)) {
+    switch (cnt) {
+#define MMSEG_WR_WAIT(N) \
+  case N: __builtin_amdgcn_s_waitcnt(0x0f70 | N); break;
+      MMSEG_WR_WAIT(1) MMSEG_WR_WAIT(2) MMSEG_WR_WAIT(3) MMSEG_WR_WAIT(4) MMSEG_WR_WAIT(5) MMSEG_WR_WAIT(6)
+#undef MMSEG_WR_WAIT
+      default: __builtin_amdgcn_s_waitcnt(0x0f70); break;
+    }
+  };
+  // NORM: relu((x - mean) * rstd) of the in-volume halo chunks this wave's own DMA brought into `slot`
+  auto normalize = [&](int slot, const WRowSeg& q, int u) __attribute__((always_inline)) {
+    if constexpr (NORM) {
+      const int n = q.col / ncol, cr = q.col - n * ncol, by = cr / ncx;
+      const int y0 = by * WROW_RY, x0 = (cr - by * ncx) * 32;
+      const int zh = q.za - 1 + u;
+      if ((unsigned)zh >= (unsigned)D) return;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int m = wave + 12 * k;
+        if (m < WROW_HI) {
+          const int y = y0 - 1 + py[k], x = x0 - 1 + px[k];
+          if (py[k] != 0xff && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) {
+            bf16_t* p = reinterpret_cast<bf16_t*>(ring + slot * WROW_SLOT + m * 1024 + lane * 16);
+            const float4* mu4 = reinterpret_cast<const float4*>(ntab + n * CK + ncc[k] * 8);
+            const float4* rs4 = reinterpret_cast<const float4*>(ntab + WROW_MAXN * CK + n * CK + ncc[k] * 8);
+            const float4 ma = mu4[0], mb = mu4[1], ra = rs4[0], rb = rs4[1];
+            const float mu[8] = {ma.x, ma.y, ma.z, ma.w, mb.x, mb.y, mb.z, mb.w};
+            const float rs[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+            V8<bf16_t> v;
+            v.load(p);
+            norm_relu8<bf16_t>(v, mu, rs);
+            v.store(p);
+          }
+        }
+      }
+    }
+  };
+
+  // fragments: lane rows x = v0 and v0 + 8 of a 32-voxel row (wgrad_dma's lane order), granule swizzle (x >> 2) & 1
+  const int g4 = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
+  const int v0 = 16 * (g4 >> 1) + 4 * (g4 & 1) + q4;
+  const int aoff = WROW_DOFF + v0 * 64 + 32 * (ih ^ (g4 & 1)) + 8 * p4;                      // + ry * 2048
+  const int boff = (v0 + kx) * 64 + 32 * (jh ^ (((v0 + kx) >> 2) & 1)) + 8 * p4;            // + hy * 2176
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+  f32x4 acc[3][3], accb = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  bf16x8 areg[3][WROW_RY];   // dy fragments of the three dy planes in the tap window (register set = plane % 3)
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int r = 0; r < WROW_RY; ++r) areg[a][r] = ones;
+
+  if (s_begin < s_end) {
+    if constexpr (NORM) {
+      for (int e = tid; e < N * CK; e += 768) {
+        const int n = e / CK, c = e - n * CK;
+        ntab[n * CK + c] = g.nmean[n * cin + c0 + c];
+        ntab[WROW_MAXN * CK + n * CK + c] = g.nrstd[n * cin + c0 + c];
+      }
+      __syncthreads();
+    }
+    // prologue: halo steps 0 .. NST - 2 issued; the DMA cursor (dq, du) points at the next step to issue
+    WRowSeg dq = seg_at(s_begin);
+    int du = 0;
+    auto dma_next = [&]() __attribute__((always_inline)) {
+      if (++du == dq.L + 2) {
+        du = 0;
+        if (dq.s + dq.L < s_end) dq = seg_at(dq.s + dq.L);
+      }
+    };
+    int h_iss = 0;
+    for (; h_iss < WROW_NST - 1 && h_iss < h_tot; ++h_iss) {
+      issue(h_iss % WROW_NST, dq, du);
+      dma_next();
+    }
+    wait_cnt(nw * (min(h_tot - 1, WROW_NST - 2)));
+    normalize(0, seg_at(s_begin), 0);
+    __syncthreads();
+
+    int h = 0;
+    // one halo step: issue step h + NST - 1, multiply step h, normalise step h + 1, barrier
+    auto step = [&](auto phc, const WRowSeg& q, int u) __attribute__((always_inline)) {
+      constexpr int PH = decltype(phc)::value;
+      if (h_iss < h_tot) {
+        issue(h_iss % WROW_NST, dq, du);
+        dma_next();
+        ++h_iss;
+      }
+      const char* S = ring + (h % WROW_NST) * WROW_SLOT;
+      bf16x8 bfr[WROW_HY];
+#pragma unroll
+      for (int hy = 0; hy < WROW_HY; ++hy) {
+        const bf16_t* pl = reinterpret_cast<const bf16_t*>(S + hy * (WROW_HX * 64) + boff);
+        bfr[hy] = tr_frag(pl, pl + 8 * 32);
+      }
+      const bool anew = u < q.L;
+      if (anew) {
+#pragma unroll
+        for (int r = 0; r < WROW_RY; ++r) {
+          const bf16_t* pa = reinterpret_cast<const bf16_t*>(S + r * (32 * 64) + aoff);
+          areg[PH][r] = tr_frag(pa, pa + 8 * 32);
+        }
+      }
+      auto mm = [&](auto kzc, const bf16x8(&a)[WROW_RY]) __attribute__((always_inline)) {
+        constexpr int KZ = decltype(kzc)::value;
+#pragma unroll
+        for (int hy = 0; hy < WROW_HY; ++hy)
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky) {
+            const int ry = hy - ky;
+            if (ry >= 0 && ry < WROW_RY)
+              acc[KZ][ky] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ry], bfr[hy], acc[KZ][ky], 0, 0, 0);
+          }
+      };
+      // kz = 2: dy plane u - 2 (register set (PH + 1) % 3), kz = 1: plane u - 1 ((PH + 2) % 3), kz = 0: plane u
+      if (u >= 2) mm(std::integral_constant<int, 2>{}, areg[(PH + 1) % 3]);
+      if (u >= 1 && u <= q.L) mm(std::integral_constant<int, 1>{}, areg[(PH + 2) % 3]);
+      if (anew) {
+        mm(std::integral_constant<int, 0>{}, areg[PH]);
+        if (do_bias && h % 6 == kx * 2 + jh) {
+#pragma unroll
+          for (int r = 0; r < WROW_RY; ++r) accb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(areg[PH][r], ones, accb, 0, 0, 0);
+        }
+      }
+      // step h + 1 landed (this wave's part), normalised, then visible to all after the barrier
+      wait_cnt(nw * (min(h_tot - 1, h + WROW_NST - 1) - (h + 1)));
+      if (h + 1 < h_tot) {
+        if (u + 1 < q.L + 2)
+          normalize((h + 1) % WROW_NST, q, u + 1);
+        else if (q.s + q.L < s_end)
+          normalize((h + 1) % WROW_NST, seg_at(q.s + q.L), 0);
+      }
+      __syncthreads();
+      ++h;
+    };
+    for (int s = s_begin; s < s_end;) {
+      const WRowSeg q = seg_at(s);
+      for (int u0 = 0; u0 < q.L + 2; u0 += 3) {
+        step(std::integral_constant<int, 0>{}, q, u0);
+        if (u0 + 1 < q.L + 2) step(std::integral_constant<int, 1>{}, q, u0 + 1);
+        if (u0 + 2 < q.L + 2) step(std::integral_constant<int, 2>{}, q, u0 + 2);
+      }
+      s += q.L;
+    }
+  }
+
+  // split partials in wgrad_dma's fragment-native layout: (tap, co tile, ci tile) fragments of 1 KB
+  float* base = g.part + (long long)ks * g.Ca * g.Ncols + (long long)ct * (32 * 27 * CK);
+#pragma unroll
+  for (int kz = 0; kz < 3; ++kz)
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int tap = kz * 9 + ky * 3 + kx;
+      *reinterpret_cast<f32x4*>(base + ((tap * 2 + ih) * 2 + jh) * 256 + lane * 4) = acc[kz][ky];
+    }
+  if (do_bias) {
+    // accb[r] on lanes i16 == 0: sum over this wave's share of the voxels of dy[.][16 ih + 4 g4 + r]
+    if (i16 == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bred[wave * 16 + 4 * g4 + r] = accb[r];
+    }
+    __syncthreads();
+    if (tid < 32) {
+      const int i = tid >> 4;
+      float sacc = 0.f;
+      for (int w = i; w < WROW_WAVES; w += 2) sacc += bred[w * 16 + (tid & 15)];
+      g.bias_part[(long long)ks * g.Ca + tid] = sacc;
+    }
+  }
+}
+
 // ------------------------------------- runtime-brick wgrad (small volumes)
 // wgrad_brick2_kernel for volumes whose sides are not multiples of (4, 4, 8)
 // (the 12^3 and 6^3 levels): brick (bz, by, bx) chosen on the host, <= 128
@@ -5376,6 +5669,15 @@ int wgrad_dma_mt(const WgradArgs& g, int elem_bytes) {
   return dma ? (wgrad_co64(g.Ca, g.V, 2) ? 4 : 2) : 0;
 }
 
+// the row-slab weight gradient (wgrad_row_kernel) takes the shape: bf16 3^3, 32 output channels, W % 32 == 0,
+// H % 4 == 0, split partials (no direct gradient, no groups, no padded rows), 32-bit DMA offsets
+bool wgrad_row_ok(const WgradArgs& g, int elem_bytes) {
+  return elem_bytes == 2 && knob("MMSEG_WGRAD_ROW", 1) && g.brick == 2 && g.Ca == 32 && g.W % 32 == 0 &&
+         g.H % WROW_RY == 0 && (8 << g.cpg_shift) % CK == 0 && g.groups == 0 && !g.pad16 && g.ksplit > 1 &&
+         g.V * g.lda * 2 < (1LL << 31) && g.V * g.ldb * 2 < (1LL << 31) && g.lda % 8 == 0 && g.ldb % 8 == 0 &&
+         g.V / ((long long)g.D * g.H * g.W) <= WROW_MAXN;
+}
+
 template <typename T, int MODE>
 int launch_wgrad(WgradArgs g, hipStream_t s) {
 #ifdef MMSEG_TIMING_PROBES
@@ -5412,6 +5714,18 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
           MMSEG_LAUNCH((wgrad_brickr_kernel<T, 2>), grid, dim3(512), 0, s, g, wb.bz, wb.by, wb.bx);
       }
       return mmseg::check_launch("wgrad_brickr");
+    }
+    if (MODE == MODE_CONV3 && g.brick == 2 && wgrad_row_ok(g, (int)sizeof(T))) {
+      MMSEG_REQUIRE(g.frag, "wgrad_row: fragment-native partials only");
+      const dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * g.ksplit);
+      if (g.nmean) {
+        mmseg::note_kernel("wgrad_row_kernel<CO32,NORM>");
+        MMSEG_LAUNCH((wgrad_row_kernel<true>), grid, dim3(768), 0, s, g);
+      } else {
+        mmseg::note_kernel("wgrad_row_kernel<CO32>");
+        MMSEG_LAUNCH((wgrad_row_kernel<false>), grid, dim3(768), 0, s, g);
+      }
+      return mmseg::check_launch("wgrad_row");
     }
     if (MODE == MODE_CONV3 && g.brick == 2) {
       const bool v3 = knob("MMSEG_WGRAD_V3", 1) != 0;
@@ -6364,7 +6678,11 @@ int conv3_wgrad_impl(const void* dy, int lddy, const void* x, int ldx, const flo
               knob("MMSEG_WGRAD_SWIZZLE", 1), p.kind, p.direct ? grad : nullptr, p.direct ? bias_grad : nullptr,
               accumulate, wgrad_kchunks(Cip, Ci), nmean, nrstd};
   hipStream_t s = (hipStream_t)stream;
-  const int fmt = knob("MMSEG_WGRAD_FRAG", 1) ? wgrad_dma_mt(g, dtype == MMSEG_BF16 ? 2 : 4) : 0;
+  g.groups = groups > 1 ? groups : 0;
+  g.pad16 = (phase & 8) ? 1 : 0;
+  // the row-slab kernel writes fragment-native partials only (2 co tiles of 16)
+  const int fmt = wgrad_row_ok(g, dtype == MMSEG_BF16 ? 2 : 4) ? 2
+                  : knob("MMSEG_WGRAD_FRAG", 1) ? wgrad_dma_mt(g, dtype == MMSEG_BF16 ? 2 : 4) : 0;
   g.frag = fmt > 0;
   g.groups = groups > 1 ? groups : 0;
   g.grad_gstride = grad_gstride;

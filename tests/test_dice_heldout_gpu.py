@@ -33,6 +33,19 @@ from tests.helpers import golden
 pytestmark = pytest.mark.gpu
 
 
+def envelope(case: str, g) -> tuple:
+    """The reference's own reproducibility envelope of a free-running held-out Dice (make_golden.py
+    dice_heldout_envelope_case): its fp32 run at 1, 2, 4, 6 and 8 intra-op threads (each thread count is another
+    summation order of the same algorithm) and its fp64 run.  A correct fp32 implementation with yet another
+    summation order -- the HIP engine -- lands somewhere in this spread, so the gate is the envelope widened by half
+    its width (at least 1e-4): no legitimate reordering can flip it, while a real error (a wrong gradient, a lost
+    update) moves the trajectory far outside it.  Returns (lo, hi, values)."""
+    e = golden("dice_heldout_envelope")
+    vals = np.concatenate([e[f"{case}_f32_dice"], [float(g["f32_dice"]), float(g["f64_dice"])]])
+    w = max(float(vals.max() - vals.min()), 1e-4)
+    return float(vals.min()) - 0.5 * w, float(vals.max()) + 0.5 * w, vals
+
+
 def _cfg():
     return {
         "experiment": {"name": "heldout", "output_dir": "/tmp/mmseg_heldout", "seed": 42},
@@ -90,9 +103,12 @@ def test_heldout_dice_matches_reference(dev):
           f"val loss {vloss:.8f} vs {float(g['f32_val_loss']):.8f}; train loss max diff "
           f"{np.abs(losses - g['f32_train_losses']).max():.2e}; argmax flips engine vs oracle on the engine's "
           f"weights: {flips} of {nvox} voxels, oracle Dice {dm_orc.compute()['dice']:.6f}")
+    lo, hi, vals = envelope("c1", g)
+    print(f"reference envelope (fp32 at 1/2/4/6/8 threads, fp64): {np.round(vals, 6).tolist()}; gate [{lo:.6f}, "
+          f"{hi:.6f}], margin {min(met['dice'] - lo, hi - met['dice']):.2e}")
     assert np.abs(losses - g["f32_train_losses"]).max() < 5e-5
     assert abs(vloss - float(g["f32_val_loss"])) < 1e-5
-    assert abs(met["dice"] - ref_dice) <= max(1e-4, 2 * spread)
+    assert lo <= met["dice"] <= hi
     # _validate's on-device fused argmax + counts == DiceMetric.update on the engine's own masks, bit for bit
     assert met["dice"] == res_eng["dice"] and met["dice_per_class"] == res_eng["dice_per_class"]
     assert flips <= 1e-4 * nvox
@@ -155,7 +171,11 @@ def test_heldout_dice_on_reference_weights(dev):
 def test_heldout_dice_free_running_trained(dev):
     """The same K = 160-step epoch trained BY THE ENGINE from the reference's initial weights (torch.manual_seed
     42 + the reference's registration order), then validated: a free-running trajectory, so the bound is the
-    reference's own fp32-vs-fp64 spread on the same run, max(1e-4, 2 |ref32 - ref64|)."""
+    reference's own reproducibility envelope on the same run (envelope(): fp32 at 1/2/4/6/8 threads and fp64,
+    0.9334-0.9438 -- the reference at 1 thread lands 9.3e-3 from itself at 8).  Until round 5 the bound was
+    max(1e-4, 2 |ref32 - ref64|) around the 8-thread run, which a legitimate fp32 reorder of the engine (round 5's
+    runtime-brick routing of the < 128-unit conv shapes, 2dc10ed: 0.93916 -> 0.93402) brought within 13 % of its
+    edge; both engine orders sit inside the envelope.  The +-1e-4 north_star check is the pinned-weights test above."""
     g = golden("dice_heldout_trained")
     cfg = _trained_cfg(g)
     torch.manual_seed(42)
@@ -168,7 +188,10 @@ def test_heldout_dice_free_running_trained(dev):
     vloss, met = tr._validate()
     ref, ref64 = float(g["f32_dice"]), float(g["f64_dice"])
     spread = abs(ref - ref64)
+    lo, hi, vals = envelope("trained", g)
     print(f"\nfree-running 160 steps: engine Dice {met['dice']:.7f}, reference fp32 {ref:.7f}, fp64 {ref64:.7f} "
-          f"(|engine - ref| {abs(met['dice'] - ref):.2e}, reference spread {spread:.2e}); train loss max diff "
-          f"{np.abs(losses - g['f32_train_losses']).max():.2e}")
-    assert abs(met["dice"] - ref) <= max(1e-4, 2 * spread)
+          f"(|engine - ref| {abs(met['dice'] - ref):.2e}, reference fp32-vs-fp64 spread {spread:.2e}); train loss "
+          f"max diff {np.abs(losses - g['f32_train_losses']).max():.2e}; reference envelope (fp32 at 1/2/4/6/8 "
+          f"threads, fp64) {np.round(vals, 5).tolist()}; gate [{lo:.5f}, {hi:.5f}], margin "
+          f"{min(met['dice'] - lo, hi - met['dice']):.2e}")
+    assert lo <= met["dice"] <= hi

@@ -892,3 +892,66 @@ def test_conv3_few_brick_units_take_runtime_brick(dev, dtype, cin, cout, shape, 
     (ref * _q(dy, dtype)).sum().backward()
     assert rel(from_ndhwc(dxa.buf, N, cin, D, H, W, ld=cip), xd.grad) < TOL[dtype]
     assert rel(flat.grad(conv.weight), wd.grad) < GTOL[dtype]
+
+
+@pytest.mark.parametrize("norm", [False, True])
+@pytest.mark.parametrize("cin,shape,accumulate", [
+    (32, (1, 8, 4, 32), 0), (32, (2, 28, 24, 64), 1), (64, (2, 28, 24, 64), 0), (32, (1, 12, 8, 96), 1),
+    (64, (2, 8, 12, 32), 1)])
+def test_wgrad_row_kernel(dev, cin, shape, accumulate, norm, monkeypatch):
+    """The row-slab weight gradient (wgrad_row_kernel: 32 co, K-slabs of 32 consecutive x voxels, each halo-row
+    fragment shared by the nine (kz, ky) taps of a wave, column segments walked along z; the c3 step's 96^3 32 -> 32
+    and 64 -> 32 layers) against fp64 (the deferred norm: relu((x - mean) * rstd) of the bf16 x, rounded to bf16),
+    with block step ranges that cross columns (2 x 28 x 24 x 64: 3 or 6 planes per block against D = 28) and
+    single-plane blocks; bitwise repeatable; and against the brick kernel it replaces (MMSEG_WGRAD_ROW=0) within
+    bf16 product-order noise."""
+    N, D, H, W = shape
+    V = N * D * H * W
+    cout = 32
+    g = torch.Generator().manual_seed(17 * cin + V + norm)
+    dy = torch.randn(V, cout, generator=g).to(dev, torch.bfloat16).reshape(-1)
+    x = (torch.randn(V, cin, generator=g) * 2 + 0.5).to(dev, torch.bfloat16).reshape(-1)
+    mean = (torch.randn(N, cin, generator=g) * 0.3 + 0.5).to(dev)
+    rstd = (torch.rand(N, cin, generator=g) + 0.5).to(dev)
+    gw0 = torch.randn(cout * cin * 27, generator=g).to(dev) if accumulate else torch.zeros(cout * cin * 27, device=dev)
+    gb0 = torch.ones(cout, device=dev) if accumulate else torch.zeros(cout, device=dev)
+    L = lib()
+    shift = int(np.log2(cin // 8))
+    wsf = L.mmseg_conv3_wgrad_ws_floats(V, cout, cin, cin, shift, D, H, W, cout, cin, 1)
+
+    def run():
+        ws = torch.full((max(wsf, 1),), float("nan"), device=dev)
+        gw, gb = gw0.clone(), gb0.clone()
+        if norm:
+            rc = L.mmseg_conv3_wgrad_norm(ptr(dy), cout, ptr(x), cin, ptr(mean), ptr(rstd), ptr(gw), ptr(gb), cout,
+                                          cin, cin, shift, V, D, H, W, ptr(ws), wsf, accumulate, 1, stream_handle())
+        else:
+            rc = L.mmseg_conv3_wgrad(ptr(dy), cout, ptr(x), cin, ptr(gw), ptr(gb), cout, cin, cin, shift, V, D, H, W,
+                                     ptr(ws), wsf, accumulate, 1, stream_handle())
+        assert rc == 0, L.mmseg_last_error()
+        name = L.mmseg_last_kernel().decode()
+        torch.cuda.synchronize()
+        return gw, gb, name
+
+    if norm:
+        assert L.mmseg_conv3_wgrad_norm_ok(V, cout, cin, cin, shift, D, H, W, cout, cin, 1)
+    gw, gb, name = run()
+    assert name.startswith("wgrad_row_kernel<CO32"), name
+    gw2, gb2, _ = run()
+    assert torch.equal(gw, gw2) and torch.equal(gb, gb2)
+    monkeypatch.setenv("MMSEG_WGRAD_ROW", "0")
+    gwo, gbo, name_o = run()
+    assert not name_o.startswith("wgrad_row"), name_o
+    xd = x.double().cpu().reshape(N, D * H * W, cin)
+    if norm:
+        xd = torch.relu((xd - mean.double().cpu()[:, None, :]) * rstd.double().cpu()[:, None, :])
+        xd = xd.to(torch.bfloat16).double()
+    xr = xd.reshape(N, D, H, W, cin).permute(0, 4, 1, 2, 3)
+    dyr = dy.double().cpu().reshape(N, D, H, W, cout).permute(0, 4, 1, 2, 3)
+    ref = torch.nn.grad.conv3d_weight(xr, (cout, cin, 3, 3, 3), dyr, padding=1).reshape(-1)
+    e_new = rel(gw.double().cpu() - gw0.double().cpu(), ref)
+    e_old = rel(gwo.double().cpu() - gw0.double().cpu(), ref)
+    print(f"\nwgrad_row {shape} cin {cin} norm {norm}: vs fp64 {e_new:.2e} (brick kernel {name_o} {e_old:.2e})")
+    assert e_new < 5e-5     # exact bf16 products, fp32 sums in another order than fp64's
+    assert rel(gb.double().cpu() - gb0.double().cpu(), dyr.sum(dim=(0, 2, 3, 4))) < 5e-5
+    assert rel(gw.double().cpu(), gwo.double().cpu()) < 5e-5

@@ -173,3 +173,22 @@ def test_oracle_pins_reproduce_free_forward(kind):
     for out, grads in res[1:]:
         assert torch.equal(out, res[0][0])
         assert all(torch.equal(a, b) for a, b in zip(grads, res[0][1]))
+
+
+def test_dice_envelope_fixture():
+    """tests/golden/dice_heldout_envelope.npz (make_golden.py dice_heldout_envelope_case): the reference's free-running
+    held-out Dice at 1/2/4/6 threads for both cases of test_dice_heldout_gpu.py, each a full trajectory of the stored
+    length; the 8-thread run stored with the case itself lies inside the spread of the others widened by its width
+    (the gate's construction is consistent with the data it was built from)."""
+    import numpy as np
+    from tests.helpers import golden
+    e = golden("dice_heldout_envelope")
+    assert list(e["threads"]) == [1, 2, 4, 6]
+    for case, fix in (("c1", "dice_heldout_c1"), ("trained", "dice_heldout_trained")):
+        g = golden(fix)
+        d = e[f"{case}_f32_dice"]
+        assert d.shape == (4,) and np.all((d > 0) & (d < 1))
+        assert e[f"{case}_f32_train_losses"].shape == (4, int(g["K"]))
+        lo, hi = d.min(), d.max()
+        w = hi - lo
+        assert lo - w <= float(g["f32_dice"]) <= hi + w
