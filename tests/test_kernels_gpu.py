@@ -952,6 +952,8 @@ def test_wgrad_row_kernel(dev, cin, shape, accumulate, norm, monkeypatch):
     e_new = rel(gw.double().cpu() - gw0.double().cpu(), ref)
     e_old = rel(gwo.double().cpu() - gw0.double().cpu(), ref)
     print(f"\nwgrad_row {shape} cin {cin} norm {norm}: vs fp64 {e_new:.2e} (brick kernel {name_o} {e_old:.2e})")
-    assert e_new < 5e-5     # exact bf16 products, fp32 sums in another order than fp64's
+    # exact bf16 products, fp32 sums in another order than fp64's; with the norm, the fp64 reference's own rounding
+    # of relu((x - mean) * rstd) to bf16 differs from the fp32 one in a few elements (both kernels measure 1.2e-4)
+    assert e_new < (GTOL[torch.bfloat16] if norm else 5e-5)
     assert rel(gb.double().cpu() - gb0.double().cpu(), dyr.sum(dim=(0, 2, 3, 4))) < 5e-5
     assert rel(gw.double().cpu(), gwo.double().cpu()) < 5e-5
