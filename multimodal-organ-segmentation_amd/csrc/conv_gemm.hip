@@ -103,10 +103,7 @@ struct GemmArgs {
   const float* inmean;
   const float* inrstd;
   float* inpart;
-  // wave priority experiments (MMSEG_PRIO, A/B only): bit 0 = brick8 waves 4-7 at s_setprio 1 (the second-dispatched
-  // half of an 8-wave block loses every issue arbitration to its SIMD partner); bit 1 = s_setprio 1 around the tap
-  // loop's MFMAs (brick2 / brick8), so a co-resident wave in its staging phase yields issue to the MFMA stream
-  int prio;
+  int prio;   // (unused: the s_setprio experiments of round 3 measured +-2 % and were removed)
   // fp8 forward (brick6 F8, mmseg_conv3_fwd_fp8): b holds e4m3 weights w * s[co] (s = 448 / max |w[co]|), wdq[co] =
   // 1 / s[co] restores the scale in the epilogue; the staged activations are e4m3 at unit scale
   const float* wdq;
@@ -804,7 +801,6 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kern
       load_w(cn, kzn);
       if (kzn == 0) load_x(cn);
     }
-    if (g.prio & 2) __builtin_amdgcn_s_setprio(1);
     if constexpr (PF) {
       // fragments of tap t+1 are read while tap t's MFMAs run (one wave per SIMD cannot hide the LDS latency
       // behind another wave's MFMAs)
@@ -843,7 +839,6 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick2_kern
           for (int j = 0; j < RN; ++j) mfma_step<T>(acc[i][j], af[i], bf[j]);
       }
     }
-    if (g.prio & 2) __builtin_amdgcn_s_setprio(0);
     PROBE_T();
     __syncthreads();
     if (more) {
@@ -941,22 +936,17 @@ __device__ __forceinline__ void buf_load_v8<float>(V8<float>& v, __amdgpu_buffer
   }
 }
 
-// WDB (MMSEG_BRICK3_WDB=1; measured 1 % slower, off): the weight stage is double-buffered in LDS (2 x 18 KB
-// for BN32 bf16; 2 blocks/CU still fit), so a stage that only swaps weights needs one barrier (after its
-// stores) instead of two; a stage that also replaces the halo keeps the barrier before its stores.
-// (sched_group_barrier interleaving of the fragment reads with the MFMAs measured 8-13 % slower.)
-// XP: the next halo chunk (or the next unit's first chunk) is loaded into registers at the FIRST stage of
-// the current chunk instead of its last, so its HBM latency is hidden behind three stages of MFMAs instead
-// of one (the registers are free from the current chunk's LDS store on; no extra VGPRs).  MMSEG_BRICK3_XP=1;
-// measured 4 % slower on the bench (q13), so off.
-template <typename T, int BN, bool WU = false, bool WDB = false, bool XP = false>
+// Measured and removed (round 6 knob pruning; numbers in DESIGN): a double-buffered weight stage (1 % slower),
+// the next halo chunk loaded at the first stage of the current one (4 % slower on the bench), unconditional
+// clamped weight loads, and sched_group_barrier interleaving of the fragment reads (8-13 % slower).
+template <typename T, int BN>
 __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kernel(GemmArgs g, int upb) {
   using L = Brick2Layout<T>;
   constexpr int BZ = 4, HZ = BZ + 2;
   constexpr int RM = 4, RN = BN / 16;
   constexpr int XQ = HZ * L::RZ;
   constexpr int WQ = 9 * BN * L::QV;
-  __shared__ __attribute__((aligned(16))) float4 lds4[XQ + (WDB ? 2 : 1) * WQ];
+  __shared__ __attribute__((aligned(16))) float4 lds4[XQ + WQ];
   T* Xl = reinterpret_cast<T*>(lds4);
   T* Wl = reinterpret_cast<T*>(lds4 + XQ);
   constexpr int EPQ = 16 / sizeof(T);
@@ -1043,8 +1033,8 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kern
 #pragma unroll
     for (int k = 0; k < W_PER; ++k) {
       const int e0 = tid + k * 256;
-      if (WU || e0 < W_ITEMS) {
-        const int e = WU ? min(e0, W_ITEMS - 1) : e0;
+      if (e0 < W_ITEMS) {
+        const int e = e0;
         const int cgw = e & 3, q = e >> 2;
         const int col = q % BN, t9 = q / BN;
         const int kgi = (kz * 9 + t9) * (cin / 8) + c * 4 + cgw;
@@ -1052,13 +1042,13 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kern
       }
     }
   };
-  auto store_w = [&](int wbuf) {
-    T* Wd = Wl + wbuf * WQ * EPQ;
+  auto store_w = [&]() {
+    T* Wd = Wl;
 #pragma unroll
     for (int k = 0; k < W_PER; ++k) {
       const int e0 = tid + k * 256;
-      if (WU || e0 < W_ITEMS) {
-        const int e = WU ? min(e0, W_ITEMS - 1) : e0;
+      if (e0 < W_ITEMS) {
+        const int e = e0;
         const int cgw = e & 3, q = e >> 2;
         wr[k].store(Wd + (q * L::QV + (cgw ^ w2_swz(q)) * L::QG) * EPQ);
       }
@@ -1085,9 +1075,8 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kern
   load_x(0);
   load_w(cur.n0, 0, 0);
   store_x();
-  store_w(0);
+  store_w();
   __syncthreads();
-  int wb = 0;    // weight buffer of the current stage (WDB)
   for (int u = u_begin; u < u_end; ++u) {
     f32x4 acc[RM][RN];
 #pragma unroll
@@ -1104,17 +1093,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kern
       const bool more = !last || unext;
       const int sn = last ? 0 : st + 1;
       const int cn = sn / 3, kzn = sn - cn * 3;
-      if constexpr (XP) {
-        if (kz == 0) {
-          if (c + 1 < nchunk) {
-            load_x(c + 1);
-          } else if (unext) {
-            set_x(nxt);
-            load_x(0);
-          }
-        }
-        if (more) load_w(last ? nxt.n0 : cur.n0, cn, kzn);
-      } else if (more) {
+      if (more) {
         if (last) set_x(nxt);
         load_w(last ? nxt.n0 : cur.n0, cn, kzn);
         if (kzn == 0) load_x(cn);
@@ -1125,7 +1104,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kern
         const int hoff = kz * L::RZ + ky * L::RY + kx * L::QV;
         V8<T> af[RM], bf[RN];
 #pragma unroll
-        for (int j = 0; j < RN; ++j) bf[j].load(Wl + (wb * WQ + t9 * BN * L::QV + bq[j]) * EPQ);
+        for (int j = 0; j < RN; ++j) bf[j].load(Wl + (t9 * BN * L::QV + bq[j]) * EPQ);
 #pragma unroll
         for (int i = 0; i < RM; ++i) af[i].load(Xl + (aq[i] + hoff) * EPQ);
 #pragma unroll
@@ -1133,25 +1112,11 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3_brick3_kern
 #pragma unroll
           for (int j = 0; j < RN; ++j) mfma_step<T>(acc[i][j], bf[j], af[i]);   // transposed: rows = channels
       }
-      if constexpr (WDB) {
-        // the other weight buffer was last read in the previous stage, which every wave finished before
-        // that stage's closing barrier; only a halo swap must wait for this stage's readers
-        if (more) {
-          if (kzn == 0) {
-            __syncthreads();
-            store_x();
-          }
-          store_w(wb ^ 1);
-          __syncthreads();
-        }
-        wb ^= 1;
-      } else {
+      __syncthreads();
+      if (more) {
+        store_w();
+        if (kzn == 0) store_x();
         __syncthreads();
-        if (more) {
-          store_w(0);
-          if (kzn == 0) store_x();
-          __syncthreads();
-        }
       }
     }
     // epilogue: lane holds channels n0 + j*16 + 4*kg + (0..3) of voxel r16 of row tile i
@@ -2530,7 +2495,7 @@ Conv3Plan plan_conv3(int M, int Ncols, int cin, int D, int H, int W, int lda, in
   const int brick = knob("MMSEG_BRICK", 2);
   const bool base_ok = cin % CK == 0 && lda % 8 == 0 && ldo % 8 == 0 && Ncols % 32 == 0;
   // 48-column multiples (SwinUNETR's feature_size 48) run the brick2 kernel with 48-column tiles
-  const bool ok48 = cin % CK == 0 && lda % 8 == 0 && ldo % 8 == 0 && Ncols % 48 == 0 && knob("MMSEG_BRICK2_BN48", 1);
+  const bool ok48 = cin % CK == 0 && lda % 8 == 0 && ldo % 8 == 0 && Ncols % 48 == 0;
   if (!force_r && brick == 2 && (base_ok || ok48) && D % 4 == 0 && H % B2_Y == 0 && W % B2_X == 0) {
     // a brick2-family launch has one block per (4x8x8 brick, column tile): at SwinUNETR's 8^3 / 16^3 levels
     // (384 / 192 channels) that is 12-48 blocks for the whole chip (brick3 at 75-290 TF/s, r05m).  Below
@@ -2557,8 +2522,7 @@ Conv3Plan plan_conv3(int M, int Ncols, int cin, int D, int H, int W, int lda, in
           if (rows > 256 || halo > BR_MAXHV || hq > br_xq(tsize)) continue;
           const int score = rows * 4 + (bx % 8 == 0 ? 2 : 0) + (by % 8 == 0 ? 1 : 0);
           // ties go to the smaller halo (12^3: 6x6x6, 512 halo voxels and the compile-time kernel, over 3x6x12)
-          const bool tie_better = score == best && knob("MMSEG_BRICKR_CUBE", 1) &&
-                                  halo < (p.bz + 2) * (p.by + 2) * (p.bx + 2);
+          const bool tie_better = score == best && halo < (p.bz + 2) * (p.by + 2) * (p.bx + 2);
           if (score > best || tie_better) {
             best = score;
             p.bz = bz; p.by = by; p.bx = bx;
@@ -2570,18 +2534,13 @@ Conv3Plan plan_conv3(int M, int Ncols, int cin, int D, int H, int W, int lda, in
       p.kind = 2;
       p.bn = (tsize == 2 && Ncols % 64 == 0) ? 64 : 32;
       const int nb = (M / (D * H * W)) * (D / p.bz) * (H / p.by) * (W / p.bx);
-      // 32-column tiles where 64-column ones leave fewer than MMSEG_BRICKR_BN32_BLK blocks: twice the blocks
-      // instead of a chunk split (no fp32 partials, no reduce launch); 12^3 / 6^3 grouped: 2-8 us per launch
-      // (r04v convbench), -0.02 ms per step
-      if (p.bn == 64 && nb * (Ncols / 64) < knob("MMSEG_BRICKR_BN32_BLK", 256)) p.bn = 32;
+      // 32-column tiles where 64-column ones leave fewer than 256 blocks: twice the blocks instead of a chunk split
+      // (no fp32 partials, no reduce launch); 12^3 / 6^3 grouped: 2-8 us per launch (r04v convbench), -0.02 ms/step
+      if (p.bn == 64 && nb * (Ncols / 64) < 256) p.bn = 32;
       const int nt = (Ncols + p.bn - 1) / p.bn;
       const int nchunk = cin / CK;
       const int slots = knob("MMSEG_BRICKR_SLOTS", 256);   // 512 measured 2-10 % slower at 12^3 / 6^3 (r02)
       int ks = (slots + nb * nt - 1) / (nb * nt);
-      // at least this many (brick, column-tile) blocks: no chunk split (24^3 grouped data gradient, 216 blocks:
-      // 42.8 us split in two against 35.3 us whole, r04p)
-      const int nosplit = knob("MMSEG_BRICKR_NOSPLIT", 0);
-      if (nosplit > 0 && nb * nt >= nosplit) ks = 1;
       if (ks > nchunk) ks = nchunk;
       if (ks < 1) ks = 1;
       const int cps = (nchunk + ks - 1) / ks;
@@ -2602,13 +2561,10 @@ bool brick5_selected(const GemmArgs& g, int tsize) {
   if (plan.kind != 1) return false;
   const int nb1 = (g.M / (g.D * g.H * g.W)) * (g.D / 4) * (g.H / B2_Y) * (g.W / B2_X);
   const int min_blocks = knob("MMSEG_BRICK2_MINBLK", 512);
-  const bool v3 = knob("MMSEG_BRICK3", 1) != 0 && knob("MMSEG_BRICK2_ZW", 1) != 2 &&
-                  (long long)g.M * g.lda * 2LL < (1LL << 31);
+  const bool v3 = (long long)g.M * g.lda * 2LL < (1LL << 31);
   const bool wide = g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks;
-  if (!v3 || g.Ncols % 32 != 0 || (knob("MMSEG_BRICK3_BN64", 0) && wide)) return false;
-  if (gemm_nchunk(g) != 1 || !knob("MMSEG_BRICK4", 1) || wide) return false;
-  return g.H % 4 == 0 && g.W % 16 == 0 && g.ldo % 8 == 0 && (reinterpret_cast<uintptr_t>(g.out) & 15) == 0 &&
-         knob("MMSEG_BRICK5", 1);
+  if (!v3 || g.Ncols % 32 != 0 || gemm_nchunk(g) != 1 || wide) return false;
+  return g.H % 4 == 0 && g.W % 16 == 0 && g.ldo % 8 == 0 && (reinterpret_cast<uintptr_t>(g.out) & 15) == 0;
 }
 
 // Every column tile of a conv launch reads weight columns [n0, n0 + BN) of the packed image [KGp][Cpad][8]: all of
@@ -2622,13 +2578,15 @@ inline bool tile_in_pitch(const GemmArgs& g, int BN) { return (long long)((g.Nco
     mmseg::note_kernel(NAME);                                                                                    \
   } while (0)
 
-int launch_brick5(const GemmArgs& g, hipStream_t s, long long* dbg, bool dma) {
+// The W % 16 one-chunk 32-column conv: brick6 (forward, deferred-norm forward, e4m3 forward, and the data gradient
+// with the InstanceNorm-backward partials); brick5 only for a partials launch with a bias term (never on the
+// engine's path: a data gradient has no bias).  Returns the bricks per block.
+int launch_brick5(const GemmArgs& g, hipStream_t s) {
   const int nt_n = g.Ncols / 32;
   const int per_nt = std::max(1, knob("MMSEG_BRICK4_BLOCKS", 256) / nt_n);
   const int nb5 = (g.M / (g.D * g.H * g.W)) * (g.D / 4) * (g.H / 4) * (g.W / 16);
   const int upb5 = ceil_div(nb5, std::min(per_nt, nb5));
   const int bpn5 = ceil_div(nb5, upb5);
-  MMSEG_TILE(g, "conv3_brick5_kernel<BN32>", 32);
   const dim3 grid(bpn5 * nt_n), block(256);
   if (g.wdq) {   // e4m3 forward (mmseg_conv3_fwd_fp8)
     MMSEG_TILE(g, "conv3_brick6_kernel<BN32,F8>", 32);
@@ -2637,41 +2595,21 @@ int launch_brick5(const GemmArgs& g, hipStream_t s, long long* dbg, bool dma) {
     return upb5;
   }
   if (g.inpart) {   // samples a block does not touch keep zero partials
-    if (!g.bias && knob("MMSEG_BRICK6", 1) && knob("MMSEG_BRICK6_INP", 1)) {   // (brick6 writes those zeros itself)
+    if (!g.bias) {   // (brick6 writes those zeros itself)
       MMSEG_TILE(g, "conv3_brick6_kernel<BN32,INP>", 32);
       MMSEG_LAUNCH((conv3_brick6_kernel<false, 6, 0, true>), grid, block, 0, s, g, upb5, bpn5);
       return upb5;
     }
+    MMSEG_TILE(g, "conv3_brick5_kernel<BN32>", 32);
     hipMemsetAsync(g.inpart, 0, sizeof(float) * 2 * (size_t)(g.M / (g.D * g.H * g.W)) * bpn5 * g.Ncols, s);
     MMSEG_LAUNCH((conv3_brick5_kernel<false, true, true>), grid, block, 0, s, g, upb5, bpn5, nullptr);
     return upb5;
   }
-  if (!dbg && !dma && knob("MMSEG_BRICK6", 1)) {
-    const int sg = knob("MMSEG_BRICK6_SG0", 6);
-    MMSEG_TILE(g, "conv3_brick6_kernel<BN32>", 32);
-#ifdef MMSEG_TIMING_PROBES
-    if (knob("MMSEG_BRICK6_DBG", 0) == 1) {
-      MMSEG_LAUNCH((conv3_brick6_kernel<false, 3, 1>), grid, block, 0, s, g, upb5, bpn5);
-      return upb5;
-    }
-    if (knob("MMSEG_BRICK6_DBG", 0) == 2) {
-      MMSEG_LAUNCH((conv3_brick6_kernel<false, 3, 2>), grid, block, 0, s, g, upb5, bpn5);
-      return upb5;
-    }
-#endif
-#define MMSEG_B6(N, S) MMSEG_LAUNCH((conv3_brick6_kernel<N, S>), grid, block, 0, s, g, upb5, bpn5)
-    if (g.nmean) {
-      if (sg == 6) MMSEG_B6(true, 6); else if (sg == 7) MMSEG_B6(true, 7); else MMSEG_B6(true, 3);
-    } else {
-      if (sg == 6) MMSEG_B6(false, 6); else if (sg == 7) MMSEG_B6(false, 7); else MMSEG_B6(false, 3);
-    }
-#undef MMSEG_B6
-    return upb5;
-  }
-  if (dbg && dma) MMSEG_LAUNCH((conv3_brick5_kernel<true, true>), grid, block, 0, s, g, upb5, bpn5, dbg);
-  else if (dbg) MMSEG_LAUNCH((conv3_brick5_kernel<true, false>), grid, block, 0, s, g, upb5, bpn5, dbg);
-  else if (dma) MMSEG_LAUNCH((conv3_brick5_kernel<false, true>), grid, block, 0, s, g, upb5, bpn5, nullptr);
-  else MMSEG_LAUNCH((conv3_brick5_kernel<false, false>), grid, block, 0, s, g, upb5, bpn5, nullptr);
+  MMSEG_TILE(g, "conv3_brick6_kernel<BN32>", 32);
+  if (g.nmean)
+    MMSEG_LAUNCH((conv3_brick6_kernel<true, 6>), grid, block, 0, s, g, upb5, bpn5);
+  else
+    MMSEG_LAUNCH((conv3_brick6_kernel<false, 6>), grid, block, 0, s, g, upb5, bpn5);
   return upb5;
 }
 
@@ -2834,7 +2772,7 @@ struct WgradArgs {
   // activation, staged as relu((x - nmean[n][c]) * nrstd[n][c]) rounded to T
   const float* nmean;
   const float* nrstd;
-  int dbg;   // wgrad_brick2 timing probe (MMSEG_WGRAD_DBG): 1 = no global loads after the first brick, 2 = no MFMA
+  int dbg;   // brick weight-gradient timing probe (diagnostics builds): 1 = no global loads after the first brick, 2 = no MFMA
   int frag;  // wgrad_dma: split partials in the fragment-native layout (wgrad_dma_mt, WReduceArgs::frag_mt)
   int groups;  // grouped launch (wgrad_brickr only): the bricks are `groups` equal sample groups, splits
                // [gi * ksplit / groups, (gi + 1) * ksplit / groups) cover group gi's bricks only
@@ -3822,7 +3760,6 @@ __global__ __launch_bounds__(512, 1) void conv3_brick8_kernel(GemmArgs g) {
   __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): this wave's pieces have landed
   __syncthreads();
   PROBE_T();
-  if ((g.prio & 1) && __builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);
   for (int s = 0; s < nstage; ++s) {
     const int kz = s % 3, b = s & 1;
     const bool more = s + 1 < nstage;
@@ -3837,7 +3774,6 @@ __global__ __launch_bounds__(512, 1) void conv3_brick8_kernel(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < RM; ++i) af[k][i].load(Xl + (aq[i] + hoff) * EPQ);
     };
-    if (g.prio & 2) __builtin_amdgcn_s_setprio(2);
     rd(0, 0);
 #pragma unroll
     for (int t9 = 0; t9 < 9; ++t9) {
@@ -3847,12 +3783,6 @@ __global__ __launch_bounds__(512, 1) void conv3_brick8_kernel(GemmArgs g) {
       for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int j = 0; j < RN; ++j) mfma_step<T>(acc[i][j], af[t9 & 1][i], bf[t9 & 1][j]);
-    }
-    if (g.prio & 2) {
-      if ((g.prio & 1) && __builtin_amdgcn_readfirstlane(wave) >= 4)
-        __builtin_amdgcn_s_setprio(1);
-      else
-        __builtin_amdgcn_s_setprio(0);
     }
     if (more) {
       if ((s + 1) % 3 == 0) {           // next chunk: every wave is done with this halo, then refill it
@@ -4356,9 +4286,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
 // each halo-row fragment it reads from LDS feeds up to nine MFMAs and each dy fragment (kept in registers while
 // its plane is in the 3-plane tap window) up to nine: ~0.28 LDS fragments per MFMA against 0.65 for the brick
 // kernels (wgrad_brick2 / wgrad_dma: each halo fragment feeds 2 MFMAs, DESIGN (d) 8a).
-// A block owns a contiguous range of dy-plane steps: columns (sample n, 4 y rows, 32 x) walked along z, so a
-// halo plane is staged ONCE per column (6 rows x 34 voxels for 4 x 32 dy voxels: 1.6x the x bytes, against 2.8x
-// for a 4 x 4 x 8 brick's halo).  Step u of a column segment stages halo plane z_a - 1 + u and dy plane z_a + u
+// A block owns a contiguous range of dy-plane steps: columns (sample n, RY = 6 y rows (4 where H % 6 != 0), 32 x)
+// walked along z, so a halo plane is staged ONCE per column (8 rows x 34 voxels for 6 x 32 dy voxels: 1.4x the x
+// bytes, against 2.8x for a 4 x 4 x 8 brick's halo).  Step u of a column segment stages halo plane z_a - 1 + u and dy plane z_a + u
 // into one slot of a 4-slot LDS ring by LDS-DMA (buffer_load ... lds; the same 32-B XOR swizzle as wgrad_dma,
 // conflict-free for every kx shift) three steps ahead; the multiply pairs the halo plane with the dy planes
 // u, u - 1, u - 2 (kz = 0, 1, 2), whose fragments rotate through three register sets.  One barrier per step.
@@ -4366,25 +4296,33 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
 // instructions brought in (its own vmcnt orders them), one step before they are multiplied: no extra barrier.
 // Bias gradient: dy fragments times a ones fragment, dealt round-robin over the six waves of a co half.
 // Partials: the fragment-native layout of wgrad_dma (WReduceArgs::frag_mt = 2), summed by the same reduce.
-constexpr int WROW_RY = 4;                                   // dy rows (y) per plane step
-constexpr int WROW_HY = WROW_RY + 2, WROW_HX = 34;           // halo rows per plane, voxels per halo row
-constexpr int WROW_HI = (WROW_HY * WROW_HX * 4 + 63) / 64;   // halo DMA wave-instructions per plane (13)
-constexpr int WROW_DI = WROW_RY * 32 * 4 / 64;               // dy DMA wave-instructions per plane (8)
-constexpr int WROW_NI = WROW_HI + WROW_DI;                   // 21 per step
-constexpr int WROW_DOFF = WROW_HI * 1024;                    // dy image offset in a slot (bytes)
-constexpr int WROW_SLOT = WROW_NI * 1024;                    // bytes per ring slot
-constexpr int WROW_NST = 4;                                  // ring: computed, two landing, one being issued
+constexpr int WROW_HX = 34;                                  // voxels per halo row
 constexpr int WROW_WAVES = 12;                               // (kx, ci half, co half)
 constexpr int WROW_MAXN = 16;                                // samples whose norm statistics fit the LDS table
+// per plane step of RY dy rows: halo rows, halo / dy DMA wave-instructions, slot geometry (bytes)
+template <int RY>
+struct WRowGeo {
+  static constexpr int HY = RY + 2;
+  static constexpr int HI = (HY * WROW_HX * 4 + 63) / 64;   // halo chunks (16 B) / 64 lanes (RY 4: 13)
+  static constexpr int DI = RY * 32 * 4 / 64;                // dy (RY 4: 8)
+  static constexpr int NI = HI + DI;
+  static constexpr int KI = (NI + WROW_WAVES - 1) / WROW_WAVES;   // DMA instructions per wave per step (at most)
+  static constexpr int DOFF = HI * 1024;                     // dy image offset in a slot
+  static constexpr int SLOT = NI * 1024;
+};
 
 // a column segment of a block's step range: column col (sample, 4 y rows, 32 x), dy planes [za, za + L)
 struct WRowSeg {
   int s, col, za, L;
 };
 
-template <bool NORM>
+// RY dy rows per step (4 or 6; 8 spills at 168 VGPRs), NST ring slots (DMA NST - 1 steps ahead)
+template <bool NORM, int RY = 6, int NST = 4>
 __global__ __launch_bounds__(768, 1) void wgrad_row_kernel(WgradArgs g) {
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  typedef WRowGeo<RY> G;
+  constexpr int WROW_RY = RY, WROW_HY = G::HY, WROW_HI = G::HI, WROW_NI = G::NI, WROW_DOFF = G::DOFF;
+  constexpr int WROW_SLOT = G::SLOT, WROW_NST = NST, KI = G::KI;
   __shared__ __attribute__((aligned(16))) char ring[WROW_NST * WROW_SLOT];
   __shared__ __attribute__((aligned(16))) float ntab[NORM ? 2 * WROW_MAXN * CK : 4];
   __shared__ float bred[WROW_WAVES * 16];
@@ -4424,10 +4362,10 @@ __global__ __launch_bounds__(768, 1) void wgrad_row_kernel(WgradArgs g) {
 
   // the wave's DMA instructions (m = wave, wave + 12 < WROW_NI): m < WROW_HI halo chunks, else dy chunks.  Per
   // instruction: the lane's byte offset from the plane origin and its (y, x) position in the plane
-  const int nw = wave + 12 < WROW_NI ? 2 : 1;
-  int rel[2], py[2], px[2], ncc[2];
+  int nw = 0;
+  int rel[KI], py[KI], px[KI], ncc[KI];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < KI; ++k) {
     const int m = wave + 12 * k;
     rel[k] = 0, py[k] = 0xff, px[k] = 0, ncc[k] = 0;
     if (m < WROW_HI) {
@@ -4442,6 +4380,7 @@ __global__ __launch_bounds__(768, 1) void wgrad_row_kernel(WgradArgs g) {
       const int cc = (((cs >> 1) ^ ((x >> 2) & 1)) << 1) | (cs & 1);
       rel[k] = ((ry * W + x) * g.lda + cc * 8) * 2;
     }
+    if (m < WROW_NI) ++nw;
   }
   // DMA of halo step (segment q, step u) into ring slot `slot`
   auto issue = [&](int slot, const WRowSeg& q, int u) __attribute__((always_inline)) {
@@ -4453,7 +4392,7 @@ __global__ __launch_bounds__(768, 1) void wgrad_row_kernel(WgradArgs g) {
     const int db = (((n * D + zd) * H + y0) * W + x0) * g.lda * 2;
     const uint32_t lbase = (uint32_t)(uintptr_t)(lds_ptr_t)(ring + slot * WROW_SLOT);
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < KI; ++k) {
       const int m = wave + 12 * k;
       if (m < WROW_HI) {
         const int y = y0 - 1 + py[k], x = x0 - 1 + px[k];
@@ -4469,6 +4408,8 @@ __global__ __launch_bounds__(768, 1) void wgrad_row_kernel(WgradArgs g) {
 #define MMSEG_WR_WAIT(N) \
   case N: __builtin_amdgcn_s_waitcnt(0x0f70 | N); break;
       MMSEG_WR_WAIT(1) MMSEG_WR_WAIT(2) MMSEG_WR_WAIT(3) MMSEG_WR_WAIT(4) MMSEG_WR_WAIT(5) MMSEG_WR_WAIT(6)
+      MMSEG_WR_WAIT(7) MMSEG_WR_WAIT(8) MMSEG_WR_WAIT(9) MMSEG_WR_WAIT(10) MMSEG_WR_WAIT(11) MMSEG_WR_WAIT(12)
+      MMSEG_WR_WAIT(13) MMSEG_WR_WAIT(14) MMSEG_WR_WAIT(15)
 #undef MMSEG_WR_WAIT
       default: __builtin_amdgcn_s_waitcnt(0x0f70); break;
     }
@@ -4481,7 +4422,7 @@ __global__ __launch_bounds__(768, 1) void wgrad_row_kernel(WgradArgs g) {
       const int zh = q.za - 1 + u;
       if ((unsigned)zh >= (unsigned)D) return;
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
+      for (int k = 0; k < KI; ++k) {
         const int m = wave + 12 * k;
         if (m < WROW_HI) {
           const int y = y0 - 1 + py[k], x = x0 - 1 + px[k];
@@ -4857,8 +4798,7 @@ WBrick plan_wgrad_brickr(int D, int H, int W) {
         const int halo = (bz + 2) * (by + 2) * (bx + 2);
         if (rows > 128 || halo > WR_MAXHV) continue;
         // ties go to the smaller halo (12^3: 3x6x6, the compile-time kernel, over 3x3x12)
-        const bool tie_better = rows == brows && knob("MMSEG_BRICKR_CUBE", 1) &&
-                                halo < (best.bz + 2) * (best.by + 2) * (best.bx + 2);
+        const bool tie_better = rows == brows && halo < (best.bz + 2) * (best.by + 2) * (best.bx + 2);
         if (rows > brows || tie_better) {
           brows = rows;
           best = {bz, by, bx};
@@ -5283,8 +5223,7 @@ int launch_splitk_reduce(const GemmArgs& g, hipStream_t s) {
   const long long total = (long long)g.M * g.Ncols;
   const bool vec = MODE != MODE_CONVT_FWD && splitk_vec<MODE>(g);   // (the sliced reduce: not the transposed conv)
   int S = 1;
-  const int rpt = knob("MMSEG_SPLITK_RPT", 4);
-  while (S < 16 && g.ksplit / (2 * S) >= rpt) S *= 2;
+  while (S < 16 && g.ksplit / (2 * S) >= 4) S *= 2;
   if (vec && S > 1) {
     const int nb = ceil_div(total / 4, 256 / S);
     if (S == 16) MMSEG_LAUNCH((gemm_splitk_reduce_s<T, 16>), dim3(nb), dim3(256), 0, s, g);
@@ -5299,11 +5238,10 @@ int launch_splitk_reduce(const GemmArgs& g, hipStream_t s) {
 
 template <typename T, int MODE>
 int launch_gemm(GemmArgs g, hipStream_t s) {
-  g.prio = knob("MMSEG_PRIO", 0);
   if (g.nmean) {   // deferred InstanceNorm + ReLU of A: brick5 only (mmseg_conv3_norm_ok)
     MMSEG_REQUIRE(MODE == MODE_CONV3 && brick5_selected(g, (int)sizeof(T)),
                   "conv3 with a deferred norm needs the brick5 kernel for this shape (mmseg_conv3_norm_ok)");
-    launch_brick5(g, s, nullptr, false);
+    launch_brick5(g, s);
     return mmseg::check_launch("conv3_brick5_norm");
   }
   const int Cbig = g.Ncols >= 64;
@@ -5321,77 +5259,22 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     const int cps = (nchunk + g.ksplit - 1) / g.ksplit;
     g.ksplit = (nchunk + cps - 1) / cps;
     const dim3 grid(nb * ((g.Ncols + plan.bn - 1) / plan.bn) * g.ksplit);
-    const bool b666 = plan.bz == 6 && plan.by == 6 && plan.bx == 6 && knob("MMSEG_BRICKR_CT", 1);
-    // 4 x 8 x 8: the grouped 48^3 / 24^3 levels (MMSEG_GROUP_FORCE_R), compile-time as 6 x 6 x 6
-    const bool b488 = plan.bz == 4 && plan.by == 8 && plan.bx == 8 && knob("MMSEG_BRICKR_CT488", 1);
-    // 32-bit offset halo staging (bf16 only, as conv3_brick2_kernel's B32)
-    const bool rb32 = (sizeof(T) == 2 || knob("MMSEG_B32_F32", 0)) && knob("MMSEG_BRICKR_B32", 1) &&
-                      (long long)g.M * g.lda * (long long)sizeof(T) < (1LL << 31);
+    // compile-time bricks: 6 x 6 x 6 (the 12^3 / 6^3 levels) and 4 x 8 x 8 (the grouped 48^3 / 24^3 levels)
+    const bool b666 = plan.bz == 6 && plan.by == 6 && plan.bx == 6;
+    const bool b488 = plan.bz == 4 && plan.by == 8 && plan.bx == 8;
+    // 32-bit offset halo staging (bf16 only, as conv3_brick2_kernel's B32; MMSEG_B32=0: the 64-bit staging)
+    const bool rb32 = sizeof(T) == 2 && knob("MMSEG_B32", 1) && (long long)g.M * g.lda * (long long)sizeof(T) < (1LL << 31);
     if (plan.bn == 64) {
       if constexpr (sizeof(T) == 2) {
         MMSEG_TILE(g, "conv3_brickr_kernel<BN64>", 64);
-#ifdef MMSEG_TIMING_PROBES
-        // timing probes (diagnostics only, wrong results): built only with -DMMSEG_TIMING_PROBES
-        const int dbg = knob("MMSEG_BRICKR_DBG", 0);
-        if (b666 && dbg == 1)
-          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 1>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
-        else if (b666 && dbg == 2)
-          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 2>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
-        else if (b666 && dbg == 3)
-          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 3>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
-        else if (dbg == 4) {
-          static long long* dp = nullptr;
-          const int nlong = 4 * 4096 + 64;
-          if (!dp) hipMalloc(&dp, nlong * sizeof(long long));
-          hipMemsetAsync(dp, 0, nlong * sizeof(long long), s);
-          const bool pf = knob("MMSEG_BRICKR_PF", 0);
-          if (b666 && pf)
-            MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 4, true>), grid, block, 0, s, g, 6, 6, 6, dp);
-          else if (b666)
-            MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 4>), grid, block, 0, s, g, 6, 6, 6, dp);
-          else if (pf)
-            MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 0, 0, 0, 4, true>), grid, block, 0, s, g, plan.bz, plan.by,
-                               plan.bx, dp);
-          else
-            MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 0, 0, 0, 4>), grid, block, 0, s, g, plan.bz, plan.by,
-                               plan.bx, dp);
-          std::vector<long long> h(nlong);
-          hipStreamSynchronize(s);
-          hipMemcpy(h.data(), dp, nlong * sizeof(long long), hipMemcpyDeviceToHost);
-          const int nbk = std::min((int)grid.x, 4096);
-          long long t0 = h[0], t1 = h[2], sumdur = 0;
-          for (int b = 0; b < nbk; ++b) {
-            t0 = std::min(t0, h[4 * b]);
-            t1 = std::max(t1, h[4 * b + 2]);
-            sumdur += h[4 * b + 2] - h[4 * b];
-          }
-          long long lastst = 0;
-          for (int b = 0; b < nbk; ++b) lastst = std::max(lastst, h[4 * b] - t0);
-          fprintf(stderr, "brickr dbg grid %d brick %dx%dx%d ks %d: span %.2f us, mean block %.2f us, last start %.2f us, "
-                  "block0 %.0f cycles / %.2f us:", (int)grid.x, plan.bz, plan.by, plan.bx, g.ksplit, (t1 - t0) * 0.01,
-                  sumdur * 0.01 / nbk, lastst * 0.01, (double)(h[3] - h[1]), (h[2] - h[0]) * 0.01);
-          const long long* q = h.data() + 4 * 4096;
-          for (int i = 1; i < 64 && q[i]; ++i) fprintf(stderr, " %lld", q[i] - q[i - 1]);
-          fprintf(stderr, "\n");
-        } else
-#endif
-        if (b666 && rb32 && knob("MMSEG_BRICKR_PF", 0))
-          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 0, true, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
-        else if (b666 && knob("MMSEG_BRICKR_PF", 0))
-          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 0, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
-        else if (b666 && rb32)
+        if (b666 && rb32)
           MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6, 0, false, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
         else if (b666)
           MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 6, 6, 6>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
-        else if (b488 && rb32 && knob("MMSEG_BRICKR_PF488", 0))
-          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 4, 8, 8, 0, true, true>), grid, block, 0, s, g, 4, 8, 8, (long long*)nullptr);
         else if (b488 && rb32)
           MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 4, 8, 8, 0, false, true>), grid, block, 0, s, g, 4, 8, 8, (long long*)nullptr);
         else if (b488)
           MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 4, 8, 8>), grid, block, 0, s, g, 4, 8, 8, (long long*)nullptr);
-        else if (knob("MMSEG_BRICKR_PF", 0))
-          MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 0, 0, 0, 0, true>), grid, block, 0, s, g, plan.bz, plan.by,
-                             plan.bx, (long long*)nullptr);
         else if (rb32)
           MMSEG_LAUNCH((conv3_brickr_kernel<T, 64, 0, 0, 0, 0, false, true>), grid, block, 0, s, g, plan.bz,
                              plan.by, plan.bx, (long long*)nullptr);
@@ -5399,37 +5282,27 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
           MMSEG_LAUNCH((conv3_brickr_kernel<T, 64>), grid, block, 0, s, g, plan.bz, plan.by, plan.bx, (long long*)nullptr);
       }
     } else if (b666) {
-      // KW = 2 (MMSEG_BRICKR_KW, default 2): two waves per SIMD from an in-block split of the chunks (see the kernel)
-      const bool kw2 = sizeof(T) == 2 && !g.stats && cps >= 2 && knob("MMSEG_BRICKR_KW", 2) == 2;
-      mmseg::note_kernel(kw2 ? "conv3_brickr_kernel<BN32,KW2>" : "conv3_brickr_kernel<BN32>");
-      // (MMSEG_BRICKR_PF32: tap t+1's fragments read during tap t's MFMAs -- at 12^3 / 6^3 a CU holds one block;
-      // 5-10 % per launch, r04ab convbench)
+      // KW = 2: two waves per SIMD from an in-block split of the chunks (see the kernel); tap t + 1's fragments
+      // read during tap t's MFMAs (PF: at 12^3 / 6^3 a CU holds one block; 5-10 % per launch, r04ab convbench)
+      const bool kw2 = sizeof(T) == 2 && !g.stats && cps >= 2;
+      MMSEG_TILE(g, kw2 ? "conv3_brickr_kernel<BN32,KW2>" : "conv3_brickr_kernel<BN32>", 32);
       bool done = false;
       if constexpr (sizeof(T) == 2) {   // (the fp32 form's two stage sets exceed the LDS)
-        const bool pf = knob("MMSEG_BRICKR_PF32", 1);
         const dim3 b2(512);
-        if (kw2 && pf && rb32)
+        if (kw2 && rb32)
           MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, true, true, 2>), grid, b2, 0, s, g, 6, 6, 6, nullptr);
-        else if (kw2 && rb32)
-          MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, false, true, 2>), grid, b2, 0, s, g, 6, 6, 6, nullptr);
-        else if (kw2 && pf)
-          MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, true, false, 2>), grid, b2, 0, s, g, 6, 6, 6, nullptr);
         else if (kw2)
-          MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, false, false, 2>), grid, b2, 0, s, g, 6, 6, 6, nullptr);
+          MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, true, false, 2>), grid, b2, 0, s, g, 6, 6, 6, nullptr);
         done = kw2;
       }
       if (done) {
-      } else if (rb32 && knob("MMSEG_BRICKR_PF32", 1))
+      } else if (rb32)
         MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, true, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
-      else if (rb32)
-        MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6, 0, false, true>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
       else
         MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 6, 6, 6>), grid, block, 0, s, g, 6, 6, 6, (long long*)nullptr);
     } else if (b488) {
       MMSEG_TILE(g, "conv3_brickr_kernel<BN32>", 32);
-      if (rb32 && knob("MMSEG_BRICKR_PF488", 0))
-        MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 4, 8, 8, 0, true, true>), grid, block, 0, s, g, 4, 8, 8, (long long*)nullptr);
-      else if (rb32)
+      if (rb32)
         MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 4, 8, 8, 0, false, true>), grid, block, 0, s, g, 4, 8, 8, (long long*)nullptr);
       else
         MMSEG_LAUNCH((conv3_brickr_kernel<T, 32, 4, 8, 8>), grid, block, 0, s, g, 4, 8, 8, (long long*)nullptr);
@@ -5478,20 +5351,16 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     // v3 is bf16 only: its fp32 instantiation (f32 16x16x4 MFMA with swapped operands) returned the first
     // row of each 4-row accumulator group in all four registers (tools/diag_b3.py); the fp32 parity path
     // keeps the v2 kernel.
-    const bool v3 = sizeof(T) == 2 && g.stats == nullptr && knob("MMSEG_BRICK3", 1) != 0 &&
-                    knob("MMSEG_BRICK2_ZW", 1) != 2 &&
-                    (long long)g.M * g.lda * (long long)sizeof(T) < (1LL << 31);
+    const bool v3 = sizeof(T) == 2 && g.stats == nullptr && (long long)g.M * g.lda * (long long)sizeof(T) < (1LL << 31);
     // persistent: at most one wave of resident blocks (2 per CU), each over a contiguous range of units
     const int maxblk = knob("MMSEG_BRICK3_BLOCKS", 512);
-    // (BN64 stays on v2 unless asked for: at 256 VGPRs the v3 instantiation spills and measured no faster)
-    // 32-bit offset halo staging (brick2 B32; bf16 only, see the BN64 branch)
-    const bool b32 = (sizeof(T) == 2 || knob("MMSEG_B32_F32", 0)) && knob("MMSEG_BRICK2_B32", 1) &&
-                     (long long)g.M * g.lda * (long long)sizeof(T) < (1LL << 31);
+    // 32-bit offset halo staging (brick2 B32; bf16 only, see the runtime-brick branch)
+    const bool b32 = sizeof(T) == 2 && knob("MMSEG_B32", 1) && (long long)g.M * g.lda * (long long)sizeof(T) < (1LL << 31);
+    const bool wide = g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks;
     // 48-column tiles also for multiples of 96 that are not of 64 (SwinUNETR's 96-column convs: two 48-column tiles
     // read the A halo twice, three 32-column brick3 tiles three times -- 128^3 96-column dgrad 0.74 ms at 706 TF/s
     // on brick3, r05c timer)
-    const bool bn48 = g.Ncols % 32 != 0 ||
-                      (g.Ncols % 96 == 0 && g.Ncols % 64 != 0 && g.stats == nullptr && knob("MMSEG_BRICK2_BN48X", 1));
+    const bool bn48 = g.Ncols % 32 != 0 || (g.Ncols % 96 == 0 && g.Ncols % 64 != 0 && g.stats == nullptr);
     if (bn48) {    // a multiple of 48 (plan_conv3)
       MMSEG_TILE(g, "conv3_brick2_kernel<BN48,ZW1>", 48);
       if (b32) {
@@ -5499,79 +5368,32 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
         return mmseg::check_launch("conv3_brick2");
       }
       MMSEG_LAUNCH((conv3_brick2_kernel<T, 48, 1>), dim3(nb1 * (g.Ncols / 48)), block, 0, s, g);
-    } else if (v3 && knob("MMSEG_BRICK3_BN64", 0) && g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
-      const int units = nb1 * (g.Ncols / 64);
-      const int upb = maxblk > 0 ? ceil_div(units, maxblk) : 1;
-      MMSEG_TILE(g, "conv3_brick3_kernel<BN64>", 64);
-      MMSEG_LAUNCH((conv3_brick3_kernel<T, 64>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
-    } else if (v3 && gemm_nchunk(g) == 1 && g.Ncols % 32 == 0 && knob("MMSEG_BRICK4", 1) &&
-               !(g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks)) {
+    } else if (v3 && gemm_nchunk(g) == 1 && g.Ncols % 32 == 0 && !wide) {
       if constexpr (sizeof(T) == 2) {
         // one persistent block per CU, each over a contiguous brick range of one 32-column tile
         const int nt_n = g.Ncols / 32;
         const int per_nt = std::max(1, knob("MMSEG_BRICK4_BLOCKS", 256) / nt_n);
         const int upb = ceil_div(nb1, std::min(per_nt, nb1));
         const int bpn = ceil_div(nb1, upb);
-        if (g.H % 4 == 0 && g.W % 16 == 0 && g.ldo % 8 == 0 && (reinterpret_cast<uintptr_t>(g.out) & 15) == 0 &&
-            knob("MMSEG_BRICK5", 1)) {   // (16-B output stores)
-          const bool dma = knob("MMSEG_BRICK5_DMA", 0) != 0;
-#ifdef MMSEG_TIMING_PROBES
-          if (knob("MMSEG_BRICK5_DBG", 0)) {   // phase timing probe (diagnostics only, -DMMSEG_TIMING_PROBES)
-            static long long* dbg = nullptr;
-            if (!dbg) hipMalloc(&dbg, 4 * 128 * sizeof(long long));
-            hipMemsetAsync(dbg, 0, 4 * 128 * sizeof(long long), s);
-            const int upb5 = launch_brick5(g, s, dbg, dma);
-            long long h[4 * 128];
-            hipStreamSynchronize(s);
-            hipMemcpy(h, dbg, sizeof(h), hipMemcpyDeviceToHost);
-            for (int w = 0; w < 4; ++w) {
-              const long long* q = h + w * 128;
-              int n = 1;
-              while (n < 64 && q[n]) ++n;
-              fprintf(stderr, "brick5 dbg slot %d upb %d: clock %.3f GHz:", w, upb5,
-                      (double)(q[n - 1] - q[0]) / (double)(q[64 + n - 1] - q[64] + 1) * 0.1);
-              for (int i = 1; i < n; ++i) fprintf(stderr, " %lld", q[i] - q[i - 1]);
-              fprintf(stderr, "\n");
-            }
-          } else
-#endif
-          {
-            launch_brick5(g, s, nullptr, dma);
-          }
+        if (g.H % 4 == 0 && g.W % 16 == 0 && g.ldo % 8 == 0 && (reinterpret_cast<uintptr_t>(g.out) & 15) == 0) {
+          launch_brick5(g, s);   // (16-B output stores)
         } else {
           MMSEG_TILE(g, "conv3_brick4_kernel<BN32>", 32);
           MMSEG_LAUNCH(conv3_brick4_kernel, dim3(bpn * nt_n), block, 0, s, g, upb, bpn);
         }
       }
-    } else if (v3 && !(g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks)) {
+    } else if (v3 && !wide) {
       const int units = nb1 * (g.Ncols / 32);
       const int upb = maxblk > 0 ? ceil_div(units, maxblk) : 1;
       MMSEG_TILE(g, "conv3_brick3_kernel<BN32>", 32);
-      if (knob("MMSEG_BRICK3_WU", 0))
-        MMSEG_LAUNCH((conv3_brick3_kernel<T, 32, true>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
-      else if (knob("MMSEG_BRICK3_XP", 0))
-        MMSEG_LAUNCH((conv3_brick3_kernel<T, 32, false, false, true>), dim3(ceil_div(units, upb)), block, 0, s,
-                           g, upb);
-      else if (knob("MMSEG_BRICK3_WDB", 0))
-        MMSEG_LAUNCH((conv3_brick3_kernel<T, 32, false, true>), dim3(ceil_div(units, upb)), block, 0, s, g,
-                           upb);
-      else
-        MMSEG_LAUNCH((conv3_brick3_kernel<T, 32, false>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
-    } else if (g.Ncols % 64 == 0 && nb1 * (g.Ncols / 64) >= min_blocks) {
+      MMSEG_LAUNCH((conv3_brick3_kernel<T, 32>), dim3(ceil_div(units, upb)), block, 0, s, g, upb);
+    } else if (wide) {
+      // each tap's fragments read while the previous tap's MFMAs run (2 % on the 48^3 64-channel layers, r02)
       MMSEG_TILE(g, "conv3_brick2_kernel<BN64,ZW1>", 64);
-      if (knob("MMSEG_TAP_PF", 1) && b32) {
+      if (b32)
         MMSEG_LAUNCH((conv3_brick2_kernel<T, 64, 1, true, true>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
-        return mmseg::check_launch("conv3_brick2");
-      }
-      if (knob("MMSEG_TAP_PF", 1))   // 2 % on the 48^3 64-channel layers (r02)
-        MMSEG_LAUNCH((conv3_brick2_kernel<T, 64, 1, true>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
       else
-        MMSEG_LAUNCH((conv3_brick2_kernel<T, 64, 1>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
-    } else if (sizeof(T) == 2 && g.D % 8 == 0 && knob("MMSEG_BRICK2_ZW", 1) == 2) {
-      if constexpr (sizeof(T) == 2) {
-        MMSEG_TILE(g, "conv3_brick2_kernel<BN32,ZW2>", 32);
-        MMSEG_LAUNCH((conv3_brick2_kernel<T, 32, 2>), dim3(nb1 / 2 * (g.Ncols / 32)), block, 0, s, g);
-      }
+        MMSEG_LAUNCH((conv3_brick2_kernel<T, 64, 1, true>), dim3(nb1 * (g.Ncols / 64)), block, 0, s, g);
     } else {
       MMSEG_TILE(g, "conv3_brick2_kernel<BN32,ZW1>", 32);
       MMSEG_LAUNCH((conv3_brick2_kernel<T, 32, 1>), dim3(nb1 * (g.Ncols / 32)), block, 0, s, g);
@@ -5581,7 +5403,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
   if (MODE == MODE_CONV3 && g.ksplit == 1 && brick == 1 && (8 << g.cpg_shift) % CK == 0 &&
       g.D % BRK_Z == 0 && g.H % BRK_Y == 0 && g.W % BRK_X == 0 && g.lda % 8 == 0) {
     const int nb = (g.M / (g.D * g.H * g.W)) * (g.D / BRK_Z) * (g.H / BRK_Y) * (g.W / BRK_X);
-    const int bn = (g.Ncols >= 64 && knob("MMSEG_BRICK_BN", 64) == 64) ? 64 : 32;
+    const int bn = g.Ncols >= 64 ? 64 : 32;
     MMSEG_TILE(g, bn == 64 ? "conv3_brick_kernel<BN64>" : "conv3_brick_kernel<BN32>", bn);
     if (bn == 64) {
       MMSEG_LAUNCH((conv3_brick_kernel<T, 64>), dim3(nb * ceil_div(g.Ncols, 64)), block, 0, s, g);
@@ -5590,28 +5412,12 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     }
     return mmseg::check_launch("conv3_brick");
   }
-  if (MODE == MODE_CONVT_FWD && g.Ncols % 256 == 0 && knob("MMSEG_CONVT_FWD_WIDE", 1)) {
+  if (MODE == MODE_CONVT_FWD && g.Ncols % 256 == 0) {
     // BM=64, BN=256: a block writes all 8 taps x 32 (or a quarter of 8 x 128 ...) output channels of its 64 input
     // voxels, so each input row is read by one block instead of by Ncols / 64 column tiles
     MMSEG_TILE(g, "conv_gemm_kernel<convT_fwd,64x256>", 256);
     dim3 grid(ceil_div(g.M, 64) * (g.Ncols / 256) * g.ksplit);
     MMSEG_LAUNCH((conv_gemm_kernel<T, MODE, 1, 4, 4, 4>), grid, block, 0, s, g);
-    if (mmseg::check_launch("conv_gemm")) return 1;
-    if (g.ksplit > 1) return launch_splitk_reduce<T, MODE>(g, s);
-    return 0;
-  }
-  if (MODE == MODE_CONVT_DGRAD && g.Ncols % 64 == 0 && knob("MMSEG_CONVT_DGRAD_TILE", 0) == 1) {
-    MMSEG_TILE(g, "conv_gemm_kernel<convT_dgrad,64x64>", 64);
-    dim3 grid(ceil_div(g.M, 64) * (g.Ncols / 64) * g.ksplit);
-    MMSEG_LAUNCH((conv_gemm_kernel<T, MODE, 2, 2, 2, 2>), grid, block, 0, s, g);
-    if (mmseg::check_launch("conv_gemm")) return 1;
-    if (g.ksplit > 1) return launch_splitk_reduce<T, MODE>(g, s);
-    return 0;
-  }
-  if (MODE == MODE_CONVT_DGRAD && g.Ncols % 128 == 0 && knob("MMSEG_CONVT_DGRAD_TILE", 0) == 2) {
-    MMSEG_TILE(g, "conv_gemm_kernel<convT_dgrad,64x128>", 128);
-    dim3 grid(ceil_div(g.M, 64) * (g.Ncols / 128) * g.ksplit);
-    MMSEG_LAUNCH((conv_gemm_kernel<T, MODE, 1, 4, 4, 2>), grid, block, 0, s, g);
     if (mmseg::check_launch("conv_gemm")) return 1;
     if (g.ksplit > 1) return launch_splitk_reduce<T, MODE>(g, s);
     return 0;
@@ -5663,34 +5469,32 @@ int launch_gemm_mode(GemmArgs g, int mode, hipStream_t s) {
 bool wgrad_co64(int Ca, long long V, int kind);
 
 int wgrad_dma_mt(const WgradArgs& g, int elem_bytes) {
-  const bool dma = elem_bytes == 2 && g.brick == 2 && knob("MMSEG_WGRAD_V3", 1) != 0 && knob("MMSEG_WGRAD_DMA", 1) &&
-                   (g.nmean == nullptr || knob("MMSEG_WGRAD_DMA_NORM", 0)) && g.V * g.lda * 2 < (1LL << 31) &&
+  const bool dma = elem_bytes == 2 && g.brick == 2 && knob("MMSEG_WGRAD_DMA", 1) && g.nmean == nullptr &&
+                   g.V * g.lda * 2 < (1LL << 31) &&
                    g.V * g.ldb * 2 < (1LL << 31) && (g.lda % 8) == 0 && (g.ldb % 8) == 0;
   return dma ? (wgrad_co64(g.Ca, g.V, 2) ? 4 : 2) : 0;
 }
 
 // the row-slab weight gradient (wgrad_row_kernel) takes the shape: bf16 3^3, 32 output channels, W % 32 == 0,
 // H % 4 == 0, split partials (no direct gradient, no groups, no padded rows), 32-bit DMA offsets
+// rows per step: 6 where H allows (r06c, 96^3 B=2: 32 -> 32 deferred norm 128.6 -> 113.6 us, 64 -> 32 196 -> 179 us
+// against 4 rows; five ring slots or s_setprio for waves 6..11 measured no change), else 4
 bool wgrad_row_ok(const WgradArgs& g, int elem_bytes) {
   return elem_bytes == 2 && knob("MMSEG_WGRAD_ROW", 1) && g.brick == 2 && g.Ca == 32 && g.W % 32 == 0 &&
-         g.H % WROW_RY == 0 && (8 << g.cpg_shift) % CK == 0 && g.groups == 0 && !g.pad16 && g.ksplit > 1 &&
+         g.H % 4 == 0 && (8 << g.cpg_shift) % CK == 0 && g.groups == 0 && !g.pad16 && g.ksplit > 1 &&
          g.V * g.lda * 2 < (1LL << 31) && g.V * g.ldb * 2 < (1LL << 31) && g.lda % 8 == 0 && g.ldb % 8 == 0 &&
          g.V / ((long long)g.D * g.H * g.W) <= WROW_MAXN;
 }
 
 template <typename T, int MODE>
 int launch_wgrad(WgradArgs g, hipStream_t s) {
-#ifdef MMSEG_TIMING_PROBES
-  g.dbg = knob("MMSEG_WGRAD_DBG", 0);   // 1 = no loads after the first brick, 2 = no MFMA (wrong results)
-#else
-  g.dbg = 0;
-#endif
+  g.dbg = 0;   // (the timing probes of the brick weight-gradient kernels: 1 no loads, 2 no MFMA; diagnostics only)
   dim3 block(256);
   if constexpr (sizeof(T) == 2) {
     if (MODE == MODE_CONV3 && g.brick == 3) {
       const WBrick wb = plan_wgrad_brickr(g.D, g.H, g.W);
-      const bool b366 = wb.bz == 3 && wb.by == 6 && wb.bx == 6 && knob("MMSEG_BRICKR_CT", 1);
-      const bool b448 = wb.bz == 4 && wb.by == 4 && wb.bx == 8 && knob("MMSEG_BRICKR_CT488", 1);   // grouped 48^3 / 24^3
+      const bool b366 = wb.bz == 3 && wb.by == 6 && wb.bx == 6;
+      const bool b448 = wb.bz == 4 && wb.by == 4 && wb.bx == 8;   // grouped 48^3 / 24^3
       if (wgrad_co64(g.Ca, g.V, 3)) {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 64) * g.ksplit);
         // (the compile-time bricks under their rocprofv3 family names, tools/rocprof_families.py)
@@ -5718,82 +5522,53 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
     if (MODE == MODE_CONV3 && g.brick == 2 && wgrad_row_ok(g, (int)sizeof(T))) {
       MMSEG_REQUIRE(g.frag, "wgrad_row: fragment-native partials only");
       const dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * g.ksplit);
+      auto run = [&](auto normc) {
+        constexpr bool NRM = decltype(normc)::value;
+        if (g.H % 6 == 0)
+          MMSEG_LAUNCH((wgrad_row_kernel<NRM, 6>), grid, dim3(768), 0, s, g);
+        else
+          MMSEG_LAUNCH((wgrad_row_kernel<NRM, 4>), grid, dim3(768), 0, s, g);
+      };
       if (g.nmean) {
         mmseg::note_kernel("wgrad_row_kernel<CO32,NORM>");
-        MMSEG_LAUNCH((wgrad_row_kernel<true>), grid, dim3(768), 0, s, g);
+        run(std::true_type{});
       } else {
         mmseg::note_kernel("wgrad_row_kernel<CO32>");
-        MMSEG_LAUNCH((wgrad_row_kernel<false>), grid, dim3(768), 0, s, g);
+        run(std::false_type{});
       }
       return mmseg::check_launch("wgrad_row");
     }
     if (MODE == MODE_CONV3 && g.brick == 2) {
-      const bool v3 = knob("MMSEG_WGRAD_V3", 1) != 0;
       if (const int mt = wgrad_dma_mt(g, (int)sizeof(T))) {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / (16 * mt)) * g.ksplit);
-        const bool st4 = knob("MMSEG_WGRAD_DMA_ST", 3) >= 4;   // ring depth (4 x 38.5 KB fits at 64 co)
-        // fragment prefetch two steps ahead (32 co; at 64 co the extra registers spill: 59.5 -> 72.3 us)
-        const bool pipe = mt == 2 && knob("MMSEG_WGRAD_DMA_PIPE", 1) != 0;
-        const bool norm = g.nmean != nullptr;
-        // z-plane halo ring (MMSEG_WGRAD_RING): no deferred norm, three stages
-        const bool ring = !norm && !st4 && knob("MMSEG_WGRAD_RING", 0) != 0;
         if (mt == 4) {
           mmseg::note_kernel("wgrad_dma_kernel<CO64>");
-          const bool p16 = g.pad16 && !norm && !ring && !st4 && g.Ca == 64 && knob("MMSEG_WGRAD_PAD16", 1);
-          if (p16 && knob("MMSEG_WGRAD_PAD16_PIPE", 1))   // 48 rows leave room for the pipelined multiply
+          // 48 real rows of 64 (SwinUNETR's 48-channel levels): three row tiles, room for the pipelined multiply
+          if (g.pad16 && g.Ca == 64)
             MMSEG_LAUNCH((wgrad_dma_kernel<4, false, 3, true, false, 3>), grid, dim3(512), 0, s, g);
-          else if (p16)
-            MMSEG_LAUNCH((wgrad_dma_kernel<4, false, 3, false, false, 3>), grid, dim3(512), 0, s, g);
-          else if (norm)
-            MMSEG_LAUNCH((wgrad_dma_kernel<4, true>), grid, dim3(512), 0, s, g);
-          else if (ring)
-            MMSEG_LAUNCH((wgrad_dma_kernel<4, false, 3, false, true>), grid, dim3(512), 0, s, g);
-          else if (st4)
-            MMSEG_LAUNCH((wgrad_dma_kernel<4, false, 4>), grid, dim3(512), 0, s, g);
-          else
+          else   // (fragment prefetch two steps ahead spills at 64 co: 59.5 -> 72.3 us)
             MMSEG_LAUNCH((wgrad_dma_kernel<4>), grid, dim3(512), 0, s, g);
         } else {
           mmseg::note_kernel("wgrad_dma_kernel<CO32>");
-          if (norm && pipe)
-            MMSEG_LAUNCH((wgrad_dma_kernel<2, true, 3, true>), grid, dim3(512), 0, s, g);
-          else if (norm)
-            MMSEG_LAUNCH((wgrad_dma_kernel<2, true>), grid, dim3(512), 0, s, g);
-          else if (ring && pipe)
-            MMSEG_LAUNCH((wgrad_dma_kernel<2, false, 3, true, true>), grid, dim3(512), 0, s, g);
-          else if (ring)
-            MMSEG_LAUNCH((wgrad_dma_kernel<2, false, 3, false, true>), grid, dim3(512), 0, s, g);
-          else if (pipe)
-            MMSEG_LAUNCH((wgrad_dma_kernel<2, false, 3, true>), grid, dim3(512), 0, s, g);
-          else if (st4)
-            MMSEG_LAUNCH((wgrad_dma_kernel<2, false, 4>), grid, dim3(512), 0, s, g);
-          else
-            MMSEG_LAUNCH((wgrad_dma_kernel<2>), grid, dim3(512), 0, s, g);
+          MMSEG_LAUNCH((wgrad_dma_kernel<2, false, 3, true>), grid, dim3(512), 0, s, g);
         }
         return mmseg::check_launch("wgrad_dma");
       }
       if (wgrad_co64(g.Ca, g.V, 2)) {
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 64) * g.ksplit);
-        mmseg::note_kernel(v3 ? "wgrad_brick2_kernel<CO64,V3>" : "wgrad_brick2_kernel<CO64>");
-        if (v3 && g.nmean)
+        mmseg::note_kernel("wgrad_brick2_kernel<CO64,V3>");
+        if (g.nmean)
           MMSEG_LAUNCH((wgrad_brick2_kernel<T, 4, 3, true>), grid, dim3(512), 0, s, g);
-        else if (v3)
+        else
           MMSEG_LAUNCH((wgrad_brick2_kernel<T, 4, 3>), grid, dim3(512), 0, s, g);
-        else
-          MMSEG_LAUNCH((wgrad_brick2_kernel<T, 4, 2>), grid, dim3(512), 0, s, g);
       } else {
+        // (fragment reads software-pipelined, r05: the deferred-norm 96^3 layers 136 -> 125 us before wgrad_row)
         dim3 grid(wgrad_nchunk(g.cpg_shift, g.kchunks) * (g.Ca / 32) * g.ksplit);
-        mmseg::note_kernel(v3 ? "wgrad_brick2_kernel<CO32,V3>" : "wgrad_brick2_kernel<CO32>");
-        const bool pipe = knob("MMSEG_WGRAD_B2_PIPE", 1) != 0;
-        if (v3 && g.nmean && pipe)
+        mmseg::note_kernel("wgrad_brick2_kernel<CO32,V3>");
+        if (g.nmean)
           MMSEG_LAUNCH((wgrad_brick2_kernel<T, 2, 3, true, true>), grid, dim3(512), 0, s, g);
-        else if (v3 && g.nmean)
-          MMSEG_LAUNCH((wgrad_brick2_kernel<T, 2, 3, true>), grid, dim3(512), 0, s, g);
-        else if (v3 && pipe)
-          MMSEG_LAUNCH((wgrad_brick2_kernel<T, 2, 3, false, true>), grid, dim3(512), 0, s, g);
-        else if (v3)
-          MMSEG_LAUNCH((wgrad_brick2_kernel<T, 2, 3>), grid, dim3(512), 0, s, g);
         else
-          MMSEG_LAUNCH((wgrad_brick2_kernel<T, 2, 2>), grid, dim3(512), 0, s, g);
+          MMSEG_LAUNCH((wgrad_brick2_kernel<T, 2, 3, false, true>), grid, dim3(512), 0, s, g);
       }
       return mmseg::check_launch("wgrad_brick2");
     }
@@ -5804,26 +5579,15 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
     MMSEG_LAUNCH((wgrad_brick_kernel<T>), grid, block, 0, s, g);
     return mmseg::check_launch("wgrad_brick");
   }
-  const int bn = knob("MMSEG_WGRAD_BN", 64);
   static const char* nm[4] = {"wgrad_kernel<conv3>", "wgrad_kernel<point>", "wgrad_kernel<convT_fwd>",
                               "wgrad_kernel<convT_dgrad>"};
   mmseg::note_kernel(nm[MODE]);
   if (g.Ca % 64 == 0) {
-    if (bn == 128) {
-      dim3 grid(ceil_div(g.Ncols, 128) * (g.Ca / 64) * g.ksplit);
-      MMSEG_LAUNCH((wgrad_kernel<T, MODE, 2, 2, 2, 4, 64>), grid, block, 0, s, g);
-    } else {
-      dim3 grid(ceil_div(g.Ncols, 64) * (g.Ca / 64) * g.ksplit);
-      MMSEG_LAUNCH((wgrad_kernel<T, MODE, 2, 2, 2, 2, 64>), grid, block, 0, s, g);
-    }
+    dim3 grid(ceil_div(g.Ncols, 64) * (g.Ca / 64) * g.ksplit);
+    MMSEG_LAUNCH((wgrad_kernel<T, MODE, 2, 2, 2, 2, 64>), grid, block, 0, s, g);
   } else {
-    if (bn == 128) {
-      dim3 grid(ceil_div(g.Ncols, 128) * ceil_div(g.Ca, 32) * g.ksplit);
-      MMSEG_LAUNCH((wgrad_kernel<T, MODE, 1, 4, 2, 2, 64>), grid, block, 0, s, g);
-    } else {
-      dim3 grid(ceil_div(g.Ncols, 64) * ceil_div(g.Ca, 32) * g.ksplit);
-      MMSEG_LAUNCH((wgrad_kernel<T, MODE, 1, 4, 2, 1, 64>), grid, block, 0, s, g);
-    }
+    dim3 grid(ceil_div(g.Ncols, 64) * ceil_div(g.Ca, 32) * g.ksplit);
+    MMSEG_LAUNCH((wgrad_kernel<T, MODE, 1, 4, 2, 1, 64>), grid, block, 0, s, g);
   }
   return mmseg::check_launch("wgrad");
 }
@@ -5848,11 +5612,8 @@ int wgrad_brick_ok(int Ca, int cpg_shift, int D, int H, int W, int lda, int ldb,
 // A block's split partial is its whole tile, so at small volumes -- where the ~256 resident blocks each see a
 // few bricks -- the partials outweigh the inputs (24^3: 54 MB written and re-read per launch against 35-65 MB
 // of input); 32-co tiles halve them at the price of reading the halo once per row tile.  Below V voxels
-// MMSEG_WGRAD_CO64_MINV (kind 2) / MMSEG_WGRAD_RCO64_MINV (kind 3) the 32-co tiles are used.
-bool wgrad_co64(int Ca, long long V, int kind) {
-  if (Ca % 64 != 0) return false;
-  return V >= (long long)knob(kind == 3 ? "MMSEG_WGRAD_RCO64_MINV" : "MMSEG_WGRAD_CO64_MINV", 0);
-}
+// a threshold the 32-co tiles were tried below (r04: equal or slower at 24^3), so 64-co tiles throughout.
+bool wgrad_co64(int Ca, long long V, int kind) { return Ca % 64 == 0; }
 
 int brick_wgrad_splits(long long V, int cap, int Ca, int cpg_shift, int kind, int D, int H, int W,
                        int kchunks = 0) {
@@ -5863,10 +5624,8 @@ int brick_wgrad_splits(long long V, int cap, int Ca, int cpg_shift, int kind, in
   // a partial second wave of 512-thread blocks costs a whole block time.
   long long ks;
   if (kind >= 2) {
-    const int slots = (kind == 2 && Ca % 64 != 0 && knob("MMSEG_WGRAD_V3", 1) == 0) ? 512
-                      : kind == 3 ? knob("MMSEG_WGRAD_RSLOTS", 256)   // runtime-brick kernel (24^3 .. 6^3 levels)
-                                  : knob("MMSEG_WGRAD_SLOTS", 256);
-    ks = (long long)slots * knob("MMSEG_WGRAD_WAVES", 1) / tiles;
+    // (256 slots for the runtime-brick kernel too: 128 / 384 / 512 measured +0.04..0.15 ms per step, r04ah)
+    ks = 256LL / tiles;
   } else {
     ks = (1024 + tiles - 1) / tiles;
   }
@@ -5875,10 +5634,9 @@ int brick_wgrad_splits(long long V, int cap, int Ca, int cpg_shift, int kind, in
   if (kind == 3) {
     const WBrick wb = plan_wgrad_brickr(D, H, W);
     nbrick = V / (wb.bz * wb.by * wb.bx);
-    // at least MMSEG_WGRAD_RMINB bricks per split: at 6^3 (4 bricks) one split writes the gradient directly;
-    // two splits moved 2x the 28 MB fp32 gradient of a 512->512 layer through partials and a reduce
-    // (41 -> 24 us, r02 convbench)
-    const long long minb = knob("MMSEG_WGRAD_RMINB", 4);
+    // at least 4 bricks per split: at 6^3 (4 bricks) one split writes the gradient directly; two splits moved 2x
+    // the 28 MB fp32 gradient of a 512->512 layer through partials and a reduce (41 -> 24 us, r02 convbench)
+    const long long minb = 4;
     if (ks > nbrick / minb) ks = nbrick / minb;
   }
   if (ks > nbrick) ks = nbrick;
@@ -5895,14 +5653,14 @@ int mmseg_wgrad_splits_impl(long long V, int ksplit) {
 
 // Real 32-channel chunks of a channel-padded x (Ci < Cip), 0 = all (the brick wgrad kernels skip the rest; the
 // split reduction never reads the skipped columns' partials into the gradient).
-int wgrad_kchunks(int Cip, int Ci) { return (Ci < Cip && knob("MMSEG_KCHUNKS", 1)) ? (Ci + 31) / 32 : 0; }
+int wgrad_kchunks(int Cip, int Ci) { return Ci < Cip ? (Ci + 31) / 32 : 0; }
 
 // A single-split brick weight gradient writes the torch-layout gradient [co][ci][27] itself when its input
 // channels are unpadded, or padded past whole real 32-channel chunks (Ci % 32 == 0: SwinUNETR's 768 of 1024): the
 // kernel computes only the real chunks (wgrad_kchunks), whose rows then land at pitch 27 Ci (WgradArgs::grad_ld)
-// -- no partial, no relayout reduce (MMSEG_WGRAD_PDIRECT=0: through the partial as before).
+// -- no partial, no relayout reduce.
 bool wgrad_direct_ok(int Cip, int Ci) {
-  return Ci == Cip || (Ci % 32 == 0 && wgrad_kchunks(Cip, Ci) == Ci / 32 && knob("MMSEG_WGRAD_PDIRECT", 1));
+  return Ci == Cip || (Ci % 32 == 0 && wgrad_kchunks(Cip, Ci) == Ci / 32);
 }
 
 // CONV3 weight-gradient plan (mmseg_conv3_wgrad): kernel kind (wgrad_brick_ok), split count, whether the
@@ -5920,13 +5678,11 @@ Conv3WgradPlan plan_conv3_wgrad(long long V, int Co, int Cip, int Ci, int cpg_sh
   const long long per_split = (long long)Co * ncols + Co;
   int cap = (int)(ws_cap / per_split);
   if (cap < 1) cap = 1;
-  // MMSEG_WGRAD_FORCE_R=1: the runtime-brick weight gradient for ungrouped launches too (microbenchmarks)
-  if (knob("MMSEG_WGRAD_FORCE_R", 0)) force_r = true;
   p.kind = wgrad_brick_ok(Co, cpg_shift, D, H, W, lda, ldb, dtype, force_r);
   if (p.kind) {
     p.ksplit = brick_wgrad_splits(V, cap, Co, cpg_shift, p.kind, D, H, W, wgrad_kchunks(Cip, Ci));
   } else {
-    const int bn = knob("MMSEG_WGRAD_BN", 64);
+    const int bn = 64;
     const long long tiles = ((ncols + bn - 1) / bn) * ((Co + (Co % 64 == 0 ? 63 : 31)) / (Co % 64 == 0 ? 64 : 32));
     long long want = (1024 + tiles - 1) / tiles;
     if (want > V / 512) want = V / 512;
@@ -5939,16 +5695,15 @@ Conv3WgradPlan plan_conv3_wgrad(long long V, int Co, int Cip, int Ci, int cpg_sh
   return p;
 }
 
-// split slices S of a reduce: about MMSEG_WGRAD_RPT (default 8) split loads per thread, the slice sums a pairwise
+// split slices S of a reduce: about 8 split loads per thread, the slice sums a pairwise
 // LDS tree; small gradients over many splits (the stem: 1,056 values x 1,024 splits) take more slices until the
 // grid fills the chip, down to 2 loads per thread (S = 64 left it at 66 blocks, 12.8 us for 4 MB)
 int wred_slices(const WReduceArgs& g) {
   const int ksplit = g.ksplit;
   const long long total = (long long)g.Ca * g.Ncols + (g.bias_part ? g.Ca : 0);
-  const int rpt = knob("MMSEG_WGRAD_RPT", 8);
   int S = 1;
-  while (S < 64 && ksplit / (2 * S) >= rpt) S *= 2;
-  while (S < 256 && (total * S + 1023) / 1024 < knob("MMSEG_WGRAD_RBLK", 512) && ksplit / (2 * S) >= 2) S *= 2;
+  while (S < 64 && ksplit / (2 * S) >= 8) S *= 2;
+  while (S < 256 && (total * S + 1023) / 1024 < 512 && ksplit / (2 * S) >= 2) S *= 2;
   return S;
 }
 
@@ -5961,8 +5716,8 @@ struct PendingWred {
 std::vector<PendingWred> g_wred_pending;
 extern "C" int mmseg_wgrad_reduce_flush(void* stream);
 
-// Queue a deferred reduce; once the partials queued on its stream pass MMSEG_WRED_FLUSH_MB (0: never), flush them
-// there and then, while they may still sit in the Infinity Cache (the whole step's partials do not).
+// Queue a deferred reduce (summed by the next mmseg_wgrad_reduce_flush on its stream).  (Flushing early, once
+// 60-240 MB of partials are queued so they are re-read from the Infinity Cache, measured +0.03..0.12 ms: r04.)
 int wred_push(const WReduceArgs& r, int groups, void* stream) {
   // a queued reduce reads its partials when the queue is flushed: a second weight-gradient kernel into the same
   // partial buffer before that would have overwritten them (the engine flushes first: Runtime.own_part)
@@ -5973,28 +5728,16 @@ int wred_push(const WReduceArgs& r, int groups, void* stream) {
       return -1;
     }
   g_wred_pending.push_back({r, groups, stream});
-  const long long cap = (long long)knob("MMSEG_WRED_FLUSH_MB", 0) << 20;
-  if (cap <= 0) return 0;
-  long long bytes = 0;
-  for (const auto& e : g_wred_pending)
-    if (e.stream == stream)
-      bytes += 4LL * e.r.ksplit * e.groups * ((long long)e.r.Ca * e.r.Ncols + (e.r.bias_part ? e.r.Ca : 0));
-  return bytes >= cap && mmseg_wgrad_reduce_flush(stream) < 0 ? -1 : 0;
+  return 0;
 }
 
 int launch_wgrad_reduce(WReduceArgs g, void* stream, int groups = 1) {
   const long long total = (long long)g.Ca * g.Ncols + (g.bias_part ? g.Ca : 0);
   hipStream_t s = (hipStream_t)stream;
   const int S = wred_slices(g);
-  const int U = knob("MMSEG_WRED_U", 4);
 #define MMSEG_WRED(SS, NB)                                                                             \
   case SS:                                                                                             \
-    if (U >= 16)                                                                                       \
-      MMSEG_LAUNCH((wgrad_reduce_kernel<SS, 16>), dim3(ceil_div(total, NB), groups), dim3(256), 0, s, g); \
-    else if (U >= 8)                                                                                   \
-      MMSEG_LAUNCH((wgrad_reduce_kernel<SS, 8>), dim3(ceil_div(total, NB), groups), dim3(256), 0, s, g);  \
-    else                                                                                               \
-      MMSEG_LAUNCH((wgrad_reduce_kernel<SS, 4>), dim3(ceil_div(total, NB), groups), dim3(256), 0, s, g);  \
+    MMSEG_LAUNCH((wgrad_reduce_kernel<SS, 4>), dim3(ceil_div(total, NB), groups), dim3(256), 0, s, g);  \
     break;
   switch (S) {
     MMSEG_WRED(256, 4)
@@ -6099,18 +5842,10 @@ int mmseg_pack_weights_batched(const void* descs, int n, long long total, int dt
 // Bricks per sample whose InstanceNorm partials the CONV3 kernel for this shape
 // can emit from its epilogue (mmseg_conv_gemm_stats), or 0 when it cannot
 // (gather GEMM, split-K).  Every brick holds V / (bricks per sample) voxels.
+// The brick epilogues' fused statistics measured no net gain against the statistics pass (bench r01 q11; the
+// grouped form equal per step, r04ad), so no shape offers them: 0 for every shape (the ABI entry stays).
 int mmseg_conv3_stats_bricks(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,
                              int dtype) {
-  if (!knob("MMSEG_FUSED_STATS", 0)) return 0;   // off by default: no net gain measured (bench r01 q11)
-  const int tsize = dtype == MMSEG_BF16 ? 2 : 4;
-  const Conv3Plan p = plan_conv3(M, Ncols, 8 << cpg_shift, D, H, W, lda, ldo, tsize);
-  if (p.kind == 2) return p.ks == 1 ? (D / p.bz) * (H / p.by) * (W / p.bx) : 0;
-  if (p.kind == 1) {
-    const int nb1 = (M / (D * H * W)) * (D / 4) * (H / B2_Y) * (W / B2_X);
-    const bool bn64 = Ncols % 64 == 0 && nb1 * (Ncols / 64) >= knob("MMSEG_BRICK2_MINBLK", 512);
-    const int zw = (!bn64 && tsize == 2 && D % 8 == 0 && knob("MMSEG_BRICK2_ZW", 1) == 2) ? 2 : 1;
-    return (D / (4 * zw)) * (H / B2_Y) * (W / B2_X);
-  }
   return 0;
 }
 
@@ -6270,7 +6005,7 @@ int conv_gemm_impl(const void* a, int lda, const void* wpacked, const float* bia
   ksplit = ceil_div(KGp, kps);
   GemmArgs g{a, lda, wpacked, bias, out, ldo, splitk_ws, M, Ncols, Cpad, KG, cpg_shift, D, H, W, ksplit, kps,
              knob("MMSEG_SWIZZLE", 1), stats_part,
-             (mode == MODE_CONV3 && knob("MMSEG_KCHUNKS", 1)) ? (cin_real + 31) / 32 : 0, nullptr, nullptr, out2,
+             mode == MODE_CONV3 ? (cin_real + 31) / 32 : 0, nullptr, nullptr, out2,
              ldo2, split};
   if (groups > 1) {
     g.grp_n = M / (D * H * W) / groups;
@@ -6314,7 +6049,6 @@ int mmseg_conv3_fwd_norm(const void* a, int lda, const float* nmean, const float
 
 // Mixed bf16/fp8 forward (config c5): the brick6 shapes of a 3^3 conv with e4m3 operands and fp32 accumulation.
 int mmseg_conv3_fp8_ok(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo) {
-  if (!knob("MMSEG_FP8", 1)) return 0;
   GemmArgs g{};
   g.lda = lda; g.ldo = ldo; g.M = M; g.Ncols = Ncols; g.Cpad = Cpad; g.KG = KG; g.cpg_shift = cpg_shift;
   g.D = D; g.H = H; g.W = W; g.ksplit = 1;
@@ -6345,7 +6079,7 @@ int mmseg_conv3_fwd_fp8(const void* a, int lda, const float* nmean, const float*
   GemmArgs g{a, lda, w8, bias, out, ldo, nullptr, M, Ncols, Cpad, KG, cpg_shift, D, H, W, 1, KGp,
              knob("MMSEG_SWIZZLE", 1), nullptr, 0, nmean, nrstd};
   g.wdq = wdq;
-  launch_brick5(g, (hipStream_t)stream, nullptr, false);
+  launch_brick5(g, (hipStream_t)stream);
   return mmseg::check_launch("conv3_fwd_fp8");
 }
 
@@ -6384,7 +6118,7 @@ int mmseg_conv3_dgrad_in(const void* a, int lda, const void* wpacked, void* out,
   g.inmean = inmean;
   g.inrstd = inrstd;
   g.inpart = inpart;
-  launch_brick5(g, (hipStream_t)stream, nullptr, true);
+  launch_brick5(g, (hipStream_t)stream);
   return mmseg::check_launch("conv3_dgrad_in");
 }
 
@@ -6413,13 +6147,10 @@ int mmseg_conv3_wgrad_group_ok(long long V, int Co, int Cip, int Ci, int cpg_shi
 }
 // split count of a grouped conv (mmseg_conv_gemm_group): the runtime-brick plan's
 // Bricks per sample for which the grouped (forced runtime-brick) conv can emit fused InstanceNorm partials
-// (mmseg_conv_gemm_group_stats): the plan runs one split; 0 otherwise or without MMSEG_GROUP_STATS=1.
+// (mmseg_conv_gemm_group_stats): none (see the function).
 int mmseg_conv3_group_stats_bricks(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda,
                                    int ldo, int dtype) {
-  if (!knob("MMSEG_GROUP_STATS", 0)) return 0;   // off: equal per step (r04ad), the epilogue costs what the pass did
-  const Conv3Plan p = plan_conv3(M, Ncols, 8 << cpg_shift, D, H, W, lda, ldo, dtype == MMSEG_BF16 ? 2 : 4, true);
-  if (p.kind != 2 || p.ks != 1) return 0;
-  return (D / p.bz) * (H / p.by) * (W / p.bx);
+  return 0;   // (as mmseg_conv3_stats_bricks: equal per step, r04ad -- the epilogue costs what the pass did)
 }
 
 int mmseg_conv3_group_splits(int M, int Ncols, int Cpad, int KG, int cpg_shift, int D, int H, int W, int lda, int ldo,
@@ -6459,7 +6190,7 @@ int mmseg_wgrad(const void* a, int lda, const void* b, int ldb, float* part, flo
     ksplit = (int)((V + vps - 1) / vps);
   }
   WgradArgs g{a, lda, b, ldb, part, bias_part, Ca, Ncols, cpg_shift, V, D, H, W, ksplit, vps,
-              knob("MMSEG_WGRAD_SWIZZLE", 1), brick, nullptr, nullptr, 0};
+              1, brick, nullptr, nullptr, 0};
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMSEG_BF16) {
     switch (mode) {
@@ -6512,7 +6243,7 @@ int mmseg_wgrad_reduce_defer(const float* part, float* grad, const float* bias_p
 // ws holds mmseg_conv3_wgrad_ws_floats() floats (more lets it split further, fewer is clamped).
 long long mmseg_conv3_wgrad_ws_floats(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W,
                                       int lddy, int ldx, int dtype) {
-  const long long cap = (long long)knob("MMSEG_WGRAD_CAP_MF", 16) << 20;
+  const long long cap = 16LL << 20;
   return plan_conv3_wgrad(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype, cap).ws;
 }
 
@@ -6526,14 +6257,14 @@ Conv3WgradPlan plan_conv3_wgrad_grouped(long long V, int Co, int Cip, int Ci, in
   if (p.ksplit < groups) p.ksplit = groups;
   // one split per group (the deepest levels): each writes its group's gradient directly, as the ungrouped
   // single-split launch does -- a reduce would only copy 2 x 28 MB there (28.8 us, r04d)
-  p.direct = p.kind >= 2 && p.ksplit == groups && Ci == Cip && knob("MMSEG_WGRAD_GDIRECT", 1);
+  p.direct = p.kind >= 2 && p.ksplit == groups && Ci == Cip;
   p.ws = p.direct ? 0 : (long long)p.ksplit * ((long long)Co * 27 * Cip + Co);
   return p;
 }
 
 long long mmseg_conv3_wgrad_group_ws_floats(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W,
                                             int lddy, int ldx, int groups, int dtype) {
-  const long long cap = (long long)knob("MMSEG_WGRAD_CAP_MF", 16) << 20;
+  const long long cap = 16LL << 20;
   return plan_conv3_wgrad_grouped(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype, cap, groups).ws;
 }
 
@@ -6567,7 +6298,7 @@ int mmseg_conv3_wgrad(const void* dy, int lddy, const void* x, int ldx, float* g
 // a deferred InstanceNorm + ReLU to x), no channel padding, bf16.
 int mmseg_conv3_wgrad_norm_ok(long long V, int Co, int Cip, int Ci, int cpg_shift, int D, int H, int W, int lddy,
                               int ldx, int dtype) {
-  if (dtype != MMSEG_BF16 || Ci != Cip || !knob("MMSEG_WGRAD_V3", 1) || !knob("MMSEG_DEFER_CONV_NORM", 1)) return 0;
+  if (dtype != MMSEG_BF16 || Ci != Cip || !knob("MMSEG_DEFER_CONV_NORM", 1)) return 0;
   return plan_conv3_wgrad(V, Co, Cip, Ci, cpg_shift, D, H, W, lddy, ldx, dtype, 1LL << 40).kind == 2 ? 1 : 0;
 }
 
@@ -6629,11 +6360,6 @@ int mmseg_wgrad_reduce_flush(void* stream) {
       blk += b.nbx[k] * e.groups;
     }
     b.blk0[b.n] = blk;
-    if (knob("MMSEG_WRED_LOG", 0))   // diagnostics: what each batched launch sums
-      for (int k = 0; k < b.n; ++k)
-        fprintf(stderr, "wred_batch %zu.%d: Ca %d Ncols %d ksplit %d groups %d S %d MB %.1f\n", i0, k, b.d[k].Ca,
-                b.d[k].Ncols, b.d[k].ksplit, mine[i0 + k].groups, b.S[k],
-                4.0 * b.d[k].ksplit * mine[i0 + k].groups * b.d[k].Ca * b.d[k].Ncols / 1048576.0);
     mmseg::note_kernel("wgrad_reduce_batch_kernel");
     MMSEG_LAUNCH(wgrad_reduce_batch_kernel, dim3(blk), dim3(256), 0, (hipStream_t)stream, b);
     if (mmseg::check_launch("wgrad_reduce_batch")) return -1;
@@ -6671,18 +6397,18 @@ int conv3_wgrad_impl(const void* dy, int lddy, const void* x, int ldx, const flo
   float* part = p.direct ? nullptr : ws;
   float* bpart = (p.direct || bias_grad == nullptr) ? nullptr : ws + (long long)p.ksplit * Co * ncols;
   const long long vps = ((V + p.ksplit - 1) / p.ksplit + 63) / 64 * 64;
-  // XCD swizzle (MMSEG_WGRAD_SWIZZLE): each XCD walks a contiguous range of (split, row tile, channel chunk) tiles,
+  // XCD swizzle: each XCD walks a contiguous range of (split, row tile, channel chunk) tiles,
   // so the chunks of one brick range -- which all read the same dy -- and neighbouring brick ranges -- which share
   // halo planes -- meet in one L2 (r04e A/B: 6.38 -> 6.35 ms/step)
   WgradArgs g{dy, lddy, x, ldx, part, p.direct ? bias_grad : bpart, Co, ncols, cpg_shift, V, D, H, W, p.ksplit, vps,
-              knob("MMSEG_WGRAD_SWIZZLE", 1), p.kind, p.direct ? grad : nullptr, p.direct ? bias_grad : nullptr,
+              1, p.kind, p.direct ? grad : nullptr, p.direct ? bias_grad : nullptr,
               accumulate, wgrad_kchunks(Cip, Ci), nmean, nrstd};
   hipStream_t s = (hipStream_t)stream;
   g.groups = groups > 1 ? groups : 0;
   g.pad16 = (phase & 8) ? 1 : 0;
   // the row-slab kernel writes fragment-native partials only (2 co tiles of 16)
   const int fmt = wgrad_row_ok(g, dtype == MMSEG_BF16 ? 2 : 4) ? 2
-                  : knob("MMSEG_WGRAD_FRAG", 1) ? wgrad_dma_mt(g, dtype == MMSEG_BF16 ? 2 : 4) : 0;
+                  : wgrad_dma_mt(g, dtype == MMSEG_BF16 ? 2 : 4);
   g.frag = fmt > 0;
   g.groups = groups > 1 ? groups : 0;
   g.grad_gstride = grad_gstride;
@@ -6697,7 +6423,7 @@ int conv3_wgrad_impl(const void* dy, int lddy, const void* x, int ldx, const flo
   const int ng = groups > 1 ? groups : 1;
   WReduceArgs r{part, grad, bpart, bias_grad, Co, ncols, p.ksplit / ng, Cip, Ci, 27, accumulate, p.kind >= 2 ? 1 : 0,
                 fmt, wgrad_nchunk(cpg_shift, g.kchunks), grad_gstride, bias_gstride};
-  r.vec4 = knob("MMSEG_WRED_V4", 1) && r.chmajor && !r.frag_mt && ((uintptr_t)grad & 15) == 0 &&
+  r.vec4 = r.chmajor && !r.frag_mt && ((uintptr_t)grad & 15) == 0 &&
            (ng == 1 || grad_gstride % 4 == 0) && r.Ncols % 4 == 0 && ((long long)r.creal * r.ntap) % 4 == 0;
   if (phase & 4) {   // deferred: summed by the next mmseg_wgrad_reduce_flush on this stream
     return wred_push(r, ng, stream);

@@ -1384,15 +1384,9 @@ bool head_bf16() {
   return e ? atoi(e) != 0 : true;
 }
 
-int loss_vpc() {
-  static const int v = [] {
-    // 1,728 voxels: 1,024 blocks at 96^3 B=2, one full round of the fused statistics kernel (118 VGPRs: 4 blocks
-    // per CU); 2,048 left 864 blocks, 3-4 per CU (83 -> 75 us, tools/headbench.py)
-    const char* e = getenv("MMSEG_LOSS_VPC");
-    return e ? atoi(e) : 1728;
-  }();
-  return v;
-}
+// 1,728 voxels: 1,024 blocks at 96^3 B=2, one full round of the fused statistics kernel (118 VGPRs: 4 blocks per
+// CU); 2,048 left 864 blocks, 3-4 per CU (83 -> 75 us, tools/headbench.py)
+int loss_vpc() { return 1728; }
 
 int loss_chunks(long long V, long long* vpc) {
   const int want = loss_vpc();
@@ -1405,13 +1399,9 @@ int loss_chunks(long long V, long long* vpc) {
 
 // Voxel chunks of the fused head + loss backward, its own grid: 249 VGPRs hold it at two waves per SIMD, so
 // 3,456 voxels (512 blocks at 96^3 B=2) are one full round of 256 CUs x 2 blocks; the statistics pass's 1,024 /
-// 864 blocks took two (114 / 129 -> 110 us, tools/headbench.py).  MMSEG_HEAD_BWD_VPC, 0 = the statistics chunking.
+// 864 blocks took two (114 / 129 -> 110 us, tools/headbench.py).
 int head_bwd_chunks(long long V, long long* vpc) {
-  static const int want = [] {
-    const char* e = getenv("MMSEG_HEAD_BWD_VPC");
-    return e ? atoi(e) : 3456;
-  }();
-  if (want <= 0) return loss_chunks(V, vpc);
+  const int want = 3456;
   long long nch = (V + want - 1) / want;
   if (nch > 4096) nch = 4096;
   if (nch < 1) nch = 1;

@@ -1137,7 +1137,7 @@ __global__ __launch_bounds__(SMALL_T) void in_small_bwd_r(const T* __restrict__ 
   }
 }
 
-// The previous form (MMSEG_IN_SMALL_T=1024): 1024 threads, 10-level LDS tree.
+// (A 1024-thread form with a 10-level LDS tree measured slower and was dropped.)
 constexpr int SMALL_T1K = 1024;
 
 template <typename T, bool RELU>
@@ -1535,22 +1535,13 @@ int knob_small_v() {   // read per call (A/B runs and tests flip it in-process)
   return e ? atoi(e) : 4096;
 }
 
-int knob_small_reg() {   // register-resident small-volume kernels (in_small_fwd_r / in_small_bwd_r)
-  const char* e = getenv("MMSEG_IN_SMALL_REG");
-  return e ? atoi(e) : 1;
-}
+int knob_small_reg() { return 1; }   // register-resident small-volume kernels (in_small_fwd_r / in_small_bwd_r)
 
-int knob_small_t() {
-  const char* e = getenv("MMSEG_IN_SMALL_T");
-  return e ? atoi(e) : 256;
-}
+int knob_small_t() { return 256; }
 
-// at least MMSEG_IN_MINCH chunks per sample (down to 2 voxels per thread): the 48^3 / 24^3 levels otherwise ran
-// 108..432 blocks of 16 voxels per thread, latency-bound
-int knob_in_minch() {
-  const char* e = getenv("MMSEG_IN_MINCH");
-  return e ? atoi(e) : 256;
-}
+// at least 256 chunks per sample (down to 2 voxels per thread): the 48^3 / 24^3 levels otherwise ran 108..432
+// blocks of 16 voxels per thread, latency-bound (128 / 512 measured within noise, r03u)
+int knob_in_minch() { return 256; }
 
 int chunks_for(long long V, int C, long long* vpc) {
   // reduction passes: ~16 voxels per thread (lanes_v = 256 / C8 voxel lanes), at most 1024 chunks
@@ -1965,8 +1956,8 @@ int mmseg_fuse_norm_fwd(const void* const* srcs, const int* lds, const float* co
   s.wts = wts;
   hipStream_t st = (hipStream_t)stream;
   const int grid = grid_for((long long)N * V * (C / 8));
-  const char* e = getenv("MMSEG_FUSE_M");   // 0: the runtime-M kernel (A/B); M = 4 spilled, stays runtime-M
-  const bool cm = (!e || atoi(e) != 0) && M >= 2 && ((long long)grid * 256) % (C / 8) == 0;
+  // compile-time M for 2 and 3 sources (M = 4 spilled and stays runtime-M)
+  const bool cm = M >= 2 && ((long long)grid * 256) % (C / 8) == 0;
   auto run = [&](auto tag) {
     using T = decltype(tag);
     if (cm && M == 2)

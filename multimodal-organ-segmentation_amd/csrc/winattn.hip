@@ -43,8 +43,8 @@ struct WinAttnArgs {
   int B, N, C, heads, hd, nw, T, ldn;
   int w0, w1, w2;        // the module's full window
   float scale;
-  int mixall;            // MMSEG_WINATTN_MIXALL=1: every window takes the mixed-region score code (A/B only)
-  int swz;               // XCD-aware block order (MMSEG_WINATTN_SWZ, default on): a window's heads / query groups,
+  int mixall;            // 1: every window takes the mixed-region score code (the A/B form; 0 in the engine)
+  int swz;               // XCD-aware block order (on): a window's heads / query groups,
                          // which stage the same qkv rows (a head's 32-B slice of each), run on one XCD and share its L2
 };
 
@@ -1085,8 +1085,8 @@ int mmseg_winattn_fwd(const void* qkv, int B, int N, int C, int heads, const flo
                       int w2, const uint8_t* region, int nw, float scale, void* O, float* lse, void* stream) {
   WinAttnArgs a{(const bf16_t*)qkv, nullptr, nullptr, (bf16_t*)O, lse, nullptr, table, region,
                 B, N, C, heads, C / heads, nw, T, 0, w0, w1, w2, scale};
-  a.swz = knob_i("MMSEG_WINATTN_SWZ", 1);
-  a.mixall = knob_i("MMSEG_WINATTN_MIXALL", 0);
+  a.swz = 1;      // XCD-aware block order (r05 (iii))
+  a.mixall = 0;   // the region compare only for windows that mix shifted regions (r05 (vi))
   if (check_args(a)) return 1;
   if (knob_i("MMSEG_WINATTN_FWD1", 1)) {
     mmseg::note_kernel("winattn_fwd1_kernel");
@@ -1106,8 +1106,8 @@ int mmseg_winattn_bwd(const void* qkv, const void* O, const void* dO, const floa
                       void* dqkv, void* dS, int ldn, void* stream) {
   WinAttnArgs a{(const bf16_t*)qkv, (const bf16_t*)O, (const bf16_t*)dO, (bf16_t*)dqkv, const_cast<float*>(lse),
                 (bf16_t*)dS, table, region, B, N, C, heads, C / heads, nw, T, ldn, w0, w1, w2, scale};
-  a.swz = knob_i("MMSEG_WINATTN_SWZ", 1);
-  a.mixall = knob_i("MMSEG_WINATTN_MIXALL", 0);
+  a.swz = 1;      // XCD-aware block order (r05 (iii))
+  a.mixall = 0;   // the region compare only for windows that mix shifted regions (r05 (vi))
   if (check_args(a)) return 1;
   MMSEG_REQUIRE(ldn >= N && ldn % 8 == 0, "winattn_bwd: ldn >= N, multiple of 8");
   hipStream_t s = (hipStream_t)stream;
@@ -1137,8 +1137,8 @@ int mmseg_winattn_bwd_sum(const void* qkv, const void* O, const void* dO, const 
                           float scale, void* dqkv, float* dsum, int ldn, void* stream) {
   WinAttnArgs a{(const bf16_t*)qkv, (const bf16_t*)O, (const bf16_t*)dO, (bf16_t*)dqkv, const_cast<float*>(lse),
                 nullptr, table, region, B, N, C, heads, C / heads, nw, T, ldn, w0, w1, w2, scale};
-  a.swz = knob_i("MMSEG_WINATTN_SWZ", 1);
-  a.mixall = knob_i("MMSEG_WINATTN_MIXALL", 0);
+  a.swz = 1;      // XCD-aware block order (r05 (iii))
+  a.mixall = 0;   // the region compare only for windows that mix shifted regions (r05 (vi))
   if (check_args(a)) return 1;
   MMSEG_REQUIRE(ldn >= N && ldn % 8 == 0 && mmseg_winattn_sum_groups(B, N, heads) > 0,
                 "winattn_bwd_sum: ldn >= N (multiple of 8) and enough windows (mmseg_winattn_sum_groups)");

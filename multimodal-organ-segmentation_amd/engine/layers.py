@@ -68,13 +68,12 @@ def _gemm_ksplit(M: int, ncols: int, KG: int) -> int:
 class Packer:
     """Weight packing of a whole program per step: every 3^3 conv's two operand images in ONE launch
     (mmseg_pack_conv3_batched: one coalesced read of the fp32 weights), the transposed / 1x1 / token-linear
-    images in one more (mmseg_pack_weights_batched).  MMSEG_PACK=0 selects the per-layer element-wise pack
-    (A/B only)."""
+    images in one more (mmseg_pack_weights_batched)."""
 
     def __init__(self, rt: Runtime, descs):
         import struct
         self.rt = rt
-        self.per_layer = list(descs) if os.environ.get("MMSEG_PACK", "1") == "0" else []
+        self.per_layer = []
         self.table = self.gtable = None
         if self.per_layer:
             return
@@ -120,7 +119,7 @@ class Packer:
 
 
 def _wgrad_ksplit(rows: int, ncols: int, V: int) -> int:
-    bn = int(os.environ.get("MMSEG_WGRAD_BN", "64"))
+    bn = 64
     tiles = -(-ncols // bn) * -(-rows // (64 if rows % 64 == 0 else 32))
     return max(1, min(-(-TARGET_BLOCKS // tiles), V // 512))
 
@@ -147,12 +146,6 @@ class DySpec:
     # > 0: p1 holds p1_nmod samples and sample n reads p1's sample n % p1_nmod -- the fused level's gradient shared
     # by the M modality groups of a grouped block (mmseg_instnorm_relu_bwd_group), instead of an M-fold copy
     p1_nmod: int = 0
-
-
-def _aliases(x: Act, dx) -> bool:
-    """True when the data-gradient output(s) dx share a buffer with the weight gradient's input x."""
-    outs = dx if isinstance(dx, tuple) else (dx,)
-    return any(o.buf.data_ptr() == x.buf.data_ptr() for o in outs)
 
 
 class Conv3:
@@ -247,20 +240,16 @@ class Conv3:
         implicit-GEMM path."""
         if self.Co == 48 and self.conv.bias is not None:
             return False
-        return (not self.need_dgrad and self.Cip == 8 and os.environ.get("MMSEG_STEM", "1") != "0"
+        return (not self.need_dgrad and self.Cip == 8
                 and bool(self.rt.lib.mmseg_stem_ok(self.Ci, self.Co, x.D, x.H, x.W, x.ld, y_ld)))
 
     def stats_bricks(self, x: Act, y: Act) -> int:
         """Bricks per sample for which fwd() can emit fused InstanceNorm partials (0 = not available)."""
         if self._stem(x, y.ld):
-            if self.Co == 48:   # the 48-channel stem has no fused statistics (power-of-two lane merges only)
-                return 0
-            # the stem's epilogue can emit its output's statistics per 64-voxel slice (MMSEG_STEM_STATS=1), but off by
-            # default: stem +14.5 us and the slice merge (in_stats_from_bricks, 13,824 slices per sample) 105 us per
-            # launch against a 20 + 5 us statistics pass (rocprofv3 r02h)
-            if os.environ.get("MMSEG_STEM_STATS", "0") != "1":
-                return 0
-            return self.rt.lib.mmseg_stem_stats_bricks(x.D, x.H, x.W)
+            # the stem's epilogue can emit its output's statistics per 64-voxel slice, but that measured slower
+            # (stem +14.5 us and the slice merge 105 us per launch against a 20 + 5 us statistics pass, rocprofv3
+            # r02h): the statistics pass runs (mmseg_stem_fwd_stats stays in the ABI)
+            return 0
         return self.rt.lib.mmseg_conv3_stats_bricks(x.N * x.V, self.Co, self.Cpad, self.KG, self.cpg_shift, x.D, x.H,
                                                     x.W, x.ld, y.ld, self.rt.code)
 
@@ -368,7 +357,7 @@ class Conv3:
         if dx is None and norm is None and (inb is not None or self._stem(x, dy.ld)):
             # 1,024 splits: one round of resident blocks at 96^3 B=2 and half the partials of 2,048 (r02 stembench:
             # 42 + 12.8 us against 44 + 19.7 us with the reduce)
-            ks = L.mmseg_stem_wgrad_splits(x.N, x.D, x.H, x.W, int(os.environ.get("MMSEG_STEM_SPLITS", "1024")))
+            ks = L.mmseg_stem_wgrad_splits(x.N, x.D, x.H, x.W, 1024)
             kp = L.mmseg_stem_kp(self.Ci)
             defer = self.rt.defer_wred(self.flat)
             part = self._part(ks * self.Co * kp + ks * self.Co, own=defer)
@@ -404,25 +393,15 @@ class Conv3:
         # the kernel and its split reduce are timed separately (the roofline family is the kernel alone, as in
         # the rocprofv3 trace)
         # the staged gradient's last 16 rows are output-channel padding (48 of 64): the 64-row kernel skips them
-        pad16 = 8 if (self.wg_stage is not None and rows - self.Co == 16
-                      and os.environ.get("MMSEG_WGRAD_PAD16", "1") != "0") else 0
+        pad16 = 8 if (self.wg_stage is not None and rows - self.Co == 16) else 0
 
         def wkernel(s1):
             with TIMER.region(_gemm_name(self.rt, 0, "conv3"), flops=2.0 * V * self.Co * 27 * self.Ci,
                               nbytes=_io_bytes(self.rt, V, self.Cip, self.Co, 27 * self.Cip * self.Co, 4)):
                 L.mmseg_conv3_wgrad_ex(*args, 1 | pad16, code, s1)
 
-        # weight gradient (kernel + reduce) beside the data gradient (MMSEG_WD_CONC): both only read dy, so when dx
-        # does not overwrite x the two MFMA launches can share the chip -- the tail of one (a partial last round of
-        # blocks, the partials' write burst) overlaps the other
-        conc = (wsf > 0 and dx is not None and self.rt.async_wred and os.environ.get("MMSEG_WD_CONC", "0") != "0"
-                and not _aliases(x, dx))
-        if conc:
-            def both(s2):
-                wkernel(s2)
-                reduce(s2)
-        else:
-            wkernel(s)
+        # (the weight gradient beside the data gradient on a side stream measured slower: DESIGN (d) round 4)
+        wkernel(s)
 
         def reduce(s2):
             with TIMER.region("wgrad_reduce_kernel"):
@@ -434,9 +413,7 @@ class Conv3:
                 else:
                     wgrad.view(-1).copy_(self.wg_stage[:n])
             self.flat.mark(*[p for p in (self.conv.weight, self.conv.bias) if p is not None])
-        if conc:
-            self._reduce_after(both)
-        elif wsf > 0:
+        if wsf > 0:
             self._reduce_after(reduce)
         else:
             reduce(s)
@@ -725,12 +702,6 @@ class Block:
         if not out_done:
             self._norm_bwd(self.x2, st[2], st[3], dy, g2)
         dy1 = self.y1                     # conv2 wgrad reads y1 before dgrad overwrites it
-        if not self.defer1 and os.environ.get("MMSEG_WD_CONC", "0") != "0":
-            # a buffer of its own, so conv2's weight and data gradients can run side by side (Conv3.bwd)
-            if getattr(self, "_dy1b", None) is None or self._dy1b.buf.numel() != self.y1.buf.numel():
-                y1 = self.y1
-                self._dy1b = self.rt.act(y1.N, y1.D, y1.H, y1.W, y1.C, y1.ld)
-            dy1 = self._dy1b
         # conv2's data gradient may also sum conv1's InstanceNorm-backward partials (brick5 shapes)
         inp = (self.x1, st[0], st[1])
         if self.defer1:                   # (y1 was never written: the weight gradient normalises x1 itself)
@@ -851,13 +822,8 @@ class ConvGroup:
                 L.mmseg_conv3_wgrad_group(*args, 6 if defer else 2, code, s2)
             for cc in self.convs:
                 self.flat.mark(*[p for p in (cc.conv.weight, cc.conv.bias) if p is not None])
-        conc = (dx is not None and self.rt.async_wred and os.environ.get("MMSEG_WD_CONC", "0") != "0"
-                and not _aliases(x, dx))
-        if conc:                          # weight gradient beside the data gradient (Conv3.bwd)
-            c._reduce_after(lambda s2: (wkernel(s2), reduce(s2)))
-        else:
-            wkernel(self.rt.stream)
-            c._reduce_after(reduce)
+        wkernel(self.rt.stream)
+        c._reduce_after(reduce)
         try:
             if dx is None:
                 return
@@ -944,11 +910,6 @@ class GroupBlock(Block):
         g2 = self.x2
         self._norm_bwd(self.x2, st[2], st[3], dy, g2)
         dy1 = self.y1                     # the weight gradient reads y1 before the data gradient overwrites it
-        if os.environ.get("MMSEG_WD_CONC", "0") != "0":
-            if getattr(self, "_dy1b", None) is None or self._dy1b.buf.numel() != self.y1.buf.numel():
-                y1 = self.y1
-                self._dy1b = self.rt.act(y1.N, y1.D, y1.H, y1.W, y1.C, y1.ld)
-            dy1 = self._dy1b
         self.g2.bwd(self.y1, g2, dy1, accumulate)
         g1 = self.x1
         self._norm_bwd(self.x1, st[0], st[1], DySpec(p1=dy1), g1)

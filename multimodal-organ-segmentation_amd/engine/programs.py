@@ -111,7 +111,7 @@ class _Decoder:
         """Returns the gradient of `bottom` (aliases `bottom`'s buffer).  gout (a device scalar) instead of
         dlogits: the fused head + loss backward of a forward that ran with `loss`."""
         nl = len(self.F) - 1
-        self.split_bwd = os.environ.get("MMSEG_SPLIT_DCAT", "1") != "0"
+        self.split_bwd = True     # d(cat) as two dense tensors (mmseg_conv_gemm_split)
         dh = self.dout[0]
         hpart = None
         if gout is not None:
@@ -169,10 +169,8 @@ class UNetProgram:
         self.xin = rt.act(N, *dims[0], 8)
         self.dec.setup(N, dims)
         self.pooled = [None] + [rt.act(N, *dims[l], F[l - 1]) for l in range(1, self.L)]
-        # d(pooled): over pooled itself, or (MMSEG_WD_CONC) buffers of their own so that a block's conv1 weight and
-        # data gradients do not alias and can run side by side (layers.Conv3.bwd)
-        self.dpooled = ([None] + [rt.act(N, *dims[l], F[l - 1]) for l in range(1, self.L)] if _wd_conc()
-                        else self.pooled)
+        # d(pooled): over pooled itself (the weight gradient reads pooled before the data gradient overwrites it)
+        self.dpooled = self.pooled
         self.idx = [None] + [torch.empty(N * dims[l][0] * dims[l][1] * dims[l][2] * F[l - 1], dtype=torch.uint8,
                                          device=rt.device) for l in range(1, self.L)]
         self.bottom = rt.act(N, *dims[-1], F[-1])
@@ -289,13 +287,11 @@ class DualEncoderProgram:
         # views of it (a grouped op reads all modalities at once, everything else its own view)
         vol = [d[0] * d[1] * d[2] for d in dims]
         self.pooled_c = [None] + [rt.act(M * N, *dims[l], F[l - 1]) for l in range(1, self.L)]
-        self.dpooled_c = ([None] + [rt.act(M * N, *dims[l], F[l - 1]) for l in range(1, self.L)] if _wd_conc()
-                          else self.pooled_c)
+        self.dpooled_c = self.pooled_c   # (gradients over the pooled tensors, as UNetProgram)
         self.idx_c = [None] + [torch.empty(M * N * vol[l] * F[l - 1], dtype=torch.uint8, device=rt.device)
                                for l in range(1, self.L)]
         self.pooled = [[None] + [act_group_view(self.pooled_c[l], m, N) for l in range(1, self.L)] for m in range(M)]
-        self.dpooled = ([[None] + [act_group_view(self.dpooled_c[l], m, N) for l in range(1, self.L)]
-                         for m in range(M)] if _wd_conc() else self.pooled)
+        self.dpooled = self.pooled
         self.idx = [[None] + [self.idx_c[l][m * N * vol[l] * F[l - 1]:(m + 1) * N * vol[l] * F[l - 1]]
                               for l in range(1, self.L)] for m in range(M)]
         self.bottom = rt.act(N, *dims[-1], F[-1])
@@ -325,8 +321,6 @@ class DualEncoderProgram:
             self.pooled_g[l] = xin
             self.dpooled_g[l] = self.dpooled_c[l]
             self.y_g[l] = rt.act(M * N, *dims[l], F[l])
-            if os.environ.get("MMSEG_GROUP_REPLICATE", "0") != "0":
-                self.rep[l] = rt.act(M * N, *dims[l], F[l])
             self.idx_g[l] = self.idx_c[l]
             for mm in range(M):
                 self.y[mm][l] = act_group_view(self.y_g[l], mm, N)
@@ -353,15 +347,6 @@ class DualEncoderProgram:
                 b.x2 = act_group_view(x2c, m, N)
                 b.stats = stc[:, m * N * C:(m + 1) * N * C]
             self.x2c[l], self.statsc[l] = x2c, stc
-
-    def _replicate(self, src: Act, dst: Act):
-        """dst (M x N samples) = src (N samples) repeated M times: the fused level's gradient, which every modality's
-        InstanceNorm backward reads (scaled 1/M), for the grouped one-launch backward."""
-        N, V, C = src.N, src.V, src.C
-        # element (n, v, c) at buf[(n V + v) ld + off + c] (off may reach past the first row: decoder dsplit halves)
-        s = src.buf.as_strided((N * V, C), (src.ld, 1), src.buf.storage_offset() + src.off)
-        d = dst.buf.as_strided((self.M, N * V, C), (N * V * dst.ld, dst.ld, 1), dst.buf.storage_offset() + dst.off)
-        d.copy_(s.unsqueeze(0).expand(self.M, N * V, C))
 
     def fused_out(self, l: int) -> Act:
         return self.dec.skip_slot(l) if l < self.L - 1 else self.bottom
@@ -438,7 +423,7 @@ class DualEncoderProgram:
     def stream_level(self) -> int:
         """First level whose encoder work runs on the modality streams: the 96^3 / 48^3 levels fill the chip
         on their own (run concurrently they only contend for L2 / Infinity Cache), the smaller ones do not."""
-        return int(os.environ.get("MMSEG_STREAM_FROM_LEVEL", "2"))
+        return 2
 
     def _group_fwd_levels(self):
         """Levels l0 .. L-1 for all modalities at once (the maxpool into l0 ran per modality, into the views)."""
@@ -577,12 +562,9 @@ class DualEncoderProgram:
 
         if self.l0 < self.L:                          # grouped small levels: all modalities per launch
             for l in range(self.L - 1, self.l0 - 1, -1):
-                if os.environ.get("MMSEG_GROUP_REPLICATE", "0") != "0":   # the previous M-fold copy (A/B)
-                    self._replicate(self.dfused(l), self.rep[l])
-                    dy = DySpec(p1=self.rep[l], scale1=sc)
-                else:   # every modality group reads the fused gradient's sample n % N (no copy)
-                    p1 = self.dfused(l)
-                    dy = DySpec(p1=p1, scale1=sc, p1_nmod=p1.N)
+                # every modality group reads the fused gradient's sample n % N (no M-fold copy: -0.03 ms, r04aa)
+                p1 = self.dfused(l)
+                dy = DySpec(p1=p1, scale1=sc, p1_nmod=p1.N)
                 if l < self.L - 1:
                     dy.pool_dy = self.dpooled_g[l + 1]
                     dy.pool_idx = self.idx_g[l + 1]
@@ -620,10 +602,6 @@ class DualEncoderProgram:
             levels(m, split, 0)
 
 
-def _wd_conc() -> bool:
-    return os.environ.get("MMSEG_WD_CONC", "0") != "0"
-
-
 def _ptr_array(ptrs):
     return (ctypes.c_void_p * len(ptrs))(*ptrs)
 
@@ -638,7 +616,7 @@ def _pack_input(rt, block, x: torch.Tensor, c0: int, cnt: int, xin: Act) -> Act:
     halo reads move 2*cnt bytes per voxel instead of 16; otherwise the 8-channel engine layout."""
     N, Ctot, D, H, W = x.shape
     xc = Act(xin.buf, 0, cnt, cnt, xin.N, xin.D, xin.H, xin.W)
-    if os.environ.get("MMSEG_STEM_COMPACT", "1") != "0" and block.c1._stem(xc, block.Co):
+    if block.c1._stem(xc, block.Co):
         rt.lib.mmseg_pack_input_compact(ptr(x), Ctot, c0, cnt, N, D * H * W, xc.ptr, rt.code, rt.stream)
         return xc
     rt.lib.mmseg_pack_input(ptr(x), Ctot, c0, cnt, N, D * H * W, xin.ptr, rt.code, rt.stream)

@@ -97,11 +97,10 @@ class Runtime:
         self.fp8 = fp8
         self.lib = lib()
         self._ws: Dict[int, torch.Tensor] = {}      # one scratch arena per HIP stream
-        # weight-gradient split reduces on a side stream (MMSEG_ASYNC_WRED=1): each reduce waits for its own
-        # weight-gradient kernel only, so it can run beside the layer's data-gradient kernel.  Off by default:
-        # measured +0.3 ms per 96^3 step (6.45 -> 6.75 ms, r04c A/B) -- in the captured graph every fork / join
-        # is a cross-queue dependency that costs more than the overlap wins
-        self.async_wred = os.environ.get("MMSEG_ASYNC_WRED", "0") != "0"
+        # weight-gradient split reduces in line: on a side stream beside the layer's data-gradient kernel they
+        # measured +0.3 ms per 96^3 step (6.45 -> 6.75 ms, r04c A/B) -- in the captured graph every fork / join is a
+        # cross-queue dependency that costs more than the overlap wins -- and were removed (round 6)
+        self.async_wred = False
         self._side: Optional[torch.cuda.Stream] = None
         self._side_pending = False
         # weight-gradient split reduces batched (MMSEG_WRED_BATCH): inside a backward session (`wred_session`) each

@@ -399,7 +399,7 @@ class SwinBlockProg:
             offs, pairs, T = geo["csr"]
             # many windows: the score gradient summed over window groups on chip (fp32, mmseg_winattn_bwd_sum),
             # so the bias-table gradient folds a few group sums instead of every window's bf16 dS
-            ng = L.mmseg_winattn_sum_groups(B, Nw, self.heads) if os.environ.get("MMSEG_WINATTN_SUM", "1") != "0" else 0
+            ng = L.mmseg_winattn_sum_groups(B, Nw, self.heads)
             # algorithmic backward work: dP = dO V^T, dV = P^T dO, dK = dS^T Q (the key pass, 3 x 2 Nw^2 hd) and
             # dQ = dS K (the query pass, 2 Nw^2 hd); the recomputed scores are not counted
             v2 = "2" if os.environ.get("MMSEG_WINATTN_BWD2", "1") != "0" else ""   # (winattn.hip's default)

@@ -167,8 +167,7 @@ class Trainer:
         # collective (one batched launch per bucket instead of one reduce launch per layer)
         bb = getattr(self.model, "backbone", self.model)
         rt = getattr(bb.__dict__.get("_engine"), "rt", None)
-        batched = (communicate and rt is not None and rt.batch_wred
-                   and os.environ.get("MMSEG_DP_WRED_BATCH", "1") != "0")
+        batched = communicate and rt is not None and rt.batch_wred   # (per-layer reduces under DP: +0.05 ms, r05h)
         flat.flush_before_ready = rt.flush_wred if batched else None
 
         def pre_reduce():

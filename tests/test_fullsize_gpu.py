@@ -269,9 +269,11 @@ def test_group_force_runs_other_kernels(dev, monkeypatch):
         tr = Trainer(cfg, m)
         m.train()
         TIMER.start()
-        lossv = tr._fused_loss(x, y)
-        lossv.backward()
-        TIMER.stop()
+        try:
+            lossv = tr._fused_loss(x, y)
+            lossv.backward()
+        finally:
+            TIMER.stop()          # (a failure here must not leave the timer on for later tests: it disables graphs)
         fams = {}
         for fam, *_ in TIMER.records():
             fams[fam] = fams.get(fam, 0) + 1

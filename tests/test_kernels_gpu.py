@@ -55,38 +55,28 @@ def test_conv3_fwd_dgrad_wgrad(dev, dtype, cin, cout, shape):
     ({"MMSEG_BRICK2_MINBLK": "0"}, 64, 64, (2, 8, 16, 8)),          # BN64 ZW1
     ({"MMSEG_BRICK2_MINBLK": "0"}, 32, 128, (1, 4, 8, 16)),         # BN64 ZW1, 2 column tiles
     # brick v3 (bf16 BN32 default; f32 takes v2): persistent blocks over several bricks / column tiles
-    ({"MMSEG_BRICK4": "0", "MMSEG_BRICK3_BLOCKS": "2"}, 32, 32, (2, 8, 16, 8)),   # 8 bricks over 2 blocks
     ({"MMSEG_BRICK3_BLOCKS": "3"}, 64, 128, (1, 4, 16, 16)),         # 4 col tiles x 4 bricks, ragged ranges
-    ({"MMSEG_BRICK4": "0", "MMSEG_BRICK3_BLOCKS": "0"}, 32, 32, (1, 12, 8, 24)),  # one unit per block, border
+    ({"MMSEG_BRICK3_BLOCKS": "0"}, 64, 32, (1, 12, 8, 24)),          # one unit per block, border (2 chunks)
     # brick v4 (bf16, Cin 32, register-resident weights, double-buffered halo; f32 takes v2)
     ({"MMSEG_BRICK4_BLOCKS": "3"}, 32, 32, (2, 8, 16, 8)),           # 8 bricks over 3 blocks, ragged ranges
     ({"MMSEG_BRICK4_BLOCKS": "4"}, 32, 64, (1, 4, 8, 16)),           # 2 column tiles x 2 blocks each
     ({}, 32, 32, (1, 12, 8, 24)),                                    # one brick per block, border bricks
-    ({"MMSEG_BRICK4_BLOCKS": "1", "MMSEG_BRICK5": "0"}, 32, 32, (2, 8, 16, 16)),   # v4, one block, 16 bricks
     # brick v5 (W % 16: 4x4x16 bricks, ky-shared A fragments)
     ({"MMSEG_BRICK4_BLOCKS": "1"}, 32, 32, (2, 8, 16, 16)),          # one block over all 16 bricks of 2 samples
     ({"MMSEG_BRICK4_BLOCKS": "3"}, 32, 32, (2, 8, 8, 32)),           # 16 bricks over 3 blocks, ragged ranges
     ({}, 32, 32, (1, 12, 12, 16)),                                   # border bricks on every side
     ({"MMSEG_BRICK4_BLOCKS": "4"}, 32, 64, (1, 4, 4, 32)),           # 2 column tiles
-    # brick v6 (v5's register-staged path with the staging interleaved between the MFMAs; default) against v5,
-    # and with the staged rows written from group 6 / 7 on
-    ({"MMSEG_BRICK6": "0", "MMSEG_BRICK4_BLOCKS": "3"}, 32, 32, (2, 8, 8, 32)),
-    ({"MMSEG_BRICK6_SG0": "6", "MMSEG_BRICK4_BLOCKS": "3"}, 32, 32, (2, 8, 8, 32)),
-    ({"MMSEG_BRICK6_SG0": "7"}, 32, 32, (1, 12, 12, 16)),
-    ({"MMSEG_BRICK6_SG0": "6", "MMSEG_BRICK4_BLOCKS": "1"}, 32, 32, (2, 4, 4, 16)),   # one brick per sample
-    ({"MMSEG_BRICK3_BN64": "1", "MMSEG_BRICK2_MINBLK": "0", "MMSEG_BRICK3_BLOCKS": "2"}, 64, 64, (2, 8, 8, 8)),
-    ({"MMSEG_BRICK2_ZW": "2"}, 32, 32, (1, 8, 8, 16)),              # BN32 ZW2 (bf16 only; f32 takes ZW1)
-    ({"MMSEG_BRICK2_ZW": "2"}, 64, 32, (2, 8, 8, 8)),               # BN32 ZW2, dgrad with 2 input chunks
+    # brick v6 (v5's register-staged path with the staging interleaved between the MFMAs)
+    ({"MMSEG_BRICK4_BLOCKS": "1"}, 32, 32, (2, 4, 4, 16)),           # one brick per sample
     ({}, 128, 32, (1, 4, 16, 8)),                                   # BN32 ZW1, 4 input chunks
     ({}, 256, 128, (2, 12, 12, 12)),                                 # runtime brick (3,6,12) + chunk split-K
     ({}, 512, 256, (1, 6, 6, 6)),                                    # runtime brick (6,6,6), 16 chunks
     ({"MMSEG_BRICKR": "0"}, 256, 128, (2, 12, 12, 12)),              # same through the gather GEMM
-    # runtime brick 6x6x6 with the in-block K split over two 256-thread halves (KW = 2, bf16; r05) against KW = 1,
-    # and an odd chunk count per block (2 + 1: half 1 idles through the last stages' barriers)
-    ({"MMSEG_BRICKR_KW": "1"}, 512, 256, (1, 6, 6, 6)),
+    # runtime brick 6x6x6 with the in-block K split over two 256-thread halves (KW = 2, bf16; r05), and an odd chunk
+    # count per block (2 + 1: half 1 idles through the last stages' barriers)
     ({}, 256, 256, (4, 12, 12, 12)),                                 # the grouped 12^3 shape (N = M x B = 4)
     ({"MMSEG_BRICKR_SLOTS": "6"}, 256, 32, (2, 6, 6, 6)),           # 8 chunks over 3 splits: 3 (2 + 1), 3, 2
-    ({"MMSEG_BRICKR_SLOTS": "1", "MMSEG_BRICKR_PF32": "0"}, 128, 32, (2, 6, 6, 6)),
+    ({"MMSEG_BRICKR_SLOTS": "1"}, 128, 32, (2, 6, 6, 6)),
     ({"MMSEG_WGRAD_BRICK": "1"}, 64, 128, (2, 4, 8, 8)),             # v1 brick wgrad (32 co per block)
     ({"MMSEG_WGRAD_BRICK": "0"}, 64, 64, (1, 4, 8, 8)),              # generic wgrad
     ({}, 32, 128, (1, 8, 4, 16)),                                    # v2 brick wgrad, 2 row tiles of 64 co
@@ -124,14 +114,13 @@ def test_conv3_kernel_variants(dev, dtype, knobs, cin, cout, shape, monkeypatch)
     (64, 32, (1, 8, 16, 24), {"MMSEG_BRICK": "3"}, "conv3_brickr_kernel<BN32>"),
 ])
 def test_b32_halo_staging(dev, dtype, cin, cout, shape, extra, kernel, monkeypatch):
-    """The 32-bit-offset halo staging (MMSEG_BRICK2_B32 / MMSEG_BRICKR_B32: buffer loads whose out-of-volume lanes
-    read zeros) against the 64-bit staging, in BOTH storage types (fp32 through MMSEG_B32_F32=1), on shapes with
-    border bricks on every side: forward and data gradient bitwise equal (only the loads differ), and both against
-    the fp64 evaluation (_check_conv3).  (The 48-column brick2 variant is covered by the SwinUNETR tests, whose
-    48-channel layers are its only users.)"""
+    """The 32-bit-offset halo staging of the bf16 brick2 / runtime-brick kernels (MMSEG_B32: buffer loads whose
+    out-of-volume lanes read zeros) against the 64-bit staging (=0; the fp32 path's), on shapes with border bricks
+    on every side: forward and data gradient bitwise equal (only the loads differ), and both against the fp64
+    evaluation (_check_conv3).  (The 48-column brick2 variant is covered by the SwinUNETR tests, whose 48-channel
+    layers are its only users.)"""
     for k, v in extra.items():
         monkeypatch.setenv(k, v)
-    monkeypatch.setenv("MMSEG_B32_F32", "1")
     torch.manual_seed(cin + cout)
     conv = nn.Conv3d(cin, cout, 3, padding=1).to(dev)
     N, D, H, W = shape
@@ -139,8 +128,7 @@ def test_b32_halo_staging(dev, dtype, cin, cout, shape, extra, kernel, monkeypat
     dy = torch.randn(N, cout, D, H, W, device=dev)
     res = []
     for b32 in ("1", "0"):
-        monkeypatch.setenv("MMSEG_BRICK2_B32", b32)
-        monkeypatch.setenv("MMSEG_BRICKR_B32", b32)
+        monkeypatch.setenv("MMSEG_B32", b32)
         rt = Runtime(dev, dtype)
         flat = FlatParams(list(conv.parameters()))
         layer = Conv3(rt, conv, flat)
@@ -504,42 +492,11 @@ def test_batched_conv3_pack_matches_per_layer_pack(dev, dtype):
             assert torch.equal(wd, l.wd)
 
 
-@pytest.mark.parametrize("dtype", DTYPES)
-@pytest.mark.parametrize("knobs,cin,cout,shape", [
-    ({"MMSEG_FUSED_STATS": "1"}, 32, 32, (2, 8, 8, 16)),                              # brick2 BN32
-    ({"MMSEG_FUSED_STATS": "1", "MMSEG_BRICK2_MINBLK": "0"}, 32, 64, (1, 4, 8, 8)),   # brick2 BN64
-    ({"MMSEG_FUSED_STATS": "1", "MMSEG_BRICK2_ZW": "2"}, 32, 32, (1, 8, 8, 8)),      # brick2 ZW2 (bf16 only)
-    ({"MMSEG_FUSED_STATS": "1"}, 64, 64, (2, 6, 6, 6)),                               # runtime brick, no split
-])
-def test_conv3_fused_instnorm_stats(dev, dtype, knobs, cin, cout, shape, monkeypatch):
-    """per-brick (mean, M2) from the conv epilogue + mmseg_instnorm_stats_bricks == InstanceNorm statistics of the
-    stored output (fp64 reference on the same stored values)."""
-    for k, v in knobs.items():
-        monkeypatch.setenv(k, v)
-    torch.manual_seed(cin * 7 + cout)
-    conv = nn.Conv3d(cin, cout, 3, padding=1).to(dev)
-    rt = Runtime(dev, dtype)
-    flat = FlatParams(list(conv.parameters()))
-    layer = Conv3(rt, conv, flat)
-    N, D, H, W = shape
-    x = torch.randn(N, cin, D, H, W, device=dev)
-    xa = _act(x, dtype)
-    ya = rt.act(N, D, H, W, cout)
-    layer.pack()
-    nb = layer.stats_bricks(xa, ya)
-    if nb == 0:
-        pytest.skip("no fused-statistics kernel for this shape/dtype")
-    part = torch.empty(N * nb * cout * 2, device=dev)
-    layer.fwd(xa, ya, stats_part=part)
-    mean = torch.empty(N * cout, device=dev)
-    rstd = torch.empty(N * cout, device=dev)
-    lib().mmseg_instnorm_stats_bricks(ptr(part), N, cout, nb, D * H * W // nb, 1e-5, ptr(mean), cout, ptr(rstd),
-                                      stream_handle())
-    y = from_ndhwc(ya.buf, N, cout, D, H, W).double().cpu().reshape(N, cout, -1)
-    m_ref = y.mean(-1)
-    r_ref = 1.0 / torch.sqrt(y.var(-1, unbiased=False) + 1e-5)
-    assert rel(mean.cpu().reshape(N, cout), m_ref) < 1e-5
-    assert rel(rstd.cpu().reshape(N, cout), r_ref) < 1e-5
+def test_conv3_fused_stats_not_offered(dev):
+    """The brick epilogues' fused InstanceNorm statistics measured no net gain (DESIGN round 2 / 4) and were removed
+    with their knobs in round 6: the library offers them for no shape, so the engine always runs the statistics
+    pass."""
+    assert lib().mmseg_conv3_stats_bricks(2 * 8 * 8 * 16, 32, 32, 27 * 4, 2, 8, 8, 16, 32, 32, 1) == 0
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
@@ -615,49 +572,11 @@ def test_conv3_dgrad_split_output(dev, dtype, knobs, cin, cout, shape, monkeypat
 
 
 @pytest.mark.parametrize("cin,cout,shape,accumulate", [
-    (64, 64, (2, 8, 12, 16), 0), (32, 128, (2, 8, 8, 16), 1), (64, 32, (2, 8, 4, 16), 1),
-    (32, 32, (2, 12, 8, 24), 0), (64, 64, (2, 24, 24, 24), 1), (64, 32, (2, 24, 24, 24), 0)])
-def test_wgrad_dma_halo_ring(dev, cin, cout, shape, accumulate, monkeypatch):
-    """wgrad_dma with the z-plane halo ring (MMSEG_WGRAD_RING=1: bricks walked z-fastest, a column's next brick
-    stages only its four new halo planes into rotating slots) against the per-brick halo (=0) and against fp64.
-    The ring changes which bricks a split sums and in what order, so the two agree to bf16-input rounding of the
-    fp32 sums, not bitwise; both held to the fp64 weight / bias gradient."""
-    N, D, H, W = shape
-    V = N * D * H * W
-    g = torch.Generator().manual_seed(7 * cin + cout + V)
-    dy = torch.randn(V, cout, generator=g).to(dev, torch.bfloat16).reshape(-1)
-    x = torch.randn(V, cin, generator=g).to(dev, torch.bfloat16).reshape(-1)
-    gw0 = torch.randn(cout * cin * 27, generator=g).to(dev) if accumulate else torch.zeros(cout * cin * 27, device=dev)
-    gb0 = torch.ones(cout, device=dev) if accumulate else torch.zeros(cout, device=dev)
-    L = lib()
-    shift = int(np.log2(cin // 8))
-    wsf = L.mmseg_conv3_wgrad_ws_floats(V, cout, cin, cin, shift, D, H, W, cout, cin, 1)
-    out = {}
-    for ring in ("0", "1"):
-        monkeypatch.setenv("MMSEG_WGRAD_RING", ring)
-        ws = torch.full((max(wsf, 1),), float("nan"), device=dev)
-        gw, gb = gw0.clone(), gb0.clone()
-        L.mmseg_conv3_wgrad(ptr(dy), cout, ptr(x), cin, ptr(gw), ptr(gb), cout, cin, cin, shift, V, D, H, W,
-                            ptr(ws), wsf, accumulate, 1, stream_handle())
-        assert L.mmseg_last_kernel().decode().startswith("wgrad_dma_kernel")
-        torch.cuda.synchronize()
-        out[ring] = (gw.double().cpu() - gw0.double().cpu(), gb.double().cpu() - gb0.double().cpu())
-    xr = x.double().cpu().reshape(N, D, H, W, cin).permute(0, 4, 1, 2, 3)
-    dyr = dy.double().cpu().reshape(N, D, H, W, cout).permute(0, 4, 1, 2, 3)
-    ref = torch.nn.grad.conv3d_weight(xr, (cout, cin, 3, 3, 3), dyr, padding=1).reshape(-1)
-    refb = dyr.sum(dim=(0, 2, 3, 4))
-    for ring in ("0", "1"):
-        assert rel(out[ring][0], ref) < 1e-4 and rel(out[ring][1], refb) < 1e-4, ring
-    assert rel(out["1"][0], out["0"][0]) < 1e-4
-
-
-@pytest.mark.parametrize("cin,cout,shape,accumulate", [
     (64, 64, (2, 8, 12, 16), 0), (32, 128, (2, 8, 8, 16), 1), (64, 32, (2, 8, 4, 16), 0),
-    (128, 64, (2, 8, 8, 16), 1), (32, 32, (2, 12, 8, 24), 0)])
-def test_wgrad_dma_fragment_partials_bitwise(dev, cin, cout, shape, accumulate, monkeypatch):
-    """wgrad_dma's split partials in the accumulators' own layout (MMSEG_WGRAD_FRAG=1, direct 16-B stores from
-    registers) against the channel-major layout through the LDS transpose (=0): the reduce sums every element
-    over the same splits in the same fixed order, so weight and bias gradients must be BITWISE equal."""
+    (128, 64, (2, 8, 8, 16), 1), (32, 32, (2, 12, 8, 24), 0), (64, 64, (2, 24, 24, 24), 1)])
+def test_wgrad_dma_fragment_partials(dev, cin, cout, shape, accumulate):
+    """wgrad_dma's split partials in the accumulators' own layout (direct 16-B stores from registers; the reduce maps
+    them to the torch order in a fixed split order): weight and bias gradients against fp64, bitwise repeatable."""
     N, D, H, W = shape
     V = N * D * H * W
     g = torch.Generator().manual_seed(cin + cout + V)
@@ -669,34 +588,31 @@ def test_wgrad_dma_fragment_partials_bitwise(dev, cin, cout, shape, accumulate, 
     shift = int(np.log2(cin // 8))
     wsf = L.mmseg_conv3_wgrad_ws_floats(V, cout, cin, cin, shift, D, H, W, cout, cin, 1)
     assert wsf > 0, "single split: nothing to reduce"
-    out = {}
-    for frag in ("0", "1"):
-        monkeypatch.setenv("MMSEG_WGRAD_FRAG", frag)
+    out = []
+    for _ in range(2):
         ws = torch.full((wsf,), float("nan"), device=dev)
         gw, gb = gw0.clone(), gb0.clone()
         L.mmseg_conv3_wgrad(ptr(dy), cout, ptr(x), cin, ptr(gw), ptr(gb), cout, cin, cin, shift, V, D, H, W,
                             ptr(ws), wsf, accumulate, 1, stream_handle())
         assert L.mmseg_last_kernel().decode().startswith("wgrad_dma_kernel")
         torch.cuda.synchronize()
-        out[frag] = (gw, gb)
-    assert torch.equal(out["0"][0], out["1"][0]) and torch.equal(out["0"][1], out["1"][1])
-    # and against fp64 (the torch layout the reduce writes)
+        out.append((gw, gb))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
     xr = x.double().cpu().reshape(N, D, H, W, cin).permute(0, 4, 1, 2, 3)
     dyr = dy.double().cpu().reshape(N, D, H, W, cout).permute(0, 4, 1, 2, 3)
     ref = torch.nn.grad.conv3d_weight(xr, (cout, cin, 3, 3, 3), dyr, padding=1).reshape(-1)
-    got = out["1"][0].double().cpu() - gw0.double().cpu()
+    got = out[1][0].double().cpu() - gw0.double().cpu()
     assert rel(got, ref) < GTOL[torch.bfloat16]
-    assert rel(out["1"][1].double().cpu() - gb0.double().cpu(), dyr.sum(dim=(0, 2, 3, 4))) < GTOL[torch.bfloat16]
+    assert rel(out[1][1].double().cpu() - gb0.double().cpu(), dyr.sum(dim=(0, 2, 3, 4))) < GTOL[torch.bfloat16]
 
 
 @pytest.mark.parametrize("norm", [False, True])
 @pytest.mark.parametrize("cin,cout,shape,accumulate", [
     (32, 32, (2, 12, 8, 24), 0), (64, 32, (2, 8, 4, 16), 1), (32, 32, (1, 8, 8, 8), 1), (32, 32, (2, 24, 24, 24), 0)])
-def test_wgrad_brick2_pipelined_bitwise(dev, cin, cout, shape, accumulate, norm, monkeypatch):
-    """The 32-co register-staged brick wgrad (the deferred-norm form is the c3 step's 96^3 32 -> 32 layers) with its
-    fragment reads software-pipelined (MMSEG_WGRAD_B2_PIPE=1, default) against the read-then-multiply form (=0):
-    every accumulator sums the same products in the same order, so weight and bias gradients are BITWISE equal;
-    and both against fp64 (the deferred norm: relu((x - mean) * rstd) of the bf16 x, rounded to bf16)."""
+def test_wgrad_brick2_pipelined(dev, cin, cout, shape, accumulate, norm, monkeypatch):
+    """The 32-co register-staged brick wgrad with its fragment reads software-pipelined (the 32-co layers whose W is
+    not a multiple of 32; at 96^3 wgrad_row runs) against fp64 (the deferred norm: relu((x - mean) * rstd) of the bf16
+    x, rounded to bf16), bitwise repeatable."""
     monkeypatch.setenv("MMSEG_WGRAD_DMA", "0")
     N, D, H, W = shape
     V = N * D * H * W
@@ -714,7 +630,6 @@ def test_wgrad_brick2_pipelined_bitwise(dev, cin, cout, shape, accumulate, norm,
     wsf = L.mmseg_conv3_wgrad_ws_floats(V, cout, cin, cin, shift, D, H, W, cout, cin, 1)
     out = {}
     for pipe in ("0", "1"):
-        monkeypatch.setenv("MMSEG_WGRAD_B2_PIPE", pipe)
         ws = torch.full((max(wsf, 1),), float("nan"), device=dev)
         gw, gb = gw0.clone(), gb0.clone()
         if norm:
@@ -742,11 +657,10 @@ def test_wgrad_brick2_pipelined_bitwise(dev, cin, cout, shape, accumulate, norm,
 @pytest.mark.parametrize("cip,ci,cout,shape,accumulate", [
     (32, 32, 32, (2, 12, 8, 24), 0), (64, 48, 64, (1, 8, 8, 16), 1), (128, 96, 64, (1, 12, 12, 12), 0),
     (64, 64, 128, (2, 12, 12, 12), 1), (1024, 768, 64, (1, 8, 8, 8), 0)])
-def test_wgrad_reduce_vec4_bitwise(dev, cip, ci, cout, shape, accumulate, monkeypatch):
+def test_wgrad_reduce_vec4(dev, cip, ci, cout, shape, accumulate, monkeypatch):
     """The split reduce of channel-major weight-gradient partials (brick2 / runtime-brick kernels) storing each
-    thread's four sums as one 16-B store (MMSEG_WRED_V4=1, default) against four 4-B stores (=0): the same sums to
-    the same torch offsets, padded input channels (ci < cip) dropped -- weight and bias gradients BITWISE equal; and
-    against fp64."""
+    thread's four sums as one 16-B store, padded input channels (ci < cip) dropped: against fp64, bitwise
+    repeatable."""
     monkeypatch.setenv("MMSEG_WGRAD_DMA", "0")
     N, D, H, W = shape
     V = N * D * H * W
@@ -763,7 +677,6 @@ def test_wgrad_reduce_vec4_bitwise(dev, cip, ci, cout, shape, accumulate, monkey
     assert wsf > 0, "a direct single-split gradient has no reduce"
     out = {}
     for v4 in ("0", "1"):
-        monkeypatch.setenv("MMSEG_WRED_V4", v4)
         ws = torch.full((wsf,), float("nan"), device=dev)
         gw, gb = gw0.clone(), gb0.clone()
         assert L.mmseg_conv3_wgrad(ptr(dy), cout, ptr(x), cip, ptr(gw), ptr(gb), cout, cip, ci, shift, V, D, H, W,
@@ -782,10 +695,10 @@ def test_wgrad_reduce_vec4_bitwise(dev, cip, ci, cout, shape, accumulate, monkey
 @pytest.mark.parametrize("cip,ci,cout,shape,accumulate", [
     (1024, 768, 64, (1, 4, 4, 4), 0), (1024, 768, 384, (1, 8, 8, 8), 1), (128, 96, 64, (1, 4, 4, 8), 1),
     (64, 32, 64, (1, 4, 4, 8), 0)])
-def test_wgrad_direct_chunk_padded_bitwise(dev, cip, ci, cout, shape, accumulate, monkeypatch):
+def test_wgrad_direct_chunk_padded(dev, cip, ci, cout, shape, accumulate, monkeypatch):
     """A single-split brick weight gradient over chunk-padded input channels (ci % 32 == 0 < cip: SwinUNETR's 768 of
-    1024) writes the torch-layout gradient itself at row pitch 27 ci (MMSEG_WGRAD_PDIRECT=1, default: no workspace)
-    instead of a partial + relayout reduce (=0): BITWISE the same weight and bias gradients; and against fp64."""
+    1024) writes the torch-layout gradient itself at row pitch 27 ci (no workspace, no relayout reduce): against
+    fp64, bitwise repeatable."""
     N, D, H, W = shape
     V = N * D * H * W
     g = torch.Generator().manual_seed(cip + ci + cout + V)
@@ -799,9 +712,8 @@ def test_wgrad_direct_chunk_padded_bitwise(dev, cip, ci, cout, shape, accumulate
     shift = int(np.log2(cip // 8))
     out = {}
     for pd in ("0", "1"):
-        monkeypatch.setenv("MMSEG_WGRAD_PDIRECT", pd)
         wsf = L.mmseg_conv3_wgrad_ws_floats(V, cout, cip, ci, shift, D, H, W, cout, cip, 1)
-        assert (wsf == 0) == (pd == "1")
+        assert wsf == 0
         ws = torch.full((max(wsf, 1),), float("nan"), device=dev)
         gw, gb = gw0.clone(), gb0.clone()
         assert L.mmseg_conv3_wgrad(ptr(dy), cout, ptr(x), cip, ptr(gw), ptr(gb), cout, cip, ci, shift, V, D, H, W,
@@ -816,14 +728,12 @@ def test_wgrad_direct_chunk_padded_bitwise(dev, cip, ci, cout, shape, accumulate
     assert rel(out["1"][1].double().cpu() - gb0.double().cpu(), dyr.sum(dim=(0, 2, 3, 4))) < GTOL[torch.bfloat16]
 
 
-@pytest.mark.parametrize("pipe", ["0", "1"])
 @pytest.mark.parametrize("cip,ci,shape,accumulate", [
     (64, 48, (1, 16, 16, 16), 0), (128, 96, (1, 8, 16, 16), 1), (64, 48, (2, 8, 8, 16), 1), (64, 64, (1, 12, 8, 24), 0)])
-def test_wgrad_pad16_rows_bitwise(dev, cip, ci, shape, accumulate, pipe, monkeypatch):
+def test_wgrad_pad16_rows_bitwise(dev, cip, ci, shape, accumulate, monkeypatch):
     """mmseg_conv3_wgrad_ex phase bit 8 (SwinUNETR's 48 real output channels in 64-row tiles): the LDS-DMA kernel
-    multiplies 3 of its 4 row tiles (MMSEG_WGRAD_PAD16_PIPE: with / without the pipelined multiply).  Rows 0..47 of
-    the weight and bias gradients are BITWISE those of the full 64-row launch; rows 48..63 receive zeros."""
-    monkeypatch.setenv("MMSEG_WGRAD_PAD16_PIPE", pipe)
+    multiplies 3 of its 4 row tiles (with the pipelined multiply).  Rows 0..47 of the weight and bias gradients are
+    BITWISE those of the full 64-row launch; rows 48..63 receive zeros."""
     N, D, H, W = shape
     V = N * D * H * W
     co = 64

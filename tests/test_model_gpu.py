@@ -511,9 +511,9 @@ def test_deferred_head_norm_bitwise(dev, tag, dtype, monkeypatch):
 @pytest.mark.parametrize("wgrad_dma", ["0", "1"])
 @pytest.mark.parametrize("model", ["unet", "dual_encoder"])
 def test_deferred_conv_norm_bitwise(dev, model, wgrad_dma, monkeypatch):
-    """bf16, 32-channel top level (the brick5 / brick2 kernels): conv1's InstanceNorm + ReLU applied by conv2's
-    forward and weight-gradient kernels on staging (y1 never written) gives a bit-identical loss and gradients
-    to the materialised path (MMSEG_DEFER_CONV_NORM=0)."""
+    """bf16, 32-channel top level (the brick6 forward and the wgrad_row weight gradient at W = 32): conv1's
+    InstanceNorm + ReLU applied by conv2's forward and weight-gradient kernels on staging (y1 never written) gives a
+    bit-identical loss and gradients to the materialised path (MMSEG_DEFER_CONV_NORM=0)."""
     from mmseg_amd.engine.engine import fused_loss_supported, run_engine_loss
     from mmseg_amd.trainer.losses import DiceCELoss
     gen = torch.Generator().manual_seed(5)
@@ -523,7 +523,6 @@ def test_deferred_conv_norm_bitwise(dev, model, wgrad_dma, monkeypatch):
     # register-staged / LDS-DMA weight-gradient kernels, the same kind on both paths (their bias gradients sum
     # in different orders)
     monkeypatch.setenv("MMSEG_WGRAD_DMA", wgrad_dma)
-    monkeypatch.setenv("MMSEG_WGRAD_DMA_NORM", wgrad_dma)
     for defer in ("1", "0"):
         monkeypatch.setenv("MMSEG_DEFER_CONV_NORM", defer)
         cfg = make_config(model, ["CT", "PET"], 3, [32, 64, 128], dtype="bfloat16")
@@ -585,38 +584,6 @@ def test_head_in_partials(dev, model, dtype, knob, defer_head, monkeypatch):
     a, b = res[0][1].double(), res[1][1].double()
     err = ((a - b).norm() / b.norm()).item()
     assert err < (1e-5 if dtype == "float32" else 1e-2), err
-
-
-@pytest.mark.parametrize("model", ["unet", "dual_encoder"])
-def test_fused_forward_stats(dev, model, monkeypatch):
-    """bf16, 32-channel top level: the InstanceNorm statistics of the top blocks' conv1 come from the stem forward's
-    epilogue (one (mean, M2) per 64-voxel brick slice) instead of a statistics pass.  Same math up to summation
-    order: loss 1e-5, gradients 1e-2 normwise (bf16 activations re-round near ties) against the statistics-pass
-    path (MMSEG_STEM_STATS=0)."""
-    knob = "MMSEG_STEM_STATS"
-    from mmseg_amd.engine.engine import fused_loss_supported, run_engine_loss
-    from mmseg_amd.trainer.losses import DiceCELoss
-    gen = torch.Generator().manual_seed(13)
-    x = torch.randn(2, 2, 32, 32, 32, generator=gen).to(dev)
-    y = torch.randint(0, 3, (2, 32, 32, 32), generator=gen).to(dev)
-    res = []
-    for fused in ("1", "0"):
-        monkeypatch.setenv(knob, fused)
-        cfg = make_config(model, ["CT", "PET"], 3, [32, 64, 128], dtype="bfloat16")
-        torch.manual_seed(0)
-        m = build_model(cfg).to(dev)
-        m.train()
-        assert fused_loss_supported(m.backbone, model, x)
-        loss = run_engine_loss(m.backbone, model, x, y, DiceCELoss()._spec(), None)
-        loss.backward()
-        torch.cuda.synchronize()
-        prog = m.backbone.__dict__["_engine"].program
-        top = prog.init if model == "unet" else prog.encs[0][0]
-        assert bool(top.nb[0]) == (fused == "1")
-        res.append((loss.detach().double().item(), torch.cat([p.grad.reshape(-1) for p in m.parameters()]).clone()))
-    assert abs(res[0][0] - res[1][0]) <= 1e-5 * abs(res[1][0])
-    a, b = res[0][1].double(), res[1][1].double()
-    assert ((a - b).norm() / b.norm()).item() < 1e-2
 
 
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
@@ -702,23 +669,20 @@ def test_batched_weight_gradient_reduce_bitwise(dev, dtype, monkeypatch):
 
 @pytest.mark.parametrize("tag,force", [("dual_tiny_cross_attention", "0"), ("dual_tiny_add", "0"),
                                        ("dual_tiny_m3_tversky", "0"), ("dual_tiny_cross_attention", "1"),
-                                       ("dual_tiny_m3_tversky", "1"), ("dual_tiny_cross_attention", "w"),
-                                       ("dual_tiny_cross_attention", "s")])
+                                       ("dual_tiny_m3_tversky", "1"), ("dual_tiny_cross_attention", "w")])
 def test_grouped_modalities_match_per_modality(dev, tag, force, monkeypatch):
     """bf16 (the dtype whose small levels take the runtime-brick kernels): the modality-grouped small levels and the
     grouped encoder output-norm backward (MMSEG_GROUP_SMALL / MMSEG_GROUP_OUTNORM, programs.DualEncoderProgram)
     against the per-modality launches on the same weights and batch.  The grouped launches split the reductions
     differently (one launch over M x N samples), so the two differ by bf16 rounding: loss within 1e-3 relative,
     logits within 2e-2 and every gradient within 5e-2 normwise (L2).  force=1 (MMSEG_GROUP_FORCE_R): the 24^3
-    level is grouped too, on the runtime-brick kernels instead of the (4, 8, 8)-brick family; force=s: the same
-    with that level's InstanceNorm statistics from the conv epilogue (MMSEG_GROUP_STATS, mmseg_conv_gemm_group_stats)."""
-    monkeypatch.setenv("MMSEG_GROUP_FORCE_R", "1" if force in ("1", "s") else "0")
-    monkeypatch.setenv("MMSEG_GROUP_STATS", "1" if force == "s" else "0")
+    level is grouped too, on the runtime-brick kernels instead of the (4, 8, 8)-brick family."""
+    monkeypatch.setenv("MMSEG_GROUP_FORCE_R", "1" if force == "1" else "0")
     kind, mods, C, fusion, lossname = TINY[tag]
     g = golden(tag)
     # 96^3 (B = 1, the tiny features): levels 12^3 / 6^3 take the runtime-brick kernels, as in the bench
     gen = torch.Generator().manual_seed(11)
-    B = 2 if force == "s" else 1   # (s: 4 samples at 24^3 leave the runtime-brick conv one split, as in the bench)
+    B = 1
     x = torch.randn(B, len(mods), 96, 96, 96, generator=gen)
     y = torch.randint(0, C, (B, 96, 96, 96), generator=gen)
     res = {}
@@ -727,7 +691,7 @@ def test_grouped_modalities_match_per_modality(dev, tag, force, monkeypatch):
         monkeypatch.setenv("MMSEG_GROUP_OUTNORM", flag)
         # (force: features whose 24^3 convs have unpadded channels -- the tiny fixture's 16 -> 32 conv pads its
         # input channels, which keeps that level per modality)
-        feats = [16, 32, 64, 128, 256] if force in ("1", "w", "s") else list(g["features"])
+        feats = [16, 32, 64, 128, 256] if force in ("1", "w") else list(g["features"])
         cfg = make_config(kind, mods, C, feats, fusion=fusion, loss=lossname, dtype="bfloat16")
         torch.manual_seed(int(g["seed"]))
         m = build_model(cfg)
@@ -741,17 +705,14 @@ def test_grouped_modalities_match_per_modality(dev, tag, force, monkeypatch):
         res[flag] = (loss.item(), logits, {n: p.grad.detach().double().cpu().clone()
                                            for n, p in m.backbone.named_parameters()}, prog.l0, prog.L,
                      prog.group_outnorm)
-        if flag == "1":
-            gnb = tuple(getattr(prog.gblocks[prog.l0], "gnb", None) or (0, 0))
     (l1, lg1, g1, l0, L, go), (l2, lg2, g2, l0b, _, gob) = res["1"], res["0"]
     print(f"\n{tag}: grouped from level {l0} of {L} (output norm grouped: {go}); loss {l1:.6f} vs {l2:.6f}")
-    assert l0 == (2 if force in ("1", "s") else 3) and go and l0b == L and not gob
-    assert (min(gnb) > 0) == (force == "s"), gnb   # force=s: the 24^3 statistics came from the conv epilogue
+    assert l0 == (2 if force == "1" else 3) and go and l0b == L and not gob
     bad_all = {n: float((g1[n] - g2[n]).norm() / g2[n].norm()) for n in g2 if g2[n].norm() > 0}
     print("largest gradient differences:", sorted(bad_all.items(), key=lambda kv: -kv[1])[:6])
     assert abs(l1 - l2) < 1e-3 * abs(l2)
     assert float((lg1 - lg2).norm() / lg2.norm()) < 2e-2
-    if force in ("1", "s"):
+    if force == "1":
         # the forced 24^3 level runs other kernels (runtime-brick) than the per-modality step, so the two bf16
         # steps differ by rounding amplified through kink flips (up to ~0.15 on these random-input gradients, the
         # size of any two bf16 kernel paths here); its parity is held to the pinned fp64 oracle instead
