@@ -346,7 +346,7 @@ def main():
                          "captured step at the points each rank of the N-GPU job issues them.  At world size 1 the "
                          "collective is SUM (AVG is the identity there; RCCL's single-rank AVG adds a scaling pass, "
                          "~0.24 ms/step, that an N-rank AVG folds into the reduction), so that pass is not in the "
-                         "rehearsed time (MMSEG_DP_AVG1=1 keeps AVG)")
+                         "rehearsed time")
     ap.add_argument("--bucket-mb", type=float, default=32.0, help="DP gradient bucket size (distributed.bucket_mb)")
     ap.add_argument("--infer", action="store_true",
                     help="secondary line: sliding-window inference (Trainer._sliding_window_inference, reference "

@@ -1556,6 +1556,7 @@ __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int up
   }
   // block-wide: the sums of sample in_n -> inpart[in_n][blk][n0 + c] (fixed order: 16-lane tree, then waves 0..3)
   auto in_flush = [&]() {
+   if constexpr (INP) {   // (the 1-wave LDS array of the plain instantiations is never read)
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1)
 #pragma unroll
@@ -1580,6 +1581,7 @@ __global__ __launch_bounds__(256, 1) void conv3_brick5_kernel(GemmArgs g, int up
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 8; ++k) isg[k] = isgx[k] = 0.f;
+   }
   };
   auto in_load = [&](const Unit& q) {   // x of the lane's 4 output voxels (consumed by the brick's epilogue)
     const T* X = reinterpret_cast<const T*>(g.inx) + (long long)q.n * vox_per_n * g.ldinx + n0 + 8 * kg;
@@ -1966,7 +1968,8 @@ __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int up
 #pragma unroll
     for (int i = 0; i < BY; ++i) xin[i].zero();
   }
-  auto in_flush = [&]() {   // block-wide, fixed order: 16-lane tree, then waves 0..3
+  auto in_flush = [&]() {
+   if constexpr (INP) {   // (the 1-wave LDS array of the plain instantiations is never read)   // block-wide, fixed order: 16-lane tree, then waves 0..3
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1)
 #pragma unroll
@@ -1991,6 +1994,7 @@ __global__ __launch_bounds__(256, 1) void conv3_brick6_kernel(GemmArgs g, int up
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 8; ++k) isg[k] = isgx[k] = 0.f;
+   }
   };
   auto in_begin = [&](const Unit& q) {   // block-uniform: the sample of the epilogue's brick
     if constexpr (INP) {
@@ -2508,7 +2512,7 @@ Conv3Plan plan_conv3(int M, int Ncols, int cin, int D, int H, int W, int lda, in
     }
     k1_ok = true;
   }
-  if (brick >= 2 && base_ok && knob("MMSEG_BRICKR", 1)) {
+  if (brick >= 2 && base_ok) {
     int best = 0;
     for (int bz = 1; bz <= D && bz <= 8; ++bz) {
       if (D % bz) continue;
@@ -3826,16 +3830,9 @@ __global__ __launch_bounds__(512, 1) void conv3_brick8_kernel(GemmArgs g) {
   PROBE_BLOCK(true);
 }
 // PIPE: the fragment reads of the next (dy plane, tap) step are issued before the current step's MFMAs
-// RING: the halo is a ring of z-plane slots and a block walks its bricks z-fastest, so a brick that continues the
-// previous one's (x, y) column reuses the two halo planes they share and stages only its four new ones: halo
-// bytes per brick 1.875x the brick's voxels instead of 2.81x (6 x 6 x 10 of 4 x 4 x 8).  Slot of the halo's first
-// plane: sb(b) = 4 (b - b_begin) + 2 (column starts in (b_begin, b]) mod RSLOT -- a brick starting a column takes
-// six fresh slots; with NST = 3 the bricks in flight span at most 18 of the 24 slots.
-constexpr int RSLOT = 24;                 // halo plane slots
-constexpr int RPLANE_I = 4;               // DMA wave-instructions per plane slot (6 x 10 voxels x 4 chunks = 240 lanes)
 // MTC < MT: only the first MTC 16-row tiles are multiplied (the rest are output-channel padding, WgradArgs::pad16);
 // staging and the epilogue keep the MT-row layout, the skipped rows' accumulators stay zero
-template <int MT, bool NORM = false, int NST = 3, bool PIPE = false, bool RING = false, int MTC = MT>
+template <int MT, bool NORM = false, int NST = 3, bool PIPE = false, int MTC = MT>
 __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
   typedef bf16_t T;
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -3845,11 +3842,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
   constexpr int NXI = (HLO_V * XCH + 63) / 64;          // halo wave-instructions (23, the last one half)
   constexpr int NI = NDI + NXI, KI = (NI + 7) / 8;      // per brick; per wave (8 waves)
   constexpr int DS = 128 * CO, XS = NXI * 64 * 8;       // elements per stage (halo padded to whole instructions)
-  constexpr int SS = RING ? DS : DS + XS;
-  constexpr int PLANE_E = RPLANE_I * 512;               // elements per halo plane slot (4 KB)
-  static_assert(!RING || (!NORM && NST == 3), "RING: no deferred norm, three stages");
-  __shared__ __attribute__((aligned(16))) T st[NST * SS];   // ring of NST stage images (RING: dy only)
-  __shared__ __attribute__((aligned(16))) T xr[RING ? RSLOT * PLANE_E : 8];   // RING: halo plane slots
+  constexpr int SS = DS + XS;
+  __shared__ __attribute__((aligned(16))) T st[NST * SS];   // ring of NST stage images
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cin = 8 << g.cpg_shift;
@@ -3896,81 +3890,16 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
       ++nw;
     }
   }
-  // RING: per plane-slot instruction j4 (0..3) the lane's byte offset within the plane and its (hy, hx)
-  uint32_t prel[RING ? RPLANE_I : 1], ppos[RING ? RPLANE_I : 1];
-  if constexpr (RING) {
-#pragma unroll
-    for (int j4 = 0; j4 < RPLANE_I; ++j4) {
-      const int p = j4 * 64 + lane, h = p >> 2, c = p & 3;
-      prel[j4] = 0;
-      ppos[j4] = 0xffu;
-      if (h < HLO_Y * HLO_X) {
-        const int hx = h % HLO_X, hy = h / HLO_X;
-        const int cc = (((c >> 1) ^ ((hx >> 2) & 1)) << 1) | (c & 1);
-        prel[j4] = (uint32_t)(((hy * g.W + hx) * g.ldb + c0 + cc * 8) * 2);
-        ppos[j4] = (uint32_t)(hy | (hx << 8));
-      }
-    }
-  }
-  // brick b's origin: x fastest, or (RING) z fastest so consecutive bricks of a block share halo planes
+  // brick b's origin: x fastest
   auto brick_at = [&](int b, int& n, int& z0, int& y0, int& x0) __attribute__((always_inline)) {
     int q = b;
-    if constexpr (RING) {
-      const int bz = q % bz_n;
-      q /= bz_n;
-      const int bx = q % bx_n;
-      q /= bx_n;
-      const int by = q % by_n;
-      n = q / by_n;
-      z0 = bz * BRK_Z, y0 = by * BRK_Y, x0 = bx * BRK_X;
-    } else {
-      const int bx = q % bx_n;
-      q /= bx_n;
-      const int by = q % by_n;
-      q /= by_n;
-      const int bz = q % bz_n;
-      n = q / bz_n;
-      z0 = bz * BRK_Z, y0 = by * BRK_Y, x0 = bx * BRK_X;
-    }
-  };
-  auto ring_cont = [&](int b) __attribute__((always_inline)) { return b > b_begin && b % bz_n != 0; };
-  auto ring_sb = [&](int b) __attribute__((always_inline)) {
-    return (4 * (b - b_begin) + 2 * (b / bz_n - b_begin / bz_n)) % RSLOT;
-  };
-  // this wave's DMA instructions for brick b (RING: dy + 4 or 6 planes x 4, dealt round-robin over the waves)
-  auto ring_count = [&](int b) __attribute__((always_inline)) {
-    const int tot = NDI + RPLANE_I * (ring_cont(b) ? 4 : 6);
-    return tot > wave ? (tot - 1 - wave) / 8 + 1 : 0;
-  };
-  auto issue_ring = [&](T* dst, int b) __attribute__((always_inline)) {
-    int n, z0, y0, x0;
-    brick_at(b, n, z0, y0, x0);
-    const int vb = (n * g.D + z0) * HW + y0 * g.W + x0;
-    const int dbase = vb * g.lda * 2;
-#pragma unroll
-    for (int k = 0; k < KI; ++k) {
-      const int m = wave + 8 * k;
-      if (m < NDI)
-        wd_dma16(__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)(lds_ptr_t)(dst + m * 512)),
-                 (uint32_t)(dbase + (int)rel[k]), drsrc);
-    }
-    const int p0 = ring_cont(b) ? 2 : 0, sb = ring_sb(b);
-    const int tot = NDI + RPLANE_I * (6 - p0);
-    for (int m = NDI + ((wave - NDI) & 7); m < tot; m += 8) {   // this wave's halo instructions
-      const int hi = m - NDI, p = p0 + (hi >> 2), j4 = hi & 3;
-      int slot = sb + p;
-      if (slot >= RSLOT) slot -= RSLOT;
-      const int z = z0 - 1 + p;
-      // the lane's (hy, hx) for instruction j4 (j4 is wave-uniform: select among the four precomputed values)
-      const uint32_t hp = j4 == 0 ? ppos[0] : j4 == 1 ? ppos[1] : j4 == 2 ? ppos[2] : ppos[3];
-      const uint32_t rl = j4 == 0 ? prel[0] : j4 == 1 ? prel[1] : j4 == 2 ? prel[2] : prel[3];
-      const int y = y0 - 1 + (int)(hp & 0xff), x = x0 - 1 + (int)(hp >> 8);
-      const bool ok = hp != 0xffu && (unsigned)z < (unsigned)g.D && (unsigned)y < (unsigned)g.H &&
-                      (unsigned)x < (unsigned)g.W;
-      const int pbase = (((n * g.D + z) * g.H + (y0 - 1)) * g.W + (x0 - 1)) * g.ldb * 2;
-      wd_dma16(__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)(lds_ptr_t)(xr + slot * PLANE_E + j4 * 512)),
-               ok ? (uint32_t)(pbase + (int)rl) : WD_OOB, xrsrc);
-    }
+    const int bx = q % bx_n;
+    q /= bx_n;
+    const int by = q % by_n;
+    q /= by_n;
+    const int bz = q % bz_n;
+    n = q / bz_n;
+    z0 = bz * BRK_Z, y0 = by * BRK_Y, x0 = bx * BRK_X;
   };
   auto issue = [&](T* dst, int b) __attribute__((always_inline)) {
     int n, z0, y0, x0;
@@ -4007,19 +3936,6 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
       default: __builtin_amdgcn_s_waitcnt(0x0f70); break;
     }
   };
-  // wait until at most `cnt` of this wave's DMA instructions are in flight
-  auto wait_cnt = [&](int cnt) __attribute__((always_inline)) {
-    switch (cnt) {
-#define MMSEG_WD_WAIT(N) \
-  case N: __builtin_amdgcn_s_waitcnt(0x0f70 | N); break;
-      MMSEG_WD_WAIT(1) MMSEG_WD_WAIT(2) MMSEG_WD_WAIT(3) MMSEG_WD_WAIT(4) MMSEG_WD_WAIT(5) MMSEG_WD_WAIT(6)
-      MMSEG_WD_WAIT(7) MMSEG_WD_WAIT(8) MMSEG_WD_WAIT(9) MMSEG_WD_WAIT(10) MMSEG_WD_WAIT(11) MMSEG_WD_WAIT(12)
-      MMSEG_WD_WAIT(13) MMSEG_WD_WAIT(14) MMSEG_WD_WAIT(15)
-#undef MMSEG_WD_WAIT
-      default: __builtin_amdgcn_s_waitcnt(0x0f70); break;
-    }
-  };
-
   // NORM: thread owns channel group cg = tid & 3 of halo rows (tid >> 2) + 128 k
   int norm_n = -1;
   float nmu[NORM ? 8 : 1], nrs[NORM ? 8 : 1];
@@ -4079,15 +3995,10 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
   bf16x8 ones;
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
-  // halo row of tap (kz, ky, kx) for the lane's voxels in brick z-plane vz (RING: plane slot sb + vz + kz)
+  // halo row of tap (kz, ky, kx) for the lane's voxels in brick z-plane vz
   auto xrow = [&](const char* Xb, int sb, int vz, int kz, int ky, int kx) __attribute__((always_inline)) {
-    if constexpr (RING) {
-      int slot = sb + vz + kz;
-      if (slot >= RSLOT) slot -= RSLOT;
-      return reinterpret_cast<const char*>(xr) + slot * (PLANE_E * 2) + (hlo0 + ky * HLO_X + kx) * (CK * 2);
-    } else {
-      return Xb + (hlo0 + (vz + kz) * (HLO_Y * HLO_X) + ky * HLO_X + kx) * (CK * 2);
-    }
+    (void)sb;
+    return Xb + (hlo0 + (vz + kz) * (HLO_Y * HLO_X) + ky * HLO_X + kx) * (CK * 2);
   };
   auto compute = [&](const T* S, int sb) __attribute__((always_inline)) {
     const char* Db = reinterpret_cast<const char*>(S);
@@ -4178,16 +4089,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
 
   // prologue: bricks b_begin .. b_begin + NST - 2 in flight, the first one landed
   for (int k = 0; k < NST - 1; ++k) {
-    if (b_begin + k < b_end) {
-      if constexpr (RING)
-        issue_ring(st + k * SS, b_begin + k);
-      else
-        issue(st + k * SS, b_begin + k);
-    }
+    if (b_begin + k < b_end) issue(st + k * SS, b_begin + k);
   }
-  if constexpr (RING) {
-    wait_cnt(b_begin + 1 < b_end ? ring_count(b_begin + 1) : 0);   // NST = 3: only brick b_begin + 1 may follow
-  } else {
+  {
     const int inflight = b_end - b_begin - 1 < NST - 2 ? b_end - b_begin - 1 : NST - 2;
     wait_bricks(inflight > 0 ? inflight : 0);
   }
@@ -4204,13 +4108,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
   for (int b = b_begin, sc = 0; b < b_end; ++b, sc = sc + 1 == NST ? 0 : sc + 1) {
     // issue brick b + NST - 1 into the stage brick b - 1 used (every wave passed the barrier after it)
     const int sn = sc == 0 ? NST - 1 : sc - 1;
-    if (b + NST - 1 < b_end && g.dbg != 1) {
-      if constexpr (RING)
-        issue_ring(st + sn * SS, b + NST - 1);
-      else
-        issue(st + sn * SS, b + NST - 1);
-    }
-    const int sb = RING ? ring_sb(b) : 0;
+    if (b + NST - 1 < b_end && g.dbg != 1) issue(st + sn * SS, b + NST - 1);
+    const int sb = 0;
     if (g.dbg != 2) {
       if constexpr (PIPE)
         compute_pipe(st + sc * SS, sb, tcc);
@@ -4218,9 +4117,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
         compute(st + sc * SS, sb);
     }
     // brick b + 1 has landed once at most min(NST - 2, bricks issued after it) bricks are in flight
-    if constexpr (RING) {
-      wait_cnt(b + 2 < b_end ? ring_count(b + 2) : 0);
-    } else {
+    {
       const int after = b_end - b - 2 < NST - 2 ? b_end - b - 2 : NST - 2;
       wait_bricks(after > 0 ? after : 0);
     }
@@ -4238,7 +4135,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
   else
     brick_loop(std::integral_constant<int, 3>{});
 
-  static_assert((RING ? sizeof(xr) : sizeof(st)) >= 16 * WEP_P * sizeof(float),
+  static_assert(sizeof(st) >= 16 * WEP_P * sizeof(float),
                 "epilogue staging must fit the stage ring");
   if (g.frag && !(g.grad != nullptr && g.ksplit == 1)) {
     // split partials in the accumulators' own layout: every (tap, i, j) fragment is 1 KB contiguous (lane l's
@@ -4257,8 +4154,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(WgradArgs g) {
           *reinterpret_cast<f32x4*>(base + ((tap * MT + i) * 2 + j) * 256 + lane * 4) = acc[t][i][j];
     }
   } else {
-    __syncthreads();   // (RING: the halo slots are the epilogue's staging)
-    wgrad_store_chmajor<MT>(acc, t_begin, t_cnt, RING ? reinterpret_cast<float*>(xr) : reinterpret_cast<float*>(st),
+    __syncthreads();
+    wgrad_store_chmajor<MT>(acc, t_begin, t_cnt, reinterpret_cast<float*>(st),
                             g, ks, row0, c0);
   }
   if (bias_wave && i16 == 0) {
@@ -5422,7 +5319,7 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     if (g.ksplit > 1) return launch_splitk_reduce<T, MODE>(g, s);
     return 0;
   }
-  if (MODE == MODE_POINT && g.Ncols % 96 == 0 && g.Ncols % 64 != 0 && knob("MMSEG_POINT_BN96", 1)) {
+  if (MODE == MODE_POINT && g.Ncols % 96 == 0 && g.Ncols % 64 != 0) {
     // BM=128, BN=96: the 96 / 288 / 480-column 1x1 GEMMs (SwinUNETR's 96-channel stage, the 96 -> 48 residual
     // conv's data gradient) in whole tiles -- BN=64 left a half-empty last column tile that re-read every A row
     if constexpr (MODE == MODE_POINT) {
@@ -5545,7 +5442,7 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
           mmseg::note_kernel("wgrad_dma_kernel<CO64>");
           // 48 real rows of 64 (SwinUNETR's 48-channel levels): three row tiles, room for the pipelined multiply
           if (g.pad16 && g.Ca == 64)
-            MMSEG_LAUNCH((wgrad_dma_kernel<4, false, 3, true, false, 3>), grid, dim3(512), 0, s, g);
+            MMSEG_LAUNCH((wgrad_dma_kernel<4, false, 3, true, 3>), grid, dim3(512), 0, s, g);
           else   // (fragment prefetch two steps ahead spills at 64 co: 59.5 -> 72.3 us)
             MMSEG_LAUNCH((wgrad_dma_kernel<4>), grid, dim3(512), 0, s, g);
         } else {
@@ -5599,10 +5496,10 @@ int wgrad_brick_ok(int Ca, int cpg_shift, int D, int H, int W, int lda, int ldb,
   const int k = knob("MMSEG_WGRAD_BRICK", 2);
   if (!(k && Ca % 32 == 0 && (8 << cpg_shift) % CK == 0 && lda % 8 == 0 && ldb % 8 == 0)) return 0;
   if (force_r)   // grouped launches: only the runtime-brick weight gradient splits by sample group
-    return (k >= 2 && dtype == MMSEG_BF16 && knob("MMSEG_WGRAD_BRICKR", 1) && plan_wgrad_brickr(D, H, W).bz) ? 3 : 0;
+    return (k >= 2 && dtype == MMSEG_BF16 && plan_wgrad_brickr(D, H, W).bz) ? 3 : 0;
   if (D % BRK_Z == 0 && H % BRK_Y == 0 && W % BRK_X == 0)
-    return (k >= 2 && dtype == MMSEG_BF16 && (Ca % 64 == 0 || knob("MMSEG_WGRAD_BRICK2_CO32", 1))) ? 2 : 1;
-  if (k >= 2 && dtype == MMSEG_BF16 && knob("MMSEG_WGRAD_BRICKR", 1) && plan_wgrad_brickr(D, H, W).bz) return 3;
+    return (k >= 2 && dtype == MMSEG_BF16) ? 2 : 1;
+  if (k >= 2 && dtype == MMSEG_BF16 && plan_wgrad_brickr(D, H, W).bz) return 3;
   return 0;
 }
 
@@ -5940,7 +5837,7 @@ int mmseg_conv_gemm_gelu(const void* a, int lda, const void* wpacked, const floa
                 "conv_gemm_gelu: ldo, Ncols multiples of 8, 16-B aligned buffers");
   const int KGp = (KG + 3) & ~3;
   GemmArgs g{a, lda, wpacked, bias, out, ldo, nullptr, M, Ncols, Cpad, KG, 0, 1, 1, 1, 1, KGp,
-             knob("MMSEG_SWIZZLE", 1), nullptr, 0, nullptr, nullptr};
+             1 /* XCD-aware block remap */, nullptr, 0, nullptr, nullptr};
   MMSEG_REQUIRE(lda % 8 == 0, "conv_gemm_gelu: lda must be a multiple of 8");
   MMSEG_REQUIRE(Cpad >= ((Ncols + (Ncols >= 64 ? 63 : 31)) / (Ncols >= 64 ? 64 : 32)) * (Ncols >= 64 ? 64 : 32),
                 "conv_gemm_gelu: packed weights must be padded to the column tile (Cpad=%d, Ncols=%d)", Cpad, Ncols);
@@ -6004,7 +5901,7 @@ int conv_gemm_impl(const void* a, int lda, const void* wpacked, const float* bia
   int kps = ((ceil_div(KGp, ksplit) + 3) / 4) * 4;
   ksplit = ceil_div(KGp, kps);
   GemmArgs g{a, lda, wpacked, bias, out, ldo, splitk_ws, M, Ncols, Cpad, KG, cpg_shift, D, H, W, ksplit, kps,
-             knob("MMSEG_SWIZZLE", 1), stats_part,
+             1 /* XCD-aware block remap */, stats_part,
              mode == MODE_CONV3 ? (cin_real + 31) / 32 : 0, nullptr, nullptr, out2,
              ldo2, split};
   if (groups > 1) {
@@ -6043,7 +5940,7 @@ int mmseg_conv3_fwd_norm(const void* a, int lda, const float* nmean, const float
                 "conv3_fwd_norm: unsupported shape (mmseg_conv3_norm_ok)");
   const int KGp = (KG + 3) & ~3;
   GemmArgs g{a, lda, wpacked, bias, out, ldo, nullptr, M, Ncols, Cpad, KG, cpg_shift, D, H, W, 1, KGp,
-             knob("MMSEG_SWIZZLE", 1), nullptr, 0, nmean, nrstd};
+             1 /* XCD-aware block remap */, nullptr, 0, nmean, nrstd};
   return launch_gemm<bf16_t, MODE_CONV3>(g, (hipStream_t)stream);
 }
 
@@ -6077,7 +5974,7 @@ int mmseg_conv3_fwd_fp8(const void* a, int lda, const float* nmean, const float*
                 "conv3_fwd_fp8: unsupported shape (mmseg_conv3_fp8_ok)");
   const int KGp = (KG + 3) & ~3;
   GemmArgs g{a, lda, w8, bias, out, ldo, nullptr, M, Ncols, Cpad, KG, cpg_shift, D, H, W, 1, KGp,
-             knob("MMSEG_SWIZZLE", 1), nullptr, 0, nmean, nrstd};
+             1 /* XCD-aware block remap */, nullptr, 0, nmean, nrstd};
   g.wdq = wdq;
   launch_brick5(g, (hipStream_t)stream);
   return mmseg::check_launch("conv3_fwd_fp8");
@@ -6112,7 +6009,7 @@ int mmseg_conv3_dgrad_in(const void* a, int lda, const void* wpacked, void* out,
                 "conv3_dgrad_in: unsupported shape (mmseg_conv3_dgrad_in_chunks)");
   const int KGp = (KG + 3) & ~3;
   GemmArgs g{a, lda, wpacked, nullptr, out, ldo, nullptr, M, Ncols, Cpad, KG, cpg_shift, D, H, W, 1, KGp,
-             knob("MMSEG_SWIZZLE", 1), nullptr, 0, nullptr, nullptr};
+             1 /* XCD-aware block remap */, nullptr, 0, nullptr, nullptr};
   g.inx = inx;
   g.ldinx = ldinx;
   g.inmean = inmean;

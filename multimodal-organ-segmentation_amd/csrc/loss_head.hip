@@ -150,10 +150,6 @@ __global__ __launch_bounds__(256) void head_fwd_u_kernel(const T* __restrict__ x
 // dot products from LDS: the logit stores of a class are consecutive voxels.  Same per-logit fma order as
 // head_fwd_u (bias, then channels 0..Cin-1), so the logits are bitwise head_fwd_u's.
 constexpr int HT_V = 128;
-int head_knob(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
 template <typename T, int CG, int CC>
 __global__ __launch_bounds__(256) void head_fwd_t_kernel(const T* __restrict__ x, int ldx,
                                                          const float* __restrict__ Wt, const float* __restrict__ bias,
@@ -1472,7 +1468,7 @@ int mmseg_head_fwd(const void* x, int ldx, int Cin, const float* W, const float*
     using T = decltype(tag);
     constexpr int CG = decltype(cg_c)::value, CC = decltype(cc_c)::value;
     if (Cin != CG * 8 || C != CC) return false;
-    if (CG == 6 && !dscale && head_knob("MMSEG_HEAD_TILE", 1)) {   // padded 48-channel rows: the tile-staged form
+    if (CG == 6 && !dscale) {   // padded 48-channel rows: the tile-staged form
       const int tgrid = (int)std::min<long long>(ceil_div((long long)N * V, (long long)HT_V), 4096LL);
       MMSEG_LAUNCH((head_fwd_t_kernel<T, CG, CC>), dim3(tgrid), dim3(256), 0, s, (const T*)x, ldx, W, b, V, N,
                    logits);

@@ -776,10 +776,9 @@ int ln_blocks(long long rows) {
   return (int)(b < 1024 ? (b < 1 ? 1 : b) : 1024);
 }
 
-// (G, V) of the row-group LayerNorm kernels for C (0: not covered -> the wave-per-row kernels); MMSEG_LN_G=0 too
+// (G, V) of the row-group LayerNorm kernels for C (0: not covered -> the wave-per-row kernels)
 int ln_gv(int C, int ldx, int ldy, int* V) {
-  const char* e = getenv("MMSEG_LN_G");
-  if ((e && atoi(e) == 0) || C % 8 || ldx % 8 || ldy % 8) return 0;
+  if (C % 8 || ldx % 8 || ldy % 8) return 0;
   const int c8 = C / 8;
   int G = 8;
   while (G < c8 && G < 64) G *= 2;

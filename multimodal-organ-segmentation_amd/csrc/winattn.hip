@@ -198,88 +198,8 @@ __device__ __forceinline__ void scores_k(const f32x4& acc, bool kv, const float*
   }
 }
 
-// ------------------------------------------------------------------ forward
-// Two passes over the key tiles per query tile: (1) running max / sum of the row (each lane holds one query,
-// merged over the 4 lanes sharing it), (2) scores recomputed (one MFMA each), P = exp(s - lse), O += P V.
-__global__ __launch_bounds__(512) void winattn_fwd_kernel(WinAttnArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16_t Qs[NPMAX][16];
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
-  __shared__ __attribute__((aligned(16))) bf16_t Vt[16][TP];
-  __shared__ float tab[TMAX];
-  __shared__ __attribute__((aligned(16))) int code[NPMAX];
-  __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
-  const int bh = wa_block(a), b = bh / a.heads, h = bh % a.heads;
-  const int np = (a.N + 15) & ~15, nt = np / 16;
-  const Stage st{b, h, a.N, np};
-  const int C3 = 3 * a.C, hoff = h * a.hd;
-  stage_rows(Qs, a.qkv, C3, hoff, st, a.hd, nullptr);
-  stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, nullptr);
-  stage_rows(nullptr, a.qkv, C3, 2 * a.C + hoff, st, a.hd, Vt);
-  stage_table(tab, a, h);
-  stage_codes(code, a, np);
-  stage_region(reg, a, b);
-  __syncthreads();
-  const float* ctab = tab + code_off(a);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r16 = lane & 15, g4 = lane >> 4;
-  for (int qt = wave; qt < nt; qt += WAVES) {
-    const int q = qt * 16 + r16;
-    const s4 bq = ld4(&Qs[q][4 * g4]);
-    const bool qv = q < a.N;
-    const float* tq = ctab + code[q];
-    const uint32_t rq = reg[q];
-    float mx = -INFINITY, sum = 0.f;
-    for (int k0 = 0; k0 < nt; k0 += 4) {     // 4 key tiles per step: independent MFMAs / LDS lookups in flight
-      float v[4][4];
-      float tm = -INFINITY;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int kt = k0 + u < nt ? k0 + u : nt - 1;
-        const f32x4 acc = mma(ld4(&Ks[kt * 16 + r16][4 * g4]), bq, (f32x4){0.f, 0.f, 0.f, 0.f});
-        scores_q(acc, qv && k0 + u < nt, tq, rq, kt * 16 + 4 * g4, a, code, reg, v[u]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) tm = fmaxf(tm, v[u][r]);
-      }
-      if (tm > mx) {
-        sum *= __expf(mx - tm);
-        mx = tm;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sum += v[u][r] == -INFINITY ? 0.f : __expf(v[u][r] - mx);
-    }
-    // merge (max, sum) over the 4 lanes holding this query (xor 16, 32)
-#pragma unroll
-    for (int o = 16; o <= 32; o <<= 1) {
-      const float om = __shfl_xor(mx, o, 64), os = __shfl_xor(sum, o, 64);
-      const float m2 = fmaxf(mx, om);
-      sum = (mx == -INFINITY ? 0.f : sum * __expf(mx - m2)) + (om == -INFINITY ? 0.f : os * __expf(om - m2));
-      mx = m2;
-    }
-    const float lse = mx == -INFINITY ? 0.f : mx + __logf(sum);
-    if (g4 == 0 && q < a.N) a.lse[(long long)bh * NPMAX + q] = lse;
-    f32x4 o = {0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < nt; ++kt) {
-      const f32x4 acc = mma(ld4(&Ks[kt * 16 + r16][4 * g4]), bq, (f32x4){0.f, 0.f, 0.f, 0.f});
-      float p[4];
-      scores_q(acc, qv, tq, rq, kt * 16 + 4 * g4, a, code, reg, p);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) p[r] = p[r] == -INFINITY ? 0.f : __expf(p[r] - lse);
-      o = mma(pack4(p[0], p[1], p[2], p[3]), ld4(&Vt[r16][kt * 16 + 4 * g4]), o);
-    }
-    if (r16 < a.hd) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int qq = qt * 16 + 4 * g4 + r;
-        if (qq < a.N) a.out[(long long)(b * a.N + qq) * a.C + hoff + r16] = (bf16_t)o[r];
-      }
-    }
-  }
-}
-
 // ------------------------------------------------------ forward, one pass
-// (r05; default, MMSEG_WINATTN_FWD1=0 restores winattn_fwd_kernel.)  A query tile's whole score row stays in
+// (r05; replaced the r04 two-pass kernel, which recomputed S^T and exp for P V.)  A query tile's whole score row stays in
 // registers (22 key tiles x 4 keys per lane = 88 VGPRs), so the scores, their bias / mask and the exponentials are
 // computed ONCE instead of twice (the two-pass form recomputed S^T and exp for P V): the kernel was VALU-issue-bound
 // at ~50 VALU instructions per MFMA (r05a SQ counters).  Scores are taken in the log2 domain (the table and the scale
@@ -439,268 +359,11 @@ __device__ __forceinline__ void stage_D(float* Dq, const WinAttnArgs& a, const S
   }
 }
 
-// ------------------------------------------------------- backward: dK, dV
-__global__ __launch_bounds__(512) void winattn_bwd_kv_kernel(WinAttnArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16_t Qs[NPMAX][16];
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[NPMAX][16];
-  __shared__ __attribute__((aligned(16))) bf16_t dOs[NPMAX][16];
-  __shared__ __attribute__((aligned(16))) bf16_t Qt[16][TP];
-  __shared__ __attribute__((aligned(16))) bf16_t dOt[16][TP];
-  __shared__ float tab[TMAX];
-  __shared__ __attribute__((aligned(16))) float lse[NPMAX];
-  __shared__ __attribute__((aligned(16))) float Dq[NPMAX];
-  __shared__ __attribute__((aligned(16))) int code[NPMAX];
-  __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
-  const int bh = wa_block(a), b = bh / a.heads, h = bh % a.heads;
-  const int np = (a.N + 15) & ~15, nt = np / 16;
-  const Stage st{b, h, a.N, np};
-  const int C3 = 3 * a.C, hoff = h * a.hd;
-  stage_rows(Qs, a.qkv, C3, hoff, st, a.hd, Qt);
-  stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, nullptr);
-  stage_rows(Vs, a.qkv, C3, 2 * a.C + hoff, st, a.hd, nullptr);
-  stage_rows(dOs, a.dO, a.C, hoff, st, a.hd, dOt);
-  stage_table(tab, a, h);
-  stage_codes(code, a, np);
-  stage_region(reg, a, b);
-  stage_D(Dq, a, st);
-  for (int n = threadIdx.x; n < np; n += blockDim.x) lse[n] = n < a.N ? a.lse[(long long)bh * NPMAX + n] : 0.f;
-  __syncthreads();
-  const float* ctab = tab + code_off(a);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r16 = lane & 15, g4 = lane >> 4;
-  for (int kt = wave; kt < nt; kt += WAVES) {
-    const int key = kt * 16 + r16;
-    const s4 bk = ld4(&Ks[key][4 * g4]);
-    const s4 bv = ld4(&Vs[key][4 * g4]);
-    const bool kv = key < a.N;
-    const float* tk = ctab - code[key];
-    const uint32_t rk = reg[key];
-    f32x4 dk = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
-    for (int qt = 0; qt < nt; ++qt) {
-      const f32x4 sc = mma(ld4(&Qs[qt * 16 + r16][4 * g4]), bk, (f32x4){0.f, 0.f, 0.f, 0.f});   // S[q][key]
-      const f32x4 dp = mma(ld4(&dOs[qt * 16 + r16][4 * g4]), bv, (f32x4){0.f, 0.f, 0.f, 0.f}); // dP[q][key]
-      float p[4], ds[4];
-      const int q0 = qt * 16 + 4 * g4;
-      scores_k(sc, kv, tk, rk, q0, a, code, reg, p);
-      const float4 l4 = *reinterpret_cast<const float4*>(lse + q0);
-      const float4 d4 = *reinterpret_cast<const float4*>(Dq + q0);
-      const float lq[4] = {l4.x, l4.y, l4.z, l4.w}, dq4[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        p[r] = p[r] == -INFINITY ? 0.f : __expf(p[r] - lq[r]);
-        ds[r] = p[r] * (dp[r] - dq4[r]);
-      }
-      dv = mma(pack4(p[0], p[1], p[2], p[3]), ld4(&dOt[r16][qt * 16 + 4 * g4]), dv);
-      dk = mma(pack4(ds[0], ds[1], ds[2], ds[3]), ld4(&Qt[r16][qt * 16 + 4 * g4]), dk);
-    }
-    if (r16 < a.hd) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int kk = kt * 16 + 4 * g4 + r;
-        if (kk < a.N) {
-          bf16_t* row = a.out + (long long)(b * a.N + kk) * C3;
-          row[a.C + hoff + r16] = (bf16_t)(dk[r] * a.scale);
-          row[2 * a.C + hoff + r16] = (bf16_t)dv[r];
-        }
-      }
-    }
-  }
-}
+constexpr int QB_TILES = 8;                        // query tiles per block (one per wave) of the query pass
 
-// ---------------------------------------------------- backward: dQ and dS
-__global__ __launch_bounds__(512) void winattn_bwd_q_kernel(WinAttnArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16_t Qs[NPMAX][16];
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[NPMAX][16];
-  __shared__ __attribute__((aligned(16))) bf16_t dOs[NPMAX][16];
-  __shared__ __attribute__((aligned(16))) bf16_t Kt[16][TP];
-  __shared__ float tab[TMAX];
-  __shared__ __attribute__((aligned(16))) float lse[NPMAX];
-  __shared__ __attribute__((aligned(16))) float Dq[NPMAX];
-  __shared__ __attribute__((aligned(16))) int code[NPMAX];
-  __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
-  const int bh = wa_block(a), b = bh / a.heads, h = bh % a.heads;
-  const int np = (a.N + 15) & ~15, nt = np / 16;
-  const Stage st{b, h, a.N, np};
-  const int C3 = 3 * a.C, hoff = h * a.hd;
-  stage_rows(Qs, a.qkv, C3, hoff, st, a.hd, nullptr);
-  stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, Kt);
-  stage_rows(Vs, a.qkv, C3, 2 * a.C + hoff, st, a.hd, nullptr);
-  stage_rows(dOs, a.dO, a.C, hoff, st, a.hd, nullptr);
-  stage_table(tab, a, h);
-  stage_codes(code, a, np);
-  stage_region(reg, a, b);
-  stage_D(Dq, a, st);
-  for (int n = threadIdx.x; n < np; n += blockDim.x) lse[n] = n < a.N ? a.lse[(long long)bh * NPMAX + n] : 0.f;
-  __syncthreads();
-  const float* ctab = tab + code_off(a);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r16 = lane & 15, g4 = lane >> 4;
-  for (int qt = wave; qt < nt; qt += WAVES) {
-    const int q = qt * 16 + r16;
-    const s4 bq = ld4(&Qs[q][4 * g4]);
-    const s4 bdo = ld4(&dOs[q][4 * g4]);
-    const float lq = lse[q], dq_ = Dq[q];
-    const bool qv = q < a.N;
-    const float* tq = ctab + code[q];
-    const uint32_t rq = reg[q];
-    f32x4 dq = {0.f, 0.f, 0.f, 0.f};
-    bf16_t* dsrow = a.dS + ((long long)bh * a.N + q) * a.ldn;
-    for (int kt = 0; kt < nt; ++kt) {
-      const f32x4 sc = mma(ld4(&Ks[kt * 16 + r16][4 * g4]), bq, (f32x4){0.f, 0.f, 0.f, 0.f});   // S^T[key][q]
-      const f32x4 dp = mma(ld4(&Vs[kt * 16 + r16][4 * g4]), bdo, (f32x4){0.f, 0.f, 0.f, 0.f}); // dP^T[key][q]
-      float ds[4];
-      scores_q(sc, qv, tq, rq, kt * 16 + 4 * g4, a, code, reg, ds);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = ds[r] == -INFINITY ? 0.f : __expf(ds[r] - lq);
-        ds[r] = p * (dp[r] - dq_);
-      }
-      const s4 dsa = pack4(ds[0], ds[1], ds[2], ds[3]);
-      dq = mma(dsa, ld4(&Kt[r16][kt * 16 + 4 * g4]), dq);
-      if (q < a.N) {
-        const int k0 = kt * 16 + 4 * g4;
-        if (k0 + 3 < a.ldn) {
-          *reinterpret_cast<s4*>(dsrow + k0) = dsa;     // keys >= N carry ds = 0
-        } else {
-          typedef __bf16 b4 __attribute__((ext_vector_type(4)));
-          const b4 v = __builtin_bit_cast(b4, dsa);
-          for (int r = 0; r < 4 && k0 + r < a.ldn; ++r) dsrow[k0 + r] = v[r];
-        }
-      }
-    }
-    if (r16 < a.hd) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int qq = qt * 16 + 4 * g4 + r;
-        if (qq < a.N) a.out[(long long)(b * a.N + qq) * C3 + hoff + r16] = (bf16_t)(dq[r] * a.scale);
-      }
-    }
-  }
-}
-
-// ------------------------------------- backward: dQ and the window-summed dS
-// bwd_q for many windows per block: block = (window group wg of wpg windows, head h, query-tile group qg of 8
-// tiles); wave w owns query tile qg * 8 + w of every window in the group.  Per window it computes dQ as bwd_q
-// does (the same MFMAs on the same operands, so dQ is bitwise bwd_q's) and adds its fp32 dS[q][keys] into
-// registers; after the group it writes the sum once, dsum[wg][h][q][ldn] (fp32, keys >= N zero).  The bias-table
-// gradient then folds nwg window sums instead of B bf16 score gradients: at SwinUNETR stage 0 (1,000 windows of
-// 343 tokens, 3 heads) 79 MB instead of 708 MB written and read back per attention layer.
-constexpr int QB_TILES = 8;                        // query tiles per block (one per wave)
-
-__global__ __launch_bounds__(512) void winattn_bwd_qb_kernel(WinAttnArgs a, int wpg, int nqg, float* dsum) {
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[NPMAX][16];
-  __shared__ __attribute__((aligned(16))) bf16_t Kt[16][TP];
-  __shared__ __attribute__((aligned(16))) bf16_t Qs[QB_TILES * 16][16];
-  __shared__ __attribute__((aligned(16))) bf16_t dOs[QB_TILES * 16][16];
-  __shared__ float tab[TMAX];
-  __shared__ float lse[QB_TILES * 16];
-  __shared__ float Dq[QB_TILES * 16];
-  __shared__ __attribute__((aligned(16))) int code[NPMAX];
-  __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
-  const int blk = wa_block(a), qg = blk % nqg, h = (blk / nqg) % a.heads, wg = blk / (nqg * a.heads);
-  const int np = (a.N + 15) & ~15, nt = np / 16;
-  const int q0 = qg * QB_TILES * 16;
-  const int C3 = 3 * a.C, hoff = h * a.hd;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r16 = lane & 15, g4 = lane >> 4;
-  const int qt = qg * QB_TILES + wave;
-  const int q = qt * 16 + r16;
-  const bool qv = q < a.N;
-  stage_table(tab, a, h);
-  stage_codes(code, a, np);
-  const float* ctab = tab + code_off(a);
-  float acc[NTMAX][4];
-#pragma unroll
-  for (int kt = 0; kt < NTMAX; ++kt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) acc[kt][r] = 0.f;
-  const int b0 = wg * wpg, b1 = b0 + wpg < a.B ? b0 + wpg : a.B;
-  for (int b = b0; b < b1; ++b) {
-    const int bh = b * a.heads + h;
-    const Stage st{b, h, a.N, np};
-    __syncthreads();   // the previous window's operands are consumed
-    stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, Kt);
-    stage_rows(Vs, a.qkv, C3, 2 * a.C + hoff, st, a.hd, nullptr);
-    stage_region(reg, a, b);
-    // this group's queries (zeros past N): rows q0 .. q0 + 127 of Q, dO; their lse and D = dO . O
-    for (int e = threadIdx.x; e < QB_TILES * 16 * 2; e += blockDim.x) {
-      const int n = e >> 1, half = e & 1, qq = q0 + n;
-      V8<bf16_t> vq, vo;
-      vq.zero();
-      vo.zero();
-      if (qq < a.N && half * 8 < a.hd) {
-        vq.load(a.qkv + (long long)(b * a.N + qq) * C3 + hoff + half * 8);
-        vo.load(a.dO + (long long)(b * a.N + qq) * a.C + hoff + half * 8);
-      }
-      vq.store(&Qs[n][half * 8]);
-      vo.store(&dOs[n][half * 8]);
-    }
-    for (int n = threadIdx.x; n < QB_TILES * 16; n += blockDim.x) {
-      const int qq = q0 + n;
-      float d = 0.f, l = 0.f;
-      if (qq < a.N) {
-        d = dot_dO_O(a, (long long)(b * a.N + qq) * a.C + hoff);
-        l = a.lse[(long long)bh * NPMAX + qq];
-      }
-      Dq[n] = d;
-      lse[n] = l;
-    }
-    __syncthreads();
-    if (qt < nt) {
-      const int ql = wave * 16 + r16;
-      const s4 bq = ld4(&Qs[ql][4 * g4]);
-      const s4 bdo = ld4(&dOs[ql][4 * g4]);
-      const float lq = lse[ql], dq_ = Dq[ql];
-      const float* tq = ctab + code[q];
-      const uint32_t rq = reg[q];
-      f32x4 dq = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kt = 0; kt < NTMAX; ++kt) {
-        if (kt < nt) {
-          const f32x4 sc = mma(ld4(&Ks[kt * 16 + r16][4 * g4]), bq, (f32x4){0.f, 0.f, 0.f, 0.f});
-          const f32x4 dp = mma(ld4(&Vs[kt * 16 + r16][4 * g4]), bdo, (f32x4){0.f, 0.f, 0.f, 0.f});
-          float ds[4];
-          scores_q(sc, qv, tq, rq, kt * 16 + 4 * g4, a, code, reg, ds);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float p = ds[r] == -INFINITY ? 0.f : __expf(ds[r] - lq);
-            ds[r] = p * (dp[r] - dq_);
-            acc[kt][r] += ds[r];
-          }
-          dq = mma(pack4(ds[0], ds[1], ds[2], ds[3]), ld4(&Kt[r16][kt * 16 + 4 * g4]), dq);
-        }
-      }
-      if (r16 < a.hd) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int qq = qt * 16 + 4 * g4 + r;
-          if (qq < a.N) a.out[(long long)(b * a.N + qq) * C3 + hoff + r16] = (bf16_t)(dq[r] * a.scale);
-        }
-      }
-    }
-  }
-  if (qt < nt && qv) {
-    float* row = dsum + (((long long)wg * a.heads + h) * a.N + q) * a.ldn;
-#pragma unroll
-    for (int kt = 0; kt < NTMAX; ++kt) {
-      const int k0 = kt * 16 + 4 * g4;
-      if (kt < nt && k0 < a.ldn) {
-        if (k0 + 3 < a.ldn) {
-          *reinterpret_cast<float4*>(row + k0) = make_float4(acc[kt][0], acc[kt][1], acc[kt][2], acc[kt][3]);
-        } else {
-          for (int r = 0; r < 4 && k0 + r < a.ldn; ++r) row[k0 + r] = acc[kt][r];
-        }
-      }
-    }
-  }
-}
-
-// ----------------------------------------------- backward, r05 forms (default)
-// (MMSEG_WINATTN_BWD2=0 restores winattn_bwd_kv_kernel / winattn_bwd_qb_kernel.)  Same decomposition as the r04
-// kernels (key pass: dV, dK; query pass: dQ and the window-summed dS), with what the VALU-issue-bound loops spent
+// ----------------------------------------------- backward, r05 forms
+// (r05; replaced the r04 kernels.)  Key pass: dV, dK; query pass: dQ and the dS summed over a group of wpg windows on
+// chip (the bias-table gradient then folds B / wpg window sums instead of B bf16 score gradients), with what the VALU-issue-bound loops spent
 // per score cut: scores in the log2 domain (table and scale pre-multiplied by log2 e, lse staged as lse * log2 e,
 // one FMA + one v_exp_f32 per probability); in the key pass invalid queries carry lse = +inf (p = 0 with no select)
 // and invalid keys need no mask (their dV / dK rows are never stored); the products that contract over tokens
@@ -1088,16 +751,11 @@ int mmseg_winattn_fwd(const void* qkv, int B, int N, int C, int heads, const flo
   a.swz = 1;      // XCD-aware block order (r05 (iii))
   a.mixall = 0;   // the region compare only for windows that mix shifted regions (r05 (vi))
   if (check_args(a)) return 1;
-  if (knob_i("MMSEG_WINATTN_FWD1", 1)) {
-    mmseg::note_kernel("winattn_fwd1_kernel");
-    if (wa_full(a))
-      MMSEG_LAUNCH(winattn_fwd1_kernel<true>, dim3(B * heads), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
-    else
-      MMSEG_LAUNCH(winattn_fwd1_kernel<false>, dim3(B * heads), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
-  } else {
-    mmseg::note_kernel("winattn_fwd_kernel");
-    MMSEG_LAUNCH(winattn_fwd_kernel, dim3(B * heads), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
-  }
+  mmseg::note_kernel("winattn_fwd1_kernel");
+  if (wa_full(a))
+    MMSEG_LAUNCH(winattn_fwd1_kernel<true>, dim3(B * heads), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+  else
+    MMSEG_LAUNCH(winattn_fwd1_kernel<false>, dim3(B * heads), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
   return mmseg::check_launch("winattn_fwd");
 }
 
@@ -1111,15 +769,12 @@ int mmseg_winattn_bwd(const void* qkv, const void* O, const void* dO, const floa
   if (check_args(a)) return 1;
   MMSEG_REQUIRE(ldn >= N && ldn % 8 == 0, "winattn_bwd: ldn >= N, multiple of 8");
   hipStream_t s = (hipStream_t)stream;
-  const bool v2 = knob_i("MMSEG_WINATTN_BWD2", 1) != 0;
-  if (v2 && wa_full(a)) MMSEG_LAUNCH(winattn_bwd_kv2_kernel<true>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
-  else if (v2) MMSEG_LAUNCH(winattn_bwd_kv2_kernel<false>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
-  else MMSEG_LAUNCH(winattn_bwd_kv_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  if (wa_full(a)) MMSEG_LAUNCH(winattn_bwd_kv2_kernel<true>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  else MMSEG_LAUNCH(winattn_bwd_kv2_kernel<false>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
   if (mmseg::check_launch("winattn_bwd_kv")) return 1;
-  if (v2 && wa_full(a)) MMSEG_LAUNCH(winattn_bwd_q2_kernel<true>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
-  else if (v2) MMSEG_LAUNCH(winattn_bwd_q2_kernel<false>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
-  else MMSEG_LAUNCH(winattn_bwd_q_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
-  mmseg::note_kernel(v2 ? "winattn_bwd_kv2_kernel" : "winattn_bwd_kv_kernel");
+  if (wa_full(a)) MMSEG_LAUNCH(winattn_bwd_q2_kernel<true>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  else MMSEG_LAUNCH(winattn_bwd_q2_kernel<false>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  mmseg::note_kernel("winattn_bwd_kv2_kernel");
   return mmseg::check_launch("winattn_bwd_q");
 }
 
@@ -1143,19 +798,16 @@ int mmseg_winattn_bwd_sum(const void* qkv, const void* O, const void* dO, const 
   MMSEG_REQUIRE(ldn >= N && ldn % 8 == 0 && mmseg_winattn_sum_groups(B, N, heads) > 0,
                 "winattn_bwd_sum: ldn >= N (multiple of 8) and enough windows (mmseg_winattn_sum_groups)");
   hipStream_t s = (hipStream_t)stream;
-  const bool v2 = knob_i("MMSEG_WINATTN_BWD2", 1) != 0;
-  if (v2 && wa_full(a)) MMSEG_LAUNCH(winattn_bwd_kv2_kernel<true>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
-  else if (v2) MMSEG_LAUNCH(winattn_bwd_kv2_kernel<false>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
-  else MMSEG_LAUNCH(winattn_bwd_kv_kernel, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  if (wa_full(a)) MMSEG_LAUNCH(winattn_bwd_kv2_kernel<true>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
+  else MMSEG_LAUNCH(winattn_bwd_kv2_kernel<false>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
   if (mmseg::check_launch("winattn_bwd_kv")) return 1;
   const int wpg = qb_windows_per_group(B, N, heads);
   const int nt = ((N + 15) & ~15) / 16, nqg = (nt + QB_TILES - 1) / QB_TILES, nwg = (B + wpg - 1) / wpg;
-  if (v2 && wa_full(a))
+  if (wa_full(a))
     MMSEG_LAUNCH(winattn_bwd_qb2_kernel<true>, dim3(nwg * heads * nqg), dim3(64 * WAVES), 0, s, a, wpg, nqg, dsum);
-  else if (v2)
+  else
     MMSEG_LAUNCH(winattn_bwd_qb2_kernel<false>, dim3(nwg * heads * nqg), dim3(64 * WAVES), 0, s, a, wpg, nqg, dsum);
-  else MMSEG_LAUNCH(winattn_bwd_qb_kernel, dim3(nwg * heads * nqg), dim3(64 * WAVES), 0, s, a, wpg, nqg, dsum);
-  mmseg::note_kernel(v2 ? "winattn_bwd_kv2_kernel" : "winattn_bwd_kv_kernel");
+  mmseg::note_kernel("winattn_bwd_kv2_kernel");
   return mmseg::check_launch("winattn_bwd_qb");
 }
 

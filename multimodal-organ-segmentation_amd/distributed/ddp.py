@@ -137,9 +137,7 @@ class GradBuckets:
                 if dist.get_backend(self.group) == "nccl":
                     # AVG over ranks; at world size 1 (reduce_single_rank: the one-GPU rehearsal) AVG is the
                     # identity and SUM is the same collective without RCCL's single-rank scaling pass
-                    # (MMSEG_DP_AVG1=1 keeps AVG there)
-                    op = dist.ReduceOp.AVG if (self.w > 1 or os.environ.get("MMSEG_DP_AVG1", "0") == "1") \
-                        else dist.ReduceOp.SUM
+                    op = dist.ReduceOp.AVG if self.w > 1 else dist.ReduceOp.SUM
                 else:                       # gloo has no AVG: pre-scale on the comm stream, then SUM
                     t.div_(self.w)
                     op = dist.ReduceOp.SUM

@@ -729,8 +729,8 @@ class Block:
         """conv1's InstanceNorm backward applied inside the stem weight gradient (no input gradient written):
         conv1 takes the stem path, has no data gradient, and the volume is above the one-launch small-IN size
         (whose backward sums in another order)."""
-        return (os.environ.get("MMSEG_STEM_INB", "1") != "0" and not self.c1.need_dgrad and self.c1.Co != 48
-                and self.x1.V > SMALL_IN_V and self.c1._stem(xin, self.x1.ld))
+        return (not self.c1.need_dgrad and self.c1.Co != 48 and self.x1.V > SMALL_IN_V
+                and self.c1._stem(xin, self.x1.ld))
 
 
 class ConvGroup:

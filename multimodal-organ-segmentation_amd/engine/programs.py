@@ -334,7 +334,7 @@ class DualEncoderProgram:
         rt, F, M, dims = self.rt, self.F, self.M, self.dims
         self.x2c, self.statsc = {}, {}
         self.group_outnorm = (M > 1 and self.fusion in ("mean", "add") and not self.multistream
-                              and os.environ.get("MMSEG_GROUP_OUTNORM", "1") != "0")
+                              and os.environ.get("MMSEG_GROUP_SMALL", "1") != "0")   # (one switch for grouping)
         if not self.group_outnorm:
             return
         for l in range(min(self.l0, self.L)):

@@ -402,11 +402,10 @@ class SwinBlockProg:
             ng = L.mmseg_winattn_sum_groups(B, Nw, self.heads)
             # algorithmic backward work: dP = dO V^T, dV = P^T dO, dK = dS^T Q (the key pass, 3 x 2 Nw^2 hd) and
             # dQ = dS K (the query pass, 2 Nw^2 hd); the recomputed scores are not counted
-            v2 = "2" if os.environ.get("MMSEG_WINATTN_BWD2", "1") != "0" else ""   # (winattn.hip's default)
-            kv_w = (f"winattn_bwd_kv{v2}_kernel", 6.0 * B * Nw * Nw * C, 2.0 * Mw * 8 * C)
+            kv_w = ("winattn_bwd_kv2_kernel", 6.0 * B * Nw * Nw * C, 2.0 * Mw * 8 * C)
             if ng > 0:
                 dsum = torch.empty(ng * self.heads * Nw * ldn, dtype=torch.float32, device=rt.device)
-                with TIMER.region(*kv_w, more=[(f"winattn_bwd_qb{v2}_kernel", 2.0 * B * Nw * Nw * C, 2.0 * Mw * 7 * C)]):
+                with TIMER.region(*kv_w, more=[("winattn_bwd_qb2_kernel", 2.0 * B * Nw * Nw * C, 2.0 * Mw * 7 * C)]):
                     L.mmseg_winattn_bwd_sum(ptr(st["qkv"]), ptr(st["O"]), ptr(dO), ptr(st["P"]), B, Nw, C,
                                             self.heads, ptr(self._table_t()), self.table.shape[0], w0, w1, w2,
                                             ptr(region), nw, self.core.scale, ptr(dqkv), ptr(dsum), ldn, s)
@@ -415,7 +414,7 @@ class SwinBlockProg:
                 del dsum
             else:
                 dS = self._empty(B * self.heads * Nw * ldn)
-                with TIMER.region(*kv_w, more=[(f"winattn_bwd_q{v2}_kernel", 2.0 * B * Nw * Nw * C, 2.0 * Mw * 7 * C)]):
+                with TIMER.region(*kv_w, more=[("winattn_bwd_q2_kernel", 2.0 * B * Nw * Nw * C, 2.0 * Mw * 7 * C)]):
                     L.mmseg_winattn_bwd(ptr(st["qkv"]), ptr(st["O"]), ptr(dO), ptr(st["P"]), B, Nw, C, self.heads,
                                         ptr(self._table_t()), self.table.shape[0], w0, w1, w2, ptr(region), nw,
                                         self.core.scale, ptr(dqkv), ptr(dS), ldn, s)

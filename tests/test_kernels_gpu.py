@@ -71,7 +71,6 @@ def test_conv3_fwd_dgrad_wgrad(dev, dtype, cin, cout, shape):
     ({}, 128, 32, (1, 4, 16, 8)),                                   # BN32 ZW1, 4 input chunks
     ({}, 256, 128, (2, 12, 12, 12)),                                 # runtime brick (3,6,12) + chunk split-K
     ({}, 512, 256, (1, 6, 6, 6)),                                    # runtime brick (6,6,6), 16 chunks
-    ({"MMSEG_BRICKR": "0"}, 256, 128, (2, 12, 12, 12)),              # same through the gather GEMM
     # runtime brick 6x6x6 with the in-block K split over two 256-thread halves (KW = 2, bf16; r05), and an odd chunk
     # count per block (2 + 1: half 1 idles through the last stages' barriers)
     ({}, 256, 256, (4, 12, 12, 12)),                                 # the grouped 12^3 shape (N = M x B = 4)
@@ -81,7 +80,6 @@ def test_conv3_fwd_dgrad_wgrad(dev, dtype, cin, cout, shape):
     ({"MMSEG_WGRAD_BRICK": "0"}, 64, 64, (1, 4, 8, 8)),              # generic wgrad
     ({}, 32, 128, (1, 8, 4, 16)),                                    # v2 brick wgrad, 2 row tiles of 64 co
     ({}, 64, 32, (2, 4, 4, 16)),                                     # v2 brick wgrad, 32 co per block
-    ({"MMSEG_WGRAD_BRICK2_CO32": "0"}, 64, 32, (2, 4, 4, 16)),       # v1 for 32 co
     # v2 brick wgrad with LDS-DMA staging (bf16; f32 keeps the register-staged kernel): 3-stage ring, border
     # halos, ragged brick ranges over the splits
     ({"MMSEG_WGRAD_DMA": "1"}, 32, 128, (1, 8, 4, 16)),              # 64 co, 2 row tiles

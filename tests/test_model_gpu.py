@@ -588,32 +588,30 @@ def test_head_in_partials(dev, model, dtype, knob, defer_head, monkeypatch):
 
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
 @pytest.mark.parametrize("model", ["unet", "dual_encoder"])
-def test_stem_inb_bitwise(dev, model, dtype, monkeypatch):
+def test_stem_inb_engaged(dev, model, dtype):
     """The top block's conv1 is the stem: its InstanceNorm backward is applied by the stem weight gradient while it
-    stages dy (mmseg_instnorm_bwd_coef + mmseg_stem_wgrad_inb, the norm's input gradient never written) -- the
-    same loss and bit-identical gradients as the materialised path (MMSEG_STEM_INB=0)."""
+    stages dy (mmseg_instnorm_bwd_coef + mmseg_stem_wgrad_inb, the norm's input gradient never written).  Here: it
+    engages at 32^3 and yields finite gradients; its values are held to the reference by the golden whole-model and
+    full-size pinned tests, which run it (its materialised A/B switch measured bitwise equal, r04, and was removed
+    in round 6)."""
     from mmseg_amd.engine.engine import fused_loss_supported, run_engine_loss
     from mmseg_amd.trainer.losses import DiceCELoss
     gen = torch.Generator().manual_seed(11)
     x = torch.randn(2, 2, 32, 32, 32, generator=gen).to(dev)
     y = torch.randint(0, 3, (2, 32, 32, 32), generator=gen).to(dev)
-    res = []
-    for inb in ("1", "0"):
-        monkeypatch.setenv("MMSEG_STEM_INB", inb)
-        cfg = make_config(model, ["CT", "PET"], 3, [32, 64, 128], dtype=dtype)
-        torch.manual_seed(0)
-        m = build_model(cfg).to(dev)
-        m.train()
-        assert fused_loss_supported(m.backbone, model, x)
-        loss = run_engine_loss(m.backbone, model, x, y, DiceCELoss()._spec(), None)
-        loss.backward()
-        torch.cuda.synchronize()
-        prog = m.backbone.__dict__["_engine"].program
-        top = prog.init if model == "unet" else prog.encs[0][0]
-        assert (getattr(top, "_coef", None) is not None) == (inb == "1")
-        res.append((loss.detach().clone(), torch.cat([p.grad.reshape(-1) for p in m.parameters()]).clone()))
-    assert torch.equal(res[0][0], res[1][0])
-    assert torch.equal(res[0][1], res[1][1])
+    cfg = make_config(model, ["CT", "PET"], 3, [32, 64, 128], dtype=dtype)
+    torch.manual_seed(0)
+    m = build_model(cfg).to(dev)
+    m.train()
+    assert fused_loss_supported(m.backbone, model, x)
+    loss = run_engine_loss(m.backbone, model, x, y, DiceCELoss()._spec(), None)
+    loss.backward()
+    torch.cuda.synchronize()
+    prog = m.backbone.__dict__["_engine"].program
+    top = prog.init if model == "unet" else prog.encs[0][0]
+    assert getattr(top, "_coef", None) is not None
+    g = torch.cat([p.grad.reshape(-1) for p in m.parameters()])
+    assert torch.isfinite(g).all() and torch.isfinite(loss)
 
 
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
@@ -672,7 +670,7 @@ def test_batched_weight_gradient_reduce_bitwise(dev, dtype, monkeypatch):
                                        ("dual_tiny_m3_tversky", "1"), ("dual_tiny_cross_attention", "w")])
 def test_grouped_modalities_match_per_modality(dev, tag, force, monkeypatch):
     """bf16 (the dtype whose small levels take the runtime-brick kernels): the modality-grouped small levels and the
-    grouped encoder output-norm backward (MMSEG_GROUP_SMALL / MMSEG_GROUP_OUTNORM, programs.DualEncoderProgram)
+    grouped encoder output-norm backward (MMSEG_GROUP_SMALL, programs.DualEncoderProgram)
     against the per-modality launches on the same weights and batch.  The grouped launches split the reductions
     differently (one launch over M x N samples), so the two differ by bf16 rounding: loss within 1e-3 relative,
     logits within 2e-2 and every gradient within 5e-2 normwise (L2).  force=1 (MMSEG_GROUP_FORCE_R): the 24^3
@@ -687,8 +685,7 @@ def test_grouped_modalities_match_per_modality(dev, tag, force, monkeypatch):
     y = torch.randint(0, C, (B, 96, 96, 96), generator=gen)
     res = {}
     for flag in ("1", "0"):
-        monkeypatch.setenv("MMSEG_GROUP_SMALL", flag)
-        monkeypatch.setenv("MMSEG_GROUP_OUTNORM", flag)
+        monkeypatch.setenv("MMSEG_GROUP_SMALL", flag)       # (grouped small levels and grouped output norm)
         # (force: features whose 24^3 convs have unpadded channels -- the tiny fixture's 16 -> 32 conv pads its
         # input channels, which keeps that level per modality)
         feats = [16, 32, 64, 128, 256] if force in ("1", "w") else list(g["features"])
