@@ -5319,7 +5319,22 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
     if (g.ksplit > 1) return launch_splitk_reduce<T, MODE>(g, s);
     return 0;
   }
-  if (MODE == MODE_POINT && g.Ncols % 96 == 0 && g.Ncols % 64 != 0) {
+  if (MODE == MODE_POINT && g.ksplit == 1 && g.Ncols > 128 && g.Ncols <= 192 && g.Cpad >= 192) {
+    // BM=64, BN=192: SwinUNETR's 144 / 192-column token linears (qkv, MLP fc1, fc2's data gradient) with every A
+    // row read by one block -- 128x64 tiles re-read each K-wide row from L2 / HBM once per column tile
+    if constexpr (MODE == MODE_POINT) {
+      MMSEG_TILE(g, "conv_gemm_kernel<point,64x192>", 192);
+      dim3 grid(ceil_div(g.M, 64));
+      MMSEG_LAUNCH((conv_gemm_kernel<T, MODE, 1, 4, 4, 3>), grid, block, 0, s, g);
+    }
+  } else if (MODE == MODE_POINT && g.ksplit == 1 && g.Ncols > 32 && g.Ncols <= 48 && g.Ncols % 16 == 0) {
+    // BM=128, BN=48: the 48-column token linears / 1x1 convs (feature_size 48) in one column tile (BN=32 took two)
+    if constexpr (MODE == MODE_POINT) {
+      MMSEG_TILE(g, "conv_gemm_kernel<point,128x48>", 48);
+      dim3 grid(ceil_div(g.M, 128));
+      MMSEG_LAUNCH((conv_gemm_kernel<T, MODE, 4, 1, 2, 3>), grid, block, 0, s, g);
+    }
+  } else if (MODE == MODE_POINT && g.Ncols % 96 == 0 && g.Ncols % 64 != 0) {
     // BM=128, BN=96: the 96 / 288 / 480-column 1x1 GEMMs (SwinUNETR's 96-channel stage, the 96 -> 48 residual
     // conv's data gradient) in whole tiles -- BN=64 left a half-empty last column tile that re-read every A row
     if constexpr (MODE == MODE_POINT) {
@@ -5479,8 +5494,11 @@ int launch_wgrad(WgradArgs g, hipStream_t s) {
   static const char* nm[4] = {"wgrad_kernel<conv3>", "wgrad_kernel<point>", "wgrad_kernel<convT_fwd>",
                               "wgrad_kernel<convT_dgrad>"};
   mmseg::note_kernel(nm[MODE]);
-  if (g.Ca % 64 == 0) {
-    dim3 grid(ceil_div(g.Ncols, 64) * (g.Ca / 64) * g.ksplit);
+  // 1x1 weight gradients take 64-row tiles whatever the row count (rows past Ca are masked): every row tile re-reads
+  // the whole B operand (x), and these launches are HBM-bound -- 48 / 144-row layers read x once / three times
+  // instead of twice / five times with 32-row tiles
+  if (g.Ca % 64 == 0 || MODE == MODE_POINT) {
+    dim3 grid(ceil_div(g.Ncols, 64) * ceil_div(g.Ca, 64) * g.ksplit);
     MMSEG_LAUNCH((wgrad_kernel<T, MODE, 2, 2, 2, 2, 64>), grid, block, 0, s, g);
   } else {
     dim3 grid(ceil_div(g.Ncols, 64) * ceil_div(g.Ca, 32) * g.ksplit);

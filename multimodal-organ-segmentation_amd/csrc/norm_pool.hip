@@ -1137,156 +1137,6 @@ __global__ __launch_bounds__(SMALL_T) void in_small_bwd_r(const T* __restrict__ 
   }
 }
 
-// (A 1024-thread form with a 10-level LDS tree measured slower and was dropped.)
-constexpr int SMALL_T1K = 1024;
-
-template <typename T, bool RELU>
-__global__ __launch_bounds__(SMALL_T1K) void in_small_fwd_1k(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy,
-                                                       int V, int C, float eps, float* __restrict__ mean,
-                                                       int mean_ld, float* __restrict__ rstd) {
-  __shared__ float smu[SMALL_T1K * 8], sm2[SMALL_T1K * 8], scnt[SMALL_T1K];
-  const int cg = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
-  const T* xn = x + (long long)n * V * ldx + cg * 8;
-  float mu[8], m2[8], cnt = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) mu[j] = m2[j] = 0.f;
-  auto upd = [&](const V8<T>& a) {
-    cnt += 1.f;
-    const float inv = 1.f / cnt;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float xv = a.get(j), d = xv - mu[j];
-      mu[j] = fmaf(d, inv, mu[j]);
-      m2[j] = fmaf(d, xv - mu[j], m2[j]);
-    }
-  };
-  int v = tid;
-  for (; v + 3 * SMALL_T1K < V; v += 4 * SMALL_T1K) {   // 4 loads in flight
-    V8<T> a[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) a[u].load(xn + (long long)(v + u * SMALL_T1K) * ldx);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) upd(a[u]);
-  }
-  for (; v < V; v += SMALL_T1K) {
-    V8<T> a;
-    a.load(xn + (long long)v * ldx);
-    upd(a);
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    smu[tid * 8 + j] = mu[j];
-    sm2[tid * 8 + j] = m2[j];
-  }
-  scnt[tid] = cnt;
-  __syncthreads();
-  for (int st = SMALL_T1K / 2; st > 0; st >>= 1) {   // Chan merge of thread t and t + st, fixed pairs
-    if (tid < st) {
-      const float na = scnt[tid], nb = scnt[tid + st], nn = na + nb;
-      if (nb > 0.f) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float ma = smu[tid * 8 + j], mb = smu[(tid + st) * 8 + j], dl = mb - ma;
-          smu[tid * 8 + j] = ma + dl * (nb / nn);
-          sm2[tid * 8 + j] = sm2[tid * 8 + j] + sm2[(tid + st) * 8 + j] + dl * dl * (na * nb / nn);
-        }
-        scnt[tid] = nn;
-      }
-    }
-    __syncthreads();
-  }
-  float m[8], rs[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    m[j] = smu[j];
-    rs[j] = 1.f / sqrtf(sm2[j] / (float)V + eps);
-  }
-  if (tid < 8) {
-    mean[(long long)n * mean_ld + cg * 8 + tid] = smu[tid];
-    rstd[n * C + cg * 8 + tid] = 1.f / sqrtf(sm2[tid] / (float)V + eps);
-  }
-  T* yn = y + (long long)n * V * ldy + cg * 8;
-  for (int v = tid; v < V; v += SMALL_T1K) {
-    V8<T> a, o;
-    a.load(xn + (long long)v * ldx);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float h = (a.get(j) - m[j]) * rs[j];
-      o.set(j, (!RELU || h > 0.f) ? h : 0.f);
-    }
-    o.store(yn + (long long)v * ldy);
-  }
-}
-
-template <typename T, int ACT>
-__global__ __launch_bounds__(SMALL_T1K) void in_small_bwd_1k(const T* __restrict__ x, int ldx, const float* __restrict__ mean,
-                                                       const float* __restrict__ rstd, DySrc s, T* __restrict__ dx,
-                                                       int lddx, int V, int C, int D, int H, int W) {
-  __shared__ float sa[SMALL_T1K * 8], sb[SMALL_T1K * 8];
-  const int cg = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
-  float mu[8], rs[8], ga[8], gb[8];
-  load8f(mean + n * C + cg * 8, mu);
-  load8f(rstd + n * C + cg * 8, rs);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ga[j] = gb[j] = 0.f;
-  const DyCtx<T> dc(s, n, V, cg, C, D, H, W);
-  const T* xn = x + (long long)n * V * ldx + cg * 8;
-  for (int v = tid; v < V; v += SMALL_T1K) {
-    V8<T> a;
-    typename DyCtx<T>::Raw r;
-    a.load(xn + (long long)v * ldx);
-    dc.load(v, r);
-    float dy[8];
-    dc.combine(r, dy);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float h = (a.get(j) - mu[j]) * rs[j];
-      const float g = act_grad<ACT>(h, dy[j], s.slope);
-      ga[j] += g;
-      gb[j] = fmaf(g, h, gb[j]);
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    sa[tid * 8 + j] = ga[j];
-    sb[tid * 8 + j] = gb[j];
-  }
-  __syncthreads();
-  for (int st = SMALL_T1K / 2; st > 0; st >>= 1) {
-    if (tid < st) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        sa[tid * 8 + j] += sa[(tid + st) * 8 + j];
-        sb[tid * 8 + j] += sb[(tid + st) * 8 + j];
-      }
-    }
-    __syncthreads();
-  }
-  float ca[8], cb[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    ca[j] = sa[j] / (float)V;
-    cb[j] = sb[j] / (float)V;
-  }
-  T* dxn = dx + (long long)n * V * lddx + cg * 8;
-  for (int v = tid; v < V; v += SMALL_T1K) {
-    V8<T> a;
-    typename DyCtx<T>::Raw r;
-    a.load(xn + (long long)v * ldx);
-    dc.load(v, r);
-    float dy[8];
-    dc.combine(r, dy);
-    V8<T> o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float h = (a.get(j) - mu[j]) * rs[j];
-      const float g = act_grad<ACT>(h, dy[j], s.slope);
-      o.set(j, rs[j] * (g - ca[j] - h * cb[j]));
-    }
-    o.store(dxn + (long long)v * lddx);
-  }
-}
-
 // ---------------------------------------------------------------- fusion
 // out[n,v,c] = sum_m w_m * src_m[n,v,c],  w_m = wconst or wts[n*M + m]
 struct FuseSrc {
@@ -1535,9 +1385,7 @@ int knob_small_v() {   // read per call (A/B runs and tests flip it in-process)
   return e ? atoi(e) : 4096;
 }
 
-int knob_small_reg() { return 1; }   // register-resident small-volume kernels (in_small_fwd_r / in_small_bwd_r)
 
-int knob_small_t() { return 256; }
 
 // at least 256 chunks per sample (down to 2 voxels per thread): the 48^3 / 24^3 levels otherwise ran 108..432
 // blocks of 16 voxels per thread, latency-bound (128 / 512 measured within noise, r03u)
@@ -1633,13 +1481,10 @@ int mmseg_instnorm_fwd(const void* x, int ldx, void* y, int ldy, int N, long lon
   auto run = [&](auto tag, auto relu_c) {
     using T = decltype(tag);
     constexpr bool R = decltype(relu_c)::value;
-    if (knob_small_t() == 1024)
-      MMSEG_LAUNCH((in_small_fwd_1k<T, R>), grid, dim3(SMALL_T1K), 0, s, (const T*)x, ldx, (T*)y, ldy, (int)V, C,
-                         eps, mean, mean_ld, rstd);
-    else if (knob_small_reg() && V <= SMALL_T)
+    if (V <= SMALL_T)
       MMSEG_LAUNCH((in_small_fwd_r<T, R, 1>), grid, dim3(SMALL_T), 0, s, (const T*)x, ldx, (T*)y, ldy, (int)V, C,
                          eps, mean, mean_ld, rstd);
-    else if (knob_small_reg() && V <= 8 * SMALL_T)
+    else if (V <= 8 * SMALL_T)
       MMSEG_LAUNCH((in_small_fwd_r<T, R, 8>), grid, dim3(SMALL_T), 0, s, (const T*)x, ldx, (T*)y, ldy, (int)V, C,
                          eps, mean, mean_ld, rstd);
     else
@@ -1836,13 +1681,10 @@ int instnorm_bwd_impl(const void* x, int ldx, const float* mean, const float* rs
       return;
     }
     if (small) {
-      if (knob_small_t() == 1024)
-        MMSEG_LAUNCH((in_small_bwd_1k<T, R>), dim3(C / 8, N), dim3(SMALL_T1K), 0, s, (const T*)x, ldx, mean, rstd,
-                           src, (T*)dx, lddx, (int)V, C, D, H, W);
-      else if (knob_small_reg() && V <= SMALL_T)
+      if (V <= SMALL_T)
         MMSEG_LAUNCH((in_small_bwd_r<T, R, 1>), dim3(C / 8, N), dim3(SMALL_T), 0, s, (const T*)x, ldx, mean, rstd,
                            src, (T*)dx, lddx, (int)V, C, D, H, W);
-      else if (knob_small_reg() && V <= 8 * SMALL_T)
+      else if (V <= 8 * SMALL_T)
         MMSEG_LAUNCH((in_small_bwd_r<T, R, 8>), dim3(C / 8, N), dim3(SMALL_T), 0, s, (const T*)x, ldx, mean, rstd,
                            src, (T*)dx, lddx, (int)V, C, D, H, W);
       else

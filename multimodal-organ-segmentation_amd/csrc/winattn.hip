@@ -170,34 +170,6 @@ __device__ __forceinline__ bool stage_region(uint8_t* reg, const WinAttnArgs& a,
   return __syncthreads_or(mixed) != 0;
 }
 
-// bias + mask of one query against 4 consecutive keys k0..k0+3 (the S^T lane layout), -inf past N
-__device__ __forceinline__ void scores_q(const f32x4& acc, bool qv, const float* tq, uint32_t rq, int k0,
-                                         const WinAttnArgs& a, const int* code, const uint8_t* reg, float v[4]) {
-  const int4 ck = *reinterpret_cast<const int4*>(code + k0);
-  const uint32_t rk = a.region ? *reinterpret_cast<const uint32_t*>(reg + k0) : 0u;
-  const int c[4] = {ck.x, ck.y, ck.z, ck.w};
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float t = acc[r] * a.scale + tq[-c[r]];
-    if (a.region && ((rk >> (8 * r)) & 255u) != rq) t -= 100.0f;
-    v[r] = (qv && k0 + r < a.N) ? t : -INFINITY;
-  }
-}
-
-// bias + mask of one key against 4 consecutive queries q0..q0+3 (the S lane layout)
-__device__ __forceinline__ void scores_k(const f32x4& acc, bool kv, const float* tk, uint32_t rk, int q0,
-                                         const WinAttnArgs& a, const int* code, const uint8_t* reg, float v[4]) {
-  const int4 cq = *reinterpret_cast<const int4*>(code + q0);
-  const uint32_t rq = a.region ? *reinterpret_cast<const uint32_t*>(reg + q0) : 0u;
-  const int c[4] = {cq.x, cq.y, cq.z, cq.w};
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float t = acc[r] * a.scale + tk[c[r]];
-    if (a.region && ((rq >> (8 * r)) & 255u) != rk) t -= 100.0f;
-    v[r] = (kv && q0 + r < a.N) ? t : -INFINITY;
-  }
-}
-
 // ------------------------------------------------------ forward, one pass
 // (r05; replaced the r04 two-pass kernel, which recomputed S^T and exp for P V.)  A query tile's whole score row stays in
 // registers (22 key tiles x 4 keys per lane = 88 VGPRs), so the scores, their bias / mask and the exponentials are
