@@ -5327,6 +5327,14 @@ int launch_gemm(GemmArgs g, hipStream_t s) {
       dim3 grid(ceil_div(g.M, 64));
       MMSEG_LAUNCH((conv_gemm_kernel<T, MODE, 1, 4, 4, 3>), grid, block, 0, s, g);
     }
+  } else if (MODE == MODE_POINT && g.ksplit == 1 && g.Ncols > 64 && g.Ncols <= 128 && g.Ncols % 96 != 0) {
+    // BM=64, BN=128: 128-column outputs (the residual 1x1 convs' data gradients written as whole 96-of-128 rows)
+    // in one column tile -- the 128x64 tile read every A row twice (the 128^3 decoder's: 295 us, r06k)
+    if constexpr (MODE == MODE_POINT) {
+      MMSEG_TILE(g, "conv_gemm_kernel<point,64x128>", 128);
+      dim3 grid(ceil_div(g.M, 64));
+      MMSEG_LAUNCH((conv_gemm_kernel<T, MODE, 1, 4, 4, 2>), grid, block, 0, s, g);
+    }
   } else if (MODE == MODE_POINT && g.ksplit == 1 && g.Ncols > 32 && g.Ncols <= 48 && g.Ncols % 16 == 0) {
     // BM=128, BN=48: the 48-column token linears / 1x1 convs (feature_size 48) in one column tile (BN=32 took two)
     if constexpr (MODE == MODE_POINT) {

@@ -368,7 +368,24 @@ struct DySrc {
   int p1_nmod;           // > 0: p1 holds p1_nmod samples, sample n reads p1 sample n % p1_nmod (the fused level's
                          // gradient shared by the M modality groups of a grouped backward)
   float slope;           // ACT 2: the LeakyReLU's negative slope
+  // > 1 (with p1_nmod): the partial / apply grids are (chunks x gsplit, p1_nmod) -- the gsplit modality samples
+  // that read one p1 sample take adjacent blocks of each chunk, so the second read of that p1 chunk is served by
+  // the Infinity Cache instead of HBM (launched sample-major, the re-read came ~2 samples = 240 MB later)
+  int gsplit;
 };
+
+// (sample, chunk, chunks) of a partial / apply block (DySrc::gsplit)
+__device__ __forceinline__ void in_block(const DySrc& s, int& n, int& chunk, int& nchunk) {
+  if (s.gsplit > 1) {
+    chunk = (int)blockIdx.x / s.gsplit;
+    n = ((int)blockIdx.x % s.gsplit) * s.p1_nmod + (int)blockIdx.y;
+    nchunk = (int)gridDim.x / s.gsplit;
+  } else {
+    n = (int)blockIdx.y;
+    chunk = (int)blockIdx.x;
+    nchunk = (int)gridDim.x;
+  }
+}
 
 // gradient through the activation that follows the norm (h: the normalised value; an activation keeps the sign,
 // so h > 0 is where its output is > 0): ACT 0 none, 1 ReLU, 2 LeakyReLU
@@ -460,7 +477,8 @@ template <typename T, int ACT = 1>
 __global__ void in_bwd_partial(const T* __restrict__ x, int ldx, const float* __restrict__ mean,
                                const float* __restrict__ rstd, DySrc s, int V, int C, int D, int H, int W, int vpc,
                                float* __restrict__ part) {
-  const int n = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
+  int n, chunk, nchunk;
+  in_block(s, n, chunk, nchunk);
   const int C8 = C >> 3;
   const int lanes_v = 256 / C8;
   const int tid = threadIdx.x;
@@ -587,7 +605,8 @@ template <typename T, int ACT = 1, bool ZP = false>
 __global__ void in_bwd_apply(const T* __restrict__ x, int ldx, const float* __restrict__ mean,
                              const float* __restrict__ rstd, DySrc s, const float* __restrict__ coef, T* __restrict__ dx,
                              int lddx, int V, int C, int D, int H, int W, int vpc, int npad) {
-  const int n = blockIdx.y;
+  int n, chunk, nchunk;
+  in_block(s, n, chunk, nchunk);
   const int C8 = C >> 3, lanes_v = 256 / C8;
   const int cg = threadIdx.x % C8, vl = threadIdx.x / C8;
   if (vl >= lanes_v) return;
@@ -607,7 +626,7 @@ __global__ void in_bwd_apply(const T* __restrict__ x, int ldx, const float* __re
   const DyCtx<T> dc(s, n, V, cg, C, D, H, W);
   const T* xn = x + (long long)n * V * ldx + cg * 8;
   T* dxn = dx + (long long)n * V * lddx + cg * 8;
-  const int v0 = blockIdx.x * vpc;
+  const int v0 = chunk * vpc;
   const int v1 = v0 + vpc < V ? v0 + vpc : V;
   for (int vb = v0 + vl; vb < v1; vb += UNR * lanes_v) {
     V8<T> a[UNR];
@@ -1665,6 +1684,11 @@ int instnorm_bwd_impl(const void* x, int ldx, const float* mean, const float* rs
   float* part = ws;
   float* coef = ws + (long long)N * nch * C * 2;
   dim3 grid(nch, N), agrid(anch, N);
+  if (p1_nmod > 0 && N / p1_nmod > 1) {   // modality groups sharing a p1 sample: chunk-major grids (DySrc::gsplit)
+    src.gsplit = N / p1_nmod;
+    grid = dim3(nch * src.gsplit, p1_nmod);
+    agrid = dim3(anch * src.gsplit, p1_nmod);
+  }
   const bool small = V <= knob_small_v() && !part_in;
   if (part_in) coef = ws;
   auto run = [&](auto tag, auto act_c) {

@@ -14,7 +14,7 @@ from mmseg_amd import _lib  # noqa: E402
 # (M tokens, K = Ci, N = Co): stage-0 / stage-1 swin linears, the merge reductions, the decoder's 1x1 residual convs
 SHAPES = [(262144, 48, 144), (262144, 48, 48), (262144, 48, 192), (262144, 192, 48), (32768, 384, 96),
           (32768, 96, 288), (32768, 96, 96), (32768, 96, 384), (32768, 384, 96), (2097152, 96, 48),
-          (262144, 192, 96)]
+          (262144, 192, 96), (2097152, 48, 128), (262144, 48, 128)]
 
 
 def main():

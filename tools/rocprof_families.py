@@ -26,7 +26,8 @@ from collections import defaultdict
 
 _MODES = {"0": "conv3", "1": "point", "2": "convT_fwd", "3": "convT_dgrad"}
 _GEMM_TILES = {("4", "1", "2", "2"): "128x32", ("2", "2", "4", "2"): "128x64", ("1", "4", "4", "4"): "64x256",
-               ("2", "2", "2", "2"): "64x64", ("1", "4", "4", "2"): "64x128"}
+               ("2", "2", "2", "2"): "64x64", ("1", "4", "4", "2"): "64x128", ("2", "2", "4", "3"): "128x96",
+               ("1", "4", "4", "3"): "64x192", ("4", "1", "2", "3"): "128x48"}
 
 
 def _mangled_base(name: str):
@@ -86,6 +87,9 @@ def family(name: str) -> str:
         # compile-time bricks of the runtime-brick kernel: 3x6x6 (12^3 / 6^3, "V3"), 4x4x8 (grouped 48^3 / 24^3)
         v3 = {"3": ",V3", "4": ",B448"}.get(m.group(3), "")
         return f"wgrad_brick{m.group(1)}_kernel<CO{int(m.group(2)) * 16}{v3}>[{dt}]"
+    m = re.search(r"wgrad_row_kernelILb([01])E|wgrad_row_kernel<(true|false)", name)
+    if m:   # (the deferred-norm and plain forms under the timer's names; bf16, 32 co only)
+        return "wgrad_row_kernel<CO32" + (",NORM" if (m.group(1) or m.group(2)) in ("1", "true") else "") + ">[bf16]"
     m = re.search(r"wgrad_dma_kernelILi(\d+)E|wgrad_dma_kernel<(\d+)", name)
     if m:
         return f"wgrad_dma_kernel<CO{int(m.group(1) or m.group(2)) * 16}>"
