@@ -74,7 +74,7 @@ def main():
             if op == "fwd":
                 layer.fwd(x, y)
             elif op == "fwds":
-                assert nb > 0, "no fused-statistics kernel for this shape (MMSEG_FUSED_STATS=1)"
+                assert nb > 0, "no fused-statistics kernel for this shape (the library offers none since round 5)"
                 layer.fwd(x, y, stats_part=part)
             elif op == "fwdn":
                 layer.fwd_norm(x, mean, rstd, y)

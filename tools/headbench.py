@@ -4,7 +4,7 @@
     python tools/headbench.py [--iters 20] [--step-only]
 
 The step form (deferred InstanceNorm input, InstanceNorm-backward partials) is timed too; its loss / checksums
-let A/B runs of the kernel variants (MMSEG_HEAD_PF, MMSEG_LOSS_VPC, MMSEG_HEAD_BWD_VPC) be compared.
+let two builds of the library be compared (the round-4 chunking / prefetch variants are fixed constants now).
 """
 import argparse
 import json

@@ -1,7 +1,7 @@
 """In-process A/B of kernel variants (env knobs read at launch time), interleaved
 rounds in ONE process (cdna_hip_programming.md §5.4 rule 24).
 
-    python tools/kbench.py --variants "MMSEG_SWIZZLE=0,1" "MMSEG_WGRAD_BN=64,128"
+    python tools/kbench.py --variants "MMSEG_WGRAD_ROW=0,1" "MMSEG_BRICK8=0,1"
 Prints per-variant median step time and per-kernel-family ms/step.
 """
 import argparse
