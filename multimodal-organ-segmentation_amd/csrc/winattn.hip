@@ -62,6 +62,16 @@ __device__ __forceinline__ int wa_block(const WinAttnArgs& a) {
 
 __device__ __forceinline__ s4 ld4(const bf16_t* p) { return *reinterpret_cast<const s4*>(p); }
 
+// The transposed operand of a token-contracting product from a row image [tokens][16] (ds_read_b64_tr_b16): each
+// 16-lane group reads a 4-token x 16-dim block, lane (q = (lane & 15) >> 2, p4 = lane & 3) addressing its token q,
+// dims 4 p4 .. +3; lane r16 then holds dim r16 of the 4 tokens -- what the [16][tokens] transposed images held, with
+// no transposed copy staged (the per-element LDS stores of that copy were a large share of the staging).
+typedef __attribute__((address_space(3))) s4 lds_s4;
+__device__ __forceinline__ s4 ld4t(const bf16_t (*rows)[16], int t0) {
+  const int lane = threadIdx.x & 63;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(&rows[t0 + ((lane & 15) >> 2)][4 * (lane & 3)]));
+}
+
 __device__ __forceinline__ s4 pack4(float a, float b, float c, float d) {
   typedef __bf16 b4 __attribute__((ext_vector_type(4)));
   b4 v = {(bf16_t)a, (bf16_t)b, (bf16_t)c, (bf16_t)d};
@@ -192,6 +202,8 @@ template <bool FULL>
 __global__ __launch_bounds__(512) void winattn_fwd1_kernel(WinAttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Qs[NPMAX][16];
   __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
+  // (V stays a transposed [16][tokens] image here: the transposed reads of a row image took this kernel from 126 to
+  // 130 VGPRs, past the 4-waves-per-SIMD budget)
   __shared__ __attribute__((aligned(16))) bf16_t Vt[16][TP];
   __shared__ float tab[TMAX];
   __shared__ __attribute__((aligned(16))) int code[NPMAX];
@@ -351,8 +363,6 @@ __global__ __launch_bounds__(512) void winattn_bwd_kv2_kernel(WinAttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[NPMAX][16];
   __shared__ __attribute__((aligned(16))) bf16_t dOs[NPMAX][16];
-  __shared__ __attribute__((aligned(16))) bf16_t Qt[16][TP];
-  __shared__ __attribute__((aligned(16))) bf16_t dOt[16][TP];
   __shared__ float tab[TMAX];
   __shared__ __attribute__((aligned(16))) float lse2[NPMAX];
   __shared__ __attribute__((aligned(16))) float Dq[NPMAX];
@@ -362,10 +372,10 @@ __global__ __launch_bounds__(512) void winattn_bwd_kv2_kernel(WinAttnArgs a) {
   const int np = FULL ? NPMAX : (a.N + 15) & ~15, nt = FULL ? NTMAX : np / 16;   // FULL: 22 key tiles, compile-time
   const Stage st{b, h, a.N, np};
   const int C3 = 3 * a.C, hoff = h * a.hd;
-  stage_rows(Qs, a.qkv, C3, hoff, st, a.hd, Qt);
+  stage_rows(Qs, a.qkv, C3, hoff, st, a.hd, nullptr);
   stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, nullptr);
   stage_rows(Vs, a.qkv, C3, 2 * a.C + hoff, st, a.hd, nullptr);
-  stage_rows(dOs, a.dO, a.C, hoff, st, a.hd, dOt);
+  stage_rows(dOs, a.dO, a.C, hoff, st, a.hd, nullptr);
   {
     stage_table_m(tab, a.table + (long long)h * a.T, a.T, LOG2E);
   }
@@ -423,8 +433,8 @@ __global__ __launch_bounds__(512) void winattn_bwd_kv2_kernel(WinAttnArgs a) {
           }
         }
         const bool hi = qt + 1 < nt;
-        const s4 o0 = ld4(&dOt[r16][qt * 16 + 4 * g4]), o1 = hi ? ld4(&dOt[r16][(qt + 1) * 16 + 4 * g4]) : z4;
-        const s4 q0 = ld4(&Qt[r16][qt * 16 + 4 * g4]), q1 = hi ? ld4(&Qt[r16][(qt + 1) * 16 + 4 * g4]) : z4;
+        const s4 o0 = ld4t(dOs, qt * 16 + 4 * g4), o1 = hi ? ld4t(dOs, (qt + 1) * 16 + 4 * g4) : z4;
+        const s4 q0 = ld4t(Qs, qt * 16 + 4 * g4), q1 = hi ? ld4t(Qs, (qt + 1) * 16 + 4 * g4) : z4;
         dv = mma32(pp[0], pp[1], o0, o1, dv);
         dk = mma32(dd[0], dd[1], q0, q1, dk);
       }
@@ -451,7 +461,6 @@ template <bool FULL>
 __global__ __launch_bounds__(512) void winattn_bwd_qb2_kernel(WinAttnArgs a, int wpg, int nqg, float* dsum) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[NPMAX][16];
-  __shared__ __attribute__((aligned(16))) bf16_t Kt[16][TP];
   __shared__ __attribute__((aligned(16))) bf16_t Qs[QB_TILES * 16][16];
   __shared__ __attribute__((aligned(16))) bf16_t dOs[QB_TILES * 16][16];
   __shared__ float tab[TMAX];
@@ -485,7 +494,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_qb2_kernel(WinAttnArgs a, int
     const int bh = b * a.heads + h;
     const Stage st{b, h, a.N, np};
     __syncthreads();   // the previous window's operands are consumed
-    stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, Kt);
+    stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, nullptr);
     stage_rows(Vs, a.qkv, C3, 2 * a.C + hoff, st, a.hd, nullptr);
     const bool rmix = stage_region(reg, a, b);
     for (int e = threadIdx.x; e < QB_TILES * 16 * 2; e += blockDim.x) {
@@ -557,7 +566,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_qb2_kernel(WinAttnArgs a, int
           const int kt0 = 2 * k2;
           if (kt0 < nt) {
             const bool hi = kt0 + 1 < nt;
-            const s4 k0v = ld4(&Kt[r16][kt0 * 16 + 4 * g4]), k1v = hi ? ld4(&Kt[r16][(kt0 + 1) * 16 + 4 * g4]) : z4;
+            const s4 k0v = ld4t(Ks, kt0 * 16 + 4 * g4), k1v = hi ? ld4t(Ks, (kt0 + 1) * 16 + 4 * g4) : z4;
             dq = mma32(dd[0], dd[1], k0v, k1v, dq);
           }
         }
@@ -599,7 +608,6 @@ __global__ __launch_bounds__(512) void winattn_bwd_q2_kernel(WinAttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[NPMAX][16];
   __shared__ __attribute__((aligned(16))) bf16_t dOs[NPMAX][16];
-  __shared__ __attribute__((aligned(16))) bf16_t Kt[16][TP];
   __shared__ float tab[TMAX];
   __shared__ __attribute__((aligned(16))) float lse2[NPMAX];
   __shared__ __attribute__((aligned(16))) float Dq[NPMAX];
@@ -610,7 +618,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_q2_kernel(WinAttnArgs a) {
   const Stage st{b, h, a.N, np};
   const int C3 = 3 * a.C, hoff = h * a.hd;
   stage_rows(Qs, a.qkv, C3, hoff, st, a.hd, nullptr);
-  stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, Kt);
+  stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, nullptr);
   stage_rows(Vs, a.qkv, C3, 2 * a.C + hoff, st, a.hd, nullptr);
   stage_rows(dOs, a.dO, a.C, hoff, st, a.hd, nullptr);
   {
@@ -674,7 +682,7 @@ __global__ __launch_bounds__(512) void winattn_bwd_q2_kernel(WinAttnArgs a) {
       const int kt0 = 2 * k2;
       if (kt0 < nt) {
         const bool hi = kt0 + 1 < nt;
-        const s4 k0v = ld4(&Kt[r16][kt0 * 16 + 4 * g4]), k1v = hi ? ld4(&Kt[r16][(kt0 + 1) * 16 + 4 * g4]) : z4;
+        const s4 k0v = ld4t(Ks, kt0 * 16 + 4 * g4), k1v = hi ? ld4t(Ks, (kt0 + 1) * 16 + 4 * g4) : z4;
         dq = mma32(dd[0], dd[1], k0v, k1v, dq);
       }
     }

@@ -1,7 +1,7 @@
 """Window-attention kernels at SwinUNETR c4's shapes (128^3, feature_size 48: 64^3 / 32^3 / 16^3 / 8^3 tokens,
 7^3 windows, head_dim 16): times mmseg_winattn_fwd, mmseg_winattn_bwd_sum (key pass + grouped query pass) and
 mmseg_winattn_bwd per stage with HIP events; run under rocprofv3 --kernel-trace --stats for the per-kernel split.
-    python tools/wabench.py [--reps 20] [--stages 0,1]"""
+    python tools/wabench.py [--reps 20] [--stages 0,1] [--lib PATH]"""
 import argparse
 import sys
 
@@ -19,7 +19,11 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--stages", default="0,1")
     ap.add_argument("--masked", type=int, default=1)
+    ap.add_argument("--lib", default="", help="time another build of the library")
     args = ap.parse_args()
+    if args.lib:
+        from mmseg_amd import _lib as _l
+        _l._LIB = _l._Lib(args.lib)
     dev = torch.device("cuda", 0)
     L, s = lib(), stream_handle()
     N, hd, nwin = 343, 16, 8
