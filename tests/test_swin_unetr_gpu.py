@@ -279,11 +279,17 @@ def test_lrelu_bwd_in_part_bitwise(dev, dtype, C, ld, has_b):
         assert torch.equal(d, want)
 
 
-@pytest.mark.parametrize("Co,Ci,M", [(96, 48, 3000), (288, 96, 2000), (96, 384, 1000), (96, 96, 70000)])
+@pytest.mark.parametrize("Co,Ci,M,tile", [(96, 48, 3000, "128x96"), (288, 96, 2000, "128x96"), (96, 384, 1000, "128x96"),
+                                          (96, 96, 70000, "128x96"), (144, 48, 5000, "64x192"),
+                                          (192, 48, 3001, "64x192"), (48, 192, 4000, "128x48"),
+                                          (48, 48, 777, "128x48"), (128, 48, 3000, "64x128"),
+                                          (112, 96, 1500, "64x128")])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_point_gemm_96_column_tile(dev, dtype, Co, Ci, M):
-    """96 / 288-column 1x1 GEMMs on the 128x96 tile (whole column tiles): the forward (plain, residual and GELU
-    epilogues) and the data gradient (plain and dx +=) against fp64."""
+def test_point_gemm_column_tiles(dev, dtype, Co, Ci, M, tile):
+    """The token-linear (1x1) GEMM's whole-layer column tiles -- 128x96 for 96 / 288 columns, 64x192 for 129-192,
+    64x128 for 65-128, 128x48 for 33-48 (each A row read by one block) -- on ragged row counts: the forward (plain,
+    residual and GELU epilogues), the data gradient (plain and dx +=) and the weight / bias gradient (64-row tiles
+    whatever the row count) against fp64."""
     from mmseg_amd.engine.runtime import FlatParams, Runtime
     from mmseg_amd.engine.swin import Lin
     torch.manual_seed(Co + Ci)
@@ -299,8 +305,7 @@ def test_point_gemm_96_column_tile(dev, dtype, Co, Ci, M):
     dx0 = torch.randn(M * Ci, device=dev).to(dtype)
     y = torch.full((M * Co,), float("nan"), device=dev, dtype=dtype)
     L.fwd(x, Ci, M, y, Co)
-    if Co % 64:
-        assert lib().mmseg_last_kernel().decode() == "conv_gemm_kernel<point,128x96>"
+    assert lib().mmseg_last_kernel().decode() == f"conv_gemm_kernel<point,{tile}>"
     yr = torch.full((M * Co,), float("nan"), device=dev, dtype=dtype)
     L.fwd(x, Ci, M, yr, Co, res=res)
     h = torch.full((M * Co,), float("nan"), device=dev, dtype=dtype)
@@ -308,6 +313,7 @@ def test_point_gemm_96_column_tile(dev, dtype, Co, Ci, M):
     L.fwd_gelu(x, Ci, M, h, gl)
     dx = torch.full((M * Ci,), float("nan"), device=dev, dtype=dtype)
     L.bwd(x, Ci, dy, Co, M, dx, Ci, False)
+    dw, db = flat.grad(lin.weight).clone(), flat.grad(lin.bias).clone()
     dxa = dx0.clone()
     add = L.dgrad_splits(M) == 1
     if add:
@@ -323,6 +329,10 @@ def test_point_gemm_96_column_tile(dev, dtype, Co, Ci, M):
     assert rel(dx.view(M, Ci), refd) < tol
     if add:
         assert rel(dxa.view(M, Ci), refd + dx0.view(M, Ci).double()) < tol
+    # weight / bias gradient: fp32 sums of the bf16 (or fp32) operands
+    refw = dy.view(M, Co).double().t() @ x.view(M, Ci).double()
+    assert rel(dw.view(Co, Ci), refw) < 1e-5
+    assert rel(db, dy.view(M, Co).double().sum(0)) < 1e-5
 
 
 @pytest.mark.parametrize("Co,Ci,M", [(48, 192, 3000), (96, 64, 5000), (384, 1536, 700)])
