@@ -3615,26 +3615,7 @@ __global__ __launch_bounds__(512, (MT == 2 && V == 2) ? 2 : 1) void wgrad_brick2
 // (8 consecutive halo x positions, or 8 aligned dy rows, then cover the 64 banks once).  The bias gradient
 // is one more MFMA chain against a ones fragment in wave 7's free tap slot.  NORM: the deferred InstanceNorm +
 // ReLU is applied in place to the landed halo (each thread its fixed channel group), one extra barrier.
-constexpr uint32_t WD_OOB = 0x80000000u;   // buffer offset past every tensor: the DMA writes zeros
-typedef int wd_rsrc_t __attribute__((ext_vector_type(4)));
-// raw buffer descriptor (base, stride 0, num_records bytes) in SGPRs
-__device__ __forceinline__ wd_rsrc_t wd_rsrc(const void* p, uint32_t bytes) {
-  const unsigned long long a = (unsigned long long)p;
-  wd_rsrc_t r;
-  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
-  r[1] = __builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32) & 0xffff);
-  r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
-  r[3] = 0x00020000;
-  return r;
-}
-// one wave-instruction of 16-B LDS-DMA: lane l's chunk lands at LDS byte lds + 16 l.  Issued through inline asm
-// so the compiler's waitcnt tracking does not see it: it would otherwise wait for every pending LDS-DMA before
-// any LDS read (it cannot tell the stage buffers apart), which serialises the prefetch.  The kernel waits for
-// these loads itself (s_waitcnt vmcnt).
-__device__ __forceinline__ void wd_dma16(uint32_t lds, uint32_t voff, wd_rsrc_t r) {
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds), "v"(voff), "s"(r)
-               : "memory", "m0");
-}
+// (WD_OOB, wd_rsrc, wd_dma16: mmseg_common.h)
 
 // ------------------------------------------------- brick conv v8 (3^3, bf16, 8 waves, LDS-DMA staging)
 // conv3_brick2's BN-column tile with the block grown to an (8 ZP) x 8 x 8 brick: 8 waves, wave w owns z planes

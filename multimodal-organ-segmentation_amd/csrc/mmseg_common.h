@@ -136,6 +136,28 @@ __device__ __forceinline__ uint32_t tap_valid_mask(int z, int y, int x, int D, i
 // Returns a logical tile id such that each XCD walks a CONTIGUOUS range of
 // logical tiles (neighbouring tiles share operand panels in that XCD's L2).
 // Bijective for any T (speed only; correctness never depends on placement).
+// ---- LDS-DMA (buffer_load ... lds), shared by the conv weight-gradient / brick8 kernels and the window attention
+constexpr uint32_t WD_OOB = 0x80000000u;   // buffer offset past every tensor: the DMA writes zeros
+typedef int wd_rsrc_t __attribute__((ext_vector_type(4)));
+// raw buffer descriptor (base, stride 0, num_records bytes) in SGPRs
+__device__ __forceinline__ wd_rsrc_t wd_rsrc(const void* p, uint32_t bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  wd_rsrc_t r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32) & 0xffff);
+  r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
+  r[3] = 0x00020000;
+  return r;
+}
+// one wave-instruction of 16-B LDS-DMA: lane l's chunk lands at LDS byte lds + 16 l.  Issued through inline asm
+// so the compiler's waitcnt tracking does not see it: it would otherwise wait for every pending LDS-DMA before
+// any LDS read (it cannot tell the stage buffers apart), which serialises the prefetch.  The kernel waits for
+// these loads itself (s_waitcnt vmcnt).
+__device__ __forceinline__ void wd_dma16(uint32_t lds, uint32_t voff, wd_rsrc_t r) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds), "v"(voff), "s"(r)
+               : "memory", "m0");
+}
+
 __device__ __forceinline__ int xcd_swizzle(int b, int T) {
   const int xcd = b & 7, j = b >> 3, q = T >> 3, r = T & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;

@@ -457,17 +457,28 @@ __global__ __launch_bounds__(512) void winattn_bwd_kv2_kernel(WinAttnArgs a) {
   }
 }
 
+// LDS-DMA image of one window for the grouped query pass (double-buffered): each source in its own 1-KB-aligned
+// run of 16-B chunks (a wave-instruction moves 64 chunks from ONE buffer resource), chunk c of a run at byte 16 c.
+//   K, V: [NPMAX][16] bf16 rows (chunk 2 n + half)      11 instructions each
+//   Q, dO, O: the block's 128 queries, [128][16]          4 each
+//   lse: [128] f32 (32 chunks)                           1
+// Invalid chunks (tokens / queries >= N, the upper 8 dims when head_dim = 8) read through the out-of-range offset
+// and land as zeros, as the register staging wrote them.  (The region labels are not DMA'd: a window's row starts
+// at byte w N, which a 16-B buffer load cannot address unaligned; one byte per thread, loaded during the previous
+// window and stored before its barrier.)
+struct QbImg {
+  static constexpr int K = 0, V = 11, Q = 22, DO = 26, O = 30, L = 34, NI = 35;   // in 1-KB instructions
+  static constexpr int BYTES = NI * 1024;
+};
+
 template <bool FULL>
 __global__ __launch_bounds__(512) void winattn_bwd_qb2_kernel(WinAttnArgs a, int wpg, int nqg, float* dsum) {
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[NPMAX][16];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[NPMAX][16];
-  __shared__ __attribute__((aligned(16))) bf16_t Qs[QB_TILES * 16][16];
-  __shared__ __attribute__((aligned(16))) bf16_t dOs[QB_TILES * 16][16];
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  __shared__ __attribute__((aligned(16))) char img[2][QbImg::BYTES];
+  __shared__ float Dq[2][QB_TILES * 16];
+  __shared__ __attribute__((aligned(16))) uint8_t regs[2][NPMAX];
   __shared__ float tab[TMAX];
-  __shared__ float lse2[QB_TILES * 16];
-  __shared__ float Dq[QB_TILES * 16];
   __shared__ __attribute__((aligned(16))) int code[NPMAX];
-  __shared__ __attribute__((aligned(16))) uint8_t reg[NPMAX];
   const int blk = wa_block(a), qg = blk % nqg, h = (blk / nqg) % a.heads, wg = blk / (nqg * a.heads);
   const int np = FULL ? NPMAX : (a.N + 15) & ~15, nt = FULL ? NTMAX : np / 16;   // FULL: 22 key tiles, compile-time
   const int q0 = qg * QB_TILES * 16;
@@ -490,43 +501,114 @@ __global__ __launch_bounds__(512) void winattn_bwd_qb2_kernel(WinAttnArgs a, int
 #pragma unroll
     for (int r = 0; r < 4; ++r) acc[kt][r] = 0.f;
   const int b0 = wg * wpg, b1 = b0 + wpg < a.B ? b0 + wpg : a.B;
-  for (int b = b0; b < b1; ++b) {
-    const int bh = b * a.heads + h;
-    const Stage st{b, h, a.N, np};
-    __syncthreads();   // the previous window's operands are consumed
-    stage_rows(Ks, a.qkv, C3, a.C + hoff, st, a.hd, nullptr);
-    stage_rows(Vs, a.qkv, C3, 2 * a.C + hoff, st, a.hd, nullptr);
-    const bool rmix = stage_region(reg, a, b);
-    for (int e = threadIdx.x; e < QB_TILES * 16 * 2; e += blockDim.x) {
-      const int n = e >> 1, half = e & 1, qq = q0 + n;
-      V8<bf16_t> vq, vo;
-      vq.zero();
-      vo.zero();
-      if (qq < a.N && half * 8 < a.hd) {
-        vq.load(a.qkv + (long long)(b * a.N + qq) * C3 + hoff + half * 8);
-        vo.load(a.dO + (long long)(b * a.N + qq) * a.C + hoff + half * 8);
+
+  // the DMA of window b into image `buf`.  Wave w issues instructions m = w, w + 8, ... (waves 0-3 five, 4-7 four);
+  // instruction m fills 1-KB slot qb_slot(m) of the image: waves 0-3 fetch the dO AND the O rows of the same 32
+  // queries (m = 24 + j, 32 + j), so each computes those queries' D = dO . O from its own landed chunks (its vmcnt
+  // orders them) before the window's barrier -- no extra barrier, no staging registers.
+  const wd_rsrc_t rq_qkv = wd_rsrc(a.qkv, (uint32_t)((long long)a.B * a.N * C3 * 2));
+  const wd_rsrc_t rq_do = wd_rsrc(a.dO, (uint32_t)((long long)a.B * a.N * a.C * 2));
+  const wd_rsrc_t rq_o = wd_rsrc(a.O, (uint32_t)((long long)a.B * a.N * a.C * 2));
+  const wd_rsrc_t rq_l = wd_rsrc(a.lse, (uint32_t)((long long)a.B * a.heads * NPMAX * 4));
+  const int wv = __builtin_amdgcn_readfirstlane(wave);   // (wave-uniform: every source / slot choice is scalar)
+  auto issue = [&](int buf, int b) __attribute__((always_inline)) {
+    const uint32_t lbase = (uint32_t)(uintptr_t)(lds_ptr_t)(&img[buf][0]);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      int m = wv + 8 * k;
+      // (opaque per call: the per-lane offsets below are recomputed per window instead of hoisted out of the window
+      // loop for every (k, source) pair the compiler cannot rule out -- that kept ~30 VGPRs live and spilled)
+      asm volatile("" : "+s"(m));
+      if (m == 31 || m >= 36) continue;   // (31: no source -- the region labels are not DMA'd)
+      if (m < 22) {   // K / V rows of the window's tokens: slots 0-21
+        const uint32_t lds = lbase + m * 1024;
+        const int c = (m < QbImg::V ? m : m - QbImg::V) * 64 + lane, n = c >> 1, half = c & 1;
+        const bool ok = n < a.N && half * 8 < a.hd;
+        const int col = (m < QbImg::V ? a.C : 2 * a.C) + hoff + half * 8;
+        wd_dma16(lds, ok ? (uint32_t)(((b * a.N + n) * C3 + col) * 2) : WD_OOB, rq_qkv);
+      } else if (m < 24 || (m >= 28 && m < 30)) {   // Q rows of the block's queries: slots 22-25
+        const int j = m < 24 ? m - 22 : m - 26;
+        const uint32_t lds = lbase + (QbImg::Q + j) * 1024;
+        const int c = j * 64 + lane, n = c >> 1, half = c & 1, qq = q0 + n;
+        const bool ok = qq < a.N && half * 8 < a.hd;
+        wd_dma16(lds, ok ? (uint32_t)(((b * a.N + qq) * C3 + hoff + half * 8) * 2) : WD_OOB, rq_qkv);
+      } else if (m < 28 || m >= 32) {   // dO (m 24-27) / O (m 32-35) rows of queries 32 j .. 32 j + 31
+        const bool isdo = m < 28;
+        const int j = isdo ? m - 24 : m - 32;
+        const uint32_t lds = lbase + ((isdo ? QbImg::DO : QbImg::O) + j) * 1024;
+        const int c = j * 64 + lane, n = c >> 1, half = c & 1, qq = q0 + n;
+        const bool ok = qq < a.N && half * 8 < a.hd;
+        wd_dma16(lds, ok ? (uint32_t)(((b * a.N + qq) * a.C + hoff + half * 8) * 2) : WD_OOB, isdo ? rq_do : rq_o);
+      } else {   // m == 30: lse of the block's queries (entries past N are masked when read)
+        const int bh = b * a.heads + h;
+        wd_dma16(lbase + QbImg::L * 1024, lane < 32 ? (uint32_t)((bh * NPMAX + q0 + 4 * lane) * 4) : WD_OOB, rq_l);
       }
-      vq.store(&Qs[n][half * 8]);
-      vo.store(&dOs[n][half * 8]);
     }
-    for (int n = threadIdx.x; n < QB_TILES * 16; n += blockDim.x) {
-      const int qq = q0 + n;
-      float d = 0.f, l = 0.f;
-      if (qq < a.N) {
-        d = dot_dO_O(a, (long long)(b * a.N + qq) * a.C + hoff);
-        l = a.lse[(long long)bh * NPMAX + qq];
+  };
+  // D = dO . O (dot_dO_O's arithmetic) of the 32 queries whose dO / O rows this wave fetched into `buf`, after its
+  // vmcnt wait; into Dq[buf] for the next window's multiply
+  auto dots = [&](int buf) __attribute__((always_inline)) {
+    if (wv < 4 && lane < 32) {
+      const int n = 32 * wv + lane;
+      const bf16_t(*dOs)[16] = reinterpret_cast<const bf16_t(*)[16]>(&img[buf][QbImg::DO * 1024]);
+      const bf16_t(*Os)[16] = reinterpret_cast<const bf16_t(*)[16]>(&img[buf][QbImg::O * 1024]);
+      float d = 0.f;
+      if (q0 + n < a.N) {
+        V8<bf16_t> g0, o0;
+        g0.load(&dOs[n][0]);
+        o0.load(&Os[n][0]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d += g0.get(j) * o0.get(j);
+        if (a.hd == 16) {
+          V8<bf16_t> g1, o1;
+          g1.load(&dOs[n][8]);
+          o1.load(&Os[n][8]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) d += g1.get(j) * o1.get(j);
+        }
       }
-      Dq[n] = d;
-      lse2[n] = l * LOG2E;
+      Dq[buf][n] = d;
     }
+  };
+  const int tid = threadIdx.x;
+  auto region_byte = [&](int b) __attribute__((always_inline)) -> uint8_t {   // stage_region's value of token tid
+    return (a.region && tid < a.N) ? a.region[(long long)(b % a.nw) * a.N + tid] : (uint8_t)0;
+  };
+  if (b0 < b1) {
+    if (tid < NPMAX) regs[0][tid] = region_byte(b0);
+    __syncthreads();   // table / codes / first labels staged
+    issue(0, b0);
+    __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): this wave's chunks landed
+    dots(0);
     __syncthreads();
+  }
+  for (int b = b0; b < b1; ++b) {
+    const int cur = (b - b0) & 1;
+    if (b + 1 < b1) issue(cur ^ 1, b + 1);   // (the other image was last read before the previous barrier)
+    const uint8_t nreg = b + 1 < b1 ? region_byte(b + 1) : (uint8_t)0;   // (stored before this window's barrier)
+    const char* I = img[cur];
+    const bf16_t(*Ks)[16] = reinterpret_cast<const bf16_t(*)[16]>(I + QbImg::K * 1024);
+    const bf16_t(*Vs)[16] = reinterpret_cast<const bf16_t(*)[16]>(I + QbImg::V * 1024);
+    const bf16_t(*Qs)[16] = reinterpret_cast<const bf16_t(*)[16]>(I + QbImg::Q * 1024);
+    const bf16_t(*dOs)[16] = reinterpret_cast<const bf16_t(*)[16]>(I + QbImg::DO * 1024);
+    const float* Ls = reinterpret_cast<const float*>(I + QbImg::L * 1024);
+    const uint8_t* reg = regs[cur];
+    // windows that mix shifted regions (stage_region's vote, per wave over the landed labels)
+    bool rmix = false;
+    if (a.region) {
+      const uint8_t r0 = reg[0];
+      int mixed = 0;
+      for (int n = lane; n < a.N; n += 64) mixed |= reg[n] != r0;
+      rmix = __any(mixed);
+    }
     if (qt < nt) {
       const int ql = wave * 16 + r16;
       const s4 bq = ld4(&Qs[ql][4 * g4]);
       const s4 bdo = ld4(&dOs[ql][4 * g4]);
-      const float lq = lse2[ql], dq_ = Dq[ql];
+      const float dq_ = Dq[cur][ql];
+      const float lq = (qv ? Ls[ql] : 0.f) * LOG2E;
       const float* tq = ctab + code[q];
-      const uint32_t rq = reg[q];
+      const uint32_t rq = a.region ? reg[q] : 0u;
       f32x4 dq = {0.f, 0.f, 0.f, 0.f};
       // instantiated for mixed-region windows and for the rest (no per-score mask compare or select)
       auto tiles = [&](auto mixc) __attribute__((always_inline)) {
@@ -583,6 +665,12 @@ __global__ __launch_bounds__(512) void winattn_bwd_qb2_kernel(WinAttnArgs a, int
         }
       }
     }
+    __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): this wave's chunks of window b + 1 landed
+    if (b + 1 < b1) {
+      dots(cur ^ 1);
+      if (tid < NPMAX) regs[cur ^ 1][tid] = nreg;
+    }
+    __syncthreads();
   }
   if (qt < nt && qv) {
     float* row = dsum + (((long long)wg * a.heads + h) * a.N + q) * a.ldn;
@@ -777,6 +865,8 @@ int mmseg_winattn_bwd_sum(const void* qkv, const void* O, const void* dO, const 
   if (check_args(a)) return 1;
   MMSEG_REQUIRE(ldn >= N && ldn % 8 == 0 && mmseg_winattn_sum_groups(B, N, heads) > 0,
                 "winattn_bwd_sum: ldn >= N (multiple of 8) and enough windows (mmseg_winattn_sum_groups)");
+  MMSEG_REQUIRE((long long)B * N * 3 * C * 2 < (1LL << 31) && (long long)B * heads * NPMAX * 4 < (1LL << 31),
+                "winattn_bwd_sum: the query pass's 32-bit DMA offsets need qkv and lse under 2 GB");
   hipStream_t s = (hipStream_t)stream;
   if (wa_full(a)) MMSEG_LAUNCH(winattn_bwd_kv2_kernel<true>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
   else MMSEG_LAUNCH(winattn_bwd_kv2_kernel<false>, dim3(B * heads), dim3(64 * WAVES), 0, s, a);
