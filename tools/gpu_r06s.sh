@@ -1,5 +1,5 @@
 #!/bin/bash
-# r06s: timing-only experiment -- the key pass with staging only (2) / compute only (3), rocprofv3 per-kernel times
+# r06s: timing-only experiment -- a window-attention pass with staging only (2) / compute only (3), rocprofv3 per-kernel times
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/r06s
