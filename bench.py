@@ -183,7 +183,7 @@ def pmc_step_bytes():
     d, src = _profile("pmc_traffic")
     if d is None:
         return None, None
-    steps = d.get("_steps") or d.get("adamw4_kernel", {}).get("launches")
+    steps = d.get("_steps") or (d.get("adamw_pack_kernel") or d.get("adamw4_kernel") or {}).get("launches")
     if not steps:
         return None, src
     tot = sum(v["hbm_bytes_per_launch"] * v["launches"] for k, v in d.items()

@@ -590,6 +590,18 @@ int mmseg_adamw(float* p, const float* g, float* m, float* v, long long n, float
 int mmseg_adamw_hyper(float lr, float beta1, float beta2, float eps, float wd, int step, float* hyper);
 int mmseg_adamw_dev(float* p, const float* g, float* m, float* v, long long n, const float* hyper, const float* skip,
                     void* stream);
+/* mmseg_adamw_dev fused with the weight packs (a captured training step's optimizer launch): the same update of
+ * the whole arena, and every packed weight's new value also written into its operand images exactly as
+ * mmseg_pack_conv3_batched / mmseg_pack_weights_batched write them from the updated weights, so the next forward
+ * skips its pack (mmseg_adamw_pack: hyper-parameters by value, as mmseg_adamw).  descs: device table of n descriptors (mmseg_adamw_pack_desc_bytes() each, sorted by first
+ * block; built by engine/layers.py Packer.adam_table) covering every arena element exactly once -- 3^3 conv tiles,
+ * 1x1 / transposed-conv tiles and plain ranges -- nblocks blocks in all.  p, g, m, v 16-B aligned. */
+int mmseg_adamw_pack_desc_bytes(void);
+int mmseg_adamw_pack(float* p, const float* g, float* m, float* v, const void* descs, int n, int nblocks, float lr,
+                     float beta1, float beta2, float eps, float wd, int step, const float* skip, int dtype,
+                     void* stream);
+int mmseg_adamw_pack_dev(float* p, const float* g, float* m, float* v, const void* descs, int n, int nblocks,
+                         const float* hyper, const float* skip, int dtype, void* stream);
 
 #ifdef __cplusplus
 }

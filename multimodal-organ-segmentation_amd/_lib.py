@@ -58,6 +58,7 @@ class MmsegError(RuntimeError):
 
 # int-returning entry points that return a value, not a status
 _VALUE_FUNCS = ("mmseg_abi_version", "mmseg_wgrad_splits", "mmseg_wgrad_splits_conv3", "mmseg_conv3_splits", "mmseg_pack_desc_bytes", "mmseg_pack3_desc_bytes",
+                "mmseg_adamw_pack_desc_bytes",
                 "mmseg_stem_ok", "mmseg_stem_kp", "mmseg_stem_wgrad_splits", "mmseg_conv3_stats_bricks",
                 "mmseg_head_loss_ok", "mmseg_conv3_norm_ok", "mmseg_conv3_wgrad_norm_ok", "mmseg_head_loss_in_chunks",
                 "mmseg_conv3_dgrad_in_chunks", "mmseg_stem_stats_bricks", "mmseg_conv3_fp8_ok",

@@ -5001,6 +5001,39 @@ struct Pack3Desc {
   int pad1;
 };
 
+// The two operand images of one (8 co x 32 ci) tile of a 3^3 conv's weight staged in sw[co][ci][tap] (ci >= cis
+// zero): forward image (tap, 8-ci group, co) and data-gradient image (tap s -> kgi = (26 - s) * Cop/8 + co0/8,
+// column ci, 8 co per vector; rows co >= Co of a padded image are zero from allocation), 16-B stores.
+template <typename T>
+__device__ __forceinline__ void pack3_write(const float (*sw)[33][29], void* wfp, void* wdp, int Co, int Cip, int Cpad,
+                                            int Cpad_d, int Cop, int co0, int ci0, int cis) {
+  const int tid = threadIdx.x;
+  const int cpg = Cip >> 3;
+  const int ngrp = ((Cip - ci0) < 32 ? (Cip - ci0) : 32) >> 3;
+  T* wf = reinterpret_cast<T*>(wfp);
+  for (int e = tid; e < 27 * 4 * 8; e += 256) {
+    const int co = e & 7, cg = (e >> 3) & 3, t = e >> 5;
+    if (cg >= ngrp || co0 + co >= Co) continue;
+    V8<T> v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v.set(j, sw[co][cg * 8 + j][t]);
+    const long long kgi = (long long)t * cpg + (ci0 >> 3) + cg;
+    v.store(wf + (kgi * Cpad + co0 + co) * 8);
+  }
+  if (wdp == nullptr) return;
+  const int cpgd = (Cop > 0 ? Cop : Co) >> 3;
+  T* wd = reinterpret_cast<T*>(wdp);
+  for (int e = tid; e < 27 * 32; e += 256) {
+    const int ci = e & 31, t = e >> 5;
+    if (ci >= cis) continue;
+    V8<T> v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v.set(j, sw[j][ci][t]);
+    const long long kgi = (long long)(26 - t) * cpgd + (co0 >> 3);
+    v.store(wd + (kgi * Cpad_d + ci0 + ci) * 8);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void pack_conv3_batched_kernel(const Pack3Desc* __restrict__ descs, int n) {
   __shared__ float sw[8][33][29];   // padded: conflict-free image reads (the [8][32][28] form was 32-way on the forward image)
@@ -5037,33 +5070,7 @@ __global__ __launch_bounds__(256) void pack_conv3_batched_kernel(const Pack3Desc
     }
   }
   __syncthreads();
-  // forward image: (t, 8-ci group, co) -> 16 B
-  const int cpg = d.Cip >> 3;
-  const int ngrp = ((d.Cip - ci0) < 32 ? (d.Cip - ci0) : 32) >> 3;
-  T* wf = reinterpret_cast<T*>(d.wf);
-  for (int e = tid; e < 27 * 4 * 8; e += 256) {
-    const int co = e & 7, cg = (e >> 3) & 3, t = e >> 5;
-    if (cg >= ngrp || co0 + co >= d.Co) continue;
-    V8<T> v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v.set(j, sw[co][cg * 8 + j][t]);
-    const long long kgi = (long long)t * cpg + (ci0 >> 3) + cg;
-    v.store(wf + (kgi * d.Cpad + co0 + co) * 8);
-  }
-  if (d.wd == nullptr) return;
-  // data-gradient image: tap s -> kgi = (26 - s) * Cop/8 + co0/8, column ci, 8 co per vector (rows co >= Co of a
-  // padded image are zero from allocation)
-  const int cpgd = (d.Cop > 0 ? d.Cop : d.Co) >> 3;
-  T* wd = reinterpret_cast<T*>(d.wd);
-  for (int e = tid; e < 27 * 32; e += 256) {
-    const int ci = e & 31, t = e >> 5;
-    if (ci >= cis) continue;
-    V8<T> v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v.set(j, sw[j][ci][t]);
-    const long long kgi = (long long)(26 - t) * cpgd + (co0 >> 3);
-    v.store(wd + (kgi * d.Cpad_d + ci0 + ci) * 8);
-  }
+  pack3_write<T>(sw, d.wf, d.wd, d.Co, d.Cip, d.Cpad, d.Cpad_d, d.Cop, co0, ci0, cis);
 }
 
 // Batched pack: one launch packs every layer of a model (descriptor table in device memory).
@@ -5092,6 +5099,173 @@ __global__ void pack_weight_batched_kernel(const PackDesc* __restrict__ descs, i
     const int kgi = (int)(q / d.Cpad);
     const float v = kgi < d.KG ? pack_value(d.w, d.mode, d.Co, d.Ci, d.Cip, kgi, col, j) : 0.f;
     reinterpret_cast<T*>(d.dst)[li] = from_f<T>(v);
+  }
+}
+
+// ------------------------------------------------------------ fused AdamW + weight pack
+// The captured training step's optimizer launch (mmseg_adamw_pack_dev): the AdamW update of the whole flat arena
+// (adamw_one: mmseg_adamw_dev's per-element bits) with every packed weight's NEW value also written into its
+// operand images -- what mmseg_pack_conv3_batched / mmseg_pack_weights_batched would write from the updated fp32
+// weights at the next forward, which then skips its pack (one read of the fp32 weights and two launches less per
+// step).  Blocks by descriptor kind:
+//   0  3^3 conv: (8 co x 32 ci x 27 taps) tiles, pack_conv3_batched_kernel's tiles and image writes;
+//   1  1x1 / token linear W[Co][Ci] (pack modes 2 / 3) or transposed conv W[Ci][Co][8] (modes 4 / 5 / 7):
+//      8 source rows x up to AP_KT columns staged in LDS, written as 16-B vectors per image;
+//   2  a plain range of the arena (biases, norm / LayerNorm parameters, tables): the update only.
+// The host table (engine/layers.py Packer.adam_table) covers every arena element exactly once.  Entries no block
+// owns (K / channel padding) stay zero from allocation, as with the batched packs.
+constexpr int AP_KT = 512;      // kind-1 tile columns (a multiple of 64: whole 8-co groups of a transposed conv)
+constexpr int AP_RANGE = 4096;  // kind-2 elements per block
+struct AdamPackDesc {
+  void* d0;            // kind 0: forward image; kind 1: the mode0 image
+  void* d1;            // data-gradient image / the mode1 image (null: none)
+  long long off;       // first arena element of the weight (kind 0 / 1) or of the range (kind 2)
+  int kind, block_begin;
+  int R, K;            // kind 1: source rows x columns; kind 2: K = the range's length
+  int mode0, mode1;    // kind 1: pack modes of d0 / d1
+  int Co, Ci, Cip, Cpad, Cpad_d, Cop;   // kind 0: Pack3Desc's fields; kind 1: the weight's Co, Ci, Cpad / Cpad_d
+                                        // of d0 / d1, Cop of mode 7
+};
+
+// AdamW over `rows` runs of `len` arena elements (run r starts at a0 + r * stride); the new value of element
+// (r, i) goes to put(r, i, value).  float4 lanes when every run is 16-B aligned.
+template <typename PUT>
+__device__ __forceinline__ void ap_update(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                          float* __restrict__ v, long long a0, long long stride, int rows, int len,
+                                          const AdamHyper& h, PUT&& put) {
+  const int tid = threadIdx.x;
+  if (((a0 | stride | (long long)len) & 3) == 0) {
+    const int n4 = len >> 2, tot = rows * n4;
+    for (int e = tid; e < tot; e += 256) {
+      const int r = e / n4, q = e - r * n4;
+      const long long k = ((a0 + r * stride) >> 2) + q;
+      float4 pv = reinterpret_cast<const float4*>(p)[k];
+      const float4 gv = reinterpret_cast<const float4*>(g)[k];
+      float4 mv = reinterpret_cast<const float4*>(m)[k];
+      float4 vv = reinterpret_cast<const float4*>(v)[k];
+      adamw_one(pv.x, gv.x, mv.x, vv.x, h);
+      adamw_one(pv.y, gv.y, mv.y, vv.y, h);
+      adamw_one(pv.z, gv.z, mv.z, vv.z, h);
+      adamw_one(pv.w, gv.w, mv.w, vv.w, h);
+      reinterpret_cast<float4*>(p)[k] = pv;
+      reinterpret_cast<float4*>(m)[k] = mv;
+      reinterpret_cast<float4*>(v)[k] = vv;
+      put(r, 4 * q, pv.x);
+      put(r, 4 * q + 1, pv.y);
+      put(r, 4 * q + 2, pv.z);
+      put(r, 4 * q + 3, pv.w);
+    }
+  } else {
+    const int tot = rows * len;
+    for (int e = tid; e < tot; e += 256) {
+      const int r = e / len, i = e - r * len;
+      const long long k = a0 + r * stride + i;
+      float pv = p[k], mv = m[k], vv = v[k];
+      adamw_one(pv, g[k], mv, vv, h);
+      p[k] = pv;
+      m[k] = mv;
+      v[k] = vv;
+      put(r, i, pv);
+    }
+  }
+}
+
+// one image of a kind-1 tile: s[8][AP_KT + 1] rows r0 .. r0 + 7, columns k0 .. k0 + kt (kt8: kt rounded up to 8,
+// zero past kt)
+template <typename T>
+__device__ __forceinline__ void ap_write1(const float (*s)[AP_KT + 1], int mode, void* dstp, int cpad, int Co, int Cop,
+                                          int r0, int k0, int kt, int kt8) {
+  const int tid = threadIdx.x;
+  T* dst = reinterpret_cast<T*>(dstp);
+  if (mode == 2) {            // 1x1 forward: (ci group, co) <- 8 ci of row co
+    for (int e = tid; e < kt8; e += 256) {
+      const int rr = e & 7, cg = e >> 3;
+      V8<T> w;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w.set(j, s[rr][cg * 8 + j]);
+      w.store(dst + ((long long)((k0 >> 3) + cg) * cpad + r0 + rr) * 8);
+    }
+  } else if (mode == 3) {     // 1x1 data gradient: (co group r0 / 8, ci) <- the tile's 8 rows of column ci
+    for (int c = tid; c < kt; c += 256) {
+      V8<T> w;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w.set(j, s[j][c]);
+      w.store(dst + ((long long)(r0 >> 3) * cpad + k0 + c) * 8);
+    }
+  } else if (mode == 4) {     // transposed forward: (ci group r0 / 8, t Co + co) <- 8 rows of column co 8 + t
+    const int ncol8 = kt >> 3;
+    for (int e = tid; e < kt; e += 256) {
+      const int t = e / ncol8, col = e - t * ncol8;
+      V8<T> w;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w.set(j, s[j][col * 8 + t]);
+      w.store(dst + ((long long)(r0 >> 3) * cpad + t * Co + (k0 >> 3) + col) * 8);
+    }
+  } else {                    // 5 / 7 transposed data gradient: (t Cop/8 + co group, ci) <- 8 co of row ci, tap t
+    const int cpgd = (mode == 7 ? Cop : Co) >> 3, ngrp = kt >> 6;
+    for (int e = tid; e < 64 * ngrp; e += 256) {
+      const int rr = e & 7, t = (e >> 3) & 7, cg = e >> 6;
+      V8<T> w;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w.set(j, s[rr][(cg * 8 + j) * 8 + t]);
+      const int co = (k0 >> 3) + cg * 8;
+      w.store(dst + ((long long)(t * cpgd + (co >> 3)) * cpad + r0 + rr) * 8);
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void adamw_pack_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                         float* __restrict__ m, float* __restrict__ v,
+                                                         const AdamPackDesc* __restrict__ descs, int n,
+                                                         AdamHyper hv, const AdamHyper* __restrict__ hp,
+                                                         const float* __restrict__ skip) {
+  __shared__ float sw[8][33][29];
+  AdamHyper h;
+  if (!adamw_load(hv, hp, skip, h)) return;
+  int lo = 0, hi = n - 1;
+  const int b = blockIdx.x;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (descs[mid].block_begin <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const AdamPackDesc d = descs[lo];
+  const int lb = b - d.block_begin;
+  const int tid = threadIdx.x;
+  if (d.kind == 0) {
+    const int nci = (d.Ci + 31) / 32;
+    const int co0 = (lb / nci) * 8, ci0 = (lb % nci) * 32;
+    const int cis = d.Ci - ci0 < 32 ? d.Ci - ci0 : 32;
+    if (co0 >= d.Co) return;
+    for (int e = tid; e < 8 * (32 - cis) * 27; e += 256) {   // the tile's channel padding reads as zero
+      const int co = e / ((32 - cis) * 27), r = e - co * ((32 - cis) * 27);
+      sw[co][cis + r / 27][r % 27] = 0.f;
+    }
+    ap_update(p, g, m, v, d.off + ((long long)co0 * d.Ci + ci0) * 27, (long long)d.Ci * 27, 8, cis * 27, h,
+              [&](int r, int i, float x) __attribute__((always_inline)) {
+                const int ci = i / 27;
+                sw[r][ci][i - ci * 27] = x;
+              });
+    __syncthreads();
+    pack3_write<T>(sw, d.d0, d.d1, d.Co, d.Cip, d.Cpad, d.Cpad_d, d.Cop, co0, ci0, cis);
+  } else if (d.kind == 1) {
+    float (*s)[AP_KT + 1] = reinterpret_cast<float (*)[AP_KT + 1]>(&sw[0][0][0]);
+    const int nkt = (d.K + AP_KT - 1) / AP_KT;
+    const int r0 = (lb / nkt) * 8, k0 = (lb % nkt) * AP_KT;
+    const int kt = d.K - k0 < AP_KT ? d.K - k0 : AP_KT, kt8 = (kt + 7) & ~7;
+    if (r0 >= d.R) return;
+    for (int e = tid; e < 8 * (kt8 - kt); e += 256) s[e / (kt8 - kt)][kt + e % (kt8 - kt)] = 0.f;
+    ap_update(p, g, m, v, d.off + (long long)r0 * d.K + k0, d.K, 8, kt, h,
+              [&](int r, int i, float x) __attribute__((always_inline)) { s[r][i] = x; });
+    __syncthreads();
+    ap_write1<T>(s, d.mode0, d.d0, d.Cpad, d.Co, d.Cop, r0, k0, kt, kt8);
+    if (d.d1 != nullptr) ap_write1<T>(s, d.mode1, d.d1, d.Cpad_d, d.Co, d.Cop, r0, k0, kt, kt8);
+  } else {
+    if (lb * AP_RANGE >= d.K) return;
+    const long long a0 = d.off + (long long)lb * AP_RANGE;
+    const int len = d.K - lb * AP_RANGE < AP_RANGE ? d.K - lb * AP_RANGE : AP_RANGE;
+    ap_update(p, g, m, v, a0, 0, 1, len, h, [](int, int, float) __attribute__((always_inline)) {});
   }
 }
 
@@ -5705,6 +5879,41 @@ int mmseg_pack_weight(const float* w, void* dst, int mode, int Co, int Ci, int C
 }
 
 int mmseg_pack3_desc_bytes(void) { return (int)sizeof(Pack3Desc); }
+
+int mmseg_adamw_pack_desc_bytes(void) { return (int)sizeof(AdamPackDesc); }
+
+static int adamw_pack_launch(float* p, const float* g, float* m, float* v, const void* descs, int n, int nblocks,
+                             const AdamHyper& hv, const AdamHyper* hp, const float* skip, int dtype,
+                             hipStream_t s) {
+  MMSEG_REQUIRE(n >= 1 && nblocks >= 1 && descs != nullptr, "adamw_pack: a descriptor table (Packer.adam_table)");
+  MMSEG_REQUIRE(((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
+                  reinterpret_cast<uintptr_t>(v)) & 15) == 0, "adamw_pack: p, g, m, v must be 16-B aligned");
+  if (dtype == MMSEG_BF16)
+    MMSEG_LAUNCH(adamw_pack_kernel<bf16_t>, dim3(nblocks), dim3(256), 0, s, p, g, m, v, (const AdamPackDesc*)descs,
+                 n, hv, hp, skip);
+  else
+    MMSEG_LAUNCH(adamw_pack_kernel<float>, dim3(nblocks), dim3(256), 0, s, p, g, m, v, (const AdamPackDesc*)descs,
+                 n, hv, hp, skip);
+  return mmseg::check_launch("adamw_pack");
+}
+
+// descs: device array of n AdamPackDesc sorted by block_begin, nblocks blocks in all (Packer.adam_table); the
+// step's hyper-parameters by value (as mmseg_adamw) or as the 8 device floats of mmseg_adamw_hyper (as
+// mmseg_adamw_dev); skip as there.  p / g / m / v: the flat arenas, 16-B aligned.
+int mmseg_adamw_pack(float* p, const float* g, float* m, float* v, const void* descs, int n, int nblocks, float lr,
+                     float beta1, float beta2, float eps, float wd, int step, const float* skip, int dtype,
+                     void* stream) {
+  MMSEG_REQUIRE(step >= 1, "adamw_pack: step counts from 1");
+  return adamw_pack_launch(p, g, m, v, descs, n, nblocks, adamw_hyper(lr, beta1, beta2, eps, wd, step), nullptr, skip,
+                           dtype, (hipStream_t)stream);
+}
+
+int mmseg_adamw_pack_dev(float* p, const float* g, float* m, float* v, const void* descs, int n, int nblocks,
+                         const float* hyper, const float* skip, int dtype, void* stream) {
+  MMSEG_REQUIRE(hyper != nullptr, "adamw_pack_dev: hyper (8 device floats from mmseg_adamw_hyper) required");
+  return adamw_pack_launch(p, g, m, v, descs, n, nblocks, AdamHyper{}, reinterpret_cast<const AdamHyper*>(hyper),
+                           skip, dtype, (hipStream_t)stream);
+}
 
 #ifdef MMSEG_TIMING_PROBES
 // probe builds only (tools/convbench.py --probe): buffer of 8 * PROBE_NB + 32 * 16 * 64 longs, or null to stop

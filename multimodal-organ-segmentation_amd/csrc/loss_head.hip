@@ -1262,22 +1262,8 @@ __global__ void dice_counts_idx_kernel(const PT* __restrict__ pred, const LT* __
     if (sc[k]) atomicAdd(&counts[k], (unsigned long long)sc[k]);
 }
 
-// ------------------------------------------------------------------ AdamW
-// Hyper-parameters of one step, either by value (eager launches) or read from device memory (a captured step
-// graph replays the same launch every step; the host refreshes the 8 floats before each replay):
-// [decay, omb1, beta2, omb2, eps, step_size, bc2_sqrt, unused].  `skip` (nullable): a device float, the
-// step's count of out-of-range labels (summed over the ranks under DP); non-zero leaves p, m, v untouched,
-// so a batch the trainer is about to raise on never updates the model.
-struct AdamHyper {
-  float decay, omb1, beta2, omb2, eps, step_size, bc2_sqrt, pad;
-};
-__device__ __forceinline__ bool adamw_load(const AdamHyper& hv, const AdamHyper* hp, const float* skip,
-                                           AdamHyper& h) {
-  if (skip && *skip != 0.f) return false;
-  h = hp ? *hp : hv;
-  return true;
-}
-
+// ------------------------------------------------------------------ AdamW (AdamHyper, adamw_load, adamw_one:
+// mmseg_common.h)
 __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                              float* __restrict__ v, long long n, AdamHyper hv, const AdamHyper* __restrict__ hp,
                              const float* __restrict__ skip) {
@@ -1305,16 +1291,6 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
 
 // float4 lanes, two vectors in flight per thread (the scalar kernel above kept one 4-B load of each stream in
 // flight per thread: 177 us for the DualEncoder's 20 M parameters).  Same per-element arithmetic (bitwise equal).
-__device__ __forceinline__ float adamw_one(float& pv, float gv, float& mv, float& vv, float decay, float omb1,
-                                           float beta2, float omb2, float eps, float step_size, float bc2_sqrt) {
-#pragma clang fp contract(off)
-  pv = pv * decay;
-  mv = omb1 < 0.5f ? mv + omb1 * (gv - mv) : gv - (gv - mv) * (1.f - omb1);
-  vv = vv * beta2 + (omb2 * gv) * gv;
-  const float denom = sqrtf(vv) / bc2_sqrt + eps;
-  pv = pv + (-step_size) * (mv / denom);
-  return pv;
-}
 // ntail (< 4): the scalar elements after the last float4, done by block 0's first threads (the same
 // per-element operations as adamw_kernel, so bitwise its results) -- no second launch per step for them.
 __global__ __launch_bounds__(256) void adamw4_kernel(float4* __restrict__ p, const float4* __restrict__ g,
@@ -1323,15 +1299,13 @@ __global__ __launch_bounds__(256) void adamw4_kernel(float4* __restrict__ p, con
                                                      const float* __restrict__ skip, int ntail) {
   AdamHyper h;
   if (!adamw_load(hv, hp, skip, h)) return;
-  const float decay = h.decay, omb1 = h.omb1, beta2 = h.beta2, omb2 = h.omb2, eps = h.eps, step_size = h.step_size,
-              bc2_sqrt = h.bc2_sqrt;
   if (blockIdx.x == 0 && (int)threadIdx.x < ntail) {
     const long long k = 4 * n4 + threadIdx.x;
     float* ps = reinterpret_cast<float*>(p);
     float* ms = reinterpret_cast<float*>(m);
     float* vs = reinterpret_cast<float*>(v);
     float pv = ps[k], mv = ms[k], vv = vs[k];
-    adamw_one(pv, reinterpret_cast<const float*>(g)[k], mv, vv, decay, omb1, beta2, omb2, eps, step_size, bc2_sqrt);
+    adamw_one(pv, reinterpret_cast<const float*>(g)[k], mv, vv, h);
     ps[k] = pv;
     ms[k] = mv;
     vs[k] = vv;
@@ -1354,10 +1328,10 @@ __global__ __launch_bounds__(256) void adamw4_kernel(float4* __restrict__ p, con
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       if (u == 1 && !two) break;
-      adamw_one(pv[u].x, gv[u].x, mv[u].x, vv[u].x, decay, omb1, beta2, omb2, eps, step_size, bc2_sqrt);
-      adamw_one(pv[u].y, gv[u].y, mv[u].y, vv[u].y, decay, omb1, beta2, omb2, eps, step_size, bc2_sqrt);
-      adamw_one(pv[u].z, gv[u].z, mv[u].z, vv[u].z, decay, omb1, beta2, omb2, eps, step_size, bc2_sqrt);
-      adamw_one(pv[u].w, gv[u].w, mv[u].w, vv[u].w, decay, omb1, beta2, omb2, eps, step_size, bc2_sqrt);
+      adamw_one(pv[u].x, gv[u].x, mv[u].x, vv[u].x, h);
+      adamw_one(pv[u].y, gv[u].y, mv[u].y, vv[u].y, h);
+      adamw_one(pv[u].z, gv[u].z, mv[u].z, vv[u].z, h);
+      adamw_one(pv[u].w, gv[u].w, mv[u].w, vv[u].w, h);
       const long long k = u == 0 ? i : i2;
       p[k] = pv[u];
       m[k] = mv[u];
@@ -1747,22 +1721,6 @@ int mmseg_dice_counts_idx(const void* pred, int pred_bytes, const void* labels, 
   else DCI(uint8_t, uint8_t);
 #undef DCI
   return mmseg::check_launch("dice_counts_idx");
-}
-
-static AdamHyper adamw_hyper(float lr, float beta1, float beta2, float eps, float wd, int step) {
-  // torch.optim.AdamW (single-tensor, foreach=False): bias corrections in double, as Python floats
-  const double bc1 = 1.0 - pow((double)beta1, step);
-  const double bc2 = 1.0 - pow((double)beta2, step);
-  AdamHyper h;
-  h.decay = (float)(1.0 - (double)lr * (double)wd);
-  h.omb1 = (float)(1.0 - (double)beta1);
-  h.beta2 = beta2;
-  h.omb2 = (float)(1.0 - (double)beta2);
-  h.eps = eps;
-  h.step_size = (float)(lr / bc1);
-  h.bc2_sqrt = (float)sqrt(bc2);
-  h.pad = 0.f;
-  return h;
 }
 
 static int adamw_launch(float* p, const float* g, float* m, float* v, long long n, const AdamHyper& hv,

@@ -132,10 +132,6 @@ __device__ __forceinline__ uint32_t tap_valid_mask(int z, int y, int x, int D, i
   return m;
 }
 
-// XCD-aware block remap (MI355X: 8 XCDs, blocks dealt round-robin b -> b % 8).
-// Returns a logical tile id such that each XCD walks a CONTIGUOUS range of
-// logical tiles (neighbouring tiles share operand panels in that XCD's L2).
-// Bijective for any T (speed only; correctness never depends on placement).
 // ---- LDS-DMA (buffer_load ... lds), shared by the conv weight-gradient / brick8 kernels and the window attention
 constexpr uint32_t WD_OOB = 0x80000000u;   // buffer offset past every tensor: the DMA writes zeros
 typedef int wd_rsrc_t __attribute__((ext_vector_type(4)));
@@ -158,6 +154,10 @@ __device__ __forceinline__ void wd_dma16(uint32_t lds, uint32_t voff, wd_rsrc_t 
                : "memory", "m0");
 }
 
+// XCD-aware block remap (MI355X: 8 XCDs, blocks dealt round-robin b -> b % 8).
+// Returns a logical tile id such that each XCD walks a CONTIGUOUS range of
+// logical tiles (neighbouring tiles share operand panels in that XCD's L2).
+// Bijective for any T (speed only; correctness never depends on placement).
 __device__ __forceinline__ int xcd_swizzle(int b, int T) {
   const int xcd = b & 7, j = b >> 3, q = T >> 3, r = T & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
@@ -168,4 +168,48 @@ __device__ __forceinline__ int xcd_swizzle(int b, int T) {
 __device__ __forceinline__ float mmseg_gelu(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float mmseg_gelu_grad(float x) {
   return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+}
+
+// ------------------------------------------------------------ AdamW
+// Hyper-parameters of one step, either by value (eager launches) or read from device memory (a captured step
+// graph replays the same launch every step; the host refreshes the 8 floats before each replay):
+// [decay, omb1, beta2, omb2, eps, step_size, bc2_sqrt, unused].  `skip` (nullable): a device float, the
+// step's count of out-of-range labels (summed over the ranks under DP); non-zero leaves p, m, v untouched,
+// so a batch the trainer is about to raise on never updates the model.  Shared by the AdamW kernels
+// (loss_head.hip) and the fused AdamW + weight pack (conv_gemm.hip): one per-element formula, one set of bits.
+struct AdamHyper {
+  float decay, omb1, beta2, omb2, eps, step_size, bc2_sqrt, pad;
+};
+__device__ __forceinline__ bool adamw_load(const AdamHyper& hv, const AdamHyper* hp, const float* skip,
+                                           AdamHyper& h) {
+  if (skip && *skip != 0.f) return false;
+  h = hp ? *hp : hv;
+  return true;
+}
+// torch.optim.AdamW's single-tensor op order (param.mul_(1 - lr wd); exp_avg.lerp_; exp_avg_sq.mul_.addcmul_;
+// param.addcdiv_(exp_avg, denom, -step_size)), no contraction
+__device__ __forceinline__ float adamw_one(float& pv, float gv, float& mv, float& vv, const AdamHyper& h) {
+#pragma clang fp contract(off)
+  pv = pv * h.decay;
+  mv = h.omb1 < 0.5f ? mv + h.omb1 * (gv - mv) : gv - (gv - mv) * (1.f - h.omb1);
+  vv = vv * h.beta2 + (h.omb2 * gv) * gv;
+  const float denom = sqrtf(vv) / h.bc2_sqrt + h.eps;
+  pv = pv + (-h.step_size) * (mv / denom);
+  return pv;
+}
+// host: one step's hyper-parameters as torch.optim.AdamW (single-tensor, foreach=False) derives them -- the bias
+// corrections in double, as Python floats
+static inline AdamHyper adamw_hyper(float lr, float beta1, float beta2, float eps, float wd, int step) {
+  const double bc1 = 1.0 - pow((double)beta1, step);
+  const double bc2 = 1.0 - pow((double)beta2, step);
+  AdamHyper h;
+  h.decay = (float)(1.0 - (double)lr * (double)wd);
+  h.omb1 = (float)(1.0 - (double)beta1);
+  h.beta2 = beta2;
+  h.omb2 = (float)(1.0 - (double)beta2);
+  h.eps = eps;
+  h.step_size = (float)(lr / bc1);
+  h.bc2_sqrt = (float)sqrt(bc2);
+  h.pad = 0.f;
+  return h;
 }

@@ -73,6 +73,11 @@ class Packer:
     def __init__(self, rt: Runtime, descs):
         import struct
         self.rt = rt
+        self.descs = list(descs)
+        # FlatParams.version() the images were last written for (by run() or by the fused AdamW + pack launch);
+        # None: unknown -- the next pack writes them
+        self.fresh = None
+        self._adam = None
         self.per_layer = []
         self.table = self.gtable = None
         if self.per_layer:
@@ -107,6 +112,84 @@ class Packer:
             assert len(gblob) == len(rest) * rt.lib.mmseg_pack_desc_bytes()
             self.gtable = torch.frombuffer(gblob, dtype=torch.uint8).to(rt.device)
             self.gn, self.gtotal = len(rest), total
+
+    AP_KT, AP_RANGE = 512, 4096   # conv_gemm.hip: kind-1 tile columns, kind-2 elements per block
+
+    def adam(self, flat) -> Optional[Tuple[torch.Tensor, int, int]]:
+        """adam_table(flat), built once per arena."""
+        key = (id(flat), flat.flat.data_ptr(), flat.numel)
+        if self._adam is None or self._adam[0] != key:
+            self._adam = (key, self.adam_table(flat))
+        return self._adam[1]
+
+    def adam_table(self, flat) -> Optional[Tuple[torch.Tensor, int, int]]:
+        """(device table, descriptors, blocks) of the fused AdamW + pack (mmseg_adamw_pack_dev) over `flat`'s arena:
+        every packed weight as tiles that also write its operand images (3^3 convs: kind 0, pack_conv3_batched's
+        tiles; 1x1 / token-linear and transposed convs: kind 1), every other arena element in a plain range (kind
+        2), each element exactly once.  None when some weight's images do not fit those kinds (the captured step
+        then keeps the pack in its forward)."""
+        import struct
+        if self.per_layer or not self.descs:
+            return None
+        base, numel = flat.flat.data_ptr(), flat.numel
+        groups = {}
+        for d in self.descs:
+            g = groups.setdefault(d[0], {})
+            if d[2] in g and g[d[2]] != d:
+                return None          # one weight, two different images of one mode
+            g[d[2]] = d
+        recs = []
+        for w, bym in groups.items():
+            modes = sorted(bym)
+            if (w - base) % 4:
+                return None
+            off = (w - base) // 4
+            if modes in ([0], [0, 1], [0, 6]):
+                f, dd = bym[0], bym.get(1) or bym.get(6)
+                Co, Ci, Cip, Cpad = f[3], f[4], f[5], f[8]
+                if Co % 8:
+                    return None
+                rec = (0, off, Co * Ci * 27, (Co // 8) * -(-Ci // 32), f[1], dd[1] if dd else 0, 0, 0, 0, -1, Co, Ci,
+                       Cip, Cpad, dd[8] if dd else 0, dd[5] if dd is not None and dd[2] == 6 else 0)
+            elif modes in ([2], [2, 3]):
+                f, dd = bym[2], bym.get(3)
+                Co, Ci = f[3], f[4]
+                if Co % 8:
+                    return None
+                rec = (1, off, Co * Ci, (Co // 8) * -(-Ci // self.AP_KT), f[1], dd[1] if dd else 0, Co, Ci, 2,
+                       3 if dd else -1, Co, Ci, 0, f[8], dd[8] if dd else 0, 0)
+            elif modes in ([4], [4, 5], [4, 7]):
+                f, dd = bym[4], bym.get(5) or bym.get(7)
+                Co, Ci = f[3], f[4]
+                if Co % 8 or Ci % 8:
+                    return None
+                rec = (1, off, Ci * Co * 8, (Ci // 8) * -(-(Co * 8) // self.AP_KT), f[1], dd[1] if dd else 0, Ci,
+                       Co * 8, 4, dd[2] if dd else -1, Co, Ci, 0, f[8], dd[8] if dd else 0,
+                       dd[5] if dd is not None and dd[2] == 7 else 0)
+            else:
+                return None
+            if off < 0 or off + rec[2] > numel:
+                return None
+            recs.append(rec)
+        recs.sort(key=lambda r: r[1])
+        full, pos = [], 0
+        for r in recs:
+            if r[1] < pos:
+                return None          # overlapping weights
+            if r[1] > pos:
+                n = r[1] - pos
+                full.append((2, pos, n, -(-n // self.AP_RANGE), 0, 0, 0, n, 0, -1, 0, 0, 0, 0, 0, 0))
+            full.append(r)
+            pos = r[1] + r[2]
+        if pos < numel:
+            n = numel - pos
+            full.append((2, pos, n, -(-n // self.AP_RANGE), 0, 0, 0, n, 0, -1, 0, 0, 0, 0, 0, 0))
+        blob, blk = bytearray(), 0
+        for (kind, off, _n, nblk, d0, d1, R, K, m0, m1, Co, Ci, Cip, Cpad, Cpad_d, Cop) in full:
+            blob += struct.pack("<QQq12i", d0, d1, off, kind, blk, R, K, m0, m1, Co, Ci, Cip, Cpad, Cpad_d, Cop)
+            blk += nblk
+        assert len(blob) == len(full) * self.rt.lib.mmseg_adamw_pack_desc_bytes()
+        return torch.frombuffer(blob, dtype=torch.uint8).to(self.rt.device), len(full), blk
 
     def run(self):
         L, s, code = self.rt.lib, self.rt.stream, self.rt.code

@@ -153,10 +153,21 @@ class UNetProgram:
         self.dec = _Decoder(rt, m.decoders, m.out_conv, m.dropout_p, flat, self.F)
         self.shape = None
 
-    def pack(self):
+    def packer(self) -> Packer:
         if getattr(self, "_packer", None) is None:
             self._packer = Packer(self.rt, self._all_descs())
-        self._packer.run()
+        return self._packer
+
+    def pack(self):
+        """The weights' operand images from the current fp32 weights -- skipped while a step graph whose fused
+        AdamW + pack launch keeps them current is captured (trainer/step_graph.py)."""
+        if getattr(self, "skip_pack", False):
+            return
+        pk = self.packer()
+        v = self.flat.version()
+        if pk.fresh != v:
+            pk.run()
+            pk.fresh = v
 
     def setup(self, N, D, H, W):
         if self.shape == (N, D, H, W):
@@ -261,10 +272,21 @@ class DualEncoderProgram:
                 d += p.descs()
         return d + self.dec.descs()
 
-    def pack(self):
+    def packer(self) -> Packer:
         if getattr(self, "_packer", None) is None:
             self._packer = Packer(self.rt, self._all_descs())
-        self._packer.run()
+        return self._packer
+
+    def pack(self):
+        """The weights' operand images from the current fp32 weights -- skipped while a step graph whose fused
+        AdamW + pack launch keeps them current is captured (trainer/step_graph.py)."""
+        if getattr(self, "skip_pack", False):
+            return
+        pk = self.packer()
+        v = self.flat.version()
+        if pk.fresh != v:
+            pk.run()
+            pk.fresh = v
 
     def setup(self, N, D, H, W):
         if self.shape == (N, D, H, W):

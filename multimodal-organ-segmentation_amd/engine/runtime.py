@@ -17,7 +17,7 @@ import math
 import os
 from contextlib import contextmanager
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -226,6 +226,13 @@ class FlatParams:
         if self.on_ready is not None:
             for p in params:
                 self.on_ready(self.index[id(p)])
+
+    def version(self) -> Tuple[int, int]:
+        """Torch's in-place version counters of the arena and of every parameter: any torch write to the weights
+        (load_state_dict, an in-place op on a parameter or on the arena) changes it.  The engine's own kernels
+        bypass the counters; FlatAdamW bumps them after its update (torch's AdamW does as much).  The weight packs
+        (layers.Packer.fresh) compare against it to skip re-packing unchanged weights."""
+        return self.flat._version, sum(p._version for p in self.params)
 
     def intact(self) -> bool:
         """True if every p.data is still a view of the arena (a .to()/load may rebind it)."""

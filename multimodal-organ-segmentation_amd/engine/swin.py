@@ -712,11 +712,21 @@ class SwinUNETRProgram:
             d += u.descs()
         return d
 
-    def pack(self):
-        """Every packed weight image of the network in two launches (layers.Packer)."""
+    def packer(self) -> Packer:
         if self._packed is None:
             self._packed = Packer(self.rt, self._descs())
-        self._packed.run()
+        return self._packed
+
+    def pack(self):
+        """Every packed weight image of the network in two launches (layers.Packer); skipped while a step graph
+        with the fused AdamW + pack launch is captured (trainer/step_graph.py)."""
+        if getattr(self, "skip_pack", False):
+            return
+        pk = self.packer()
+        v = self.flat.version()
+        if pk.fresh != v:
+            pk.run()
+            pk.fresh = v
 
     def setup(self, N, D, H, W):
         if self.shape == (N, D, H, W):

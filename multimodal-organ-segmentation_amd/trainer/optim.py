@@ -6,6 +6,7 @@ build.py:170-180): per-parameter state 'step', 'exp_avg', 'exp_avg_sq', where
 exp_avg / exp_avg_sq are views of two flat fp32 moment buffers."""
 from __future__ import annotations
 
+import weakref
 from typing import List, Optional
 
 import torch
@@ -25,6 +26,24 @@ def _arena_of(params: List[torch.Tensor]):
             return None
         off += p.numel()
     return base, off
+
+
+def pack_source(model: torch.nn.Module):
+    """For FlatAdamW._pack_source: () -> (layers.Packer, FlatParams) of the HIP engine bound to `model` (weakly
+    referenced), or None before its first forward."""
+    ref = weakref.ref(model)
+
+    def src():
+        mdl = ref()
+        if mdl is None:
+            return None
+        bb = getattr(mdl, "backbone", mdl)
+        eng = bb.__dict__.get("_engine")
+        prog = getattr(eng, "program", None)
+        if prog is None or getattr(eng, "flat", None) is None or not hasattr(prog, "packer"):
+            return None
+        return prog.packer(), eng.flat
+    return src
 
 
 class FlatAdamW(torch.optim.AdamW):
@@ -103,7 +122,23 @@ class FlatAdamW(torch.optim.AdamW):
             step = int(st.item()) + 1
             st.fill_(float(step))
             b1, b2 = group["betas"]
-            lib().mmseg_adamw(base, garena[0], ptr(m), ptr(v), n, float(group["lr"]), float(b1), float(b2),
-                              float(group["eps"]), float(group["weight_decay"]), step, ptr(self.guard),
-                              stream_handle())
+            hyper = (float(group["lr"]), float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]), step)
+            # the engine's weight images updated in the same launch (mmseg_adamw_pack) when this arena is the
+            # engine's and the images were current, so the next forward skips its pack
+            src = self.__dict__.get("_pack_source")
+            fp = src() if src is not None and len(self.param_groups) == 1 else None
+            pk = tab = None
+            if fp is not None and fp[1].flat.data_ptr() == base and fp[1].numel == n:
+                pk, flat = fp
+                v0 = flat.version()
+                tab = pk.adam(flat) if pk.fresh == v0 else None
+            if tab is not None:
+                lib().mmseg_adamw_pack(base, garena[0], ptr(m), ptr(v), ptr(tab[0]), tab[1], tab[2], *hyper,
+                                       ptr(self.guard), pk.rt.code, stream_handle())
+            else:
+                lib().mmseg_adamw(base, garena[0], ptr(m), ptr(v), n, *hyper, ptr(self.guard), stream_handle())
+            # the kernel wrote the weights behind torch's in-place counters: bump them, as torch's AdamW would
+            torch.autograd.graph.increment_version(params)
+            if tab is not None:
+                pk.fresh = flat.version()
         return loss

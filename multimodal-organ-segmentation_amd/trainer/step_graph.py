@@ -135,6 +135,11 @@ class StepGraphs:
         flat = eng.flat
         m, v = opt._moments(0, grp, flat.numel, self.dev)
         L = lib()
+        # the fused AdamW + pack launch (mmseg_adamw_pack_dev) keeps the weight images current, so the captured
+        # forward leaves out its pack; run() packs eagerly before a replay only when the images are not current
+        prog = eng.program
+        pk = prog.packer() if hasattr(prog, "packer") else None
+        fused = pk.adam(flat) if pk is not None else None
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize(self.dev)
         # no cyclic garbage collection while capturing: a collected object owning a graph (or anything that frees
@@ -142,6 +147,7 @@ class StepGraphs:
         gc_on = gc.isenabled()
         gc.collect()
         gc.disable()
+        prog.skip_pack = fused is not None
         try:
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 loss = eng.forward_loss(x, True, y, spec, cw)
@@ -155,8 +161,13 @@ class StepGraphs:
                 eng.rt.join_side()
                 if tr.dp and tr._buckets is not None:
                     tr._buckets.finish()
-                L.mmseg_adamw_dev(ptr(flat.flat), ptr(flat.grad_flat), ptr(m), ptr(v), flat.numel,
-                                  ptr(self.hyper_dev), ptr(ws[-1:]), stream_handle())
+                if fused is not None:
+                    L.mmseg_adamw_pack_dev(ptr(flat.flat), ptr(flat.grad_flat), ptr(m), ptr(v), ptr(fused[0]),
+                                           fused[1], fused[2], ptr(self.hyper_dev), ptr(ws[-1:]), eng.rt.code,
+                                           stream_handle())
+                else:
+                    L.mmseg_adamw_dev(ptr(flat.flat), ptr(flat.grad_flat), ptr(m), ptr(v), flat.numel,
+                                      ptr(self.hyper_dev), ptr(ws[-1:]), stream_handle())
         except BaseException:
             # a capture that fails part-way through the backward (e.g. a collective RCCL cannot capture) has
             # already decremented bucket counts and stored works / events: drop them so the eager fallback
@@ -165,9 +176,11 @@ class StepGraphs:
                 tr._buckets.reset()
             raise
         finally:
+            prog.skip_pack = False
             if gc_on:
                 gc.enable()
-        return {"graph": g, "loss": loss, "ws": ws, "x": x, "y": y, "cw": cw}
+        return {"graph": g, "loss": loss, "ws": ws, "x": x, "y": y, "cw": cw, "prog": prog, "packer": pk,
+                "fused_pack": fused is not None, "fused_table": fused}
 
     def _entry(self, images: torch.Tensor, labels: torch.Tensor) -> dict:
         ek = self._engine_key()
@@ -225,8 +238,15 @@ class StepGraphs:
         """One training step by graph replay; returns (loss, guard) -- both device tensors owned by the graph (the
         loss is overwritten by the next replay of the same graph)."""
         e = self._entry(images, labels)
+        pk = e["packer"]
+        if e["fused_pack"]:
+            # the captured forward has no pack: the images must be current before the replay (its first one, or
+            # weights changed outside the graph since the last); the replay's AdamW + pack keeps them current
+            e["prog"].pack()
         self._push_hyper()
         e["graph"].replay()
+        if pk is not None and not e["fused_pack"]:
+            pk.fresh = None      # the replayed AdamW wrote the weights after the captured pack read them
         # what torch's LRScheduler step wrapper records (lr_scheduler.py patch_track_step_called): the optimizer
         # stepped before the scheduler does, so scheduler.step() raises no "called before optimizer.step()" warning
         self.tr.optimizer.__dict__["_opt_called"] = True

@@ -34,7 +34,7 @@ from ..distributed import ddp
 from ..models.build import kernels_from_config, load_checkpoint, save_checkpoint
 from .losses import get_loss
 from .metrics import DiceMetric, get_metrics
-from .optim import FlatAdamW
+from .optim import FlatAdamW, pack_source
 
 try:
     from tqdm import tqdm
@@ -56,6 +56,9 @@ class Trainer:
         self.model = self.model.to(self.device)
         self.kernels = kernels_from_config(config)
         self.optimizer = self._setup_optimizer()
+        if isinstance(self.optimizer, FlatAdamW):
+            # its launch also refreshes the engine's weight images (mmseg_adamw_pack): no pack in the next forward
+            self.optimizer._pack_source = pack_source(self.model)
         self.scheduler = self._setup_scheduler()
         self.criterion = get_loss(config)
         self.metrics = get_metrics(config)

@@ -131,10 +131,14 @@ def steady(trace_csv: str, last: int = 8):
     bias prof_kernel_stats.csv's all-dispatch averages; bench.py's timer window runs after the timed steps."""
     with open(trace_csv) as f:
         rows = sorted(csv.DictReader(f), key=lambda r: int(r["Start_Timestamp"]))
-    ends = [i for i, r in enumerate(rows) if family(r["Kernel_Name"]) in ("adamw4_kernel", "adamw_kernel")]
-    # one AdamW family per step: with both kernels present (large + small parameter groups) keep adamw4's
-    if any(family(rows[i]["Kernel_Name"]) == "adamw4_kernel" for i in ends):
-        ends = [i for i in ends if family(rows[i]["Kernel_Name"]) == "adamw4_kernel"]
+    opt = ("adamw_pack_kernel", "adamw4_kernel", "adamw_kernel")
+    ends = [i for i, r in enumerate(rows) if family(r["Kernel_Name"]) in opt]
+    # one AdamW family per step (the fused AdamW + pack, else adamw4, else the scalar kernel): with several
+    # present (large + small parameter groups, or an eager first step) keep the first of those that occurs
+    for k in opt:
+        if any(family(rows[i]["Kernel_Name"]) == k for i in ends):
+            ends = [i for i in ends if family(rows[i]["Kernel_Name"]) == k]
+            break
     if len(ends) < 2:
         raise SystemExit("steady: fewer than two AdamW launches in the trace")
     last = min(last, len(ends) - 1)
