@@ -525,6 +525,11 @@ long long mmseg_head_ws_floats(int C, int Cin, int N, long long V);
 int mmseg_head_bwd(const void* x, int ldx, int Cin, const float* W, const float* dscale, int C, int N, long long V,
                    const float* dlogits, void* dx, int lddx, float* gW, float* gb, float* ws, int accumulate, int dtype,
                    void* stream);
+/* mmseg_head_bwd writing zcols (Cin <= zcols <= lddx, a multiple of 8) channels per dx row: zeros past Cin, so the
+ * rows of a dx that owns its padding are written whole (the engine's Act.wcols). */
+int mmseg_head_bwd_zw(const void* x, int ldx, int Cin, const float* W, const float* dscale, int C, int N, long long V,
+                      const float* dlogits, void* dx, int lddx, int zcols, float* gW, float* gb, float* ws,
+                      int accumulate, int dtype, void* stream);
 /* Fused softmax + Dice/Tversky + CE statistics and loss (losses.py:39-80, 160-185,
  * 216-228).  type 0: dice_w*Dice + ce_w*CE ; type 1: dice_w*Tversky + ce_w*CE ; type 2: FocalLoss
  * (losses.py:83-125: mean of (1 - exp(-ce_i))^gamma * ce_i with ce_i the class-weighted voxel CE; gamma is

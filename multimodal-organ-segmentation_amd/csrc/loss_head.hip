@@ -226,38 +226,67 @@ __global__ void head_dgrad_kernel(const float* __restrict__ dlog, const float* _
 }
 
 
-// Quad-per-voxel head data gradient: lane q of a 4-lane quad writes the 8-channel groups q, q+4, ... of its
-// voxel, so a wave stores 16 voxels x 64 contiguous bytes with 16-B lanes (71 us vs 86 us for the
-// one-voxel-per-lane form at 96^3 B=2; the same quad form of the forward measured slower and is not used).
-template <typename T>
-__global__ __launch_bounds__(256) void head_dgrad_q_kernel(const float* __restrict__ dlog,
+// Head data gradient, one lane per (voxel, 8-channel group): a wave stores consecutive voxels' groups (64 16-B
+// lanes over ~64 B .. 1 KB of contiguous rows) whatever Cin / 8 is -- the quad-per-voxel form (lane q of 4 took the
+// groups q, q + 4, ...) left SwinUNETR's 6 groups at 2 / 2 / 1 / 1 per quad (165 us at 128^3, 1.5 TB/s, r06y).
+// The grid stride is a whole number of voxels (the last Cin/8 - 1 threads of the grid idle), so a lane keeps its
+// group -- its 8 x C weights in registers -- and walks voxels without dividing.  Same per-channel fma order
+// (classes 0..C-1 from 0, then the Dropout3d scale), so bitwise the quad form's dx.
+template <typename T, int CM>   // CM >= C: classes held per lane (8 or CMAX)
+__global__ __launch_bounds__(256) void head_dgrad_g_kernel(const float* __restrict__ dlog,
                                                            const float* __restrict__ Wt,
                                                            const float* __restrict__ dscale, int C, int Cin,
-                                                           long long V, int N, T* __restrict__ dx, int lddx) {
-  extern __shared__ float sw[];
-  for (int i = threadIdx.x; i < C * Cin; i += blockDim.x) sw[i] = Wt[i];
-  __syncthreads();
-  const int q = threadIdx.x & 3, C8 = Cin >> 3;
-  const long long total = (long long)N * V;
-  for (long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 2; i < total;
-       i += ((long long)gridDim.x * blockDim.x) >> 2) {
-    const long long n = i / V, v = i - n * V;
-    float d[CMAX];
+                                                           long long V, int N, T* __restrict__ dx, int lddx,
+                                                           int Z8) {
+  // Z8 >= Cin / 8 groups per row are written: the groups past Cin get zeros (whole 128-B rows of a view that owns
+  // its padding, Act.wcols: a row's partial last line would cost the memory a read-modify-write)
+  const int C8 = Cin >> 3;
+  const long long G = (long long)gridDim.x * blockDim.x, gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long vstep = G / Z8;   // voxels per grid stride
+  if (gid >= vstep * Z8) return;
+  const int cg = (int)(gid % Z8);
+  const bool real = cg < C8;
+  float w[8][CM];
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c) d[c] = c < C ? dlog[(n * C + c) * V + v] : 0.f;
-    for (int cg = q; cg < C8; cg += 4) {
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int c = 0; c < CM; ++c) w[j][c] = real && c < C ? Wt[c * Cin + cg * 8 + j] : 0.f;
+  const long long total = (long long)N * V;
+  long long i = gid / Z8;
+  long long n = i / V, v = i - n * V;
+  const long long nstep = vstep / V, vrem = vstep - nstep * V;
+  // U voxels per round, all their dlogits loads issued before the first fma (one round trip per round)
+  constexpr int U = 4;
+  for (; i < total; i += U * vstep) {
+    float d[U][CM];
+    long long nu[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      nu[u] = n;
+      const bool ok = real && i + u * vstep < total;
+#pragma unroll
+      for (int c = 0; c < CM; ++c) d[u][c] = ok && c < C ? dlog[(n * C + c) * V + v] : 0.f;
+      n += nstep;
+      v += vrem;
+      if (v >= V) {
+        v -= V;
+        ++n;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (i + u * vstep >= total) break;
       V8<T> o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int ci = cg * 8 + j;
         float a = 0.f;
 #pragma unroll
-        for (int c = 0; c < CMAX; ++c)
-          if (c < C) a = fmaf(d[c], sw[c * Cin + ci], a);
-        if (dscale) a *= dscale[n * Cin + ci];
+        for (int c = 0; c < CM; ++c)
+          if (c < C) a = fmaf(d[u][c], w[j][c], a);
+        if (dscale && real) a *= dscale[nu[u] * Cin + cg * 8 + j];
         o.set(j, a);
       }
-      o.store(dx + i * lddx + cg * 8);
+      o.store(dx + (i + u * vstep) * lddx + cg * 8);
     }
   }
 }
@@ -270,9 +299,14 @@ __global__ __launch_bounds__(256) void head_wgrad_partial(const T* __restrict__ 
                                    long long vpc, float* __restrict__ part) {
   __shared__ float red[256 * 8 + 4];
   const int C8 = Cin >> 3;
-  const int lanes_v = 256 / C8;
+  // channel groups padded to a power of two (<= 32: the shuffle-tree reduction; SwinUNETR's 6 groups take 8 lanes,
+  // 2 idle) -- the serial LDS sweep over 256 / C8 voxel lanes per class cost ~10 us per block at C8 = 6 (r06y)
+  int C8p = 1;
+  while (C8p < C8) C8p <<= 1;
+  if (C8p > 32) C8p = C8;
+  const int lanes_v = 256 / C8p;
   const int tid = threadIdx.x;
-  const int cg = tid % C8, vl = tid / C8;
+  const int cg = tid % C8p, vl = tid / C8p;
   const long long total = (long long)N * V;
   const long long e0 = (long long)blockIdx.x * vpc;
   long long e1 = e0 + vpc;
@@ -286,7 +320,7 @@ __global__ __launch_bounds__(256) void head_wgrad_partial(const T* __restrict__ 
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
     }
-    if (vl < lanes_v) {
+    if (vl < lanes_v && cg < C8) {
       // U voxels per step: their feature and dlogits loads are issued before any FMA
       constexpr int U = 2;
       for (long long eb = e0 + vl; eb < e1; eb += U * lanes_v) {
@@ -320,10 +354,10 @@ __global__ __launch_bounds__(256) void head_wgrad_partial(const T* __restrict__ 
         }
       }
     }
-    if ((C8 & (C8 - 1)) == 0 && C8 <= 32) {
+    if (C8p <= 32) {
       // power-of-two channel groups: shuffle tree over the voxel lanes of each wave (fixed order), then
       // the 4 waves in order through LDS (the serial 64-lane LDS sweep per class cost ~2 us per block)
-      for (int o = 32; o >= C8; o >>= 1) {
+      for (int o = 32; o >= C8p; o >>= 1) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           bacc[k] += __shfl_down(bacc[k], o, 64);
@@ -334,9 +368,9 @@ __global__ __launch_bounds__(256) void head_wgrad_partial(const T* __restrict__ 
       const int lane = tid & 63, wave = tid >> 6;
       for (int k = 0; k < 8 && c0 + k < C; ++k) {
         __syncthreads();
-        if (lane < C8) {
+        if (lane < C8p) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) red[(wave * C8 + lane) * 8 + j] = acc[k][j];
+          for (int j = 0; j < 8; ++j) red[(wave * C8p + lane) * 8 + j] = acc[k][j];
           if (lane == 0) red[4 * 32 * 8 + wave] = bacc[k];
         }
         __syncthreads();
@@ -344,7 +378,7 @@ __global__ __launch_bounds__(256) void head_wgrad_partial(const T* __restrict__ 
           const int g = ci >> 3, j = ci & 7;
           float sacc = 0.f;
 #pragma unroll
-          for (int w = 0; w < 4; ++w) sacc += red[(w * C8 + g) * 8 + j];
+          for (int w = 0; w < 4; ++w) sacc += red[(w * C8p + g) * 8 + j];
           part[(long long)blockIdx.x * npairs + (c0 + k) * Cin + ci] = sacc;
         }
         if (tid == 0) {
@@ -1481,11 +1515,19 @@ long long mmseg_head_ws_floats(int C, int Cin, int N, long long V) {
 int mmseg_head_bwd(const void* x, int ldx, int Cin, const float* W, const float* dscale, int C, int N, long long V,
                    const float* dlogits, void* dx, int lddx, float* gW, float* gb, float* ws, int accumulate, int dtype,
                    void* stream) {
+  return mmseg_head_bwd_zw(x, ldx, Cin, W, dscale, C, N, V, dlogits, dx, lddx, Cin, gW, gb, ws, accumulate, dtype,
+                           stream);
+}
+
+int mmseg_head_bwd_zw(const void* x, int ldx, int Cin, const float* W, const float* dscale, int C, int N, long long V,
+                      const float* dlogits, void* dx, int lddx, int zcols, float* gW, float* gb, float* ws,
+                      int accumulate, int dtype, void* stream) {
   MMSEG_REQUIRE(C >= 1 && C <= CMAX && Cin % 8 == 0 && Cin <= 2048, "head_bwd: shape");
+  MMSEG_REQUIRE(zcols >= Cin && zcols % 8 == 0 && (!dx || zcols <= lddx), "head_bwd: zcols %d (Cin %d, lddx %d)",
+                zcols, Cin, lddx);
   hipStream_t s = (hipStream_t)stream;
   const long long total = (long long)N * V;
-  const int qgrid = grid_for(4 * total);
-  const size_t shm = (size_t)C * Cin * sizeof(float);
+  const int qgrid = grid_for(total * (zcols / 8));
   long long nblk = 2048;
   long long vpc = ((total + nblk - 1) / nblk + 63) / 64 * 64;
   nblk = (total + vpc - 1) / vpc;
@@ -1494,15 +1536,21 @@ int mmseg_head_bwd(const void* x, int ldx, int Cin, const float* W, const float*
   if (dtype == MMSEG_BF16) {
     MMSEG_LAUNCH(head_wgrad_partial<bf16_t>, dim3((int)nblk), dim3(256), shm2, s, (const bf16_t*)x, ldx, dlogits,
                        dscale, C, Cin, V, N, vpc, ws);
-    if (dx)
-      MMSEG_LAUNCH(head_dgrad_q_kernel<bf16_t>, dim3(qgrid), dim3(256), shm, s, dlogits, W, dscale, C, Cin, V,
-                         N, (bf16_t*)dx, lddx);
+    if (dx && C <= 8)
+      MMSEG_LAUNCH((head_dgrad_g_kernel<bf16_t, 8>), dim3(qgrid), dim3(256), 0, s, dlogits, W, dscale, C, Cin, V, N,
+                   (bf16_t*)dx, lddx, zcols / 8);
+    else if (dx)
+      MMSEG_LAUNCH((head_dgrad_g_kernel<bf16_t, CMAX>), dim3(qgrid), dim3(256), 0, s, dlogits, W, dscale, C, Cin, V,
+                   N, (bf16_t*)dx, lddx, zcols / 8);
   } else {
     MMSEG_LAUNCH(head_wgrad_partial<float>, dim3((int)nblk), dim3(256), shm2, s, (const float*)x, ldx, dlogits,
                        dscale, C, Cin, V, N, vpc, ws);
-    if (dx)
-      MMSEG_LAUNCH(head_dgrad_q_kernel<float>, dim3(qgrid), dim3(256), shm, s, dlogits, W, dscale, C, Cin, V, N,
-                         (float*)dx, lddx);
+    if (dx && C <= 8)
+      MMSEG_LAUNCH((head_dgrad_g_kernel<float, 8>), dim3(qgrid), dim3(256), 0, s, dlogits, W, dscale, C, Cin, V, N,
+                   (float*)dx, lddx, zcols / 8);
+    else if (dx)
+      MMSEG_LAUNCH((head_dgrad_g_kernel<float, CMAX>), dim3(qgrid), dim3(256), 0, s, dlogits, W, dscale, C, Cin, V,
+                   N, (float*)dx, lddx, zcols / 8);
   }
   if (mmseg::check_launch("head_bwd")) return 1;
   MMSEG_LAUNCH(head_wgrad_reduce, dim3(ceil_div(C * Cin + C, 4)), dim3(256), 0, s, ws, (int)nblk, C, Cin, gW,

@@ -1058,8 +1058,9 @@ class Head:
     def bwd(self, x: Act, dlogits: torch.Tensor, dx: Optional[Act], accumulate: bool):
         L = self.rt.lib
         ws = self.rt.ws(L.mmseg_head_ws_floats(self.C, self.Cin, x.N, x.V))
-        L.mmseg_head_bwd(x.ptr, x.ld, self.Cin, ptr(self.conv.weight), ptr(self.dscale), self.C, x.N, x.V,
-                         ptr(dlogits), dx.ptr if dx is not None else None, dx.ld if dx is not None else 0,
-                         ptr(self.flat.grad(self.conv.weight)), ptr(self.flat.grad(self.conv.bias)), ptr(ws),
-                         int(accumulate), self.rt.code, self.rt.stream)
+        L.mmseg_head_bwd_zw(x.ptr, x.ld, self.Cin, ptr(self.conv.weight), ptr(self.dscale), self.C, x.N, x.V,
+                            ptr(dlogits), dx.ptr if dx is not None else None, dx.ld if dx is not None else 0,
+                            dx.wcols if dx is not None else self.Cin, ptr(self.flat.grad(self.conv.weight)),
+                            ptr(self.flat.grad(self.conv.bias)), ptr(ws), int(accumulate), self.rt.code,
+                            self.rt.stream)
         self.flat.mark(self.conv.weight, self.conv.bias)

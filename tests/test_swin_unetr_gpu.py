@@ -917,10 +917,12 @@ def test_window_attention_full_windows_bitwise(dev, masked, monkeypatch):
     assert torch.equal(res["1"][0], res["1"][2])   # dQ of the grouped query pass is the per-window pass's
 
 
+@pytest.mark.parametrize("Cin,ld,C", [(48, 64, 6), (24, 32, 10)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_head_48_channels_tile(dev, dtype):
-    """SwinUNETR's 1x1 head on 48 channels at pitch 64 (the tile-staged forward) against torch fp64."""
-    N, V, Cin, ld, C = 1, 3000, 48, 64, 6
+def test_head_48_channels_tile(dev, dtype, Cin, ld, C):
+    """SwinUNETR's 1x1 head on 48 channels at pitch 64 (the tile-staged forward) against torch fp64; the backward
+    (per-(voxel, group) data gradient, power-of-two-padded channel groups in the weight-gradient partials) too."""
+    N, V = 1, 3000
     g = torch.Generator().manual_seed(41)
     x = torch.randn(N * V, ld, generator=g).to(dtype)
     x[:, Cin:] = 0
@@ -932,6 +934,25 @@ def test_head_48_channels_tile(dev, dtype):
     L.mmseg_head_fwd(ptr(xd), ld, Cin, ptr(Wd), ptr(bd), None, C, N, V, ptr(lg), CODE[dtype], s)
     ref = x[:, :Cin].double() @ W.double().t() + b.double()
     assert rel(lg.view(C, V).t(), ref) < 1e-5
+    dl = torch.randn(N * C * V, generator=g)
+    dld = dl.to(dev)
+    dx = torch.zeros(N * V, ld, dtype=dtype, device=dev)
+    gW = torch.empty(C * Cin, device=dev)
+    gb = torch.empty(C, device=dev)
+    ws = torch.empty(L.mmseg_head_ws_floats(C, Cin, N, V), device=dev)
+    L.mmseg_head_bwd(ptr(xd), ld, Cin, ptr(Wd), None, C, N, V, ptr(dld), ptr(dx), ld, ptr(gW), ptr(gb), ptr(ws), 0,
+                     CODE[dtype], s)
+    dlv = dl.view(C, V).t().double()
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel(dx[:, :Cin].float(), dlv @ W.double()) < tol
+    assert torch.count_nonzero(dx[:, Cin:]) == 0
+    assert rel(gW.view(C, Cin), dlv.t() @ x[:, :Cin].double()) < 1e-5
+    assert rel(gb, dlv.sum(0)) < 1e-5
+    # whole-row form (a dx owning its padding): the same real channels, zeros written over the padding
+    dx2 = torch.full((N * V, ld), 7.0, dtype=dtype, device=dev)
+    L.mmseg_head_bwd_zw(ptr(xd), ld, Cin, ptr(Wd), None, C, N, V, ptr(dld), ptr(dx2), ld, ld, ptr(gW), ptr(gb),
+                        ptr(ws), 0, CODE[dtype], s)
+    assert torch.equal(dx2[:, :Cin], dx[:, :Cin]) and torch.count_nonzero(dx2[:, Cin:]) == 0
 
 
 def test_swin_sliding_window_c4_at_size(dev):
