@@ -50,7 +50,10 @@ def main():
         def dgrad():
             ln.bwd(x, K, dy, N, M, dx, K, False)
 
-        for nm, fn in (("fwd", fwd), ("bwd", dgrad)):
+        def wgrad():
+            ln.bwd(x, K, dy, N, M, None, K, False)
+
+        for nm, fn in (("fwd", fwd), ("bwd", dgrad), ("wgrad", wgrad)):
             fn()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -63,11 +66,13 @@ def main():
         gb = (M * K + M * N) * 2 / 1e9
         tot["fwd"] += res["fwd"]
         tot["dgrad"] += res["bwd"]
+        tot["wgrad"] += res["wgrad"]
         print(f"M={M:8d} K={K:4d} N={N:4d}: fwd {res['fwd']:7.1f} us ({gb / res['fwd'] * 1e6:6.0f} GB/s)  "
               f"bwd (wgrad + dgrad) {res['bwd']:7.1f} us ({2 * gb / res['bwd'] * 1e6:6.0f} GB/s)  "
+              f"wgrad {res['wgrad']:7.1f} us ({gb / res['wgrad'] * 1e6:6.0f} GB/s)  "
               f"y {y.float().abs().sum().item():.5e} dx {dx.float().abs().sum().item():.5e} "
               f"dw {flat.grad(lin.weight).abs().sum().item():.5e}", flush=True)
-    print("total fwd %.1f us, bwd %.1f us" % (tot["fwd"], tot["dgrad"]))
+    print("total fwd %.1f us, bwd %.1f us, wgrad alone %.1f us" % (tot["fwd"], tot["dgrad"], tot["wgrad"]))
 
 
 if __name__ == "__main__":
