@@ -1527,7 +1527,10 @@ int mmseg_head_bwd_zw(const void* x, int ldx, int Cin, const float* W, const flo
                 zcols, Cin, lddx);
   hipStream_t s = (hipStream_t)stream;
   const long long total = (long long)N * V;
-  const int qgrid = grid_for(total * (zcols / 8));
+#ifndef HEAD_DGRAD_GRID_CAP
+#define HEAD_DGRAD_GRID_CAP 2048
+#endif
+  const int qgrid = std::min(grid_for(total * (zcols / 8)), HEAD_DGRAD_GRID_CAP);
   long long nblk = 2048;
   long long vpc = ((total + nblk - 1) / nblk + 63) / 64 * 64;
   nblk = (total + vpc - 1) / vpc;
